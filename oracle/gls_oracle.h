@@ -1,0 +1,113 @@
+/* gls_oracle.h — CPU oracle for the GLS Navier–Stokes hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is a plain-C restatement of the reference
+ * algorithm, used as the checker for the HIP product path. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the
+ * product library (softx_2020_200_amd/) never links or calls it.
+ *
+ * Reference followed (read-only, /root/reference):
+ *   assembleGLS<assemble_matrix, scheme, velocity_source>
+ *       source/solvers/gls_navier_stokes.cc:230-777
+ *   bdf_coefficients / delta      source/core/bdf.cc:23-75
+ *   sdirk_coefficients            source/core/sdirk.cc:11-44
+ *   scheme predicates             include/core/time_integration_utilities.h:12-141
+ *   calculate_L2_error            source/solvers/navier_stokes_base.cc:253-380
+ *   AffineConstraints::distribute_local_to_global (deal.II 9.2, not vendored):
+ *       constrained rows/cols dropped, diagonal += |local(i,i)| (or the mean
+ *       |diagonal| of the local matrix when that entry is 0), rhs rows zero.
+ *
+ * Pinning: the restatement is checked end-to-end against the reference's own
+ * golden outputs (mms2d_gls / mms3d_gls L2 error tables, restart_01, bdf_01);
+ * see tests/test_oracle_goldens.py. Per-DoF residual / Jacobian vectors have
+ * no reference golden — they are pinned only through those
+ * end-to-end results.
+ */
+#ifndef GLS_ORACLE_H
+#define GLS_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* TimeSteppingMethod, same order as include/core/parameters.h:56-69 */
+enum {
+  OR_STEADY = 0, OR_BDF1, OR_BDF2, OR_BDF3, OR_SDIRK2, OR_SDIRK2_1, OR_SDIRK2_2,
+  OR_SDIRK3, OR_SDIRK3_1, OR_SDIRK3_2, OR_SDIRK3_3
+};
+
+typedef struct {
+  int dim;               /* 2 or 3 */
+  int k;                 /* velocity FE_Q degree */
+  int kp;                /* pressure FE_Q degree */
+  int nq1d;              /* QGauss points per direction (reference: k+1) */
+  int n_cells;
+  const double *cell_x0; /* [n_cells*dim] lower corner of the (axis-aligned) cell */
+  const double *cell_h;  /* [n_cells*dim] cell extents */
+  const int *cell_vnodes;/* [n_cells*(k+1)^dim] global velocity node, lexicographic local order */
+  const int *cell_pnodes;/* [n_cells*(kp+1)^dim] global pressure node */
+  int n_vnodes, n_pnodes;/* global vector = [vnode*dim+c ... | dim*n_vnodes + pnode] */
+  const unsigned char *constrained; /* [n_dofs]: 1 = DoF in zero_constraints */
+  double viscosity;
+  int scheme;            /* OR_* */
+  double time_steps[4];  /* SimulationControl::get_time_steps_vector() */
+  const double *force_q; /* [n_cells*nq*dim] forcing at quadrature points, NULL = NoForce */
+  int srf;               /* VelocitySourceType::srf */
+  double omega[3];       /* omega_x, omega_y, omega_z */
+} gls_oracle_problem;
+
+int gls_oracle_n_dofs(const gls_oracle_problem *p);
+int gls_oracle_dofs_per_cell(const gls_oracle_problem *p);
+int gls_oracle_cell_dofs(const gls_oracle_problem *p, int cell, int *dofs);
+
+/* physical quadrature points of one cell for QGauss(nq1d): out[nq*dim] */
+int gls_oracle_qpoints(const gls_oracle_problem *p, int nq1d, int cell, double *out);
+
+/* one cell of assembleGLS (gls_navier_stokes.cc:338-749): Ke [ndofs*ndofs] row-major (may be NULL), Fe [ndofs] */
+int gls_oracle_local_system(const gls_oracle_problem *p, int cell,
+                            const double *u, const double *u1, const double *u2, const double *u3,
+                            double *Ke, double *Fe);
+
+/* assemble_rhs: rhs = distribute(Fe) with zero constraints (constrained rows 0) */
+int gls_oracle_assemble_rhs(const gls_oracle_problem *p,
+                            const double *u, const double *u1, const double *u2, const double *u3,
+                            double *rhs);
+
+/* assemble_matrix_and_rhs into COO triplets (duplicates summed by the caller).
+ * rows/cols/vals must hold n_cells*ndofs*ndofs entries; *nnz returns the count used. */
+int gls_oracle_assemble_coo(const gls_oracle_problem *p,
+                            const double *u, const double *u1, const double *u2, const double *u3,
+                            int *rows, int *cols, double *vals, long long *nnz, double *rhs);
+
+/* y = J v for the reference's assembled (constraint-eliminated) Jacobian, element by element */
+int gls_oracle_jacobian_apply(const gls_oracle_problem *p,
+                              const double *u, const double *u1, const double *u2, const double *u3,
+                              const double *v, double *y);
+
+/* diagonal of the assembled Jacobian (constrained DoFs: sum over cells of |local(i,i)|) */
+int gls_oracle_jacobian_diagonal(const gls_oracle_problem *p,
+                                 const double *u, const double *u1, const double *u2, const double *u3,
+                                 double *d);
+
+/* L2 errors (navier_stokes_base.cc:253-380) with QGauss(nq1d_err);
+ * exact_q[n_cells*nqe*(dim+1)] = exact (u,v,[w],p) at gls_oracle_qpoints(nq1d_err) */
+int gls_oracle_l2_error(const gls_oracle_problem *p, int nq1d_err, const double *sol,
+                        const double *exact_q, double *err_u, double *err_p);
+
+/* L2-projection system (assemble_L2_projection, gls_navier_stokes.cc:830-914) as COO + rhs */
+int gls_oracle_l2_projection_coo(const gls_oracle_problem *p, const double *uvwp_q,
+                                 int *rows, int *cols, double *vals, long long *nnz, double *rhs);
+
+/* time coefficients (bdf.cc:45-75, sdirk.cc:11-44); sdirk out is row-major [order][order+1] */
+int gls_oracle_bdf_coefficients(int order, const double *dt, int n_dt, double *alpha);
+int gls_oracle_sdirk_coefficients(int order, double dt, double *out);
+
+/* CPU baseline: compute local systems of cells [c0, c0+count) with nthreads OpenMP threads;
+ * returns a checksum so the work cannot be elided. */
+double gls_oracle_time_local_systems(const gls_oracle_problem *p,
+                                     const double *u, const double *u1, const double *u2, const double *u3,
+                                     int c0, int count, int with_matrix, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,402 @@
+"""ctypes front-end of the CPU oracle + the test-side problem builders.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.
+
+What lives here:
+  * ``Oracle``: bindings to oracle/libgls_oracle.so (gls_oracle.c restates
+    source/solvers/gls_navier_stokes.cc:230-777 of the reference).
+  * ``StructuredProblem``: a hyper_cube mesh (GridGenerator::hyper_cube +
+    refine_global, grids.cc:12-60) with the canonical DoF numbering shared with
+    the product: velocity node = lexicographic index on the
+    (k*n+1)^dim lattice, DoF = node*dim + c; pressure node on the
+    (kp*n+1)^dim lattice, DoF = dim*n_vnodes + node.
+  * Dirichlet constraints with deal.II's first-bc-wins rule
+    (gls_navier_stokes.cc:80-184; VectorTools::interpolate_boundary_values skips
+    DoFs that are already constrained).
+  * ``newton_solve``: the damped Newton of include/core/newton_non_linear_solver.h:74-139
+    with a sparse direct solve (scipy) in place of Trilinos GMRES+ILU — the
+    converged solution is independent of the linear solver at tol 1e-8.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libgls_oracle.so")
+
+SCHEMES = {
+    "steady": 0, "bdf1": 1, "bdf2": 2, "bdf3": 3, "sdirk2": 4, "sdirk2_1": 5, "sdirk2_2": 6,
+    "sdirk3": 7, "sdirk3_1": 8, "sdirk3_2": 9, "sdirk3_3": 10,
+}
+
+
+class _Problem(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int), ("k", C.c_int), ("kp", C.c_int), ("nq1d", C.c_int), ("n_cells", C.c_int),
+        ("cell_x0", C.POINTER(C.c_double)), ("cell_h", C.POINTER(C.c_double)),
+        ("cell_vnodes", C.POINTER(C.c_int)), ("cell_pnodes", C.POINTER(C.c_int)),
+        ("n_vnodes", C.c_int), ("n_pnodes", C.c_int),
+        ("constrained", C.POINTER(C.c_ubyte)),
+        ("viscosity", C.c_double), ("scheme", C.c_int), ("time_steps", C.c_double * 4),
+        ("force_q", C.POINTER(C.c_double)), ("srf", C.c_int), ("omega", C.c_double * 3),
+    ]
+
+
+def build_oracle() -> str:
+    """Compile the oracle (gcc) if needed; returns the .so path."""
+    src = os.path.join(HERE, "gls_oracle.c")
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build_oracle())
+        d = C.POINTER(C.c_double)
+        P = C.POINTER(_Problem)
+        for name in ("gls_oracle_assemble_rhs", "gls_oracle_jacobian_diagonal"):
+            getattr(_lib, name).argtypes = [P, d, d, d, d, d]
+        _lib.gls_oracle_jacobian_apply.argtypes = [P, d, d, d, d, d, d]
+        _lib.gls_oracle_assemble_coo.argtypes = [P, d, d, d, d, C.POINTER(C.c_int), C.POINTER(C.c_int), d,
+                                                 C.POINTER(C.c_longlong), d]
+        _lib.gls_oracle_local_system.argtypes = [P, C.c_int, d, d, d, d, d, d]
+        _lib.gls_oracle_qpoints.argtypes = [P, C.c_int, C.c_int, d]
+        _lib.gls_oracle_l2_error.argtypes = [P, C.c_int, d, d, d, d]
+        _lib.gls_oracle_l2_projection_coo.argtypes = [P, d, C.POINTER(C.c_int), C.POINTER(C.c_int), d,
+                                                      C.POINTER(C.c_longlong), d]
+        _lib.gls_oracle_bdf_coefficients.argtypes = [C.c_int, d, C.c_int, d]
+        _lib.gls_oracle_sdirk_coefficients.argtypes = [C.c_int, C.c_double, d]
+        _lib.gls_oracle_cell_dofs.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
+        _lib.gls_oracle_time_local_systems.argtypes = [P, d, d, d, d, C.c_int, C.c_int, C.c_int, C.c_int]
+        _lib.gls_oracle_time_local_systems.restype = C.c_double
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else C.POINTER(C.c_double)()
+
+
+def bdf_coefficients(order, dts):
+    dts = np.ascontiguousarray(dts, dtype=np.float64)
+    out = np.zeros(order + 1)
+    assert lib().gls_oracle_bdf_coefficients(order, _dp(dts), len(dts), _dp(out)) == 0
+    return out
+
+
+def sdirk_coefficients(order, dt):
+    out = np.zeros(order * (order + 1))
+    assert lib().gls_oracle_sdirk_coefficients(order, dt, _dp(out)) == 0
+    return out.reshape(order, order + 1)
+
+
+# ----------------------------------------------------------------------------------------------
+# structured hyper_cube problem
+# ----------------------------------------------------------------------------------------------
+class StructuredProblem:
+    """hyper_cube(lo, hi, colorize) refined to n cells per direction, FESystem(FE_Q(k)^dim, FE_Q(kp))."""
+
+    def __init__(self, dim, n, k=1, kp=None, lo=-1.0, hi=1.0, colorize=False, viscosity=1.0,
+                 scheme="steady", time_steps=(1.0, 1.0, 1.0, 1.0), nq1d=None, srf=False, omega=(0, 0, 0),
+                 periodic=()):
+        kp = k if kp is None else kp
+        # periodic directions: make_periodicity_constraints (gls_navier_stokes.cc:127-136) restated as
+        # node identification on the lattice (master = low face), which is what the condensed system solves
+        self.periodic = tuple(periodic)
+        self.dim, self.n, self.k, self.kp = dim, n, k, kp
+        self.lo, self.hi, self.colorize = lo, hi, colorize
+        self.nq1d = nq1d or (k + 1)
+        self.viscosity = viscosity
+        self.scheme = scheme
+        self.time_steps = list(time_steps) + [1.0] * (4 - len(time_steps))
+        self.srf, self.omega = srf, omega
+        hc = (hi - lo) / n
+        self.hc = hc
+        nc = n ** dim
+        idx = np.indices((n,) * dim).reshape(dim, -1)[::-1].T  # lexicographic cells, x fastest
+        self.cell_ijk = np.ascontiguousarray(idx)
+        self.cell_x0 = np.ascontiguousarray(lo + idx * hc, dtype=np.float64)
+        self.cell_h = np.full((nc, dim), hc, dtype=np.float64)
+        self.nvx = k * n + 1
+        self.npx = kp * n + 1
+        self.vshape = [k * n if d in self.periodic else k * n + 1 for d in range(dim)]
+        self.pshape = [kp * n if d in self.periodic else kp * n + 1 for d in range(dim)]
+        self.n_vnodes = int(np.prod(self.vshape))
+        self.n_pnodes = int(np.prod(self.pshape))
+        self.cell_vnodes = self._cell_nodes(k, self.vshape)
+        self.cell_pnodes = self._cell_nodes(kp, self.pshape)
+        self.n_dofs = dim * self.n_vnodes + self.n_pnodes
+        self.constrained = np.zeros(self.n_dofs, dtype=np.uint8)
+        self.dirichlet = {}  # dof -> value (nonzero_constraints)
+        self.force_q = None
+
+    def _cell_nodes(self, k, shape):
+        dim = self.dim
+        loc = np.indices((k + 1,) * dim).reshape(dim, -1)[::-1].T  # local lexicographic
+        base = self.cell_ijk * k
+        gl = base[:, None, :] + loc[None, :, :]
+        ids = np.zeros(gl.shape[:2], dtype=np.int64)
+        stride = 1
+        for d in range(dim):
+            ids += (gl[:, :, d] % shape[d]) * stride
+            stride *= shape[d]
+        return np.ascontiguousarray(ids.astype(np.int32))
+
+    # --- geometry of the velocity lattice
+    def vnode_coords(self):
+        dim = self.dim
+        ijk = np.indices(tuple(self.vshape[::-1])).reshape(dim, -1)[::-1].T
+        return self.lo + ijk * (self.hc / self.k)
+
+    def boundary_ids_of_vnodes(self):
+        """list of sets: boundary ids each velocity node lies on (colorize rule of hyper_cube)."""
+        X = self.vnode_coords()
+        tol = 1e-12 * (self.hi - self.lo)
+        ids = [set() for _ in range(X.shape[0])]
+        for d in range(self.dim):
+            lo_ = np.nonzero(np.abs(X[:, d] - self.lo) < tol)[0]
+            hi_ = np.nonzero(np.abs(X[:, d] - self.hi) < tol)[0]
+            for i in lo_:
+                ids[i].add(2 * d if self.colorize else 0)
+            for i in hi_:
+                ids[i].add(2 * d + 1 if self.colorize else 0)
+        return ids
+
+    def set_dirichlet(self, bcs):
+        """bcs: list of (type, id, func) in bc order; type in {'noslip','function'};
+        func(X) -> (n, dim) values for 'function'. First bc wins (deal.II)."""
+        X = self.vnode_coords()
+        bids = self.boundary_ids_of_vnodes()
+        self.constrained[:] = 0
+        self.dirichlet = {}
+        for typ, bid, func in bcs:
+            nodes = np.array([i for i, s in enumerate(bids) if bid in s], dtype=np.int64)
+            if nodes.size == 0:
+                continue
+            if typ == "noslip":
+                vals = np.zeros((nodes.size, self.dim))
+            elif typ == "function":
+                vals = np.asarray(func(X[nodes]), dtype=np.float64).reshape(nodes.size, self.dim)
+            else:
+                raise ValueError(typ)
+            for nd, v in zip(nodes, vals):
+                for c in range(self.dim):
+                    dof = nd * self.dim + c
+                    if not self.constrained[dof]:
+                        self.constrained[dof] = 1
+                        self.dirichlet[dof] = float(v[c])
+        return self
+
+    def apply_nonzero_constraints(self, x):
+        for dof, v in self.dirichlet.items():
+            x[dof] = v
+        return x
+
+    def qpoints(self, nq1d=None):
+        nq1d = nq1d or self.nq1d
+        nq = nq1d ** self.dim
+        out = np.zeros((self.n_cells, nq, self.dim))
+        L = lib()
+        P = self.struct()
+        for c in range(self.n_cells):
+            L.gls_oracle_qpoints(C.byref(P), nq1d, c, _dp(out[c]))
+        return out
+
+    @property
+    def n_cells(self):
+        return self.cell_x0.shape[0]
+
+    def set_force(self, func):
+        """func(X[..., dim]) -> (..., dim) forcing at the assembly quadrature points."""
+        X = self.qpoints()
+        self.force_q = np.ascontiguousarray(np.asarray(func(X.reshape(-1, self.dim)), dtype=np.float64)
+                                            .reshape(self.n_cells, -1, self.dim))
+        return self
+
+    def struct(self):
+        P = _Problem()
+        P.dim, P.k, P.kp, P.nq1d, P.n_cells = self.dim, self.k, self.kp, self.nq1d, self.n_cells
+        P.cell_x0 = _dp(self.cell_x0)
+        P.cell_h = _dp(self.cell_h)
+        P.cell_vnodes = self.cell_vnodes.ctypes.data_as(C.POINTER(C.c_int))
+        P.cell_pnodes = self.cell_pnodes.ctypes.data_as(C.POINTER(C.c_int))
+        P.n_vnodes, P.n_pnodes = self.n_vnodes, self.n_pnodes
+        P.constrained = self.constrained.ctypes.data_as(C.POINTER(C.c_ubyte))
+        P.viscosity = self.viscosity
+        P.scheme = SCHEMES[self.scheme]
+        for i in range(4):
+            P.time_steps[i] = self.time_steps[i]
+        P.force_q = _dp(self.force_q)
+        P.srf = 1 if self.srf else 0
+        for i in range(3):
+            P.omega[i] = self.omega[i]
+        self._keep = (self.cell_x0, self.cell_h, self.cell_vnodes, self.cell_pnodes, self.constrained,
+                      self.force_q)
+        return P
+
+
+class Oracle:
+    def __init__(self, prob: StructuredProblem):
+        self.p = prob
+        self.L = lib()
+
+    def _hist(self, u1, u2, u3):
+        z = np.zeros(self.p.n_dofs)
+        return [np.ascontiguousarray(a if a is not None else z, dtype=np.float64) for a in (u1, u2, u3)]
+
+    def residual(self, u, u1=None, u2=None, u3=None):
+        P = self.p.struct()
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        h = self._hist(u1, u2, u3)
+        rhs = np.zeros(self.p.n_dofs)
+        assert self.L.gls_oracle_assemble_rhs(C.byref(P), _dp(u), _dp(h[0]), _dp(h[1]), _dp(h[2]), _dp(rhs)) == 0
+        return rhs
+
+    def jacobian_apply(self, u, v, u1=None, u2=None, u3=None):
+        P = self.p.struct()
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        h = self._hist(u1, u2, u3)
+        y = np.zeros(self.p.n_dofs)
+        assert self.L.gls_oracle_jacobian_apply(C.byref(P), _dp(u), _dp(h[0]), _dp(h[1]), _dp(h[2]), _dp(v),
+                                                _dp(y)) == 0
+        return y
+
+    def jacobian_diagonal(self, u, u1=None, u2=None, u3=None):
+        P = self.p.struct()
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        h = self._hist(u1, u2, u3)
+        d = np.zeros(self.p.n_dofs)
+        assert self.L.gls_oracle_jacobian_diagonal(C.byref(P), _dp(u), _dp(h[0]), _dp(h[1]), _dp(h[2]), _dp(d)) == 0
+        return d
+
+    def matrix_and_rhs(self, u, u1=None, u2=None, u3=None):
+        import scipy.sparse as sp
+        P = self.p.struct()
+        nd = self.L.gls_oracle_dofs_per_cell(C.byref(P))
+        cap = self.p.n_cells * nd * nd
+        rows = np.zeros(cap, dtype=np.int32)
+        cols = np.zeros(cap, dtype=np.int32)
+        vals = np.zeros(cap)
+        nnz = C.c_longlong(0)
+        rhs = np.zeros(self.p.n_dofs)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        h = self._hist(u1, u2, u3)
+        assert self.L.gls_oracle_assemble_coo(C.byref(P), _dp(u), _dp(h[0]), _dp(h[1]), _dp(h[2]),
+                                              rows.ctypes.data_as(C.POINTER(C.c_int)),
+                                              cols.ctypes.data_as(C.POINTER(C.c_int)), _dp(vals), C.byref(nnz),
+                                              _dp(rhs)) == 0
+        n = nnz.value
+        A = sp.coo_matrix((vals[:n], (rows[:n], cols[:n])), shape=(self.p.n_dofs,) * 2).tocsr()
+        A.sum_duplicates()
+        return A, rhs
+
+    def l2_projection(self, func):
+        """set_initial_condition(L2projection): assemble_L2_projection + exact solve
+        (gls_navier_stokes.cc:795-803, 830-914). func(X) -> (m, dim+1)."""
+        import scipy.sparse as sp
+        import scipy.sparse.linalg as spla
+        X = self.p.qpoints()
+        ic = np.ascontiguousarray(np.asarray(func(X.reshape(-1, self.p.dim)), dtype=np.float64))
+        P = self.p.struct()
+        nd = self.L.gls_oracle_dofs_per_cell(C.byref(P))
+        cap = self.p.n_cells * nd * nd
+        rows = np.zeros(cap, dtype=np.int32)
+        cols = np.zeros(cap, dtype=np.int32)
+        vals = np.zeros(cap)
+        nnz = C.c_longlong(0)
+        rhs = np.zeros(self.p.n_dofs)
+        assert self.L.gls_oracle_l2_projection_coo(C.byref(P), _dp(ic), rows.ctypes.data_as(C.POINTER(C.c_int)),
+                                                   cols.ctypes.data_as(C.POINTER(C.c_int)), _dp(vals),
+                                                   C.byref(nnz), _dp(rhs)) == 0
+        n = nnz.value
+        A = sp.coo_matrix((vals[:n], (rows[:n], cols[:n])), shape=(self.p.n_dofs,) * 2).tocsc()
+        return spla.spsolve(A, rhs)
+
+    def l2_error(self, sol, exact_func, nq1d_err=None):
+        """exact_func(X[m,dim]) -> (m, dim+1). QGauss(n_q+1) as calculate_L2_error."""
+        nq1d_err = nq1d_err or (self.p.nq1d + 1)
+        X = self.p.qpoints(nq1d_err)
+        ex = np.ascontiguousarray(np.asarray(exact_func(X.reshape(-1, self.p.dim)), dtype=np.float64))
+        P = self.p.struct()
+        eu, ep = C.c_double(0), C.c_double(0)
+        sol = np.ascontiguousarray(sol, dtype=np.float64)
+        assert self.L.gls_oracle_l2_error(C.byref(P), nq1d_err, _dp(sol), _dp(ex), C.byref(eu), C.byref(ep)) == 0
+        return eu.value, ep.value
+
+
+def newton_solve(prob: StructuredProblem, x0=None, u1=None, u2=None, u3=None, tol=1e-8, max_it=10, log=None):
+    """NewtonNonLinearSolver::solve (newton_non_linear_solver.h:74-139) with an exact sparse
+    linear solve; the single constant-pressure null mode is removed by pinning pressure DoF 0."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    orc = Oracle(prob)
+    x = np.zeros(prob.n_dofs) if x0 is None else np.array(x0, dtype=np.float64)
+    prob.apply_nonzero_constraints(x)
+    pin = prob.dim * prob.n_vnodes
+    last_res, cur_res, it = 1.0, 1.0, 0
+    while cur_res > tol and it < max_it:
+        A, rhs = orc.matrix_and_rhs(x, u1, u2, u3)
+        if it == 0:
+            cur_res = np.linalg.norm(rhs)
+            last_res = cur_res
+        if log is not None:
+            log.append(("newton", it, cur_res))
+        A = A.tolil()
+        A[pin, :] = 0
+        A[:, pin] = 0
+        A[pin, pin] = 1.0
+        b = rhs.copy()
+        b[pin] = 0.0
+        dx = spla.spsolve(sp.csc_matrix(A), b)
+        dx[prob.constrained.astype(bool)] = 0.0  # zero_constraints.distribute
+        alpha = 1.0
+        while alpha > 1e-3:
+            xt = x + alpha * dx
+            prob.apply_nonzero_constraints(xt)
+            r = orc.residual(xt, u1, u2, u3)
+            cur_res = np.linalg.norm(r)
+            if log is not None:
+                log.append(("alpha", alpha, cur_res))
+            if cur_res < 0.9 * last_res or last_res < tol:
+                break
+            alpha *= 0.5
+        x = xt
+        last_res = cur_res
+        it += 1
+    return x, it, cur_res
+
+
+def muparser_to_numpy(expr: str, constants=None):
+    """Tiny test-side translator of the reference's muParser 'Function expression' strings
+    (components separated by ';') to a numpy callable f(X[m,dim]) -> (m, ncomp)."""
+    comps = [c.strip() for c in expr.split(";")]
+    ns = {"sin": np.sin, "cos": np.cos, "tan": np.tan, "exp": np.exp, "log": np.log, "sqrt": np.sqrt,
+          "abs": np.abs, "pi": math.pi, "atan": np.arctan, "tanh": np.tanh, "sinh": np.sinh, "cosh": np.cosh}
+    if constants:
+        ns.update(constants)
+    codes = [compile(c.replace("^", "**"), "<muparser>", "eval") for c in comps]
+
+    def f(X):
+        X = np.asarray(X)
+        env = dict(ns)
+        env["x"] = X[:, 0]
+        env["y"] = X[:, 1]
+        env["z"] = X[:, 2] if X.shape[1] > 2 else np.zeros(X.shape[0])
+        env["t"] = 0.0
+        out = np.zeros((X.shape[0], len(codes)))
+        for i, c in enumerate(codes):
+            out[:, i] = eval(c, {"__builtins__": {}}, env)
+        return out
+
+    return f
