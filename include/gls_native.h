@@ -1,0 +1,173 @@
+/* gls_native.h — C-ABI of the MI355X-native GLS Navier–Stokes hot path.
+ *
+ * Drop-in boundary for Lethe's GLSNavierStokesSolver assembly + linear-solve path.
+ * Every entry point below names the reference interface it replaces
+ * (paths relative to the reference tree, LMNS3d/SOFTX_2020_200).
+ *
+ * Conventions
+ *   - Plain C types only: pointers, sizes, doubles. No torch / HIP types in signatures
+ *     (streams are passed as void*; NULL = the context's own stream).
+ *   - Return 0 on success or a negative GLS_E* code; gls_last_error() gives the text
+ *     (thread-local). No C++ exception ever crosses this boundary
+ *     (the reference throws std::runtime_error, gls_navier_stokes.cc:825, :1158).
+ *   - Vectors are FP64, global layout [velocity node-major, comps interleaved | pressure]:
+ *       dof(vnode, c) = vnode*dim + c,  dof(pnode) = dim*n_vnodes + pnode.
+ *   - Operator entry points take DEVICE pointers (hipMalloc / torch cuda tensors); calls are
+ *     stream-ordered on the context stream. Host-pointer entry points say so.
+ *   - One context per GPU; the multi-GPU context (gls_dist_*) wraps RCCL.
+ */
+#ifndef GLS_NATIVE_H
+#define GLS_NATIVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GLS_OK 0
+#define GLS_EINVAL -1   /* bad argument / unsupported configuration */
+#define GLS_EHIP -2     /* HIP runtime error */
+#define GLS_ENOMEM -3   /* device allocation failed */
+#define GLS_ENOCONV -4  /* linear solver did not converge (informational) */
+#define GLS_EIO -5      /* file / parse error */
+#define GLS_ECOMM -6    /* RCCL error */
+
+/* TimeSteppingMethod, same order as include/core/parameters.h:56-69 */
+enum gls_scheme {
+  GLS_STEADY = 0, GLS_BDF1, GLS_BDF2, GLS_BDF3, GLS_SDIRK2, GLS_SDIRK2_1, GLS_SDIRK2_2,
+  GLS_SDIRK3, GLS_SDIRK3_1, GLS_SDIRK3_2, GLS_SDIRK3_3
+};
+
+const char *gls_last_error(void);
+const char *gls_version(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Mesh / DoF map description (host pointers, copied at gls_create).
+ * Replaces NavierStokesBase ctor FESystem(FE_Q(k)^dim, FE_Q(kp)) + QGauss(k+1)
+ * (source/solvers/navier_stokes_base.cc:62,70) and GLSNavierStokesSolver::setup_dofs
+ * (source/solvers/gls_navier_stokes.cc:55-228): cell->DoF map, zero_constraints mask.
+ * Cells are axis-aligned boxes (hyper_cube / subdivided meshes, MappingQ affine on them).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int dim;                      /* 2 or 3 */
+  int k;                        /* velocity degree (1..3) */
+  int kp;                       /* pressure degree (1..k) */
+  int nq1d;                     /* QGauss points per direction, 0 = k+1 (navier_stokes_base.cc:70, :93-94) */
+  int n_cells;
+  int n_vnodes, n_pnodes;
+  const int32_t *cell_vnodes;   /* [n_cells*(k+1)^dim], lexicographic local node order (x fastest) */
+  const int32_t *cell_pnodes;   /* [n_cells*(kp+1)^dim]; NULL when kp==k and pressure nodes == velocity nodes */
+  const double *cell_x0;        /* [n_cells*dim] lower corner (used by the SRF source term); may be NULL */
+  const double *cell_h;         /* [n_cells*dim] extents */
+  const uint8_t *vnode_mask;    /* [n_vnodes] bit c set = velocity comp c is in zero_constraints; NULL = none */
+  double viscosity;             /* physical properties/kinematic viscosity */
+  int srf;                      /* velocity source = srf (parameters.h:511-515) */
+  double omega[3];
+  const double *force_q;        /* [n_cells*nq*dim] forcing at quadrature points; NULL = NoForce */
+} gls_mesh_desc;
+
+typedef struct gls_ctx gls_ctx;
+
+/* setup_dofs equivalent: uploads the DoF map, geometry, tabulated 1D bases. */
+int gls_create(const gls_mesh_desc *desc, gls_ctx **out);
+int gls_destroy(gls_ctx *ctx);
+int gls_set_stream(gls_ctx *ctx, void *hip_stream);
+int gls_n_dofs(const gls_ctx *ctx, int64_t *n_dofs);
+/* Rewrite the forcing at quadrature points (host pointer, [n_cells*nq*dim]) or clear it (NULL). */
+int gls_set_force(gls_ctx *ctx, const double *force_q);
+int gls_set_viscosity(gls_ctx *ctx, double viscosity);
+
+/* Time-stepping state for the next assembly (replaces the top of assembleGLS,
+ * gls_navier_stokes.cc:295-329: time_steps_vector -> bdf_coefficients / sdirk_coefficients). */
+int gls_set_time(gls_ctx *ctx, int scheme, const double time_steps[4]);
+
+/* Evaluation point and history (DEVICE pointers, borrowed until the next call):
+ * evaluation_point, solution_m1..m3 of PhysicsSolver (include/core/physics_solver.h:107-111).
+ * u1..u3 may be NULL when the scheme does not read them. */
+int gls_set_state(gls_ctx *ctx, const double *u, const double *u1, const double *u2, const double *u3);
+
+/* assemble_rhs (gls_navier_stokes.cc:1023-1128 -> assembleGLS<false,...>):
+ * rhs = -R(u) with zero_constraints (constrained rows 0). DEVICE pointer, length n_dofs. */
+int gls_residual(gls_ctx *ctx, double *rhs);
+
+/* Matrix-free action of the reference's assembled Jacobian (assembleGLS<true,...>,
+ * gls_navier_stokes.cc:519-625, distributed with zero_constraints :758-765):
+ * Jv = P J P v + D_c v, D_c = sum over cells of |local(i,i)| on constrained DoFs (deal.II rule).
+ * Replaces system_matrix.vmult inside Trilinos GMRES (gls_navier_stokes.cc:1276-1279). */
+int gls_jacobian_apply(gls_ctx *ctx, const double *v, double *Jv);
+
+/* Diagonal of that assembled Jacobian (DEVICE pointer). */
+int gls_jacobian_diagonal(gls_ctx *ctx, double *diag);
+
+/* Apply nonzero_constraints.distribute to a DEVICE vector: x[dof] = value for listed DoFs
+ * (PhysicsSolver::apply_constraints, physics_solver.h:98-102). Host arrays, copied. */
+int gls_set_dirichlet(gls_ctx *ctx, int64_t n, const int64_t *dofs, const double *values);
+int gls_apply_dirichlet(gls_ctx *ctx, double *x);
+
+/* ------------------------------------------------------------------------------------------
+ * Linear solve: replaces solve_system_GMRES + setup_ILU (gls_navier_stokes.cc:1242-1289,
+ * :1161-1176). Right-preconditioned restarted GMRES on the matrix-free operator with a
+ * Jacobi (diagonal) preconditioner; tolerance = max(rel*||rhs||, abs) as the reference.
+ * x and rhs are DEVICE pointers. Returns GLS_OK or GLS_ENOCONV (x holds the last iterate).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  int max_iterations;     /* linear solver/max iters */
+  int restart;            /* GMRES restart (deal.II default 30) */
+  double relative_residual, minimum_residual;
+  int iterations;         /* out */
+  double final_residual;  /* out */
+} gls_linear_params;
+int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_params *prm);
+
+/* ------------------------------------------------------------------------------------------
+ * Nonlinear solve: NewtonNonLinearSolver::solve (include/core/newton_non_linear_solver.h:74-139)
+ * on device vectors: present (in/out, DEVICE, length n_dofs). History from gls_set_state's u1..u3
+ * slots is given here explicitly.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+  double tolerance;       /* non-linear solver/tolerance */
+  int max_iterations;     /* non-linear solver/max iterations */
+  int verbosity;          /* 0 quiet, 1 verbose (prints the reference's Newton lines) */
+  gls_linear_params lin;
+  int newton_iterations;  /* out */
+  int linear_iterations;  /* out: total */
+  int residual_evaluations; /* out */
+  double final_residual;  /* out */
+} gls_newton_params;
+int gls_newton_solve(gls_ctx *ctx, double *present, const double *u1, const double *u2, const double *u3,
+                     gls_newton_params *prm);
+
+/* ------------------------------------------------------------------------------------------
+ * Host-side building blocks (host pointers).
+ * ------------------------------------------------------------------------------------------ */
+/* bdf_coefficients (source/core/bdf.cc:45-75): alpha[order+1] */
+int gls_bdf_coefficients(int order, const double *dt, int n_dt, double *alpha);
+/* sdirk_coefficients (source/core/sdirk.cc:11-44): out[order*(order+1)] row-major */
+int gls_sdirk_coefficients(int order, double dt, double *out);
+/* Newton driver KAT: the reference's fake physics x0^2+x1=0, 2x1+3=0
+ * (tests/core/non_linear_test_system_01.h:50-129) through the same Newton template. */
+int gls_newton_selftest(double x_out[2]);
+
+/* hyper_cube mesh + canonical DoF numbering (GridGenerator::hyper_cube + refine_global,
+ * source/core/grids.cc:12-60). Periodic directions identify the high face with the low face.
+ * Cells are emitted in Morton (p4est z-)order. Arrays are allocated by the caller with the
+ * sizes from gls_mesh_hyper_cube_sizes. boundary ids: colorize ? 2d / 2d+1 : 0. */
+int gls_mesh_hyper_cube_sizes(int dim, int n, int k, int kp, int periodic_mask,
+                              int64_t *n_cells, int64_t *n_vnodes, int64_t *n_pnodes);
+int gls_mesh_hyper_cube(int dim, int n, int k, int kp, double lo, double hi, int periodic_mask,
+                        int32_t *cell_vnodes, int32_t *cell_pnodes, double *cell_x0, double *cell_h);
+
+/* ------------------------------------------------------------------------------------------
+ * Profiling hooks: time the next operator launches on the context stream with HIP events.
+ * ------------------------------------------------------------------------------------------ */
+int gls_timing_reset(gls_ctx *ctx);
+/* which: 0 residual, 1 jacobian_apply, 2 diagonal; returns total ms and launch count */
+int gls_timing_get(gls_ctx *ctx, int which, double *total_ms, int64_t *count);
+int gls_timing_enable(gls_ctx *ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

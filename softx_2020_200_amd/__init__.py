@@ -1,0 +1,13 @@
+"""softx_2020_200_amd — MI355X-native GLS (SUPG/PSPG) Navier–Stokes hot path.
+
+Drop-in for Lethe's GLSNavierStokesSolver assembly + linear solve path
+(LMNS3d/SOFTX_2020_200 source/solvers/gls_navier_stokes.cc). The compute runs in
+hand-written HIP kernels for gfx950 (libgls_native.so, C-ABI in include/gls_native.h);
+this package is the thin Python front-end over that ABI.
+"""
+from .native import (GLSContext, GLSError, SCHEMES, bdf_coefficients, hyper_cube, load,  # noqa: F401
+                     newton_selftest, sdirk_coefficients)
+from .problem import CavityProblem, build_context  # noqa: F401
+
+__all__ = ["GLSContext", "GLSError", "SCHEMES", "bdf_coefficients", "sdirk_coefficients", "hyper_cube", "load",
+           "newton_selftest", "CavityProblem", "build_context"]

@@ -1,0 +1,945 @@
+// gls_api.cpp — C-ABI implementation: context lifecycle, operator dispatch, GMRES, Newton,
+// hyper_cube mesh and time-integration coefficients. Host C++17 over HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/gls_native.h"
+#include "gls_common.hpp"
+#include "gls_launch.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return set_err(GLS_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+#define GLS_TRY(expr)          \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_ < 0) return r_;     \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  int alloc(size_t count) {
+    release();
+    if (count == 0) return GLS_OK;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+      p = nullptr;
+      return set_err(GLS_ENOMEM, "hipMalloc of %zu bytes failed", count * sizeof(T));
+    }
+    n = count;
+    return GLS_OK;
+  }
+  int upload(const T *h, size_t count) {
+    GLS_TRY(alloc(count));
+    if (count && hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+      return set_err(GLS_EHIP, "upload failed");
+    return GLS_OK;
+  }
+};
+
+// ---------------- time coefficients (host) ----------------
+// Variable-step BDF via divided differences of the backward time levels
+// (restates source/core/bdf.cc:23-75: alpha = sum_j prod_{i<j}(t0-ti) * delta_j).
+void bdf_delta(int p, int n, int j, const double *times, double *out) {
+  if (j == 0) {
+    for (int i = 0; i <= p; ++i) out[i] = 0.;
+    out[n] = 1.;
+    return;
+  }
+  double a[8], b[8];
+  bdf_delta(p, n, j - 1, times, a);
+  bdf_delta(p, n + 1, j - 1, times, b);
+  const double inv = 1.0 / (times[n] - times[n + j]);
+  for (int i = 0; i <= p; ++i) out[i] = (a[i] - b[i]) * inv;
+}
+
+bool is_sdirk(int s) { return s >= GLS_SDIRK2 && s <= GLS_SDIRK3_3; }
+
+}  // namespace
+
+extern "C" {
+
+const char *gls_last_error(void) { return g_err.c_str(); }
+const char *gls_version(void) { return "softx_2020_200_amd 0.1 (gfx950)"; }
+
+int gls_bdf_coefficients(int order, const double *dt, int n_dt, double *alpha) {
+  if (order < 1 || order > 5 || !dt || !alpha || n_dt < order) return set_err(GLS_EINVAL, "bdf order/dt");
+  double times[8];
+  for (int i = 0; i <= order; ++i) {
+    times[i] = 0.;
+    for (int j = 0; j < i; ++j) times[i] -= dt[j];
+  }
+  for (int i = 0; i <= order; ++i) alpha[i] = 0.;
+  double d[8];
+  for (int j = 1; j <= order; ++j) {
+    double factor = 1.;
+    for (int i = 1; i < j; ++i) factor *= times[0] - times[i];
+    bdf_delta(order, 0, j, times, d);
+    for (int i = 0; i <= order; ++i) alpha[i] += factor * d[i];
+  }
+  return GLS_OK;
+}
+
+// SDIRK2 (alpha = 1 - 1/sqrt(2)) and the 3-stage L-stable SDIRK3 tables of source/core/sdirk.cc:11-44,
+// expressed as stage residual coefficients [stage][outcome, step n, intermediate stages...].
+int gls_sdirk_coefficients(int order, double dt, double *c) {
+  if (!c || dt == 0.) return set_err(GLS_EINVAL, "sdirk args");
+  const double sdt = 1. / dt;
+  if (order == 2) {
+    const double a = (2. - std::sqrt(2.)) / 2.;
+    const double v[6] = {1. / a * sdt, -1. / a * sdt, 0., 1. / a * sdt, -(2 * a - 1) / a / a * sdt,
+                         -(1 - a) / a / a * sdt};
+    std::memcpy(c, v, sizeof(v));
+    return GLS_OK;
+  }
+  if (order == 3) {
+    const double g = 2.29428036027904;
+    const double v[12] = {g, -g, 0., 0., g, -0.809559354637498, -1.48472100564154, 0.,
+                          g, 2.87009860433106, -8.55612780155264, 3.39174883694255};
+    for (int i = 0; i < 12; ++i) c[i] = v[i] * sdt;
+    return GLS_OK;
+  }
+  return set_err(GLS_EINVAL, "sdirk order %d", order);
+}
+
+}  // extern "C"
+
+// ============================================================================================
+// FE tables
+// ============================================================================================
+namespace {
+
+void legendre_pd(int n, double x, double &P, double &dP) {
+  double p0 = 1., p1 = x;
+  if (n == 0) { P = 1.; dP = 0.; return; }
+  for (int m = 2; m <= n; ++m) {
+    const double p2 = ((2. * m - 1.) * x * p1 - (m - 1.) * p0) / m;
+    p0 = p1;
+    p1 = p2;
+  }
+  P = p1;
+  dP = n * (x * p1 - p0) / (x * x - 1.);
+}
+
+// QGauss(n) on [0,1]: Newton on the Legendre roots, ascending.
+void gauss_points(int n, double *x, double *w) {
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), P, dP;
+    for (int it = 0; it < 100; ++it) {
+      legendre_pd(n, z, P, dP);
+      const double dz = P / dP;
+      z -= dz;
+      if (std::fabs(dz) < 1e-17) break;
+    }
+    legendre_pd(n, z, P, dP);
+    x[n - 1 - i] = 0.5 * (1. + z);
+    w[n - 1 - i] = 1. / ((1. - z * z) * dP * dP);
+  }
+}
+
+// FE_Q support points (Gauss–Lobatto) on [0,1]
+void lobatto_points(int k, double *x) {
+  x[0] = 0.;
+  x[k] = 1.;
+  for (int i = 1; i < k; ++i) {
+    double z = -std::cos(M_PI * i / k);
+    for (int it = 0; it < 100; ++it) {
+      double P, dP;
+      legendre_pd(k, z, P, dP);
+      const double d2P = (2. * z * dP - k * (k + 1.) * P) / (1. - z * z);
+      const double dz = dP / d2P;
+      z -= dz;
+      if (std::fabs(dz) < 1e-17) break;
+    }
+    x[i] = 0.5 * (1. + z);
+  }
+  if (k == 2) x[1] = 0.5;
+}
+
+// Lagrange basis i on nodes xn (degree k): value, first and second derivative at s,
+// via the barycentric-style product expansions.
+void lagrange_1d(int k, const double *xn, int i, double s, double &v, double &d, double &dd) {
+  v = 1.;
+  d = 0.;
+  dd = 0.;
+  for (int j = 0; j <= k; ++j)
+    if (j != i) v *= (s - xn[j]) / (xn[i] - xn[j]);
+  for (int m = 0; m <= k; ++m) {
+    if (m == i) continue;
+    double t = 1. / (xn[i] - xn[m]);
+    for (int j = 0; j <= k; ++j)
+      if (j != i && j != m) t *= (s - xn[j]) / (xn[i] - xn[j]);
+    d += t;
+    for (int l = 0; l <= k; ++l) {
+      if (l == i || l == m) continue;
+      double t2 = 1. / ((xn[i] - xn[m]) * (xn[i] - xn[l]));
+      for (int j = 0; j <= k; ++j)
+        if (j != i && j != m && j != l) t2 *= (s - xn[j]) / (xn[i] - xn[j]);
+      dd += t2;
+    }
+  }
+}
+
+gls::Tables1D make_tables(int k, int kp, int nq1d) {
+  gls::Tables1D T;
+  std::memset(&T, 0, sizeof(T));
+  double xq[gls::kMaxQ1D], wq[gls::kMaxQ1D], xv[gls::kMaxNodes1D], xp[gls::kMaxNodes1D];
+  gauss_points(nq1d, xq, wq);
+  lobatto_points(k, xv);
+  lobatto_points(kp, xp);
+  for (int q = 0; q < nq1d; ++q) {
+    T.w[q] = wq[q];
+    T.xi[q] = xq[q];
+    for (int a = 0; a <= k; ++a) lagrange_1d(k, xv, a, xq[q], T.V[q][a], T.D[q][a], T.S[q][a]);
+    for (int a = 0; a <= kp; ++a) {
+      double dd;
+      lagrange_1d(kp, xp, a, xq[q], T.Vp[q][a], T.Dp[q][a], dd);
+    }
+  }
+  return T;
+}
+
+}  // namespace
+
+// ============================================================================================
+// context
+// ============================================================================================
+struct gls_ctx {
+  int dim = 0, k = 0, kp = 0, nq1d = 0, n_cells = 0, n_vnodes = 0, n_pnodes = 0, nq = 0;
+  int64_t n_dofs = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  gls::Tables1D tables;
+  DevBuf<int32_t> cell_vnodes, cell_pnodes;
+  DevBuf<double> geo, x0, force_q;
+  DevBuf<uint8_t> vmask;
+  DevBuf<int64_t> con_dofs;  // zero_constraints DoF list
+  DevBuf<int64_t> dir_dofs;  // nonzero_constraints (Dirichlet) list
+  DevBuf<double> dir_vals;
+  double viscosity = 1.0;
+  int srf = 0;
+  double omega[3] = {0, 0, 0};
+  // time state
+  int scheme = GLS_STEADY;
+  double alpha[4] = {0, 0, 0, 0}, alpha_jac = 0., sdt2 = 0.;
+  int n_hist = 0;
+  // evaluation state (borrowed device pointers)
+  const double *u = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;
+  DevBuf<double> diag;  // diagonal at the current state (also D_c for constrained rows)
+  bool diag_valid = false;
+  // solver workspace
+  DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
+  DevBuf<double> krylov;      // (restart+1) x n_dofs
+  int krylov_m = 0;
+  DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
+  // timing
+  bool timing = false;
+  struct Ev { int which; hipEvent_t a, b; };
+  std::vector<Ev> events;
+  double t_ms[3] = {0, 0, 0};
+  int64_t t_n[3] = {0, 0, 0};
+
+  ~gls_ctx() {
+    for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+int check_ctx(gls_ctx *c) {
+  if (!c) return set_err(GLS_EINVAL, "null context");
+  return GLS_OK;
+}
+
+gls::OpParams make_params(gls_ctx *c) {
+  gls::OpParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.n_cells = c->n_cells;
+  P.n_vnodes = c->n_vnodes;
+  P.n_pnodes = c->n_pnodes;
+  P.n_hist = c->n_hist;
+  P.cell_vnodes = c->cell_vnodes.p;
+  P.cell_pnodes = c->cell_pnodes.p;
+  P.geo = c->geo.p;
+  P.x0 = c->x0.p;
+  P.force_q = c->force_q.p;
+  P.vmask = c->vmask.p;
+  P.u = c->u;
+  P.h1 = c->u1 ? c->u1 : c->u;
+  P.h2 = c->u2 ? c->u2 : c->u;
+  P.h3 = c->u3 ? c->u3 : c->u;
+  P.nu = c->viscosity;
+  for (int i = 0; i < 4; ++i) P.alpha[i] = c->alpha[i];
+  P.alpha_jac = c->alpha_jac;
+  P.sdt2 = c->sdt2;
+  P.srf = c->srf;
+  for (int i = 0; i < 3; ++i) P.omega[i] = c->omega[i];
+  return P;
+}
+
+struct TimedLaunch {
+  gls_ctx *c;
+  int which;
+  hipEvent_t a = nullptr, b = nullptr;
+  TimedLaunch(gls_ctx *c_, int w) : c(c_), which(w) {
+    if (c->timing) {
+      (void)hipEventCreate(&a);
+      (void)hipEventCreate(&b);
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~TimedLaunch() {
+    if (c->timing) {
+      (void)hipEventRecord(b, c->stream);
+      c->events.push_back({which, a, b});
+    }
+  }
+};
+
+int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
+  if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
+  if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
+  if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
+  gls::OpParams P = make_params(c);
+  P.v = v;
+  P.y = y;
+  HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
+  {
+    TimedLaunch t(c, mode);
+    HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+  }
+  return GLS_OK;
+}
+
+int ensure_diag(gls_ctx *c) {
+  if (c->diag_valid) return GLS_OK;
+  GLS_TRY(run_cell(c, gls::MODE_DIAG, nullptr, c->diag.p));
+  c->diag_valid = true;
+  return GLS_OK;
+}
+
+int device_dot(gls_ctx *c, const double *a, const double *b, double *host_out) {
+  HIP_TRY(gls::vec_multidot(a, 0, 1, b, c->n_dofs, c->scal.p, c->work.p, c->stream));
+  HIP_TRY(hipMemcpyAsync(host_out, c->scal.p, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
+  if (!d || !out) return set_err(GLS_EINVAL, "null argument");
+  *out = nullptr;
+  const int nq1d = d->nq1d > 0 ? d->nq1d : d->k + 1;
+  if (d->dim != 2 && d->dim != 3) return set_err(GLS_EINVAL, "dim must be 2 or 3");
+  if (!gls::cell_kernel_supported(d->dim, d->k, d->kp, nq1d))
+    return set_err(GLS_EINVAL, "unsupported element Q%d-Q%d (dim %d, QGauss %d)", d->k, d->kp, d->dim, nq1d);
+  if (d->n_cells < 0 || d->n_vnodes <= 0 || d->n_pnodes <= 0 || !d->cell_vnodes || !d->cell_h)
+    return set_err(GLS_EINVAL, "incomplete mesh description");
+  if (d->kp != d->k && !d->cell_pnodes) return set_err(GLS_EINVAL, "cell_pnodes required when kp != k");
+  if (d->srf && !d->cell_x0) return set_err(GLS_EINVAL, "srf requires cell_x0");
+  std::unique_ptr<gls_ctx> c(new gls_ctx);
+  c->dim = d->dim;
+  c->k = d->k;
+  c->kp = d->kp;
+  c->nq1d = nq1d;
+  c->n_cells = d->n_cells;
+  c->n_vnodes = d->n_vnodes;
+  c->n_pnodes = d->n_pnodes;
+  c->nq = gls::ipow(nq1d, d->dim);
+  c->n_dofs = (int64_t)d->dim * d->n_vnodes + d->n_pnodes;
+  c->viscosity = d->viscosity;
+  c->srf = d->srf;
+  for (int i = 0; i < 3; ++i) c->omega[i] = d->omega[i];
+  c->tables = make_tables(d->k, d->kp, nq1d);
+  const int nv = gls::ipow(d->k + 1, d->dim), np = gls::ipow(d->kp + 1, d->dim);
+  // validate indices
+  for (int64_t i = 0; i < (int64_t)d->n_cells * nv; ++i)
+    if (d->cell_vnodes[i] < 0 || d->cell_vnodes[i] >= d->n_vnodes) return set_err(GLS_EINVAL, "cell_vnodes out of range");
+  if (d->cell_pnodes)
+    for (int64_t i = 0; i < (int64_t)d->n_cells * np; ++i)
+      if (d->cell_pnodes[i] < 0 || d->cell_pnodes[i] >= d->n_pnodes) return set_err(GLS_EINVAL, "cell_pnodes out of range");
+  if (!d->cell_pnodes && d->n_pnodes != d->n_vnodes) return set_err(GLS_EINVAL, "n_pnodes != n_vnodes without cell_pnodes");
+
+  GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
+  if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
+  std::vector<double> geo((size_t)d->n_cells * 4);
+  for (int cix = 0; cix < d->n_cells; ++cix) {
+    double meas = 1.;
+    for (int e = 0; e < d->dim; ++e) {
+      geo[cix * 4 + e] = d->cell_h[(size_t)cix * d->dim + e];
+      meas *= geo[cix * 4 + e];
+    }
+    if (d->dim == 2) geo[cix * 4 + 2] = 1.0;
+    // element size for tau (gls_navier_stokes.cc:340-345)
+    geo[cix * 4 + 3] = d->dim == 2 ? std::sqrt(4. * meas / M_PI) / d->k : std::pow(6 * meas / M_PI, 1. / 3.) / d->k;
+  }
+  GLS_TRY(c->geo.upload(geo.data(), geo.size()));
+  if (d->cell_x0) {
+    std::vector<double> x0((size_t)d->n_cells * 3, 0.);
+    for (int cix = 0; cix < d->n_cells; ++cix)
+      for (int e = 0; e < d->dim; ++e) x0[cix * 3 + e] = d->cell_x0[(size_t)cix * d->dim + e];
+    GLS_TRY(c->x0.upload(x0.data(), x0.size()));
+  }
+  if (d->force_q) GLS_TRY(c->force_q.upload(d->force_q, (size_t)d->n_cells * c->nq * d->dim));
+  std::vector<int64_t> con;
+  if (d->vnode_mask) {
+    GLS_TRY(c->vmask.upload(d->vnode_mask, (size_t)d->n_vnodes));
+    for (int64_t n = 0; n < d->n_vnodes; ++n)
+      for (int e = 0; e < d->dim; ++e)
+        if ((d->vnode_mask[n] >> e) & 1) con.push_back(n * d->dim + e);
+  }
+  GLS_TRY(c->con_dofs.upload(con.data(), con.size()));
+  GLS_TRY(c->diag.alloc(c->n_dofs));
+  GLS_TRY(c->work.alloc(gls::multidot_work_size()));
+  GLS_TRY(c->scal.alloc(64));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return set_err(GLS_EHIP, "stream create failed");
+  c->own_stream = true;
+  HIP_TRY(hipDeviceSynchronize());
+  *out = c.release();
+  return GLS_OK;
+}
+
+int gls_destroy(gls_ctx *c) {
+  if (!c) return GLS_OK;
+  (void)hipStreamSynchronize(c->stream);
+  delete c;
+  return GLS_OK;
+}
+
+int gls_set_stream(gls_ctx *c, void *s) {
+  GLS_TRY(check_ctx(c));
+  if (c->own_stream && c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  c->own_stream = false;
+  c->stream = (hipStream_t)s;
+  return GLS_OK;
+}
+
+int gls_n_dofs(const gls_ctx *c, int64_t *n) {
+  if (!c || !n) return set_err(GLS_EINVAL, "null argument");
+  *n = c->n_dofs;
+  return GLS_OK;
+}
+
+int gls_set_force(gls_ctx *c, const double *f) {
+  GLS_TRY(check_ctx(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (!f) {
+    c->force_q.release();
+  } else {
+    GLS_TRY(c->force_q.upload(f, (size_t)c->n_cells * c->nq * c->dim));
+  }
+  c->diag_valid = false;
+  return GLS_OK;
+}
+
+int gls_set_viscosity(gls_ctx *c, double nu) {
+  GLS_TRY(check_ctx(c));
+  c->viscosity = nu;
+  c->diag_valid = false;
+  return GLS_OK;
+}
+
+// assembleGLS preamble: gls_navier_stokes.cc:295-329 and the scheme branches :477-516, :530-533
+int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
+  GLS_TRY(check_ctx(c));
+  if (scheme < GLS_STEADY || scheme > GLS_SDIRK3_3) return set_err(GLS_EINVAL, "scheme %d", scheme);
+  if (scheme != GLS_STEADY && (!ts || ts[0] == 0.)) return set_err(GLS_EINVAL, "time steps required");
+  c->scheme = scheme;
+  for (double &a : c->alpha) a = 0.;
+  c->alpha_jac = 0.;
+  c->sdt2 = 0.;
+  c->n_hist = 0;
+  if (scheme != GLS_STEADY) {
+    const double sdt = 1. / ts[0];
+    c->sdt2 = sdt * sdt;
+  }
+  if (scheme == GLS_BDF1 || scheme == GLS_BDF2 || scheme == GLS_BDF3) {
+    const int order = scheme - GLS_BDF1 + 1;
+    double a[6];
+    GLS_TRY(gls_bdf_coefficients(order, ts, 4, a));
+    for (int i = 0; i <= order; ++i) c->alpha[i] = a[i];
+    c->alpha_jac = a[0];
+    c->n_hist = order;
+  } else if (is_sdirk(scheme)) {
+    const bool three = scheme == GLS_SDIRK3 || scheme == GLS_SDIRK3_1 || scheme == GLS_SDIRK3_2 || scheme == GLS_SDIRK3_3;
+    const int order = three ? 3 : 2;
+    double t[12];
+    GLS_TRY(gls_sdirk_coefficients(order, ts[0], t));
+    int stage = 0;  // sdirk2 / sdirk3 (no stage) contribute no time term, like the reference
+    if (scheme == GLS_SDIRK2_1 || scheme == GLS_SDIRK3_1) stage = 1;
+    if (scheme == GLS_SDIRK2_2 || scheme == GLS_SDIRK3_2) stage = 2;
+    if (scheme == GLS_SDIRK3_3) stage = 3;
+    c->alpha_jac = t[0];
+    if (stage > 0) {
+      for (int i = 0; i <= stage; ++i) c->alpha[i] = t[(stage - 1) * (order + 1) + i];
+      c->n_hist = stage;
+    }
+  }
+  c->diag_valid = false;
+  return GLS_OK;
+}
+
+int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u2, const double *u3) {
+  GLS_TRY(check_ctx(c));
+  if (!u) return set_err(GLS_EINVAL, "u is null");
+  c->u = u;
+  c->u1 = u1;
+  c->u2 = u2;
+  c->u3 = u3;
+  c->diag_valid = false;
+  return GLS_OK;
+}
+
+int gls_residual(gls_ctx *c, double *rhs) {
+  GLS_TRY(check_ctx(c));
+  if (!rhs) return set_err(GLS_EINVAL, "rhs is null");
+  GLS_TRY(run_cell(c, gls::MODE_RESIDUAL, nullptr, rhs));
+  HIP_TRY(gls::vec_set_indexed(rhs, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, c->stream));
+  return GLS_OK;
+}
+
+int gls_jacobian_diagonal(gls_ctx *c, double *d) {
+  GLS_TRY(check_ctx(c));
+  GLS_TRY(ensure_diag(c));
+  if (d && d != c->diag.p) HIP_TRY(gls::vec_copy(d, c->diag.p, c->n_dofs, c->stream));
+  return GLS_OK;
+}
+
+int gls_jacobian_apply(gls_ctx *c, const double *v, double *y) {
+  GLS_TRY(check_ctx(c));
+  if (!v || !y || v == y) return set_err(GLS_EINVAL, "v/y null or aliased");
+  if (c->con_dofs.n) GLS_TRY(ensure_diag(c));
+  GLS_TRY(run_cell(c, gls::MODE_JV, v, y));
+  HIP_TRY(gls::vec_gather_scale_set(y, c->diag.p, v, c->con_dofs.p, (int64_t)c->con_dofs.n, c->stream));
+  return GLS_OK;
+}
+
+int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *vals) {
+  GLS_TRY(check_ctx(c));
+  if (n < 0 || (n > 0 && (!dofs || !vals))) return set_err(GLS_EINVAL, "dirichlet arrays");
+  for (int64_t i = 0; i < n; ++i)
+    if (dofs[i] < 0 || dofs[i] >= c->n_dofs) return set_err(GLS_EINVAL, "dirichlet dof out of range");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  GLS_TRY(c->dir_dofs.upload(dofs, (size_t)n));
+  GLS_TRY(c->dir_vals.upload(vals, (size_t)n));
+  return GLS_OK;
+}
+
+int gls_apply_dirichlet(gls_ctx *c, double *x) {
+  GLS_TRY(check_ctx(c));
+  HIP_TRY(gls::vec_set_indexed(x, c->dir_dofs.p, c->dir_vals.p, (int64_t)c->dir_dofs.n, c->stream));
+  return GLS_OK;
+}
+
+// --------------------------------------------------------------------------------------------
+// GMRES(m), right preconditioned by the Jacobian diagonal. Classical Gram–Schmidt with one
+// DGKS re-orthogonalisation pass; fused multi-dot / multi-axpy kernels (one pass over the
+// Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
+// ||b - A x|| <= max(rel*||b||, abs) (deal.II SolverControl / AztecOO AZ_noscaled).
+// --------------------------------------------------------------------------------------------
+int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *prm) {
+  GLS_TRY(check_ctx(c));
+  if (!b || !x || !prm) return set_err(GLS_EINVAL, "null argument");
+  const int m = prm->restart > 0 ? std::min(prm->restart, 200) : 30;
+  const int64_t n = c->n_dofs;
+  if (c->krylov_m != m || !c->krylov.p) {
+    GLS_TRY(c->krylov.alloc((size_t)(m + 1) * n));
+    GLS_TRY(c->coef.alloc((size_t)m + 8));
+    if (c->scal.n < (size_t)m + 8) GLS_TRY(c->scal.alloc((size_t)m + 8));
+    c->krylov_m = m;
+  }
+  if (!c->tmp1.p) {
+    GLS_TRY(c->tmp1.alloc(n));
+    GLS_TRY(c->tmp2.alloc(n));
+  }
+  GLS_TRY(ensure_diag(c));
+  double *V = c->krylov.p, *z = c->tmp1.p, *r = c->tmp2.p;
+  const double *dg = c->diag.p;
+  hipStream_t s = c->stream;
+  double bnorm2;
+  GLS_TRY(device_dot(c, b, b, &bnorm2));
+  const double tol = std::max(prm->relative_residual * std::sqrt(bnorm2), prm->minimum_residual);
+  HIP_TRY(gls::vec_fill(x, n, 0.0, s));
+  HIP_TRY(gls::vec_copy(r, b, n, s));
+  double beta = std::sqrt(bnorm2);
+  int it = 0;
+  std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hcol(m + 2), y(m);
+  bool converged = beta <= tol;
+  while (!converged && it < prm->max_iterations) {
+    HIP_TRY(gls::vec_axpby(V, 1.0 / beta, r, 0.0, n, s));
+    std::fill(g.begin(), g.end(), 0.);
+    g[0] = beta;
+    int j = 0;
+    double res = beta;
+    for (; j < m && it < prm->max_iterations; ++j) {
+      double *vj = V + (int64_t)j * n, *w = V + (int64_t)(j + 1) * n;
+      HIP_TRY(gls::vec_div(z, vj, dg, n, s));
+      GLS_TRY(gls_jacobian_apply(c, z, w));
+      // h = V[0..j]^T w and ||w||^2 in one pass
+      HIP_TRY(gls::vec_multidot(V, n, j + 2, w, n, c->scal.p, c->work.p, s));
+      HIP_TRY(hipMemcpyAsync(hcol.data(), c->scal.p, sizeof(double) * (j + 2), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      const double wnorm0 = std::sqrt(std::max(hcol[j + 1], 0.0));
+      for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hcol[i];
+      HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+      HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
+      double wn2;
+      GLS_TRY(device_dot(c, w, w, &wn2));
+      double wnorm = std::sqrt(std::max(wn2, 0.0));
+      if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation
+        HIP_TRY(gls::vec_multidot(V, n, j + 1, w, n, c->scal.p, c->work.p, s));
+        HIP_TRY(hipMemcpyAsync(hcol.data(), c->scal.p, sizeof(double) * (j + 1), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hcol[i];
+        HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+        HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
+        GLS_TRY(device_dot(c, w, w, &wn2));
+        wnorm = std::sqrt(std::max(wn2, 0.0));
+      }
+      H[(size_t)(j + 1) * m + j] = wnorm;
+      if (wnorm > 0) HIP_TRY(gls::vec_scale(w, 1.0 / wnorm, n, s));
+      // Givens
+      for (int i = 0; i < j; ++i) {
+        const double a = H[(size_t)i * m + j], bb = H[(size_t)(i + 1) * m + j];
+        H[(size_t)i * m + j] = cs[i] * a + sn[i] * bb;
+        H[(size_t)(i + 1) * m + j] = -sn[i] * a + cs[i] * bb;
+      }
+      const double a = H[(size_t)j * m + j], bb = H[(size_t)(j + 1) * m + j];
+      const double rr = std::hypot(a, bb);
+      cs[j] = rr > 0 ? a / rr : 1.0;
+      sn[j] = rr > 0 ? bb / rr : 0.0;
+      H[(size_t)j * m + j] = rr;
+      H[(size_t)(j + 1) * m + j] = 0.;
+      g[j + 1] = -sn[j] * g[j];
+      g[j] = cs[j] * g[j];
+      res = std::fabs(g[j + 1]);
+      ++it;
+      if (res <= tol || wnorm == 0.) { ++j; break; }
+    }
+    // back substitution and update x += M^{-1} V y
+    const int kdim = j;
+    for (int i = kdim - 1; i >= 0; --i) {
+      double s_ = g[i];
+      for (int l = i + 1; l < kdim; ++l) s_ -= H[(size_t)i * m + l] * y[l];
+      y[i] = H[(size_t)i * m + i] != 0. ? s_ / H[(size_t)i * m + i] : 0.;
+    }
+    HIP_TRY(hipMemcpyAsync(c->coef.p, y.data(), sizeof(double) * kdim, hipMemcpyHostToDevice, s));
+    HIP_TRY(gls::vec_fill(r, n, 0.0, s));
+    HIP_TRY(gls::vec_multiaxpy(r, V, n, kdim, c->coef.p, -1.0, n, s));  // r = V y
+    HIP_TRY(gls::vec_div(z, r, dg, n, s));
+    HIP_TRY(gls::vec_axpy(x, 1.0, z, n, s));
+    // true residual r = b - A x
+    GLS_TRY(gls_jacobian_apply(c, x, r));
+    HIP_TRY(gls::vec_axpby(r, 1.0, b, -1.0, n, s));
+    double rn2;
+    GLS_TRY(device_dot(c, r, r, &rn2));
+    beta = std::sqrt(rn2);
+    converged = beta <= tol;
+    if (beta == 0.) break;
+  }
+  prm->iterations = it;
+  prm->final_residual = beta;
+  if (!converged) return set_err(GLS_ENOCONV, "GMRES: %d iterations, residual %.3e > %.3e", it, beta, tol);
+  return GLS_OK;
+}
+
+// --------------------------------------------------------------------------------------------
+// NewtonNonLinearSolver::solve (include/core/newton_non_linear_solver.h:74-139), one template
+// driving any "physics" with the PhysicsSolver hooks (include/core/physics_solver.h:64-102).
+// --------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+struct NewtonStats {
+  int outer = 0, linear = 0, residuals = 0;
+  double final_res = 0.;
+};
+
+template <class Phys>
+int newton_template(Phys &ph, double tolerance, int max_iterations, int verbosity, NewtonStats &st) {
+  double current_res = 1.0, last_res = 1.0;
+  int outer = 0;
+  while (current_res > tolerance && outer < max_iterations) {
+    GLS_TRY(ph.evaluation_point_from_present());          // evaluation_point = present_solution
+    GLS_TRY(ph.assemble_matrix_and_rhs());
+    ++st.residuals;
+    if (outer == 0) {
+      GLS_TRY(ph.rhs_norm(current_res));
+      last_res = current_res;
+    }
+    if (verbosity) printf("Newton iteration: %d  - Residual:  %g\n", outer, current_res);
+    int lin_it = 0;
+    GLS_TRY(ph.solve_linear_system(lin_it));
+    st.linear += lin_it;
+    for (double alpha = 1.0; alpha > 1e-3; alpha *= 0.5) {
+      GLS_TRY(ph.line_point(alpha));  // local_eval = present + alpha*update; apply_constraints; eval = local_eval
+      GLS_TRY(ph.assemble_rhs());
+      ++st.residuals;
+      GLS_TRY(ph.rhs_norm(current_res));
+      if (verbosity) printf("\t\talpha = %6g res = %g\n", alpha, current_res);
+      if (current_res < 0.9 * last_res || last_res < tolerance) break;
+    }
+    GLS_TRY(ph.present_from_evaluation_point());  // present_solution = evaluation_point
+    last_res = current_res;
+    ++outer;
+  }
+  st.outer = outer;
+  st.final_res = current_res;
+  return GLS_OK;
+}
+
+// GLS physics on device vectors (the GLSNavierStokesSolver side of the plugin API)
+struct DevicePhysics {
+  gls_ctx *c;
+  double *present, *eval, *update, *rhs;
+  const double *u1, *u2, *u3;
+  gls_linear_params lin;
+  int verbosity;
+  int evaluation_point_from_present() {
+    HIP_TRY(gls::vec_copy(eval, present, c->n_dofs, c->stream));
+    return gls_set_state(c, eval, u1, u2, u3);
+  }
+  int assemble_matrix_and_rhs() {  // matrix-free: residual + the Jacobian diagonal at this state
+    GLS_TRY(gls_residual(c, rhs));
+    return ensure_diag(c);
+  }
+  int assemble_rhs() { return gls_residual(c, rhs); }
+  int rhs_norm(double &r) {
+    double r2;
+    GLS_TRY(device_dot(c, rhs, rhs, &r2));
+    r = std::sqrt(r2);
+    return GLS_OK;
+  }
+  int solve_linear_system(int &its) {
+    gls_linear_params lp = lin;
+    const int rc = gls_solve_linear(c, rhs, update, &lp);
+    if (rc < 0 && rc != GLS_ENOCONV) return rc;
+    its = lp.iterations;
+    if (verbosity) printf("  -Iterative solver took : %d steps \n", lp.iterations);
+    // zero_constraints.distribute(solution): constrained entries of the update are 0
+    HIP_TRY(gls::vec_set_indexed(update, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, c->stream));
+    return GLS_OK;
+  }
+  int line_point(double alpha) {
+    HIP_TRY(gls::vec_copy(eval, present, c->n_dofs, c->stream));
+    HIP_TRY(gls::vec_axpy(eval, alpha, update, c->n_dofs, c->stream));
+    GLS_TRY(gls_apply_dirichlet(c, eval));  // nonzero_constraints.distribute
+    return gls_set_state(c, eval, u1, u2, u3);
+  }
+  int present_from_evaluation_point() {
+    HIP_TRY(gls::vec_copy(present, eval, c->n_dofs, c->stream));
+    return GLS_OK;
+  }
+};
+
+// the reference's fake physics (tests/core/non_linear_test_system_01.h:50-129)
+struct KatPhysics {
+  double present[2] = {1., 0.}, eval[2] = {0, 0}, update[2] = {0, 0}, rhs[2] = {0, 0};
+  double J[2][2] = {{0, 0}, {0, 0}};
+  int evaluation_point_from_present() { eval[0] = present[0]; eval[1] = present[1]; return GLS_OK; }
+  int assemble_matrix_and_rhs() {
+    J[0][0] = 2 * eval[0]; J[0][1] = 1; J[1][0] = 0; J[1][1] = 2;
+    return assemble_rhs();
+  }
+  int assemble_rhs() {
+    rhs[0] = -(eval[0] * eval[0] + eval[1]);
+    rhs[1] = -(2 * eval[1] + 3);
+    return GLS_OK;
+  }
+  int rhs_norm(double &r) { r = std::sqrt(rhs[0] * rhs[0] + rhs[1] * rhs[1]); return GLS_OK; }
+  int solve_linear_system(int &its) {
+    const double det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    if (det == 0.) return set_err(GLS_EINVAL, "singular KAT Jacobian");
+    update[0] = (rhs[0] * J[1][1] - J[0][1] * rhs[1]) / det;
+    update[1] = (J[0][0] * rhs[1] - J[1][0] * rhs[0]) / det;
+    its = 1;
+    return GLS_OK;
+  }
+  int line_point(double a) { eval[0] = present[0] + a * update[0]; eval[1] = present[1] + a * update[1]; return GLS_OK; }
+  int present_from_evaluation_point() { present[0] = eval[0]; present[1] = eval[1]; return GLS_OK; }
+};
+
+}  // namespace
+
+extern "C" {
+
+int gls_newton_solve(gls_ctx *c, double *present, const double *u1, const double *u2, const double *u3,
+                     gls_newton_params *prm) {
+  GLS_TRY(check_ctx(c));
+  if (!present || !prm) return set_err(GLS_EINVAL, "null argument");
+  const int64_t n = c->n_dofs;
+  if (!c->tmp3.p) {
+    GLS_TRY(c->tmp3.alloc(n));  // evaluation_point
+    GLS_TRY(c->tmp4.alloc(n));  // newton_update
+    GLS_TRY(c->tmp5.alloc(n));  // system_rhs
+  }
+  DevicePhysics ph{c, present, c->tmp3.p, c->tmp4.p, c->tmp5.p, u1, u2, u3, prm->lin, prm->verbosity};
+  NewtonStats st;
+  GLS_TRY(newton_template(ph, prm->tolerance, prm->max_iterations, prm->verbosity, st));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prm->newton_iterations = st.outer;
+  prm->linear_iterations = st.linear;
+  prm->residual_evaluations = st.residuals;
+  prm->final_residual = st.final_res;
+  return GLS_OK;
+}
+
+// Newton KAT (tests/core/newton_non_linear_solver_01.cc: tol 1e-8, max 10 iterations)
+int gls_newton_selftest(double xo[2]) {
+  if (!xo) return set_err(GLS_EINVAL, "null");
+  KatPhysics ph;
+  NewtonStats st;
+  GLS_TRY(newton_template(ph, 1e-8, 10, 0, st));
+  xo[0] = ph.present[0];
+  xo[1] = ph.present[1];
+  return GLS_OK;
+}
+
+// --------------------------------------------------------------------------------------------
+// hyper_cube + refine_global, Morton (z-order) cells, lexicographic nodes
+// --------------------------------------------------------------------------------------------
+int gls_mesh_hyper_cube_sizes(int dim, int n, int k, int kp, int pmask, int64_t *nc, int64_t *nv, int64_t *np) {
+  if ((dim != 2 && dim != 3) || n <= 0 || k <= 0 || kp <= 0) return set_err(GLS_EINVAL, "mesh args");
+  int64_t c = 1, v = 1, p = 1;
+  for (int d = 0; d < dim; ++d) {
+    const bool per = (pmask >> d) & 1;
+    c *= n;
+    v *= (int64_t)k * n + (per ? 0 : 1);
+    p *= (int64_t)kp * n + (per ? 0 : 1);
+  }
+  if (nc) *nc = c;
+  if (nv) *nv = v;
+  if (np) *np = p;
+  return GLS_OK;
+}
+
+int gls_mesh_hyper_cube(int dim, int n, int k, int kp, double lo, double hi, int pmask, int32_t *cv, int32_t *cp,
+                        double *x0, double *h) {
+  int64_t nc, nv, np;
+  GLS_TRY(gls_mesh_hyper_cube_sizes(dim, n, k, kp, pmask, &nc, &nv, &np));
+  if (nv > INT32_MAX || np > INT32_MAX) return set_err(GLS_EINVAL, "mesh too large for int32 node ids");
+  int L = 0;
+  while ((1 << L) < n) ++L;
+  const double hc = (hi - lo) / n;
+  int vsh[3], psh[3];
+  for (int d = 0; d < 3; ++d) {
+    const bool per = (pmask >> d) & 1;
+    vsh[d] = k * n + (per ? 0 : 1);
+    psh[d] = kp * n + (per ? 0 : 1);
+  }
+  const int nvl = gls::ipow(k + 1, dim), npl = gls::ipow(kp + 1, dim);
+  int64_t cell = 0;
+  const int64_t total = (int64_t)1 << (dim * L);
+  for (int64_t mcode = 0; mcode < total; ++mcode) {
+    int ijk[3] = {0, 0, 0};
+    for (int b = 0; b < L; ++b)
+      for (int d = 0; d < dim; ++d) ijk[d] |= (int)((mcode >> (b * dim + d)) & 1) << b;
+    bool inside = true;
+    for (int d = 0; d < dim; ++d) inside = inside && ijk[d] < n;
+    if (!inside) continue;
+    for (int a = 0; a < nvl; ++a) {
+      int loc[3] = {a % (k + 1), (a / (k + 1)) % (k + 1), a / ((k + 1) * (k + 1))};
+      int64_t id = 0, stride = 1;
+      for (int d = 0; d < dim; ++d) {
+        id += (int64_t)((ijk[d] * k + loc[d]) % vsh[d]) * stride;
+        stride *= vsh[d];
+      }
+      cv[cell * nvl + a] = (int32_t)id;
+    }
+    if (cp) {
+      for (int a = 0; a < npl; ++a) {
+        int loc[3] = {a % (kp + 1), (a / (kp + 1)) % (kp + 1), a / ((kp + 1) * (kp + 1))};
+        int64_t id = 0, stride = 1;
+        for (int d = 0; d < dim; ++d) {
+          id += (int64_t)((ijk[d] * kp + loc[d]) % psh[d]) * stride;
+          stride *= psh[d];
+        }
+        cp[cell * npl + a] = (int32_t)id;
+      }
+    }
+    for (int d = 0; d < dim; ++d) {
+      if (x0) x0[cell * dim + d] = lo + ijk[d] * hc;
+      if (h) h[cell * dim + d] = hc;
+    }
+    ++cell;
+  }
+  return cell == nc ? GLS_OK : set_err(GLS_EINVAL, "morton enumeration mismatch");
+}
+
+// --------------------------------------------------------------------------------------------
+// timing
+// --------------------------------------------------------------------------------------------
+int gls_timing_enable(gls_ctx *c, int en) {
+  GLS_TRY(check_ctx(c));
+  c->timing = en != 0;
+  return GLS_OK;
+}
+int gls_timing_reset(gls_ctx *c) {
+  GLS_TRY(check_ctx(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto &e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  c->events.clear();
+  for (int i = 0; i < 3; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
+  return GLS_OK;
+}
+int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
+  GLS_TRY(check_ctx(c));
+  if (which < 0 || which > 2) return set_err(GLS_EINVAL, "which");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto &e : c->events) {
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, e.a, e.b));
+    c->t_ms[e.which] += t;
+    c->t_n[e.which] += 1;
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  c->events.clear();
+  if (ms) *ms = c->t_ms[which];
+  if (cnt) *cnt = c->t_n[which];
+  return GLS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,464 @@
+// gls_cell_kernels.hip — per-cell GLS (SUPG/PSPG) Navier–Stokes operators for gfx950.
+//
+// One workgroup = a batch of CB cells (CB*NQ <= 256 threads: Q2 3D -> 9 cells x 27 q).
+// Phases (all in one launch):
+//   1. gather   : cell->node index rows (coalesced int32 reads) -> DoF values of u, history,
+//                 and v (JV) into LDS, Dirichlet columns masked (P v).
+//   2. evaluate : one thread per (cell, q): dense basis x coefficient contraction over the
+//                 cell's nodes; the Qk basis is formed from 1D tables staged in LDS
+//                 (tensor product), so no n_dofs x n_q table is read from memory.
+//   3. pointwise: tau, strong residual R_s, S(v) and the test-function coefficients
+//                 (restated from gls_navier_stokes.cc:387-748, Appendix A of SURVEY.md).
+//   4. integrate: one thread per (cell, node): transposed contraction sum_q B^T coef.
+//   5. scatter  : FP64 global atomics into the output vector.
+//
+// Modes: residual (assemble_rhs), Jacobian action (matrix-free assembleGLS<true> . v),
+// Jacobian diagonal (for the Jacobi preconditioner and the deal.II constrained-row diagonal).
+#include "gls_common.hpp"
+#include "gls_launch.hpp"
+
+namespace gls {
+
+template <int DIM, int K, int KP, int NQ1>
+struct Cfg {
+  static constexpr int NV = ipow(K + 1, DIM);
+  static constexpr int NP = ipow(KP + 1, DIM);
+  static constexpr int NQ = ipow(NQ1, DIM);
+  static constexpr int CB = 256 / NQ;
+  static constexpr int NT = DIM * (DIM + 1) + DIM + 1;  // test coefficients per q
+  static constexpr int K1 = K + 1, KP1 = KP + 1;
+  static constexpr int TABN = 5 * kMaxQ1D * kMaxNodes1D + 2 * kMaxQ1D;
+};
+
+template <int DIM, int K, int KP, int NQ1, int MODE>
+__global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const Tables1D T) {
+  using C = Cfg<DIM, K, KP, NQ1>;
+  constexpr int NV = C::NV, NP = C::NP, NQ = C::NQ, CB = C::CB, NT = C::NT;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double *sTab = smem;                              // Tables1D copy
+  double *sU = sTab + ((C::TABN + 1) & ~1);         // [CB][NV][DIM]
+  double *sP = sU + CB * NV * DIM;                  // [CB][NP]
+  double *sH = sP + CB * NP;                        // [n_hist][CB][NV][DIM]
+  double *sV = sH + 3 * CB * NV * DIM;              // [CB][NV][DIM]   (JV)
+  double *sVP = sV + CB * NV * DIM;                 // [CB][NP]        (JV)
+  double *sT = sVP + CB * NP;                       // [CB][NQ][NT]
+
+  const double(*tV)[kMaxNodes1D] = reinterpret_cast<const double(*)[kMaxNodes1D]>(sTab);
+  const double(*tD)[kMaxNodes1D] = tV + kMaxQ1D;
+  const double(*tS)[kMaxNodes1D] = tD + kMaxQ1D;
+  const double(*tVp)[kMaxNodes1D] = tS + kMaxQ1D;
+  const double(*tDp)[kMaxNodes1D] = tVp + kMaxQ1D;
+  const double *tW = sTab + 5 * kMaxQ1D * kMaxNodes1D;
+  const double *tXi = tW + kMaxQ1D;
+
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.x * CB;
+  const int ncb = min(CB, P.n_cells - c0);
+  const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
+
+  // ---- stage tables
+  {
+    const double *src = reinterpret_cast<const double *>(&T);
+    for (int i = tid; i < C::TABN; i += blockDim.x) sTab[i] = src[i];
+  }
+  // ---- 1. gather (velocity-type fields)
+  for (int i = tid; i < ncb * NV; i += blockDim.x) {
+    const int node = P.cell_vnodes[(int64_t)c0 * NV + i];
+    const int64_t b = (int64_t)node * DIM;
+#pragma unroll
+    for (int c = 0; c < DIM; ++c) sU[i * DIM + c] = P.u[b + c];
+    if (P.n_hist > 0) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) sH[i * DIM + c] = P.h1[b + c];
+    }
+    if (P.n_hist > 1) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) sH[CB * NV * DIM + i * DIM + c] = P.h2[b + c];
+    }
+    if (P.n_hist > 2) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) sH[2 * CB * NV * DIM + i * DIM + c] = P.h3[b + c];
+    }
+    if constexpr (MODE == MODE_JV) {
+      const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) sV[i * DIM + c] = ((m >> c) & 1u) ? 0.0 : P.v[b + c];
+    }
+  }
+  for (int i = tid; i < ncb * NP; i += blockDim.x) {
+    const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+    sP[i] = P.u[voff + pn];
+    if constexpr (MODE == MODE_JV) sVP[i] = P.v[voff + pn];
+  }
+  __syncthreads();
+
+  // ---- 2./3. evaluate + pointwise, one thread per (cell, q)
+  if (tid < ncb * NQ) {
+    const int cl = tid / NQ, q = tid % NQ;
+    const int cell = c0 + cl;
+    const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
+    const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
+    const double hst = P.geo[cell * 4 + 3];
+    const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
+    const double JxW = tW[qx] * tW[qy] * (DIM == 3 ? tW[qz] : 1.0) * hx * hy * (DIM == 3 ? hz : 1.0);
+    // Laplacian weights relative to x (1 for cubes)
+    const double wy = (hx * hx) / (hy * hy), wz = (hx * hx) / (hz * hz);
+
+    double u[DIM] = {}, gu[DIM][DIM] = {}, lu[DIM] = {}, pq = 0., gp[DIM] = {};
+    double h1[DIM] = {}, h2[DIM] = {}, h3[DIM] = {};
+    double v[DIM] = {}, gv[DIM][DIM] = {}, lv[DIM] = {}, vp = 0., gvp[DIM] = {};
+    const double *cu = sU + cl * NV * DIM;
+    const double *cv = sV + cl * NV * DIM;
+    const double *ch = sH + cl * NV * DIM;
+    const int nh = P.n_hist;
+#pragma unroll
+    for (int az = 0; az < (DIM == 3 ? C::K1 : 1); ++az) {
+      const double vz = DIM == 3 ? tV[qz][az] : 1.0, dz = DIM == 3 ? tD[qz][az] : 0.0,
+                   sz = DIM == 3 ? tS[qz][az] : 0.0;
+#pragma unroll
+      for (int ay = 0; ay < C::K1; ++ay) {
+        const double vy = tV[qy][ay], dy = tD[qy][ay], sy = tS[qy][ay];
+#pragma unroll
+        for (int ax = 0; ax < C::K1; ++ax) {
+          const double vx = tV[qx][ax], dx = tD[qx][ax], sx = tS[qx][ax];
+          const int a = ax + C::K1 * (ay + C::K1 * az);
+          const double N = vx * vy * vz;
+          const double g0 = dx * vy * vz, g1 = vx * dy * vz, g2 = vx * vy * dz;
+          const double L = sx * vy * vz + wy * vx * sy * vz + (DIM == 3 ? wz * vx * vy * sz : 0.0);
+          const double gr[3] = {g0, g1, g2};
+#pragma unroll
+          for (int c = 0; c < DIM; ++c) {
+            const double val = cu[a * DIM + c];
+            u[c] += val * N;
+            lu[c] += val * L;
+#pragma unroll
+            for (int e = 0; e < DIM; ++e) gu[c][e] += val * gr[e];
+            if constexpr (MODE == MODE_JV) {
+              const double vv = cv[a * DIM + c];
+              v[c] += vv * N;
+              lv[c] += vv * L;
+#pragma unroll
+              for (int e = 0; e < DIM; ++e) gv[c][e] += vv * gr[e];
+            }
+            if (nh > 0) h1[c] += ch[a * DIM + c] * N;
+            if (nh > 1) h2[c] += ch[CB * NV * DIM + a * DIM + c] * N;
+            if (nh > 2) h3[c] += ch[2 * CB * NV * DIM + a * DIM + c] * N;
+          }
+        }
+      }
+    }
+    {
+      const double *cp = sP + cl * NP;
+      const double *cvp = sVP + cl * NP;
+#pragma unroll
+      for (int az = 0; az < (DIM == 3 ? C::KP1 : 1); ++az) {
+        const double vz = DIM == 3 ? tVp[qz][az] : 1.0, dz = DIM == 3 ? tDp[qz][az] : 0.0;
+#pragma unroll
+        for (int ay = 0; ay < C::KP1; ++ay) {
+          const double vy = tVp[qy][ay], dy = tDp[qy][ay];
+#pragma unroll
+          for (int ax = 0; ax < C::KP1; ++ax) {
+            const double vx = tVp[qx][ax], dx = tDp[qx][ax];
+            const int a = ax + C::KP1 * (ay + C::KP1 * az);
+            const double N = vx * vy * vz;
+            const double gr[3] = {dx * vy * vz, vx * dy * vz, vx * vy * dz};
+            const double pv = cp[a];
+            if constexpr (MODE == MODE_RESIDUAL) pq += pv * N;
+#pragma unroll
+            for (int e = 0; e < DIM; ++e) gp[e] += pv * gr[e];
+            if constexpr (MODE == MODE_JV) {
+              const double w = cvp[a];
+              vp += w * N;
+#pragma unroll
+              for (int e = 0; e < DIM; ++e) gvp[e] += w * gr[e];
+            }
+          }
+        }
+      }
+    }
+    // reference -> physical derivatives (affine box map)
+    const double il2 = ih[0] * ih[0];
+#pragma unroll
+    for (int c = 0; c < DIM; ++c) {
+      lu[c] *= il2;
+      lv[c] *= il2;
+#pragma unroll
+      for (int e = 0; e < DIM; ++e) { gu[c][e] *= ih[e]; gv[c][e] *= ih[e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < DIM; ++e) { gp[e] *= ih[e]; gvp[e] *= ih[e]; }
+
+    // ---- pointwise (gls_navier_stokes.cc:391-516)
+    const double nu = P.nu;
+    double un2 = 0.;
+#pragma unroll
+    for (int c = 0; c < DIM; ++c) un2 += u[c] * u[c];
+    const double u_mag = fmax(sqrt(un2), 1e-12);
+    const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
+    const double tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
+    double f[DIM] = {};
+    if (P.force_q) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) f[c] = P.force_q[((int64_t)cell * NQ + q) * DIM + c];
+    }
+    double Gu[DIM], R[DIM], srf_cor[DIM] = {}, srf_cen[DIM] = {};
+#pragma unroll
+    for (int c = 0; c < DIM; ++c) {
+      double s = 0.;
+#pragma unroll
+      for (int e = 0; e < DIM; ++e) s += gu[c][e] * u[e];
+      Gu[c] = s;
+      R[c] = s + gp[c] - nu * lu[c] - f[c];
+    }
+    double om[3] = {P.omega[0], P.omega[1], P.omega[2]};
+    if (P.srf) {
+      double xq[3];
+      xq[0] = P.x0[cell * 3 + 0] + hx * tXi[qx];
+      xq[1] = P.x0[cell * 3 + 1] + hy * tXi[qy];
+      xq[2] = DIM == 3 ? P.x0[cell * 3 + 2] + hz * tXi[qz] : 0.0;
+      if constexpr (DIM == 2) {
+        const double wz_ = om[2];
+        srf_cor[0] = 2 * wz_ * (-1.) * u[1];
+        srf_cor[1] = 2 * wz_ * (-1.) * (-u[0]);
+        const double a0 = wz_ * (-1.) * xq[1], a1 = wz_ * (-1.) * (-xq[0]);
+        srf_cen[0] = wz_ * (-1.) * a1;
+        srf_cen[1] = wz_ * (-1.) * (-a0);
+      } else {
+        const double cx[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
+        const double ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2],
+                              om[0] * xq[1] - om[1] * xq[0]};
+        srf_cor[0] = 2 * cx[0]; srf_cor[1] = 2 * cx[1]; srf_cor[DIM - 1] = 2 * cx[DIM - 1];
+        const double cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) srf_cen[c] = cc[c];
+      }
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) R[c] += srf_cor[c] + srf_cen[c];
+    }
+    double Tt[DIM];  // time term sum_k alpha_k u^(k)
+#pragma unroll
+    for (int c = 0; c < DIM; ++c) {
+      double s = P.alpha[0] * u[c];
+      if (nh > 0) s += P.alpha[1] * h1[c];
+      if (nh > 1) s += P.alpha[2] * h2[c];
+      if (nh > 2) s += P.alpha[3] * h3[c];
+      Tt[c] = s;
+      R[c] += s;
+    }
+
+    double *Tq = sT + (cl * NQ + q) * NT;
+    if constexpr (MODE == MODE_RESIDUAL) {
+      double divu = 0.;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) divu += gu[c][c];
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        Tq[c * (DIM + 1)] = JxW * (-Gu[c] + f[c] - Tt[c] - srf_cor[c] - srf_cen[c]);
+#pragma unroll
+        for (int e = 0; e < DIM; ++e)
+          Tq[c * (DIM + 1) + 1 + e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]) * ih[e];
+      }
+      Tq[DIM * (DIM + 1)] = -JxW * divu;
+#pragma unroll
+      for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = -JxW * tau * R[e] * ih[e];
+    } else if constexpr (MODE == MODE_JV) {
+      const double aj = P.alpha_jac;
+      double S[DIM], A[DIM], divv = 0.;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        double gvu = 0., guv = 0.;
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) { guv += gu[c][e] * v[e]; gvu += gv[c][e] * u[e]; }
+        A[c] = guv + gvu + aj * v[c];
+        S[c] = guv + gvu + gvp[c] - nu * lv[c] + aj * v[c];
+        divv += gv[c][c];
+      }
+      if (P.srf) {
+        double cj[DIM];
+        if constexpr (DIM == 2) {
+          cj[0] = 2 * om[2] * (-1.) * v[1];
+          cj[1] = 2 * om[2] * (-1.) * (-v[0]);
+        } else {
+          cj[0] = 2 * (om[1] * v[2] - om[2] * v[1]);
+          cj[1] = 2 * (om[2] * v[0] - om[0] * v[2]);
+          cj[DIM - 1] = 2 * (om[0] * v[1] - om[1] * v[0]);
+        }
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) { A[c] += cj[c]; S[c] += cj[c]; }
+      }
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        Tq[c * (DIM + 1)] = JxW * A[c];
+#pragma unroll
+        for (int e = 0; e < DIM; ++e)
+          Tq[c * (DIM + 1) + 1 + e] =
+              JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
+      }
+      Tq[DIM * (DIM + 1)] = JxW * divv;
+#pragma unroll
+      for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = JxW * tau * S[e] * ih[e];
+    } else {  // MODE_DIAG: per-q state for the diagonal
+      Tq[0] = JxW;
+      Tq[1] = tau;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        Tq[2 + c] = u[c];
+        Tq[2 + DIM + c] = gu[c][c];
+        Tq[2 + 2 * DIM + c] = R[c];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 4./5. integrate + scatter, one thread per (cell, node)
+  for (int i = tid; i < ncb * NV; i += blockDim.x) {
+    const int cl = i / NV, a = i % NV;
+    const int ax = a % C::K1, ay = (a / C::K1) % C::K1, az = DIM == 3 ? a / (C::K1 * C::K1) : 0;
+    const double *Tc = sT + cl * NQ * NT;
+    const int node = P.cell_vnodes[(int64_t)c0 * NV + i];
+    if constexpr (MODE != MODE_DIAG) {
+      double out[DIM] = {};
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
+        const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
+        const double N = vx * vy * vz;
+        const double gr[3] = {tD[qx][ax] * vy * vz, vx * tD[qy][ay] * vz, DIM == 3 ? vx * vy * tD[qz][az] : 0.0};
+        const double *Tq = Tc + q * NT;
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) {
+          double s = N * Tq[c * (DIM + 1)];
+#pragma unroll
+          for (int e = 0; e < DIM; ++e) s += gr[e] * Tq[c * (DIM + 1) + 1 + e];
+          out[c] += s;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], out[c]);
+    } else {
+      const int cell = c0 + cl;
+      const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
+      const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
+      const double nu = P.nu, aj = P.alpha_jac;
+      double out[DIM] = {};
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
+        const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
+        const double N = vx * vy * vz;
+        const double g[3] = {tD[qx][ax] * vy * vz * ih[0], vx * tD[qy][ay] * vz * ih[1],
+                             DIM == 3 ? vx * vy * tD[qz][az] * ih[2] : 0.0};
+        const double L = tS[qx][ax] * vy * vz * ih[0] * ih[0] + vx * tS[qy][ay] * vz * ih[1] * ih[1] +
+                         (DIM == 3 ? vx * vy * tS[qz][az] * ih[2] * ih[2] : 0.0);
+        const double *Tq = Tc + q * NT;
+        const double JxW = Tq[0], tau = Tq[1];
+        double ug = 0., gg = 0.;
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) { ug += Tq[2 + e] * g[e]; gg += g[e] * g[e]; }
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) {
+          const double Gcc = Tq[2 + DIM + c], Rc = Tq[2 + 2 * DIM + c];
+          const double Sc = Gcc * N + ug - nu * L + aj * N;
+          out[c] += JxW * (nu * gg + Gcc * N * N + ug * N + aj * N * N + tau * Sc * ug + tau * Rc * g[c] * N);
+        }
+      }
+      const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], ((m >> c) & 1u) ? fabs(out[c]) : out[c]);
+    }
+  }
+  for (int i = tid; i < ncb * NP; i += blockDim.x) {
+    const int cl = i / NP, a = i % NP;
+    const int ax = a % C::KP1, ay = (a / C::KP1) % C::KP1, az = DIM == 3 ? a / (C::KP1 * C::KP1) : 0;
+    const double *Tc = sT + cl * NQ * NT;
+    const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+    double out = 0.;
+    if constexpr (MODE != MODE_DIAG) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
+        const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;
+        const double *Tq = Tc + q * NT + DIM * (DIM + 1);
+        double s = vx * vy * vz * Tq[0];
+        s += tDp[qx][ax] * vy * vz * Tq[1];
+        s += vx * tDp[qy][ay] * vz * Tq[2];
+        if (DIM == 3) s += vx * vy * tDp[qz][az] * Tq[DIM];
+        out += s;
+      }
+    } else {
+      const int cell = c0 + cl;
+      const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
+        const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;
+        const double g0 = tDp[qx][ax] * vy * vz / hx, g1 = vx * tDp[qy][ay] * vz / hy,
+                     g2 = DIM == 3 ? vx * vy * tDp[qz][az] / hz : 0.0;
+        const double *Tq = Tc + q * NT;
+        out += Tq[0] * Tq[1] * (g0 * g0 + g1 * g1 + g2 * g2);
+      }
+    }
+    atomicAdd(&P.y[voff + pn], out);
+  }
+}
+
+template <int DIM, int K, int KP, int NQ1>
+size_t cell_kernel_lds_bytes() {
+  using C = Cfg<DIM, K, KP, NQ1>;
+  size_t n = ((C::TABN + 1) & ~1) + C::CB * C::NV * DIM + C::CB * C::NP + 3 * C::CB * C::NV * DIM +
+             C::CB * C::NV * DIM + C::CB * C::NP + C::CB * C::NQ * C::NT;
+  return n * sizeof(double);
+}
+
+template <int DIM, int K, int KP, int NQ1>
+hipError_t launch_cell_t(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
+  using C = Cfg<DIM, K, KP, NQ1>;
+  if (P.n_cells <= 0) return hipSuccess;
+  const int blocks = (P.n_cells + C::CB - 1) / C::CB;
+  const size_t lds = cell_kernel_lds_bytes<DIM, K, KP, NQ1>();
+  static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  switch (mode) {
+    case MODE_RESIDUAL:
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL>), dim3(blocks), dim3(256), lds, s, P, T);
+      break;
+    case MODE_JV:
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV>), dim3(blocks), dim3(256), lds, s, P, T);
+      break;
+    default:
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG>), dim3(blocks), dim3(256), lds, s, P, T);
+  }
+  return hipGetLastError();
+}
+
+// Supported element families (dim, k, kp) with the reference quadrature QGauss(k+1).
+hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
+                              hipStream_t s) {
+#define GLS_CASE(D, KK, KKP)                                                         \
+  if (dim == D && k == KK && kp == KKP && nq1d == KK + 1) return launch_cell_t<D, KK, KKP, KK + 1>(mode, P, T, s);
+  GLS_CASE(2, 1, 1)
+  GLS_CASE(2, 2, 1)
+  GLS_CASE(2, 2, 2)
+  GLS_CASE(2, 3, 3)
+  GLS_CASE(3, 1, 1)
+  GLS_CASE(3, 2, 1)
+  GLS_CASE(3, 2, 2)
+#undef GLS_CASE
+  return hipErrorNotSupported;
+}
+
+bool cell_kernel_supported(int dim, int k, int kp, int nq1d) {
+  if (nq1d != k + 1) return false;
+  return (dim == 2 && ((k == 1 && kp == 1) || (k == 2 && (kp == 1 || kp == 2)) || (k == 3 && kp == 3))) ||
+         (dim == 3 && ((k == 1 && kp == 1) || (k == 2 && (kp == 1 || kp == 2))));
+}
+
+}  // namespace gls

@@ -1,0 +1,52 @@
+// gls_common.hpp — shared host/device definitions of the MI355X GLS Navier–Stokes path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gls {
+
+constexpr int kMaxNodes1D = 4;  // k <= 3
+constexpr int kMaxQ1D = 5;      // QGauss(n) with n <= 5
+
+constexpr int ipow(int b, int e) { return e == 0 ? 1 : b * ipow(b, e - 1); }
+
+enum Mode { MODE_RESIDUAL = 0, MODE_JV = 1, MODE_DIAG = 2 };
+
+// Reference-cell 1D tables on [0,1] (deal.II unit cell): Lagrange basis on Gauss–Lobatto
+// support points evaluated at QGauss points. [q][node].
+struct Tables1D {
+  double V[kMaxQ1D][kMaxNodes1D];   // velocity basis value
+  double D[kMaxQ1D][kMaxNodes1D];   // d/dxi
+  double S[kMaxQ1D][kMaxNodes1D];   // d2/dxi2
+  double Vp[kMaxQ1D][kMaxNodes1D];  // pressure basis value
+  double Dp[kMaxQ1D][kMaxNodes1D];  // pressure d/dxi
+  double w[kMaxQ1D];                // Gauss weights on [0,1]
+  double xi[kMaxQ1D];               // Gauss points on [0,1]
+};
+
+// Per-launch operator parameters (device pointers).
+struct OpParams {
+  int n_cells;
+  int n_vnodes;
+  int n_pnodes;
+  int n_hist;                 // history vectors read by this scheme (0..3)
+  const int32_t *cell_vnodes;
+  const int32_t *cell_pnodes; // nullptr -> use cell_vnodes (kp == k)
+  const double *geo;          // [n_cells][4]: h_x, h_y, h_z, h_stab
+  const double *x0;           // [n_cells][3] (SRF only)
+  const double *force_q;      // [n_cells][nq][dim] or nullptr
+  const uint8_t *vmask;       // [n_vnodes] zero_constraints bits, nullptr = none
+  const double *u;
+  const double *h1, *h2, *h3; // history (solution_m1..m3)
+  const double *v;            // JV input
+  double *y;                  // output (accumulated with atomics)
+  double nu;
+  double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs
+  double alpha_jac;           // mass coefficient of the Jacobian (bdf[0] / sdirk[0][0])
+  double sdt2;                // (1/dt)^2 for transient tau, 0 when steady
+  int srf;
+  double omega[3];
+};
+
+}  // namespace gls

@@ -1,0 +1,30 @@
+// gls_launch.hpp — host-side launch entry points of the device kernels.
+#pragma once
+#include "gls_common.hpp"
+
+namespace gls {
+
+hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
+                              hipStream_t s);
+bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
+
+// ---- BLAS-1 style kernels on device vectors (gls_vector_kernels.hip)
+hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s);
+hipError_t vec_copy(double *y, const double *x, int64_t n, hipStream_t s);
+hipError_t vec_axpy(double *y, double a, const double *x, int64_t n, hipStream_t s);          // y += a x
+hipError_t vec_axpby(double *y, double a, const double *x, double b, int64_t n, hipStream_t s);  // y = a x + b y
+hipError_t vec_scale(double *x, double a, int64_t n, hipStream_t s);
+hipError_t vec_div(double *y, const double *x, const double *d, int64_t n, hipStream_t s);       // y = x / d
+// partial dot products: out[k] = sum_i A[k][i] * w[i] for k < nk (A rows have stride lda),
+// written as per-block partials into work, reduced into out (device) by a second kernel.
+hipError_t vec_multidot(const double *A, int64_t lda, int nk, const double *w, int64_t n, double *out,
+                        double *work, hipStream_t s);
+// w -= sum_k h[k] * A[k]  (h on device)
+hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
+                         hipStream_t s);
+hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
+                                hipStream_t s);  // y[idx] = d[idx]*v[idx]
+hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
+int multidot_work_size();
+
+}  // namespace gls

@@ -1,0 +1,185 @@
+// gls_vector_kernels.hip — Krylov vector kernels (HBM-bound; 16-byte accesses where aligned).
+#include "gls_launch.hpp"
+
+namespace gls {
+
+namespace {
+constexpr int kBlock = 256;
+constexpr int kMaxBlocks = 2048;  // 256 CUs x 8
+constexpr int kDotChunk = 8;      // vectors per multidot pass
+
+inline int grid_for(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  return (int)(b < kMaxBlocks ? (b > 0 ? b : 1) : kMaxBlocks);
+}
+
+__global__ void k_fill(double *x, int64_t n, double a) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] = a;
+}
+__global__ void k_copy(double *__restrict__ y, const double *__restrict__ x, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) y[i] = x[i];
+}
+__global__ void k_axpy(double *__restrict__ y, double a, const double *__restrict__ x, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] += a * x[i];
+}
+__global__ void k_axpby(double *__restrict__ y, double a, const double *__restrict__ x, double b, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = a * x[i] + b * y[i];
+}
+__global__ void k_scale(double *x, double a, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] *= a;
+}
+__global__ void k_div(double *__restrict__ y, const double *__restrict__ x, const double *__restrict__ d, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = x[i] / d[i];
+}
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// partial sums of up to kDotChunk dot products per block; work[k*gridDim + block]
+template <int NK>
+__global__ void __launch_bounds__(kBlock) k_multidot(const double *__restrict__ A, int64_t lda,
+                                                     const double *__restrict__ w, int64_t n, double *work) {
+  double acc[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) acc[k] = 0.;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double wi = w[i];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) acc[k] += A[k * lda + i] * wi;
+  }
+  __shared__ double red[NK][kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const double s = wave_sum(acc[k]);
+    if (lane == 0) red[k][wv] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NK) {
+    double s = 0.;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; ++j) s += red[threadIdx.x][j];
+    work[threadIdx.x * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// out[k] = sum_b work[k*nb + b]; one block per k, deterministic order
+__global__ void __launch_bounds__(kBlock) k_reduce_rows(const double *work, int nb, double *out) {
+  double s = 0.;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += work[blockIdx.x * nb + b];
+  __shared__ double red[kBlock / 64];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.;
+    for (int j = 0; j < kBlock / 64; ++j) t += red[j];
+    out[blockIdx.x] = t;
+  }
+}
+
+template <int NK>
+__global__ void __launch_bounds__(kBlock) k_multiaxpy(double *__restrict__ w, const double *__restrict__ A, int64_t lda,
+                                                      const double *__restrict__ h, double sign, int64_t n) {
+  double hk[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) hk[k] = sign * h[k];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = w[i];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s -= hk[k] * A[k * lda + i];
+    w[i] = s;
+  }
+}
+
+__global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = idx[j];
+    y[i] = d[i] * v[i];
+  }
+}
+__global__ void k_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
+    y[idx[j]] = vals ? vals[j] : 0.0;
+}
+}  // namespace
+
+int multidot_work_size() { return kDotChunk * kMaxBlocks; }
+
+hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, n, a);
+  return hipGetLastError();
+}
+hipError_t vec_copy(double *y, const double *x, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy, dim3(grid_for(n)), dim3(kBlock), 0, s, y, x, n);
+  return hipGetLastError();
+}
+hipError_t vec_axpy(double *y, double a, const double *x, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpy, dim3(grid_for(n)), dim3(kBlock), 0, s, y, a, x, n);
+  return hipGetLastError();
+}
+hipError_t vec_axpby(double *y, double a, const double *x, double b, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_axpby, dim3(grid_for(n)), dim3(kBlock), 0, s, y, a, x, b, n);
+  return hipGetLastError();
+}
+hipError_t vec_scale(double *x, double a, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale, dim3(grid_for(n)), dim3(kBlock), 0, s, x, a, n);
+  return hipGetLastError();
+}
+hipError_t vec_div(double *y, const double *x, const double *d, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_div, dim3(grid_for(n)), dim3(kBlock), 0, s, y, x, d, n);
+  return hipGetLastError();
+}
+
+hipError_t vec_multidot(const double *A, int64_t lda, int nk, const double *w, int64_t n, double *out, double *work,
+                        hipStream_t s) {
+  const int nb = grid_for(n);
+  for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
+    const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;
+    const double *Ak = A + (int64_t)k0 * lda;
+    switch (m) {
+#define MD(M) \
+  case M: hipLaunchKernelGGL(k_multidot<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n, work); break;
+      MD(1) MD(2) MD(3) MD(4) MD(5) MD(6) MD(7) MD(8)
+#undef MD
+    }
+    hipLaunchKernelGGL(k_reduce_rows, dim3(m), dim3(kBlock), 0, s, work, nb, out + k0);
+  }
+  return hipGetLastError();
+}
+
+hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
+                         hipStream_t s) {
+  const int nb = grid_for(n);
+  for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
+    const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;
+    const double *Ak = A + (int64_t)k0 * lda;
+    switch (m) {
+#define MA(M) \
+  case M: hipLaunchKernelGGL(k_multiaxpy<M>, dim3(nb), dim3(kBlock), 0, s, w, Ak, lda, h + k0, sign, n); break;
+      MA(1) MA(2) MA(3) MA(4) MA(5) MA(6) MA(7) MA(8)
+#undef MA
+    }
+  }
+  return hipGetLastError();
+}
+
+hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
+                                hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_scale_set, dim3(grid_for(m)), dim3(kBlock), 0, s, y, d, v, idx, m);
+  return hipGetLastError();
+}
+hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_indexed, dim3(grid_for(m)), dim3(kBlock), 0, s, y, idx, vals, m);
+  return hipGetLastError();
+}
+
+}  // namespace gls

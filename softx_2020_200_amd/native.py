@@ -1,0 +1,308 @@
+"""ctypes binding of libgls_native.so (include/gls_native.h).
+
+The product path: every operator call goes to the HIP kernels in libgls_native.so.
+There is no CPU fallback — if the extension is missing or no HIP device is present,
+``load()`` / ``GLSContext`` raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgls_native.so")
+
+GLS_OK, GLS_EINVAL, GLS_EHIP, GLS_ENOMEM, GLS_ENOCONV, GLS_EIO, GLS_ECOMM = 0, -1, -2, -3, -4, -5, -6
+
+SCHEMES = {
+    "steady": 0, "bdf1": 1, "bdf2": 2, "bdf3": 3, "sdirk2": 4, "sdirk2_1": 5, "sdirk2_2": 6,
+    "sdirk3": 7, "sdirk3_1": 8, "sdirk3_2": 9, "sdirk3_3": 10,
+}
+
+# every symbol declared in include/gls_native.h (checked by tests/test_native_abi.py)
+EXPORTS = [
+    "gls_last_error", "gls_version", "gls_create", "gls_destroy", "gls_set_stream", "gls_n_dofs", "gls_set_force",
+    "gls_set_viscosity", "gls_set_time", "gls_set_state", "gls_residual", "gls_jacobian_apply",
+    "gls_jacobian_diagonal", "gls_set_dirichlet", "gls_apply_dirichlet", "gls_solve_linear", "gls_newton_solve",
+    "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
+    "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable",
+]
+
+
+class GLSError(RuntimeError):
+    pass
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int), ("k", C.c_int), ("kp", C.c_int), ("nq1d", C.c_int), ("n_cells", C.c_int),
+        ("n_vnodes", C.c_int), ("n_pnodes", C.c_int),
+        ("cell_vnodes", C.POINTER(C.c_int32)), ("cell_pnodes", C.POINTER(C.c_int32)),
+        ("cell_x0", C.POINTER(C.c_double)), ("cell_h", C.POINTER(C.c_double)),
+        ("vnode_mask", C.POINTER(C.c_uint8)),
+        ("viscosity", C.c_double), ("srf", C.c_int), ("omega", C.c_double * 3),
+        ("force_q", C.POINTER(C.c_double)),
+    ]
+
+
+class LinearParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int), ("restart", C.c_int), ("relative_residual", C.c_double),
+                ("minimum_residual", C.c_double), ("iterations", C.c_int), ("final_residual", C.c_double)]
+
+
+class NewtonParams(C.Structure):
+    _fields_ = [("tolerance", C.c_double), ("max_iterations", C.c_int), ("verbosity", C.c_int),
+                ("lin", LinearParams), ("newton_iterations", C.c_int), ("linear_iterations", C.c_int),
+                ("residual_evaluations", C.c_int), ("final_residual", C.c_double)]
+
+
+_lib = None
+
+
+def load():
+    """Load the HIP extension; raise loudly if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GLSError("HIP extension %s is missing — run `python -m softx_2020_200_amd.build` "
+                       "(or __graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, d, i64 = C.c_void_p, C.POINTER(C.c_double), C.c_int64
+    L.gls_last_error.restype = C.c_char_p
+    L.gls_version.restype = C.c_char_p
+    L.gls_create.argtypes = [C.POINTER(MeshDesc), C.POINTER(vp)]
+    L.gls_destroy.argtypes = [vp]
+    L.gls_set_stream.argtypes = [vp, vp]
+    L.gls_n_dofs.argtypes = [vp, C.POINTER(i64)]
+    L.gls_set_force.argtypes = [vp, d]
+    L.gls_set_viscosity.argtypes = [vp, C.c_double]
+    L.gls_set_time.argtypes = [vp, C.c_int, d]
+    L.gls_set_state.argtypes = [vp, vp, vp, vp, vp]
+    L.gls_residual.argtypes = [vp, vp]
+    L.gls_jacobian_apply.argtypes = [vp, vp, vp]
+    L.gls_jacobian_diagonal.argtypes = [vp, vp]
+    L.gls_set_dirichlet.argtypes = [vp, i64, C.POINTER(i64), d]
+    L.gls_apply_dirichlet.argtypes = [vp, vp]
+    L.gls_solve_linear.argtypes = [vp, vp, vp, C.POINTER(LinearParams)]
+    L.gls_newton_solve.argtypes = [vp, vp, vp, vp, vp, C.POINTER(NewtonParams)]
+    L.gls_bdf_coefficients.argtypes = [C.c_int, d, C.c_int, d]
+    L.gls_sdirk_coefficients.argtypes = [C.c_int, C.c_double, d]
+    L.gls_newton_selftest.argtypes = [d]
+    L.gls_mesh_hyper_cube_sizes.argtypes = [C.c_int] * 5 + [C.POINTER(i64)] * 3
+    L.gls_mesh_hyper_cube.argtypes = [C.c_int] * 4 + [C.c_double, C.c_double, C.c_int,
+                                                      C.POINTER(C.c_int32), C.POINTER(C.c_int32), d, d]
+    L.gls_timing_reset.argtypes = [vp]
+    L.gls_timing_get.argtypes = [vp, C.c_int, d, C.POINTER(i64)]
+    L.gls_timing_enable.argtypes = [vp, C.c_int]
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc < 0:
+        msg = load().gls_last_error().decode()
+        raise GLSError("%s failed (%d): %s" % (what, rc, msg))
+    return rc
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double)) if a is not None else C.POINTER(C.c_double)()
+
+
+# ---------------------------------------------------------------------------------------------
+# host-only helpers (no GPU needed)
+# ---------------------------------------------------------------------------------------------
+def bdf_coefficients(order, dts):
+    dts = np.ascontiguousarray(dts, dtype=np.float64)
+    out = np.zeros(order + 1)
+    check(load().gls_bdf_coefficients(order, _dp(dts), len(dts), _dp(out)), "gls_bdf_coefficients")
+    return out
+
+
+def sdirk_coefficients(order, dt):
+    out = np.zeros(order * (order + 1))
+    check(load().gls_sdirk_coefficients(order, dt, _dp(out)), "gls_sdirk_coefficients")
+    return out.reshape(order, order + 1)
+
+
+def newton_selftest():
+    out = np.zeros(2)
+    check(load().gls_newton_selftest(_dp(out)), "gls_newton_selftest")
+    return out
+
+
+def hyper_cube(dim, n, k, kp=None, lo=-1.0, hi=1.0, periodic=()):
+    """GridGenerator::hyper_cube + refine_global through the C++ mesh builder (Morton cells)."""
+    kp = k if kp is None else kp
+    L = load()
+    pm = sum(1 << d for d in periodic)
+    nc, nv, npn = C.c_int64(), C.c_int64(), C.c_int64()
+    check(L.gls_mesh_hyper_cube_sizes(dim, n, k, kp, pm, C.byref(nc), C.byref(nv), C.byref(npn)), "mesh sizes")
+    nc, nv, npn = nc.value, nv.value, npn.value
+    cv = np.zeros((nc, (k + 1) ** dim), dtype=np.int32)
+    cp = np.zeros((nc, (kp + 1) ** dim), dtype=np.int32)
+    x0 = np.zeros((nc, dim))
+    h = np.zeros((nc, dim))
+    check(L.gls_mesh_hyper_cube(dim, n, k, kp, lo, hi, pm, cv.ctypes.data_as(C.POINTER(C.c_int32)),
+                                cp.ctypes.data_as(C.POINTER(C.c_int32)), _dp(x0), _dp(h)), "gls_mesh_hyper_cube")
+    return dict(dim=dim, k=k, kp=kp, n_cells=nc, n_vnodes=nv, n_pnodes=npn, cell_vnodes=cv, cell_pnodes=cp,
+                cell_x0=x0, cell_h=h)
+
+
+# ---------------------------------------------------------------------------------------------
+# device context
+# ---------------------------------------------------------------------------------------------
+def _ptr(t):
+    if t is None:
+        return None
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float64 or not t.is_contiguous():
+        raise GLSError("expected a contiguous float64 CUDA (HIP) tensor")
+    return C.c_void_p(t.data_ptr())
+
+
+class GLSContext:
+    """Owner of one gls_ctx (one GPU). Vectors are torch float64 tensors on cuda."""
+
+    def __init__(self, dim, k, kp, cell_vnodes, cell_pnodes, cell_h, n_vnodes, n_pnodes, viscosity=1.0,
+                 cell_x0=None, vnode_mask=None, force_q=None, srf=False, omega=(0.0, 0.0, 0.0), nq1d=0,
+                 stream=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise GLSError("no HIP device visible: the GLS operators run only on the GPU")
+        self.L = load()
+        self.dim, self.k, self.kp = dim, k, kp
+        keep = []
+
+        def arr(a, dt):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a
+
+        cv = arr(cell_vnodes, np.int32)
+        cp = arr(cell_pnodes, np.int32) if (cell_pnodes is not None and kp != k) else None
+        if cp is None and kp != k:
+            raise GLSError("cell_pnodes required for kp != k")
+        hh = arr(cell_h, np.float64)
+        x0 = arr(cell_x0, np.float64)
+        vm = arr(vnode_mask, np.uint8)
+        fq = arr(force_q, np.float64)
+        D = MeshDesc()
+        D.dim, D.k, D.kp, D.nq1d = dim, k, kp, nq1d
+        D.n_cells = cv.shape[0]
+        D.n_vnodes, D.n_pnodes = int(n_vnodes), int(n_pnodes)
+        D.cell_vnodes = cv.ctypes.data_as(C.POINTER(C.c_int32))
+        D.cell_pnodes = cp.ctypes.data_as(C.POINTER(C.c_int32)) if cp is not None else C.POINTER(C.c_int32)()
+        D.cell_x0 = _dp(x0)
+        D.cell_h = _dp(hh)
+        D.vnode_mask = vm.ctypes.data_as(C.POINTER(C.c_uint8)) if vm is not None else C.POINTER(C.c_uint8)()
+        D.viscosity = viscosity
+        D.srf = 1 if srf else 0
+        for i in range(3):
+            D.omega[i] = omega[i]
+        D.force_q = _dp(fq)
+        h = C.c_void_p()
+        check(self.L.gls_create(C.byref(D), C.byref(h)), "gls_create")
+        self.h = h
+        n = C.c_int64()
+        check(self.L.gls_n_dofs(self.h, C.byref(n)), "gls_n_dofs")
+        self.n_dofs = n.value
+        self.n_cells = D.n_cells
+        # stream-ordered with torch: run on the caller's current torch stream unless told otherwise
+        if stream is None:
+            stream = torch.cuda.current_stream().cuda_stream
+        self.stream = stream
+        check(self.L.gls_set_stream(self.h, C.c_void_p(stream)), "gls_set_stream")
+        self._state = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.gls_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def zeros(self):
+        import torch
+        return torch.zeros(self.n_dofs, dtype=torch.float64, device="cuda")
+
+    def set_time(self, scheme, time_steps=(1.0, 1.0, 1.0, 1.0)):
+        ts = np.zeros(4)
+        ts[:len(time_steps)] = time_steps[:4]
+        check(self.L.gls_set_time(self.h, SCHEMES[scheme] if isinstance(scheme, str) else scheme, _dp(ts)),
+              "gls_set_time")
+
+    def set_state(self, u, u1=None, u2=None, u3=None):
+        self._state = (u, u1, u2, u3)  # keep tensors alive while borrowed
+        check(self.L.gls_set_state(self.h, _ptr(u), _ptr(u1), _ptr(u2), _ptr(u3)), "gls_set_state")
+
+    def set_force(self, force_q):
+        f = None if force_q is None else np.ascontiguousarray(force_q, dtype=np.float64)
+        check(self.L.gls_set_force(self.h, _dp(f)), "gls_set_force")
+
+    def set_viscosity(self, nu):
+        check(self.L.gls_set_viscosity(self.h, nu), "gls_set_viscosity")
+
+    def residual(self, out=None):
+        out = self.zeros() if out is None else out
+        check(self.L.gls_residual(self.h, _ptr(out)), "gls_residual")
+        return out
+
+    def jacobian_apply(self, v, out=None):
+        out = self.zeros() if out is None else out
+        check(self.L.gls_jacobian_apply(self.h, _ptr(v), _ptr(out)), "gls_jacobian_apply")
+        return out
+
+    def jacobian_diagonal(self, out=None):
+        out = self.zeros() if out is None else out
+        check(self.L.gls_jacobian_diagonal(self.h, _ptr(out)), "gls_jacobian_diagonal")
+        return out
+
+    def set_dirichlet(self, dofs, values):
+        dofs = np.ascontiguousarray(dofs, dtype=np.int64)
+        vals = np.ascontiguousarray(values, dtype=np.float64)
+        self._dir = (dofs, vals)
+        check(self.L.gls_set_dirichlet(self.h, len(dofs), dofs.ctypes.data_as(C.POINTER(C.c_int64)), _dp(vals)),
+              "gls_set_dirichlet")
+
+    def apply_dirichlet(self, x):
+        check(self.L.gls_apply_dirichlet(self.h, _ptr(x)), "gls_apply_dirichlet")
+        return x
+
+    def solve_linear(self, rhs, x=None, max_iterations=1000, restart=30, relative_residual=1e-4,
+                     minimum_residual=1e-12):
+        x = self.zeros() if x is None else x
+        p = LinearParams(max_iterations, restart, relative_residual, minimum_residual, 0, 0.0)
+        rc = self.L.gls_solve_linear(self.h, _ptr(rhs), _ptr(x), C.byref(p))
+        if rc < 0 and rc != GLS_ENOCONV:
+            check(rc, "gls_solve_linear")
+        return x, p.iterations, p.final_residual, rc == GLS_OK
+
+    def newton(self, present, u1=None, u2=None, u3=None, tolerance=1e-8, max_iterations=10, verbosity=0,
+               lin_max_iterations=1000, restart=30, relative_residual=1e-4, minimum_residual=1e-12):
+        self._state = (present, u1, u2, u3)
+        lp = LinearParams(lin_max_iterations, restart, relative_residual, minimum_residual, 0, 0.0)
+        p = NewtonParams(tolerance, max_iterations, verbosity, lp, 0, 0, 0, 0.0)
+        check(self.L.gls_newton_solve(self.h, _ptr(present), _ptr(u1), _ptr(u2), _ptr(u3), C.byref(p)),
+              "gls_newton_solve")
+        return dict(newton_iterations=p.newton_iterations, linear_iterations=p.linear_iterations,
+                    residual_evaluations=p.residual_evaluations, final_residual=p.final_residual)
+
+    # profiling
+    def timing(self, enable=True):
+        check(self.L.gls_timing_enable(self.h, 1 if enable else 0), "gls_timing_enable")
+        check(self.L.gls_timing_reset(self.h), "gls_timing_reset")
+
+    def timing_get(self, which):
+        ms, n = C.c_double(), C.c_int64()
+        check(self.L.gls_timing_get(self.h, which, C.byref(ms), C.byref(n)), "gls_timing_get")
+        return ms.value, n.value

@@ -1,0 +1,78 @@
+"""Problem setup on the product side: hyper_cube mesh (C++ builder), boundary
+classification and Dirichlet constraints (setup_dofs, gls_navier_stokes.cc:80-184),
+and the 3D lid-driven cavity of the benchmark.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .native import GLSContext, hyper_cube
+
+
+def vnode_boundary_ids(mesh, n, lo, hi, colorize):
+    """per velocity node: bitmask of hyper_cube boundary ids it lies on (colorize: x-=0,x+=1,y-=2,...)."""
+    dim, k = mesh["dim"], mesh["k"]
+    nx = k * n + 1
+    idx = np.indices((nx,) * dim).reshape(dim, -1)[::-1].T  # lexicographic, x fastest
+    bits = np.zeros(idx.shape[0], dtype=np.int64)
+    for d in range(dim):
+        lo_b = 1 << (2 * d if colorize else 0)
+        hi_b = 1 << (2 * d + 1 if colorize else 0)
+        bits |= np.where(idx[:, d] == 0, lo_b, 0)
+        bits |= np.where(idx[:, d] == nx - 1, hi_b, 0)
+    coords = lo + idx * ((hi - lo) / (k * n))
+    return bits, coords
+
+
+def dirichlet_from_bcs(mesh, n, lo, hi, colorize, bcs):
+    """bcs: list of (type, boundary_id, values) in bc order, type in {noslip, function};
+    values: callable(coords[m,dim]) -> [m,dim] or a constant tuple. deal.II first-wins rule.
+    Returns (vnode_mask uint8, dofs int64, values float64)."""
+    dim = mesh["dim"]
+    bits, X = vnode_boundary_ids(mesh, n, lo, hi, colorize)
+    nv = bits.shape[0]
+    taken = np.zeros((nv, dim), dtype=bool)
+    vals = np.zeros((nv, dim))
+    for typ, bid, f in bcs:
+        sel = np.nonzero(bits & (1 << bid))[0]
+        if sel.size == 0:
+            continue
+        if typ == "noslip":
+            v = np.zeros((sel.size, dim))
+        elif typ == "function":
+            v = np.asarray(f(X[sel]) if callable(f) else np.broadcast_to(np.asarray(f, dtype=float)[:dim],
+                                                                          (sel.size, dim)), dtype=float)
+        else:
+            raise ValueError("unsupported bc type %s" % typ)
+        free = ~taken[sel]
+        vals[sel] = np.where(free, v, vals[sel])
+        taken[sel] = True
+    mask = np.zeros(nv, dtype=np.uint8)
+    for c in range(dim):
+        mask |= (taken[:, c].astype(np.uint8) << c)
+    nodes, comps = np.nonzero(taken)
+    dofs = nodes.astype(np.int64) * dim + comps
+    return mask, dofs, vals[nodes, comps]
+
+
+def build_context(mesh, viscosity=1.0, vnode_mask=None, force_q=None, srf=False, omega=(0, 0, 0), stream=None):
+    return GLSContext(mesh["dim"], mesh["k"], mesh["kp"], mesh["cell_vnodes"], mesh["cell_pnodes"], mesh["cell_h"],
+                      mesh["n_vnodes"], mesh["n_pnodes"], viscosity=viscosity, cell_x0=mesh["cell_x0"],
+                      vnode_mask=vnode_mask, force_q=force_q, srf=srf, omega=omega, stream=stream)
+
+
+class CavityProblem:
+    """3D (or 2D) lid-driven cavity on hyper_cube(-1, 1, colorize=true): walls noslip, lid y=+1
+    (boundary id 3) u=(1,0,0) — examples/01-cavity/cavity.prm:46-55 extended to 3D.
+    The lid bc is listed last so the wall edges keep u=0 (first bc wins)."""
+
+    def __init__(self, dim=3, n=8, k=2, kp=None, viscosity=0.01, stream=None):
+        kp = k if kp is None else kp
+        self.dim, self.n, self.k, self.kp = dim, n, k, kp
+        self.mesh = hyper_cube(dim, n, k, kp, -1.0, 1.0)
+        walls = [i for i in range(2 * dim) if i != 3]
+        bcs = [("noslip", b, None) for b in walls] + [("function", 3, (1.0, 0.0, 0.0))]
+        self.vnode_mask, self.dir_dofs, self.dir_vals = dirichlet_from_bcs(self.mesh, n, -1.0, 1.0, True, bcs)
+        self.ctx = build_context(self.mesh, viscosity=viscosity, vnode_mask=self.vnode_mask, stream=stream)
+        self.ctx.set_dirichlet(self.dir_dofs, self.dir_vals)
+        self.n_dofs = self.ctx.n_dofs
