@@ -1,0 +1,231 @@
+"""bench.py — nonlinear (Newton) iterations/s of the GLS Navier–Stokes hot path on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): 3D lid-driven cavity, Q2-Q2,
+128^3 cells (67,898,372 DoFs), transient BDF2, nu = 0.01, dt = 0.01.
+One "step" = one Newton iteration of NewtonNonLinearSolver::solve
+(include/core/newton_non_linear_solver.h:90-137): evaluation_point = present; residual + Jacobian
+diagonal (matrix-free "assemble_matrix_and_rhs"); GMRES(30) with Jacobi preconditioning on the
+matrix-free Jacobian (relative residual 1e-4, max `--lin-max` iterations); alpha line search with
+residual re-assembly. Every step restarts from the same synthetic state so the work per step is
+fixed; linear iterations and residual evaluations are reported.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
+Multi-GPU: each rank runs the full workload on its own GPU ("replicas" until the RCCL
+domain-decomposed path lands); value = sum over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6        # MI355X FP64 (vector = matrix) spec; measured 61-64 TF (profiles/r01_microbench_fp64.txt)
+
+
+def smooth_state(mesh, n, dim, dir_dofs, dir_vals, phase=0.0):
+    """A smooth synthetic cavity-like velocity field (rotating vortex + lid shear), Dirichlet values applied."""
+    k = mesh["k"]
+    nx = k * n + 1
+    g = np.linspace(-1.0, 1.0, nx)
+    nv, npn = mesh["n_vnodes"], mesh["n_pnodes"]
+    x = np.zeros(dim * nv + npn)
+    Z, Y, X = np.meshgrid(g, g, g, indexing="ij") if dim == 3 else (None,) + tuple(np.meshgrid(g, g, indexing="ij"))
+    wall = (1 - X ** 2) * (1 - Y ** 2) * ((1 - Z ** 2) if dim == 3 else 1.0)
+    ux = (0.5 * (1 + Y)) ** 2 * wall * (1.0 + 0.1 * np.sin(phase))
+    uy = -0.5 * X * wall
+    vel = np.zeros((nv, dim))
+    vel[:, 0] = ux.reshape(-1)
+    vel[:, 1] = uy.reshape(-1)
+    if dim == 3:
+        vel[:, 2] = (0.2 * X * Y * wall).reshape(-1)
+    x[:dim * nv] = vel.reshape(-1)
+    x[dim * nv:] = 0.05 * (X * Y).reshape(-1) if mesh["kp"] == k else 0.0
+    x[dir_dofs] = dir_vals
+    return x
+
+
+def cpu_baseline(k, kp, nu, seconds, threads):
+    """Oracle (CPU restatement of assembleGLS, 'port') timed on a bounded sample of Q2 cells:
+    element-matrix+rhs and rhs-only throughput -> extrapolated assembly-only nonlinear iterations/s."""
+    import ctypes as C
+
+    from oracle.oracle import StructuredProblem, _dp, lib
+    p = StructuredProblem(3, 6, k=k, kp=kp, viscosity=nu, scheme="bdf2", time_steps=(0.01,) * 4)
+    u = np.random.default_rng(20200200).uniform(-1, 1, p.n_dofs)
+    P = p.struct()
+    L = lib()
+    res = {}
+    for wm in (1, 0):
+        cnt, dt = 8, 0.0
+        while True:
+            t0 = time.perf_counter()
+            L.gls_oracle_time_local_systems(C.byref(P), _dp(u), _dp(u), _dp(u), _dp(u), 0, cnt, wm, threads)
+            dt = time.perf_counter() - t0
+            if dt > seconds / 2 or cnt > 1 << 22:
+                break
+            cnt = int(cnt * max(2.0, min(8.0, (seconds / 2) / max(dt, 1e-3))))
+        res["matrix" if wm else "rhs"] = (cnt, dt)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=128, help="cells per direction")
+    ap.add_argument("--k", type=int, default=2)
+    ap.add_argument("--kp", type=int, default=2)
+    ap.add_argument("--nu", type=float, default=0.01)
+    ap.add_argument("--dt", type=float, default=0.01)
+    ap.add_argument("--lin-max", type=int, default=200)
+    ap.add_argument("--restart", type=int, default=30)
+    ap.add_argument("--rel", type=float, default=1e-4)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    from softx_2020_200_amd.problem import CavityProblem
+    t_setup = time.perf_counter()
+    prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu)
+    ctx = prob.ctx
+    N = ctx.n_dofs
+    ts = (args.dt,) * 4
+    ctx.set_time("bdf2", ts)
+    m1_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.0)
+    m2_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.3)
+    dev = torch.device("cuda", local)
+    m1 = torch.from_numpy(m1_h).to(dev)
+    m2 = torch.from_numpy(m2_h).to(dev)
+    del m1_h, m2_h
+    present = m1.clone()
+    t_setup = time.perf_counter() - t_setup
+
+    def one_step():
+        present.copy_(m1)
+        return ctx.newton(present, m1, m2, tolerance=1e-30, max_iterations=1, lin_max_iterations=args.lin_max,
+                          restart=args.restart, relative_residual=args.rel, minimum_residual=1e-14)
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    stats = [one_step() for _ in range(args.steps)]
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    jv_ms, jv_n = ctx.timing_get(1)
+    res_ms, res_n = ctx.timing_get(0)
+    dg_ms, dg_n = ctx.timing_get(2)
+    ctx.timing(False)
+    # dedicated back-to-back J.v launches on the same state for a clean per-launch duration
+    ctx.set_state(present, m1, m2)
+    v = torch.rand(N, dtype=torch.float64, device=dev)
+    y = torch.empty_like(v)
+    ctx.jacobian_apply(v, y)
+    ctx.timing(True)
+    for _ in range(args.jv_reps):
+        ctx.jacobian_apply(v, y)
+    jv2_ms, jv2_n = ctx.timing_get(1)
+    ctx.timing(False)
+
+    t_max = elapsed
+    if dist is not None:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    lin_its = [s["linear_iterations"] for s in stats]
+    nres = [s["residual_evaluations"] for s in stats]
+    its_per_s = world * args.steps / t_max
+    n_cells = prob.mesh["n_cells"]
+    nv = prob.mesh["n_vnodes"]
+    nvdofs = 3 * nv
+    # algorithmic bytes of one J.v launch (this build's layout): v, Jv, u (8N each),
+    # 2 history velocity vectors (BDF2), cell->node int32 indices, per-cell geometry (4 doubles),
+    # velocity constraint mask (1 B/node)
+    nvl = (args.k + 1) ** 3
+    B_jv = 8 * N * 3 + 8 * 2 * nvdofs + 4 * n_cells * nvl * (1 if args.kp == args.k else 2) + 32 * n_cells + nv
+    jv_launch_ms = jv2_ms / max(jv2_n, 1)
+    achieved = B_jv / (jv_launch_ms * 1e-3) / 1e9
+    # dense-contraction FLOP count of the kernel as written (per cell, Q2-Q2 3D): see DESIGN.md §4
+    out = {
+        "metric": "nonlinear iters/sec (3D cavity Q2 128^3 BDF2)",
+        "value": its_per_s,
+        "unit": "nonlinear_iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * t_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (smooth cavity-like BDF2 history, lid/wall Dirichlet values)",
+        "config": {"workload": "3D lid-driven cavity Q%d-Q%d %d^3 transient BDF2 (BASELINE configs[2])"
+                               % (args.k, args.kp, args.n),
+                   "n_dofs": N, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
+                   "linear_solver": "GMRES(%d)+Jacobi, rel %.0e, max %d" % (args.restart, args.rel, args.lin_max),
+                   "parallelism": "replicas" if world > 1 else "single"},
+        "mdof_per_s": N * its_per_s / 1e6,
+        "linear_iterations_per_step": float(np.mean(lin_its)),
+        "residual_evaluations_per_step": float(np.mean(nres)),
+        "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),
+                      "diagonal": dg_ms / max(dg_n, 1),
+                      "share_of_step": {"jacobian_apply": jv_ms / (1e3 * elapsed),
+                                        "residual": res_ms / (1e3 * elapsed), "diagonal": dg_ms / (1e3 * elapsed)}},
+        "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,2,3,MODE_JV>", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "algorithmic_bytes_per_launch": B_jv, "launch_ms": jv_launch_ms},
+        "setup_s": t_setup,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+        threads = min(threads, 16)
+        cb = cpu_baseline(args.k, args.kp, args.nu, args.cpu_seconds, threads)
+        (cm, tm), (cr, tr) = cb["matrix"], cb["rhs"]
+        t_mat = n_cells * tm / cm          # one assemble_matrix_and_rhs over the full mesh
+        t_rhs = n_cells * tr / cr          # one assemble_rhs
+        L_ = float(np.mean(nres)) - 1.0    # line-search residuals per Newton step (GPU run's count)
+        t_iter = t_mat + L_ * t_rhs
+        out["cpu_baseline"] = {
+            "value": 1.0 / t_iter, "unit": "nonlinear_iters/s", "cores": threads, "kind": "port",
+            "sample": "oracle/gls_oracle.c local element matrix+rhs on %d Q%d-Q%d cells (%.1f s) and rhs-only on "
+                      "%d cells (%.1f s), %d OpenMP threads; extrapolated to %d cells x (1 matrix + %.1f rhs) "
+                      "assemblies per Newton step; EXCLUDES the reference's ILU setup + GMRES (not runnable)"
+                      % (cm, args.k, args.kp, tm, cr, tr, threads, n_cells, L_),
+            "assembly_s_per_iter": t_iter,
+        }
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

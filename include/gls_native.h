@@ -75,6 +75,9 @@ int gls_create(const gls_mesh_desc *desc, gls_ctx **out);
 int gls_destroy(gls_ctx *ctx);
 int gls_set_stream(gls_ctx *ctx, void *hip_stream);
 int gls_n_dofs(const gls_ctx *ctx, int64_t *n_dofs);
+/* 1 when the context runs the sum-factorized brick kernels (3D Qk-Qk on Morton 2x2x2 bricks),
+ * 0 for the general per-cell kernels. GLS_DISABLE_BRICK=1 in the environment forces 0. */
+int gls_uses_brick_kernels(const gls_ctx *ctx);
 /* Rewrite the forcing at quadrature points (host pointer, [n_cells*nq*dim]) or clear it (NULL). */
 int gls_set_force(gls_ctx *ctx, const double *force_q);
 int gls_set_viscosity(gls_ctx *ctx, double viscosity);

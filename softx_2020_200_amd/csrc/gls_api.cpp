@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -264,6 +265,7 @@ struct gls_ctx {
   DevBuf<double> krylov;      // (restart+1) x n_dofs
   int krylov_m = 0;
   DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
+  bool use_brick = false;  // sum-factorized brick kernels (3D Qk-Qk, Morton 2x2x2 bricks)
   // timing
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
@@ -278,6 +280,45 @@ struct gls_ctx {
 };
 
 namespace {
+
+// The brick kernels need: 3D, equal order k==kp in {1,2}, QGauss(k+1), pressure on the velocity
+// nodes, and every 8 consecutive cells forming a conforming 2x2x2 brick (Morton order) whose
+// interior nodes belong to no other brick (they are written with plain stores).
+bool detect_bricks(const gls_mesh_desc *d, int nq1d) {
+  if (getenv("GLS_DISABLE_BRICK")) return false;
+  if (d->dim != 3 || d->k != d->kp || (d->k != 1 && d->k != 2) || nq1d != d->k + 1) return false;
+  if (d->cell_pnodes || d->n_cells % 8 != 0 || d->n_cells == 0) return false;
+  const int K = d->k, K1 = K + 1, N3 = K1 * K1 * K1, BN = 2 * K + 1;
+  const int nb = d->n_cells / 8;
+  std::vector<int32_t> owner((size_t)d->n_vnodes, -1);
+  std::vector<int32_t> bnode((size_t)BN * BN * BN);
+  for (int b = 0; b < nb; ++b) {
+    std::fill(bnode.begin(), bnode.end(), -1);
+    for (int cc = 0; cc < 8; ++cc) {
+      const int cx = cc & 1, cy = (cc >> 1) & 1, cz = cc >> 2;
+      const int32_t *cv = d->cell_vnodes + ((size_t)b * 8 + cc) * N3;
+      for (int a = 0; a < N3; ++a) {
+        const int ax = a % K1, ay = (a / K1) % K1, az = a / (K1 * K1);
+        const int n = (K * cx + ax) + BN * ((K * cy + ay) + BN * (K * cz + az));
+        if (bnode[n] == -1) bnode[n] = cv[a];
+        else if (bnode[n] != cv[a]) return false;  // not a conforming brick
+      }
+    }
+    for (int Z = 1; Z < BN - 1; ++Z)
+      for (int Y = 1; Y < BN - 1; ++Y)
+        for (int X = 1; X < BN - 1; ++X) {
+          const int32_t node = bnode[X + BN * (Y + BN * Z)];
+          if (owner[node] != -1) return false;
+          owner[node] = b;
+        }
+  }
+  for (int cix = 0; cix < d->n_cells; ++cix)
+    for (int a = 0; a < N3; ++a) {
+      const int32_t o = owner[d->cell_vnodes[(size_t)cix * N3 + a]];
+      if (o != -1 && o != cix / 8) return false;
+    }
+  return true;
+}
 
 int check_ctx(gls_ctx *c) {
   if (!c) return set_err(GLS_EINVAL, "null context");
@@ -340,7 +381,10 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode);
-    HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+    if (c->use_brick && mode != gls::MODE_DIAG)
+      HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
+    else
+      HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
   return GLS_OK;
 }
@@ -398,6 +442,7 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
   if (!d->cell_pnodes && d->n_pnodes != d->n_vnodes) return set_err(GLS_EINVAL, "n_pnodes != n_vnodes without cell_pnodes");
 
   GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
+  c->use_brick = detect_bricks(d, nq1d);
   if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
   std::vector<double> geo((size_t)d->n_cells * 4);
   for (int cix = 0; cix < d->n_cells; ++cix) {
@@ -454,6 +499,8 @@ int gls_set_stream(gls_ctx *c, void *s) {
   c->stream = (hipStream_t)s;
   return GLS_OK;
 }
+
+int gls_uses_brick_kernels(const gls_ctx *c) { return c && c->use_brick ? 1 : 0; }
 
 int gls_n_dofs(const gls_ctx *c, int64_t *n) {
   if (!c || !n) return set_err(GLS_EINVAL, "null argument");

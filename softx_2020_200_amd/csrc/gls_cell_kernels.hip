@@ -111,11 +111,11 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     const double *cv = sV + cl * NV * DIM;
     const double *ch = sH + cl * NV * DIM;
     const int nh = P.n_hist;
-#pragma unroll
+#pragma nounroll
     for (int az = 0; az < (DIM == 3 ? C::K1 : 1); ++az) {
       const double vz = DIM == 3 ? tV[qz][az] : 1.0, dz = DIM == 3 ? tD[qz][az] : 0.0,
                    sz = DIM == 3 ? tS[qz][az] : 0.0;
-#pragma unroll
+#pragma nounroll
       for (int ay = 0; ay < C::K1; ++ay) {
         const double vy = tV[qy][ay], dy = tD[qy][ay], sy = tS[qy][ay];
 #pragma unroll
@@ -150,10 +150,10 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     {
       const double *cp = sP + cl * NP;
       const double *cvp = sVP + cl * NP;
-#pragma unroll
+#pragma nounroll
       for (int az = 0; az < (DIM == 3 ? C::KP1 : 1); ++az) {
         const double vz = DIM == 3 ? tVp[qz][az] : 1.0, dz = DIM == 3 ? tDp[qz][az] : 0.0;
-#pragma unroll
+#pragma nounroll
         for (int ay = 0; ay < C::KP1; ++ay) {
           const double vy = tVp[qy][ay], dy = tDp[qy][ay];
 #pragma unroll
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     const int node = P.cell_vnodes[(int64_t)c0 * NV + i];
     if constexpr (MODE != MODE_DIAG) {
       double out[DIM] = {};
-#pragma unroll
+#pragma nounroll
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
@@ -341,7 +341,7 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
       const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
       const double nu = P.nu, aj = P.alpha_jac;
       double out[DIM] = {};
-#pragma unroll
+#pragma nounroll
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
     double out = 0.;
     if constexpr (MODE != MODE_DIAG) {
-#pragma unroll
+#pragma nounroll
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     } else {
       const int cell = c0 + cl;
       const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
-#pragma unroll
+#pragma nounroll
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;

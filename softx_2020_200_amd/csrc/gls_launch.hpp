@@ -7,6 +7,8 @@ namespace gls {
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s);
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
+// sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
+hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 
 // ---- BLAS-1 style kernels on device vectors (gls_vector_kernels.hip)
 hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s);

@@ -27,7 +27,7 @@ EXPORTS = [
     "gls_set_viscosity", "gls_set_time", "gls_set_state", "gls_residual", "gls_jacobian_apply",
     "gls_jacobian_diagonal", "gls_set_dirichlet", "gls_apply_dirichlet", "gls_solve_linear", "gls_newton_solve",
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
-    "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable",
+    "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
 ]
 
 
@@ -97,6 +97,7 @@ def load():
     L.gls_timing_reset.argtypes = [vp]
     L.gls_timing_get.argtypes = [vp, C.c_int, d, C.POINTER(i64)]
     L.gls_timing_enable.argtypes = [vp, C.c_int]
+    L.gls_uses_brick_kernels.argtypes = [vp]
     _lib = L
     return L
 
@@ -230,6 +231,10 @@ class GLSContext:
             self.close()
         except Exception:
             pass
+
+    @property
+    def uses_brick_kernels(self):
+        return bool(self.L.gls_uses_brick_kernels(self.h))
 
     def zeros(self):
         import torch
