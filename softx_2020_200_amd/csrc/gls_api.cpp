@@ -702,6 +702,8 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       g[j] = cs[j] * g[j];
       res = std::fabs(g[j + 1]);
       ++it;
+      if (getenv("GLS_GMRES_VERBOSE") && (it % 10 == 0 || it == 1))
+        printf("  gmres it %d  res %.6e  (tol %.3e)\n", it, res, tol);
       if (res <= tol || wnorm == 0.) { ++j; break; }
     }
     // back substitution and update x += M^{-1} V y

@@ -2,20 +2,23 @@
 //
 // Why this shape (MI355X-first): on gfx950 FP64 MFMA (v_mfma_f64_16x16x4) and FP64 VALU share
 // one ~62 TF budget (profiles/r01_microbench_fp64.txt: 61.3 / 63.5 / 59.1 TF mixed), so the lever
-// is FLOPs, not the pipe. Tensor-product sum factorization does the basis x coefficient work
-// in ~24 kFLOP per Q2 cell (dense n_dofs x n_q contraction: ~86 kFLOP). The 1D matrices are
-// uniform across the wave and indexed with compile-time constants, so they live in SGPRs.
+// is FLOPs and latency, not the pipe. Tensor-product sum factorization does the basis x
+// coefficient work in ~24 kFLOP per Q2 cell (a dense n_dofs x n_q contraction: ~86 kFLOP). The 1D
+// matrices are uniform across the wave and indexed with compile-time constants (SGPR operands).
 //
-// Work unit: one Morton brick = 8 consecutive cells forming a 2x2x2 block (the hyper_cube
-// builder emits cells in p4est z-order). Per brick the unique (2k+1)^3 nodes are gathered once
-// into LDS (u, p, history combination H = sum_k alpha_k u^(k), and v / v_p for J.v),
-// the cells' contributions are summed in LDS in a fixed order (deterministic), brick-interior
-// nodes are written with plain stores and brick-boundary nodes with FP64 atomics.
+// Work unit: one workgroup = one Morton brick = 8 consecutive cells forming a 2x2x2 block (the
+// hyper_cube builder emits p4est z-order). The brick's unique (2k+1)^3 nodes are gathered once
+// into LDS (u, p, the history combination H = sum_k alpha_k u^(k), and v / v_p for J.v); each
+// wave then owns 2 cells and runs its whole per-cell pipeline wave-locally (LDS exchanges ordered
+// by in-order LDS execution within a wave: no workgroup barriers); the cells' node contributions
+// are summed per brick node in a fixed order (deterministic), brick-interior nodes are written
+// with plain stores and brick-boundary nodes with FP64 atomics.
 //
-// Per-cell pipeline (all LDS line sweeps, one task = one 1D line of one array):
-//   state  : x/y/z sweeps of u (value, grad, Laplacian), grad p (+p), H (value)   -> pointwise
-//   v      : x/y/z sweeps of v (value, grad, Laplacian), v_p (value, grad)        -> pointwise (J.v)
-//   test   : transposed z/y/x sweeps of the 4 x (value, grad) test coefficients  -> node sums
+// Per-cell pipeline, one field at a time (keeps ~3 KB of LDS per cell -> 4 workgroups per CU):
+//   x sweep (brick -> X), y sweep (X -> Y), z sweep fused into the pointwise read (Y -> registers)
+//   state  : u (value, grad, Laplacian) x 3 comps, then {p (value, grad), H (value) x 3}
+//   J.v    : v (value, grad, Laplacian) x 3 comps, then v_p (value, grad)
+//   test   : per test field, transposed z/y/x sweeps of (value, grad) coefficients -> node array
 // The pointwise algebra restates gls_navier_stokes.cc:387-748.
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
@@ -29,10 +32,11 @@ struct BrickCfg {
   static constexpr int L2 = K1 * K1;         // lines per array
   static constexpr int BN = 2 * K + 1;       // brick nodes per direction
   static constexpr int BN3 = BN * BN * BN;
-  static constexpr int NB = K == 1 ? 2 : 1;  // bricks per workgroup
-  static constexpr int NC = 8 * NB;          // cells per workgroup
-  static constexpr int THREADS = NC * N3;
-  static constexpr int R1N = 18, R2N = 22;   // per-cell LDS array slots
+  static constexpr int CPW = 64 / N3 >= 2 ? 2 : 1;  // cells per wave (Q1: 8 q -> could be 8; keep 2)
+  static constexpr int WAVES = 8 / CPW;      // waves per workgroup (one brick)
+  static constexpr int THREADS = 64 * WAVES;
+  static constexpr int NX = 5, NY = 6, NO = 4;  // per-cell LDS arrays: X, Y, out
+  static constexpr int PER_CELL = NX + NY + NO;
 };
 
 // offset of element e of line l in a [K1][K1][K1] array ([z][y][x], x fastest), sweep dim D
@@ -43,19 +47,27 @@ __device__ __forceinline__ int loff(int l, int e) {
   else return l + K1 * K1 * e;
 }
 
-// forward 1D contraction: out[j] = sum_i M[j][i] in[i]   (nodes -> quadrature)
+// forward: out[j] = sum_i M[j][i] in[i] (nodes -> q);  transposed: out[i] = sum_j M[j][i] in[j]
 template <int K1>
-__device__ __forceinline__ void fwd(const double (&M)[kMaxQ1D][kMaxNodes1D], const double *in, double *out,
-                                    double scale = 1.0) {
+__device__ __forceinline__ void fwd(const double (&M)[kMaxQ1D][kMaxNodes1D], const double *in, double *out) {
 #pragma unroll
   for (int j = 0; j < K1; ++j) {
     double s = 0.;
 #pragma unroll
     for (int i = 0; i < K1; ++i) s += M[j][i] * in[i];
-    out[j] = s * scale;
+    out[j] = s;
   }
 }
-// transposed: out[i] += sum_j M[j][i] in[j]   (quadrature -> nodes)
+template <int K1>
+__device__ __forceinline__ void bwd(const double (&M)[kMaxQ1D][kMaxNodes1D], const double *in, double *out) {
+#pragma unroll
+  for (int i = 0; i < K1; ++i) {
+    double s = 0.;
+#pragma unroll
+    for (int j = 0; j < K1; ++j) s += M[j][i] * in[j];
+    out[i] = s;
+  }
+}
 template <int K1>
 __device__ __forceinline__ void bwd_add(const double (&M)[kMaxQ1D][kMaxNodes1D], const double *in, double *out) {
 #pragma unroll
@@ -67,466 +79,435 @@ __device__ __forceinline__ void bwd_add(const double (&M)[kMaxQ1D][kMaxNodes1D],
   }
 }
 
+// LDS hand-off between lanes of ONE wave: LDS ops of a wave execute in order; the asm keeps the
+// compiler from moving LDS accesses across this point.
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int K, int MODE>
 __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
-  constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, NB = C::NB, NC = C::NC;
-  constexpr int R1N = C::R1N, R2N = C::R2N;
+  constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
   constexpr bool JV = MODE == MODE_JV;
   constexpr int NF = JV ? 11 : 7;  // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double *sB = smem;                         // [NB][NF][BN3]
-  double *sR1 = sB + NB * NF * BN3;          // [NC][R1N][N3]
-  double *sR2 = sR1 + NC * R1N * N3;         // [NC][R2N][N3]
-  int *sNode = reinterpret_cast<int *>(sR2 + NC * R2N * N3);  // [NB][BN3]
-  auto A1 = [&](int c, int s) { return sR1 + (c * R1N + s) * N3; };
-  auto A2 = [&](int c, int s) { return sR2 + (c * R2N + s) * N3; };
-  auto BF = [&](int b, int f) { return sB + (b * NF + f) * BN3; };
+  double *sB = smem;                                   // [NF][BN3]
+  double *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
+  int *sNode = reinterpret_cast<int *>(sC + 8 * C::PER_CELL * N3);  // [BN3]
+  auto BF = [&](int f) { return sB + f * BN3; };
 
   const int tid = threadIdx.x;
-  const int n_bricks = P.n_cells / 8;
-  const int b0 = blockIdx.x * NB;
-  const int nb = min(NB, n_bricks - b0);
-  const int ncell = 8 * nb;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int brick = blockIdx.x;
   const int64_t voff = (int64_t)3 * P.n_vnodes;
 
-  // ---------------- gather brick nodes
-  for (int t = tid; t < nb * BN3; t += blockDim.x) {
-    const int b = t / BN3, n = t % BN3;
+  // ---------------- gather the brick's nodes (all waves)
+  for (int t = tid; t < 3 * BN3; t += blockDim.x) {
+    const int g = t / BN3, n = t % BN3;
     const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
     const int cx = min(X / K, 1), cy = min(Y / K, 1), cz = min(Z / K, 1);
     const int a = (X - K * cx) + K1 * ((Y - K * cy) + K1 * (Z - K * cz));
-    const int cell = (b0 + b) * 8 + cx + 2 * cy + 4 * cz;
-    const int node = P.cell_vnodes[(int64_t)cell * N3 + a];
-    sNode[b * BN3 + n] = node;
+    const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * N3 + a];
     const int64_t i3 = (int64_t)node * 3;
+    if (g == 0) {
+      sNode[n] = node;
+      BF(0)[n] = P.u[i3];
+      BF(1)[n] = P.u[i3 + 1];
+      BF(2)[n] = P.u[i3 + 2];
+      BF(3)[n] = P.u[voff + node];
+    } else if (g == 1) {
+      double h[3] = {0., 0., 0.};
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      BF(b, c)[n] = P.u[i3 + c];
-      double h = 0.;
-      if (P.n_hist > 0) h += P.alpha[1] * P.h1[i3 + c];
-      if (P.n_hist > 1) h += P.alpha[2] * P.h2[i3 + c];
-      if (P.n_hist > 2) h += P.alpha[3] * P.h3[i3 + c];
-      BF(b, 4 + c)[n] = h;
-    }
-    BF(b, 3)[n] = P.u[voff + node];
-    if constexpr (JV) {
+      for (int c = 0; c < 3; ++c) {
+        if (P.n_hist > 0) h[c] += P.alpha[1] * P.h1[i3 + c];
+        if (P.n_hist > 1) h[c] += P.alpha[2] * P.h2[i3 + c];
+        if (P.n_hist > 2) h[c] += P.alpha[3] * P.h3[i3 + c];
+      }
+      BF(4)[n] = h[0];
+      BF(5)[n] = h[1];
+      BF(6)[n] = h[2];
+    } else if (JV) {
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) BF(b, 7 + c)[n] = ((m >> c) & 1u) ? 0.0 : P.v[i3 + c];
-      BF(b, 10)[n] = P.v[voff + node];
+      BF(7)[n] = (m & 1u) ? 0.0 : P.v[i3];
+      BF(8)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
+      BF(9)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
+      BF(10)[n] = P.v[voff + node];
     }
   }
   __syncthreads();
 
-  // per-cell geometry (cell of this thread in the pointwise phases)
-  auto cell_h = [&](int ci, double &hx, double &hy, double &hz) {
-    const int cell = b0 * 8 + ci;
-    hx = P.geo[cell * 4 + 0];
-    hy = P.geo[cell * 4 + 1];
-    hz = P.geo[cell * 4 + 2];
+  // ---------------- per-wave: cells 2*wave, 2*wave+1 of the brick
+  auto X = [&](int ci, int s) { return sC + (ci * C::PER_CELL + s) * N3; };
+  auto Yr = [&](int ci, int s) { return sC + (ci * C::PER_CELL + C::NX + s) * N3; };
+  auto Out = [&](int ci, int f) { return sC + (ci * C::PER_CELL + C::NX + C::NY + f) * N3; };
+  const int cbase = wave * CPW;
+  // pointwise lane mapping: lane -> (cell, q)
+  const bool pact = lane < CPW * N3;
+  const int pci = cbase + (pact ? lane / N3 : 0);
+  const int q = pact ? lane % N3 : 0;
+  const int qx = q % K1, qy = (q / K1) % K1, qz = q / (K1 * K1);
+  const int gcell = brick * 8 + pci;
+  const double hx = P.geo[gcell * 4 + 0], hy = P.geo[gcell * 4 + 1], hz = P.geo[gcell * 4 + 2];
+  const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
+  const double wx = ih[0] * ih[0], wy = ih[1] * ih[1], wz = ih[2] * ih[2];
+  // this lane's rows of the z matrices (q-dependent -> registers)
+  double Bz[K1], Dz[K1], Sz[K1];
+#pragma unroll
+  for (int i = 0; i < K1; ++i) { Bz[i] = T.V[qz][i]; Dz[i] = T.D[qz][i]; Sz[i] = T.S[qz][i]; }
+
+  // brick-array line base for (cell-in-brick, line (i1,i2)) in an x sweep
+  auto bline = [&](int ci, int l) {
+    const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
+    return K * cx + BN * (K * cy + l % K1) + BN * BN * (K * cz + l / K1);
   };
 
-  // ---------------- x sweep from the brick: field f of brick -> R2 slots (phase A: f=0..6, phase B: f=7..10)
-  auto sweep_x = [&](int f0, int nvel, int out_vel, int out_p, int out_h, int nh) {
-    // jobs: [0,nvel): velocity comps (B,D,S); nvel: pressure (B,D); then nh value-only fields
-    const int jobs = nvel + 1 + nh;
-    for (int t = tid; t < ncell * jobs * L2; t += blockDim.x) {
-      const int ci = t / (jobs * L2), r = t % (jobs * L2), job = r / L2, l = r % L2;
-      const int b = ci / 8, cc = ci % 8, cx = cc & 1, cy = (cc >> 1) & 1, cz = cc >> 2;
-      const int i1 = l % K1, i2 = l / K1;
-      const int base = K * cx + BN * (K * cy + i1) + BN * BN * (K * cz + i2);
-      const int f = job < nvel ? f0 + job : (job == nvel ? f0 + nvel : f0 + nvel + 1 + (job - nvel - 1));
+  // velocity-type field (value, grad, Laplacian): brick field f -> (val, g0, g1, g2, lap) for this lane
+  auto vel_field = [&](int f, double &val, double (&g)[3], double &lap) {
+    // x sweep: tasks (cell, line, mat) = CPW*L2*3
+    for (int t = lane; t < CPW * L2 * 3; t += 64) {
+      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
+      const double *src = BF(f) + bline(ci, l);
       double in[K1], o[K1];
-      const double *src = BF(b, f) + base;
 #pragma unroll
       for (int e = 0; e < K1; ++e) in[e] = src[e];
-      if (job < nvel) {
-        double *d0 = A2(ci, out_vel + 3 * job), *d1 = d0 + N3, *d2 = d1 + N3;
-        fwd<K1>(T.V, in, o);
+      if (m == 0) fwd<K1>(T.V, in, o);
+      else if (m == 1) fwd<K1>(T.D, in, o);
+      else fwd<K1>(T.S, in, o);
+      double *dst = X(ci, m);
 #pragma unroll
-        for (int e = 0; e < K1; ++e) d0[loff<0, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) dst[loff<0, K1>(l, e)] = o[e];
+    }
+    wave_sync();
+    // y sweep: tasks (cell, line, type): 0: X_B -> BB, BD; 1: X_D -> DB; 2: L = wx B(X_S) + wy S(X_B)
+    for (int t = lane; t < CPW * L2 * 3; t += 64) {
+      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
+      double a[K1], o[K1];
+      if (m == 0) {
+        const double *s = X(ci, 0);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
+        fwd<K1>(T.V, a, o);
+        double *d = Yr(ci, 0);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+        fwd<K1>(T.D, a, o);
+        d = Yr(ci, 1);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+      } else if (m == 1) {
+        const double *s = X(ci, 1);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
+        fwd<K1>(T.V, a, o);
+        double *d = Yr(ci, 2);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+      } else {
+        const int cg = brick * 8 + ci;
+        const double hx_ = P.geo[cg * 4 + 0], hy_ = P.geo[cg * 4 + 1];
+        const double wxx = 1.0 / (hx_ * hx_), wyy = 1.0 / (hy_ * hy_);
+        const double *s0 = X(ci, 0), *s2 = X(ci, 2);
+        double b[K1], o2[K1];
+#pragma unroll
+        for (int e = 0; e < K1; ++e) { a[e] = s0[loff<1, K1>(l, e)]; b[e] = s2[loff<1, K1>(l, e)]; }
+        fwd<K1>(T.S, a, o);
+        fwd<K1>(T.V, b, o2);
+        double *d = Yr(ci, 3);
+#pragma unroll
+        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = wyy * o[e] + wxx * o2[e];
+      }
+    }
+    wave_sync();
+    // z sweep fused into the pointwise read
+    if (pact) {
+      const int l = qx + K1 * qy;
+      double bb[K1], bd[K1], db[K1], ll[K1];
+#pragma unroll
+      for (int e = 0; e < K1; ++e) {
+        bb[e] = Yr(pci, 0)[loff<2, K1>(l, e)];
+        bd[e] = Yr(pci, 1)[loff<2, K1>(l, e)];
+        db[e] = Yr(pci, 2)[loff<2, K1>(l, e)];
+        ll[e] = Yr(pci, 3)[loff<2, K1>(l, e)];
+      }
+      double v = 0., gz = 0., zz = 0., gx = 0., gy = 0., lp = 0.;
+#pragma unroll
+      for (int e = 0; e < K1; ++e) {
+        v += Bz[e] * bb[e];
+        gz += Dz[e] * bb[e];
+        zz += Sz[e] * bb[e];
+        gx += Bz[e] * db[e];
+        gy += Bz[e] * bd[e];
+        lp += Bz[e] * ll[e];
+      }
+      val = v;
+      g[0] = gx * ih[0];
+      g[1] = gy * ih[1];
+      g[2] = gz * ih[2];
+      lap = lp + wz * zz;
+    }
+    wave_sync();  // Y is rewritten by the next field's y sweep
+  };
+
+  // pressure-type field (value, grad) [+ up to 3 value-only fields]: fp -> (pv, pg); fh.. -> hv[]
+  auto scal_fields = [&](int fp, int nh, int fh0, double &pv, double (&pg)[3], double (&hv)[3]) {
+    // x: tasks (cell, line, job): job 0: p (B -> X0, D -> X1); job 1..nh: H comp (B -> X2+j)
+    const int nj = 1 + nh;
+    for (int t = lane; t < CPW * L2 * nj; t += 64) {
+      const int ci = cbase + t / (L2 * nj), r = t % (L2 * nj), l = r / nj, j = r % nj;
+      const double *src = BF(j == 0 ? fp : fh0 + j - 1) + bline(ci, l);
+      double in[K1], o[K1];
+#pragma unroll
+      for (int e = 0; e < K1; ++e) in[e] = src[e];
+      fwd<K1>(T.V, in, o);
+      double *d = X(ci, j == 0 ? 0 : 1 + j);
+#pragma unroll
+      for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
+      if (j == 0) {
         fwd<K1>(T.D, in, o);
+        d = X(ci, 1);
 #pragma unroll
-        for (int e = 0; e < K1; ++e) d1[loff<0, K1>(l, e)] = o[e];
-        fwd<K1>(T.S, in, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d2[loff<0, K1>(l, e)] = o[e];
-      } else if (job == nvel) {
-        double *d0 = A2(ci, out_p), *d1 = d0 + N3;
-        fwd<K1>(T.V, in, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d0[loff<0, K1>(l, e)] = o[e];
-        fwd<K1>(T.D, in, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d1[loff<0, K1>(l, e)] = o[e];
-      } else {
-        double *d0 = A2(ci, out_h + (job - nvel - 1));
-        fwd<K1>(T.V, in, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d0[loff<0, K1>(l, e)] = o[e];
+        for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
       }
     }
-  };
-
-  // ---------------- y sweep R2 -> R1: velocity comps (X_B,X_D,X_S -> BB,BD,DB,L), pressure (BB,BD,DB), H (BB)
-  auto sweep_y = [&](int nvel, int in_p, int in_h, int nh) {
-    const int jobs = nvel + 1 + nh;
-    for (int t = tid; t < ncell * jobs * L2; t += blockDim.x) {
-      const int ci = t / (jobs * L2), r = t % (jobs * L2), job = r / L2, l = r % L2;
-      double hx, hy, hz;
-      cell_h(ci, hx, hy, hz);
-      double a[K1], bq[K1], o[K1], o2[K1];
-      if (job < nvel) {
-        const double *xb = A2(ci, 3 * job), *xd = xb + N3, *xs = xd + N3;
-        double *dbb = A1(ci, 4 * job), *dbd = dbb + N3, *ddb = dbd + N3, *dl = ddb + N3;
+    wave_sync();
+    // y: job 0: X0 -> BB (Y0), BD (Y1); job 1: X1 -> DB (Y2); job 1+j: X(1+j) -> Y(2+j)
+    const int ny = 2 + nh;
+    for (int t = lane; t < CPW * L2 * ny; t += 64) {
+      const int ci = cbase + t / (L2 * ny), r = t % (L2 * ny), l = r / ny, j = r % ny;
+      const double *s = X(ci, j == 0 ? 0 : j);
+      double a[K1], o[K1];
 #pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = xb[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
+      for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
+      fwd<K1>(T.V, a, o);
+      double *d = Yr(ci, j == 0 ? 0 : 1 + j);
 #pragma unroll
-        for (int e = 0; e < K1; ++e) dbb[loff<1, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+      if (j == 0) {
         fwd<K1>(T.D, a, o);
+        d = Yr(ci, 1);
 #pragma unroll
-        for (int e = 0; e < K1; ++e) dbd[loff<1, K1>(l, e)] = o[e];
-        fwd<K1>(T.S, a, o, 1.0 / (hy * hy));
-#pragma unroll
-        for (int e = 0; e < K1; ++e) bq[e] = xs[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, bq, o2, 1.0 / (hx * hx));
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dl[loff<1, K1>(l, e)] = o[e] + o2[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = xd[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) ddb[loff<1, K1>(l, e)] = o[e];
-      } else if (job == nvel) {
-        const double *xb = A2(ci, in_p), *xd = xb + N3;
-        double *dbb = A1(ci, 12), *dbd = dbb + N3, *ddb = dbd + N3;
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = xb[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dbb[loff<1, K1>(l, e)] = o[e];
-        fwd<K1>(T.D, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dbd[loff<1, K1>(l, e)] = o[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = xd[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) ddb[loff<1, K1>(l, e)] = o[e];
-      } else {
-        const int hcmp = job - nvel - 1;
-        const double *xb = A2(ci, in_h + hcmp);
-        double *dbb = A1(ci, 15 + hcmp);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = xb[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dbb[loff<1, K1>(l, e)] = o[e];
+        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
       }
     }
-  };
-
-  // ---------------- z sweep R1 -> R2: velocity -> (val,gx,gy,gz,L) at 5c; pressure -> (gx,gy,gz,val) at 15..18; H -> 19..
-  auto sweep_z = [&](int nvel, int nh) {
-    const int jobs = nvel + 1 + nh;
-    for (int t = tid; t < ncell * jobs * L2; t += blockDim.x) {
-      const int ci = t / (jobs * L2), r = t % (jobs * L2), job = r / L2, l = r % L2;
-      double hx, hy, hz;
-      cell_h(ci, hx, hy, hz);
-      double a[K1], o[K1], o2[K1];
-      if (job < nvel) {
-        const double *ybb = A1(ci, 4 * job), *ybd = ybb + N3, *ydb = ybd + N3, *yl = ydb + N3;
-        double *dv = A2(ci, 5 * job), *dgx = dv + N3, *dgy = dgx + N3, *dgz = dgy + N3, *dl = dgz + N3;
+    wave_sync();
+    if (pact) {
+      const int l = qx + K1 * qy;
+      double bb[K1], bd[K1], db[K1];
 #pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ybb[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
+      for (int e = 0; e < K1; ++e) {
+        bb[e] = Yr(pci, 0)[loff<2, K1>(l, e)];
+        bd[e] = Yr(pci, 1)[loff<2, K1>(l, e)];
+        db[e] = Yr(pci, 2)[loff<2, K1>(l, e)];
+      }
+      double v = 0., gz = 0., gx = 0., gy = 0.;
 #pragma unroll
-        for (int e = 0; e < K1; ++e) dv[loff<2, K1>(l, e)] = o[e];
-        fwd<K1>(T.D, a, o);
+      for (int e = 0; e < K1; ++e) {
+        v += Bz[e] * bb[e];
+        gz += Dz[e] * bb[e];
+        gx += Bz[e] * db[e];
+        gy += Bz[e] * bd[e];
+      }
+      pv = v;
+      pg[0] = gx * ih[0];
+      pg[1] = gy * ih[1];
+      pg[2] = gz * ih[2];
+      for (int j = 0; j < nh; ++j) {
+        double s = 0.;
 #pragma unroll
-        for (int e = 0; e < K1; ++e) dgz[loff<2, K1>(l, e)] = o[e];
-        fwd<K1>(T.S, a, o, 1.0 / (hz * hz));
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = yl[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o2);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dl[loff<2, K1>(l, e)] = o[e] + o2[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ydb[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dgx[loff<2, K1>(l, e)] = o[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ybd[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dgy[loff<2, K1>(l, e)] = o[e];
-      } else if (job == nvel) {
-        const double *ybb = A1(ci, 12), *ybd = ybb + N3, *ydb = ybd + N3;
-        double *dgx = A2(ci, 15), *dgy = dgx + N3, *dgz = dgy + N3, *dv = dgz + N3;
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ybb[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dv[loff<2, K1>(l, e)] = o[e];
-        fwd<K1>(T.D, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dgz[loff<2, K1>(l, e)] = o[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ydb[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dgx[loff<2, K1>(l, e)] = o[e];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ybd[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dgy[loff<2, K1>(l, e)] = o[e];
-      } else {
-        const int hcmp = job - nvel - 1;
-        const double *ybb = A1(ci, 15 + hcmp);
-        double *dv = A2(ci, 19 + hcmp);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = ybb[loff<2, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) dv[loff<2, K1>(l, e)] = o[e];
+        for (int e = 0; e < K1; ++e) s += Bz[e] * Yr(pci, 3 + j)[loff<2, K1>(l, e)];
+        hv[j] = s;
       }
     }
+    wave_sync();
   };
 
-  // ---------------- phase A: state at quadrature points
-  sweep_x(0, 3, 0, 9, 11, 3);
-  __syncthreads();
-  sweep_y(3, 9, 11, 3);
-  __syncthreads();
-  sweep_z(3, 3);
-  __syncthreads();
+  // ---------------- phase A: state at this lane's quadrature point
+  double u[3] = {0., 0., 0.}, gu[3][3] = {}, lu[3] = {0., 0., 0.};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) vel_field(c, u[c], gu[c], lu[c]);
+  double pq = 0., gp[3] = {0., 0., 0.}, Hq[3] = {0., 0., 0.};
+  scal_fields(3, 3, 4, pq, gp, Hq);
 
-  const bool active = tid < ncell * N3;
-  const int ci = tid / N3, q = tid % N3;
-  double hx = 1, hy = 1, hz = 1;
-  double u[3] = {}, gu[3][3] = {}, R[3] = {}, tau = 0., JxW = 0.;
+  const double nu = P.nu;
+  const double JxW = T.w[qx] * T.w[qy] * T.w[qz] * hx * hy * hz;
+  const double hst = P.geo[gcell * 4 + 3];
+  const double un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  const double u_mag = fmax(sqrt(un2), 1e-12);
+  const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
+  const double tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
+  double f[3] = {0., 0., 0.};
+  if (P.force_q && pact) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) f[c] = P.force_q[((int64_t)gcell * N3 + q) * 3 + c];
+  }
+  double Gu[3], R[3], srf[3] = {0., 0., 0.};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Gu[c] = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
+    R[c] = Gu[c] + gp[c] - nu * lu[c] - f[c];
+  }
+  if (P.srf) {
+    const double *om = P.omega;
+    const double xq[3] = {P.x0[gcell * 3 + 0] + hx * T.xi[qx], P.x0[gcell * 3 + 1] + hy * T.xi[qy],
+                          P.x0[gcell * 3 + 2] + hz * T.xi[qz]};
+    const double cx_[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
+    const double ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2], om[0] * xq[1] - om[1] * xq[0]};
+    const double cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      srf[c] = 2 * cx_[c] + cc[c];
+      R[c] += srf[c];
+    }
+  }
+  double Tt[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Tt[c] = P.alpha[0] * u[c] + Hq[c];
+    R[c] += Tt[c];
+  }
+
   double Tc[16];
-  if (active) {
-    cell_h(ci, hx, hy, hz);
-    const int cell = b0 * 8 + ci;
-    const int qx = q % K1, qy = (q / K1) % K1, qz = q / (K1 * K1);
-    const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
-    const double hst = P.geo[cell * 4 + 3];
-    JxW = T.w[qx] * T.w[qy] * T.w[qz] * hx * hy * hz;
-    double lu[3], gp[3], Hq[3], pq;
+  if constexpr (!JV) {  // residual test coefficients (rhs = -R)
+    const double divu = gu[0][0] + gu[1][1] + gu[2][2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      u[c] = A2(ci, 5 * c)[q];
+      Tc[4 * c] = JxW * (-Gu[c] + f[c] - Tt[c] - srf[c]);
 #pragma unroll
-      for (int e = 0; e < 3; ++e) gu[c][e] = A2(ci, 5 * c + 1 + e)[q] * ih[e];
-      lu[c] = A2(ci, 5 * c + 4)[q];
-      gp[c] = A2(ci, 15 + c)[q] * ih[c];
-      Hq[c] = A2(ci, 19 + c)[q];
+      for (int e = 0; e < 3; ++e)
+        Tc[4 * c + 1 + e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]) * ih[e];
     }
-    pq = A2(ci, 18)[q];
-    const double nu = P.nu;
-    const double un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
-    const double u_mag = fmax(sqrt(un2), 1e-12);
-    const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
-    tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
-    double f[3] = {0., 0., 0.};
-    if (P.force_q) {
+    Tc[12] = -JxW * divu;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) f[c] = P.force_q[((int64_t)cell * N3 + q) * 3 + c];
-    }
-    double Gu[3], srf[3] = {0., 0., 0.};
+    for (int e = 0; e < 3; ++e) Tc[13 + e] = -JxW * tau * R[e] * ih[e];
+  } else {
+    // ---------------- phase B: the trial function v at this lane's quadrature point
+    double v[3] = {0., 0., 0.}, gv[3][3] = {}, lv[3] = {0., 0., 0.};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) vel_field(7 + c, v[c], gv[c], lv[c]);
+    double vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
+    scal_fields(10, 0, 0, vp, gvp, dummy);
+    const double aj = P.alpha_jac;
+    double S[3], A[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      Gu[c] = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
-      R[c] = Gu[c] + gp[c] - nu * lu[c] - f[c];
+      const double guv = gu[c][0] * v[0] + gu[c][1] * v[1] + gu[c][2] * v[2];
+      const double gvu = gv[c][0] * u[0] + gv[c][1] * u[1] + gv[c][2] * u[2];
+      A[c] = guv + gvu + aj * v[c];
+      S[c] = guv + gvu + gvp[c] - nu * lv[c] + aj * v[c];
     }
     if (P.srf) {
       const double *om = P.omega;
-      const double xq[3] = {P.x0[cell * 3 + 0] + hx * T.xi[qx], P.x0[cell * 3 + 1] + hy * T.xi[qy],
-                            P.x0[cell * 3 + 2] + hz * T.xi[qz]};
-      const double cx_[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
-      const double ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2], om[0] * xq[1] - om[1] * xq[0]};
-      const double cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
+      const double cj[3] = {2 * (om[1] * v[2] - om[2] * v[1]), 2 * (om[2] * v[0] - om[0] * v[2]),
+                            2 * (om[0] * v[1] - om[1] * v[0])};
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        srf[c] = 2 * cx_[c] + cc[c];
-        R[c] += srf[c];
-      }
+      for (int c = 0; c < 3; ++c) { A[c] += cj[c]; S[c] += cj[c]; }
     }
-    double Tt[3];
+    const double divv = gv[0][0] + gv[1][1] + gv[2][2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      Tt[c] = P.alpha[0] * u[c] + Hq[c];
-      R[c] += Tt[c];
+      Tc[4 * c] = JxW * A[c];
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        Tc[4 * c + 1 + e] = JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
     }
-    if constexpr (!JV) {  // residual test coefficients (rhs = -R)
-      const double divu = gu[0][0] + gu[1][1] + gu[2][2];
+    Tc[12] = JxW * divv;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        Tc[4 * c] = JxW * (-Gu[c] + f[c] - Tt[c] - srf[c]);
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          Tc[4 * c + 1 + e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]) * ih[e];
-      }
-      Tc[12] = -JxW * divu;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) Tc[13 + e] = -JxW * tau * R[e] * ih[e];
-    }
-  }
-  __syncthreads();  // R1/R2 reusable
-
-  if constexpr (JV) {
-    // ---------------- phase B: trial function v at quadrature points
-    sweep_x(7, 3, 0, 9, 0, 0);
-    __syncthreads();
-    sweep_y(3, 9, 0, 0);
-    __syncthreads();
-    sweep_z(3, 0);
-    __syncthreads();
-    if (active) {
-      const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
-      const double nu = P.nu, aj = P.alpha_jac;
-      double v[3], gv[3][3], lv[3], gvp[3], vp;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        v[c] = A2(ci, 5 * c)[q];
-#pragma unroll
-        for (int e = 0; e < 3; ++e) gv[c][e] = A2(ci, 5 * c + 1 + e)[q] * ih[e];
-        lv[c] = A2(ci, 5 * c + 4)[q];
-        gvp[c] = A2(ci, 15 + c)[q] * ih[c];
-      }
-      vp = A2(ci, 18)[q];
-      double S[3], A[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const double guv = gu[c][0] * v[0] + gu[c][1] * v[1] + gu[c][2] * v[2];
-        const double gvu = gv[c][0] * u[0] + gv[c][1] * u[1] + gv[c][2] * u[2];
-        A[c] = guv + gvu + aj * v[c];
-        S[c] = guv + gvu + gvp[c] - nu * lv[c] + aj * v[c];
-      }
-      if (P.srf) {
-        const double *om = P.omega;
-        const double cj[3] = {2 * (om[1] * v[2] - om[2] * v[1]), 2 * (om[2] * v[0] - om[0] * v[2]),
-                              2 * (om[0] * v[1] - om[1] * v[0])};
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { A[c] += cj[c]; S[c] += cj[c]; }
-      }
-      const double divv = gv[0][0] + gv[1][1] + gv[2][2];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        Tc[4 * c] = JxW * A[c];
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          Tc[4 * c + 1 + e] =
-              JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
-      }
-      Tc[12] = JxW * divv;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) Tc[13 + e] = JxW * tau * S[e] * ih[e];
-    }
-    __syncthreads();
+    for (int e = 0; e < 3; ++e) Tc[13 + e] = JxW * tau * S[e] * ih[e];
   }
 
-  // ---------------- test coefficients -> R1 slots 4f + {val, gx, gy, gz}
-  if (active) {
+  // ---------------- integration, one test field at a time (wave-local)
 #pragma unroll
-    for (int s = 0; s < 16; ++s) A1(ci, s)[q] = Tc[s];
-  }
-  __syncthreads();
-  // transposed z: Z0 = B^T Tv + D^T Tz, Z1 = B^T Tx, Z2 = B^T Ty  -> R2 3f+{0,1,2}
-  for (int t = tid; t < ncell * 4 * L2; t += blockDim.x) {
-    const int c_ = t / (4 * L2), r = t % (4 * L2), fld = r / L2, l = r % L2;
-    const double *tv = A1(c_, 4 * fld), *tx = tv + N3, *ty = tx + N3, *tz = ty + N3;
-    double a[K1], o[K1];
-    double *z0 = A2(c_, 3 * fld), *z1 = z0 + N3, *z2 = z1 + N3;
+  for (int fld = 0; fld < 4; ++fld) {
+    if (pact) {
+      X(pci, 0)[q] = Tc[4 * fld];
+      X(pci, 1)[q] = Tc[4 * fld + 1];
+      X(pci, 2)[q] = Tc[4 * fld + 2];
+      X(pci, 3)[q] = Tc[4 * fld + 3];
+    }
+    wave_sync();
+    // transposed z: Z0 = B^T Tv + D^T Tz -> Y0; Z1 = B^T Tx -> Y1; Z2 = B^T Ty -> Y2
+    for (int t = lane; t < CPW * L2 * 3; t += 64) {
+      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
+      double a[K1], o[K1];
+      const double *s = X(ci, m == 0 ? 0 : m);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = 0.;
+      for (int e = 0; e < K1; ++e) a[e] = s[loff<2, K1>(l, e)];
+      bwd<K1>(T.V, a, o);
+      if (m == 0) {
+        const double *s3 = X(ci, 3);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) a[e] = tv[loff<2, K1>(l, e)];
-    bwd_add<K1>(T.V, a, o);
+        for (int e = 0; e < K1; ++e) a[e] = s3[loff<2, K1>(l, e)];
+        bwd_add<K1>(T.D, a, o);
+      }
+      double *d = Yr(ci, m);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) a[e] = tz[loff<2, K1>(l, e)];
-    bwd_add<K1>(T.D, a, o);
+      for (int e = 0; e < K1; ++e) d[loff<2, K1>(l, e)] = o[e];
+    }
+    wave_sync();
+    // transposed y: W0 = B^T Z0 + D^T Z2 -> X0; W1 = B^T Z1 -> X1
+    for (int t = lane; t < CPW * L2 * 2; t += 64) {
+      const int ci = cbase + t / (L2 * 2), r = t % (L2 * 2), l = r / 2, m = r % 2;
+      double a[K1], o[K1];
+      const double *s = Yr(ci, m);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) z0[loff<2, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
+      bwd<K1>(T.V, a, o);
+      if (m == 0) {
+        const double *s2 = Yr(ci, 2);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) { a[e] = tx[loff<2, K1>(l, e)]; o[e] = 0.; }
-    bwd_add<K1>(T.V, a, o);
+        for (int e = 0; e < K1; ++e) a[e] = s2[loff<1, K1>(l, e)];
+        bwd_add<K1>(T.D, a, o);
+      }
+      double *d = X(ci, m);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) z1[loff<2, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+    }
+    wave_sync();
+    // transposed x: out = B^T W0 + D^T W1 (node-indexed)
+    for (int t = lane; t < CPW * L2; t += 64) {
+      const int ci = cbase + t / L2, l = t % L2;
+      double a[K1], o[K1];
+      const double *s0 = X(ci, 0), *s1 = X(ci, 1);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) { a[e] = ty[loff<2, K1>(l, e)]; o[e] = 0.; }
-    bwd_add<K1>(T.V, a, o);
+      for (int e = 0; e < K1; ++e) a[e] = s0[loff<0, K1>(l, e)];
+      bwd<K1>(T.V, a, o);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) z2[loff<2, K1>(l, e)] = o[e];
-  }
-  __syncthreads();
-  // transposed y: W0 = B^T Z0 + D^T Z2, W1 = B^T Z1 -> R1 2f+{0,1}
-  for (int t = tid; t < ncell * 4 * L2; t += blockDim.x) {
-    const int c_ = t / (4 * L2), r = t % (4 * L2), fld = r / L2, l = r % L2;
-    const double *z0 = A2(c_, 3 * fld), *z1 = z0 + N3, *z2 = z1 + N3;
-    double *w0 = A1(c_, 2 * fld), *w1 = w0 + N3;
-    double a[K1], o[K1];
+      for (int e = 0; e < K1; ++e) a[e] = s1[loff<0, K1>(l, e)];
+      bwd_add<K1>(T.D, a, o);
+      double *d = Out(ci, fld);
 #pragma unroll
-    for (int e = 0; e < K1; ++e) { a[e] = z0[loff<1, K1>(l, e)]; o[e] = 0.; }
-    bwd_add<K1>(T.V, a, o);
-#pragma unroll
-    for (int e = 0; e < K1; ++e) a[e] = z2[loff<1, K1>(l, e)];
-    bwd_add<K1>(T.D, a, o);
-#pragma unroll
-    for (int e = 0; e < K1; ++e) w0[loff<1, K1>(l, e)] = o[e];
-#pragma unroll
-    for (int e = 0; e < K1; ++e) { a[e] = z1[loff<1, K1>(l, e)]; o[e] = 0.; }
-    bwd_add<K1>(T.V, a, o);
-#pragma unroll
-    for (int e = 0; e < K1; ++e) w1[loff<1, K1>(l, e)] = o[e];
-  }
-  __syncthreads();
-  // transposed x: out = B^T W0 + D^T W1 -> R2 slot 12+f (node-indexed)
-  for (int t = tid; t < ncell * 4 * L2; t += blockDim.x) {
-    const int c_ = t / (4 * L2), r = t % (4 * L2), fld = r / L2, l = r % L2;
-    const double *w0 = A1(c_, 2 * fld), *w1 = w0 + N3;
-    double *out = A2(c_, 12 + fld);
-    double a[K1], o[K1];
-#pragma unroll
-    for (int e = 0; e < K1; ++e) { a[e] = w0[loff<0, K1>(l, e)]; o[e] = 0.; }
-    bwd_add<K1>(T.V, a, o);
-#pragma unroll
-    for (int e = 0; e < K1; ++e) a[e] = w1[loff<0, K1>(l, e)];
-    bwd_add<K1>(T.D, a, o);
-#pragma unroll
-    for (int e = 0; e < K1; ++e) out[loff<0, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
+    }
+    wave_sync();
   }
   __syncthreads();
 
   // ---------------- brick reduction (fixed order) + scatter
-  for (int t = tid; t < nb * BN3 * 4; t += blockDim.x) {
-    const int b = t / (BN3 * 4), r = t % (BN3 * 4), n = r / 4, fld = r % 4;
-    const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
+  for (int t = tid; t < BN3 * 4; t += blockDim.x) {
+    const int n = t >> 2, fld = t & 3;
+    const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
     double s = 0.;
 #pragma unroll
     for (int cz = 0; cz < 2; ++cz) {
-      const int az = Z - K * cz;
+      const int az = Zn - K * cz;
       if (az < 0 || az > K) continue;
 #pragma unroll
       for (int cy = 0; cy < 2; ++cy) {
-        const int ay = Y - K * cy;
+        const int ay = Yn - K * cy;
         if (ay < 0 || ay > K) continue;
 #pragma unroll
         for (int cx = 0; cx < 2; ++cx) {
-          const int ax = X - K * cx;
+          const int ax = Xn - K * cx;
           if (ax < 0 || ax > K) continue;
-          s += A2(b * 8 + cx + 2 * cy + 4 * cz, 12 + fld)[ax + K1 * (ay + K1 * az)];
+          s += Out(cx + 2 * cy + 4 * cz, fld)[ax + K1 * (ay + K1 * az)];
         }
       }
     }
-    const int node = sNode[b * BN3 + n];
+    const int node = sNode[n];
     const int64_t gi = fld < 3 ? (int64_t)node * 3 + fld : voff + node;
-    const bool interior = X > 0 && X < BN - 1 && Y > 0 && Y < BN - 1 && Z > 0 && Z < BN - 1;
+    const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
     if (interior) P.y[gi] = s;
     else atomicAdd(&P.y[gi], s);
   }
@@ -536,8 +517,7 @@ template <int K>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
   const int NF = mode == MODE_JV ? 11 : 7;
-  return sizeof(double) * ((size_t)C::NB * NF * C::BN3 + (size_t)C::NC * (C::R1N + C::R2N) * C::N3) +
-         sizeof(int) * (size_t)C::NB * C::BN3;
+  return sizeof(double) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3) + sizeof(int) * (size_t)C::BN3;
 }
 
 template <int K>
@@ -545,20 +525,11 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   using C = BrickCfg<K>;
   const int n_bricks = P.n_cells / 8;
   if (n_bricks <= 0) return hipSuccess;
-  const int blocks = (n_bricks + C::NB - 1) / C::NB;
   const size_t lds = brick_lds_bytes<K>(mode);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void *)gls_brick_kernel<K, MODE_RESIDUAL>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)brick_lds_bytes<K>(MODE_JV));
-    (void)hipFuncSetAttribute((const void *)gls_brick_kernel<K, MODE_JV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)brick_lds_bytes<K>(MODE_JV));
-    attr = true;
-  }
   if (mode == MODE_JV)
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(blocks), dim3(C::THREADS), lds, s, P, T);
+    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
   else
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(blocks), dim3(C::THREADS), lds, s, P, T);
+    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
   return hipGetLastError();
 }
 
