@@ -23,6 +23,13 @@
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
 
+#ifndef GLS_ABL
+#define GLS_ABL 0  // timing-only ablations: 1 no global gather, 2 no scatter, 4 no sweeps
+#endif
+#ifndef GLS_BRICK_WAVES_PER_EU
+#define GLS_BRICK_WAVES_PER_EU 4
+#endif
+
 namespace gls {
 
 template <int K>
@@ -82,12 +89,16 @@ __device__ __forceinline__ void bwd_add(const double (&M)[kMaxQ1D][kMaxNodes1D],
 // LDS hand-off between lanes of ONE wave: LDS ops of a wave execute in order; the asm keeps the
 // compiler from moving LDS accesses across this point.
 __device__ __forceinline__ void wave_sync() {
+#ifdef GLS_WAVE_SYNC_DRAIN
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+  asm volatile("" ::: "memory");
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 
 template <int K, int MODE>
-__global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const OpParams P, const Tables1D T) {
+__global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
   constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
   constexpr bool JV = MODE == MODE_JV;
@@ -95,7 +106,8 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *sB = smem;                                   // [NF][BN3]
   double *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
-  int *sNode = reinterpret_cast<int *>(sC + 8 * C::PER_CELL * N3);  // [BN3]
+  double *sM = sC + 8 * C::PER_CELL * N3;             // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4]
+  int *sNode = reinterpret_cast<int *>(sM + 5 * 16 + 8);  // [BN3]
   auto BF = [&](int f) { return sB + f * BN3; };
 
   const int tid = threadIdx.x;
@@ -103,9 +115,29 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
   const int brick = blockIdx.x;
   const int64_t voff = (int64_t)3 * P.n_vnodes;
 
+  if (tid < 5 * 16) {
+    const int mat = tid >> 4, r = (tid >> 2) & 3, c = tid & 3;
+    double v = 0.;
+    if (r < K1 && c < K1) {
+      if (mat == 0) v = T.V[r][c];
+      else if (mat == 1) v = T.D[r][c];
+      else if (mat == 2) v = T.S[r][c];
+      else if (mat == 3) v = T.V[c][r];
+      else v = T.D[c][r];
+    }
+    sM[tid] = v;
+  } else if (tid < 5 * 16 + 8) {
+    const int j = (tid - 80) & 3;
+    sM[tid] = j < K1 ? (tid < 84 ? T.w[j] : T.xi[j]) : 0.0;
+  }
   // ---------------- gather the brick's nodes (all waves)
   for (int t = tid; t < 3 * BN3; t += blockDim.x) {
     const int g = t / BN3, n = t % BN3;
+    if (GLS_ABL & 1) {
+      for (int f = 0; f < NF; ++f) BF(f)[n] = 0.001 * (n + f);
+      if (g == 0) sNode[n] = (brick * 37 + n) % P.n_vnodes;
+      continue;
+    }
     const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
     const int cx = min(X / K, 1), cy = min(Y / K, 1), cz = min(Z / K, 1);
     const int a = (X - K * cx) + K1 * ((Y - K * cy) + K1 * (Z - K * cz));
@@ -151,173 +183,134 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
   const int gcell = brick * 8 + pci;
   const double hx = P.geo[gcell * 4 + 0], hy = P.geo[gcell * 4 + 1], hz = P.geo[gcell * 4 + 2];
   const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
-  const double wx = ih[0] * ih[0], wy = ih[1] * ih[1], wz = ih[2] * ih[2];
-  // this lane's rows of the z matrices (q-dependent -> registers)
+  const double wz = ih[2] * ih[2];
+  // this lane's rows of the z matrices (q-dependent -> registers; tables staged in LDS above)
   double Bz[K1], Dz[K1], Sz[K1];
 #pragma unroll
-  for (int i = 0; i < K1; ++i) { Bz[i] = T.V[qz][i]; Dz[i] = T.D[qz][i]; Sz[i] = T.S[qz][i]; }
+  for (int i = 0; i < K1; ++i) { Bz[i] = sM[0 * 16 + qz * 4 + i]; Dz[i] = sM[1 * 16 + qz * 4 + i]; Sz[i] = sM[2 * 16 + qz * 4 + i]; }
 
-  // brick-array line base for (cell-in-brick, line (i1,i2)) in an x sweep
-  auto bline = [&](int ci, int l) {
-    const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
-    return K * cx + BN * (K * cy + l % K1) + BN * BN * (K * cz + l / K1);
+  // Lane <-> output element: every stage computes entry [i2][i1][i0] of its output arrays for the
+  // lane's cell (the same lanes as the pointwise (cell, q) mapping), reading one 1D line of each
+  // input array; per-lane matrix rows come from the LDS copy of the 1D tables. No divergence.
+  const int i0 = qx, i1 = qy, i2 = qz;
+  const int me = q;  // offset of this lane's element in a per-cell array
+  // brick x-line base of this lane's (cell, y=i1, z=i2) line
+  const int cxb = pci & 1, cyb = (pci >> 1) & 1, czb = pci >> 2;
+  const int bx_base = K * cxb + BN * (K * cyb + i1) + BN * BN * (K * czb + i2);
+  auto row = [&](int mat, int r, double (&o)[K1]) {  // o[k] = M[r][k], mat: 0 V, 1 D, 2 S, 3 V^T, 4 D^T
+    const double *m = sM + mat * 16 + r * 4;
+#pragma unroll
+    for (int k = 0; k < K1; ++k) o[k] = m[k];
+  };
+  auto dot = [&](const double (&a)[K1], const double (&b)[K1]) {
+    double s = 0.;
+#pragma unroll
+    for (int k = 0; k < K1; ++k) s += a[k] * b[k];
+    return s;
+  };
+  // line of array A through this lane's element along dim D
+  auto lineD0 = [&](const double *A, double (&o)[K1]) {
+#pragma unroll
+    for (int e = 0; e < K1; ++e) o[e] = A[e + K1 * (i1 + K1 * i2)];
+  };
+  auto lineD1 = [&](const double *A, double (&o)[K1]) {
+#pragma unroll
+    for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (e + K1 * i2)];
+  };
+  auto lineD2 = [&](const double *A, double (&o)[K1]) {
+#pragma unroll
+    for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (i1 + K1 * e)];
   };
 
   // velocity-type field (value, grad, Laplacian): brick field f -> (val, g0, g1, g2, lap) for this lane
   auto vel_field = [&](int f, double &val, double (&g)[3], double &lap) {
-    // x sweep: tasks (cell, line, mat) = CPW*L2*3
-    for (int t = lane; t < CPW * L2 * 3; t += 64) {
-      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
-      const double *src = BF(f) + bline(ci, l);
-      double in[K1], o[K1];
+    if (GLS_ABL & 4) { val = BF(f)[bx_base]; g[0] = g[1] = g[2] = val; lap = val; return; }
+    if (pact) {  // x sweep: X_B, X_D, X_S at [i2][i1][i0]
+      double in[K1], r[K1];
 #pragma unroll
-      for (int e = 0; e < K1; ++e) in[e] = src[e];
-      if (m == 0) fwd<K1>(T.V, in, o);
-      else if (m == 1) fwd<K1>(T.D, in, o);
-      else fwd<K1>(T.S, in, o);
-      double *dst = X(ci, m);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) dst[loff<0, K1>(l, e)] = o[e];
+      for (int e = 0; e < K1; ++e) in[e] = BF(f)[bx_base + e];
+      row(0, i0, r);
+      X(pci, 0)[me] = dot(r, in);
+      row(1, i0, r);
+      X(pci, 1)[me] = dot(r, in);
+      row(2, i0, r);
+      X(pci, 2)[me] = dot(r, in);
     }
     wave_sync();
-    // y sweep: tasks (cell, line, type): 0: X_B -> BB, BD; 1: X_D -> DB; 2: L = wx B(X_S) + wy S(X_B)
-    for (int t = lane; t < CPW * L2 * 3; t += 64) {
-      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
-      double a[K1], o[K1];
-      if (m == 0) {
-        const double *s = X(ci, 0);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-        double *d = Yr(ci, 0);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
-        fwd<K1>(T.D, a, o);
-        d = Yr(ci, 1);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
-      } else if (m == 1) {
-        const double *s = X(ci, 1);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
-        fwd<K1>(T.V, a, o);
-        double *d = Yr(ci, 2);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
-      } else {
-        const int cg = brick * 8 + ci;
-        const double hx_ = P.geo[cg * 4 + 0], hy_ = P.geo[cg * 4 + 1];
-        const double wxx = 1.0 / (hx_ * hx_), wyy = 1.0 / (hy_ * hy_);
-        const double *s0 = X(ci, 0), *s2 = X(ci, 2);
-        double b[K1], o2[K1];
-#pragma unroll
-        for (int e = 0; e < K1; ++e) { a[e] = s0[loff<1, K1>(l, e)]; b[e] = s2[loff<1, K1>(l, e)]; }
-        fwd<K1>(T.S, a, o);
-        fwd<K1>(T.V, b, o2);
-        double *d = Yr(ci, 3);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = wyy * o[e] + wxx * o2[e];
-      }
+    if (pact) {  // y sweep: BB, BD, DB, L = wy S_y(X_B) + wx B_y(X_S)
+      double xb[K1], xd[K1], xs[K1], rb[K1], rd[K1], rs[K1];
+      lineD1(X(pci, 0), xb);
+      lineD1(X(pci, 1), xd);
+      lineD1(X(pci, 2), xs);
+      row(0, i1, rb);
+      row(1, i1, rd);
+      row(2, i1, rs);
+      Yr(pci, 0)[me] = dot(rb, xb);
+      Yr(pci, 1)[me] = dot(rd, xb);
+      Yr(pci, 2)[me] = dot(rb, xd);
+      Yr(pci, 3)[me] = ih[1] * ih[1] * dot(rs, xb) + ih[0] * ih[0] * dot(rb, xs);
     }
     wave_sync();
-    // z sweep fused into the pointwise read
-    if (pact) {
-      const int l = qx + K1 * qy;
+    if (pact) {  // z sweep fused into the pointwise read
       double bb[K1], bd[K1], db[K1], ll[K1];
-#pragma unroll
-      for (int e = 0; e < K1; ++e) {
-        bb[e] = Yr(pci, 0)[loff<2, K1>(l, e)];
-        bd[e] = Yr(pci, 1)[loff<2, K1>(l, e)];
-        db[e] = Yr(pci, 2)[loff<2, K1>(l, e)];
-        ll[e] = Yr(pci, 3)[loff<2, K1>(l, e)];
-      }
-      double v = 0., gz = 0., zz = 0., gx = 0., gy = 0., lp = 0.;
-#pragma unroll
-      for (int e = 0; e < K1; ++e) {
-        v += Bz[e] * bb[e];
-        gz += Dz[e] * bb[e];
-        zz += Sz[e] * bb[e];
-        gx += Bz[e] * db[e];
-        gy += Bz[e] * bd[e];
-        lp += Bz[e] * ll[e];
-      }
-      val = v;
-      g[0] = gx * ih[0];
-      g[1] = gy * ih[1];
-      g[2] = gz * ih[2];
-      lap = lp + wz * zz;
+      lineD2(Yr(pci, 0), bb);
+      lineD2(Yr(pci, 1), bd);
+      lineD2(Yr(pci, 2), db);
+      lineD2(Yr(pci, 3), ll);
+      val = dot(Bz, bb);
+      g[0] = dot(Bz, db) * ih[0];
+      g[1] = dot(Bz, bd) * ih[1];
+      g[2] = dot(Dz, bb) * ih[2];
+      lap = dot(Bz, ll) + wz * dot(Sz, bb);
     }
     wave_sync();  // Y is rewritten by the next field's y sweep
   };
 
   // pressure-type field (value, grad) [+ up to 3 value-only fields]: fp -> (pv, pg); fh.. -> hv[]
   auto scal_fields = [&](int fp, int nh, int fh0, double &pv, double (&pg)[3], double (&hv)[3]) {
-    // x: tasks (cell, line, job): job 0: p (B -> X0, D -> X1); job 1..nh: H comp (B -> X2+j)
-    const int nj = 1 + nh;
-    for (int t = lane; t < CPW * L2 * nj; t += 64) {
-      const int ci = cbase + t / (L2 * nj), r = t % (L2 * nj), l = r / nj, j = r % nj;
-      const double *src = BF(j == 0 ? fp : fh0 + j - 1) + bline(ci, l);
-      double in[K1], o[K1];
+    if (GLS_ABL & 4) { pv = BF(fp)[bx_base]; pg[0] = pg[1] = pg[2] = pv; for (int j = 0; j < nh; ++j) hv[j] = pv; return; }
+    if (pact) {  // x: p -> X0 (B), X1 (D); H_j -> X(2+j) (B)
+      double in[K1], rb[K1], rd[K1];
+      row(0, i0, rb);
+      row(1, i0, rd);
 #pragma unroll
-      for (int e = 0; e < K1; ++e) in[e] = src[e];
-      fwd<K1>(T.V, in, o);
-      double *d = X(ci, j == 0 ? 0 : 1 + j);
+      for (int e = 0; e < K1; ++e) in[e] = BF(fp)[bx_base + e];
+      X(pci, 0)[me] = dot(rb, in);
+      X(pci, 1)[me] = dot(rd, in);
+      for (int j = 0; j < nh; ++j) {
 #pragma unroll
-      for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
-      if (j == 0) {
-        fwd<K1>(T.D, in, o);
-        d = X(ci, 1);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
+        for (int e = 0; e < K1; ++e) in[e] = BF(fh0 + j)[bx_base + e];
+        X(pci, 2 + j)[me] = dot(rb, in);
       }
     }
     wave_sync();
-    // y: job 0: X0 -> BB (Y0), BD (Y1); job 1: X1 -> DB (Y2); job 1+j: X(1+j) -> Y(2+j)
-    const int ny = 2 + nh;
-    for (int t = lane; t < CPW * L2 * ny; t += 64) {
-      const int ci = cbase + t / (L2 * ny), r = t % (L2 * ny), l = r / ny, j = r % ny;
-      const double *s = X(ci, j == 0 ? 0 : j);
-      double a[K1], o[K1];
-#pragma unroll
-      for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
-      fwd<K1>(T.V, a, o);
-      double *d = Yr(ci, j == 0 ? 0 : 1 + j);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
-      if (j == 0) {
-        fwd<K1>(T.D, a, o);
-        d = Yr(ci, 1);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+    if (pact) {  // y: X0 -> BB (Y0), BD (Y1); X1 -> DB (Y2); X(2+j) -> Y(3+j)
+      double a[K1], rb[K1], rd[K1];
+      row(0, i1, rb);
+      row(1, i1, rd);
+      lineD1(X(pci, 0), a);
+      Yr(pci, 0)[me] = dot(rb, a);
+      Yr(pci, 1)[me] = dot(rd, a);
+      lineD1(X(pci, 1), a);
+      Yr(pci, 2)[me] = dot(rb, a);
+      for (int j = 0; j < nh; ++j) {
+        lineD1(X(pci, 2 + j), a);
+        Yr(pci, 3 + j)[me] = dot(rb, a);
       }
     }
     wave_sync();
     if (pact) {
-      const int l = qx + K1 * qy;
       double bb[K1], bd[K1], db[K1];
-#pragma unroll
-      for (int e = 0; e < K1; ++e) {
-        bb[e] = Yr(pci, 0)[loff<2, K1>(l, e)];
-        bd[e] = Yr(pci, 1)[loff<2, K1>(l, e)];
-        db[e] = Yr(pci, 2)[loff<2, K1>(l, e)];
-      }
-      double v = 0., gz = 0., gx = 0., gy = 0.;
-#pragma unroll
-      for (int e = 0; e < K1; ++e) {
-        v += Bz[e] * bb[e];
-        gz += Dz[e] * bb[e];
-        gx += Bz[e] * db[e];
-        gy += Bz[e] * bd[e];
-      }
-      pv = v;
-      pg[0] = gx * ih[0];
-      pg[1] = gy * ih[1];
-      pg[2] = gz * ih[2];
+      lineD2(Yr(pci, 0), bb);
+      lineD2(Yr(pci, 1), bd);
+      lineD2(Yr(pci, 2), db);
+      pv = dot(Bz, bb);
+      pg[0] = dot(Bz, db) * ih[0];
+      pg[1] = dot(Bz, bd) * ih[1];
+      pg[2] = dot(Dz, bb) * ih[2];
       for (int j = 0; j < nh; ++j) {
-        double s = 0.;
-#pragma unroll
-        for (int e = 0; e < K1; ++e) s += Bz[e] * Yr(pci, 3 + j)[loff<2, K1>(l, e)];
-        hv[j] = s;
+        lineD2(Yr(pci, 3 + j), bb);
+        hv[j] = dot(Bz, bb);
       }
     }
     wave_sync();
@@ -331,7 +324,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
   scal_fields(3, 3, 4, pq, gp, Hq);
 
   const double nu = P.nu;
-  const double JxW = T.w[qx] * T.w[qy] * T.w[qz] * hx * hy * hz;
+  const double JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
   const double hst = P.geo[gcell * 4 + 3];
   const double un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
   const double u_mag = fmax(sqrt(un2), 1e-12);
@@ -350,8 +343,8 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
   }
   if (P.srf) {
     const double *om = P.omega;
-    const double xq[3] = {P.x0[gcell * 3 + 0] + hx * T.xi[qx], P.x0[gcell * 3 + 1] + hy * T.xi[qy],
-                          P.x0[gcell * 3 + 2] + hz * T.xi[qz]};
+    const double xq[3] = {P.x0[gcell * 3 + 0] + hx * sM[84 + qx], P.x0[gcell * 3 + 1] + hy * sM[84 + qy],
+                          P.x0[gcell * 3 + 2] + hz * sM[84 + qz]};
     const double cx_[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
     const double ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2], om[0] * xq[1] - om[1] * xq[0]};
     const double cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
@@ -417,68 +410,49 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
     for (int e = 0; e < 3; ++e) Tc[13 + e] = JxW * tau * S[e] * ih[e];
   }
 
-  // ---------------- integration, one test field at a time (wave-local)
+  // ---------------- integration, one test field at a time (wave-local, lane <-> output element)
+  double cb2[K1], cd2[K1], cb1[K1], cd1[K1], cb0[K1], cd0[K1];  // columns of V, D (transposed rows)
+  row(3, i2, cb2);
+  row(4, i2, cd2);
+  row(3, i1, cb1);
+  row(4, i1, cd1);
+  row(3, i0, cb0);
+  row(4, i0, cd0);
 #pragma unroll
   for (int fld = 0; fld < 4; ++fld) {
+    if (GLS_ABL & 4) { if (pact) Out(pci, fld)[me] = Tc[4 * fld] + Tc[4 * fld + 1] + Tc[4 * fld + 2] + Tc[4 * fld + 3]; continue; }
     if (pact) {
-      X(pci, 0)[q] = Tc[4 * fld];
-      X(pci, 1)[q] = Tc[4 * fld + 1];
-      X(pci, 2)[q] = Tc[4 * fld + 2];
-      X(pci, 3)[q] = Tc[4 * fld + 3];
+      X(pci, 0)[me] = Tc[4 * fld];
+      X(pci, 1)[me] = Tc[4 * fld + 1];
+      X(pci, 2)[me] = Tc[4 * fld + 2];
+      X(pci, 3)[me] = Tc[4 * fld + 3];
     }
     wave_sync();
-    // transposed z: Z0 = B^T Tv + D^T Tz -> Y0; Z1 = B^T Tx -> Y1; Z2 = B^T Ty -> Y2
-    for (int t = lane; t < CPW * L2 * 3; t += 64) {
-      const int ci = cbase + t / (L2 * 3), r = t % (L2 * 3), l = r / 3, m = r % 3;
-      double a[K1], o[K1];
-      const double *s = X(ci, m == 0 ? 0 : m);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) a[e] = s[loff<2, K1>(l, e)];
-      bwd<K1>(T.V, a, o);
-      if (m == 0) {
-        const double *s3 = X(ci, 3);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = s3[loff<2, K1>(l, e)];
-        bwd_add<K1>(T.D, a, o);
-      }
-      double *d = Yr(ci, m);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) d[loff<2, K1>(l, e)] = o[e];
+    if (pact) {  // transposed z (output index az = i2): Z0 = B^T Tv + D^T Tz, Z1 = B^T Tx, Z2 = B^T Ty
+      double tv[K1], tx[K1], ty[K1], tz[K1];
+      lineD2(X(pci, 0), tv);
+      lineD2(X(pci, 1), tx);
+      lineD2(X(pci, 2), ty);
+      lineD2(X(pci, 3), tz);
+      Yr(pci, 0)[me] = dot(cb2, tv) + dot(cd2, tz);
+      Yr(pci, 1)[me] = dot(cb2, tx);
+      Yr(pci, 2)[me] = dot(cb2, ty);
     }
     wave_sync();
-    // transposed y: W0 = B^T Z0 + D^T Z2 -> X0; W1 = B^T Z1 -> X1
-    for (int t = lane; t < CPW * L2 * 2; t += 64) {
-      const int ci = cbase + t / (L2 * 2), r = t % (L2 * 2), l = r / 2, m = r % 2;
-      double a[K1], o[K1];
-      const double *s = Yr(ci, m);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) a[e] = s[loff<1, K1>(l, e)];
-      bwd<K1>(T.V, a, o);
-      if (m == 0) {
-        const double *s2 = Yr(ci, 2);
-#pragma unroll
-        for (int e = 0; e < K1; ++e) a[e] = s2[loff<1, K1>(l, e)];
-        bwd_add<K1>(T.D, a, o);
-      }
-      double *d = X(ci, m);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) d[loff<1, K1>(l, e)] = o[e];
+    if (pact) {  // transposed y (ay = i1): W0 = B^T Z0 + D^T Z2, W1 = B^T Z1
+      double z0[K1], z1[K1], z2[K1];
+      lineD1(Yr(pci, 0), z0);
+      lineD1(Yr(pci, 1), z1);
+      lineD1(Yr(pci, 2), z2);
+      X(pci, 0)[me] = dot(cb1, z0) + dot(cd1, z2);
+      X(pci, 1)[me] = dot(cb1, z1);
     }
     wave_sync();
-    // transposed x: out = B^T W0 + D^T W1 (node-indexed)
-    for (int t = lane; t < CPW * L2; t += 64) {
-      const int ci = cbase + t / L2, l = t % L2;
-      double a[K1], o[K1];
-      const double *s0 = X(ci, 0), *s1 = X(ci, 1);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) a[e] = s0[loff<0, K1>(l, e)];
-      bwd<K1>(T.V, a, o);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) a[e] = s1[loff<0, K1>(l, e)];
-      bwd_add<K1>(T.D, a, o);
-      double *d = Out(ci, fld);
-#pragma unroll
-      for (int e = 0; e < K1; ++e) d[loff<0, K1>(l, e)] = o[e];
+    if (pact) {  // transposed x (ax = i0): out = B^T W0 + D^T W1
+      double w0[K1], w1[K1];
+      lineD0(X(pci, 0), w0);
+      lineD0(X(pci, 1), w1);
+      Out(pci, fld)[me] = dot(cb0, w0) + dot(cd0, w1);
     }
     wave_sync();
   }
@@ -508,7 +482,9 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS) gls_brick_kernel(const O
     const int node = sNode[n];
     const int64_t gi = fld < 3 ? (int64_t)node * 3 + fld : voff + node;
     const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
-    if (interior) P.y[gi] = s;
+    if (GLS_ABL & 2) {
+      if (s == 123.456) P.y[gi] = s;
+    } else if (interior) P.y[gi] = s;
     else atomicAdd(&P.y[gi], s);
   }
 }
@@ -517,7 +493,7 @@ template <int K>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
   const int NF = mode == MODE_JV ? 11 : 7;
-  return sizeof(double) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3) + sizeof(int) * (size_t)C::BN3;
+  return sizeof(double) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3 + 5 * 16 + 8) + sizeof(int) * (size_t)C::BN3;
 }
 
 template <int K>

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgls_native.so")
+LIB_PATH = os.environ.get("GLS_NATIVE_LIB") or os.path.join(HERE, "libgls_native.so")  # override: experiments only
 
 GLS_OK, GLS_EINVAL, GLS_EHIP, GLS_ENOMEM, GLS_ENOCONV, GLS_EIO, GLS_ECOMM = 0, -1, -2, -3, -4, -5, -6
 
