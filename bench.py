@@ -10,8 +10,10 @@ residual re-assembly. Every step restarts from the same synthetic state so the w
 fixed; linear iterations and residual evaluations are reported.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
-Multi-GPU: each rank runs the full workload on its own GPU ("replicas" until the RCCL
-domain-decomposed path lands); value = sum over ranks.
+Multi-GPU (N>1): the 128^3 mesh is partitioned into contiguous Morton brick ranges (one per GPU,
+p4est-like); ghost import / export-add and the GMRES dot products go over RCCL (torch.distributed
+"nccl") through the C-ABI callbacks (softx_2020_200_amd/dist.py). Fixed total problem ->
+"scaling": "strong"; value = nonlinear iterations/s of the whole job.
 """
 from __future__ import annotations
 
@@ -81,7 +83,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=128, help="cells per direction")
+    ap.add_argument("--cells", dest="n", type=int, default=128, help="cells per direction")
     ap.add_argument("--k", type=int, default=2)
     ap.add_argument("--kp", type=int, default=2)
     ap.add_argument("--nu", type=float, default=0.01)
@@ -92,17 +94,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo stages through the host (testing on one GPU)")
     args = ap.parse_args()
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         torch.cuda.synchronize()
@@ -111,14 +118,32 @@ def main():
 
     from softx_2020_200_amd.problem import CavityProblem
     t_setup = time.perf_counter()
-    prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu)
-    ctx = prob.ctx
-    N = ctx.n_dofs
-    ts = (args.dt,) * 4
-    ctx.set_time("bdf2", ts)
-    m1_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.0)
-    m2_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.3)
     dev = torch.device("cuda", local)
+    ts = (args.dt,) * 4
+    if world == 1:
+        prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu)
+        ctx = prob.ctx
+        mesh = prob.mesh
+        N = N_global = ctx.n_dofs
+        m1_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.0)
+        m2_h = smooth_state(prob.mesh, args.n, 3, prob.dir_dofs, prob.dir_vals, 0.3)
+    else:
+        import softx_2020_200_amd as sx
+        from softx_2020_200_amd.dist import DistributedProblem, local_vector
+        from softx_2020_200_amd.problem import dirichlet_from_bcs
+        mesh = sx.hyper_cube(3, args.n, args.k, args.kp, -1.0, 1.0)
+        bcs = [("noslip", b, None) for b in (0, 1, 2, 4, 5)] + [("function", 3, (1.0, 0.0, 0.0))]
+        mask, ddofs, dvals = dirichlet_from_bcs(mesh, args.n, -1.0, 1.0, True, bcs)
+        dp = DistributedProblem(mesh, rank, world, dev, viscosity=args.nu, vnode_mask=mask, dirichlet=(ddofs, dvals),
+                                backend=args.dist_backend)
+        ctx = dp.ctx
+        N = ctx.n_dofs
+        N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
+        m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
+        m2_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.3), mesh["n_vnodes"])
+    ctx.set_time("bdf2", ts)
+    if dist is not None:
+        dist.barrier()  # first collective before any batched P2P (NCCL requirement)
     m1 = torch.from_numpy(m1_h).to(dev)
     m2 = torch.from_numpy(m2_h).to(dev)
     del m1_h, m2_h
@@ -156,21 +181,25 @@ def main():
 
     t_max = elapsed
     if dist is not None:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        tt = tt.to(dev) if args.dist_backend == "nccl" else tt
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
 
     lin_its = [s["linear_iterations"] for s in stats]
     nres = [s["residual_evaluations"] for s in stats]
-    its_per_s = world * args.steps / t_max
-    n_cells = prob.mesh["n_cells"]
-    nv = prob.mesh["n_vnodes"]
+    its_per_s = args.steps / t_max  # the whole job advances one Newton iteration per step
+    n_cells = mesh["n_cells"]
+    nv = mesh["n_vnodes"]
     nvdofs = 3 * nv
     # algorithmic bytes of one J.v launch (this build's layout): v, Jv, u (8N each),
     # 2 history velocity vectors (BDF2), cell->node int32 indices, per-cell geometry (4 doubles),
     # velocity constraint mask (1 B/node)
     nvl = (args.k + 1) ** 3
-    B_jv = 8 * N * 3 + 8 * 2 * nvdofs + 4 * n_cells * nvl * (1 if args.kp == args.k else 2) + 32 * n_cells + nv
+    n_cells_rank = n_cells // world
+    nv_rank = (N // 4) if world > 1 else nv
+    B_jv = 8 * N * 3 + 8 * 2 * 3 * nv_rank + 4 * n_cells_rank * nvl * (1 if args.kp == args.k else 2) + \
+        32 * n_cells_rank + nv_rank
     jv_launch_ms = jv2_ms / max(jv2_n, 1)
     achieved = B_jv / (jv_launch_ms * 1e-3) / 1e9
     # dense-contraction FLOP count of the kernel as written (per cell, Q2-Q2 3D): see DESIGN.md §4
@@ -183,23 +212,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * t_max / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (smooth cavity-like BDF2 history, lid/wall Dirichlet values)",
         "config": {"workload": "3D lid-driven cavity Q%d-Q%d %d^3 transient BDF2 (BASELINE configs[2])"
                                % (args.k, args.kp, args.n),
-                   "n_dofs": N, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
+                   "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+Jacobi, rel %.0e, max %d" % (args.restart, args.rel, args.lin_max),
-                   "parallelism": "replicas" if world > 1 else "single"},
-        "mdof_per_s": N * its_per_s / 1e6,
+                   "parallelism": "domain decomposition x%d (RCCL P2P ghosts)" % world if world > 1 else "single"},
+        "mdof_per_s": N_global * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean(lin_its)),
         "residual_evaluations_per_step": float(np.mean(nres)),
         "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),
                       "diagonal": dg_ms / max(dg_n, 1),
                       "share_of_step": {"jacobian_apply": jv_ms / (1e3 * elapsed),
                                         "residual": res_ms / (1e3 * elapsed), "diagonal": dg_ms / (1e3 * elapsed)}},
-        "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,2,3,MODE_JV>", "achieved": achieved,
+        "roofline": {"bound": "hbm", "kernel": "gls_brick_kernel<%d,MODE_JV>" % args.k if ctx.uses_brick_kernels
+                     else "gls_cell_kernel<3,%d,%d,%d,MODE_JV>" % (args.k, args.kp, args.k + 1), "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "algorithmic_bytes_per_launch": B_jv, "launch_ms": jv_launch_ms},
         "setup_s": t_setup,

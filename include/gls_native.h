@@ -143,6 +143,38 @@ int gls_newton_solve(gls_ctx *ctx, double *present, const double *u1, const doub
                      gls_newton_params *prm);
 
 /* ------------------------------------------------------------------------------------------
+ * Multi-GPU (one process per GPU). Replaces the MPI domain decomposition of
+ * parallel::distributed::Triangulation + Trilinos ghosted vectors (navier_stokes_base.cc:55-60,
+ * gls_navier_stokes.cc:186-202) and compress(add) (:774-776).
+ *   gls_part_*      : partition plan of a Morton brick mesh (host): rank-local mesh with owned
+ *                     nodes first, ghosts after; import/export lists per neighbour rank.
+ *   gls_dist_attach : turns a context built on the rank-local mesh into a distributed one.
+ *                     Ghost import (before residual / J.v / set_state) and export-add (after)
+ *                     pack into caller-owned DEVICE buffers (4 doubles per node: u,v,w,p) and call
+ *                     xchg(user, 0 = import: send send_buf segments to neighbours, receive into
+ *                     recv_buf | 1 = export: send recv_buf segments, receive into send_buf);
+ *                     dot products sum owned DoFs and call allreduce(user, dev_buf, n) (sum).
+ *                     The caller implements both with RCCL (torch.distributed "nccl") over xGMI.
+ *                     Calls are made on the context stream's order; callbacks must return 0.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct gls_part gls_part;
+int gls_part_create(int n_cells, int nodes_per_cell, const int32_t *cell_vnodes, int n_vnodes, int rank, int world,
+                    gls_part **out);
+int gls_part_sizes(const gls_part *p, int64_t *cell_begin, int64_t *cell_end, int64_t *n_owned_nodes,
+                   int64_t *n_local_nodes, int *n_nbrs, int64_t *n_send, int64_t *n_recv);
+int gls_part_get(const gls_part *p, int32_t *local_cell_vnodes, int64_t *local_to_global, int *nbr_ranks,
+                 int64_t *send_offsets, int32_t *send_nodes, int64_t *recv_offsets, int32_t *recv_nodes);
+int gls_part_destroy(gls_part *p);
+
+typedef int (*gls_exchange_fn)(void *user, int phase);
+typedef int (*gls_allreduce_fn)(void *user, double *dev_buf, int n);
+int gls_dist_attach(gls_ctx *ctx, int64_t n_owned_nodes, int n_nbrs, const int64_t *send_offsets,
+                    const int32_t *send_nodes, const int64_t *recv_offsets, const int32_t *recv_nodes, double *send_buf,
+                    double *recv_buf, double *red_buf, gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user);
+/* refresh ghost entries of a DEVICE vector (e.g. the history vectors once per time step) */
+int gls_dist_import(gls_ctx *ctx, double *x);
+
+/* ------------------------------------------------------------------------------------------
  * Host-side building blocks (host pointers).
  * ------------------------------------------------------------------------------------------ */
 /* bdf_coefficients (source/core/bdf.cc:45-75): alpha[order+1] */

@@ -90,6 +90,8 @@ bool is_sdirk(int s) { return s >= GLS_SDIRK2 && s <= GLS_SDIRK3_3; }
 
 }  // namespace
 
+int gls_internal_set_err(int code, const char *msg) { return set_err(code, "%s", msg); }
+
 extern "C" {
 
 const char *gls_last_error(void) { return g_err.c_str(); }
@@ -266,6 +268,16 @@ struct gls_ctx {
   int krylov_m = 0;
   DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
   bool use_brick = false;  // sum-factorized brick kernels (3D Qk-Qk, Morton 2x2x2 bricks)
+  // distributed (rank-local mesh): owned nodes [0, n_owned), ghosts after; exchange via callbacks
+  struct Dist {
+    bool on = false;
+    int64_t n_owned = 0, n_send = 0, n_recv = 0;
+    DevBuf<int32_t> send_nodes, recv_nodes;
+    double *send_buf = nullptr, *recv_buf = nullptr, *red_buf = nullptr;
+    gls_exchange_fn xchg = nullptr;
+    gls_allreduce_fn allreduce = nullptr;
+    void *user = nullptr;
+  } dist;
   // timing
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
@@ -370,11 +382,46 @@ struct TimedLaunch {
   }
 };
 
+// ---- distributed hooks (no-ops on a single rank)
+int dist_import(gls_ctx *c, double *x) {
+  if (!c->dist.on) return GLS_OK;
+  const int64_t voff = 3 * (int64_t)c->n_vnodes;
+  HIP_TRY(gls::vec_pack_nodes(x, c->dist.send_nodes.p, c->dist.n_send, voff, c->dist.send_buf, c->stream));
+  if (c->dist.xchg(c->dist.user, 0) != 0) return set_err(GLS_ECOMM, "ghost import exchange failed");
+  HIP_TRY(gls::vec_unpack_nodes(x, c->dist.recv_nodes.p, c->dist.n_recv, voff, c->dist.recv_buf, 0, c->stream));
+  return GLS_OK;
+}
+int dist_export_add(gls_ctx *c, double *y) {
+  if (!c->dist.on) return GLS_OK;
+  const int64_t voff = 3 * (int64_t)c->n_vnodes;
+  HIP_TRY(gls::vec_pack_nodes(y, c->dist.recv_nodes.p, c->dist.n_recv, voff, c->dist.recv_buf, c->stream));
+  if (c->dist.xchg(c->dist.user, 1) != 0) return set_err(GLS_ECOMM, "ghost export exchange failed");
+  HIP_TRY(gls::vec_unpack_nodes(y, c->dist.send_nodes.p, c->dist.n_send, voff, c->dist.send_buf, 1, c->stream));
+  return GLS_OK;
+}
+// out[k] = sum over OWNED DoFs of A[k] . w, reduced over ranks (host result)
+int dist_multidot(gls_ctx *c, const double *A, int64_t lda, int nk, const double *w, double *host_out) {
+  const int64_t n1 = c->dist.on ? 3 * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? 3 * (int64_t)c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned : 0;
+  HIP_TRY(gls::vec_multidot2(A, lda, nk, w, n1, off2, n2, c->scal.p, c->work.p, c->stream));
+  if (c->dist.on) {
+    HIP_TRY(hipMemcpyAsync(c->dist.red_buf, c->scal.p, sizeof(double) * nk, hipMemcpyDeviceToDevice, c->stream));
+    if (c->dist.allreduce(c->dist.user, c->dist.red_buf, nk) != 0) return set_err(GLS_ECOMM, "allreduce failed");
+    HIP_TRY(hipMemcpyAsync(host_out, c->dist.red_buf, sizeof(double) * nk, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    HIP_TRY(hipMemcpyAsync(host_out, c->scal.p, sizeof(double) * nk, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GLS_OK;
+}
+
 int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
+  if (mode == gls::MODE_JV) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
   gls::OpParams P = make_params(c);
   P.v = v;
   P.y = y;
@@ -386,21 +433,24 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     else
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
+  GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
   return GLS_OK;
 }
 
 int ensure_diag(gls_ctx *c) {
   if (c->diag_valid) return GLS_OK;
   GLS_TRY(run_cell(c, gls::MODE_DIAG, nullptr, c->diag.p));
+  if (c->dist.on) {  // ghost rows are not owned here: keep the Jacobi division finite
+    const int64_t nl = c->n_vnodes, no = c->dist.n_owned;
+    HIP_TRY(gls::vec_fill(c->diag.p + 3 * no, 3 * (nl - no), 1.0, c->stream));
+    HIP_TRY(gls::vec_fill(c->diag.p + 3 * nl + no, nl - no, 1.0, c->stream));
+  }
   c->diag_valid = true;
   return GLS_OK;
 }
 
 int device_dot(gls_ctx *c, const double *a, const double *b, double *host_out) {
-  HIP_TRY(gls::vec_multidot(a, 0, 1, b, c->n_dofs, c->scal.p, c->work.p, c->stream));
-  HIP_TRY(hipMemcpyAsync(host_out, c->scal.p, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return GLS_OK;
+  return dist_multidot(c, a, 0, 1, b, host_out);
 }
 
 }  // namespace
@@ -575,6 +625,42 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
   c->u2 = u2;
   c->u3 = u3;
   c->diag_valid = false;
+  // distributed: refresh the ghost values of the evaluation point (history vectors are imported
+  // by the caller once per time step with gls_dist_import)
+  return dist_import(c, const_cast<double *>(u));
+}
+
+int gls_dist_import(gls_ctx *c, double *x) {
+  GLS_TRY(check_ctx(c));
+  return dist_import(c, x);
+}
+
+int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t *send_offsets,
+                    const int32_t *send_nodes, const int64_t *recv_offsets, const int32_t *recv_nodes, double *send_buf,
+                    double *recv_buf, double *red_buf, gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user) {
+  GLS_TRY(check_ctx(c));
+  if (c->dim != 3 || c->k != c->kp || c->cell_pnodes.p) return set_err(GLS_EINVAL, "distributed path: 3D Qk-Qk only");
+  if (n_owned_nodes < 0 || n_owned_nodes > c->n_vnodes || n_nbrs < 0 || !xchg || !allreduce || !red_buf)
+    return set_err(GLS_EINVAL, "gls_dist_attach: bad arguments");
+  const int64_t ns = n_nbrs ? send_offsets[n_nbrs] : 0, nr = n_nbrs ? recv_offsets[n_nbrs] : 0;
+  for (int64_t i = 0; i < ns; ++i)
+    if (send_nodes[i] < 0 || send_nodes[i] >= n_owned_nodes) return set_err(GLS_EINVAL, "send node not owned");
+  for (int64_t i = 0; i < nr; ++i)
+    if (recv_nodes[i] < n_owned_nodes || recv_nodes[i] >= c->n_vnodes) return set_err(GLS_EINVAL, "recv node not a ghost");
+  if ((ns && !send_buf) || (nr && !recv_buf)) return set_err(GLS_EINVAL, "exchange buffers missing");
+  GLS_TRY(c->dist.send_nodes.upload(send_nodes, (size_t)ns));
+  GLS_TRY(c->dist.recv_nodes.upload(recv_nodes, (size_t)nr));
+  c->dist.n_owned = n_owned_nodes;
+  c->dist.n_send = ns;
+  c->dist.n_recv = nr;
+  c->dist.send_buf = send_buf;
+  c->dist.recv_buf = recv_buf;
+  c->dist.red_buf = red_buf;
+  c->dist.xchg = xchg;
+  c->dist.allreduce = allreduce;
+  c->dist.user = user;
+  c->dist.on = true;
+  c->diag_valid = false;
   return GLS_OK;
 }
 
@@ -664,9 +750,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       HIP_TRY(gls::vec_div(z, vj, dg, n, s));
       GLS_TRY(gls_jacobian_apply(c, z, w));
       // h = V[0..j]^T w and ||w||^2 in one pass
-      HIP_TRY(gls::vec_multidot(V, n, j + 2, w, n, c->scal.p, c->work.p, s));
-      HIP_TRY(hipMemcpyAsync(hcol.data(), c->scal.p, sizeof(double) * (j + 2), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
+      GLS_TRY(dist_multidot(c, V, n, j + 2, w, hcol.data()));
       const double wnorm0 = std::sqrt(std::max(hcol[j + 1], 0.0));
       for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hcol[i];
       HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
@@ -675,9 +759,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       GLS_TRY(device_dot(c, w, w, &wn2));
       double wnorm = std::sqrt(std::max(wn2, 0.0));
       if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation
-        HIP_TRY(gls::vec_multidot(V, n, j + 1, w, n, c->scal.p, c->work.p, s));
-        HIP_TRY(hipMemcpyAsync(hcol.data(), c->scal.p, sizeof(double) * (j + 1), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        GLS_TRY(dist_multidot(c, V, n, j + 1, w, hcol.data()));
         for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hcol[i];
         HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
         HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));

@@ -21,6 +21,12 @@ hipError_t vec_div(double *y, const double *x, const double *d, int64_t n, hipSt
 // written as per-block partials into work, reduced into out (device) by a second kernel.
 hipError_t vec_multidot(const double *A, int64_t lda, int nk, const double *w, int64_t n, double *out,
                         double *work, hipStream_t s);
+hipError_t vec_multidot2(const double *A, int64_t lda, int nk, const double *w, int64_t n1, int64_t off2, int64_t n2,
+                         double *out, double *work, hipStream_t s);  // sums over [0,n1) U [off2, off2+n2)
+// ghost exchange packing: buf[j*4 + {0,1,2,3}] <-> (vel comps, pressure) of local node nodes[j]
+hipError_t vec_pack_nodes(const double *x, const int32_t *nodes, int64_t m, int64_t voff, double *buf, hipStream_t s);
+hipError_t vec_unpack_nodes(double *x, const int32_t *nodes, int64_t m, int64_t voff, const double *buf, int add,
+                            hipStream_t s);
 // w -= sum_k h[k] * A[k]  (h on device)
 hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
                          hipStream_t s);

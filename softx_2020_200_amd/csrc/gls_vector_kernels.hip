@@ -42,13 +42,17 @@ __device__ inline double wave_sum(double v) {
 }
 
 // partial sums of up to kDotChunk dot products per block; work[k*gridDim + block]
+// rows are summed over [0, n1) and [off2, off2 + n2) (the owned ranges of a rank-local vector)
 template <int NK>
 __global__ void __launch_bounds__(kBlock) k_multidot(const double *__restrict__ A, int64_t lda,
-                                                     const double *__restrict__ w, int64_t n, double *work) {
+                                                     const double *__restrict__ w, int64_t n1, int64_t off2, int64_t n2,
+                                                     double *work) {
   double acc[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) acc[k] = 0.;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t n = n1 + n2;
+  for (int64_t ii = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; ii < n; ii += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = ii < n1 ? ii : off2 + (ii - n1);
     const double wi = w[i];
 #pragma unroll
     for (int k = 0; k < NK; ++k) acc[k] += A[k * lda + i] * wi;
@@ -104,6 +108,33 @@ __global__ void k_gather_scale_set(double *y, const double *d, const double *v, 
     y[i] = d[i] * v[i];
   }
 }
+__global__ void k_pack_nodes(const double *__restrict__ x, const int32_t *__restrict__ nodes, int64_t m, int64_t voff,
+                             double *__restrict__ buf) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = nodes[j];
+    buf[j * 4 + 0] = x[n * 3 + 0];
+    buf[j * 4 + 1] = x[n * 3 + 1];
+    buf[j * 4 + 2] = x[n * 3 + 2];
+    buf[j * 4 + 3] = x[voff + n];
+  }
+}
+__global__ void k_unpack_nodes(double *__restrict__ x, const int32_t *__restrict__ nodes, int64_t m, int64_t voff,
+                               const double *__restrict__ buf, int add) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = nodes[j];
+    if (add) {
+      atomicAdd(&x[n * 3 + 0], buf[j * 4 + 0]);
+      atomicAdd(&x[n * 3 + 1], buf[j * 4 + 1]);
+      atomicAdd(&x[n * 3 + 2], buf[j * 4 + 2]);
+      atomicAdd(&x[voff + n], buf[j * 4 + 3]);
+    } else {
+      x[n * 3 + 0] = buf[j * 4 + 0];
+      x[n * 3 + 1] = buf[j * 4 + 1];
+      x[n * 3 + 2] = buf[j * 4 + 2];
+      x[voff + n] = buf[j * 4 + 3];
+    }
+  }
+}
 __global__ void k_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
     y[idx[j]] = vals ? vals[j] : 0.0;
@@ -139,13 +170,18 @@ hipError_t vec_div(double *y, const double *x, const double *d, int64_t n, hipSt
 
 hipError_t vec_multidot(const double *A, int64_t lda, int nk, const double *w, int64_t n, double *out, double *work,
                         hipStream_t s) {
-  const int nb = grid_for(n);
+  return vec_multidot2(A, lda, nk, w, n, 0, 0, out, work, s);
+}
+
+hipError_t vec_multidot2(const double *A, int64_t lda, int nk, const double *w, int64_t n1, int64_t off2, int64_t n2,
+                         double *out, double *work, hipStream_t s) {
+  const int nb = grid_for(n1 + n2);
   for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
     const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;
     const double *Ak = A + (int64_t)k0 * lda;
     switch (m) {
 #define MD(M) \
-  case M: hipLaunchKernelGGL(k_multidot<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n, work); break;
+  case M: hipLaunchKernelGGL(k_multidot<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n1, off2, n2, work); break;
       MD(1) MD(2) MD(3) MD(4) MD(5) MD(6) MD(7) MD(8)
 #undef MD
     }
@@ -174,6 +210,17 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
                                 hipStream_t s) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_gather_scale_set, dim3(grid_for(m)), dim3(kBlock), 0, s, y, d, v, idx, m);
+  return hipGetLastError();
+}
+hipError_t vec_pack_nodes(const double *x, const int32_t *nodes, int64_t m, int64_t voff, double *buf, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_nodes, dim3(grid_for(m)), dim3(kBlock), 0, s, x, nodes, m, voff, buf);
+  return hipGetLastError();
+}
+hipError_t vec_unpack_nodes(double *x, const int32_t *nodes, int64_t m, int64_t voff, const double *buf, int add,
+                            hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_nodes, dim3(grid_for(m)), dim3(kBlock), 0, s, x, nodes, m, voff, buf, add);
   return hipGetLastError();
 }
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s) {

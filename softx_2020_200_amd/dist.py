@@ -1,0 +1,219 @@
+"""Multi-GPU driver glue: one process per GPU, torch.distributed ("nccl" = RCCL over xGMI).
+
+The partition plan and every kernel (pack/unpack, operators, GMRES, Newton) live in
+libgls_native.so (csrc/gls_dist.cpp, gls_api.cpp). This module only
+  * calls gls_part_* to get the rank-local mesh and exchange lists,
+  * owns the device exchange buffers (4 doubles per exchanged node: u, v, w, p),
+  * implements the two callbacks the C++ side calls: ghost exchange (grouped point-to-point
+    isend/irecv to the neighbour ranks) and the sum all-reduce of dot products.
+Backend "nccl" exchanges device buffers directly (RCCL P2P over xGMI); backend "gloo" stages
+through host memory (used by the CPU/one-GPU tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import traceback
+
+import numpy as np
+
+from .native import GLSContext, GLSError, check, load
+
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int)
+
+
+def _bind(L):
+    if getattr(L, "_dist_bound", False):
+        return L
+    i64, vp = C.c_int64, C.c_void_p
+    L.gls_part_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int32), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+    L.gls_part_sizes.argtypes = [vp] + [C.POINTER(i64)] * 4 + [C.POINTER(C.c_int)] + [C.POINTER(i64)] * 2
+    L.gls_part_get.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(i64), C.POINTER(C.c_int), C.POINTER(i64),
+                               C.POINTER(C.c_int32), C.POINTER(i64), C.POINTER(C.c_int32)]
+    L.gls_part_destroy.argtypes = [vp]
+    L.gls_dist_attach.argtypes = [vp, i64, C.c_int, C.POINTER(i64), C.POINTER(C.c_int32), C.POINTER(i64),
+                                  C.POINTER(C.c_int32), vp, vp, vp, EXCHANGE_FN, ALLREDUCE_FN, vp]
+    L.gls_dist_import.argtypes = [vp, vp]
+    L._dist_bound = True
+    return L
+
+
+def partition(cell_vnodes, n_vnodes, rank, world):
+    """Partition plan (C++): returns dict with the rank-local mesh and exchange lists."""
+    L = _bind(load())
+    cv = np.ascontiguousarray(cell_vnodes, dtype=np.int32)
+    h = C.c_void_p()
+    check(L.gls_part_create(cv.shape[0], cv.shape[1], cv.ctypes.data_as(C.POINTER(C.c_int32)), int(n_vnodes), rank,
+                            world, C.byref(h)), "gls_part_create")
+    try:
+        cb, ce, no, nl, ns, nr = (C.c_int64() for _ in range(6))
+        nn = C.c_int()
+        check(L.gls_part_sizes(h, C.byref(cb), C.byref(ce), C.byref(no), C.byref(nl), C.byref(nn), C.byref(ns),
+                               C.byref(nr)), "gls_part_sizes")
+        nc = ce.value - cb.value
+        out = dict(cell_begin=cb.value, cell_end=ce.value, n_owned=no.value, n_local=nl.value,
+                   local_cells=np.zeros((nc, cv.shape[1]), dtype=np.int32),
+                   local_to_global=np.zeros(nl.value, dtype=np.int64),
+                   nbrs=np.zeros(nn.value, dtype=np.int32), send_off=np.zeros(nn.value + 1, dtype=np.int64),
+                   send_nodes=np.zeros(ns.value, dtype=np.int32), recv_off=np.zeros(nn.value + 1, dtype=np.int64),
+                   recv_nodes=np.zeros(nr.value, dtype=np.int32))
+        check(L.gls_part_get(h, out["local_cells"].ctypes.data_as(C.POINTER(C.c_int32)),
+                             out["local_to_global"].ctypes.data_as(C.POINTER(C.c_int64)),
+                             out["nbrs"].ctypes.data_as(C.POINTER(C.c_int)),
+                             out["send_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                             out["send_nodes"].ctypes.data_as(C.POINTER(C.c_int32)),
+                             out["recv_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                             out["recv_nodes"].ctypes.data_as(C.POINTER(C.c_int32))), "gls_part_get")
+        if nn.value == 0:
+            out["send_off"] = np.zeros(1, dtype=np.int64)
+            out["recv_off"] = np.zeros(1, dtype=np.int64)
+        return out
+    finally:
+        L.gls_part_destroy(h)
+
+
+class Exchanger:
+    """Device exchange buffers + the C callbacks (torch.distributed point-to-point / all-reduce)."""
+
+    def __init__(self, plan, device, backend="nccl", group=None):
+        import torch
+        self.torch = torch
+        self.dist = torch.distributed
+        self.plan = plan
+        self.backend = backend
+        self.group = group
+        ns, nr = int(plan["send_off"][-1]), int(plan["recv_off"][-1])
+        self.send_buf = torch.zeros(max(ns, 1) * 4, dtype=torch.float64, device=device)
+        self.recv_buf = torch.zeros(max(nr, 1) * 4, dtype=torch.float64, device=device)
+        self.red_buf = torch.zeros(256, dtype=torch.float64, device=device)
+        self._xchg = EXCHANGE_FN(self._exchange)
+        self._allred = ALLREDUCE_FN(self._allreduce)
+
+    def _segments(self, phase):
+        p = self.plan
+        sb, rb = (self.send_buf, self.recv_buf) if phase == 0 else (self.recv_buf, self.send_buf)
+        so, ro = (p["send_off"], p["recv_off"]) if phase == 0 else (p["recv_off"], p["send_off"])
+        for i, nbr in enumerate(p["nbrs"]):
+            yield int(nbr), sb[4 * so[i]:4 * so[i + 1]], rb[4 * ro[i]:4 * ro[i + 1]]
+
+    def _exchange(self, user, phase):
+        try:
+            d = self.dist
+            if self.backend == "nccl":
+                ops = []
+                for nbr, s, r in self._segments(phase):
+                    if s.numel():
+                        ops.append(d.P2POp(d.isend, s, nbr, group=self.group))
+                    if r.numel():
+                        ops.append(d.P2POp(d.irecv, r, nbr, group=self.group))
+                if ops:
+                    for w in d.batch_isend_irecv(ops):
+                        w.wait()
+            else:  # gloo: stage through host memory
+                segs = list(self._segments(phase))
+                host_s = [s.cpu() for _, s, _ in segs]
+                host_r = [self.torch.empty(r.numel(), dtype=self.torch.float64) for _, _, r in segs]
+                reqs = []
+                for (nbr, s, r), hs, hr in zip(segs, host_s, host_r):
+                    if hs.numel():
+                        reqs.append(d.isend(hs, nbr, group=self.group))
+                    if hr.numel():
+                        reqs.append(d.irecv(hr, nbr, group=self.group))
+                for q in reqs:
+                    q.wait()
+                for (_, _, r), hr in zip(segs, host_r):
+                    if r.numel():
+                        r.copy_(hr.to(r.device))
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return -1
+
+    def _allreduce(self, user, dev_ptr, n):
+        try:
+            assert dev_ptr == self.red_buf.data_ptr() and n <= self.red_buf.numel()
+            view = self.red_buf[:n]
+            if self.backend == "nccl":
+                self.dist.all_reduce(view, group=self.group)
+            else:
+                h = view.cpu()
+                self.dist.all_reduce(h, group=self.group)
+                view.copy_(h.to(view.device))
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return -1
+
+
+def attach(ctx: GLSContext, plan, exchanger: Exchanger):
+    L = _bind(load())
+    p = plan
+    check(L.gls_dist_attach(ctx.h, int(p["n_owned"]), len(p["nbrs"]),
+                            p["send_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                            p["send_nodes"].ctypes.data_as(C.POINTER(C.c_int32)),
+                            p["recv_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                            p["recv_nodes"].ctypes.data_as(C.POINTER(C.c_int32)),
+                            C.c_void_p(exchanger.send_buf.data_ptr()), C.c_void_p(exchanger.recv_buf.data_ptr()),
+                            C.c_void_p(exchanger.red_buf.data_ptr()), exchanger._xchg, exchanger._allred, None),
+          "gls_dist_attach")
+    ctx._exchanger = exchanger  # keep callbacks alive
+    ctx._plan = plan
+
+
+def dist_import(ctx, x):
+    L = _bind(load())
+    check(L.gls_dist_import(ctx.h, C.c_void_p(x.data_ptr())), "gls_dist_import")
+
+
+def local_vector(plan, global_vec, n_vnodes_global, dim=3):
+    """Restrict a global [vel interleaved | pressure] vector to the rank-local layout (Qk-Qk)."""
+    l2g = plan["local_to_global"]
+    nl = l2g.shape[0]
+    out = np.zeros(dim * nl + nl)
+    gv = np.asarray(global_vec)
+    for c in range(dim):
+        out[c:dim * nl:dim] = gv[dim * l2g + c]
+    out[dim * nl:] = gv[dim * n_vnodes_global + l2g]
+    return out
+
+
+def owned_global_dofs(plan, n_vnodes_global, dim=3):
+    """(local dof indices of owned DoFs, their global dof indices)."""
+    l2g = plan["local_to_global"]
+    nl, no = l2g.shape[0], plan["n_owned"]
+    loc, glo = [], []
+    for c in range(dim):
+        loc.append(dim * np.arange(no) + c)
+        glo.append(dim * l2g[:no] + c)
+    loc.append(dim * nl + np.arange(no))
+    glo.append(dim * n_vnodes_global + l2g[:no])
+    return np.concatenate(loc), np.concatenate(glo)
+
+
+class DistributedProblem:
+    """Rank-local GLS context on a Morton brick mesh (3D Qk-Qk), attached to the exchanger."""
+
+    def __init__(self, mesh, rank, world, device, viscosity=1.0, vnode_mask=None, dirichlet=None, force_q=None,
+                 backend="nccl", group=None):
+        if mesh["k"] != mesh["kp"] or mesh["dim"] != 3:
+            raise GLSError("distributed path: 3D Qk-Qk only")
+        plan = partition(mesh["cell_vnodes"], mesh["n_vnodes"], rank, world)
+        self.plan = plan
+        cb, ce = plan["cell_begin"], plan["cell_end"]
+        l2g = plan["local_to_global"]
+        nl = l2g.shape[0]
+        self.n_vnodes_global = mesh["n_vnodes"]
+        lmask = vnode_mask[l2g] if vnode_mask is not None else None
+        fq = force_q[cb:ce] if force_q is not None else None
+        self.ctx = GLSContext(3, mesh["k"], mesh["kp"], plan["local_cells"], None, mesh["cell_h"][cb:ce], nl, nl,
+                              viscosity=viscosity, cell_x0=mesh["cell_x0"][cb:ce], vnode_mask=lmask, force_q=fq)
+        if dirichlet is not None:
+            gdofs, gvals = dirichlet
+            g2l = np.full(mesh["n_vnodes"], -1, dtype=np.int64)
+            g2l[l2g] = np.arange(nl)
+            node = g2l[gdofs // 3]
+            sel = node >= 0
+            self.ctx.set_dirichlet(3 * node[sel] + gdofs[sel] % 3, np.asarray(gvals)[sel])
+        self.exchanger = Exchanger(plan, device, backend=backend, group=group)
+        attach(self.ctx, plan, self.exchanger)
+        self.n_dofs_local = self.ctx.n_dofs

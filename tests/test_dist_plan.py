@@ -1,0 +1,119 @@
+"""Multi-GPU path, host side (CPU, gloo): the C++ partition plan (softx_2020_200_amd/csrc/gls_dist.cpp)
+and the ghost-exchange protocol, checked end to end with the oracle as the per-rank compute:
+sum over ranks of (local residual, export-added to owners) == the global residual."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import softx_2020_200_amd as sx
+from softx_2020_200_amd.dist import local_vector, owned_global_dofs, partition
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_partition_invariants(world):
+    m = sx.hyper_cube(3, 4, 2, 2)
+    cv, nv = m["cell_vnodes"], m["n_vnodes"]
+    plans = [partition(cv, nv, r, world) for r in range(world)]
+    owned = np.concatenate([p["local_to_global"][:p["n_owned"]] for p in plans])
+    assert np.array_equal(np.sort(owned), np.arange(nv))          # every node owned exactly once
+    assert sum(p["cell_end"] - p["cell_begin"] for p in plans) == m["n_cells"]
+    for r, p in enumerate(plans):
+        assert (p["cell_end"] - p["cell_begin"]) % 8 == 0            # whole bricks
+        l2g = p["local_to_global"]
+        assert np.array_equal(l2g[p["local_cells"]], cv[p["cell_begin"]:p["cell_end"]])
+        for i, s in enumerate(p["nbrs"]):
+            # my recv list from s == s's send list to me (same global ids, same order)
+            q = plans[s]
+            j = list(q["nbrs"]).index(r)
+            mine = l2g[p["recv_nodes"][p["recv_off"][i]:p["recv_off"][i + 1]]]
+            theirs = q["local_to_global"][q["send_nodes"][q["send_off"][j]:q["send_off"][j + 1]]]
+            assert np.array_equal(mine, theirs)
+            mine_s = l2g[p["send_nodes"][p["send_off"][i]:p["send_off"][i + 1]]]
+            theirs_r = q["local_to_global"][q["recv_nodes"][q["recv_off"][j]:q["recv_off"][j + 1]]]
+            assert np.array_equal(mine_s, theirs_r)
+        # ghosts are owned by lower ranks only (lowest-rank ownership)
+        gh = l2g[p["n_owned"]:]
+        for other in range(r, world):
+            po = plans[other]
+            assert not np.intersect1d(gh, po["local_to_global"][:po["n_owned"]]).size or other < r
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from oracle.oracle import Oracle, StructuredProblem
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = sx.hyper_cube(3, 4, 2, 2)
+        p = StructuredProblem(3, 4, k=2, viscosity=0.05, scheme="bdf1", time_steps=(0.01,) * 4)
+        p.cell_vnodes, p.cell_x0, p.cell_h = m["cell_vnodes"], m["cell_x0"], m["cell_h"]
+        p.cell_pnodes = m["cell_pnodes"]
+        p.set_dirichlet([("noslip", 0, None)])
+        rng = np.random.default_rng(20200200)
+        u, u1 = rng.uniform(-1, 1, p.n_dofs), rng.uniform(-1, 1, p.n_dofs)
+        r_glob = Oracle(p).residual(u, u1)
+        plan = partition(m["cell_vnodes"], m["n_vnodes"], rank, world)
+        # rank-local problem for the oracle (local mesh, local vectors with ghost values)
+        l2g = plan["local_to_global"]
+        nl = len(l2g)
+        cb, ce = plan["cell_begin"], plan["cell_end"]
+        pl = StructuredProblem(3, 4, k=2, viscosity=0.05, scheme="bdf1", time_steps=(0.01,) * 4)
+        pl.cell_vnodes = plan["local_cells"]
+        pl.cell_pnodes = plan["local_cells"]
+        pl.cell_x0, pl.cell_h = m["cell_x0"][cb:ce], m["cell_h"][cb:ce]
+        pl.n_vnodes = pl.n_pnodes = nl
+        pl.n_dofs = 4 * nl
+        pl.constrained = local_vector(plan, p.constrained.astype(float), m["n_vnodes"]).astype(np.uint8)
+        r_loc = Oracle(pl).residual(local_vector(plan, u, m["n_vnodes"]), local_vector(plan, u1, m["n_vnodes"]))
+        # export-add: ghost contributions -> owners (the protocol of gls_dist_attach, phase 1)
+        y = torch.tensor(r_loc)
+        pieces = []
+        for i, nbr in enumerate(plan["nbrs"]):
+            rn = plan["recv_nodes"][plan["recv_off"][i]:plan["recv_off"][i + 1]]
+            sn = plan["send_nodes"][plan["send_off"][i]:plan["send_off"][i + 1]]
+            pieces.append((int(nbr), rn, sn))
+        reqs, bufs = [], []
+        for nbr, rn, sn in pieces:
+            if len(rn):
+                out = torch.tensor(np.stack([r_loc[3 * rn], r_loc[3 * rn + 1], r_loc[3 * rn + 2], r_loc[3 * nl + rn]], 1)
+                                   .reshape(-1).copy())
+                reqs.append(dist.isend(out, nbr))
+                bufs.append(out)
+            if len(sn):
+                inc = torch.zeros(4 * len(sn), dtype=torch.float64)
+                reqs.append(dist.irecv(inc, nbr))
+                bufs.append((sn, inc))
+        for w in reqs:
+            w.wait()
+        for b in bufs:
+            if isinstance(b, tuple):
+                sn, inc = b
+                inc = inc.numpy().reshape(-1, 4)
+                for c in range(3):
+                    np.add.at(r_loc, 3 * sn + c, inc[:, c])
+                np.add.at(r_loc, 3 * nl + sn, inc[:, 3])
+        loc, glo = owned_global_dofs(plan, m["n_vnodes"])
+        con = p.constrained.astype(bool)
+        err = np.abs(np.where(con[glo], 0.0, r_loc[loc]) - r_glob[glo]).max() / np.abs(r_glob).max()
+        q.put((rank, float(err)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_residual_equals_global_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + world * 7 + os.getpid() % 500
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, err in res:
+        assert err < 1e-13, (rank, err)
