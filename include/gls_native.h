@@ -124,6 +124,21 @@ typedef struct {
 } gls_linear_params;
 int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_params *prm);
 
+/* Geometric multigrid preconditioner (matrix-free, monolithic), replacing the Jacobi default of
+ * gls_solve_linear (the reference's ILU / ML-AMG setup, gls_navier_stokes.cc:1161-1240).
+ * levels[0] = ctx; levels[l] = caller-created contexts of the same problem on the nested
+ * hyper_cube with n/2^l cells per direction (same k, same boundary conditions and Dirichlet
+ * lists). Each V-cycle: damped-Jacobi smoothing with the level's own matrix-free GLS Jacobian at
+ * the injected state, exact Qk restriction/prolongation. 3D Q1-Q1 / Q2-Q2, single GPU. */
+typedef struct {
+  int n_levels;
+  gls_ctx **levels;
+  int pre_smooth, post_smooth, coarse_sweeps;  /* 0 -> defaults 2, 2, 30 */
+  double omega;                               /* 0 -> 0.6 */
+} gls_mg_params;
+int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
+int gls_mg_detach(gls_ctx *ctx);
+
 /* ------------------------------------------------------------------------------------------
  * Nonlinear solve: NewtonNonLinearSolver::solve (include/core/newton_non_linear_solver.h:74-139)
  * on device vectors: present (in/out, DEVICE, length n_dofs). History from gls_set_state's u1..u3

@@ -46,6 +46,14 @@ template <class T>
 struct DevBuf {
   T *p = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
   ~DevBuf() { release(); }
   void release() {
     if (p) (void)hipFree(p);
@@ -278,6 +286,18 @@ struct gls_ctx {
     gls_allreduce_fn allreduce = nullptr;
     void *user = nullptr;
   } dist;
+  // geometric multigrid preconditioner (levels[0] == this context)
+  struct MG {
+    bool on = false;
+    std::vector<gls_ctx *> lev;
+    std::vector<int> n1d;  // lattice nodes per direction per level
+    int k = 2, pre = 2, post = 2, csweeps = 30;
+    double omega = 0.6;
+    std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
+    DevBuf<double> t1, t2;
+    bool dirty = true;
+  } mg;
+  double time_steps[4] = {1, 1, 1, 1};
   // timing
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
@@ -583,6 +603,9 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
   if (scheme < GLS_STEADY || scheme > GLS_SDIRK3_3) return set_err(GLS_EINVAL, "scheme %d", scheme);
   if (scheme != GLS_STEADY && (!ts || ts[0] == 0.)) return set_err(GLS_EINVAL, "time steps required");
   c->scheme = scheme;
+  if (ts)
+    for (int i = 0; i < 4; ++i) c->time_steps[i] = ts[i];
+  c->mg.dirty = true;
   for (double &a : c->alpha) a = 0.;
   c->alpha_jac = 0.;
   c->sdt2 = 0.;
@@ -625,6 +648,7 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
   c->u2 = u2;
   c->u3 = u3;
   c->diag_valid = false;
+  c->mg.dirty = true;
   // distributed: refresh the ghost values of the evaluation point (history vectors are imported
   // by the caller once per time step with gls_dist_import)
   return dist_import(c, const_cast<double *>(u));
@@ -706,6 +730,127 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
 }
 
 // --------------------------------------------------------------------------------------------
+// Geometric multigrid V-cycle (right preconditioner). Levels are nested hyper_cube meshes; the
+// coarse operators are the same GLS Jacobian re-discretised on the coarse mesh at the injected
+// state (Galerkin-free, matrix-free), smoothed by damped Jacobi on their own diagonals.
+// --------------------------------------------------------------------------------------------
+namespace {
+enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_N };
+double *mgbuf(gls_ctx *c, int l, int which) { return c->mg.bufs[(size_t)l * MB_N + which]->p; }
+
+int mg_prepare(gls_ctx *c) {
+  auto &mg = c->mg;
+  if (!mg.dirty) return GLS_OK;
+  const int L = (int)mg.lev.size();
+  for (int l = 1; l < L; ++l) {
+    gls_ctx *f = mg.lev[l - 1], *g = mg.lev[l];
+    const double *fu = l == 1 ? c->u : mgbuf(c, l - 1, MB_U);
+    const double *fh[3] = {l == 1 ? c->u1 : (c->u1 ? mgbuf(c, l - 1, MB_U1) : nullptr),
+                           l == 1 ? c->u2 : (c->u2 ? mgbuf(c, l - 1, MB_U2) : nullptr),
+                           l == 1 ? c->u3 : (c->u3 ? mgbuf(c, l - 1, MB_U3) : nullptr)};
+    (void)f;
+    HIP_TRY(gls::mg_inject(fu, mgbuf(c, l, MB_U), mg.n1d[l - 1], mg.n1d[l], c->stream));
+    GLS_TRY(gls_apply_dirichlet(g, mgbuf(c, l, MB_U)));
+    double *gh[3] = {nullptr, nullptr, nullptr};
+    for (int h = 0; h < 3; ++h)
+      if (fh[h]) {
+        gh[h] = mgbuf(c, l, MB_U1 + h);
+        HIP_TRY(gls::mg_inject(fh[h], gh[h], mg.n1d[l - 1], mg.n1d[l], c->stream));
+      }
+    g->viscosity = c->viscosity;
+    GLS_TRY(gls_set_time(g, c->scheme, c->time_steps));
+    GLS_TRY(gls_set_state(g, mgbuf(c, l, MB_U), gh[0], gh[1], gh[2]));
+    GLS_TRY(ensure_diag(g));
+  }
+  mg.dirty = false;
+  return GLS_OK;
+}
+
+// x = V-cycle(b) on level l (x, b are level-l vectors)
+int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
+  auto &mg = c->mg;
+  const int L = (int)mg.lev.size();
+  gls_ctx *g = mg.lev[l];
+  GLS_TRY(ensure_diag(g));
+  const int64_t n = g->n_dofs;
+  double *y = mgbuf(c, l, MB_Y);
+  const double *d = g->diag.p;
+  hipStream_t s = c->stream;
+  const int pre = l == L - 1 ? mg.csweeps : mg.pre;
+  HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, mg.omega, n, 1, s));  // first sweep from x = 0
+  for (int it = 1; it < pre; ++it) {
+    GLS_TRY(gls_jacobian_apply(g, x, y));
+    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
+  }
+  if (l == L - 1) return GLS_OK;
+  // residual -> coarse right-hand side
+  GLS_TRY(gls_jacobian_apply(g, x, y));
+  HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
+  gls_ctx *h = mg.lev[l + 1];
+  double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
+  HIP_TRY(gls::mg_transfer(y, bc, mg.n1d[l], mg.n1d[l + 1], mg.k, 0, c->mg.t1.p, c->mg.t2.p, s));
+  HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
+  GLS_TRY(mg_vcycle(c, l + 1, bc, xc));
+  HIP_TRY(gls::mg_transfer(xc, y, mg.n1d[l + 1], mg.n1d[l], mg.k, 1, c->mg.t1.p, c->mg.t2.p, s));
+  HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
+  HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
+  for (int it = 0; it < mg.post; ++it) {
+    GLS_TRY(gls_jacobian_apply(g, x, y));
+    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
+  }
+  return GLS_OK;
+}
+
+// z = M^{-1} v : Jacobi, or a multigrid V-cycle when attached
+int apply_prec(gls_ctx *c, const double *v, double *z) {
+  if (c->mg.on) return mg_vcycle(c, 0, v, z);
+  HIP_TRY(gls::vec_div(z, v, c->diag.p, c->n_dofs, c->stream));
+  return GLS_OK;
+}
+}  // namespace
+
+int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
+  GLS_TRY(check_ctx(c));
+  if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
+  if (c->dist.on) return set_err(GLS_EINVAL, "mg: distributed multigrid not supported yet");
+  if (c->dim != 3 || c->k > 2 || c->k != c->kp) return set_err(GLS_EINVAL, "mg: 3D Q1-Q1 / Q2-Q2 only");
+  auto &mg = c->mg;
+  mg = gls_ctx::MG();
+  for (int l = 0; l < p->n_levels; ++l) {
+    gls_ctx *g = p->levels[l];
+    if (!g || g->dim != 3 || g->k != c->k || g->kp != c->kp || g->dist.on) return set_err(GLS_EINVAL, "mg level %d", l);
+    const int n = (int)std::lround(std::cbrt((double)g->n_vnodes));
+    if ((int64_t)n * n * n != g->n_vnodes) return set_err(GLS_EINVAL, "mg level %d is not an n^3 lattice", l);
+    if (l > 0 && mg.n1d.back() != 2 * n - 1) return set_err(GLS_EINVAL, "mg level %d not nested", l);
+    mg.lev.push_back(g);
+    mg.n1d.push_back(n);
+  }
+  mg.k = c->k;
+  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : 2;
+  mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
+  mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
+  mg.omega = p->omega > 0 ? p->omega : 0.6;
+  for (int l = 0; l < p->n_levels; ++l)
+    for (int b = 0; b < MB_N; ++b) {
+      mg.bufs.emplace_back(new DevBuf<double>());
+      const bool need = l > 0 || b == MB_Y;
+      if (need) GLS_TRY(mg.bufs.back()->alloc((size_t)mg.lev[l]->n_dofs));
+    }
+  const int64_t nf = mg.n1d[0], nc = mg.n1d[1];
+  GLS_TRY(mg.t1.alloc((size_t)(nf * nf * nc * 3)));  // largest separable pass (prolong to level 0)
+  GLS_TRY(mg.t2.alloc((size_t)(nf * nf * nc * 3)));
+  mg.on = true;
+  mg.dirty = true;
+  return GLS_OK;
+}
+
+int gls_mg_detach(gls_ctx *c) {
+  GLS_TRY(check_ctx(c));
+  c->mg = gls_ctx::MG();
+  return GLS_OK;
+}
+
+// --------------------------------------------------------------------------------------------
 // GMRES(m), right preconditioned by the Jacobian diagonal. Classical Gram–Schmidt with one
 // DGKS re-orthogonalisation pass; fused multi-dot / multi-axpy kernels (one pass over the
 // Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
@@ -727,6 +872,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     GLS_TRY(c->tmp2.alloc(n));
   }
   GLS_TRY(ensure_diag(c));
+  if (c->mg.on) GLS_TRY(mg_prepare(c));
   double *V = c->krylov.p, *z = c->tmp1.p, *r = c->tmp2.p;
   const double *dg = c->diag.p;
   hipStream_t s = c->stream;
@@ -747,7 +893,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     double res = beta;
     for (; j < m && it < prm->max_iterations; ++j) {
       double *vj = V + (int64_t)j * n, *w = V + (int64_t)(j + 1) * n;
-      HIP_TRY(gls::vec_div(z, vj, dg, n, s));
+      GLS_TRY(apply_prec(c, vj, z));
       GLS_TRY(gls_jacobian_apply(c, z, w));
       // h = V[0..j]^T w and ||w||^2 in one pass
       GLS_TRY(dist_multidot(c, V, n, j + 2, w, hcol.data()));
@@ -798,7 +944,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     HIP_TRY(hipMemcpyAsync(c->coef.p, y.data(), sizeof(double) * kdim, hipMemcpyHostToDevice, s));
     HIP_TRY(gls::vec_fill(r, n, 0.0, s));
     HIP_TRY(gls::vec_multiaxpy(r, V, n, kdim, c->coef.p, -1.0, n, s));  // r = V y
-    HIP_TRY(gls::vec_div(z, r, dg, n, s));
+    GLS_TRY(apply_prec(c, r, z));
     HIP_TRY(gls::vec_axpy(x, 1.0, z, n, s));
     // true residual r = b - A x
     GLS_TRY(gls_jacobian_apply(c, x, r));

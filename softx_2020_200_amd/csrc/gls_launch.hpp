@@ -35,4 +35,11 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();
 
+// ---- geometric multigrid (gls_mg_kernels.hip): nested n^3 Qk lattices, k <= 2
+hipError_t mg_transfer(const double *in, double *out, int nin, int nout, int k, int prolong, double *tmp1,
+                       double *tmp2, hipStream_t s);
+hipError_t mg_inject(const double *fine, double *coarse, int nf, int nc, hipStream_t s);
+hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
+                            int zero_start, hipStream_t s);
+
 }  // namespace gls

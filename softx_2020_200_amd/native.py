@@ -29,6 +29,7 @@ EXPORTS = [
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import",
+    "gls_mg_attach", "gls_mg_detach",
 ]
 
 
@@ -51,6 +52,11 @@ class MeshDesc(C.Structure):
 class LinearParams(C.Structure):
     _fields_ = [("max_iterations", C.c_int), ("restart", C.c_int), ("relative_residual", C.c_double),
                 ("minimum_residual", C.c_double), ("iterations", C.c_int), ("final_residual", C.c_double)]
+
+
+class MGParams(C.Structure):
+    _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
+                ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double)]
 
 
 class NewtonParams(C.Structure):
@@ -99,6 +105,8 @@ def load():
     L.gls_timing_get.argtypes = [vp, C.c_int, d, C.POINTER(i64)]
     L.gls_timing_enable.argtypes = [vp, C.c_int]
     L.gls_uses_brick_kernels.argtypes = [vp]
+    L.gls_mg_attach.argtypes = [vp, C.POINTER(MGParams)]
+    L.gls_mg_detach.argtypes = [vp]
     _lib = L
     return L
 
@@ -302,6 +310,19 @@ class GLSContext:
               "gls_newton_solve")
         return dict(newton_iterations=p.newton_iterations, linear_iterations=p.linear_iterations,
                     residual_evaluations=p.residual_evaluations, final_residual=p.final_residual)
+
+    def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6):
+        """GMRES right preconditioner = geometric multigrid V-cycle over [self] + coarse_levels
+        (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive."""
+        levels = [self] + list(coarse_levels)
+        arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
+        p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega)
+        check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
+        self._mg_levels = levels
+
+    def detach_multigrid(self):
+        check(self.L.gls_mg_detach(self.h), "gls_mg_detach")
+        self._mg_levels = None
 
     # profiling
     def timing(self, enable=True):

@@ -66,7 +66,8 @@ class CavityProblem:
     (boundary id 3) u=(1,0,0) — examples/01-cavity/cavity.prm:46-55 extended to 3D.
     The lid bc is listed last so the wall edges keep u=0 (first bc wins)."""
 
-    def __init__(self, dim=3, n=8, k=2, kp=None, viscosity=0.01, stream=None):
+    def __init__(self, dim=3, n=8, k=2, kp=None, viscosity=0.01, stream=None, multigrid=False, mg_coarsest=4,
+                 **mg_opts):
         kp = k if kp is None else kp
         self.dim, self.n, self.k, self.kp = dim, n, k, kp
         self.mesh = hyper_cube(dim, n, k, kp, -1.0, 1.0)
@@ -76,3 +77,10 @@ class CavityProblem:
         self.ctx = build_context(self.mesh, viscosity=viscosity, vnode_mask=self.vnode_mask, stream=stream)
         self.ctx.set_dirichlet(self.dir_dofs, self.dir_vals)
         self.n_dofs = self.ctx.n_dofs
+        self.levels = []
+        if multigrid:  # nested hyper_cube levels n/2, n/4, ... down to mg_coarsest cells per direction
+            m = n
+            while m % 2 == 0 and m // 2 >= mg_coarsest:
+                m //= 2
+                self.levels.append(CavityProblem(dim, m, k, kp, viscosity, stream))
+            self.ctx.attach_multigrid([lv.ctx for lv in self.levels], **mg_opts)
