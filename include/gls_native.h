@@ -88,7 +88,10 @@ int gls_set_time(gls_ctx *ctx, int scheme, const double time_steps[4]);
 
 /* Evaluation point and history (DEVICE pointers, borrowed until the next call):
  * evaluation_point, solution_m1..m3 of PhysicsSolver (include/core/physics_solver.h:107-111).
- * u1..u3 may be NULL when the scheme does not read them. */
+ * u1..u3 may be NULL when the scheme does not read them. The state is captured here: the
+ * Jacobian diagonal and the J.v linearization (per quadrature point) are cached until the next
+ * gls_set_state / gls_set_time / gls_set_viscosity / gls_set_force, so changing the vectors'
+ * contents in place requires calling gls_set_state again. */
 int gls_set_state(gls_ctx *ctx, const double *u, const double *u1, const double *u2, const double *u3);
 
 /* assemble_rhs (gls_navier_stokes.cc:1023-1128 -> assembleGLS<false,...>):
@@ -129,7 +132,11 @@ int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_para
  * levels[0] = ctx; levels[l] = caller-created contexts of the same problem on the nested
  * hyper_cube with n/2^l cells per direction (same k, same boundary conditions and Dirichlet
  * lists). Each V-cycle: damped-Jacobi smoothing with the level's own matrix-free GLS Jacobian at
- * the injected state, exact Qk restriction/prolongation. 3D Q1-Q1 / Q2-Q2, single GPU. */
+ * the injected state, exact Qk restriction/prolongation. 3D Q1-Q1 / Q2-Q2.
+ * Multi-GPU: every level is a distributed context (gls_dist_attach on the partition of its own
+ * hyper_cube; nested partitions: rank r's coarse cells are the parents of its fine cells) that
+ * also declared its lattice embedding with gls_set_lattice. Restriction sums owned fine rows and
+ * export-adds the coarse ghost rows; prolongation imports the coarse ghosts first. */
 typedef struct {
   int n_levels;
   gls_ctx **levels;
@@ -137,6 +144,11 @@ typedef struct {
   double omega;                               /* 0 -> 0.6 */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
+/* Lattice embedding of a (rank-local) mesh: its velocity nodes are a subset of the global n1d^3
+ * Qk node lattice of hyper_cube in canonical numbering (global id = x + n1d*(y + n1d*z)), local
+ * node i being global node local_to_global[i] (host array, n_vnodes entries). The local nodes
+ * must fill an axis-aligned box (Morton partitions of a 2^m-cube over 2^j ranks do). */
+int gls_set_lattice(gls_ctx *ctx, int n1d, const int64_t *local_to_global);
 int gls_mg_detach(gls_ctx *ctx);
 
 /* ------------------------------------------------------------------------------------------
@@ -213,7 +225,8 @@ int gls_mesh_hyper_cube(int dim, int n, int k, int kp, double lo, double hi, int
  * Profiling hooks: time the next operator launches on the context stream with HIP events.
  * ------------------------------------------------------------------------------------------ */
 int gls_timing_reset(gls_ctx *ctx);
-/* which: 0 residual, 1 jacobian_apply, 2 diagonal; returns total ms and launch count */
+/* which: 0 residual, 1 jacobian_apply, 2 diagonal, 3 J.v linearization (once per state);
+ * returns total ms and launch count */
 int gls_timing_get(gls_ctx *ctx, int which, double *total_ms, int64_t *count);
 int gls_timing_enable(gls_ctx *ctx, int enable);
 

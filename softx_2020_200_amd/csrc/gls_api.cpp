@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -270,6 +271,9 @@ struct gls_ctx {
   const double *u = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;
   DevBuf<double> diag;  // diagonal at the current state (also D_c for constrained rows)
   bool diag_valid = false;
+  DevBuf<double> qdata;   // brick J.v linearization at the quadrature points (MODE_LIN output)
+  bool qd_valid = false;  // invalidated with the diagonal by every state / parameter change
+  bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
   // solver workspace
   DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
   DevBuf<double> krylov;      // (restart+1) x n_dofs
@@ -286,11 +290,18 @@ struct gls_ctx {
     gls_allreduce_fn allreduce = nullptr;
     void *user = nullptr;
   } dist;
+  // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
+  struct Lattice {
+    bool set = false;
+    int n1d = 0, box0[3] = {0, 0, 0}, bdim[3] = {0, 0, 0};
+    DevBuf<int32_t> map;  // box node (x fastest) -> local node
+  } lat;
   // geometric multigrid preconditioner (levels[0] == this context)
   struct MG {
     bool on = false;
+    bool boxed = false;    // distributed levels: transfers go through box gather / scatter
     std::vector<gls_ctx *> lev;
-    std::vector<int> n1d;  // lattice nodes per direction per level
+    std::vector<std::array<int, 3>> dims;  // box lattice nodes per direction per level
     int k = 2, pre = 2, post = 2, csweeps = 30;
     double omega = 0.6;
     std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
@@ -302,8 +313,8 @@ struct gls_ctx {
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
   std::vector<Ev> events;
-  double t_ms[3] = {0, 0, 0};
-  int64_t t_n[3] = {0, 0, 0};
+  double t_ms[4] = {0, 0, 0, 0};  // residual, J.v, diagonal, J.v linearization
+  int64_t t_n[4] = {0, 0, 0, 0};
 
   ~gls_ctx() {
     for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -436,6 +447,21 @@ int dist_multidot(gls_ctx *c, const double *A, int64_t lda, int nk, const double
   return GLS_OK;
 }
 
+// J.v linearization (u, grad u, tau, R_s at every quadrature point), once per state
+int ensure_qdata(gls_ctx *c) {
+  if (c->qd_valid) return GLS_OK;
+  const size_t n = gls::brick_qdata_size(c->k, c->n_cells);
+  if (c->qdata.n != n) GLS_TRY(c->qdata.alloc(n));
+  gls::OpParams P = make_params(c);
+  P.qd = c->qdata.p;
+  {
+    TimedLaunch t(c, 3);
+    HIP_TRY(gls::launch_brick_kernel(c->k, gls::MODE_LIN, P, c->tables, c->stream));
+  }
+  c->qd_valid = true;
+  return GLS_OK;
+}
+
 int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
@@ -443,11 +469,16 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
   if (mode == gls::MODE_JV) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
   gls::OpParams P = make_params(c);
+  if (mode == gls::MODE_JV && c->use_brick && c->use_qdata) {
+    GLS_TRY(ensure_qdata(c));
+    P.qd = c->qdata.p;
+    mode = gls::MODE_JVQ;
+  }
   P.v = v;
   P.y = y;
   HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
-    TimedLaunch t(c, mode);
+    TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : mode);
     if (c->use_brick && mode != gls::MODE_DIAG)
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     else
@@ -513,6 +544,7 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
 
   GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
   c->use_brick = detect_bricks(d, nq1d);
+  if (const char *e = std::getenv("GLS_JV_RECOMPUTE")) c->use_qdata = std::atoi(e) == 0;
   if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
   std::vector<double> geo((size_t)d->n_cells * 4);
   for (int cix = 0; cix < d->n_cells; ++cix) {
@@ -587,6 +619,7 @@ int gls_set_force(gls_ctx *c, const double *f) {
     GLS_TRY(c->force_q.upload(f, (size_t)c->n_cells * c->nq * c->dim));
   }
   c->diag_valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -594,6 +627,7 @@ int gls_set_viscosity(gls_ctx *c, double nu) {
   GLS_TRY(check_ctx(c));
   c->viscosity = nu;
   c->diag_valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -637,6 +671,7 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
     }
   }
   c->diag_valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -648,6 +683,7 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
   c->u2 = u2;
   c->u3 = u3;
   c->diag_valid = false;
+  c->qd_valid = false;
   c->mg.dirty = true;
   // distributed: refresh the ghost values of the evaluation point (history vectors are imported
   // by the caller once per time step with gls_dist_import)
@@ -685,6 +721,7 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   c->dist.user = user;
   c->dist.on = true;
   c->diag_valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -726,6 +763,11 @@ int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *
 int gls_apply_dirichlet(gls_ctx *c, double *x) {
   GLS_TRY(check_ctx(c));
   HIP_TRY(gls::vec_set_indexed(x, c->dir_dofs.p, c->dir_vals.p, (int64_t)c->dir_dofs.n, c->stream));
+  if (x == c->u || x == c->u1 || x == c->u2 || x == c->u3) {  // the captured state changed
+    c->diag_valid = false;
+    c->qd_valid = false;
+    c->mg.dirty = true;
+  }
   return GLS_OK;
 }
 
@@ -735,27 +777,57 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
 // state (Galerkin-free, matrix-free), smoothed by damped Jacobi on their own diagonals.
 // --------------------------------------------------------------------------------------------
 namespace {
-enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_N };
+enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_BOX, MB_N };
 double *mgbuf(gls_ctx *c, int l, int which) { return c->mg.bufs[(size_t)l * MB_N + which]->p; }
+int64_t mg_nbox(const gls_ctx *c, int l) {
+  const auto &d = c->mg.dims[(size_t)l];
+  return (int64_t)d[0] * d[1] * d[2];
+}
+// level-l local vector -> box lattice layout (identity on a single GPU: returns loc itself)
+const double *mg_to_box(gls_ctx *c, int l, const double *loc, bool owned_only) {
+  if (!c->mg.boxed) return loc;
+  gls_ctx *g = c->mg.lev[(size_t)l];
+  double *box = mgbuf(c, l, MB_BOX);
+  if (gls::mg_box_gather(loc, box, g->lat.map.p, mg_nbox(c, l), g->n_vnodes, owned_only ? g->dist.n_owned : -1,
+                         c->stream) != hipSuccess)
+    return nullptr;
+  return box;
+}
+// where a transfer writing level-l data must put it (the box buffer, or loc itself)
+double *mg_box_target(gls_ctx *c, int l, double *loc) { return c->mg.boxed ? mgbuf(c, l, MB_BOX) : loc; }
+int mg_from_box(gls_ctx *c, int l, double *loc) {
+  if (!c->mg.boxed) return GLS_OK;
+  gls_ctx *g = c->mg.lev[(size_t)l];
+  HIP_TRY(gls::mg_box_scatter(mgbuf(c, l, MB_BOX), loc, g->lat.map.p, mg_nbox(c, l), g->n_vnodes, c->stream));
+  return GLS_OK;
+}
+
+// injected coarse state (every second lattice node); history likewise
+int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
+  const double *fb = mg_to_box(c, l - 1, fine, false);
+  if (!fb) return set_err(GLS_EHIP, "mg box gather failed");
+  HIP_TRY(gls::mg_inject(fb, mg_box_target(c, l, coarse), c->mg.dims[(size_t)l - 1].data(), c->mg.dims[(size_t)l].data(),
+                         c->stream));
+  return mg_from_box(c, l, coarse);
+}
 
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
   const int L = (int)mg.lev.size();
   for (int l = 1; l < L; ++l) {
-    gls_ctx *f = mg.lev[l - 1], *g = mg.lev[l];
+    gls_ctx *g = mg.lev[l];
     const double *fu = l == 1 ? c->u : mgbuf(c, l - 1, MB_U);
     const double *fh[3] = {l == 1 ? c->u1 : (c->u1 ? mgbuf(c, l - 1, MB_U1) : nullptr),
                            l == 1 ? c->u2 : (c->u2 ? mgbuf(c, l - 1, MB_U2) : nullptr),
                            l == 1 ? c->u3 : (c->u3 ? mgbuf(c, l - 1, MB_U3) : nullptr)};
-    (void)f;
-    HIP_TRY(gls::mg_inject(fu, mgbuf(c, l, MB_U), mg.n1d[l - 1], mg.n1d[l], c->stream));
+    GLS_TRY(mg_inject_level(c, l, fu, mgbuf(c, l, MB_U)));
     GLS_TRY(gls_apply_dirichlet(g, mgbuf(c, l, MB_U)));
     double *gh[3] = {nullptr, nullptr, nullptr};
     for (int h = 0; h < 3; ++h)
       if (fh[h]) {
         gh[h] = mgbuf(c, l, MB_U1 + h);
-        HIP_TRY(gls::mg_inject(fh[h], gh[h], mg.n1d[l - 1], mg.n1d[l], c->stream));
+        GLS_TRY(mg_inject_level(c, l, fh[h], gh[h]));
       }
     g->viscosity = c->viscosity;
     GLS_TRY(gls_set_time(g, c->scheme, c->time_steps));
@@ -783,15 +855,26 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
     HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
   }
   if (l == L - 1) return GLS_OK;
-  // residual -> coarse right-hand side
+  // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
   GLS_TRY(gls_jacobian_apply(g, x, y));
   HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
   gls_ctx *h = mg.lev[l + 1];
   double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
-  HIP_TRY(gls::mg_transfer(y, bc, mg.n1d[l], mg.n1d[l + 1], mg.k, 0, c->mg.t1.p, c->mg.t2.p, s));
+  const double *yb = mg_to_box(c, l, y, true);
+  if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
+  HIP_TRY(gls::mg_transfer(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), mg.k, 0,
+                           c->mg.t1.p, c->mg.t2.p, s));
+  GLS_TRY(mg_from_box(c, l + 1, bc));
+  GLS_TRY(dist_export_add(h, bc));
   HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
   GLS_TRY(mg_vcycle(c, l + 1, bc, xc));
-  HIP_TRY(gls::mg_transfer(xc, y, mg.n1d[l + 1], mg.n1d[l], mg.k, 1, c->mg.t1.p, c->mg.t2.p, s));
+  // prolongate the coarse correction (ghost values imported first)
+  GLS_TRY(dist_import(h, xc));
+  const double *xb = mg_to_box(c, l + 1, xc, false);
+  if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
+  HIP_TRY(gls::mg_transfer(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), mg.k, 1, c->mg.t1.p,
+                           c->mg.t2.p, s));
+  GLS_TRY(mg_from_box(c, l, y));
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
   for (int it = 0; it < mg.post; ++it) {
@@ -809,21 +892,65 @@ int apply_prec(gls_ctx *c, const double *v, double *z) {
 }
 }  // namespace
 
+int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {
+  GLS_TRY(check_ctx(c));
+  if (c->dim != 3 || n1d < 2 || !l2g) return set_err(GLS_EINVAL, "gls_set_lattice: 3D, n1d >= 2, map required");
+  int lo[3] = {n1d, n1d, n1d}, hi[3] = {-1, -1, -1};
+  for (int i = 0; i < c->n_vnodes; ++i) {
+    const int64_t g = l2g[i];
+    if (g < 0 || g >= (int64_t)n1d * n1d * n1d) return set_err(GLS_EINVAL, "lattice node out of range");
+    const int x[3] = {(int)(g % n1d), (int)((g / n1d) % n1d), (int)(g / ((int64_t)n1d * n1d))};
+    for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], x[a]); hi[a] = std::max(hi[a], x[a]); }
+  }
+  int bd[3];
+  for (int a = 0; a < 3; ++a) bd[a] = hi[a] - lo[a] + 1;
+  const int64_t nbox = (int64_t)bd[0] * bd[1] * bd[2];
+  if (nbox != c->n_vnodes) return set_err(GLS_EINVAL, "local nodes do not fill a box (%lld != %d)", (long long)nbox, c->n_vnodes);
+  std::vector<int32_t> map((size_t)nbox, -1);
+  for (int i = 0; i < c->n_vnodes; ++i) {
+    const int64_t g = l2g[i];
+    const int64_t x = g % n1d - lo[0], y = (g / n1d) % n1d - lo[1], z = g / ((int64_t)n1d * n1d) - lo[2];
+    int32_t &m = map[(size_t)((z * bd[1] + y) * bd[0] + x)];
+    if (m >= 0) return set_err(GLS_EINVAL, "duplicate lattice node");
+    m = i;
+  }
+  GLS_TRY(c->lat.map.upload(map.data(), map.size()));
+  c->lat.n1d = n1d;
+  for (int a = 0; a < 3; ++a) { c->lat.box0[a] = lo[a]; c->lat.bdim[a] = bd[a]; }
+  c->lat.set = true;
+  return GLS_OK;
+}
+
 int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   GLS_TRY(check_ctx(c));
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
-  if (c->dist.on) return set_err(GLS_EINVAL, "mg: distributed multigrid not supported yet");
   if (c->dim != 3 || c->k > 2 || c->k != c->kp) return set_err(GLS_EINVAL, "mg: 3D Q1-Q1 / Q2-Q2 only");
   auto &mg = c->mg;
   mg = gls_ctx::MG();
+  mg.boxed = c->dist.on;
   for (int l = 0; l < p->n_levels; ++l) {
     gls_ctx *g = p->levels[l];
-    if (!g || g->dim != 3 || g->k != c->k || g->kp != c->kp || g->dist.on) return set_err(GLS_EINVAL, "mg level %d", l);
-    const int n = (int)std::lround(std::cbrt((double)g->n_vnodes));
-    if ((int64_t)n * n * n != g->n_vnodes) return set_err(GLS_EINVAL, "mg level %d is not an n^3 lattice", l);
-    if (l > 0 && mg.n1d.back() != 2 * n - 1) return set_err(GLS_EINVAL, "mg level %d not nested", l);
+    if (!g || g->dim != 3 || g->k != c->k || g->kp != c->kp || g->dist.on != mg.boxed)
+      return set_err(GLS_EINVAL, "mg level %d: order / distribution differs from level 0", l);
+    std::array<int, 3> dm;
+    if (mg.boxed) {
+      if (!g->lat.set) return set_err(GLS_EINVAL, "mg level %d: distributed level without gls_set_lattice", l);
+      for (int a = 0; a < 3; ++a) dm[a] = g->lat.bdim[a];
+      if (l > 0) {
+        const gls_ctx *f = p->levels[l - 1];
+        if (f->lat.n1d != 2 * g->lat.n1d - 1) return set_err(GLS_EINVAL, "mg level %d not nested", l);
+        for (int a = 0; a < 3; ++a)
+          if (f->lat.box0[a] != 2 * g->lat.box0[a] || f->lat.bdim[a] != 2 * g->lat.bdim[a] - 1)
+            return set_err(GLS_EINVAL, "mg level %d: partition not nested (rank box %d)", l, a);
+      }
+    } else {
+      const int n = (int)std::lround(std::cbrt((double)g->n_vnodes));
+      if ((int64_t)n * n * n != g->n_vnodes) return set_err(GLS_EINVAL, "mg level %d is not an n^3 lattice", l);
+      if (l > 0 && mg.dims.back()[0] != 2 * n - 1) return set_err(GLS_EINVAL, "mg level %d not nested", l);
+      dm = {n, n, n};
+    }
     mg.lev.push_back(g);
-    mg.n1d.push_back(n);
+    mg.dims.push_back(dm);
   }
   mg.k = c->k;
   mg.pre = p->pre_smooth > 0 ? p->pre_smooth : 2;
@@ -833,12 +960,12 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
-      const bool need = l > 0 || b == MB_Y;
-      if (need) GLS_TRY(mg.bufs.back()->alloc((size_t)mg.lev[l]->n_dofs));
+      const bool need = b == MB_BOX ? mg.boxed : (l > 0 || b == MB_Y);
+      if (need) GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
     }
-  const int64_t nf = mg.n1d[0], nc = mg.n1d[1];
-  GLS_TRY(mg.t1.alloc((size_t)(nf * nf * nc * 3)));  // largest separable pass (prolong to level 0)
-  GLS_TRY(mg.t2.alloc((size_t)(nf * nf * nc * 3)));
+  // largest intermediate separable pass: level-0 box x 3 components
+  GLS_TRY(mg.t1.alloc((size_t)(3 * mg_nbox(c, 0))));
+  GLS_TRY(mg.t2.alloc((size_t)(3 * mg_nbox(c, 0))));
   mg.on = true;
   mg.dirty = true;
   return GLS_OK;
@@ -1198,12 +1325,12 @@ int gls_timing_reset(gls_ctx *c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   c->events.clear();
-  for (int i = 0; i < 3; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
+  for (int i = 0; i < 4; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
   return GLS_OK;
 }
 int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
   GLS_TRY(check_ctx(c));
-  if (which < 0 || which > 2) return set_err(GLS_EINVAL, "which");
+  if (which < 0 || which > 3) return set_err(GLS_EINVAL, "which");
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) {
     float t = 0;

@@ -101,8 +101,12 @@ template <int K, int MODE>
 __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
   constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
-  constexpr bool JV = MODE == MODE_JV;
-  constexpr int NF = JV ? 11 : 7;  // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]
+  constexpr bool JV = MODE == MODE_JV || MODE == MODE_JVQ;
+  constexpr bool CACHED = MODE == MODE_JVQ;  // linearization read from P.qd (no state sweeps)
+  constexpr bool LIN = MODE == MODE_LIN;     // store the linearization to P.qd, no integration
+  // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]; JVQ: v0 v1 v2 vp only
+  constexpr int NF = CACHED ? 4 : (JV ? 11 : 7);
+  constexpr int FV = CACHED ? 0 : 7;         // first v field
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *sB = smem;                                   // [NF][BN3]
   double *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
@@ -131,11 +135,12 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     sM[tid] = j < K1 ? (tid < 84 ? T.w[j] : T.xi[j]) : 0.0;
   }
   // ---------------- gather the brick's nodes (all waves)
-  for (int t = tid; t < 3 * BN3; t += blockDim.x) {
-    const int g = t / BN3, n = t % BN3;
+  constexpr int NG = CACHED ? 1 : (JV ? 3 : 2);  // gather groups: state (u, p) | history | v
+  for (int t = tid; t < NG * BN3; t += blockDim.x) {
+    const int g = CACHED ? 2 : t / BN3, n = t % BN3;
     if (GLS_ABL & 1) {
       for (int f = 0; f < NF; ++f) BF(f)[n] = 0.001 * (n + f);
-      if (g == 0) sNode[n] = (brick * 37 + n) % P.n_vnodes;
+      if (g == 0 || CACHED) sNode[n] = (brick * 37 + n) % P.n_vnodes;
       continue;
     }
     const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
@@ -143,8 +148,8 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     const int a = (X - K * cx) + K1 * ((Y - K * cy) + K1 * (Z - K * cz));
     const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * N3 + a];
     const int64_t i3 = (int64_t)node * 3;
+    if (g == 0 || CACHED) sNode[n] = node;
     if (g == 0) {
-      sNode[n] = node;
       BF(0)[n] = P.u[i3];
       BF(1)[n] = P.u[i3 + 1];
       BF(2)[n] = P.u[i3 + 2];
@@ -162,10 +167,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
       BF(6)[n] = h[2];
     } else if (JV) {
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
-      BF(7)[n] = (m & 1u) ? 0.0 : P.v[i3];
-      BF(8)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
-      BF(9)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
-      BF(10)[n] = P.v[voff + node];
+      BF(FV)[n] = (m & 1u) ? 0.0 : P.v[i3];
+      BF(FV + 1)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
+      BF(FV + 2)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
+      BF(FV + 3)[n] = P.v[voff + node];
     }
   }
   __syncthreads();
@@ -316,31 +321,44 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     wave_sync();
   };
 
-  // ---------------- phase A: state at this lane's quadrature point
-  double u[3] = {0., 0., 0.}, gu[3][3] = {}, lu[3] = {0., 0., 0.};
-#pragma unroll
-  for (int c = 0; c < 3; ++c) vel_field(c, u[c], gu[c], lu[c]);
-  double pq = 0., gp[3] = {0., 0., 0.}, Hq[3] = {0., 0., 0.};
-  scal_fields(3, 3, 4, pq, gp, Hq);
-
   const double nu = P.nu;
   const double JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
+  // linearization storage: per wave CPW*N3 lanes x kQData values, value-major (coalesced)
+  constexpr int QW = CPW * N3;
+  double *qdw = P.qd ? P.qd + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane : nullptr;
+
+  // ---------------- phase A: state at this lane's quadrature point
+  double u[3] = {0., 0., 0.}, gu[3][3] = {}, R[3] = {0., 0., 0.}, tau = 0.;
+  double pq = 0., f[3] = {0., 0., 0.}, Tt[3] = {0., 0., 0.}, srf[3] = {0., 0., 0.};
+  if constexpr (CACHED) {
+    if (pact) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) u[c] = qdw[c * QW];
+#pragma unroll
+      for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = qdw[(3 + c) * QW];
+      tau = qdw[12 * QW];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) R[c] = qdw[(13 + c) * QW];
+    }
+  } else {
+  double lu[3] = {0., 0., 0.};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) vel_field(c, u[c], gu[c], lu[c]);
+  double gp[3] = {0., 0., 0.}, Hq[3] = {0., 0., 0.};
+  scal_fields(3, 3, 4, pq, gp, Hq);
+
   const double hst = P.geo[gcell * 4 + 3];
   const double un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
   const double u_mag = fmax(sqrt(un2), 1e-12);
   const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
-  const double tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
-  double f[3] = {0., 0., 0.};
+  tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
   if (P.force_q && pact) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) f[c] = P.force_q[((int64_t)gcell * N3 + q) * 3 + c];
   }
-  double Gu[3], R[3], srf[3] = {0., 0., 0.};
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    Gu[c] = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
-    R[c] = Gu[c] + gp[c] - nu * lu[c] - f[c];
-  }
+  for (int c = 0; c < 3; ++c)
+    R[c] = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2] + gp[c] - nu * lu[c] - f[c];
   if (P.srf) {
     const double *om = P.omega;
     const double xq[3] = {P.x0[gcell * 3 + 0] + hx * sM[84 + qx], P.x0[gcell * 3 + 1] + hy * sM[84 + qy],
@@ -354,11 +372,24 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
       R[c] += srf[c];
     }
   }
-  double Tt[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     Tt[c] = P.alpha[0] * u[c] + Hq[c];
     R[c] += Tt[c];
+  }
+  }  // !CACHED
+
+  if constexpr (LIN) {  // store the linearization; the integration below is J.v's (MODE_JVQ)
+    if (pact) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) qdw[c * QW] = u[c];
+#pragma unroll
+      for (int c = 0; c < 9; ++c) qdw[(3 + c) * QW] = gu[c / 3][c % 3];
+      qdw[12 * QW] = tau;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) qdw[(13 + c) * QW] = R[c];
+    }
+    return;
   }
 
   double Tc[16];
@@ -366,7 +397,8 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     const double divu = gu[0][0] + gu[1][1] + gu[2][2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      Tc[4 * c] = JxW * (-Gu[c] + f[c] - Tt[c] - srf[c]);
+      const double Gu = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
+      Tc[4 * c] = JxW * (-Gu + f[c] - Tt[c] - srf[c]);
 #pragma unroll
       for (int e = 0; e < 3; ++e)
         Tc[4 * c + 1 + e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]) * ih[e];
@@ -378,9 +410,9 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     // ---------------- phase B: the trial function v at this lane's quadrature point
     double v[3] = {0., 0., 0.}, gv[3][3] = {}, lv[3] = {0., 0., 0.};
 #pragma unroll
-    for (int c = 0; c < 3; ++c) vel_field(7 + c, v[c], gv[c], lv[c]);
+    for (int c = 0; c < 3; ++c) vel_field(FV + c, v[c], gv[c], lv[c]);
     double vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
-    scal_fields(10, 0, 0, vp, gvp, dummy);
+    scal_fields(FV + 3, 0, 0, vp, gvp, dummy);
     const double aj = P.alpha_jac;
     double S[3], A[3];
 #pragma unroll
@@ -492,8 +524,14 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
 template <int K>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
-  const int NF = mode == MODE_JV ? 11 : 7;
+  const int NF = mode == MODE_JVQ ? 4 : (mode == MODE_JV ? 11 : 7);
   return sizeof(double) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3 + 5 * 16 + 8) + sizeof(int) * (size_t)C::BN3;
+}
+
+template <int K>
+size_t brick_qdata_doubles(int n_cells) {
+  using C = BrickCfg<K>;
+  return (size_t)(n_cells / 8) * C::WAVES * kQData * C::CPW * C::N3;
 }
 
 template <int K>
@@ -504,9 +542,17 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   const size_t lds = brick_lds_bytes<K>(mode);
   if (mode == MODE_JV)
     hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
+  else if (mode == MODE_JVQ)
+    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
+  else if (mode == MODE_LIN)
+    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_LIN>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
   else
     hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
   return hipGetLastError();
+}
+
+size_t brick_qdata_size(int k, int n_cells) {
+  return k == 1 ? brick_qdata_doubles<1>(n_cells) : (k == 2 ? brick_qdata_doubles<2>(n_cells) : 0);
 }
 
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {

@@ -11,7 +11,10 @@ constexpr int kMaxQ1D = 5;      // QGauss(n) with n <= 5
 
 constexpr int ipow(int b, int e) { return e == 0 ? 1 : b * ipow(b, e - 1); }
 
-enum Mode { MODE_RESIDUAL = 0, MODE_JV = 1, MODE_DIAG = 2 };
+// MODE_LIN / MODE_JVQ (brick kernels only): MODE_LIN stores the linearization at every quadrature
+// point (u, grad u, tau, R_s: kQData doubles) once per state; MODE_JVQ applies J.v from it.
+enum Mode { MODE_RESIDUAL = 0, MODE_JV = 1, MODE_DIAG = 2, MODE_LIN = 3, MODE_JVQ = 4 };
+constexpr int kQData = 16;  // u[3], grad u[3][3], tau, R_s[3]
 
 // Reference-cell 1D tables on [0,1] (deal.II unit cell): Lagrange basis on Gauss–Lobatto
 // support points evaluated at QGauss points. [q][node].
@@ -40,6 +43,7 @@ struct OpParams {
   const double *u;
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input
+  double *qd;                 // MODE_LIN output / MODE_JVQ input (brick wave-major layout)
   double *y;                  // output (accumulated with atomics)
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs

@@ -9,6 +9,7 @@ hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const 
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
+size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
 
 // ---- BLAS-1 style kernels on device vectors (gls_vector_kernels.hip)
 hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s);
@@ -35,10 +36,14 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();
 
-// ---- geometric multigrid (gls_mg_kernels.hip): nested n^3 Qk lattices, k <= 2
-hipError_t mg_transfer(const double *in, double *out, int nin, int nout, int k, int prolong, double *tmp1,
-                       double *tmp2, hipStream_t s);
-hipError_t mg_inject(const double *fine, double *coarse, int nf, int nc, hipStream_t s);
+// ---- geometric multigrid (gls_mg_kernels.hip): nested Qk node lattices (boxes), k <= 2
+hipError_t mg_transfer(const double *in, double *out, const int nin[3], const int nout[3], int k, int prolong,
+                       double *tmp1, double *tmp2, hipStream_t s);
+hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s);
+hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
+                         int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes
+hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,
+                          hipStream_t s);
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s);
 

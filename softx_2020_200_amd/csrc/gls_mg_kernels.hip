@@ -5,6 +5,8 @@
 // interpolates the coarse Qk field exactly at the fine nodes; restriction is its transpose.
 // Both are applied as three separable 1D passes over a [n2][n1][n0][ncomp] lattice array
 // (velocity: ncomp 3 interleaved, pressure: ncomp 1), each thread producing one output entry.
+// Multi-GPU: each rank works on the box sub-lattice its cells span (box gather / scatter through
+// a box -> local node map); nested partitions keep the coarse box the fine box's every-second node.
 #include "gls_launch.hpp"
 
 namespace gls {
@@ -67,16 +69,41 @@ __global__ void k_transfer_axis(const double *__restrict__ in, double *__restric
   }
 }
 
-// coarse (I,J,K) <- fine (2I,2J,2K), velocity (3 comps) and pressure parts
-__global__ void k_inject(const double *__restrict__ fine, double *__restrict__ coarse, int nf, int nc) {
-  const int64_t nvc = (int64_t)nc * nc * nc, nvf = (int64_t)nf * nf * nf;
+// coarse (I,J,K) <- fine (2I,2J,2K) on box lattices, velocity (3 comps) and pressure parts
+__global__ void k_inject(const double *__restrict__ fine, double *__restrict__ coarse, int f0, int f1, int f2, int c0,
+                         int c1, int c2) {
+  const int64_t nvc = (int64_t)c0 * c1 * c2, nvf = (int64_t)f0 * f1 * f2;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nvc; t += (int64_t)gridDim.x * blockDim.x) {
-    const int I = (int)(t % nc), J = (int)((t / nc) % nc), K = (int)(t / ((int64_t)nc * nc));
-    const int64_t f = ((int64_t)(2 * K) * nf + 2 * J) * nf + 2 * I;
+    const int I = (int)(t % c0), J = (int)((t / c0) % c1), K = (int)(t / ((int64_t)c0 * c1));
+    const int64_t f = ((int64_t)(2 * K) * f1 + 2 * J) * f0 + 2 * I;
     coarse[3 * t + 0] = fine[3 * f + 0];
     coarse[3 * t + 1] = fine[3 * f + 1];
     coarse[3 * t + 2] = fine[3 * f + 2];
     coarse[3 * nvc + t] = fine[3 * nvf + f];
+  }
+}
+
+// rank-local vector [vel (3 interleaved) | p] over n_vnodes nodes <-> box lattice vector over nbox
+// nodes (box node t is local node map[t]); gather zeroes non-owned nodes when n_owned >= 0
+__global__ void k_box_gather(const double *__restrict__ loc, double *__restrict__ box, const int32_t *__restrict__ map,
+                             int64_t nbox, int64_t nvl, int64_t n_owned) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nbox; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t li = map[t];
+    const bool on = n_owned < 0 || li < n_owned;
+    box[3 * t + 0] = on ? loc[3 * li + 0] : 0.0;
+    box[3 * t + 1] = on ? loc[3 * li + 1] : 0.0;
+    box[3 * t + 2] = on ? loc[3 * li + 2] : 0.0;
+    box[3 * nbox + t] = on ? loc[3 * nvl + li] : 0.0;
+  }
+}
+__global__ void k_box_scatter(const double *__restrict__ box, double *__restrict__ loc, const int32_t *__restrict__ map,
+                              int64_t nbox, int64_t nvl) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nbox; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t li = map[t];
+    loc[3 * li + 0] = box[3 * t + 0];
+    loc[3 * li + 1] = box[3 * t + 1];
+    loc[3 * li + 2] = box[3 * t + 2];
+    loc[3 * nvl + li] = box[3 * nbox + t];
   }
 }
 
@@ -96,29 +123,44 @@ int grid_for(int64_t n) {
 
 }  // namespace
 
-// out = T(in) for one Qk vector [vel (3 comps interleaved) | pressure] on an n^3 node lattice,
-// T = prolongation (nc -> nf) or restriction (nf -> nc); tmp1/tmp2 hold intermediate passes.
-hipError_t mg_transfer(const double *in, double *out, int nin, int nout, int k, int prolong, double *tmp1,
-                       double *tmp2, hipStream_t s) {
-  const int64_t nvi = (int64_t)nin * nin * nin, nvo = (int64_t)nout * nout * nout;
+// out = T(in) for one Qk vector [vel (3 comps interleaved) | pressure] on a box node lattice
+// (dims x, y, z), T = prolongation (nin -> nout = 2 nin - 1 per axis) or restriction (nin -> nout,
+// nin = 2 nout - 1); tmp1/tmp2 hold the intermediate passes.
+hipError_t mg_transfer(const double *in, double *out, const int nin[3], const int nout[3], int k, int prolong,
+                       double *tmp1, double *tmp2, hipStream_t s) {
+  const int64_t nvi = (int64_t)nin[0] * nin[1] * nin[2], nvo = (int64_t)nout[0] * nout[1] * nout[2];
   for (int part = 0; part < 2; ++part) {
     const int nc = part == 0 ? 3 : 1;
     const double *src = in + (part == 0 ? 0 : 3 * nvi);
     double *dst = out + (part == 0 ? 0 : 3 * nvo);
-    // axis 0: (nin,nin,nin) -> (nout,nin,nin); axis 1 -> (nout,nout,nin); axis 2 -> (nout,nout,nout)
-    const int64_t s1 = (int64_t)nout * nin * nin * nc, s2 = (int64_t)nout * nout * nin * nc, s3 = nvo * nc;
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s1)), dim3(256), 0, s, src, tmp1, nin, nin, nin, 0, nout, nc, k,
-                       prolong);
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s2)), dim3(256), 0, s, tmp1, tmp2, nout, nin, nin, 1, nout, nc,
-                       k, prolong);
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s3)), dim3(256), 0, s, tmp2, dst, nout, nout, nin, 2, nout, nc,
-                       k, prolong);
+    // axis 0: (i0,i1,i2) -> (o0,i1,i2); axis 1 -> (o0,o1,i2); axis 2 -> (o0,o1,o2)
+    const int64_t s1 = (int64_t)nout[0] * nin[1] * nin[2] * nc, s2 = (int64_t)nout[0] * nout[1] * nin[2] * nc,
+                  s3 = nvo * nc;
+    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s1)), dim3(256), 0, s, src, tmp1, nin[0], nin[1], nin[2], 0,
+                       nout[0], nc, k, prolong);
+    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s2)), dim3(256), 0, s, tmp1, tmp2, nout[0], nin[1], nin[2], 1,
+                       nout[1], nc, k, prolong);
+    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s3)), dim3(256), 0, s, tmp2, dst, nout[0], nout[1], nin[2], 2,
+                       nout[2], nc, k, prolong);
   }
   return hipGetLastError();
 }
 
-hipError_t mg_inject(const double *fine, double *coarse, int nf, int nc, hipStream_t s) {
-  hipLaunchKernelGGL(k_inject, dim3(grid_for((int64_t)nc * nc * nc)), dim3(256), 0, s, fine, coarse, nf, nc);
+hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s) {
+  hipLaunchKernelGGL(k_inject, dim3(grid_for((int64_t)nc[0] * nc[1] * nc[2])), dim3(256), 0, s, fine, coarse, nf[0],
+                     nf[1], nf[2], nc[0], nc[1], nc[2]);
+  return hipGetLastError();
+}
+
+hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
+                         int64_t n_owned, hipStream_t s) {
+  hipLaunchKernelGGL(k_box_gather, dim3(grid_for(nbox)), dim3(256), 0, s, loc, box, map, nbox, nvl, n_owned);
+  return hipGetLastError();
+}
+
+hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_box_scatter, dim3(grid_for(nbox)), dim3(256), 0, s, box, loc, map, nbox, nvl);
   return hipGetLastError();
 }
 

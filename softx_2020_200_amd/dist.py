@@ -217,3 +217,27 @@ class DistributedProblem:
         self.exchanger = Exchanger(plan, device, backend=backend, group=group)
         attach(self.ctx, plan, self.exchanger)
         self.n_dofs_local = self.ctx.n_dofs
+
+    def set_lattice(self):
+        """Declare this rank's nodes as a box of the global hyper_cube node lattice (multigrid)."""
+        n1d = int(round(self.n_vnodes_global ** (1.0 / 3.0)))
+        self.ctx.set_lattice(n1d, self.plan["local_to_global"])
+
+
+def multigrid_levels(n, world, coarsest=4):
+    """Cells per direction of the nested levels below n usable by a distributed V-cycle: every level
+    keeps whole 2x2x2 bricks and a brick count divisible by the rank count (nested partitions)."""
+    out = []
+    m = n
+    while m % 2 == 0 and m // 2 >= coarsest and ((m // 2) ** 3 // 8) % world == 0 and (m // 2) % 2 == 0:
+        m //= 2
+        out.append(m)
+    return out
+
+
+def attach_distributed_multigrid(levels, **mg_opts):
+    """levels: [DistributedProblem] on nested hyper_cubes (fine first), same ranks / boundary data."""
+    for lv in levels:
+        lv.set_lattice()
+    levels[0].ctx.attach_multigrid([lv.ctx for lv in levels[1:]], **mg_opts)
+    levels[0]._mg_levels = levels

@@ -29,7 +29,7 @@ EXPORTS = [
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import",
-    "gls_mg_attach", "gls_mg_detach",
+    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice",
 ]
 
 
@@ -107,6 +107,7 @@ def load():
     L.gls_uses_brick_kernels.argtypes = [vp]
     L.gls_mg_attach.argtypes = [vp, C.POINTER(MGParams)]
     L.gls_mg_detach.argtypes = [vp]
+    L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     _lib = L
     return L
 
@@ -319,6 +320,11 @@ class GLSContext:
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega)
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
+
+    def set_lattice(self, n1d, local_to_global):
+        """Declare the (rank-local) nodes as a box of the global n1d^3 hyper_cube node lattice."""
+        l2g = np.ascontiguousarray(local_to_global, dtype=np.int64)
+        check(self.L.gls_set_lattice(self.h, int(n1d), l2g.ctypes.data_as(C.POINTER(C.c_int64))), "gls_set_lattice")
 
     def detach_multigrid(self):
         check(self.L.gls_mg_detach(self.h), "gls_mg_detach")

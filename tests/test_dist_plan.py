@@ -12,6 +12,35 @@ import softx_2020_200_amd as sx
 from softx_2020_200_amd.dist import local_vector, owned_global_dofs, partition
 
 
+
+def _box(l2g, n1d):
+    x, y, z = l2g % n1d, (l2g // n1d) % n1d, l2g // (n1d * n1d)
+    lo = np.array([x.min(), y.min(), z.min()])
+    dims = np.array([x.max(), y.max(), z.max()]) - lo + 1
+    return lo, dims, int(np.prod(dims)) == l2g.size
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_partitions_are_nested_boxes(world):
+    """Distributed multigrid precondition (gls_set_lattice / gls_mg_attach): on 2^j ranks every
+    rank's nodes fill a box of the node lattice, and the rank's box on the n/2 mesh is every
+    second node of its box on the n mesh (coarse cells = parents of the fine cells)."""
+    from softx_2020_200_amd.dist import multigrid_levels
+    n, k = 8, 2
+    levels = [n] + multigrid_levels(n, world, 2)
+    assert levels[1] == 4
+    for r in range(world):
+        boxes = []
+        for m in levels:
+            mesh = sx.hyper_cube(3, m, k, k)
+            p = partition(mesh["cell_vnodes"], mesh["n_vnodes"], r, world)
+            lo, dims, full = _box(p["local_to_global"], k * m + 1)
+            assert full, (world, r, m)
+            boxes.append((lo, dims))
+        for (flo, fd), (clo, cd) in zip(boxes[:-1], boxes[1:]):
+            assert np.array_equal(flo, 2 * clo) and np.array_equal(fd, 2 * cd - 1)
+
+
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_partition_invariants(world):
     m = sx.hyper_cube(3, 4, 2, 2)

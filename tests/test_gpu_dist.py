@@ -95,3 +95,94 @@ def test_two_ranks_one_gpu_matches_single_rank():
         assert e["res"] < 1e-12 and e["jv"] < 1e-12 and e["diag"] < 1e-12, (rank, e)
         assert e["newton_res"][1] < 1e-9, (rank, e)
         assert e["newton_u"] < 1e-7, (rank, e)
+
+
+def _mg_worker(rank, world, port, q):
+    """Distributed multigrid (every level partitioned, nested rank boxes) vs the single-rank V-cycle:
+    the preconditioned GMRES and one Newton step must agree (same iterations, same solution)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import softx_2020_200_amd as sx
+    from softx_2020_200_amd.dist import (DistributedProblem, attach_distributed_multigrid, dist_import,
+                                         local_vector, multigrid_levels, owned_global_dofs)
+    from softx_2020_200_amd.problem import CavityProblem, dirichlet_from_bcs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, nu, ts = 8, 0.02, (0.01, 0.01, 0.01, 0.01)
+        single = CavityProblem(dim=3, n=n, k=2, viscosity=nu, multigrid=True, mg_coarsest=4)
+        g = single.ctx
+        g.set_time("bdf2", ts)
+        m = single.mesh
+        N = g.n_dofs
+        rng = np.random.default_rng(20200200 + 1)
+        u1, u2, b = (0.3 * rng.uniform(-1, 1, N) for _ in range(3))
+        u1[single.dir_dofs] = single.dir_vals
+        u2[single.dir_dofs] = single.dir_vals
+        b[single.dir_dofs] = 0.0
+        cu = lambda a: torch.tensor(a, dtype=torch.float64, device="cuda")
+        g.set_state(cu(u1), cu(u1), cu(u2))
+        xg, its_g, res_g, ok_g = g.solve_linear(cu(b), max_iterations=100, restart=30, relative_residual=1e-8)
+        # distributed levels with the same boundary data
+        bcs = [("noslip", bb, None) for bb in (0, 1, 2, 4, 5)] + [("function", 3, (1.0, 0.0, 0.0))]
+        levels = []
+        for mm_n in [n] + multigrid_levels(n, world, 4):
+            mm = sx.hyper_cube(3, mm_n, 2, 2, -1.0, 1.0)
+            mk, dd, dv = dirichlet_from_bcs(mm, mm_n, -1.0, 1.0, True, bcs)
+            levels.append(DistributedProblem(mm, rank, world, "cuda", viscosity=nu, vnode_mask=mk, dirichlet=(dd, dv),
+                                             backend="gloo"))
+        assert len(levels) == 1 + len(single.levels)
+        attach_distributed_multigrid(levels)
+        dp = levels[0]
+        c = dp.ctx
+        c.set_time("bdf2", ts)
+        lv = lambda a: cu(local_vector(dp.plan, a, m["n_vnodes"]))
+        U1, U2, B = lv(u1), lv(u2), lv(b)
+        dist_import(c, U1)
+        dist_import(c, U2)
+        c.set_state(U1, U1, U2)
+        xd, its_d, res_d, ok_d = c.solve_linear(B, max_iterations=100, restart=30, relative_residual=1e-8)
+        loc, glo = owned_global_dofs(dp.plan, m["n_vnodes"])
+        xgn = xg.cpu().numpy()
+        errs = {"lin_its": (its_g, its_d), "ok": (ok_g, ok_d),
+                "x_rel": float(np.abs(xd.cpu().numpy()[loc] - xgn[glo]).max() / np.abs(xgn).max())}
+        # one Newton step with the multigrid-preconditioned GMRES
+        x_g = cu(u1.copy())
+        stg = g.newton(x_g, cu(u1), cu(u2), tolerance=1e-30, max_iterations=1, lin_max_iterations=100,
+                       relative_residual=1e-6)
+        X = lv(u1.copy())
+        std = c.newton(X, U1, U2, tolerance=1e-30, max_iterations=1, lin_max_iterations=100, relative_residual=1e-6)
+        xs = x_g.cpu().numpy()
+        errs["newton_lin_its"] = (stg["linear_iterations"], std["linear_iterations"])
+        errs["newton_x"] = float(np.abs(X.cpu().numpy()[loc] - xs[glo]).max() / np.abs(xs).max())
+        q.put((rank, errs))
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_multigrid_matches_single_rank(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30300 + 10 * world + os.getpid() % 400
+    procs = [ctx.Process(target=_mg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, e in res:
+        assert "error" not in e, e
+        assert e["ok"] == (True, True), (rank, e)
+        assert abs(e["lin_its"][0] - e["lin_its"][1]) <= 1, (rank, e)
+        assert e["x_rel"] < 1e-7, (rank, e)
+        assert abs(e["newton_lin_its"][0] - e["newton_lin_its"][1]) <= 1, (rank, e)
+        assert e["newton_x"] < 1e-7, (rank, e)

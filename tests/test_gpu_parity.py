@@ -189,3 +189,31 @@ def test_brick_deterministic():
     a = ctx.jacobian_apply(cuda(v)).cpu().numpy()
     b = ctx.jacobian_apply(cuda(v)).cpu().numpy()
     assert relerr(a, b) < 1e-14
+
+
+@pytest.mark.gpu
+def test_jv_linearization_cache(monkeypatch):
+    """J.v reads the per-quadrature-point linearization (MODE_LIN once per state, MODE_JVQ per call).
+    It equals the recompute-every-call kernel (GLS_JV_RECOMPUTE=1) and the oracle, and is refreshed
+    by every state / time-step / viscosity change (a stale cache would fail the oracle checks)."""
+    p = _morton_problem(4, 2, "bdf2", 0.02)
+    u, u1, u2, u3, v = _states(p)
+    ctx = context_for(p)
+    monkeypatch.setenv("GLS_JV_RECOMPUTE", "1")
+    ref_ctx = context_for(p)
+    monkeypatch.delenv("GLS_JV_RECOMPUTE")
+    orc = Oracle(p)
+    for c in (ctx, ref_ctx):
+        c.set_state(cuda(u), cuda(u1), cuda(u2))
+    a = ctx.jacobian_apply(cuda(v)).cpu().numpy()
+    assert relerr(a, ref_ctx.jacobian_apply(cuda(v)).cpu().numpy()) < 1e-14
+    assert relerr(a, orc.jacobian_apply(u, v, u1, u2)) < TOL
+    # new state through set_state
+    ctx.set_state(cuda(u3), cuda(u1), cuda(u2))
+    assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u3, v, u1, u2)) < TOL
+    # new time steps (alpha, tau's transient term) and viscosity
+    p2 = _morton_problem(4, 2, "bdf2", 0.05)
+    p2.time_steps = (0.02, 0.013, 0.011, 0.009)
+    ctx.set_time("bdf2", p2.time_steps)
+    ctx.set_viscosity(0.05)
+    assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), Oracle(p2).jacobian_apply(u3, v, u1, u2)) < TOL

@@ -16,7 +16,9 @@ m2 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.di
 ctx.set_state(m1, m1, m2)
 v = torch.rand(ctx.n_dofs, dtype=torch.float64, device="cuda")
 y = torch.empty_like(v)
+ctx.timing(True)
 ctx.jacobian_apply(v, y); ctx.residual(y); torch.cuda.synchronize()
+ms_l, n_l = ctx.timing_get(3)
 ctx.timing(True)
 for _ in range(reps):
     ctx.jacobian_apply(v, y)
@@ -25,5 +27,6 @@ for _ in range(reps // 4 + 1):
 ms_jv, n_jv = ctx.timing_get(1)
 ms_r, n_r = ctx.timing_get(0)
 ms_d, n_d = ctx.timing_get(2)
-print("n=%d k=%d brick=%s  J.v %.3f ms  residual %.3f ms  diag %.3f ms  (cells %d, dofs %d)" % (
-    n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_r / n_r, ms_d / max(n_d, 1), prob.mesh["n_cells"], ctx.n_dofs))
+print("n=%d k=%d brick=%s  J.v %.3f ms  residual %.3f ms  diag %.3f ms  linearize %.3f ms (cells %d, dofs %d)" % (
+    n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_r / n_r, ms_d / max(n_d, 1), ms_l / max(n_l, 1),
+    prob.mesh["n_cells"], ctx.n_dofs))
