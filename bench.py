@@ -95,6 +95,9 @@ def main():
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="GMRES right preconditioner: geometric multigrid V-cycle (default) or Jacobi")
     ap.add_argument("--mg-coarsest", type=int, default=4)
+    ap.add_argument("--mg-smooth", type=int, nargs=2, default=(1, 1), metavar=("PRE", "POST"),
+                    help="damped-Jacobi sweeps before / after the coarse correction")
+    ap.add_argument("--mg-omega", type=float, default=0.6)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
@@ -126,7 +129,8 @@ def main():
     ts = (args.dt,) * 4
     if world == 1:
         prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu,
-                             multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest)
+                             multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
+                             pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega)
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -150,7 +154,8 @@ def main():
                 mk, dd, dv = dirichlet_from_bcs(mm, m, -1.0, 1.0, True, bcs)
                 lv.append(DistributedProblem(mm, rank, world, dev, viscosity=args.nu, vnode_mask=mk,
                                              dirichlet=(dd, dv), backend=args.dist_backend))
-            attach_distributed_multigrid(lv)
+            attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
+                                         omega=args.mg_omega)
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
@@ -235,7 +240,7 @@ def main():
                                % (args.k, args.kp, args.n),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
-                       args.restart, "GMG V(2,2)-cycle" if args.precond == "mg" else "Jacobi",
+                       args.restart, "GMG V(%d,%d)-cycle" % tuple(args.mg_smooth) if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
                    "parallelism": "domain decomposition x%d (RCCL P2P ghosts)" % world if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,

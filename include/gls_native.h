@@ -33,6 +33,7 @@ extern "C" {
 #define GLS_ENOCONV -4  /* linear solver did not converge (informational) */
 #define GLS_EIO -5      /* file / parse error */
 #define GLS_ECOMM -6    /* RCCL error */
+#define GLS_ENOTFOUND -7 /* parameter entry absent (gls_prm_get; the caller applies the default) */
 
 /* TimeSteppingMethod, same order as include/core/parameters.h:56-69 */
 enum gls_scheme {
@@ -220,6 +221,39 @@ int gls_mesh_hyper_cube_sizes(int dim, int n, int k, int kp, int periodic_mask,
                               int64_t *n_cells, int64_t *n_vnodes, int64_t *n_pnodes);
 int gls_mesh_hyper_cube(int dim, int n, int k, int kp, double lo, double hi, int periodic_mask,
                         int32_t *cell_vnodes, int32_t *cell_pnodes, double *cell_x0, double *cell_h);
+
+/* ------------------------------------------------------------------------------------------
+ * Drop-in I/O surface, host side.
+ * Parameter files: deal.II ParameterHandler text (`subsection`/`end`, `set key = value`, `#`
+ * comments, `\` continuation) as read by Parameters::*::parse_parameters (source/core/
+ * parameters.cc) and BoundaryConditions (boundary_conditions.h:130-425). Entries are addressed
+ * "subsection/subsection/key" with deal.II's whitespace normalisation.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct gls_prm gls_prm;
+int gls_prm_parse(const char *text_or_path, int is_path, gls_prm **out);
+int gls_prm_get(const gls_prm *prm, const char *path, char *buf, int cap); /* length, or GLS_ENOTFOUND */
+int gls_prm_n_entries(const gls_prm *prm);
+int gls_prm_entry(const gls_prm *prm, int i, char *path, int path_cap, char *value, int value_cap);
+void gls_prm_destroy(gls_prm *prm);
+
+/* Function expressions: deal.II Functions::ParsedFunction / FunctionParser over muParser
+ * ("Function expression" = ';'-separated components, "Function constants" = "a=1, b=2",
+ * variables "x,y,z,t"; pi/Pi predefined; deal.II's extra functions if/int/ceil/floor/cot/csc/
+ * sec/pow/erfc and log = natural log). out[p*n_comp + c], values[p*n_vars + v] (HOST arrays). */
+typedef struct gls_expr gls_expr;
+int gls_expr_create(const char *expr, const char *vars, const char *constants, gls_expr **out);
+int gls_expr_n_components(const gls_expr *e);
+int gls_expr_eval(const gls_expr *e, int64_t n_points, const double *values, double *out);
+void gls_expr_destroy(gls_expr *e);
+
+/* Output: NavierStokesBase::write_output_results (navier_stokes_base.cc:998-1086) — one patch per
+ * cell with `subdivision` intervals (Lagrange cells when k > 1), point data velocity, pressure,
+ * subdomain, vorticity, q_criterion [, velocity_eulerian when mesh->srf]; solution is a HOST
+ * vector in this library's layout. Master records: write_vtu_and_pvd (solutions_output.cc:14-59). */
+int gls_vtu_write(const char *filename, const gls_mesh_desc *mesh, const double *solution, int subdivision,
+                  int subdomain, int binary);
+int gls_pvtu_write(const char *filename, int dim, int srf, int n_pieces, const char *const *piece_files);
+int gls_pvd_write(const char *filename, int n, const double *times, const char *const *files);
 
 /* ------------------------------------------------------------------------------------------
  * Profiling hooks: time the next operator launches on the context stream with HIP events.

@@ -100,6 +100,14 @@ bool is_sdirk(int s) { return s >= GLS_SDIRK2 && s <= GLS_SDIRK3_3; }
 }  // namespace
 
 int gls_internal_set_err(int code, const char *msg) { return set_err(code, "%s", msg); }
+int gls_io_set_error(int code, const char *fmt, ...) {  // gls_io.cpp
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return set_err(code, "%s", buf);
+}
 
 extern "C" {
 

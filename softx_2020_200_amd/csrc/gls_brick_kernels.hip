@@ -330,17 +330,19 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   // ---------------- phase A: state at this lane's quadrature point
   double u[3] = {0., 0., 0.}, gu[3][3] = {}, R[3] = {0., 0., 0.}, tau = 0.;
   double pq = 0., f[3] = {0., 0., 0.}, Tt[3] = {0., 0., 0.}, srf[3] = {0., 0., 0.};
-  if constexpr (CACHED) {
+  // JVQ: the linearization is loaded after the v sweeps (short live ranges: no spills)
+  auto load_qd = [&]() {
     if (pact) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) u[c] = qdw[c * QW];
+      for (int c = 0; c < 3; ++c) u[c] = __builtin_nontemporal_load(qdw + c * QW);
 #pragma unroll
-      for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = qdw[(3 + c) * QW];
-      tau = qdw[12 * QW];
+      for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = __builtin_nontemporal_load(qdw + (3 + c) * QW);
+      tau = __builtin_nontemporal_load(qdw + 12 * QW);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) R[c] = qdw[(13 + c) * QW];
+      for (int c = 0; c < 3; ++c) R[c] = __builtin_nontemporal_load(qdw + (13 + c) * QW);
     }
-  } else {
+  };
+  if constexpr (!CACHED) {
   double lu[3] = {0., 0., 0.};
 #pragma unroll
   for (int c = 0; c < 3; ++c) vel_field(c, u[c], gu[c], lu[c]);
@@ -413,6 +415,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     for (int c = 0; c < 3; ++c) vel_field(FV + c, v[c], gv[c], lv[c]);
     double vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
     scal_fields(FV + 3, 0, 0, vp, gvp, dummy);
+    if constexpr (CACHED) load_qd();
     const double aj = P.alpha_jac;
     double S[3], A[3];
 #pragma unroll

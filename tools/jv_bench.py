@@ -24,6 +24,8 @@ for _ in range(reps):
     ctx.jacobian_apply(v, y)
 for _ in range(reps // 4 + 1):
     ctx.residual(y)
+d_out = torch.empty_like(v)
+ctx.jacobian_diagonal(out=d_out)  # k_copy of n_dofs doubles: PMC byte calibration (tools/pmc_traffic.sh)
 ms_jv, n_jv = ctx.timing_get(1)
 ms_r, n_r = ctx.timing_get(0)
 ms_d, n_d = ctx.timing_get(2)
