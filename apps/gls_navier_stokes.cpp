@@ -1,0 +1,1024 @@
+// gls_navier_stokes — parameter-file driven GLS Navier–Stokes application on MI355X: the drop-in
+// for the reference's applications/gls_navier_stokes_{2d,3d} (the GLSNavierStokesSolver::solve
+// flow, gls_navier_stokes.cc:1395-1423), built only on the C-ABI of libgls_native.so:
+//   read prm (gls_prm_*) -> hyper_cube mesh + boundary conditions (setup_dofs :55-228) ->
+//   initial condition (nodal | L2projection | viscous, :784-827) -> time loop (integrate, first
+//   step with the BDF start-up, SDIRK stages; navier_stokes_base.cc:426-590) with the device
+//   Newton/GMRES (gls_newton_solve) -> post-processing (L2 error vs the analytical solution,
+//   enstrophy, kinetic energy, CFL; VTU/PVTU/PVD output).
+// Results are printed as `key = value` lines and a final error table (own format); the numbers
+// are what the parity tests compare with the reference's outputs.
+//
+// Usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm
+// Scope: mesh type dealii / grid type hyper_cube (+ initial refinement, uniform refinement for
+// steady "number mesh adapt"); bc types noslip, function, periodic (slip: SURVEY §8 f2, next).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../include/gls_native.h"
+
+namespace {
+
+[[noreturn]] void die(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::fprintf(stderr, "gls_navier_stokes: ");
+  std::vfprintf(stderr, fmt, ap);
+  std::fprintf(stderr, "\n");
+  va_end(ap);
+  std::exit(2);
+}
+void ck(int rc, const char *what) {
+  if (rc < 0 && rc != GLS_ENOCONV) die("%s failed (%d): %s", what, rc, gls_last_error());
+}
+void hk(hipError_t e, const char *what) {
+  if (e != hipSuccess) die("%s: %s", what, hipGetErrorString(e));
+}
+std::string trim(const std::string &s) {
+  const size_t a = s.find_first_not_of(" \t"), b = s.find_last_not_of(" \t");
+  return a == std::string::npos ? "" : s.substr(a, b - a + 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// parameters: entry names / defaults follow the reference's declarations
+// (source/core/parameters.cc, include/core/boundary_conditions.h:130-330)
+// ---------------------------------------------------------------------------------------------
+struct Prm {
+  gls_prm *h = nullptr;
+  explicit Prm(const char *path) { ck(gls_prm_parse(path, 1, &h), "reading the parameter file"); }
+  ~Prm() { gls_prm_destroy(h); }
+  std::string get(const std::string &path, const std::string &dflt) const {
+    const int n = gls_prm_get(h, path.c_str(), nullptr, 0);
+    if (n == GLS_ENOTFOUND) return dflt;
+    ck(n, "gls_prm_get");
+    std::vector<char> buf((size_t)n + 1);
+    gls_prm_get(h, path.c_str(), buf.data(), n + 1);
+    return std::string(buf.data());
+  }
+  double d(const std::string &p, double dflt) const {
+    const std::string s = get(p, "");
+    if (s.empty()) return dflt;
+    char *e = nullptr;
+    const double v = std::strtod(s.c_str(), &e);
+    if (e == s.c_str()) die("%s = '%s' is not a number", p.c_str(), s.c_str());
+    return v;
+  }
+  int i(const std::string &p, int dflt) const { return (int)std::lround(d(p, dflt)); }
+  bool b(const std::string &p, bool dflt) const {
+    const std::string s = get(p, dflt ? "true" : "false");
+    if (s == "true" || s == "yes") return true;
+    if (s == "false" || s == "no") return false;
+    die("%s = '%s' is not a bool", p.c_str(), s.c_str());
+  }
+};
+
+// a ParsedFunction-style function read from subsection `sec`
+struct Function {
+  gls_expr *e = nullptr;
+  int nc = 0;
+  Function() = default;
+  Function(const Prm &p, const std::string &sec, int dim, const std::string &dflt_expr) {
+    const std::string vars = p.get(sec + "/Variable names", dim == 3 ? "x,y,z,t" : "x,y,t");
+    const std::string ex = p.get(sec + "/Function expression", dflt_expr);
+    const std::string cs = p.get(sec + "/Function constants", "");
+    ck(gls_expr_create(ex.c_str(), vars.c_str(), cs.c_str(), &e), (sec + "/Function expression").c_str());
+    nc = gls_expr_n_components(e);
+    if (std::count(vars.begin(), vars.end(), ',') != dim) die("%s: expected %d variables", sec.c_str(), dim + 1);
+  }
+  Function(const Function &) = delete;
+  Function &operator=(const Function &) = delete;
+  Function(Function &&o) noexcept : e(o.e), nc(o.nc) { o.e = nullptr; }
+  Function &operator=(Function &&o) noexcept {
+    std::swap(e, o.e);
+    nc = o.nc;
+    return *this;
+  }
+  ~Function() { gls_expr_destroy(e); }
+  // out[p*nc + c] at the points X[p*dim + d] and time t
+  void eval(const std::vector<double> &X, int dim, double t, std::vector<double> &out) const {
+    const int64_t n = (int64_t)X.size() / dim;
+    std::vector<double> v((size_t)n * (dim + 1));
+    for (int64_t q = 0; q < n; ++q) {
+      for (int d = 0; d < dim; ++d) v[(size_t)(q * (dim + 1) + d)] = X[(size_t)(q * dim + d)];
+      v[(size_t)(q * (dim + 1) + dim)] = t;
+    }
+    out.resize((size_t)n * nc);
+    ck(gls_expr_eval(e, n, v.data(), out.data()), "gls_expr_eval");
+  }
+};
+
+enum class Method { steady, bdf1, bdf2, bdf3, sdirk2, sdirk3 };
+
+struct BC {
+  std::string type;
+  int id = 0, periodic_direction = 0;
+  Function f[3];
+};
+
+struct Params {
+  int dim = 3;
+  Method method = Method::steady;
+  double dt = 1.0, t_end = 1.0, startup = 0.4;
+  int mesh_adapt = 0, output_frequency = 1, subdivision = 1, log_frequency = 1;
+  std::string output_path = "./", output_name = "out";
+  double nu = 1.0;
+  int k = 1, kp = 1;
+  double lo = -1, hi = 1;
+  bool colorize = false;
+  int refinement = 0;
+  std::vector<BC> bcs;
+  bool source = false;
+  Function force;
+  std::string ic_type = "nodal";
+  Function ic;
+  double ic_nu = 1.0;
+  bool analytical = false, analytical_verbose = false;
+  std::string analytical_file = "L2Error";
+  Function exact;
+  bool enstrophy = false, kinetic = false, pp_verbose = false;
+  double newton_tol = 1e-6;
+  int newton_max = 10, newton_verbose = 0, lin_max = 1000, restart = 30;
+  double lin_rel = 1e-3, lin_min = 1e-8;
+  bool srf = false;
+  double omega[3] = {0, 0, 0};
+};
+
+Method parse_method(const std::string &s) {
+  const char *names[] = {"steady", "bdf1", "bdf2", "bdf3", "sdirk2", "sdirk3"};
+  for (int i = 0; i < 6; ++i)
+    if (s == names[i]) return (Method)i;
+  die("unknown time stepping method '%s'", s.c_str());
+}
+
+Params read_params(const Prm &p, int dim) {
+  Params P;
+  P.dim = dim;
+  const std::string sc = "simulation control/";
+  P.method = parse_method(p.get(sc + "method", "steady"));
+  P.dt = p.d(sc + "time step", 1.0);
+  P.t_end = p.d(sc + "time end", 1.0);
+  P.startup = p.d(sc + "startup time scaling", 0.4);
+  P.mesh_adapt = p.i(sc + "number mesh adapt", 0);
+  P.output_frequency = p.i(sc + "output frequency", 1);
+  P.log_frequency = p.i(sc + "log frequency", 1);
+  P.subdivision = p.i(sc + "subdivision", 1);
+  P.output_path = p.get(sc + "output path", "./");
+  P.output_name = p.get(sc + "output name", "out");
+  if (p.b(sc + "adapt", false)) die("adaptive time stepping is not supported");
+  P.nu = p.d("physical properties/kinematic viscosity", 1.0);
+  P.k = p.i("FEM/velocity order", 1);
+  P.kp = p.i("FEM/pressure order", 1);
+  if (p.get("mesh/type", "dealii") != "dealii") die("mesh type '%s' is not supported", p.get("mesh/type", "").c_str());
+  const std::string gt = p.get("mesh/grid type", "hyper_cube");
+  if (gt != "hyper_cube") die("grid type '%s' is not supported (hyper_cube only)", gt.c_str());
+  {
+    const std::string a = p.get("mesh/grid arguments", "-1 : 1 : false");
+    std::vector<std::string> parts;
+    std::stringstream ss(a);
+    std::string tok;
+    while (std::getline(ss, tok, ':')) parts.push_back(trim(tok));
+    if (parts.size() != 3) die("grid arguments '%s': expected 'lo : hi : colorize'", a.c_str());
+    P.lo = std::atof(parts[0].c_str());
+    P.hi = std::atof(parts[1].c_str());
+    P.colorize = parts[2] == "true";
+  }
+  P.refinement = p.i("mesh/initial refinement", 0);
+  const std::string madapt = p.get("mesh adaptation/type", "none");
+  if (P.method == Method::steady && P.mesh_adapt > 0 && madapt != "uniform")
+    die("mesh adaptation type '%s' is not supported (uniform only)", madapt.c_str());
+  const int nbc = p.i("boundary conditions/number", 0);
+  for (int i = 0; i < nbc; ++i) {
+    const std::string s = "boundary conditions/bc " + std::to_string(i) + "/";
+    BC b;
+    b.type = p.get(s + "type", "noslip");
+    b.id = p.i(s + "id", i);
+    b.periodic_direction = p.i(s + "periodic_direction", 0);
+    if (b.type == "function") {
+      const char *nm[3] = {"u", "v", "w"};
+      for (int c = 0; c < dim; ++c) b.f[c] = Function(p, s + nm[c], dim, "0");
+    } else if (b.type == "slip") {
+      die("bc %d: slip boundary conditions are not supported yet", i);
+    } else if (b.type != "noslip" && b.type != "periodic") {
+      die("bc %d: unknown type '%s'", i, b.type.c_str());
+    }
+    P.bcs.push_back(std::move(b));
+  }
+  const std::string zeros = dim == 3 ? "0; 0; 0; 0" : "0; 0; 0";
+  P.source = p.b("source term/enable", false);
+  if (P.source) P.force = Function(p, "source term/xyz", dim, zeros);
+  P.ic_type = p.get("initial conditions/type", "nodal");
+  P.ic = Function(p, "initial conditions/uvwp", dim, zeros);
+  P.ic_nu = p.d("initial conditions/viscosity", 1.0);
+  P.analytical = p.b("analytical solution/enable", false);
+  P.analytical_verbose = p.get("analytical solution/verbosity", "quiet") == "verbose";
+  P.analytical_file = p.get("analytical solution/filename", "L2Error");
+  if (P.analytical) P.exact = Function(p, "analytical solution/uvwp", dim, zeros);
+  P.enstrophy = p.b("post-processing/calculate enstrophy", false);
+  P.kinetic = p.b("post-processing/calculate kinetic energy", false);
+  P.pp_verbose = p.get("post-processing/verbosity", "quiet") == "verbose";
+  P.newton_tol = p.d("non-linear solver/tolerance", 1e-6);
+  P.newton_max = p.i("non-linear solver/max iterations", 10);
+  P.newton_verbose = p.get("non-linear solver/verbosity", "verbose") == "verbose" ? 1 : 0;
+  P.lin_max = p.i("linear solver/max iters", 1000);
+  P.lin_rel = p.d("linear solver/relative residual", 1e-3);
+  P.lin_min = p.d("linear solver/minimum residual", 1e-8);
+  P.srf = p.get("velocity source/type", "none") == "srf";
+  P.omega[0] = p.d("velocity source/omega_x", 0.);
+  P.omega[1] = p.d("velocity source/omega_y", 0.);
+  P.omega[2] = p.d("velocity source/omega_z", 0.);
+  return P;
+}
+
+// ---------------------------------------------------------------------------------------------
+// mesh and constraints
+// ---------------------------------------------------------------------------------------------
+struct Mesh {
+  int dim = 3, n = 1, k = 1, kp = 1, pmask = 0;
+  double lo = 0, hi = 1, hc = 1;
+  int64_t nc = 0, nv = 0, np = 0;
+  int vsh[3] = {1, 1, 1}, psh[3] = {1, 1, 1};  // lattice nodes per direction (periodic: wrapped)
+  std::vector<int32_t> cv, cp;
+  std::vector<double> x0, h;
+  int64_t n_dofs() const { return (int64_t)dim * nv + np; }
+  void coord(int64_t node, bool vel, double *x, int *idx) const {
+    const int *sh = vel ? vsh : psh;
+    const int deg = vel ? k : kp;
+    for (int d = 0; d < dim; ++d) {
+      idx[d] = (int)(node % sh[d]);
+      node /= sh[d];
+      x[d] = lo + idx[d] * hc / deg;
+    }
+  }
+};
+
+Mesh build_mesh(const Params &P, int n, int pmask) {
+  Mesh m;
+  m.dim = P.dim;
+  m.n = n;
+  m.k = P.k;
+  m.kp = P.kp;
+  m.pmask = pmask;
+  m.lo = P.lo;
+  m.hi = P.hi;
+  m.hc = (P.hi - P.lo) / n;
+  ck(gls_mesh_hyper_cube_sizes(P.dim, n, P.k, P.kp, pmask, &m.nc, &m.nv, &m.np), "gls_mesh_hyper_cube_sizes");
+  int nvl = 1, npl = 1;
+  for (int d = 0; d < P.dim; ++d) {
+    nvl *= P.k + 1;
+    npl *= P.kp + 1;
+  }
+  for (int d = 0; d < 3; ++d) {
+    const bool per = (pmask >> d) & 1;
+    m.vsh[d] = P.k * n + (per ? 0 : 1);
+    m.psh[d] = P.kp * n + (per ? 0 : 1);
+  }
+  m.cv.resize((size_t)(m.nc * nvl));
+  m.cp.resize((size_t)(m.nc * npl));
+  m.x0.resize((size_t)(m.nc * P.dim));
+  m.h.resize((size_t)(m.nc * P.dim));
+  ck(gls_mesh_hyper_cube(P.dim, n, P.k, P.kp, P.lo, P.hi, pmask, m.cv.data(), m.cp.data(), m.x0.data(), m.h.data()),
+     "gls_mesh_hyper_cube");
+  return m;
+}
+
+// boundary ids of a lattice node (hyper_cube: colorize -> faces 2d / 2d+1, else all id 0)
+unsigned face_bits(const Mesh &m, const int *idx, bool colorize) {
+  unsigned b = 0;
+  for (int d = 0; d < m.dim; ++d) {
+    if ((m.pmask >> d) & 1) continue;
+    if (idx[d] == 0) b |= 1u << (colorize ? 2 * d : 0);
+    if (idx[d] == m.vsh[d] - 1) b |= 1u << (colorize ? 2 * d + 1 : 0);
+  }
+  return b;
+}
+
+struct Constraints {
+  std::vector<uint8_t> mask;  // per velocity node, bit c = component c constrained
+  std::vector<int64_t> dofs;
+  std::vector<double> vals;
+};
+
+// Dirichlet data of the noslip / function boundary conditions at the velocity support points;
+// a component already set by an earlier bc keeps its value (deal.II's first-constraint rule)
+Constraints make_constraints(const Params &P, const Mesh &m, double t) {
+  Constraints C;
+  C.mask.assign((size_t)m.nv, 0);
+  std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
+  for (const BC &b : P.bcs) {
+    if (b.type == "periodic") continue;
+    std::vector<int64_t> sel;
+    std::vector<double> X;
+    for (int64_t v = 0; v < m.nv; ++v) {
+      double x[3];
+      int idx[3];
+      m.coord(v, true, x, idx);
+      if (face_bits(m, idx, P.colorize) & (1u << b.id)) {
+        sel.push_back(v);
+        X.insert(X.end(), x, x + m.dim);
+      }
+    }
+    std::vector<double> fv[3];
+    if (b.type == "function")
+      for (int c = 0; c < m.dim; ++c) b.f[c].eval(X, m.dim, t, fv[c]);
+    for (size_t s = 0; s < sel.size(); ++s)
+      for (int c = 0; c < m.dim; ++c) {
+        uint8_t &mk = C.mask[(size_t)sel[s]];
+        if (mk & (1u << c)) continue;
+        mk |= (uint8_t)(1u << c);
+        val[(size_t)(sel[s] * m.dim + c)] = b.type == "function" ? fv[c][s * (size_t)b.f[c].nc] : 0.0;
+      }
+  }
+  for (int64_t v = 0; v < m.nv; ++v)
+    for (int c = 0; c < m.dim; ++c)
+      if (C.mask[(size_t)v] & (1u << c)) {
+        C.dofs.push_back(v * m.dim + c);
+        C.vals.push_back(val[(size_t)(v * m.dim + c)]);
+      }
+  return C;
+}
+
+// ---------------------------------------------------------------------------------------------
+// host quadrature for post-processing: Gauss points on [0,1], Lagrange on Gauss-Lobatto nodes
+// ---------------------------------------------------------------------------------------------
+void gauss01(int n, std::vector<double> &x, std::vector<double> &w) {
+  x.assign((size_t)n, 0.);
+  w.assign((size_t)n, 0.);
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), dp = 1;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1, p1 = 0;
+      for (int j = 1; j <= n; ++j) {
+        const double p2 = p1;
+        p1 = p0;
+        p0 = ((2 * j - 1) * z * p1 - (j - 1) * p2) / j;
+      }
+      dp = n * (z * p0 - p1) / (z * z - 1);
+      const double dz = p0 / dp;
+      z -= dz;
+      if (std::fabs(dz) < 1e-16) break;
+    }
+    x[(size_t)(n - 1 - i)] = 0.5 * (z + 1);
+    w[(size_t)(n - 1 - i)] = 1.0 / ((1 - z * z) * dp * dp);
+  }
+}
+std::vector<double> lobatto01(int k) {
+  if (k == 1) return {0., 1.};
+  if (k == 2) return {0., .5, 1.};
+  const double a = 0.5 * (1.0 - 1.0 / std::sqrt(5.0));
+  return {0., a, 1. - a, 1.};
+}
+void lag1d(const std::vector<double> &xn, double x, double *v, double *dv) {
+  const int n = (int)xn.size();
+  for (int a = 0; a < n; ++a) {
+    double val = 1, der = 0;
+    for (int b = 0; b < n; ++b) {
+      if (b == a) continue;
+      const double f = (x - xn[(size_t)b]) / (xn[(size_t)a] - xn[(size_t)b]);
+      der = der * f + val / (xn[(size_t)a] - xn[(size_t)b]);
+      val *= f;
+    }
+    v[a] = val;
+    dv[a] = der;
+  }
+}
+
+// FE solution (velocity, gradient, pressure) at the tensor-product Gauss points of every cell
+struct CellEval {
+  const Mesh &m;
+  int nq1, nq, nvl, npl;
+  std::vector<double> xq, wq, Vv, Dv, Vp;  // 1D tables [q][node]
+  CellEval(const Mesh &m_, int nq1d) : m(m_), nq1(nq1d) {
+    gauss01(nq1, xq, wq);
+    const std::vector<double> xv = lobatto01(m.k), xp = lobatto01(m.kp);
+    const int k1 = m.k + 1, kp1 = m.kp + 1;
+    Vv.resize((size_t)(nq1 * k1));
+    Dv.resize((size_t)(nq1 * k1));
+    Vp.resize((size_t)(nq1 * kp1));
+    std::vector<double> tmp((size_t)kp1);
+    for (int q = 0; q < nq1; ++q) {
+      lag1d(xv, xq[(size_t)q], &Vv[(size_t)(q * k1)], &Dv[(size_t)(q * k1)]);
+      lag1d(xp, xq[(size_t)q], &Vp[(size_t)(q * kp1)], tmp.data());
+    }
+    nq = m.dim == 3 ? nq1 * nq1 * nq1 : nq1 * nq1;
+    nvl = m.dim == 3 ? k1 * k1 * k1 : k1 * k1;
+    npl = m.dim == 3 ? kp1 * kp1 * kp1 : kp1 * kp1;
+  }
+  void qidx(int q, int *qq) const {
+    qq[0] = q % nq1;
+    qq[1] = (q / nq1) % nq1;
+    qq[2] = m.dim == 3 ? q / (nq1 * nq1) : 0;
+  }
+  void point(int64_t c, int q, double *x, double &JxW) const {
+    int qq[3];
+    qidx(q, qq);
+    JxW = 1;
+    for (int d = 0; d < m.dim; ++d) {
+      const double hd = m.h[(size_t)(c * m.dim + d)];
+      x[d] = m.x0[(size_t)(c * m.dim + d)] + hd * xq[(size_t)qq[d]];
+      JxW *= hd * wq[(size_t)qq[d]];
+    }
+  }
+  double phi_v(int a, const int *qq) const {
+    const int k1 = m.k + 1, a0 = a % k1, a1 = (a / k1) % k1, a2 = m.dim == 3 ? a / (k1 * k1) : 0;
+    return Vv[(size_t)(qq[0] * k1 + a0)] * Vv[(size_t)(qq[1] * k1 + a1)] * (m.dim == 3 ? Vv[(size_t)(qq[2] * k1 + a2)] : 1.);
+  }
+  double phi_p(int a, const int *qq) const {
+    const int k1 = m.kp + 1, a0 = a % k1, a1 = (a / k1) % k1, a2 = m.dim == 3 ? a / (k1 * k1) : 0;
+    return Vp[(size_t)(qq[0] * k1 + a0)] * Vp[(size_t)(qq[1] * k1 + a1)] * (m.dim == 3 ? Vp[(size_t)(qq[2] * k1 + a2)] : 1.);
+  }
+  void at(const double *sol, int64_t c, int q, double *u, double G[3][3], double &p) const {
+    const int dim = m.dim, k1 = m.k + 1;
+    int qq[3];
+    qidx(q, qq);
+    const double *hh = &m.h[(size_t)(c * dim)];
+    for (int d = 0; d < 3; ++d) {
+      u[d] = 0;
+      for (int e = 0; e < 3; ++e) G[d][e] = 0;
+    }
+    p = 0;
+    const int32_t *cv = &m.cv[(size_t)(c * nvl)];
+    for (int a = 0; a < nvl; ++a) {
+      const int a0 = a % k1, a1 = (a / k1) % k1, a2 = dim == 3 ? a / (k1 * k1) : 0;
+      const double b0 = Vv[(size_t)(qq[0] * k1 + a0)], b1 = Vv[(size_t)(qq[1] * k1 + a1)];
+      const double b2 = dim == 3 ? Vv[(size_t)(qq[2] * k1 + a2)] : 1.0;
+      const double g[3] = {Dv[(size_t)(qq[0] * k1 + a0)] * b1 * b2 / hh[0], b0 * Dv[(size_t)(qq[1] * k1 + a1)] * b2 / hh[1],
+                           dim == 3 ? b0 * b1 * Dv[(size_t)(qq[2] * k1 + a2)] / hh[2] : 0.0};
+      for (int d = 0; d < dim; ++d) {
+        const double ud = sol[(size_t)cv[a] * dim + d];
+        u[d] += ud * b0 * b1 * b2;
+        for (int e = 0; e < dim; ++e) G[d][e] += ud * g[e];
+      }
+    }
+    const int32_t *cp = &m.cp[(size_t)(c * npl)];
+    const int64_t voff = (int64_t)dim * m.nv;
+    for (int a = 0; a < npl; ++a) p += sol[(size_t)(voff + cp[a])] * phi_p(a, qq);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// the solver
+// ---------------------------------------------------------------------------------------------
+struct Solver {
+  Params &P;
+  bool use_mg;
+  Mesh m;
+  Constraints C;
+  gls_ctx *ctx = nullptr;
+  std::vector<gls_ctx *> mg_levels;
+  double *d_present = nullptr, *d_m1 = nullptr, *d_m2 = nullptr, *d_m3 = nullptr;
+  std::vector<double> present, m1, m2, m3;
+  int step = 0;
+  double time = 0.0, dt_now = 0.0, cfl = 0.0;
+  double dts[4] = {0, 0, 0, 0};  // time steps, most recent first (BDF coefficients)
+  int newton_its = 0, linear_its = 0;
+  std::vector<std::vector<double>> errors;  // steady: cells, e_u, e_p ; transient: t, e_u
+  std::vector<std::pair<double, std::string>> pvd;
+
+  Solver(Params &p, bool mg) : P(p), use_mg(mg) {}
+  ~Solver() { release(); }
+
+  void release() {
+    for (gls_ctx *g : mg_levels) gls_destroy(g);
+    mg_levels.clear();
+    if (ctx) gls_destroy(ctx);
+    ctx = nullptr;
+    for (double *q : {d_present, d_m1, d_m2, d_m3})
+      if (q) (void)hipFree(q);
+    d_present = d_m1 = d_m2 = d_m3 = nullptr;
+  }
+
+  int periodic_mask() const {
+    int pm = 0;
+    for (const BC &b : P.bcs)
+      if (b.type == "periodic") pm |= 1 << b.periodic_direction;
+    return pm;
+  }
+
+  gls_ctx *make_context(const Mesh &mm, const Constraints &cc) {
+    std::vector<double> fq;
+    if (P.source) {  // source term at the quadrature points QGauss(k+1)
+      CellEval ev(mm, mm.k + 1);
+      std::vector<double> X, F;
+      X.reserve((size_t)(mm.nc * ev.nq * mm.dim));
+      for (int64_t c = 0; c < mm.nc; ++c)
+        for (int q = 0; q < ev.nq; ++q) {
+          double x[3], w;
+          ev.point(c, q, x, w);
+          X.insert(X.end(), x, x + mm.dim);
+        }
+      P.force.eval(X, mm.dim, time, F);
+      fq.resize(X.size());
+      for (size_t i = 0; i < fq.size() / mm.dim; ++i)
+        for (int d = 0; d < mm.dim; ++d) fq[i * mm.dim + d] = F[i * (size_t)P.force.nc + d];
+    }
+    gls_mesh_desc D;
+    std::memset(&D, 0, sizeof(D));
+    D.dim = mm.dim;
+    D.k = mm.k;
+    D.kp = mm.kp;
+    D.n_cells = (int)mm.nc;
+    D.n_vnodes = (int)mm.nv;
+    D.n_pnodes = (int)mm.np;
+    D.cell_vnodes = mm.cv.data();
+    D.cell_pnodes = (mm.kp == mm.k) ? nullptr : mm.cp.data();
+    D.cell_x0 = mm.x0.data();
+    D.cell_h = mm.h.data();
+    D.vnode_mask = cc.mask.data();
+    D.viscosity = P.nu;
+    D.srf = P.srf ? 1 : 0;
+    for (int i = 0; i < 3; ++i) D.omega[i] = P.omega[i];
+    D.force_q = P.source ? fq.data() : nullptr;
+    gls_ctx *g = nullptr;
+    ck(gls_create(&D, &g), "gls_create");
+    ck(gls_set_dirichlet(g, (int64_t)cc.dofs.size(), cc.dofs.data(), cc.vals.data()), "gls_set_dirichlet");
+    return g;
+  }
+
+  void setup(int n) {
+    release();
+    m = build_mesh(P, n, periodic_mask());
+    C = make_constraints(P, m, time);
+    ctx = make_context(m, C);
+    const int64_t N = m.n_dofs();
+    for (double **q : {&d_present, &d_m1, &d_m2, &d_m3}) {
+      hk(hipMalloc(q, sizeof(double) * (size_t)N), "hipMalloc");
+      hk(hipMemset(*q, 0, sizeof(double) * (size_t)N), "hipMemset");
+    }
+    present.assign((size_t)N, 0.);
+    m1 = m2 = m3 = present;
+    // geometric multigrid on nested hyper_cubes (3D, k == kp <= 2, no periodicity)
+    if (use_mg && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && n >= 8 && (n & (n - 1)) == 0) {
+      std::vector<gls_ctx *> lv{ctx};
+      for (int c = n / 2; c >= 4; c /= 2) {
+        const Mesh mc = build_mesh(P, c, 0);
+        const Constraints cc = make_constraints(P, mc, time);
+        gls_ctx *g = make_context(mc, cc);
+        mg_levels.push_back(g);
+        lv.push_back(g);
+      }
+      gls_mg_params mp;
+      std::memset(&mp, 0, sizeof(mp));
+      mp.n_levels = (int)lv.size();
+      mp.levels = lv.data();
+      mp.pre_smooth = 1;
+      mp.post_smooth = 1;
+      mp.coarse_sweeps = 30;
+      mp.omega = 0.7;
+      ck(gls_mg_attach(ctx, &mp), "gls_mg_attach");
+    }
+    std::printf("mesh: cells = %lld, dofs = %lld, levels = %d\n", (long long)m.nc, (long long)N,
+                1 + (int)mg_levels.size());
+  }
+
+  void upload(const std::vector<double> &h, double *d) {
+    hk(hipMemcpy(d, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice), "upload");
+  }
+  void download(const double *d, std::vector<double> &h) {
+    hk(hipMemcpy(h.data(), d, sizeof(double) * h.size(), hipMemcpyDeviceToHost), "download");
+  }
+
+  // ---- initial conditions
+  void nodal_values(const Function &f, std::vector<double> &x) {  // interpolation + Dirichlet values
+    for (int part = 0; part < 2; ++part) {
+      const bool vel = part == 0;
+      const int64_t nn = vel ? m.nv : m.np;
+      std::vector<double> X, F;
+      for (int64_t v = 0; v < nn; ++v) {
+        double c[3];
+        int idx[3];
+        m.coord(v, vel, c, idx);
+        X.insert(X.end(), c, c + m.dim);
+      }
+      f.eval(X, m.dim, time, F);
+      for (int64_t v = 0; v < nn; ++v) {
+        if (vel)
+          for (int d = 0; d < m.dim; ++d) x[(size_t)(v * m.dim + d)] = F[(size_t)(v * f.nc + d)];
+        else
+          x[(size_t)(m.dim * m.nv + v)] = F[(size_t)(v * f.nc + m.dim)];
+      }
+    }
+    for (size_t i = 0; i < C.dofs.size(); ++i) x[(size_t)C.dofs[i]] = C.vals[i];
+  }
+
+  // L2 projection of uvwp onto the velocity-pressure space: consistent mass matrix (block diagonal
+  // per component), host conjugate gradients to 1e-15 relative; Dirichlet rows keep their values
+  void l2_projection(const Function &f, std::vector<double> &x) {
+    const int nq1 = m.k + 1, dim = m.dim;
+    CellEval ev(m, nq1);
+    const int64_t N = m.n_dofs(), voff = (int64_t)dim * m.nv;
+    std::vector<double> X, F, rhs((size_t)N, 0.0), wq((size_t)(m.nc * ev.nq));
+    for (int64_t c = 0; c < m.nc; ++c)
+      for (int q = 0; q < ev.nq; ++q) {
+        double xx[3], w;
+        ev.point(c, q, xx, w);
+        wq[(size_t)(c * ev.nq + q)] = w;
+        X.insert(X.end(), xx, xx + dim);
+      }
+    f.eval(X, dim, time, F);
+    for (int64_t c = 0; c < m.nc; ++c)
+      for (int q = 0; q < ev.nq; ++q) {
+        int qq[3];
+        ev.qidx(q, qq);
+        const double w = wq[(size_t)(c * ev.nq + q)];
+        const double *fv = &F[(size_t)((c * ev.nq + q) * f.nc)];
+        for (int a = 0; a < ev.nvl; ++a) {
+          const double ph = ev.phi_v(a, qq) * w;
+          for (int d = 0; d < dim; ++d) rhs[(size_t)(m.cv[(size_t)(c * ev.nvl + a)] * dim + d)] += ph * fv[d];
+        }
+        for (int a = 0; a < ev.npl; ++a) rhs[(size_t)(voff + m.cp[(size_t)(c * ev.npl + a)])] += ev.phi_p(a, qq) * w * fv[dim];
+      }
+    std::vector<char> fixed((size_t)N, 0);
+    for (size_t i = 0; i < C.dofs.size(); ++i) fixed[(size_t)C.dofs[i]] = 1;
+    auto mass = [&](const std::vector<double> &in, std::vector<double> &out) {
+      std::fill(out.begin(), out.end(), 0.0);
+      for (int64_t c = 0; c < m.nc; ++c)
+        for (int q = 0; q < ev.nq; ++q) {
+          int qq[3];
+          ev.qidx(q, qq);
+          const double w = wq[(size_t)(c * ev.nq + q)];
+          double uq[3] = {0, 0, 0}, pq = 0;
+          for (int a = 0; a < ev.nvl; ++a) {
+            const double ph = ev.phi_v(a, qq);
+            for (int d = 0; d < dim; ++d) uq[d] += ph * in[(size_t)(m.cv[(size_t)(c * ev.nvl + a)] * dim + d)];
+          }
+          for (int a = 0; a < ev.npl; ++a) pq += ev.phi_p(a, qq) * in[(size_t)(voff + m.cp[(size_t)(c * ev.npl + a)])];
+          for (int a = 0; a < ev.nvl; ++a) {
+            const double ph = ev.phi_v(a, qq) * w;
+            for (int d = 0; d < dim; ++d) out[(size_t)(m.cv[(size_t)(c * ev.nvl + a)] * dim + d)] += ph * uq[d];
+          }
+          for (int a = 0; a < ev.npl; ++a) out[(size_t)(voff + m.cp[(size_t)(c * ev.npl + a)])] += ev.phi_p(a, qq) * w * pq;
+        }
+    };
+    std::fill(x.begin(), x.end(), 0.0);
+    for (size_t i = 0; i < C.dofs.size(); ++i) x[(size_t)C.dofs[i]] = C.vals[i];
+    std::vector<double> r((size_t)N), pd((size_t)N), Ap((size_t)N);
+    mass(x, Ap);
+    double rr = 0, bb = 0;
+    for (int64_t i = 0; i < N; ++i) {
+      r[(size_t)i] = fixed[(size_t)i] ? 0.0 : rhs[(size_t)i] - Ap[(size_t)i];
+      rr += r[(size_t)i] * r[(size_t)i];
+      bb += rhs[(size_t)i] * rhs[(size_t)i];
+    }
+    pd = r;
+    for (int it = 0; it < 10000 && rr > 1e-30 * std::max(bb, 1e-300); ++it) {
+      mass(pd, Ap);
+      double pAp = 0;
+      for (int64_t i = 0; i < N; ++i) {
+        if (fixed[(size_t)i]) Ap[(size_t)i] = 0.0;
+        pAp += pd[(size_t)i] * Ap[(size_t)i];
+      }
+      const double alpha = rr / pAp;
+      double rr2 = 0;
+      for (int64_t i = 0; i < N; ++i) {
+        x[(size_t)i] += alpha * pd[(size_t)i];
+        r[(size_t)i] -= alpha * Ap[(size_t)i];
+        rr2 += r[(size_t)i] * r[(size_t)i];
+      }
+      const double beta = rr2 / rr;
+      rr = rr2;
+      for (int64_t i = 0; i < N; ++i) pd[(size_t)i] = r[(size_t)i] + beta * pd[(size_t)i];
+    }
+  }
+
+  // ---- one nonlinear solve of `scheme` from the current present solution and history
+  void solve_nonlinear(int scheme, double nu_override = -1.0) {
+    double ts[4];
+    for (int i = 0; i < 4; ++i) ts[i] = dts[i] > 0 ? dts[i] : 1.0;
+    ck(gls_set_time(ctx, scheme, ts), "gls_set_time");
+    if (nu_override > 0) ck(gls_set_viscosity(ctx, nu_override), "gls_set_viscosity");
+    upload(present, d_present);
+    upload(m1, d_m1);
+    upload(m2, d_m2);
+    upload(m3, d_m3);
+    ck(gls_apply_dirichlet(ctx, d_present), "gls_apply_dirichlet");
+    gls_newton_params np;
+    std::memset(&np, 0, sizeof(np));
+    np.tolerance = P.newton_tol;
+    np.max_iterations = P.newton_max;
+    np.verbosity = P.newton_verbose;
+    np.lin.max_iterations = P.lin_max;
+    np.lin.restart = P.restart;
+    np.lin.relative_residual = P.lin_rel;
+    np.lin.minimum_residual = P.lin_min;
+    ck(gls_newton_solve(ctx, d_present, d_m1, d_m2, d_m3, &np), "gls_newton_solve");
+    download(d_present, present);
+    newton_its += np.newton_iterations;
+    linear_its += np.linear_iterations;
+    if (nu_override > 0) ck(gls_set_viscosity(ctx, P.nu), "gls_set_viscosity");
+  }
+  void push_dt(double dt) {  // the newest step first, older ones shifted
+    for (int i = 3; i > 0; --i) dts[i] = dts[i - 1];
+    dts[0] = dt;
+    dt_now = dt;
+  }
+
+  // one time step with the scheme's stages (SDIRK stage results become m2 / m3)
+  void advance() {
+    if (P.method == Method::sdirk2) {
+      solve_nonlinear(GLS_SDIRK2_1);
+      m2 = present;
+      solve_nonlinear(GLS_SDIRK2_2);
+    } else if (P.method == Method::sdirk3) {
+      solve_nonlinear(GLS_SDIRK3_1);
+      m2 = present;
+      solve_nonlinear(GLS_SDIRK3_2);
+      m3 = present;
+      solve_nonlinear(GLS_SDIRK3_3);
+    } else {
+      const int sch[] = {GLS_STEADY, GLS_BDF1, GLS_BDF2, GLS_BDF3};
+      solve_nonlinear(sch[(int)P.method]);
+    }
+  }
+  // first step of BDF2 / BDF3: Euler sub-steps of `startup`*dt, then the high-order step
+  // completing dt (navier_stokes_base.cc:507-586)
+  void first_step() {
+    if (P.method != Method::bdf2 && P.method != Method::bdf3) {
+      advance();
+      return;
+    }
+    const double dt = P.dt, s = P.startup;
+    push_dt(dt * s);
+    solve_nonlinear(GLS_BDF1);
+    m2 = m1;
+    m1 = present;
+    if (P.method == Method::bdf2) {
+      push_dt(dt * (1. - s));
+      solve_nonlinear(GLS_BDF2);
+    } else {
+      push_dt(dt * s);
+      solve_nonlinear(GLS_BDF1);
+      m3 = m2;
+      m2 = m1;
+      m1 = present;
+      push_dt(dt * (1. - 2. * s));
+      solve_nonlinear(GLS_BDF3);
+    }
+    dt_now = dt;
+  }
+
+  // ---- post-processing
+  std::pair<double, double> l2_error() {  // QGauss(k+2), pressures compared mean-free
+    CellEval ev(m, m.k + 2);
+    std::vector<double> X, E;
+    for (int64_t c = 0; c < m.nc; ++c)
+      for (int q = 0; q < ev.nq; ++q) {
+        double x[3], w;
+        ev.point(c, q, x, w);
+        X.insert(X.end(), x, x + m.dim);
+      }
+    P.exact.eval(X, m.dim, time, E);
+    const int ne = P.exact.nc;
+    double pint = 0, peint = 0, vol = 0, eu = 0, ep = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      int64_t idx = 0;
+      for (int64_t c = 0; c < m.nc; ++c)
+        for (int q = 0; q < ev.nq; ++q, ++idx) {
+          double x[3], JxW, u[3], G[3][3], p;
+          ev.point(c, q, x, JxW);
+          ev.at(present.data(), c, q, u, G, p);
+          const double *ex = &E[(size_t)(idx * ne)];
+          const double pe = ne > m.dim ? ex[m.dim] : 0.0;
+          if (pass == 0) {
+            pint += p * JxW;
+            peint += pe * JxW;
+            vol += JxW;
+          } else {
+            for (int d = 0; d < m.dim; ++d) eu += (u[d] - ex[d]) * (u[d] - ex[d]) * JxW;
+            const double dp = (p - pint / vol) - (pe - peint / vol);
+            ep += dp * dp * JxW;
+          }
+        }
+    }
+    return {std::sqrt(eu), std::sqrt(ep)};
+  }
+  // volume averages with QGauss(k+1): 0.5|curl u|^2 (enstrophy) or 0.5|u|^2 (kinetic energy)
+  double volume_average(bool enstrophy) {
+    CellEval ev(m, std::max(m.k, m.kp) + 1);
+    double s = 0, vol = 0;
+    for (int64_t c = 0; c < m.nc; ++c)
+      for (int q = 0; q < ev.nq; ++q) {
+        double x[3], JxW, u[3], G[3][3], p;
+        ev.point(c, q, x, JxW);
+        ev.at(present.data(), c, q, u, G, p);
+        vol += JxW;
+        if (enstrophy) {
+          const double wz = G[1][0] - G[0][1];
+          s += 0.5 * wz * wz * JxW;
+          if (m.dim == 3) {
+            const double wx = G[2][1] - G[1][2], wy = G[0][2] - G[2][0];
+            s += 0.5 * (wx * wx + wy * wy) * JxW;
+          }
+        } else {
+          for (int d = 0; d < m.dim; ++d) s += 0.5 * u[d] * u[d] * JxW;
+        }
+      }
+    return s / vol;
+  }
+  // CFL from the velocity at the cell centre and h = (6|K|/pi)^(1/3)/k (3D), sqrt(4|K|/pi)/k (2D)
+  double compute_cfl(double dt) {
+    CellEval ev(m, 1);
+    const int deg = std::max(m.k, m.kp);
+    double cmax = 0;
+    for (int64_t c = 0; c < m.nc; ++c) {
+      double u[3], G[3][3], p, meas = 1;
+      ev.at(present.data(), c, 0, u, G, p);
+      for (int d = 0; d < m.dim; ++d) meas *= m.h[(size_t)(c * m.dim + d)];
+      const double hh = m.dim == 2 ? std::sqrt(4. * meas / M_PI) / deg : std::cbrt(6. * meas / M_PI) / deg;
+      double un = 0;
+      for (int d = 0; d < m.dim; ++d) un += u[d] * u[d];
+      cmax = std::max(cmax, std::sqrt(un) / hh * dt);
+    }
+    return cmax;
+  }
+  void write_output() {
+    char tag[32];
+    std::snprintf(tag, sizeof(tag), ".%05d", step);
+    const std::string stem = P.output_name + tag, piece = stem + ".00000.vtu", master = stem + ".pvtu";
+    gls_mesh_desc D;
+    std::memset(&D, 0, sizeof(D));
+    D.dim = m.dim;
+    D.k = m.k;
+    D.kp = m.kp;
+    D.n_cells = (int)m.nc;
+    D.n_vnodes = (int)m.nv;
+    D.n_pnodes = (int)m.np;
+    D.cell_vnodes = m.cv.data();
+    D.cell_pnodes = m.cp.data();
+    D.cell_x0 = m.x0.data();
+    D.cell_h = m.h.data();
+    D.srf = P.srf ? 1 : 0;
+    for (int i = 0; i < 3; ++i) D.omega[i] = P.omega[i];
+    ck(gls_vtu_write((P.output_path + piece).c_str(), &D, present.data(), P.subdivision, 0, 1), "gls_vtu_write");
+    const char *pc[1] = {piece.c_str()};
+    ck(gls_pvtu_write((P.output_path + master).c_str(), m.dim, P.srf ? 1 : 0, 1, pc), "gls_pvtu_write");
+    pvd.emplace_back(time, master);
+    std::vector<double> tt;
+    std::vector<const char *> ff;
+    for (auto &e : pvd) {
+      tt.push_back(e.first);
+      ff.push_back(e.second.c_str());
+    }
+    ck(gls_pvd_write((P.output_path + P.output_name + ".pvd").c_str(), (int)pvd.size(), tt.data(), ff.data()),
+       "gls_pvd_write");
+  }
+  void postprocess(bool initial) {
+    if (P.output_frequency > 0 && step % P.output_frequency == 0) write_output();
+    if (P.enstrophy && P.pp_verbose) std::printf("enstrophy = %.10g\n", volume_average(true));
+    if (P.kinetic && P.pp_verbose) std::printf("kinetic_energy = %.10g\n", volume_average(false));
+    if (!initial && P.analytical) {
+      const auto e = l2_error();
+      if (P.method == Method::steady) errors.push_back({(double)m.nc, e.first, e.second});
+      else errors.push_back({time, e.first});
+      if (P.analytical_verbose) std::printf("l2_error_velocity = %.10g\n", e.first);
+    }
+  }
+  void end_of_step() {  // history shift + CFL of the step just taken
+    if (P.method == Method::steady) return;
+    m3 = m2;
+    m2 = m1;
+    m1 = present;
+    cfl = compute_cfl(dt_now);
+  }
+  // uniform refinement with interpolation of the Qk fields onto the refined lattice
+  void refine_uniform() {
+    const Mesh old = m;
+    const std::vector<double> sol = present;
+    setup(m.n * 2);
+    const int dim = old.dim;
+    auto value_at = [&](const double *x, int comp) {
+      const bool vel = comp < dim;
+      const int kk = (vel ? old.k : old.kp) + 1;
+      const std::vector<double> xn = lobatto01(kk - 1);
+      int ci[3] = {0, 0, 0};
+      double b[3][4], db[4];
+      for (int d = 0; d < dim; ++d) {
+        const double s = (x[d] - old.lo) / old.hc;
+        ci[d] = std::min((int)std::floor(s), old.n - 1);
+        lag1d(xn, s - ci[d], b[d], db);
+      }
+      const int nl = dim == 3 ? kk * kk * kk : kk * kk;
+      double s = 0;
+      for (int a = 0; a < nl; ++a) {
+        const int la[3] = {a % kk, (a / kk) % kk, dim == 3 ? a / (kk * kk) : 0};
+        int64_t id = 0, stride = 1;
+        for (int d = 0; d < dim; ++d) {
+          const int sh = vel ? old.vsh[d] : old.psh[d];
+          id += (int64_t)((ci[d] * (kk - 1) + la[d]) % sh) * stride;
+          stride *= sh;
+        }
+        const double w = b[0][la[0]] * b[1][la[1]] * (dim == 3 ? b[2][la[2]] : 1.0);
+        s += w * (vel ? sol[(size_t)(id * dim + comp)] : sol[(size_t)(dim * old.nv + id)]);
+      }
+      return s;
+    };
+    for (int part = 0; part < 2; ++part) {
+      const bool vel = part == 0;
+      for (int64_t v = 0; v < (vel ? m.nv : m.np); ++v) {
+        double x[3];
+        int idx[3];
+        m.coord(v, vel, x, idx);
+        if (vel)
+          for (int d = 0; d < dim; ++d) present[(size_t)(v * dim + d)] = value_at(x, d);
+        else
+          present[(size_t)(dim * m.nv + v)] = value_at(x, dim);
+      }
+    }
+  }
+  void report() {
+    if (!P.analytical || errors.empty()) return;
+    std::ostringstream o;
+    char line[160];
+    if (P.method == Method::steady) {
+      o << "# cells  e_velocity  rate  e_pressure  rate\n";
+      for (size_t i = 0; i < errors.size(); ++i) {
+        const auto &r = errors[i];
+        const double ru = i ? std::log2(errors[i - 1][1] / r[1]) : NAN, rp = i ? std::log2(errors[i - 1][2] / r[2]) : NAN;
+        std::snprintf(line, sizeof(line), "%lld %.6e %.3f %.6e %.3f\n", (long long)r[0], r[1], ru, r[2], rp);
+        o << line;
+      }
+    } else {
+      o << "# time  e_velocity\n";
+      for (const auto &r : errors) {
+        std::snprintf(line, sizeof(line), "%.6f %.6e\n", r[0], r[1]);
+        o << line;
+      }
+    }
+    std::printf("%s", o.str().c_str());
+    std::ofstream(P.analytical_file + ".dat") << o.str();
+  }
+
+  void run() {
+    dt_now = P.dt;
+    dts[0] = P.dt;
+    setup(1 << P.refinement);
+    if (P.ic_type == "nodal" || P.ic_type == "viscous") {
+      nodal_values(P.ic, present);
+      if (P.ic_type == "viscous") solve_nonlinear(GLS_STEADY, P.ic_nu);
+    } else if (P.ic_type == "L2projection") {
+      l2_projection(P.ic, present);
+    } else {
+      die("initial condition type '%s' is not supported", P.ic_type.c_str());
+    }
+    end_of_step();
+    postprocess(true);
+    const bool steady = P.method == Method::steady;
+    while (steady ? step < P.mesh_adapt + 1 : time < P.t_end - 1e-12 * dt_now) {
+      ++step;
+      if (steady) {
+        time = step;
+      } else {
+        const double dt = std::min(dt_now, P.t_end - time);
+        push_dt(dt);
+        time += dt;
+      }
+      if (P.log_frequency > 0 && step % P.log_frequency == 0) {
+        if (steady) std::printf("step %d/%d (steady)\n", step, P.mesh_adapt + 1);
+        else std::printf("step %d: t = %.10g, dt = %.10g, cfl = %.6g\n", step, time, dt_now, cfl);
+      }
+      if (step == 1) {
+        first_step();
+      } else {
+        if (steady) refine_uniform();
+        advance();
+      }
+      postprocess(false);
+      end_of_step();
+    }
+    report();
+    std::printf("newton_iterations = %d, linear_iterations = %d\n", newton_its, linear_its);
+  }
+};
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  int dim = 0;
+  bool mg = true;
+  const char *file = nullptr;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--dim") && i + 1 < argc) dim = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) mg = std::strcmp(argv[++i], "jacobi") != 0;
+    else if (argv[i][0] != '-') file = argv[i];
+    else die("unknown option %s", argv[i]);
+  }
+  if (!file) die("usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm");
+  if (dim == 0) dim = 3;
+  if (dim != 2 && dim != 3) die("--dim must be 2 or 3");
+  Prm prm(file);
+  Params P = read_params(prm, dim);
+  Solver s(P, mg);
+  s.run();
+  return 0;
+}

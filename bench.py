@@ -55,6 +55,30 @@ def smooth_state(mesh, n, dim, dir_dofs, dir_vals, phase=0.0):
     return x
 
 
+def pmc_traffic(path, kernel_mode, n_dofs):
+    """HBM bytes per launch of gls_brick_kernel<k, mode> from a tools/pmc_traffic.sh summary
+    (separate rocprofv3 --pmc passes for FETCH_SIZE and WRITE_SIZE, KiB per dispatch), corrected
+    with the k_copy calibration in the same file (it moves 8 * n_dofs bytes each way; on gfx950
+    FETCH_SIZE reports half of a streaming read, MI355X_MICROARCH.md 'HBM')."""
+    if not os.path.exists(path):
+        return None
+    cur, vals = None, {}
+    for line in open(path):
+        if not line.startswith(" "):
+            cur = line.strip()
+            continue
+        f = line.split()
+        if cur and f and f[0] in ("FETCH_SIZE", "WRITE_SIZE"):
+            vals.setdefault(cur, {})[f[0]] = float(f[1]) * 1024.0
+    copy = next((v for k_, v in vals.items() if "k_copy" in k_), None)
+    kern = next((v for k_, v in vals.items() if "gls_brick_kernel<2, %d>" % kernel_mode in k_), None)
+    if not copy or not kern or len(copy) < 2 or len(kern) < 2:
+        return None
+    fetch_corr = 8.0 * n_dofs / copy["FETCH_SIZE"]
+    write_corr = 8.0 * n_dofs / copy["WRITE_SIZE"]
+    return kern["FETCH_SIZE"] * fetch_corr + kern["WRITE_SIZE"] * write_corr, fetch_corr, write_corr
+
+
 def cpu_baseline(k, kp, nu, seconds, threads):
     """Oracle (CPU restatement of assembleGLS, 'port') timed on a bounded sample of Q2 cells:
     element-matrix+rhs and rhs-only throughput -> extrapolated assembly-only nonlinear iterations/s."""
@@ -97,7 +121,8 @@ def main():
     ap.add_argument("--mg-coarsest", type=int, default=4)
     ap.add_argument("--mg-smooth", type=int, nargs=2, default=(1, 1), metavar=("PRE", "POST"),
                     help="damped-Jacobi sweeps before / after the coarse correction")
-    ap.add_argument("--mg-omega", type=float, default=0.6)
+    ap.add_argument("--mg-omega", type=float, default=0.7)
+    ap.add_argument("--mg-coarse-sweeps", type=int, default=30)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
@@ -130,7 +155,8 @@ def main():
     if world == 1:
         prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu,
                              multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
-                             pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega)
+                             pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
+                             coarse_sweeps=args.mg_coarse_sweeps)
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -155,7 +181,7 @@ def main():
                 lv.append(DistributedProblem(mm, rank, world, dev, viscosity=args.nu, vnode_mask=mk,
                                              dirichlet=(dd, dv), backend=args.dist_backend))
             attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
-                                         omega=args.mg_omega)
+                                         omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps)
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
@@ -259,6 +285,15 @@ def main():
                      "traffic": None, "algorithmic_bytes_per_launch": B_jv, "launch_ms": jv_launch_ms},
         "setup_s": t_setup,
     }
+    # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
+    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic_jvq_128.txt"), 4, N_global) \
+        if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
+    if tr is not None:
+        out["roofline"]["traffic"] = tr[0]
+        out["roofline"]["traffic_source"] = ("profiles/r01_pmc_traffic_jvq_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
+                                             "%.2f (k_copy calibration); includes the per-quadrature-point "
+                                             "linearization stream (16 doubles/q) the cached J.v reads instead "
+                                             "of re-deriving u, grad u, tau, R_s" % (tr[1], tr[2]))
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
         threads = min(threads, 16)

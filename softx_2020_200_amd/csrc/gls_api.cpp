@@ -313,7 +313,12 @@ struct gls_ctx {
     int k = 2, pre = 2, post = 2, csweeps = 30;
     double omega = 0.6;
     std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
-    DevBuf<double> t1, t2;
+    // per level pair (l, l+1) and axis: 1D tap tables [n_out][5] of prolongation / restriction
+    struct Taps {
+      DevBuf<int32_t> pi[3], ri[3];
+      DevBuf<double> pw[3], rw[3];
+    };
+    std::vector<std::unique_ptr<Taps>> taps;
     bool dirty = true;
   } mg;
   double time_steps[4] = {1, 1, 1, 1};
@@ -870,8 +875,12 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
   const double *yb = mg_to_box(c, l, y, true);
   if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
-  HIP_TRY(gls::mg_transfer(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), mg.k, 0,
-                           c->mg.t1.p, c->mg.t2.p, s));
+  {
+    const auto &T = *mg.taps[(size_t)l];
+    const int32_t *ti[3] = {T.ri[0].p, T.ri[1].p, T.ri[2].p};
+    const double *tw[3] = {T.rw[0].p, T.rw[1].p, T.rw[2].p};
+    HIP_TRY(gls::mg_transfer3d(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), ti, tw, s));
+  }
   GLS_TRY(mg_from_box(c, l + 1, bc));
   GLS_TRY(dist_export_add(h, bc));
   HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
@@ -880,8 +889,12 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   GLS_TRY(dist_import(h, xc));
   const double *xb = mg_to_box(c, l + 1, xc, false);
   if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
-  HIP_TRY(gls::mg_transfer(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), mg.k, 1, c->mg.t1.p,
-                           c->mg.t2.p, s));
+  {
+    const auto &T = *mg.taps[(size_t)l];
+    const int32_t *ti[3] = {T.pi[0].p, T.pi[1].p, T.pi[2].p};
+    const double *tw[3] = {T.pw[0].p, T.pw[1].p, T.pw[2].p};
+    HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, s));
+  }
   GLS_TRY(mg_from_box(c, l, y));
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
@@ -971,9 +984,43 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
       const bool need = b == MB_BOX ? mg.boxed : (l > 0 || b == MB_Y);
       if (need) GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
     }
-  // largest intermediate separable pass: level-0 box x 3 components
-  GLS_TRY(mg.t1.alloc((size_t)(3 * mg_nbox(c, 0))));
-  GLS_TRY(mg.t2.alloc((size_t)(3 * mg_nbox(c, 0))));
+  // 1D transfer taps: fine lattice index i sits at x = i / (2k) coarse cells from the box origin;
+  // prolongation interpolates the coarse Qk field of the parent cell (equidistant nodes, k <= 2)
+  const int K = c->k;
+  for (int l = 0; l + 1 < p->n_levels; ++l) {
+    std::unique_ptr<gls_ctx::MG::Taps> T(new gls_ctx::MG::Taps);
+    for (int a = 0; a < 3; ++a) {
+      const int nf = mg.dims[l][a], nc = mg.dims[l + 1][a], ncc = (nf - 1) / (2 * K);
+      std::vector<int32_t> pi((size_t)nf * 5, 0), ri((size_t)nc * 5, 0);
+      std::vector<double> pw((size_t)nf * 5, 0.0), rw((size_t)nc * 5, 0.0);
+      std::vector<int> rn((size_t)nc, 0);
+      for (int i = 0; i < nf; ++i) {
+        const double x = (double)i / (2.0 * K);
+        const int cc = std::min((int)std::floor(x), ncc - 1);
+        const double xi = x - cc;
+        int np = 0;
+        for (int q = 0; q <= K; ++q) {
+          double L = 1.0;
+          for (int b = 0; b <= K; ++b)
+            if (b != q) L *= (xi * K - b) / (double)(q - b);
+          if (L == 0.0) continue;
+          const int j = cc * K + q;
+          pi[(size_t)i * 5 + np] = j;
+          pw[(size_t)i * 5 + np] = L;
+          ++np;
+          if (rn[(size_t)j] >= 5) return set_err(GLS_EINVAL, "mg: restriction stencil wider than 5");
+          ri[(size_t)j * 5 + rn[(size_t)j]] = i;
+          rw[(size_t)j * 5 + rn[(size_t)j]] = L;
+          ++rn[(size_t)j];
+        }
+      }
+      GLS_TRY(T->pi[a].upload(pi.data(), pi.size()));
+      GLS_TRY(T->pw[a].upload(pw.data(), pw.size()));
+      GLS_TRY(T->ri[a].upload(ri.data(), ri.size()));
+      GLS_TRY(T->rw[a].upload(rw.data(), rw.size()));
+    }
+    mg.taps.push_back(std::move(T));
+  }
   mg.on = true;
   mg.dirty = true;
   return GLS_OK;

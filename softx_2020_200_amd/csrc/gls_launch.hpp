@@ -37,9 +37,10 @@ hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, in
 int multidot_work_size();
 
 // ---- geometric multigrid (gls_mg_kernels.hip): nested Qk node lattices (boxes), k <= 2
-hipError_t mg_transfer(const double *in, double *out, const int nin[3], const int nout[3], int k, int prolong,
-                       double *tmp1, double *tmp2, hipStream_t s);
 hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s);
+// one-pass 3D transfer with per-axis tap tables [n_out][5] (index, weight; weight 0 = unused)
+hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const int nout[3],
+                         const int32_t *const taps[3], const double *const w[3], hipStream_t s);
 hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
                          int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes
 hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,

@@ -2,9 +2,10 @@
 //
 // Nested hyper_cube levels: the Qk node lattice of level l+1 (n/2 cells per direction) is every
 // second node of level l (k <= 2: Gauss-Lobatto support points are equidistant). Prolongation
-// interpolates the coarse Qk field exactly at the fine nodes; restriction is its transpose.
-// Both are applied as three separable 1D passes over a [n2][n1][n0][ncomp] lattice array
-// (velocity: ncomp 3 interleaved, pressure: ncomp 1), each thread producing one output entry.
+// interpolates the coarse Qk field exactly at the fine nodes; restriction is its transpose. Both
+// run as ONE gather pass per transfer (thread per output node, tensor product of per-axis tap
+// tables built on the host), velocity and pressure together: the fine vector is read or written
+// once (the earlier three separable passes moved ~3.5x the bytes).
 // Multi-GPU: each rank works on the box sub-lattice its cells span (box gather / scatter through
 // a box -> local node map); nested partitions keep the coarse box the fine box's every-second node.
 #include "gls_launch.hpp"
@@ -13,59 +14,44 @@ namespace gls {
 
 namespace {
 
-// parent coarse cell and local coordinate of fine lattice index i (k = degree, ncc = coarse cells)
-__device__ __forceinline__ void parent(int i, int k, int ncc, int &c, double &xi) {
-  const double x = (double)i / (2.0 * k);  // in coarse-cell units
-  c = min((int)floor(x), ncc - 1);
-  xi = x - c;
-}
-__device__ __forceinline__ double lag_eq(int k, int a, double xi) {  // equidistant Lagrange on [0,1]
-  double L = 1.0;
-  for (int b = 0; b <= k; ++b)
-    if (b != a) L *= (xi * k - b) / (double)(a - b);
-  return L;
-}
-
-// one separable pass along `axis`: in dims (d0,d1,d2) -> out dims with d_axis replaced by nout
-__global__ void k_transfer_axis(const double *__restrict__ in, double *__restrict__ out, int d0, int d1, int d2,
-                                int axis, int nout, int ncomp, int k, int prolong) {
-  int od[3] = {d0, d1, d2};
-  od[axis] = nout;
-  const int64_t total = (int64_t)od[0] * od[1] * od[2] * ncomp;
-  const int nin = axis == 0 ? d0 : (axis == 1 ? d1 : d2);
-  const int nfine = prolong ? nout : nin;
-  const int ncc = (nfine - 1) / (2 * k);  // coarse cells along the axis
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int comp = (int)(t % ncomp);
-    int64_t r = t / ncomp;
-    int o[3];
-    o[0] = (int)(r % od[0]);
-    r /= od[0];
-    o[1] = (int)(r % od[1]);
-    o[2] = (int)(r / od[1]);
-    const int oi = o[axis];
-    auto in_at = [&](int j) {
-      int p[3] = {o[0], o[1], o[2]};
-      p[axis] = j;
-      return in[(((int64_t)p[2] * d1 + p[1]) * d0 + p[0]) * ncomp + comp];
-    };
-    double s = 0.;
-    if (prolong) {
-      int c;
-      double xi;
-      parent(oi, k, ncc, c, xi);
-      for (int a = 0; a <= k; ++a) s += lag_eq(k, a, xi) * in_at(c * k + a);
-    } else {
-      const int lo = max(0, 2 * oi - (2 * k - 1)), hi = min(nin - 1, 2 * oi + (2 * k - 1));
-      for (int i = lo; i <= hi; ++i) {
-        int c;
-        double xi;
-        parent(i, k, ncc, c, xi);
-        const int a = oi - c * k;
-        if (a >= 0 && a <= k) s += lag_eq(k, a, xi) * in_at(i);
+// Direct 3D transfer: out[o] = sum over the tensor product of per-axis taps (<= kMaxTaps each,
+// weight 0 pads) of w_x w_y w_z in[i]; velocity (3 interleaved) and pressure in one pass. The tap
+// tables are the 1D prolongation (fine <- coarse) or its transpose (restriction) per axis.
+constexpr int kMaxTaps = 5;
+__global__ void __launch_bounds__(256) k_transfer3d(const double *__restrict__ in, double *__restrict__ out, int i0,
+                                                    int i1, int i2, int o0, int o1, int o2,
+                                                    const int32_t *__restrict__ tx, const double *__restrict__ wx,
+                                                    const int32_t *__restrict__ ty, const double *__restrict__ wy,
+                                                    const int32_t *__restrict__ tz, const double *__restrict__ wz) {
+  const int64_t nin = (int64_t)i0 * i1 * i2, nout = (int64_t)o0 * o1 * o2;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nout; t += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(t % o0), y = (int)((t / o0) % o1), z = (int)(t / ((int64_t)o0 * o1));
+    double s0 = 0., s1 = 0., s2 = 0., sp = 0.;
+    for (int c = 0; c < kMaxTaps; ++c) {
+      const double az = wz[z * kMaxTaps + c];
+      if (az == 0.0) continue;
+      const int64_t bz = (int64_t)tz[z * kMaxTaps + c] * i1;
+      for (int b = 0; b < kMaxTaps; ++b) {
+        const double ay = wy[y * kMaxTaps + b];
+        if (ay == 0.0) continue;
+        const int64_t by = (bz + ty[y * kMaxTaps + b]) * i0;
+        const double ayz = ay * az;
+        for (int a = 0; a < kMaxTaps; ++a) {
+          const double ax = wx[x * kMaxTaps + a];
+          if (ax == 0.0) continue;
+          const int64_t n = by + tx[x * kMaxTaps + a];
+          const double w = ax * ayz;
+          s0 += w * in[3 * n];
+          s1 += w * in[3 * n + 1];
+          s2 += w * in[3 * n + 2];
+          sp += w * in[3 * nin + n];
+        }
       }
     }
-    out[t] = s;
+    out[3 * t] = s0;
+    out[3 * t + 1] = s1;
+    out[3 * t + 2] = s2;
+    out[3 * nout + t] = sp;
   }
 }
 
@@ -123,26 +109,12 @@ int grid_for(int64_t n) {
 
 }  // namespace
 
-// out = T(in) for one Qk vector [vel (3 comps interleaved) | pressure] on a box node lattice
-// (dims x, y, z), T = prolongation (nin -> nout = 2 nin - 1 per axis) or restriction (nin -> nout,
-// nin = 2 nout - 1); tmp1/tmp2 hold the intermediate passes.
-hipError_t mg_transfer(const double *in, double *out, const int nin[3], const int nout[3], int k, int prolong,
-                       double *tmp1, double *tmp2, hipStream_t s) {
-  const int64_t nvi = (int64_t)nin[0] * nin[1] * nin[2], nvo = (int64_t)nout[0] * nout[1] * nout[2];
-  for (int part = 0; part < 2; ++part) {
-    const int nc = part == 0 ? 3 : 1;
-    const double *src = in + (part == 0 ? 0 : 3 * nvi);
-    double *dst = out + (part == 0 ? 0 : 3 * nvo);
-    // axis 0: (i0,i1,i2) -> (o0,i1,i2); axis 1 -> (o0,o1,i2); axis 2 -> (o0,o1,o2)
-    const int64_t s1 = (int64_t)nout[0] * nin[1] * nin[2] * nc, s2 = (int64_t)nout[0] * nout[1] * nin[2] * nc,
-                  s3 = nvo * nc;
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s1)), dim3(256), 0, s, src, tmp1, nin[0], nin[1], nin[2], 0,
-                       nout[0], nc, k, prolong);
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s2)), dim3(256), 0, s, tmp1, tmp2, nout[0], nin[1], nin[2], 1,
-                       nout[1], nc, k, prolong);
-    hipLaunchKernelGGL(k_transfer_axis, dim3(grid_for(s3)), dim3(256), 0, s, tmp2, dst, nout[0], nout[1], nin[2], 2,
-                       nout[2], nc, k, prolong);
-  }
+hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const int nout[3],
+                         const int32_t *const taps[3], const double *const w[3], hipStream_t s) {
+  const int64_t n = (int64_t)nout[0] * nout[1] * nout[2];
+  const int64_t b = (n + 255) / 256;
+  hipLaunchKernelGGL(k_transfer3d, dim3((int)(b < 65536 ? (b > 0 ? b : 1) : 65536)), dim3(256), 0, s, in, out, nin[0],
+                     nin[1], nin[2], nout[0], nout[1], nout[2], taps[0], w[0], taps[1], w[1], taps[2], w[2]);
   return hipGetLastError();
 }
 

@@ -1,0 +1,212 @@
+"""End-to-end drop-in check of the C++ application (apps/gls_navier_stokes): parameter files in the
+reference's format are generated here from the golden fixture data (forcing / exact solution
+expressions, mesh sizes, schemes of the reference's application tests), the app runs the full
+prm -> mesh -> initial condition -> time loop -> Newton/GMRES on the GPU -> L2 error path, and its
+errors are compared with the numbers the reference printed."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+APP = os.path.join(ROOT, "apps", "gls_navier_stokes")
+G = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_goldens.json")))
+
+
+def run_app(tmp_path, prm, dim, *extra):
+    f = tmp_path / "case.prm"
+    f.write_text(prm)
+    if not os.path.exists(APP):
+        pytest.fail("apps/gls_navier_stokes is not built (run __graft_entry__.build())")
+    out = subprocess.run([APP, "--dim", str(dim), *extra, str(f)], cwd=str(tmp_path), capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return out.stdout
+
+
+def table(stdout):
+    rows, on = [], False
+    for line in stdout.splitlines():
+        if line.startswith("# "):
+            on = True
+            continue
+        if on and line.strip() and not line.startswith("newton_iterations"):
+            rows.append([float(v) for v in line.split()])
+    return rows
+
+
+def mms_prm(g, dim, refinement, adapt):
+    zeros = "; ".join(["0"] * (dim + 1))
+    return f"""
+subsection simulation control
+  set method            = steady
+  set number mesh adapt = {adapt}
+  set output frequency  = 0
+end
+subsection physical properties
+  set kinematic viscosity = 1.0
+end
+subsection mesh
+  set type               = dealii
+  set grid type          = hyper_cube
+  set grid arguments     = -1 : 1 : false
+  set initial refinement = {refinement}
+end
+subsection mesh adaptation
+  set type = uniform
+end
+subsection FEM
+  set velocity order = 1
+  set pressure order = 1
+end
+subsection boundary conditions
+  set number = 1
+  subsection bc 0
+    set type = noslip
+  end
+end
+subsection source term
+  set enable = true
+  subsection xyz
+    set Function expression = {g["force"]}
+  end
+end
+subsection initial conditions
+  set type = nodal
+  subsection uvwp
+    set Function expression = {zeros}
+  end
+end
+subsection analytical solution
+  set enable = true
+  subsection uvwp
+    set Function expression = {g["exact"]}
+  end
+end
+subsection non-linear solver
+  set tolerance      = 1e-10
+  set max iterations = 10
+  set verbosity      = quiet
+end
+subsection linear solver
+  set max iters         = 2000
+  set relative residual = 1e-12
+  set minimum residual  = 1e-14
+end
+"""
+
+
+def close(a, b, digits):
+    return abs(a - b) <= 0.5 * 10 ** (int(f"{b:e}".split("e")[1]) - digits + 1) + 1e-15
+
+
+@pytest.mark.gpu
+def test_app_mms3d_with_uniform_refinement(tmp_path):
+    g = G["mms3d_gls"]
+    out = run_app(tmp_path, mms_prm(g, 3, 2, 1), 3)
+    rows = table(out)
+    assert [int(r[0]) for r in rows] == [64, 512], out
+    for i, r in enumerate(rows):
+        assert close(r[1], g["error_velocity"][i], 5), (r, g)
+        assert close(r[3], g["error_pressure"][i], 5), (r, g)
+    assert (tmp_path / "L2Error.dat").exists()
+
+
+@pytest.mark.gpu
+def test_app_mms2d(tmp_path):
+    g = G["mms2d_gls"]
+    out = run_app(tmp_path, mms_prm(g, 2, 3, 2), 2)
+    rows = table(out)
+    assert [int(r[0]) for r in rows] == [64, 256, 1024]
+    for i, r in enumerate(rows):
+        assert close(r[1], g["error_velocity"][i], 5), (r, g)
+        assert close(r[3], g["error_pressure"][i], 5), (r, g)
+
+
+def tgv_prm(method, k, kp, refinement, dt, t_end, output_frequency=0):
+    c = G["tgv_common"]
+    nu = c["viscosity"]
+    bcs = "\n".join(f"""  subsection bc {i}
+    set type               = periodic
+    set id                 = {a}
+    set periodic_id        = {b}
+    set periodic_direction = {d}
+  end""" for i, (a, b, d) in enumerate(c["periodic"]))
+    return f"""
+subsection simulation control
+  set method           = {method}
+  set time step        = {dt}
+  set time end         = {t_end}
+  set output frequency = {output_frequency}
+  set output name      = tgv
+end
+subsection physical properties
+  set kinematic viscosity = {nu}
+end
+subsection mesh
+  set type               = dealii
+  set grid type          = hyper_cube
+  set grid arguments     = {c["domain"][0]} : {c["domain"][1]} : true
+  set initial refinement = {refinement}
+end
+subsection FEM
+  set velocity order = {k}
+  set pressure order = {kp}
+end
+subsection boundary conditions
+  set number = {len(c["periodic"])}
+{bcs}
+end
+subsection initial conditions
+  set type = L2projection
+  subsection uvwp
+    set Function expression = {c["initial_condition"]}
+  end
+end
+subsection analytical solution
+  set enable    = true
+  set verbosity = verbose
+  subsection uvwp
+    set Function constants  = viscosity={nu}
+    set Function expression = exp(-2*viscosity*t)*cos(x)*sin(y); -sin(x)*cos(y)*exp(-2*viscosity*t); 0
+  end
+end
+subsection post-processing
+  set verbosity                = verbose
+  set calculate enstrophy      = true
+  set calculate kinetic energy = true
+end
+subsection non-linear solver
+  set tolerance      = {c["newton_tol"]}
+  set max iterations = {c["newton_max_it"]}
+  set verbosity      = quiet
+end
+subsection linear solver
+  set max iters         = 5000
+  set relative residual = 1e-13
+  set minimum residual  = 1e-14
+end
+"""
+
+
+@pytest.mark.gpu
+def test_app_tgv_sdirk2_l2projection_periodic(tmp_path):
+    g = G["tgv_sdirk2"]
+    out = run_app(tmp_path, tgv_prm("sdirk2", g["k"], g["kp"], 6, g["dt"], g["t_end"]), 2)
+    e = [float(l.split("=")[1]) for l in out.splitlines() if l.startswith("l2_error_velocity")]
+    assert len(e) == 1 and close(e[0], g["error_velocity_log"], 6), out
+    # the initial state's kinetic energy and enstrophy of the TGV field are 1/4 and 1/2
+    ke = [float(l.split("=")[1]) for l in out.splitlines() if l.startswith("kinetic_energy")]
+    en = [float(l.split("=")[1]) for l in out.splitlines() if l.startswith("enstrophy")]
+    assert abs(ke[0] - 0.25) < 1e-3 and abs(en[0] - 0.5) < 2e-3
+
+
+@pytest.mark.gpu
+def test_app_tgv_bdf1_first_step_and_output(tmp_path):
+    g = G["tgv_bdf1"]
+    out = run_app(tmp_path, tgv_prm("bdf1", g["k"], g["kp"], 5, g["dt"], g["dt"], output_frequency=1), 2)
+    e = [float(l.split("=")[1]) for l in out.splitlines() if l.startswith("l2_error_velocity")]
+    assert close(e[0], g["checkpoints"]["0.01"], 5), out
+    for f in ("tgv.pvd", "tgv.00000.pvtu", "tgv.00001.pvtu", "tgv.00001.00000.vtu"):
+        assert (tmp_path / f).exists(), f

@@ -169,3 +169,25 @@ def test_pvtu_pvd(tmp_path):
     assert names == ["velocity", "pressure", "subdomain", "vorticity", "q_criterion"]
     ds = list(ET.parse(str(tmp_path / "a.pvd")).getroot().iter("DataSet"))
     assert [(float(d.get("timestep")), d.get("file")) for d in ds] == [(0.0, "a.00000.pvtu"), (0.05, "a.00001.pvtu")]
+
+
+def _app(tmp_path, prm_text, *args):
+    import os
+    import subprocess
+    app = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "apps", "gls_navier_stokes")
+    f = tmp_path / "c.prm"
+    f.write_text(prm_text)
+    return subprocess.run([app, *args, str(f)], capture_output=True, text=True, timeout=60)
+
+
+@pytest.mark.parametrize("text,msg", [
+    ("subsection mesh\n  set grid type = hyper_ball\nend\n", "hyper_cube only"),
+    ("subsection simulation control\n  set method = rk4\nend\n", "unknown time stepping method"),
+    ("subsection boundary conditions\n set number = 1\n subsection bc 0\n  set type = slip\n end\nend\n", "slip"),
+    ("subsection source term\n set enable = true\n subsection xyz\n  set Function expression = q*2; 0; 0; 0\n"
+     " end\nend\n", "unknown variable 'q'"),
+    ("subsection mesh\n set initial refinement = 2\n", "not closed"),
+])
+def test_app_rejects_unsupported_input_before_touching_the_gpu(tmp_path, text, msg):
+    out = _app(tmp_path, text, "--dim", "3")
+    assert out.returncode == 2 and msg in out.stderr, out.stderr

@@ -16,7 +16,7 @@ G = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_goldens.json
 
 def test_header_symbols_exported():
     hdr = open(os.path.join(ROOT, "include", "gls_native.h")).read()
-    declared = set(re.findall(r"^(?:int|const char \*)\s*(gls_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^(?:int|void|const char \*)\s*(gls_\w+)\s*\(", hdr, re.M))
     assert declared, "no declarations parsed"
     L = load()
     for name in sorted(declared):
