@@ -559,9 +559,9 @@ struct Solver {
     present.assign((size_t)N, 0.);
     m1 = m2 = m3 = present;
     // geometric multigrid on nested hyper_cubes (3D, k == kp <= 2, no periodicity)
-    if (use_mg && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && n >= 8 && (n & (n - 1)) == 0) {
+    if (use_mg && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && n >= 4 && (n & (n - 1)) == 0) {
       std::vector<gls_ctx *> lv{ctx};
-      for (int c = n / 2; c >= 4; c /= 2) {
+      for (int c = n / 2; c >= 2; c /= 2) {
         const Mesh mc = build_mesh(P, c, 0);
         const Constraints cc = make_constraints(P, mc, time);
         gls_ctx *g = make_context(mc, cc);
@@ -574,8 +574,9 @@ struct Solver {
       mp.levels = lv.data();
       mp.pre_smooth = 1;
       mp.post_smooth = 1;
-      mp.coarse_sweeps = 30;
-      mp.omega = 0.7;
+      mp.coarse_sweeps = 100;
+      mp.omega = 0.9;
+      mp.coarse_omega = 0.7;
       ck(gls_mg_attach(ctx, &mp), "gls_mg_attach");
     }
     std::printf("mesh: cells = %lld, dofs = %lld, levels = %d\n", (long long)m.nc, (long long)N,

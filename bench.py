@@ -121,8 +121,9 @@ def main():
     ap.add_argument("--mg-coarsest", type=int, default=4)
     ap.add_argument("--mg-smooth", type=int, nargs=2, default=(1, 1), metavar=("PRE", "POST"),
                     help="damped-Jacobi sweeps before / after the coarse correction")
-    ap.add_argument("--mg-omega", type=float, default=0.7)
-    ap.add_argument("--mg-coarse-sweeps", type=int, default=30)
+    ap.add_argument("--mg-omega", type=float, default=0.9)
+    ap.add_argument("--mg-coarse-sweeps", type=int, default=100)
+    ap.add_argument("--mg-coarse-omega", type=float, default=0.7, help="0 = --mg-omega")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
@@ -156,7 +157,7 @@ def main():
         prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu,
                              multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
                              pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
-                             coarse_sweeps=args.mg_coarse_sweeps)
+                             coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega)
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -181,7 +182,8 @@ def main():
                 lv.append(DistributedProblem(mm, rank, world, dev, viscosity=args.nu, vnode_mask=mk,
                                              dirichlet=(dd, dv), backend=args.dist_backend))
             attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
-                                         omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps)
+                                         omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
+                                         coarse_omega=args.mg_coarse_omega)
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])

@@ -133,7 +133,8 @@ int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_para
  * levels[0] = ctx; levels[l] = caller-created contexts of the same problem on the nested
  * hyper_cube with n/2^l cells per direction (same k, same boundary conditions and Dirichlet
  * lists). Each V-cycle: damped-Jacobi smoothing with the level's own matrix-free GLS Jacobian at
- * the injected state, exact Qk restriction/prolongation. 3D Q1-Q1 / Q2-Q2.
+ * the injected state, exact Qk restriction/prolongation. 3D Q1-Q1 / Q2-Q2. The coarse levels are
+ * switched to ctx's stream (and follow later gls_set_stream calls on ctx).
  * Multi-GPU: every level is a distributed context (gls_dist_attach on the partition of its own
  * hyper_cube; nested partitions: rank r's coarse cells are the parents of its fine cells) that
  * also declared its lattice embedding with gls_set_lattice. Restriction sums owned fine rows and
@@ -142,9 +143,15 @@ typedef struct {
   int n_levels;
   gls_ctx **levels;
   int pre_smooth, post_smooth, coarse_sweeps;  /* 0 -> defaults 2, 2, 30 */
-  double omega;                               /* 0 -> 0.6 */
+  double omega;                               /* damped-Jacobi weight of the smoother, 0 -> 0.6 */
+  double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
+  int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
+                                                 with <= 2048 DoFs), 1 exact solve, -1 Jacobi sweeps */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
+/* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
+ * attached, else Jacobi): the reference's preconditioner vmult (DEVICE pointers, no aliasing). */
+int gls_apply_preconditioner(gls_ctx *ctx, const double *v, double *z);
 /* Lattice embedding of a (rank-local) mesh: its velocity nodes are a subset of the global n1d^3
  * Qk node lattice of hyper_cube in canonical numbering (global id = x + n1d*(y + n1d*z)), local
  * node i being global node local_to_global[i] (host array, n_vnodes entries). The local nodes

@@ -311,7 +311,7 @@ struct gls_ctx {
     std::vector<gls_ctx *> lev;
     std::vector<std::array<int, 3>> dims;  // box lattice nodes per direction per level
     int k = 2, pre = 2, post = 2, csweeps = 30;
-    double omega = 0.6;
+    double omega = 0.6, comega = 0.6;
     std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
     // per level pair (l, l+1) and axis: 1D tap tables [n_out][5] of prolongation / restriction
     struct Taps {
@@ -319,6 +319,10 @@ struct gls_ctx {
       DevBuf<double> pw[3], rw[3];
     };
     std::vector<std::unique_ptr<Taps>> taps;
+    // coarsest level: direct solve with the probed, regularised, inverted Jacobian
+    bool direct = false, direct_ok = false;
+    DevBuf<double> probe, aug, unit;
+    DevBuf<int> status;
     bool dirty = true;
   } mg;
   double time_steps[4] = {1, 1, 1, 1};
@@ -612,6 +616,9 @@ int gls_set_stream(gls_ctx *c, void *s) {
   }
   c->own_stream = false;
   c->stream = (hipStream_t)s;
+  // multigrid levels run on the fine level's stream (the V-cycle interleaves their kernels)
+  if (c->mg.on)
+    for (size_t l = 1; l < c->mg.lev.size(); ++l) GLS_TRY(gls_set_stream(c->mg.lev[l], s));
   return GLS_OK;
 }
 
@@ -847,6 +854,23 @@ int mg_prepare(gls_ctx *c) {
     GLS_TRY(gls_set_state(g, mgbuf(c, l, MB_U), gh[0], gh[1], gh[2]));
     GLS_TRY(ensure_diag(g));
   }
+  mg.direct_ok = false;
+  if (mg.direct) {  // probe A = J_coarse column by column, then invert on the device
+    gls_ctx *g = mg.lev[(size_t)L - 1];
+    const int64_t n = g->n_dofs;
+    HIP_TRY(gls::vec_fill(mg.unit.p, n, 0.0, c->stream));
+    for (int64_t j = 0; j < n; ++j) {
+      HIP_TRY(gls::mg_unit_step(mg.unit.p, j, c->stream));
+      GLS_TRY(gls_jacobian_apply(g, mg.unit.p, mg.probe.p + j * n));
+    }
+    HIP_TRY(gls::mg_dense_invert(mg.probe.p, mg.aug.p, (int)n, mg.status.p, c->stream));
+    int st = -1;
+    HIP_TRY(hipMemcpyAsync(&st, mg.status.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // a couple of dependent columns (pressure gauge) are expected; many mean a broken operator
+    mg.direct_ok = st >= 0 && st <= 4;
+    if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse direct solve n=%lld dropped=%d ok=%d\n", (long long)n, st, (int)mg.direct_ok);
+  }
   mg.dirty = false;
   return GLS_OK;
 }
@@ -861,11 +885,16 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   double *y = mgbuf(c, l, MB_Y);
   const double *d = g->diag.p;
   hipStream_t s = c->stream;
+  if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
+    HIP_TRY(gls::mg_dense_apply(mg.aug.p, (int)n, b, x, c->stream));
+    return GLS_OK;
+  }
   const int pre = l == L - 1 ? mg.csweeps : mg.pre;
-  HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, mg.omega, n, 1, s));  // first sweep from x = 0
+  const double om = l == L - 1 ? mg.comega : mg.omega;
+  HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
   for (int it = 1; it < pre; ++it) {
     GLS_TRY(gls_jacobian_apply(g, x, y));
-    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
+    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, om, n, 0, s));
   }
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
@@ -912,6 +941,14 @@ int apply_prec(gls_ctx *c, const double *v, double *z) {
   return GLS_OK;
 }
 }  // namespace
+
+int gls_apply_preconditioner(gls_ctx *c, const double *v, double *z) {
+  GLS_TRY(check_ctx(c));
+  if (!v || !z || v == z) return set_err(GLS_EINVAL, "v/z null or aliased");
+  GLS_TRY(ensure_diag(c));
+  if (c->mg.on) GLS_TRY(mg_prepare(c));
+  return apply_prec(c, v, z);
+}
 
 int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {
   GLS_TRY(check_ctx(c));
@@ -978,6 +1015,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
   mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
   mg.omega = p->omega > 0 ? p->omega : 0.6;
+  mg.comega = p->coarse_omega > 0 ? p->coarse_omega : mg.omega;
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
@@ -1021,8 +1059,24 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     }
     mg.taps.push_back(std::move(T));
   }
+  // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
+  {
+    const int64_t nco = mg.lev.back()->n_dofs;
+    const int want = p->coarse_direct;
+    if (want > 0 && (mg.boxed || nco > 8192)) return set_err(GLS_EINVAL, "mg: direct coarse solve needs one GPU, <= 8192 DoFs");
+    mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
+    if (mg.direct) {
+      GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
+      GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
+      GLS_TRY(mg.unit.alloc((size_t)nco));
+      GLS_TRY(mg.status.alloc(1));
+    }
+  }
   mg.on = true;
   mg.dirty = true;
+  // one stream for the whole V-cycle: the coarse levels' kernels are ordered with the transfers
+  for (size_t l = 1; l < mg.lev.size(); ++l)
+    if (mg.lev[l]->stream != c->stream) GLS_TRY(gls_set_stream(mg.lev[l], c->stream));
   return GLS_OK;
 }
 

@@ -45,6 +45,10 @@ hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int
                          int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes
 hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,
                           hipStream_t s);
+// coarsest-level direct solve: invert the probed matrix (Y column-major) into aug = [I | A^-1]
+hipError_t mg_dense_invert(const double *Y, double *aug, int n, int *status, hipStream_t s);  // status: dropped columns
+hipError_t mg_unit_step(double *e, int64_t j, hipStream_t s);  // e[j-1] = 0, e[j] = 1
+hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, hipStream_t s);
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s);
 

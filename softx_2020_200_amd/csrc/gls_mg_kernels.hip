@@ -55,6 +55,111 @@ __global__ void __launch_bounds__(256) k_transfer3d(const double *__restrict__ i
   }
 }
 
+// Coarsest-level direct solve. The coarse Jacobian A (n <= a few thousand DoFs) is probed
+// column by column (Y[j*n + i] = (A e_j)_i) and inverted by Gauss-Jordan with partial pivoting
+// on [A | I] in ONE workgroup; each V-cycle then applies x = A^+ b (dense GEMV). A pivot below
+// 1e-12 max|A| marks a dependent column (the enclosed-flow Jacobian has the constant-pressure
+// null vector): that unknown is dropped (set to 0), which gives a particular solution of the
+// consistent part instead of amplifying the null direction. status = number of dropped columns.
+constexpr int kGJThreads = 1024;
+__global__ void __launch_bounds__(kGJThreads) k_gauss_jordan(const double *__restrict__ Y, double *__restrict__ aug, int n,
+                                                          int *status) {
+  __shared__ double red_v[kGJThreads];
+  __shared__ int red_i[kGJThreads];
+  const int tid = threadIdx.x, w = 2 * n;
+  double amax = 0.0;
+  for (int64_t t = tid; t < (int64_t)n * w; t += kGJThreads) {
+    const int i = (int)(t / w), j = (int)(t % w);
+    double v;
+    if (j < n) {
+      v = Y[(int64_t)j * n + i];
+      amax = fmax(amax, fabs(v));
+    } else {
+      v = (j - n == i) ? 1.0 : 0.0;
+    }
+    aug[t] = v;
+  }
+  red_v[tid] = amax;
+  __syncthreads();
+  for (int st = kGJThreads / 2; st > 0; st >>= 1) {
+    if (tid < st) red_v[tid] = fmax(red_v[tid], red_v[tid + st]);
+    __syncthreads();
+  }
+  const double tiny = 1e-12 * red_v[0];
+  __syncthreads();
+  int dropped = 0;
+  for (int k = 0; k < n; ++k) {
+    // pivot search in column k, rows k..n-1
+    double best = -1.0;
+    int bi = k;
+    for (int i = k + tid; i < n; i += kGJThreads) {
+      const double a = fabs(aug[(int64_t)i * w + k]);
+      if (a > best) { best = a; bi = i; }
+    }
+    red_v[tid] = best;
+    red_i[tid] = bi;
+    __syncthreads();
+    for (int st = kGJThreads / 2; st > 0; st >>= 1) {
+      if (tid < st && (red_v[tid + st] > red_v[tid] || (red_v[tid + st] == red_v[tid] && red_i[tid + st] < red_i[tid]))) {
+        red_v[tid] = red_v[tid + st];
+        red_i[tid] = red_i[tid + st];
+      }
+      __syncthreads();
+    }
+    const int piv = red_i[0];
+    const double pval = red_v[0];
+    __syncthreads();
+    if (!(pval > tiny)) {  // dependent column: drop unknown k
+      for (int i = tid; i < n; i += kGJThreads) aug[(int64_t)i * w + k] = 0.0;
+      __syncthreads();
+      for (int j = tid; j < w; j += kGJThreads) aug[(int64_t)k * w + j] = (j == k) ? 1.0 : 0.0;
+      ++dropped;
+      __syncthreads();
+      continue;
+    }
+    if (piv != k)
+      for (int j = tid; j < w; j += kGJThreads) {
+        const double t0 = aug[(int64_t)k * w + j];
+        aug[(int64_t)k * w + j] = aug[(int64_t)piv * w + j];
+        aug[(int64_t)piv * w + j] = t0;
+      }
+    __syncthreads();
+    const double inv = 1.0 / aug[(int64_t)k * w + k];
+    __syncthreads();
+    for (int j = tid; j < w; j += kGJThreads) aug[(int64_t)k * w + j] *= inv;
+    __syncthreads();
+    // eliminate column k from every other row: a wave per row, lanes along the row; row k is
+    // zero left of column k, so only columns > k change
+    {
+      const int wave = tid >> 6, lane = tid & 63;
+      const double *rk = aug + (int64_t)k * w;
+      for (int i = wave; i < n; i += kGJThreads / 64) {
+        if (i == k) continue;
+        double *ri = aug + (int64_t)i * w;
+        const double f = ri[k];
+        if (f == 0.0) continue;
+        for (int j = k + 1 + lane; j < w; j += 64) ri[j] -= f * rk[j];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kGJThreads)
+      if (i != k) aug[(int64_t)i * w + k] = 0.0;
+    __syncthreads();
+  }
+  if (tid == 0) *status = dropped;
+}
+
+// x = A^-1 b with A^-1 the right half of the Gauss-Jordan result (row stride 2n)
+__global__ void k_dense_inv_apply(const double *__restrict__ aug, int n, const double *__restrict__ b,
+                                  double *__restrict__ x) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double *row = aug + (int64_t)i * 2 * n + n;
+  double s = 0.0;
+  for (int j = 0; j < n; ++j) s += row[j] * b[j];
+  x[i] = s;
+}
+
 // coarse (I,J,K) <- fine (2I,2J,2K) on box lattices, velocity (3 comps) and pressure parts
 __global__ void k_inject(const double *__restrict__ fine, double *__restrict__ coarse, int f0, int f1, int f2, int c0,
                          int c1, int c2) {
@@ -133,6 +238,27 @@ hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int
 hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,
                           hipStream_t s) {
   hipLaunchKernelGGL(k_box_scatter, dim3(grid_for(nbox)), dim3(256), 0, s, box, loc, map, nbox, nvl);
+  return hipGetLastError();
+}
+
+__global__ void k_unit(double *e, int64_t j) {  // e_{j-1} -> e_j (probing)
+  if (threadIdx.x == 0) {
+    if (j > 0) e[j - 1] = 0.0;
+    e[j] = 1.0;
+  }
+}
+hipError_t mg_unit_step(double *e, int64_t j, hipStream_t s) {
+  hipLaunchKernelGGL(k_unit, dim3(1), dim3(64), 0, s, e, j);
+  return hipGetLastError();
+}
+
+hipError_t mg_dense_invert(const double *Y, double *aug, int n, int *status, hipStream_t s) {
+  hipLaunchKernelGGL(k_gauss_jordan, dim3(1), dim3(kGJThreads), 0, s, Y, aug, n, status);
+  return hipGetLastError();
+}
+
+hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, hipStream_t s) {
+  hipLaunchKernelGGL(k_dense_inv_apply, dim3((n + 255) / 256), dim3(256), 0, s, aug, n, b, x);
   return hipGetLastError();
 }
 

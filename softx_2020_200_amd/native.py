@@ -29,7 +29,7 @@ EXPORTS = [
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import",
-    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice",
+    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice", "gls_apply_preconditioner",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -59,7 +59,8 @@ class LinearParams(C.Structure):
 
 class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
-                ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double)]
+                ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
+                ("coarse_omega", C.c_double), ("coarse_direct", C.c_int)]
 
 
 class NewtonParams(C.Structure):
@@ -111,6 +112,7 @@ def load():
     L.gls_mg_attach.argtypes = [vp, C.POINTER(MGParams)]
     L.gls_mg_detach.argtypes = [vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
+    L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
     _lib = L
     return L
 
@@ -315,14 +317,21 @@ class GLSContext:
         return dict(newton_iterations=p.newton_iterations, linear_iterations=p.linear_iterations,
                     residual_evaluations=p.residual_evaluations, final_residual=p.final_residual)
 
-    def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6):
+    def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6,
+                         coarse_omega=0.0, coarse_direct=0):
         """GMRES right preconditioner = geometric multigrid V-cycle over [self] + coarse_levels
         (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive."""
         levels = [self] + list(coarse_levels)
         arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
-        p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega)
+        p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
+                     coarse_omega, coarse_direct)
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
+
+    def apply_preconditioner(self, v, out=None):
+        out = self.zeros() if out is None else out
+        check(self.L.gls_apply_preconditioner(self.h, _ptr(v), _ptr(out)), "gls_apply_preconditioner")
+        return out
 
     def set_lattice(self, n1d, local_to_global):
         """Declare the (rank-local) nodes as a box of the global n1d^3 hyper_cube node lattice."""

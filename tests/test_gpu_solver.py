@@ -82,3 +82,29 @@ def test_multigrid_preconditioner(k):
     assert out[True][1]["linear_iterations"] * 5 < out[False][1]["linear_iterations"], (out[True][1], out[False][1])
     nv = 3 * (k * n + 1) ** 3
     assert np.abs(out[True][0][:nv] - out[False][0][:nv]).max() < 1e-7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_multigrid_steady_two_levels(k):
+    """Steady Stokes-like regime (nu = 1) on 8^3 with one coarse level (4^3): the V-cycle
+    preconditioned Newton matches the Jacobi one."""
+    import torch
+    import bench
+    from softx_2020_200_amd.problem import CavityProblem
+    n = 8
+    out = {}
+    for mg in (False, True):
+        prob = CavityProblem(dim=3, n=n, k=k, viscosity=1.0, multigrid=mg, pre_smooth=1, post_smooth=1,
+                             omega=0.9, coarse_sweeps=100, coarse_omega=0.7, mg_coarsest=2)
+        ctx = prob.ctx
+        ctx.set_time("steady")
+        u = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.0)).cuda()
+        x = u.clone()
+        st = ctx.newton(x, tolerance=1e-10, max_iterations=8, lin_max_iterations=2000, restart=60,
+                        relative_residual=1e-8, minimum_residual=1e-14)
+        out[mg] = (x.cpu().numpy(), st)
+        assert np.isfinite(out[mg][0]).all(), (mg, st)
+    assert out[True][1]["final_residual"] < 1e-10, out[True][1]
+    nv = 3 * (k * n + 1) ** 3
+    assert np.abs(out[True][0][:nv] - out[False][0][:nv]).max() < 1e-7
