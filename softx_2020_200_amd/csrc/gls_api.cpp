@@ -285,6 +285,7 @@ struct gls_ctx {
   // solver workspace
   DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
   DevBuf<double> krylov;      // (restart+1) x n_dofs
+  DevBuf<double> zbasis;      // restart x n_dofs: M^-1 v_j when the preconditioner is the V-cycle
   int krylov_m = 0;
   DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
   bool use_brick = false;  // sum-factorized brick kernels (3D Qk-Qk, Morton 2x2x2 bricks)
@@ -315,7 +316,7 @@ struct gls_ctx {
     std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
     // per level pair (l, l+1) and axis: 1D tap tables [n_out][5] of prolongation / restriction
     struct Taps {
-      DevBuf<int32_t> pi[3], ri[3];
+      DevBuf<int32_t> pi[3], ri[3], pc[3], rc[3];
       DevBuf<double> pw[3], rw[3];
     };
     std::vector<std::unique_ptr<Taps>> taps;
@@ -491,17 +492,26 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     P.qd = c->qdata.p;
     mode = gls::MODE_JVQ;
   }
+  bool lin_diag = false;  // brick path: the diagonal comes out of the linearization pass
+  if (mode == gls::MODE_DIAG && c->use_brick && c->use_qdata) {
+    const size_t nq = gls::brick_qdata_size(c->k, c->n_cells);
+    if (c->qdata.n != nq) GLS_TRY(c->qdata.alloc(nq));
+    P.qd = c->qdata.p;
+    mode = gls::MODE_LIN;
+    lin_diag = true;
+  }
   P.v = v;
   P.y = y;
   HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
-    TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : mode);
+    TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
     if (c->use_brick && mode != gls::MODE_DIAG)
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     else
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
   GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
+  if (lin_diag) c->qd_valid = true;  // the same launch stored the J.v linearization
   return GLS_OK;
 }
 
@@ -858,10 +868,27 @@ int mg_prepare(gls_ctx *c) {
   if (mg.direct) {  // probe A = J_coarse column by column, then invert on the device
     gls_ctx *g = mg.lev[(size_t)L - 1];
     const int64_t n = g->n_dofs;
-    HIP_TRY(gls::vec_fill(mg.unit.p, n, 0.0, c->stream));
-    for (int64_t j = 0; j < n; ++j) {
-      HIP_TRY(gls::mg_unit_step(mg.unit.p, j, c->stream));
-      GLS_TRY(gls_jacobian_apply(g, mg.unit.p, mg.probe.p + j * n));
+    if (g->use_brick && g->use_qdata) {  // all unit vectors in one launch per batch
+      GLS_TRY(ensure_diag(g));
+      GLS_TRY(ensure_qdata(g));
+      gls::OpParams P = make_params(g);
+      P.qd = g->qdata.p;
+      P.y = mg.probe.p;
+      HIP_TRY(hipMemsetAsync(mg.probe.p, 0, sizeof(double) * (size_t)(n * n), c->stream));
+      const int batch = 4096;
+      for (int64_t j0 = 0; j0 < n; j0 += batch) {
+        const int nb = (int)std::min<int64_t>(batch, n - j0);
+        P.y = mg.probe.p + j0 * n;
+        HIP_TRY(gls::launch_brick_probe(g->k, P, g->tables, j0, nb, c->stream));
+        HIP_TRY(gls::mg_probe_fix(mg.probe.p + j0 * n, n, j0, nb, g->con_dofs.p, (int64_t)g->con_dofs.n, g->diag.p,
+                                  c->stream));
+      }
+    } else {
+      HIP_TRY(gls::vec_fill(mg.unit.p, n, 0.0, c->stream));
+      for (int64_t j = 0; j < n; ++j) {
+        HIP_TRY(gls::mg_unit_step(mg.unit.p, j, c->stream));
+        GLS_TRY(gls_jacobian_apply(g, mg.unit.p, mg.probe.p + j * n));
+      }
     }
     HIP_TRY(gls::mg_dense_invert(mg.probe.p, mg.aug.p, (int)n, mg.status.p, c->stream));
     int st = -1;
@@ -906,9 +933,10 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
   {
     const auto &T = *mg.taps[(size_t)l];
-    const int32_t *ti[3] = {T.ri[0].p, T.ri[1].p, T.ri[2].p};
+    const int32_t *ti[3] = {T.ri[0].p, T.ri[1].p, T.ri[2].p}, *tc[3] = {T.rc[0].p, T.rc[1].p, T.rc[2].p};
     const double *tw[3] = {T.rw[0].p, T.rw[1].p, T.rw[2].p};
-    HIP_TRY(gls::mg_transfer3d(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), ti, tw, s));
+    HIP_TRY(gls::mg_transfer3d(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), ti, tw, tc,
+                               s));
   }
   GLS_TRY(mg_from_box(c, l + 1, bc));
   GLS_TRY(dist_export_add(h, bc));
@@ -920,9 +948,9 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
   {
     const auto &T = *mg.taps[(size_t)l];
-    const int32_t *ti[3] = {T.pi[0].p, T.pi[1].p, T.pi[2].p};
+    const int32_t *ti[3] = {T.pi[0].p, T.pi[1].p, T.pi[2].p}, *tc[3] = {T.pc[0].p, T.pc[1].p, T.pc[2].p};
     const double *tw[3] = {T.pw[0].p, T.pw[1].p, T.pw[2].p};
-    HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, s));
+    HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, tc, s));
   }
   GLS_TRY(mg_from_box(c, l, y));
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
@@ -1031,7 +1059,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
       const int nf = mg.dims[l][a], nc = mg.dims[l + 1][a], ncc = (nf - 1) / (2 * K);
       std::vector<int32_t> pi((size_t)nf * 5, 0), ri((size_t)nc * 5, 0);
       std::vector<double> pw((size_t)nf * 5, 0.0), rw((size_t)nc * 5, 0.0);
-      std::vector<int> rn((size_t)nc, 0);
+      std::vector<int32_t> rn((size_t)nc, 0), pn((size_t)nf, 0);
       for (int i = 0; i < nf; ++i) {
         const double x = (double)i / (2.0 * K);
         const int cc = std::min((int)std::floor(x), ncc - 1);
@@ -1051,11 +1079,14 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
           rw[(size_t)j * 5 + rn[(size_t)j]] = L;
           ++rn[(size_t)j];
         }
+        pn[(size_t)i] = np;
       }
       GLS_TRY(T->pi[a].upload(pi.data(), pi.size()));
       GLS_TRY(T->pw[a].upload(pw.data(), pw.size()));
       GLS_TRY(T->ri[a].upload(ri.data(), ri.size()));
       GLS_TRY(T->rw[a].upload(rw.data(), rw.size()));
+      GLS_TRY(T->pc[a].upload(pn.data(), pn.size()));
+      GLS_TRY(T->rc[a].upload(rn.data(), rn.size()));
     }
     mg.taps.push_back(std::move(T));
   }
@@ -1109,6 +1140,10 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   }
   GLS_TRY(ensure_diag(c));
   if (c->mg.on) GLS_TRY(mg_prepare(c));
+  // with the V-cycle, keep Z = M^-1 V (flexible-GMRES storage): the update x += Z y then needs no
+  // extra preconditioner application per restart cycle
+  const bool keepz = c->mg.on;
+  if (keepz && c->zbasis.n != (size_t)m * n) GLS_TRY(c->zbasis.alloc((size_t)m * n));
   double *V = c->krylov.p, *z = c->tmp1.p, *r = c->tmp2.p;
   const double *dg = c->diag.p;
   hipStream_t s = c->stream;
@@ -1129,8 +1164,9 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     double res = beta;
     for (; j < m && it < prm->max_iterations; ++j) {
       double *vj = V + (int64_t)j * n, *w = V + (int64_t)(j + 1) * n;
-      GLS_TRY(apply_prec(c, vj, z));
-      GLS_TRY(gls_jacobian_apply(c, z, w));
+      double *zj = keepz ? c->zbasis.p + (int64_t)j * n : z;
+      GLS_TRY(apply_prec(c, vj, zj));
+      GLS_TRY(gls_jacobian_apply(c, zj, w));
       // h = V[0..j]^T w and ||w||^2 in one pass
       GLS_TRY(dist_multidot(c, V, n, j + 2, w, hcol.data()));
       const double wnorm0 = std::sqrt(std::max(hcol[j + 1], 0.0));
@@ -1178,10 +1214,21 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       y[i] = H[(size_t)i * m + i] != 0. ? s_ / H[(size_t)i * m + i] : 0.;
     }
     HIP_TRY(hipMemcpyAsync(c->coef.p, y.data(), sizeof(double) * kdim, hipMemcpyHostToDevice, s));
-    HIP_TRY(gls::vec_fill(r, n, 0.0, s));
-    HIP_TRY(gls::vec_multiaxpy(r, V, n, kdim, c->coef.p, -1.0, n, s));  // r = V y
-    GLS_TRY(apply_prec(c, r, z));
-    HIP_TRY(gls::vec_axpy(x, 1.0, z, n, s));
+    if (keepz) {
+      HIP_TRY(gls::vec_multiaxpy(x, c->zbasis.p, n, kdim, c->coef.p, -1.0, n, s));  // x += Z y
+    } else {
+      HIP_TRY(gls::vec_fill(r, n, 0.0, s));
+      HIP_TRY(gls::vec_multiaxpy(r, V, n, kdim, c->coef.p, -1.0, n, s));  // r = V y
+      GLS_TRY(apply_prec(c, r, z));
+      HIP_TRY(gls::vec_axpy(x, 1.0, z, n, s));
+    }
+    // converged on the recurrence estimate: done (as deal.II's SolverGMRES, which recomputes the
+    // true residual only at a restart)
+    if (res <= tol) {
+      beta = res;
+      converged = true;
+      break;
+    }
     // true residual r = b - A x
     GLS_TRY(gls_jacobian_apply(c, x, r));
     HIP_TRY(gls::vec_axpby(r, 1.0, b, -1.0, n, s));

@@ -116,7 +116,13 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int brick = blockIdx.x;
+  const int n_bricks = P.n_cells / 8;
+  // probing (MODE_JVQ): block -> (unit vector, brick); v = e_j, output column j of the batch
+  const int pj = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x / n_bricks) : 0;
+  const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks) : (int)blockIdx.x;
+  const int64_t unit_dof = (CACHED && P.n_probe > 0) ? P.probe_base + pj : -1;
+  double *const Yout = (CACHED && P.n_probe > 0)
+                           ? P.y + (int64_t)pj * ((int64_t)3 * P.n_vnodes + P.n_vnodes) : P.y;
   const int64_t voff = (int64_t)3 * P.n_vnodes;
 
   if (tid < 5 * 16) {
@@ -167,10 +173,17 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
       BF(6)[n] = h[2];
     } else if (JV) {
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
-      BF(FV)[n] = (m & 1u) ? 0.0 : P.v[i3];
-      BF(FV + 1)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
-      BF(FV + 2)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
-      BF(FV + 3)[n] = P.v[voff + node];
+      if (unit_dof >= 0) {
+        BF(FV)[n] = (m & 1u) ? 0.0 : (i3 == unit_dof ? 1.0 : 0.0);
+        BF(FV + 1)[n] = (m & 2u) ? 0.0 : (i3 + 1 == unit_dof ? 1.0 : 0.0);
+        BF(FV + 2)[n] = (m & 4u) ? 0.0 : (i3 + 2 == unit_dof ? 1.0 : 0.0);
+        BF(FV + 3)[n] = voff + node == unit_dof ? 1.0 : 0.0;
+      } else {
+        BF(FV)[n] = (m & 1u) ? 0.0 : P.v[i3];
+        BF(FV + 1)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
+        BF(FV + 2)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
+        BF(FV + 3)[n] = P.v[voff + node];
+      }
     }
   }
   __syncthreads();
@@ -391,8 +404,73 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
 #pragma unroll
       for (int c = 0; c < 3; ++c) qdw[(13 + c) * QW] = R[c];
     }
-    return;
-  }
+    if (P.y == nullptr) return;  // linearization only (uniform over the block)
+    // Jacobian diagonal from the same linearization (replaces the dense MODE_DIAG kernel): for the
+    // trial/test pair phi_i e_c (gls_navier_stokes.cc:548-622 with v = phi_i e_c)
+    //   J_ii(c) = sum_q JxW [A phi + nu |grad phi|^2 + tau (A - nu lap phi) a + tau R_c phi d_c phi],
+    //   A = (du_c/dx_c + alpha_jac) phi + a,  a = u . grad phi;   J_ii(p) = sum_q JxW tau |grad psi|^2
+    // with deal.II's |K_e(i,i)| on constrained rows. Lane <-> node i of its cell, loop over q.
+    if (pact) {
+      X(pci, 0)[me] = u[0];
+      X(pci, 1)[me] = u[1];
+      X(pci, 2)[me] = u[2];
+      X(pci, 3)[me] = gu[0][0] + P.alpha_jac;
+      X(pci, 4)[me] = gu[1][1] + P.alpha_jac;
+      Yr(pci, 0)[me] = gu[2][2] + P.alpha_jac;
+      Yr(pci, 1)[me] = tau;
+      Yr(pci, 2)[me] = R[0];
+      Yr(pci, 3)[me] = R[1];
+      Yr(pci, 4)[me] = R[2];
+      Yr(pci, 5)[me] = JxW;
+    }
+    wave_sync();
+    if (pact) {
+      double V0[K1], D0[K1], S0[K1];  // x-direction table column of this lane's node (registers)
+#pragma unroll
+      for (int t = 0; t < K1; ++t) {
+        V0[t] = sM[0 * 16 + t * 4 + i0];
+        D0[t] = sM[1 * 16 + t * 4 + i0] * ih[0];
+        S0[t] = sM[2 * 16 + t * 4 + i0] * ih[0] * ih[0];
+      }
+      double acc[4] = {0., 0., 0., 0.};
+#pragma nounroll
+      for (int a2 = 0; a2 < K1; ++a2) {
+        const double b2 = sM[0 * 16 + a2 * 4 + i2], d2 = sM[16 + a2 * 4 + i2] * ih[2];
+        const double s2 = sM[32 + a2 * 4 + i2] * ih[2] * ih[2];
+#pragma nounroll
+        for (int a1 = 0; a1 < K1; ++a1) {
+          const double b1 = sM[0 * 16 + a1 * 4 + i1], d1 = sM[16 + a1 * 4 + i1] * ih[1];
+          const double s1 = sM[32 + a1 * 4 + i1] * ih[1] * ih[1];
+#pragma unroll
+          for (int a0 = 0; a0 < K1; ++a0) {
+            const int qq = a0 + K1 * (a1 + K1 * a2);
+            const double b0 = V0[a0];
+            const double phi = b0 * b1 * b2;
+            const double g[3] = {D0[a0] * b1 * b2, b0 * d1 * b2, b0 * b1 * d2};
+            const double lap = S0[a0] * b1 * b2 + b0 * s1 * b2 + b0 * b1 * s2;
+            const double uq[3] = {X(pci, 0)[qq], X(pci, 1)[qq], X(pci, 2)[qq]};
+            const double gc[3] = {X(pci, 3)[qq], X(pci, 4)[qq], Yr(pci, 0)[qq]};
+            const double tq = Yr(pci, 1)[qq], jw = Yr(pci, 5)[qq];
+            const double Rq[3] = {Yr(pci, 2)[qq], Yr(pci, 3)[qq], Yr(pci, 4)[qq]};
+            const double av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
+            const double g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const double A = gc[c] * phi + av;
+              acc[c] += jw * (A * phi + nu * g2 + tq * (A - nu * lap) * av + tq * Rq[c] * phi * g[c]);
+            }
+            acc[3] += jw * tq * g2;
+          }
+        }
+      }
+      // deal.II's constrained-row rule: |K_e(i,i)| summed over cells
+      const int bn = (K * cxb + i0) + BN * ((K * cyb + i1) + BN * (K * czb + i2));
+      const unsigned msk = P.vmask ? P.vmask[sNode[bn]] : 0u;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Out(pci, c)[me] = (msk >> c) & 1u ? fabs(acc[c]) : acc[c];
+      Out(pci, 3)[me] = acc[3];
+    }
+  } else {
 
   double Tc[16];
   if constexpr (!JV) {  // residual test coefficients (rhs = -R)
@@ -491,6 +569,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
   }
+  }  // !LIN
   __syncthreads();
 
   // ---------------- brick reduction (fixed order) + scatter
@@ -518,9 +597,9 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     const int64_t gi = fld < 3 ? (int64_t)node * 3 + fld : voff + node;
     const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
     if (GLS_ABL & 2) {
-      if (s == 123.456) P.y[gi] = s;
-    } else if (interior) P.y[gi] = s;
-    else atomicAdd(&P.y[gi], s);
+      if (s == 123.456) Yout[gi] = s;
+    } else if (interior) Yout[gi] = s;
+    else atomicAdd(&Yout[gi], s);
   }
 }
 
@@ -552,6 +631,25 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   else
     hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
   return hipGetLastError();
+}
+
+// J e_j for j in [j0, j0 + nprobe) into Y[(j - j0) * n_dofs + :] (Y zeroed by the caller)
+template <int K>
+hipError_t launch_brick_probe_t(const OpParams &P0, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s) {
+  using C = BrickCfg<K>;
+  const int n_bricks = P0.n_cells / 8;
+  if (n_bricks <= 0 || nprobe <= 0) return hipSuccess;
+  OpParams P = P0;
+  P.n_probe = nprobe;
+  P.probe_base = j0;
+  hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ>), dim3((unsigned)((int64_t)n_bricks * nprobe)), dim3(C::THREADS),
+                     brick_lds_bytes<K>(MODE_JVQ), s, P, T);
+  return hipGetLastError();
+}
+hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s) {
+  if (k == 1) return launch_brick_probe_t<1>(P, T, j0, nprobe, s);
+  if (k == 2) return launch_brick_probe_t<2>(P, T, j0, nprobe, s);
+  return hipErrorNotSupported;
 }
 
 size_t brick_qdata_size(int k, int n_cells) {

@@ -44,6 +44,8 @@ struct OpParams {
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input
   double *qd;                 // MODE_LIN output / MODE_JVQ input (brick wave-major layout)
+  int n_probe;                // MODE_JVQ probing: > 0 -> block b computes J e_(probe_base + b / n_bricks)
+  int64_t probe_base;         //   into y + (b / n_bricks) * n_dofs (v unused)
   double *y;                  // output (accumulated with atomics)
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs

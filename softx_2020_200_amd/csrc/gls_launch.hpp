@@ -10,6 +10,8 @@ bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
+// batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
+hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 
 // ---- BLAS-1 style kernels on device vectors (gls_vector_kernels.hip)
 hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s);
@@ -38,9 +40,10 @@ int multidot_work_size();
 
 // ---- geometric multigrid (gls_mg_kernels.hip): nested Qk node lattices (boxes), k <= 2
 hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s);
-// one-pass 3D transfer with per-axis tap tables [n_out][5] (index, weight; weight 0 = unused)
+// one-pass 3D transfer with per-axis tap tables [n_out][5] (index, weight) and tap counts [n_out]
 hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const int nout[3],
-                         const int32_t *const taps[3], const double *const w[3], hipStream_t s);
+                         const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
+                         hipStream_t s);
 hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
                          int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes
 hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,
@@ -48,6 +51,9 @@ hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, in
 // coarsest-level direct solve: invert the probed matrix (Y column-major) into aug = [I | A^-1]
 hipError_t mg_dense_invert(const double *Y, double *aug, int n, int *status, hipStream_t s);  // status: dropped columns
 hipError_t mg_unit_step(double *e, int64_t j, hipStream_t s);  // e[j-1] = 0, e[j] = 1
+// probed columns: constrained rows of column j become D_c(j) delta_ij (gls_jacobian_apply's rule)
+hipError_t mg_probe_fix(double *Y, int64_t n, int64_t j0, int nprobe, const int64_t *con, int64_t ncon, const double *d,
+                        hipStream_t s);
 hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, hipStream_t s);
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s);

@@ -14,33 +14,33 @@ namespace gls {
 
 namespace {
 
-// Direct 3D transfer: out[o] = sum over the tensor product of per-axis taps (<= kMaxTaps each,
-// weight 0 pads) of w_x w_y w_z in[i]; velocity (3 interleaved) and pressure in one pass. The tap
-// tables are the 1D prolongation (fine <- coarse) or its transpose (restriction) per axis.
+// Direct 3D transfer: out[o] = sum over the tensor product of per-axis taps of w_x w_y w_z in[i];
+// velocity (3 interleaved) and pressure in one pass. The tap tables are the 1D prolongation
+// (fine <- coarse) or its transpose (restriction) per axis: [n_out][kMaxTaps] (index, weight),
+// nonzero taps first, their count in cnt[n_out]. 32-bit lattice indices (boxes < 2^31 nodes).
 constexpr int kMaxTaps = 5;
 __global__ void __launch_bounds__(256) k_transfer3d(const double *__restrict__ in, double *__restrict__ out, int i0,
                                                     int i1, int i2, int o0, int o1, int o2,
                                                     const int32_t *__restrict__ tx, const double *__restrict__ wx,
-                                                    const int32_t *__restrict__ ty, const double *__restrict__ wy,
-                                                    const int32_t *__restrict__ tz, const double *__restrict__ wz) {
-  const int64_t nin = (int64_t)i0 * i1 * i2, nout = (int64_t)o0 * o1 * o2;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nout; t += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(t % o0), y = (int)((t / o0) % o1), z = (int)(t / ((int64_t)o0 * o1));
+                                                    const int32_t *__restrict__ cx, const int32_t *__restrict__ ty,
+                                                    const double *__restrict__ wy, const int32_t *__restrict__ cy,
+                                                    const int32_t *__restrict__ tz, const double *__restrict__ wz,
+                                                    const int32_t *__restrict__ cz) {
+  const int nin = i0 * i1 * i2, nout = o0 * o1 * o2;
+  const int plane = o0 * o1;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nout; t += gridDim.x * blockDim.x) {
+    const int z = t / plane, r = t - z * plane, y = r / o0, x = r - y * o0;
+    const int nzz = cz[z], nyy = cy[y], nxx = cx[x];
     double s0 = 0., s1 = 0., s2 = 0., sp = 0.;
-    for (int c = 0; c < kMaxTaps; ++c) {
+    for (int c = 0; c < nzz; ++c) {
       const double az = wz[z * kMaxTaps + c];
-      if (az == 0.0) continue;
-      const int64_t bz = (int64_t)tz[z * kMaxTaps + c] * i1;
-      for (int b = 0; b < kMaxTaps; ++b) {
-        const double ay = wy[y * kMaxTaps + b];
-        if (ay == 0.0) continue;
-        const int64_t by = (bz + ty[y * kMaxTaps + b]) * i0;
-        const double ayz = ay * az;
-        for (int a = 0; a < kMaxTaps; ++a) {
-          const double ax = wx[x * kMaxTaps + a];
-          if (ax == 0.0) continue;
-          const int64_t n = by + tx[x * kMaxTaps + a];
-          const double w = ax * ayz;
+      const int bz = tz[z * kMaxTaps + c] * i1;
+      for (int b = 0; b < nyy; ++b) {
+        const double ayz = wy[y * kMaxTaps + b] * az;
+        const int by = (bz + ty[y * kMaxTaps + b]) * i0;
+        for (int a = 0; a < nxx; ++a) {
+          const int n = by + tx[x * kMaxTaps + a];
+          const double w = wx[x * kMaxTaps + a] * ayz;
           s0 += w * in[3 * n];
           s1 += w * in[3 * n + 1];
           s2 += w * in[3 * n + 2];
@@ -215,11 +215,13 @@ int grid_for(int64_t n) {
 }  // namespace
 
 hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const int nout[3],
-                         const int32_t *const taps[3], const double *const w[3], hipStream_t s) {
+                         const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
+                         hipStream_t s) {
   const int64_t n = (int64_t)nout[0] * nout[1] * nout[2];
   const int64_t b = (n + 255) / 256;
   hipLaunchKernelGGL(k_transfer3d, dim3((int)(b < 65536 ? (b > 0 ? b : 1) : 65536)), dim3(256), 0, s, in, out, nin[0],
-                     nin[1], nin[2], nout[0], nout[1], nout[2], taps[0], w[0], taps[1], w[1], taps[2], w[2]);
+                     nin[1], nin[2], nout[0], nout[1], nout[2], taps[0], w[0], cnt[0], taps[1], w[1], cnt[1], taps[2],
+                     w[2], cnt[2]);
   return hipGetLastError();
 }
 
@@ -249,6 +251,21 @@ __global__ void k_unit(double *e, int64_t j) {  // e_{j-1} -> e_j (probing)
 }
 hipError_t mg_unit_step(double *e, int64_t j, hipStream_t s) {
   hipLaunchKernelGGL(k_unit, dim3(1), dim3(64), 0, s, e, j);
+  return hipGetLastError();
+}
+
+__global__ void k_probe_fix(double *Y, int64_t n, int64_t j0, int nprobe, const int64_t *con, int64_t ncon,
+                            const double *d) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= (int64_t)nprobe * ncon) return;
+  const int64_t j = t / ncon, c = con[t % ncon];
+  Y[j * n + c] = (c == j0 + j) ? d[c] : 0.0;
+}
+hipError_t mg_probe_fix(double *Y, int64_t n, int64_t j0, int nprobe, const int64_t *con, int64_t ncon, const double *d,
+                        hipStream_t s) {
+  const int64_t tot = (int64_t)nprobe * ncon;
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_fix, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Y, n, j0, nprobe, con, ncon, d);
   return hipGetLastError();
 }
 

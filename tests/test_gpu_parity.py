@@ -162,6 +162,8 @@ def test_brick_kernels_vs_oracle(case):
     ctx.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))
     orc = Oracle(p)
     assert relerr(ctx.residual().cpu().numpy(), orc.residual(u, u1, u2, u3)) < TOL
+    # the brick path derives the diagonal in the linearization pass (incl. |K_ii| on constrained rows)
+    assert relerr(ctx.jacobian_diagonal().cpu().numpy(), orc.jacobian_diagonal(u, u1, u2, u3)) < TOL
     assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1, u2, u3)) < TOL
 
 
@@ -175,6 +177,7 @@ def test_brick_periodic_wrap():
     ctx.set_state(cuda(u), cuda(u1))
     orc = Oracle(p)
     assert relerr(ctx.residual().cpu().numpy(), orc.residual(u, u1)) < TOL
+    assert relerr(ctx.jacobian_diagonal().cpu().numpy(), orc.jacobian_diagonal(u, u1)) < TOL
     assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1)) < TOL
 
 

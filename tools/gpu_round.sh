@@ -14,7 +14,6 @@ echo "pytest rc=$rc" >> $O/round.log
 timeout -k 10 120 python tools/jv_bench.py 128 20 > $O/jv.log 2>&1 || stop jv_bench $?
 GLS_JV_RECOMPUTE=1 timeout -k 10 120 python tools/jv_bench.py 128 20 >> $O/jv.log 2>&1 || stop jv_bench_recompute $?
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 > $O/bench.json 2> $O/bench.err || stop bench $?
-timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --mg-smooth 1 1 > $O/bench_v11.json 2>> $O/bench.err || stop bench_v11 $?
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/prof_bench.log 2>&1 || stop rocprof_stats $?
