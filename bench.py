@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--mg-omega", type=float, default=0.9)
     ap.add_argument("--mg-coarse-sweeps", type=int, default=100)
     ap.add_argument("--mg-coarse-omega", type=float, default=0.7, help="0 = --mg-omega")
+    ap.add_argument("--mg-precision", default="f32", choices=["f32", "f64"],
+                    help="arithmetic of the V-cycle's J.v (f32: FP32 linearization + FP32 sweeps; the outer "
+                         "GMRES operator, Newton residual and all vectors stay FP64)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
@@ -157,7 +160,8 @@ def main():
         prob = CavityProblem(dim=3, n=args.n, k=args.k, kp=args.kp, viscosity=args.nu,
                              multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
                              pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
-                             coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega)
+                             coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega,
+                             mixed_precision=args.mg_precision == "f32")
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -183,7 +187,8 @@ def main():
                                              dirichlet=(dd, dv), backend=args.dist_backend))
             attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
                                          omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
-                                         coarse_omega=args.mg_coarse_omega)
+                                         coarse_omega=args.mg_coarse_omega,
+                                         mixed_precision=args.mg_precision == "f32")
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
@@ -215,6 +220,7 @@ def main():
     res_ms, res_n = ctx.timing_get(0)
     dg_ms, dg_n = ctx.timing_get(2)
     lin_ms, lin_n = ctx.timing_get(3)
+    f32_ms, f32_n = ctx.timing_get(4)
     ctx.timing(False)
     # dedicated back-to-back J.v launches on the same state for a clean per-launch duration
     ctx.set_state(present, m1, m2)
@@ -276,11 +282,14 @@ def main():
         "residual_evaluations_per_step": float(np.mean(nres)),
         "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),
                       "diagonal": dg_ms / max(dg_n, 1), "jv_linearization": lin_ms / max(lin_n, 1),
+                      "smoother_jv_f32": f32_ms / max(f32_n, 1),
                       "launches_per_step": {"jacobian_apply": jv_n / args.steps, "residual": res_n / args.steps,
-                                            "diagonal": dg_n / args.steps, "jv_linearization": lin_n / args.steps},
+                                            "diagonal": dg_n / args.steps, "jv_linearization": lin_n / args.steps,
+                                            "smoother_jv_f32": f32_n / args.steps},
                       "share_of_step": {"jacobian_apply": jv_ms / (1e3 * elapsed),
                                         "residual": res_ms / (1e3 * elapsed), "diagonal": dg_ms / (1e3 * elapsed),
-                                        "jv_linearization": lin_ms / (1e3 * elapsed)}},
+                                        "jv_linearization": lin_ms / (1e3 * elapsed),
+                                        "smoother_jv_f32": f32_ms / (1e3 * elapsed)}},
         "roofline": {"bound": "hbm", "kernel": "gls_brick_kernel<%d,MODE_JVQ>" % args.k if ctx.uses_brick_kernels
                      else "gls_cell_kernel<3,%d,%d,%d,MODE_JV>" % (args.k, args.kp, args.k + 1), "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

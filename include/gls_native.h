@@ -105,6 +105,12 @@ int gls_residual(gls_ctx *ctx, double *rhs);
  * Replaces system_matrix.vmult inside Trilinos GMRES (gls_navier_stokes.cc:1276-1279). */
 int gls_jacobian_apply(gls_ctx *ctx, const double *v, double *Jv);
 
+/* The same operator evaluated in FP32 arithmetic from an FP32 copy of the linearization (3D
+ * Qk-Qk brick path only; v, Jv are FP64 DEVICE vectors): the operator the mixed-precision
+ * multigrid V-cycle smooths with (gls_mg_params.mixed_precision). Not a reference interface: a
+ * preconditioner-internal operator, exposed for parity tests (relative error ~1e-6). */
+int gls_jacobian_apply_f32(gls_ctx *ctx, const double *v, double *Jv);
+
 /* Diagonal of that assembled Jacobian (DEVICE pointer). */
 int gls_jacobian_diagonal(gls_ctx *ctx, double *diag);
 
@@ -147,6 +153,10 @@ typedef struct {
   double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
                                                  with <= 2048 DoFs), 1 exact solve, -1 Jacobi sweeps */
+  int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
+                                                 arithmetic from an FP32 copy of the linearization
+                                                 (brick path; vectors, transfers and the outer GMRES
+                                                 operator stay FP64). 0: all FP64 */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
@@ -266,7 +276,8 @@ int gls_pvd_write(const char *filename, int n, const double *times, const char *
  * Profiling hooks: time the next operator launches on the context stream with HIP events.
  * ------------------------------------------------------------------------------------------ */
 int gls_timing_reset(gls_ctx *ctx);
-/* which: 0 residual, 1 jacobian_apply, 2 diagonal, 3 J.v linearization (once per state);
+/* which: 0 residual, 1 jacobian_apply, 2 diagonal, 3 J.v linearization (once per state),
+ * 4 FP32 J.v of the mixed-precision V-cycle;
  * returns total ms and launch count */
 int gls_timing_get(gls_ctx *ctx, int which, double *total_ms, int64_t *count);
 int gls_timing_enable(gls_ctx *ctx, int enable);

@@ -281,6 +281,9 @@ struct gls_ctx {
   bool diag_valid = false;
   DevBuf<double> qdata;   // brick J.v linearization at the quadrature points (MODE_LIN output)
   bool qd_valid = false;  // invalidated with the diagonal by every state / parameter change
+  DevBuf<float> qdata32;  // FP32 copy of qdata: the multigrid smoother's J.v (mixed precision)
+  bool qd32_valid = false;  // stale whenever qdata is recomputed
+  bool smooth_f32 = false;  // this level's V-cycle J.v runs in FP32 (gls_mg_params.mixed_precision)
   bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
   // solver workspace
   DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
@@ -331,8 +334,8 @@ struct gls_ctx {
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
   std::vector<Ev> events;
-  double t_ms[4] = {0, 0, 0, 0};  // residual, J.v, diagonal, J.v linearization
-  int64_t t_n[4] = {0, 0, 0, 0};
+  double t_ms[5] = {0, 0, 0, 0, 0};  // residual, J.v, diagonal, J.v linearization, FP32 smoother J.v
+  int64_t t_n[5] = {0, 0, 0, 0, 0};
 
   ~gls_ctx() {
     for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -477,6 +480,7 @@ int ensure_qdata(gls_ctx *c) {
     HIP_TRY(gls::launch_brick_kernel(c->k, gls::MODE_LIN, P, c->tables, c->stream));
   }
   c->qd_valid = true;
+  c->qd32_valid = false;
   return GLS_OK;
 }
 
@@ -511,7 +515,10 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
   GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
-  if (lin_diag) c->qd_valid = true;  // the same launch stored the J.v linearization
+  if (lin_diag) {  // the same launch stored the J.v linearization
+    c->qd_valid = true;
+    c->qd32_valid = false;
+  }
   return GLS_OK;
 }
 
@@ -779,6 +786,46 @@ int gls_jacobian_apply(gls_ctx *c, const double *v, double *y) {
   return GLS_OK;
 }
 
+namespace {
+// the V-cycle's operator on level g: J.v in FP32 arithmetic from the FP32 linearization when the
+// level smooths in mixed precision (brick path), else the FP64 gls_jacobian_apply. Same
+// constraint handling (constrained rows D_c v) and ghost exchange as gls_jacobian_apply.
+int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
+  if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  GLS_TRY(ensure_diag(g));
+  GLS_TRY(ensure_qdata(g));
+  if (!g->qd32_valid) {
+    if (g->qdata32.n != g->qdata.n) GLS_TRY(g->qdata32.alloc(g->qdata.n));
+    HIP_TRY(gls::vec_to_f32(g->qdata.p, g->qdata32.p, (int64_t)g->qdata.n, g->stream));
+    g->qd32_valid = true;
+  }
+  GLS_TRY(dist_import(g, const_cast<double *>(v)));
+  gls::OpParams P = make_params(g);
+  P.qdf = g->qdata32.p;
+  P.v = v;
+  P.y = y;
+  HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
+  {
+    TimedLaunch t(g, 4);
+    HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
+  }
+  GLS_TRY(dist_export_add(g, y));
+  HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream));
+  return GLS_OK;
+}
+int smoother_apply(gls_ctx *g, const double *v, double *y) {
+  if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y);
+  return gls_jacobian_apply(g, v, y);
+}
+}  // namespace
+
+int gls_jacobian_apply_f32(gls_ctx *c, const double *v, double *y) {
+  GLS_TRY(check_ctx(c));
+  if (!v || !y || v == y) return set_err(GLS_EINVAL, "v/y null or aliased");
+  if (!(c->use_brick && c->use_qdata)) return set_err(GLS_EINVAL, "FP32 J.v needs the 3D Qk-Qk brick path");
+  return jacobian_apply_f32(c, v, y);
+}
+
 int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *vals) {
   GLS_TRY(check_ctx(c));
   if (n < 0 || (n > 0 && (!dofs || !vals))) return set_err(GLS_EINVAL, "dirichlet arrays");
@@ -920,12 +967,12 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   const double om = l == L - 1 ? mg.comega : mg.omega;
   HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
   for (int it = 1; it < pre; ++it) {
-    GLS_TRY(gls_jacobian_apply(g, x, y));
+    GLS_TRY(smoother_apply(g, x, y));
     HIP_TRY(gls::mg_jacobi_update(x, b, y, d, om, n, 0, s));
   }
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
-  GLS_TRY(gls_jacobian_apply(g, x, y));
+  GLS_TRY(smoother_apply(g, x, y));
   HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
   gls_ctx *h = mg.lev[l + 1];
   double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
@@ -956,7 +1003,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
   for (int it = 0; it < mg.post; ++it) {
-    GLS_TRY(gls_jacobian_apply(g, x, y));
+    GLS_TRY(smoother_apply(g, x, y));
     HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
   }
   return GLS_OK;
@@ -1044,6 +1091,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
   mg.omega = p->omega > 0 ? p->omega : 0.6;
   mg.comega = p->coarse_omega > 0 ? p->coarse_omega : mg.omega;
+  for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
@@ -1113,6 +1161,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
 
 int gls_mg_detach(gls_ctx *c) {
   GLS_TRY(check_ctx(c));
+  for (auto *g : c->mg.lev) g->smooth_f32 = false;
   c->mg = gls_ctx::MG();
   return GLS_OK;
 }
@@ -1481,12 +1530,12 @@ int gls_timing_reset(gls_ctx *c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   c->events.clear();
-  for (int i = 0; i < 4; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
+  for (int i = 0; i < 5; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
   return GLS_OK;
 }
 int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
   GLS_TRY(check_ctx(c));
-  if (which < 0 || which > 3) return set_err(GLS_EINVAL, "which");
+  if (which < 0 || which > 4) return set_err(GLS_EINVAL, "which");
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) {
     float t = 0;

@@ -23,6 +23,9 @@
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
 
+#include <algorithm>
+#include <type_traits>
+
 #ifndef GLS_ABL
 #define GLS_ABL 0  // timing-only ablations: 1 no global gather, 2 no scatter, 4 no sweeps
 #endif
@@ -97,7 +100,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int K, int MODE>
+template <int K, int MODE, typename Real = double>
 __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
   constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
@@ -107,10 +110,11 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]; JVQ: v0 v1 v2 vp only
   constexpr int NF = CACHED ? 4 : (JV ? 11 : 7);
   constexpr int FV = CACHED ? 0 : 7;         // first v field
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  double *sB = smem;                                   // [NF][BN3]
-  double *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
-  double *sM = sC + 8 * C::PER_CELL * N3;             // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4]
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  Real *const smem = reinterpret_cast<Real *>(smem_raw);
+  Real *sB = smem;                                   // [NF][BN3]
+  Real *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
+  Real *sM = sC + 8 * C::PER_CELL * N3;             // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4]
   int *sNode = reinterpret_cast<int *>(sM + 5 * 16 + 8);  // [BN3]
   auto BF = [&](int f) { return sB + f * BN3; };
 
@@ -127,7 +131,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
 
   if (tid < 5 * 16) {
     const int mat = tid >> 4, r = (tid >> 2) & 3, c = tid & 3;
-    double v = 0.;
+    Real v = 0.;
     if (r < K1 && c < K1) {
       if (mat == 0) v = T.V[r][c];
       else if (mat == 1) v = T.D[r][c];
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
       BF(2)[n] = P.u[i3 + 2];
       BF(3)[n] = P.u[voff + node];
     } else if (g == 1) {
-      double h[3] = {0., 0., 0.};
+      Real h[3] = {0., 0., 0.};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         if (P.n_hist > 0) h[c] += P.alpha[1] * P.h1[i3 + c];
@@ -199,11 +203,11 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   const int q = pact ? lane % N3 : 0;
   const int qx = q % K1, qy = (q / K1) % K1, qz = q / (K1 * K1);
   const int gcell = brick * 8 + pci;
-  const double hx = P.geo[gcell * 4 + 0], hy = P.geo[gcell * 4 + 1], hz = P.geo[gcell * 4 + 2];
-  const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
-  const double wz = ih[2] * ih[2];
+  const Real hx = P.geo[gcell * 4 + 0], hy = P.geo[gcell * 4 + 1], hz = P.geo[gcell * 4 + 2];
+  const Real ih[3] = {Real(1) / hx, Real(1) / hy, Real(1) / hz};
+  const Real wz = ih[2] * ih[2];
   // this lane's rows of the z matrices (q-dependent -> registers; tables staged in LDS above)
-  double Bz[K1], Dz[K1], Sz[K1];
+  Real Bz[K1], Dz[K1], Sz[K1];
 #pragma unroll
   for (int i = 0; i < K1; ++i) { Bz[i] = sM[0 * 16 + qz * 4 + i]; Dz[i] = sM[1 * 16 + qz * 4 + i]; Sz[i] = sM[2 * 16 + qz * 4 + i]; }
 
@@ -215,36 +219,36 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   // brick x-line base of this lane's (cell, y=i1, z=i2) line
   const int cxb = pci & 1, cyb = (pci >> 1) & 1, czb = pci >> 2;
   const int bx_base = K * cxb + BN * (K * cyb + i1) + BN * BN * (K * czb + i2);
-  auto row = [&](int mat, int r, double (&o)[K1]) {  // o[k] = M[r][k], mat: 0 V, 1 D, 2 S, 3 V^T, 4 D^T
-    const double *m = sM + mat * 16 + r * 4;
+  auto row = [&](int mat, int r, Real (&o)[K1]) {  // o[k] = M[r][k], mat: 0 V, 1 D, 2 S, 3 V^T, 4 D^T
+    const Real *m = sM + mat * 16 + r * 4;
 #pragma unroll
     for (int k = 0; k < K1; ++k) o[k] = m[k];
   };
-  auto dot = [&](const double (&a)[K1], const double (&b)[K1]) {
-    double s = 0.;
+  auto dot = [&](const Real (&a)[K1], const Real (&b)[K1]) {
+    Real s = 0.;
 #pragma unroll
     for (int k = 0; k < K1; ++k) s += a[k] * b[k];
     return s;
   };
   // line of array A through this lane's element along dim D
-  auto lineD0 = [&](const double *A, double (&o)[K1]) {
+  auto lineD0 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
     for (int e = 0; e < K1; ++e) o[e] = A[e + K1 * (i1 + K1 * i2)];
   };
-  auto lineD1 = [&](const double *A, double (&o)[K1]) {
+  auto lineD1 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
     for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (e + K1 * i2)];
   };
-  auto lineD2 = [&](const double *A, double (&o)[K1]) {
+  auto lineD2 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
     for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (i1 + K1 * e)];
   };
 
   // velocity-type field (value, grad, Laplacian): brick field f -> (val, g0, g1, g2, lap) for this lane
-  auto vel_field = [&](int f, double &val, double (&g)[3], double &lap) {
+  auto vel_field = [&](int f, Real &val, Real (&g)[3], Real &lap) {
     if (GLS_ABL & 4) { val = BF(f)[bx_base]; g[0] = g[1] = g[2] = val; lap = val; return; }
     if (pact) {  // x sweep: X_B, X_D, X_S at [i2][i1][i0]
-      double in[K1], r[K1];
+      Real in[K1], r[K1];
 #pragma unroll
       for (int e = 0; e < K1; ++e) in[e] = BF(f)[bx_base + e];
       row(0, i0, r);
@@ -256,7 +260,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // y sweep: BB, BD, DB, L = wy S_y(X_B) + wx B_y(X_S)
-      double xb[K1], xd[K1], xs[K1], rb[K1], rd[K1], rs[K1];
+      Real xb[K1], xd[K1], xs[K1], rb[K1], rd[K1], rs[K1];
       lineD1(X(pci, 0), xb);
       lineD1(X(pci, 1), xd);
       lineD1(X(pci, 2), xs);
@@ -270,7 +274,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // z sweep fused into the pointwise read
-      double bb[K1], bd[K1], db[K1], ll[K1];
+      Real bb[K1], bd[K1], db[K1], ll[K1];
       lineD2(Yr(pci, 0), bb);
       lineD2(Yr(pci, 1), bd);
       lineD2(Yr(pci, 2), db);
@@ -285,10 +289,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   };
 
   // pressure-type field (value, grad) [+ up to 3 value-only fields]: fp -> (pv, pg); fh.. -> hv[]
-  auto scal_fields = [&](int fp, int nh, int fh0, double &pv, double (&pg)[3], double (&hv)[3]) {
+  auto scal_fields = [&](int fp, int nh, int fh0, Real &pv, Real (&pg)[3], Real (&hv)[3]) {
     if (GLS_ABL & 4) { pv = BF(fp)[bx_base]; pg[0] = pg[1] = pg[2] = pv; for (int j = 0; j < nh; ++j) hv[j] = pv; return; }
     if (pact) {  // x: p -> X0 (B), X1 (D); H_j -> X(2+j) (B)
-      double in[K1], rb[K1], rd[K1];
+      Real in[K1], rb[K1], rd[K1];
       row(0, i0, rb);
       row(1, i0, rd);
 #pragma unroll
@@ -303,7 +307,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // y: X0 -> BB (Y0), BD (Y1); X1 -> DB (Y2); X(2+j) -> Y(3+j)
-      double a[K1], rb[K1], rd[K1];
+      Real a[K1], rb[K1], rd[K1];
       row(0, i1, rb);
       row(1, i1, rd);
       lineD1(X(pci, 0), a);
@@ -318,7 +322,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {
-      double bb[K1], bd[K1], db[K1];
+      Real bb[K1], bd[K1], db[K1];
       lineD2(Yr(pci, 0), bb);
       lineD2(Yr(pci, 1), bd);
       lineD2(Yr(pci, 2), db);
@@ -334,15 +338,20 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     wave_sync();
   };
 
-  const double nu = P.nu;
-  const double JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
+  const Real nu = P.nu;
+  const Real JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
   // linearization storage: per wave CPW*N3 lanes x kQData values, value-major (coalesced)
   constexpr int QW = CPW * N3;
-  double *qdw = P.qd ? P.qd + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane : nullptr;
+  Real *qdw = nullptr;
+  if constexpr (std::is_same<Real, double>::value) {
+    if (P.qd) qdw = P.qd + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane;
+  } else {
+    if (P.qdf) qdw = P.qdf + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane;
+  }
 
   // ---------------- phase A: state at this lane's quadrature point
-  double u[3] = {0., 0., 0.}, gu[3][3] = {}, R[3] = {0., 0., 0.}, tau = 0.;
-  double pq = 0., f[3] = {0., 0., 0.}, Tt[3] = {0., 0., 0.}, srf[3] = {0., 0., 0.};
+  Real u[3] = {0., 0., 0.}, gu[3][3] = {}, R[3] = {0., 0., 0.}, tau = 0.;
+  Real pq = 0., f[3] = {0., 0., 0.}, Tt[3] = {0., 0., 0.}, srf[3] = {0., 0., 0.};
   // JVQ: the linearization is loaded after the v sweeps (short live ranges: no spills)
   auto load_qd = [&]() {
     if (pact) {
@@ -356,16 +365,16 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
   };
   if constexpr (!CACHED) {
-  double lu[3] = {0., 0., 0.};
+  Real lu[3] = {0., 0., 0.};
 #pragma unroll
   for (int c = 0; c < 3; ++c) vel_field(c, u[c], gu[c], lu[c]);
-  double gp[3] = {0., 0., 0.}, Hq[3] = {0., 0., 0.};
+  Real gp[3] = {0., 0., 0.}, Hq[3] = {0., 0., 0.};
   scal_fields(3, 3, 4, pq, gp, Hq);
 
-  const double hst = P.geo[gcell * 4 + 3];
-  const double un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
-  const double u_mag = fmax(sqrt(un2), 1e-12);
-  const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
+  const Real hst = P.geo[gcell * 4 + 3];
+  const Real un2 = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+  const Real u_mag = fmax(sqrt(un2), 1e-12);
+  const Real t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
   tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
   if (P.force_q && pact) {
 #pragma unroll
@@ -375,12 +384,12 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   for (int c = 0; c < 3; ++c)
     R[c] = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2] + gp[c] - nu * lu[c] - f[c];
   if (P.srf) {
-    const double *om = P.omega;
-    const double xq[3] = {P.x0[gcell * 3 + 0] + hx * sM[84 + qx], P.x0[gcell * 3 + 1] + hy * sM[84 + qy],
+    const Real *om = P.omega;
+    const Real xq[3] = {P.x0[gcell * 3 + 0] + hx * sM[84 + qx], P.x0[gcell * 3 + 1] + hy * sM[84 + qy],
                           P.x0[gcell * 3 + 2] + hz * sM[84 + qz]};
-    const double cx_[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
-    const double ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2], om[0] * xq[1] - om[1] * xq[0]};
-    const double cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
+    const Real cx_[3] = {om[1] * u[2] - om[2] * u[1], om[2] * u[0] - om[0] * u[2], om[0] * u[1] - om[1] * u[0]};
+    const Real ox[3] = {om[1] * xq[2] - om[2] * xq[1], om[2] * xq[0] - om[0] * xq[2], om[0] * xq[1] - om[1] * xq[0]};
+    const Real cc[3] = {om[1] * ox[2] - om[2] * ox[1], om[2] * ox[0] - om[0] * ox[2], om[0] * ox[1] - om[1] * ox[0]};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       srf[c] = 2 * cx_[c] + cc[c];
@@ -425,38 +434,38 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {
-      double V0[K1], D0[K1], S0[K1];  // x-direction table column of this lane's node (registers)
+      Real V0[K1], D0[K1], S0[K1];  // x-direction table column of this lane's node (registers)
 #pragma unroll
       for (int t = 0; t < K1; ++t) {
         V0[t] = sM[0 * 16 + t * 4 + i0];
         D0[t] = sM[1 * 16 + t * 4 + i0] * ih[0];
         S0[t] = sM[2 * 16 + t * 4 + i0] * ih[0] * ih[0];
       }
-      double acc[4] = {0., 0., 0., 0.};
+      Real acc[4] = {0., 0., 0., 0.};
 #pragma nounroll
       for (int a2 = 0; a2 < K1; ++a2) {
-        const double b2 = sM[0 * 16 + a2 * 4 + i2], d2 = sM[16 + a2 * 4 + i2] * ih[2];
-        const double s2 = sM[32 + a2 * 4 + i2] * ih[2] * ih[2];
+        const Real b2 = sM[0 * 16 + a2 * 4 + i2], d2 = sM[16 + a2 * 4 + i2] * ih[2];
+        const Real s2 = sM[32 + a2 * 4 + i2] * ih[2] * ih[2];
 #pragma nounroll
         for (int a1 = 0; a1 < K1; ++a1) {
-          const double b1 = sM[0 * 16 + a1 * 4 + i1], d1 = sM[16 + a1 * 4 + i1] * ih[1];
-          const double s1 = sM[32 + a1 * 4 + i1] * ih[1] * ih[1];
+          const Real b1 = sM[0 * 16 + a1 * 4 + i1], d1 = sM[16 + a1 * 4 + i1] * ih[1];
+          const Real s1 = sM[32 + a1 * 4 + i1] * ih[1] * ih[1];
 #pragma unroll
           for (int a0 = 0; a0 < K1; ++a0) {
             const int qq = a0 + K1 * (a1 + K1 * a2);
-            const double b0 = V0[a0];
-            const double phi = b0 * b1 * b2;
-            const double g[3] = {D0[a0] * b1 * b2, b0 * d1 * b2, b0 * b1 * d2};
-            const double lap = S0[a0] * b1 * b2 + b0 * s1 * b2 + b0 * b1 * s2;
-            const double uq[3] = {X(pci, 0)[qq], X(pci, 1)[qq], X(pci, 2)[qq]};
-            const double gc[3] = {X(pci, 3)[qq], X(pci, 4)[qq], Yr(pci, 0)[qq]};
-            const double tq = Yr(pci, 1)[qq], jw = Yr(pci, 5)[qq];
-            const double Rq[3] = {Yr(pci, 2)[qq], Yr(pci, 3)[qq], Yr(pci, 4)[qq]};
-            const double av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
-            const double g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
+            const Real b0 = V0[a0];
+            const Real phi = b0 * b1 * b2;
+            const Real g[3] = {D0[a0] * b1 * b2, b0 * d1 * b2, b0 * b1 * d2};
+            const Real lap = S0[a0] * b1 * b2 + b0 * s1 * b2 + b0 * b1 * s2;
+            const Real uq[3] = {X(pci, 0)[qq], X(pci, 1)[qq], X(pci, 2)[qq]};
+            const Real gc[3] = {X(pci, 3)[qq], X(pci, 4)[qq], Yr(pci, 0)[qq]};
+            const Real tq = Yr(pci, 1)[qq], jw = Yr(pci, 5)[qq];
+            const Real Rq[3] = {Yr(pci, 2)[qq], Yr(pci, 3)[qq], Yr(pci, 4)[qq]};
+            const Real av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
+            const Real g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-              const double A = gc[c] * phi + av;
+              const Real A = gc[c] * phi + av;
               acc[c] += jw * (A * phi + nu * g2 + tq * (A - nu * lap) * av + tq * Rq[c] * phi * g[c]);
             }
             acc[3] += jw * tq * g2;
@@ -472,12 +481,12 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
   } else {
 
-  double Tc[16];
+  Real Tc[16];
   if constexpr (!JV) {  // residual test coefficients (rhs = -R)
-    const double divu = gu[0][0] + gu[1][1] + gu[2][2];
+    const Real divu = gu[0][0] + gu[1][1] + gu[2][2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const double Gu = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
+      const Real Gu = gu[c][0] * u[0] + gu[c][1] * u[1] + gu[c][2] * u[2];
       Tc[4 * c] = JxW * (-Gu + f[c] - Tt[c] - srf[c]);
 #pragma unroll
       for (int e = 0; e < 3; ++e)
@@ -488,35 +497,35 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     for (int e = 0; e < 3; ++e) Tc[13 + e] = -JxW * tau * R[e] * ih[e];
   } else {
     // ---------------- phase B: the trial function v at this lane's quadrature point
-    double v[3] = {0., 0., 0.}, gv[3][3] = {}, lv[3] = {0., 0., 0.};
+    Real v[3] = {0., 0., 0.}, gv[3][3] = {}, lv[3] = {0., 0., 0.};
 #pragma unroll
     for (int c = 0; c < 3; ++c) vel_field(FV + c, v[c], gv[c], lv[c]);
-    double vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
+    Real vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
     scal_fields(FV + 3, 0, 0, vp, gvp, dummy);
     if constexpr (CACHED) load_qd();
-    const double aj = P.alpha_jac;
-    double S[3], A[3];
+    const Real aj = P.alpha_jac;
+    Real S[3], A[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const double guv = gu[c][0] * v[0] + gu[c][1] * v[1] + gu[c][2] * v[2];
-      const double gvu = gv[c][0] * u[0] + gv[c][1] * u[1] + gv[c][2] * u[2];
+      const Real guv = gu[c][0] * v[0] + gu[c][1] * v[1] + gu[c][2] * v[2];
+      const Real gvu = gv[c][0] * u[0] + gv[c][1] * u[1] + gv[c][2] * u[2];
       A[c] = guv + gvu + aj * v[c];
       S[c] = guv + gvu + gvp[c] - nu * lv[c] + aj * v[c];
     }
     if (P.srf) {
-      const double *om = P.omega;
-      const double cj[3] = {2 * (om[1] * v[2] - om[2] * v[1]), 2 * (om[2] * v[0] - om[0] * v[2]),
+      const Real om[3] = {(Real)P.omega[0], (Real)P.omega[1], (Real)P.omega[2]};
+      const Real cj[3] = {2 * (om[1] * v[2] - om[2] * v[1]), 2 * (om[2] * v[0] - om[0] * v[2]),
                             2 * (om[0] * v[1] - om[1] * v[0])};
 #pragma unroll
       for (int c = 0; c < 3; ++c) { A[c] += cj[c]; S[c] += cj[c]; }
     }
-    const double divv = gv[0][0] + gv[1][1] + gv[2][2];
+    const Real divv = gv[0][0] + gv[1][1] + gv[2][2];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       Tc[4 * c] = JxW * A[c];
 #pragma unroll
       for (int e = 0; e < 3; ++e)
-        Tc[4 * c + 1 + e] = JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
+        Tc[4 * c + 1 + e] = JxW * (nu * gv[c][e] - (c == e ? vp : Real(0)) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
     }
     Tc[12] = JxW * divv;
 #pragma unroll
@@ -524,7 +533,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   }
 
   // ---------------- integration, one test field at a time (wave-local, lane <-> output element)
-  double cb2[K1], cd2[K1], cb1[K1], cd1[K1], cb0[K1], cd0[K1];  // columns of V, D (transposed rows)
+  Real cb2[K1], cd2[K1], cb1[K1], cd1[K1], cb0[K1], cd0[K1];  // columns of V, D (transposed rows)
   row(3, i2, cb2);
   row(4, i2, cd2);
   row(3, i1, cb1);
@@ -542,7 +551,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // transposed z (output index az = i2): Z0 = B^T Tv + D^T Tz, Z1 = B^T Tx, Z2 = B^T Ty
-      double tv[K1], tx[K1], ty[K1], tz[K1];
+      Real tv[K1], tx[K1], ty[K1], tz[K1];
       lineD2(X(pci, 0), tv);
       lineD2(X(pci, 1), tx);
       lineD2(X(pci, 2), ty);
@@ -553,7 +562,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // transposed y (ay = i1): W0 = B^T Z0 + D^T Z2, W1 = B^T Z1
-      double z0[K1], z1[K1], z2[K1];
+      Real z0[K1], z1[K1], z2[K1];
       lineD1(Yr(pci, 0), z0);
       lineD1(Yr(pci, 1), z1);
       lineD1(Yr(pci, 2), z2);
@@ -562,7 +571,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     }
     wave_sync();
     if (pact) {  // transposed x (ax = i0): out = B^T W0 + D^T W1
-      double w0[K1], w1[K1];
+      Real w0[K1], w1[K1];
       lineD0(X(pci, 0), w0);
       lineD0(X(pci, 1), w1);
       Out(pci, fld)[me] = dot(cb0, w0) + dot(cd0, w1);
@@ -576,7 +585,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   for (int t = tid; t < BN3 * 4; t += blockDim.x) {
     const int n = t >> 2, fld = t & 3;
     const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
-    double s = 0.;
+    Real s = 0.;
 #pragma unroll
     for (int cz = 0; cz < 2; ++cz) {
       const int az = Zn - K * cz;
@@ -599,15 +608,15 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     if (GLS_ABL & 2) {
       if (s == 123.456) Yout[gi] = s;
     } else if (interior) Yout[gi] = s;
-    else atomicAdd(&Yout[gi], s);
+    else atomicAdd(&Yout[gi], (double)s);
   }
 }
 
-template <int K>
+template <int K, typename Real = double>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
   const int NF = mode == MODE_JVQ ? 4 : (mode == MODE_JV ? 11 : 7);
-  return sizeof(double) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3 + 5 * 16 + 8) + sizeof(int) * (size_t)C::BN3;
+  return sizeof(Real) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3 + 5 * 16 + 8) + sizeof(int) * (size_t)C::BN3;
 }
 
 template <int K>
@@ -650,6 +659,36 @@ hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64
   if (k == 1) return launch_brick_probe_t<1>(P, T, j0, nprobe, s);
   if (k == 2) return launch_brick_probe_t<2>(P, T, j0, nprobe, s);
   return hipErrorNotSupported;
+}
+
+// FP32 J.v from the FP32 copy of the linearization (P.qdf): the multigrid smoother's operator
+// (mixed-precision preconditioner; v and y stay FP64 vectors, arithmetic and LDS in FP32)
+template <int K>
+hipError_t launch_brick_jv_f32_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
+  using C = BrickCfg<K>;
+  const int n_bricks = P.n_cells / 8;
+  if (n_bricks <= 0) return hipSuccess;
+  if (!P.qdf || P.n_probe > 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ, float>), dim3(n_bricks), dim3(C::THREADS),
+                     (brick_lds_bytes<K, float>(MODE_JVQ)), s, P, T);
+  return hipGetLastError();
+}
+hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (k == 1) return launch_brick_jv_f32_t<1>(P, T, s);
+  if (k == 2) return launch_brick_jv_f32_t<2>(P, T, s);
+  return hipErrorNotSupported;
+}
+
+__global__ void k_to_f32(const double *__restrict__ a, float *__restrict__ b, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    b[i] = (float)__builtin_nontemporal_load(a + i);
+}
+hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1 << 16);
+  hipLaunchKernelGGL(k_to_f32, dim3((unsigned)blocks), dim3(256), 0, s, a, b, n);
+  return hipGetLastError();
 }
 
 size_t brick_qdata_size(int k, int n_cells) {

@@ -44,6 +44,7 @@ struct OpParams {
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input
   double *qd;                 // MODE_LIN output / MODE_JVQ input (brick wave-major layout)
+  float *qdf;                 // FP32 copy of qd (MODE_JVQ in FP32: the multigrid smoother's J.v)
   int n_probe;                // MODE_JVQ probing: > 0 -> block b computes J e_(probe_base + b / n_bricks)
   int64_t probe_base;         //   into y + (b / n_bricks) * n_dofs (v unused)
   double *y;                  // output (accumulated with atomics)

@@ -10,6 +10,9 @@ bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
+// J.v in FP32 arithmetic from P.qdf (FP32 linearization); v, y FP64 (multigrid smoother operator)
+hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
+hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 

@@ -25,6 +25,7 @@ SCHEMES = {
 EXPORTS = [
     "gls_last_error", "gls_version", "gls_create", "gls_destroy", "gls_set_stream", "gls_n_dofs", "gls_set_force",
     "gls_set_viscosity", "gls_set_time", "gls_set_state", "gls_residual", "gls_jacobian_apply",
+    "gls_jacobian_apply_f32",
     "gls_jacobian_diagonal", "gls_set_dirichlet", "gls_apply_dirichlet", "gls_solve_linear", "gls_newton_solve",
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
@@ -60,7 +61,7 @@ class LinearParams(C.Structure):
 class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
                 ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
-                ("coarse_omega", C.c_double), ("coarse_direct", C.c_int)]
+                ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int)]
 
 
 class NewtonParams(C.Structure):
@@ -94,6 +95,7 @@ def load():
     L.gls_set_state.argtypes = [vp, vp, vp, vp, vp]
     L.gls_residual.argtypes = [vp, vp]
     L.gls_jacobian_apply.argtypes = [vp, vp, vp]
+    L.gls_jacobian_apply_f32.argtypes = [vp, vp, vp]
     L.gls_jacobian_diagonal.argtypes = [vp, vp]
     L.gls_set_dirichlet.argtypes = [vp, i64, C.POINTER(i64), d]
     L.gls_apply_dirichlet.argtypes = [vp, vp]
@@ -282,6 +284,12 @@ class GLSContext:
         check(self.L.gls_jacobian_apply(self.h, _ptr(v), _ptr(out)), "gls_jacobian_apply")
         return out
 
+    def jacobian_apply_f32(self, v, out=None):
+        """J.v in FP32 arithmetic (the mixed-precision V-cycle's operator); FP64 in/out vectors."""
+        out = self.zeros() if out is None else out
+        check(self.L.gls_jacobian_apply_f32(self.h, _ptr(v), _ptr(out)), "gls_jacobian_apply_f32")
+        return out
+
     def jacobian_diagonal(self, out=None):
         out = self.zeros() if out is None else out
         check(self.L.gls_jacobian_diagonal(self.h, _ptr(out)), "gls_jacobian_diagonal")
@@ -318,13 +326,13 @@ class GLSContext:
                     residual_evaluations=p.residual_evaluations, final_residual=p.final_residual)
 
     def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6,
-                         coarse_omega=0.0, coarse_direct=0):
+                         coarse_omega=0.0, coarse_direct=0, mixed_precision=0):
         """GMRES right preconditioner = geometric multigrid V-cycle over [self] + coarse_levels
         (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive."""
         levels = [self] + list(coarse_levels)
         arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct)
+                     coarse_omega, coarse_direct, int(mixed_precision))
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
 

@@ -220,3 +220,26 @@ def test_jv_linearization_cache(monkeypatch):
     ctx.set_time("bdf2", p2.time_steps)
     ctx.set_viscosity(0.05)
     assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), Oracle(p2).jacobian_apply(u3, v, u1, u2)) < TOL
+
+
+TOL_F32 = 1e-5  # FP32 arithmetic (unit roundoff 6e-8) over ~100-term quadrature sums, max-norm relative
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BRICK_CASES, ids=lambda c: "n%d_Q%d_%s_srf%d" % (c[0], c[1], c[2], c[4]))
+def test_brick_jv_f32_vs_oracle(case):
+    """The mixed-precision V-cycle's operator (gls_jacobian_apply_f32: FP32 linearization copy,
+    FP32 sweeps and pointwise algebra, FP64 vectors) is the oracle's J.v to FP32 accuracy, and
+    follows state changes (the FP32 copy is refreshed with the FP64 linearization)."""
+    n, k, scheme, nu, srf = case
+    p = _morton_problem(n, k, scheme, nu, srf=srf)
+    u, u1, u2, u3, v = _states(p)
+    ctx = context_for(p)
+    assert ctx.uses_brick_kernels
+    orc = Oracle(p)
+    ctx.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))
+    e1 = relerr(ctx.jacobian_apply_f32(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1, u2, u3))
+    ctx.set_state(cuda(u3), cuda(u1), cuda(u2), cuda(u))
+    e2 = relerr(ctx.jacobian_apply_f32(cuda(v)).cpu().numpy(), orc.jacobian_apply(u3, v, u1, u2, u))
+    print("FP32 J.v rel err %.2e %.2e" % (e1, e2))
+    assert e1 < TOL_F32 and e2 < TOL_F32, (e1, e2)
