@@ -292,6 +292,11 @@ struct gls_ctx {
   int krylov_m = 0;
   DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
   bool use_brick = false;  // sum-factorized brick kernels (3D Qk-Qk, Morton 2x2x2 bricks)
+  // brick-boundary node sums without atomics: each brick stores its partial sums of its NBND
+  // surface nodes into a slab; k_slab_sum adds a node's slots in a fixed order (CSR node -> slots)
+  bool use_slab = false;
+  DevBuf<double> slab;
+  DevBuf<int32_t> sum_nodes, sum_off, sum_slots;
   // distributed (rank-local mesh): owned nodes [0, n_owned), ghosts after; exchange via callbacks
   struct Dist {
     bool on = false;
@@ -382,6 +387,54 @@ bool detect_bricks(const gls_mesh_desc *d, int nq1d) {
       if (o != -1 && o != cix / 8) return false;
     }
   return true;
+}
+
+// node -> slab slots of the bricks whose surface holds it (CSR sorted by node, slots ascending)
+int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
+  const int K = d->k, K1 = K + 1, N3 = K1 * K1 * K1, BN = 2 * K + 1;
+  const int nbnd = gls::brick_boundary_nodes(K);
+  const int64_t nb = d->n_cells / 8;
+  if (nb * nbnd >= INT32_MAX) return GLS_OK;  // keep atomics beyond int32 slot ids
+  std::vector<int32_t> cnt((size_t)d->n_vnodes + 1, 0), slot_node((size_t)(nb * nbnd));
+  for (int64_t b = 0; b < nb; ++b) {
+    int j = 0;
+    for (int Z = 0; Z < BN; ++Z)
+      for (int Y = 0; Y < BN; ++Y)
+        for (int X = 0; X < BN; ++X) {
+          if (X > 0 && X < BN - 1 && Y > 0 && Y < BN - 1 && Z > 0 && Z < BN - 1) continue;
+          const int cx = std::min(X / K, 1), cy = std::min(Y / K, 1), cz = std::min(Z / K, 1);
+          const int a = (X - K * cx) + K1 * ((Y - K * cy) + K1 * (Z - K * cz));
+          const int32_t node = d->cell_vnodes[((size_t)b * 8 + cx + 2 * cy + 4 * cz) * N3 + a];
+          slot_node[(size_t)(b * nbnd + j)] = node;
+          ++cnt[(size_t)node + 1];
+          ++j;
+        }
+    if (j != nbnd) return set_err(GLS_EINVAL, "brick boundary count %d != %d", j, nbnd);
+  }
+  std::vector<int32_t> nodes, off{0};
+  std::vector<int32_t> start((size_t)d->n_vnodes + 1, 0);
+  for (int64_t n = 0; n < d->n_vnodes; ++n) {
+    start[(size_t)n + 1] = start[(size_t)n] + cnt[(size_t)n + 1];
+    if (cnt[(size_t)n + 1] > 0) {
+      nodes.push_back((int32_t)n);
+      off.push_back(start[(size_t)n + 1]);
+    }
+  }
+  std::vector<int32_t> slots((size_t)(nb * nbnd)), fill(start.begin(), start.end() - 1);
+  for (int64_t sl = 0; sl < nb * nbnd; ++sl) slots[(size_t)fill[(size_t)slot_node[(size_t)sl]]++] = (int32_t)sl;
+  GLS_TRY(c->sum_nodes.upload(nodes.data(), nodes.size()));
+  GLS_TRY(c->sum_off.upload(off.data(), off.size()));
+  GLS_TRY(c->sum_slots.upload(slots.data(), slots.size()));
+  c->use_slab = true;
+  return GLS_OK;
+}
+
+// brick launch output: slab (allocated on first use) or nullptr (atomics into a zeroed y)
+double *brick_slab(gls_ctx *c) {
+  if (!c->use_slab) return nullptr;
+  const size_t n = (size_t)(c->n_cells / 8) * gls::brick_boundary_nodes(c->k) * 4;
+  if (c->slab.n != n && c->slab.alloc(n) != GLS_OK) return nullptr;
+  return c->slab.p;
 }
 
 int check_ctx(gls_ctx *c) {
@@ -484,6 +537,11 @@ int ensure_qdata(gls_ctx *c) {
   return GLS_OK;
 }
 
+hipError_t slab_sum(gls_ctx *c, double *y) {
+  return gls::brick_slab_sum(c->slab.p, c->sum_nodes.p, c->sum_off.p, c->sum_slots.p, (int64_t)c->sum_nodes.n,
+                             c->n_vnodes, y, c->stream);
+}
+
 int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
@@ -506,13 +564,17 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   }
   P.v = v;
   P.y = y;
-  HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
+  const bool brick = c->use_brick && mode != gls::MODE_DIAG;
+  P.slab = brick ? brick_slab(c) : nullptr;  // every node is then written exactly once: no zeroing
+  if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
-    if (c->use_brick && mode != gls::MODE_DIAG)
+    if (brick) {
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
-    else
+      if (P.slab) HIP_TRY(slab_sum(c, y));
+    } else {
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+    }
   }
   GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
   if (lin_diag) {  // the same launch stored the J.v linearization
@@ -578,6 +640,7 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
 
   GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
   c->use_brick = detect_bricks(d, nq1d);
+  if (c->use_brick && !std::getenv("GLS_BRICK_ATOMICS")) GLS_TRY(build_slab_map(c.get(), d));
   if (const char *e = std::getenv("GLS_JV_RECOMPUTE")) c->use_qdata = std::atoi(e) == 0;
   if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
   std::vector<double> geo((size_t)d->n_cells * 4);
@@ -804,10 +867,12 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
   P.qdf = g->qdata32.p;
   P.v = v;
   P.y = y;
-  HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
+  P.slab = brick_slab(g);
+  if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
   {
     TimedLaunch t(g, 4);
     HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
+    if (P.slab) HIP_TRY(slab_sum(g, y));
   }
   GLS_TRY(dist_export_add(g, y));
   HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream));

@@ -42,12 +42,33 @@ struct BrickCfg {
   static constexpr int L2 = K1 * K1;         // lines per array
   static constexpr int BN = 2 * K + 1;       // brick nodes per direction
   static constexpr int BN3 = BN * BN * BN;
+  static constexpr int NBND = BN3 - (BN - 2) * (BN - 2) * (BN - 2);  // brick-boundary nodes
   static constexpr int CPW = 64 / N3 >= 2 ? 2 : 1;  // cells per wave (Q1: 8 q -> could be 8; keep 2)
   static constexpr int WAVES = 8 / CPW;      // waves per workgroup (one brick)
   static constexpr int THREADS = 64 * WAVES;
   static constexpr int NX = 5, NY = 6, NO = 4;  // per-cell LDS arrays: X, Y, out
   static constexpr int PER_CELL = NX + NY + NO;
 };
+
+// rank of brick-lattice node (X, Y, Z) among the brick-boundary nodes (lexicographic, x fastest):
+// its index minus the interior nodes that precede it
+template <int BN>
+__device__ __forceinline__ int bnd_index(int X, int Y, int Z) {
+  constexpr int I = BN - 2;
+  const int n = X + BN * (Y + BN * Z);
+  int before = min(max(Z - 1, 0), I) * I * I;
+  if (Z >= 1 && Z <= I) {
+    before += min(max(Y - 1, 0), I) * I;
+    if (Y >= 1 && Y <= I) before += min(max(X - 1, 0), I);
+  }
+  return n - before;
+}
+
+// bijective XCD swizzle of n work items: orig % 8 labels the blocks that share an XCD
+__device__ __forceinline__ int xcd_swizzle(int orig, int n) {
+  const int q = n / 8, r = n % 8, x = orig % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
+}
 
 // offset of element e of line l in a [K1][K1][K1] array ([z][y][x], x fastest), sweep dim D
 template <int D, int K1>
@@ -123,11 +144,14 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   const int n_bricks = P.n_cells / 8;
   // probing (MODE_JVQ): block -> (unit vector, brick); v = e_j, output column j of the batch
   const int pj = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x / n_bricks) : 0;
-  const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks) : (int)blockIdx.x;
+  // XCD-aware order (blocks b, b+8, b+16, ... share an XCD): each XCD walks a contiguous Morton
+  // range of bricks, so the nodes neighbouring bricks share stay in that XCD's L2
+  const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks) : xcd_swizzle((int)blockIdx.x, n_bricks);
   const int64_t unit_dof = (CACHED && P.n_probe > 0) ? P.probe_base + pj : -1;
   double *const Yout = (CACHED && P.n_probe > 0)
                            ? P.y + (int64_t)pj * ((int64_t)3 * P.n_vnodes + P.n_vnodes) : P.y;
   const int64_t voff = (int64_t)3 * P.n_vnodes;
+  const bool use_slab = P.slab != nullptr && !(CACHED && P.n_probe > 0);
 
   if (tid < 5 * 16) {
     const int mat = tid >> 4, r = (tid >> 2) & 3, c = tid & 3;
@@ -182,11 +206,12 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
         BF(FV + 1)[n] = (m & 2u) ? 0.0 : (i3 + 1 == unit_dof ? 1.0 : 0.0);
         BF(FV + 2)[n] = (m & 4u) ? 0.0 : (i3 + 2 == unit_dof ? 1.0 : 0.0);
         BF(FV + 3)[n] = voff + node == unit_dof ? 1.0 : 0.0;
-      } else {
-        BF(FV)[n] = (m & 1u) ? 0.0 : P.v[i3];
-        BF(FV + 1)[n] = (m & 2u) ? 0.0 : P.v[i3 + 1];
-        BF(FV + 2)[n] = (m & 4u) ? 0.0 : P.v[i3 + 2];
-        BF(FV + 3)[n] = P.v[voff + node];
+      } else {  // unconditional loads (all in flight together), masked afterwards
+        const double v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
+        BF(FV)[n] = (m & 1u) ? 0.0 : v0;
+        BF(FV + 1)[n] = (m & 2u) ? 0.0 : v1;
+        BF(FV + 2)[n] = (m & 4u) ? 0.0 : v2;
+        BF(FV + 3)[n] = vp;
       }
     }
   }
@@ -606,8 +631,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     const int64_t gi = fld < 3 ? (int64_t)node * 3 + fld : voff + node;
     const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
     if (GLS_ABL & 2) {
-      if (s == 123.456) Yout[gi] = s;
+      if (s == Real(123.5)) Yout[gi] = s;
     } else if (interior) Yout[gi] = s;
+    else if (use_slab)  // brick-boundary node: this brick's partial sum, summed per node by k_slab_sum
+      P.slab[((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4 + fld] = (double)s;
     else atomicAdd(&Yout[gi], (double)s);
   }
 }
@@ -688,6 +715,39 @@ hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1 << 16);
   hipLaunchKernelGGL(k_to_f32, dim3((unsigned)blocks), dim3(256), 0, s, a, b, n);
+  return hipGetLastError();
+}
+
+int brick_boundary_nodes(int k) { return k == 1 ? BrickCfg<1>::NBND : (k == 2 ? BrickCfg<2>::NBND : 0); }
+
+// y[node] (4 fields) = sum of the bricks' partial sums over the node's slab slots (fixed order:
+// deterministic, no atomics). One thread per brick-boundary node.
+__global__ void k_slab_sum(const double *__restrict__ slab, const int32_t *__restrict__ nodes,
+                           const int32_t *__restrict__ off, const int32_t *__restrict__ slots, int64_t n_sum,
+                           int64_t voff, double *__restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_sum) return;
+  double s0 = 0., s1 = 0., s2 = 0., s3 = 0.;
+  for (int j = off[i]; j < off[i + 1]; ++j) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 *e = reinterpret_cast<const d2 *>(slab + (int64_t)slots[j] * 4);
+    const d2 a = __builtin_nontemporal_load(e), b = __builtin_nontemporal_load(e + 1);
+    s0 += a.x;
+    s1 += a.y;
+    s2 += b.x;
+    s3 += b.y;
+  }
+  const int64_t node = nodes[i];
+  y[node * 3] = s0;
+  y[node * 3 + 1] = s1;
+  y[node * 3 + 2] = s2;
+  y[voff + node] = s3;
+}
+hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
+                          int64_t n_sum, int64_t n_vnodes, double *y, hipStream_t s) {
+  if (n_sum <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((n_sum + 255) / 256)), dim3(256), 0, s, slab, nodes, off, slots,
+                     n_sum, 3 * n_vnodes, y);
   return hipGetLastError();
 }
 

@@ -47,7 +47,9 @@ struct OpParams {
   float *qdf;                 // FP32 copy of qd (MODE_JVQ in FP32: the multigrid smoother's J.v)
   int n_probe;                // MODE_JVQ probing: > 0 -> block b computes J e_(probe_base + b / n_bricks)
   int64_t probe_base;         //   into y + (b / n_bricks) * n_dofs (v unused)
-  double *y;                  // output (accumulated with atomics)
+  double *y;                  // output (brick-interior nodes: plain stores; others: slab or atomics)
+  double *slab;               // brick path: [n_bricks][NBND][4] partial sums of brick-boundary nodes
+                              //   (nullptr -> FP64 atomics into y, which the caller zeroes)
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs
   double alpha_jac;           // mass coefficient of the Jacobian (bdf[0] / sdirk[0][0])

@@ -13,6 +13,10 @@ size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
 // J.v in FP32 arithmetic from P.qdf (FP32 linearization); v, y FP64 (multigrid smoother operator)
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
+int brick_boundary_nodes(int k);  // NBND: brick-lattice nodes on the 2x2x2 brick's surface
+// y[nodes[i]] = sum_{j in [off[i], off[i+1])} slab[slots[j]] (4 fields per node)
+hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
+                          int64_t n_sum, int64_t n_vnodes, double *y, hipStream_t s);
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 
