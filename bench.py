@@ -124,6 +124,8 @@ def main():
     ap.add_argument("--mg-omega", type=float, default=0.9)
     ap.add_argument("--mg-coarse-sweeps", type=int, default=100)
     ap.add_argument("--mg-coarse-omega", type=float, default=0.7, help="0 = --mg-omega")
+    ap.add_argument("--mg-coarse-direct", type=int, default=0,
+                    help="coarsest level: 0 auto (exact solve on one GPU when <= 2048 DoFs), 1 exact (LU above 2048), -1 Jacobi sweeps")
     ap.add_argument("--mg-precision", default="f32", choices=["f32", "f64"],
                     help="arithmetic of the V-cycle's J.v (f32: FP32 linearization + FP32 sweeps; the outer "
                          "GMRES operator, Newton residual and all vectors stay FP64)")
@@ -161,7 +163,7 @@ def main():
                              multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
                              pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
                              coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega,
-                             mixed_precision=args.mg_precision == "f32")
+                             mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct)
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -188,7 +190,7 @@ def main():
             attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
                                          omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
                                          coarse_omega=args.mg_coarse_omega,
-                                         mixed_precision=args.mg_precision == "f32")
+                                         mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct)
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])

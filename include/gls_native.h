@@ -152,7 +152,9 @@ typedef struct {
   double omega;                               /* damped-Jacobi weight of the smoother, 0 -> 0.6 */
   double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
-                                                 with <= 2048 DoFs), 1 exact solve, -1 Jacobi sweeps */
+                                                 with <= 2048 DoFs), 1 exact solve (<= 8192 DoFs; above
+                                                 2048 by rocSOLVER LU with the pressure gauge pinned),
+                                                 -1 Jacobi sweeps */
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
                                                  arithmetic from an FP32 copy of the linearization
                                                  (brick path; vectors, transfers and the outer GMRES

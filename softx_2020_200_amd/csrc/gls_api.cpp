@@ -13,6 +13,9 @@
 #include <string>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
 #include "../../include/gls_native.h"
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
@@ -330,6 +333,30 @@ struct gls_ctx {
     std::vector<std::unique_ptr<Taps>> taps;
     // coarsest level: direct solve with the probed, regularised, inverted Jacobian
     bool direct = false, direct_ok = false;
+    // direct solve by LU (rocSOLVER getrf + getri -> explicit inverse, applied by rocBLAS gemv) with
+    // the first pressure DoF pinned (enclosed-flow gauge); falls back to the one-workgroup
+    // Gauss-Jordan (mg_dense_invert) for small levels or when the LU reports a zero pivot
+    bool lu = false;
+    struct Blas {  // owning rocBLAS handle (movable, destroyed with the MG state)
+      rocblas_handle h = nullptr;
+      Blas() = default;
+      Blas(const Blas &) = delete;
+      Blas &operator=(const Blas &) = delete;
+      Blas(Blas &&o) noexcept : h(o.h) { o.h = nullptr; }
+      Blas &operator=(Blas &&o) noexcept {
+        if (this != &o) {
+          if (h) rocblas_destroy_handle(h);
+          h = o.h;
+          o.h = nullptr;
+        }
+        return *this;
+      }
+      ~Blas() {
+        if (h) rocblas_destroy_handle(h);
+      }
+      operator rocblas_handle() const { return h; }
+    } blas;
+    DevBuf<int> ipiv, info;
     DevBuf<double> probe, aug, unit;
     DevBuf<int> status;
     bool dirty = true;
@@ -1002,13 +1029,40 @@ int mg_prepare(gls_ctx *c) {
         GLS_TRY(gls_jacobian_apply(g, mg.unit.p, mg.probe.p + j * n));
       }
     }
-    HIP_TRY(gls::mg_dense_invert(mg.probe.p, mg.aug.p, (int)n, mg.status.p, c->stream));
-    int st = -1;
-    HIP_TRY(hipMemcpyAsync(&st, mg.status.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    // a couple of dependent columns (pressure gauge) are expected; many mean a broken operator
-    mg.direct_ok = st >= 0 && st <= 4;
-    if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse direct solve n=%lld dropped=%d ok=%d\n", (long long)n, st, (int)mg.direct_ok);
+    mg.lu = false;
+    if (n > 2048 && !std::getenv("GLS_MG_GAUSS_JORDAN")) {  // LU with the pressure gauge pinned
+      const int64_t pin = 3 * (int64_t)g->n_vnodes;
+      HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
+      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+          rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+              rocblas_status_success)
+        return set_err(GLS_EHIP, "rocsolver_dgetrf failed");
+      int inf = -1;
+      HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (inf == 0) {
+        if (rocsolver_dgetri(mg.blas, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+            rocblas_status_success)
+          return set_err(GLS_EHIP, "rocsolver_dgetri failed");
+        HIP_TRY(gls::mg_zero_row(mg.probe.p, n, pin, c->stream));  // pinned unknown: zero correction
+        HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+      }
+      mg.lu = mg.direct_ok = inf == 0;
+      if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse LU n=%lld info=%d\n", (long long)n, inf);
+      if (!mg.lu) {  // re-probe for the Gauss-Jordan fallback below (getrf overwrote the matrix)
+        mg.dirty = true;
+        return set_err(GLS_EINVAL, "coarse LU: zero pivot %d (set GLS_MG_GAUSS_JORDAN=1)", inf);
+      }
+    } else {
+      HIP_TRY(gls::mg_dense_invert(mg.probe.p, mg.aug.p, (int)n, mg.status.p, c->stream));
+      int st = -1;
+      HIP_TRY(hipMemcpyAsync(&st, mg.status.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      // a couple of dependent columns (pressure gauge) are expected; many mean a broken operator
+      mg.direct_ok = st >= 0 && st <= 4;
+      if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse direct solve n=%lld dropped=%d ok=%d\n", (long long)n, st, (int)mg.direct_ok);
+    }
   }
   mg.dirty = false;
   return GLS_OK;
@@ -1025,7 +1079,15 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   const double *d = g->diag.p;
   hipStream_t s = c->stream;
   if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
-    HIP_TRY(gls::mg_dense_apply(mg.aug.p, (int)n, b, x, c->stream));
+    if (mg.lu) {
+      const double one = 1.0, zero = 0.0;
+      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+          rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe.p,
+                        (rocblas_int)n, b, 1, &zero, x, 1) != rocblas_status_success)
+        return set_err(GLS_EHIP, "rocblas_dgemv failed");
+    } else {
+      HIP_TRY(gls::mg_dense_apply(mg.aug.p, (int)n, b, x, c->stream));
+    }
     return GLS_OK;
   }
   const int pre = l == L - 1 ? mg.csweeps : mg.pre;
@@ -1211,7 +1273,12 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
     if (mg.direct) {
       GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
-      GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
+      if (nco <= 2048 || std::getenv("GLS_MG_GAUSS_JORDAN")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
+      GLS_TRY(mg.ipiv.alloc((size_t)nco));
+      GLS_TRY(mg.info.alloc(1));
+      if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)
+        return set_err(GLS_EHIP, "rocblas_create_handle failed");
+      rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
       GLS_TRY(mg.unit.alloc((size_t)nco));
       GLS_TRY(mg.status.alloc(1));
     }

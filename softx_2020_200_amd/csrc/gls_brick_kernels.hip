@@ -24,10 +24,14 @@
 #include "gls_launch.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #ifndef GLS_ABL
-#define GLS_ABL 0  // timing-only ablations: 1 no global gather, 2 no scatter, 4 no sweeps
+#define GLS_ABL 0  // timing-only ablations: 1 no global gather, 2 no scatter, 4 no sweeps, 8 no qd loads
+#endif
+#ifndef GLS_ROWS_REG
+#define GLS_ROWS_REG 1  // bit 0: FP32 kernels keep the x/y matrix rows in registers; bit 1: FP64
 #endif
 #ifndef GLS_BRICK_WAVES_PER_EU
 #define GLS_BRICK_WAVES_PER_EU 4
@@ -135,8 +139,12 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   Real *const smem = reinterpret_cast<Real *>(smem_raw);
   Real *sB = smem;                                   // [NF][BN3]
   Real *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
-  Real *sM = sC + 8 * C::PER_CELL * N3;             // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4]
-  int *sNode = reinterpret_cast<int *>(sM + 5 * 16 + 8);  // [BN3]
+  // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4] in a SEPARATE shared object: the compiler then
+  // knows table reads never alias the stage arrays, so it can issue them ahead of a stage's stores
+  // (in the dynamic array every row read after an X store waited for it: serialized LDS latency)
+  __shared__ Real sTab[5 * 16 + 8];
+  Real *const sM = sTab;
+  int *sNode = reinterpret_cast<int *>(sC + 8 * C::PER_CELL * N3);  // [BN3]
   auto BF = [&](int f) { return sB + f * BN3; };
 
   const int tid = threadIdx.x;
@@ -249,6 +257,26 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
 #pragma unroll
     for (int k = 0; k < K1; ++k) o[k] = m[k];
   };
+  // this lane's rows of the x / y 1D matrices (V, D, S at i0 and i1): registers when GLS_ROWS_REG
+  // is set for this precision (the sweeps are LDS-bound), else one LDS read per use
+  constexpr bool RREG = std::is_same<Real, float>::value ? (GLS_ROWS_REG & 1) : (GLS_ROWS_REG & 2);
+  Real rr[RREG ? 6 : 1][K1];
+  if constexpr (RREG) {
+    row(0, i0, rr[0]);
+    row(1, i0, rr[1]);
+    row(2, i0, rr[2]);
+    row(0, i1, rr[3]);
+    row(1, i1, rr[4]);
+    row(2, i1, rr[5]);
+  }
+  auto rowq = [&](int mat, int which, Real (&o)[K1]) {  // which: 0 -> row i0, 1 -> row i1
+    if constexpr (RREG) {
+#pragma unroll
+      for (int k = 0; k < K1; ++k) o[k] = rr[which * 3 + mat][k];
+    } else {
+      row(mat, which ? i1 : i0, o);
+    }
+  };
   auto dot = [&](const Real (&a)[K1], const Real (&b)[K1]) {
     Real s = 0.;
 #pragma unroll
@@ -273,15 +301,16 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   auto vel_field = [&](int f, Real &val, Real (&g)[3], Real &lap) {
     if (GLS_ABL & 4) { val = BF(f)[bx_base]; g[0] = g[1] = g[2] = val; lap = val; return; }
     if (pact) {  // x sweep: X_B, X_D, X_S at [i2][i1][i0]
-      Real in[K1], r[K1];
+      Real in[K1], r0[K1], r1[K1], r2[K1];  // every load of the stage before its stores
 #pragma unroll
       for (int e = 0; e < K1; ++e) in[e] = BF(f)[bx_base + e];
-      row(0, i0, r);
-      X(pci, 0)[me] = dot(r, in);
-      row(1, i0, r);
-      X(pci, 1)[me] = dot(r, in);
-      row(2, i0, r);
-      X(pci, 2)[me] = dot(r, in);
+      rowq(0, 0, r0);
+      rowq(1, 0, r1);
+      rowq(2, 0, r2);
+      const Real o0 = dot(r0, in), o1 = dot(r1, in), o2 = dot(r2, in);
+      X(pci, 0)[me] = o0;
+      X(pci, 1)[me] = o1;
+      X(pci, 2)[me] = o2;
     }
     wave_sync();
     if (pact) {  // y sweep: BB, BD, DB, L = wy S_y(X_B) + wx B_y(X_S)
@@ -289,9 +318,9 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
       lineD1(X(pci, 0), xb);
       lineD1(X(pci, 1), xd);
       lineD1(X(pci, 2), xs);
-      row(0, i1, rb);
-      row(1, i1, rd);
-      row(2, i1, rs);
+      rowq(0, 1, rb);
+      rowq(1, 1, rd);
+      rowq(2, 1, rs);
       Yr(pci, 0)[me] = dot(rb, xb);
       Yr(pci, 1)[me] = dot(rd, xb);
       Yr(pci, 2)[me] = dot(rb, xd);
@@ -317,33 +346,30 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   auto scal_fields = [&](int fp, int nh, int fh0, Real &pv, Real (&pg)[3], Real (&hv)[3]) {
     if (GLS_ABL & 4) { pv = BF(fp)[bx_base]; pg[0] = pg[1] = pg[2] = pv; for (int j = 0; j < nh; ++j) hv[j] = pv; return; }
     if (pact) {  // x: p -> X0 (B), X1 (D); H_j -> X(2+j) (B)
-      Real in[K1], rb[K1], rd[K1];
-      row(0, i0, rb);
-      row(1, i0, rd);
+      Real in[K1], rb[K1], rd[K1], ih_[3][K1];
+      rowq(0, 0, rb);
+      rowq(1, 0, rd);
 #pragma unroll
       for (int e = 0; e < K1; ++e) in[e] = BF(fp)[bx_base + e];
+      for (int j = 0; j < nh; ++j)
+#pragma unroll
+        for (int e = 0; e < K1; ++e) ih_[j][e] = BF(fh0 + j)[bx_base + e];
       X(pci, 0)[me] = dot(rb, in);
       X(pci, 1)[me] = dot(rd, in);
-      for (int j = 0; j < nh; ++j) {
-#pragma unroll
-        for (int e = 0; e < K1; ++e) in[e] = BF(fh0 + j)[bx_base + e];
-        X(pci, 2 + j)[me] = dot(rb, in);
-      }
+      for (int j = 0; j < nh; ++j) X(pci, 2 + j)[me] = dot(rb, ih_[j]);
     }
     wave_sync();
     if (pact) {  // y: X0 -> BB (Y0), BD (Y1); X1 -> DB (Y2); X(2+j) -> Y(3+j)
-      Real a[K1], rb[K1], rd[K1];
-      row(0, i1, rb);
-      row(1, i1, rd);
+      Real a[K1], a1[K1], rb[K1], rd[K1], ah[3][K1];
+      rowq(0, 1, rb);
+      rowq(1, 1, rd);
       lineD1(X(pci, 0), a);
+      lineD1(X(pci, 1), a1);
+      for (int j = 0; j < nh; ++j) lineD1(X(pci, 2 + j), ah[j]);
       Yr(pci, 0)[me] = dot(rb, a);
       Yr(pci, 1)[me] = dot(rd, a);
-      lineD1(X(pci, 1), a);
-      Yr(pci, 2)[me] = dot(rb, a);
-      for (int j = 0; j < nh; ++j) {
-        lineD1(X(pci, 2 + j), a);
-        Yr(pci, 3 + j)[me] = dot(rb, a);
-      }
+      Yr(pci, 2)[me] = dot(rb, a1);
+      for (int j = 0; j < nh; ++j) Yr(pci, 3 + j)[me] = dot(rb, ah[j]);
     }
     wave_sync();
     if (pact) {
@@ -379,6 +405,16 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
   Real pq = 0., f[3] = {0., 0., 0.}, Tt[3] = {0., 0., 0.}, srf[3] = {0., 0., 0.};
   // JVQ: the linearization is loaded after the v sweeps (short live ranges: no spills)
   auto load_qd = [&]() {
+    if (GLS_ABL & 8) {  // timing-only: no linearization stream
+#pragma unroll
+      for (int c = 0; c < 3; ++c) u[c] = JxW * (c + 1);
+#pragma unroll
+      for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = hx * c;
+      tau = JxW;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) R[c] = hy * c;
+      return;
+    }
     if (pact) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) u[c] = __builtin_nontemporal_load(qdw + c * QW);
@@ -643,7 +679,7 @@ template <int K, typename Real = double>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
   const int NF = mode == MODE_JVQ ? 4 : (mode == MODE_JV ? 11 : 7);
-  return sizeof(Real) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3 + 5 * 16 + 8) + sizeof(int) * (size_t)C::BN3;
+  return sizeof(Real) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3) + sizeof(int) * (size_t)C::BN3;
 }
 
 template <int K>
@@ -682,7 +718,27 @@ hipError_t launch_brick_probe_t(const OpParams &P0, const Tables1D &T, int64_t j
                      brick_lds_bytes<K>(MODE_JVQ), s, P, T);
   return hipGetLastError();
 }
+// Kernel choice per element order (measured at 128^3, profiles/r01_jv_kernel_ab.txt):
+//   Q1: the persistent wave-per-brick kernel (gls_brick_wave.hip: one round of 8 cells fills all
+//       64 lanes) for every mode;
+//   Q2: J.v from the cached linearization -> the interleaved-stage kernel (gls_brick_jvq.hip);
+//       residual, linearization(+diagonal) and probing -> the workgroup-per-brick kernel here.
+// Timing-only overrides: GLS_BRICK_V1=1 (this file's kernel everywhere), GLS_BRICK_WAVE=1 (the
+// wave kernel everywhere). The Q2 linearization layout is the same in all three kernels.
+static int brick_impl(int k) {  // 0 this file, 1 wave kernel
+  static const int v1 = std::getenv("GLS_BRICK_V1") != nullptr ? 1 : 0;
+  static const int wv = std::getenv("GLS_BRICK_WAVE") != nullptr ? 1 : 0;
+  if (v1) return 0;
+  if (wv) return 1;
+  return k == 1 ? 1 : 0;
+}
+static bool jvq2_on(int k) {  // interleaved-stage J.v: opt-in (GLS_JVQ2=1), slower on gfx950 so far
+  static const bool on = std::getenv("GLS_JVQ2") != nullptr;
+  return k == 2 && on;
+}
+
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s) {
+  if (brick_impl(k) == 1) return launch_brick_wave_probe(k, P, T, j0, nprobe, s);
   if (k == 1) return launch_brick_probe_t<1>(P, T, j0, nprobe, s);
   if (k == 2) return launch_brick_probe_t<2>(P, T, j0, nprobe, s);
   return hipErrorNotSupported;
@@ -701,6 +757,8 @@ hipError_t launch_brick_jv_f32_t(const OpParams &P, const Tables1D &T, hipStream
   return hipGetLastError();
 }
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (jvq2_on(k)) return launch_brick_jvq2(k, true, P, T, s);
+  if (brick_impl(k) == 1) return launch_brick_wave_jv_f32(k, P, T, s);
   if (k == 1) return launch_brick_jv_f32_t<1>(P, T, s);
   if (k == 2) return launch_brick_jv_f32_t<2>(P, T, s);
   return hipErrorNotSupported;
@@ -752,11 +810,14 @@ hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_
 }
 
 size_t brick_qdata_size(int k, int n_cells) {
+  if (brick_impl(k) == 1) return brick_wave_qdata_size(k, n_cells);
   return k == 1 ? brick_qdata_doubles<1>(n_cells) : (k == 2 ? brick_qdata_doubles<2>(n_cells) : 0);
 }
 
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (mode == MODE_DIAG) return hipErrorNotSupported;
+  if (mode == MODE_JVQ && P.n_probe == 0 && jvq2_on(k)) return launch_brick_jvq2(k, false, P, T, s);
+  if (brick_impl(k) == 1) return launch_brick_wave(k, mode, P, T, s);
   if (k == 1) return launch_brick_t<1>(mode, P, T, s);
   if (k == 2) return launch_brick_t<2>(mode, P, T, s);
   return hipErrorNotSupported;

@@ -13,6 +13,13 @@ size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
 // J.v in FP32 arithmetic from P.qdf (FP32 linearization); v, y FP64 (multigrid smoother operator)
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
+// persistent wave-per-brick versions (gls_brick_wave.hip), selected by the launchers above
+hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
+hipError_t launch_brick_wave_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
+hipError_t launch_brick_wave_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
+size_t brick_wave_qdata_size(int k, int n_cells);
+// J.v from the cached linearization, two fields interleaved per sweep stage (gls_brick_jvq.hip), Q2
+hipError_t launch_brick_jvq2(int k, bool f32, const OpParams &P, const Tables1D &T, hipStream_t s);
 int brick_boundary_nodes(int k);  // NBND: brick-lattice nodes on the 2x2x2 brick's surface
 // y[nodes[i]] = sum_{j in [off[i], off[i+1])} slab[slots[j]] (4 fields per node)
 hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
@@ -62,6 +69,9 @@ hipError_t mg_unit_step(double *e, int64_t j, hipStream_t s);  // e[j-1] = 0, e[
 hipError_t mg_probe_fix(double *Y, int64_t n, int64_t j0, int nprobe, const int64_t *con, int64_t ncon, const double *d,
                         hipStream_t s);
 hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, hipStream_t s);
+// column-major n x n: row / column `pin` -> identity; zero one row (the LU path's gauge pin)
+hipError_t mg_pin_dof(double *A, int64_t n, int64_t pin, hipStream_t s);
+hipError_t mg_zero_row(double *A, int64_t n, int64_t row, hipStream_t s);
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s);
 

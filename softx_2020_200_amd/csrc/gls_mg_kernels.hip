@@ -269,6 +269,26 @@ hipError_t mg_probe_fix(double *Y, int64_t n, int64_t j0, int nprobe, const int6
   return hipGetLastError();
 }
 
+// column-major A (n x n): row and column `pin` -> identity (fixes the enclosed-flow pressure gauge)
+__global__ void k_pin(double *A, int64_t n, int64_t pin) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    A[pin * n + t] = t == pin ? 1.0 : 0.0;  // column pin
+    A[t * n + pin] = t == pin ? 1.0 : 0.0;  // row pin
+  }
+}
+hipError_t mg_pin_dof(double *A, int64_t n, int64_t pin, hipStream_t s) {
+  hipLaunchKernelGGL(k_pin, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, n, pin);
+  return hipGetLastError();
+}
+__global__ void k_zero_row(double *A, int64_t n, int64_t row) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x)
+    A[t * n + row] = 0.0;
+}
+hipError_t mg_zero_row(double *A, int64_t n, int64_t row, hipStream_t s) {
+  hipLaunchKernelGGL(k_zero_row, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, A, n, row);
+  return hipGetLastError();
+}
+
 hipError_t mg_dense_invert(const double *Y, double *aug, int n, int *status, hipStream_t s) {
   hipLaunchKernelGGL(k_gauss_jordan, dim3(1), dim3(kGJThreads), 0, s, Y, aug, n, status);
   return hipGetLastError();

@@ -26,9 +26,13 @@ for _ in range(reps // 4 + 1):
     ctx.residual(y)
 d_out = torch.empty_like(v)
 ctx.jacobian_diagonal(out=d_out)  # k_copy of n_dofs doubles: PMC byte calibration (tools/pmc_traffic.sh)
+if ctx.uses_brick_kernels:  # FP32 smoother operator (timing slot 4)
+    for _ in range(reps):
+        ctx.jacobian_apply_f32(v, y)
 ms_jv, n_jv = ctx.timing_get(1)
+ms_f, n_f = ctx.timing_get(4)
 ms_r, n_r = ctx.timing_get(0)
 ms_d, n_d = ctx.timing_get(2)
-print("n=%d k=%d brick=%s  J.v %.3f ms  residual %.3f ms  diag %.3f ms  linearize %.3f ms (cells %d, dofs %d)" % (
-    n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_r / n_r, ms_d / max(n_d, 1), ms_l / max(n_l, 1),
-    prob.mesh["n_cells"], ctx.n_dofs))
+print("n=%d k=%d brick=%s  J.v %.3f ms  J.v(f32) %.3f ms  residual %.3f ms  diag %.3f ms  linearize %.3f ms "
+      "(cells %d, dofs %d)" % (n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_f / max(n_f, 1), ms_r / n_r,
+                              ms_d / max(n_d, 1), ms_l / max(n_l, 1), prob.mesh["n_cells"], ctx.n_dofs))
