@@ -721,8 +721,8 @@ hipError_t launch_brick_probe_t(const OpParams &P0, const Tables1D &T, int64_t j
 // Kernel choice per element order (measured at 128^3, profiles/r01_jv_kernel_ab.txt):
 //   Q1: the persistent wave-per-brick kernel (gls_brick_wave.hip: one round of 8 cells fills all
 //       64 lanes) for every mode;
-//   Q2: J.v from the cached linearization -> the interleaved-stage kernel (gls_brick_jvq.hip);
-//       residual, linearization(+diagonal) and probing -> the workgroup-per-brick kernel here.
+//   Q2: the workgroup-per-brick kernel here (the wave kernel at 3 waves / SIMD, and a variant
+//       interleaving two fields per sweep stage, both measured slower: LDS-issue bound).
 // Timing-only overrides: GLS_BRICK_V1=1 (this file's kernel everywhere), GLS_BRICK_WAVE=1 (the
 // wave kernel everywhere). The Q2 linearization layout is the same in all three kernels.
 static int brick_impl(int k) {  // 0 this file, 1 wave kernel
@@ -731,10 +731,6 @@ static int brick_impl(int k) {  // 0 this file, 1 wave kernel
   if (v1) return 0;
   if (wv) return 1;
   return k == 1 ? 1 : 0;
-}
-static bool jvq2_on(int k) {  // interleaved-stage J.v: opt-in (GLS_JVQ2=1), slower on gfx950 so far
-  static const bool on = std::getenv("GLS_JVQ2") != nullptr;
-  return k == 2 && on;
 }
 
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s) {
@@ -757,7 +753,6 @@ hipError_t launch_brick_jv_f32_t(const OpParams &P, const Tables1D &T, hipStream
   return hipGetLastError();
 }
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s) {
-  if (jvq2_on(k)) return launch_brick_jvq2(k, true, P, T, s);
   if (brick_impl(k) == 1) return launch_brick_wave_jv_f32(k, P, T, s);
   if (k == 1) return launch_brick_jv_f32_t<1>(P, T, s);
   if (k == 2) return launch_brick_jv_f32_t<2>(P, T, s);
@@ -816,7 +811,6 @@ size_t brick_qdata_size(int k, int n_cells) {
 
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (mode == MODE_DIAG) return hipErrorNotSupported;
-  if (mode == MODE_JVQ && P.n_probe == 0 && jvq2_on(k)) return launch_brick_jvq2(k, false, P, T, s);
   if (brick_impl(k) == 1) return launch_brick_wave(k, mode, P, T, s);
   if (k == 1) return launch_brick_t<1>(mode, P, T, s);
   if (k == 2) return launch_brick_t<2>(mode, P, T, s);

@@ -18,8 +18,7 @@ hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D 
 hipError_t launch_brick_wave_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t launch_brick_wave_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 size_t brick_wave_qdata_size(int k, int n_cells);
-// J.v from the cached linearization, two fields interleaved per sweep stage (gls_brick_jvq.hip), Q2
-hipError_t launch_brick_jvq2(int k, bool f32, const OpParams &P, const Tables1D &T, hipStream_t s);
+
 int brick_boundary_nodes(int k);  // NBND: brick-lattice nodes on the 2x2x2 brick's surface
 // y[nodes[i]] = sum_{j in [off[i], off[i+1])} slab[slots[j]] (4 fields per node)
 hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
