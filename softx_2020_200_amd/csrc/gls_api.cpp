@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
@@ -623,6 +624,27 @@ int ensure_diag(gls_ctx *c) {
   return GLS_OK;
 }
 
+// w -= V[0..nk) h (h on device, nk <= 8) fused with host_out[k] = V_k . w_new (k < nk, when dots) and
+// host_out[dots ? nk : 0] = ||w_new||^2 over owned DoFs, reduced over ranks
+int dist_multiaxpy_dots(gls_ctx *c, double *w, const double *V, int64_t lda, int nk, const double *h, bool dots,
+                        double *host_out) {
+  const int64_t n1 = c->dist.on ? 3 * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? 3 * (int64_t)c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned : 0;
+  const int nd = dots ? nk + 1 : 1;
+  HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, c->scal.p, c->work.p,
+                                  c->stream));
+  if (c->dist.on) {
+    HIP_TRY(hipMemcpyAsync(c->dist.red_buf, c->scal.p, sizeof(double) * nd, hipMemcpyDeviceToDevice, c->stream));
+    if (c->dist.allreduce(c->dist.user, c->dist.red_buf, nd) != 0) return set_err(GLS_ECOMM, "allreduce failed");
+    HIP_TRY(hipMemcpyAsync(host_out, c->dist.red_buf, sizeof(double) * nd, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    HIP_TRY(hipMemcpyAsync(host_out, c->scal.p, sizeof(double) * nd, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GLS_OK;
+}
+
 int device_dot(gls_ctx *c, const double *a, const double *b, double *host_out) {
   return dist_multidot(c, a, 0, 1, b, host_out);
 }
@@ -983,6 +1005,15 @@ int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
+  const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
+  auto tick = [&]() {  // host wall time of the preparation phases (verbose only: synchronizes)
+    if (verbose) (void)hipStreamSynchronize(c->stream);
+    return std::chrono::steady_clock::now();
+  };
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const auto t0 = tick();
   const int L = (int)mg.lev.size();
   for (int l = 1; l < L; ++l) {
     gls_ctx *g = mg.lev[l];
@@ -1029,6 +1060,7 @@ int mg_prepare(gls_ctx *c) {
         GLS_TRY(gls_jacobian_apply(g, mg.unit.p, mg.probe.p + j * n));
       }
     }
+    const auto t1 = tick();
     mg.lu = false;
     if (n > 2048 && !std::getenv("GLS_MG_GAUSS_JORDAN")) {  // LU with the pressure gauge pinned
       const int64_t pin = 3 * (int64_t)g->n_vnodes;
@@ -1040,6 +1072,8 @@ int mg_prepare(gls_ctx *c) {
       int inf = -1;
       HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
+      const auto t2 = tick();
+      if (verbose) std::printf("mg: levels+probe %.2f ms, getrf %.2f ms\n", ms(t0, t1), ms(t1, t2));
       if (inf == 0) {
         if (rocsolver_dgetri(mg.blas, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
             rocblas_status_success)
@@ -1049,7 +1083,7 @@ int mg_prepare(gls_ctx *c) {
         HIP_TRY(hipStreamSynchronize(c->stream));
       }
       mg.lu = mg.direct_ok = inf == 0;
-      if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse LU n=%lld info=%d\n", (long long)n, inf);
+      if (verbose) std::printf("mg: coarse LU n=%lld info=%d, getri done at %.2f ms\n", (long long)n, inf, ms(t0, tick()));
       if (!mg.lu) {  // re-probe for the Gauss-Jordan fallback below (getrf overwrote the matrix)
         mg.dirty = true;
         return set_err(GLS_EINVAL, "coarse LU: zero pivot %d (set GLS_MG_GAUSS_JORDAN=1)", inf);
@@ -1335,7 +1369,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   HIP_TRY(gls::vec_copy(r, b, n, s));
   double beta = std::sqrt(bnorm2);
   int it = 0;
-  std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hcol(m + 2), y(m);
+  std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hcol(m + 2), hc2(m + 2), y(m);
   bool converged = beta <= tol;
   while (!converged && it < prm->max_iterations) {
     HIP_TRY(gls::vec_axpby(V, 1.0 / beta, r, 0.0, n, s));
@@ -1353,17 +1387,29 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       const double wnorm0 = std::sqrt(std::max(hcol[j + 1], 0.0));
       for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hcol[i];
       HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
-      HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
-      double wn2;
-      GLS_TRY(device_dot(c, w, w, &wn2));
-      double wnorm = std::sqrt(std::max(wn2, 0.0));
-      if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation
-        GLS_TRY(dist_multidot(c, V, n, j + 1, w, hcol.data()));
-        for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hcol[i];
-        HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+      double wn2, wnorm;
+      if (j + 1 <= 8) {
+        // projection fused with the DGKS dots and the norm: one pass over V instead of three
+        GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, true, hc2.data()));
+        wnorm = std::sqrt(std::max(hc2[j + 1], 0.0));
+        if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation with the dots of the fused pass
+          for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hc2[i];
+          HIP_TRY(hipMemcpyAsync(c->coef.p, hc2.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+          GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2));
+          wnorm = std::sqrt(std::max(wn2, 0.0));
+        }
+      } else {
         HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
         GLS_TRY(device_dot(c, w, w, &wn2));
         wnorm = std::sqrt(std::max(wn2, 0.0));
+        if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation
+          GLS_TRY(dist_multidot(c, V, n, j + 1, w, hcol.data()));
+          for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hcol[i];
+          HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+          HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
+          GLS_TRY(device_dot(c, w, w, &wn2));
+          wnorm = std::sqrt(std::max(wn2, 0.0));
+        }
       }
       H[(size_t)(j + 1) * m + j] = wnorm;
       if (wnorm > 0) HIP_TRY(gls::vec_scale(w, 1.0 / wnorm, n, s));

@@ -46,6 +46,11 @@ hipError_t vec_unpack_nodes(double *x, const int32_t *nodes, int64_t m, int64_t 
 // w -= sum_k h[k] * A[k]  (h on device)
 hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
                          hipStream_t s);
+// w -= sign * sum_k h[k] A[k] (nk <= 8, h on device), fused with out[k] = A[k] . w_new (k < nk, when
+// dots) and out[dots ? nk : 0] = ||w_new||^2, both over the owned rows [0, n1) U [off2, off2 + n2)
+hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
+                              int64_t n1, int64_t off2, int64_t n2, bool dots, double *out, double *work,
+                              hipStream_t s);
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
                                 hipStream_t s);  // y[idx] = d[idx]*v[idx]
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)

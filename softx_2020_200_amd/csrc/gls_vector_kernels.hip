@@ -102,6 +102,52 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy(double *__restrict__ w, co
   }
 }
 
+// w -= sign * sum_k h[k] A[k]; in the same pass the partial sums of A[k] . w_new (DOTS) and
+// ||w_new||^2 over the owned rows [0, n1) U [off2, off2 + n2) -> work[d * gridDim + block]
+// (the fused classical Gram-Schmidt step: projection + the re-orthogonalisation dots + norm)
+template <int NK, bool DOTS>
+__global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w, const double *__restrict__ A,
+                                                          int64_t lda, const double *__restrict__ h, double sign,
+                                                          int64_t n, int64_t n1, int64_t off2, int64_t n2,
+                                                          double *work) {
+  constexpr int ND = (DOTS ? NK : 0) + 1;
+  double hk[NK], acc[ND];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) hk[k] = sign * h[k];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) acc[d] = 0.;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double a[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) a[k] = A[k * lda + i];
+    double s = w[i];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s -= hk[k] * a[k];
+    w[i] = s;
+    if (i < n1 || (i >= off2 && i < off2 + n2)) {
+      if constexpr (DOTS) {
+#pragma unroll
+        for (int k = 0; k < NK; ++k) acc[k] += a[k] * s;
+      }
+      acc[ND - 1] += s * s;
+    }
+  }
+  __shared__ double red[ND][kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const double t = wave_sum(acc[d]);
+    if (lane == 0) red[d][wv] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < ND) {
+    double t = 0.;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; ++j) t += red[threadIdx.x][j];
+    work[threadIdx.x * gridDim.x + blockIdx.x] = t;
+  }
+}
+
 __global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = idx[j];
@@ -141,7 +187,7 @@ __global__ void k_set_indexed(double *y, const int64_t *idx, const double *vals,
 }
 }  // namespace
 
-int multidot_work_size() { return kDotChunk * kMaxBlocks; }
+int multidot_work_size() { return (kDotChunk + 1) * kMaxBlocks; }
 
 hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s) {
   hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, n, a);
@@ -203,6 +249,28 @@ hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const 
 #undef MA
     }
   }
+  return hipGetLastError();
+}
+
+hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
+                              int64_t n1, int64_t off2, int64_t n2, bool dots, double *out, double *work,
+                              hipStream_t s) {
+  if (nk < 1 || nk > kDotChunk) return hipErrorInvalidValue;
+  const int nb = grid_for(n);
+  switch (nk * 2 + (dots ? 1 : 0)) {
+#define MX(M)                                                                                                         \
+  case 2 * M:                                                                                                         \
+    hipLaunchKernelGGL((k_multiaxpy_dot<M, false>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2, \
+                       work);                                                                                         \
+    break;                                                                                                            \
+  case 2 * M + 1:                                                                                                     \
+    hipLaunchKernelGGL((k_multiaxpy_dot<M, true>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2,  \
+                       work);                                                                                         \
+    break;
+    MX(1) MX(2) MX(3) MX(4) MX(5) MX(6) MX(7) MX(8)
+#undef MX
+  }
+  hipLaunchKernelGGL(k_reduce_rows, dim3(dots ? nk + 1 : 1), dim3(kBlock), 0, s, work, nb, out);
   return hipGetLastError();
 }
 
