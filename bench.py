@@ -71,7 +71,7 @@ def pmc_traffic(path, kernel_mode, n_dofs):
         if cur and f and f[0] in ("FETCH_SIZE", "WRITE_SIZE"):
             vals.setdefault(cur, {})[f[0]] = float(f[1]) * 1024.0
     copy = next((v for k_, v in vals.items() if "k_copy" in k_), None)
-    kern = next((v for k_, v in vals.items() if "gls_brick_kernel<2, %d>" % kernel_mode in k_), None)
+    kern = next((v for k_, v in vals.items() if "gls_brick_kernel<2, %d, double>" % kernel_mode in k_), None)
     if not copy or not kern or len(copy) < 2 or len(kern) < 2:
         return None
     fetch_corr = 8.0 * n_dofs / copy["FETCH_SIZE"]
@@ -223,6 +223,7 @@ def main():
     dg_ms, dg_n = ctx.timing_get(2)
     lin_ms, lin_n = ctx.timing_get(3)
     f32_ms, f32_n = ctx.timing_get(4)
+    sl_ms, sl_n = ctx.timing_get(5)
     ctx.timing(False)
     # dedicated back-to-back J.v launches on the same state for a clean per-launch duration
     ctx.set_state(present, m1, m2)
@@ -284,14 +285,15 @@ def main():
         "residual_evaluations_per_step": float(np.mean(nres)),
         "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),
                       "diagonal": dg_ms / max(dg_n, 1), "jv_linearization": lin_ms / max(lin_n, 1),
-                      "smoother_jv_f32": f32_ms / max(f32_n, 1),
+                      "smoother_jv_f32": f32_ms / max(f32_n, 1), "slab_sum": sl_ms / max(sl_n, 1),
                       "launches_per_step": {"jacobian_apply": jv_n / args.steps, "residual": res_n / args.steps,
                                             "diagonal": dg_n / args.steps, "jv_linearization": lin_n / args.steps,
-                                            "smoother_jv_f32": f32_n / args.steps},
+                                            "smoother_jv_f32": f32_n / args.steps, "slab_sum": sl_n / args.steps},
                       "share_of_step": {"jacobian_apply": jv_ms / (1e3 * elapsed),
                                         "residual": res_ms / (1e3 * elapsed), "diagonal": dg_ms / (1e3 * elapsed),
                                         "jv_linearization": lin_ms / (1e3 * elapsed),
-                                        "smoother_jv_f32": f32_ms / (1e3 * elapsed)}},
+                                        "smoother_jv_f32": f32_ms / (1e3 * elapsed),
+                                        "slab_sum": sl_ms / (1e3 * elapsed)}},
         "roofline": {"bound": "hbm", "kernel": "gls_brick_kernel<%d,MODE_JVQ>" % args.k if ctx.uses_brick_kernels
                      else "gls_cell_kernel<3,%d,%d,%d,MODE_JV>" % (args.k, args.kp, args.k + 1), "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -111,6 +111,20 @@ int gls_jacobian_apply(gls_ctx *ctx, const double *v, double *Jv);
  * preconditioner-internal operator, exposed for parity tests (relative error ~1e-6). */
 int gls_jacobian_apply_f32(gls_ctx *ctx, const double *v, double *Jv);
 
+/* Hanging-node constraints (DoF level), after the Dirichlet mask of gls_create:
+ *   DoF dofs[i] = sum_{j in [offsets[i], offsets[i+1])} weights[j] * DoF masters[j]
+ * (DoFTools::make_hanging_node_constraints, gls_navier_stokes.cc:84, 143; host arrays). Hanging
+ * DoFs must not carry a Dirichlet mask bit (deal.II: interpolate_boundary_values skips DoFs that
+ * are already constrained) and may not be masters; Dirichlet masters drop out of the operators
+ * (closed zero_constraints). The operators then are those of the reference's condensed system
+ * (AffineConstraints::distribute_local_to_global): residual and J.v rows of hanging DoFs are
+ * condensed onto their masters, the hanging rows themselves are 0 / D_c v; gls_apply_dirichlet
+ * also distributes the hanging values (nonzero_constraints.distribute). The diagonal returned by
+ * gls_jacobian_diagonal stays the element-diagonal sum on unconstrained rows (a Jacobi scaling,
+ * not the condensed diagonal). Single GPU, per-cell kernels (no bricks, no multigrid). */
+int gls_set_hanging(gls_ctx *ctx, int64_t n_lines, const int64_t *dofs, const int64_t *offsets,
+                    const int64_t *masters, const double *weights);
+
 /* Diagonal of that assembled Jacobian (DEVICE pointer). */
 int gls_jacobian_diagonal(gls_ctx *ctx, double *diag);
 
@@ -241,6 +255,35 @@ int gls_mesh_hyper_cube_sizes(int dim, int n, int k, int kp, int periodic_mask,
 int gls_mesh_hyper_cube(int dim, int n, int k, int kp, double lo, double hi, int periodic_mask,
                         int32_t *cell_vnodes, int32_t *cell_pnodes, double *cell_x0, double *cell_h);
 
+/* Locally refined hyper_cube (one extra level): hyper_cube(lo, hi) with n^dim cells, the cells
+ * flagged in refine[n^dim] (lexicographic, x fastest; NULL = none) split into 2^dim children
+ * (execute_coarsening_and_refinement on a p4est forest, navier_stokes_base.cc:592-780). Nodes are
+ * numbered lexicographically on the fine node lattice; hanging nodes are constrained to the
+ * unrefined neighbour's nodes: value(node) = sum_j w_j value(master_j) (node level, for every
+ * component; see gls_set_hanging for the DoF-level lines). Velocity FE_Q(k) and pressure
+ * FE_Q(kp) spaces, 1 <= kp <= k <= 2. Owned storage, freed by gls_mesh_refined_destroy. */
+typedef struct {
+  int dim, k, kp;
+  int64_t n_cells, n_vnodes, n_pnodes;
+  const int32_t *cell_vnodes;   /* [n_cells][(k+1)^dim] lexicographic local order */
+  const int32_t *cell_pnodes;   /* [n_cells][(kp+1)^dim] */
+  const int32_t *cell_level;    /* [n_cells] 0 unrefined, 1 child of a refined cell */
+  const double *cell_x0, *cell_h;  /* [n_cells][dim] */
+  const double *vnode_x, *pnode_x; /* [n_vnodes][dim], [n_pnodes][dim] */
+  int64_t n_vhang;              /* hanging velocity node vhang_node[i] = sum over j in           */
+  const int64_t *vhang_node;    /*   [vhang_off[i], vhang_off[i+1]) of vhang_w[j] * node          */
+  const int64_t *vhang_off;     /*   vhang_master[j]                                              */
+  const int64_t *vhang_master;
+  const double *vhang_w;
+  int64_t n_phang;              /* the same for the pressure nodes */
+  const int64_t *phang_node, *phang_off, *phang_master;
+  const double *phang_w;
+  void *impl_;                  /* owned storage (opaque) */
+} gls_refined_mesh;
+int gls_mesh_refined_create(int dim, int n, int k, int kp, double lo, double hi, const int32_t *refine,
+                            gls_refined_mesh **out);
+int gls_mesh_refined_destroy(gls_refined_mesh *mesh);
+
 /* ------------------------------------------------------------------------------------------
  * Drop-in I/O surface, host side.
  * Parameter files: deal.II ParameterHandler text (`subsection`/`end`, `set key = value`, `#`
@@ -279,7 +322,7 @@ int gls_pvd_write(const char *filename, int n, const double *times, const char *
  * ------------------------------------------------------------------------------------------ */
 int gls_timing_reset(gls_ctx *ctx);
 /* which: 0 residual, 1 jacobian_apply, 2 diagonal, 3 J.v linearization (once per state),
- * 4 FP32 J.v of the mixed-precision V-cycle;
+ * 4 FP32 J.v of the mixed-precision V-cycle, 5 brick-surface slab sums (after each brick launch);
  * returns total ms and launch count */
 int gls_timing_get(gls_ctx *ctx, int which, double *total_ms, int64_t *count);
 int gls_timing_enable(gls_ctx *ctx, int enable);

@@ -535,6 +535,27 @@ int gls_oracle_local_system(const gls_oracle_problem *p, int cell,
   return 0;
 }
 
+/* where local DoF row/column g of an element lands in the condensed system: itself when
+ * unconstrained, its unconstrained masters (weights) when hanging, nowhere when Dirichlet */
+#define MAXT 64
+static int dof_targets(const gls_oracle_problem *p, int g, int *tg, double *tw) {
+  if (!p->constrained[g]) {
+    tg[0] = g;
+    tw[0] = 1.0;
+    return 1;
+  }
+  if (!p->hang_off) return 0;
+  int n = 0;
+  for (int j = p->hang_off[g]; j < p->hang_off[g + 1] && n < MAXT; ++j) {
+    const int m = p->hang_master[j];
+    if (p->constrained[m]) continue;
+    tg[n] = m;
+    tw[n] = p->hang_w[j];
+    ++n;
+  }
+  return n;
+}
+
 int gls_oracle_assemble_rhs(const gls_oracle_problem *p,
                             const double *u, const double *u1, const double *u2, const double *u3,
                             double *rhs) {
@@ -547,8 +568,12 @@ int gls_oracle_assemble_rhs(const gls_oracle_problem *p,
   for (int c = 0; c < p->n_cells; ++c) {
     local_system(p, &t, c, u, u1, u2, u3, NULL, Fe, dofs);
     /* zero_constraints.distribute_local_to_global(local_rhs, ...), :767-771 */
-    for (int i = 0; i < nd; ++i)
-      if (!p->constrained[dofs[i]]) rhs[dofs[i]] += Fe[i];
+    for (int i = 0; i < nd; ++i) {
+      int tg[MAXT];
+      double tw[MAXT];
+      const int nt = dof_targets(p, dofs[i], tg, tw);
+      for (int a = 0; a < nt; ++a) rhs[tg[a]] += tw[a] * Fe[i];
+    }
   }
   free(Fe); free(dofs); tab_free(&t);
   return 0;
@@ -561,6 +586,28 @@ static double constrained_diag(const double *Ke, int nd, int i) {
   double avg = 0.;
   for (int j = 0; j < nd; ++j) avg += fabs(Ke[(size_t)j * nd + j]);
   return avg / nd;
+}
+
+/* number of COO triplets gls_oracle_assemble_coo will emit (hanging rows/cols expand onto masters) */
+long long gls_oracle_coo_size(const gls_oracle_problem *p) {
+  const int nd = gls_oracle_dofs_per_cell(p);
+  int *dofs = malloc(sizeof(int) * nd);
+  int *cnt = malloc(sizeof(int) * nd);
+  long long n = 0;
+  for (int c = 0; c < p->n_cells; ++c) {
+    gls_oracle_cell_dofs(p, c, dofs);
+    long long row = 0;
+    for (int i = 0; i < nd; ++i) {
+      int tg[MAXT];
+      double tw[MAXT];
+      cnt[i] = dof_targets(p, dofs[i], tg, tw);
+      row += cnt[i];
+      if (p->constrained[dofs[i]]) ++n;
+    }
+    for (int i = 0; i < nd; ++i) n += (long long)cnt[i] * row;
+  }
+  free(cnt); free(dofs);
+  return n;
 }
 
 int gls_oracle_assemble_coo(const gls_oracle_problem *p,
@@ -578,15 +625,17 @@ int gls_oracle_assemble_coo(const gls_oracle_problem *p,
     local_system(p, &t, c, u, u1, u2, u3, Ke, Fe, dofs);
     for (int i = 0; i < nd; ++i) {
       const int gi = dofs[i];
-      if (p->constrained[gi]) {
-        rows[n] = gi; cols[n] = gi; vals[n] = constrained_diag(Ke, nd, i); ++n;
-        continue;
-      }
-      rhs[gi] += Fe[i];
+      if (p->constrained[gi]) { rows[n] = gi; cols[n] = gi; vals[n] = constrained_diag(Ke, nd, i); ++n; }
+      int ti[MAXT], tj[MAXT];
+      double wi[MAXT], wj[MAXT];
+      const int ni = dof_targets(p, gi, ti, wi);
+      for (int a = 0; a < ni; ++a) rhs[ti[a]] += wi[a] * Fe[i];
       for (int j = 0; j < nd; ++j) {
-        const int gj = dofs[j];
-        if (p->constrained[gj]) continue;
-        rows[n] = gi; cols[n] = gj; vals[n] = Ke[(size_t)i * nd + j]; ++n;
+        const int nj = dof_targets(p, dofs[j], tj, wj);
+        for (int a = 0; a < ni; ++a)
+          for (int b = 0; b < nj; ++b) {
+            rows[n] = ti[a]; cols[n] = tj[b]; vals[n] = wi[a] * wj[b] * Ke[(size_t)i * nd + j]; ++n;
+          }
       }
     }
   }
@@ -604,19 +653,30 @@ int gls_oracle_jacobian_apply(const gls_oracle_problem *p,
   int *dofs = malloc(sizeof(int) * nd);
   double *Fe = malloc(sizeof(double) * nd);
   double *Ke = malloc(sizeof(double) * nd * nd);
+  double *vloc = malloc(sizeof(double) * nd);
   for (int i = 0; i < N; ++i) y[i] = 0.;
   for (int c = 0; c < p->n_cells; ++c) {
     local_system(p, &t, c, u, u1, u2, u3, Ke, Fe, dofs);
+    for (int j = 0; j < nd; ++j) {  /* (C v) at the element's DoFs */
+      int tj[MAXT];
+      double wj[MAXT];
+      const int nj = dof_targets(p, dofs[j], tj, wj);
+      double x = 0.;
+      for (int b = 0; b < nj; ++b) x += wj[b] * v[tj[b]];
+      vloc[j] = x;
+    }
     for (int i = 0; i < nd; ++i) {
       const int gi = dofs[i];
-      if (p->constrained[gi]) { y[gi] += constrained_diag(Ke, nd, i) * v[gi]; continue; }
+      if (p->constrained[gi]) y[gi] += constrained_diag(Ke, nd, i) * v[gi];
       double s = 0.;
-      for (int j = 0; j < nd; ++j)
-        if (!p->constrained[dofs[j]]) s += Ke[(size_t)i * nd + j] * v[dofs[j]];
-      y[gi] += s;
+      for (int j = 0; j < nd; ++j) s += Ke[(size_t)i * nd + j] * vloc[j];
+      int ti[MAXT];
+      double wi[MAXT];
+      const int ni = dof_targets(p, gi, ti, wi);
+      for (int a = 0; a < ni; ++a) y[ti[a]] += wi[a] * s;
     }
   }
-  free(Ke); free(Fe); free(dofs); tab_free(&t);
+  free(vloc); free(Ke); free(Fe); free(dofs); tab_free(&t);
   return 0;
 }
 
@@ -634,7 +694,20 @@ int gls_oracle_jacobian_diagonal(const gls_oracle_problem *p,
     local_system(p, &t, c, u, u1, u2, u3, Ke, Fe, dofs);
     for (int i = 0; i < nd; ++i) {
       const int gi = dofs[i];
-      dg[gi] += p->constrained[gi] ? constrained_diag(Ke, nd, i) : Ke[(size_t)i * nd + i];
+      if (p->constrained[gi]) dg[gi] += constrained_diag(Ke, nd, i);
+      if (!p->hang_off) {
+        if (!p->constrained[gi]) dg[gi] += Ke[(size_t)i * nd + i];
+        continue;
+      }
+      int ti[MAXT], tj[MAXT];  /* exact diagonal of C^T K C */
+      double wi[MAXT], wj[MAXT];
+      const int ni = dof_targets(p, gi, ti, wi);
+      for (int j = 0; j < nd; ++j) {
+        const int nj = dof_targets(p, dofs[j], tj, wj);
+        for (int a = 0; a < ni; ++a)
+          for (int b = 0; b < nj; ++b)
+            if (ti[a] == tj[b]) dg[ti[a]] += wi[a] * wj[b] * Ke[(size_t)i * nd + j];
+      }
     }
   }
   free(Ke); free(Fe); free(dofs); tab_free(&t);

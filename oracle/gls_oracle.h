@@ -14,7 +14,8 @@
  *   calculate_L2_error            source/solvers/navier_stokes_base.cc:253-380
  *   AffineConstraints::distribute_local_to_global (deal.II 9.2, not vendored):
  *       constrained rows/cols dropped, diagonal += |local(i,i)| (or the mean
- *       |diagonal| of the local matrix when that entry is 0), rhs rows zero.
+ *       |diagonal| of the local matrix when that entry is 0), rhs rows zero;
+ *       hanging rows/cols condensed onto their masters (C^T K C, C^T F).
  *
  * Pinning: the restatement is checked end-to-end against the reference's own
  * golden outputs (mms2d_gls / mms3d_gls L2 error tables, restart_01, bdf_01);
@@ -53,6 +54,13 @@ typedef struct {
   const double *force_q; /* [n_cells*nq*dim] forcing at quadrature points, NULL = NoForce */
   int srf;               /* VelocitySourceType::srf */
   double omega[3];       /* omega_x, omega_y, omega_z */
+  /* hanging-node constraint lines (DoFTools::make_hanging_node_constraints, gls_navier_stokes.cc:84,143):
+   * DoF i (constrained[i] = 1) = sum_{j in [hang_off[i], hang_off[i+1])} hang_w[j] * DoF hang_master[j];
+   * hang_off[n_dofs+1] per DoF (empty range: not hanging), NULL = no hanging nodes. Constrained
+   * masters drop out (AffineConstraints::close on zero_constraints). */
+  const int *hang_off;
+  const int *hang_master;
+  const double *hang_w;
 } gls_oracle_problem;
 
 int gls_oracle_n_dofs(const gls_oracle_problem *p);
@@ -77,6 +85,8 @@ int gls_oracle_assemble_rhs(const gls_oracle_problem *p,
 int gls_oracle_assemble_coo(const gls_oracle_problem *p,
                             const double *u, const double *u1, const double *u2, const double *u3,
                             int *rows, int *cols, double *vals, long long *nnz, double *rhs);
+
+long long gls_oracle_coo_size(const gls_oracle_problem *p);
 
 /* y = J v for the reference's assembled (constraint-eliminated) Jacobian, element by element */
 int gls_oracle_jacobian_apply(const gls_oracle_problem *p,

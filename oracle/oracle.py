@@ -45,6 +45,7 @@ class _Problem(C.Structure):
         ("constrained", C.POINTER(C.c_ubyte)),
         ("viscosity", C.c_double), ("scheme", C.c_int), ("time_steps", C.c_double * 4),
         ("force_q", C.POINTER(C.c_double)), ("srf", C.c_int), ("omega", C.c_double * 3),
+        ("hang_off", C.POINTER(C.c_int)), ("hang_master", C.POINTER(C.c_int)), ("hang_w", C.POINTER(C.c_double)),
     ]
 
 
@@ -80,6 +81,8 @@ def lib():
         _lib.gls_oracle_cell_dofs.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
         _lib.gls_oracle_time_local_systems.argtypes = [P, d, d, d, d, C.c_int, C.c_int, C.c_int, C.c_int]
         _lib.gls_oracle_time_local_systems.restype = C.c_double
+        _lib.gls_oracle_coo_size.argtypes = [P]
+        _lib.gls_oracle_coo_size.restype = C.c_longlong
     return _lib
 
 
@@ -139,6 +142,24 @@ class StructuredProblem:
         self.constrained = np.zeros(self.n_dofs, dtype=np.uint8)
         self.dirichlet = {}  # dof -> value (nonzero_constraints)
         self.force_q = None
+        self.hang = None  # (off[n_dofs+1], master[], w[]) hanging-node lines per DoF
+
+    @classmethod
+    def from_refined(cls, mesh, lo=-1.0, hi=1.0, colorize=False, **kw):
+        """Problem on a locally refined hyper_cube (the product's gls_mesh_refined_create arrays, a
+        plain mesh description): per-cell boxes and node maps, explicit node coordinates; the
+        hanging lines are set separately (set_hanging) and become constrained DoFs."""
+        dim, k, kp = mesh["dim"], mesh["k"], mesh["kp"]
+        p = cls(dim, 1, k=k, kp=kp, lo=lo, hi=hi, colorize=colorize, **kw)
+        p.cell_x0 = np.ascontiguousarray(mesh["cell_x0"], dtype=np.float64)
+        p.cell_h = np.ascontiguousarray(mesh["cell_h"], dtype=np.float64)
+        p.cell_vnodes = np.ascontiguousarray(mesh["cell_vnodes"], dtype=np.int32)
+        p.cell_pnodes = np.ascontiguousarray(mesh["cell_pnodes"], dtype=np.int32)
+        p.n_vnodes, p.n_pnodes = int(mesh["n_vnodes"]), int(mesh["n_pnodes"])
+        p.n_dofs = dim * p.n_vnodes + p.n_pnodes
+        p.constrained = np.zeros(p.n_dofs, dtype=np.uint8)
+        p._vx = np.ascontiguousarray(mesh["vnode_x"], dtype=np.float64)
+        return p
 
     def _cell_nodes(self, k, shape):
         dim = self.dim
@@ -154,6 +175,8 @@ class StructuredProblem:
 
     # --- geometry of the velocity lattice
     def vnode_coords(self):
+        if getattr(self, "_vx", None) is not None:
+            return self._vx
         dim = self.dim
         ijk = np.indices(tuple(self.vshape[::-1])).reshape(dim, -1)[::-1].T
         return self.lo + ijk * (self.hc / self.k)
@@ -178,6 +201,8 @@ class StructuredProblem:
         X = self.vnode_coords()
         bids = self.boundary_ids_of_vnodes()
         self.constrained[:] = 0
+        if self.hang is not None:  # hanging DoFs stay constrained to their masters (first constraint wins)
+            self.constrained[np.nonzero(self.hang[0][1:] > self.hang[0][:-1])[0]] = 1
         self.dirichlet = {}
         for typ, bid, func in bcs:
             nodes = np.array([i for i, s in enumerate(bids) if bid in s], dtype=np.int64)
@@ -198,9 +223,31 @@ class StructuredProblem:
         return self
 
     def apply_nonzero_constraints(self, x):
+        """nonzero_constraints.distribute: Dirichlet values, then hanging values from their masters."""
         for dof, v in self.dirichlet.items():
             x[dof] = v
+        if self.hang is not None:
+            off, mas, w = self.hang
+            for i in np.nonzero(off[1:] > off[:-1])[0]:
+                x[i] = float(np.dot(w[off[i]:off[i + 1]], x[mas[off[i]:off[i + 1]]]))
         return x
+
+    def set_hanging(self, dofs, offsets, masters, weights):
+        """hanging-node lines (DoF level, as gls_set_hanging): the hanging DoFs become constrained."""
+        cnt = np.zeros(self.n_dofs + 1, dtype=np.int64)
+        lines = {}
+        for i, d in enumerate(dofs):
+            lines[int(d)] = (masters[offsets[i]:offsets[i + 1]], weights[offsets[i]:offsets[i + 1]])
+            cnt[int(d) + 1] = offsets[i + 1] - offsets[i]
+        off = np.cumsum(cnt)
+        mas = np.zeros(int(off[-1]), dtype=np.int32)
+        w = np.zeros(int(off[-1]))
+        for d, (m, ww) in lines.items():
+            mas[off[d]:off[d + 1]] = m
+            w[off[d]:off[d + 1]] = ww
+            self.constrained[d] = 1
+        self.hang = (np.ascontiguousarray(off, dtype=np.int32), mas, w)
+        return self
 
     def qpoints(self, nq1d=None):
         nq1d = nq1d or self.nq1d
@@ -240,8 +287,12 @@ class StructuredProblem:
         P.srf = 1 if self.srf else 0
         for i in range(3):
             P.omega[i] = self.omega[i]
+        if self.hang is not None:
+            P.hang_off = self.hang[0].ctypes.data_as(C.POINTER(C.c_int))
+            P.hang_master = self.hang[1].ctypes.data_as(C.POINTER(C.c_int))
+            P.hang_w = _dp(self.hang[2])
         self._keep = (self.cell_x0, self.cell_h, self.cell_vnodes, self.cell_pnodes, self.constrained,
-                      self.force_q)
+                      self.force_q, self.hang)
         return P
 
 
@@ -283,8 +334,7 @@ class Oracle:
     def matrix_and_rhs(self, u, u1=None, u2=None, u3=None):
         import scipy.sparse as sp
         P = self.p.struct()
-        nd = self.L.gls_oracle_dofs_per_cell(C.byref(P))
-        cap = self.p.n_cells * nd * nd
+        cap = max(1, int(self.L.gls_oracle_coo_size(C.byref(P))))
         rows = np.zeros(cap, dtype=np.int32)
         cols = np.zeros(cap, dtype=np.int32)
         vals = np.zeros(cap)

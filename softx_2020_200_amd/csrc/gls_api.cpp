@@ -311,6 +311,16 @@ struct gls_ctx {
     gls_allreduce_fn allreduce = nullptr;
     void *user = nullptr;
   } dist;
+  // hanging-node constraints (gls_set_hanging): lines dof <- sum w * master
+  struct Hang {
+    bool on = false;
+    DevBuf<int64_t> dof, off, master, ooff, omaster;  // all lines; operator lines (Dirichlet masters dropped)
+    DevBuf<double> w, ow;
+    DevBuf<int64_t> tm, toff, tdof;                     // operator lines transposed: master -> (hanging dof, w)
+    DevBuf<double> tw;
+    DevBuf<uint8_t> hmask;                             // hanging velocity components per node
+    DevBuf<double> vbuf;                               // C v for J.v
+  } hang;
   // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
   struct Lattice {
     bool set = false;
@@ -367,8 +377,9 @@ struct gls_ctx {
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
   std::vector<Ev> events;
-  double t_ms[5] = {0, 0, 0, 0, 0};  // residual, J.v, diagonal, J.v linearization, FP32 smoother J.v
-  int64_t t_n[5] = {0, 0, 0, 0, 0};
+  // residual, J.v, diagonal, J.v linearization, FP32 smoother J.v, brick-surface slab sums
+  double t_ms[6] = {0, 0, 0, 0, 0, 0};
+  int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
 
   ~gls_ctx() {
     for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -590,21 +601,32 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     mode = gls::MODE_LIN;
     lin_diag = true;
   }
+  if (mode == gls::MODE_JV && c->hang.on) {  // C v: hanging entries interpolated from their masters
+    if (c->hang.vbuf.n != (size_t)c->n_dofs) GLS_TRY(c->hang.vbuf.alloc((size_t)c->n_dofs));
+    HIP_TRY(gls::vec_copy(c->hang.vbuf.p, v, c->n_dofs, c->stream));
+    HIP_TRY(gls::vec_csr_gather_set(c->hang.vbuf.p, c->hang.vbuf.p, c->hang.dof.p, c->hang.ooff.p, c->hang.omaster.p,
+                                    c->hang.ow.p, (int64_t)c->hang.dof.n, c->stream));
+    v = c->hang.vbuf.p;
+  }
   P.v = v;
   P.y = y;
+  P.hmask = c->hang.on ? c->hang.hmask.p : nullptr;
   const bool brick = c->use_brick && mode != gls::MODE_DIAG;
   P.slab = brick ? brick_slab(c) : nullptr;  // every node is then written exactly once: no zeroing
   if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
-    if (brick) {
-      HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
-      if (P.slab) HIP_TRY(slab_sum(c, y));
-    } else {
-      HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
-    }
+    if (brick) HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
+    else HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+  }
+  if (brick && P.slab) {
+    TimedLaunch t(c, 5);
+    HIP_TRY(slab_sum(c, y));
   }
   GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
+  if (c->hang.on && (mode == gls::MODE_RESIDUAL || mode == gls::MODE_JV))  // C^T y: rows onto masters
+    HIP_TRY(gls::vec_csr_condense(y, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
+                                  (int64_t)c->hang.tm.n, c->stream));
   if (lin_diag) {  // the same launch stored the J.v linearization
     c->qd_valid = true;
     c->qd32_valid = false;
@@ -921,7 +943,10 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
   {
     TimedLaunch t(g, 4);
     HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
-    if (P.slab) HIP_TRY(slab_sum(g, y));
+  }
+  if (P.slab) {
+    TimedLaunch t(g, 5);
+    HIP_TRY(slab_sum(g, y));
   }
   GLS_TRY(dist_export_add(g, y));
   HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream));
@@ -954,11 +979,95 @@ int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *
 int gls_apply_dirichlet(gls_ctx *c, double *x) {
   GLS_TRY(check_ctx(c));
   HIP_TRY(gls::vec_set_indexed(x, c->dir_dofs.p, c->dir_vals.p, (int64_t)c->dir_dofs.n, c->stream));
+  if (c->hang.on)  // hanging values from their masters (all masters: Dirichlet values included)
+    HIP_TRY(gls::vec_csr_gather_set(x, x, c->hang.dof.p, c->hang.off.p, c->hang.master.p, c->hang.w.p,
+                                    (int64_t)c->hang.dof.n, c->stream));
   if (x == c->u || x == c->u1 || x == c->u2 || x == c->u3) {  // the captured state changed
     c->diag_valid = false;
     c->qd_valid = false;
     c->mg.dirty = true;
   }
+  return GLS_OK;
+}
+
+int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *off, const int64_t *masters,
+                    const double *w) {
+  GLS_TRY(check_ctx(c));
+  if (n < 0 || (n > 0 && (!dofs || !off || !masters || !w))) return set_err(GLS_EINVAL, "gls_set_hanging: arrays");
+  if (c->dist.on || c->mg.on) return set_err(GLS_EINVAL, "hanging constraints: single GPU, no multigrid");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int dim = c->dim;
+  const int64_t N = c->n_dofs, nvd = (int64_t)dim * c->n_vnodes;
+  std::vector<uint8_t> vm((size_t)c->n_vnodes, 0);
+  if (c->vmask.p) HIP_TRY(hipMemcpy(vm.data(), c->vmask.p, (size_t)c->n_vnodes, hipMemcpyDeviceToHost));
+  auto dirichlet = [&](int64_t d) { return d < nvd && ((vm[(size_t)(d / dim)] >> (d % dim)) & 1); };
+  std::vector<char> is_h((size_t)N, 0);
+  if (n > 0 && off[0] != 0) return set_err(GLS_EINVAL, "gls_set_hanging: offsets[0] != 0");
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t d = dofs[i];
+    if (d < 0 || d >= N || off[i + 1] < off[i]) return set_err(GLS_EINVAL, "gls_set_hanging: line %lld", (long long)i);
+    if (dirichlet(d)) return set_err(GLS_EINVAL, "hanging DoF %lld carries a Dirichlet mask bit", (long long)d);
+    if (is_h[(size_t)d]) return set_err(GLS_EINVAL, "hanging DoF %lld listed twice", (long long)d);
+    is_h[(size_t)d] = 1;
+  }
+  const int64_t nm = n ? off[n] : 0;
+  for (int64_t j = 0; j < nm; ++j)
+    if (masters[j] < 0 || masters[j] >= N || is_h[(size_t)masters[j]])
+      return set_err(GLS_EINVAL, "gls_set_hanging: master %lld out of range or hanging itself", (long long)masters[j]);
+  // operator lines (closed zero_constraints: Dirichlet masters drop out) and their transpose
+  std::vector<int64_t> ooff{0}, omas, cnt((size_t)N + 1, 0);
+  std::vector<double> ow;
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t j = off[i]; j < off[i + 1]; ++j)
+      if (!dirichlet(masters[j])) {
+        omas.push_back(masters[j]);
+        ow.push_back(w[j]);
+        ++cnt[(size_t)masters[j] + 1];
+      }
+    ooff.push_back((int64_t)omas.size());
+  }
+  std::vector<int64_t> tm, toff{0};
+  std::vector<int64_t> start((size_t)N + 1, 0);
+  for (int64_t m = 0; m < N; ++m) {
+    start[(size_t)m + 1] = start[(size_t)m] + cnt[(size_t)m + 1];
+    if (cnt[(size_t)m + 1]) {
+      tm.push_back(m);
+      toff.push_back(start[(size_t)m + 1]);
+    }
+  }
+  std::vector<int64_t> tdof(omas.size()), fill(start.begin(), start.end() - 1);
+  std::vector<double> tw(omas.size());
+  for (int64_t i = 0; i < n; ++i)  // lines in order: each master sums its hanging rows in a fixed order
+    for (int64_t j = ooff[(size_t)i]; j < ooff[(size_t)i + 1]; ++j) {
+      const int64_t slot = fill[(size_t)omas[(size_t)j]]++;
+      tdof[(size_t)slot] = dofs[i];
+      tw[(size_t)slot] = ow[(size_t)j];
+    }
+  std::vector<uint8_t> hm((size_t)c->n_vnodes, 0);
+  std::vector<int64_t> con;  // zero_constraints: Dirichlet + hanging
+  for (int64_t d = 0; d < N; ++d) {
+    if (is_h[(size_t)d] && d < nvd) hm[(size_t)(d / dim)] |= (uint8_t)(1u << (d % dim));
+    if (is_h[(size_t)d] || dirichlet(d)) con.push_back(d);
+  }
+  auto &h = c->hang;
+  GLS_TRY(h.dof.upload(dofs, (size_t)n));
+  GLS_TRY(h.off.upload(off, (size_t)(n ? n + 1 : 0)));
+  GLS_TRY(h.master.upload(masters, (size_t)nm));
+  GLS_TRY(h.w.upload(w, (size_t)nm));
+  GLS_TRY(h.ooff.upload(ooff.data(), n ? ooff.size() : 0));
+  GLS_TRY(h.omaster.upload(omas.data(), omas.size()));
+  GLS_TRY(h.ow.upload(ow.data(), ow.size()));
+  GLS_TRY(h.tm.upload(tm.data(), tm.size()));
+  GLS_TRY(h.toff.upload(toff.data(), tm.empty() ? 0 : toff.size()));
+  GLS_TRY(h.tdof.upload(tdof.data(), tdof.size()));
+  GLS_TRY(h.tw.upload(tw.data(), tw.size()));
+  GLS_TRY(h.hmask.upload(hm.data(), hm.size()));
+  GLS_TRY(c->con_dofs.upload(con.data(), con.size()));
+  h.on = n > 0;
+  c->use_brick = false;  // mixed cell sizes: the general per-cell kernels
+  c->use_slab = false;
+  c->diag_valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -1219,6 +1328,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   GLS_TRY(check_ctx(c));
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
   if (c->dim != 3 || c->k > 2 || c->k != c->kp) return set_err(GLS_EINVAL, "mg: 3D Q1-Q1 / Q2-Q2 only");
+  if (c->hang.on) return set_err(GLS_EINVAL, "mg: not with hanging-node constraints");
   auto &mg = c->mg;
   mg = gls_ctx::MG();
   mg.boxed = c->dist.on;
@@ -1708,12 +1818,12 @@ int gls_timing_reset(gls_ctx *c) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   c->events.clear();
-  for (int i = 0; i < 5; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
+  for (int i = 0; i < 6; ++i) { c->t_ms[i] = 0; c->t_n[i] = 0; }
   return GLS_OK;
 }
 int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
   GLS_TRY(check_ctx(c));
-  if (which < 0 || which > 4) return set_err(GLS_EINVAL, "which");
+  if (which < 0 || which > 5) return set_err(GLS_EINVAL, "which");
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto &e : c->events) {
     float t = 0;

@@ -362,7 +362,8 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
           out[c] += JxW * (nu * gg + Gcc * N * N + ug * N + aj * N * N + tau * Sc * ug + tau * Rc * g[c] * N);
         }
       }
-      const unsigned m = P.vmask ? P.vmask[node] : 0u;
+      // constrained rows (Dirichlet or hanging) get deal.II's |K_e(i,i)| per cell
+      const unsigned m = (P.vmask ? P.vmask[node] : 0u) | (P.hmask ? P.hmask[node] : 0u);
 #pragma unroll
       for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], ((m >> c) & 1u) ? fabs(out[c]) : out[c]);
     }

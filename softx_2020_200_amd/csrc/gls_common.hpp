@@ -40,6 +40,7 @@ struct OpParams {
   const double *x0;           // [n_cells][3] (SRF only)
   const double *force_q;      // [n_cells][nq][dim] or nullptr
   const uint8_t *vmask;       // [n_vnodes] zero_constraints bits, nullptr = none
+  const uint8_t *hmask;       // [n_vnodes] hanging velocity components (MODE_DIAG: |K_ii| per cell)
   const double *u;
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input

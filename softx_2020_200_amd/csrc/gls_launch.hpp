@@ -51,6 +51,11 @@ hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const 
 hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
                               int64_t n1, int64_t off2, int64_t n2, bool dots, double *out, double *work,
                               hipStream_t s);
+// hanging-node constraint lines (CSR): distribute x[dof] = sum w src[master]; condense onto masters
+hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, const int64_t *off,
+                              const int64_t *master, const double *w, int64_t n, hipStream_t s);
+hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
+                            int64_t n, hipStream_t s);
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
                                 hipStream_t s);  // y[idx] = d[idx]*v[idx]
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)

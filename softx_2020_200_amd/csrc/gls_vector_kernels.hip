@@ -148,6 +148,28 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
   }
 }
 
+// constraint lines: x[dof[i]] = sum_{j in [off[i], off[i+1])} w[j] * src[master[j]]
+// (masters are never constrained lines themselves, so src may alias x)
+__global__ void k_csr_gather_set(double *x, const double *src, const int64_t *__restrict__ dof,
+                                 const int64_t *__restrict__ off, const int64_t *__restrict__ master,
+                                 const double *__restrict__ w, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.;
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) s += w[j] * src[master[j]];
+    x[dof[i]] = s;
+  }
+}
+// condensation onto masters: y[tm[i]] += sum_{j in [toff[i], toff[i+1])} tw[j] * y[tdof[j]]
+// (one thread per master, fixed order: deterministic)
+__global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const int64_t *__restrict__ toff,
+                               const int64_t *__restrict__ tdof, const double *__restrict__ tw, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.;
+    for (int64_t j = toff[i]; j < toff[i + 1]; ++j) s += tw[j] * y[tdof[j]];
+    y[tm[i]] += s;
+  }
+}
+
 __global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = idx[j];
@@ -271,6 +293,19 @@ hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, c
 #undef MX
   }
   hipLaunchKernelGGL(k_reduce_rows, dim3(dots ? nk + 1 : 1), dim3(kBlock), 0, s, work, nb, out);
+  return hipGetLastError();
+}
+
+hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, const int64_t *off,
+                              const int64_t *master, const double *w, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_csr_gather_set, dim3(grid_for(n)), dim3(kBlock), 0, s, x, src, dof, off, master, w, n);
+  return hipGetLastError();
+}
+hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
+                            int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_csr_condense, dim3(grid_for(n)), dim3(kBlock), 0, s, y, tm, toff, tdof, tw, n);
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ EXPORTS = [
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
+    "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
 ]
 
 
@@ -62,6 +63,20 @@ class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
                 ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
                 ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int)]
+
+
+class RefinedMesh(C.Structure):
+    _fields_ = [("dim", C.c_int), ("k", C.c_int), ("kp", C.c_int),
+                ("n_cells", C.c_int64), ("n_vnodes", C.c_int64), ("n_pnodes", C.c_int64),
+                ("cell_vnodes", C.POINTER(C.c_int32)), ("cell_pnodes", C.POINTER(C.c_int32)),
+                ("cell_level", C.POINTER(C.c_int32)),
+                ("cell_x0", C.POINTER(C.c_double)), ("cell_h", C.POINTER(C.c_double)),
+                ("vnode_x", C.POINTER(C.c_double)), ("pnode_x", C.POINTER(C.c_double)),
+                ("n_vhang", C.c_int64), ("vhang_node", C.POINTER(C.c_int64)), ("vhang_off", C.POINTER(C.c_int64)),
+                ("vhang_master", C.POINTER(C.c_int64)), ("vhang_w", C.POINTER(C.c_double)),
+                ("n_phang", C.c_int64), ("phang_node", C.POINTER(C.c_int64)), ("phang_off", C.POINTER(C.c_int64)),
+                ("phang_master", C.POINTER(C.c_int64)), ("phang_w", C.POINTER(C.c_double)),
+                ("impl_", C.c_void_p)]
 
 
 class NewtonParams(C.Structure):
@@ -115,6 +130,11 @@ def load():
     L.gls_mg_detach.argtypes = [vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
+    P64 = C.POINTER(i64)
+    L.gls_set_hanging.argtypes = [vp, i64, P64, P64, P64, d]
+    L.gls_mesh_refined_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                          C.POINTER(C.c_int32), C.POINTER(C.POINTER(RefinedMesh))]
+    L.gls_mesh_refined_destroy.argtypes = [C.POINTER(RefinedMesh)]
     _lib = L
     return L
 
@@ -168,6 +188,69 @@ def hyper_cube(dim, n, k, kp=None, lo=-1.0, hi=1.0, periodic=()):
                                 cp.ctypes.data_as(C.POINTER(C.c_int32)), _dp(x0), _dp(h)), "gls_mesh_hyper_cube")
     return dict(dim=dim, k=k, kp=kp, n_cells=nc, n_vnodes=nv, n_pnodes=npn, cell_vnodes=cv, cell_pnodes=cp,
                 cell_x0=x0, cell_h=h)
+
+
+def refined_cube(dim, n, k, kp=None, refine=None, lo=-1.0, hi=1.0):
+    """hyper_cube(lo, hi) with n^dim cells, the flagged cells (refine[n^dim], lexicographic) split
+    once more; hanging-node constraint lines per node (C++ builder, gls_mesh_refined_create)."""
+    kp = k if kp is None else kp
+    L = load()
+    nc = n ** dim
+    flags = np.zeros(nc, dtype=np.int32) if refine is None else np.ascontiguousarray(refine, dtype=np.int32)
+    if flags.size != nc:
+        raise GLSError("refine must hold n^dim flags")
+    pm = C.POINTER(RefinedMesh)()
+    check(L.gls_mesh_refined_create(dim, n, k, kp, lo, hi, flags.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    C.byref(pm)), "gls_mesh_refined_create")
+    try:
+        m = pm.contents
+
+        def take(ptr, count, dt, shape=None):
+            a = np.ctypeslib.as_array(ptr, shape=(int(count),)).astype(dt, copy=True) if count else np.zeros(0, dt)
+            return a.reshape(shape) if shape is not None else a
+
+        ncl = int(m.n_cells)
+        out = dict(dim=dim, k=k, kp=kp, n_cells=ncl, n_vnodes=int(m.n_vnodes), n_pnodes=int(m.n_pnodes),
+                   cell_vnodes=take(m.cell_vnodes, ncl * (k + 1) ** dim, np.int32, (ncl, (k + 1) ** dim)),
+                   cell_pnodes=take(m.cell_pnodes, ncl * (kp + 1) ** dim, np.int32, (ncl, (kp + 1) ** dim)),
+                   cell_level=take(m.cell_level, ncl, np.int32),
+                   cell_x0=take(m.cell_x0, ncl * dim, np.float64, (ncl, dim)),
+                   cell_h=take(m.cell_h, ncl * dim, np.float64, (ncl, dim)),
+                   vnode_x=take(m.vnode_x, m.n_vnodes * dim, np.float64, (int(m.n_vnodes), dim)),
+                   pnode_x=take(m.pnode_x, m.n_pnodes * dim, np.float64, (int(m.n_pnodes), dim)))
+        for tag, nh in (("v", int(m.n_vhang)), ("p", int(m.n_phang))):
+            offs = take(getattr(m, tag + "hang_off"), nh + 1, np.int64)
+            nm = int(offs[-1]) if nh else 0
+            out[tag + "hang"] = (take(getattr(m, tag + "hang_node"), nh, np.int64), offs,
+                                 take(getattr(m, tag + "hang_master"), nm, np.int64),
+                                 take(getattr(m, tag + "hang_w"), nm, np.float64))
+        return out
+    finally:
+        L.gls_mesh_refined_destroy(pm)
+
+
+def hanging_dof_lines(mesh):
+    """node-level hanging lines of refined_cube -> DoF-level CSR (dofs, offsets, masters, weights):
+    velocity DoF node*dim + c per component, pressure DoF dim*n_vnodes + node."""
+    dim, nv = mesh["dim"], mesh["n_vnodes"]
+    dofs, offs, mas, ws = [], [0], [], []
+    vn, vo, vm, vw = mesh["vhang"]
+    for i, nd in enumerate(vn):
+        sl = slice(vo[i], vo[i + 1])
+        for c in range(dim):
+            dofs.append(nd * dim + c)
+            mas.extend((vm[sl] * dim + c).tolist())
+            ws.extend(vw[sl].tolist())
+            offs.append(len(mas))
+    pn, po, pmas, pw = mesh["phang"]
+    for i, nd in enumerate(pn):
+        sl = slice(po[i], po[i + 1])
+        dofs.append(dim * nv + nd)
+        mas.extend((dim * nv + pmas[sl]).tolist())
+        ws.extend(pw[sl].tolist())
+        offs.append(len(mas))
+    return (np.array(dofs, dtype=np.int64), np.array(offs, dtype=np.int64), np.array(mas, dtype=np.int64),
+            np.array(ws, dtype=np.float64))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -266,6 +349,14 @@ class GLSContext:
     def set_state(self, u, u1=None, u2=None, u3=None):
         self._state = (u, u1, u2, u3)  # keep tensors alive while borrowed
         check(self.L.gls_set_state(self.h, _ptr(u), _ptr(u1), _ptr(u2), _ptr(u3)), "gls_set_state")
+
+    def set_hanging(self, dofs, offsets, masters, weights):
+        """Hanging-node constraint lines (gls_set_hanging): DoF dofs[i] = sum w * masters."""
+        arrs = [np.ascontiguousarray(a, dtype=t) for a, t in ((dofs, np.int64), (offsets, np.int64),
+                                                               (masters, np.int64), (weights, np.float64))]
+        P64 = C.POINTER(C.c_int64)
+        check(self.L.gls_set_hanging(self.h, len(arrs[0]), arrs[0].ctypes.data_as(P64), arrs[1].ctypes.data_as(P64),
+                                     arrs[2].ctypes.data_as(P64), _dp(arrs[3])), "gls_set_hanging")
 
     def set_force(self, force_q):
         f = None if force_q is None else np.ascontiguousarray(force_q, dtype=np.float64)

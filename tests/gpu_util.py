@@ -3,7 +3,11 @@ import numpy as np
 
 
 def vnode_mask_of(p):
-    c = p.constrained[:p.dim * p.n_vnodes].reshape(p.n_vnodes, p.dim).astype(np.uint8)
+    """zero_constraints mask of the Dirichlet DoFs (hanging DoFs are passed as lines, not masked)."""
+    c = p.constrained[:p.dim * p.n_vnodes].copy()
+    if getattr(p, "hang", None) is not None:
+        c[np.nonzero(p.hang[0][1:p.dim * p.n_vnodes + 1] > p.hang[0][:p.dim * p.n_vnodes])[0]] = 0
+    c = c.reshape(p.n_vnodes, p.dim).astype(np.uint8)
     m = np.zeros(p.n_vnodes, dtype=np.uint8)
     for d in range(p.dim):
         m |= c[:, d] << d
@@ -16,6 +20,8 @@ def context_for(p, **kw):
                      p.n_vnodes, p.n_pnodes, viscosity=p.viscosity, cell_x0=p.cell_x0, vnode_mask=vnode_mask_of(p),
                      force_q=p.force_q, srf=p.srf, omega=p.omega, **kw)
     ctx.set_time(p.scheme, p.time_steps)
+    if getattr(p, "hang_lines", None) is not None:
+        ctx.set_hanging(*p.hang_lines)
     if p.dirichlet:
         dofs = np.array(sorted(p.dirichlet), dtype=np.int64)
         ctx.set_dirichlet(dofs, np.array([p.dirichlet[d] for d in dofs]))

@@ -1,0 +1,175 @@
+"""Hanging-node constraints on a locally refined hyper_cube (reference:
+DoFTools::make_hanging_node_constraints in setup_dofs, gls_navier_stokes.cc:84, 143, and the
+AffineConstraints condensation of assembleGLS, :751-771).
+
+CPU: the C++ builder's constraint weights reproduce every Q_k polynomial (what FE_Q hanging
+constraints must do) and are a partition of unity; the oracle's condensed operators equal an
+independent numpy condensation C^T K C of its own element matrices.
+GPU: residual and J.v of the HIP path equal the oracle's on refined 2D/3D meshes (1e-12), and the
+device Newton/GMRES reaches the oracle's direct-Newton solution of the mms3d_gls problem on a
+refined mesh. Parity of the refined-mesh results is pinned by the oracle only (no reference
+golden exists for this mesh)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, StructuredProblem, muparser_to_numpy, newton_solve
+import softx_2020_200_amd as sx
+
+SEED = 20200200
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.json")))
+
+CASES = [  # dim, n, k, kp, refined coarse cells
+    (2, 3, 1, 1, (0, 4)),
+    (2, 3, 2, 2, (4, 5)),
+    (2, 3, 2, 1, (0, 4, 8)),
+    (3, 2, 1, 1, (0,)),
+    (3, 2, 2, 2, (3,)),
+    (3, 3, 1, 1, (13, 0)),
+]
+
+
+def refined_problem(dim, n, k, kp, cells, scheme="bdf2", nu=0.05, force=True):
+    flags = np.zeros(n ** dim, dtype=np.int32)
+    flags[list(cells)] = 1
+    mesh = sx.refined_cube(dim, n, k, kp, flags)
+    p = StructuredProblem.from_refined(mesh, viscosity=nu, scheme=scheme, time_steps=(0.01, 0.013, 0.011, 0.009))
+    lines = sx.hanging_dof_lines(mesh)
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    p.set_dirichlet([("noslip", 0, None)])
+    if force:
+        p.set_force(lambda X: np.stack([np.sin(X[:, 0] + 2 * X[:, 1]) for _ in range(dim)], 1))
+    return p, mesh
+
+
+def poly_values(X, c):
+    v = np.zeros(X.shape[0])
+    for idx in np.ndindex(*c.shape):
+        t = np.full(X.shape[0], c[idx])
+        for d in range(X.shape[1]):
+            t = t * X[:, d] ** idx[d]
+        v += t
+    return v
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "d%d_n%d_Q%dQ%d" % c[:4])
+def test_hanging_weights_reproduce_qk(case):
+    dim, n, k, kp, cells = case
+    flags = np.zeros(n ** dim, dtype=np.int32)
+    flags[list(cells)] = 1
+    m = sx.refined_cube(dim, n, k, kp, flags)
+    rng = np.random.default_rng(SEED)
+    for tag, deg, X in (("vhang", k, m["vnode_x"]), ("phang", kp, m["pnode_x"])):
+        nodes, off, mas, w = m[tag]
+        assert len(nodes) > 0
+        f = poly_values(X, rng.normal(size=(deg + 1,) * dim))
+        for i, nd in enumerate(nodes):
+            sl = slice(off[i], off[i + 1])
+            assert abs(np.sum(w[sl]) - 1.0) < 1e-13
+            assert abs(np.dot(w[sl], f[mas[sl]]) - f[nd]) < 1e-12 * max(1.0, np.abs(f).max())
+            assert len(set(mas[sl].tolist()) & set(nodes.tolist())) == 0  # masters are never hanging
+    # the refined cells' children tile their parents
+    assert m["n_cells"] == n ** dim + (2 ** dim - 1) * len(cells)
+    assert abs(np.prod(m["cell_h"], axis=1).sum() - 2.0 ** dim) < 1e-12
+
+
+@pytest.mark.parametrize("case", CASES[:4], ids=lambda c: "d%d_n%d_Q%dQ%d" % c[:4])
+def test_oracle_condensation_matches_numpy(case):
+    """Oracle condensed J.v / residual / diagonal == C^T K C, C^T F from its own element systems,
+    condensed here in numpy (independent of the oracle's dof_targets)."""
+    p, mesh = refined_problem(*case)
+    rng = np.random.default_rng(SEED)
+    u, u1, u2, v = (rng.uniform(-1, 1, p.n_dofs) for _ in range(4))
+    import ctypes as C
+    from oracle.oracle import lib, _dp
+    L = lib()
+    P = p.struct()
+    nd = L.gls_oracle_dofs_per_cell(C.byref(P))
+    N = p.n_dofs
+    K = np.zeros((N, N))
+    F = np.zeros(N)
+    dofs = np.zeros(nd, dtype=np.int32)
+    Ke = np.zeros(nd * nd)
+    Fe = np.zeros(nd)
+    for c in range(p.n_cells):
+        L.gls_oracle_local_system(C.byref(P), c, _dp(u), _dp(u1), _dp(u2), _dp(u2), _dp(Ke), _dp(Fe))
+        L.gls_oracle_cell_dofs(C.byref(P), c, dofs.ctypes.data_as(C.POINTER(C.c_int)))
+        K[np.ix_(dofs, dofs)] += Ke.reshape(nd, nd)
+        F[dofs] += Fe
+    con = p.constrained.astype(bool)
+    Cm = np.zeros((N, N))  # u_full = Cm u_free: free DoFs map to themselves, hanging to their free masters
+    off, mas, w = p.hang
+    for i in range(N):
+        if not con[i]:
+            Cm[i, i] = 1.0
+        else:
+            for j in range(off[i], off[i + 1]):
+                if not con[mas[j]]:
+                    Cm[i, mas[j]] += w[j]
+    A = Cm.T @ K @ Cm
+    b = Cm.T @ F
+    A[con, :] = 0.0
+    A[:, con] = 0.0
+    b[con] = 0.0
+    orc = Oracle(p)
+    jv = orc.jacobian_apply(u, v, u1, u2)
+    free = ~con
+    assert np.abs(jv[free] - (A @ v)[free]).max() < 1e-11 * np.abs(jv).max()
+    r = orc.residual(u, u1, u2)
+    assert np.abs(r - b).max() < 1e-11 * np.abs(b).max()
+    d = orc.jacobian_diagonal(u, u1, u2)
+    assert np.abs(d[free] - np.diag(A)[free]).max() < 1e-11 * np.abs(d).max()
+    Acsr, rhs = orc.matrix_and_rhs(u, u1, u2)
+    assert np.abs((Acsr @ v)[free] - jv[free]).max() < 1e-11 * np.abs(jv).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "d%d_n%d_Q%dQ%d" % c[:4])
+def test_hanging_gpu_vs_oracle(case):
+    from tests.gpu_util import context_for, cuda, relerr
+    p, mesh = refined_problem(*case)
+    rng = np.random.default_rng(SEED)
+    u, u1, u2, v = (rng.uniform(-1, 1, p.n_dofs) for _ in range(4))
+    p.apply_nonzero_constraints(u)  # an evaluation point satisfies the constraints
+    orc = Oracle(p)
+    ctx = context_for(p)
+    assert not ctx.uses_brick_kernels
+    ctx.set_state(cuda(u), cuda(u1), cuda(u2))
+    r = ctx.residual().cpu().numpy()
+    assert relerr(r, orc.residual(u, u1, u2)) < 1e-12
+    jv = ctx.jacobian_apply(cuda(v)).cpu().numpy()
+    assert relerr(jv, orc.jacobian_apply(u, v, u1, u2)) < 1e-12
+    # nonzero_constraints.distribute on the device == the oracle's
+    x = rng.uniform(-1, 1, p.n_dofs)
+    X = cuda(x)
+    ctx.apply_dirichlet(X)
+    assert np.abs(X.cpu().numpy() - p.apply_nonzero_constraints(x.copy())).max() < 1e-14
+
+
+@pytest.mark.gpu
+def test_hanging_newton_mms3d():
+    """mms3d_gls (applications_tests/gls_navier_stokes_3d/mms3d_gls.prm) on a 4^3 mesh with the
+    centre 2^3 cells refined: device Newton + GMRES(Jacobi) == the oracle's direct Newton, and the
+    L2 error lies between the reference's uniform 4^3 and 8^3 errors (mms3d_gls.output:17-18)."""
+    from tests.gpu_util import context_for, cuda
+    g = G["mms3d_gls"]
+    F = muparser_to_numpy(g["force"])
+    E = muparser_to_numpy(g["exact"])
+    n = 4
+    cells = [i + n * (j + n * kz) for kz in (1, 2) for j in (1, 2) for i in (1, 2)]
+    p, mesh = refined_problem(3, n, 1, 1, cells, scheme="steady", nu=1.0, force=False)
+    p.set_force(lambda X: F(X)[:, :3])
+    x_ref, its, res = newton_solve(p, tol=1e-10)
+    ctx = context_for(p)
+    x = cuda(p.apply_nonzero_constraints(np.zeros(p.n_dofs)))
+    st = ctx.newton(x, tolerance=1e-10, max_iterations=10, lin_max_iterations=5000, restart=200,
+                    relative_residual=1e-10, minimum_residual=1e-13)
+    assert st["final_residual"] < 1e-10, st
+    xs = x.cpu().numpy()
+    nvd = 3 * p.n_vnodes
+    assert np.abs(xs[:nvd] - x_ref[:nvd]).max() < 1e-8
+    eu, ep = Oracle(p).l2_error(xs, E)
+    assert g["error_velocity"][1] < eu < g["error_velocity"][0], (eu, g["error_velocity"])
