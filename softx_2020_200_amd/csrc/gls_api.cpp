@@ -461,6 +461,26 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   }
   std::vector<int32_t> slots((size_t)(nb * nbnd)), fill(start.begin(), start.end() - 1);
   for (int64_t sl = 0; sl < nb * nbnd; ++sl) slots[(size_t)fill[(size_t)slot_node[(size_t)sl]]++] = (int32_t)sl;
+  // sum order: nodes by their first (lowest) slot, i.e. in slab order of their lowest brick, so
+  // that consecutive threads of k_slab_sum read consecutive slab entries (node order would leave
+  // the x-face nodes of every brick row 4 lattice points apart: 2.3x read amplification, PMC)
+  if (!std::getenv("GLS_SLAB_NODE_ORDER")) {
+    const size_t m = nodes.size();
+    std::vector<int32_t> perm(m);
+    for (size_t i = 0; i < m; ++i) perm[i] = (int32_t)i;
+    std::sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return slots[(size_t)off[a]] < slots[(size_t)off[b]]; });
+    std::vector<int32_t> n2(m), off2{0}, s2;
+    s2.reserve(slots.size());
+    for (size_t i = 0; i < m; ++i) {
+      const int32_t a = perm[i];
+      n2[i] = nodes[(size_t)a];
+      for (int32_t j = off[(size_t)a]; j < off[(size_t)a + 1]; ++j) s2.push_back(slots[(size_t)j]);
+      off2.push_back((int32_t)s2.size());
+    }
+    nodes.swap(n2);
+    off.swap(off2);
+    slots.swap(s2);
+  }
   GLS_TRY(c->sum_nodes.upload(nodes.data(), nodes.size()));
   GLS_TRY(c->sum_off.upload(off.data(), off.size()));
   GLS_TRY(c->sum_slots.upload(slots.data(), slots.size()));

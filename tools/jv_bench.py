@@ -31,8 +31,10 @@ if ctx.uses_brick_kernels:  # FP32 smoother operator (timing slot 4)
         ctx.jacobian_apply_f32(v, y)
 ms_jv, n_jv = ctx.timing_get(1)
 ms_f, n_f = ctx.timing_get(4)
+ms_s, n_s = ctx.timing_get(5)
 ms_r, n_r = ctx.timing_get(0)
 ms_d, n_d = ctx.timing_get(2)
-print("n=%d k=%d brick=%s  J.v %.3f ms  J.v(f32) %.3f ms  residual %.3f ms  diag %.3f ms  linearize %.3f ms "
-      "(cells %d, dofs %d)" % (n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_f / max(n_f, 1), ms_r / n_r,
-                              ms_d / max(n_d, 1), ms_l / max(n_l, 1), prob.mesh["n_cells"], ctx.n_dofs))
+print("n=%d k=%d brick=%s  J.v %.3f ms  J.v(f32) %.3f ms  slab sum %.3f ms  residual %.3f ms  diag %.3f ms  "
+      "linearize %.3f ms (cells %d, dofs %d)" % (n, k, ctx.uses_brick_kernels, ms_jv / n_jv, ms_f / max(n_f, 1),
+                                                 ms_s / max(n_s, 1), ms_r / n_r, ms_d / max(n_d, 1),
+                                                 ms_l / max(n_l, 1), prob.mesh["n_cells"], ctx.n_dofs))
