@@ -11,7 +11,7 @@
 //
 // Usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm
 // Scope: mesh type dealii / grid type hyper_cube (+ initial refinement, uniform refinement for
-// steady "number mesh adapt"); bc types noslip, function, periodic (slip: SURVEY §8 f2, next).
+// steady "number mesh adapt"); bc types noslip, function, periodic, slip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -208,9 +208,7 @@ Params read_params(const Prm &p, int dim) {
     if (b.type == "function") {
       const char *nm[3] = {"u", "v", "w"};
       for (int c = 0; c < dim; ++c) b.f[c] = Function(p, s + nm[c], dim, "0");
-    } else if (b.type == "slip") {
-      die("bc %d: slip boundary conditions are not supported yet", i);
-    } else if (b.type != "noslip" && b.type != "periodic") {
+    } else if (b.type != "noslip" && b.type != "periodic" && b.type != "slip") {
       die("bc %d: unknown type '%s'", i, b.type.c_str());
     }
     P.bcs.push_back(std::move(b));
@@ -310,8 +308,22 @@ struct Constraints {
   std::vector<double> vals;
 };
 
-// Dirichlet data of the noslip / function boundary conditions at the velocity support points;
-// a component already set by an earlier bc keeps its value (deal.II's first-constraint rule)
+// normal axes of the faces with boundary id `id` that node idx lies on (bit d = face normal e_d)
+unsigned face_normals(const Mesh &m, const int *idx, bool colorize, int id) {
+  unsigned a = 0;
+  for (int d = 0; d < m.dim; ++d) {
+    if ((m.pmask >> d) & 1) continue;
+    if (idx[d] == 0 && (colorize ? 2 * d : 0) == id) a |= 1u << d;
+    if (idx[d] == m.vsh[d] - 1 && (colorize ? 2 * d + 1 : 0) == id) a |= 1u << d;
+  }
+  return a;
+}
+
+// Dirichlet data of the noslip / function / slip boundary conditions at the velocity support
+// points; a component already set by an earlier bc keeps its value (deal.II's first-constraint
+// rule). slip = VectorTools::compute_no_normal_flux_constraints (gls_navier_stokes.cc:100-110,
+// 149-160) on the box's axis-aligned faces: n.u = 0 constrains the normal component(s) to 0
+// (every face normal of this boundary at edges / corners).
 Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   Constraints C;
   C.mask.assign((size_t)m.nv, 0);
@@ -320,6 +332,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
     if (b.type == "periodic") continue;
     std::vector<int64_t> sel;
     std::vector<double> X;
+    std::vector<unsigned> nrm;
     for (int64_t v = 0; v < m.nv; ++v) {
       double x[3];
       int idx[3];
@@ -327,6 +340,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       if (face_bits(m, idx, P.colorize) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
+        nrm.push_back(face_normals(m, idx, P.colorize, b.id));
       }
     }
     std::vector<double> fv[3];
@@ -336,6 +350,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       for (int c = 0; c < m.dim; ++c) {
         uint8_t &mk = C.mask[(size_t)sel[s]];
         if (mk & (1u << c)) continue;
+        if (b.type == "slip" && !((nrm[s] >> c) & 1u)) continue;
         mk |= (uint8_t)(1u << c);
         val[(size_t)(sel[s] * m.dim + c)] = b.type == "function" ? fv[c][s * (size_t)b.f[c].nc] : 0.0;
       }

@@ -178,6 +178,12 @@ int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
  * attached, else Jacobi): the reference's preconditioner vmult (DEVICE pointers, no aliasing). */
 int gls_apply_preconditioner(gls_ctx *ctx, const double *v, double *z);
+/* Multigrid grid transfer between levels `level` and `level`+1 of the attached hierarchy (DEVICE
+ * pointers): direction 0 restricts a level-`level` vector into level `level`+1 (transpose of the
+ * Qk interpolation, the reference's MGTransfer restrict_and_add into a zeroed vector), direction 1
+ * prolongates a level-`level`+1 vector onto level `level` (exact Qk interpolation). Constrained
+ * rows are not touched here; the V-cycle zeroes them. */
+int gls_mg_transfer(gls_ctx *ctx, int level, int direction, const double *in, double *out);
 /* Lattice embedding of a (rank-local) mesh: its velocity nodes are a subset of the global n1d^3
  * Qk node lattice of hyper_cube in canonical numbering (global id = x + n1d*(y + n1d*z)), local
  * node i being global node local_to_global[i] (host array, n_vnodes entries). The local nodes

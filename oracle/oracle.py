@@ -196,8 +196,11 @@ class StructuredProblem:
         return ids
 
     def set_dirichlet(self, bcs):
-        """bcs: list of (type, id, func) in bc order; type in {'noslip','function'};
-        func(X) -> (n, dim) values for 'function'. First bc wins (deal.II)."""
+        """bcs: list of (type, id, func) in bc order; type in {'noslip','function','slip'};
+        func(X) -> (n, dim) values for 'function'. First bc wins (deal.II). 'slip' restates
+        VectorTools::compute_no_normal_flux_constraints (gls_navier_stokes.cc:100-110, 149-160) for
+        the box's axis-aligned faces: n.u = 0 with n = e_d for every face of that id the node lies
+        on (edges / corners: all those normal components), homogeneous."""
         X = self.vnode_coords()
         bids = self.boundary_ids_of_vnodes()
         self.constrained[:] = 0
@@ -208,14 +211,24 @@ class StructuredProblem:
             nodes = np.array([i for i, s in enumerate(bids) if bid in s], dtype=np.int64)
             if nodes.size == 0:
                 continue
+            comps = np.ones((nodes.size, self.dim), dtype=bool)
             if typ == "noslip":
                 vals = np.zeros((nodes.size, self.dim))
             elif typ == "function":
                 vals = np.asarray(func(X[nodes]), dtype=np.float64).reshape(nodes.size, self.dim)
+            elif typ == "slip":
+                vals = np.zeros((nodes.size, self.dim))
+                tol = 1e-12 * (self.hi - self.lo)
+                for d in range(self.dim):
+                    on_lo = (np.abs(X[nodes, d] - self.lo) < tol) & ((2 * d if self.colorize else 0) == bid)
+                    on_hi = (np.abs(X[nodes, d] - self.hi) < tol) & ((2 * d + 1 if self.colorize else 0) == bid)
+                    comps[:, d] = on_lo | on_hi
             else:
                 raise ValueError(typ)
-            for nd, v in zip(nodes, vals):
+            for nd, v, cm in zip(nodes, vals, comps):
                 for c in range(self.dim):
+                    if not cm[c]:
+                        continue
                     dof = nd * self.dim + c
                     if not self.constrained[dof]:
                         self.constrained[dof] = 1

@@ -340,8 +340,10 @@ struct gls_ctx {
     struct Taps {
       DevBuf<int32_t> pi[3], ri[3], pc[3], rc[3];
       DevBuf<double> pw[3], rw[3];
+      bool two_pass = false;  // the xy tiles of mg_transfer_2pass fit these tables
     };
     std::vector<std::unique_ptr<Taps>> taps;
+    DevBuf<double> xwork;  // two-pass transfer intermediate (coarse xy x fine z, 4 fields)
     // coarsest level: direct solve with the probed, regularised, inverted Jacobian
     bool direct = false, direct_ok = false;
     // direct solve by LU (rocSOLVER getrf + getri -> explicit inverse, applied by rocBLAS gemv) with
@@ -944,21 +946,29 @@ namespace {
 // the V-cycle's operator on level g: J.v in FP32 arithmetic from the FP32 linearization when the
 // level smooths in mixed precision (brick path), else the FP64 gls_jacobian_apply. Same
 // constraint handling (constrained rows D_c v) and ghost exchange as gls_jacobian_apply.
-int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
-  if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
-  GLS_TRY(ensure_diag(g));
+int ensure_qdata32(gls_ctx *g) {
   GLS_TRY(ensure_qdata(g));
   if (!g->qd32_valid) {
     if (g->qdata32.n != g->qdata.n) GLS_TRY(g->qdata32.alloc(g->qdata.n));
     HIP_TRY(gls::vec_to_f32(g->qdata.p, g->qdata32.p, (int64_t)g->qdata.n, g->stream));
     g->qd32_valid = true;
   }
+  return GLS_OK;
+}
+// FP32 kernels write their brick-surface partial sums in FP32 (half the slab traffic; summed in FP64)
+bool slab_f32() { return std::getenv("GLS_SLAB_F64") == nullptr; }
+int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
+  if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  GLS_TRY(ensure_diag(g));
+  GLS_TRY(ensure_qdata32(g));
   GLS_TRY(dist_import(g, const_cast<double *>(v)));
   gls::OpParams P = make_params(g);
   P.qdf = g->qdata32.p;
   P.v = v;
   P.y = y;
   P.slab = brick_slab(g);
+  P.slabf = P.slab && slab_f32() && gls::brick_fused_jacobi_supported(g->k) ? reinterpret_cast<float *>(P.slab)
+                                                                             : nullptr;
   if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
   {
     TimedLaunch t(g, 4);
@@ -966,7 +976,9 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
   }
   if (P.slab) {
     TimedLaunch t(g, 5);
-    HIP_TRY(slab_sum(g, y));
+    HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
+                                   (int64_t)g->sum_nodes.n, g->n_vnodes, y, nullptr, nullptr, nullptr, 0.0,
+                                   g->stream));
   }
   GLS_TRY(dist_export_add(g, y));
   HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream));
@@ -975,6 +987,45 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
 int smoother_apply(gls_ctx *g, const double *v, double *y) {
   if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y);
   return gls_jacobian_apply(g, v, y);
+}
+// one damped-Jacobi sweep x <- x + omega D^-1 (b - A x) with the smoother's operator A (constrained
+// rows D_c x). Single rank on the brick path: fused into the J.v (brick-interior nodes) and the slab
+// sum (brick-surface nodes), so A x is never stored; otherwise smoother_apply + mg_jacobi_update.
+int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double omega) {
+  const bool nofuse = std::getenv("GLS_MG_NO_FUSE") != nullptr;
+  const bool brick = g->use_brick && g->use_qdata && brick_slab(g) && !g->dist.on && !g->hang.on &&
+                     gls::brick_fused_jacobi_supported(g->k);
+  if (nofuse || !brick) {
+    GLS_TRY(smoother_apply(g, x, y));
+    HIP_TRY(gls::mg_jacobi_update(x, b, y, g->diag.p, omega, g->n_dofs, 0, g->stream));
+    return GLS_OK;
+  }
+  if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  GLS_TRY(ensure_diag(g));
+  const bool f32 = g->smooth_f32;
+  GLS_TRY(f32 ? ensure_qdata32(g) : ensure_qdata(g));
+  gls::OpParams P = make_params(g);
+  P.v = x;
+  P.y = x;
+  P.jx = x;
+  P.jb = b;
+  P.jd = g->diag.p;
+  P.jomega = omega;
+  P.slab = brick_slab(g);
+  if (f32) {
+    P.qdf = g->qdata32.p;
+    P.slabf = slab_f32() ? reinterpret_cast<float *>(P.slab) : nullptr;
+    TimedLaunch t(g, 4);
+    HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
+  } else {
+    P.qd = g->qdata.p;
+    TimedLaunch t(g, 1);
+    HIP_TRY(gls::launch_brick_kernel(g->k, gls::MODE_JVQ, P, g->tables, g->stream));
+  }
+  TimedLaunch t(g, 5);
+  HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
+                                 (int64_t)g->sum_nodes.n, g->n_vnodes, x, g->vmask.p, b, g->diag.p, omega, g->stream));
+  return GLS_OK;
 }
 }  // namespace
 
@@ -1191,13 +1242,23 @@ int mg_prepare(gls_ctx *c) {
     }
     const auto t1 = tick();
     mg.lu = false;
-    if (n > 2048 && !std::getenv("GLS_MG_GAUSS_JORDAN")) {  // LU with the pressure gauge pinned
+    const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");  // gj | lu | lu_npvt (default: size rule)
+    const bool use_lu = cs ? std::strncmp(cs, "lu", 2) == 0 : n > 2048;
+    const bool npvt = cs && std::strcmp(cs, "lu_npvt") == 0;
+    if (use_lu) {  // LU with the pressure gauge pinned
       const int64_t pin = 3 * (int64_t)g->n_vnodes;
       HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
       if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-          rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
-              rocblas_status_success)
+          (npvt ? rocsolver_dgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.info.p)
+                : rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p,
+                                   mg.info.p)) != rocblas_status_success)
         return set_err(GLS_EHIP, "rocsolver_dgetrf failed");
+      if (npvt) {  // identity permutation for getri
+        std::vector<int> id((size_t)n);
+        for (int64_t i = 0; i < n; ++i) id[(size_t)i] = (int)(i + 1);
+        HIP_TRY(hipMemcpyAsync(mg.ipiv.p, id.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+      }
       int inf = -1;
       HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1215,7 +1276,7 @@ int mg_prepare(gls_ctx *c) {
       if (verbose) std::printf("mg: coarse LU n=%lld info=%d, getri done at %.2f ms\n", (long long)n, inf, ms(t0, tick()));
       if (!mg.lu) {  // re-probe for the Gauss-Jordan fallback below (getrf overwrote the matrix)
         mg.dirty = true;
-        return set_err(GLS_EINVAL, "coarse LU: zero pivot %d (set GLS_MG_GAUSS_JORDAN=1)", inf);
+        return set_err(GLS_EINVAL, "coarse LU: zero pivot %d (set GLS_MG_COARSE_SOLVER=gj)", inf);
       }
     } else {
       HIP_TRY(gls::mg_dense_invert(mg.probe.p, mg.aug.p, (int)n, mg.status.p, c->stream));
@@ -1228,6 +1289,51 @@ int mg_prepare(gls_ctx *c) {
     }
   }
   mg.dirty = false;
+  return GLS_OK;
+}
+
+// coarse rhs bc (level l+1) = R y (y on level l): restrict the owned rows, export-add coarse ghost rows
+int mg_restrict(gls_ctx *c, int l, const double *y, double *bc) {
+  auto &mg = c->mg;
+  gls_ctx *h = mg.lev[(size_t)l + 1];
+  hipStream_t s = c->stream;
+  const double *yb = mg_to_box(c, l, y, true);
+  if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
+  {
+    const auto &T = *mg.taps[(size_t)l];
+    const int32_t *ti[3] = {T.ri[0].p, T.ri[1].p, T.ri[2].p}, *tc[3] = {T.rc[0].p, T.rc[1].p, T.rc[2].p};
+    const double *tw[3] = {T.rw[0].p, T.rw[1].p, T.rw[2].p};
+    if (T.two_pass)
+      HIP_TRY(gls::mg_transfer_2pass(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), 1, ti,
+                                     tw, tc, mg.xwork.p, s));
+    else
+      HIP_TRY(gls::mg_transfer3d(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), ti, tw,
+                                 tc, s));
+  }
+  GLS_TRY(mg_from_box(c, l + 1, bc));
+  GLS_TRY(dist_export_add(h, bc));
+  return GLS_OK;
+}
+
+// y (level l) = P xc (xc on level l+1; its ghost values are imported first)
+int mg_prolong(gls_ctx *c, int l, double *xc, double *y) {
+  auto &mg = c->mg;
+  gls_ctx *h = mg.lev[(size_t)l + 1];
+  hipStream_t s = c->stream;
+  GLS_TRY(dist_import(h, xc));
+  const double *xb = mg_to_box(c, l + 1, xc, false);
+  if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
+  {
+    const auto &T = *mg.taps[(size_t)l];
+    const int32_t *ti[3] = {T.pi[0].p, T.pi[1].p, T.pi[2].p}, *tc[3] = {T.pc[0].p, T.pc[1].p, T.pc[2].p};
+    const double *tw[3] = {T.pw[0].p, T.pw[1].p, T.pw[2].p};
+    if (T.two_pass)
+      HIP_TRY(gls::mg_transfer_2pass(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), 0, ti, tw,
+                                     tc, mg.xwork.p, s));
+    else
+      HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, tc, s));
+  }
+  GLS_TRY(mg_from_box(c, l, y));
   return GLS_OK;
 }
 
@@ -1256,46 +1362,21 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   const int pre = l == L - 1 ? mg.csweeps : mg.pre;
   const double om = l == L - 1 ? mg.comega : mg.omega;
   HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
-  for (int it = 1; it < pre; ++it) {
-    GLS_TRY(smoother_apply(g, x, y));
-    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, om, n, 0, s));
-  }
+  for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
   GLS_TRY(smoother_apply(g, x, y));
   HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
   gls_ctx *h = mg.lev[l + 1];
   double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
-  const double *yb = mg_to_box(c, l, y, true);
-  if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
-  {
-    const auto &T = *mg.taps[(size_t)l];
-    const int32_t *ti[3] = {T.ri[0].p, T.ri[1].p, T.ri[2].p}, *tc[3] = {T.rc[0].p, T.rc[1].p, T.rc[2].p};
-    const double *tw[3] = {T.rw[0].p, T.rw[1].p, T.rw[2].p};
-    HIP_TRY(gls::mg_transfer3d(yb, mg_box_target(c, l + 1, bc), mg.dims[l].data(), mg.dims[l + 1].data(), ti, tw, tc,
-                               s));
-  }
-  GLS_TRY(mg_from_box(c, l + 1, bc));
-  GLS_TRY(dist_export_add(h, bc));
+  GLS_TRY(mg_restrict(c, l, y, bc));
   HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
   GLS_TRY(mg_vcycle(c, l + 1, bc, xc));
   // prolongate the coarse correction (ghost values imported first)
-  GLS_TRY(dist_import(h, xc));
-  const double *xb = mg_to_box(c, l + 1, xc, false);
-  if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
-  {
-    const auto &T = *mg.taps[(size_t)l];
-    const int32_t *ti[3] = {T.pi[0].p, T.pi[1].p, T.pi[2].p}, *tc[3] = {T.pc[0].p, T.pc[1].p, T.pc[2].p};
-    const double *tw[3] = {T.pw[0].p, T.pw[1].p, T.pw[2].p};
-    HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, tc, s));
-  }
-  GLS_TRY(mg_from_box(c, l, y));
+  GLS_TRY(mg_prolong(c, l, xc, y));
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
-  for (int it = 0; it < mg.post; ++it) {
-    GLS_TRY(smoother_apply(g, x, y));
-    HIP_TRY(gls::mg_jacobi_update(x, b, y, d, mg.omega, n, 0, s));
-  }
+  for (int it = 0; it < mg.post; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega));
   return GLS_OK;
 }
 
@@ -1313,6 +1394,18 @@ int gls_apply_preconditioner(gls_ctx *c, const double *v, double *z) {
   GLS_TRY(ensure_diag(c));
   if (c->mg.on) GLS_TRY(mg_prepare(c));
   return apply_prec(c, v, z);
+}
+
+int gls_mg_transfer(gls_ctx *c, int level, int direction, const double *in, double *out) {
+  GLS_TRY(check_ctx(c));
+  auto &mg = c->mg;
+  if (!mg.on) return set_err(GLS_EINVAL, "gls_mg_transfer: no multigrid attached");
+  if (level < 0 || level + 1 >= (int)mg.lev.size() || (direction != 0 && direction != 1) || !in || !out || in == out)
+    return set_err(GLS_EINVAL, "gls_mg_transfer: bad level / direction / pointers");
+  if (direction == 0) return mg_restrict(c, level, in, out);
+  double *xc = mgbuf(c, level + 1, MB_X);  // ghost import writes into the coarse vector: work on a copy
+  HIP_TRY(gls::vec_copy(xc, in, mg.lev[(size_t)level + 1]->n_dofs, c->stream));
+  return mg_prolong(c, level, xc, out);
 }
 
 int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {
@@ -1392,8 +1485,12 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   // 1D transfer taps: fine lattice index i sits at x = i / (2k) coarse cells from the box origin;
   // prolongation interpolates the coarse Qk field of the parent cell (equidistant nodes, k <= 2)
   const int K = c->k;
+  const bool two_pass_ok = !std::getenv("GLS_MG_ONEPASS");
+  size_t xwork = 0;
   for (int l = 0; l + 1 < p->n_levels; ++l) {
     std::unique_ptr<gls_ctx::MG::Taps> T(new gls_ctx::MG::Taps);
+    T->two_pass = two_pass_ok;
+    xwork = std::max(xwork, (size_t)4 * mg.dims[l + 1][0] * mg.dims[l + 1][1] * mg.dims[l][2]);
     for (int a = 0; a < 3; ++a) {
       const int nf = mg.dims[l][a], nc = mg.dims[l + 1][a], ncc = (nf - 1) / (2 * K);
       std::vector<int32_t> pi((size_t)nf * 5, 0), ri((size_t)nc * 5, 0);
@@ -1420,6 +1517,9 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
         }
         pn[(size_t)i] = np;
       }
+      if (a < 2)
+        T->two_pass = T->two_pass && gls::mg_transfer_tile_fits(0, a, nf, pi.data(), pn.data()) &&
+                      gls::mg_transfer_tile_fits(1, a, nc, ri.data(), rn.data());
       GLS_TRY(T->pi[a].upload(pi.data(), pi.size()));
       GLS_TRY(T->pw[a].upload(pw.data(), pw.size()));
       GLS_TRY(T->ri[a].upload(ri.data(), ri.size()));
@@ -1429,6 +1529,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     }
     mg.taps.push_back(std::move(T));
   }
+  if (xwork) GLS_TRY(mg.xwork.alloc(xwork));
   // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
   {
     const int64_t nco = mg.lev.back()->n_dofs;
@@ -1437,7 +1538,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
     if (mg.direct) {
       GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
-      if (nco <= 2048 || std::getenv("GLS_MG_GAUSS_JORDAN")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
+      if (nco <= 2048 || std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
       GLS_TRY(mg.ipiv.alloc((size_t)nco));
       GLS_TRY(mg.info.alloc(1));
       if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)
@@ -1490,7 +1591,6 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   const bool keepz = c->mg.on;
   if (keepz && c->zbasis.n != (size_t)m * n) GLS_TRY(c->zbasis.alloc((size_t)m * n));
   double *V = c->krylov.p, *z = c->tmp1.p, *r = c->tmp2.p;
-  const double *dg = c->diag.p;
   hipStream_t s = c->stream;
   double bnorm2;
   GLS_TRY(device_dot(c, b, b, &bnorm2));

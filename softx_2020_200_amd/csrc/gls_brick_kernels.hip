@@ -668,10 +668,21 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) 
     const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
     if (GLS_ABL & 2) {
       if (s == Real(123.5)) Yout[gi] = s;
-    } else if (interior) Yout[gi] = s;
-    else if (use_slab)  // brick-boundary node: this brick's partial sum, summed per node by k_slab_sum
-      P.slab[((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4 + fld] = (double)s;
-    else atomicAdd(&Yout[gi], (double)s);
+    } else if (interior) {
+      if (MODE == MODE_JVQ && P.jx) {  // fused damped-Jacobi sweep on this brick-owned node
+        const bool con = fld < 3 && P.vmask && ((P.vmask[node] >> fld) & 1u);
+        const double x = P.jx[gi], dd = P.jd[gi];
+        P.jx[gi] = x + P.jomega * (P.jb[gi] - (con ? dd * x : (double)s)) / dd;
+      } else {
+        Yout[gi] = s;
+      }
+    } else if (use_slab) {  // brick-boundary node: this brick's partial sum, summed per node by k_slab_sum
+      const int64_t si = ((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4 + fld;
+      if (std::is_same<Real, float>::value && P.slabf) P.slabf[si] = (float)s;
+      else P.slab[si] = (double)s;
+    } else {
+      atomicAdd(&Yout[gi], (double)s);
+    }
   }
 }
 
@@ -775,34 +786,80 @@ int brick_boundary_nodes(int k) { return k == 1 ? BrickCfg<1>::NBND : (k == 2 ? 
 
 // y[node] (4 fields) = sum of the bricks' partial sums over the node's slab slots (fixed order:
 // deterministic, no atomics). One thread per brick-boundary node.
-__global__ void k_slab_sum(const double *__restrict__ slab, const int32_t *__restrict__ nodes,
+// S = double / float (FP32 smoother slabs, summed in FP64). With J (fused Jacobi sweep) the node's
+// row of y = A v is not stored: x <- x + omega (b - y) / d, y = d x on zero_constraints components.
+template <typename S>
+struct SlabQuad;
+template <>
+struct SlabQuad<double> {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  __device__ static void load(const double *p, double &a, double &b, double &c, double &d) {
+    const d2 *e = reinterpret_cast<const d2 *>(p);
+    const d2 u = __builtin_nontemporal_load(e), v = __builtin_nontemporal_load(e + 1);
+    a = u.x, b = u.y, c = v.x, d = v.y;
+  }
+};
+template <>
+struct SlabQuad<float> {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __device__ static void load(const float *p, double &a, double &b, double &c, double &d) {
+    const f4 u = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
+    a = u.x, b = u.y, c = u.z, d = u.w;
+  }
+};
+template <typename S, bool J>
+__global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict__ nodes,
                            const int32_t *__restrict__ off, const int32_t *__restrict__ slots, int64_t n_sum,
-                           int64_t voff, double *__restrict__ y) {
+                           int64_t voff, double *__restrict__ y, const uint8_t *__restrict__ vmask,
+                           const double *__restrict__ jb, const double *__restrict__ jd, double jomega) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
-  double s0 = 0., s1 = 0., s2 = 0., s3 = 0.;
+  double s[4] = {0., 0., 0., 0.};
   for (int j = off[i]; j < off[i + 1]; ++j) {
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    const d2 *e = reinterpret_cast<const d2 *>(slab + (int64_t)slots[j] * 4);
-    const d2 a = __builtin_nontemporal_load(e), b = __builtin_nontemporal_load(e + 1);
-    s0 += a.x;
-    s1 += a.y;
-    s2 += b.x;
-    s3 += b.y;
+    double a, b, c, d;
+    SlabQuad<S>::load(slab + (int64_t)slots[j] * 4, a, b, c, d);
+    s[0] += a;
+    s[1] += b;
+    s[2] += c;
+    s[3] += d;
   }
   const int64_t node = nodes[i];
-  y[node * 3] = s0;
-  y[node * 3 + 1] = s1;
-  y[node * 3 + 2] = s2;
-  y[voff + node] = s3;
+  const int64_t gi[4] = {node * 3, node * 3 + 1, node * 3 + 2, voff + node};
+  if constexpr (J) {
+    const unsigned m = vmask ? vmask[node] : 0u;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const double x = y[gi[f]], dd = jd[gi[f]];
+      y[gi[f]] = x + jomega * (jb[gi[f]] - ((f < 3 && ((m >> f) & 1u)) ? dd * x : s[f])) / dd;
+    }
+  } else {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) y[gi[f]] = s[f];
+  }
 }
 hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
                           int64_t n_sum, int64_t n_vnodes, double *y, hipStream_t s) {
   if (n_sum <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((n_sum + 255) / 256)), dim3(256), 0, s, slab, nodes, off, slots,
-                     n_sum, 3 * n_vnodes, y);
+  hipLaunchKernelGGL((k_slab_sum<double, false>), dim3((unsigned)((n_sum + 255) / 256)), dim3(256), 0, s, slab, nodes,
+                     off, slots, n_sum, 3 * n_vnodes, y, nullptr, nullptr, nullptr, 0.0);
   return hipGetLastError();
 }
+hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32_t *nodes, const int32_t *off,
+                             const int32_t *slots, int64_t n_sum, int64_t n_vnodes, double *y, const uint8_t *vmask,
+                             const double *jb, const double *jd, double jomega, hipStream_t s) {
+  if (n_sum <= 0) return hipSuccess;
+  const dim3 g((unsigned)((n_sum + 255) / 256)), b(256);
+  const int64_t voff = 3 * n_vnodes;
+  if (slabf) {
+    if (jb) hipLaunchKernelGGL((k_slab_sum<float, true>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+    else hipLaunchKernelGGL((k_slab_sum<float, false>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+  } else {
+    if (jb) hipLaunchKernelGGL((k_slab_sum<double, true>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+    else hipLaunchKernelGGL((k_slab_sum<double, false>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+  }
+  return hipGetLastError();
+}
+bool brick_fused_jacobi_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 
 size_t brick_qdata_size(int k, int n_cells) {
   if (brick_impl(k) == 1) return brick_wave_qdata_size(k, n_cells);

@@ -51,6 +51,13 @@ struct OpParams {
   double *y;                  // output (brick-interior nodes: plain stores; others: slab or atomics)
   double *slab;               // brick path: [n_bricks][NBND][4] partial sums of brick-boundary nodes
                               //   (nullptr -> FP64 atomics into y, which the caller zeroes)
+  float *slabf;               // FP32 kernels: the same slab in FP32 when set (takes precedence)
+  // fused damped-Jacobi sweep (MODE_JVQ brick kernel, interior nodes; the slab sum does the rest):
+  // instead of y = A v, jx <- jx + jomega (jb - y) / jd with y = jd * jx on zero_constraints rows
+  // (jx aliases v: a brick's interior nodes are read and written by that brick only)
+  double *jx;
+  const double *jb, *jd;
+  double jomega;
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs
   double alpha_jac;           // mass coefficient of the Jacobian (bdf[0] / sdirk[0][0])

@@ -23,6 +23,12 @@ int brick_boundary_nodes(int k);  // NBND: brick-lattice nodes on the 2x2x2 bric
 // y[nodes[i]] = sum_{j in [off[i], off[i+1])} slab[slots[j]] (4 fields per node)
 hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
                           int64_t n_sum, int64_t n_vnodes, double *y, hipStream_t s);
+// the same with an FP32 slab (slabf != nullptr) and/or a fused damped-Jacobi sweep (jb != nullptr:
+// y holds x and is updated x <- x + jomega (jb - A x) / jd, rows in vmask use (A x)_i = jd_i x_i)
+hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32_t *nodes, const int32_t *off,
+                             const int32_t *slots, int64_t n_sum, int64_t n_vnodes, double *y, const uint8_t *vmask,
+                             const double *jb, const double *jd, double jomega, hipStream_t s);
+bool brick_fused_jacobi_supported(int k);  // the selected brick kernel honours OpParams::jx and ::slabf
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 
@@ -67,6 +73,12 @@ hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const 
 hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const int nout[3],
                          const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
                          hipStream_t s);
+// two-pass transfer (LDS-tiled xy pass + z pass); work holds 4 * (xy of the smaller lattice) * (z of the
+// larger) doubles. tile_fits: host check that a per-axis tap table (axis 0/1) fits the kernel's tiles.
+hipError_t mg_transfer_2pass(const double *in, double *out, const int nin[3], const int nout[3], int restrict_,
+                             const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
+                             double *work, hipStream_t s);
+int mg_transfer_tile_fits(int restrict_, int axis, int n_out, const int32_t *taps, const int32_t *cnt);
 hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
                          int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes
 hipError_t mg_box_scatter(const double *box, double *loc, const int32_t *map, int64_t nbox, int64_t nvl,

@@ -30,7 +30,7 @@ EXPORTS = [
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import",
-    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice", "gls_apply_preconditioner",
+    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -130,6 +130,7 @@ def load():
     L.gls_mg_detach.argtypes = [vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
+    L.gls_mg_transfer.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     P64 = C.POINTER(i64)
     L.gls_set_hanging.argtypes = [vp, i64, P64, P64, P64, d]
     L.gls_mesh_refined_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
@@ -314,6 +315,7 @@ class GLSContext:
         check(self.L.gls_n_dofs(self.h, C.byref(n)), "gls_n_dofs")
         self.n_dofs = n.value
         self.n_cells = D.n_cells
+        self.n_vnodes, self.n_pnodes = D.n_vnodes, D.n_pnodes
         # stream-ordered with torch: run on the caller's current torch stream unless told otherwise
         if stream is None:
             stream = torch.cuda.current_stream().cuda_stream
@@ -430,6 +432,11 @@ class GLSContext:
     def apply_preconditioner(self, v, out=None):
         out = self.zeros() if out is None else out
         check(self.L.gls_apply_preconditioner(self.h, _ptr(v), _ptr(out)), "gls_apply_preconditioner")
+        return out
+
+    def mg_transfer(self, level, direction, v, out):
+        """Restrict (direction 0: level -> level+1) or prolongate (1: level+1 -> level) a device vector."""
+        check(self.L.gls_mg_transfer(self.h, int(level), int(direction), _ptr(v), _ptr(out)), "gls_mg_transfer")
         return out
 
     def set_lattice(self, n1d, local_to_global):

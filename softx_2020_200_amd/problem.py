@@ -25,11 +25,15 @@ def vnode_boundary_ids(mesh, n, lo, hi, colorize):
 
 
 def dirichlet_from_bcs(mesh, n, lo, hi, colorize, bcs):
-    """bcs: list of (type, boundary_id, values) in bc order, type in {noslip, function};
+    """bcs: list of (type, boundary_id, values) in bc order, type in {noslip, function, slip};
     values: callable(coords[m,dim]) -> [m,dim] or a constant tuple. deal.II first-wins rule.
+    slip: compute_no_normal_flux_constraints (gls_navier_stokes.cc:100-110, 149-160) on the box's
+    axis-aligned faces, i.e. the normal component(s) of the faces with that id are set to 0.
     Returns (vnode_mask uint8, dofs int64, values float64)."""
-    dim = mesh["dim"]
+    dim, k = mesh["dim"], mesh["k"]
     bits, X = vnode_boundary_ids(mesh, n, lo, hi, colorize)
+    nx = k * n + 1
+    idx = np.indices((nx,) * dim).reshape(dim, -1)[::-1].T
     nv = bits.shape[0]
     taken = np.zeros((nv, dim), dtype=bool)
     vals = np.zeros((nv, dim))
@@ -37,16 +41,23 @@ def dirichlet_from_bcs(mesh, n, lo, hi, colorize, bcs):
         sel = np.nonzero(bits & (1 << bid))[0]
         if sel.size == 0:
             continue
+        comps = np.ones((sel.size, dim), dtype=bool)
         if typ == "noslip":
             v = np.zeros((sel.size, dim))
         elif typ == "function":
             v = np.asarray(f(X[sel]) if callable(f) else np.broadcast_to(np.asarray(f, dtype=float)[:dim],
                                                                           (sel.size, dim)), dtype=float)
+        elif typ == "slip":
+            v = np.zeros((sel.size, dim))
+            for d in range(dim):
+                on_lo = (idx[sel, d] == 0) & ((2 * d if colorize else 0) == bid)
+                on_hi = (idx[sel, d] == nx - 1) & ((2 * d + 1 if colorize else 0) == bid)
+                comps[:, d] = on_lo | on_hi
         else:
             raise ValueError("unsupported bc type %s" % typ)
-        free = ~taken[sel]
+        free = ~taken[sel] & comps
         vals[sel] = np.where(free, v, vals[sel])
-        taken[sel] = True
+        taken[sel] |= comps
     mask = np.zeros(nv, dtype=np.uint8)
     for c in range(dim):
         mask |= (taken[:, c].astype(np.uint8) << c)

@@ -135,3 +135,80 @@ def test_multigrid_mixed_precision():
         out[0][1], out[1][1])
     nv = 3 * (2 * n + 1) ** 3
     assert np.abs(out[1][0][:nv] - out[0][0][:nv]).max() < 1e-7
+
+
+def _interp_1d(nf, nc, k):
+    """Qk interpolation on nested equidistant node lattices (numpy, independent of the C++ tap
+    tables): fine lattice node i sits at x = i / (2k) coarse cells."""
+    P = np.zeros((nf, nc))
+    ncc = (nc - 1) // k
+    for i in range(nf):
+        x = i / (2.0 * k)
+        cc = min(int(np.floor(x)), ncc - 1)
+        xi = x - cc
+        for q in range(k + 1):
+            L = 1.0
+            for b in range(k + 1):
+                if b != q:
+                    L *= (xi * k - b) / (q - b)
+            P[i, cc * k + q] = L
+    return P
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(1, 16), (2, 16), (2, 24)])
+def test_multigrid_transfers_exact(k, n):
+    """gls_mg_transfer: prolongation == tensor-product Qk interpolation (numpy, 1e-13) on every level
+    pair, restriction == its transpose (<R f, c> == <f, P c>), for velocity and pressure."""
+    import torch
+    from softx_2020_200_amd.problem import CavityProblem
+    prob = CavityProblem(dim=3, n=n, k=k, viscosity=0.01, multigrid=True, mg_coarsest=2 if n % 3 else 3)
+    ctx = prob.ctx
+    levels = ctx._mg_levels
+    rng = np.random.default_rng(20200200)
+    for l in range(len(levels) - 1):
+        nf = round(levels[l].n_vnodes ** (1 / 3))
+        nc = round(levels[l + 1].n_vnodes ** (1 / 3))
+        P1 = _interp_1d(nf, nc, k)
+        c = rng.uniform(-1, 1, levels[l + 1].n_dofs)
+        f = rng.uniform(-1, 1, levels[l].n_dofs)
+        out_f = torch.zeros(levels[l].n_dofs, dtype=torch.float64, device="cuda")
+        out_c = torch.zeros(levels[l + 1].n_dofs, dtype=torch.float64, device="cuda")
+        ctx.mg_transfer(l, 1, torch.from_numpy(c).cuda(), out_f)
+        ctx.mg_transfer(l, 0, torch.from_numpy(f).cuda(), out_c)
+        pf, rc = out_f.cpu().numpy(), out_c.cpu().numpy()
+        ncn, nfn = nc ** 3, nf ** 3
+        fields_c = [c[3 * np.arange(ncn) + a] for a in range(3)] + [c[3 * ncn:]]
+        fields_f = [pf[3 * np.arange(nfn) + a] for a in range(3)] + [pf[3 * nfn:]]
+        for fc, ff in zip(fields_c, fields_f):
+            ref = np.einsum("zc,yb,xa,cba->zyx", P1, P1, P1, fc.reshape(nc, nc, nc), optimize=True).reshape(-1)
+            assert np.abs(ff - ref).max() < 1e-13 * max(1.0, np.abs(ref).max()), (l, np.abs(ff - ref).max())
+        lhs, rhs = np.dot(rc, c), np.dot(f, pf)
+        assert abs(lhs - rhs) < 1e-12 * np.abs(f).sum(), (l, lhs, rhs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mp", [0, 1])
+def test_fused_jacobi_sweeps_match_unfused(mp, monkeypatch):
+    """The V-cycle's damped-Jacobi sweeps fused into the brick J.v + slab sum (single rank) give the
+    same preconditioner application as J.v followed by the separate update (FP64 smoother: to
+    rounding; FP32 smoother with FP32 slabs vs FP64 slabs: to FP32 rounding)."""
+    import torch
+    import bench
+    from softx_2020_200_amd.problem import CavityProblem
+    n = 16
+    prob = CavityProblem(dim=3, n=n, k=2, viscosity=0.01, multigrid=True, pre_smooth=2, post_smooth=2,
+                         omega=0.9, coarse_sweeps=20, coarse_omega=0.7, mixed_precision=mp)
+    ctx = prob.ctx
+    ctx.set_time("bdf2", (0.01,) * 4)
+    m1 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.0)).cuda()
+    m2 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.3)).cuda()
+    ctx.set_state(m1, m1, m2)
+    v = torch.from_numpy(np.random.default_rng(20200200).uniform(-1, 1, ctx.n_dofs)).cuda()
+    z_fused = ctx.apply_preconditioner(v).cpu().numpy()
+    monkeypatch.setenv("GLS_MG_NO_FUSE", "1")
+    monkeypatch.setenv("GLS_SLAB_F64", "1")
+    z_ref = ctx.apply_preconditioner(v).cpu().numpy()
+    rel = np.abs(z_fused - z_ref).max() / np.abs(z_ref).max()
+    assert rel < (1e-5 if mp else 1e-12), rel
+    assert np.abs(z_ref).max() > 0

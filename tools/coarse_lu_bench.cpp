@@ -1,0 +1,53 @@
+// Times the dense coarsest-level factorization options for an n x n FP64 matrix (n = 2916 is the
+// Q2-Q2 4^3 coarsest MG level): rocSOLVER getrf / getrf_npvt / getri / getrs and a plain dgemm.
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#define CK(x) do { auto e_ = (x); if (e_ != 0) { std::printf("fail %s: %d\n", #x, (int)e_); return 1; } } while (0)
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? std::atoi(argv[1]) : 2916;
+  std::vector<double> A((size_t)n * n);
+  srand(1);
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) A[(size_t)j * n + i] = (i == j ? n : 0.0) + (double)rand() / RAND_MAX - 0.5;
+  double *dA, *dB, *dC;
+  int *ipiv, *info;
+  CK(hipMalloc(&dA, sizeof(double) * n * n));
+  CK(hipMalloc(&dB, sizeof(double) * n * n));
+  CK(hipMalloc(&dC, sizeof(double) * n * n));
+  CK(hipMalloc(&ipiv, sizeof(int) * n));
+  CK(hipMalloc(&info, sizeof(int)));
+  rocblas_handle h;
+  CK(rocblas_create_handle(&h));
+  auto now = [] { (void)hipDeviceSynchronize(); return std::chrono::steady_clock::now(); };
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(dA, A.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+    auto t0 = now();
+    CK(rocsolver_dgetrf(h, n, n, dA, n, ipiv, info));
+    auto t1 = now();
+    CK(rocsolver_dgetri(h, n, dA, n, ipiv, info));
+    auto t2 = now();
+    CK(hipMemcpy(dA, A.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+    auto t3 = now();
+    CK(rocsolver_dgetrf_npvt(h, n, n, dA, n, info));
+    auto t4 = now();
+    CK(hipMemcpy(dB, A.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+    auto t5 = now();
+    CK(rocsolver_dgetrs(h, rocblas_operation_none, n, 1, dA, n, ipiv, dB, n));
+    auto t6 = now();
+    const double one = 1.0, zero = 0.0;
+    CK(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, n, n, n, &one, dA, n, dB, n, &zero, dC, n));
+    auto t7 = now();
+    CK(rocblas_dgemv(h, rocblas_operation_none, n, n, &one, dA, n, dB, 1, &zero, dC, 1));
+    auto t8 = now();
+    std::printf("n=%d getrf %.2f ms getri %.2f ms getrf_npvt %.2f ms getrs(1 rhs) %.3f ms dgemm %.3f ms (%.1f TF) dgemv %.3f ms\n",
+                n, ms(t0, t1), ms(t1, t2), ms(t3, t4), ms(t5, t6), ms(t6, t7), 2.0 * n * n * (double)n / ms(t6, t7) / 1e9,
+                ms(t7, t8));
+  }
+  return 0;
+}
