@@ -162,7 +162,8 @@ int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_para
 typedef struct {
   int n_levels;
   gls_ctx **levels;
-  int pre_smooth, post_smooth, coarse_sweeps;  /* 0 -> defaults 2, 2, 30 */
+  int pre_smooth, post_smooth, coarse_sweeps;  /* pre: 0 -> 2, < 0 -> none (x = 0, residual = rhs);
+                                                  post: < 0 -> 2, 0 -> none; coarse: 0 -> 30 */
   double omega;                               /* damped-Jacobi weight of the smoother, 0 -> 0.6 */
   double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU

@@ -1361,12 +1361,20 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   }
   const int pre = l == L - 1 ? mg.csweeps : mg.pre;
   const double om = l == L - 1 ? mg.comega : mg.omega;
-  HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
-  for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
+  if (pre > 0) {
+    HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
+    for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
+  } else {
+    HIP_TRY(gls::vec_fill(x, n, 0.0, s));
+  }
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
-  GLS_TRY(smoother_apply(g, x, y));
-  HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
+  if (pre > 0) {
+    GLS_TRY(smoother_apply(g, x, y));
+    HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
+  } else {
+    HIP_TRY(gls::vec_copy(y, b, n, s));  // x = 0: the residual is b
+  }
   gls_ctx *h = mg.lev[l + 1];
   double *bc = mgbuf(c, l + 1, MB_B), *xc = mgbuf(c, l + 1, MB_X);
   GLS_TRY(mg_restrict(c, l, y, bc));
@@ -1470,7 +1478,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.dims.push_back(dm);
   }
   mg.k = c->k;
-  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : 2;
+  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : (p->pre_smooth < 0 ? 0 : 2);
   mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
   mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
   mg.omega = p->omega > 0 ? p->omega : 0.6;

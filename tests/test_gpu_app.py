@@ -212,3 +212,27 @@ def test_app_tgv_bdf1_first_step_and_output(tmp_path):
     assert close(e[0], g["checkpoints"]["0.01"], 5), out
     for f in ("tgv.pvd", "tgv.00000.pvtu", "tgv.00001.pvtu", "tgv.00001.00000.vtu"):
         assert (tmp_path / f).exists(), f
+
+
+@pytest.mark.gpu
+def test_app_mms2d_slip_walls_matches_oracle(tmp_path):
+    """bc type = slip (compute_no_normal_flux_constraints, gls_navier_stokes.cc:100-110) on every wall of
+    the mms2d case: the app's velocity L2 error equals the oracle's direct-Newton solution of the same
+    constrained problem (no reference golden exists for slip on this mesh: parity pinned by the oracle)."""
+    import numpy as np
+    from oracle.oracle import Oracle, StructuredProblem, muparser_to_numpy, newton_solve
+    g = G["mms2d_gls"]
+    prm = mms_prm(g, 2, 3, 1).replace("    set type = noslip", "    set type = slip")
+    out = run_app(tmp_path, prm, 2)
+    rows = table(out)
+    assert [int(r[0]) for r in rows] == [64]
+    F, E = muparser_to_numpy(g["force"]), muparser_to_numpy(g["exact"])
+    p = StructuredProblem(2, 8, k=1, viscosity=1.0)
+    p.set_force(lambda X: F(X)[:, :2])
+    p.set_dirichlet([("slip", 0, None)])
+    x, its, res = newton_solve(p, tol=1e-10)
+    eu, ep = Oracle(p).l2_error(x, E)
+    assert abs(rows[0][1] - eu) <= 1e-6 * eu, (rows[0], eu)
+    # slip is not noslip: the error differs from the reference's noslip golden
+    assert abs(eu - g["error_velocity"][0]) > 1e-3 * g["error_velocity"][0]
+    assert np.isfinite(ep)
