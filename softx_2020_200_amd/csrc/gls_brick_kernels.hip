@@ -39,6 +39,9 @@
 #ifndef GLS_BRICK_WAVES_PER_EU
 #define GLS_BRICK_WAVES_PER_EU 4
 #endif
+#ifndef GLS_BRICK_WPE_F32
+#define GLS_BRICK_WPE_F32 6  // FP32 kernels: 80 VGPRs, 6 waves/SIMD (1.96 -> 1.92 ms; 7 waves spill, 2.45 ms)
+#endif
 
 namespace gls {
 
@@ -129,7 +132,9 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 template <int K, int MODE, typename Real = double>
-__global__ void __launch_bounds__(BrickCfg<K>::THREADS, GLS_BRICK_WAVES_PER_EU) gls_brick_kernel(const OpParams P, const Tables1D T) {
+__global__ void __launch_bounds__(BrickCfg<K>::THREADS,
+                                  (std::is_same<Real, float>::value ? GLS_BRICK_WPE_F32 : GLS_BRICK_WAVES_PER_EU))
+    gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
   constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
   constexpr bool JV = MODE == MODE_JV || MODE == MODE_JVQ;
