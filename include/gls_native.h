@@ -290,6 +290,22 @@ typedef struct {
 int gls_mesh_refined_create(int dim, int n, int k, int kp, double lo, double hi, const int32_t *refine,
                             gls_refined_mesh **out);
 int gls_mesh_refined_destroy(gls_refined_mesh *mesh);
+/* Kelly error indicator per cell: KellyErrorEstimator<dim>::estimate as
+ * refine_mesh_kelly calls it (navier_stokes_base.cc:612-652) — face rule QGauss<dim-1>(n_q + 1),
+ * no Neumann boundaries (boundary faces add nothing), deal.II's default cell_diameter_over_24:
+ * eta_K = sqrt(sum over interior faces F of K of diam(K)/24 * int_F sum_c [d u_c / dn]^2) over the
+ * velocity components (variable 0) or the pressure (variable 1). Conforming meshes (no hanging
+ * nodes). sol, eta: DEVICE pointers (eta: n_cells doubles; deal.II stores them as float). */
+int gls_kelly_estimate(gls_ctx *ctx, const double *sol, int variable, double *eta);
+/* GridRefinement::refine_and_coarsen_fixed_number, refinement part (navier_stokes_base.cc:654-661;
+ * serial deal.II rule): flags[i] = 1 for the int(top_fraction * n_cells) largest criteria (every
+ * cell >= the threshold value). Returns the number of flagged cells. HOST arrays. */
+int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_fraction, int32_t *flags);
+/* SolutionTransfer::interpolate (navier_stokes_base.cc:689-733) for the first refinement of the
+ * uniform hyper_cube(n, lo, hi) that `mesh` was built from: coarse in canonical lattice numbering
+ * ([velocity node-major | pressure]), fine in the refined mesh's numbering. HOST arrays. */
+int gls_mesh_refined_interpolate(const gls_refined_mesh *mesh, int n, double lo, double hi, const double *coarse,
+                                 double *fine);
 
 /* ------------------------------------------------------------------------------------------
  * Drop-in I/O surface, host side.

@@ -12,7 +12,9 @@
 // node, which is what make_hanging_node_constraints yields for FE_Q. Nodes live on the fine
 // lattice of spacing h_fine / k; ids follow lexicographic lattice order (x fastest) over the used
 // points. Velocity and pressure spaces are built separately (kp may be < k).
+#include <algorithm>
 #include <cmath>
+#include <functional>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -223,6 +225,71 @@ int gls_mesh_refined_create(int dim, int n, int k, int kp, double lo, double hi,
 
 int gls_mesh_refined_destroy(gls_refined_mesh *m) {
   if (m) delete static_cast<RefinedMeshImpl *>(m->impl_);
+  return GLS_OK;
+}
+
+// GridRefinement::refine_and_coarsen_fixed_number, refinement part (navier_stokes_base.cc:654-661 with
+// the serial deal.II rule): n_refine = int(top_fraction * n_cells); threshold = the n_refine-th largest
+// indicator (std::nth_element); every cell with criteria >= threshold is flagged (GridRefinement::refine).
+int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_fraction, int32_t *flags) {
+  if (n_cells < 0 || (n_cells && (!criteria || !flags)) || top_fraction < 0 || top_fraction > 1)
+    return gls_io_set_error(GLS_EINVAL, "gls_refine_fixed_number: bad arguments");
+  for (int64_t i = 0; i < n_cells; ++i) flags[i] = 0;
+  const int64_t nr = (int64_t)(top_fraction * (double)n_cells);
+  if (nr <= 0) return 0;
+  std::vector<float> tmp(criteria, criteria + n_cells);
+  std::nth_element(tmp.begin(), tmp.begin() + (nr - 1), tmp.end(), std::greater<float>());
+  const float thr = tmp[(size_t)(nr - 1)];
+  int cnt = 0;
+  for (int64_t i = 0; i < n_cells; ++i)
+    if (std::fabs(criteria[i]) >= thr) {
+      flags[i] = 1;
+      ++cnt;
+    }
+  return cnt;
+}
+
+// SolutionTransfer::interpolate for the first refinement of a uniform mesh (navier_stokes_base.cc:
+// 689-733): every node of the refined mesh lies in a cell of hyper_cube(n, lo, hi), whose Qk
+// interpolant it samples (exact for the refined space, which contains the coarse one).
+int gls_mesh_refined_interpolate(const gls_refined_mesh *m, int n, double lo, double hi, const double *coarse,
+                                 double *fine) {
+  if (!m || !coarse || !fine || n < 1 || !(hi > lo)) return gls_io_set_error(GLS_EINVAL, "gls_mesh_refined_interpolate: bad arguments");
+  const int dim = m->dim;
+  const double hc = (hi - lo) / n;
+  auto sample = [&](int kk, const double *x, int ncomp, int64_t base, int stride, double *out) {
+    const int64_t np1 = (int64_t)kk * n + 1;
+    int cidx[3] = {0, 0, 0};
+    double xi[3] = {0, 0, 0};
+    for (int d = 0; d < dim; ++d) {
+      const double t = (x[d] - lo) / hc;
+      cidx[d] = std::min(std::max((int)std::floor(t), 0), n - 1);
+      xi[d] = t - cidx[d];
+    }
+    for (int c = 0; c < ncomp; ++c) out[c] = 0.0;
+    const int na = dim == 3 ? (kk + 1) * (kk + 1) * (kk + 1) : (kk + 1) * (kk + 1);
+    for (int a = 0; a < na; ++a) {
+      const int ai[3] = {a % (kk + 1), (a / (kk + 1)) % (kk + 1), dim == 3 ? a / ((kk + 1) * (kk + 1)) : 0};
+      double w = 1.0;
+      int64_t node = 0, st = 1;
+      for (int d = 0; d < dim; ++d) {
+        w *= lagrange(kk, ai[d], xi[d]);
+        node += ((int64_t)cidx[d] * kk + ai[d]) * st;
+        st *= np1;
+      }
+      if (w == 0.0) continue;
+      for (int c = 0; c < ncomp; ++c) out[c] += w * coarse[base + node * stride + c];
+    }
+  };
+  int64_t nvc = 1, npc = 1;
+  for (int d = 0; d < dim; ++d) {
+    nvc *= (int64_t)m->k * n + 1;
+    npc *= (int64_t)m->kp * n + 1;
+  }
+  (void)npc;
+  for (int64_t i = 0; i < m->n_vnodes; ++i) sample(m->k, m->vnode_x + i * dim, dim, 0, dim, fine + i * dim);
+  const int64_t fvoff = (int64_t)dim * m->n_vnodes, cvoff = (int64_t)dim * nvc;
+  for (int64_t i = 0; i < m->n_pnodes; ++i) sample(m->kp, m->pnode_x + i * dim, 1, cvoff, 1, fine + fvoff + i);
   return GLS_OK;
 }
 

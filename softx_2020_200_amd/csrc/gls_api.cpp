@@ -10,6 +10,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <array>
 #include <memory>
 #include <string>
 #include <vector>
@@ -267,6 +269,7 @@ struct gls_ctx {
   bool own_stream = false;
   gls::Tables1D tables;
   DevBuf<int32_t> cell_vnodes, cell_pnodes;
+  DevBuf<int32_t> face_nbr;  // [n_cells][2 dim] face neighbours (Kelly), built on first use
   DevBuf<double> geo, x0, force_q;
   DevBuf<uint8_t> vmask;
   DevBuf<int64_t> con_dofs;  // zero_constraints DoF list
@@ -1414,6 +1417,81 @@ int gls_mg_transfer(gls_ctx *c, int level, int direction, const double *in, doub
   double *xc = mgbuf(c, level + 1, MB_X);  // ghost import writes into the coarse vector: work on a copy
   HIP_TRY(gls::vec_copy(xc, in, mg.lev[(size_t)level + 1]->n_dofs, c->stream));
   return mg_prolong(c, level, xc, out);
+}
+
+// --------------------------------------------------------------------------------------------
+// Kelly error indicator (navier_stokes_base.cc:612-652)
+// --------------------------------------------------------------------------------------------
+namespace {
+// face neighbours of a conforming mesh: faces match by their vertex node ids (periodic wraps share
+// node ids, so a wrapped face has its periodic neighbour)
+int build_face_neighbours(gls_ctx *c) {
+  const int dim = c->dim, k = c->k, nv = gls::ipow(k + 1, dim);
+  std::vector<int32_t> cn((size_t)c->n_cells * nv);
+  if (!cn.empty() && hipMemcpy(cn.data(), c->cell_vnodes.p, cn.size() * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return set_err(GLS_EHIP, "cell map download failed");
+  std::map<std::array<int32_t, 4>, std::pair<int, int>> open;  // face key -> (cell, face slot)
+  std::vector<int32_t> nbr((size_t)c->n_cells * 2 * dim, -1);
+  for (int cell = 0; cell < c->n_cells; ++cell)
+    for (int d = 0; d < dim; ++d)
+      for (int sd = 0; sd < 2; ++sd) {
+        std::array<int32_t, 4> key = {-1, -1, -1, -1};
+        int nk = 0;
+        for (int v = 0; v < (1 << dim); ++v) {  // cell vertices with coordinate d on side sd
+          if (((v >> d) & 1) != sd) continue;
+          int a = 0, st = 1;
+          for (int e = 0; e < dim; ++e, st *= k + 1) a += ((v >> e) & 1) * k * st;
+          key[nk++] = cn[(size_t)cell * nv + a];
+        }
+        std::sort(key.begin(), key.begin() + nk);
+        auto it = open.find(key);
+        if (it == open.end()) {
+          open.emplace(key, std::make_pair(cell, 2 * d + sd));
+        } else {
+          nbr[(size_t)cell * 2 * dim + 2 * d + sd] = it->second.first;
+          nbr[(size_t)it->second.first * 2 * dim + it->second.second] = cell;
+          open.erase(it);
+        }
+      }
+  return c->face_nbr.upload(nbr.data(), nbr.size());
+}
+
+gls::KellyTables kelly_tables(int m, int nq) {
+  gls::KellyTables T;
+  std::memset(&T, 0, sizeof(T));
+  double xq[gls::kMaxQ1D], wq[gls::kMaxQ1D], xn[gls::kMaxNodes1D];
+  gauss_points(nq, xq, wq);
+  lobatto_points(m, xn);
+  T.nq = nq;
+  for (int a = 0; a <= m; ++a) {
+    double v, dd, s2;
+    for (int q = 0; q < nq; ++q) {
+      lagrange_1d(m, xn, a, xq[q], v, dd, s2);
+      T.V[q][a] = v;
+    }
+    lagrange_1d(m, xn, a, 0.0, v, dd, s2);
+    T.De[0][a] = dd;
+    lagrange_1d(m, xn, a, 1.0, v, dd, s2);
+    T.De[1][a] = dd;
+  }
+  for (int q = 0; q < nq; ++q) T.w[q] = wq[q];
+  return T;
+}
+}  // namespace
+
+int gls_kelly_estimate(gls_ctx *c, const double *sol, int variable, double *eta) {
+  GLS_TRY(check_ctx(c));
+  if (!sol || !eta || (variable != 0 && variable != 1)) return set_err(GLS_EINVAL, "gls_kelly_estimate: bad arguments");
+  if (c->hang.on) return set_err(GLS_EINVAL, "gls_kelly_estimate: conforming meshes only (no hanging nodes)");
+  if (c->nq1d + 1 > gls::kMaxQ1D) return set_err(GLS_EINVAL, "gls_kelly_estimate: face rule too large");
+  if (!c->face_nbr.p && c->n_cells > 0) GLS_TRY(build_face_neighbours(c));
+  const bool pres = variable == 1;
+  const int m = pres ? c->kp : c->k;
+  const int32_t *nodes = pres && c->cell_pnodes.p ? c->cell_pnodes.p : c->cell_vnodes.p;
+  const gls::KellyTables T = kelly_tables(m, c->nq1d + 1);  // QGauss<dim-1>(n_q + 1)
+  HIP_TRY(gls::launch_kelly(c->dim, m, nodes, c->face_nbr.p, c->geo.p, sol, c->n_cells, pres ? 1 : c->dim,
+                            pres ? (int64_t)c->dim * c->n_vnodes : 0, pres ? 1 : c->dim, T, eta, c->stream));
+  return GLS_OK;
 }
 
 int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {

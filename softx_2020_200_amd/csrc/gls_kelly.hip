@@ -1,0 +1,97 @@
+// gls_kelly.hip — Kelly error indicator on conforming axis-aligned Qk meshes.
+//
+// Restates KellyErrorEstimator<dim>::estimate as refine_mesh_kelly calls it
+// (navier_stokes_base.cc:612-652: QGauss<dim-1>(n_q + 1) on the faces, no Neumann boundaries, the
+// velocity or the pressure component mask, deal.II's default cell_diameter_over_24 strategy):
+//   eta_K^2 = sum over the interior faces F of K of  diam(K)/24 * int_F sum_c [d u_c / dn]^2.
+// One thread per cell; each face integral is evaluated from both sides' nodal values (the
+// neighbour's face quadrature points coincide on a conforming box mesh), so no atomics are needed.
+#include "gls_launch.hpp"
+
+namespace gls {
+
+namespace {
+
+template <int DIM, int M>
+__global__ void __launch_bounds__(256) k_kelly(const int32_t *__restrict__ cell_nodes, const int32_t *__restrict__ nbr,
+                                               const double *__restrict__ geo, const double *__restrict__ sol,
+                                               int n_cells, int ncomp, int64_t base, int stride, KellyTables T,
+                                               double *__restrict__ eta) {
+  constexpr int M1 = M + 1;
+  constexpr int NN = DIM == 3 ? M1 * M1 * M1 : M1 * M1;
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= n_cells) return;
+  const int nqf = T.nq;
+  double h[3] = {geo[cell * 4 + 0], geo[cell * 4 + 1], DIM == 3 ? geo[cell * 4 + 2] : 1.0};
+  const double diam = sqrt(h[0] * h[0] + h[1] * h[1] + (DIM == 3 ? h[2] * h[2] : 0.0));
+  double acc = 0.0;
+  for (int d = 0; d < DIM; ++d) {
+    for (int s = 0; s < 2; ++s) {
+      const int nb = nbr[(int64_t)cell * 2 * DIM + 2 * d + s];
+      if (nb < 0) continue;  // boundary face: no jump (no Neumann map)
+      const double hn[3] = {geo[nb * 4 + 0], geo[nb * 4 + 1], DIM == 3 ? geo[nb * 4 + 2] : 1.0};
+      // tangential directions
+      int t0 = -1, t1 = -1;
+      for (int e = 0; e < DIM; ++e)
+        if (e != d) {
+          if (t0 < 0) t0 = e;
+          else t1 = e;
+        }
+      const double area = h[t0] * (DIM == 3 ? h[t1] : 1.0);
+      const int nq1 = DIM == 3 ? nqf : 1;
+      double integral = 0.0;
+      for (int qa = 0; qa < nqf; ++qa)
+        for (int qb = 0; qb < nq1; ++qb) {
+          const double w = T.w[qa] * (DIM == 3 ? T.w[qb] : 1.0) * area;
+          double jump2 = 0.0;
+          for (int c = 0; c < ncomp; ++c) {
+            double g[2] = {0.0, 0.0};
+            for (int side = 0; side < 2; ++side) {  // 0: this cell (face at xi_d = s), 1: neighbour (1 - s)
+              const int cc = side ? nb : cell;
+              const int end = side ? 1 - s : s;
+              const double inv = 1.0 / (side ? hn[d] : h[d]);
+              double sum = 0.0;
+              for (int a = 0; a < NN; ++a) {
+                int ai[3] = {a % M1, (a / M1) % M1, DIM == 3 ? a / (M1 * M1) : 0};
+                double phi = T.De[end][ai[d]] * inv;
+                phi *= T.V[qa][ai[t0]];
+                if (DIM == 3) phi *= T.V[qb][ai[t1]];
+                const int node = cell_nodes[(int64_t)cc * NN + a];
+                sum += phi * sol[base + (int64_t)node * stride + c];
+              }
+              g[side] = sum;
+            }
+            const double j = g[0] - g[1];
+            jump2 += j * j;
+          }
+          integral += w * jump2;
+        }
+      acc += diam / 24.0 * integral;
+    }
+  }
+  eta[cell] = sqrt(acc);
+}
+
+}  // namespace
+
+hipError_t launch_kelly(int dim, int m, const int32_t *cell_nodes, const int32_t *nbr, const double *geo,
+                        const double *sol, int n_cells, int ncomp, int64_t base, int stride, const KellyTables &T,
+                        double *eta, hipStream_t s) {
+  if (n_cells <= 0) return hipSuccess;
+  const dim3 g((unsigned)((n_cells + 255) / 256)), b(256);
+#define GLS_KELLY_CASE(D, MM)                                                                                 \
+  if (dim == D && m == MM) {                                                                                \
+    hipLaunchKernelGGL((k_kelly<D, MM>), g, b, 0, s, cell_nodes, nbr, geo, sol, n_cells, ncomp, base, stride, \
+                       T, eta);                                                                             \
+    return hipGetLastError();                                                                               \
+  }
+  GLS_KELLY_CASE(2, 1)
+  GLS_KELLY_CASE(2, 2)
+  GLS_KELLY_CASE(2, 3)
+  GLS_KELLY_CASE(3, 1)
+  GLS_KELLY_CASE(3, 2)
+#undef GLS_KELLY_CASE
+  return hipErrorNotSupported;
+}
+
+}  // namespace gls

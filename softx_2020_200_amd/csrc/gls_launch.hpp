@@ -67,6 +67,19 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();
 
+// ---- Kelly error indicator (gls_kelly.hip): 1D tables of the selected space at the face rule
+struct KellyTables {
+  int nq;                             // face quadrature points per direction
+  double w[kMaxQ1D];                  // Gauss weights on [0, 1]
+  double V[kMaxQ1D][kMaxNodes1D];     // basis values at the face points
+  double De[2][kMaxNodes1D];          // basis derivatives at xi = 0 and xi = 1
+};
+// eta[cell] = sqrt(sum over faces with nbr >= 0 of diam/24 * int_F sum_c [d_n u_c]^2); component c of
+// node n at sol[base + n * stride + c], c < ncomp; cell_nodes [n_cells][(m+1)^dim]; nbr [n_cells][2 dim]
+hipError_t launch_kelly(int dim, int m, const int32_t *cell_nodes, const int32_t *nbr, const double *geo,
+                        const double *sol, int n_cells, int ncomp, int64_t base, int stride, const KellyTables &T,
+                        double *eta, hipStream_t s);
+
 // ---- geometric multigrid (gls_mg_kernels.hip): nested Qk node lattices (boxes), k <= 2
 hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s);
 // one-pass 3D transfer with per-axis tap tables [n_out][5] (index, weight) and tap counts [n_out]

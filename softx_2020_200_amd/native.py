@@ -35,6 +35,7 @@ EXPORTS = [
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
+    "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate",
 ]
 
 
@@ -136,6 +137,10 @@ def load():
     L.gls_mesh_refined_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                           C.POINTER(C.c_int32), C.POINTER(C.POINTER(RefinedMesh))]
     L.gls_mesh_refined_destroy.argtypes = [C.POINTER(RefinedMesh)]
+    L.gls_kelly_estimate.argtypes = [vp, vp, C.c_int, vp]
+    L.gls_refine_fixed_number.argtypes = [i64, C.POINTER(C.c_float), C.c_double, C.POINTER(C.c_int32)]
+    L.gls_mesh_refined_interpolate.argtypes = [C.POINTER(RefinedMesh), C.c_int, C.c_double, C.c_double,
+                                               C.POINTER(C.c_double), C.POINTER(C.c_double)]
     _lib = L
     return L
 
@@ -226,6 +231,34 @@ def refined_cube(dim, n, k, kp=None, refine=None, lo=-1.0, hi=1.0):
                                  take(getattr(m, tag + "hang_master"), nm, np.int64),
                                  take(getattr(m, tag + "hang_w"), nm, np.float64))
         return out
+    finally:
+        L.gls_mesh_refined_destroy(pm)
+
+
+def refine_fixed_number(criteria, top_fraction):
+    """GridRefinement::refine_and_coarsen_fixed_number, refinement flags (gls_refine_fixed_number)."""
+    c = np.ascontiguousarray(criteria, dtype=np.float32)
+    flags = np.zeros(c.size, dtype=np.int32)
+    rc = load().gls_refine_fixed_number(c.size, c.ctypes.data_as(C.POINTER(C.c_float)), float(top_fraction),
+                                        flags.ctypes.data_as(C.POINTER(C.c_int32)))
+    check(min(rc, 0), "gls_refine_fixed_number")
+    return flags
+
+
+def refined_interpolate(dim, n, k, kp, refine, coarse, lo=-1.0, hi=1.0):
+    """SolutionTransfer::interpolate of a hyper_cube(n) solution onto refined_cube(dim, n, k, kp,
+    refine) (gls_mesh_refined_interpolate; host arrays)."""
+    L = load()
+    flags = np.ascontiguousarray(refine, dtype=np.int32)
+    pm = C.POINTER(RefinedMesh)()
+    check(L.gls_mesh_refined_create(dim, n, k, kp, lo, hi, flags.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    C.byref(pm)), "gls_mesh_refined_create")
+    try:
+        m = pm.contents
+        fine = np.zeros(dim * int(m.n_vnodes) + int(m.n_pnodes))
+        src = np.ascontiguousarray(coarse, dtype=np.float64)
+        check(L.gls_mesh_refined_interpolate(pm, n, lo, hi, _dp(src), _dp(fine)), "gls_mesh_refined_interpolate")
+        return fine
     finally:
         L.gls_mesh_refined_destroy(pm)
 
@@ -432,6 +465,13 @@ class GLSContext:
     def apply_preconditioner(self, v, out=None):
         out = self.zeros() if out is None else out
         check(self.L.gls_apply_preconditioner(self.h, _ptr(v), _ptr(out)), "gls_apply_preconditioner")
+        return out
+
+    def kelly_estimate(self, sol, variable=0, out=None):
+        """Kelly error indicator per cell (gls_kelly_estimate): variable 0 velocity, 1 pressure."""
+        import torch
+        out = torch.empty(self.n_cells, dtype=torch.float64, device=sol.device) if out is None else out
+        check(self.L.gls_kelly_estimate(self.h, _ptr(sol), int(variable), _ptr(out)), "gls_kelly_estimate")
         return out
 
     def mg_transfer(self, level, direction, v, out):
