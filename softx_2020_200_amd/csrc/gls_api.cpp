@@ -375,6 +375,31 @@ struct gls_ctx {
     DevBuf<int> ipiv, info;
     DevBuf<double> probe, aug, unit;
     DevBuf<int> status;
+    // coarsest-level Jacobi sweeps (single rank, fused brick path) replayed as one HIP graph: the
+    // ~2×csweeps tiny launches per V-cycle are captured once per state (mg_prepare) and launched
+    // as a single graph by every V-cycle of that Newton step
+    struct Graph {
+      hipGraphExec_t h = nullptr;
+      Graph() = default;
+      Graph(const Graph &) = delete;
+      Graph &operator=(const Graph &) = delete;
+      Graph(Graph &&o) noexcept : h(o.h) { o.h = nullptr; }
+      Graph &operator=(Graph &&o) noexcept {
+        if (this != &o) {
+          reset();
+          h = o.h;
+          o.h = nullptr;
+        }
+        return *this;
+      }
+      void reset() {
+        if (h) (void)hipGraphExecDestroy(h);
+        h = nullptr;
+      }
+      ~Graph() { reset(); }
+    } cgraph;
+    std::vector<unsigned char> cgraph_key;  // launch parameters the graph was captured with
+    bool cgraph_failed = false;  // capture refused once: stay on plain launches
     bool dirty = true;
   } mg;
   double time_steps[4] = {1, 1, 1, 1};
@@ -1340,6 +1365,69 @@ int mg_prolong(gls_ctx *c, int l, double *xc, double *y) {
   return GLS_OK;
 }
 
+// coarsest level by HIP graph (opt-in, GLS_MG_GRAPH=1: measured at 128^3, 138.0 vs 138.6 ms per
+// Newton step -- the coarse sweeps are bound by the kernels' own latency, not by launch overhead,
+// profiles/r01_coarse_graph_bench.txt): one rank, fused brick sweeps, the level's own b / x buffers (the
+// captured launches bake in their pointers and this state's OpParams; mg_prepare drops the graph)
+bool coarse_graph_eligible(gls_ctx *c, gls_ctx *g, const double *b, const double *x) {
+  const int l = (int)c->mg.lev.size() - 1;
+  return !c->mg.cgraph_failed && !c->mg.boxed && !g->dist.on && !g->hang.on && g->use_brick && g->use_qdata &&
+         brick_slab(g) && gls::brick_fused_jacobi_supported(g->k) && g->stream == c->stream &&
+         b == mgbuf(c, l, MB_B) && x == mgbuf(c, l, MB_X) && std::getenv("GLS_MG_NO_FUSE") == nullptr &&
+         std::getenv("GLS_MG_GRAPH") != nullptr;
+}
+// everything the captured launches bake in: the level's OpParams (pointers, time coefficients,
+// viscosity), the sweep count and damping, and the buffers the sweeps read and write. Buffer
+// CONTENTS (state, linearization, diagonal) are read at replay time, so a new Newton state with
+// unchanged parameters replays the same graph.
+std::vector<unsigned char> coarse_graph_key(gls_ctx *g, const double *b, const double *x, const double *y, int pre,
+                                            double om) {
+  const gls::OpParams P = make_params(g);
+  const void *ptrs[7] = {b, x, y, g->diag.p, g->qdata.p, g->qdata32.p, brick_slab(g)};
+  const int64_t ints[4] = {pre, g->n_dofs, (int64_t)g->smooth_f32, (int64_t)slab_f32()};
+  std::vector<unsigned char> k(sizeof(P) + sizeof(ptrs) + sizeof(ints) + sizeof(om));
+  unsigned char *o = k.data();
+  std::memcpy(o, &P, sizeof(P));
+  std::memcpy(o += sizeof(P), ptrs, sizeof(ptrs));
+  std::memcpy(o += sizeof(ptrs), ints, sizeof(ints));
+  std::memcpy(o + sizeof(ints), &om, sizeof(om));
+  return k;
+}
+// capture x = csweeps damped-Jacobi sweeps from x = 0 on c's stream; a refused capture leaves the
+// plain launches in place (cgraph_failed)
+int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, double *y, int pre, double om) {
+  auto &mg = c->mg;
+  hipStream_t s = c->stream;
+  GLS_TRY(ensure_diag(g));
+  GLS_TRY(g->smooth_f32 ? ensure_qdata32(g) : ensure_qdata(g));
+  const bool tim = g->timing;
+  g->timing = false;  // no event records inside the capture
+  hipGraph_t gr = nullptr;
+  int rc = GLS_OK;
+  hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+  if (e == hipSuccess) {
+    if (hipError_t e1 = gls::mg_jacobi_update(x, b, nullptr, g->diag.p, om, g->n_dofs, 1, s); e1 != hipSuccess)
+      e = e1;
+    for (int it = 1; it < pre && rc == GLS_OK && e == hipSuccess; ++it) rc = smoother_sweep(g, x, b, y, om);
+    const hipError_t e2 = hipStreamEndCapture(s, &gr);
+    if (e == hipSuccess) e = e2;
+  }
+  g->timing = tim;
+  hipGraphExec_t ex = nullptr;
+  if (rc == GLS_OK && e == hipSuccess && gr) e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+  if (gr) (void)hipGraphDestroy(gr);
+  if (rc != GLS_OK || e != hipSuccess || !ex) {
+    (void)hipGetLastError();
+    if (ex) (void)hipGraphExecDestroy(ex);
+    mg.cgraph_failed = true;
+    if (std::getenv("GLS_MG_VERBOSE")) std::printf("mg: coarse graph capture refused (%s)\n", hipGetErrorString(e));
+    return GLS_OK;
+  }
+  mg.cgraph.h = ex;
+  mg.cgraph_key = coarse_graph_key(g, b, x, y, pre, om);
+  return GLS_OK;
+}
+
 // x = V-cycle(b) on level l (x, b are level-l vectors)
 int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   auto &mg = c->mg;
@@ -1364,6 +1452,16 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   }
   const int pre = l == L - 1 ? mg.csweeps : mg.pre;
   const double om = l == L - 1 ? mg.comega : mg.omega;
+  if (l == L - 1 && l > 0 && pre > 1 && coarse_graph_eligible(c, g, b, x)) {
+    GLS_TRY(ensure_diag(g));  // contents the replay reads: current for this state
+    GLS_TRY(g->smooth_f32 ? ensure_qdata32(g) : ensure_qdata(g));
+    if (mg.cgraph.h && mg.cgraph_key != coarse_graph_key(g, b, x, y, pre, om)) mg.cgraph.reset();
+    if (!mg.cgraph.h) GLS_TRY(coarse_graph_capture(c, g, b, x, y, pre, om));
+    if (mg.cgraph.h) {
+      HIP_TRY(hipGraphLaunch(mg.cgraph.h, s));
+      return GLS_OK;
+    }
+  }
   if (pre > 0) {
     HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
     for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
