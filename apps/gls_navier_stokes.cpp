@@ -10,8 +10,9 @@
 // are what the parity tests compare with the reference's outputs.
 //
 // Usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm
-// Scope: mesh type dealii / grid type hyper_cube (+ initial refinement, uniform refinement for
-// steady "number mesh adapt"); bc types noslip, function, periodic, slip.
+// Scope: mesh type dealii / grid type hyper_cube (+ initial refinement; steady "number mesh adapt"
+// with mesh adaptation type uniform, or kelly = one Kelly-driven local refinement with hanging
+// nodes: fraction type number, no coarsening); bc types noslip, function, periodic, slip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -153,6 +154,11 @@ struct Params {
   double lin_rel = 1e-3, lin_min = 1e-8;
   bool srf = false;
   double omega[3] = {0, 0, 0};
+  // mesh adaptation (parameters.cc:649-731): uniform, or kelly = one Kelly-driven refinement
+  std::string madapt = "none";
+  int kelly_variable = 0;  // 0 velocity, 1 pressure
+  double frac_refine = 0.1;
+  int max_level = 10;
 };
 
 Method parse_method(const std::string &s) {
@@ -196,8 +202,24 @@ Params read_params(const Prm &p, int dim) {
   }
   P.refinement = p.i("mesh/initial refinement", 0);
   const std::string madapt = p.get("mesh adaptation/type", "none");
-  if (P.method == Method::steady && P.mesh_adapt > 0 && madapt != "uniform")
-    die("mesh adaptation type '%s' is not supported (uniform only)", madapt.c_str());
+  P.madapt = madapt;
+  if (P.method == Method::steady && P.mesh_adapt > 0 && madapt != "uniform" && madapt != "kelly")
+    die("mesh adaptation type '%s' is not supported (uniform or kelly)", madapt.c_str());
+  if (madapt == "kelly") {  // refine_mesh_kelly (navier_stokes_base.cc:610-780), first adaptation only
+    const std::string ma = "mesh adaptation/";
+    const std::string var = p.get(ma + "variable", "velocity");
+    if (var != "velocity" && var != "pressure") die("mesh adaptation variable '%s' is unknown", var.c_str());
+    P.kelly_variable = var == "pressure" ? 1 : 0;
+    if (p.get(ma + "fraction type", "number") != "number")
+      die("mesh adaptation: fraction type '%s' is not supported (number only)", p.get(ma + "fraction type", "").c_str());
+    P.frac_refine = p.d(ma + "fraction refinement", 0.1);
+    P.max_level = p.i(ma + "max refinement level", 10);
+    if (p.d(ma + "fraction coarsening", 0.05) != 0.0)
+      die("mesh adaptation: coarsening is not supported (set fraction coarsening = 0)");
+    if (P.method != Method::steady) die("kelly mesh adaptation: steady simulations only");
+    if (P.mesh_adapt > 1) die("kelly mesh adaptation: one adaptation (one refinement level) at most");
+    if (P.k > 2 || P.kp > P.k) die("kelly mesh adaptation: 1 <= pressure order <= velocity order <= 2");
+  }
   const int nbc = p.i("boundary conditions/number", 0);
   for (int i = 0; i < nbc; ++i) {
     const std::string s = "boundary conditions/bc " + std::to_string(i) + "/";
@@ -249,8 +271,22 @@ struct Mesh {
   int vsh[3] = {1, 1, 1}, psh[3] = {1, 1, 1};  // lattice nodes per direction (periodic: wrapped)
   std::vector<int32_t> cv, cp;
   std::vector<double> x0, h;
+  // locally refined mesh (gls_mesh_refined_create): explicit support points, hanging nodes and
+  // their DoF-level constraint lines (empty on the uniform lattice)
+  std::vector<double> vx, px;
+  std::vector<uint8_t> vhanging;  // per velocity node
+  std::vector<int64_t> hang_dofs, hang_off{0}, hang_master;
+  std::vector<double> hang_w;
   int64_t n_dofs() const { return (int64_t)dim * nv + np; }
   void coord(int64_t node, bool vel, double *x, int *idx) const {
+    if (!vx.empty()) {  // refined mesh: no lattice index
+      const double *src = &(vel ? vx : px)[(size_t)(node * dim)];
+      for (int d = 0; d < dim; ++d) {
+        x[d] = src[d];
+        idx[d] = -1;
+      }
+      return;
+    }
     const int *sh = vel ? vsh : psh;
     const int deg = vel ? k : kp;
     for (int d = 0; d < dim; ++d) {
@@ -291,13 +327,18 @@ Mesh build_mesh(const Params &P, int n, int pmask) {
   return m;
 }
 
-// boundary ids of a lattice node (hyper_cube: colorize -> faces 2d / 2d+1, else all id 0)
-unsigned face_bits(const Mesh &m, const int *idx, bool colorize) {
+// the support point x lies on the box face lo (side 0) / hi (side 1) of axis d
+bool on_face(const Mesh &m, const double *x, int d, int side) {
+  const double tol = 1e-12 * (m.hi - m.lo);
+  return std::fabs(x[d] - (side ? m.hi : m.lo)) <= tol;
+}
+// boundary ids of a support point (hyper_cube: colorize -> faces 2d / 2d+1, else all id 0)
+unsigned face_bits(const Mesh &m, const double *x, bool colorize) {
   unsigned b = 0;
   for (int d = 0; d < m.dim; ++d) {
     if ((m.pmask >> d) & 1) continue;
-    if (idx[d] == 0) b |= 1u << (colorize ? 2 * d : 0);
-    if (idx[d] == m.vsh[d] - 1) b |= 1u << (colorize ? 2 * d + 1 : 0);
+    if (on_face(m, x, d, 0)) b |= 1u << (colorize ? 2 * d : 0);
+    if (on_face(m, x, d, 1)) b |= 1u << (colorize ? 2 * d + 1 : 0);
   }
   return b;
 }
@@ -309,12 +350,12 @@ struct Constraints {
 };
 
 // normal axes of the faces with boundary id `id` that node idx lies on (bit d = face normal e_d)
-unsigned face_normals(const Mesh &m, const int *idx, bool colorize, int id) {
+unsigned face_normals(const Mesh &m, const double *x, bool colorize, int id) {
   unsigned a = 0;
   for (int d = 0; d < m.dim; ++d) {
     if ((m.pmask >> d) & 1) continue;
-    if (idx[d] == 0 && (colorize ? 2 * d : 0) == id) a |= 1u << d;
-    if (idx[d] == m.vsh[d] - 1 && (colorize ? 2 * d + 1 : 0) == id) a |= 1u << d;
+    if (on_face(m, x, d, 0) && (colorize ? 2 * d : 0) == id) a |= 1u << d;
+    if (on_face(m, x, d, 1) && (colorize ? 2 * d + 1 : 0) == id) a |= 1u << d;
   }
   return a;
 }
@@ -337,10 +378,13 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       double x[3];
       int idx[3];
       m.coord(v, true, x, idx);
-      if (face_bits(m, idx, P.colorize) & (1u << b.id)) {
+      // hanging nodes keep their hanging constraint (interpolate_boundary_values skips DoFs that
+      // are already constrained, gls_navier_stokes.cc:84-110)
+      if (!m.vhanging.empty() && m.vhanging[(size_t)v]) continue;
+      if (face_bits(m, x, P.colorize) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
-        nrm.push_back(face_normals(m, idx, P.colorize, b.id));
+        nrm.push_back(face_normals(m, x, P.colorize, b.id));
       }
     }
     std::vector<double> fv[3];
@@ -491,6 +535,7 @@ struct Solver {
   Mesh m;
   Constraints C;
   gls_ctx *ctx = nullptr;
+  gls_refined_mesh *rmesh = nullptr;  // the locally refined mesh m was built from (kelly)
   std::vector<gls_ctx *> mg_levels;
   double *d_present = nullptr, *d_m1 = nullptr, *d_m2 = nullptr, *d_m3 = nullptr;
   std::vector<double> present, m1, m2, m3;
@@ -509,6 +554,8 @@ struct Solver {
     mg_levels.clear();
     if (ctx) gls_destroy(ctx);
     ctx = nullptr;
+    if (rmesh) gls_mesh_refined_destroy(rmesh);
+    rmesh = nullptr;
     for (double *q : {d_present, d_m1, d_m2, d_m3})
       if (q) (void)hipFree(q);
     d_present = d_m1 = d_m2 = d_m3 = nullptr;
@@ -547,6 +594,7 @@ struct Solver {
     D.n_vnodes = (int)mm.nv;
     D.n_pnodes = (int)mm.np;
     D.cell_vnodes = mm.cv.data();
+    if (mm.kp == mm.k && (mm.cp != mm.cv || mm.np != mm.nv)) die("equal-order mesh with distinct pressure nodes");
     D.cell_pnodes = (mm.kp == mm.k) ? nullptr : mm.cp.data();
     D.cell_x0 = mm.x0.data();
     D.cell_h = mm.h.data();
@@ -561,11 +609,7 @@ struct Solver {
     return g;
   }
 
-  void setup(int n) {
-    release();
-    m = build_mesh(P, n, periodic_mask());
-    C = make_constraints(P, m, time);
-    ctx = make_context(m, C);
+  void alloc_vectors() {
     const int64_t N = m.n_dofs();
     for (double **q : {&d_present, &d_m1, &d_m2, &d_m3}) {
       hk(hipMalloc(q, sizeof(double) * (size_t)N), "hipMalloc");
@@ -573,6 +617,74 @@ struct Solver {
     }
     present.assign((size_t)N, 0.);
     m1 = m2 = m3 = present;
+  }
+
+  // the hyper_cube(2^refinement) with the flagged cells split once (hanging nodes): mesh,
+  // Dirichlet constraints (hanging nodes excluded), hanging constraint lines on the context.
+  // Per-cell kernels and a Jacobi-preconditioned GMRES (no multigrid on refined meshes).
+  void setup_refined(int n, const std::vector<int32_t> &flags) {
+    release();
+    ck(gls_mesh_refined_create(P.dim, n, P.k, P.kp, P.lo, P.hi, flags.data(), &rmesh), "gls_mesh_refined_create");
+    const gls_refined_mesh &R = *rmesh;
+    const int dim = P.dim;
+    const int nvl = dim == 3 ? (P.k + 1) * (P.k + 1) * (P.k + 1) : (P.k + 1) * (P.k + 1);
+    const int npl = dim == 3 ? (P.kp + 1) * (P.kp + 1) * (P.kp + 1) : (P.kp + 1) * (P.kp + 1);
+    Mesh r;
+    r.dim = dim;
+    r.n = n;
+    r.k = P.k;
+    r.kp = P.kp;
+    r.lo = P.lo;
+    r.hi = P.hi;
+    r.hc = (P.hi - P.lo) / n;
+    r.nc = R.n_cells;
+    r.nv = R.n_vnodes;
+    r.np = R.n_pnodes;
+    r.cv.assign(R.cell_vnodes, R.cell_vnodes + r.nc * nvl);
+    r.cp.assign(R.cell_pnodes, R.cell_pnodes + r.nc * npl);
+    r.x0.assign(R.cell_x0, R.cell_x0 + r.nc * dim);
+    r.h.assign(R.cell_h, R.cell_h + r.nc * dim);
+    r.vx.assign(R.vnode_x, R.vnode_x + r.nv * dim);
+    r.px.assign(R.pnode_x, R.pnode_x + r.np * dim);
+    r.vhanging.assign((size_t)r.nv, 0);
+    // DoF-level lines: velocity DoF node*dim + c per component, pressure DoF dim*nv + node
+    for (int64_t i = 0; i < R.n_vhang; ++i) {
+      r.vhanging[(size_t)R.vhang_node[i]] = 1;
+      for (int c = 0; c < dim; ++c) {
+        r.hang_dofs.push_back(R.vhang_node[i] * dim + c);
+        for (int64_t j = R.vhang_off[i]; j < R.vhang_off[i + 1]; ++j) {
+          r.hang_master.push_back(R.vhang_master[j] * dim + c);
+          r.hang_w.push_back(R.vhang_w[j]);
+        }
+        r.hang_off.push_back((int64_t)r.hang_master.size());
+      }
+    }
+    for (int64_t i = 0; i < R.n_phang; ++i) {
+      r.hang_dofs.push_back(dim * r.nv + R.phang_node[i]);
+      for (int64_t j = R.phang_off[i]; j < R.phang_off[i + 1]; ++j) {
+        r.hang_master.push_back(dim * r.nv + R.phang_master[j]);
+        r.hang_w.push_back(R.phang_w[j]);
+      }
+      r.hang_off.push_back((int64_t)r.hang_master.size());
+    }
+    m = std::move(r);
+    C = make_constraints(P, m, time);
+    ctx = make_context(m, C);
+    ck(gls_set_hanging(ctx, (int64_t)m.hang_dofs.size(), m.hang_dofs.data(), m.hang_off.data(),
+                       m.hang_master.data(), m.hang_w.data()),
+       "gls_set_hanging");
+    alloc_vectors();
+    std::printf("mesh: cells = %lld, dofs = %lld, hanging dofs = %lld, levels = 1\n", (long long)m.nc,
+                (long long)m.n_dofs(), (long long)m.hang_dofs.size());
+  }
+
+  void setup(int n) {
+    release();
+    m = build_mesh(P, n, periodic_mask());
+    C = make_constraints(P, m, time);
+    ctx = make_context(m, C);
+    const int64_t N = m.n_dofs();
+    alloc_vectors();
     // geometric multigrid on nested hyper_cubes (3D, k == kp <= 2, no periodicity)
     if (use_mg && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && n >= 4 && (n & (n - 1)) == 0) {
       std::vector<gls_ctx *> lv{ctx};
@@ -952,6 +1064,45 @@ struct Solver {
       }
     }
   }
+  // refine_mesh_kelly (navier_stokes_base.cc:610-780) for the first adaptation of the uniform
+  // mesh: Kelly indicator of the velocity or pressure on the device (gls_kelly_estimate, stored as
+  // float like deal.II's Vector<float>), refine_and_coarsen_fixed_number (refinement part;
+  // coarsening is rejected at parameter time), max refinement level, SolutionTransfer
+  void refine_kelly() {
+    const Mesh old = m;
+    if (old.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
+    if (!old.vx.empty()) die("kelly mesh adaptation: the mesh is already refined once");
+    upload(present, d_present);
+    double *d_eta = nullptr;
+    hk(hipMalloc(&d_eta, sizeof(double) * (size_t)old.nc), "hipMalloc");
+    ck(gls_kelly_estimate(ctx, d_present, P.kelly_variable, d_eta), "gls_kelly_estimate");
+    hk(hipDeviceSynchronize(), "kelly estimate");  // the context stream is not the null stream
+    std::vector<double> eta((size_t)old.nc);
+    download(d_eta, eta);
+    (void)hipFree(d_eta);
+    std::vector<float> crit(eta.begin(), eta.end());
+    std::vector<int32_t> cflag((size_t)old.nc, 0), flags((size_t)old.nc, 0);
+    const int nflag = gls_refine_fixed_number(old.nc, crit.data(), P.frac_refine, cflag.data());
+    ck(nflag, "gls_refine_fixed_number");
+    // cells at max refinement level keep their refine flag cleared (tria.n_levels() > max level)
+    if (P.max_level <= P.refinement) std::fill(cflag.begin(), cflag.end(), 0);
+    // the hyper_cube's cell order -> the lexicographic order gls_mesh_refined_create expects
+    for (int64_t c = 0; c < old.nc; ++c) {
+      int64_t lex = 0, stride = 1;
+      for (int d = 0; d < old.dim; ++d) {
+        const int i = (int)std::lround((old.x0[(size_t)(c * old.dim + d)] - old.lo) / old.hc);
+        lex += (int64_t)i * stride;
+        stride *= old.n;
+      }
+      flags[(size_t)lex] = cflag[(size_t)c];
+    }
+    std::printf("kelly: %d of %lld cells flagged for refinement\n", P.max_level <= P.refinement ? 0 : nflag,
+                (long long)old.nc);
+    const std::vector<double> sol = present;
+    setup_refined(old.n, flags);
+    ck(gls_mesh_refined_interpolate(rmesh, old.n, P.lo, P.hi, sol.data(), present.data()),
+       "gls_mesh_refined_interpolate");
+  }
   void report() {
     if (!P.analytical || errors.empty()) return;
     std::ostringstream o;
@@ -1006,7 +1157,10 @@ struct Solver {
       if (step == 1) {
         first_step();
       } else {
-        if (steady) refine_uniform();
+        if (steady) {
+          if (P.madapt == "kelly") refine_kelly();
+          else refine_uniform();
+        }
         advance();
       }
       postprocess(false);

@@ -237,3 +237,53 @@ def test_app_mms2d_slip_walls_matches_oracle(tmp_path):
         assert np.isfinite(ep)
     # slip is not noslip: the error differs from the reference's noslip golden
     assert abs(rows[0][1] - g["error_velocity"][0]) > 1e-3 * g["error_velocity"][0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,variable", [(2, "velocity"), (2, "pressure"), (3, "velocity")])
+def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable):
+    """mesh adaptation type = kelly (refine_mesh_kelly, navier_stokes_base.cc:610-780) in the app, first
+    adaptation of the uniform 8^2 (mms2d) / 8^3 (mms3d) Q1 mesh: Kelly indicator on the device, top 30 % flagged
+    (fraction type number, no coarsening), one refinement with hanging nodes, solution transfer,
+    Newton on the refined mesh. The first row equals the reference golden; the refined row equals the
+    oracle's own pipeline (solve -> Kelly -> flag -> refine -> condensed solve). Parity unpinned beyond
+    the oracle: the reference holds no Kelly golden on this mesh."""
+    import numpy as np
+    from oracle.oracle import Oracle, StructuredProblem, kelly_estimate, muparser_to_numpy, newton_solve
+    import softx_2020_200_amd as sx
+    g = G["mms2d_gls" if dim == 2 else "mms3d_gls"]
+    n, gi = (8, 0) if dim == 2 else (8, 1)  # 4^3: the discrete velocity is ~0, Kelly is roundoff
+    prm = mms_prm(g, dim, 3, 1).replace("  set type = uniform\n", f"""  set type = kelly
+  set variable = {variable}
+  set fraction type = number
+  set fraction refinement = 0.3
+  set fraction coarsening = 0
+""")
+    out = run_app(tmp_path, prm, dim, "--precond", "jacobi")
+    rows = table(out)
+    assert len(rows) == 2, out
+    assert int(rows[0][0]) == n ** dim and close(rows[0][1], g["error_velocity"][gi], 5), (rows, out)
+    # the oracle's pipeline on the same mesh
+    F, E = muparser_to_numpy(g["force"]), muparser_to_numpy(g["exact"])
+    p = StructuredProblem(dim, n, k=1, viscosity=1.0)
+    p.set_force(lambda X: F(X)[:, :dim])
+    p.set_dirichlet([("noslip", 0, None)])
+    x, _, _ = newton_solve(p, tol=1e-10)
+    eta = kelly_estimate(p, x, 0 if variable == "velocity" else 1)
+    flags = sx.refine_fixed_number(eta.astype(np.float32), 0.3)
+    assert int(rows[1][0]) == n ** dim + (2 ** dim - 1) * int(flags.sum()), (rows, int(flags.sum()))
+    mesh = sx.refined_cube(dim, n, 1, 1, flags)
+    q = StructuredProblem.from_refined(mesh, viscosity=1.0)
+    lines = sx.hanging_dof_lines(mesh)
+    q.set_hanging(*lines)
+    q.hang_lines = lines
+    q.set_dirichlet([("noslip", 0, None)])
+    q.set_force(lambda X: F(X)[:, :dim])
+    x0 = q.apply_nonzero_constraints(sx.refined_interpolate(dim, n, 1, 1, flags, x))
+    y, _, _ = newton_solve(q, x0=x0.copy(), tol=1e-10)
+    eu, ep = Oracle(q).l2_error(y, E)
+    assert abs(rows[1][1] - eu) <= 1e-6 * eu, (rows[1], eu)
+    assert abs(rows[1][3] - ep) <= 1e-6 * ep, (rows[1], ep)
+    assert rows[1][1] < rows[0][1]
+    assert f"kelly: {int(flags.sum())} of {n ** dim} cells flagged" in out
+    assert "hanging dofs = %d" % len(lines[0]) in out
