@@ -301,6 +301,16 @@ int gls_kelly_estimate(gls_ctx *ctx, const double *sol, int variable, double *et
  * serial deal.II rule): flags[i] = 1 for the int(top_fraction * n_cells) largest criteria (every
  * cell >= the threshold value). Returns the number of flagged cells. HOST arrays. */
 int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_fraction, int32_t *flags);
+/* parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number (fraction_type 0) and
+ * refine_and_coarsen_fixed_fraction (fraction_type 1), refinement part — the calls refine_mesh_kelly
+ * makes (navier_stokes_base.cc:654-667; deal.II 9.2 distributed/grid_refinement.cc): bisection for
+ * the threshold (25 steps at most) between the widened extremes of the criteria, the target being
+ * int(f * n_cells) cells (f = top_fraction capped by adjust_refine_and_coarsen_number_fraction<dim>
+ * so the refined mesh has at most max_n_cells cells) or top_fraction of the summed criteria;
+ * flags[i] = 1 where criteria[i] >= threshold. criteria >= 0 over ALL cells (gathered), HOST
+ * arrays; threshold may be NULL. Returns the number of flagged cells. */
+int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
+                  int64_t max_n_cells, int32_t *flags, double *threshold);
 /* SolutionTransfer::interpolate (navier_stokes_base.cc:689-733) for the first refinement of the
  * uniform hyper_cube(n, lo, hi) that `mesh` was built from: coarse in canonical lattice numbering
  * ([velocity node-major | pressure]), fine in the refined mesh's numbering. HOST arrays. */

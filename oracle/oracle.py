@@ -523,6 +523,57 @@ def kelly_estimate(p: StructuredProblem, sol, variable=0):
     return np.sqrt(eta2)
 
 
+def pd_refine_fixed(criteria, dim, top_fraction, fraction_type="number", max_n_cells=100000000):
+    """Refinement flags of parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number /
+    refine_and_coarsen_fixed_fraction as refine_mesh_kelly calls them (navier_stokes_base.cc:654-667;
+    deal.II 9.2 source/distributed/grid_refinement.cc, third party, not vendored: restated from its
+    published algorithm — adjust_refine_and_coarsen_number_fraction<dim>, adjust_interesting_range,
+    compute_threshold's 25-step bisection, GridRefinement::refine's `>=` marking). Pure Python loops
+    over the cells (test-size inputs). Returns (flags, threshold)."""
+    c = [float(x) for x in np.asarray(criteria, dtype=np.float32)]
+    n = len(c)
+    if n == 0:
+        return np.zeros(0, dtype=np.int32), 0.0
+    gmin, gmax = min(c), max(c)
+    if fraction_type == "number":
+        frac = float(top_fraction)
+        inc = float(2 ** dim - 1)
+        if n >= max_n_cells:
+            frac = 0.0
+        elif int(n + n * top_fraction * inc) > max_n_cells:
+            alpha = 1.0 * (max_n_cells - n) / (n * top_fraction * inc)
+            frac = alpha * top_fraction
+        target = float(int(frac * n))
+    else:
+        tot = np.float32(0.0)
+        for x in np.asarray(criteria, dtype=np.float32):  # summed in the indicator type (float)
+            tot = np.float32(tot + x)
+        target = float(top_fraction) * float(tot)
+    lo, hi = gmin, gmax
+    if lo > 0:
+        lo *= 0.99
+    if hi > 0:
+        hi *= 1.01
+    else:
+        hi += 0.01 * (hi - lo)
+    it = 0
+    while lo != hi:
+        test = math.sqrt(lo * hi) if lo > 0 else (lo + hi) / 2
+        above = sum((1.0 if fraction_type == "number" else x) for x in c if x > test)
+        if above > target:
+            lo = test
+        elif above < target:
+            hi = test
+        else:
+            lo = hi = test
+        it += 1
+        if it == 25:
+            lo = hi = test
+    thr = min(lo, gmax) if fraction_type == "fraction" else lo
+    flags = np.array([1 if abs(x) >= thr else 0 for x in c], dtype=np.int32)
+    return flags, thr
+
+
 def evaluate_field(p: StructuredProblem, sol, X):
     """FE field of a hyper_cube problem at points X [npts, dim]: (velocity [npts, dim], pressure
     [npts]) — the coarse interpolant SolutionTransfer samples (navier_stokes_base.cc:689-733)."""

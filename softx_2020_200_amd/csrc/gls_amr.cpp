@@ -249,6 +249,72 @@ int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_f
   return cnt;
 }
 
+// parallel::distributed::GridRefinement, the call refine_mesh_kelly makes
+// (navier_stokes_base.cc:654-667; deal.II 9.2 source/distributed/grid_refinement.cc, not vendored).
+// The threshold is found by bisection between the slightly widened indicator extremes (geometric
+// mean while the lower end is > 0), 25 steps at most: the number (or summed error) of cells strictly
+// above the test value decides the half kept. Cells with criteria >= threshold are flagged
+// (dealii::GridRefinement::refine). The summed quantities are global sums, so with per-rank
+// indicators the caller gathers them first (the app adapts on one process).
+int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
+                  int64_t max_n_cells, int32_t *flags, double *threshold) {
+  if (n_cells < 0 || (n_cells && (!criteria || !flags)) || (dim != 2 && dim != 3) || top_fraction < 0 ||
+      top_fraction > 1 || (fraction_type != 0 && fraction_type != 1) || max_n_cells < 0)
+    return gls_io_set_error(GLS_EINVAL, "gls_refine_pd: bad arguments");
+  for (int64_t i = 0; i < n_cells; ++i) flags[i] = 0;
+  if (threshold) *threshold = 0.0;
+  if (n_cells == 0) return 0;
+  double lo = criteria[0], hi = criteria[0];
+  float total = 0.0f;  // compute_global_sum accumulates in the indicator type
+  for (int64_t i = 0; i < n_cells; ++i) {
+    if (!(criteria[i] >= 0.0f)) return gls_io_set_error(GLS_EINVAL, "gls_refine_pd: criteria must be >= 0");
+    lo = std::min(lo, (double)criteria[i]);
+    hi = std::max(hi, (double)criteria[i]);
+    total += criteria[i];
+  }
+  const double gmax = hi;
+  double target;
+  if (fraction_type == 0) {
+    // GridRefinement::adjust_refine_and_coarsen_number_fraction<dim> (no coarsening): cap the
+    // refined count so that the mesh grows to at most max_n_cells
+    double frac = top_fraction;
+    const double nc = (double)n_cells, inc = (double)((1 << dim) - 1);
+    if (n_cells >= max_n_cells) frac = 0.0;
+    else if ((int64_t)(nc + nc * top_fraction * inc) > max_n_cells)
+      frac = (double)(max_n_cells - n_cells) / (nc * top_fraction * inc) * top_fraction;
+    target = (double)(int64_t)(frac * nc);
+  } else {
+    target = top_fraction * total;  // L1 norm: fraction of the summed indicators
+  }
+  // adjust_interesting_range
+  if (lo > 0) lo *= 0.99;
+  if (hi > 0) hi *= 1.01;
+  else hi += 0.01 * (hi - lo);
+  double thr = lo;
+  for (int it = 0;; ++it) {
+    if (lo == hi) {
+      thr = fraction_type == 1 ? std::min(lo, gmax) : lo;
+      break;
+    }
+    const double test = lo > 0 ? std::sqrt(lo * hi) : (lo + hi) / 2;
+    double above = 0.0;
+    for (int64_t i = 0; i < n_cells; ++i)
+      if (criteria[i] > test) above += fraction_type == 0 ? 1.0 : (double)criteria[i];
+    if (above > target) lo = test;
+    else if (above < target) hi = test;
+    else lo = hi = test;
+    if (it + 1 == 25) lo = hi = test;
+  }
+  int cnt = 0;
+  for (int64_t i = 0; i < n_cells; ++i)
+    if (std::fabs(criteria[i]) >= thr) {
+      flags[i] = 1;
+      ++cnt;
+    }
+  if (threshold) *threshold = thr;
+  return cnt;
+}
+
 // SolutionTransfer::interpolate for the first refinement of a uniform mesh (navier_stokes_base.cc:
 // 689-733): every node of the refined mesh lies in a cell of hyper_cube(n, lo, hi), whose Qk
 // interpolant it samples (exact for the refined space, which contains the coarse one).

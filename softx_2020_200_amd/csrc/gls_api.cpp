@@ -1380,8 +1380,9 @@ bool coarse_graph_eligible(gls_ctx *c, gls_ctx *g, const double *b, const double
 // viscosity), the sweep count and damping, and the buffers the sweeps read and write. Buffer
 // CONTENTS (state, linearization, diagonal) are read at replay time, so a new Newton state with
 // unchanged parameters replays the same graph.
-std::vector<unsigned char> coarse_graph_key(gls_ctx *g, const double *b, const double *x, const double *y, int pre,
-                                            double om) {
+}  // extern "C"
+static std::vector<unsigned char> coarse_graph_key(gls_ctx *g, const double *b, const double *x, const double *y,
+                                                   int pre, double om) {
   const gls::OpParams P = make_params(g);
   const void *ptrs[7] = {b, x, y, g->diag.p, g->qdata.p, g->qdata32.p, brick_slab(g)};
   const int64_t ints[4] = {pre, g->n_dofs, (int64_t)g->smooth_f32, (int64_t)slab_f32()};
@@ -1393,6 +1394,7 @@ std::vector<unsigned char> coarse_graph_key(gls_ctx *g, const double *b, const d
   std::memcpy(o + sizeof(ints), &om, sizeof(om));
   return k;
 }
+extern "C" {
 // capture x = csweeps damped-Jacobi sweeps from x = 0 on c's stream; a refused capture leaves the
 // plain launches in place (cgraph_failed)
 int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, double *y, int pre, double om) {

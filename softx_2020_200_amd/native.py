@@ -35,7 +35,7 @@ EXPORTS = [
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
-    "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate",
+    "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
 ]
 
 
@@ -139,6 +139,8 @@ def load():
     L.gls_mesh_refined_destroy.argtypes = [C.POINTER(RefinedMesh)]
     L.gls_kelly_estimate.argtypes = [vp, vp, C.c_int, vp]
     L.gls_refine_fixed_number.argtypes = [i64, C.POINTER(C.c_float), C.c_double, C.POINTER(C.c_int32)]
+    L.gls_refine_pd.argtypes = [i64, C.POINTER(C.c_float), C.c_int, C.c_int, C.c_double, i64,
+                                C.POINTER(C.c_int32), C.POINTER(C.c_double)]
     L.gls_mesh_refined_interpolate.argtypes = [C.POINTER(RefinedMesh), C.c_int, C.c_double, C.c_double,
                                                C.POINTER(C.c_double), C.POINTER(C.c_double)]
     _lib = L
@@ -243,6 +245,19 @@ def refine_fixed_number(criteria, top_fraction):
                                         flags.ctypes.data_as(C.POINTER(C.c_int32)))
     check(min(rc, 0), "gls_refine_fixed_number")
     return flags
+
+
+def refine_pd(criteria, dim, top_fraction, fraction_type="number", max_n_cells=100000000):
+    """parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number / _fixed_fraction,
+    refinement flags (gls_refine_pd; navier_stokes_base.cc:654-667). Returns (flags, threshold)."""
+    c = np.ascontiguousarray(criteria, dtype=np.float32)
+    flags = np.zeros(c.size, dtype=np.int32)
+    thr = C.c_double(0.0)
+    ft = {"number": 0, "fraction": 1}[fraction_type]
+    rc = load().gls_refine_pd(c.size, c.ctypes.data_as(C.POINTER(C.c_float)), int(dim), ft, float(top_fraction),
+                              int(max_n_cells), flags.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(thr))
+    check(min(rc, 0), "gls_refine_pd")
+    return flags, thr.value
 
 
 def refined_interpolate(dim, n, k, kp, refine, coarse, lo=-1.0, hi=1.0):

@@ -16,7 +16,8 @@ import os
 import numpy as np
 import pytest
 
-from oracle.oracle import Oracle, StructuredProblem, evaluate_field, kelly_estimate, muparser_to_numpy, newton_solve
+from oracle.oracle import (Oracle, StructuredProblem, evaluate_field, kelly_estimate, muparser_to_numpy, newton_solve,
+                           pd_refine_fixed)
 import softx_2020_200_amd as sx
 
 SEED = 20200200
@@ -50,6 +51,37 @@ def test_refine_fixed_number_matches_numpy():
             thr = np.sort(c)[::-1][nr - 1]
             exp = (c >= thr).astype(np.int32)
         assert np.array_equal(f, exp)
+
+
+def test_pd_refine_known_answers():
+    """parallel::distributed fixed-number / fixed-fraction thresholds on hand-checkable inputs."""
+    c = np.arange(1, 11, dtype=np.float32)
+    for impl in (lambda *a, **k: sx.refine_pd(*a, **k), pd_refine_fixed):
+        f, thr = impl(c, 2, 0.3)  # target int(0.3 * 10) = 3 cells strictly above the bisection value
+        assert f.tolist() == [0] * 7 + [1] * 3 and 7 < thr <= 8
+        f, _ = impl(np.array([1, 1, 1, 1, 6], np.float32), 2, 0.5, "fraction")  # 6 of 10 >= half
+        assert f.tolist() == [0, 0, 0, 0, 1]
+        # max number elements: 100 + 30 * 3 > 130 -> alpha = 30 / 90 -> 10 cells
+        f, _ = impl(np.linspace(0.1, 1, 100).astype(np.float32), 2, 0.3, "number", 130)
+        assert f.sum() == 10 and f[-10:].all()
+        f, _ = impl(c, 3, 0.3, "number", 10)  # already at the cap: nothing refines
+        assert f.sum() == 0
+        f, _ = impl(np.zeros(8, np.float32), 3, 0.5)  # all-zero indicators (lo = hi = 0)
+        assert f.sum() == 8
+
+
+@pytest.mark.parametrize("ftype", ["number", "fraction"])
+def test_pd_refine_matches_oracle(ftype):
+    rng = np.random.default_rng(SEED)
+    for n, frac, dim, cap in ((100, 0.3, 2, 10 ** 8), (512, 0.1, 3, 10 ** 8), (37, 0.5, 2, 60), (64, 0.0, 3, 10 ** 8),
+                              (200, 0.25, 3, 500), (1000, 0.05, 2, 10 ** 8)):
+        c = (10.0 ** rng.uniform(-6, 0, n)).astype(np.float32)  # Kelly-like spread over decades
+        c[: n // 7] = c[n // 7]  # ties
+        f, thr = sx.refine_pd(c, dim, frac, ftype, cap)
+        fo, thro = pd_refine_fixed(c, dim, frac, ftype, cap)
+        assert thr == thro and np.array_equal(f, fo), (n, frac, dim, cap)
+        if ftype == "number" and cap == 10 ** 8 and frac > 0:  # bisection lands near int(frac * n) cells
+            assert abs(int(f.sum()) - int(frac * n)) <= n // 7 + 1
 
 
 @pytest.mark.parametrize("dim,n,k,kp", [(2, 3, 1, 1), (2, 3, 2, 1), (3, 2, 2, 2), (3, 3, 1, 1)])

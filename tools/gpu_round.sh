@@ -8,7 +8,7 @@ O=$R/gpurun_out
 mkdir -p $O
 cd $R
 stop() { echo "step '$1' ended with $2" >> $O/round.log; exit $2; }
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/gputests.log 2>&1; rc=$?
+[ -n "$SKIP_TESTS" ] || timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gputests.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> $O/round.log
 [ $rc -gt 1 ] && stop pytest $rc
 timeout -k 10 120 python tools/jv_bench.py 128 20 > $O/jv.log 2>&1 || stop jv_bench $?

@@ -26,7 +26,7 @@ for _ in range(reps // 4 + 1):
     ctx.residual(y)
 d_out = torch.empty_like(v)
 ctx.jacobian_diagonal(out=d_out)  # k_copy of n_dofs doubles: PMC byte calibration (tools/pmc_traffic.sh)
-if ctx.uses_brick_kernels:  # FP32 smoother operator (timing slot 4)
+if ctx.uses_brick_kernels and not os.environ.get("GLS_JV_RECOMPUTE"):  # FP32 smoother J.v (slot 4; cached path only)
     for _ in range(reps):
         ctx.jacobian_apply_f32(v, y)
 ms_jv, n_jv = ctx.timing_get(1)
