@@ -12,7 +12,7 @@
 // Usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm
 // Scope: mesh type dealii / grid type hyper_cube (+ initial refinement; steady "number mesh adapt"
 // with mesh adaptation type uniform, or kelly = one Kelly-driven local refinement with hanging
-// nodes: fraction type number, no coarsening); bc types noslip, function, periodic, slip.
+// nodes: fraction type number or fraction, no coarsening); bc types noslip, function, periodic, slip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -158,6 +158,8 @@ struct Params {
   std::string madapt = "none";
   int kelly_variable = 0;  // 0 velocity, 1 pressure
   double frac_refine = 0.1;
+  int frac_type = 0;            // 0 fixed number, 1 fixed fraction (of the summed indicators)
+  int64_t max_cells = 100000000;  // max number elements
   int max_level = 10;
 };
 
@@ -210,8 +212,10 @@ Params read_params(const Prm &p, int dim) {
     const std::string var = p.get(ma + "variable", "velocity");
     if (var != "velocity" && var != "pressure") die("mesh adaptation variable '%s' is unknown", var.c_str());
     P.kelly_variable = var == "pressure" ? 1 : 0;
-    if (p.get(ma + "fraction type", "number") != "number")
-      die("mesh adaptation: fraction type '%s' is not supported (number only)", p.get(ma + "fraction type", "").c_str());
+    const std::string ftype = p.get(ma + "fraction type", "number");
+    if (ftype != "number" && ftype != "fraction") die("mesh adaptation: fraction type '%s' is unknown", ftype.c_str());
+    P.frac_type = ftype == "fraction" ? 1 : 0;
+    P.max_cells = (int64_t)p.d(ma + "max number elements", 100000000);
     P.frac_refine = p.d(ma + "fraction refinement", 0.1);
     P.max_level = p.i(ma + "max refinement level", 10);
     if (p.d(ma + "fraction coarsening", 0.05) != 0.0)
@@ -1082,8 +1086,10 @@ struct Solver {
     (void)hipFree(d_eta);
     std::vector<float> crit(eta.begin(), eta.end());
     std::vector<int32_t> cflag((size_t)old.nc, 0), flags((size_t)old.nc, 0);
-    const int nflag = gls_refine_fixed_number(old.nc, crit.data(), P.frac_refine, cflag.data());
-    ck(nflag, "gls_refine_fixed_number");
+    // parallel::distributed::GridRefinement::refine_and_coarsen_fixed_{number,fraction} (:654-667)
+    const int nflag = gls_refine_pd(old.nc, crit.data(), old.dim, P.frac_type, P.frac_refine, P.max_cells,
+                                    cflag.data(), nullptr);
+    ck(nflag, "gls_refine_pd");
     // cells at max refinement level keep their refine flag cleared (tria.n_levels() > max level)
     if (P.max_level <= P.refinement) std::fill(cflag.begin(), cflag.end(), 0);
     // the hyper_cube's cell order -> the lexicographic order gls_mesh_refined_create expects

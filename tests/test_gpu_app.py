@@ -240,22 +240,25 @@ def test_app_mms2d_slip_walls_matches_oracle(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,variable", [(2, "velocity"), (2, "pressure"), (3, "velocity")])
-def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable):
+@pytest.mark.parametrize("dim,variable,ftype", [(2, "velocity", "number"), (2, "pressure", "number"),
+                                                (3, "velocity", "number"), (2, "velocity", "fraction")])
+def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable, ftype):
     """mesh adaptation type = kelly (refine_mesh_kelly, navier_stokes_base.cc:610-780) in the app, first
-    adaptation of the uniform 8^2 (mms2d) / 8^3 (mms3d) Q1 mesh: Kelly indicator on the device, top 30 % flagged
-    (fraction type number, no coarsening), one refinement with hanging nodes, solution transfer,
+    adaptation of the uniform 8^2 (mms2d) / 8^3 (mms3d) Q1 mesh: Kelly indicator on the device, 30 % flagged
+    by parallel::distributed::GridRefinement (fraction type number: cells; fraction: summed indicator; no
+    coarsening), one refinement with hanging nodes, solution transfer,
     Newton on the refined mesh. The first row equals the reference golden; the refined row equals the
     oracle's own pipeline (solve -> Kelly -> flag -> refine -> condensed solve). Parity unpinned beyond
     the oracle: the reference holds no Kelly golden on this mesh."""
     import numpy as np
-    from oracle.oracle import Oracle, StructuredProblem, kelly_estimate, muparser_to_numpy, newton_solve
+    from oracle.oracle import (Oracle, StructuredProblem, kelly_estimate, muparser_to_numpy, newton_solve,
+                               pd_refine_fixed)
     import softx_2020_200_amd as sx
     g = G["mms2d_gls" if dim == 2 else "mms3d_gls"]
     n, gi = (8, 0) if dim == 2 else (8, 1)  # 4^3: the discrete velocity is ~0, Kelly is roundoff
     prm = mms_prm(g, dim, 3, 1).replace("  set type = uniform\n", f"""  set type = kelly
   set variable = {variable}
-  set fraction type = number
+  set fraction type = {ftype}
   set fraction refinement = 0.3
   set fraction coarsening = 0
 """)
@@ -270,7 +273,7 @@ def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable):
     p.set_dirichlet([("noslip", 0, None)])
     x, _, _ = newton_solve(p, tol=1e-10)
     eta = kelly_estimate(p, x, 0 if variable == "velocity" else 1)
-    flags = sx.refine_fixed_number(eta.astype(np.float32), 0.3)
+    flags, _ = pd_refine_fixed(eta.astype(np.float32), dim, 0.3, ftype)
     assert int(rows[1][0]) == n ** dim + (2 ** dim - 1) * int(flags.sum()), (rows, int(flags.sum()))
     mesh = sx.refined_cube(dim, n, 1, 1, flags)
     q = StructuredProblem.from_refined(mesh, viscosity=1.0)
