@@ -1,5 +1,6 @@
-"""Size-independent properties at the benchmark's full size (BASELINE configs[2]: 3D cavity Q2-Q2
-128^3, BDF2, nu = 0.01, dt = 0.01; 67.9 M DoFs), where the oracle cannot run.
+"""Size-independent properties at BASELINE's full sizes, where the oracle cannot run:
+configs[2] (the bench: 3D cavity Q2-Q2 128^3, BDF2, nu = 0.01, dt = 0.01; 67.9 M DoFs) and configs[1]
+(3D cavity Q1-Q1 64^3, steady, nu = 1; 1.1 M DoFs, the persistent wave-per-brick kernel).
 
 * patch test: a constant velocity c (history = c, Dirichlet = c on every wall), the linear pressure
   p = x + 2y + 3z and the force f = grad p solve the discrete GLS equations exactly
@@ -10,13 +11,16 @@
   oracle parity tests pin at small sizes) on a seeded random state: residual and J.v to 1e-12;
 * J.v is deterministic (atomic-free brick sums: bitwise equal on repeat) and linear;
 * the FP32 smoother J.v equals the FP64 one to FP32 accuracy.
-GLS_FULLSIZE_N overrides the 128 cells per direction (the GPU suite runs the full size)."""
+GLS_FULLSIZE_N overrides the cells per direction of both (the GPU suite runs the full sizes)."""
 import os
 
 import numpy as np
 import pytest
 
-N = int(os.environ.get("GLS_FULLSIZE_N", "128"))
+_NO = os.environ.get("GLS_FULLSIZE_N")
+# (k, cells per direction, scheme, viscosity)
+CONFIGS = [(2, int(_NO or 128), "bdf2", 0.01), (1, int(_NO or 64), "steady", 1.0)]
+IDS = ["Q2_128_bdf2", "Q1_64_steady"]
 SEED = 20200200
 DT = (0.01, 0.01, 0.01, 0.01)
 
@@ -28,12 +32,14 @@ def _relmax(a, b):
     return float((a - b).abs().max() / b.abs().max())
 
 
-@pytest.fixture(scope="module")
-def cavity():
+@pytest.fixture(scope="module", params=CONFIGS, ids=IDS)
+def cavity(request):
     import torch
     from softx_2020_200_amd.problem import CavityProblem
-    prob = CavityProblem(3, N, 2, 2, viscosity=0.01)
-    prob.ctx.set_time("bdf2", DT)
+    k, n, scheme, nu = request.param
+    prob = CavityProblem(3, n, k, k, viscosity=nu)
+    prob.ctx.set_time(scheme, DT)
+    prob.cfg = request.param
     assert prob.ctx.uses_brick_kernels
     g = torch.Generator(device="cuda").manual_seed(SEED)
     r = lambda: torch.rand(prob.n_dofs, dtype=torch.float64, device="cuda", generator=g) * 2 - 1
@@ -43,22 +49,24 @@ def cavity():
     del prob
 
 
-def test_fullsize_patch_test_linear_pressure():
+@pytest.mark.parametrize("cfg", CONFIGS, ids=IDS)
+def test_fullsize_patch_test_linear_pressure(cfg):
     import torch
     from softx_2020_200_amd.problem import build_context, dirichlet_from_bcs, vnode_boundary_ids
     from softx_2020_200_amd import hyper_cube
-    mesh = hyper_cube(3, N, 2, 2, -1.0, 1.0)
+    k, n, scheme, nu = cfg
+    mesh = hyper_cube(3, n, k, k, -1.0, 1.0)
     c = (0.3, -0.2, 0.1)
-    mask, dofs, vals = dirichlet_from_bcs(mesh, N, -1.0, 1.0, True, [("function", b, c) for b in range(6)])
-    nq = 27
+    mask, dofs, vals = dirichlet_from_bcs(mesh, n, -1.0, 1.0, True, [("function", b, c) for b in range(6)])
+    nq = (k + 1) ** 3
     force = np.empty((mesh["n_cells"] * nq, 3))
     force[:] = (1.0, 2.0, 3.0)
-    ctx = build_context(mesh, viscosity=0.01, vnode_mask=mask, force_q=force)
+    ctx = build_context(mesh, viscosity=nu, vnode_mask=mask, force_q=force)
     del force
-    ctx.set_time("bdf2", DT)
+    ctx.set_time(scheme, DT)
     ctx.set_dirichlet(dofs, vals)
     assert ctx.uses_brick_kernels
-    _, X = vnode_boundary_ids(mesh, N, -1.0, 1.0, True)  # pressure nodes = velocity nodes (Q2-Q2)
+    _, X = vnode_boundary_ids(mesh, n, -1.0, 1.0, True)  # pressure nodes = velocity nodes (Qk-Qk)
     nv = mesh["n_vnodes"]
     U = np.empty(ctx.n_dofs)
     U[:3 * nv] = np.tile(c, nv)
@@ -78,13 +86,14 @@ def test_fullsize_patch_test_linear_pressure():
 def test_fullsize_brick_equals_cell_kernels(cavity, monkeypatch):
     from softx_2020_200_amd.problem import build_context
     prob, (u, u1, u2, v, _) = cavity
+    k, n, scheme, nu = prob.cfg
     r_b = prob.ctx.residual().clone()
     jv_b = prob.ctx.jacobian_apply(v).clone()
     monkeypatch.setenv("GLS_DISABLE_BRICK", "1")
-    ctx = build_context(prob.mesh, viscosity=0.01, vnode_mask=prob.vnode_mask)
+    ctx = build_context(prob.mesh, viscosity=nu, vnode_mask=prob.vnode_mask)
     monkeypatch.delenv("GLS_DISABLE_BRICK")
     assert not ctx.uses_brick_kernels
-    ctx.set_time("bdf2", DT)
+    ctx.set_time(scheme, DT)
     ctx.set_dirichlet(prob.dir_dofs, prob.dir_vals)
     ctx.set_state(u, u1, u2)
     er = _relmax(ctx.residual(), r_b)
