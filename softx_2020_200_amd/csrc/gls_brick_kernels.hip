@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
                                   (std::is_same<Real, float>::value ? GLS_BRICK_WPE_F32 : GLS_BRICK_WAVES_PER_EU))
     gls_brick_kernel(const OpParams P, const Tables1D T) {
   using C = BrickCfg<K>;
-  constexpr int K1 = C::K1, N3 = C::N3, L2 = C::L2, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
+  constexpr int K1 = C::K1, N3 = C::N3, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
   constexpr bool JV = MODE == MODE_JV || MODE == MODE_JVQ;
   constexpr bool CACHED = MODE == MODE_JVQ;  // linearization read from P.qd (no state sweeps)
   constexpr bool LIN = MODE == MODE_LIN;     // store the linearization to P.qd, no integration

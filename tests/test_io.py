@@ -187,6 +187,11 @@ def _app(tmp_path, prm_text, *args):
     ("subsection source term\n set enable = true\n subsection xyz\n  set Function expression = q*2; 0; 0; 0\n"
      " end\nend\n", "unknown variable 'q'"),
     ("subsection mesh\n set initial refinement = 2\n", "not closed"),
+    ("subsection simulation control\n set method = steady\n set number mesh adapt = 1\nend\n"
+     "subsection mesh adaptation\n set type = kelly\n set fraction type = banana\nend\n", "fraction type 'banana' is unknown"),
+    ("subsection simulation control\n set method = steady\n set number mesh adapt = 1\nend\n"
+     "subsection mesh adaptation\n set type = kelly\n set fraction type = fraction\nend\n",  # default coarsening 0.05
+     "coarsening is not supported"),
 ])
 def test_app_rejects_unsupported_input_before_touching_the_gpu(tmp_path, text, msg):
     out = _app(tmp_path, text, "--dim", "3")
