@@ -133,6 +133,7 @@ struct Params {
   Method method = Method::steady;
   double dt = 1.0, t_end = 1.0, startup = 0.4;
   int mesh_adapt = 0, output_frequency = 1, subdivision = 1, log_frequency = 1;
+  int adapt_frequency = 1;  // mesh adaptation/frequency (refine_mesh: step % frequency == 0)
   std::string output_path = "./", output_name = "out";
   double nu = 1.0;
   int k = 1, kp = 1;
@@ -151,6 +152,7 @@ struct Params {
   bool enstrophy = false, kinetic = false, pp_verbose = false;
   double newton_tol = 1e-6;
   int newton_max = 10, newton_verbose = 0, lin_max = 1000, restart = 30;
+  int nl_solver = GLS_NEWTON, skip_iterations = 1;  // non-linear solver/solver, skip iterations
   double lin_rel = 1e-3, lin_min = 1e-8;
   bool srf = false;
   double omega[3] = {0, 0, 0};
@@ -205,6 +207,8 @@ Params read_params(const Prm &p, int dim) {
   P.refinement = p.i("mesh/initial refinement", 0);
   const std::string madapt = p.get("mesh adaptation/type", "none");
   P.madapt = madapt;
+  P.adapt_frequency = p.i("mesh adaptation/frequency", 1);
+  if (P.adapt_frequency < 1) die("mesh adaptation/frequency must be >= 1");
   if (P.method == Method::steady && P.mesh_adapt > 0 && madapt != "uniform" && madapt != "kelly")
     die("mesh adaptation type '%s' is not supported (uniform or kelly)", madapt.c_str());
   if (madapt == "kelly") {  // refine_mesh_kelly (navier_stokes_base.cc:610-780), first adaptation only
@@ -255,6 +259,13 @@ Params read_params(const Prm &p, int dim) {
   P.newton_tol = p.d("non-linear solver/tolerance", 1e-6);
   P.newton_max = p.i("non-linear solver/max iterations", 10);
   P.newton_verbose = p.get("non-linear solver/verbosity", "verbose") == "verbose" ? 1 : 0;
+  {
+    const std::string sv = p.get("non-linear solver/solver", "newton");
+    if (sv == "skip_newton") P.nl_solver = GLS_SKIP_NEWTON;
+    else if (sv != "newton") die("non-linear solver '%s' is unknown (newton|skip_newton)", sv.c_str());
+    P.skip_iterations = p.i("non-linear solver/skip iterations", 1);
+    if (P.skip_iterations < 1) die("non-linear solver/skip iterations must be >= 1");
+  }
   P.lin_max = p.i("linear solver/max iters", 1000);
   P.lin_rel = p.d("linear solver/relative residual", 1e-3);
   P.lin_min = p.d("linear solver/minimum residual", 1e-8);
@@ -825,7 +836,8 @@ struct Solver {
   }
 
   // ---- one nonlinear solve of `scheme` from the current present solution and history
-  void solve_nonlinear(int scheme, double nu_override = -1.0) {
+  // solve_non_linear_system(method, first_iteration = false, force_matrix_renewal)
+  void solve_nonlinear(int scheme, double nu_override = -1.0, bool force_renewal = false) {
     double ts[4];
     for (int i = 0; i < 4; ++i) ts[i] = dts[i] > 0 ? dts[i] : 1.0;
     ck(gls_set_time(ctx, scheme, ts), "gls_set_time");
@@ -844,7 +856,13 @@ struct Solver {
     np.lin.restart = P.restart;
     np.lin.relative_residual = P.lin_rel;
     np.lin.minimum_residual = P.lin_min;
+    np.solver = P.nl_solver;
+    np.skip_iterations = P.skip_iterations;
+    np.is_initial_step = 0;
+    np.force_matrix_renewal = force_renewal ? 1 : 0;
     ck(gls_newton_solve(ctx, d_present, d_m1, d_m2, d_m3, &np), "gls_newton_solve");
+    if (np.linear_failures > 0)
+      printf("  -Warning: %d linear solve(s) stopped at the iteration limit before the tolerance\n", np.linear_failures);
     download(d_present, present);
     newton_its += np.newton_iterations;
     linear_its += np.linear_iterations;
@@ -882,20 +900,20 @@ struct Solver {
     }
     const double dt = P.dt, s = P.startup;
     push_dt(dt * s);
-    solve_nonlinear(GLS_BDF1);
+    solve_nonlinear(GLS_BDF1, -1.0, true);  // start-up solves force a fresh matrix (:534-574)
     m2 = m1;
     m1 = present;
     if (P.method == Method::bdf2) {
       push_dt(dt * (1. - s));
-      solve_nonlinear(GLS_BDF2);
+      solve_nonlinear(GLS_BDF2, -1.0, true);
     } else {
       push_dt(dt * s);
-      solve_nonlinear(GLS_BDF1);
+      solve_nonlinear(GLS_BDF1, -1.0, true);
       m3 = m2;
       m2 = m1;
       m1 = present;
       push_dt(dt * (1. - 2. * s));
-      solve_nonlinear(GLS_BDF3);
+      solve_nonlinear(GLS_BDF3, -1.0, true);
     }
     dt_now = dt;
   }
@@ -1163,7 +1181,7 @@ struct Solver {
       if (step == 1) {
         first_step();
       } else {
-        if (steady) {
+        if (steady && step % P.adapt_frequency == 0) {  // refine_mesh (navier_stokes_base.cc:592-607)
           if (P.madapt == "kelly") refine_kelly();
           else refine_uniform();
         }

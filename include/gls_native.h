@@ -197,6 +197,8 @@ int gls_mg_detach(gls_ctx *ctx);
  * on device vectors: present (in/out, DEVICE, length n_dofs). History from gls_set_state's u1..u3
  * slots is given here explicitly.
  * ------------------------------------------------------------------------------------------ */
+#define GLS_NEWTON 0
+#define GLS_SKIP_NEWTON 1
 typedef struct {
   double tolerance;       /* non-linear solver/tolerance */
   int max_iterations;     /* non-linear solver/max iterations */
@@ -206,7 +208,19 @@ typedef struct {
   int linear_iterations;  /* out: total */
   int residual_evaluations; /* out */
   double final_residual;  /* out */
+  int solver;             /* non-linear solver/solver: GLS_NEWTON | GLS_SKIP_NEWTON (parameters.cc:385-440) */
+  int skip_iterations;    /* non-linear solver/skip iterations (skip_newton only; >= 1) */
+  int is_initial_step;    /* solve_non_linear_system(method, first_iteration, force_matrix_renewal) */
+  int force_matrix_renewal; /*   flags (physics_solver.h:92-96, navier_stokes_base.cc:461-590) */
+  int linear_failures;    /* out: linear solves that stopped at max iterations (the reference's
+                             SolverControl throws NoConvergence there; this library continues) */
 } gls_newton_params;
+/* Freeze (1) / release (0) the Jacobian at the current state: the skip_newton matrix reuse
+ * (skip_newton_non_linear_solver.h:66-70, 126-130). While frozen, gls_jacobian_apply,
+ * gls_jacobian_diagonal, the J.v linearization and the multigrid levels stay at the snapshot of
+ * the state vectors and time coefficients taken here; gls_set_state / gls_set_time move only the
+ * residual. gls_newton_solve with solver = GLS_SKIP_NEWTON drives this itself. */
+int gls_freeze_jacobian(gls_ctx *ctx, int freeze);
 int gls_newton_solve(gls_ctx *ctx, double *present, const double *u1, const double *u2, const double *u3,
                      gls_newton_params *prm);
 
@@ -252,6 +266,9 @@ int gls_sdirk_coefficients(int order, double dt, double *out);
 /* Newton driver KAT: the reference's fake physics x0^2+x1=0, 2x1+3=0
  * (tests/core/non_linear_test_system_01.h:50-129) through the same Newton template. */
 int gls_newton_selftest(double x_out[2]);
+/* SkipNewton KAT (tests/core/skip_newton_non_linear_solver_01.cc): same fake physics through the
+ * SkipNewton template (skip_newton_non_linear_solver.h:54-131), tol 1e-8, 10 iterations. */
+int gls_skip_newton_selftest(int skip_iterations, double x_out[2]);
 
 /* hyper_cube mesh + canonical DoF numbering (GridGenerator::hyper_cube + refine_global,
  * source/core/grids.cc:12-60). Periodic directions identify the high face with the low face.

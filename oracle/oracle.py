@@ -570,8 +570,22 @@ def pd_refine_fixed(criteria, dim, top_fraction, fraction_type="number", max_n_c
         if it == 25:
             lo = hi = test
     thr = min(lo, gmax) if fraction_type == "fraction" else lo
-    flags = np.array([1 if abs(x) >= thr else 0 for x in c], dtype=np.int32)
-    return flags, thr
+    return refine_mark(c, thr)
+
+
+def refine_mark(c, thr):
+    """dealii::GridRefinement::refine's marking (deal.II 9.2 source/grid/grid_refinement.cc, not
+    vendored): no flags when every indicator is 0; a zero threshold becomes the smallest positive
+    indicator, scanning from c[0] as deal.II does; flag |c| >= threshold. Returns (flags, threshold)."""
+    c = [float(x) for x in c]
+    if all(x == 0.0 for x in c):
+        return np.zeros(len(c), dtype=np.int32), thr
+    if thr == 0.0:
+        thr = c[0]
+        for x in c[1:]:
+            if 0 < x < thr:
+                thr = x
+    return np.array([1 if abs(x) >= thr else 0 for x in c], dtype=np.int32), thr
 
 
 def evaluate_field(p: StructuredProblem, sol, X):

@@ -228,6 +228,32 @@ int gls_mesh_refined_destroy(gls_refined_mesh *m) {
   return GLS_OK;
 }
 
+// dealii::GridRefinement::refine (deal.II 9.2 source/grid/grid_refinement.cc, not vendored), the
+// marking step both refinement rules end in: nothing is flagged when every indicator is zero;
+// a zero threshold is raised to the smallest positive indicator, the scan starting from
+// criteria[0] as deal.II's does (so a leading zero keeps it at 0); cells with |c| >= threshold
+// are flagged. Returns the number flagged.
+static int refine_mark(int64_t n_cells, const float *criteria, double threshold, int32_t *flags, double *used) {
+  bool all_zero = true;
+  for (int64_t i = 0; i < n_cells && all_zero; ++i) all_zero = criteria[i] == 0.0f;
+  if (used) *used = threshold;
+  if (all_zero) return 0;
+  double thr = threshold;
+  if (thr == 0.0) {
+    thr = criteria[0];
+    for (int64_t i = 1; i < n_cells; ++i)
+      if (criteria[i] > 0 && criteria[i] < thr) thr = criteria[i];
+  }
+  if (used) *used = thr;
+  int cnt = 0;
+  for (int64_t i = 0; i < n_cells; ++i)
+    if (std::fabs(criteria[i]) >= thr) {
+      flags[i] = 1;
+      ++cnt;
+    }
+  return cnt;
+}
+
 // GridRefinement::refine_and_coarsen_fixed_number, refinement part (navier_stokes_base.cc:654-661 with
 // the serial deal.II rule): n_refine = int(top_fraction * n_cells); threshold = the n_refine-th largest
 // indicator (std::nth_element); every cell with criteria >= threshold is flagged (GridRefinement::refine).
@@ -240,13 +266,7 @@ int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_f
   std::vector<float> tmp(criteria, criteria + n_cells);
   std::nth_element(tmp.begin(), tmp.begin() + (nr - 1), tmp.end(), std::greater<float>());
   const float thr = tmp[(size_t)(nr - 1)];
-  int cnt = 0;
-  for (int64_t i = 0; i < n_cells; ++i)
-    if (std::fabs(criteria[i]) >= thr) {
-      flags[i] = 1;
-      ++cnt;
-    }
-  return cnt;
+  return refine_mark(n_cells, criteria, thr, flags, nullptr);
 }
 
 // parallel::distributed::GridRefinement, the call refine_mesh_kelly makes
@@ -305,14 +325,7 @@ int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_
     else lo = hi = test;
     if (it + 1 == 25) lo = hi = test;
   }
-  int cnt = 0;
-  for (int64_t i = 0; i < n_cells; ++i)
-    if (std::fabs(criteria[i]) >= thr) {
-      flags[i] = 1;
-      ++cnt;
-    }
-  if (threshold) *threshold = thr;
-  return cnt;
+  return refine_mark(n_cells, criteria, thr, flags, threshold);
 }
 
 // SolutionTransfer::interpolate for the first refinement of a uniform mesh (navier_stokes_base.cc:

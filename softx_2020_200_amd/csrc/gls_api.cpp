@@ -403,6 +403,18 @@ struct gls_ctx {
     bool dirty = true;
   } mg;
   double time_steps[4] = {1, 1, 1, 1};
+  // frozen Jacobian (skip_newton: the matrix and its preconditioner are reused across Newton
+  // iterations, skip_newton_non_linear_solver.h:66-70, 126-130): snapshot of the state and time
+  // coefficients the Jacobian operators (J.v, diagonal, linearization, multigrid levels) are taken
+  // at, while gls_set_state / gls_set_time move only the residual's state
+  struct JacFreeze {
+    bool on = false;
+    DevBuf<double> u, h[3];
+    bool has[3] = {false, false, false};
+    double alpha[4] = {0, 0, 0, 0}, alpha_jac = 0., sdt2 = 0., ts[4] = {1, 1, 1, 1};
+    int n_hist = 0, scheme = GLS_STEADY;
+  } jf;
+  int skip_consecutive = 0;  // SkipNewtonNonLinearSolver::consecutive_iters (persists across solves)
   // timing
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
@@ -531,7 +543,8 @@ int check_ctx(gls_ctx *c) {
   return GLS_OK;
 }
 
-gls::OpParams make_params(gls_ctx *c) {
+// jac: parameters of the Jacobian operators (the frozen snapshot when gls_freeze_jacobian is on)
+gls::OpParams make_params(gls_ctx *c, bool jac = false) {
   gls::OpParams P;
   std::memset(&P, 0, sizeof(P));
   P.n_cells = c->n_cells;
@@ -554,6 +567,17 @@ gls::OpParams make_params(gls_ctx *c) {
   P.sdt2 = c->sdt2;
   P.srf = c->srf;
   for (int i = 0; i < 3; ++i) P.omega[i] = c->omega[i];
+  if (jac && c->jf.on) {
+    const auto &j = c->jf;
+    P.u = j.u.p;
+    P.h1 = j.has[0] ? j.h[0].p : j.u.p;
+    P.h2 = j.has[1] ? j.h[1].p : j.u.p;
+    P.h3 = j.has[2] ? j.h[2].p : j.u.p;
+    P.n_hist = j.n_hist;
+    for (int i = 0; i < 4; ++i) P.alpha[i] = j.alpha[i];
+    P.alpha_jac = j.alpha_jac;
+    P.sdt2 = j.sdt2;
+  }
   return P;
 }
 
@@ -615,7 +639,7 @@ int ensure_qdata(gls_ctx *c) {
   if (c->qd_valid) return GLS_OK;
   const size_t n = gls::brick_qdata_size(c->k, c->n_cells);
   if (c->qdata.n != n) GLS_TRY(c->qdata.alloc(n));
-  gls::OpParams P = make_params(c);
+  gls::OpParams P = make_params(c, true);
   P.qd = c->qdata.p;
   {
     TimedLaunch t(c, 3);
@@ -637,7 +661,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
   if (mode == gls::MODE_JV) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
-  gls::OpParams P = make_params(c);
+  gls::OpParams P = make_params(c, mode != gls::MODE_RESIDUAL);
   if (mode == gls::MODE_JV && c->use_brick && c->use_qdata) {
     GLS_TRY(ensure_qdata(c));
     P.qd = c->qdata.p;
@@ -860,7 +884,7 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
   c->scheme = scheme;
   if (ts)
     for (int i = 0; i < 4; ++i) c->time_steps[i] = ts[i];
-  c->mg.dirty = true;
+  if (!c->jf.on) c->mg.dirty = true;
   for (double &a : c->alpha) a = 0.;
   c->alpha_jac = 0.;
   c->sdt2 = 0.;
@@ -891,8 +915,10 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
       c->n_hist = stage;
     }
   }
-  c->diag_valid = false;
-  c->qd_valid = false;
+  if (!c->jf.on) {  // a frozen Jacobian keeps its own time coefficients
+    c->diag_valid = false;
+    c->qd_valid = false;
+  }
   return GLS_OK;
 }
 
@@ -903,12 +929,54 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
   c->u1 = u1;
   c->u2 = u2;
   c->u3 = u3;
-  c->diag_valid = false;
-  c->qd_valid = false;
-  c->mg.dirty = true;
+  if (!c->jf.on) {  // a frozen Jacobian stays at its snapshot (gls_freeze_jacobian)
+    c->diag_valid = false;
+    c->qd_valid = false;
+    c->mg.dirty = true;
+  }
   // distributed: refresh the ghost values of the evaluation point (history vectors are imported
   // by the caller once per time step with gls_dist_import)
   return dist_import(c, const_cast<double *>(u));
+}
+
+// Jacobian snapshot for skip_newton (skip_newton_non_linear_solver.h:66-70, 126-130): freeze = 1
+// copies the current state vectors and time coefficients; the Jacobian operators (J.v, diagonal,
+// linearization, multigrid levels) stay at that snapshot while later gls_set_state / gls_set_time
+// calls move only the residual. freeze = 0 releases it (everything is re-derived lazily).
+int gls_freeze_jacobian(gls_ctx *c, int freeze) {
+  GLS_TRY(check_ctx(c));
+  auto &j = c->jf;
+  if (!freeze) {
+    if (j.on) {
+      j.on = false;
+      c->diag_valid = false;
+      c->qd_valid = false;
+      c->mg.dirty = true;
+    }
+    return GLS_OK;
+  }
+  if (!c->u) return set_err(GLS_EINVAL, "gls_freeze_jacobian: gls_set_state was not called");
+  if (j.on) return GLS_OK;  // already frozen at its snapshot
+  const size_t n = (size_t)c->n_dofs;
+  if (j.u.n != n) GLS_TRY(j.u.alloc(n));
+  HIP_TRY(hipMemcpyAsync(j.u.p, c->u, sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+  const double *hs[3] = {c->u1, c->u2, c->u3};
+  for (int h = 0; h < 3; ++h) {
+    j.has[h] = hs[h] != nullptr && h < c->n_hist;
+    if (!j.has[h]) continue;
+    if (j.h[h].n != n) GLS_TRY(j.h[h].alloc(n));
+    HIP_TRY(hipMemcpyAsync(j.h[h].p, hs[h], sizeof(double) * n, hipMemcpyDeviceToDevice, c->stream));
+  }
+  for (int i = 0; i < 4; ++i) {
+    j.alpha[i] = c->alpha[i];
+    j.ts[i] = c->time_steps[i];
+  }
+  j.alpha_jac = c->alpha_jac;
+  j.sdt2 = c->sdt2;
+  j.n_hist = c->n_hist;
+  j.scheme = c->scheme;
+  j.on = true;  // diag / linearization / multigrid computed so far belong to this very state
+  return GLS_OK;
 }
 
 int gls_dist_import(gls_ctx *c, double *x) {
@@ -990,7 +1058,7 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
   GLS_TRY(ensure_diag(g));
   GLS_TRY(ensure_qdata32(g));
   GLS_TRY(dist_import(g, const_cast<double *>(v)));
-  gls::OpParams P = make_params(g);
+  gls::OpParams P = make_params(g, true);
   P.qdf = g->qdata32.p;
   P.v = v;
   P.y = y;
@@ -1032,7 +1100,7 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   GLS_TRY(ensure_diag(g));
   const bool f32 = g->smooth_f32;
   GLS_TRY(f32 ? ensure_qdata32(g) : ensure_qdata(g));
-  gls::OpParams P = make_params(g);
+  gls::OpParams P = make_params(g, true);
   P.v = x;
   P.y = x;
   P.jx = x;
@@ -1081,7 +1149,7 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
   if (c->hang.on)  // hanging values from their masters (all masters: Dirichlet values included)
     HIP_TRY(gls::vec_csr_gather_set(x, x, c->hang.dof.p, c->hang.off.p, c->hang.master.p, c->hang.w.p,
                                     (int64_t)c->hang.dof.n, c->stream));
-  if (x == c->u || x == c->u1 || x == c->u2 || x == c->u3) {  // the captured state changed
+  if (!c->jf.on && (x == c->u || x == c->u1 || x == c->u2 || x == c->u3)) {  // the captured state changed
     c->diag_valid = false;
     c->qd_valid = false;
     c->mg.dirty = true;
@@ -1223,12 +1291,20 @@ int mg_prepare(gls_ctx *c) {
   };
   const auto t0 = tick();
   const int L = (int)mg.lev.size();
+  // the levels are re-discretised at the Jacobian's state (the frozen snapshot under skip_newton)
+  const bool fz = c->jf.on;
+  const double *ju = fz ? c->jf.u.p : c->u;
+  const double *jh[3] = {fz ? (c->jf.has[0] ? c->jf.h[0].p : nullptr) : c->u1,
+                         fz ? (c->jf.has[1] ? c->jf.h[1].p : nullptr) : c->u2,
+                         fz ? (c->jf.has[2] ? c->jf.h[2].p : nullptr) : c->u3};
+  const int jscheme = fz ? c->jf.scheme : c->scheme;
+  const double *jts = fz ? c->jf.ts : c->time_steps;
   for (int l = 1; l < L; ++l) {
     gls_ctx *g = mg.lev[l];
-    const double *fu = l == 1 ? c->u : mgbuf(c, l - 1, MB_U);
-    const double *fh[3] = {l == 1 ? c->u1 : (c->u1 ? mgbuf(c, l - 1, MB_U1) : nullptr),
-                           l == 1 ? c->u2 : (c->u2 ? mgbuf(c, l - 1, MB_U2) : nullptr),
-                           l == 1 ? c->u3 : (c->u3 ? mgbuf(c, l - 1, MB_U3) : nullptr)};
+    const double *fu = l == 1 ? ju : mgbuf(c, l - 1, MB_U);
+    const double *fh[3] = {l == 1 ? jh[0] : (jh[0] ? mgbuf(c, l - 1, MB_U1) : nullptr),
+                           l == 1 ? jh[1] : (jh[1] ? mgbuf(c, l - 1, MB_U2) : nullptr),
+                           l == 1 ? jh[2] : (jh[2] ? mgbuf(c, l - 1, MB_U3) : nullptr)};
     GLS_TRY(mg_inject_level(c, l, fu, mgbuf(c, l, MB_U)));
     GLS_TRY(gls_apply_dirichlet(g, mgbuf(c, l, MB_U)));
     double *gh[3] = {nullptr, nullptr, nullptr};
@@ -1238,7 +1314,7 @@ int mg_prepare(gls_ctx *c) {
         GLS_TRY(mg_inject_level(c, l, fh[h], gh[h]));
       }
     g->viscosity = c->viscosity;
-    GLS_TRY(gls_set_time(g, c->scheme, c->time_steps));
+    GLS_TRY(gls_set_time(g, jscheme, jts));
     GLS_TRY(gls_set_state(g, mgbuf(c, l, MB_U), gh[0], gh[1], gh[2]));
     GLS_TRY(ensure_diag(g));
   }
@@ -1249,7 +1325,7 @@ int mg_prepare(gls_ctx *c) {
     if (g->use_brick && g->use_qdata) {  // all unit vectors in one launch per batch
       GLS_TRY(ensure_diag(g));
       GLS_TRY(ensure_qdata(g));
-      gls::OpParams P = make_params(g);
+      gls::OpParams P = make_params(g, true);
       P.qd = g->qdata.p;
       P.y = mg.probe.p;
       HIP_TRY(hipMemsetAsync(mg.probe.p, 0, sizeof(double) * (size_t)(n * n), c->stream));
@@ -1900,6 +1976,51 @@ struct NewtonStats {
   double final_res = 0.;
 };
 
+// SkipNewtonNonLinearSolver::solve (include/core/skip_newton_non_linear_solver.h:54-131): the
+// Jacobian (and its preconditioner) is assembled only when consecutive_iters == 0, on the initial
+// step or when forced, and only in the first outer iteration; every later iteration reuses it.
+template <class Phys>
+int skip_newton_template(Phys &ph, double tolerance, int max_iterations, int verbosity, int skip_iterations,
+                         bool is_initial_step, bool force_matrix_renewal, int &consecutive, NewtonStats &st) {
+  double current_res = 1.0, last_res = 1.0;
+  int outer = 0;
+  bool assembly_needed = consecutive == 0 || is_initial_step || force_matrix_renewal;
+  while (current_res > tolerance && outer < max_iterations) {
+    GLS_TRY(ph.evaluation_point_from_present());
+    if (assembly_needed) {
+      GLS_TRY(ph.assemble_matrix_and_rhs());
+      ++st.residuals;
+    } else if (outer == 0) {
+      GLS_TRY(ph.assemble_rhs());
+      ++st.residuals;
+    }
+    if (outer == 0) {
+      GLS_TRY(ph.rhs_norm(current_res));
+      last_res = current_res;
+    }
+    if (verbosity) printf("Newton iteration: %d  - Residual:  %g\n", outer, current_res);
+    int lin_it = 0;
+    GLS_TRY(ph.solve_linear_system(lin_it));  // renewed_matrix = assembly_needed: reused otherwise
+    st.linear += lin_it;
+    for (double alpha = 1.0; alpha > 1e-3; alpha *= 0.5) {
+      GLS_TRY(ph.line_point(alpha));
+      GLS_TRY(ph.assemble_rhs());
+      ++st.residuals;
+      GLS_TRY(ph.rhs_norm(current_res));
+      if (verbosity) printf("\t\talpha = %6g res = %g\n", alpha, current_res);
+      if (current_res < 0.9 * last_res || last_res < tolerance) break;
+    }
+    GLS_TRY(ph.present_from_evaluation_point());
+    last_res = current_res;
+    ++outer;
+    assembly_needed = false;
+  }
+  if (!force_matrix_renewal) consecutive = (consecutive + 1) % std::max(skip_iterations, 1);
+  st.outer = outer;
+  st.final_res = current_res;
+  return GLS_OK;
+}
+
 template <class Phys>
 int newton_template(Phys &ph, double tolerance, int max_iterations, int verbosity, NewtonStats &st) {
   double current_res = 1.0, last_res = 1.0;
@@ -1940,13 +2061,20 @@ struct DevicePhysics {
   const double *u1, *u2, *u3;
   gls_linear_params lin;
   int verbosity;
+  bool skip = false;  // skip_newton: the Jacobian is frozen between assemblies (gls_freeze_jacobian)
+  int linear_failures = 0;
   int evaluation_point_from_present() {
     HIP_TRY(gls::vec_copy(eval, present, c->n_dofs, c->stream));
     return gls_set_state(c, eval, u1, u2, u3);
   }
   int assemble_matrix_and_rhs() {  // matrix-free: residual + the Jacobian diagonal at this state
+    if (skip) {  // renew the frozen Jacobian at this evaluation point
+      GLS_TRY(gls_freeze_jacobian(c, 0));
+      GLS_TRY(gls_set_state(c, eval, u1, u2, u3));
+    }
     GLS_TRY(gls_residual(c, rhs));
-    return ensure_diag(c);
+    GLS_TRY(ensure_diag(c));
+    return skip ? gls_freeze_jacobian(c, 1) : GLS_OK;
   }
   int assemble_rhs() { return gls_residual(c, rhs); }
   int rhs_norm(double &r) {
@@ -1959,6 +2087,10 @@ struct DevicePhysics {
     gls_linear_params lp = lin;
     const int rc = gls_solve_linear(c, rhs, update, &lp);
     if (rc < 0 && rc != GLS_ENOCONV) return rc;
+    if (rc == GLS_ENOCONV) {
+      ++linear_failures;
+      if (verbosity) printf("  -Iterative solver did not converge: %d steps, residual %g\n", lp.iterations, lp.final_residual);
+    }
     its = lp.iterations;
     if (verbosity) printf("  -Iterative solver took : %d steps \n", lp.iterations);
     // zero_constraints.distribute(solution): constrained entries of the update are 0
@@ -2020,12 +2152,20 @@ int gls_newton_solve(gls_ctx *c, double *present, const double *u1, const double
   }
   DevicePhysics ph{c, present, c->tmp3.p, c->tmp4.p, c->tmp5.p, u1, u2, u3, prm->lin, prm->verbosity};
   NewtonStats st;
-  GLS_TRY(newton_template(ph, prm->tolerance, prm->max_iterations, prm->verbosity, st));
+  if (prm->solver == GLS_SKIP_NEWTON) {
+    ph.skip = true;
+    GLS_TRY(skip_newton_template(ph, prm->tolerance, prm->max_iterations, prm->verbosity, prm->skip_iterations,
+                                 prm->is_initial_step != 0, prm->force_matrix_renewal != 0, c->skip_consecutive, st));
+  } else {
+    GLS_TRY(gls_freeze_jacobian(c, 0));
+    GLS_TRY(newton_template(ph, prm->tolerance, prm->max_iterations, prm->verbosity, st));
+  }
   HIP_TRY(hipStreamSynchronize(c->stream));
   prm->newton_iterations = st.outer;
   prm->linear_iterations = st.linear;
   prm->residual_evaluations = st.residuals;
   prm->final_residual = st.final_res;
+  prm->linear_failures = ph.linear_failures;
   return GLS_OK;
 }
 
@@ -2035,6 +2175,19 @@ int gls_newton_selftest(double xo[2]) {
   KatPhysics ph;
   NewtonStats st;
   GLS_TRY(newton_template(ph, 1e-8, 10, 0, st));
+  xo[0] = ph.present[0];
+  xo[1] = ph.present[1];
+  return GLS_OK;
+}
+
+// SkipNewton KAT (tests/core/skip_newton_non_linear_solver_01.cc: tol 1e-8, max 10 iterations,
+// skip iterations as given; solve_non_linear_system(steady, true, true))
+int gls_skip_newton_selftest(int skip_iterations, double xo[2]) {
+  if (!xo || skip_iterations < 1) return set_err(GLS_EINVAL, "gls_skip_newton_selftest arguments");
+  KatPhysics ph;
+  NewtonStats st;
+  int consecutive = 0;
+  GLS_TRY(skip_newton_template(ph, 1e-8, 10, 0, skip_iterations, true, true, consecutive, st));
   xo[0] = ph.present[0];
   xo[1] = ph.present[1];
   return GLS_OK;

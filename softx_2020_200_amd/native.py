@@ -36,6 +36,7 @@ EXPORTS = [
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
     "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
+    "gls_freeze_jacobian", "gls_skip_newton_selftest",
 ]
 
 
@@ -83,7 +84,9 @@ class RefinedMesh(C.Structure):
 class NewtonParams(C.Structure):
     _fields_ = [("tolerance", C.c_double), ("max_iterations", C.c_int), ("verbosity", C.c_int),
                 ("lin", LinearParams), ("newton_iterations", C.c_int), ("linear_iterations", C.c_int),
-                ("residual_evaluations", C.c_int), ("final_residual", C.c_double)]
+                ("residual_evaluations", C.c_int), ("final_residual", C.c_double),
+                ("solver", C.c_int), ("skip_iterations", C.c_int), ("is_initial_step", C.c_int),
+                ("force_matrix_renewal", C.c_int), ("linear_failures", C.c_int)]
 
 
 _lib = None
@@ -120,6 +123,8 @@ def load():
     L.gls_bdf_coefficients.argtypes = [C.c_int, d, C.c_int, d]
     L.gls_sdirk_coefficients.argtypes = [C.c_int, C.c_double, d]
     L.gls_newton_selftest.argtypes = [d]
+    L.gls_skip_newton_selftest.argtypes = [C.c_int, d]
+    L.gls_freeze_jacobian.argtypes = [vp, C.c_int]
     L.gls_mesh_hyper_cube_sizes.argtypes = [C.c_int] * 5 + [C.POINTER(i64)] * 3
     L.gls_mesh_hyper_cube.argtypes = [C.c_int] * 4 + [C.c_double, C.c_double, C.c_int,
                                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32), d, d]
@@ -177,6 +182,12 @@ def sdirk_coefficients(order, dt):
 def newton_selftest():
     out = np.zeros(2)
     check(load().gls_newton_selftest(_dp(out)), "gls_newton_selftest")
+    return out
+
+
+def skip_newton_selftest(skip_iterations=1):
+    out = np.zeros(2)
+    check(load().gls_skip_newton_selftest(int(skip_iterations), _dp(out)), "gls_skip_newton_selftest")
     return out
 
 
@@ -457,14 +468,23 @@ class GLSContext:
         return x, p.iterations, p.final_residual, rc == GLS_OK
 
     def newton(self, present, u1=None, u2=None, u3=None, tolerance=1e-8, max_iterations=10, verbosity=0,
-               lin_max_iterations=1000, restart=30, relative_residual=1e-4, minimum_residual=1e-12):
+               lin_max_iterations=1000, restart=30, relative_residual=1e-4, minimum_residual=1e-12,
+               solver="newton", skip_iterations=1, is_initial_step=False, force_matrix_renewal=False):
+        """NewtonNonLinearSolver::solve / SkipNewtonNonLinearSolver::solve (solver="skip_newton")."""
         self._state = (present, u1, u2, u3)
         lp = LinearParams(lin_max_iterations, restart, relative_residual, minimum_residual, 0, 0.0)
-        p = NewtonParams(tolerance, max_iterations, verbosity, lp, 0, 0, 0, 0.0)
+        p = NewtonParams(tolerance, max_iterations, verbosity, lp, 0, 0, 0, 0.0,
+                         {"newton": 0, "skip_newton": 1}[solver], int(skip_iterations), int(is_initial_step),
+                         int(force_matrix_renewal), 0)
         check(self.L.gls_newton_solve(self.h, _ptr(present), _ptr(u1), _ptr(u2), _ptr(u3), C.byref(p)),
               "gls_newton_solve")
         return dict(newton_iterations=p.newton_iterations, linear_iterations=p.linear_iterations,
-                    residual_evaluations=p.residual_evaluations, final_residual=p.final_residual)
+                    residual_evaluations=p.residual_evaluations, final_residual=p.final_residual,
+                    linear_failures=p.linear_failures)
+
+    def freeze_jacobian(self, freeze=True):
+        """Keep the Jacobian operators at the current state (skip_newton matrix reuse)."""
+        check(self.L.gls_freeze_jacobian(self.h, 1 if freeze else 0), "gls_freeze_jacobian")
 
     def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6,
                          coarse_omega=0.0, coarse_direct=0, mixed_precision=0):

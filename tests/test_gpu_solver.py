@@ -241,3 +241,61 @@ def test_coarse_graph_matches_plain_launches(mp, monkeypatch):
         assert np.abs(z_plain).max() > 0
         assert np.array_equal(z_graph, z_plain), (shift, np.abs(z_graph - z_plain).max())
         assert np.array_equal(z_graph2, z_plain), shift
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_frozen_jacobian_operators(k):
+    """gls_freeze_jacobian (skip_newton matrix reuse): after freezing at state a and moving the state
+    to b, J.v and the diagonal stay those of a (bitwise), the residual is that of b; releasing the
+    freeze re-derives J at b. Brick path (k = 1, 2 in 3D) and per-cell path (2D)."""
+    import torch
+    for dim in (3, 2):
+        p = StructuredProblem(dim, 4, k=k, viscosity=0.02, scheme="bdf2", time_steps=(0.01, 0.012, 0.01, 0.01))
+        p.set_dirichlet([("noslip", 0, None)])
+        rng = np.random.default_rng(11)
+        a, b, h1, h2, v = (cuda(rng.uniform(-1, 1, p.n_dofs)) for _ in range(5))
+        ctx = context_for(p)
+        ctx.set_state(a, h1, h2)
+        ja, da, ra = ctx.jacobian_apply(v).clone(), ctx.jacobian_diagonal().clone(), ctx.residual().clone()
+        ctx.freeze_jacobian(True)
+        ctx.set_time("bdf1", (0.02, 0.01, 0.01, 0.01))  # the residual's scheme moves, J keeps bdf2
+        ctx.set_state(b, h1)
+        rb_frozen = ctx.residual().clone()
+        assert torch.equal(ctx.jacobian_apply(v), ja)
+        assert torch.equal(ctx.jacobian_diagonal(), da)
+        ctx.freeze_jacobian(False)
+        jb = ctx.jacobian_apply(v).clone()
+        rb = ctx.residual().clone()
+        assert torch.equal(rb_frozen, rb) and not torch.equal(rb, ra)
+        ref = context_for(p)
+        ref.set_time("bdf1", (0.02, 0.01, 0.01, 0.01))
+        ref.set_state(b, h1)
+        assert torch.equal(jb, ref.jacobian_apply(v))
+
+
+@pytest.mark.gpu
+def test_skip_newton_reaches_newton_solution():
+    """SkipNewtonNonLinearSolver (skip_newton_non_linear_solver.h:54-131) on the 3D Q2 cavity BDF2
+    step: the chord iterations (Jacobian of the first iteration reused) converge to the Newton
+    solution; more Newton iterations, one assembly."""
+    p = StructuredProblem(3, 4, k=2, viscosity=0.05, scheme="bdf2", time_steps=(0.01, 0.01, 0.01, 0.01),
+                          colorize=True)
+    p.set_dirichlet([("noslip", b, None) for b in (0, 1, 2, 4, 5)] +
+                    [("function", 3, lambda X: np.stack([np.ones(len(X)), 0 * X[:, 0], 0 * X[:, 0]], 1))])
+    rng = np.random.default_rng(5)
+    m1 = p.apply_nonzero_constraints(0.1 * rng.uniform(-1, 1, p.n_dofs))
+    m2 = p.apply_nonzero_constraints(0.1 * rng.uniform(-1, 1, p.n_dofs))
+    out = {}
+    for solver in ("newton", "skip_newton"):
+        ctx = context_for(p)
+        x = cuda(m1)
+        st = ctx.newton(x, cuda(m1), cuda(m2), tolerance=1e-10, max_iterations=30, lin_max_iterations=2000,
+                        restart=60, relative_residual=1e-10, minimum_residual=1e-14, solver=solver,
+                        skip_iterations=3, is_initial_step=False, force_matrix_renewal=True)
+        assert st["final_residual"] < 1e-10, (solver, st)
+        out[solver] = (x.cpu().numpy(), st)
+    (xn, sn), (xs, ss) = out["newton"], out["skip_newton"]
+    assert ss["newton_iterations"] > sn["newton_iterations"]
+    nu_ = p.dim * p.n_vnodes
+    assert np.abs(xs[:nu_] - xn[:nu_]).max() < 1e-8

@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle.oracle import (Oracle, StructuredProblem, evaluate_field, kelly_estimate, muparser_to_numpy, newton_solve,
+from oracle.oracle import (Oracle, StructuredProblem, evaluate_field, kelly_estimate, muparser_to_numpy, newton_solve, refine_mark,
                            pd_refine_fixed)
 import softx_2020_200_amd as sx
 
@@ -66,8 +66,22 @@ def test_pd_refine_known_answers():
         assert f.sum() == 10 and f[-10:].all()
         f, _ = impl(c, 3, 0.3, "number", 10)  # already at the cap: nothing refines
         assert f.sum() == 0
-        f, _ = impl(np.zeros(8, np.float32), 3, 0.5)  # all-zero indicators (lo = hi = 0)
-        assert f.sum() == 8
+        f, _ = impl(np.zeros(8, np.float32), 3, 0.5)  # all-zero indicators: GridRefinement::refine
+        assert f.sum() == 0                             # returns before marking anything
+
+
+def test_refine_zero_threshold_rules():
+    """dealii::GridRefinement::refine's zero rules through the fixed-number path, whose threshold is
+    0 when fewer cells than requested have a positive indicator."""
+    assert sx.refine_fixed_number(np.zeros(8, np.float32), 0.5).sum() == 0  # all zero: no flags
+    # the zero threshold becomes the smallest positive indicator: zero cells stay unflagged
+    z = np.array([0.5, 0, 0, 0.25, 0, 1.0, 0, 0], np.float32)
+    assert sx.refine_fixed_number(z, 0.75).tolist() == [1, 0, 0, 1, 0, 1, 0, 0]
+    assert refine_mark(z, 0.0)[0].tolist() == [1, 0, 0, 1, 0, 1, 0, 0]
+    # deal.II's scan starts from criteria[0]: with a leading zero the threshold stays 0
+    lead = np.array([0, 0.5, 0.25, 1.0, 0], np.float32)
+    assert sx.refine_fixed_number(lead, 1.0).sum() == 5
+    assert refine_mark(lead, 0.0)[0].sum() == 5
 
 
 @pytest.mark.parametrize("ftype", ["number", "fraction"])

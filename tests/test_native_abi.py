@@ -46,6 +46,19 @@ def test_newton_kat():
     assert abs(x[0] - gold[0]) < 1e-5 and abs(x[1] - gold[1]) < 1e-12
 
 
+def test_skip_newton_kat():
+    """SkipNewton KAT: the Jacobian of the first iteration is reused by every later one (a chord
+    iteration), which still reaches the printed 1.22474 -1.50000 within 10 iterations."""
+    gold = G["skip_newton_01"]["solution"]
+    x = sx.skip_newton_selftest(1)
+    assert abs(x[0] - gold[0]) < 0.5e-5 and abs(x[1] - gold[1]) < 0.5e-5
+    # the chord iteration is not quadratic: after 10 steps it is still visibly off the root
+    # (Newton reaches it to machine precision), so the template really froze the Jacobian
+    assert 1e-12 < abs(x[0] - np.sqrt(1.5)) < 1e-6
+    xn = sx.newton_selftest()
+    assert abs(xn[0] - np.sqrt(1.5)) < 1e-12
+
+
 def test_hyper_cube_dof_numbering_matches_oracle():
     """bit-exact DoF indexing: the C++ mesh builder (Morton cells) and the oracle's lexicographic
     builder give the same node ids for every cell."""
