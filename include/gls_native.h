@@ -67,6 +67,14 @@ typedef struct {
   int srf;                      /* velocity source = srf (parameters.h:511-515) */
   double omega[3];
   const double *force_q;        /* [n_cells*nq*dim] forcing at quadrature points; NULL = NoForce */
+  /* General (curved / unstructured) cells: MappingQ(map_degree) of FEValues (gls_navier_stokes.cc:
+   * 245-252). 0 = axis-aligned boxes given by cell_x0 / cell_h (the brick fast path). > 0: the
+   * cells' mapping support points, lexicographic on the equidistant (map_degree+1)^dim lattice
+   * (Q1 cells of a MappingQ(k, qmapping_all = false) mesh are passed as their exact Qk embedding).
+   * Jacobians, JxW, the Hessian mapping correction and the quadrature points are derived per
+   * quadrature point at gls_create; cell->measure() (h of tau) from the cell's corner vertices. */
+  int map_degree;
+  const double *cell_support;   /* [n_cells][(map_degree+1)^dim][dim] */
 } gls_mesh_desc;
 
 typedef struct gls_ctx gls_ctx;
@@ -76,6 +84,10 @@ int gls_create(const gls_mesh_desc *desc, gls_ctx **out);
 int gls_destroy(gls_ctx *ctx);
 int gls_set_stream(gls_ctx *ctx, void *hip_stream);
 int gls_n_dofs(const gls_ctx *ctx, int64_t *n_dofs);
+/* Physical quadrature points QGauss(nq1d) of every cell (HOST array [n_cells][nq][dim]): where the
+ * caller evaluates forcing (gls_set_force) and analytical functions; the mapped points for
+ * general cells. */
+int gls_quadrature_points(const gls_ctx *ctx, double *xq);
 /* 1 when the context runs the sum-factorized brick kernels (3D Qk-Qk on Morton 2x2x2 bricks),
  * 0 for the general per-cell kernels. GLS_DISABLE_BRICK=1 in the environment forces 0. */
 int gls_uses_brick_kernels(const gls_ctx *ctx);
@@ -333,6 +345,56 @@ int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_
  * ([velocity node-major | pressure]), fine in the refined mesh's numbering. HOST arrays. */
 int gls_mesh_refined_interpolate(const gls_refined_mesh *mesh, int n, double lo, double hi, const double *coarse,
                                  double *fine);
+
+/* ------------------------------------------------------------------------------------------
+ * Unstructured quadrilateral / hexahedral meshes, host side.
+ * gls_umesh_generate: GridGenerator::generate_from_name_and_arguments (source/core/grids.cc:30-36)
+ *   for hyper_cube ("lo : hi : colorize"), hyper_rectangle ("p1 : p2 : colorize"),
+ *   subdivided_hyper_rectangle ("n1,n2[,n3] : p1 : p2 : colorize"), hyper_shell (2D,
+ *   "center : inner : outer : n_cells : colorize"; inner boundary 0, outer 1; SphericalManifold on
+ *   every object), cylinder (3D, "radius : half_length"; axis x, hull 0, x = -L 1, x = +L 2;
+ *   CylindricalManifold on the hull) and cylinder_shell (3D, "length : inner : outer : n_radial :
+ *   n_axial"; axis z, builder-defined colouring inner 0, outer 1, z = 0 2, z = length 3;
+ *   CylindricalManifold on every object).
+ * gls_umesh_read_gmsh: GridIn::read_msh (grids.cc:21-28), ASCII 2.2 / 4.0 / 4.1; quads (2D) or
+ *   hexes (3D); boundary id = physical tag of the boundary element (the entity tag when none).
+ * gls_umesh_set_manifold / gls_umesh_boundary_manifold: set_manifold + set_all_manifold_ids_on_
+ *   boundary (source/core/manifolds.cc:226-247); type 0 flat, 1 spherical(center), 2 cylindrical
+ *   (axis through center).
+ * gls_umesh_refine_global: refine_global with deal.II 9.2's new-vertex placement (line midpoints
+ *   on the line's manifold, quad / hex centres by transfinite-interpolation weights); cells stay
+ *   parent-major (children of cell c are 2^dim c + lexicographic child index).
+ * gls_umesh_fe_space: FE_Q(k)^dim x FE_Q(kp) nodes (1 <= kp <= k <= 2), MappingQ(k, qmapping_all)
+ *   support points per cell, node support points, boundary-id bits per node (bit b: the node lies
+ *   on a boundary face with id b), cell->measure(); periodic pairs (id_a, id_b, direction) triples
+ *   identify the nodes of id_b with their translates on id_a (make_periodicity_constraints).
+ * gls_fe_space_transfer: SolutionTransfer::interpolate across one global refinement (HOST vectors).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct gls_umesh gls_umesh;
+typedef struct {
+  int dim, k, kp;
+  int64_t n_cells, n_vnodes, n_pnodes;
+  const int32_t *cell_vnodes, *cell_pnodes;   /* [n_cells][(k+1)^dim], [n_cells][(kp+1)^dim] lexicographic */
+  const double *vnode_x, *pnode_x;            /* [n][dim] support points (mapped) */
+  const uint32_t *vnode_bid, *pnode_bid;      /* boundary-id bits per node */
+  const double *cell_support;                 /* [n_cells][(k+1)^dim][dim]: gls_mesh_desc.cell_support, map_degree = k */
+  const int32_t *cell_mapping;                /* mapping degree used per cell (1 or k) */
+  const double *cell_measure;                 /* cell->measure() */
+  double volume;                              /* GridTools::volume (sum of measures) */
+  void *impl_;
+} gls_fe_space;
+int gls_umesh_generate(int dim, const char *grid_type, const char *grid_arguments, gls_umesh **out);
+int gls_umesh_read_gmsh(int dim, const char *path, gls_umesh **out);
+int gls_umesh_set_manifold(gls_umesh *mesh, int manifold_id, int type, const double *center, const double *axis);
+int gls_umesh_boundary_manifold(gls_umesh *mesh, int boundary_id, int manifold_id);
+int gls_umesh_refine_global(gls_umesh *mesh, int times);
+int gls_umesh_info(const gls_umesh *mesh, int64_t *n_cells, int64_t *n_vertices, double *volume);
+void gls_umesh_destroy(gls_umesh *mesh);
+int gls_umesh_fe_space(const gls_umesh *mesh, int k, int kp, int qmapping_all, int n_periodic,
+                       const int32_t *periodic, gls_fe_space **out);
+int gls_fe_space_destroy(gls_fe_space *space);
+int gls_fe_space_transfer(const gls_fe_space *coarse, const gls_fe_space *fine, const double *coarse_vec,
+                          double *fine_vec);
 
 /* ------------------------------------------------------------------------------------------
  * Drop-in I/O surface, host side.

@@ -187,10 +187,101 @@ int gls_oracle_cell_dofs(const gls_oracle_problem *p, int cell, int *dofs) {
   return dim * nv + np;
 }
 
+/* MappingQ(md) at reference point xi of one cell: x, J[i][a] = dx_i/dxi_a, Hx[k][a][b] */
+static void map_eval(const gls_oracle_problem *p, int cell, const double *xi, double *x, double J[3][3],
+                     double Hx[3][3][3]) {
+  const int dim = p->dim, md = p->map_degree, m1 = md + 1, ns = ipow(m1, dim);
+  double xn[4];
+  for (int i = 0; i <= md; ++i) xn[i] = (double)i / md;
+  const double *S = p->cell_support + (size_t)cell * ns * dim;
+  for (int i = 0; i < 3; ++i) {
+    x[i] = 0.;
+    for (int a = 0; a < 3; ++a) {
+      J[i][a] = 0.;
+      for (int b = 0; b < 3; ++b) Hx[i][a][b] = 0.;
+    }
+  }
+  for (int s = 0; s < ns; ++s) {
+    const int si[3] = {s % m1, (s / m1) % m1, s / (m1 * m1)};
+    double L[3], dL[3], ddL[3];
+    for (int d = 0; d < dim; ++d) {
+      L[d] = lag(md, xn, si[d], xi[d]);
+      dL[d] = lag_d(md, xn, si[d], xi[d]);
+      ddL[d] = lag_dd(md, xn, si[d], xi[d]);
+    }
+    for (int i = 0; i < dim; ++i) {
+      const double X = S[s * dim + i];
+      double v = X;
+      for (int d = 0; d < dim; ++d) v *= L[d];
+      x[i] += v;
+      for (int a = 0; a < dim; ++a) {
+        double g = X;
+        for (int d = 0; d < dim; ++d) g *= d == a ? dL[d] : L[d];
+        J[i][a] += g;
+        for (int b = 0; b < dim; ++b) {
+          double h = X;
+          for (int d = 0; d < dim; ++d) h *= (d == a && d == b) ? ddL[d] : ((d == a || d == b) ? dL[d] : L[d]);
+          Hx[i][a][b] += h;
+        }
+      }
+    }
+  }
+}
+
+/* deal.II cell->measure(): exact volume of the multilinear cell through its corner vertices */
+static double cell_measure(const gls_oracle_problem *p, int cell) {
+  const int dim = p->dim;
+  if (!p->map_degree) {
+    double m = 1.;
+    for (int d = 0; d < dim; ++d) m *= p->cell_h[cell * dim + d];
+    return m;
+  }
+  const int md = p->map_degree, m1 = md + 1, ns = ipow(m1, dim);
+  const double *S = p->cell_support + (size_t)cell * ns * dim;
+  /* corner vertices -> Q1 map, integrated with the 2-point Gauss rule (exact) */
+  double V[8][3];
+  for (int v = 0; v < (1 << dim); ++v) {
+    int s = 0, st = 1;
+    for (int d = 0; d < dim; ++d) { s += ((v >> d) & 1) * md * st; st *= m1; }
+    for (int i = 0; i < dim; ++i) V[v][i] = S[s * dim + i];
+  }
+  double xg[2], wg[2];
+  gauss_1d(2, xg, wg);
+  double vol = 0.;
+  for (int q = 0; q < (1 << dim); ++q) {
+    double xi[3] = {xg[q & 1], xg[(q >> 1) & 1], xg[(q >> 2) & 1]}, w = 1.;
+    for (int d = 0; d < dim; ++d) w *= wg[(q >> d) & 1];
+    double J[3][3] = {{0}};
+    for (int v = 0; v < (1 << dim); ++v)
+      for (int a = 0; a < dim; ++a) {
+        double g = ((v >> a) & 1) ? 1. : -1.;
+        for (int d = 0; d < dim; ++d)
+          if (d != a) g *= ((v >> d) & 1) ? xi[d] : 1. - xi[d];
+        for (int i = 0; i < dim; ++i) J[i][a] += g * V[v][i];
+      }
+    const double det = dim == 2 ? J[0][0] * J[1][1] - J[0][1] * J[1][0]
+                                : J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) -
+                                      J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                                      J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+    vol += w * det;
+  }
+  return vol;
+}
+
 int gls_oracle_qpoints(const gls_oracle_problem *p, int nq1d, int cell, double *out) {
   double xq[MAXN], wq[MAXN];
   gauss_1d(nq1d, xq, wq);
   const int dim = p->dim, nq = ipow(nq1d, dim);
+  if (p->map_degree) {
+    for (int q = 0; q < nq; ++q) {
+      int qi[3] = {q % nq1d, (q / nq1d) % nq1d, q / (nq1d * nq1d)};
+      double xi[3] = {0, 0, 0}, x[3], J[3][3], Hx[3][3][3];
+      for (int d = 0; d < dim; ++d) xi[d] = xq[qi[d]];
+      map_eval(p, cell, xi, x, J, Hx);
+      for (int d = 0; d < dim; ++d) out[q * dim + d] = x[d];
+    }
+    return nq;
+  }
   for (int q = 0; q < nq; ++q) {
     int qi[3] = {q % nq1d, (q / nq1d) % nq1d, q / (nq1d * nq1d)};
     for (int d = 0; d < dim; ++d)
@@ -258,6 +349,74 @@ static void tab_free(cell_tab *t) {
   free(t->phi_p); free(t->grad_p); free(t->JxW); free(t->xq);
 }
 
+/* scalar Qk shape function on the reference cell: value, gradient, Hessian (d/dxi) */
+static void shape_ref(int dim, int k, const double *xn, int a, const double *xi, double *val, double g[3],
+                      double H[3][3]) {
+  int ai[3] = {a % (k + 1), (a / (k + 1)) % (k + 1), a / ((k + 1) * (k + 1))};
+  double L[3], dL[3], ddL[3];
+  for (int d = 0; d < dim; ++d) {
+    L[d] = lag(k, xn, ai[d], xi[d]);
+    dL[d] = lag_d(k, xn, ai[d], xi[d]);
+    ddL[d] = lag_dd(k, xn, ai[d], xi[d]);
+  }
+  double v = 1.;
+  for (int d = 0; d < dim; ++d) v *= L[d];
+  *val = v;
+  for (int e = 0; e < dim; ++e) {
+    g[e] = 1.;
+    for (int d = 0; d < dim; ++d) g[e] *= d == e ? dL[d] : L[d];
+    for (int f = 0; f < dim; ++f) {
+      H[e][f] = 1.;
+      for (int d = 0; d < dim; ++d) H[e][f] *= (d == e && d == f) ? ddL[d] : ((d == e || d == f) ? dL[d] : L[d]);
+    }
+  }
+}
+
+static void invert(int dim, double J[3][3], double Ji[3][3], double *det) {
+  if (dim == 2) {
+    *det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    Ji[0][0] = J[1][1] / *det; Ji[0][1] = -J[0][1] / *det;
+    Ji[1][0] = -J[1][0] / *det; Ji[1][1] = J[0][0] / *det;
+    return;
+  }
+  *det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+         J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+  Ji[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / *det;
+  Ji[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / *det;
+  Ji[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / *det;
+  Ji[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / *det;
+  Ji[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / *det;
+  Ji[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / *det;
+  Ji[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / *det;
+  Ji[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / *det;
+  Ji[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / *det;
+}
+
+/* mapped scalar shape function: physical gradient and Laplacian (trace of the pushed-forward Hessian) */
+static void shape_mapped(int dim, int k, const double *xn, int a, const double *xi, double Ji[3][3],
+                         double Hx[3][3][3], double *val, double *grad, double *lap) {
+  double g[3], H[3][3];
+  shape_ref(dim, k, xn, a, xi, val, g, H);
+  for (int i = 0; i < dim; ++i) {  /* grad_i = sum_a dxi_a/dx_i g_a, Ji[a][i] = dxi_a/dx_i (J^-1 = Ji) */
+    grad[i] = 0.;
+    for (int e = 0; e < dim; ++e) grad[i] += Ji[e][i] * g[e];
+  }
+  double Hc[3][3];  /* H_ref - sum_k grad_k d2x_k */
+  for (int e = 0; e < dim; ++e)
+    for (int f = 0; f < dim; ++f) {
+      Hc[e][f] = H[e][f];
+      for (int kk = 0; kk < dim; ++kk) Hc[e][f] -= grad[kk] * Hx[kk][e][f];
+    }
+  double lp = 0.;
+  for (int i = 0; i < dim; ++i) {
+    double hii = 0.;
+    for (int e = 0; e < dim; ++e)
+      for (int f = 0; f < dim; ++f) hii += Ji[e][i] * Hc[e][f] * Ji[f][i];
+    lp += hii;
+  }
+  *lap = lp;
+}
+
 /* fe_values.reinit(cell) + the per-q shape tabulation of gls_navier_stokes.cc:412-423 */
 static void tab_fill(cell_tab *t, const gls_oracle_problem *p, int cell) {
   const int dim = p->dim, nq1 = p->nq1d;
@@ -273,8 +432,17 @@ static void tab_fill(cell_tab *t, const gls_oracle_problem *p, int cell) {
     int qi[3] = {q % nq1, (q / nq1) % nq1, q / (nq1 * nq1)};
     double xi[3] = {0, 0, 0}, w = 1.;
     for (int d = 0; d < dim; ++d) { xi[d] = xq1[qi[d]]; w *= wq1[qi[d]]; }
-    t->JxW[q] = w * meas;
-    for (int d = 0; d < dim; ++d) t->xq[q * 3 + d] = x0[d] + h[d] * xi[d];
+    double Ji[3][3] = {{0}}, Hx[3][3][3];
+    if (p->map_degree) {
+      double x[3], J[3][3], det;
+      map_eval(p, cell, xi, x, J, Hx);
+      invert(dim, J, Ji, &det);
+      t->JxW[q] = w * det;
+      for (int d = 0; d < dim; ++d) t->xq[q * 3 + d] = x[d];
+    } else {
+      t->JxW[q] = w * meas;
+      for (int d = 0; d < dim; ++d) t->xq[q * 3 + d] = x0[d] + h[d] * xi[d];
+    }
     for (int kk = 0; kk < t->nd; ++kk) {
       size_t o = (size_t)q * t->nd + kk;
       for (int d = 0; d < 3; ++d) { t->phi_u[o * 3 + d] = 0.; t->lap_u[o * 3 + d] = 0.; t->grad_p[o * 3 + d] = 0.; }
@@ -284,14 +452,16 @@ static void tab_fill(cell_tab *t, const gls_oracle_problem *p, int cell) {
       double val, grad[3], lap;
       if (kk < dim * t->nv) {
         int a = kk / dim, c = kk % dim;
-        shape_eval(dim, p->k, xnv, a, xi, h, &val, grad, &lap);
+        if (p->map_degree) shape_mapped(dim, p->k, xnv, a, xi, Ji, Hx, &val, grad, &lap);
+        else shape_eval(dim, p->k, xnv, a, xi, h, &val, grad, &lap);
         t->phi_u[o * 3 + c] = val;
         for (int e = 0; e < dim; ++e) t->grad_u[o * 9 + c * 3 + e] = grad[e];
         t->lap_u[o * 3 + c] = lap;
         t->div_u[o] = grad[c];
       } else {
         int a = kk - dim * t->nv;
-        shape_eval(dim, p->kp, xnp, a, xi, h, &val, grad, &lap);
+        if (p->map_degree) shape_mapped(dim, p->kp, xnp, a, xi, Ji, Hx, &val, grad, &lap);
+        else shape_eval(dim, p->kp, xnp, a, xi, h, &val, grad, &lap);
         t->phi_p[o] = val;
         for (int e = 0; e < dim; ++e) t->grad_p[o * 3 + e] = grad[e];
       }
@@ -322,9 +492,8 @@ static void local_system(const gls_oracle_problem *p, cell_tab *t, int cell,
   double omega[3] = {p->omega[0], p->omega[1], dim == 3 ? p->omega[2] : 0.};
   const double omega_z = p->omega[2];
 
-  /* element size, :340-345 */
-  double meas = 1.;
-  for (int d = 0; d < dim; ++d) meas *= p->cell_h[cell * dim + d];
+  /* element size, :340-345 (cell->measure(): Q1 volume through the vertices) */
+  const double meas = cell_measure(p, cell);
   double h = dim == 2 ? sqrt(4. * meas / M_PI) / p->k : pow(6 * meas / M_PI, 1. / 3.) / p->k;
 
   if (Ke) memset(Ke, 0, sizeof(double) * nd * nd);
@@ -733,9 +902,7 @@ int gls_oracle_l2_error(const gls_oracle_problem *p, int nq1d_err, const double 
       p_int += pq * t.JxW[q];
       pex_int += exact_q[((size_t)c * nq + q) * (dim + 1) + dim] * t.JxW[q];
     }
-    double m = 1.;
-    for (int d = 0; d < dim; ++d) m *= p->cell_h[c * dim + d];
-    vol += m;
+    vol += cell_measure(p, c);  /* GridTools::volume(triangulation): the Q1 volume */
   }
   const double pavg = p_int / vol, pexavg = pex_int / vol;
   double eu = 0., ep = 0.;

@@ -61,6 +61,14 @@ typedef struct {
   const int *hang_off;
   const int *hang_master;
   const double *hang_w;
+  /* mapped (curved / unstructured) cells: MappingQ(map_degree) with support points
+   * cell_support[n_cells][(map_degree+1)^dim][dim] (lexicographic, equidistant); 0 = the
+   * axis-aligned boxes cell_x0 / cell_h. FEValues restated per quadrature point: J, J^-1, JxW,
+   * physical gradients J^-T grad_ref and Hessians J^-T (H_ref - sum_k (grad phi)_k H_ref(x_k)) J^-1
+   * (deal.II update_hessians on MappingQ, gls_navier_stokes.cc:245-252); h from the Q1 measure of
+   * the cell's corner vertices (cell->measure(), :340-345). */
+  int map_degree;
+  const double *cell_support;
 } gls_oracle_problem;
 
 int gls_oracle_n_dofs(const gls_oracle_problem *p);

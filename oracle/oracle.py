@@ -46,6 +46,7 @@ class _Problem(C.Structure):
         ("viscosity", C.c_double), ("scheme", C.c_int), ("time_steps", C.c_double * 4),
         ("force_q", C.POINTER(C.c_double)), ("srf", C.c_int), ("omega", C.c_double * 3),
         ("hang_off", C.POINTER(C.c_int)), ("hang_master", C.POINTER(C.c_int)), ("hang_w", C.POINTER(C.c_double)),
+        ("map_degree", C.c_int), ("cell_support", C.POINTER(C.c_double)),
     ]
 
 
@@ -304,9 +305,47 @@ class StructuredProblem:
             P.hang_off = self.hang[0].ctypes.data_as(C.POINTER(C.c_int))
             P.hang_master = self.hang[1].ctypes.data_as(C.POINTER(C.c_int))
             P.hang_w = _dp(self.hang[2])
+        sup = getattr(self, "cell_support", None)
+        if sup is not None:
+            P.map_degree = self.map_degree
+            P.cell_support = _dp(sup)
         self._keep = (self.cell_x0, self.cell_h, self.cell_vnodes, self.cell_pnodes, self.constrained,
-                      self.force_q, self.hang)
+                      self.force_q, self.hang, sup)
         return P
+
+
+class MappedProblem(StructuredProblem):
+    """A problem on mapped (curved / unstructured) cells: the node maps, support points, boundary-id
+    bits and MappingQ support points of a mesh description (the product's gls_umesh_fe_space
+    arrays, i.e. the mesh itself — GridGenerator / GridIn / refine_global — is shared input, like
+    the hyper_cube numbering); the oracle restates FEValues on it (gls_oracle.c tab_fill)."""
+
+    def __init__(self, space, viscosity=1.0, scheme="steady", time_steps=(1.0, 1.0, 1.0, 1.0), srf=False,
+                 omega=(0, 0, 0)):
+        dim, k, kp = space["dim"], space["k"], space["kp"]
+        super().__init__(dim, 1, k=k, kp=kp, viscosity=viscosity, scheme=scheme, time_steps=time_steps, srf=srf,
+                         omega=omega)
+        nc = int(space["n_cells"])
+        self.cell_x0 = np.zeros((nc, dim))
+        self.cell_h = np.ones((nc, dim))
+        self.cell_vnodes = np.ascontiguousarray(space["cell_vnodes"], dtype=np.int32)
+        self.cell_pnodes = np.ascontiguousarray(space["cell_pnodes"], dtype=np.int32)
+        self.n_vnodes, self.n_pnodes = int(space["n_vnodes"]), int(space["n_pnodes"])
+        self.n_dofs = dim * self.n_vnodes + self.n_pnodes
+        self.constrained = np.zeros(self.n_dofs, dtype=np.uint8)
+        self._vx = np.ascontiguousarray(space["vnode_x"], dtype=np.float64)
+        self.vnode_bid = np.asarray(space["vnode_bid"], dtype=np.uint32)
+        self.map_degree = k
+        self.cell_support = np.ascontiguousarray(space["cell_support"], dtype=np.float64)
+        self.volume = float(space["volume"])
+
+    def boundary_ids_of_vnodes(self):
+        return [set(b for b in range(32) if (int(m) >> b) & 1) for m in self.vnode_bid]
+
+    def set_dirichlet(self, bcs):
+        if any(t == "slip" for t, _, _ in bcs):
+            raise ValueError("slip on mapped cells (curved normals) is not restated")
+        return super().set_dirichlet(bcs)
 
 
 class Oracle:
@@ -621,7 +660,8 @@ def muparser_to_numpy(expr: str, constants=None):
     (components separated by ';') to a numpy callable f(X[m,dim]) -> (m, ncomp)."""
     comps = [c.strip() for c in expr.split(";")]
     ns = {"sin": np.sin, "cos": np.cos, "tan": np.tan, "exp": np.exp, "log": np.log, "sqrt": np.sqrt,
-          "abs": np.abs, "pi": math.pi, "atan": np.arctan, "tanh": np.tanh, "sinh": np.sinh, "cosh": np.cosh}
+          "abs": np.abs, "pi": math.pi, "atan": np.arctan, "tanh": np.tanh, "sinh": np.sinh, "cosh": np.cosh,
+          "atan2": np.arctan2, "ln": np.log, "log10": np.log10, "asin": np.arcsin, "acos": np.arccos}
     if constants:
         ns.update(constants)
     codes = [compile(c.replace("^", "**"), "<muparser>", "eval") for c in comps]

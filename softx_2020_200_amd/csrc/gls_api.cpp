@@ -271,6 +271,9 @@ struct gls_ctx {
   DevBuf<int32_t> cell_vnodes, cell_pnodes;
   DevBuf<int32_t> face_nbr;  // [n_cells][2 dim] face neighbours (Kelly), built on first use
   DevBuf<double> geo, x0, force_q;
+  DevBuf<double> gq;               // mapped cells: per-q geometry [n_cells][nq][kGeo] (nullptr: boxes)
+  std::vector<double> host_x0, host_h, host_support;  // host geometry for gls_quadrature_points
+  int map_degree = 0;
   DevBuf<uint8_t> vmask;
   DevBuf<int64_t> con_dofs;  // zero_constraints DoF list
   DevBuf<int64_t> dir_dofs;  // nonzero_constraints (Dirichlet) list
@@ -538,6 +541,121 @@ double *brick_slab(gls_ctx *c) {
   return c->slab.p;
 }
 
+// MappingQ(md) on one cell at the QGauss(nq1d) points: x_q, JxW, J^-1, G = J^-1 J^-T and the
+// Hessian correction c_k = sum_ab G_ab d2x_k/dxi_a dxi_b (kGeo layout, gls_common.hpp); support
+// points S[(md+1)^dim][dim] on the equidistant lattice (Gauss-Lobatto for md <= 2)
+void mapped_geometry(int dim, int md, int nq1d, const double *S, double *out) {
+  double xq[gls::kMaxQ1D], wq[gls::kMaxQ1D];
+  gauss_points(nq1d, xq, wq);
+  const int m1 = md + 1, ns = gls::ipow(m1, dim), nq = gls::ipow(nq1d, dim);
+  double xn[4];
+  for (int i = 0; i <= md; ++i) xn[i] = (double)i / md;
+  double L[gls::kMaxQ1D][4], dL[gls::kMaxQ1D][4], ddL[gls::kMaxQ1D][4];
+  for (int q = 0; q < nq1d; ++q)
+    for (int a = 0; a <= md; ++a) lagrange_1d(md, xn, a, xq[q], L[q][a], dL[q][a], ddL[q][a]);
+  for (int q = 0; q < nq; ++q) {
+    const int qi[3] = {q % nq1d, (q / nq1d) % nq1d, dim == 3 ? q / (nq1d * nq1d) : 0};
+    double x[3] = {0, 0, 0}, J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    double H[3][3][3] = {};
+    for (int b = 0; b < ns; ++b) {
+      const int ib[3] = {b % m1, (b / m1) % m1, dim == 3 ? b / (m1 * m1) : 0};
+      double v[3], dv[3], ddv[3];
+      for (int d = 0; d < 3; ++d) {
+        v[d] = d < dim ? L[qi[d]][ib[d]] : 1.0;
+        dv[d] = d < dim ? dL[qi[d]][ib[d]] : 0.0;
+        ddv[d] = d < dim ? ddL[qi[d]][ib[d]] : 0.0;
+      }
+      const double N = v[0] * v[1] * v[2];
+      double g[3], h[3][3];
+      for (int a = 0; a < dim; ++a) {
+        g[a] = 1.0;
+        for (int d = 0; d < dim; ++d) g[a] *= d == a ? dv[d] : v[d];
+        for (int a2 = 0; a2 < dim; ++a2) {
+          h[a][a2] = 1.0;
+          for (int d = 0; d < dim; ++d) h[a][a2] *= (d == a && d == a2) ? ddv[d] : ((d == a || d == a2) ? dv[d] : v[d]);
+        }
+      }
+      for (int i = 0; i < dim; ++i) {
+        const double Sb = S[b * dim + i];
+        x[i] += N * Sb;
+        for (int a = 0; a < dim; ++a) {
+          J[i][a] += Sb * g[a];
+          for (int a2 = 0; a2 < dim; ++a2) H[i][a][a2] += Sb * h[a][a2];
+        }
+      }
+    }
+    double det, JI[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    if (dim == 2) {
+      det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+      JI[0][0] = J[1][1] / det;
+      JI[0][1] = -J[0][1] / det;
+      JI[1][0] = -J[1][0] / det;
+      JI[1][1] = J[0][0] / det;
+    } else {
+      det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+            J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+      for (int a = 0; a < 3; ++a)
+        for (int i = 0; i < 3; ++i) {  // inverse = adjugate / det: JI[a][i] = cof(J)[i][a] / det
+          const int r0 = (i + 1) % 3, r1 = (i + 2) % 3, c0 = (a + 1) % 3, c1 = (a + 2) % 3;
+          JI[a][i] = (J[r0][c0] * J[r1][c1] - J[r0][c1] * J[r1][c0]) / det;
+        }
+    }
+    double G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int a = 0; a < dim; ++a)
+      for (int b = 0; b < dim; ++b)
+        for (int i = 0; i < dim; ++i) G[a][b] += JI[a][i] * JI[b][i];
+    double *o = out + (size_t)q * gls::kGeo;
+    for (int i = 0; i < gls::kGeo; ++i) o[i] = 0.0;
+    double w = 1.0;
+    for (int d = 0; d < dim; ++d) w *= wq[qi[d]];
+    for (int i = 0; i < dim; ++i) o[gls::kGeoX + i] = x[i];
+    o[gls::kGeoJxW] = w * det;
+    for (int a = 0; a < dim; ++a)
+      for (int i = 0; i < dim; ++i) o[gls::kGeoJI + 3 * a + i] = JI[a][i];
+    o[gls::kGeoG + 0] = G[0][0];
+    o[gls::kGeoG + 1] = G[1][1];
+    o[gls::kGeoG + 2] = G[2][2];
+    o[gls::kGeoG + 3] = G[0][1];
+    o[gls::kGeoG + 4] = G[0][2];
+    o[gls::kGeoG + 5] = G[1][2];
+    for (int k = 0; k < dim; ++k) {
+      double cs = 0;
+      for (int a = 0; a < dim; ++a)
+        for (int b = 0; b < dim; ++b) cs += G[a][b] * H[k][a][b];
+      o[gls::kGeoC + k] = cs;
+    }
+  }
+}
+
+// cell->measure() of a mapped cell from its corner support points (exact bilinear / trilinear
+// volume: 2-point Gauss of the multilinear det J)
+double corner_measure(int dim, int md, const double *S) {
+  const int m1 = md + 1;
+  double X[8][3] = {};
+  for (int v = 0; v < (1 << dim); ++v) {
+    const int b = (v & 1) * md + m1 * (((v >> 1) & 1) * md + (dim == 3 ? m1 * (((v >> 2) & 1) * md) : 0));
+    for (int i = 0; i < dim; ++i) X[v][i] = S[b * dim + i];
+  }
+  const double g = 0.5 / std::sqrt(3.0), xs[2] = {0.5 - g, 0.5 + g};
+  double vol = 0;
+  for (int q = 0; q < (1 << dim); ++q) {
+    const double xi[3] = {xs[q & 1], xs[(q >> 1) & 1], xs[(q >> 2) & 1]};
+    double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int v = 0; v < (1 << dim); ++v)
+      for (int a = 0; a < dim; ++a) {
+        double gr = ((v >> a) & 1) ? 1.0 : -1.0;
+        for (int b = 0; b < dim; ++b)
+          if (b != a) gr *= ((v >> b) & 1) ? xi[b] : 1 - xi[b];
+        for (int i = 0; i < dim; ++i) J[i][a] += gr * X[v][i];
+      }
+    vol += (dim == 2 ? J[0][0] * J[1][1] - J[0][1] * J[1][0]
+                     : J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                           J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0])) /
+           (1 << dim);
+  }
+  return vol;
+}
+
 int check_ctx(gls_ctx *c) {
   if (!c) return set_err(GLS_EINVAL, "null context");
   return GLS_OK;
@@ -555,6 +673,7 @@ gls::OpParams make_params(gls_ctx *c, bool jac = false) {
   P.cell_pnodes = c->cell_pnodes.p;
   P.geo = c->geo.p;
   P.x0 = c->x0.p;
+  P.gq = c->gq.p;
   P.force_q = c->force_q.p;
   P.vmask = c->vmask.p;
   P.u = c->u;
@@ -756,10 +875,13 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
   if (d->dim != 2 && d->dim != 3) return set_err(GLS_EINVAL, "dim must be 2 or 3");
   if (!gls::cell_kernel_supported(d->dim, d->k, d->kp, nq1d))
     return set_err(GLS_EINVAL, "unsupported element Q%d-Q%d (dim %d, QGauss %d)", d->k, d->kp, d->dim, nq1d);
-  if (d->n_cells < 0 || d->n_vnodes <= 0 || d->n_pnodes <= 0 || !d->cell_vnodes || !d->cell_h)
+  const bool mapped = d->map_degree > 0;
+  if (d->n_cells < 0 || d->n_vnodes <= 0 || d->n_pnodes <= 0 || !d->cell_vnodes || (!mapped && !d->cell_h))
     return set_err(GLS_EINVAL, "incomplete mesh description");
+  if (mapped && (d->map_degree > 2 || !d->cell_support))
+    return set_err(GLS_EINVAL, "mapped cells: map_degree 1 or 2 with cell_support");
   if (d->kp != d->k && !d->cell_pnodes) return set_err(GLS_EINVAL, "cell_pnodes required when kp != k");
-  if (d->srf && !d->cell_x0) return set_err(GLS_EINVAL, "srf requires cell_x0");
+  if (d->srf && !d->cell_x0 && !mapped) return set_err(GLS_EINVAL, "srf requires cell_x0");
   std::unique_ptr<gls_ctx> c(new gls_ctx);
   c->dim = d->dim;
   c->k = d->k;
@@ -784,22 +906,45 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
   if (!d->cell_pnodes && d->n_pnodes != d->n_vnodes) return set_err(GLS_EINVAL, "n_pnodes != n_vnodes without cell_pnodes");
 
   GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
-  c->use_brick = detect_bricks(d, nq1d);
+  c->use_brick = !mapped && detect_bricks(d, nq1d);
   if (c->use_brick && !std::getenv("GLS_BRICK_ATOMICS")) GLS_TRY(build_slab_map(c.get(), d));
   if (const char *e = std::getenv("GLS_JV_RECOMPUTE")) c->use_qdata = std::atoi(e) == 0;
   if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
   std::vector<double> geo((size_t)d->n_cells * 4);
+  const int nsup = mapped ? gls::ipow(d->map_degree + 1, d->dim) : 0;
   for (int cix = 0; cix < d->n_cells; ++cix) {
     double meas = 1.;
-    for (int e = 0; e < d->dim; ++e) {
-      geo[cix * 4 + e] = d->cell_h[(size_t)cix * d->dim + e];
-      meas *= geo[cix * 4 + e];
+    if (mapped) {
+      meas = corner_measure(d->dim, d->map_degree, d->cell_support + (size_t)cix * nsup * d->dim);
+      if (!(meas > 0)) return set_err(GLS_EINVAL, "cell %d: non-positive measure (inverted cell)", cix);
+      geo[cix * 4 + 0] = geo[cix * 4 + 1] = geo[cix * 4 + 2] = 1.0;
+    } else {
+      for (int e = 0; e < d->dim; ++e) {
+        geo[cix * 4 + e] = d->cell_h[(size_t)cix * d->dim + e];
+        meas *= geo[cix * 4 + e];
+      }
+      if (d->dim == 2) geo[cix * 4 + 2] = 1.0;
     }
-    if (d->dim == 2) geo[cix * 4 + 2] = 1.0;
     // element size for tau (gls_navier_stokes.cc:340-345)
     geo[cix * 4 + 3] = d->dim == 2 ? std::sqrt(4. * meas / M_PI) / d->k : std::pow(6 * meas / M_PI, 1. / 3.) / d->k;
   }
   GLS_TRY(c->geo.upload(geo.data(), geo.size()));
+  if (mapped) {  // FEValues geometry per quadrature point (MappingQ(map_degree))
+    c->map_degree = d->map_degree;
+    c->host_support.assign(d->cell_support, d->cell_support + (size_t)d->n_cells * nsup * d->dim);
+    std::vector<double> gq((size_t)d->n_cells * c->nq * gls::kGeo);
+    for (int cix = 0; cix < d->n_cells; ++cix) {
+      mapped_geometry(d->dim, d->map_degree, nq1d, d->cell_support + (size_t)cix * nsup * d->dim,
+                      gq.data() + (size_t)cix * c->nq * gls::kGeo);
+      for (int q = 0; q < c->nq; ++q)
+        if (!(gq[((size_t)cix * c->nq + q) * gls::kGeo + gls::kGeoJxW] > 0))
+          return set_err(GLS_EINVAL, "cell %d: non-positive Jacobian at quadrature point %d", cix, q);
+    }
+    GLS_TRY(c->gq.upload(gq.data(), gq.size()));
+  } else {
+    c->host_h.assign(d->cell_h, d->cell_h + (size_t)d->n_cells * d->dim);
+    if (d->cell_x0) c->host_x0.assign(d->cell_x0, d->cell_x0 + (size_t)d->n_cells * d->dim);
+  }
   if (d->cell_x0) {
     std::vector<double> x0((size_t)d->n_cells * 3, 0.);
     for (int cix = 0; cix < d->n_cells; ++cix)
@@ -848,6 +993,30 @@ int gls_set_stream(gls_ctx *c, void *s) {
 }
 
 int gls_uses_brick_kernels(const gls_ctx *c) { return c && c->use_brick ? 1 : 0; }
+
+int gls_quadrature_points(const gls_ctx *c, double *xq) {
+  if (!c || !xq) return set_err(GLS_EINVAL, "null argument");
+  const int dim = c->dim, nq = c->nq;
+  if (c->map_degree > 0) {
+    const int nsup = gls::ipow(c->map_degree + 1, dim);
+    std::vector<double> g((size_t)nq * gls::kGeo);
+    for (int cix = 0; cix < c->n_cells; ++cix) {
+      mapped_geometry(dim, c->map_degree, c->nq1d, c->host_support.data() + (size_t)cix * nsup * dim, g.data());
+      for (int q = 0; q < nq; ++q)
+        for (int e = 0; e < dim; ++e) xq[((size_t)cix * nq + q) * dim + e] = g[(size_t)q * gls::kGeo + gls::kGeoX + e];
+    }
+    return GLS_OK;
+  }
+  if (c->host_x0.empty()) return set_err(GLS_EINVAL, "gls_quadrature_points: the mesh was created without cell_x0");
+  for (int cix = 0; cix < c->n_cells; ++cix)
+    for (int q = 0; q < nq; ++q) {
+      const int qi[3] = {q % c->nq1d, (q / c->nq1d) % c->nq1d, q / (c->nq1d * c->nq1d)};
+      for (int e = 0; e < dim; ++e)
+        xq[((size_t)cix * nq + q) * dim + e] =
+            c->host_x0[(size_t)cix * dim + e] + c->host_h[(size_t)cix * dim + e] * c->tables.xi[qi[e]];
+    }
+  return GLS_OK;
+}
 
 int gls_n_dofs(const gls_ctx *c, int64_t *n) {
   if (!c || !n) return set_err(GLS_EINVAL, "null argument");
@@ -1659,6 +1828,7 @@ int gls_kelly_estimate(gls_ctx *c, const double *sol, int variable, double *eta)
   GLS_TRY(check_ctx(c));
   if (!sol || !eta || (variable != 0 && variable != 1)) return set_err(GLS_EINVAL, "gls_kelly_estimate: bad arguments");
   if (c->hang.on) return set_err(GLS_EINVAL, "gls_kelly_estimate: conforming meshes only (no hanging nodes)");
+  if (c->map_degree > 0) return set_err(GLS_EINVAL, "gls_kelly_estimate: axis-aligned box cells only");
   if (c->nq1d + 1 > gls::kMaxQ1D) return set_err(GLS_EINVAL, "gls_kelly_estimate: face rule too large");
   if (!c->face_nbr.p && c->n_cells > 0) GLS_TRY(build_face_neighbours(c));
   const bool pres = variable == 1;
@@ -1704,6 +1874,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
   if (c->dim != 3 || c->k > 2 || c->k != c->kp) return set_err(GLS_EINVAL, "mg: 3D Q1-Q1 / Q2-Q2 only");
   if (c->hang.on) return set_err(GLS_EINVAL, "mg: not with hanging-node constraints");
+  if (c->map_degree > 0) return set_err(GLS_EINVAL, "mg: nested hyper_cube levels only (not mapped cells)");
   auto &mg = c->mg;
   mg = gls_ctx::MG();
   mg.boxed = c->dist.on;

@@ -14,6 +14,11 @@
 //
 // Modes: residual (assemble_rhs), Jacobian action (matrix-free assembleGLS<true> . v),
 // Jacobian diagonal (for the Jacobi preconditioner and the deal.II constrained-row diagonal).
+// GEN: mapped (curved / unstructured) cells. The contractions stay on the reference cell; the
+// per-q geometry (P.gq: J^-1, JxW, G = J^-1 J^-T, the Hessian correction c, x_q) turns reference
+// gradients into physical ones (J^-T), the reference Hessian into the physical Laplacian
+// (sum G_ab H_ab - c . grad), and physical test coefficients back to reference ones (J^-1) —
+// FEValues with MappingQ (gls_navier_stokes.cc:245-252) restated per quadrature point.
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
 
@@ -30,7 +35,7 @@ struct Cfg {
   static constexpr int TABN = 5 * kMaxQ1D * kMaxNodes1D + 2 * kMaxQ1D;
 };
 
-template <int DIM, int K, int KP, int NQ1, int MODE>
+template <int DIM, int K, int KP, int NQ1, int MODE, bool GEN = false>
 __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const Tables1D T) {
   using C = Cfg<DIM, K, KP, NQ1>;
   constexpr int NV = C::NV, NP = C::NP, NQ = C::NQ, CB = C::CB, NT = C::NT;
@@ -100,9 +105,48 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
     const double hst = P.geo[cell * 4 + 3];
     const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
-    const double JxW = tW[qx] * tW[qy] * (DIM == 3 ? tW[qz] : 1.0) * hx * hy * (DIM == 3 ? hz : 1.0);
+    // mapped cells: this q's geometry (J^-1 [a][i], G, c, JxW, x_q)
+    const double *gqq = GEN ? P.gq + ((int64_t)cell * NQ + q) * kGeo : nullptr;
+    double JI[3][3] = {}, Gm[6] = {}, cg[3] = {};
+    if constexpr (GEN) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) JI[a][i] = gqq[kGeoJI + 3 * a + i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Gm[i] = gqq[kGeoG + i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) cg[i] = gqq[kGeoC + i];
+    }
+    const double JxW = GEN ? gqq[kGeoJxW]
+                           : tW[qx] * tW[qy] * (DIM == 3 ? tW[qz] : 1.0) * hx * hy * (DIM == 3 ? hz : 1.0);
     // Laplacian weights relative to x (1 for cubes)
     const double wy = (hx * hx) / (hy * hy), wz = (hx * hx) / (hz * hz);
+    // reference gradient -> physical (J^-T), physical test coefficient -> reference (J^-1)
+    auto to_phys = [&](double (&g)[DIM]) {
+      double o[DIM];
+#pragma unroll
+      for (int i = 0; i < DIM; ++i) {
+        double s = 0.;
+#pragma unroll
+        for (int a = 0; a < DIM; ++a) s += JI[a][i] * g[a];
+        o[i] = s;
+      }
+#pragma unroll
+      for (int i = 0; i < DIM; ++i) g[i] = o[i];
+    };
+    auto to_ref = [&](double (&t)[DIM]) {
+      double o[DIM];
+#pragma unroll
+      for (int a = 0; a < DIM; ++a) {
+        double s = 0.;
+#pragma unroll
+        for (int i = 0; i < DIM; ++i) s += JI[a][i] * t[i];
+        o[a] = s;
+      }
+#pragma unroll
+      for (int a = 0; a < DIM; ++a) t[a] = o[a];
+    };
 
     double u[DIM] = {}, gu[DIM][DIM] = {}, lu[DIM] = {}, pq = 0., gp[DIM] = {};
     double h1[DIM] = {}, h2[DIM] = {}, h3[DIM] = {};
@@ -124,7 +168,11 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
           const int a = ax + C::K1 * (ay + C::K1 * az);
           const double N = vx * vy * vz;
           const double g0 = dx * vy * vz, g1 = vx * dy * vz, g2 = vx * vy * dz;
-          const double L = sx * vy * vz + wy * vx * sy * vz + (DIM == 3 ? wz * vx * vy * sz : 0.0);
+          // box: x-scaled Laplacian; mapped: sum_ab G_ab d2_ref (the -c . grad part comes after)
+          const double L = GEN ? (Gm[0] * sx * vy * vz + Gm[1] * vx * sy * vz + 2 * Gm[3] * dx * dy * vz +
+                                  (DIM == 3 ? Gm[2] * vx * vy * sz + 2 * Gm[4] * dx * vy * dz + 2 * Gm[5] * vx * dy * dz
+                                            : 0.0))
+                               : sx * vy * vz + wy * vx * sy * vz + (DIM == 3 ? wz * vx * vy * sz : 0.0);
           const double gr[3] = {g0, g1, g2};
 #pragma unroll
           for (int c = 0; c < DIM; ++c) {
@@ -176,17 +224,28 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
         }
       }
     }
-    // reference -> physical derivatives (affine box map)
-    const double il2 = ih[0] * ih[0];
+    if constexpr (GEN) {  // reference -> physical derivatives (MappingQ)
 #pragma unroll
-    for (int c = 0; c < DIM; ++c) {
-      lu[c] *= il2;
-      lv[c] *= il2;
+      for (int c = 0; c < DIM; ++c) {
+        to_phys(gu[c]);
+        to_phys(gv[c]);
 #pragma unroll
-      for (int e = 0; e < DIM; ++e) { gu[c][e] *= ih[e]; gv[c][e] *= ih[e]; }
+        for (int k = 0; k < DIM; ++k) { lu[c] -= cg[k] * gu[c][k]; lv[c] -= cg[k] * gv[c][k]; }
+      }
+      to_phys(gp);
+      to_phys(gvp);
+    } else {  // reference -> physical derivatives (affine box map)
+      const double il2 = ih[0] * ih[0];
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        lu[c] *= il2;
+        lv[c] *= il2;
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) { gu[c][e] *= ih[e]; gv[c][e] *= ih[e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < DIM; ++e) { gp[e] *= ih[e]; gvp[e] *= ih[e]; }
     }
-#pragma unroll
-    for (int e = 0; e < DIM; ++e) { gp[e] *= ih[e]; gvp[e] *= ih[e]; }
 
     // ---- pointwise (gls_navier_stokes.cc:391-516)
     const double nu = P.nu;
@@ -213,9 +272,15 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     double om[3] = {P.omega[0], P.omega[1], P.omega[2]};
     if (P.srf) {
       double xq[3];
-      xq[0] = P.x0[cell * 3 + 0] + hx * tXi[qx];
-      xq[1] = P.x0[cell * 3 + 1] + hy * tXi[qy];
-      xq[2] = DIM == 3 ? P.x0[cell * 3 + 2] + hz * tXi[qz] : 0.0;
+      if constexpr (GEN) {
+        xq[0] = gqq[kGeoX];
+        xq[1] = gqq[kGeoX + 1];
+        xq[2] = DIM == 3 ? gqq[kGeoX + 2] : 0.0;
+      } else {
+        xq[0] = P.x0[cell * 3 + 0] + hx * tXi[qx];
+        xq[1] = P.x0[cell * 3 + 1] + hy * tXi[qy];
+        xq[2] = DIM == 3 ? P.x0[cell * 3 + 2] + hz * tXi[qz] : 0.0;
+      }
       if constexpr (DIM == 2) {
         const double wz_ = om[2];
         srf_cor[0] = 2 * wz_ * (-1.) * u[1];
@@ -254,13 +319,22 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
 #pragma unroll
       for (int c = 0; c < DIM; ++c) {
         Tq[c * (DIM + 1)] = JxW * (-Gu[c] + f[c] - Tt[c] - srf_cor[c] - srf_cen[c]);
+        double t[DIM];
 #pragma unroll
-        for (int e = 0; e < DIM; ++e)
-          Tq[c * (DIM + 1) + 1 + e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]) * ih[e];
+        for (int e = 0; e < DIM; ++e) t[e] = JxW * (-nu * gu[c][e] + (c == e ? pq : 0.0) - tau * R[c] * u[e]);
+        if constexpr (GEN) to_ref(t);
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) Tq[c * (DIM + 1) + 1 + e] = GEN ? t[e] : t[e] * ih[e];
       }
       Tq[DIM * (DIM + 1)] = -JxW * divu;
+      {
+        double t[DIM];
 #pragma unroll
-      for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = -JxW * tau * R[e] * ih[e];
+        for (int e = 0; e < DIM; ++e) t[e] = -JxW * tau * R[e];
+        if constexpr (GEN) to_ref(t);
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = GEN ? t[e] : t[e] * ih[e];
+      }
     } else if constexpr (MODE == MODE_JV) {
       const double aj = P.alpha_jac;
       double S[DIM], A[DIM], divv = 0.;
@@ -289,14 +363,22 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
 #pragma unroll
       for (int c = 0; c < DIM; ++c) {
         Tq[c * (DIM + 1)] = JxW * A[c];
+        double t[DIM];
 #pragma unroll
-        for (int e = 0; e < DIM; ++e)
-          Tq[c * (DIM + 1) + 1 + e] =
-              JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]) * ih[e];
+        for (int e = 0; e < DIM; ++e) t[e] = JxW * (nu * gv[c][e] - (c == e ? vp : 0.0) + tau * S[c] * u[e] + tau * R[c] * v[e]);
+        if constexpr (GEN) to_ref(t);
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) Tq[c * (DIM + 1) + 1 + e] = GEN ? t[e] : t[e] * ih[e];
       }
       Tq[DIM * (DIM + 1)] = JxW * divv;
+      {
+        double t[DIM];
 #pragma unroll
-      for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = JxW * tau * S[e] * ih[e];
+        for (int e = 0; e < DIM; ++e) t[e] = JxW * tau * S[e];
+        if constexpr (GEN) to_ref(t);
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) Tq[DIM * (DIM + 1) + 1 + e] = GEN ? t[e] : t[e] * ih[e];
+      }
     } else {  // MODE_DIAG: per-q state for the diagonal
       Tq[0] = JxW;
       Tq[1] = tau;
@@ -346,10 +428,28 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
         const double N = vx * vy * vz;
-        const double g[3] = {tD[qx][ax] * vy * vz * ih[0], vx * tD[qy][ay] * vz * ih[1],
-                             DIM == 3 ? vx * vy * tD[qz][az] * ih[2] : 0.0};
-        const double L = tS[qx][ax] * vy * vz * ih[0] * ih[0] + vx * tS[qy][ay] * vz * ih[1] * ih[1] +
-                         (DIM == 3 ? vx * vy * tS[qz][az] * ih[2] * ih[2] : 0.0);
+        double g[3] = {tD[qx][ax] * vy * vz * ih[0], vx * tD[qy][ay] * vz * ih[1],
+                       DIM == 3 ? vx * vy * tD[qz][az] * ih[2] : 0.0};
+        double L = tS[qx][ax] * vy * vz * ih[0] * ih[0] + vx * tS[qy][ay] * vz * ih[1] * ih[1] +
+                   (DIM == 3 ? vx * vy * tS[qz][az] * ih[2] * ih[2] : 0.0);
+        if constexpr (GEN) {  // physical gradient / Laplacian of the test function on the mapped cell
+          const double *gg = P.gq + ((int64_t)cell * NQ + q) * kGeo;
+          const double dxv = tD[qx][ax], dyv = tD[qy][ay], dzv = DIM == 3 ? tD[qz][az] : 0.0;
+          const double gr[3] = {dxv * vy * vz, vx * dyv * vz, vx * vy * dzv};
+          const double sx = tS[qx][ax], sy = tS[qy][ay], sz = DIM == 3 ? tS[qz][az] : 0.0;
+          L = gg[kGeoG] * sx * vy * vz + gg[kGeoG + 1] * vx * sy * vz + 2 * gg[kGeoG + 3] * dxv * dyv * vz +
+              (DIM == 3 ? gg[kGeoG + 2] * vx * vy * sz + 2 * gg[kGeoG + 4] * dxv * vy * dzv + 2 * gg[kGeoG + 5] * vx * dyv * dzv
+                        : 0.0);
+#pragma unroll
+          for (int i = 0; i < DIM; ++i) {
+            double s = 0.;
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) s += gg[kGeoJI + 3 * a + i] * gr[a];
+            g[i] = s;
+          }
+#pragma unroll
+          for (int i = 0; i < DIM; ++i) L -= gg[kGeoC + i] * g[i];
+        }
         const double *Tq = Tc + q * NT;
         const double JxW = Tq[0], tau = Tq[1];
         double ug = 0., gg = 0.;
@@ -393,8 +493,20 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;
-        const double g0 = tDp[qx][ax] * vy * vz / hx, g1 = vx * tDp[qy][ay] * vz / hy,
-                     g2 = DIM == 3 ? vx * vy * tDp[qz][az] / hz : 0.0;
+        double g0 = tDp[qx][ax] * vy * vz / hx, g1 = vx * tDp[qy][ay] * vz / hy,
+               g2 = DIM == 3 ? vx * vy * tDp[qz][az] / hz : 0.0;
+        if constexpr (GEN) {
+          const double *gg = P.gq + ((int64_t)cell * NQ + q) * kGeo;
+          const double gr[3] = {tDp[qx][ax] * vy * vz, vx * tDp[qy][ay] * vz, DIM == 3 ? vx * vy * tDp[qz][az] : 0.0};
+          double ph[3] = {0., 0., 0.};
+#pragma unroll
+          for (int i = 0; i < DIM; ++i)
+#pragma unroll
+            for (int a = 0; a < DIM; ++a) ph[i] += gg[kGeoJI + 3 * a + i] * gr[a];
+          g0 = ph[0];
+          g1 = ph[1];
+          g2 = ph[2];
+        }
         const double *Tq = Tc + q * NT;
         out += Tq[0] * Tq[1] * (g0 * g0 + g1 * g1 + g2 * g2);
       }
@@ -411,33 +523,38 @@ size_t cell_kernel_lds_bytes() {
   return n * sizeof(double);
 }
 
-template <int DIM, int K, int KP, int NQ1>
-hipError_t launch_cell_t(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
+template <int DIM, int K, int KP, int NQ1, bool GEN>
+hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
   using C = Cfg<DIM, K, KP, NQ1>;
-  if (P.n_cells <= 0) return hipSuccess;
   const int blocks = (P.n_cells + C::CB - 1) / C::CB;
   const size_t lds = cell_kernel_lds_bytes<DIM, K, KP, NQ1>();
   static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL>,
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL, GEN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV>,
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG>,
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG, GEN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
   switch (mode) {
     case MODE_RESIDUAL:
-      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL>), dim3(blocks), dim3(256), lds, s, P, T);
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
       break;
     case MODE_JV:
-      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV>), dim3(blocks), dim3(256), lds, s, P, T);
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
       break;
     default:
-      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG>), dim3(blocks), dim3(256), lds, s, P, T);
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
   }
   return hipGetLastError();
+}
+template <int DIM, int K, int KP, int NQ1>
+hipError_t launch_cell_t(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (P.n_cells <= 0) return hipSuccess;
+  if (P.gq) return launch_cell_g<DIM, K, KP, NQ1, true>(mode, P, T, s);
+  return launch_cell_g<DIM, K, KP, NQ1, false>(mode, P, T, s);
 }
 
 // Supported element families (dim, k, kp) with the reference quadrature QGauss(k+1).

@@ -28,6 +28,13 @@ struct Tables1D {
   double xi[kMaxQ1D];               // Gauss points on [0,1]
 };
 
+// General (mapped) cells: per quadrature point geometry, [n_cells][nq][kGeo] doubles:
+//   x_q (3), JxW, J^-1 [a][i] = d xi_a / d x_i (9, row-major), G = J^-1 J^-T (6: 00 11 22 01 02 12),
+//   c_k = sum_ab G_ab d2 x_k / d xi_a d xi_b (3): grad phi = J^-T grad_ref phi and
+//   lap phi = sum_ab G_ab d2_ref phi - c . grad phi (FEValues hessians on MappingQ cells)
+constexpr int kGeo = 22;
+constexpr int kGeoX = 0, kGeoJxW = 3, kGeoJI = 4, kGeoG = 13, kGeoC = 19;
+
 // Per-launch operator parameters (device pointers).
 struct OpParams {
   int n_cells;
@@ -38,6 +45,7 @@ struct OpParams {
   const int32_t *cell_pnodes; // nullptr -> use cell_vnodes (kp == k)
   const double *geo;          // [n_cells][4]: h_x, h_y, h_z, h_stab
   const double *x0;           // [n_cells][3] (SRF only)
+  const double *gq;           // [n_cells][nq][kGeo] mapped-cell geometry, nullptr = axis-aligned boxes
   const double *force_q;      // [n_cells][nq][dim] or nullptr
   const uint8_t *vmask;       // [n_vnodes] zero_constraints bits, nullptr = none
   const uint8_t *hmask;       // [n_vnodes] hanging velocity components (MODE_DIAG: |K_ii| per cell)

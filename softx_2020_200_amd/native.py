@@ -36,7 +36,10 @@ EXPORTS = [
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
     "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
-    "gls_freeze_jacobian", "gls_skip_newton_selftest",
+    "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
+    "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
+    "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
+    "gls_fe_space_transfer",
 ]
 
 
@@ -53,7 +56,18 @@ class MeshDesc(C.Structure):
         ("vnode_mask", C.POINTER(C.c_uint8)),
         ("viscosity", C.c_double), ("srf", C.c_int), ("omega", C.c_double * 3),
         ("force_q", C.POINTER(C.c_double)),
+        ("map_degree", C.c_int), ("cell_support", C.POINTER(C.c_double)),
     ]
+
+
+class FESpace(C.Structure):
+    _fields_ = [("dim", C.c_int), ("k", C.c_int), ("kp", C.c_int),
+                ("n_cells", C.c_int64), ("n_vnodes", C.c_int64), ("n_pnodes", C.c_int64),
+                ("cell_vnodes", C.POINTER(C.c_int32)), ("cell_pnodes", C.POINTER(C.c_int32)),
+                ("vnode_x", C.POINTER(C.c_double)), ("pnode_x", C.POINTER(C.c_double)),
+                ("vnode_bid", C.POINTER(C.c_uint32)), ("pnode_bid", C.POINTER(C.c_uint32)),
+                ("cell_support", C.POINTER(C.c_double)), ("cell_mapping", C.POINTER(C.c_int32)),
+                ("cell_measure", C.POINTER(C.c_double)), ("volume", C.c_double), ("impl_", C.c_void_p)]
 
 
 class LinearParams(C.Structure):
@@ -148,6 +162,19 @@ def load():
                                 C.POINTER(C.c_int32), C.POINTER(C.c_double)]
     L.gls_mesh_refined_interpolate.argtypes = [C.POINTER(RefinedMesh), C.c_int, C.c_double, C.c_double,
                                                C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.gls_quadrature_points.argtypes = [vp, d]
+    L.gls_umesh_generate.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.POINTER(vp)]
+    L.gls_umesh_read_gmsh.argtypes = [C.c_int, C.c_char_p, C.POINTER(vp)]
+    L.gls_umesh_set_manifold.argtypes = [vp, C.c_int, C.c_int, d, d]
+    L.gls_umesh_boundary_manifold.argtypes = [vp, C.c_int, C.c_int]
+    L.gls_umesh_refine_global.argtypes = [vp, C.c_int]
+    L.gls_umesh_info.argtypes = [vp, C.POINTER(i64), C.POINTER(i64), d]
+    L.gls_umesh_destroy.argtypes = [vp]
+    L.gls_umesh_destroy.restype = None
+    L.gls_umesh_fe_space.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32),
+                                     C.POINTER(C.POINTER(FESpace))]
+    L.gls_fe_space_destroy.argtypes = [C.POINTER(FESpace)]
+    L.gls_fe_space_transfer.argtypes = [C.POINTER(FESpace), C.POINTER(FESpace), d, d]
     _lib = L
     return L
 
@@ -532,3 +559,84 @@ class GLSContext:
         ms, n = C.c_double(), C.c_int64()
         check(self.L.gls_timing_get(self.h, which, C.byref(ms), C.byref(n)), "gls_timing_get")
         return ms.value, n.value
+
+
+# ---------------------------------------------------------------------------------------------
+# unstructured / curved meshes (host side, gls_umesh_* / gls_fe_space_*)
+# ---------------------------------------------------------------------------------------------
+MANIFOLD_TYPES = {"flat": 0, "spherical": 1, "cylindrical": 2}
+
+
+class UMesh:
+    """Owner of a gls_umesh: GridGenerator grids (hyper_cube, hyper_rectangle,
+    subdivided_hyper_rectangle, hyper_shell, cylinder, cylinder_shell) or a gmsh file, manifolds,
+    global refinement. fe_space() discretizes it (numpy arrays, see gls_fe_space)."""
+
+    def __init__(self, dim, grid_type=None, grid_arguments="", gmsh=None):
+        self.L = load()
+        self.dim = dim
+        h = C.c_void_p()
+        if gmsh is not None:
+            check(self.L.gls_umesh_read_gmsh(dim, str(gmsh).encode(), C.byref(h)), "gls_umesh_read_gmsh")
+        else:
+            check(self.L.gls_umesh_generate(dim, grid_type.encode(), grid_arguments.encode(), C.byref(h)),
+                  "gls_umesh_generate")
+        self.h = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.L.gls_umesh_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def set_manifold(self, manifold_id, kind, center=(0.0, 0.0, 0.0), axis=(0.0, 0.0, 1.0)):
+        c = np.ascontiguousarray(list(center) + [0.0] * (3 - len(center)), dtype=np.float64)
+        a = np.ascontiguousarray(list(axis) + [0.0] * (3 - len(axis)), dtype=np.float64)
+        check(self.L.gls_umesh_set_manifold(self.h, int(manifold_id), MANIFOLD_TYPES[kind], _dp(c), _dp(a)),
+              "gls_umesh_set_manifold")
+
+    def boundary_manifold(self, boundary_id, manifold_id):
+        check(self.L.gls_umesh_boundary_manifold(self.h, int(boundary_id), int(manifold_id)),
+              "gls_umesh_boundary_manifold")
+
+    def refine_global(self, times=1):
+        check(self.L.gls_umesh_refine_global(self.h, int(times)), "gls_umesh_refine_global")
+
+    def info(self):
+        nc, nv, vol = C.c_int64(), C.c_int64(), C.c_double()
+        check(self.L.gls_umesh_info(self.h, C.byref(nc), C.byref(nv), C.byref(vol)), "gls_umesh_info")
+        return nc.value, nv.value, vol.value
+
+    def fe_space(self, k, kp=None, qmapping_all=False, periodic=()):
+        """FE_Q(k)^dim x FE_Q(kp) on this mesh -> dict of numpy arrays (gls_umesh_fe_space)."""
+        kp = k if kp is None else kp
+        per = np.ascontiguousarray(np.array(periodic, dtype=np.int32).reshape(-1))
+        pm = C.POINTER(FESpace)()
+        check(self.L.gls_umesh_fe_space(self.h, int(k), int(kp), 1 if qmapping_all else 0, len(per) // 3,
+                                        per.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pm)), "gls_umesh_fe_space")
+        try:
+            return _fe_space_dict(pm.contents)
+        finally:
+            self.L.gls_fe_space_destroy(pm)
+
+
+def _fe_space_dict(m):
+    dim, k, kp = m.dim, m.k, m.kp
+    nc, nv, npn = int(m.n_cells), int(m.n_vnodes), int(m.n_pnodes)
+    nl, npl = (k + 1) ** dim, (kp + 1) ** dim
+
+    def take(ptr, count, dt, shape):
+        return np.ctypeslib.as_array(ptr, shape=(int(count),)).astype(dt, copy=True).reshape(shape)
+
+    return dict(dim=dim, k=k, kp=kp, n_cells=nc, n_vnodes=nv, n_pnodes=npn,
+                cell_vnodes=take(m.cell_vnodes, nc * nl, np.int32, (nc, nl)),
+                cell_pnodes=take(m.cell_pnodes, nc * npl, np.int32, (nc, npl)),
+                vnode_x=take(m.vnode_x, nv * dim, np.float64, (nv, dim)),
+                pnode_x=take(m.pnode_x, npn * dim, np.float64, (npn, dim)),
+                vnode_bid=take(m.vnode_bid, nv, np.uint32, (nv,)),
+                pnode_bid=take(m.pnode_bid, npn, np.uint32, (npn,)),
+                cell_support=take(m.cell_support, nc * nl * dim, np.float64, (nc, nl, dim)),
+                cell_mapping=take(m.cell_mapping, nc, np.int32, (nc,)),
+                cell_measure=take(m.cell_measure, nc, np.float64, (nc,)), volume=float(m.volume))
