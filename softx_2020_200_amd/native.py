@@ -357,7 +357,7 @@ class GLSContext:
 
     def __init__(self, dim, k, kp, cell_vnodes, cell_pnodes, cell_h, n_vnodes, n_pnodes, viscosity=1.0,
                  cell_x0=None, vnode_mask=None, force_q=None, srf=False, omega=(0.0, 0.0, 0.0), nq1d=0,
-                 stream=None):
+                 stream=None, map_degree=0, cell_support=None):
         import torch
         if not torch.cuda.is_available():
             raise GLSError("no HIP device visible: the GLS operators run only on the GPU")
@@ -394,6 +394,9 @@ class GLSContext:
         for i in range(3):
             D.omega[i] = omega[i]
         D.force_q = _dp(fq)
+        if map_degree:  # mapped (curved / unstructured) cells: MappingQ support points per cell
+            D.map_degree = int(map_degree)
+            D.cell_support = _dp(arr(cell_support, np.float64))
         h = C.c_void_p()
         check(self.L.gls_create(C.byref(D), C.byref(h)), "gls_create")
         self.h = h
@@ -408,6 +411,13 @@ class GLSContext:
         self.stream = stream
         check(self.L.gls_set_stream(self.h, C.c_void_p(stream)), "gls_set_stream")
         self._state = None
+        self.nq = (nq1d or (k + 1)) ** dim
+
+    def quadrature_points(self):
+        """physical QGauss points [n_cells, nq, dim] (gls_quadrature_points; mapped for curved cells)"""
+        out = np.zeros((self.n_cells, self.nq, self.dim))
+        check(self.L.gls_quadrature_points(self.h, _dp(out)), "gls_quadrature_points")
+        return out
 
     def close(self):
         if getattr(self, "h", None):

@@ -16,8 +16,12 @@ def vnode_mask_of(p):
 
 def context_for(p, **kw):
     from softx_2020_200_amd import GLSContext
-    ctx = GLSContext(p.dim, p.k, p.kp, p.cell_vnodes, p.cell_pnodes if p.kp != p.k else None, p.cell_h,
-                     p.n_vnodes, p.n_pnodes, viscosity=p.viscosity, cell_x0=p.cell_x0, vnode_mask=vnode_mask_of(p),
+    mapped = getattr(p, "cell_support", None) is not None
+    if mapped:
+        kw = dict(kw, map_degree=p.map_degree, cell_support=p.cell_support)
+    ctx = GLSContext(p.dim, p.k, p.kp, p.cell_vnodes, p.cell_pnodes if p.kp != p.k else None,
+                     None if mapped else p.cell_h, p.n_vnodes, p.n_pnodes, viscosity=p.viscosity,
+                     cell_x0=None if mapped else p.cell_x0, vnode_mask=vnode_mask_of(p),
                      force_q=p.force_q, srf=p.srf, omega=p.omega, **kw)
     ctx.set_time(p.scheme, p.time_steps)
     if getattr(p, "hang_lines", None) is not None:

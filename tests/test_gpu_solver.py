@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from oracle.oracle import Oracle, StructuredProblem, muparser_to_numpy, newton_solve
-from tests.gpu_util import context_for, cuda
+from tests.gpu_util import context_for, cuda, relerr
 
 G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.json")))
 
@@ -262,16 +262,18 @@ def test_frozen_jacobian_operators(k):
         ctx.set_time("bdf1", (0.02, 0.01, 0.01, 0.01))  # the residual's scheme moves, J keeps bdf2
         ctx.set_state(b, h1)
         rb_frozen = ctx.residual().clone()
-        assert torch.equal(ctx.jacobian_apply(v), ja)
-        assert torch.equal(ctx.jacobian_diagonal(), da)
+        # (the Q1 wave kernel sums its brick in LDS atomics: equal up to summation order)
+        same = lambda x, y: relerr(x.cpu().numpy(), y.cpu().numpy()) < 1e-13  # noqa: E731
+        assert same(ctx.jacobian_apply(v), ja)
+        assert same(ctx.jacobian_diagonal(), da)
         ctx.freeze_jacobian(False)
         jb = ctx.jacobian_apply(v).clone()
         rb = ctx.residual().clone()
-        assert torch.equal(rb_frozen, rb) and not torch.equal(rb, ra)
+        assert same(rb_frozen, rb) and not same(rb, ra) and not same(jb, ja)
         ref = context_for(p)
         ref.set_time("bdf1", (0.02, 0.01, 0.01, 0.01))
         ref.set_state(b, h1)
-        assert torch.equal(jb, ref.jacobian_apply(v))
+        assert same(jb, ref.jacobian_apply(v))
 
 
 @pytest.mark.gpu
