@@ -124,7 +124,7 @@ enum class Method { steady, bdf1, bdf2, bdf3, sdirk2, sdirk3 };
 
 struct BC {
   std::string type;
-  int id = 0, periodic_direction = 0;
+  int id = 0, periodic_id = 1, periodic_direction = 0;
   Function f[3];
 };
 
@@ -140,6 +140,13 @@ struct Params {
   double lo = -1, hi = 1;
   bool colorize = false;
   int refinement = 0;
+  // general meshes (gls_umesh): mesh type gmsh or a non-hyper_cube deal.II grid
+  bool general = false;
+  std::string mesh_type = "dealii", grid_type = "hyper_cube", grid_args = "-1 : 1 : false", mesh_file;
+  bool qmapping_all = false;
+  struct ManifoldPrm { int id = 0; std::string type = "none"; double arg[3] = {0, 0, 0}; };
+  std::vector<ManifoldPrm> manifolds;
+  int display_precision = 4, residual_precision = 4;
   std::vector<BC> bcs;
   bool source = false;
   Function force;
@@ -190,11 +197,30 @@ Params read_params(const Prm &p, int dim) {
   P.nu = p.d("physical properties/kinematic viscosity", 1.0);
   P.k = p.i("FEM/velocity order", 1);
   P.kp = p.i("FEM/pressure order", 1);
-  if (p.get("mesh/type", "dealii") != "dealii") die("mesh type '%s' is not supported", p.get("mesh/type", "").c_str());
+  P.qmapping_all = p.b("FEM/qmapping all", false);
+  P.mesh_type = p.get("mesh/type", "dealii");
+  if (P.mesh_type != "dealii" && P.mesh_type != "gmsh") die("mesh type '%s' is not supported (dealii | gmsh)", P.mesh_type.c_str());
   const std::string gt = p.get("mesh/grid type", "hyper_cube");
-  if (gt != "hyper_cube") die("grid type '%s' is not supported (hyper_cube only)", gt.c_str());
-  {
-    const std::string a = p.get("mesh/grid arguments", "-1 : 1 : false");
+  P.grid_type = gt;
+  P.grid_args = p.get("mesh/grid arguments", "-1 : 1 : false");
+  P.mesh_file = p.get("mesh/file name", "none");
+  P.general = P.mesh_type == "gmsh" || gt != "hyper_cube";
+  {  // manifolds (source/core/manifolds.cc:133-186): spherical on boundary ids
+    const int nm = p.i("manifolds/number", 0);
+    for (int i = 0; i < nm; ++i) {
+      const std::string ms = "manifolds/manifold " + std::to_string(i) + "/";
+      Params::ManifoldPrm mp;
+      mp.type = p.get(ms + "type", "none");
+      mp.id = p.i(ms + "id", i);
+      for (int a = 0; a < 3; ++a) mp.arg[a] = p.d(ms + "arg" + std::to_string(a + 1), 0.0);
+      if (mp.type != "none" && mp.type != "spherical") die("manifold %d: type '%s' is not supported (none | spherical)", i, mp.type.c_str());
+      P.manifolds.push_back(mp);
+    }
+  }
+  P.display_precision = p.i("simulation control/display precision", 4);
+  P.residual_precision = p.i("non-linear solver/residual precision", 4);
+  if (!P.general) {
+    const std::string a = P.grid_args;
     std::vector<std::string> parts;
     std::stringstream ss(a);
     std::string tok;
@@ -225,6 +251,7 @@ Params read_params(const Prm &p, int dim) {
     if (p.d(ma + "fraction coarsening", 0.05) != 0.0)
       die("mesh adaptation: coarsening is not supported (set fraction coarsening = 0)");
     if (P.method != Method::steady) die("kelly mesh adaptation: steady simulations only");
+    if (P.general) die("kelly mesh adaptation: hyper_cube meshes only");
     if (P.mesh_adapt > 1) die("kelly mesh adaptation: one adaptation (one refinement level) at most");
     if (P.k > 2 || P.kp > P.k) die("kelly mesh adaptation: 1 <= pressure order <= velocity order <= 2");
   }
@@ -235,6 +262,7 @@ Params read_params(const Prm &p, int dim) {
     b.type = p.get(s + "type", "noslip");
     b.id = p.i(s + "id", i);
     b.periodic_direction = p.i(s + "periodic_direction", 0);
+    b.periodic_id = p.i(s + "periodic_id", 1);
     if (b.type == "function") {
       const char *nm[3] = {"u", "v", "w"};
       for (int c = 0; c < dim; ++c) b.f[c] = Function(p, s + nm[c], dim, "0");
@@ -252,7 +280,11 @@ Params read_params(const Prm &p, int dim) {
   P.analytical = p.b("analytical solution/enable", false);
   P.analytical_verbose = p.get("analytical solution/verbosity", "quiet") == "verbose";
   P.analytical_file = p.get("analytical solution/filename", "L2Error");
-  if (P.analytical) P.exact = Function(p, "analytical solution/uvwp", dim, zeros);
+  if (P.analytical) {  // the reference's subsection is "uvw" (analytical_solutions.cc:69-70); "uvwp" accepted too
+    const bool uvw = p.get("analytical solution/uvw/Function expression", "\x01") != "\x01" ||
+                     p.get("analytical solution/uvwp/Function expression", "\x01") == "\x01";
+    P.exact = Function(p, uvw ? "analytical solution/uvw" : "analytical solution/uvwp", dim, zeros);
+  }
   P.enstrophy = p.b("post-processing/calculate enstrophy", false);
   P.kinetic = p.b("post-processing/calculate kinetic energy", false);
   P.pp_verbose = p.get("post-processing/verbosity", "quiet") == "verbose";
@@ -292,6 +324,11 @@ struct Mesh {
   std::vector<uint8_t> vhanging;  // per velocity node
   std::vector<int64_t> hang_dofs, hang_off{0}, hang_master;
   std::vector<double> hang_w;
+  // general (curved / unstructured) cells: MappingQ(k) support points per cell, cell->measure(),
+  // boundary-id bits per velocity node (gls_umesh_fe_space)
+  bool general = false;
+  std::vector<double> support, measure;
+  std::vector<uint32_t> vbid;
   int64_t n_dofs() const { return (int64_t)dim * nv + np; }
   void coord(int64_t node, bool vel, double *x, int *idx) const {
     if (!vx.empty()) {  // refined mesh: no lattice index
@@ -386,6 +423,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
   for (const BC &b : P.bcs) {
     if (b.type == "periodic") continue;
+    if (b.type == "slip" && m.general) die("slip boundaries on curved / unstructured meshes are not supported");
     std::vector<int64_t> sel;
     std::vector<double> X;
     std::vector<unsigned> nrm;
@@ -396,7 +434,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       // hanging nodes keep their hanging constraint (interpolate_boundary_values skips DoFs that
       // are already constrained, gls_navier_stokes.cc:84-110)
       if (!m.vhanging.empty() && m.vhanging[(size_t)v]) continue;
-      if (face_bits(m, x, P.colorize) & (1u << b.id)) {
+      if ((m.general ? m.vbid[(size_t)v] : face_bits(m, x, P.colorize)) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
         nrm.push_back(face_normals(m, x, P.colorize, b.id));
@@ -494,9 +532,46 @@ struct CellEval {
     qq[1] = (q / nq1) % nq1;
     qq[2] = m.dim == 3 ? q / (nq1 * nq1) : 0;
   }
+  // MappingQ(k) of a general cell at Gauss point q: x, J^-1 [a][i], det J (k <= 2: equidistant)
+  void mapped(int64_t c, int q, double *x, double JI[3][3], double &det) const {
+    const int dim = m.dim, k1 = m.k + 1;
+    int qq[3];
+    qidx(q, qq);
+    double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int d = 0; d < 3; ++d) x[d] = 0;
+    const double *S = &m.support[(size_t)(c * nvl * dim)];
+    for (int b = 0; b < nvl; ++b) {
+      const int b0 = b % k1, b1 = (b / k1) % k1, b2 = dim == 3 ? b / (k1 * k1) : 0;
+      const double v0 = Vv[(size_t)(qq[0] * k1 + b0)], v1 = Vv[(size_t)(qq[1] * k1 + b1)];
+      const double v2 = dim == 3 ? Vv[(size_t)(qq[2] * k1 + b2)] : 1.0;
+      const double g[3] = {Dv[(size_t)(qq[0] * k1 + b0)] * v1 * v2, v0 * Dv[(size_t)(qq[1] * k1 + b1)] * v2,
+                           dim == 3 ? v0 * v1 * Dv[(size_t)(qq[2] * k1 + b2)] : 0.0};
+      for (int i = 0; i < dim; ++i) {
+        x[i] += S[b * dim + i] * v0 * v1 * v2;
+        for (int a = 0; a < dim; ++a) J[i][a] += S[b * dim + i] * g[a];
+      }
+    }
+    if (dim == 2) {
+      det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+      JI[0][0] = J[1][1] / det; JI[0][1] = -J[0][1] / det; JI[1][0] = -J[1][0] / det; JI[1][1] = J[0][0] / det;
+    } else {
+      det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+            J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+      for (int a = 0; a < 3; ++a)
+        for (int i = 0; i < 3; ++i)
+          JI[a][i] = (J[(i + 1) % 3][(a + 1) % 3] * J[(i + 2) % 3][(a + 2) % 3] -
+                      J[(i + 1) % 3][(a + 2) % 3] * J[(i + 2) % 3][(a + 1) % 3]) / det;
+    }
+  }
   void point(int64_t c, int q, double *x, double &JxW) const {
     int qq[3];
     qidx(q, qq);
+    if (m.general) {
+      double JI[3][3], det;
+      mapped(c, q, x, JI, det);
+      JxW = det * wq[(size_t)qq[0]] * wq[(size_t)qq[1]] * (m.dim == 3 ? wq[(size_t)qq[2]] : 1.0);
+      return;
+    }
     JxW = 1;
     for (int d = 0; d < m.dim; ++d) {
       const double hd = m.h[(size_t)(c * m.dim + d)];
@@ -516,7 +591,13 @@ struct CellEval {
     const int dim = m.dim, k1 = m.k + 1;
     int qq[3];
     qidx(q, qq);
-    const double *hh = &m.h[(size_t)(c * dim)];
+    const double one[3] = {1.0, 1.0, 1.0};
+    const double *hh = m.general ? one : &m.h[(size_t)(c * dim)];
+    double JI[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    if (m.general) {
+      double x[3], det;
+      mapped(c, q, x, JI, det);
+    }
     for (int d = 0; d < 3; ++d) {
       u[d] = 0;
       for (int e = 0; e < 3; ++e) G[d][e] = 0;
@@ -527,8 +608,14 @@ struct CellEval {
       const int a0 = a % k1, a1 = (a / k1) % k1, a2 = dim == 3 ? a / (k1 * k1) : 0;
       const double b0 = Vv[(size_t)(qq[0] * k1 + a0)], b1 = Vv[(size_t)(qq[1] * k1 + a1)];
       const double b2 = dim == 3 ? Vv[(size_t)(qq[2] * k1 + a2)] : 1.0;
-      const double g[3] = {Dv[(size_t)(qq[0] * k1 + a0)] * b1 * b2 / hh[0], b0 * Dv[(size_t)(qq[1] * k1 + a1)] * b2 / hh[1],
-                           dim == 3 ? b0 * b1 * Dv[(size_t)(qq[2] * k1 + a2)] / hh[2] : 0.0};
+      const double gr[3] = {Dv[(size_t)(qq[0] * k1 + a0)] * b1 * b2 / hh[0], b0 * Dv[(size_t)(qq[1] * k1 + a1)] * b2 / hh[1],
+                            dim == 3 ? b0 * b1 * Dv[(size_t)(qq[2] * k1 + a2)] / hh[2] : 0.0};
+      double g[3] = {gr[0], gr[1], gr[2]};
+      if (m.general)
+        for (int i = 0; i < dim; ++i) {
+          g[i] = 0.0;
+          for (int e = 0; e < dim; ++e) g[i] += JI[e][i] * gr[e];
+        }
       for (int d = 0; d < dim; ++d) {
         const double ud = sol[(size_t)cv[a] * dim + d];
         u[d] += ud * b0 * b1 * b2;
@@ -551,6 +638,8 @@ struct Solver {
   Constraints C;
   gls_ctx *ctx = nullptr;
   gls_refined_mesh *rmesh = nullptr;  // the locally refined mesh m was built from (kelly)
+  gls_umesh *um = nullptr;            // general meshes: the triangulation (kept across refinements)
+  gls_fe_space *space = nullptr;      // and its current FE space
   std::vector<gls_ctx *> mg_levels;
   double *d_present = nullptr, *d_m1 = nullptr, *d_m2 = nullptr, *d_m3 = nullptr;
   std::vector<double> present, m1, m2, m3;
@@ -561,8 +650,19 @@ struct Solver {
   std::vector<std::vector<double>> errors;  // steady: cells, e_u, e_p ; transient: t, e_u
   std::vector<std::pair<double, std::string>> pvd;
 
+  int precision = 4;    // error-table digits (ConvergenceTable scientific precision)
+  bool stats = false;   // print the solver iteration totals at the end (--stats)
+  static std::string g6(double v) {  // std::ostream's default formatting (6 significant digits)
+    char b[64];
+    std::snprintf(b, sizeof(b), "%g", v);
+    return b;
+  }
   Solver(Params &p, bool mg) : P(p), use_mg(mg) {}
-  ~Solver() { release(); }
+  ~Solver() {
+    release();
+    if (space) gls_fe_space_destroy(space);
+    if (um) gls_umesh_destroy(um);
+  }
 
   void release() {
     for (gls_ctx *g : mg_levels) gls_destroy(g);
@@ -585,7 +685,7 @@ struct Solver {
 
   gls_ctx *make_context(const Mesh &mm, const Constraints &cc) {
     std::vector<double> fq;
-    if (P.source) {  // source term at the quadrature points QGauss(k+1)
+    if (P.source && !mm.general) {  // source term at the quadrature points QGauss(k+1)
       CellEval ev(mm, mm.k + 1);
       std::vector<double> X, F;
       X.reserve((size_t)(mm.nc * ev.nq * mm.dim));
@@ -611,15 +711,30 @@ struct Solver {
     D.cell_vnodes = mm.cv.data();
     if (mm.kp == mm.k && (mm.cp != mm.cv || mm.np != mm.nv)) die("equal-order mesh with distinct pressure nodes");
     D.cell_pnodes = (mm.kp == mm.k) ? nullptr : mm.cp.data();
-    D.cell_x0 = mm.x0.data();
-    D.cell_h = mm.h.data();
+    if (mm.general) {  // MappingQ(k) support points (gls_umesh_fe_space)
+      D.map_degree = mm.k;
+      D.cell_support = mm.support.data();
+    } else {
+      D.cell_x0 = mm.x0.data();
+      D.cell_h = mm.h.data();
+    }
     D.vnode_mask = cc.mask.data();
     D.viscosity = P.nu;
     D.srf = P.srf ? 1 : 0;
     for (int i = 0; i < 3; ++i) D.omega[i] = P.omega[i];
-    D.force_q = P.source ? fq.data() : nullptr;
+    D.force_q = (P.source && !mm.general) ? fq.data() : nullptr;
     gls_ctx *g = nullptr;
     ck(gls_create(&D, &g), "gls_create");
+    if (P.source && mm.general) {  // forcing at the library's (mapped) quadrature points
+      const int nq1 = mm.k + 1, nq = mm.dim == 3 ? nq1 * nq1 * nq1 : nq1 * nq1;
+      std::vector<double> X((size_t)(mm.nc * nq * mm.dim)), F;
+      ck(gls_quadrature_points(g, X.data()), "gls_quadrature_points");
+      P.force.eval(X, mm.dim, time, F);
+      fq.resize(X.size());
+      for (size_t i = 0; i < fq.size() / mm.dim; ++i)
+        for (int d = 0; d < mm.dim; ++d) fq[i * mm.dim + d] = F[i * (size_t)P.force.nc + d];
+      ck(gls_set_force(g, fq.data()), "gls_set_force");
+    }
     ck(gls_set_dirichlet(g, (int64_t)cc.dofs.size(), cc.dofs.data(), cc.vals.data()), "gls_set_dirichlet");
     return g;
   }
@@ -689,8 +804,8 @@ struct Solver {
                        m.hang_master.data(), m.hang_w.data()),
        "gls_set_hanging");
     alloc_vectors();
-    std::printf("mesh: cells = %lld, dofs = %lld, hanging dofs = %lld, levels = 1\n", (long long)m.nc,
-                (long long)m.n_dofs(), (long long)m.hang_dofs.size());
+    print_setup(std::pow(P.hi - P.lo, P.dim));
+    std::printf("   Hanging node DoFs:            %lld\n", (long long)m.hang_dofs.size());
   }
 
   void setup(int n) {
@@ -721,8 +836,65 @@ struct Solver {
       mp.coarse_omega = 0.7;
       ck(gls_mg_attach(ctx, &mp), "gls_mg_attach");
     }
-    std::printf("mesh: cells = %lld, dofs = %lld, levels = %d\n", (long long)m.nc, (long long)N,
-                1 + (int)mg_levels.size());
+    (void)N;
+    print_setup(std::pow(P.hi - P.lo, P.dim));
+  }
+
+  // general meshes: the triangulation (gmsh file or GridGenerator grid with its manifolds and the
+  // prm's spherical boundary manifolds, refine_global(initial refinement)), read once
+  void create_umesh() {
+    if (P.mesh_type == "gmsh") ck(gls_umesh_read_gmsh(P.dim, P.mesh_file.c_str(), &um), "reading the gmsh mesh");
+    else ck(gls_umesh_generate(P.dim, P.grid_type.c_str(), P.grid_args.c_str(), &um), "GridGenerator");
+    for (const auto &mp : P.manifolds) {  // attach_manifolds_to_triangulation (manifolds.cc:226-247)
+      if (mp.type != "spherical") continue;
+      ck(gls_umesh_set_manifold(um, mp.id, 1, mp.arg, nullptr), "gls_umesh_set_manifold");
+      ck(gls_umesh_boundary_manifold(um, mp.id, mp.id), "gls_umesh_boundary_manifold");
+    }
+    ck(gls_umesh_refine_global(um, P.refinement), "refine_global");
+  }
+  // FE space, constraints and context on the current triangulation (per-cell kernels with MappingQ
+  // geometry, Jacobi-preconditioned GMRES)
+  void setup_general() {
+    release();
+    if (space) gls_fe_space_destroy(space);
+    space = nullptr;
+    std::vector<int32_t> per;
+    for (const BC &b : P.bcs)
+      if (b.type == "periodic") {  // make_periodicity_constraints(id, periodic_id, direction)
+        per.push_back(b.id);
+        per.push_back(b.periodic_id);
+        per.push_back(b.periodic_direction);
+      }
+    ck(gls_umesh_fe_space(um, P.k, P.kp, P.qmapping_all ? 1 : 0, (int)per.size() / 3, per.data(), &space), "gls_umesh_fe_space");
+    const gls_fe_space &F = *space;
+    Mesh r;
+    r.dim = P.dim;
+    r.k = P.k;
+    r.kp = P.kp;
+    r.general = true;
+    r.nc = F.n_cells;
+    r.nv = F.n_vnodes;
+    r.np = F.n_pnodes;
+    const int nvl = P.dim == 3 ? (P.k + 1) * (P.k + 1) * (P.k + 1) : (P.k + 1) * (P.k + 1);
+    const int npl = P.dim == 3 ? (P.kp + 1) * (P.kp + 1) * (P.kp + 1) : (P.kp + 1) * (P.kp + 1);
+    r.cv.assign(F.cell_vnodes, F.cell_vnodes + r.nc * nvl);
+    r.cp.assign(F.cell_pnodes, F.cell_pnodes + r.nc * npl);
+    r.vx.assign(F.vnode_x, F.vnode_x + r.nv * P.dim);
+    r.px.assign(F.pnode_x, F.pnode_x + r.np * P.dim);
+    r.vbid.assign(F.vnode_bid, F.vnode_bid + r.nv);
+    r.support.assign(F.cell_support, F.cell_support + r.nc * nvl * P.dim);
+    r.measure.assign(F.cell_measure, F.cell_measure + r.nc);
+    m = std::move(r);
+    C = make_constraints(P, m, time);
+    ctx = make_context(m, C);
+    alloc_vectors();
+    print_setup(F.volume);
+  }
+  // setup_dofs' summary lines (gls_navier_stokes.cc:220-227)
+  void print_setup(double volume) {
+    std::printf("   Number of active cells:       %lld\n   Number of degrees of freedom: %lld\n", (long long)m.nc,
+                (long long)m.n_dofs());
+    std::printf("   Volume of triangulation:      %g\n", volume);
   }
 
   void upload(const std::vector<double> &h, double *d) {
@@ -852,8 +1024,12 @@ struct Solver {
     np.tolerance = P.newton_tol;
     np.max_iterations = P.newton_max;
     np.verbosity = P.newton_verbose;
-    np.lin.max_iterations = P.lin_max;
-    np.lin.restart = P.restart;
+    // The reference's iteration caps are tuned for ILU / AMG; the matrix-free Jacobi-preconditioned
+    // GMRES used where no multigrid hierarchy exists (curved, unstructured and locally refined meshes)
+    // needs more iterations to reach the same tolerance, so its cap and restart are raised there.
+    const bool jacobi = mg_levels.empty();
+    np.lin.max_iterations = jacobi ? std::max(P.lin_max, 20000) : P.lin_max;
+    np.lin.restart = jacobi ? std::max(P.restart, 100) : P.restart;
     np.lin.relative_residual = P.lin_rel;
     np.lin.minimum_residual = P.lin_min;
     np.solver = P.nl_solver;
@@ -931,6 +1107,9 @@ struct Solver {
     P.exact.eval(X, m.dim, time, E);
     const int ne = P.exact.nc;
     double pint = 0, peint = 0, vol = 0, eu = 0, ep = 0;
+    // GridTools::volume(triangulation) = the Q1 measure of the cells (navier_stokes_base.cc:320)
+    if (m.general)
+      for (double v : m.measure) vol += v;
     for (int pass = 0; pass < 2; ++pass) {
       int64_t idx = 0;
       for (int64_t c = 0; c < m.nc; ++c)
@@ -943,7 +1122,7 @@ struct Solver {
           if (pass == 0) {
             pint += p * JxW;
             peint += pe * JxW;
-            vol += JxW;
+            vol += m.general ? 0.0 : JxW;
           } else {
             for (int d = 0; d < m.dim; ++d) eu += (u[d] - ex[d]) * (u[d] - ex[d]) * JxW;
             const double dp = (p - pint / vol) - (pe - peint / vol);
@@ -984,7 +1163,9 @@ struct Solver {
     for (int64_t c = 0; c < m.nc; ++c) {
       double u[3], G[3][3], p, meas = 1;
       ev.at(present.data(), c, 0, u, G, p);
-      for (int d = 0; d < m.dim; ++d) meas *= m.h[(size_t)(c * m.dim + d)];
+      if (m.general) meas = m.measure[(size_t)c];
+      else
+        for (int d = 0; d < m.dim; ++d) meas *= m.h[(size_t)(c * m.dim + d)];
       const double hh = m.dim == 2 ? std::sqrt(4. * meas / M_PI) / deg : std::cbrt(6. * meas / M_PI) / deg;
       double un = 0;
       for (int d = 0; d < m.dim; ++d) un += u[d] * u[d];
@@ -1006,8 +1187,13 @@ struct Solver {
     D.n_pnodes = (int)m.np;
     D.cell_vnodes = m.cv.data();
     D.cell_pnodes = m.cp.data();
-    D.cell_x0 = m.x0.data();
-    D.cell_h = m.h.data();
+    if (m.general) {
+      D.map_degree = m.k;
+      D.cell_support = m.support.data();
+    } else {
+      D.cell_x0 = m.x0.data();
+      D.cell_h = m.h.data();
+    }
     D.srf = P.srf ? 1 : 0;
     for (int i = 0; i < 3; ++i) D.omega[i] = P.omega[i];
     ck(gls_vtu_write((P.output_path + piece).c_str(), &D, present.data(), P.subdivision, 0, 1), "gls_vtu_write");
@@ -1025,13 +1211,15 @@ struct Solver {
   }
   void postprocess(bool initial) {
     if (P.output_frequency > 0 && step % P.output_frequency == 0) write_output();
-    if (P.enstrophy && P.pp_verbose) std::printf("enstrophy = %.10g\n", volume_average(true));
-    if (P.kinetic && P.pp_verbose) std::printf("kinetic_energy = %.10g\n", volume_average(false));
+    // post-processing lines of NavierStokesBase::postprocess (navier_stokes_base.cc:791-853)
+    if (P.enstrophy && P.pp_verbose) std::printf("Enstrophy  : %s\n", g6(volume_average(true)).c_str());
+    if (P.kinetic && P.pp_verbose) std::printf("Kinetic energy : %s\n", g6(volume_average(false)).c_str());
     if (!initial && P.analytical) {
       const auto e = l2_error();
       if (P.method == Method::steady) errors.push_back({(double)m.nc, e.first, e.second});
       else errors.push_back({time, e.first});
-      if (P.analytical_verbose) std::printf("l2_error_velocity = %.10g\n", e.first);
+      if (P.analytical_verbose && P.method != Method::steady)
+        std::printf("L2 error velocity : %s\n", g6(e.first).c_str());
     }
   }
   void end_of_step() {  // history shift + CFL of the step just taken
@@ -1043,6 +1231,16 @@ struct Solver {
   }
   // uniform refinement with interpolation of the Qk fields onto the refined lattice
   void refine_uniform() {
+    if (m.general) {  // refine_global + SolutionTransfer (gls_fe_space_transfer)
+      const std::vector<double> sol = present;
+      gls_fe_space *old_space = space;
+      space = nullptr;  // keep the old space alive across setup_general
+      ck(gls_umesh_refine_global(um, 1), "refine_global");
+      setup_general();
+      ck(gls_fe_space_transfer(old_space, space, sol.data(), present.data()), "gls_fe_space_transfer");
+      gls_fe_space_destroy(old_space);
+      return;
+    }
     const Mesh old = m;
     const std::vector<double> sol = present;
     setup(m.n * 2);
@@ -1127,24 +1325,63 @@ struct Solver {
     ck(gls_mesh_refined_interpolate(rmesh, old.n, P.lo, P.hi, sol.data(), present.data()),
        "gls_mesh_refined_interpolate");
   }
+  // NavierStokesBase::finish_simulation's error table (navier_stokes_base.cc:382-424): deal.II
+  // ConvergenceTable text layout — steady: cells | error_velocity + log2 reduction rate |
+  // error_pressure + rate, errors in scientific notation with `precision` digits, rates fixed 2,
+  // "-" where no rate, supercolumn headers centred over their span; transient: time (fixed 4) |
+  // error_velocity
   void report() {
     if (!P.analytical || errors.empty()) return;
     std::ostringstream o;
-    char line[160];
+    auto sci = [&](double v) {
+      char b[64];
+      std::snprintf(b, sizeof(b), "%.*e", precision, v);
+      return std::string(b);
+    };
+    auto fixed = [](double v, int d) {
+      char b[64];
+      std::snprintf(b, sizeof(b), "%.*f", d, v);
+      return std::string(b);
+    };
+    auto rpad = [](const std::string &t, size_t w) { return std::string(w > t.size() ? w - t.size() : 0, ' ') + t; };
+    auto lpad = [](const std::string &t, size_t w) { return t + std::string(w > t.size() ? w - t.size() : 0, ' '); };
+    auto centre = [](const std::string &t, size_t w) {
+      const size_t f = w > t.size() ? (w - t.size()) / 2 : 0, r = w > t.size() ? w - t.size() - f : 0;
+      return std::string(f, ' ') + t + std::string(r, ' ');
+    };
+    const size_t n = errors.size();
     if (P.method == Method::steady) {
-      o << "# cells  e_velocity  rate  e_pressure  rate\n";
-      for (size_t i = 0; i < errors.size(); ++i) {
+      std::vector<std::string> c0, eu, ru, ep, rp;
+      for (size_t i = 0; i < n; ++i) {
         const auto &r = errors[i];
-        const double ru = i ? std::log2(errors[i - 1][1] / r[1]) : NAN, rp = i ? std::log2(errors[i - 1][2] / r[2]) : NAN;
-        std::snprintf(line, sizeof(line), "%lld %.6e %.3f %.6e %.3f\n", (long long)r[0], r[1], ru, r[2], rp);
-        o << line;
+        c0.push_back(std::to_string((long long)r[0]));
+        eu.push_back(sci(r[1]));
+        ep.push_back(sci(r[2]));
+        ru.push_back(i ? fixed(std::log2(errors[i - 1][1] / r[1]), 2) : "-");
+        rp.push_back(i ? fixed(std::log2(errors[i - 1][2] / r[2]), 2) : "-");
       }
+      auto width = [](const std::vector<std::string> &v, size_t w0) {
+        size_t w = w0;
+        for (auto &t : v) w = std::max(w, t.size());
+        return w;
+      };
+      const size_t w0 = width(c0, 5), w1 = width(eu, 0), w2 = width(ru, 0), w3 = width(ep, 0), w4 = width(rp, 0);
+      o << centre("cells", w0) << ' ' << centre("error_velocity", w1 + 1 + w2) << ' '
+        << centre("error_pressure", w3 + 1 + w4) << ' ' << '\n';
+      for (size_t i = 0; i < n; ++i)
+        o << rpad(c0[i], w0) << ' ' << rpad(eu[i], w1) << ' ' << rpad(ru[i], w2) << ' ' << rpad(ep[i], w3) << ' '
+          << rpad(rp[i], w4) << ' ' << '\n';
     } else {
-      o << "# time  e_velocity\n";
-      for (const auto &r : errors) {
-        std::snprintf(line, sizeof(line), "%.6f %.6e\n", r[0], r[1]);
-        o << line;
+      std::vector<std::string> t0, eu;
+      for (auto &r : errors) {
+        t0.push_back(fixed(r[0], 4));
+        eu.push_back(sci(r[1]));
       }
+      size_t w0 = 4, w1 = 14;
+      for (auto &t : t0) w0 = std::max(w0, t.size());
+      for (auto &t : eu) w1 = std::max(w1, t.size());
+      o << centre("time", w0) << ' ' << centre("error_velocity", w1) << ' ' << '\n';
+      for (size_t i = 0; i < n; ++i) o << rpad(t0[i], w0) << ' ' << lpad(eu[i], w1) << ' ' << '\n';
     }
     std::printf("%s", o.str().c_str());
     std::ofstream(P.analytical_file + ".dat") << o.str();
@@ -1153,7 +1390,13 @@ struct Solver {
   void run() {
     dt_now = P.dt;
     dts[0] = P.dt;
-    setup(1 << P.refinement);
+    std::printf("Running on 1 MPI rank(s)...\n");  // navier_stokes_base.cc:115-117 (one rank per GPU)
+    if (P.general) {
+      create_umesh();
+      setup_general();
+    } else {
+      setup(1 << P.refinement);
+    }
     if (P.ic_type == "nodal" || P.ic_type == "viscous") {
       nodal_values(P.ic, present);
       if (P.ic_type == "viscous") solve_nonlinear(GLS_STEADY, P.ic_nu);
@@ -1175,8 +1418,13 @@ struct Solver {
         time += dt;
       }
       if (P.log_frequency > 0 && step % P.log_frequency == 0) {
-        if (steady) std::printf("step %d/%d (steady)\n", step, P.mesh_adapt + 1);
-        else std::printf("step %d: t = %.10g, dt = %.10g, cfl = %.6g\n", step, time, dt_now, cfl);
+        // SimulationControl{Steady,Transient}::print_progression (simulation_control.cc:92-107, 242-255)
+        const char *stars = "*****************************************************************";
+        if (steady)
+          std::printf("\n%s\nSteady iteration : %8d/%d\n%s\n", stars, step, P.mesh_adapt + 1, stars);
+        else
+          std::printf("\n%s\nTransient iteration : %-8d Time : %-8s Time step : %-8s CFL : %-8s\n%s\n", stars, step,
+                      g6(time).c_str(), g6(dt_now).c_str(), g6(cfl).c_str(), stars);
       }
       if (step == 1) {
         first_step();
@@ -1191,28 +1439,43 @@ struct Solver {
       end_of_step();
     }
     report();
-    std::printf("newton_iterations = %d, linear_iterations = %d\n", newton_its, linear_its);
+    if (stats) std::printf("newton_iterations = %d, linear_iterations = %d\n", newton_its, linear_its);
   }
 };
 
 }  // namespace
 
 int main(int argc, char **argv) {
+  // gls_navier_stokes_2d / gls_navier_stokes_3d <file.prm> (applications/gls_navier_stokes_{2d,3d},
+  // gls_navier_stokes_3d.cc:22-46): the dimension comes from the program name; the generic
+  // binary takes --dim. Extra options: --precond mg|jacobi, --precision N (error table digits),
+  // --stats (solver iteration totals).
   int dim = 0;
-  bool mg = true;
+  bool mg = true, stats = false;
+  int precision = 4;
   const char *file = nullptr;
+  const std::string prog = argv[0];
+  if (prog.size() >= 2 && prog.compare(prog.size() - 2, 2, "2d") == 0) dim = 2;
+  if (prog.size() >= 2 && prog.compare(prog.size() - 2, 2, "3d") == 0) dim = 3;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--dim") && i + 1 < argc) dim = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) mg = std::strcmp(argv[++i], "jacobi") != 0;
+    else if (!std::strcmp(argv[i], "--precision") && i + 1 < argc) precision = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--stats")) stats = true;
     else if (argv[i][0] != '-') file = argv[i];
     else die("unknown option %s", argv[i]);
   }
-  if (!file) die("usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm");
+  if (!file) {  // the reference prints its usage and exits 1 (gls_navier_stokes_3d.cc:27-31)
+    std::printf("Usage:\n%s input_file\n", argv[0]);
+    return 1;
+  }
   if (dim == 0) dim = 3;
   if (dim != 2 && dim != 3) die("--dim must be 2 or 3");
   Prm prm(file);
   Params P = read_params(prm, dim);
   Solver s(P, mg);
+  s.precision = precision;
+  s.stats = stats;
   s.run();
   return 0;
 }

@@ -703,7 +703,8 @@ extern "C" {
 // (post_processors.h:84-115), so the value at patch point p is 0.5 * sum_{p'<=p} (|W|^2 - |S|^2).
 int gls_vtu_write(const char *filename, const gls_mesh_desc *m, const double *sol, int subdivision, int subdomain,
                   int binary) {
-  if (!filename || !m || !sol || !m->cell_vnodes || !m->cell_h)
+  const bool mapped = m && m->map_degree > 0;
+  if (!filename || !m || !sol || !m->cell_vnodes || (!m->cell_h && !(mapped && m->cell_support)))
     return gls_io_set_error(GLS_EINVAL, "gls_vtu_write: null argument");
   const int dim = m->dim, k = m->k, kp = m->kp, ns = subdivision > 0 ? subdivision : 1;
   if ((dim != 2 && dim != 3) || k < 1 || k > 3 || kp < 1 || kp > k)
@@ -725,23 +726,65 @@ int gls_vtu_write(const char *filename, const gls_mesh_desc *m, const double *so
       qcr((size_t)npts), sub((size_t)npts, (double)subdomain), eul;
   if (m->srf) eul.resize((size_t)npts * 3);
   const int64_t nvdof = (int64_t)dim * m->n_vnodes;
+  // mapped cells: MappingQ(md) through the support points (build_patches(mapping, ...),
+  // navier_stokes_base.cc:1062): patch point positions and J^-T for the gradients
+  const int md = mapped ? m->map_degree : 1, nm = md + 1, nsup = dim == 3 ? nm * nm * nm : nm * nm;
+  std::vector<double> Vm(np1 * nm), Dm(np1 * nm);
+  if (mapped) {
+    const std::vector<double> xm = lobatto_nodes(md);
+    for (int t = 0; t < np1; ++t) lagrange(xm, (double)t / ns, &Vm[t * nm], &Dm[t * nm]);
+  }
+  const double one[3] = {1.0, 1.0, 1.0};
   for (int64_t c = 0; c < nc; ++c) {
     const int32_t *cv = m->cell_vnodes + c * nvl;
     const int32_t *cp = m->cell_pnodes ? m->cell_pnodes + c * npl : cv;
-    const double *h = m->cell_h + c * dim;
+    const double *h = mapped ? one : m->cell_h + c * dim;
     double p1 = 0.0, r1 = 0.0;  // see the q_criterion note above
     for (int p = 0; p < npp; ++p) {
       const int t0 = p % np1, t1 = (p / np1) % np1, t2 = dim == 3 ? p / (np1 * np1) : 0;
       const int64_t P = c * npp + p;
       double x[3] = {0, 0, 0};
       const int tt[3] = {t0, t1, t2};
-      for (int d = 0; d < dim; ++d) x[d] = (m->cell_x0 ? m->cell_x0[c * dim + d] : 0.0) + h[d] * tt[d] / ns;
+      double JI[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+      if (mapped) {
+        double J[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+        const double *S = m->cell_support + c * nsup * dim;
+        for (int b = 0; b < nsup; ++b) {
+          const int b0i = b % nm, b1i = (b / nm) % nm, b2i = dim == 3 ? b / (nm * nm) : 0;
+          const double v0 = Vm[t0 * nm + b0i], v1 = Vm[t1 * nm + b1i], v2 = dim == 3 ? Vm[t2 * nm + b2i] : 1.0;
+          const double gr[3] = {Dm[t0 * nm + b0i] * v1 * v2, v0 * Dm[t1 * nm + b1i] * v2,
+                                dim == 3 ? v0 * v1 * Dm[t2 * nm + b2i] : 0.0};
+          for (int i = 0; i < dim; ++i) {
+            x[i] += S[b * dim + i] * v0 * v1 * v2;
+            for (int a = 0; a < dim; ++a) J[i][a] += S[b * dim + i] * gr[a];
+          }
+        }
+        if (dim == 2) {
+          const double det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+          JI[0][0] = J[1][1] / det; JI[0][1] = -J[0][1] / det; JI[1][0] = -J[1][0] / det; JI[1][1] = J[0][0] / det;
+        } else {
+          const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                             J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+          for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < 3; ++i)
+              JI[a][i] = (J[(i + 1) % 3][(a + 1) % 3] * J[(i + 2) % 3][(a + 2) % 3] -
+                          J[(i + 1) % 3][(a + 2) % 3] * J[(i + 2) % 3][(a + 1) % 3]) / det;
+        }
+      } else {
+        for (int d = 0; d < dim; ++d) x[d] = (m->cell_x0 ? m->cell_x0[c * dim + d] : 0.0) + h[d] * tt[d] / ns;
+      }
       double u[3] = {0, 0, 0}, G[3][3] = {{0}}, pv = 0.0;
       for (int a = 0; a < nvl; ++a) {
         const int a0 = a % nk, a1 = (a / nk) % nk, a2 = dim == 3 ? a / (nk * nk) : 0;
         const double b0 = Vv[t0 * nk + a0], b1 = Vv[t1 * nk + a1], b2 = dim == 3 ? Vv[t2 * nk + a2] : 1.0;
-        const double g[3] = {Dv[t0 * nk + a0] * b1 * b2 / h[0], b0 * Dv[t1 * nk + a1] * b2 / h[1],
-                             dim == 3 ? b0 * b1 * Dv[t2 * nk + a2] / h[2] : 0.0};
+        const double gref[3] = {Dv[t0 * nk + a0] * b1 * b2 / h[0], b0 * Dv[t1 * nk + a1] * b2 / h[1],
+                                dim == 3 ? b0 * b1 * Dv[t2 * nk + a2] / h[2] : 0.0};
+        double g[3] = {gref[0], gref[1], gref[2]};
+        if (mapped)
+          for (int i = 0; i < dim; ++i) {
+            g[i] = 0.0;
+            for (int e = 0; e < dim; ++e) g[i] += JI[e][i] * gref[e];
+          }
         const double phi = b0 * b1 * b2;
         for (int d = 0; d < dim; ++d) {
           const double ud = sol[(int64_t)cv[a] * dim + d];
