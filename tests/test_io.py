@@ -181,7 +181,7 @@ def _app(tmp_path, prm_text, *args):
 
 
 @pytest.mark.parametrize("text,msg", [
-    ("subsection mesh\n  set grid type = hyper_ball\nend\n", "hyper_cube only"),
+    ("subsection mesh\n  set grid type = hyper_ball\nend\n", "grid type 'hyper_ball' is not supported"),
     ("subsection simulation control\n  set method = rk4\nend\n", "unknown time stepping method"),
     ("subsection boundary conditions\n set number = 1\n subsection bc 0\n  set type = outlet\n end\nend\n", "outlet"),
     ("subsection source term\n set enable = true\n subsection xyz\n  set Function expression = q*2; 0; 0; 0\n"
