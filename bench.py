@@ -5,8 +5,10 @@ Workload (BASELINE.json configs[2], the metric's config): 3D lid-driven cavity, 
 One "step" = one Newton iteration of NewtonNonLinearSolver::solve
 (include/core/newton_non_linear_solver.h:90-137): evaluation_point = present; residual + Jacobian
 diagonal (matrix-free "assemble_matrix_and_rhs"); GMRES(30) on the matrix-free Jacobian, right
-preconditioned by a geometric-multigrid V-cycle (levels 64^3..4^3, damped-Jacobi smoothing; Jacobi
-with --precond jacobi; on N GPUs every level is partitioned like the fine mesh), relative residual 1e-4, max `--lin-max` iterations; alpha line search with
+preconditioned by a geometric-multigrid V-cycle (levels 64^3..2^3, FP32 damped-Jacobi smoothing,
+2+2 sweeps on the 4^3 level, exact LU solve of the 2^3 level's 500 DoFs; Jacobi with --precond
+jacobi; on N GPUs every level is partitioned like the fine mesh and the 4^3 coarsest level gets
+100 Jacobi sweeps), relative residual 1e-4, max `--lin-max` iterations; alpha line search with
 residual re-assembly. Every step restarts from the same synthetic state so the work per step is
 fixed; linear iterations and residual evaluations are reported.
 
@@ -121,7 +123,11 @@ def main():
     ap.add_argument("--rel", type=float, default=1e-4)
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="GMRES right preconditioner: geometric multigrid V-cycle (default) or Jacobi")
-    ap.add_argument("--mg-coarsest", type=int, default=4)
+    ap.add_argument("--mg-coarsest", type=int, default=0,
+                    help="cells per direction of the coarsest level (0: 2 on one GPU -- exact LU solve of its "
+                         "500 DoFs --, 4 with Jacobi sweeps across ranks)")
+    ap.add_argument("--mg-coarse-level-sweeps", type=int, default=2,
+                    help="pre = post sweeps on the level above an exact coarsest solve")
     ap.add_argument("--mg-smooth", type=int, nargs=2, default=(1, 1), metavar=("PRE", "POST"),
                     help="damped-Jacobi sweeps before / after the coarse correction")
     ap.add_argument("--mg-omega", type=float, default=0.9)
@@ -158,6 +164,9 @@ def main():
             dist.barrier()
 
     from softx_2020_200_amd.problem import CavityProblem
+    if args.mg_coarsest == 0:
+        args.mg_coarsest = 2 if world == 1 else 4
+    lsweeps = {-2: (args.mg_coarse_level_sweeps,) * 2} if world == 1 and args.mg_coarse_direct >= 0 else None
     t_setup = time.perf_counter()
     dev = torch.device("cuda", local)
     ts = (args.dt,) * 4
@@ -166,7 +175,8 @@ def main():
                              multigrid=args.precond == "mg", mg_coarsest=args.mg_coarsest,
                              pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
                              coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega,
-                             mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct)
+                             mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct,
+                             level_sweeps=lsweeps)
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -290,7 +300,7 @@ def main():
                                % (args.k, args.kp, args.n),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
-                       args.restart, "GMG V(%d,%d)-cycle" % tuple(args.mg_smooth) if args.precond == "mg" else "Jacobi",
+                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
                    "parallelism": "domain decomposition x%d (RCCL P2P ghosts)" % world if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,

@@ -179,13 +179,18 @@ typedef struct {
   double omega;                               /* damped-Jacobi weight of the smoother, 0 -> 0.6 */
   double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
-                                                 with <= 2048 DoFs), 1 exact solve (<= 8192 DoFs; above
-                                                 2048 by rocSOLVER LU with the pressure gauge pinned),
-                                                 -1 Jacobi sweeps */
+                                                 with <= 2048 DoFs), 1 exact solve (<= 8192 DoFs), -1
+                                                 Jacobi sweeps. The exact solve probes the coarsest
+                                                 Jacobian and inverts it by rocSOLVER LU (partial
+                                                 pivoting) with the first pressure DoF pinned (the
+                                                 enclosed-flow gauge) */
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
                                                  arithmetic from an FP32 copy of the linearization
                                                  (brick path; vectors, transfers and the outer GMRES
                                                  operator stay FP64). 0: all FP64 */
+  const int *level_sweeps;                    /* optional (NULL: uniform): 2*n_levels ints, the
+                                                 pre / post sweep counts of each level (the entries of
+                                                 the coarsest level are ignored) */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when

@@ -340,6 +340,7 @@ struct gls_ctx {
     std::vector<gls_ctx *> lev;
     std::vector<std::array<int, 3>> dims;  // box lattice nodes per direction per level
     int k = 2, pre = 2, post = 2, csweeps = 30;
+    std::vector<int> lpre, lpost;  // per-level sweep counts (default pre / post)
     double omega = 0.6, comega = 0.6;
     std::vector<std::unique_ptr<DevBuf<double>>> bufs;  // per level l>=1: u,u1,u2,u3,b,x,y ; level 0: y
     // per level pair (l, l+1) and axis: 1D tap tables [n_out][5] of prolongation / restriction
@@ -1515,8 +1516,8 @@ int mg_prepare(gls_ctx *c) {
     }
     const auto t1 = tick();
     mg.lu = false;
-    const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");  // gj | lu | lu_npvt (default: size rule)
-    const bool use_lu = cs ? std::strncmp(cs, "lu", 2) == 0 : n > 2048;
+    const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");  // gj | lu | lu_npvt (default lu)
+    const bool use_lu = cs ? std::strncmp(cs, "lu", 2) == 0 : true;  // LU: 1.5-3 ms at n = 500 vs the one-workgroup GJ's ~15
     const bool npvt = cs && std::strcmp(cs, "lu_npvt") == 0;
     if (use_lu) {  // LU with the pressure gauge pinned
       const int64_t pin = 3 * (int64_t)g->n_vnodes;
@@ -1697,7 +1698,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
     }
     return GLS_OK;
   }
-  const int pre = l == L - 1 ? mg.csweeps : mg.pre;
+  const int pre = l == L - 1 ? mg.csweeps : mg.lpre[(size_t)l];
   const double om = l == L - 1 ? mg.comega : mg.omega;
   if (l == L - 1 && l > 0 && pre > 1 && coarse_graph_eligible(c, g, b, x)) {
     GLS_TRY(ensure_diag(g));  // contents the replay reads: current for this state
@@ -1732,7 +1733,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   GLS_TRY(mg_prolong(c, l, xc, y));
   HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
-  for (int it = 0; it < mg.post; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega));
+  for (int it = 0; it < mg.lpost[(size_t)l]; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega));
   return GLS_OK;
 }
 
@@ -1908,6 +1909,14 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
   mg.omega = p->omega > 0 ? p->omega : 0.6;
   mg.comega = p->coarse_omega > 0 ? p->coarse_omega : mg.omega;
+  mg.lpre.assign((size_t)p->n_levels, mg.pre);
+  mg.lpost.assign((size_t)p->n_levels, mg.post);
+  if (p->level_sweeps)
+    for (int l = 0; l < p->n_levels; ++l) {
+      if (p->level_sweeps[2 * l] < 0 || p->level_sweeps[2 * l + 1] < 0) return set_err(GLS_EINVAL, "mg: negative level sweeps");
+      mg.lpre[(size_t)l] = p->level_sweeps[2 * l];
+      mg.lpost[(size_t)l] = p->level_sweeps[2 * l + 1];
+    }
   for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
@@ -1971,7 +1980,7 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
     if (mg.direct) {
       GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
-      if (nco <= 2048 || std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));
+      if (std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));  // gj experiments
       GLS_TRY(mg.ipiv.alloc((size_t)nco));
       GLS_TRY(mg.info.alloc(1));
       if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)

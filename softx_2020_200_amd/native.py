@@ -78,7 +78,8 @@ class LinearParams(C.Structure):
 class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
                 ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
-                ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int)]
+                ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int),
+                ("level_sweeps", C.POINTER(C.c_int))]
 
 
 class RefinedMesh(C.Structure):
@@ -524,13 +525,23 @@ class GLSContext:
         check(self.L.gls_freeze_jacobian(self.h, 1 if freeze else 0), "gls_freeze_jacobian")
 
     def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6,
-                         coarse_omega=0.0, coarse_direct=0, mixed_precision=0):
+                         coarse_omega=0.0, coarse_direct=0, mixed_precision=0, level_sweeps=None):
         """GMRES right preconditioner = geometric multigrid V-cycle over [self] + coarse_levels
-        (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive."""
+        (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive.
+        level_sweeps: optional {level: (pre, post)} overriding pre_smooth / post_smooth per level
+        (negative level indices count from the coarsest)."""
         levels = [self] + list(coarse_levels)
         arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
+        ls = None
+        if level_sweeps:
+            pre0 = pre_smooth if pre_smooth > 0 else (0 if pre_smooth < 0 else 2)
+            post0 = post_smooth if post_smooth >= 0 else 2
+            flat = [pre0, post0] * len(levels)
+            for lv, (a, b) in level_sweeps.items():
+                flat[2 * (lv % len(levels))], flat[2 * (lv % len(levels)) + 1] = a, b
+            ls = (C.c_int * len(flat))(*flat)
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct, int(mixed_precision))
+                     coarse_omega, coarse_direct, int(mixed_precision), ls)
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
 

@@ -59,17 +59,23 @@ def test_cavity_q2_bdf2_step_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k", [1, 2])
-def test_multigrid_preconditioner(k):
+@pytest.mark.parametrize("k,variant", [(1, "default"), (2, "default"), (2, "bench")])
+def test_multigrid_preconditioner(k, variant):
     """GMRES + geometric multigrid V-cycle (gls_mg_attach) reaches the same Newton solution as
-    GMRES + Jacobi, in far fewer iterations (mesh-independent)."""
+    GMRES + Jacobi, in far fewer iterations (mesh-independent). "bench": bench.py's hierarchy --
+    FP32 smoothing, 2+2 sweeps on the level above an exact LU solve of the 2^3-cell coarsest level
+    (gls_mg_params.level_sweeps)."""
     import torch
     import bench
     from softx_2020_200_amd.problem import CavityProblem
     n = 16
     out = {}
+    opts = {}
+    if variant == "bench":
+        opts = dict(mg_coarsest=2, pre_smooth=1, post_smooth=1, omega=0.9, mixed_precision=True,
+                    level_sweeps={-2: (2, 2)})
     for mg in (False, True):
-        prob = CavityProblem(dim=3, n=n, k=k, viscosity=0.01, multigrid=mg)
+        prob = CavityProblem(dim=3, n=n, k=k, viscosity=0.01, multigrid=mg, **(opts if mg else {}))
         ctx = prob.ctx
         ctx.set_time("bdf2", (0.01,) * 4)
         m1 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.0)).cuda()
