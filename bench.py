@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--mg-coarsest", type=int, default=0,
                     help="cells per direction of the coarsest level (0: 2 on one GPU -- exact LU solve of its "
                          "500 DoFs --, 4 with Jacobi sweeps across ranks)")
+    ap.add_argument("--mg-fine-sweeps", type=int, nargs=2, default=None, metavar=("PRE", "POST"),
+                    help="sweeps on the finest level (default: --mg-smooth)")
     ap.add_argument("--mg-coarse-level-sweeps", type=int, default=2,
                     help="pre = post sweeps on the level above an exact coarsest solve")
     ap.add_argument("--mg-smooth", type=int, nargs=2, default=(1, 1), metavar=("PRE", "POST"),
@@ -166,7 +168,9 @@ def main():
     from softx_2020_200_amd.problem import CavityProblem
     if args.mg_coarsest == 0:
         args.mg_coarsest = 2 if world == 1 else 4
-    lsweeps = {-2: (args.mg_coarse_level_sweeps,) * 2} if world == 1 and args.mg_coarse_direct >= 0 else None
+    lsweeps = {-2: (args.mg_coarse_level_sweeps,) * 2} if world == 1 and args.mg_coarse_direct >= 0 else {}
+    if args.mg_fine_sweeps:
+        lsweeps[0] = tuple(args.mg_fine_sweeps)
     t_setup = time.perf_counter()
     dev = torch.device("cuda", local)
     ts = (args.dt,) * 4
@@ -300,7 +304,7 @@ def main():
                                % (args.k, args.kp, args.n),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
-                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
+                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if -2 in lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
                    "parallelism": "domain decomposition x%d (RCCL P2P ghosts)" % world if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,

@@ -43,7 +43,30 @@
 #define GLS_BRICK_WPE_F32 6  // FP32 kernels: 80 VGPRs, 6 waves/SIMD (1.96 -> 1.92 ms; 7 waves spill, 2.45 ms)
 #endif
 
+#ifndef GLS_LDS_SPLIT
+#define GLS_LDS_SPLIT 0  // 1 asm / 2 masked: FP64 LDS reads as single ds_read_b64 -- measured slower (profiles/r02_lds_split_ab.txt)
+#endif
+
 namespace gls {
+
+// One LDS read that the backend may not pair with another (GLS_LDS_SPLIT): ds_read2_b64 moves 16 B
+// per lane in 8 LDS cycles (4 x 16-lane groups per access, MI355X_MICROARCH.md §LDS) where two
+// ds_read_b64 take 2 + 2. Splitting every pair cuts SQ_LDS_IDX_ACTIVE of the cached J.v 37 % and
+// its bank conflicts 64 %, but costs one or two VALU address ops per load and spills at 4 waves /
+// SIMD: 3.18 -> 4.17 ms (4 waves, spills) / 3.50 ms (3 waves) at 128^3
+// (profiles/r02_lds_split_ab.txt), so the default keeps the compiler's pairing.
+template <typename T>
+__device__ __forceinline__ T lds(const T *p, unsigned zm) {
+  if constexpr (sizeof(T) == 8 && GLS_LDS_SPLIT) {
+    typedef __attribute__((address_space(3))) const T lds_t;
+    unsigned a = (unsigned)(uintptr_t)(lds_t *)p;
+    if constexpr (GLS_LDS_SPLIT == 1) asm volatile("" : "+v"(a));
+    else a += a & zm;
+    return *(lds_t *)(uintptr_t)a;
+  } else {
+    return *p;
+  }
+}
 
 template <int K>
 struct BrickCfg {
@@ -135,6 +158,7 @@ template <int K, int MODE, typename Real = double>
 __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
                                   (std::is_same<Real, float>::value ? GLS_BRICK_WPE_F32 : GLS_BRICK_WAVES_PER_EU))
     gls_brick_kernel(const OpParams P, const Tables1D T) {
+  const unsigned zm = (unsigned)(P.n_cells >> 31);  // 0 (n_cells >= 0), opaque to the compiler
   using C = BrickCfg<K>;
   constexpr int K1 = C::K1, N3 = C::N3, BN = C::BN, BN3 = C::BN3, CPW = C::CPW;
   constexpr bool JV = MODE == MODE_JV || MODE == MODE_JVQ;
@@ -263,7 +287,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   auto row = [&](int mat, int r, Real (&o)[K1]) {  // o[k] = M[r][k], mat: 0 V, 1 D, 2 S, 3 V^T, 4 D^T
     const Real *m = sM + mat * 16 + r * 4;
 #pragma unroll
-    for (int k = 0; k < K1; ++k) o[k] = m[k];
+    for (int k = 0; k < K1; ++k) o[k] = lds(m + k, zm);
   };
   // this lane's rows of the x / y 1D matrices (V, D, S at i0 and i1): registers when GLS_ROWS_REG
   // is set for this precision (the sweeps are LDS-bound), else one LDS read per use
@@ -294,15 +318,15 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   // line of array A through this lane's element along dim D
   auto lineD0 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = A[e + K1 * (i1 + K1 * i2)];
+    for (int e = 0; e < K1; ++e) o[e] = lds(A + e + K1 * (i1 + K1 * i2), zm);
   };
   auto lineD1 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (e + K1 * i2)];
+    for (int e = 0; e < K1; ++e) o[e] = lds(A + i0 + K1 * (e + K1 * i2), zm);
   };
   auto lineD2 = [&](const Real *A, Real (&o)[K1]) {
 #pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = A[i0 + K1 * (i1 + K1 * e)];
+    for (int e = 0; e < K1; ++e) o[e] = lds(A + i0 + K1 * (i1 + K1 * e), zm);
   };
 
   // velocity-type field (value, grad, Laplacian): brick field f -> (val, g0, g1, g2, lap) for this lane
@@ -311,7 +335,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     if (pact) {  // x sweep: X_B, X_D, X_S at [i2][i1][i0]
       Real in[K1], r0[K1], r1[K1], r2[K1];  // every load of the stage before its stores
 #pragma unroll
-      for (int e = 0; e < K1; ++e) in[e] = BF(f)[bx_base + e];
+      for (int e = 0; e < K1; ++e) in[e] = lds(BF(f) + bx_base + e, zm);
       rowq(0, 0, r0);
       rowq(1, 0, r1);
       rowq(2, 0, r2);
@@ -358,10 +382,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       rowq(0, 0, rb);
       rowq(1, 0, rd);
 #pragma unroll
-      for (int e = 0; e < K1; ++e) in[e] = BF(fp)[bx_base + e];
+      for (int e = 0; e < K1; ++e) in[e] = lds(BF(fp) + bx_base + e, zm);
       for (int j = 0; j < nh; ++j)
 #pragma unroll
-        for (int e = 0; e < K1; ++e) ih_[j][e] = BF(fh0 + j)[bx_base + e];
+        for (int e = 0; e < K1; ++e) ih_[j][e] = lds(BF(fh0 + j) + bx_base + e, zm);
       X(pci, 0)[me] = dot(rb, in);
       X(pci, 1)[me] = dot(rd, in);
       for (int j = 0; j < nh; ++j) X(pci, 2 + j)[me] = dot(rb, ih_[j]);
@@ -526,10 +550,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
             const Real phi = b0 * b1 * b2;
             const Real g[3] = {D0[a0] * b1 * b2, b0 * d1 * b2, b0 * b1 * d2};
             const Real lap = S0[a0] * b1 * b2 + b0 * s1 * b2 + b0 * b1 * s2;
-            const Real uq[3] = {X(pci, 0)[qq], X(pci, 1)[qq], X(pci, 2)[qq]};
-            const Real gc[3] = {X(pci, 3)[qq], X(pci, 4)[qq], Yr(pci, 0)[qq]};
-            const Real tq = Yr(pci, 1)[qq], jw = Yr(pci, 5)[qq];
-            const Real Rq[3] = {Yr(pci, 2)[qq], Yr(pci, 3)[qq], Yr(pci, 4)[qq]};
+            const Real uq[3] = {lds(X(pci, 0) + qq, zm), lds(X(pci, 1) + qq, zm), lds(X(pci, 2) + qq, zm)};
+            const Real gc[3] = {lds(X(pci, 3) + qq, zm), lds(X(pci, 4) + qq, zm), lds(Yr(pci, 0) + qq, zm)};
+            const Real tq = lds(Yr(pci, 1) + qq, zm), jw = lds(Yr(pci, 5) + qq, zm);
+            const Real Rq[3] = {lds(Yr(pci, 2) + qq, zm), lds(Yr(pci, 3) + qq, zm), lds(Yr(pci, 4) + qq, zm)};
             const Real av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
             const Real g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
 #pragma unroll
@@ -667,7 +691,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
         for (int cx = 0; cx < 2; ++cx) {
           const int ax = Xn - K * cx;
           if (ax < 0 || ax > K) continue;
-          s += Out(cx + 2 * cy + 4 * cz, fld)[ax + K1 * (ay + K1 * az)];
+          s += lds(Out(cx + 2 * cy + 4 * cz, fld) + ax + K1 * (ay + K1 * az), zm);
         }
       }
     }
