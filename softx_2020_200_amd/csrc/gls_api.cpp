@@ -754,6 +754,16 @@ int dist_multidot(gls_ctx *c, const double *A, int64_t lda, int nk, const double
   return GLS_OK;
 }
 
+// a mixed-precision smoothing level gets the FP32 copy of its linearization from the same MODE_LIN
+// launch (workgroup brick kernel): no separate FP64 -> FP32 conversion pass over the linearization
+int lin_f32_target(gls_ctx *c, gls::OpParams &P) {
+  P.qdf = nullptr;
+  if (!c->smooth_f32 || !gls::brick_fused_jacobi_supported(c->k) || std::getenv("GLS_LIN_NO_F32")) return GLS_OK;
+  if (c->qdata32.n != c->qdata.n) GLS_TRY(c->qdata32.alloc(c->qdata.n));
+  P.qdf = c->qdata32.p;
+  return GLS_OK;
+}
+
 // J.v linearization (u, grad u, tau, R_s at every quadrature point), once per state
 int ensure_qdata(gls_ctx *c) {
   if (c->qd_valid) return GLS_OK;
@@ -761,12 +771,13 @@ int ensure_qdata(gls_ctx *c) {
   if (c->qdata.n != n) GLS_TRY(c->qdata.alloc(n));
   gls::OpParams P = make_params(c, true);
   P.qd = c->qdata.p;
+  GLS_TRY(lin_f32_target(c, P));
   {
     TimedLaunch t(c, 3);
     HIP_TRY(gls::launch_brick_kernel(c->k, gls::MODE_LIN, P, c->tables, c->stream));
   }
   c->qd_valid = true;
-  c->qd32_valid = false;
+  c->qd32_valid = P.qdf != nullptr;
   return GLS_OK;
 }
 
@@ -792,6 +803,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     const size_t nq = gls::brick_qdata_size(c->k, c->n_cells);
     if (c->qdata.n != nq) GLS_TRY(c->qdata.alloc(nq));
     P.qd = c->qdata.p;
+    GLS_TRY(lin_f32_target(c, P));
     mode = gls::MODE_LIN;
     lin_diag = true;
   }
@@ -823,7 +835,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
                                   (int64_t)c->hang.tm.n, c->stream));
   if (lin_diag) {  // the same launch stored the J.v linearization
     c->qd_valid = true;
-    c->qd32_valid = false;
+    c->qd32_valid = P.qdf != nullptr;
   }
   return GLS_OK;
 }
@@ -843,12 +855,12 @@ int ensure_diag(gls_ctx *c) {
 // w -= V[0..nk) h (h on device, nk <= 8) fused with host_out[k] = V_k . w_new (k < nk, when dots) and
 // host_out[dots ? nk : 0] = ||w_new||^2 over owned DoFs, reduced over ranks
 int dist_multiaxpy_dots(gls_ctx *c, double *w, const double *V, int64_t lda, int nk, const double *h, bool dots,
-                        double *host_out) {
+                        double *host_out, double scale = 1.0) {
   const int64_t n1 = c->dist.on ? 3 * c->dist.n_owned : c->n_dofs;
   const int64_t off2 = c->dist.on ? 3 * (int64_t)c->n_vnodes : 0;
   const int64_t n2 = c->dist.on ? c->dist.n_owned : 0;
   const int nd = dots ? nk + 1 : 1;
-  HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, c->scal.p, c->work.p,
+  HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, scale, c->scal.p, c->work.p,
                                   c->stream));
   if (c->dist.on) {
     HIP_TRY(hipMemcpyAsync(c->dist.red_buf, c->scal.p, sizeof(double) * nd, hipMemcpyDeviceToDevice, c->stream));
@@ -1223,7 +1235,8 @@ int ensure_qdata32(gls_ctx *g) {
 }
 // FP32 kernels write their brick-surface partial sums in FP32 (half the slab traffic; summed in FP64)
 bool slab_f32() { return std::getenv("GLS_SLAB_F64") == nullptr; }
-int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
+// rb != nullptr: y = rb - A v (the V-cycle's residual), fused into the kernels' stores on one rank
+int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr) {
   if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   GLS_TRY(ensure_diag(g));
   GLS_TRY(ensure_qdata32(g));
@@ -1233,6 +1246,9 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
   P.v = v;
   P.y = y;
   P.slab = brick_slab(g);
+  const bool fuse_rb = rb && P.slab && !g->dist.on && gls::brick_fused_jacobi_supported(g->k) &&
+                       std::getenv("GLS_MG_NO_FUSE") == nullptr;
+  P.rb = fuse_rb ? rb : nullptr;
   P.slabf = P.slab && slab_f32() && gls::brick_fused_jacobi_supported(g->k) ? reinterpret_cast<float *>(P.slab)
                                                                              : nullptr;
   if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
@@ -1244,15 +1260,19 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y) {
     TimedLaunch t(g, 5);
     HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
                                    (int64_t)g->sum_nodes.n, g->n_vnodes, y, nullptr, nullptr, nullptr, 0.0,
-                                   g->stream));
+                                   g->stream, P.rb));
   }
   GLS_TRY(dist_export_add(g, y));
-  HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream));
+  HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream, P.rb));
+  if (rb && !fuse_rb) HIP_TRY(gls::vec_axpby(y, 1.0, rb, -1.0, g->n_dofs, g->stream));
   return GLS_OK;
 }
-int smoother_apply(gls_ctx *g, const double *v, double *y) {
-  if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y);
-  return gls_jacobian_apply(g, v, y);
+// y = A v with the level's smoothing operator; rb != nullptr: y = rb - A v
+int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nullptr) {
+  if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y, rb);
+  GLS_TRY(gls_jacobian_apply(g, v, y));
+  if (rb) HIP_TRY(gls::vec_axpby(y, 1.0, rb, -1.0, g->n_dofs, g->stream));
+  return GLS_OK;
 }
 // one damped-Jacobi sweep x <- x + omega D^-1 (b - A x) with the smoother's operator A (constrained
 // rows D_c x). Single rank on the brick path: fused into the J.v (brick-interior nodes) and the slab
@@ -1589,8 +1609,12 @@ int mg_restrict(gls_ctx *c, int l, const double *y, double *bc) {
   return GLS_OK;
 }
 
-// y (level l) = P xc (xc on level l+1; its ghost values are imported first)
-int mg_prolong(gls_ctx *c, int l, double *xc, double *y) {
+// y (level l) = P xc (xc on level l+1; its ghost values are imported first); add: y += P xc
+// (single rank, two-pass transfer only: the caller checks mg_prolong_add_ok)
+bool mg_prolong_add_ok(gls_ctx *c, int l) {
+  return !c->mg.boxed && c->mg.taps[(size_t)l]->two_pass && std::getenv("GLS_MG_NO_FUSE") == nullptr;
+}
+int mg_prolong(gls_ctx *c, int l, double *xc, double *y, bool add = false) {
   auto &mg = c->mg;
   gls_ctx *h = mg.lev[(size_t)l + 1];
   hipStream_t s = c->stream;
@@ -1603,7 +1627,9 @@ int mg_prolong(gls_ctx *c, int l, double *xc, double *y) {
     const double *tw[3] = {T.pw[0].p, T.pw[1].p, T.pw[2].p};
     if (T.two_pass)
       HIP_TRY(gls::mg_transfer_2pass(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), 0, ti, tw,
-                                     tc, mg.xwork.p, s));
+                                     tc, mg.xwork.p, s, add ? 1 : 0));
+    else if (add)
+      return set_err(GLS_EINVAL, "mg_prolong: accumulate needs the two-pass transfer");
     else
       HIP_TRY(gls::mg_transfer3d(xb, mg_box_target(c, l, y), mg.dims[l + 1].data(), mg.dims[l].data(), ti, tw, tc, s));
   }
@@ -1719,8 +1745,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
   if (pre > 0) {
-    GLS_TRY(smoother_apply(g, x, y));
-    HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, n, s));  // y = b - A x
+    GLS_TRY(smoother_apply(g, x, y, b));  // y = b - A x
   } else {
     HIP_TRY(gls::vec_copy(y, b, n, s));  // x = 0: the residual is b
   }
@@ -1729,10 +1754,17 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   GLS_TRY(mg_restrict(c, l, y, bc));
   HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
   GLS_TRY(mg_vcycle(c, l + 1, bc, xc));
-  // prolongate the coarse correction (ghost values imported first)
-  GLS_TRY(mg_prolong(c, l, xc, y));
-  HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
-  HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
+  // prolongate the coarse correction (ghost values imported first). x += P xc in the transfer's
+  // store on one rank: the coarse correction vanishes on the coarse Dirichlet rows (zero rhs rows,
+  // D_c-scaled sweeps) and the nested Qk interpolation maps them onto the fine Dirichlet rows, so
+  // P xc is exactly 0 there, as the zeroing below makes it in the general path
+  if (mg_prolong_add_ok(c, l)) {
+    GLS_TRY(mg_prolong(c, l, xc, x, true));
+  } else {
+    GLS_TRY(mg_prolong(c, l, xc, y));
+    HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
+    HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
+  }
   for (int it = 0; it < mg.lpost[(size_t)l]; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega));
   return GLS_OK;
 }
@@ -2060,6 +2092,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hcol[i];
       HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
       double wn2, wnorm;
+      bool normalized = false;  // w already scaled to v_{j+1} (H(j+1, j) set) by the fused DGKS pass
       if (j + 1 <= 8) {
         // projection fused with the DGKS dots and the norm: one pass over V instead of three
         GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, true, hc2.data()));
@@ -2067,8 +2100,21 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
         if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation with the dots of the fused pass
           for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hc2[i];
           HIP_TRY(hipMemcpyAsync(c->coef.p, hc2.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
-          GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2));
-          wnorm = std::sqrt(std::max(wn2, 0.0));
+          // ||w''||^2 = ||w'||^2 - |V^T w'|^2 (V orthonormal): the correction pass also normalises,
+          // v_{j+1} = w'' / est, and H(j+1, j) = est keeps A z_j = V H exactly (|v_{j+1}| = 1 + O(eps))
+          double h2 = 0.;
+          for (int i = 0; i <= j; ++i) h2 += hc2[i] * hc2[i];
+          const double est2 = wnorm * wnorm - h2;
+          if (est2 > 0.25 * wnorm * wnorm && est2 > 0.) {
+            const double est = std::sqrt(est2);
+            GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2, 1.0 / est));
+            H[(size_t)(j + 1) * m + j] = est;
+            normalized = true;
+            wnorm = est * std::sqrt(std::max(wn2, 0.0));
+          } else {
+            GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2));
+            wnorm = std::sqrt(std::max(wn2, 0.0));
+          }
         }
       } else {
         HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
@@ -2083,8 +2129,10 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
           wnorm = std::sqrt(std::max(wn2, 0.0));
         }
       }
-      H[(size_t)(j + 1) * m + j] = wnorm;
-      if (wnorm > 0) HIP_TRY(gls::vec_scale(w, 1.0 / wnorm, n, s));
+      if (!normalized) {
+        H[(size_t)(j + 1) * m + j] = wnorm;
+        if (wnorm > 0) HIP_TRY(gls::vec_scale(w, 1.0 / wnorm, n, s));
+      }
       // Givens
       for (int i = 0; i < j; ++i) {
         const double a = H[(size_t)i * m + j], bb = H[(size_t)(i + 1) * m + j];

@@ -505,6 +505,18 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       qdw[12 * QW] = tau;
 #pragma unroll
       for (int c = 0; c < 3; ++c) qdw[(13 + c) * QW] = R[c];
+      if constexpr (std::is_same<Real, double>::value) {
+        if (P.qdf) {  // the mixed-precision smoother's FP32 copy, written from registers
+          float *qf = P.qdf + (qdw - P.qd);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) __builtin_nontemporal_store((float)u[c], qf + c * QW);
+#pragma unroll
+          for (int c = 0; c < 9; ++c) __builtin_nontemporal_store((float)gu[c / 3][c % 3], qf + (3 + c) * QW);
+          __builtin_nontemporal_store((float)tau, qf + 12 * QW);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) __builtin_nontemporal_store((float)R[c], qf + (13 + c) * QW);
+        }
+      }
     }
     if (P.y == nullptr) return;  // linearization only (uniform over the block)
     // Jacobian diagonal from the same linearization (replaces the dense MODE_DIAG kernel): for the
@@ -705,6 +717,8 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
         const bool con = fld < 3 && P.vmask && ((P.vmask[node] >> fld) & 1u);
         const double x = P.jx[gi], dd = P.jd[gi];
         P.jx[gi] = x + P.jomega * (P.jb[gi] - (con ? dd * x : (double)s)) / dd;
+      } else if (MODE == MODE_JVQ && P.rb) {
+        Yout[gi] = P.rb[gi] - (double)s;
       } else {
         Yout[gi] = s;
       }
@@ -843,7 +857,8 @@ template <typename S, bool J>
 __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict__ nodes,
                            const int32_t *__restrict__ off, const int32_t *__restrict__ slots, int64_t n_sum,
                            int64_t voff, double *__restrict__ y, const uint8_t *__restrict__ vmask,
-                           const double *__restrict__ jb, const double *__restrict__ jd, double jomega) {
+                           const double *__restrict__ jb, const double *__restrict__ jd, double jomega,
+                           const double *__restrict__ rb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
   double s[4] = {0., 0., 0., 0.};
@@ -865,29 +880,34 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
       y[gi[f]] = x + jomega * (jb[gi[f]] - ((f < 3 && ((m >> f) & 1u)) ? dd * x : s[f])) / dd;
     }
   } else {
+    if (rb) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) y[gi[f]] = s[f];
+      for (int f = 0; f < 4; ++f) y[gi[f]] = rb[gi[f]] - s[f];
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) y[gi[f]] = s[f];
+    }
   }
 }
 hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_t *off, const int32_t *slots,
                           int64_t n_sum, int64_t n_vnodes, double *y, hipStream_t s) {
   if (n_sum <= 0) return hipSuccess;
   hipLaunchKernelGGL((k_slab_sum<double, false>), dim3((unsigned)((n_sum + 255) / 256)), dim3(256), 0, s, slab, nodes,
-                     off, slots, n_sum, 3 * n_vnodes, y, nullptr, nullptr, nullptr, 0.0);
+                     off, slots, n_sum, 3 * n_vnodes, y, nullptr, nullptr, nullptr, 0.0, nullptr);
   return hipGetLastError();
 }
 hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32_t *nodes, const int32_t *off,
                              const int32_t *slots, int64_t n_sum, int64_t n_vnodes, double *y, const uint8_t *vmask,
-                             const double *jb, const double *jd, double jomega, hipStream_t s) {
+                             const double *jb, const double *jd, double jomega, hipStream_t s, const double *rb) {
   if (n_sum <= 0) return hipSuccess;
   const dim3 g((unsigned)((n_sum + 255) / 256)), b(256);
   const int64_t voff = 3 * n_vnodes;
   if (slabf) {
-    if (jb) hipLaunchKernelGGL((k_slab_sum<float, true>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
-    else hipLaunchKernelGGL((k_slab_sum<float, false>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+    if (jb) hipLaunchKernelGGL((k_slab_sum<float, true>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega, rb);
+    else hipLaunchKernelGGL((k_slab_sum<float, false>), g, b, 0, s, slabf, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega, rb);
   } else {
-    if (jb) hipLaunchKernelGGL((k_slab_sum<double, true>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
-    else hipLaunchKernelGGL((k_slab_sum<double, false>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega);
+    if (jb) hipLaunchKernelGGL((k_slab_sum<double, true>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega, rb);
+    else hipLaunchKernelGGL((k_slab_sum<double, false>), g, b, 0, s, slab, nodes, off, slots, n_sum, voff, y, vmask, jb, jd, jomega, rb);
   }
   return hipGetLastError();
 }

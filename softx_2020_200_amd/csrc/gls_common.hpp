@@ -66,6 +66,8 @@ struct OpParams {
   double *jx;
   const double *jb, *jd;
   double jomega;
+  // residual form (MODE_JVQ brick kernels, no jx): y = rb - A v instead of y = A v (nullptr: off)
+  const double *rb;
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs
   double alpha_jac;           // mass coefficient of the Jacobian (bdf[0] / sdirk[0][0])

@@ -27,7 +27,8 @@ hipError_t brick_slab_sum(const double *slab, const int32_t *nodes, const int32_
 // y holds x and is updated x <- x + jomega (jb - A x) / jd, rows in vmask use (A x)_i = jd_i x_i)
 hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32_t *nodes, const int32_t *off,
                              const int32_t *slots, int64_t n_sum, int64_t n_vnodes, double *y, const uint8_t *vmask,
-                             const double *jb, const double *jd, double jomega, hipStream_t s);
+                             const double *jb, const double *jd, double jomega, hipStream_t s,
+                             const double *rb = nullptr);  // rb (no jb): y = rb - A x
 bool brick_fused_jacobi_supported(int k);  // the selected brick kernel honours OpParams::jx and ::slabf
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
@@ -55,15 +56,15 @@ hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const 
 // w -= sign * sum_k h[k] A[k] (nk <= 8, h on device), fused with out[k] = A[k] . w_new (k < nk, when
 // dots) and out[dots ? nk : 0] = ||w_new||^2, both over the owned rows [0, n1) U [off2, off2 + n2)
 hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
-                              int64_t n1, int64_t off2, int64_t n2, bool dots, double *out, double *work,
-                              hipStream_t s);
+                              int64_t n1, int64_t off2, int64_t n2, bool dots, double scale, double *out,
+                              double *work, hipStream_t s);
 // hanging-node constraint lines (CSR): distribute x[dof] = sum w src[master]; condense onto masters
 hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, const int64_t *off,
                               const int64_t *master, const double *w, int64_t n, hipStream_t s);
 hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
                             int64_t n, hipStream_t s);
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
-                                hipStream_t s);  // y[idx] = d[idx]*v[idx]
+                                hipStream_t s, const double *rb = nullptr);  // y[idx] = d[idx]*v[idx] (rb: rb[idx] - d v)
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();
 
@@ -90,7 +91,7 @@ hipError_t mg_transfer3d(const double *in, double *out, const int nin[3], const 
 // larger) doubles. tile_fits: host check that a per-axis tap table (axis 0/1) fits the kernel's tiles.
 hipError_t mg_transfer_2pass(const double *in, double *out, const int nin[3], const int nout[3], int restrict_,
                              const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
-                             double *work, hipStream_t s);
+                             double *work, hipStream_t s, int add = 0);  // add (prolongation): out += P in
 int mg_transfer_tile_fits(int restrict_, int axis, int n_out, const int32_t *taps, const int32_t *cnt);
 hipError_t mg_box_gather(const double *loc, double *box, const int32_t *map, int64_t nbox, int64_t nvl,
                          int64_t n_owned, hipStream_t s);  // n_owned < 0: all nodes

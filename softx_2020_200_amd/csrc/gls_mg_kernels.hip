@@ -71,7 +71,8 @@ __global__ void __launch_bounds__(256) k_transfer_xy(const double *__restrict__ 
                                                      int i1, int o0, int o1, int nz, int zb,
                                                      const int32_t *__restrict__ tx, const double *__restrict__ wx,
                                                      const int32_t *__restrict__ cx, const int32_t *__restrict__ ty,
-                                                     const double *__restrict__ wy, const int32_t *__restrict__ cy) {
+                                                     const double *__restrict__ wy, const int32_t *__restrict__ cy,
+                                                     int add) {
   __shared__ double s_in[4][IYM][IXM + 1];
   __shared__ double s_t1[4][IYM][OX + 1];
   __shared__ int s_xi[OX][kMaxTaps], s_yi[OY][kMaxTaps], s_xc[OX], s_yc[OY];
@@ -158,14 +159,16 @@ __global__ void __launch_bounds__(256) k_transfer_xy(const double *__restrict__ 
       if (o >= nox) continue;
       double s = 0.0;
       for (int b = 0; b < s_yc[oy]; ++b) s += s_yw[oy][b] * s_t1[f][s_yi[oy][b] - loy][o];
-      out[3 * (pout + (int64_t)(oy0 + oy) * o0 + ox0) + r] = s;
+      double *o_ = out + 3 * (pout + (int64_t)(oy0 + oy) * o0 + ox0) + r;
+      *o_ = add ? *o_ + s : s;
     }
     for (int e = tid; e < noy * OX; e += 256) {
       const int oy = e / OX, o = e - oy * OX;
       if (o >= nox) continue;
       double s = 0.0;
       for (int b = 0; b < s_yc[oy]; ++b) s += s_yw[oy][b] * s_t1[3][s_yi[oy][b] - loy][o];
-      out[3 * nout + pout + (int64_t)(oy0 + oy) * o0 + ox0 + o] = s;
+      double *o_ = out + 3 * nout + pout + (int64_t)(oy0 + oy) * o0 + ox0 + o;
+      *o_ = add ? *o_ + s : s;
     }
   }
 }
@@ -193,11 +196,11 @@ __global__ void __launch_bounds__(256) k_transfer_z(const double *__restrict__ i
 template <int OX, int OY, int IXM, int IYM>
 hipError_t launch_transfer_xy(const double *in, double *out, int i0, int i1, int o0, int o1, int nz,
                               const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
-                              hipStream_t s) {
+                              hipStream_t s, int add = 0) {
   const int nb = ((o0 + OX - 1) / OX) * ((o1 + OY - 1) / OY);
   const int zb = nz >= 64 ? 8 : (nz >= 16 ? 4 : 1);  // planes per block (prefetch pipeline depth)
   hipLaunchKernelGGL((k_transfer_xy<OX, OY, IXM, IYM>), dim3(nb, (nz + zb - 1) / zb), dim3(256), 0, s, in, out, i0, i1,
-                     o0, o1, nz, zb, taps[0], w[0], cnt[0], taps[1], w[1], cnt[1]);
+                     o0, o1, nz, zb, taps[0], w[0], cnt[0], taps[1], w[1], cnt[1], add);
   return hipGetLastError();
 }
 
@@ -399,7 +402,7 @@ int mg_transfer_tile_fits(int restrict_, int axis, int n_out, const int32_t *tap
 
 hipError_t mg_transfer_2pass(const double *in, double *out, const int nin[3], const int nout[3], int restrict_,
                              const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
-                             double *work, hipStream_t s) {
+                             double *work, hipStream_t s, int add) {
   if (restrict_) {  // xy (fine planes -> coarse xy), then z
     const hipError_t e = launch_transfer_xy<kRestrictTile[0], kRestrictTile[1], kRestrictIn[0], kRestrictIn[1]>(
         in, work, nin[0], nin[1], nout[0], nout[1], nin[2], taps, w, cnt, s);
@@ -409,7 +412,7 @@ hipError_t mg_transfer_2pass(const double *in, double *out, const int nin[3], co
   const hipError_t e = launch_transfer_z(in, work, (int64_t)nin[0] * nin[1], nin[2], nout[2], taps[2], w[2], cnt[2], s);
   if (e != hipSuccess) return e;
   return launch_transfer_xy<kProlongTile[0], kProlongTile[1], kProlongIn[0], kProlongIn[1]>(
-      work, out, nin[0], nin[1], nout[0], nout[1], nout[2], taps, w, cnt, s);
+      work, out, nin[0], nin[1], nout[0], nout[1], nout[2], taps, w, cnt, s, add);
 }
 
 hipError_t mg_inject(const double *fine, double *coarse, const int nf[3], const int nc[3], hipStream_t s) {

@@ -102,14 +102,15 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy(double *__restrict__ w, co
   }
 }
 
-// w -= sign * sum_k h[k] A[k]; in the same pass the partial sums of A[k] . w_new (DOTS) and
-// ||w_new||^2 over the owned rows [0, n1) U [off2, off2 + n2) -> work[d * gridDim + block]
-// (the fused classical Gram-Schmidt step: projection + the re-orthogonalisation dots + norm)
+// w = scale * (w - sign * sum_k h[k] A[k]); in the same pass the partial sums of A[k] . w_new (DOTS)
+// and ||w_new||^2 over the owned rows [0, n1) U [off2, off2 + n2) -> work[d * gridDim + block]
+// (the fused classical Gram-Schmidt step: projection + the re-orthogonalisation dots + norm; with
+// scale != 1 also the normalisation of the new Krylov vector)
 template <int NK, bool DOTS>
 __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w, const double *__restrict__ A,
                                                           int64_t lda, const double *__restrict__ h, double sign,
                                                           int64_t n, int64_t n1, int64_t off2, int64_t n2,
-                                                          double *work) {
+                                                          double scale, double *work) {
   constexpr int ND = (DOTS ? NK : 0) + 1;
   double hk[NK], acc[ND];
 #pragma unroll
@@ -123,6 +124,7 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
     double s = w[i];
 #pragma unroll
     for (int k = 0; k < NK; ++k) s -= hk[k] * a[k];
+    s *= scale;
     w[i] = s;
     if (i < n1 || (i >= off2 && i < off2 + n2)) {
       if constexpr (DOTS) {
@@ -170,10 +172,11 @@ __global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const 
   }
 }
 
-__global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m) {
+__global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
+                                   const double *rb) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = idx[j];
-    y[i] = d[i] * v[i];
+    y[i] = rb ? rb[i] - d[i] * v[i] : d[i] * v[i];
   }
 }
 __global__ void k_pack_nodes(const double *__restrict__ x, const int32_t *__restrict__ nodes, int64_t m, int64_t voff,
@@ -275,7 +278,7 @@ hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const 
 }
 
 hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
-                              int64_t n1, int64_t off2, int64_t n2, bool dots, double *out, double *work,
+                              int64_t n1, int64_t off2, int64_t n2, bool dots, double scale, double *out, double *work,
                               hipStream_t s) {
   if (nk < 1 || nk > kDotChunk) return hipErrorInvalidValue;
   const int nb = grid_for(n);
@@ -283,11 +286,11 @@ hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, c
 #define MX(M)                                                                                                         \
   case 2 * M:                                                                                                         \
     hipLaunchKernelGGL((k_multiaxpy_dot<M, false>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2, \
-                       work);                                                                                         \
+                       scale, work);                                                                                         \
     break;                                                                                                            \
   case 2 * M + 1:                                                                                                     \
     hipLaunchKernelGGL((k_multiaxpy_dot<M, true>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2,  \
-                       work);                                                                                         \
+                       scale, work);                                                                                         \
     break;
     MX(1) MX(2) MX(3) MX(4) MX(5) MX(6) MX(7) MX(8)
 #undef MX
@@ -310,9 +313,9 @@ hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, c
 }
 
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
-                                hipStream_t s) {
+                                hipStream_t s, const double *rb) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gather_scale_set, dim3(grid_for(m)), dim3(kBlock), 0, s, y, d, v, idx, m);
+  hipLaunchKernelGGL(k_gather_scale_set, dim3(grid_for(m)), dim3(kBlock), 0, s, y, d, v, idx, m, rb);
   return hipGetLastError();
 }
 hipError_t vec_pack_nodes(const double *x, const int32_t *nodes, int64_t m, int64_t voff, double *buf, hipStream_t s) {
