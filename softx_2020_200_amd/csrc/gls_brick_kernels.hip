@@ -43,11 +43,29 @@
 #define GLS_BRICK_WPE_F32 6  // FP32 kernels: 80 VGPRs, 6 waves/SIMD (1.96 -> 1.92 ms; 7 waves spill, 2.45 ms)
 #endif
 
+#ifndef GLS_QD_LITE
+// 1: the cached J.v linearization holds tau and R_s only (4 values per quadrature point); MODE_JVQ
+// gathers u with v and re-derives u and grad u by value + gradient sweeps (bit-identical to the
+// values MODE_LIN computes). 0: u, grad u, tau, R_s cached (16 values, the round-1 layout).
+#define GLS_QD_LITE 0
+#endif
+
+#ifndef GLS_STAGE_LAYOUT
+// stage-array layout per kernel (StageLayout): bit 0 FP64 J.v from the cache, bit 1 FP32 J.v, bit 2
+// residual, bit 3 linearization / recompute J.v; set = oriented lines read with ds_read_b128, clear =
+// natural [z][y][x] arrays read element-wise. Measured at Q2 128^3 (profiles/r02_stage_layout_ab.txt):
+// FP64 J.v 3.16 -> 3.00 ms; FP32 J.v 2.01 -> 2.17 ms and residual 3.48 -> 3.74 ms (spills), so 1.
+#define GLS_STAGE_LAYOUT 1
+#endif
+
 #ifndef GLS_LDS_SPLIT
 #define GLS_LDS_SPLIT 0  // 1 asm / 2 masked: FP64 LDS reads as single ds_read_b64 -- measured slower (profiles/r02_lds_split_ab.txt)
 #endif
 
 namespace gls {
+
+constexpr bool kQdLite = GLS_QD_LITE != 0;
+constexpr int kQDataBrick = kQdLite ? 4 : kQData;  // values per quadrature point in the brick layout
 
 // One LDS read that the backend may not pair with another (GLS_LDS_SPLIT): ds_read2_b64 moves 16 B
 // per lane in 8 LDS cycles (4 x 16-lane groups per access, MI355X_MICROARCH.md §LDS) where two
@@ -79,8 +97,41 @@ struct BrickCfg {
   static constexpr int CPW = 64 / N3 >= 2 ? 2 : 1;  // cells per wave (Q1: 8 q -> could be 8; keep 2)
   static constexpr int WAVES = 8 / CPW;      // waves per workgroup (one brick)
   static constexpr int THREADS = 64 * WAVES;
-  static constexpr int NX = 5, NY = 6, NO = 4;  // per-cell LDS arrays: X, Y, out
-  static constexpr int PER_CELL = NX + NY + NO;
+  static constexpr int BN3P = (BN3 + 3) & ~3;  // brick field stride (keeps the stage arrays 16-B aligned)
+  static constexpr int NO = 4;  // per-cell test-field outputs (natural [z][y][x] order, N3 each)
+};
+
+// Per-cell sweep-stage arrays in LDS. Each array is stored in the orientation its reader sweeps:
+// the lane's K1-element line along that dim is contiguous and 16-B aligned, so it is read with
+// ds_read_b128 (4 LDS cycles per 16 B per wave) instead of K1 scalar reads that the backend pairs
+// into ds_read2_b64 (8 cycles per 16 B; MI355X_MICROARCH.md §LDS).
+//  * FP64, K1 = 3 ("pair" layout): arrays come in pairs (slots 2p, 2p+1); a pair block holds the
+//    (e0, e1) halves of both arrays' 9 lines (16 B each, at 0 and A0) and one half-plane at H1 whose
+//    line L holds (e2 of slot 2p, e2 of slot 2p+1): a line costs 1.5 ds_read_b128 and no padding.
+//  * FP32 K1 = 3 (lines padded to 4 floats) and K1 = 2: one vector read per line.
+// The cell stride puts the two cells of a wave on disjoint banks (conflict-free b128 reads under
+// the lane-group model of MI355X_MICROARCH.md §LDS; checked offline for every orientation).
+template <int K, typename Real, int MODE>
+struct StageLayout {
+  static constexpr bool CACHED = MODE == MODE_JVQ;
+  static constexpr int K1 = K + 1, N3 = K1 * K1 * K1;
+  static constexpr int BIT = CACHED ? (sizeof(Real) == 8 ? 1 : 2) : (MODE == MODE_RESIDUAL ? 4 : 8);
+  static constexpr bool ORIENTED = (GLS_STAGE_LAYOUT & BIT) != 0;  // else natural arrays
+  static constexpr bool PAIR = ORIENTED && sizeof(Real) == 8 && K1 == 3;
+  static constexpr int LP = K1 == 3 ? 4 : K1;            // padded line length (non-pair layouts)
+  static constexpr int NXA = CACHED ? 4 : 5, NYA = CACHED ? 4 : 6;  // X / Y arrays in flight
+  static constexpr int XP = (NXA + 1) / 2, YP = (NYA + 1) / 2;
+  static constexpr int YB = PAIR ? 2 * XP : NXA;        // slot of Y array 0
+  static constexpr int A0 = 18, H1 = 44, PB = 62;       // pair block: halves at 0 / A0, e2 plane at H1
+  static constexpr int AS = ORIENTED ? K1 * K1 * LP : N3;  // array size (non-pair layouts)
+  static constexpr int SR0 = PAIR ? (XP + YP) * PB : (NXA + NYA) * AS;
+  static constexpr int SR = (!CACHED && SR0 < 11 * N3) ? 11 * N3 : SR0;  // MODE_LIN's diagonal: 11 plain arrays
+  static constexpr int stride(int v) {
+    if (PAIR) { while (v % 32 != 18) ++v; }
+    else if (ORIENTED && K1 == 3) { while (v % 64 != 40) ++v; }
+    return v;
+  }
+  static constexpr int CS = stride(SR);  // per-cell stride (elements)
 };
 
 // rank of brick-lattice node (X, Y, Z) among the brick-boundary nodes (lexicographic, x fastest):
@@ -164,20 +215,22 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   constexpr bool JV = MODE == MODE_JV || MODE == MODE_JVQ;
   constexpr bool CACHED = MODE == MODE_JVQ;  // linearization read from P.qd (no state sweeps)
   constexpr bool LIN = MODE == MODE_LIN;     // store the linearization to P.qd, no integration
-  // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]; JVQ: v0 v1 v2 vp only
-  constexpr int NF = CACHED ? 4 : (JV ? 11 : 7);
-  constexpr int FV = CACHED ? 0 : 7;         // first v field
+  // brick fields: u0 u1 u2 p H0 H1 H2 [v0 v1 v2 vp]; JVQ: [u0 u1 u2] v0 v1 v2 vp
+  constexpr int NF = CACHED ? (kQdLite ? 7 : 4) : (JV ? 11 : 7);
+  constexpr int FV = CACHED ? (kQdLite ? 3 : 0) : 7;  // first v field
+  using SL = StageLayout<K, Real, MODE>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Real *const smem = reinterpret_cast<Real *>(smem_raw);
-  Real *sB = smem;                                   // [NF][BN3]
-  Real *sC = sB + NF * BN3;                          // [8][PER_CELL][N3]
+  Real *sB = smem;                                   // [NF][BN3P]
+  Real *sC = sB + NF * C::BN3P;                      // [8][CS] stage arrays (StageLayout)
+  Real *sO = sC + 8 * SL::CS;                        // [8][NO][N3]
   // 1D tables [V, D, S, V^T, D^T][4][4], w[4], xi[4] in a SEPARATE shared object: the compiler then
   // knows table reads never alias the stage arrays, so it can issue them ahead of a stage's stores
   // (in the dynamic array every row read after an X store waited for it: serialized LDS latency)
   __shared__ Real sTab[5 * 16 + 8];
   Real *const sM = sTab;
-  int *sNode = reinterpret_cast<int *>(sC + 8 * C::PER_CELL * N3);  // [BN3]
-  auto BF = [&](int f) { return sB + f * BN3; };
+  int *sNode = reinterpret_cast<int *>(sO + 8 * C::NO * N3);  // [BN3]
+  auto BF = [&](int f) { return sB + f * C::BN3P; };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -209,9 +262,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     sM[tid] = j < K1 ? (tid < 84 ? T.w[j] : T.xi[j]) : 0.0;
   }
   // ---------------- gather the brick's nodes (all waves)
-  constexpr int NG = CACHED ? 1 : (JV ? 3 : 2);  // gather groups: state (u, p) | history | v
+  // gather groups: state (u, p) | history | v;  JVQ: [u (no p)] | v
+  constexpr int NG = CACHED ? (kQdLite ? 2 : 1) : (JV ? 3 : 2);
   for (int t = tid; t < NG * BN3; t += blockDim.x) {
-    const int g = CACHED ? 2 : t / BN3, n = t % BN3;
+    const int g = CACHED ? ((kQdLite && t < BN3) ? 0 : 2) : t / BN3, n = t % BN3;
     if (GLS_ABL & 1) {
       for (int f = 0; f < NF; ++f) BF(f)[n] = 0.001 * (n + f);
       if (g == 0 || CACHED) sNode[n] = (brick * 37 + n) % P.n_vnodes;
@@ -227,7 +281,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       BF(0)[n] = P.u[i3];
       BF(1)[n] = P.u[i3 + 1];
       BF(2)[n] = P.u[i3 + 2];
-      BF(3)[n] = P.u[voff + node];
+      if (!CACHED) BF(3)[n] = P.u[voff + node];
     } else if (g == 1) {
       Real h[3] = {0., 0., 0.};
 #pragma unroll
@@ -258,9 +312,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   __syncthreads();
 
   // ---------------- per-wave: cells 2*wave, 2*wave+1 of the brick
-  auto X = [&](int ci, int s) { return sC + (ci * C::PER_CELL + s) * N3; };
-  auto Yr = [&](int ci, int s) { return sC + (ci * C::PER_CELL + C::NX + s) * N3; };
-  auto Out = [&](int ci, int f) { return sC + (ci * C::PER_CELL + C::NX + C::NY + f) * N3; };
+  auto Out = [&](int ci, int f) { return sO + (ci * C::NO + f) * N3; };
   const int cbase = wave * CPW;
   // pointwise lane mapping: lane -> (cell, q)
   const bool pact = lane < CPW * N3;
@@ -315,18 +367,59 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     for (int k = 0; k < K1; ++k) s += a[k] * b[k];
     return s;
   };
-  // line of array A through this lane's element along dim D
-  auto lineD0 = [&](const Real *A, Real (&o)[K1]) {
-#pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = lds(A + e + K1 * (i1 + K1 * i2), zm);
+  // Stage arrays (StageLayout): slot g (X arrays 0.., Y arrays SL::YB..) stored d-oriented: the
+  // lane's line along dim d (index ln[d], element = the lane's coordinate along d) is contiguous.
+  Real *const cellS = sC + pci * SL::CS;
+  const int ln[3] = {i1 + K1 * i2, i0 + K1 * i2, i0 + K1 * i1};
+  const int co[3] = {i0, i1, i2};
+  auto wr = [&](int g, int d, Real val) {  // this lane's element of slot g in the d-oriented layout
+    if constexpr (SL::PAIR) {
+      // one store per lane at a selected offset (no divergent store pair)
+      const int off = co[d] < 2 ? (g & 1) * SL::A0 + 2 * ln[d] + co[d] : SL::H1 + 2 * ln[d] + (g & 1);
+      cellS[(g >> 1) * SL::PB + off] = val;
+    } else if constexpr (SL::ORIENTED) {
+      cellS[g * SL::AS + ln[d] * SL::LP + co[d]] = val;
+    } else {
+      cellS[g * SL::AS + me] = val;
+    }
   };
-  auto lineD1 = [&](const Real *A, Real (&o)[K1]) {
+  auto rdl = [&](int g, int d, Real (&o)[K1]) {  // the lane's whole line of slot g along dim d
+    if constexpr (SL::PAIR) {
+      typedef double v2 __attribute__((ext_vector_type(2)));
+      const Real *b = cellS + (g >> 1) * SL::PB;
+      const v2 a = *reinterpret_cast<const v2 *>(b + (g & 1) * SL::A0 + 2 * ln[d]);
+      const v2 t = *reinterpret_cast<const v2 *>(b + SL::H1 + 2 * ln[d]);
+      o[0] = a.x;
+      o[1] = a.y;
+      o[2] = (g & 1) ? t.y : t.x;
+      return;
+    }
+    if constexpr (!SL::ORIENTED) {  // natural [z][y][x]: K1 element reads along dim d
+      const Real *a = cellS + g * SL::AS;
+      const int st = d == 0 ? 1 : (d == 1 ? K1 : K1 * K1);
+      const int b0 = me - co[d] * st;
 #pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = lds(A + i0 + K1 * (e + K1 * i2), zm);
-  };
-  auto lineD2 = [&](const Real *A, Real (&o)[K1]) {
-#pragma unroll
-    for (int e = 0; e < K1; ++e) o[e] = lds(A + i0 + K1 * (i1 + K1 * e), zm);
+      for (int e = 0; e < K1; ++e) o[e] = lds(a + b0 + e * st, zm);
+      return;
+    }
+    const Real *p = cellS + g * SL::AS + ln[d] * SL::LP;
+    if constexpr (std::is_same<Real, double>::value) {
+      typedef double v2 __attribute__((ext_vector_type(2)));
+      const v2 a = *reinterpret_cast<const v2 *>(p);
+      o[0] = a.x;
+      o[1] = a.y;
+    } else if constexpr (K1 == 3) {
+      typedef float v4 __attribute__((ext_vector_type(4)));
+      const v4 a = *reinterpret_cast<const v4 *>(p);
+      o[0] = a.x;
+      o[1] = a.y;
+      o[2] = a.z;
+    } else {
+      typedef float v2 __attribute__((ext_vector_type(2)));
+      const v2 a = *reinterpret_cast<const v2 *>(p);
+      o[0] = a.x;
+      o[1] = a.y;
+    }
   };
 
   // velocity-type field (value, grad, Laplacian): brick field f -> (val, g0, g1, g2, lap) for this lane
@@ -340,31 +433,31 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       rowq(1, 0, r1);
       rowq(2, 0, r2);
       const Real o0 = dot(r0, in), o1 = dot(r1, in), o2 = dot(r2, in);
-      X(pci, 0)[me] = o0;
-      X(pci, 1)[me] = o1;
-      X(pci, 2)[me] = o2;
+      wr(0, 1, o0);
+      wr(1, 1, o1);
+      wr(2, 1, o2);
     }
     wave_sync();
     if (pact) {  // y sweep: BB, BD, DB, L = wy S_y(X_B) + wx B_y(X_S)
       Real xb[K1], xd[K1], xs[K1], rb[K1], rd[K1], rs[K1];
-      lineD1(X(pci, 0), xb);
-      lineD1(X(pci, 1), xd);
-      lineD1(X(pci, 2), xs);
+      rdl(0, 1, xb);
+      rdl(1, 1, xd);
+      rdl(2, 1, xs);
       rowq(0, 1, rb);
       rowq(1, 1, rd);
       rowq(2, 1, rs);
-      Yr(pci, 0)[me] = dot(rb, xb);
-      Yr(pci, 1)[me] = dot(rd, xb);
-      Yr(pci, 2)[me] = dot(rb, xd);
-      Yr(pci, 3)[me] = ih[1] * ih[1] * dot(rs, xb) + ih[0] * ih[0] * dot(rb, xs);
+      wr(SL::YB + 0, 2, dot(rb, xb));
+      wr(SL::YB + 1, 2, dot(rd, xb));
+      wr(SL::YB + 2, 2, dot(rb, xd));
+      wr(SL::YB + 3, 2, ih[1] * ih[1] * dot(rs, xb) + ih[0] * ih[0] * dot(rb, xs));
     }
     wave_sync();
     if (pact) {  // z sweep fused into the pointwise read
       Real bb[K1], bd[K1], db[K1], ll[K1];
-      lineD2(Yr(pci, 0), bb);
-      lineD2(Yr(pci, 1), bd);
-      lineD2(Yr(pci, 2), db);
-      lineD2(Yr(pci, 3), ll);
+      rdl(SL::YB + 0, 2, bb);
+      rdl(SL::YB + 1, 2, bd);
+      rdl(SL::YB + 2, 2, db);
+      rdl(SL::YB + 3, 2, ll);
       val = dot(Bz, bb);
       g[0] = dot(Bz, db) * ih[0];
       g[1] = dot(Bz, bd) * ih[1];
@@ -386,35 +479,35 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       for (int j = 0; j < nh; ++j)
 #pragma unroll
         for (int e = 0; e < K1; ++e) ih_[j][e] = lds(BF(fh0 + j) + bx_base + e, zm);
-      X(pci, 0)[me] = dot(rb, in);
-      X(pci, 1)[me] = dot(rd, in);
-      for (int j = 0; j < nh; ++j) X(pci, 2 + j)[me] = dot(rb, ih_[j]);
+      wr(0, 1, dot(rb, in));
+      wr(1, 1, dot(rd, in));
+      for (int j = 0; j < nh; ++j) wr(2 + j, 1, dot(rb, ih_[j]));
     }
     wave_sync();
     if (pact) {  // y: X0 -> BB (Y0), BD (Y1); X1 -> DB (Y2); X(2+j) -> Y(3+j)
       Real a[K1], a1[K1], rb[K1], rd[K1], ah[3][K1];
       rowq(0, 1, rb);
       rowq(1, 1, rd);
-      lineD1(X(pci, 0), a);
-      lineD1(X(pci, 1), a1);
-      for (int j = 0; j < nh; ++j) lineD1(X(pci, 2 + j), ah[j]);
-      Yr(pci, 0)[me] = dot(rb, a);
-      Yr(pci, 1)[me] = dot(rd, a);
-      Yr(pci, 2)[me] = dot(rb, a1);
-      for (int j = 0; j < nh; ++j) Yr(pci, 3 + j)[me] = dot(rb, ah[j]);
+      rdl(0, 1, a);
+      rdl(1, 1, a1);
+      for (int j = 0; j < nh; ++j) rdl(2 + j, 1, ah[j]);
+      wr(SL::YB + 0, 2, dot(rb, a));
+      wr(SL::YB + 1, 2, dot(rd, a));
+      wr(SL::YB + 2, 2, dot(rb, a1));
+      for (int j = 0; j < nh; ++j) wr(SL::YB + 3 + j, 2, dot(rb, ah[j]));
     }
     wave_sync();
     if (pact) {
       Real bb[K1], bd[K1], db[K1];
-      lineD2(Yr(pci, 0), bb);
-      lineD2(Yr(pci, 1), bd);
-      lineD2(Yr(pci, 2), db);
+      rdl(SL::YB + 0, 2, bb);
+      rdl(SL::YB + 1, 2, bd);
+      rdl(SL::YB + 2, 2, db);
       pv = dot(Bz, bb);
       pg[0] = dot(Bz, db) * ih[0];
       pg[1] = dot(Bz, bd) * ih[1];
       pg[2] = dot(Dz, bb) * ih[2];
       for (int j = 0; j < nh; ++j) {
-        lineD2(Yr(pci, 3 + j), bb);
+        rdl(SL::YB + 3 + j, 2, bb);
         hv[j] = dot(Bz, bb);
       }
     }
@@ -423,13 +516,13 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
 
   const Real nu = P.nu;
   const Real JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
-  // linearization storage: per wave CPW*N3 lanes x kQData values, value-major (coalesced)
+  // linearization storage: per wave CPW*N3 lanes x kQDataBrick values, value-major (coalesced)
   constexpr int QW = CPW * N3;
   Real *qdw = nullptr;
   if constexpr (std::is_same<Real, double>::value) {
-    if (P.qd) qdw = P.qd + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane;
+    if (P.qd) qdw = P.qd + ((int64_t)brick * C::WAVES + wave) * kQDataBrick * QW + lane;
   } else {
-    if (P.qdf) qdw = P.qdf + ((int64_t)brick * C::WAVES + wave) * kQData * QW + lane;
+    if (P.qdf) qdw = P.qdf + ((int64_t)brick * C::WAVES + wave) * kQDataBrick * QW + lane;
   }
 
   // ---------------- phase A: state at this lane's quadrature point
@@ -438,16 +531,22 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   // JVQ: the linearization is loaded after the v sweeps (short live ranges: no spills)
   auto load_qd = [&]() {
     if (GLS_ABL & 8) {  // timing-only: no linearization stream
+      if (!kQdLite) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) u[c] = JxW * (c + 1);
+        for (int c = 0; c < 3; ++c) u[c] = JxW * (c + 1);
 #pragma unroll
-      for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = hx * c;
+        for (int c = 0; c < 9; ++c) gu[c / 3][c % 3] = hx * c;
+      }
       tau = JxW;
 #pragma unroll
       for (int c = 0; c < 3; ++c) R[c] = hy * c;
       return;
     }
-    if (pact) {
+    if (pact && kQdLite) {  // u, grad u come from the u sweeps
+      tau = __builtin_nontemporal_load(qdw);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) R[c] = __builtin_nontemporal_load(qdw + (1 + c) * QW);
+    } else if (pact) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) u[c] = __builtin_nontemporal_load(qdw + c * QW);
 #pragma unroll
@@ -497,7 +596,19 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   }  // !CACHED
 
   if constexpr (LIN) {  // store the linearization; the integration below is J.v's (MODE_JVQ)
-    if (pact) {
+    if (pact && kQdLite) {
+      qdw[0] = tau;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) qdw[(1 + c) * QW] = R[c];
+      if constexpr (std::is_same<Real, double>::value) {
+        if (P.qdf) {  // the mixed-precision smoother's FP32 copy, written from registers
+          float *qf = P.qdf + (qdw - P.qd);
+          __builtin_nontemporal_store((float)tau, qf);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) __builtin_nontemporal_store((float)R[c], qf + (1 + c) * QW);
+        }
+      }
+    } else if (pact) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) qdw[c * QW] = u[c];
 #pragma unroll
@@ -524,18 +635,19 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     //   J_ii(c) = sum_q JxW [A phi + nu |grad phi|^2 + tau (A - nu lap phi) a + tau R_c phi d_c phi],
     //   A = (du_c/dx_c + alpha_jac) phi + a,  a = u . grad phi;   J_ii(p) = sum_q JxW tau |grad psi|^2
     // with deal.II's |K_e(i,i)| on constrained rows. Lane <-> node i of its cell, loop over q.
+    auto Nat = [&](int s) { return cellS + s * N3; };  // plain [z][y][x] arrays over the stage region
     if (pact) {
-      X(pci, 0)[me] = u[0];
-      X(pci, 1)[me] = u[1];
-      X(pci, 2)[me] = u[2];
-      X(pci, 3)[me] = gu[0][0] + P.alpha_jac;
-      X(pci, 4)[me] = gu[1][1] + P.alpha_jac;
-      Yr(pci, 0)[me] = gu[2][2] + P.alpha_jac;
-      Yr(pci, 1)[me] = tau;
-      Yr(pci, 2)[me] = R[0];
-      Yr(pci, 3)[me] = R[1];
-      Yr(pci, 4)[me] = R[2];
-      Yr(pci, 5)[me] = JxW;
+      Nat(0)[me] = u[0];
+      Nat(1)[me] = u[1];
+      Nat(2)[me] = u[2];
+      Nat(3)[me] = gu[0][0] + P.alpha_jac;
+      Nat(4)[me] = gu[1][1] + P.alpha_jac;
+      Nat(5)[me] = gu[2][2] + P.alpha_jac;
+      Nat(6)[me] = tau;
+      Nat(7)[me] = R[0];
+      Nat(8)[me] = R[1];
+      Nat(9)[me] = R[2];
+      Nat(10)[me] = JxW;
     }
     wave_sync();
     if (pact) {
@@ -562,10 +674,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
             const Real phi = b0 * b1 * b2;
             const Real g[3] = {D0[a0] * b1 * b2, b0 * d1 * b2, b0 * b1 * d2};
             const Real lap = S0[a0] * b1 * b2 + b0 * s1 * b2 + b0 * b1 * s2;
-            const Real uq[3] = {lds(X(pci, 0) + qq, zm), lds(X(pci, 1) + qq, zm), lds(X(pci, 2) + qq, zm)};
-            const Real gc[3] = {lds(X(pci, 3) + qq, zm), lds(X(pci, 4) + qq, zm), lds(Yr(pci, 0) + qq, zm)};
-            const Real tq = lds(Yr(pci, 1) + qq, zm), jw = lds(Yr(pci, 5) + qq, zm);
-            const Real Rq[3] = {lds(Yr(pci, 2) + qq, zm), lds(Yr(pci, 3) + qq, zm), lds(Yr(pci, 4) + qq, zm)};
+            const Real uq[3] = {lds(Nat(0) + qq, zm), lds(Nat(1) + qq, zm), lds(Nat(2) + qq, zm)};
+            const Real gc[3] = {lds(Nat(3) + qq, zm), lds(Nat(4) + qq, zm), lds(Nat(5) + qq, zm)};
+            const Real tq = lds(Nat(6) + qq, zm), jw = lds(Nat(10) + qq, zm);
+            const Real Rq[3] = {lds(Nat(7) + qq, zm), lds(Nat(8) + qq, zm), lds(Nat(9) + qq, zm)};
             const Real av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
             const Real g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
 #pragma unroll
@@ -607,6 +719,10 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     for (int c = 0; c < 3; ++c) vel_field(FV + c, v[c], gv[c], lv[c]);
     Real vp = 0., gvp[3] = {0., 0., 0.}, dummy[3];
     scal_fields(FV + 3, 0, 0, vp, gvp, dummy);
+    if constexpr (CACHED && kQdLite) {  // u, grad u: value + gradient sweeps of the gathered u
+#pragma unroll
+      for (int c = 0; c < 3; ++c) scal_fields(c, 0, 0, u[c], gu[c], dummy);
+    }
     if constexpr (CACHED) load_qd();
     const Real aj = P.alpha_jac;
     Real S[3], A[3];
@@ -649,36 +765,36 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   for (int fld = 0; fld < 4; ++fld) {
     if (GLS_ABL & 4) { if (pact) Out(pci, fld)[me] = Tc[4 * fld] + Tc[4 * fld + 1] + Tc[4 * fld + 2] + Tc[4 * fld + 3]; continue; }
     if (pact) {
-      X(pci, 0)[me] = Tc[4 * fld];
-      X(pci, 1)[me] = Tc[4 * fld + 1];
-      X(pci, 2)[me] = Tc[4 * fld + 2];
-      X(pci, 3)[me] = Tc[4 * fld + 3];
+      wr(0, 2, Tc[4 * fld]);
+      wr(1, 2, Tc[4 * fld + 1]);
+      wr(2, 2, Tc[4 * fld + 2]);
+      wr(3, 2, Tc[4 * fld + 3]);
     }
     wave_sync();
     if (pact) {  // transposed z (output index az = i2): Z0 = B^T Tv + D^T Tz, Z1 = B^T Tx, Z2 = B^T Ty
       Real tv[K1], tx[K1], ty[K1], tz[K1];
-      lineD2(X(pci, 0), tv);
-      lineD2(X(pci, 1), tx);
-      lineD2(X(pci, 2), ty);
-      lineD2(X(pci, 3), tz);
-      Yr(pci, 0)[me] = dot(cb2, tv) + dot(cd2, tz);
-      Yr(pci, 1)[me] = dot(cb2, tx);
-      Yr(pci, 2)[me] = dot(cb2, ty);
+      rdl(0, 2, tv);
+      rdl(1, 2, tx);
+      rdl(2, 2, ty);
+      rdl(3, 2, tz);
+      wr(SL::YB + 0, 1, dot(cb2, tv) + dot(cd2, tz));
+      wr(SL::YB + 1, 1, dot(cb2, tx));
+      wr(SL::YB + 2, 1, dot(cb2, ty));
     }
     wave_sync();
     if (pact) {  // transposed y (ay = i1): W0 = B^T Z0 + D^T Z2, W1 = B^T Z1
       Real z0[K1], z1[K1], z2[K1];
-      lineD1(Yr(pci, 0), z0);
-      lineD1(Yr(pci, 1), z1);
-      lineD1(Yr(pci, 2), z2);
-      X(pci, 0)[me] = dot(cb1, z0) + dot(cd1, z2);
-      X(pci, 1)[me] = dot(cb1, z1);
+      rdl(SL::YB + 0, 1, z0);
+      rdl(SL::YB + 1, 1, z1);
+      rdl(SL::YB + 2, 1, z2);
+      wr(0, 0, dot(cb1, z0) + dot(cd1, z2));
+      wr(1, 0, dot(cb1, z1));
     }
     wave_sync();
     if (pact) {  // transposed x (ax = i0): out = B^T W0 + D^T W1
       Real w0[K1], w1[K1];
-      lineD0(X(pci, 0), w0);
-      lineD0(X(pci, 1), w1);
+      rdl(0, 0, w0);
+      rdl(1, 0, w1);
       Out(pci, fld)[me] = dot(cb0, w0) + dot(cd0, w1);
     }
     wave_sync();
@@ -735,14 +851,18 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
 template <int K, typename Real = double>
 size_t brick_lds_bytes(int mode) {
   using C = BrickCfg<K>;
-  const int NF = mode == MODE_JVQ ? 4 : (mode == MODE_JV ? 11 : 7);
-  return sizeof(Real) * ((size_t)NF * C::BN3 + (size_t)8 * C::PER_CELL * C::N3) + sizeof(int) * (size_t)C::BN3;
+  const bool cached = mode == MODE_JVQ;
+  const int NF = cached ? (kQdLite ? 7 : 4) : (mode == MODE_JV ? 11 : 7);
+  const size_t cs = mode == MODE_JVQ ? StageLayout<K, Real, MODE_JVQ>::CS
+                    : (mode == MODE_RESIDUAL ? StageLayout<K, Real, MODE_RESIDUAL>::CS
+                                             : StageLayout<K, Real, MODE_LIN>::CS);
+  return sizeof(Real) * ((size_t)NF * C::BN3P + (size_t)8 * cs + (size_t)8 * C::NO * C::N3) + sizeof(int) * (size_t)C::BN3;
 }
 
 template <int K>
 size_t brick_qdata_doubles(int n_cells) {
   using C = BrickCfg<K>;
-  return (size_t)(n_cells / 8) * C::WAVES * kQData * C::CPW * C::N3;
+  return (size_t)(n_cells / 8) * C::WAVES * kQDataBrick * C::CPW * C::N3;
 }
 
 template <int K>
