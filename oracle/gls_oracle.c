@@ -326,7 +326,16 @@ typedef struct {
   double *grad_p;  /* [nq][nd][3] */
   double *JxW;     /* [nq] */
   double *xq;      /* [nq][3] */
+  /* reference-cell tables (FEValues' precomputed shape data; affine cells scale them by 1/h):
+   * per (q, scalar shape a): value, d/dxi_d, d2/dxi_d2 of the velocity (k) and pressure (kp) bases */
+  double *rv, *rg, *rs;   /* [nq][nv], [nq][nv][3], [nq][nv][3] */
+  double *rpv, *rpg;      /* [nq][np], [nq][np][3] */
 } cell_tab;
+
+/* timing path only (gls_oracle_time_local_systems): 1 = reference-cell tables, as deal.II's FEValues
+ * precomputes them; the values are bit-identical to the per-cell tabulation */
+static int g_fast_tables = 0;
+void gls_oracle_set_fast_tables(int on) { g_fast_tables = on; }
 
 static void tab_alloc(cell_tab *t, const gls_oracle_problem *p) {
   t->dim = p->dim;
@@ -343,10 +352,52 @@ static void tab_alloc(cell_tab *t, const gls_oracle_problem *p) {
   t->grad_p = calloc(nqd * 3, sizeof(double));
   t->JxW = calloc(t->nq, sizeof(double));
   t->xq = calloc((size_t)t->nq * 3, sizeof(double));
+  t->rv = t->rg = t->rs = t->rpv = t->rpg = NULL;
+  if (g_fast_tables && !p->map_degree) {
+    const int dim = p->dim, nq1 = p->nq1d;
+    double xq1[MAXN], wq1[MAXN], xnv[MAXN], xnp[MAXN];
+    gauss_1d(nq1, xq1, wq1);
+    lobatto_1d(p->k, xnv);
+    lobatto_1d(p->kp, xnp);
+    t->rv = calloc((size_t)t->nq * t->nv, sizeof(double));
+    t->rg = calloc((size_t)t->nq * t->nv * 3, sizeof(double));
+    t->rs = calloc((size_t)t->nq * t->nv * 3, sizeof(double));
+    t->rpv = calloc((size_t)t->nq * t->np, sizeof(double));
+    t->rpg = calloc((size_t)t->nq * t->np * 3, sizeof(double));
+    for (int q = 0; q < t->nq; ++q) {
+      int qi[3] = {q % nq1, (q / nq1) % nq1, q / (nq1 * nq1)};
+      double xi[3] = {0, 0, 0};
+      for (int d = 0; d < dim; ++d) xi[d] = xq1[qi[d]];
+      for (int pass = 0; pass < 2; ++pass) {
+        const int kk = pass ? p->kp : p->k, na = pass ? t->np : t->nv;
+        const double *xn = pass ? xnp : xnv;
+        for (int a = 0; a < na; ++a) {
+          int ai[3] = {a % (kk + 1), (a / (kk + 1)) % (kk + 1), a / ((kk + 1) * (kk + 1))};
+          double L[3], dL[3], ddL[3];
+          for (int d = 0; d < dim; ++d) {
+            L[d] = lag(kk, xn, ai[d], xi[d]);
+            dL[d] = lag_d(kk, xn, ai[d], xi[d]);
+            ddL[d] = lag_dd(kk, xn, ai[d], xi[d]);
+          }
+          double v = 1.;
+          for (int d = 0; d < dim; ++d) v *= L[d];
+          (pass ? t->rpv : t->rv)[(size_t)q * na + a] = v;
+          for (int d = 0; d < dim; ++d) {
+            double g = dL[d], ss = ddL[d];
+            for (int e = 0; e < dim; ++e)
+              if (e != d) { g *= L[e]; ss *= L[e]; }
+            (pass ? t->rpg : t->rg)[((size_t)q * na + a) * 3 + d] = g;
+            if (!pass) t->rs[((size_t)q * na + a) * 3 + d] = ss;
+          }
+        }
+      }
+    }
+  }
 }
 static void tab_free(cell_tab *t) {
   free(t->phi_u); free(t->grad_u); free(t->lap_u); free(t->div_u);
   free(t->phi_p); free(t->grad_p); free(t->JxW); free(t->xq);
+  free(t->rv); free(t->rg); free(t->rs); free(t->rpv); free(t->rpg);
 }
 
 /* scalar Qk shape function on the reference cell: value, gradient, Hessian (d/dxi) */
@@ -450,7 +501,24 @@ static void tab_fill(cell_tab *t, const gls_oracle_problem *p, int cell) {
       t->div_u[o] = 0.;
       t->phi_p[o] = 0.;
       double val, grad[3], lap;
-      if (kk < dim * t->nv) {
+      if (t->rv && kk < dim * t->nv) {  /* reference-cell tables scaled to the box (shape_eval's order) */
+        int a = kk / dim, c = kk % dim;
+        const size_t ra = (size_t)q * t->nv + a;
+        t->phi_u[o * 3 + c] = t->rv[ra];
+        double lp = 0.;
+        for (int e = 0; e < dim; ++e) {
+          const double ge = t->rg[ra * 3 + e] / h[e];
+          t->grad_u[o * 9 + c * 3 + e] = ge;
+          lp += t->rs[ra * 3 + e] / (h[e] * h[e]);
+        }
+        t->lap_u[o * 3 + c] = lp;
+        t->div_u[o] = t->grad_u[o * 9 + c * 3 + c];
+      } else if (t->rv) {
+        int a = kk - dim * t->nv;
+        const size_t ra = (size_t)q * t->np + a;
+        t->phi_p[o] = t->rpv[ra];
+        for (int e = 0; e < dim; ++e) t->grad_p[o * 3 + e] = t->rpg[ra * 3 + e] / h[e];
+      } else if (kk < dim * t->nv) {
         int a = kk / dim, c = kk % dim;
         if (p->map_degree) shape_mapped(dim, p->k, xnv, a, xi, Ji, Hx, &val, grad, &lap);
         else shape_eval(dim, p->k, xnv, a, xi, h, &val, grad, &lap);

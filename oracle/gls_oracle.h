@@ -121,6 +121,7 @@ int gls_oracle_sdirk_coefficients(int order, double dt, double *out);
 
 /* CPU baseline: compute local systems of cells [c0, c0+count) with nthreads OpenMP threads;
  * returns a checksum so the work cannot be elided. */
+void gls_oracle_set_fast_tables(int on); /* timing path: reference-cell tables (bit-identical) */
 double gls_oracle_time_local_systems(const gls_oracle_problem *p,
                                      const double *u, const double *u1, const double *u2, const double *u3,
                                      int c0, int count, int with_matrix, int nthreads);
