@@ -307,6 +307,18 @@ struct gls_ctx {
   bool use_slab = false;
   DevBuf<double> slab;
   DevBuf<int32_t> sum_nodes, sum_off, sum_slots;
+  // colored brick launches (opt-in GLS_BRICK_COLORS=1): bricks greedily colored in Morton order so
+  // that no two bricks of a color share a node (the 2x2x2 parity classes on a brick lattice: 8
+  // colors); surface-node sums carried across colors in acc, no slab and no k_slab_sum. Measured
+  // slower at Q2 128^3 (profiles/r02_brick_colors_ab.txt: J.v 3.66 vs 3.00 + 0.55 ms, FP32 3.18 vs
+  // 2.44 + 0.45 ms): a color's bricks are not neighbours, so the surface nodes neighbouring bricks
+  // share are fetched again from HBM by the later colors instead of hitting L2.
+  bool use_colors = false;
+  int n_colors = 0;
+  int color_off[17] = {0};
+  DevBuf<int32_t> color_bricks;
+  DevBuf<uint16_t> ncolor;
+  DevBuf<double> acc;  // running sums for the fused Jacobi sweep (which stores x, not A x)
   // distributed (rank-local mesh): owned nodes [0, n_owned), ghosts after; exchange via callbacks
   struct Dist {
     bool on = false;
@@ -507,6 +519,7 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   }
   std::vector<int32_t> slots((size_t)(nb * nbnd)), fill(start.begin(), start.end() - 1);
   for (int64_t sl = 0; sl < nb * nbnd; ++sl) slots[(size_t)fill[(size_t)slot_node[(size_t)sl]]++] = (int32_t)sl;
+  const std::vector<int32_t> slots_by_node = slots;  // node n's slots at [start[n], start[n+1])
   // sum order: nodes by their first (lowest) slot, i.e. in slab order of their lowest brick, so
   // that consecutive threads of k_slab_sum read consecutive slab entries (node order would leave
   // the x-face nodes of every brick row 4 lattice points apart: 2.3x read amplification, PMC)
@@ -531,7 +544,51 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   GLS_TRY(c->sum_off.upload(off.data(), off.size()));
   GLS_TRY(c->sum_slots.upload(slots.data(), slots.size()));
   c->use_slab = true;
+  // brick coloring: greedy in brick (Morton) order over the bricks sharing a surface node
+  if (!gls::brick_colors_supported(K) || !std::getenv("GLS_BRICK_COLORS")) return GLS_OK;
+  std::vector<int> color((size_t)nb, -1);
+  int ncol = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    uint32_t used = 0;
+    for (int j = 0; j < nbnd; ++j) {
+      const int32_t node = slot_node[(size_t)(b * nbnd + j)];
+      for (int32_t t = start[(size_t)node]; t < start[(size_t)node + 1]; ++t) {
+        const int64_t ob = slots_by_node[(size_t)t] / nbnd;
+        if (ob != b && color[(size_t)ob] >= 0) used |= 1u << color[(size_t)ob];
+      }
+    }
+    int col = 0;
+    while (col < 32 && ((used >> col) & 1u)) ++col;
+    if (col >= 16) return GLS_OK;  // more than 16 colors: keep the slab path
+    color[(size_t)b] = col;
+    ncol = std::max(ncol, col + 1);
+  }
+  std::vector<uint16_t> ncm((size_t)d->n_vnodes, 0);
+  for (int64_t sl = 0; sl < nb * nbnd; ++sl) ncm[(size_t)slot_node[(size_t)sl]] |= (uint16_t)(1u << color[(size_t)(sl / nbnd)]);
+  std::vector<int32_t> order;
+  order.reserve((size_t)nb);
+  c->color_off[0] = 0;
+  for (int col = 0; col < ncol; ++col) {
+    for (int64_t b = 0; b < nb; ++b)
+      if (color[(size_t)b] == col) order.push_back((int32_t)b);
+    c->color_off[col + 1] = (int)order.size();
+  }
+  GLS_TRY(c->color_bricks.upload(order.data(), order.size()));
+  GLS_TRY(c->ncolor.upload(ncm.data(), ncm.size()));
+  c->n_colors = ncol;
+  c->use_colors = true;
   return GLS_OK;
+}
+
+// colored brick launch: surface-node sums carried in acc (y, or scratch for the fused Jacobi sweep)
+void set_colors(gls_ctx *c, gls::OpParams &P, double *acc) {
+  P.bricks = c->color_bricks.p;
+  P.ncolor = c->ncolor.p;
+  P.acc = acc;
+  P.n_colors = c->n_colors;
+  for (int i = 0; i <= c->n_colors; ++i) P.color_off[i] = c->color_off[i];
+  P.slab = nullptr;
+  P.slabf = nullptr;
 }
 
 // brick launch output: slab (allocated on first use) or nullptr (atomics into a zeroed y)
@@ -818,14 +875,16 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   P.y = y;
   P.hmask = c->hang.on ? c->hang.hmask.p : nullptr;
   const bool brick = c->use_brick && mode != gls::MODE_DIAG;
-  P.slab = brick ? brick_slab(c) : nullptr;  // every node is then written exactly once: no zeroing
-  if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
+  const bool col = brick && c->use_colors;
+  if (col) set_colors(c, P, y);  // every node is written exactly once: no zeroing, no slab sum
+  else P.slab = brick ? brick_slab(c) : nullptr;
+  if (!col && !P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
     if (brick) HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     else HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
-  if (brick && P.slab) {
+  if (brick && !col && P.slab) {
     TimedLaunch t(c, 5);
     HIP_TRY(slab_sum(c, y));
   }
@@ -1245,13 +1304,15 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
   P.qdf = g->qdata32.p;
   P.v = v;
   P.y = y;
-  P.slab = brick_slab(g);
-  const bool fuse_rb = rb && P.slab && !g->dist.on && gls::brick_fused_jacobi_supported(g->k) &&
+  const bool col = g->use_colors;
+  P.slab = col ? nullptr : brick_slab(g);
+  const bool fuse_rb = rb && (P.slab || col) && !g->dist.on && gls::brick_fused_jacobi_supported(g->k) &&
                        std::getenv("GLS_MG_NO_FUSE") == nullptr;
   P.rb = fuse_rb ? rb : nullptr;
   P.slabf = P.slab && slab_f32() && gls::brick_fused_jacobi_supported(g->k) ? reinterpret_cast<float *>(P.slab)
                                                                              : nullptr;
-  if (!P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
+  if (col) set_colors(g, P, y);
+  if (!col && !P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
   {
     TimedLaunch t(g, 4);
     HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
@@ -1279,8 +1340,8 @@ int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nu
 // sum (brick-surface nodes), so A x is never stored; otherwise smoother_apply + mg_jacobi_update.
 int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double omega) {
   const bool nofuse = std::getenv("GLS_MG_NO_FUSE") != nullptr;
-  const bool brick = g->use_brick && g->use_qdata && brick_slab(g) && !g->dist.on && !g->hang.on &&
-                     gls::brick_fused_jacobi_supported(g->k);
+  const bool brick = g->use_brick && g->use_qdata && (g->use_colors || brick_slab(g)) && !g->dist.on &&
+                     !g->hang.on && gls::brick_fused_jacobi_supported(g->k);
   if (nofuse || !brick) {
     GLS_TRY(smoother_apply(g, x, y));
     HIP_TRY(gls::mg_jacobi_update(x, b, y, g->diag.p, omega, g->n_dofs, 0, g->stream));
@@ -1297,10 +1358,15 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   P.jb = b;
   P.jd = g->diag.p;
   P.jomega = omega;
-  P.slab = brick_slab(g);
+  if (g->use_colors) {  // surface-node running sums in a scratch vector (x is updated in place)
+    if (g->acc.n != (size_t)g->n_dofs) GLS_TRY(g->acc.alloc((size_t)g->n_dofs));
+    set_colors(g, P, g->acc.p);
+  } else {
+    P.slab = brick_slab(g);
+  }
   if (f32) {
     P.qdf = g->qdata32.p;
-    P.slabf = slab_f32() ? reinterpret_cast<float *>(P.slab) : nullptr;
+    P.slabf = P.slab && slab_f32() ? reinterpret_cast<float *>(P.slab) : nullptr;
     TimedLaunch t(g, 4);
     HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
   } else {
@@ -1308,6 +1374,7 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
     TimedLaunch t(g, 1);
     HIP_TRY(gls::launch_brick_kernel(g->k, gls::MODE_JVQ, P, g->tables, g->stream));
   }
+  if (g->use_colors) return GLS_OK;
   TimedLaunch t(g, 5);
   HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
                                  (int64_t)g->sum_nodes.n, g->n_vnodes, x, g->vmask.p, b, g->diag.p, omega, g->stream));
@@ -1423,6 +1490,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   h.on = n > 0;
   c->use_brick = false;  // mixed cell sizes: the general per-cell kernels
   c->use_slab = false;
+  c->use_colors = false;
   c->diag_valid = false;
   c->qd_valid = false;
   return GLS_OK;
@@ -1674,6 +1742,7 @@ int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, dou
   hipStream_t s = c->stream;
   GLS_TRY(ensure_diag(g));
   GLS_TRY(g->smooth_f32 ? ensure_qdata32(g) : ensure_qdata(g));
+  if (g->use_colors && g->acc.n != (size_t)g->n_dofs) GLS_TRY(g->acc.alloc((size_t)g->n_dofs));  // no malloc in capture
   const bool tim = g->timing;
   g->timing = false;  // no event records inside the capture
   hipGraph_t gr = nullptr;

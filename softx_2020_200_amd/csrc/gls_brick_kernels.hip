@@ -239,12 +239,16 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   const int pj = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x / n_bricks) : 0;
   // XCD-aware order (blocks b, b+8, b+16, ... share an XCD): each XCD walks a contiguous Morton
   // range of bricks, so the nodes neighbouring bricks share stay in that XCD's L2
-  const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks) : xcd_swizzle((int)blockIdx.x, n_bricks);
+  const bool colored = P.bricks != nullptr && !(CACHED && P.n_probe > 0);
+  const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks)
+                    : colored ? P.bricks[P.color_off[P.color] +
+                                         xcd_swizzle((int)blockIdx.x, P.color_off[P.color + 1] - P.color_off[P.color])]
+                              : xcd_swizzle((int)blockIdx.x, n_bricks);
   const int64_t unit_dof = (CACHED && P.n_probe > 0) ? P.probe_base + pj : -1;
   double *const Yout = (CACHED && P.n_probe > 0)
                            ? P.y + (int64_t)pj * ((int64_t)3 * P.n_vnodes + P.n_vnodes) : P.y;
   const int64_t voff = (int64_t)3 * P.n_vnodes;
-  const bool use_slab = P.slab != nullptr && !(CACHED && P.n_probe > 0);
+  const bool use_slab = !colored && P.slab != nullptr && !(CACHED && P.n_probe > 0);
 
   if (tid < 5 * 16) {
     const int mat = tid >> 4, r = (tid >> 2) & 3, c = tid & 3;
@@ -826,18 +830,29 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     const int node = sNode[n];
     const int64_t gi = fld < 3 ? (int64_t)node * 3 + fld : voff + node;
     const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
+    auto complete = [&](double tot) {  // the node's full row: store it (or the fused update)
+      if (MODE == MODE_JVQ && P.jx) {  // fused damped-Jacobi sweep: no other brick reads this x later
+        const bool con = fld < 3 && P.vmask && ((P.vmask[node] >> fld) & 1u);
+        const double x = P.jx[gi], dd = P.jd[gi];
+        P.jx[gi] = x + P.jomega * (P.jb[gi] - (con ? dd * x : tot)) / dd;
+      } else if (MODE == MODE_JVQ && P.rb) {
+        Yout[gi] = P.rb[gi] - tot;
+      } else {
+        Yout[gi] = tot;
+      }
+    };
     if (GLS_ABL & 2) {
       if (s == Real(123.5)) Yout[gi] = s;
     } else if (interior) {
-      if (MODE == MODE_JVQ && P.jx) {  // fused damped-Jacobi sweep on this brick-owned node
-        const bool con = fld < 3 && P.vmask && ((P.vmask[node] >> fld) & 1u);
-        const double x = P.jx[gi], dd = P.jd[gi];
-        P.jx[gi] = x + P.jomega * (P.jb[gi] - (con ? dd * x : (double)s)) / dd;
-      } else if (MODE == MODE_JVQ && P.rb) {
-        Yout[gi] = P.rb[gi] - (double)s;
-      } else {
-        Yout[gi] = s;
-      }
+      if (MODE == MODE_JVQ && (P.jx || P.rb)) complete((double)s);
+      else Yout[gi] = s;
+    } else if (colored) {  // running sum across colors, in color order
+      const unsigned cm = P.ncolor[node];
+      const bool first = (cm & ((1u << P.color) - 1u)) == 0u, last = (cm >> (P.color + 1)) == 0u;
+      double tot = (double)s;
+      if (!first) tot += P.acc[gi];
+      if (last) complete(tot);
+      else P.acc[gi] = tot;
     } else if (use_slab) {  // brick-boundary node: this brick's partial sum, summed per node by k_slab_sum
       const int64_t si = ((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4 + fld;
       if (std::is_same<Real, float>::value && P.slabf) P.slabf[si] = (float)s;
@@ -871,14 +886,23 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   const int n_bricks = P.n_cells / 8;
   if (n_bricks <= 0) return hipSuccess;
   const size_t lds = brick_lds_bytes<K>(mode);
-  if (mode == MODE_JV)
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
-  else if (mode == MODE_JVQ)
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
-  else if (mode == MODE_LIN)
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_LIN>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
-  else
-    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(n_bricks), dim3(C::THREADS), lds, s, P, T);
+  const bool colored = P.bricks != nullptr && P.y != nullptr;  // MODE_LIN without y stores no rows
+  const int nc = colored ? P.n_colors : 1;
+  OpParams Q = P;
+  if (!colored) Q.bricks = nullptr;
+  for (int col = 0; col < nc; ++col) {
+    Q.color = col;
+    const int nb = colored ? P.color_off[col + 1] - P.color_off[col] : n_bricks;
+    if (nb <= 0) continue;
+    if (mode == MODE_JV)
+      hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(nb), dim3(C::THREADS), lds, s, Q, T);
+    else if (mode == MODE_JVQ)
+      hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ>), dim3(nb), dim3(C::THREADS), lds, s, Q, T);
+    else if (mode == MODE_LIN)
+      hipLaunchKernelGGL((gls_brick_kernel<K, MODE_LIN>), dim3(nb), dim3(C::THREADS), lds, s, Q, T);
+    else
+      hipLaunchKernelGGL((gls_brick_kernel<K, MODE_RESIDUAL>), dim3(nb), dim3(C::THREADS), lds, s, Q, T);
+  }
   return hipGetLastError();
 }
 
@@ -891,6 +915,7 @@ hipError_t launch_brick_probe_t(const OpParams &P0, const Tables1D &T, int64_t j
   OpParams P = P0;
   P.n_probe = nprobe;
   P.probe_base = j0;
+  P.bricks = nullptr;
   hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ>), dim3((unsigned)((int64_t)n_bricks * nprobe)), dim3(C::THREADS),
                      brick_lds_bytes<K>(MODE_JVQ), s, P, T);
   return hipGetLastError();
@@ -925,8 +950,15 @@ hipError_t launch_brick_jv_f32_t(const OpParams &P, const Tables1D &T, hipStream
   const int n_bricks = P.n_cells / 8;
   if (n_bricks <= 0) return hipSuccess;
   if (!P.qdf || P.n_probe > 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ, float>), dim3(n_bricks), dim3(C::THREADS),
-                     (brick_lds_bytes<K, float>(MODE_JVQ)), s, P, T);
+  const int nc = P.bricks ? P.n_colors : 1;
+  OpParams Q = P;
+  for (int col = 0; col < nc; ++col) {
+    Q.color = col;
+    const int nb = P.bricks ? P.color_off[col + 1] - P.color_off[col] : n_bricks;
+    if (nb <= 0) continue;
+    hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JVQ, float>), dim3(nb), dim3(C::THREADS),
+                       (brick_lds_bytes<K, float>(MODE_JVQ)), s, Q, T);
+  }
   return hipGetLastError();
 }
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s) {
@@ -1032,6 +1064,7 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
   return hipGetLastError();
 }
 bool brick_fused_jacobi_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
+bool brick_colors_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 
 size_t brick_qdata_size(int k, int n_cells) {
   if (brick_impl(k) == 1) return brick_wave_qdata_size(k, n_cells);

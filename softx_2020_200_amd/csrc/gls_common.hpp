@@ -68,6 +68,16 @@ struct OpParams {
   double jomega;
   // residual form (MODE_JVQ brick kernels, no jx): y = rb - A v instead of y = A v (nullptr: off)
   const double *rb;
+  // colored brick launches (replace the slab + k_slab_sum): bricks are launched one color at a time
+  // (no two bricks of a color share a node); a brick-surface node's running sum lives in acc[] and
+  // is carried across colors in color order (deterministic): the node's first-color brick writes,
+  // later ones add, its last-color brick completes it (plain / residual / fused-Jacobi store)
+  const int32_t *bricks;      // brick ids sorted by color (nullptr: no coloring)
+  const uint16_t *ncolor;     // [n_vnodes] bit c set: a brick of color c holds the node
+  double *acc;                // running sums of surface nodes (y itself unless the fused Jacobi sweep)
+  int n_colors;
+  int color;                  // color of this launch (set by the launcher)
+  int color_off[17];          // bricks[color_off[c] .. color_off[c+1]) have color c
   double nu;
   double alpha[4];            // time coefficients applied to (u, u1, u2, u3) in R_s / rhs
   double alpha_jac;           // mass coefficient of the Jacobian (bdf[0] / sdirk[0][0])
