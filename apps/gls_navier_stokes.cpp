@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -161,6 +162,8 @@ struct Params {
   int newton_max = 10, newton_verbose = 0, lin_max = 1000, restart = 30;
   int nl_solver = GLS_NEWTON, skip_iterations = 1;  // non-linear solver/solver, skip iterations
   double lin_rel = 1e-3, lin_min = 1e-8;
+  double ilu_atol = 1e-8, ilu_rtol = 1.0;
+  std::string timer = "none";  // timer/type none | iteration | end (parameters.cc:136-164)
   bool srf = false;
   double omega[3] = {0, 0, 0};
   // mesh adaptation (parameters.cc:649-731): uniform, or kelly = one Kelly-driven refinement
@@ -301,11 +304,49 @@ Params read_params(const Prm &p, int dim) {
   P.lin_max = p.i("linear solver/max iters", 1000);
   P.lin_rel = p.d("linear solver/relative residual", 1e-3);
   P.lin_min = p.d("linear solver/minimum residual", 1e-8);
+  // ILU(k) of the reference's GMRES (parameters.cc:546-560); the level is 0 here (rocSPARSE csrilu0)
+  P.ilu_atol = p.d("linear solver/ilu preconditioner absolute tolerance", 1e-8);
+  P.ilu_rtol = p.d("linear solver/ilu preconditioner relative tolerance", 1.0);
+  P.timer = p.get("timer/type", "none");
+  if (P.timer != "none" && P.timer != "iteration" && P.timer != "end") die("timer/type '%s' is unknown", P.timer.c_str());
   P.srf = p.get("velocity source/type", "none") == "srf";
   P.omega[0] = p.d("velocity source/omega_x", 0.);
   P.omega[1] = p.d("velocity source/omega_y", 0.);
   P.omega[2] = p.d("velocity source/omega_z", 0.);
   return P;
+}
+
+// ---------------------------------------------------------------------------------------------
+// device CFL on box cells (calculate_CFL: |u| at the cell centre * dt / h_cell, h_cell =
+// (6|K|/pi)^(1/3) / degree, 2D sqrt(4|K|/pi) / degree): one thread per cell, per-block maxima
+// ---------------------------------------------------------------------------------------------
+__global__ void k_cfl(const int32_t *cv, const double *h, const double *u, int64_t nc, int dim, int nvl, int k1,
+                      double b0, double b1, double b2, double deg, double dt, double *blockmax) {
+  __shared__ double red[256];
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double v = 0.0;
+  if (c < nc) {
+    const double B[3] = {b0, b1, b2};
+    double uc[3] = {0, 0, 0}, meas = 1.0;
+    for (int a = 0; a < nvl; ++a) {
+      const int ax = a % k1, ay = (a / k1) % k1, az = a / (k1 * k1);
+      const double w = B[ax] * B[ay] * (dim == 3 ? B[az] : 1.0);
+      const int64_t node = cv[c * nvl + a];
+      for (int d = 0; d < dim; ++d) uc[d] += w * u[node * dim + d];
+    }
+    for (int d = 0; d < dim; ++d) meas *= h[c * dim + d];
+    const double hh = dim == 2 ? sqrt(4. * meas / M_PI) / deg : cbrt(6. * meas / M_PI) / deg;
+    double un = 0;
+    for (int d = 0; d < dim; ++d) un += uc[d] * uc[d];
+    v = sqrt(un) / hh * dt;
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) blockmax[blockIdx.x] = red[0];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -643,6 +684,12 @@ struct Solver {
   std::vector<gls_ctx *> mg_levels;
   double *d_present = nullptr, *d_m1 = nullptr, *d_m2 = nullptr, *d_m3 = nullptr;
   std::vector<double> present, m1, m2, m3;
+  // The time loop is device-resident: between solves the state and history live in d_* (history
+  // shift = pointer rotation + one device copy, CFL on the device for box meshes); the host copies
+  // are refreshed only for output, post-processing, mesh adaptation and initial conditions.
+  bool dev_ok = false, host_ok = true;  // which side holds the current state
+  int32_t *d_cv = nullptr;              // box meshes: cell -> velocity node map and extents (device CFL)
+  double *d_h = nullptr, *d_blk = nullptr;
   int step = 0;
   double time = 0.0, dt_now = 0.0, cfl = 0.0;
   double dts[4] = {0, 0, 0, 0};  // time steps, most recent first (BDF coefficients)
@@ -657,7 +704,9 @@ struct Solver {
     std::snprintf(b, sizeof(b), "%g", v);
     return b;
   }
-  Solver(Params &p, bool mg) : P(p), use_mg(mg) {}
+  Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) {}
+  bool use_ilu;              // assembled ILU(0) where no multigrid hierarchy exists (--precond jacobi: off)
+  gls_ctx *ilu_ctx = nullptr;  // the context the ILU was attached to (a new mesh builds a new context)
   ~Solver() {
     release();
     if (space) gls_fe_space_destroy(space);
@@ -668,9 +717,14 @@ struct Solver {
     for (gls_ctx *g : mg_levels) gls_destroy(g);
     mg_levels.clear();
     if (ctx) gls_destroy(ctx);
+    ilu_ctx = nullptr;
     ctx = nullptr;
     if (rmesh) gls_mesh_refined_destroy(rmesh);
     rmesh = nullptr;
+    if (d_cv) (void)hipFree(d_cv);
+    for (double *q : {d_h, d_blk}) if (q) (void)hipFree(q);
+    d_cv = nullptr;
+    d_h = d_blk = nullptr;
     for (double *q : {d_present, d_m1, d_m2, d_m3})
       if (q) (void)hipFree(q);
     d_present = d_m1 = d_m2 = d_m3 = nullptr;
@@ -747,6 +801,32 @@ struct Solver {
     }
     present.assign((size_t)N, 0.);
     m1 = m2 = m3 = present;
+    dev_ok = true;  // both sides hold zeros
+    host_ok = true;
+  }
+  void need_dev() {  // host -> device (after host-side initial conditions / transfers)
+    if (dev_ok) return;
+    upload(present, d_present);
+    upload(m1, d_m1);
+    upload(m2, d_m2);
+    upload(m3, d_m3);
+    dev_ok = true;
+  }
+  void need_host() {  // device -> host (output, post-processing, adaptation)
+    if (host_ok) return;
+    hk(hipDeviceSynchronize(), "need_host");
+    download(d_present, present);
+    download(d_m1, m1);
+    download(d_m2, m2);
+    download(d_m3, m3);
+    host_ok = true;
+  }
+  void host_changed() { dev_ok = false; host_ok = true; }
+  void dev_changed() { host_ok = false; dev_ok = true; }
+  void dcopy(double *dst, const double *src) {  // ordered against the context's own stream: synchronous
+    hk(hipDeviceSynchronize(), "device copy");
+    hk(hipMemcpy(dst, src, sizeof(double) * (size_t)m.n_dofs(), hipMemcpyDeviceToDevice), "device copy");
+    hk(hipDeviceSynchronize(), "device copy");
   }
 
   // the hyper_cube(2^refinement) with the flagged cells split once (hanging nodes): mesh,
@@ -1014,19 +1094,21 @@ struct Solver {
     for (int i = 0; i < 4; ++i) ts[i] = dts[i] > 0 ? dts[i] : 1.0;
     ck(gls_set_time(ctx, scheme, ts), "gls_set_time");
     if (nu_override > 0) ck(gls_set_viscosity(ctx, nu_override), "gls_set_viscosity");
-    upload(present, d_present);
-    upload(m1, d_m1);
-    upload(m2, d_m2);
-    upload(m3, d_m3);
+    need_dev();
     ck(gls_apply_dirichlet(ctx, d_present), "gls_apply_dirichlet");
     gls_newton_params np;
     std::memset(&np, 0, sizeof(np));
     np.tolerance = P.newton_tol;
     np.max_iterations = P.newton_max;
     np.verbosity = P.newton_verbose;
-    // The reference's iteration caps are tuned for ILU / AMG; the matrix-free Jacobi-preconditioned
-    // GMRES used where no multigrid hierarchy exists (curved, unstructured and locally refined meshes)
-    // needs more iterations to reach the same tolerance, so its cap and restart are raised there.
+    // Preconditioner: the multigrid V-cycle on nested hyper_cubes; elsewhere the assembled ILU(0)
+    // (the reference's ILU-GMRES; not with hanging nodes) unless --precond jacobi. The reference's
+    // iteration caps are tuned for ILU(k) / AMG, so the caps and restart are raised without the
+    // V-cycle (ILU(0) is weaker than the reference's ILU(1); Jacobi much weaker).
+    if (mg_levels.empty() && use_ilu && m.hang_dofs.empty() && ilu_ctx != ctx) {
+      ck(gls_ilu_attach(ctx, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
+      ilu_ctx = ctx;
+    }
     const bool jacobi = mg_levels.empty();
     np.lin.max_iterations = jacobi ? std::max(P.lin_max, 20000) : P.lin_max;
     np.lin.restart = jacobi ? std::max(P.restart, 100) : P.restart;
@@ -1039,7 +1121,7 @@ struct Solver {
     ck(gls_newton_solve(ctx, d_present, d_m1, d_m2, d_m3, &np), "gls_newton_solve");
     if (np.linear_failures > 0)
       printf("  -Warning: %d linear solve(s) stopped at the iteration limit before the tolerance\n", np.linear_failures);
-    download(d_present, present);
+    dev_changed();
     newton_its += np.newton_iterations;
     linear_its += np.linear_iterations;
     if (nu_override > 0) ck(gls_set_viscosity(ctx, P.nu), "gls_set_viscosity");
@@ -1054,13 +1136,13 @@ struct Solver {
   void advance() {
     if (P.method == Method::sdirk2) {
       solve_nonlinear(GLS_SDIRK2_1);
-      m2 = present;
+      dcopy(d_m2, d_present);
       solve_nonlinear(GLS_SDIRK2_2);
     } else if (P.method == Method::sdirk3) {
       solve_nonlinear(GLS_SDIRK3_1);
-      m2 = present;
+      dcopy(d_m2, d_present);
       solve_nonlinear(GLS_SDIRK3_2);
-      m3 = present;
+      dcopy(d_m3, d_present);
       solve_nonlinear(GLS_SDIRK3_3);
     } else {
       const int sch[] = {GLS_STEADY, GLS_BDF1, GLS_BDF2, GLS_BDF3};
@@ -1077,17 +1159,17 @@ struct Solver {
     const double dt = P.dt, s = P.startup;
     push_dt(dt * s);
     solve_nonlinear(GLS_BDF1, -1.0, true);  // start-up solves force a fresh matrix (:534-574)
-    m2 = m1;
-    m1 = present;
+    dcopy(d_m2, d_m1);
+    dcopy(d_m1, d_present);
     if (P.method == Method::bdf2) {
       push_dt(dt * (1. - s));
       solve_nonlinear(GLS_BDF2, -1.0, true);
     } else {
       push_dt(dt * s);
       solve_nonlinear(GLS_BDF1, -1.0, true);
-      m3 = m2;
-      m2 = m1;
-      m1 = present;
+      dcopy(d_m3, d_m2);
+      dcopy(d_m2, d_m1);
+      dcopy(d_m1, d_present);
       push_dt(dt * (1. - 2. * s));
       solve_nonlinear(GLS_BDF3, -1.0, true);
     }
@@ -1157,6 +1239,28 @@ struct Solver {
   }
   // CFL from the velocity at the cell centre and h = (6|K|/pi)^(1/3)/k (3D), sqrt(4|K|/pi)/k (2D)
   double compute_cfl(double dt) {
+    if (!m.general && m.vx.empty() && m.k <= 2) {  // box cells: on the device, from d_present
+      const int k1 = m.k + 1, nvl = m.dim == 3 ? k1 * k1 * k1 : k1 * k1;
+      const int64_t nb = (m.nc + 255) / 256;
+      if (!d_cv) {
+        hk(hipMalloc(&d_cv, sizeof(int32_t) * m.cv.size()), "hipMalloc");
+        hk(hipMalloc(&d_h, sizeof(double) * m.h.size()), "hipMalloc");
+        hk(hipMalloc(&d_blk, sizeof(double) * (size_t)nb), "hipMalloc");
+        hk(hipMemcpy(d_cv, m.cv.data(), sizeof(int32_t) * m.cv.size(), hipMemcpyHostToDevice), "upload");
+        hk(hipMemcpy(d_h, m.h.data(), sizeof(double) * m.h.size(), hipMemcpyHostToDevice), "upload");
+      }
+      need_dev();
+      double b[3] = {0, 0, 0}, db[4];
+      lag1d(lobatto01(m.k), 0.5, b, db);
+      hk(hipDeviceSynchronize(), "cfl");
+      hipLaunchKernelGGL(k_cfl, dim3((unsigned)nb), dim3(256), 0, 0, d_cv, d_h, d_present, m.nc, m.dim, nvl, k1, b[0], b[1],
+                         b[2], (double)std::max(m.k, m.kp), dt, d_blk);
+      hk(hipGetLastError(), "k_cfl");
+      std::vector<double> bm((size_t)nb);
+      hk(hipMemcpy(bm.data(), d_blk, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost), "download");
+      return *std::max_element(bm.begin(), bm.end());
+    }
+    need_host();
     CellEval ev(m, 1);
     const int deg = std::max(m.k, m.kp);
     double cmax = 0;
@@ -1174,6 +1278,7 @@ struct Solver {
     return cmax;
   }
   void write_output() {
+    need_host();
     char tag[32];
     std::snprintf(tag, sizeof(tag), ".%05d", step);
     const std::string stem = P.output_name + tag, piece = stem + ".00000.vtu", master = stem + ".pvtu";
@@ -1211,6 +1316,7 @@ struct Solver {
   }
   void postprocess(bool initial) {
     if (P.output_frequency > 0 && step % P.output_frequency == 0) write_output();
+    if (P.enstrophy || P.kinetic || (!initial && P.analytical)) need_host();
     // post-processing lines of NavierStokesBase::postprocess (navier_stokes_base.cc:791-853)
     if (P.enstrophy && P.pp_verbose) std::printf("Enstrophy  : %s\n", g6(volume_average(true)).c_str());
     if (P.kinetic && P.pp_verbose) std::printf("Kinetic energy : %s\n", g6(volume_average(false)).c_str());
@@ -1222,15 +1328,20 @@ struct Solver {
         std::printf("L2 error velocity : %s\n", g6(e.first).c_str());
     }
   }
-  void end_of_step() {  // history shift + CFL of the step just taken
+  void end_of_step() {  // history shift (device: pointer rotation + one copy) + CFL of the step just taken
     if (P.method == Method::steady) return;
-    m3 = m2;
-    m2 = m1;
-    m1 = present;
+    need_dev();
+    double *t = d_m3;
+    d_m3 = d_m2;
+    d_m2 = d_m1;
+    d_m1 = t;
+    dcopy(d_m1, d_present);
+    dev_changed();
     cfl = compute_cfl(dt_now);
   }
   // uniform refinement with interpolation of the Qk fields onto the refined lattice
   void refine_uniform() {
+    need_host();
     if (m.general) {  // refine_global + SolutionTransfer (gls_fe_space_transfer)
       const std::vector<double> sol = present;
       gls_fe_space *old_space = space;
@@ -1239,6 +1350,7 @@ struct Solver {
       setup_general();
       ck(gls_fe_space_transfer(old_space, space, sol.data(), present.data()), "gls_fe_space_transfer");
       gls_fe_space_destroy(old_space);
+      host_changed();
       return;
     }
     const Mesh old = m;
@@ -1283,12 +1395,14 @@ struct Solver {
           present[(size_t)(dim * m.nv + v)] = value_at(x, dim);
       }
     }
+    host_changed();
   }
   // refine_mesh_kelly (navier_stokes_base.cc:610-780) for the first adaptation of the uniform
   // mesh: Kelly indicator of the velocity or pressure on the device (gls_kelly_estimate, stored as
   // float like deal.II's Vector<float>), refine_and_coarsen_fixed_number (refinement part;
   // coarsening is rejected at parameter time), max refinement level, SolutionTransfer
   void refine_kelly() {
+    need_host();
     const Mesh old = m;
     if (old.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
     if (!old.vx.empty()) die("kelly mesh adaptation: the mesh is already refined once");
@@ -1322,6 +1436,7 @@ struct Solver {
                 (long long)old.nc);
     const std::vector<double> sol = present;
     setup_refined(old.n, flags);
+    host_changed();  // present is rewritten on the host below
     ck(gls_mesh_refined_interpolate(rmesh, old.n, P.lo, P.hi, sol.data(), present.data()),
        "gls_mesh_refined_interpolate");
   }
@@ -1399,17 +1514,22 @@ struct Solver {
     }
     if (P.ic_type == "nodal" || P.ic_type == "viscous") {
       nodal_values(P.ic, present);
+      host_changed();
       if (P.ic_type == "viscous") solve_nonlinear(GLS_STEADY, P.ic_nu);
     } else if (P.ic_type == "L2projection") {
       l2_projection(P.ic, present);
+      host_changed();
     } else {
       die("initial condition type '%s' is not supported", P.ic_type.c_str());
     }
     end_of_step();
     postprocess(true);
     const bool steady = P.method == Method::steady;
+    const auto t_start = std::chrono::steady_clock::now();
     while (steady ? step < P.mesh_adapt + 1 : time < P.t_end - 1e-12 * dt_now) {
       ++step;
+      const auto t_step = std::chrono::steady_clock::now();
+      const int nit0 = newton_its, lit0 = linear_its;
       if (steady) {
         time = step;
       } else {
@@ -1437,6 +1557,17 @@ struct Solver {
       }
       postprocess(false);
       end_of_step();
+      if (P.timer == "iteration") {  // the TimerOutput summary per iteration (navier_stokes_base.cc:449-453), condensed
+        hk(hipDeviceSynchronize(), "timer");
+        const double w = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_step).count();
+        std::printf("   Timer: iteration %d wall time %.3f s (Newton iterations %d, linear iterations %d)\n", step, w,
+                    newton_its - nit0, linear_its - lit0);
+      }
+    }
+    if (P.timer != "none") {
+      const double w = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+      std::printf("   Timer: total wall time %.3f s over %d iterations (Newton iterations %d, linear iterations %d)\n", w,
+                  step, newton_its, linear_its);
     }
     report();
     if (stats) std::printf("newton_iterations = %d, linear_iterations = %d\n", newton_its, linear_its);

@@ -208,6 +208,15 @@ int gls_mg_transfer(gls_ctx *ctx, int level, int direction, const double *in, do
  * must fill an axis-aligned box (Morton partitions of a 2^m-cube over 2^j ranks do). */
 int gls_set_lattice(gls_ctx *ctx, int n1d, const int64_t *local_to_global);
 int gls_mg_detach(gls_ctx *ctx);
+/* Assembled ILU(0) preconditioner for GMRES (replaces setup_ILU, gls_navier_stokes.cc:1161-1176, the
+ * reference's 'linear solver/method = gmres' with 'ilu preconditioner absolute / relative tolerance';
+ * fill level 0): the Jacobian is probed from the device operator into CSR with distance-2-colored
+ * unit vectors once per Jacobian state, its diagonal perturbed like Ifpack (a_ii <- rthresh a_ii +
+ * sign(a_ii) athresh) and factored by rocSPARSE. Single rank, no hanging nodes, no multigrid. */
+int gls_ilu_attach(gls_ctx *ctx, double athresh, double rthresh);
+int gls_ilu_detach(gls_ctx *ctx);
+int gls_ilu_info(const gls_ctx *ctx, int64_t *nnz, int *n_probes);
+int gls_ilu_matrix(gls_ctx *ctx, int32_t *rowp, int32_t *col, double *val); /* probed CSR (tests) */
 
 /* ------------------------------------------------------------------------------------------
  * Nonlinear solve: NewtonNonLinearSolver::solve (include/core/newton_non_linear_solver.h:74-139)

@@ -18,6 +18,7 @@
 
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
+#include <rocsparse/rocsparse.h>
 
 #include "../../include/gls_native.h"
 #include "gls_common.hpp"
@@ -329,6 +330,36 @@ struct gls_ctx {
     gls_allreduce_fn allreduce = nullptr;
     void *user = nullptr;
   } dist;
+  // assembled ILU(0) preconditioner (gls_ilu_attach; the reference's setup_ILU,
+  // gls_navier_stokes.cc:1161-1176): the Jacobian is assembled into CSR by probing the matrix-free
+  // operator with distance-2-colored unit vectors, perturbed on the diagonal like Ifpack (athresh,
+  // rthresh) and factored in place by rocSPARSE; M^-1 v = U^-1 L^-1 v (two sparse triangular solves)
+  struct ILU {
+    bool on = false, valid = false;
+    double athresh = 0., rthresh = 1.;
+    int n_probes = 0;
+    std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
+    DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
+    DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
+    DevBuf<int32_t> perm;                // DoF -> its row in the factored (renumbered) matrix
+    DevBuf<double> val, vbuf, ybuf, tbuf;
+    DevBuf<char> work;
+    rocsparse_handle h = nullptr;
+    rocsparse_mat_descr dA = nullptr, dL = nullptr, dU = nullptr;
+    rocsparse_mat_info info = nullptr;
+    int64_t nnz = 0;
+    void release() {
+      if (info) rocsparse_destroy_mat_info(info);
+      if (dA) rocsparse_destroy_mat_descr(dA);
+      if (dL) rocsparse_destroy_mat_descr(dL);
+      if (dU) rocsparse_destroy_mat_descr(dU);
+      if (h) rocsparse_destroy_handle(h);
+      info = nullptr;
+      dA = dL = dU = nullptr;
+      h = nullptr;
+    }
+    ~ILU() { release(); }
+  } ilu;
   // hanging-node constraints (gls_set_hanging): lines dof <- sum w * master
   struct Hang {
     bool on = false;
@@ -1105,6 +1136,7 @@ int gls_set_force(gls_ctx *c, const double *f) {
     GLS_TRY(c->force_q.upload(f, (size_t)c->n_cells * c->nq * c->dim));
   }
   c->diag_valid = false;
+  c->ilu.valid = false;
   c->qd_valid = false;
   return GLS_OK;
 }
@@ -1113,6 +1145,7 @@ int gls_set_viscosity(gls_ctx *c, double nu) {
   GLS_TRY(check_ctx(c));
   c->viscosity = nu;
   c->diag_valid = false;
+  c->ilu.valid = false;
   c->qd_valid = false;
   return GLS_OK;
 }
@@ -1158,6 +1191,7 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
   }
   if (!c->jf.on) {  // a frozen Jacobian keeps its own time coefficients
     c->diag_valid = false;
+    c->ilu.valid = false;
     c->qd_valid = false;
   }
   return GLS_OK;
@@ -1172,6 +1206,7 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
   c->u3 = u3;
   if (!c->jf.on) {  // a frozen Jacobian stays at its snapshot (gls_freeze_jacobian)
     c->diag_valid = false;
+    c->ilu.valid = false;
     c->qd_valid = false;
     c->mg.dirty = true;
   }
@@ -1191,6 +1226,7 @@ int gls_freeze_jacobian(gls_ctx *c, int freeze) {
     if (j.on) {
       j.on = false;
       c->diag_valid = false;
+      c->ilu.valid = false;
       c->qd_valid = false;
       c->mg.dirty = true;
     }
@@ -1251,6 +1287,7 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   c->dist.user = user;
   c->dist.on = true;
   c->diag_valid = false;
+  c->ilu.valid = false;
   c->qd_valid = false;
   return GLS_OK;
 }
@@ -1408,6 +1445,7 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
                                     (int64_t)c->hang.dof.n, c->stream));
   if (!c->jf.on && (x == c->u || x == c->u1 || x == c->u2 || x == c->u3)) {  // the captured state changed
     c->diag_valid = false;
+    c->ilu.valid = false;
     c->qd_valid = false;
     c->mg.dirty = true;
   }
@@ -1492,6 +1530,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   c->use_slab = false;
   c->use_colors = false;
   c->diag_valid = false;
+  c->ilu.valid = false;
   c->qd_valid = false;
   return GLS_OK;
 }
@@ -1838,9 +1877,79 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   return GLS_OK;
 }
 
-// z = M^{-1} v : Jacobi, or a multigrid V-cycle when attached
+#define RS_TRY(x)                                                                        \
+  do {                                                                                   \
+    const rocsparse_status rs_ = (x);                                                    \
+    if (rs_ != rocsparse_status_success) return set_err(GLS_EHIP, "%s: rocsparse status %d", #x, (int)rs_); \
+  } while (0)
+
+// assembled ILU(0): probe the operator into the CSR values (one J.v per color and DoF slot), perturb
+// the diagonal, factor in place; once per Jacobian state (invalidated with the diagonal)
+static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_jacobian_apply)
+  auto &I = c->ilu;
+  const int64_t n = c->n_dofs;
+  hipStream_t s = c->stream;
+  for (int p = 0; p < I.n_probes; ++p) {
+    HIP_TRY(gls::vec_fill(I.vbuf.p, n, 0.0, s));
+    HIP_TRY(gls::vec_set_const_indexed(I.vbuf.p, I.pdofs.p + I.pdoff[(size_t)p], I.pdoff[(size_t)p + 1] - I.pdoff[(size_t)p],
+                                       1.0, s));
+    GLS_TRY(gls_jacobian_apply(c, I.vbuf.p, I.ybuf.p));
+    HIP_TRY(gls::csr_probe_extract(I.val.p, I.pent.p + I.peoff[(size_t)p], I.prow.p + I.peoff[(size_t)p],
+                                   I.peoff[(size_t)p + 1] - I.peoff[(size_t)p], I.ybuf.p, s));
+  }
+  return GLS_OK;
+}
+static int apply_ilu(gls_ctx *c, const double *v, double *z);
+static int ensure_ilu(gls_ctx *c) {
+  auto &I = c->ilu;
+  if (!I.on || I.valid) return GLS_OK;
+  const int64_t n = c->n_dofs;
+  hipStream_t s = c->stream;
+  const bool verbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
+  auto now = [&]() {
+    if (verbose) (void)hipStreamSynchronize(s);
+    return std::chrono::steady_clock::now();
+  };
+  const auto t0 = now();
+  GLS_TRY(ilu_probe(c));
+  HIP_TRY(gls::csr_diag_perturb(I.val.p, I.didx.p, n, I.athresh, I.rthresh, s));
+  const auto t1 = now();
+  const rocsparse_int m = (rocsparse_int)n, nnz = (rocsparse_int)I.nnz;
+  RS_TRY(rocsparse_set_stream(I.h, s));
+  RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
+  I.valid = true;
+  if (verbose) {
+    const auto t2 = now();
+    rocsparse_int zp = -1;
+    const rocsparse_status st = rocsparse_csrilu0_zero_pivot(I.h, I.info, &zp);
+    GLS_TRY(apply_ilu(c, I.ybuf.p, I.ybuf.p == nullptr ? nullptr : c->tmp1.p ? c->tmp1.p : I.ybuf.p));
+    const auto t3 = now();
+    std::printf("ilu: %d probes %.2f ms, csrilu0 %.2f ms (zero pivot status %d at %d), one apply %.3f ms\n", I.n_probes,
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(t2 - t1).count(), (int)st, (int)zp,
+                std::chrono::duration<double, std::milli>(t3 - t2).count());
+  }
+  return GLS_OK;
+}
+static int apply_ilu(gls_ctx *c, const double *v, double *z) {
+  auto &I = c->ilu;
+  const rocsparse_int m = (rocsparse_int)c->n_dofs, nnz = (rocsparse_int)I.nnz;
+  const double one = 1.0;
+  RS_TRY(rocsparse_set_stream(I.h, c->stream));
+  // z = P^T U^-1 L^-1 P v (P: the Cuthill-McKee renumbering the factors live in)
+  HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
+  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dL, I.val.p, I.rowp.p, I.col.p, I.info,
+                                I.vbuf.p, I.tbuf.p, rocsparse_solve_policy_auto, I.work.p));
+  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
+                                I.tbuf.p, I.vbuf.p, rocsparse_solve_policy_auto, I.work.p));
+  HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
+  return GLS_OK;
+}
+
+// z = M^{-1} v : Jacobi, assembled ILU(0) or a multigrid V-cycle when attached
 int apply_prec(gls_ctx *c, const double *v, double *z) {
   if (c->mg.on) return mg_vcycle(c, 0, v, z);
+  if (c->ilu.on) return apply_ilu(c, v, z);
   HIP_TRY(gls::vec_div(z, v, c->diag.p, c->n_dofs, c->stream));
   return GLS_OK;
 }
@@ -1851,6 +1960,7 @@ int gls_apply_preconditioner(gls_ctx *c, const double *v, double *z) {
   if (!v || !z || v == z) return set_err(GLS_EINVAL, "v/z null or aliased");
   GLS_TRY(ensure_diag(c));
   if (c->mg.on) GLS_TRY(mg_prepare(c));
+  GLS_TRY(ensure_ilu(c));
   return apply_prec(c, v, z);
 }
 
@@ -2129,6 +2239,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   }
   GLS_TRY(ensure_diag(c));
   if (c->mg.on) GLS_TRY(mg_prepare(c));
+  GLS_TRY(ensure_ilu(c));
   // with the V-cycle, keep Z = M^-1 V (flexible-GMRES storage): the update x += Z y then needs no
   // extra preconditioner application per restart cycle
   const bool keepz = c->mg.on;
@@ -2144,7 +2255,9 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   int it = 0;
   std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hcol(m + 2), hc2(m + 2), y(m);
   bool converged = beta <= tol;
+  const bool lverbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
   while (!converged && it < prm->max_iterations) {
+    if (lverbose) std::printf("gmres: it %d residual %.6e (tol %.3e)\n", it, beta, tol);
     HIP_TRY(gls::vec_axpby(V, 1.0 / beta, r, 0.0, n, s));
     std::fill(g.begin(), g.end(), 0.);
     g[0] = beta;
@@ -2596,3 +2709,285 @@ int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
 }
 
 }  // extern "C"
+
+
+// ---------------------------------------------------------------------------------------------
+// gls_ilu_attach: the reference's ILU-preconditioned GMRES (linear solver method gmres with 'ilu
+// preconditioner fill / absolute tolerance / relative tolerance', setup_ILU gls_navier_stokes.cc:
+// 1161-1176, Ifpack ILU(k) with athresh / rthresh) on the assembled Jacobian. The fill level is 0
+// here (rocSPARSE csrilu0); the matrix is never formed by a CPU: it is probed from the device
+// operator with distance-2-colored unit vectors (no two DoFs of a probe share a row).
+// ---------------------------------------------------------------------------------------------
+extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
+  GLS_TRY(check_ctx(c));
+  auto &I = c->ilu;
+  if (c->dist.on) return set_err(GLS_EINVAL, "gls_ilu_attach: single-rank contexts only");
+  if (c->hang.on) return set_err(GLS_EINVAL, "gls_ilu_attach: not with hanging-node constraints");
+  if (c->mg.on) return set_err(GLS_EINVAL, "gls_ilu_attach: a multigrid preconditioner is attached");
+  const int dim = c->dim, nvc = gls::ipow(c->k + 1, dim);
+  const bool sep = c->cell_pnodes.p != nullptr;
+  const int npc = sep ? gls::ipow(c->kp + 1, dim) : 0;
+  const int64_t nv = c->n_vnodes, np = c->n_pnodes, nc = c->n_cells, n = c->n_dofs;
+  if (n >= INT32_MAX) return set_err(GLS_EINVAL, "gls_ilu_attach: too many DoFs for 32-bit CSR");
+  std::vector<int32_t> cv((size_t)nc * nvc), cp((size_t)nc * npc);
+  HIP_TRY(hipMemcpy(cv.data(), c->cell_vnodes.p, cv.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (sep) HIP_TRY(hipMemcpy(cp.data(), c->cell_pnodes.p, cp.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  // unified nodes: velocity nodes [0, nv), separate pressure nodes [nv, nv + np)
+  const int64_t nu = nv + (sep ? np : 0);
+  const int ncn = nvc + npc;
+  auto cell_node = [&](int64_t cell, int a) -> int64_t {
+    return a < nvc ? cv[(size_t)(cell * nvc + a)] : nv + cp[(size_t)(cell * npc + a - nvc)];
+  };
+  std::vector<int64_t> ncoff((size_t)nu + 1, 0), nccell;
+  for (int64_t e = 0; e < nc; ++e)
+    for (int a = 0; a < ncn; ++a) ++ncoff[(size_t)cell_node(e, a) + 1];
+  for (int64_t x = 0; x < nu; ++x) ncoff[(size_t)x + 1] += ncoff[(size_t)x];
+  nccell.resize((size_t)ncoff[(size_t)nu]);
+  {
+    std::vector<int64_t> fill(ncoff.begin(), ncoff.end() - 1);
+    for (int64_t e = 0; e < nc; ++e)
+      for (int a = 0; a < ncn; ++a) nccell[(size_t)fill[(size_t)cell_node(e, a)]++] = e;
+  }
+  // N1(x): nodes of the cells holding x (sorted, unique)
+  std::vector<int64_t> n1off((size_t)nu + 1, 0), n1;
+  {
+    std::vector<int64_t> stamp((size_t)nu, -1), buf;
+    for (int64_t x = 0; x < nu; ++x) {
+      buf.clear();
+      for (int64_t t = ncoff[(size_t)x]; t < ncoff[(size_t)x + 1]; ++t)
+        for (int a = 0; a < ncn; ++a) {
+          const int64_t y = cell_node(nccell[(size_t)t], a);
+          if (stamp[(size_t)y] != x) { stamp[(size_t)y] = x; buf.push_back(y); }
+        }
+      std::sort(buf.begin(), buf.end());
+      n1.insert(n1.end(), buf.begin(), buf.end());
+      n1off[(size_t)x + 1] = (int64_t)n1.size();
+    }
+  }
+  // greedy distance-2 coloring of the unified nodes
+  std::vector<int> color((size_t)nu, -1), mark;
+  int ncol = 0;
+  for (int64_t x = 0; x < nu; ++x) {
+    for (int64_t t = n1off[(size_t)x]; t < n1off[(size_t)x + 1]; ++t) {
+      const int64_t z = n1[(size_t)t];
+      for (int64_t u = n1off[(size_t)z]; u < n1off[(size_t)z + 1]; ++u) {
+        const int cy = color[(size_t)n1[(size_t)u]];
+        if (cy >= 0) {
+          if ((int)mark.size() <= cy) mark.resize((size_t)cy + 1, -1);
+          mark[(size_t)cy] = (int)x;
+        }
+      }
+    }
+    int col = 0;
+    while (col < (int)mark.size() && mark[(size_t)col] == (int)x) ++col;
+    color[(size_t)x] = col;
+    ncol = std::max(ncol, col + 1);
+  }
+  // DoFs of a unified node and their probe slot (component; dim = pressure)
+  auto node_dofs = [&](int64_t x, int64_t *d, int *slot) -> int {
+    if (x >= nv) { d[0] = dim * nv + (x - nv); slot[0] = dim; return 1; }
+    int m = 0;
+    for (int cc = 0; cc < dim; ++cc) { d[m] = x * dim + cc; slot[m++] = cc; }
+    if (!sep) { d[m] = dim * nv + x; slot[m++] = dim; }
+    return m;
+  };
+  // DoF renumbering for the factorisation: Cuthill-McKee on the node graph (deal.II renumbers the
+  // DoFs with Cuthill_McKee before Trilinos factors, gls_navier_stokes.cc:70), a node's DoFs
+  // consecutive (u, v, [w,] p): the pressure rows sit next to their velocity rows, not in a trailing
+  // block, which keeps ILU(0) of the saddle-point-like GLS matrix away from vanishing pivots
+  std::vector<int32_t> newidx((size_t)n, -1);
+  {
+    std::vector<int64_t> order;
+    order.reserve((size_t)nu);
+    std::vector<char> seen((size_t)nu, 0);
+    auto deg = [&](int64_t x) { return n1off[(size_t)x + 1] - n1off[(size_t)x]; };
+    for (int64_t start = 0; start < nu; ++start) {  // one BFS per connected component
+      if (seen[(size_t)start]) continue;
+      int64_t s0 = start;  // lowest-degree unvisited node of this component's first visit
+      seen[(size_t)s0] = 1;
+      size_t head = order.size();
+      order.push_back(s0);
+      while (head < order.size()) {
+        const int64_t x = order[head++];
+        std::vector<int64_t> nb;
+        for (int64_t t = n1off[(size_t)x]; t < n1off[(size_t)x + 1]; ++t)
+          if (!seen[(size_t)n1[(size_t)t]]) nb.push_back(n1[(size_t)t]);
+        std::stable_sort(nb.begin(), nb.end(), [&](int64_t a, int64_t b) { return deg(a) < deg(b); });
+        for (int64_t y : nb) {
+          seen[(size_t)y] = 1;
+          order.push_back(y);
+        }
+      }
+    }
+    int32_t next = 0;
+    for (int64_t x : order) {
+      int64_t d[4];
+      int sl[4];
+      const int m2 = node_dofs(x, d, sl);
+      for (int j = 0; j < m2; ++j) newidx[(size_t)d[j]] = next++;
+    }
+    if (next != n) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering covers %d of %lld DoFs", next, (long long)n);
+  }
+  std::vector<int32_t> olddof((size_t)n);
+  for (int64_t i = 0; i < n; ++i) olddof[(size_t)newidx[(size_t)i]] = (int32_t)i;
+  // CSR pattern in the new numbering (rows of a node share its N1 column set), diagonal index,
+  // probe of every entry
+  std::vector<int32_t> rowp((size_t)n + 1, 0), col, didx((size_t)n, -1);
+  std::vector<int32_t> rowof_dof_node((size_t)n, 0);
+  for (int64_t x = 0; x < nu; ++x) {
+    int64_t d[4];
+    int sl[4];
+    const int m = node_dofs(x, d, sl);
+    for (int i = 0; i < m; ++i) rowof_dof_node[(size_t)d[i]] = (int32_t)x;
+  }
+  std::vector<int32_t> eprobe;
+  col.reserve((size_t)n * 32);
+  for (int64_t r = 0; r < n; ++r) {  // r: new row; its DoF olddof[r]
+    const int64_t i = olddof[(size_t)r];
+    const int64_t x = rowof_dof_node[(size_t)i];
+    std::vector<std::pair<int64_t, int>> cols;
+    for (int64_t t = n1off[(size_t)x]; t < n1off[(size_t)x + 1]; ++t) {
+      int64_t d[4];
+      int sl[4];
+      const int64_t y = n1[(size_t)t];
+      const int m = node_dofs(y, d, sl);
+      for (int j = 0; j < m; ++j) cols.push_back({newidx[(size_t)d[j]], color[(size_t)y] * (dim + 1) + sl[j]});
+    }
+    std::sort(cols.begin(), cols.end());
+    for (auto &cp_ : cols) {
+      if (cp_.first == r) didx[(size_t)r] = (int32_t)col.size();
+      col.push_back((int32_t)cp_.first);
+      eprobe.push_back(cp_.second);
+    }
+    rowp[(size_t)r + 1] = (int32_t)col.size();
+    if (didx[(size_t)r] < 0) return set_err(GLS_EINVAL, "gls_ilu_attach: row %lld has no diagonal", (long long)r);
+  }
+  const int nprobe = ncol * (dim + 1);
+  // probe lists: unit DoFs per probe; (entry, row) per probe
+  std::vector<int64_t> pdoff((size_t)nprobe + 1, 0), peoff((size_t)nprobe + 1, 0);
+  std::vector<int32_t> pdofs, pent, prow;
+  for (int64_t x = 0; x < nu; ++x) {
+    int64_t d[4];
+    int sl[4];
+    const int m = node_dofs(x, d, sl);
+    for (int j = 0; j < m; ++j) ++pdoff[(size_t)(color[(size_t)x] * (dim + 1) + sl[j]) + 1];
+  }
+  for (size_t e = 0; e < eprobe.size(); ++e) ++peoff[(size_t)eprobe[e] + 1];
+  for (int p = 0; p < nprobe; ++p) {
+    pdoff[(size_t)p + 1] += pdoff[(size_t)p];
+    peoff[(size_t)p + 1] += peoff[(size_t)p];
+  }
+  pdofs.resize((size_t)pdoff[(size_t)nprobe]);
+  pent.resize((size_t)peoff[(size_t)nprobe]);
+  prow.resize(pent.size());
+  {
+    std::vector<int64_t> f1(pdoff.begin(), pdoff.end() - 1), f2(peoff.begin(), peoff.end() - 1);
+    for (int64_t x = 0; x < nu; ++x) {
+      int64_t d[4];
+      int sl[4];
+      const int m = node_dofs(x, d, sl);
+      for (int j = 0; j < m; ++j) pdofs[(size_t)f1[(size_t)(color[(size_t)x] * (dim + 1) + sl[j])]++] = (int32_t)d[j];
+    }
+    for (int64_t r = 0; r < n; ++r)
+      for (int32_t e = rowp[(size_t)r]; e < rowp[(size_t)r + 1]; ++e) {
+        const int64_t k = f2[(size_t)eprobe[(size_t)e]]++;
+        pent[(size_t)k] = e;
+        prow[(size_t)k] = olddof[(size_t)r];  // the probe result is indexed by the original DoF
+      }
+  }
+  I.release();
+  GLS_TRY(I.rowp.upload(rowp.data(), rowp.size()));
+  GLS_TRY(I.col.upload(col.data(), col.size()));
+  GLS_TRY(I.didx.upload(didx.data(), didx.size()));
+  GLS_TRY(I.perm.upload(newidx.data(), newidx.size()));
+  GLS_TRY(I.pdofs.upload(pdofs.data(), pdofs.size()));
+  GLS_TRY(I.pent.upload(pent.data(), pent.size()));
+  GLS_TRY(I.prow.upload(prow.data(), prow.size()));
+  GLS_TRY(I.val.alloc(col.size()));
+  HIP_TRY(hipMemset(I.val.p, 0, col.size() * sizeof(double)));
+  GLS_TRY(I.vbuf.alloc((size_t)n));
+  GLS_TRY(I.ybuf.alloc((size_t)n));
+  GLS_TRY(I.tbuf.alloc((size_t)n));
+  I.pdoff = pdoff;
+  I.peoff = peoff;
+  I.n_probes = nprobe;
+  I.nnz = (int64_t)col.size();
+  I.athresh = athresh;
+  I.rthresh = rthresh;
+  RS_TRY(rocsparse_create_handle(&I.h));
+  RS_TRY(rocsparse_set_stream(I.h, c->stream));
+  RS_TRY(rocsparse_create_mat_descr(&I.dA));
+  RS_TRY(rocsparse_create_mat_descr(&I.dL));
+  RS_TRY(rocsparse_set_mat_fill_mode(I.dL, rocsparse_fill_mode_lower));
+  RS_TRY(rocsparse_set_mat_diag_type(I.dL, rocsparse_diag_type_unit));
+  RS_TRY(rocsparse_create_mat_descr(&I.dU));
+  RS_TRY(rocsparse_set_mat_fill_mode(I.dU, rocsparse_fill_mode_upper));
+  RS_TRY(rocsparse_set_mat_diag_type(I.dU, rocsparse_diag_type_non_unit));
+  RS_TRY(rocsparse_create_mat_info(&I.info));
+  const rocsparse_int m = (rocsparse_int)n, nnz = (rocsparse_int)I.nnz;
+  size_t b0 = 0, b1 = 0, b2 = 0;
+  RS_TRY(rocsparse_dcsrilu0_buffer_size(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, &b0));
+  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp.p, I.col.p, I.info, &b1));
+  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp.p, I.col.p, I.info, &b2));
+  GLS_TRY(I.work.alloc(std::max(std::max(b0, b1), std::max(b2, (size_t)16))));
+  RS_TRY(rocsparse_dcsrilu0_analysis(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_analysis_policy_reuse,
+                                     rocsparse_solve_policy_auto, I.work.p));
+  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp.p, I.col.p, I.info,
+                                   rocsparse_analysis_policy_reuse, rocsparse_solve_policy_auto, I.work.p));
+  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
+                                   rocsparse_analysis_policy_reuse, rocsparse_solve_policy_auto, I.work.p));
+  // pivots that end below athresh in magnitude are boosted to athresh (enclosed-flow pressure mode)
+  const double btol = athresh > 0 ? athresh : 1e-300, bval = athresh > 0 ? athresh : 1e-12;
+  RS_TRY(rocsparse_dcsrilu0_numeric_boost(I.h, I.info, 1, &btol, &bval));
+  I.on = true;
+  I.valid = false;
+  if (std::getenv("GLS_ILU_VERBOSE"))
+    std::printf("ilu attach: n %lld nnz %lld colors %d probes %d\n", (long long)n, (long long)I.nnz, ncol, nprobe);
+  return GLS_OK;
+}
+extern "C" int gls_ilu_detach(gls_ctx *c) {
+  GLS_TRY(check_ctx(c));
+  c->ilu.on = false;
+  c->ilu.release();
+  return GLS_OK;
+}
+// the probed (unfactored, unperturbed) operator matrix, for tests: host CSR arrays of gls_ilu_info's nnz
+extern "C" int gls_ilu_matrix(gls_ctx *c, int32_t *rowp, int32_t *col, double *val) {
+  GLS_TRY(check_ctx(c));
+  auto &I = c->ilu;
+  if (!I.on) return set_err(GLS_EINVAL, "no ILU attached");
+  GLS_TRY(ilu_probe(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  // renumbered CSR on the device; returned in the context's DoF numbering
+  const int64_t n = c->n_dofs;
+  std::vector<int32_t> rp((size_t)n + 1), cl((size_t)I.nnz), pm((size_t)n);
+  std::vector<double> vl((size_t)I.nnz);
+  HIP_TRY(hipMemcpy(rp.data(), I.rowp.p, sizeof(int32_t) * rp.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cl.data(), I.col.p, sizeof(int32_t) * cl.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(vl.data(), I.val.p, sizeof(double) * vl.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(pm.data(), I.perm.p, sizeof(int32_t) * pm.size(), hipMemcpyDeviceToHost));
+  std::vector<int32_t> old((size_t)n);
+  for (int64_t i = 0; i < n; ++i) old[(size_t)pm[(size_t)i]] = (int32_t)i;
+  std::vector<std::vector<std::pair<int32_t, double>>> rows((size_t)n);
+  for (int64_t r = 0; r < n; ++r)
+    for (int32_t e = rp[(size_t)r]; e < rp[(size_t)r + 1]; ++e) rows[(size_t)old[(size_t)r]].push_back({old[(size_t)cl[(size_t)e]], vl[(size_t)e]});
+  int64_t k = 0;
+  if (rowp) rowp[0] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    std::sort(rows[(size_t)i].begin(), rows[(size_t)i].end());
+    for (auto &pr : rows[(size_t)i]) {
+      if (col) col[k] = pr.first;
+      if (val) val[k] = pr.second;
+      ++k;
+    }
+    if (rowp) rowp[i + 1] = (int32_t)k;
+  }
+  I.valid = false;  // the values now hold the unfactored matrix
+  return GLS_OK;
+}
+extern "C" int gls_ilu_info(const gls_ctx *c, int64_t *nnz, int *n_probes) {
+  if (!c) return set_err(GLS_EINVAL, "null context");
+  if (nnz) *nnz = c->ilu.nnz;
+  if (n_probes) *n_probes = c->ilu.n_probes;
+  return c->ilu.on ? GLS_OK : set_err(GLS_EINVAL, "no ILU attached");
+}

@@ -336,3 +336,54 @@ hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, in
 }
 
 }  // namespace gls
+
+// ---- assembled-ILU preconditioner helpers (gls_api.cpp ilu_*): probe vectors and value extraction
+namespace gls {
+namespace {
+__global__ void k_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) x[idx[i]] = a;
+}
+// CSR values of the entries whose column belongs to one probe: val[ent[i]] = y[row[i]]
+__global__ void k_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) val[ent[i]] = y[row[i]];
+}
+// Ifpack-style diagonal perturbation before the factorisation: a_ii <- rthresh a_ii + sign(a_ii) athresh
+__global__ void k_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = val[didx[i]];
+  val[didx[i]] = rthresh * a + (a < 0 ? -athresh : athresh);
+}
+// out[idx[i]] = in[i] (scatter, dir 0) or out[i] = in[idx[i]] (gather, dir 1)
+__global__ void k_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (dir == 0) out[idx[i]] = in[i];
+  else out[i] = in[idx[i]];
+}
+}  // namespace
+hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_permute, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, in, idx, n, dir);
+  return hipGetLastError();
+}
+hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_const_indexed, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, x, idx, m, a);
+  return hipGetLastError();
+}
+hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
+                             hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_extract, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, m, y);
+  return hipGetLastError();
+}
+hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_diag_perturb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, val, didx, n, athresh, rthresh);
+  return hipGetLastError();
+}
+}  // namespace gls

@@ -30,7 +30,7 @@ EXPORTS = [
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import",
-    "gls_mg_attach", "gls_mg_detach", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
+    "gls_mg_attach", "gls_mg_detach", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -570,6 +570,33 @@ class GLSContext:
     def detach_multigrid(self):
         check(self.L.gls_mg_detach(self.h), "gls_mg_detach")
         self._mg_levels = None
+
+    def attach_ilu(self, athresh=1e-8, rthresh=1.0):
+        """Assembled ILU(0) preconditioner (the reference's ILU-preconditioned GMRES, setup_ILU); the
+        Jacobian is probed from the device operator. Returns (nnz, n_probes)."""
+        self.L.gls_ilu_attach.argtypes = [C.c_void_p, C.c_double, C.c_double]
+        check(self.L.gls_ilu_attach(self.h, float(athresh), float(rthresh)), "gls_ilu_attach")
+        nnz, npr = C.c_int64(), C.c_int()
+        self.L.gls_ilu_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        check(self.L.gls_ilu_info(self.h, C.byref(nnz), C.byref(npr)), "gls_ilu_info")
+        return nnz.value, npr.value
+
+    def ilu_matrix(self):
+        """The probed operator matrix (scipy CSR) behind the attached ILU, before perturbation/factoring."""
+        import scipy.sparse as sp
+        nnz, _ = C.c_int64(), C.c_int()
+        self.L.gls_ilu_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        check(self.L.gls_ilu_info(self.h, C.byref(nnz), C.byref(_)), "gls_ilu_info")
+        rowp = np.zeros(self.n_dofs + 1, dtype=np.int32)
+        col = np.zeros(nnz.value, dtype=np.int32)
+        val = np.zeros(nnz.value)
+        self.L.gls_ilu_matrix.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        check(self.L.gls_ilu_matrix(self.h, rowp.ctypes.data, col.ctypes.data, val.ctypes.data), "gls_ilu_matrix")
+        return sp.csr_matrix((val, col, rowp), shape=(self.n_dofs, self.n_dofs))
+
+    def detach_ilu(self):
+        self.L.gls_ilu_detach.argtypes = [C.c_void_p]
+        check(self.L.gls_ilu_detach(self.h), "gls_ilu_detach")
 
     # profiling
     def timing(self, enable=True):
