@@ -23,3 +23,9 @@ TLIM=300 run taylor-couette3d 3 taylor-couette3d_q2q1.prm
 TLIM=300 run cavity3d-q1-64 3 cavity3d_q1_64_steady.prm
 TLIM=600 run cavity3d-q2-128-bdf2 3 cavity3d_q2_128_bdf2.prm
 echo done >> $O/summary.txt
+# the reference's TGV SDIRK2 / SDIRK3 application tests as shipped (inexact Newton: tol 1e-6, GMRES rel 1e-4)
+cp $R/tests/golden/app_cases/taylor-green-vortex_gls_sdirk*.prm $O/
+sed -i 's/set output frequency *= *1 /set output frequency = 1000000 /' $O/taylor-green-vortex_gls_sdirk*.prm
+TLIM=300 run tgv-sdirk2 2 taylor-green-vortex_gls_sdirk2.prm --precision 9
+TLIM=300 run tgv-sdirk3 2 taylor-green-vortex_gls_sdirk3.prm --precision 9
+echo done2 >> $O/summary.txt
