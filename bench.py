@@ -182,6 +182,9 @@ def main():
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo stages through the host (testing on one GPU)")
+    ap.add_argument("--dist-impl", default="torch", choices=["torch", "native"],
+                    help="ghost exchange / reductions: torch.distributed callbacks (default) or the library's own "
+                         "RCCL communicator (gls_dist_attach_rccl: ncclSend/ncclRecv/ncclAllReduce on the context stream)")
     args = ap.parse_args()
 
     import torch
@@ -231,7 +234,7 @@ def main():
         bcs = [("noslip", b, None) for b in (0, 1, 2, 4, 5)] + [("function", 3, (1.0, 0.0, 0.0))]
         mask, ddofs, dvals = dirichlet_from_bcs(mesh, args.n, -1.0, 1.0, True, bcs)
         dp = DistributedProblem(mesh, rank, world, dev, viscosity=args.nu, vnode_mask=mask, dirichlet=(ddofs, dvals),
-                                backend=args.dist_backend)
+                                backend=args.dist_backend, impl=args.dist_impl)
         ctx = dp.ctx
         if args.precond == "mg":  # the same V-cycle on nested per-rank boxes (RCCL ghosts per level)
             from softx_2020_200_amd.dist import attach_distributed_multigrid, multigrid_levels
@@ -240,7 +243,7 @@ def main():
                 mm = sx.hyper_cube(3, m, args.k, args.kp, -1.0, 1.0)
                 mk, dd, dv = dirichlet_from_bcs(mm, m, -1.0, 1.0, True, bcs)
                 lv.append(DistributedProblem(mm, rank, world, dev, viscosity=args.nu, vnode_mask=mk,
-                                             dirichlet=(dd, dv), backend=args.dist_backend))
+                                             dirichlet=(dd, dv), backend=args.dist_backend, impl=args.dist_impl))
             attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
                                          omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
                                          coarse_omega=args.mg_coarse_omega,

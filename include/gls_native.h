@@ -281,6 +281,20 @@ int gls_dist_attach(gls_ctx *ctx, int64_t n_owned_nodes, int n_nbrs, const int64
                     double *recv_buf, double *red_buf, gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user);
 /* refresh ghost entries of a DEVICE vector (e.g. the history vectors once per time step) */
 int gls_dist_import(gls_ctx *ctx, double *x);
+/* In-library RCCL transport (replaces the callbacks above; the reference's Trilinos ghosted vectors
+ * and compress(add), gls_navier_stokes.cc:186-202, 774-776): rank 0 calls gls_rccl_unique_id and
+ * broadcasts the GLS_RCCL_ID_BYTES bytes by any means; every rank calls gls_rccl_create (one
+ * communicator per process, shared by all contexts, e.g. every multigrid level), then
+ * gls_dist_attach_rccl per context with the gls_part_get lists. Ghost import / export-add are
+ * grouped ncclSend / ncclRecv and the dot products ncclAllReduce, all on the context stream. */
+#define GLS_RCCL_ID_BYTES 128
+typedef struct gls_rccl gls_rccl;
+int gls_rccl_unique_id(unsigned char *id_out);
+int gls_rccl_create(const unsigned char *id, int rank, int world, gls_rccl **out);
+int gls_rccl_destroy(gls_rccl *comm);
+int gls_dist_attach_rccl(gls_ctx *ctx, gls_rccl *comm, int64_t n_owned_nodes, int n_nbrs, const int *nbr_ranks,
+                         const int64_t *send_offsets, const int32_t *send_nodes, const int64_t *recv_offsets,
+                         const int32_t *recv_nodes);
 
 /* ------------------------------------------------------------------------------------------
  * Host-side building blocks (host pointers).

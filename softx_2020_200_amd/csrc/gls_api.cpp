@@ -19,6 +19,7 @@
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 #include <rocsparse/rocsparse.h>
+#include <rccl/rccl.h>
 
 #include "../../include/gls_native.h"
 #include "gls_common.hpp"
@@ -329,6 +330,12 @@ struct gls_ctx {
     gls_exchange_fn xchg = nullptr;
     gls_allreduce_fn allreduce = nullptr;
     void *user = nullptr;
+    // in-library RCCL transport (gls_dist_attach_rccl): grouped ncclSend / ncclRecv and ncclAllReduce
+    // enqueued on the context stream -- no host callback, no host synchronisation per exchange
+    ncclComm_t comm = nullptr;
+    std::vector<int> nbrs;
+    std::vector<int64_t> soff, roff;
+    DevBuf<double> own_send, own_recv, own_red;
   } dist;
   // assembled ILU(0) preconditioner (gls_ilu_attach; the reference's setup_ILU,
   // gls_navier_stokes.cc:1161-1176): the Jacobian is assembled into CSR by probing the matrix-free
@@ -2990,4 +2997,91 @@ extern "C" int gls_ilu_info(const gls_ctx *c, int64_t *nnz, int *n_probes) {
   if (nnz) *nnz = c->ilu.nnz;
   if (n_probes) *n_probes = c->ilu.n_probes;
   return c->ilu.on ? GLS_OK : set_err(GLS_EINVAL, "no ILU attached");
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// In-library RCCL over xGMI (the reference's Trilinos ghost import / compress(add) and
+// MPI_Allreduce, gls_navier_stokes.cc:186-202, 774-776): one communicator per process, shared by
+// the contexts of every multigrid level; exchanges and reductions are enqueued on the context
+// stream (RCCL orders them with the pack / unpack kernels), so no exchange blocks the host.
+// ---------------------------------------------------------------------------------------------
+struct gls_rccl {
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+};
+namespace {
+int rccl_exchange(void *user, int phase) {
+  gls_ctx *c = static_cast<gls_ctx *>(user);
+  auto &D = c->dist;
+  // phase 0 (import): send send_buf segments (owned nodes others ghost), receive into recv_buf;
+  // phase 1 (export-add): the reverse (ghost partial sums back to their owners)
+  double *sb = phase == 0 ? D.send_buf : D.recv_buf, *rb = phase == 0 ? D.recv_buf : D.send_buf;
+  const std::vector<int64_t> &so = phase == 0 ? D.soff : D.roff, &ro = phase == 0 ? D.roff : D.soff;
+  if (ncclGroupStart() != ncclSuccess) return -1;
+  for (size_t i = 0; i < D.nbrs.size(); ++i) {
+    const size_t ns = (size_t)(4 * (so[i + 1] - so[i])), nr = (size_t)(4 * (ro[i + 1] - ro[i]));
+    if (ns && ncclSend(sb + 4 * so[i], ns, ncclDouble, D.nbrs[i], D.comm, c->stream) != ncclSuccess) return -1;
+    if (nr && ncclRecv(rb + 4 * ro[i], nr, ncclDouble, D.nbrs[i], D.comm, c->stream) != ncclSuccess) return -1;
+  }
+  return ncclGroupEnd() == ncclSuccess ? 0 : -1;
+}
+int rccl_allreduce(void *user, double *buf, int n) {
+  gls_ctx *c = static_cast<gls_ctx *>(user);
+  return ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, c->dist.comm, c->stream) == ncclSuccess ? 0 : -1;
+}
+}  // namespace
+
+extern "C" int gls_rccl_unique_id(unsigned char *id_out) {
+  if (!id_out) return set_err(GLS_EINVAL, "gls_rccl_unique_id: null output");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return set_err(GLS_ECOMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  static_assert(sizeof(id) == GLS_RCCL_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id_out, &id, sizeof(id));
+  return GLS_OK;
+}
+extern "C" int gls_rccl_create(const unsigned char *id_in, int rank, int world, gls_rccl **out) {
+  if (!id_in || !out || world < 1 || rank < 0 || rank >= world) return set_err(GLS_EINVAL, "gls_rccl_create: bad arguments");
+  ncclUniqueId id;
+  std::memcpy(&id, id_in, sizeof(id));
+  auto r = std::make_unique<gls_rccl>();
+  const ncclResult_t e = ncclCommInitRank(&r->comm, world, id, rank);
+  if (e != ncclSuccess) return set_err(GLS_ECOMM, "ncclCommInitRank(%d of %d): %s", rank, world, ncclGetErrorString(e));
+  r->rank = rank;
+  r->world = world;
+  *out = r.release();
+  return GLS_OK;
+}
+extern "C" int gls_rccl_destroy(gls_rccl *r) {
+  if (!r) return GLS_OK;
+  if (r->comm) (void)ncclCommDestroy(r->comm);
+  delete r;
+  return GLS_OK;
+}
+extern "C" int gls_dist_attach_rccl(gls_ctx *c, gls_rccl *r, int64_t n_owned_nodes, int n_nbrs, const int *nbr_ranks,
+                                    const int64_t *send_offsets, const int32_t *send_nodes, const int64_t *recv_offsets,
+                                    const int32_t *recv_nodes) {
+  GLS_TRY(check_ctx(c));
+  if (!r || !r->comm || n_nbrs < 0 || (n_nbrs > 0 && (!nbr_ranks || !send_offsets || !recv_offsets)))
+    return set_err(GLS_EINVAL, "gls_dist_attach_rccl: bad arguments");
+  auto &D = c->dist;
+  const int64_t ns = n_nbrs ? send_offsets[n_nbrs] : 0, nr = n_nbrs ? recv_offsets[n_nbrs] : 0;
+  for (int i = 0; i < n_nbrs; ++i)
+    if (nbr_ranks[i] < 0 || nbr_ranks[i] >= r->world || nbr_ranks[i] == r->rank)
+      return set_err(GLS_EINVAL, "gls_dist_attach_rccl: neighbour rank %d", nbr_ranks[i]);
+  GLS_TRY(D.own_send.alloc((size_t)std::max<int64_t>(4 * ns, 1)));
+  GLS_TRY(D.own_recv.alloc((size_t)std::max<int64_t>(4 * nr, 1)));
+  GLS_TRY(D.own_red.alloc(256));
+  GLS_TRY(gls_dist_attach(c, n_owned_nodes, n_nbrs, send_offsets, send_nodes, recv_offsets, recv_nodes, D.own_send.p,
+                          D.own_recv.p, D.own_red.p, rccl_exchange, rccl_allreduce, c));
+  D.comm = r->comm;
+  D.nbrs.assign(nbr_ranks, nbr_ranks + n_nbrs);
+  D.soff.assign(send_offsets, send_offsets + n_nbrs + 1);
+  D.roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);
+  if (n_nbrs == 0) {
+    D.soff.assign(1, 0);
+    D.roff.assign(1, 0);
+  }
+  return GLS_OK;
 }

@@ -34,6 +34,11 @@ def _bind(L):
     L.gls_dist_attach.argtypes = [vp, i64, C.c_int, C.POINTER(i64), C.POINTER(C.c_int32), C.POINTER(i64),
                                   C.POINTER(C.c_int32), vp, vp, vp, EXCHANGE_FN, ALLREDUCE_FN, vp]
     L.gls_dist_import.argtypes = [vp, vp]
+    L.gls_rccl_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
+    L.gls_rccl_create.argtypes = [C.POINTER(C.c_ubyte), C.c_int, C.c_int, C.POINTER(vp)]
+    L.gls_rccl_destroy.argtypes = [vp]
+    L.gls_dist_attach_rccl.argtypes = [vp, vp, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int32),
+                                       C.POINTER(i64), C.POINTER(C.c_int32)]
     L._dist_bound = True
     return L
 
@@ -160,6 +165,42 @@ def attach(ctx: GLSContext, plan, exchanger: Exchanger):
     ctx._plan = plan
 
 
+_RCCL = {}
+
+
+def rccl_comm(rank, world, group=None):
+    """The process's in-library RCCL communicator (gls_rccl_create), created once and shared by every
+    context (all multigrid levels); rank 0's unique id travels through torch.distributed."""
+    key = (rank, world, id(group))
+    if key not in _RCCL:
+        import torch.distributed as dist
+        L = _bind(load())
+        buf = (C.c_ubyte * 128)()
+        if rank == 0:
+            check(L.gls_rccl_unique_id(buf), "gls_rccl_unique_id")
+        obj = [bytes(buf) if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0, group=group)
+        idb = (C.c_ubyte * 128).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        check(L.gls_rccl_create(idb, rank, world, C.byref(h)), "gls_rccl_create")
+        _RCCL[key] = h
+    return _RCCL[key]
+
+
+def attach_rccl(ctx: GLSContext, plan, comm):
+    """Attach the rank-local context to the in-library RCCL transport (no Python on the data path)."""
+    L = _bind(load())
+    p = plan
+    nbrs = np.ascontiguousarray(p["nbrs"], dtype=np.int32)
+    check(L.gls_dist_attach_rccl(ctx.h, comm, int(p["n_owned"]), len(nbrs), nbrs.ctypes.data_as(C.POINTER(C.c_int)),
+                                 p["send_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                                 p["send_nodes"].ctypes.data_as(C.POINTER(C.c_int32)),
+                                 p["recv_off"].ctypes.data_as(C.POINTER(C.c_int64)),
+                                 p["recv_nodes"].ctypes.data_as(C.POINTER(C.c_int32))), "gls_dist_attach_rccl")
+    ctx._plan = plan
+
+
 def dist_import(ctx, x):
     L = _bind(load())
     check(L.gls_dist_import(ctx.h, C.c_void_p(x.data_ptr())), "gls_dist_import")
@@ -194,7 +235,7 @@ class DistributedProblem:
     """Rank-local GLS context on a Morton brick mesh (3D Qk-Qk), attached to the exchanger."""
 
     def __init__(self, mesh, rank, world, device, viscosity=1.0, vnode_mask=None, dirichlet=None, force_q=None,
-                 backend="nccl", group=None):
+                 backend="nccl", group=None, impl="torch"):
         if mesh["k"] != mesh["kp"] or mesh["dim"] != 3:
             raise GLSError("distributed path: 3D Qk-Qk only")
         plan = partition(mesh["cell_vnodes"], mesh["n_vnodes"], rank, world)
@@ -214,8 +255,12 @@ class DistributedProblem:
             node = g2l[gdofs // 3]
             sel = node >= 0
             self.ctx.set_dirichlet(3 * node[sel] + gdofs[sel] % 3, np.asarray(gvals)[sel])
-        self.exchanger = Exchanger(plan, device, backend=backend, group=group)
-        attach(self.ctx, plan, self.exchanger)
+        if impl == "native":  # in-library RCCL: ncclSend / ncclRecv / ncclAllReduce on the context stream
+            self.exchanger = None
+            attach_rccl(self.ctx, plan, rccl_comm(rank, world, group))
+        else:  # torch.distributed callbacks ("nccl" = RCCL through torch, "gloo" through the host)
+            self.exchanger = Exchanger(plan, device, backend=backend, group=group)
+            attach(self.ctx, plan, self.exchanger)
         self.n_dofs_local = self.ctx.n_dofs
 
     def set_lattice(self):

@@ -16,11 +16,12 @@ run() {  # name dim prm [extra]
   echo "$name rc=$rc wall_s=$(echo "$(date +%s.%N) - $t0" | bc)" >> $O/summary.txt
   if [ $rc -ge 124 ]; then exit $rc; fi
 }
-cp $R/tests/golden/app_cases/example-0*.prm $R/apps/cases/*.prm $O/
+cp $R/tests/golden/app_cases/example-0*.prm $R/apps/cases/*.prm $R/apps/cases/*.msh $O/
 TLIM=300 run example-01-cavity 2 example-01-cavity.prm
 TLIM=300 run example-02-taylor-couette 2 example-02-taylor-couette.prm
 TLIM=300 run taylor-couette3d 3 taylor-couette3d_q2q1.prm
 TLIM=300 run cavity3d-q1-64 3 cavity3d_q1_64_steady.prm
+TLIM=400 run cylinder3d-re200 3 cylinder3d_q2q1_re200.prm
 TLIM=600 run cavity3d-q2-128-bdf2 3 cavity3d_q2_128_bdf2.prm
 echo done >> $O/summary.txt
 # the reference's TGV SDIRK2 / SDIRK3 application tests as shipped (inexact Newton: tol 1e-6, GMRES rel 1e-4)
@@ -29,3 +30,4 @@ sed -i 's/set output frequency *= *1 /set output frequency = 1000000 /' $O/taylo
 TLIM=300 run tgv-sdirk2 2 taylor-green-vortex_gls_sdirk2.prm --precision 9
 TLIM=300 run tgv-sdirk3 2 taylor-green-vortex_gls_sdirk3.prm --precision 9
 echo done2 >> $O/summary.txt
+rm -f $O/*.msh
