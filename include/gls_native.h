@@ -347,6 +347,25 @@ typedef struct {
 int gls_mesh_refined_create(int dim, int n, int k, int kp, double lo, double hi, const int32_t *refine,
                             gls_refined_mesh **out);
 int gls_mesh_refined_destroy(gls_refined_mesh *mesh);
+/* Multi-level adaptive refinement of a hyper_cube (the reference's p4est forest,
+ * navier_stokes_base.cc:55-60, 592-780): an octree over n^dim level-0 cells, leaves in p4est's
+ * depth-first Morton order. gls_octree_adapt refines flagged leaves (below max_level), coarsens
+ * complete sibling groups that are all flagged (above min_level) when that keeps the vertex 2:1
+ * balance, and restores the balance by refinement (limit_level_difference_at_vertices).
+ * gls_octree_mesh builds the FE_Q(k) x FE_Q(kp) node spaces with hanging lines whose masters are
+ * all unconstrained (make_hanging_node_constraints + close()), as a gls_refined_mesh (free it with
+ * gls_octree_mesh_destroy); gls_octree_transfer is SolutionTransfer between two such meshes of the
+ * same cube (host vectors, [velocity node-major | pressure]). */
+typedef struct gls_octree gls_octree;
+int gls_octree_create(int dim, int n, gls_octree **out);
+void gls_octree_destroy(gls_octree *tree);
+int gls_octree_info(const gls_octree *tree, int64_t *n_cells, int *max_level);
+int gls_octree_cells(const gls_octree *tree, int32_t *level, double *x0, double *h, double lo, double hi);
+int gls_octree_adapt(gls_octree *tree, const int32_t *refine, const int32_t *coarsen, int max_level, int min_level);
+int gls_octree_mesh(const gls_octree *tree, int k, int kp, double lo, double hi, gls_refined_mesh **out);
+int gls_octree_mesh_destroy(gls_refined_mesh *mesh);
+int gls_octree_transfer(const gls_refined_mesh *old_mesh, const gls_refined_mesh *new_mesh, const double *old_vec,
+                        double *new_vec);
 /* Kelly error indicator per cell: KellyErrorEstimator<dim>::estimate as
  * refine_mesh_kelly calls it (navier_stokes_base.cc:612-652) — face rule QGauss<dim-1>(n_q + 1),
  * no Neumann boundaries (boundary faces add nothing), deal.II's default cell_diameter_over_24:

@@ -1,0 +1,546 @@
+// gls_octree.cpp — multi-level adaptive refinement of a hyper_cube (host C++17).
+//
+// The reference adapts a p4est forest (parallel::distributed::Triangulation with
+// smoothing_on_refinement | smoothing_on_coarsening, navier_stokes_base.cc:55-60, 592-780):
+// refine / coarsen flags from the Kelly thresholds, at most one level of difference between cells
+// that share a vertex (limit_level_difference_at_vertices = p4est corner balance), coarsening only
+// of complete sibling groups, then DoFTools::make_hanging_node_constraints with chains closed by
+// AffineConstraints::close (gls_navier_stokes.cc:84, 143) and SolutionTransfer.
+// Here the forest is one tree over hyper_cube(lo, hi) with n^dim level-0 cells; a leaf of level l
+// covers a block of 2^(L-l) cells of the finest level L. Leaves are kept in depth-first Morton
+// order (children lexicographic, x fastest), which is p4est's order for a single tree.
+// gls_octree_mesh builds the FE_Q(k) / FE_Q(kp) node spaces on the finest node lattice with
+// hanging lines whose masters are all unconstrained (chains resolved).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gls_native.h"
+
+int gls_io_set_error(int code, const char *fmt, ...);  // gls_api.cpp
+
+struct gls_octree {
+  int dim = 3, n = 1;
+  struct Leaf {
+    int level;
+    int64_t x[3];  // origin in units of its own level's cells
+  };
+  std::vector<Leaf> leaves;
+  int max_level() const {
+    int L = 0;
+    for (const Leaf &c : leaves) L = std::max(L, c.level);
+    return L;
+  }
+};
+
+namespace {
+
+using Leaf = gls_octree::Leaf;
+
+// Morton key of a leaf's origin at level L (interleaved bits; base-grid index in the high bits)
+uint64_t morton_key(const gls_octree &t, const Leaf &c, int L) {
+  int64_t p[3] = {0, 0, 0};
+  for (int d = 0; d < t.dim; ++d) p[d] = c.x[d] << (L - c.level);
+  // base cell (level 0 block) lexicographic first, then the Morton order inside it
+  const int64_t s = (int64_t)1 << L;
+  int64_t base = 0, st = 1;
+  for (int d = 0; d < t.dim; ++d) {
+    base += (p[d] / s) * st;
+    st *= t.n;
+  }
+  uint64_t m = 0;
+  for (int b = L - 1; b >= 0; --b)
+    for (int d = t.dim - 1; d >= 0; --d) m = (m << 1) | (uint64_t)(((p[d] % s) >> b) & 1);
+  return ((uint64_t)base << (t.dim * L)) | m;
+}
+void sort_leaves(gls_octree &t) {
+  const int L = t.max_level();
+  std::stable_sort(t.leaves.begin(), t.leaves.end(),
+                   [&](const Leaf &a, const Leaf &b) { return morton_key(t, a, L) < morton_key(t, b, L); });
+}
+
+// level of the leaf covering every finest-level cell (a dense grid: small trees only)
+struct LevelGrid {
+  int dim, L;
+  int64_t N;  // finest cells per direction
+  std::vector<int8_t> lev;
+  int at(const int64_t *p) const {
+    for (int d = 0; d < dim; ++d)
+      if (p[d] < 0 || p[d] >= N) return -1;
+    int64_t id = 0, st = 1;
+    for (int d = 0; d < dim; ++d) {
+      id += p[d] * st;
+      st *= N;
+    }
+    return lev[(size_t)id];
+  }
+};
+int make_grid(const gls_octree &t, int L, LevelGrid &g) {
+  g.dim = t.dim;
+  g.L = L;
+  g.N = (int64_t)t.n << L;
+  int64_t tot = 1;
+  for (int d = 0; d < t.dim; ++d) tot *= g.N;
+  if (tot > ((int64_t)1 << 28)) return gls_io_set_error(GLS_EINVAL, "octree: finest grid too large");
+  g.lev.assign((size_t)tot, -1);
+  for (const Leaf &c : t.leaves) {
+    const int64_t s = (int64_t)1 << (L - c.level);
+    int64_t nb = 1;
+    for (int d = 0; d < t.dim; ++d) nb *= s;
+    for (int64_t b = 0; b < nb; ++b) {
+      int64_t r = b, id = 0, st = 1;
+      for (int d = 0; d < t.dim; ++d) {
+        id += (c.x[d] * s + r % s) * st;
+        r /= s;
+        st *= g.N;
+      }
+      g.lev[(size_t)id] = (int8_t)c.level;
+    }
+  }
+  return GLS_OK;
+}
+// highest leaf level in the one-cell shell around leaf c (cells sharing a vertex with c)
+int shell_max(const LevelGrid &g, const Leaf &c) {
+  const int64_t s = (int64_t)1 << (g.L - c.level);
+  int64_t lo[3] = {0, 0, 0}, ext[3] = {1, 1, 1};
+  for (int d = 0; d < g.dim; ++d) {
+    lo[d] = c.x[d] * s - 1;
+    ext[d] = s + 2;
+  }
+  int m = -1;
+  int64_t nb = 1;
+  for (int d = 0; d < g.dim; ++d) nb *= ext[d];
+  for (int64_t b = 0; b < nb; ++b) {
+    int64_t p[3] = {0, 0, 0}, r = b;
+    bool inside = true;
+    for (int d = 0; d < g.dim; ++d) {
+      p[d] = lo[d] + r % ext[d];
+      r /= ext[d];
+      inside = inside && p[d] > lo[d] && p[d] < lo[d] + ext[d] - 1;
+    }
+    if (inside) continue;
+    m = std::max(m, g.at(p));
+  }
+  return m;
+}
+
+std::vector<Leaf> children(const gls_octree &t, const Leaf &c) {
+  std::vector<Leaf> out;
+  for (int ch = 0; ch < (1 << t.dim); ++ch) {
+    Leaf k{c.level + 1, {0, 0, 0}};
+    for (int d = 0; d < t.dim; ++d) k.x[d] = 2 * c.x[d] + ((ch >> d) & 1);
+    out.push_back(k);
+  }
+  return out;
+}
+
+// 2:1 balance over vertices: refine every leaf that shares a vertex with a leaf two levels finer
+int balance(gls_octree &t) {
+  for (int it = 0; it < 64; ++it) {
+    const int L = t.max_level();
+    LevelGrid g;
+    if (int rc = make_grid(t, L, g); rc != GLS_OK) return rc;
+    std::vector<Leaf> next;
+    bool changed = false;
+    for (const Leaf &c : t.leaves) {
+      if (shell_max(g, c) >= c.level + 2) {
+        for (const Leaf &k : children(t, c)) next.push_back(k);
+        changed = true;
+      } else {
+        next.push_back(c);
+      }
+    }
+    t.leaves.swap(next);
+    if (!changed) break;
+  }
+  return GLS_OK;
+}
+
+double lagrange(int k, int a, double xi) {  // degree-k Lagrange basis a on the nodes b/k
+  double v = 1.0;
+  for (int b = 0; b <= k; ++b)
+    if (b != a) v *= (xi - (double)b / k) / ((double)(a - b) / k);
+  return v;
+}
+
+struct MeshImpl {
+  gls_refined_mesh pub{};
+  std::vector<int32_t> cell_vnodes, cell_pnodes, cell_level;
+  std::vector<double> cell_x0, cell_h, vnode_x, pnode_x;
+  std::vector<int64_t> vh_node, vh_off, vh_master, ph_node, ph_off, ph_master;
+  std::vector<double> vh_w, ph_w;
+  // for transfers: the tree geometry
+  int n = 1, L = 0;
+  double lo = 0, hi = 1;
+};
+
+// FE_Q(kk) nodes on the finest node lattice (spacing h_L / kk), hanging lines with chains closed
+int build_space(const gls_octree &t, int L, int kk, double lo, double hf, std::vector<int32_t> &cell_nodes,
+                std::vector<double> &node_x, std::vector<int64_t> &hnode, std::vector<int64_t> &hoff,
+                std::vector<double> &hw, std::vector<int64_t> &hmaster) {
+  const int dim = t.dim;
+  const int64_t np1 = (int64_t)kk * ((int64_t)t.n << L) + 1;
+  int64_t npts = 1;
+  for (int d = 0; d < dim; ++d) npts *= np1;
+  if (npts > ((int64_t)1 << 31)) return gls_io_set_error(GLS_EINVAL, "octree mesh lattice too large");
+  auto lat = [&](const int64_t *p) {
+    int64_t id = 0, st = 1;
+    for (int d = 0; d < dim; ++d) {
+      id += p[d] * st;
+      st *= np1;
+    }
+    return id;
+  };
+  const int K1 = kk + 1;
+  int npc = 1;
+  for (int d = 0; d < dim; ++d) npc *= K1;
+  // lattice point of local node a of leaf c: kk * origin + a * s, s = finest cells per leaf edge
+  auto cell_point = [&](const Leaf &c, int a, int64_t *p) {
+    const int64_t s = (int64_t)1 << (L - c.level);
+    int r = a;
+    for (int d = 0; d < dim; ++d) {
+      p[d] = (int64_t)kk * c.x[d] * s + (int64_t)(r % K1) * s;
+      r /= K1;
+    }
+  };
+  std::unordered_map<int64_t, int32_t> id;
+  id.reserve((size_t)t.leaves.size() * npc);
+  for (const Leaf &c : t.leaves)
+    for (int a = 0; a < npc; ++a) {
+      int64_t p[3];
+      cell_point(c, a, p);
+      id.emplace(lat(p), 0);
+    }
+  std::vector<int64_t> used;
+  used.reserve(id.size());
+  for (auto &kv : id) used.push_back(kv.first);
+  std::sort(used.begin(), used.end());  // lexicographic lattice order (x fastest)
+  node_x.clear();
+  for (size_t i = 0; i < used.size(); ++i) {
+    id[used[i]] = (int32_t)i;
+    int64_t r = used[i];
+    for (int d = 0; d < dim; ++d) {
+      node_x.push_back(lo + (double)(r % np1) * hf / kk);
+      r /= np1;
+    }
+  }
+  cell_nodes.resize(t.leaves.size() * (size_t)npc);
+  for (size_t ci = 0; ci < t.leaves.size(); ++ci)
+    for (int a = 0; a < npc; ++a) {
+      int64_t p[3];
+      cell_point(t.leaves[ci], a, p);
+      cell_nodes[ci * npc + a] = id[lat(p)];
+    }
+  // raw lines: a used lattice point on the closed box of a leaf that is not one of its nodes is
+  // hanging on that leaf's Qk interpolant (only a finer neighbour uses it)
+  std::map<int32_t, std::vector<std::pair<int32_t, double>>> line;
+  for (const Leaf &c : t.leaves) {
+    if (c.level == L) continue;
+    const int64_t s = (int64_t)1 << (L - c.level), span = (int64_t)kk * s;
+    int64_t nbox = 1;
+    for (int d = 0; d < dim; ++d) nbox *= span + 1;
+    for (int64_t b = 0; b < nbox; ++b) {
+      int64_t off[3] = {0, 0, 0}, p[3] = {0, 0, 0}, r = b;
+      bool on_boundary = false, is_node = true;
+      for (int d = 0; d < dim; ++d) {
+        off[d] = r % (span + 1);
+        r /= span + 1;
+        on_boundary = on_boundary || off[d] == 0 || off[d] == span;
+        is_node = is_node && off[d] % s == 0;
+        p[d] = (int64_t)kk * c.x[d] * s + off[d];
+      }
+      if (!on_boundary || is_node) continue;
+      auto it = id.find(lat(p));
+      if (it == id.end() || line.count(it->second)) continue;
+      std::vector<std::pair<int32_t, double>> ln;
+      for (int a = 0; a < npc; ++a) {
+        double w = 1.0;
+        int rr = a;
+        int64_t q[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) {
+          const int ad = rr % K1;
+          rr /= K1;
+          w *= lagrange(kk, ad, (double)off[d] / span);
+          q[d] = (int64_t)kk * c.x[d] * s + (int64_t)ad * s;
+        }
+        if (std::fabs(w) < 1e-13) continue;
+        ln.push_back({id[lat(q)], w});
+      }
+      line[it->second] = ln;
+    }
+  }
+  // close the chains (AffineConstraints::close): substitute hanging masters by their lines
+  for (int pass = 0; pass < 32; ++pass) {
+    bool changed = false;
+    for (auto &kv : line) {
+      std::map<int32_t, double> acc;
+      bool sub = false;
+      for (auto &mw : kv.second) {
+        auto it = line.find(mw.first);
+        if (it == line.end()) {
+          acc[mw.first] += mw.second;
+        } else {
+          sub = true;
+          for (auto &m2 : it->second) acc[m2.first] += mw.second * m2.second;
+        }
+      }
+      if (sub) {
+        kv.second.clear();
+        for (auto &a : acc)
+          if (std::fabs(a.second) > 1e-14) kv.second.push_back(a);
+        changed = true;
+      }
+    }
+    if (!changed) break;
+    if (pass == 31) return gls_io_set_error(GLS_EINVAL, "octree: hanging-node chains do not close");
+  }
+  hnode.clear();
+  hoff.assign(1, 0);
+  hw.clear();
+  hmaster.clear();
+  for (auto &kv : line) {
+    hnode.push_back(kv.first);
+    for (auto &mw : kv.second) {
+      hmaster.push_back(mw.first);
+      hw.push_back(mw.second);
+    }
+    hoff.push_back((int64_t)hmaster.size());
+  }
+  return GLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gls_octree_create(int dim, int n, gls_octree **out) {
+  if (!out || (dim != 2 && dim != 3) || n < 1) return gls_io_set_error(GLS_EINVAL, "gls_octree_create: dim 2/3, n >= 1");
+  auto t = std::make_unique<gls_octree>();
+  t->dim = dim;
+  t->n = n;
+  for (int64_t c = 0, nc = dim == 3 ? (int64_t)n * n * n : (int64_t)n * n; c < nc; ++c) {
+    Leaf l{0, {c % n, (c / n) % n, dim == 3 ? c / ((int64_t)n * n) : 0}};
+    t->leaves.push_back(l);
+  }
+  sort_leaves(*t);
+  *out = t.release();
+  return GLS_OK;
+}
+void gls_octree_destroy(gls_octree *t) { delete t; }
+
+int gls_octree_info(const gls_octree *t, int64_t *n_cells, int *max_level) {
+  if (!t) return gls_io_set_error(GLS_EINVAL, "null octree");
+  if (n_cells) *n_cells = (int64_t)t->leaves.size();
+  if (max_level) *max_level = t->max_level();
+  return GLS_OK;
+}
+
+int gls_octree_cells(const gls_octree *t, int32_t *level, double *x0, double *h, double lo, double hi) {
+  if (!t) return gls_io_set_error(GLS_EINVAL, "null octree");
+  for (size_t i = 0; i < t->leaves.size(); ++i) {
+    const Leaf &c = t->leaves[i];
+    const double hc = (hi - lo) / ((double)t->n * (double)((int64_t)1 << c.level));
+    if (level) level[i] = c.level;
+    for (int d = 0; d < t->dim; ++d) {
+      if (x0) x0[i * t->dim + d] = lo + c.x[d] * hc;
+      if (h) h[i * t->dim + d] = hc;
+    }
+  }
+  return GLS_OK;
+}
+
+// execute_coarsening_and_refinement: flagged leaves below max_level are refined, complete sibling
+// groups whose members are all flagged for coarsening (and none for refinement) above min_level are
+// coarsened unless that breaks the vertex 2:1 balance, then the balance is restored by refinement
+int gls_octree_adapt(gls_octree *t, const int32_t *refine, const int32_t *coarsen, int max_level, int min_level) {
+  if (!t) return gls_io_set_error(GLS_EINVAL, "null octree");
+  const size_t nc = t->leaves.size();
+  std::vector<Leaf> next;
+  std::map<std::vector<int64_t>, std::vector<size_t>> groups;  // parent key -> member leaves
+  std::vector<char> coarse_ok(nc, 0);
+  for (size_t i = 0; i < nc; ++i) {
+    const Leaf &c = t->leaves[i];
+    if (coarsen && coarsen[i] && !(refine && refine[i]) && c.level > min_level) {
+      std::vector<int64_t> key{c.level - 1, c.x[0] / 2, c.x[1] / 2, c.x[2] / 2};
+      groups[key].push_back(i);
+    }
+  }
+  // coarsening candidates: complete groups that keep the balance with the refined neighbours
+  int L = t->max_level() + 1;
+  std::vector<Leaf> refined;
+  for (size_t i = 0; i < nc; ++i) {
+    const Leaf &c = t->leaves[i];
+    if (refine && refine[i] && c.level < max_level)
+      for (const Leaf &k : children(*t, c)) refined.push_back(k);
+    else
+      refined.push_back(c);
+  }
+  gls_octree tmp = *t;
+  tmp.leaves = refined;
+  if (int rc = balance(tmp); rc != GLS_OK) return rc;
+  L = std::max(L, tmp.max_level());
+  LevelGrid g;
+  if (int rc = make_grid(tmp, tmp.max_level(), g); rc != GLS_OK) return rc;
+  std::map<std::vector<int64_t>, char> drop;  // parents that replace their children
+  std::map<std::vector<int64_t>, char> is_leaf;
+  for (const Leaf &c : tmp.leaves) is_leaf[{c.level, c.x[0], c.x[1], c.x[2]}] = 1;
+  for (auto &kv : groups) {
+    if ((int)kv.second.size() != (1 << t->dim)) continue;
+    Leaf p{(int)kv.first[0], {kv.first[1], kv.first[2], kv.first[3]}};
+    // every child is still a leaf after the refinement / balance pass, and no leaf sharing a
+    // vertex with the parent is two levels finer than the parent
+    bool ok = true;
+    for (const Leaf &ch : children(*t, p)) ok = ok && is_leaf.count({ch.level, ch.x[0], ch.x[1], ch.x[2]});
+    if (!ok || shell_max(g, p) >= p.level + 2) continue;
+    drop[kv.first] = 1;
+  }
+  next.clear();
+  std::map<std::vector<int64_t>, char> emitted;
+  for (const Leaf &c : tmp.leaves) {
+    if (c.level > 0) {
+      std::vector<int64_t> key{c.level - 1, c.x[0] / 2, c.x[1] / 2, c.x[2] / 2};
+      if (drop.count(key)) {
+        if (!emitted.count(key)) {
+          emitted[key] = 1;
+          next.push_back(Leaf{c.level - 1, {key[1], key[2], key[3]}});
+        }
+        continue;
+      }
+    }
+    next.push_back(c);
+  }
+  t->leaves.swap(next);
+  if (int rc = balance(*t); rc != GLS_OK) return rc;
+  sort_leaves(*t);
+  return GLS_OK;
+}
+
+int gls_octree_mesh(const gls_octree *t, int k, int kp, double lo, double hi, gls_refined_mesh **out) {
+  if (!t || !out || k < 1 || k > 2 || kp < 1 || kp > k || !(hi > lo))
+    return gls_io_set_error(GLS_EINVAL, "gls_octree_mesh: 1 <= kp <= k <= 2");
+  const int L = t->max_level(), dim = t->dim;
+  auto M = std::make_unique<MeshImpl>();
+  const double hf = (hi - lo) / ((double)t->n * (double)((int64_t)1 << L));
+  int rc = build_space(*t, L, k, lo, hf, M->cell_vnodes, M->vnode_x, M->vh_node, M->vh_off, M->vh_w, M->vh_master);
+  if (rc != GLS_OK) return rc;
+  rc = build_space(*t, L, kp, lo, hf, M->cell_pnodes, M->pnode_x, M->ph_node, M->ph_off, M->ph_w, M->ph_master);
+  if (rc != GLS_OK) return rc;
+  for (const Leaf &c : t->leaves) {
+    const double hc = hf * (double)((int64_t)1 << (L - c.level));
+    for (int d = 0; d < dim; ++d) {
+      M->cell_x0.push_back(lo + (double)c.x[d] * hc);
+      M->cell_h.push_back(hc);
+    }
+    M->cell_level.push_back(c.level);
+  }
+  M->n = t->n;
+  M->L = L;
+  M->lo = lo;
+  M->hi = hi;
+  gls_refined_mesh &p = M->pub;
+  p.dim = dim;
+  p.k = k;
+  p.kp = kp;
+  p.n_cells = (int64_t)t->leaves.size();
+  p.n_vnodes = (int64_t)M->vnode_x.size() / dim;
+  p.n_pnodes = (int64_t)M->pnode_x.size() / dim;
+  p.cell_vnodes = M->cell_vnodes.data();
+  p.cell_pnodes = M->cell_pnodes.data();
+  p.cell_level = M->cell_level.data();
+  p.cell_x0 = M->cell_x0.data();
+  p.cell_h = M->cell_h.data();
+  p.vnode_x = M->vnode_x.data();
+  p.pnode_x = M->pnode_x.data();
+  p.n_vhang = (int64_t)M->vh_node.size();
+  p.vhang_node = M->vh_node.data();
+  p.vhang_off = M->vh_off.data();
+  p.vhang_master = M->vh_master.data();
+  p.vhang_w = M->vh_w.data();
+  p.n_phang = (int64_t)M->ph_node.size();
+  p.phang_node = M->ph_node.data();
+  p.phang_off = M->ph_off.data();
+  p.phang_master = M->ph_master.data();
+  p.phang_w = M->ph_w.data();
+  p.impl_ = M.get();
+  *out = &M.release()->pub;
+  return GLS_OK;
+}
+int gls_octree_mesh_destroy(gls_refined_mesh *m) {
+  if (m) delete static_cast<MeshImpl *>(m->impl_);
+  return GLS_OK;
+}
+
+// SolutionTransfer between two meshes of the same hyper_cube (refinement and coarsening): every
+// node of the new mesh takes the old FE field's value at its position (the old cell containing
+// it, its Qk interpolant). Lagrange nodes of a coarsened parent coincide with its children's
+// nodes, so coarsening is exact injection, as deal.II's restriction of FE_Q is. Host vectors in
+// the [velocity node-major | pressure] layout.
+int gls_octree_transfer(const gls_refined_mesh *om, const gls_refined_mesh *nm, const double *ov, double *nv) {
+  if (!om || !nm || !ov || !nv || om->dim != nm->dim || om->k != nm->k || om->kp != nm->kp)
+    return gls_io_set_error(GLS_EINVAL, "gls_octree_transfer: incompatible meshes");
+  const int dim = om->dim;
+  const MeshImpl *O = static_cast<const MeshImpl *>(om->impl_);
+  // locate old cells through a grid of the old finest cells
+  const int64_t N = (int64_t)O->n << O->L;
+  int64_t tot = 1;
+  for (int d = 0; d < dim; ++d) tot *= N;
+  if (tot > ((int64_t)1 << 28)) return gls_io_set_error(GLS_EINVAL, "gls_octree_transfer: grid too large");
+  std::vector<int32_t> owner((size_t)tot, -1);
+  const double hf = (O->hi - O->lo) / (double)N;
+  for (int64_t c = 0; c < om->n_cells; ++c) {
+    int64_t o[3] = {0, 0, 0}, s = (int64_t)std::llround(om->cell_h[c * dim] / hf);
+    for (int d = 0; d < dim; ++d) o[d] = (int64_t)std::llround((om->cell_x0[c * dim + d] - O->lo) / hf);
+    int64_t nb = 1;
+    for (int d = 0; d < dim; ++d) nb *= s;
+    for (int64_t b = 0; b < nb; ++b) {
+      int64_t r = b, id = 0, st = 1;
+      for (int d = 0; d < dim; ++d) {
+        id += (o[d] + r % s) * st;
+        r /= s;
+        st *= N;
+      }
+      owner[(size_t)id] = (int32_t)c;
+    }
+  }
+  auto eval = [&](const double *x, int comp) {
+    const bool vel = comp < dim;
+    const int kk = vel ? om->k : om->kp, K1 = kk + 1;
+    int64_t q[3] = {0, 0, 0};
+    for (int d = 0; d < dim; ++d) {
+      int64_t v = (int64_t)std::floor((x[d] - O->lo) / hf);
+      q[d] = std::min(std::max(v, (int64_t)0), N - 1);
+    }
+    int64_t id = 0, st = 1;
+    for (int d = 0; d < dim; ++d) {
+      id += q[d] * st;
+      st *= N;
+    }
+    const int32_t c = owner[(size_t)id];
+    double xi[3] = {0, 0, 0};
+    for (int d = 0; d < dim; ++d) xi[d] = (x[d] - om->cell_x0[c * dim + d]) / om->cell_h[c * dim + d];
+    const int npc = dim == 3 ? K1 * K1 * K1 : K1 * K1;
+    const int32_t *cn = vel ? om->cell_vnodes + (int64_t)c * npc : om->cell_pnodes + (int64_t)c * npc;
+    double s = 0;
+    for (int a = 0; a < npc; ++a) {
+      double w = 1.0;
+      int r = a;
+      for (int d = 0; d < dim; ++d) {
+        w *= lagrange(kk, r % K1, xi[d]);
+        r /= K1;
+      }
+      s += w * (vel ? ov[(int64_t)cn[a] * dim + comp] : ov[(int64_t)dim * om->n_vnodes + cn[a]]);
+    }
+    return s;
+  };
+  for (int64_t v = 0; v < nm->n_vnodes; ++v)
+    for (int c = 0; c < dim; ++c) nv[v * dim + c] = eval(nm->vnode_x + v * dim, c);
+  for (int64_t p = 0; p < nm->n_pnodes; ++p) nv[(int64_t)dim * nm->n_vnodes + p] = eval(nm->pnode_x + p * dim, dim);
+  return GLS_OK;
+}
+
+}  // extern "C"

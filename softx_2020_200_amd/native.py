@@ -35,7 +35,8 @@ EXPORTS = [
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
-    "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy",
+    "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy", "gls_octree_create", "gls_octree_destroy", "gls_octree_info",
+    "gls_octree_cells", "gls_octree_adapt", "gls_octree_mesh", "gls_octree_mesh_destroy", "gls_octree_transfer",
     "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
     "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
@@ -251,6 +252,14 @@ def refined_cube(dim, n, k, kp=None, refine=None, lo=-1.0, hi=1.0):
     check(L.gls_mesh_refined_create(dim, n, k, kp, lo, hi, flags.ctypes.data_as(C.POINTER(C.c_int32)),
                                     C.byref(pm)), "gls_mesh_refined_create")
     try:
+        return _refined_mesh_dict(pm, dim, k, kp)
+    finally:
+        L.gls_mesh_refined_destroy(pm)
+
+
+def _refined_mesh_dict(pm, dim, k, kp):
+    """Copy a gls_refined_mesh (cells, node coordinates, node-level hanging lines) into numpy arrays."""
+    if True:
         m = pm.contents
 
         def take(ptr, count, dt, shape=None):
@@ -273,8 +282,85 @@ def refined_cube(dim, n, k, kp=None, refine=None, lo=-1.0, hi=1.0):
                                  take(getattr(m, tag + "hang_master"), nm, np.int64),
                                  take(getattr(m, tag + "hang_w"), nm, np.float64))
         return out
-    finally:
-        L.gls_mesh_refined_destroy(pm)
+
+
+class Octree:
+    """Multi-level adaptive hyper_cube (gls_octree_*): p4est-style refine / coarsen with vertex 2:1
+    balance; mesh(k, kp) gives the refined_cube-style dict with closed hanging-node lines."""
+
+    def __init__(self, dim, n, lo=-1.0, hi=1.0):
+        self.L = load()
+        self.L.gls_octree_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        self.L.gls_octree_destroy.argtypes = [C.c_void_p]
+        self.L.gls_octree_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        self.L.gls_octree_cells.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_double]
+        self.L.gls_octree_adapt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        self.L.gls_octree_mesh.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double,
+                                           C.POINTER(C.POINTER(RefinedMesh))]
+        self.L.gls_octree_mesh_destroy.argtypes = [C.POINTER(RefinedMesh)]
+        self.L.gls_octree_transfer.argtypes = [C.POINTER(RefinedMesh), C.POINTER(RefinedMesh), C.c_void_p, C.c_void_p]
+        self.dim, self.n, self.lo, self.hi = dim, n, lo, hi
+        self.h = C.c_void_p()
+        check(self.L.gls_octree_create(dim, n, C.byref(self.h)), "gls_octree_create")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.gls_octree_destroy(self.h)
+
+    @property
+    def n_cells(self):
+        nc, ml = C.c_int64(), C.c_int()
+        check(self.L.gls_octree_info(self.h, C.byref(nc), C.byref(ml)), "gls_octree_info")
+        return nc.value
+
+    @property
+    def max_level(self):
+        nc, ml = C.c_int64(), C.c_int()
+        check(self.L.gls_octree_info(self.h, C.byref(nc), C.byref(ml)), "gls_octree_info")
+        return ml.value
+
+    def cells(self):
+        nc = self.n_cells
+        lev = np.zeros(nc, dtype=np.int32)
+        x0 = np.zeros((nc, self.dim))
+        h = np.zeros((nc, self.dim))
+        check(self.L.gls_octree_cells(self.h, lev.ctypes.data, x0.ctypes.data, h.ctypes.data, self.lo, self.hi),
+              "gls_octree_cells")
+        return lev, x0, h
+
+    def adapt(self, refine=None, coarsen=None, max_level=30, min_level=0):
+        nc = self.n_cells
+        r = np.zeros(nc, np.int32) if refine is None else np.ascontiguousarray(refine, dtype=np.int32)
+        c = np.zeros(nc, np.int32) if coarsen is None else np.ascontiguousarray(coarsen, dtype=np.int32)
+        check(self.L.gls_octree_adapt(self.h, r.ctypes.data, c.ctypes.data, int(max_level), int(min_level)),
+              "gls_octree_adapt")
+
+    def mesh_handle(self, k, kp=None):
+        """Owned gls_refined_mesh pointer (free with free_mesh_handle)."""
+        kp = k if kp is None else kp
+        pm = C.POINTER(RefinedMesh)()
+        check(self.L.gls_octree_mesh(self.h, k, kp, self.lo, self.hi, C.byref(pm)), "gls_octree_mesh")
+        return pm
+
+    def free_mesh_handle(self, pm):
+        self.L.gls_octree_mesh_destroy(pm)
+
+    def mesh(self, k, kp=None):
+        kp = k if kp is None else kp
+        pm = self.mesh_handle(k, kp)
+        try:
+            return _refined_mesh_dict(pm, self.dim, k, kp)
+        finally:
+            self.free_mesh_handle(pm)
+
+
+def octree_transfer(old_handle, new_handle, vec, n_new):
+    """SolutionTransfer between two octree meshes (gls_octree_transfer; host vectors)."""
+    L = load()
+    src = np.ascontiguousarray(vec, dtype=np.float64)
+    out = np.zeros(n_new)
+    check(L.gls_octree_transfer(old_handle, new_handle, src.ctypes.data, out.ctypes.data), "gls_octree_transfer")
+    return out
 
 
 def refine_fixed_number(criteria, top_fraction):
