@@ -5,7 +5,7 @@ Drop-in for Lethe's GLSNavierStokesSolver assembly + linear solve path
 hand-written HIP kernels for gfx950 (libgls_native.so, C-ABI in include/gls_native.h);
 this package is the thin Python front-end over that ABI.
 """
-from .native import (GLSContext, GLSError, SCHEMES, bdf_coefficients, hanging_dof_lines, hyper_cube,  # noqa: F401
+from .native import (GLSContext, GLSError, Octree, SCHEMES, bdf_coefficients, hanging_dof_lines, hyper_cube,  # noqa: F401
                      load, newton_selftest, skip_newton_selftest, refine_fixed_number, refine_pd, refined_cube, refined_interpolate,
                      sdirk_coefficients)
 from .problem import CavityProblem, build_context  # noqa: F401

@@ -45,6 +45,39 @@ def refined_problem(dim, n, k, kp, cells, scheme="bdf2", nu=0.05, force=True):
     return p, mesh
 
 
+OCTREE_CASES = [  # dim, n, k, kp, adaptation steps: multi-level meshes (chained constraints)
+    (2, 2, 2, 1, 3),
+    (2, 2, 1, 1, 3),
+    (3, 2, 2, 2, 2),
+    (3, 2, 1, 1, 2),
+]
+
+
+def octree_mesh(dim, n, k, kp, steps, seed=3):
+    """gls_octree adaptation around a point: refine the cells near (0.55, ...), coarsen half of the
+    others at random, `steps` times (multi-level, 2:1 balanced, with coarsening)."""
+    t = sx.Octree(dim, n)
+    rng = np.random.default_rng(seed)
+    for _ in range(steps):
+        lev, x0, h = t.cells()
+        near = np.linalg.norm(x0 + 0.5 * h - 0.55, axis=1) < 0.6
+        t.adapt(refine=near.astype(np.int32), coarsen=(~near & (rng.uniform(size=len(lev)) < 0.5)).astype(np.int32),
+                max_level=4)
+    return t.mesh(k, kp)
+
+
+def octree_problem(dim, n, k, kp, steps, scheme="bdf2", nu=0.05, force=True):
+    mesh = octree_mesh(dim, n, k, kp, steps)
+    p = StructuredProblem.from_refined(mesh, viscosity=nu, scheme=scheme, time_steps=(0.01, 0.013, 0.011, 0.009))
+    lines = sx.hanging_dof_lines(mesh)
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    p.set_dirichlet([("noslip", 0, None)])
+    if force:
+        p.set_force(lambda X: np.stack([np.sin(X[:, 0] + 2 * X[:, 1]) for _ in range(dim)], 1))
+    return p, mesh
+
+
 def poly_values(X, c):
     v = np.zeros(X.shape[0])
     for idx in np.ndindex(*c.shape):
@@ -80,7 +113,18 @@ def test_hanging_weights_reproduce_qk(case):
 def test_oracle_condensation_matches_numpy(case):
     """Oracle condensed J.v / residual / diagonal == C^T K C, C^T F from its own element systems,
     condensed here in numpy (independent of the oracle's dof_targets)."""
-    p, mesh = refined_problem(*case)
+    _check_condensation(*refined_problem(*case))
+
+
+@pytest.mark.parametrize("case", OCTREE_CASES[:2] + OCTREE_CASES[3:], ids=lambda c: "d%d_n%d_Q%dQ%d_s%d" % c)
+def test_octree_oracle_condensation_matches_numpy(case):
+    """The same on multi-level (gls_octree) meshes: constraint chains closed by the builder."""
+    p, mesh = octree_problem(*case)
+    assert mesh["cell_level"].max() >= 2
+    _check_condensation(p, mesh)
+
+
+def _check_condensation(p, mesh):
     rng = np.random.default_rng(SEED)
     u, u1, u2, v = (rng.uniform(-1, 1, p.n_dofs) for _ in range(4))
     import ctypes as C
@@ -143,6 +187,27 @@ def test_hanging_gpu_vs_oracle(case):
     jv = ctx.jacobian_apply(cuda(v)).cpu().numpy()
     assert relerr(jv, orc.jacobian_apply(u, v, u1, u2)) < 1e-12
     # nonzero_constraints.distribute on the device == the oracle's
+    x = rng.uniform(-1, 1, p.n_dofs)
+    X = cuda(x)
+    ctx.apply_dirichlet(X)
+    assert np.abs(X.cpu().numpy() - p.apply_nonzero_constraints(x.copy())).max() < 1e-14
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", OCTREE_CASES, ids=lambda c: "d%d_n%d_Q%dQ%d_s%d" % c)
+def test_octree_gpu_vs_oracle(case):
+    """Multi-level adapted meshes (refinement + coarsening, 2:1 balanced): HIP residual, J.v and
+    nonzero-constraint distribution == the oracle at 1e-12."""
+    from tests.gpu_util import context_for, cuda, relerr
+    p, mesh = octree_problem(*case)
+    rng = np.random.default_rng(SEED)
+    u, u1, u2, v = (rng.uniform(-1, 1, p.n_dofs) for _ in range(4))
+    p.apply_nonzero_constraints(u)
+    orc = Oracle(p)
+    ctx = context_for(p)
+    ctx.set_state(cuda(u), cuda(u1), cuda(u2))
+    assert relerr(ctx.residual().cpu().numpy(), orc.residual(u, u1, u2)) < 1e-12
+    assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1, u2)) < 1e-12
     x = rng.uniform(-1, 1, p.n_dofs)
     X = cuda(x)
     ctx.apply_dirichlet(X)
