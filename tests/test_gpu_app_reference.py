@@ -83,3 +83,28 @@ def test_reference_application_case(tmp_path, name, dim, periodic, pressure):
             assert a[2] == b[2], (name, a, b)
         if pressure:
             assert a[3:] == b[3:], (name, a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["sdirk2", "sdirk3"])
+def test_reference_tgv_sdirk_cases(tmp_path, method):
+    """The reference's taylor-green-vortex_gls_{sdirk2,sdirk3} application tests as shipped (Q2-Q1,
+    periodic, L2-projection IC, one step of 0.1, Newton tol 1e-6, GMRES rel 1e-4 -- an inexact
+    Newton): enstrophy and kinetic energy before and after the step match the .output to all printed
+    digits. The L2 error depends on where the inexact linear solves stop: with exact solves the
+    oracle gives 1.38239e-4 (SDIRK3), with this build's ILU(0)-GMRES at the reference's tolerances
+    1.38207e-4; the reference's ILU(1)-GMRES value 1.38223e-4 lies between the two, so the error is
+    checked at the reference's inexact-Newton scale (3e-4 relative; SDIRK2: printed digits)."""
+    name = "taylor-green-vortex_gls_" + method
+    prm = open(os.path.join(CASES, name + ".prm")).read()
+    prm = re.sub(r"set output frequency\s*=\s*1 ", "set output frequency = 1000000 ", prm)
+    (tmp_path / "case.prm").write_text(prm)
+    app = os.path.join(ROOT, "apps", "gls_navier_stokes_2d")
+    out = subprocess.run([app, "case.prm"], cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    ref = open(os.path.join(CASES, name + ".output")).read()
+    pick = lambda t, key: [l.split(":")[1].strip() for l in t.splitlines() if l.startswith(key)]
+    for key in ("Enstrophy", "Kinetic energy"):
+        assert pick(out.stdout, key) == pick(ref, key), (key, pick(out.stdout, key), pick(ref, key))
+    e, r = float(pick(out.stdout, "L2 error velocity")[0]), float(pick(ref, "L2 error velocity")[0])
+    assert abs(e - r) <= (3e-4 if method == "sdirk3" else 1e-5) * r, (e, r)
