@@ -373,6 +373,14 @@ int gls_octree_transfer(const gls_refined_mesh *old_mesh, const gls_refined_mesh
  * velocity components (variable 0) or the pressure (variable 1). Conforming meshes (no hanging
  * nodes). sol, eta: DEVICE pointers (eta: n_cells doubles; deal.II stores them as float). */
 int gls_kelly_estimate(gls_ctx *ctx, const double *sol, int variable, double *eta);
+/* The same on meshes with hanging faces (gls_octree_mesh): the face pieces from gls_octree_faces
+ * (the fine side of a non-conforming face is one piece; deal.II integrates over the subfaces), the
+ * integrals on the device, each piece counted for both of its cells. sol, eta: DEVICE pointers. */
+int gls_kelly_estimate_faces(gls_ctx *ctx, const double *sol, int variable, int64_t n_faces, const int32_t *fa,
+                             const int32_t *fb, const int32_t *fdir, const double *rect_a, const double *rect_b,
+                             double *eta);
+int gls_octree_faces(const gls_refined_mesh *mesh, int64_t *n_faces, int32_t *fa, int32_t *fb, int32_t *fdir,
+                     double *rect_a, double *rect_b);
 /* GridRefinement::refine_and_coarsen_fixed_number, refinement part (navier_stokes_base.cc:654-661;
  * serial deal.II rule): flags[i] = 1 for the int(top_fraction * n_cells) largest criteria (every
  * cell >= the threshold value). Returns the number of flagged cells. HOST arrays. */

@@ -2038,7 +2038,11 @@ gls::KellyTables kelly_tables(int m, int nq) {
     lagrange_1d(m, xn, a, 1.0, v, dd, s2);
     T.De[1][a] = dd;
   }
-  for (int q = 0; q < nq; ++q) T.w[q] = wq[q];
+  for (int q = 0; q < nq; ++q) {
+    T.w[q] = wq[q];
+    T.xq[q] = xq[q];
+  }
+  for (int a = 0; a <= m; ++a) T.xn[a] = xn[a];
   return T;
 }
 }  // namespace
@@ -2056,6 +2060,51 @@ int gls_kelly_estimate(gls_ctx *c, const double *sol, int variable, double *eta)
   const gls::KellyTables T = kelly_tables(m, c->nq1d + 1);  // QGauss<dim-1>(n_q + 1)
   HIP_TRY(gls::launch_kelly(c->dim, m, nodes, c->face_nbr.p, c->geo.p, sol, c->n_cells, pres ? 1 : c->dim,
                             pres ? (int64_t)c->dim * c->n_vnodes : 0, pres ? 1 : c->dim, T, eta, c->stream));
+  return GLS_OK;
+}
+
+// Kelly indicator on meshes with hanging faces (gls_octree_faces lists the face pieces): the face
+// integrals on the device, then eta_K = sqrt(diam(K)/24 * sum of K's pieces) in a fixed order
+int gls_kelly_estimate_faces(gls_ctx *c, const double *sol, int variable, int64_t n_faces, const int32_t *fa,
+                             const int32_t *fb, const int32_t *fdir, const double *rect_a, const double *rect_b,
+                             double *eta) {
+  GLS_TRY(check_ctx(c));
+  if (!sol || !eta || (variable != 0 && variable != 1) || n_faces < 0 || (n_faces > 0 && (!fa || !fb || !fdir || !rect_a || !rect_b)))
+    return set_err(GLS_EINVAL, "gls_kelly_estimate_faces: bad arguments");
+  if (c->map_degree > 0) return set_err(GLS_EINVAL, "gls_kelly_estimate_faces: axis-aligned box cells only");
+  for (int64_t e = 0; e < n_faces; ++e)
+    if (fa[e] < 0 || fa[e] >= c->n_cells || fb[e] < 0 || fb[e] >= c->n_cells || fdir[e] < 0 || fdir[e] >= c->dim)
+      return set_err(GLS_EINVAL, "gls_kelly_estimate_faces: face %lld out of range", (long long)e);
+  const bool pres = variable == 1;
+  const int m = pres ? c->kp : c->k;
+  const int32_t *nodes = pres && c->cell_pnodes.p ? c->cell_pnodes.p : c->cell_vnodes.p;
+  const gls::KellyTables T = kelly_tables(m, c->nq1d + 1);  // QGauss<dim-1>(n_q + 1) on every piece
+  DevBuf<int32_t> dfa, dfb, dfd;
+  DevBuf<double> dra, drb, dfi;
+  GLS_TRY(dfa.upload(fa, (size_t)n_faces));
+  GLS_TRY(dfb.upload(fb, (size_t)n_faces));
+  GLS_TRY(dfd.upload(fdir, (size_t)n_faces));
+  GLS_TRY(dra.upload(rect_a, (size_t)n_faces * 4));
+  GLS_TRY(drb.upload(rect_b, (size_t)n_faces * 4));
+  GLS_TRY(dfi.alloc((size_t)std::max<int64_t>(n_faces, 1)));
+  HIP_TRY(gls::launch_kelly_faces(c->dim, m, nodes, c->geo.p, sol, n_faces, dfa.p, dfb.p, dfd.p, dra.p, drb.p,
+                                  pres ? 1 : c->dim, pres ? (int64_t)c->dim * c->n_vnodes : 0, pres ? 1 : c->dim, T,
+                                  dfi.p, c->stream));
+  std::vector<double> fi((size_t)n_faces), geo((size_t)c->n_cells * 4), acc((size_t)c->n_cells, 0.0);
+  HIP_TRY(hipMemcpyAsync(fi.data(), dfi.p, sizeof(double) * fi.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(geo.data(), c->geo.p, sizeof(double) * geo.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int64_t e = 0; e < n_faces; ++e) {  // each piece counts for both of its cells
+    acc[(size_t)fa[e]] += fi[(size_t)e];
+    acc[(size_t)fb[e]] += fi[(size_t)e];
+  }
+  for (int64_t k = 0; k < c->n_cells; ++k) {
+    double d2 = 0.0;
+    for (int d = 0; d < c->dim; ++d) d2 += geo[(size_t)k * 4 + d] * geo[(size_t)k * 4 + d];
+    acc[(size_t)k] = std::sqrt(std::sqrt(d2) / 24.0 * acc[(size_t)k]);
+  }
+  HIP_TRY(hipMemcpyAsync(eta, acc.data(), sizeof(double) * acc.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return GLS_OK;
 }
 

@@ -72,7 +72,97 @@ __global__ void __launch_bounds__(256) k_kelly(const int32_t *__restrict__ cell_
   eta[cell] = sqrt(acc);
 }
 
+// Lagrange basis a of degree M on the support points xn, and its derivative, at x
+template <int M>
+__device__ __forceinline__ void lagr(const double *xn, int a, double x, double &v, double &dv) {
+  v = 1.0;
+  dv = 0.0;
+  for (int b = 0; b <= M; ++b) {
+    if (b == a) continue;
+    const double inv = 1.0 / (xn[a] - xn[b]);
+    dv = dv * (x - xn[b]) * inv + v * inv;
+    v *= (x - xn[b]) * inv;
+  }
+}
+
+// one thread per face piece (non-conforming meshes): the jump of the normal derivative between
+// cell a (face xi_d = 1) and cell b (face xi_d = 0) integrated over the piece
+template <int DIM, int M>
+__global__ void __launch_bounds__(256) k_kelly_faces(const int32_t *__restrict__ cell_nodes, const double *__restrict__ geo,
+                                                     const double *__restrict__ sol, int64_t n_faces,
+                                                     const int32_t *__restrict__ fa, const int32_t *__restrict__ fb,
+                                                     const int32_t *__restrict__ fdir, const double *__restrict__ ra,
+                                                     const double *__restrict__ rb, int ncomp, int64_t base, int stride,
+                                                     KellyTables T, double *__restrict__ fint) {
+  constexpr int M1 = M + 1;
+  constexpr int NN = DIM == 3 ? M1 * M1 * M1 : M1 * M1;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_faces) return;
+  const int d = fdir[e];
+  int t[2] = {-1, -1}, nt = 0;
+  for (int k = 0; k < DIM; ++k)
+    if (k != d) t[nt++] = k;
+  const int cells[2] = {fa[e], fb[e]};
+  const double *rect[2] = {ra + e * 4, rb + e * 4};
+  const double ha[3] = {geo[cells[0] * 4 + 0], geo[cells[0] * 4 + 1], DIM == 3 ? geo[cells[0] * 4 + 2] : 1.0};
+  double area = 1.0;
+  for (int j = 0; j < DIM - 1; ++j) area *= (rect[0][2 * j + 1] - rect[0][2 * j]) * ha[t[j]];
+  const int nq1 = DIM == 3 ? T.nq : 1;
+  double integral = 0.0;
+  for (int qa = 0; qa < T.nq; ++qa)
+    for (int qb = 0; qb < nq1; ++qb) {
+      const double w = T.w[qa] * (DIM == 3 ? T.w[qb] : 1.0) * area;
+      double g[2][3] = {{0, 0, 0}, {0, 0, 0}};
+      for (int side = 0; side < 2; ++side) {
+        const int c = cells[side];
+        const double hd = geo[c * 4 + d];
+        double xi[3];
+        xi[d] = side == 0 ? 1.0 : 0.0;
+        xi[t[0]] = rect[side][0] + (rect[side][1] - rect[side][0]) * T.xq[qa];
+        if (DIM == 3) xi[t[1]] = rect[side][2] + (rect[side][3] - rect[side][2]) * T.xq[qb];
+        for (int a = 0; a < NN; ++a) {
+          const int ai[3] = {a % M1, (a / M1) % M1, DIM == 3 ? a / (M1 * M1) : 0};
+          double v, dv, phi = 1.0;
+          lagr<M>(T.xn, ai[d], xi[d], v, dv);
+          phi = dv / hd;
+          lagr<M>(T.xn, ai[t[0]], xi[t[0]], v, dv);
+          phi *= v;
+          if (DIM == 3) {
+            lagr<M>(T.xn, ai[t[1]], xi[t[1]], v, dv);
+            phi *= v;
+          }
+          const int64_t node = cell_nodes[(int64_t)c * NN + a];
+          for (int cc = 0; cc < ncomp; ++cc) g[side][cc] += phi * sol[base + node * stride + cc];
+        }
+      }
+      double j2 = 0.0;
+      for (int cc = 0; cc < ncomp; ++cc) j2 += (g[0][cc] - g[1][cc]) * (g[0][cc] - g[1][cc]);
+      integral += w * j2;
+    }
+  fint[e] = integral;
+}
+
 }  // namespace
+
+hipError_t launch_kelly_faces(int dim, int m, const int32_t *cell_nodes, const double *geo, const double *sol,
+                              int64_t n_faces, const int32_t *fa, const int32_t *fb, const int32_t *fdir,
+                              const double *rect_a, const double *rect_b, int ncomp, int64_t base, int stride,
+                              const KellyTables &T, double *fint, hipStream_t s) {
+  if (n_faces <= 0) return hipSuccess;
+  const dim3 g((unsigned)((n_faces + 255) / 256)), b(256);
+#define GLS_KELLYF_CASE(D, MM)                                                                                        \
+  if (dim == D && m == MM) {                                                                                          \
+    hipLaunchKernelGGL((k_kelly_faces<D, MM>), g, b, 0, s, cell_nodes, geo, sol, n_faces, fa, fb, fdir, rect_a, rect_b, \
+                       ncomp, base, stride, T, fint);                                                                \
+    return hipGetLastError();                                                                                         \
+  }
+  GLS_KELLYF_CASE(2, 1)
+  GLS_KELLYF_CASE(2, 2)
+  GLS_KELLYF_CASE(3, 1)
+  GLS_KELLYF_CASE(3, 2)
+#undef GLS_KELLYF_CASE
+  return hipErrorNotSupported;
+}
 
 hipError_t launch_kelly(int dim, int m, const int32_t *cell_nodes, const int32_t *nbr, const double *geo,
                         const double *sol, int n_cells, int ncomp, int64_t base, int stride, const KellyTables &T,

@@ -81,7 +81,16 @@ struct KellyTables {
   double w[kMaxQ1D];                  // Gauss weights on [0, 1]
   double V[kMaxQ1D][kMaxNodes1D];     // basis values at the face points
   double De[2][kMaxNodes1D];          // basis derivatives at xi = 0 and xi = 1
+  double xq[kMaxQ1D];                 // Gauss points on [0, 1]
+  double xn[kMaxNodes1D];             // support points (Gauss-Lobatto) of the basis
 };
+// face-list form for meshes with hanging faces: fint[e] = int over the piece of face e of
+// sum_c [d_n u_c]^2, the piece being rect_a / rect_b in the reference coordinates of cell fa[e]
+// (its face xi_d = 1) and fb[e] (its face xi_d = 0), d = fdir[e]; QGauss(T.nq)^(dim-1) on the piece
+hipError_t launch_kelly_faces(int dim, int m, const int32_t *cell_nodes, const double *geo, const double *sol,
+                              int64_t n_faces, const int32_t *fa, const int32_t *fb, const int32_t *fdir,
+                              const double *rect_a, const double *rect_b, int ncomp, int64_t base, int stride,
+                              const KellyTables &T, double *fint, hipStream_t s);
 // eta[cell] = sqrt(sum over faces with nbr >= 0 of diam/24 * int_F sum_c [d_n u_c]^2); component c of
 // node n at sol[base + n * stride + c], c < ncomp; cell_nodes [n_cells][(m+1)^dim]; nbr [n_cells][2 dim]
 hipError_t launch_kelly(int dim, int m, const int32_t *cell_nodes, const int32_t *nbr, const double *geo,

@@ -12,6 +12,7 @@
 // gls_octree_mesh builds the FE_Q(k) / FE_Q(kp) node spaces on the finest node lattice with
 // hanging lines whose masters are all unconstrained (chains resolved).
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -540,6 +541,73 @@ int gls_octree_transfer(const gls_refined_mesh *om, const gls_refined_mesh *nm, 
   for (int64_t v = 0; v < nm->n_vnodes; ++v)
     for (int c = 0; c < dim; ++c) nv[v * dim + c] = eval(nm->vnode_x + v * dim, c);
   for (int64_t p = 0; p < nm->n_pnodes; ++p) nv[(int64_t)dim * nm->n_vnodes + p] = eval(nm->pnode_x + p * dim, dim);
+  return GLS_OK;
+}
+
+// Interior faces of an octree mesh for KellyErrorEstimator, one entry per pair of cells sharing a
+// piece of face: cell a's face at xi_d = 1 against cell b's face at xi_d = 0. On a non-conforming
+// face the piece is the fine cell's whole face, a subface of the coarse one (deal.II integrates the
+// jump over the subfaces of a refined neighbour, internal::integrate_over_irregular_face). rect_a /
+// rect_b: [n][2 tangential dims][lo, hi] of the piece in each cell's reference coordinates.
+// Call with null arrays to get the count.
+int gls_octree_faces(const gls_refined_mesh *m, int64_t *n_faces, int32_t *fa, int32_t *fb, int32_t *fdir,
+                     double *rect_a, double *rect_b) {
+  if (!m || !n_faces) return gls_io_set_error(GLS_EINVAL, "gls_octree_faces: null argument");
+  const MeshImpl *M = static_cast<const MeshImpl *>(m->impl_);
+  const int dim = m->dim;
+  const double hf = (M->hi - M->lo) / ((double)M->n * (double)((int64_t)1 << M->L));
+  // integer finest-lattice boxes
+  std::vector<std::array<int64_t, 6>> box((size_t)m->n_cells);
+  for (int64_t c = 0; c < m->n_cells; ++c)
+    for (int d = 0; d < 3; ++d) {
+      const int64_t lo = d < dim ? (int64_t)std::llround((m->cell_x0[c * dim + d] - M->lo) / hf) : 0;
+      const int64_t s = d < dim ? (int64_t)std::llround(m->cell_h[c * dim + d] / hf) : 1;
+      box[(size_t)c][d] = lo;
+      box[(size_t)c][3 + d] = lo + s;
+    }
+  // cells by (normal dir, low-face coordinate)
+  std::map<std::pair<int, int64_t>, std::vector<int32_t>> low;
+  for (int64_t c = 0; c < m->n_cells; ++c)
+    for (int d = 0; d < dim; ++d) low[{d, box[(size_t)c][d]}].push_back((int32_t)c);
+  int64_t cnt = 0;
+  for (int64_t a = 0; a < m->n_cells; ++a)
+    for (int d = 0; d < dim; ++d) {
+      auto it = low.find({d, box[(size_t)a][3 + d]});
+      if (it == low.end()) continue;
+      for (int32_t b : it->second) {
+        int64_t olo[3], ohi[3];
+        bool overlap = true;
+        for (int e = 0; e < dim; ++e) {
+          if (e == d) continue;
+          olo[e] = std::max(box[(size_t)a][e], box[(size_t)b][e]);
+          ohi[e] = std::min(box[(size_t)a][3 + e], box[(size_t)b][3 + e]);
+          overlap = overlap && ohi[e] > olo[e];
+        }
+        if (!overlap) continue;
+        if (fa) {
+          fa[cnt] = (int32_t)a;
+          fb[cnt] = b;
+          fdir[cnt] = d;
+          int t = 0;
+          for (int e = 0; e < dim; ++e) {
+            if (e == d) continue;
+            const double sa = (double)(box[(size_t)a][3 + e] - box[(size_t)a][e]);
+            const double sb = (double)(box[(size_t)b][3 + e] - box[(size_t)b][e]);
+            rect_a[cnt * 4 + 2 * t] = (double)(olo[e] - box[(size_t)a][e]) / sa;
+            rect_a[cnt * 4 + 2 * t + 1] = (double)(ohi[e] - box[(size_t)a][e]) / sa;
+            rect_b[cnt * 4 + 2 * t] = (double)(olo[e] - box[(size_t)b][e]) / sb;
+            rect_b[cnt * 4 + 2 * t + 1] = (double)(ohi[e] - box[(size_t)b][e]) / sb;
+            ++t;
+          }
+          for (; t < 2; ++t) {
+            rect_a[cnt * 4 + 2 * t] = rect_b[cnt * 4 + 2 * t] = 0.0;
+            rect_a[cnt * 4 + 2 * t + 1] = rect_b[cnt * 4 + 2 * t + 1] = 1.0;
+          }
+        }
+        ++cnt;
+      }
+    }
+  *n_faces = cnt;
   return GLS_OK;
 }
 

@@ -36,7 +36,7 @@ EXPORTS = [
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy", "gls_octree_create", "gls_octree_destroy", "gls_octree_info",
-    "gls_octree_cells", "gls_octree_adapt", "gls_octree_mesh", "gls_octree_mesh_destroy", "gls_octree_transfer",
+    "gls_octree_cells", "gls_octree_adapt", "gls_octree_mesh", "gls_octree_mesh_destroy", "gls_octree_transfer", "gls_octree_faces", "gls_kelly_estimate_faces",
     "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
     "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
@@ -345,6 +345,21 @@ class Octree:
     def free_mesh_handle(self, pm):
         self.L.gls_octree_mesh_destroy(pm)
 
+    def faces(self, k=1, kp=None):
+        """Interior face pieces for Kelly (gls_octree_faces): (fa, fb, fdir, rect_a, rect_b)."""
+        pm = self.mesh_handle(k, kp)
+        try:
+            self.L.gls_octree_faces.argtypes = [C.POINTER(RefinedMesh), C.POINTER(C.c_int64)] + [C.c_void_p] * 5
+            n = C.c_int64()
+            check(self.L.gls_octree_faces(pm, C.byref(n), None, None, None, None, None), "gls_octree_faces")
+            fa, fb, fd = (np.zeros(n.value, np.int32) for _ in range(3))
+            ra, rb = np.zeros((n.value, 4)), np.zeros((n.value, 4))
+            check(self.L.gls_octree_faces(pm, C.byref(n), fa.ctypes.data, fb.ctypes.data, fd.ctypes.data, ra.ctypes.data,
+                                          rb.ctypes.data), "gls_octree_faces")
+            return fa, fb, fd, ra, rb
+        finally:
+            self.free_mesh_handle(pm)
+
     def mesh(self, k, kp=None):
         kp = k if kp is None else kp
         pm = self.mesh_handle(k, kp)
@@ -642,6 +657,18 @@ class GLSContext:
         import torch
         out = torch.empty(self.n_cells, dtype=torch.float64, device=sol.device) if out is None else out
         check(self.L.gls_kelly_estimate(self.h, _ptr(sol), int(variable), _ptr(out)), "gls_kelly_estimate")
+        return out
+
+    def kelly_estimate_faces(self, sol, variable, faces, out=None):
+        """Kelly indicator on a mesh with hanging faces (gls_kelly_estimate_faces); faces from
+        Octree.faces()."""
+        import torch
+        fa, fb, fd, ra, rb = faces
+        out = torch.empty(self.n_cells, dtype=torch.float64, device=sol.device) if out is None else out
+        self.L.gls_kelly_estimate_faces.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int64] + [C.c_void_p] * 6
+        check(self.L.gls_kelly_estimate_faces(self.h, _ptr(sol), int(variable), len(fa), fa.ctypes.data, fb.ctypes.data,
+                                              fd.ctypes.data, ra.ctypes.data, rb.ctypes.data, _ptr(out)),
+              "gls_kelly_estimate_faces")
         return out
 
     def mg_transfer(self, level, direction, v, out):

@@ -187,3 +187,62 @@ def test_kelly_adaptive_mms2d_pipeline():
     e0, _ = Oracle(p).l2_error(x.cpu().numpy(), E)
     e1, _ = Oracle(q).l2_error(ys, E)
     assert e1 < e0, (e0, e1)
+
+
+@pytest.mark.parametrize("dim,k,kp", [(2, 2, 1), (3, 1, 1)])
+def test_box_kelly_restatement_matches_uniform_oracle(dim, k, kp):
+    """The face-search restatement for hanging meshes (oracle.kelly_estimate_boxes) equals the
+    round-1 lattice restatement on a conforming mesh (an octree refined uniformly)."""
+    from oracle.oracle import kelly_estimate_boxes
+    p = _uniform(dim, 4, k, kp)
+    m = dict(dim=dim, k=k, kp=kp, cell_vnodes=p.cell_vnodes, cell_pnodes=p.cell_pnodes if kp != k else p.cell_vnodes,
+             cell_x0=p.cell_x0, cell_h=p.cell_h, n_vnodes=p.n_vnodes)
+    sol = np.random.default_rng(SEED).uniform(-1, 1, p.n_dofs)
+    for var in (0, 1):
+        a = kelly_estimate_boxes(m, sol, var)
+        b = kelly_estimate(p, sol, var)
+        assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max()
+
+
+def _octree_kelly_mesh(dim, k, kp):
+    t = sx.Octree(dim, 2)
+    t.adapt(refine=np.ones(t.n_cells, np.int32))
+    for _ in range(2):
+        lev, x0, h = t.cells()
+        f = (np.linalg.norm(x0 + 0.5 * h - 0.4, axis=1) < 0.5).astype(np.int32)
+        t.adapt(refine=f, max_level=4)
+    return t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,k,kp", [(2, 1, 1), (2, 2, 1), (3, 1, 1), (3, 2, 2)])
+def test_kelly_hanging_faces_gpu_vs_oracle(dim, k, kp):
+    """Kelly on a multi-level mesh with hanging faces (gls_kelly_estimate_faces with the
+    gls_octree_faces pieces) == the oracle's face-search restatement at 1e-12; on the uniform mesh
+    the face form equals the conforming kernel."""
+    from oracle.oracle import kelly_estimate_boxes
+    from tests.gpu_util import context_for, cuda, relerr
+    t = _octree_kelly_mesh(dim, k, kp)
+    m = t.mesh(k, kp)
+    assert m["cell_level"].max() >= 3
+    p = StructuredProblem.from_refined(m, viscosity=1.0)
+    lines = sx.hanging_dof_lines(m)
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    rng = np.random.default_rng(SEED)
+    sol = p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs))
+    ctx = context_for(p)
+    faces = t.faces(k, kp)
+    for var in (0, 1):
+        eta = ctx.kelly_estimate_faces(cuda(sol), var, faces).cpu().numpy()
+        ref = kelly_estimate_boxes(m, sol, var)
+        assert relerr(eta, ref) < 1e-12, (var, relerr(eta, ref))
+    u = sx.Octree(dim, 4)
+    mu = u.mesh(k, kp)
+    pu = StructuredProblem.from_refined(mu, viscosity=1.0)
+    solu = rng.uniform(-1, 1, pu.n_dofs)
+    cu = context_for(pu)
+    for var in (0, 1):
+        a = cu.kelly_estimate_faces(cuda(solu), var, u.faces(k, kp)).cpu().numpy()
+        b = cu.kelly_estimate(cuda(solu), var).cpu().numpy()
+        assert relerr(a, b) < 1e-12

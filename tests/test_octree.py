@@ -202,3 +202,27 @@ def test_transfer_exact_for_qk(dim, k, kp):
     assert np.abs(out - field(mn)).max() < 1e-12
     t.free_mesh_handle(old)
     t.free_mesh_handle(new)
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_octree_faces_tile_the_interior(dim):
+    """The face pieces cover every interior face exactly once: their total area equals the sum of
+    the interior face areas of the finest-level decomposition of the cube."""
+    t = adapted(dim, 2, 2)
+    fa, fb, fd, ra, rb = t.faces(1)
+    lev, x0, h = t.cells()
+    area = 0.0
+    for e in range(len(fa)):
+        a = 1.0
+        for j, ax in enumerate([x for x in range(dim) if x != fd[e]]):
+            a *= (ra[e, 2 * j + 1] - ra[e, 2 * j]) * h[fa[e], ax]
+            # both descriptions of the piece have the same physical extent
+            assert abs((ra[e, 2 * j + 1] - ra[e, 2 * j]) * h[fa[e], ax] - (rb[e, 2 * j + 1] - rb[e, 2 * j]) * h[fb[e], ax]) < 1e-14
+        area += a
+    # interior area of [-1, 1]^dim cut by the leaves: sum over cells of their high faces inside the cube
+    ref = 0.0
+    for i in range(len(lev)):
+        for d in range(dim):
+            if x0[i, d] + h[i, d] < 1.0 - 1e-12:
+                ref += np.prod(np.delete(h[i], d))
+    assert abs(area - ref) < 1e-12
