@@ -362,6 +362,14 @@ void gls_octree_destroy(gls_octree *tree);
 int gls_octree_info(const gls_octree *tree, int64_t *n_cells, int *max_level);
 int gls_octree_cells(const gls_octree *tree, int32_t *level, double *x0, double *h, double lo, double hi);
 int gls_octree_adapt(gls_octree *tree, const int32_t *refine, const int32_t *coarsen, int max_level, int min_level);
+/* Triangulation::prepare_coarsening_and_refinement with the reference's mesh smoothing
+ * (smoothing_on_refinement | smoothing_on_coarsening, navier_stokes_base.cc:55-60, called at :682):
+ * do_not_produce_unrefined_islands, eliminate_refined_inner/boundary_islands,
+ * limit_level_difference_at_vertices, eliminate_unrefined_islands, no double refinement at faces,
+ * complete-family coarsening that keeps the 2:1 rule (fix_coarsen_flags), iterated until the flags no
+ * longer change. refine / coarsen: per-leaf flags in the tree's order, updated in place. Returns the
+ * number of iterations. */
+int gls_octree_prepare(const gls_octree *tree, int32_t *refine, int32_t *coarsen);
 int gls_octree_mesh(const gls_octree *tree, int k, int kp, double lo, double hi, gls_refined_mesh **out);
 int gls_octree_mesh_destroy(gls_refined_mesh *mesh);
 int gls_octree_transfer(const gls_refined_mesh *old_mesh, const gls_refined_mesh *new_mesh, const double *old_vec,
@@ -395,6 +403,15 @@ int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_f
  * arrays; threshold may be NULL. Returns the number of flagged cells. */
 int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
                   int64_t max_n_cells, int32_t *flags, double *threshold);
+/* The same with coarsening (fraction coarsening = bottom_fraction): adjust_refine_and_coarsen_
+ * number_fraction<dim> caps both fractions (and coarsens (n - max) / (1 - 2^-dim) cells when the mesh
+ * already has max_n_cells); the bottom threshold leaves int((1 - bottom) * n) cells (or that fraction
+ * of the summed criteria) above it, the lowest float when bottom = 0; mark_cells: refine[i] = 1 where
+ * criteria >= top (GridRefinement::refine), coarsen[i] = 1 where criteria <= bottom and not refine
+ * (GridRefinement::coarsen). thresholds[2] = {top, bottom} (may be NULL). Returns the refined count. */
+int gls_refine_coarsen_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
+                          double bottom_fraction, int64_t max_n_cells, int32_t *refine, int32_t *coarsen,
+                          double *thresholds);
 /* SolutionTransfer::interpolate (navier_stokes_base.cc:689-733) for the first refinement of the
  * uniform hyper_cube(n, lo, hi) that `mesh` was built from: coarse in canonical lattice numbering
  * ([velocity node-major | pressure]), fine in the refined mesh's numbering. HOST arrays. */

@@ -672,6 +672,247 @@ def pd_refine_fixed(criteria, dim, top_fraction, fraction_type="number", max_n_c
     return refine_mark(c, thr)
 
 
+def _pd_threshold(c, fraction_type, target):
+    """compute_threshold of p::d::GridRefinement (deal.II 9.2, not vendored): 25-step bisection."""
+    gmin, gmax = min(c), max(c)
+    lo, hi = gmin, gmax
+    if lo > 0:
+        lo *= 0.99
+    if hi > 0:
+        hi *= 1.01
+    else:
+        hi += 0.01 * (hi - lo)
+    it = 0
+    while lo != hi:
+        test = math.sqrt(lo * hi) if lo > 0 else (lo + hi) / 2
+        above = sum((1.0 if fraction_type == "number" else x) for x in c if x > test)
+        if above > target:
+            lo = test
+        elif above < target:
+            hi = test
+        else:
+            lo = hi = test
+        it += 1
+        if it == 25:
+            lo = hi = test
+    return min(lo, gmax) if fraction_type == "fraction" else lo
+
+
+def pd_refine_coarsen(criteria, dim, top_fraction, bottom_fraction, fraction_type="number", max_n_cells=100000000):
+    """parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number / _fixed_fraction with
+    coarsening, as refine_mesh_kelly calls them (navier_stokes_base.cc:654-667; deal.II 9.2, not
+    vendored): adjust_refine_and_coarsen_number_fraction<dim> (both fractions scaled by alpha when the
+    mesh would exceed max_n_cells; coarsen (n - max) / (1 - 2^-dim) cells when it already does), the
+    top / bottom thresholds by bisection (int(top n) / int((1 - bottom) n) cells, or those fractions
+    of the float-summed indicator, above them; bottom = lowest float when the fraction is 0), then
+    GridRefinement::refine (>= top) and GridRefinement::coarsen (<= bottom, not flagged for refinement).
+    Returns (refine, coarsen, (top, bottom))."""
+    c = [float(x) for x in np.asarray(criteria, dtype=np.float32)]
+    n = len(c)
+    if n == 0:
+        return np.zeros(0, np.int32), np.zeros(0, np.int32), (0.0, 0.0)
+    top, bottom = float(top_fraction), float(bottom_fraction)
+    if fraction_type == "number":
+        inc, dec = 2.0 ** dim - 1.0, 1.0 - 1.0 / 2 ** dim
+        rc, cc = n * top, n * bottom
+        if n >= max_n_cells:
+            top, bottom = 0.0, min((n - max_n_cells) / dec / n, 1.0)
+        elif int(n + rc * inc - cc * dec) > max_n_cells:
+            alpha = (max_n_cells - n) / (rc * inc - cc * dec)
+            top, bottom = alpha * top, alpha * bottom
+        t_top, t_bot = float(int(top * n)), float(int((1.0 - bottom) * n))
+    else:
+        tot = np.float32(0.0)
+        for x in np.asarray(criteria, dtype=np.float32):
+            tot = np.float32(tot + x)
+        t_top, t_bot = top * float(tot), (1.0 - bottom) * float(tot)
+    ref, thr = refine_mark(c, _pd_threshold(c, fraction_type, t_top))
+    bthr = -float(np.finfo(np.float32).max)
+    crs = np.zeros(n, np.int32)
+    if bottom > 0:
+        bthr = _pd_threshold(c, fraction_type, t_bot)
+        crs = np.array([1 if abs(x) <= bthr and not r else 0 for x, r in zip(c, ref)], np.int32)
+    return ref, crs, (thr, bthr)
+
+
+def prepare_coarsening_and_refinement(dim, n, leaves, refine, coarsen):
+    """Triangulation::prepare_coarsening_and_refinement (deal.II 9.2 source/grid/tria.cc, third party,
+    not vendored: restated from its published algorithm) with the reference's MeshSmoothing
+    smoothing_on_refinement | smoothing_on_coarsening (navier_stokes_base.cc:55-60; called at :682), on
+    a forest of n^dim coarse cells. leaves: [(level, (x, y[, z]))] (origin in units of the level's
+    cells); refine / coarsen: per-leaf 0/1. Steps per pass, repeated until no flag changes: (1)
+    do_not_produce_unrefined_islands, (2) eliminate_refined_inner/boundary_islands, (3)
+    limit_level_difference_at_vertices, (4) eliminate_unrefined_islands, (6) no double refinement at
+    faces, (8) fix_coarsen_flags (its own vertex pass, complete families, coarsening_allowed). Cells are
+    visited level by level in Morton order (active ones in reverse for steps 3, 4, 6). Pure Python for
+    test-size trees. Returns (refine, coarsen) as int32 arrays. Parity unpinned: deal.II is absent."""
+    leaves = [(int(l), tuple(int(v) for v in x)) for l, x in leaves]
+    ref = [bool(v) for v in refine]
+    crs = [bool(v) for v in coarsen]
+    idx = {c: i for i, c in enumerate(leaves)}
+    cells = set(leaves)
+    for l, x in leaves:
+        while l > 0:
+            l, x = l - 1, tuple(v // 2 for v in x)
+            cells.add((l, x))
+    LM = max(l for l, _ in leaves)
+
+    def morton(c):
+        l, x = c
+        p = [v << (LM - l) for v in x]
+        s = 1 << LM
+        base = 0
+        for d in reversed(range(dim)):
+            base = base * n + p[d] // s
+        m = 0
+        for b in range(LM - 1, -1, -1):
+            for d in range(dim - 1, -1, -1):
+                m = (m << 1) | ((p[d] % s) >> b & 1)
+        return base, m
+
+    allc = sorted(cells, key=lambda c: (c[0], morton(c)))
+    act_rev = [idx[c] for c in reversed(allc) if c in idx]
+
+    def kids(c):
+        l, x = c
+        return [(l + 1, tuple(2 * x[d] + (k >> d & 1) for d in range(dim))) for k in range(2 ** dim)]
+
+    def nbr(c, f):  # (kind, cell): 0 boundary, 1 same level, 2 coarser
+        l, x = c
+        d, up = f // 2, f % 2
+        y = list(x)
+        y[d] += 1 if up else -1
+        if y[d] < 0 or y[d] >= n << l:
+            return 0, None
+        if (l, tuple(y)) in cells:
+            return 1, (l, tuple(y))
+        return 2, (l - 1, tuple(v // 2 for v in y))
+
+    def coarsened(c):
+        if c in idx:
+            return False
+        ks = kids(c)
+        if all(k in idx and crs[idx[k]] for k in ks):
+            return True
+        for k in ks:
+            if k in idx:
+                crs[idx[k]] = False
+        return False
+
+    def refined_by(c, f):
+        kind, m = nbr(c, f)
+        if kind != 1:
+            return False
+        return ref[idx[m]] if m in idx else not coarsened(m)
+
+    def corners(c):
+        l, x = c
+        for k in range(2 ** dim):
+            yield tuple((x[d] + (k >> d & 1)) << (LM + 1 - l) for d in range(dim))
+
+    def vertex_pass():
+        vl = {}
+        for i, c in enumerate(leaves):
+            lev = c[0] + 1 if ref[i] else c[0] - 1 if crs[i] else c[0]
+            for v in corners(c):
+                vl[v] = max(vl.get(v, 0), lev)
+        for i in act_rev:
+            if ref[i]:
+                continue
+            c = leaves[i]
+            for v in corners(c):
+                if vl[v] >= c[0] + 1:
+                    crs[i] = False
+                    if vl[v] > c[0] + 1:
+                        ref[i] = True
+                        for w in corners(c):
+                            vl[w] = max(vl[w], c[0] + 1)
+
+    def allowed(p, user):
+        for f in range(2 * dim):
+            if nbr(p, f)[0] == 0:
+                continue
+            d, up = f // 2, f % 2
+            for k in kids(p):
+                if (k[1][d] & 1) != up:
+                    continue
+                kind, m = nbr(k, f)
+                if kind != 1:
+                    continue
+                if m not in idx and m not in user:
+                    return False
+                if m in idx and ref[idx[m]]:
+                    return False
+        return True
+
+    def fix_coarsen():
+        while True:
+            before = list(crs)
+            vertex_pass()
+            for i, c in enumerate(leaves):
+                if c[0] == 0:
+                    crs[i] = False
+            user = set()
+            for c in allc:
+                if c in idx:
+                    continue
+                ks = kids(c)
+                hit = [k for k in ks if k in idx and crs[idx[k]]]
+                for k in hit:
+                    crs[idx[k]] = False
+                if len(hit) == len(ks):
+                    user.add(c)
+            for c in reversed(allc):
+                if c in user and allowed(c, user):
+                    for k in kids(c):
+                        crs[idx[k]] = True
+            if crs == before:
+                return
+
+    nf = 2 * dim
+    while True:
+        r0, c0 = list(ref), list(crs)
+        for c in allc:  # step 1
+            if c in idx or not coarsened(c):
+                continue
+            valid = [f for f in range(nf) if nbr(c, f)[0] != 0]
+            cnt = sum(1 for f in valid if refined_by(c, f))
+            if cnt == len(valid) or (cnt == len(valid) - 1 and len(valid) == nf):
+                for k in kids(c):
+                    crs[idx[k]] = False
+        for c in allc:  # step 2
+            if c in idx and not ref[idx[c]]:
+                continue
+            if c not in idx and not all(k in idx for k in kids(c)):
+                continue
+            valid = [f for f in range(nf) if nbr(c, f)[0] != 0]
+            if valid and all(not refined_by(c, f) for f in valid):
+                if c in idx:
+                    ref[idx[c]] = False
+                else:
+                    for k in kids(c):
+                        ref[idx[k]], crs[idx[k]] = False, True
+        vertex_pass()  # step 3
+        for i in act_rev:  # step 4
+            if ref[i]:
+                continue
+            valid = [f for f in range(nf) if nbr(leaves[i], f)[0] != 0]
+            r = sum(1 for f in valid if refined_by(leaves[i], f))
+            if len(valid) - r < r:
+                crs[i], ref[i] = False, True
+        for i in act_rev:  # step 6
+            if not ref[i]:
+                continue
+            for f in range(nf):
+                kind, m = nbr(leaves[i], f)
+                if kind == 2:
+                    crs[idx[m]], ref[idx[m]] = False, True
+        fix_coarsen()  # step 8
+        if ref == r0 and crs == c0:
+            break
+    return np.array(ref, np.int32), np.array(crs, np.int32)
+
+
 def refine_mark(c, thr):
     """dealii::GridRefinement::refine's marking (deal.II 9.2 source/grid/grid_refinement.cc, not
     vendored): no flags when every indicator is 0; a zero threshold becomes the smallest positive

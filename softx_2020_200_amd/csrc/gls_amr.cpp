@@ -13,6 +13,7 @@
 // lattice of spacing h_fine / k; ids follow lexicographic lattice order (x fastest) over the used
 // points. Velocity and pressure spaces are built separately (kp may be < k).
 #include <algorithm>
+#include <limits>
 #include <cmath>
 #include <functional>
 #include <cstdint>
@@ -269,53 +270,20 @@ int gls_refine_fixed_number(int64_t n_cells, const float *criteria, double top_f
   return refine_mark(n_cells, criteria, thr, flags, nullptr);
 }
 
-// parallel::distributed::GridRefinement, the call refine_mesh_kelly makes
-// (navier_stokes_base.cc:654-667; deal.II 9.2 source/distributed/grid_refinement.cc, not vendored).
-// The threshold is found by bisection between the slightly widened indicator extremes (geometric
-// mean while the lower end is > 0), 25 steps at most: the number (or summed error) of cells strictly
-// above the test value decides the half kept. Cells with criteria >= threshold are flagged
-// (dealii::GridRefinement::refine). The summed quantities are global sums, so with per-rank
-// indicators the caller gathers them first (the app adapts on one process).
-int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
-                  int64_t max_n_cells, int32_t *flags, double *threshold) {
-  if (n_cells < 0 || (n_cells && (!criteria || !flags)) || (dim != 2 && dim != 3) || top_fraction < 0 ||
-      top_fraction > 1 || (fraction_type != 0 && fraction_type != 1) || max_n_cells < 0)
-    return gls_io_set_error(GLS_EINVAL, "gls_refine_pd: bad arguments");
-  for (int64_t i = 0; i < n_cells; ++i) flags[i] = 0;
-  if (threshold) *threshold = 0.0;
-  if (n_cells == 0) return 0;
-  double lo = criteria[0], hi = criteria[0];
-  float total = 0.0f;  // compute_global_sum accumulates in the indicator type
-  for (int64_t i = 0; i < n_cells; ++i) {
-    if (!(criteria[i] >= 0.0f)) return gls_io_set_error(GLS_EINVAL, "gls_refine_pd: criteria must be >= 0");
-    lo = std::min(lo, (double)criteria[i]);
-    hi = std::max(hi, (double)criteria[i]);
-    total += criteria[i];
-  }
+// compute_threshold of parallel::distributed::GridRefinement (RefineAndCoarsenFixedNumber /
+// RefineAndCoarsenFixedFraction, deal.II 9.2 source/distributed/grid_refinement.cc, not vendored):
+// bisection between the slightly widened indicator extremes (geometric mean while the lower end is
+// > 0), 25 steps at most; the number (fraction_type 0) or summed indicator (1) of cells strictly
+// above the test value decides the half kept.
+static double pd_threshold(int64_t n_cells, const float *criteria, int fraction_type, double lo, double hi,
+                           double target) {
   const double gmax = hi;
-  double target;
-  if (fraction_type == 0) {
-    // GridRefinement::adjust_refine_and_coarsen_number_fraction<dim> (no coarsening): cap the
-    // refined count so that the mesh grows to at most max_n_cells
-    double frac = top_fraction;
-    const double nc = (double)n_cells, inc = (double)((1 << dim) - 1);
-    if (n_cells >= max_n_cells) frac = 0.0;
-    else if ((int64_t)(nc + nc * top_fraction * inc) > max_n_cells)
-      frac = (double)(max_n_cells - n_cells) / (nc * top_fraction * inc) * top_fraction;
-    target = (double)(int64_t)(frac * nc);
-  } else {
-    target = top_fraction * total;  // L1 norm: fraction of the summed indicators
-  }
   // adjust_interesting_range
   if (lo > 0) lo *= 0.99;
   if (hi > 0) hi *= 1.01;
   else hi += 0.01 * (hi - lo);
-  double thr = lo;
   for (int it = 0;; ++it) {
-    if (lo == hi) {
-      thr = fraction_type == 1 ? std::min(lo, gmax) : lo;
-      break;
-    }
+    if (lo == hi) return fraction_type == 1 ? std::min(lo, gmax) : lo;
     const double test = lo > 0 ? std::sqrt(lo * hi) : (lo + hi) / 2;
     double above = 0.0;
     for (int64_t i = 0; i < n_cells; ++i)
@@ -325,7 +293,84 @@ int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_
     else lo = hi = test;
     if (it + 1 == 25) lo = hi = test;
   }
-  return refine_mark(n_cells, criteria, thr, flags, threshold);
+}
+
+// parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number / _fixed_fraction, the call
+// refine_mesh_kelly makes (navier_stokes_base.cc:654-667). Fixed number: the fractions are first
+// capped by GridRefinement::adjust_refine_and_coarsen_number_fraction<dim> so that the mesh grows to
+// at most max_n_cells (when it is already larger, coarsen (n - max) / (1 - 2^-dim) cells and refine
+// none); top threshold: int(top * n) cells above it; bottom threshold: int((1 - bottom) * n) cells
+// above it. Fixed fraction: top * (summed indicator) / (1 - bottom) * (summed indicator) above the
+// thresholds. A zero bottom fraction gives the lowest representable threshold (no coarsening).
+// mark_cells: GridRefinement::refine (criteria >= top, see refine_mark), then GridRefinement::coarsen
+// (|criteria| <= bottom on cells not flagged for refinement). The summed quantities are global sums,
+// so with per-rank indicators the caller gathers them first (the app adapts on one process).
+int gls_refine_coarsen_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
+                          double bottom_fraction, int64_t max_n_cells, int32_t *refine, int32_t *coarsen,
+                          double *thresholds) {
+  if (n_cells < 0 || (n_cells && (!criteria || !refine)) || (dim != 2 && dim != 3) || top_fraction < 0 ||
+      top_fraction > 1 || bottom_fraction < 0 || bottom_fraction > 1 ||
+      top_fraction + bottom_fraction > 1 + 1e-15 || (fraction_type != 0 && fraction_type != 1) || max_n_cells < 0 ||
+      (bottom_fraction > 0 && n_cells && !coarsen))
+    return gls_io_set_error(GLS_EINVAL, "gls_refine_coarsen_pd: bad arguments");
+  for (int64_t i = 0; i < n_cells; ++i) refine[i] = 0;
+  if (coarsen)
+    for (int64_t i = 0; i < n_cells; ++i) coarsen[i] = 0;
+  if (thresholds) thresholds[0] = thresholds[1] = 0.0;
+  if (n_cells == 0) return 0;
+  double lo = criteria[0], hi = criteria[0];
+  float total = 0.0f;  // compute_global_sum accumulates in the indicator type
+  for (int64_t i = 0; i < n_cells; ++i) {
+    if (!(criteria[i] >= 0.0f)) return gls_io_set_error(GLS_EINVAL, "gls_refine_coarsen_pd: criteria must be >= 0");
+    lo = std::min(lo, (double)criteria[i]);
+    hi = std::max(hi, (double)criteria[i]);
+    total += criteria[i];
+  }
+  double top = top_fraction, bottom = bottom_fraction, t_top, t_bottom;
+  const double nc = (double)n_cells;
+  if (fraction_type == 0) {
+    const double inc = (double)((1 << dim) - 1), dec = 1.0 - 1.0 / (double)(1 << dim);
+    const double rc = nc * top_fraction, cc = nc * bottom_fraction;
+    if (n_cells >= max_n_cells) {
+      top = 0.0;
+      bottom = std::min((nc - (double)max_n_cells) / dec / nc, 1.0);
+    } else if ((int64_t)(nc + rc * inc - cc * dec) > max_n_cells) {
+      const double alpha = ((double)max_n_cells - nc) / (rc * inc - cc * dec);
+      top = alpha * top_fraction;
+      bottom = alpha * bottom_fraction;
+    }
+    t_top = (double)(int64_t)(top * nc);
+    t_bottom = (double)(int64_t)((1.0 - bottom) * nc);
+  } else {
+    t_top = top_fraction * total;
+    t_bottom = (1.0 - bottom_fraction) * total;
+  }
+  const double thr = pd_threshold(n_cells, criteria, fraction_type, lo, hi, t_top);
+  double used = thr;
+  const int nr = refine_mark(n_cells, criteria, thr, refine, &used);
+  double bthr = -std::numeric_limits<float>::max();  // std::numeric_limits<Number>::lowest(), Number = float
+  if (bottom > 0 && coarsen) {  // refinement-only callers pass no coarsen flags
+    bthr = pd_threshold(n_cells, criteria, fraction_type, lo, hi, t_bottom);
+    for (int64_t i = 0; i < n_cells; ++i)
+      if (std::fabs(criteria[i]) <= bthr && !refine[i]) {
+        coarsen[i] = 1;
+      }
+  }
+  if (thresholds) {
+    thresholds[0] = used;
+    thresholds[1] = bthr;
+  }
+  return nr;
+}
+
+// the refinement-only call (fraction coarsening = 0): flags of gls_refine_coarsen_pd, threshold = top.
+int gls_refine_pd(int64_t n_cells, const float *criteria, int dim, int fraction_type, double top_fraction,
+                  int64_t max_n_cells, int32_t *flags, double *threshold) {
+  double th[2];
+  const int rc = gls_refine_coarsen_pd(n_cells, criteria, dim, fraction_type, top_fraction, 0.0, max_n_cells, flags,
+                                       nullptr, th);
+  if (rc >= 0 && threshold) *threshold = th[0];
+  return rc;
 }
 
 // SolutionTransfer::interpolate for the first refinement of a uniform mesh (navier_stokes_base.cc:

@@ -315,6 +315,268 @@ int build_space(const gls_octree &t, int L, int kk, double lo, double hf, std::v
   return GLS_OK;
 }
 
+// Triangulation::prepare_coarsening_and_refinement (deal.II 9.2 source/grid/tria.cc, third party, not
+// vendored: restated from its published algorithm) with MeshSmoothing smoothing_on_refinement |
+// smoothing_on_coarsening, as the reference constructs its triangulation (navier_stokes_base.cc:55-60)
+// and calls it after the Kelly marking (:682). Cells are the tree's nodes (leaves = active cells,
+// their ancestors = refined cells); "all cells" are visited level by level in Morton order, the
+// active cells in reverse (finest level first), as deal.II's cell iterators run for a tree refined
+// from one coarse cell. Isotropic refinement only.
+struct Smoother {
+  const gls_octree &t;
+  int dim, LM;
+  std::vector<char> ref, crs;                  // per-leaf refine / coarsen flags
+  std::unordered_map<uint64_t, int32_t> node;  // (level, x) -> leaf index, or -1 for a refined cell
+  std::vector<Leaf> all;                       // every cell, level-wise Morton order
+  std::vector<size_t> active_rev;              // leaves, reverse of deal.II's active order
+  std::unordered_map<uint64_t, char> user;     // refined cells to be coarsened (fix_coarsen_flags)
+
+  static uint64_t key(int level, const int64_t *x) {
+    return ((uint64_t)level << 58) | ((uint64_t)x[0] << 38) | ((uint64_t)x[1] << 19) | (uint64_t)x[2];
+  }
+  int64_t extent(int level) const { return (int64_t)t.n << level; }
+  Smoother(const gls_octree &tree, const int32_t *r, const int32_t *c) : t(tree), dim(tree.dim) {
+    LM = tree.max_level();
+    const size_t nc = tree.leaves.size();
+    ref.resize(nc);
+    crs.resize(nc);
+    for (size_t i = 0; i < nc; ++i) {
+      ref[i] = r[i] != 0;
+      crs[i] = c[i] != 0;
+      const Leaf &l = tree.leaves[i];
+      node[key(l.level, l.x)] = (int32_t)i;
+      all.push_back(l);
+    }
+    for (size_t i = 0; i < nc; ++i) {
+      Leaf a = tree.leaves[i];
+      while (a.level > 0) {
+        a.level -= 1;
+        for (int d = 0; d < 3; ++d) a.x[d] /= 2;
+        if (node.count(key(a.level, a.x))) break;
+        node[key(a.level, a.x)] = -1;
+        all.push_back(a);
+      }
+    }
+    std::sort(all.begin(), all.end(), [&](const Leaf &a, const Leaf &b) {
+      if (a.level != b.level) return a.level < b.level;
+      return morton_key(t, a, LM) < morton_key(t, b, LM);
+    });
+    for (size_t j = all.size(); j-- > 0;) {
+      const int32_t v = node[key(all[j].level, all[j].x)];
+      if (v >= 0) active_rev.push_back((size_t)v);
+    }
+  }
+  int32_t find(int level, const int64_t *x) const {  // -2: no such cell
+    auto it = node.find(key(level, x));
+    return it == node.end() ? -2 : it->second;
+  }
+  bool is_active(const Leaf &c) const { return find(c.level, c.x) >= 0; }
+  // cell->neighbor(f): the cell of the same level across face f (active or refined), else the
+  // coarser active cell; returns 0 at the boundary, 1 same level, 2 coarser
+  int neighbor(const Leaf &c, int f, Leaf &nb) const {
+    const int d = f / 2;
+    nb = c;
+    nb.x[d] += (f & 1) ? 1 : -1;
+    if (nb.x[d] < 0 || nb.x[d] >= extent(c.level)) return 0;
+    if (find(nb.level, nb.x) != -2) return 1;
+    nb.level -= 1;
+    for (int e = 0; e < 3; ++e) nb.x[e] /= 2;
+    return 2;
+  }
+  std::vector<Leaf> kids(const Leaf &c) const { return children(t, c); }
+  size_t leaf(const Leaf &c) const { return (size_t)find(c.level, c.x); }
+  // cell_will_be_coarsened: every child active and flagged; otherwise the children's flags are cleared
+  bool will_be_coarsened(const Leaf &c) {
+    if (is_active(c)) return false;
+    int n = 0;
+    const std::vector<Leaf> ch = kids(c);
+    for (const Leaf &k : ch) {
+      const int32_t v = find(k.level, k.x);
+      if (v >= 0 && crs[(size_t)v]) ++n;
+    }
+    if (n == (int)ch.size()) return true;
+    for (const Leaf &k : ch) {
+      const int32_t v = find(k.level, k.x);
+      if (v >= 0) crs[(size_t)v] = 0;
+    }
+    return false;
+  }
+  // face_will_be_refined_by_neighbor (isotropic): a refined neighbour that stays refined, or an
+  // active one flagged for refinement, of the same level
+  bool face_refined_by_neighbor(const Leaf &c, int f) {
+    Leaf nb;
+    if (neighbor(c, f, nb) != 1) return false;
+    const int32_t v = find(nb.level, nb.x);
+    if (v < 0) return !will_be_coarsened(nb);
+    return ref[(size_t)v] != 0;
+  }
+  uint64_t vkey(const Leaf &c, int corner) const {  // vertex on the lattice of level LM + 1
+    int64_t v[3] = {0, 0, 0};
+    for (int d = 0; d < dim; ++d) v[d] = (c.x[d] + ((corner >> d) & 1)) << (LM + 1 - c.level);
+    return ((uint64_t)v[0] << 42) | ((uint64_t)v[1] << 21) | (uint64_t)v[2];
+  }
+  // limit_level_difference_at_vertices (step 3, repeated in fix_coarsen_flags): the highest future
+  // level at each vertex (a cell flagged for coarsening tentatively counts one level down), then in
+  // reverse order a cell below it loses its coarsen flag, and is refined when two levels below
+  void limit_vertex_levels() {
+    std::unordered_map<uint64_t, int> vl;
+    const int nv = 1 << dim;
+    for (size_t i = 0; i < t.leaves.size(); ++i) {
+      const Leaf &c = t.leaves[i];
+      const int lev = ref[i] ? c.level + 1 : crs[i] ? c.level - 1 : c.level;
+      for (int v = 0; v < nv; ++v) {
+        auto it = vl.find(vkey(c, v));
+        if (it == vl.end()) vl[vkey(c, v)] = std::max(0, lev);
+        else it->second = std::max(it->second, lev);
+      }
+    }
+    for (size_t i : active_rev) {
+      if (ref[i]) continue;
+      const Leaf &c = t.leaves[i];
+      for (int v = 0; v < nv; ++v) {
+        const int lv = vl[vkey(c, v)];
+        if (lv < c.level + 1) continue;
+        crs[i] = 0;
+        if (lv > c.level + 1) {
+          ref[i] = 1;
+          for (int w = 0; w < nv; ++w) vl[vkey(c, w)] = std::max(vl[vkey(c, w)], c.level + 1);
+        }
+      }
+    }
+  }
+  // coarsening_allowed: no child on a face of p may have a same-level neighbour that is refined and
+  // stays so, or is flagged for refinement (the 3D line rule is implied by the vertex rule)
+  bool coarsening_allowed(const Leaf &p) const {
+    for (int f = 0; f < 2 * dim; ++f) {
+      Leaf nb;
+      if (neighbor(p, f, nb) == 0) continue;
+      const int d = f / 2;
+      for (const Leaf &ch : kids(p)) {
+        if (((ch.x[d] & 1) != 0) != ((f & 1) != 0)) continue;  // child not on face f
+        Leaf cn;
+        if (neighbor(ch, f, cn) != 1) continue;
+        const int32_t v = find(cn.level, cn.x);
+        if (v < 0 && !user.count(key(cn.level, cn.x))) return false;
+        if (v >= 0 && ref[(size_t)v]) return false;
+      }
+    }
+    return true;
+  }
+  // fix_coarsen_flags: coarsen flags survive only on complete families whose coarsening is allowed
+  void fix_coarsen_flags() {
+    for (int it = 0; it < 1000; ++it) {
+      const std::vector<char> before = crs;
+      limit_vertex_levels();
+      for (size_t i = 0; i < t.leaves.size(); ++i)
+        if (t.leaves[i].level == 0) crs[i] = 0;
+      user.clear();
+      for (const Leaf &c : all) {
+        if (is_active(c)) continue;
+        int n = 0;
+        const std::vector<Leaf> ch = kids(c);
+        for (const Leaf &k : ch) {
+          const int32_t v = find(k.level, k.x);
+          if (v >= 0 && crs[(size_t)v]) {
+            ++n;
+            crs[(size_t)v] = 0;
+          }
+        }
+        if (n == (int)ch.size()) user[key(c.level, c.x)] = 1;
+      }
+      for (size_t j = all.size(); j-- > 0;) {
+        const Leaf &c = all[j];
+        if (!user.count(key(c.level, c.x)) || !coarsening_allowed(c)) continue;
+        for (const Leaf &k : kids(c)) crs[leaf(k)] = 1;
+      }
+      user.clear();
+      if (crs == before) break;
+    }
+  }
+  int run() {
+    const int nf = 2 * dim;
+    int loops = 0;
+    while (loops < 1000) {
+      ++loops;
+      const std::vector<char> r0 = ref, c0 = crs;
+      // step 1: do_not_produce_unrefined_islands — keep a family whose neighbours (all, or all but
+      // one of an interior cell's) will be refined
+      for (const Leaf &c : all) {
+        if (is_active(c) || !will_be_coarsened(c)) continue;
+        int n_nb = 0, cnt = 0;
+        for (int f = 0; f < nf; ++f) {
+          Leaf nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          ++n_nb;
+          if (face_refined_by_neighbor(c, f)) ++cnt;
+        }
+        if (cnt == n_nb || (cnt == n_nb - 1 && n_nb == nf))
+          for (const Leaf &k : kids(c)) crs[leaf(k)] = 0;
+      }
+      // step 2: eliminate_refined_inner_islands | eliminate_refined_boundary_islands — a cell
+      // refined (or flagged) whose neighbours will all be unrefined is coarsened (or unflagged)
+      for (const Leaf &c : all) {
+        const int32_t v = find(c.level, c.x);
+        if (v >= 0 && !ref[(size_t)v]) continue;
+        bool all_active = true;
+        if (v < 0)
+          for (const Leaf &k : kids(c)) all_active = all_active && is_active(k);
+        if (!all_active) continue;
+        int total = 0, unrefined = 0;
+        for (int f = 0; f < nf; ++f) {
+          Leaf nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          ++total;
+          if (!face_refined_by_neighbor(c, f)) ++unrefined;
+        }
+        if (unrefined != total || total == 0) continue;
+        if (v < 0) {
+          for (const Leaf &k : kids(c)) {
+            ref[leaf(k)] = 0;
+            crs[leaf(k)] = 1;
+          }
+        } else {
+          ref[(size_t)v] = 0;
+        }
+      }
+      // step 3
+      limit_vertex_levels();
+      // step 4: eliminate_unrefined_islands — refine a cell with more refined than unrefined
+      // interior neighbours
+      for (size_t i : active_rev) {
+        if (ref[i]) continue;
+        const Leaf &c = t.leaves[i];
+        int refined = 0, unrefined = 0;
+        for (int f = 0; f < nf; ++f) {
+          Leaf nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          if (face_refined_by_neighbor(c, f)) ++refined;
+          else ++unrefined;
+        }
+        if (unrefined < refined) {
+          crs[i] = 0;
+          ref[i] = 1;
+        }
+      }
+      // step 6: no double refinement at a face — the coarser neighbour of a cell to be refined is refined
+      for (size_t i : active_rev) {
+        if (!ref[i]) continue;
+        const Leaf &c = t.leaves[i];
+        for (int f = 0; f < nf; ++f) {
+          Leaf nb;
+          if (neighbor(c, f, nb) != 2) continue;
+          const size_t j = leaf(nb);
+          crs[j] = 0;
+          ref[j] = 1;
+        }
+      }
+      // step 8
+      fix_coarsen_flags();
+      if (ref == r0 && crs == c0) break;
+    }
+    return loops;
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -419,6 +681,18 @@ int gls_octree_adapt(gls_octree *t, const int32_t *refine, const int32_t *coarse
   if (int rc = balance(*t); rc != GLS_OK) return rc;
   sort_leaves(*t);
   return GLS_OK;
+}
+
+int gls_octree_prepare(const gls_octree *t, int32_t *refine, int32_t *coarsen) {
+  if (!t || (!t->leaves.empty() && (!refine || !coarsen))) return gls_io_set_error(GLS_EINVAL, "gls_octree_prepare: bad arguments");
+  if ((t->n << (t->max_level() + 1)) >= ((int64_t)1 << 19)) return gls_io_set_error(GLS_EINVAL, "gls_octree_prepare: tree too deep");
+  Smoother sm(*t, refine, coarsen);
+  const int loops = sm.run();
+  for (size_t i = 0; i < t->leaves.size(); ++i) {
+    refine[i] = sm.ref[i];
+    coarsen[i] = sm.crs[i];
+  }
+  return loops;
 }
 
 int gls_octree_mesh(const gls_octree *t, int k, int kp, double lo, double hi, gls_refined_mesh **out) {

@@ -36,8 +36,8 @@ EXPORTS = [
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
     "gls_set_hanging", "gls_mesh_refined_create", "gls_mesh_refined_destroy", "gls_octree_create", "gls_octree_destroy", "gls_octree_info",
-    "gls_octree_cells", "gls_octree_adapt", "gls_octree_mesh", "gls_octree_mesh_destroy", "gls_octree_transfer", "gls_octree_faces", "gls_kelly_estimate_faces",
-    "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd",
+    "gls_octree_cells", "gls_octree_adapt", "gls_octree_prepare", "gls_octree_mesh", "gls_octree_mesh_destroy", "gls_octree_transfer", "gls_octree_faces", "gls_kelly_estimate_faces",
+    "gls_kelly_estimate", "gls_refine_fixed_number", "gls_mesh_refined_interpolate", "gls_refine_pd", "gls_refine_coarsen_pd",
     "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
@@ -335,6 +335,17 @@ class Octree:
         check(self.L.gls_octree_adapt(self.h, r.ctypes.data, c.ctypes.data, int(max_level), int(min_level)),
               "gls_octree_adapt")
 
+    def prepare(self, refine, coarsen):
+        """Triangulation::prepare_coarsening_and_refinement with the reference's mesh smoothing
+        (gls_octree_prepare; navier_stokes_base.cc:55-60, 682). Returns (refine, coarsen, loops)."""
+        nc = self.n_cells
+        r = np.array(refine, dtype=np.int32).reshape(nc)
+        c = np.array(coarsen, dtype=np.int32).reshape(nc)
+        self.L.gls_octree_prepare.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        loops = self.L.gls_octree_prepare(self.h, r.ctypes.data, c.ctypes.data)
+        check(min(loops, 0), "gls_octree_prepare")
+        return r, c, loops
+
     def mesh_handle(self, k, kp=None):
         """Owned gls_refined_mesh pointer (free with free_mesh_handle)."""
         kp = k if kp is None else kp
@@ -399,6 +410,23 @@ def refine_pd(criteria, dim, top_fraction, fraction_type="number", max_n_cells=1
                               int(max_n_cells), flags.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(thr))
     check(min(rc, 0), "gls_refine_pd")
     return flags, thr.value
+
+
+def refine_coarsen_pd(criteria, dim, top_fraction, bottom_fraction, fraction_type="number", max_n_cells=100000000):
+    """parallel::distributed::GridRefinement::refine_and_coarsen_fixed_number / _fixed_fraction with
+    coarsening (gls_refine_coarsen_pd; navier_stokes_base.cc:654-667). Returns (refine, coarsen,
+    (top threshold, bottom threshold))."""
+    c = np.ascontiguousarray(criteria, dtype=np.float32)
+    r, k = np.zeros(c.size, dtype=np.int32), np.zeros(c.size, dtype=np.int32)
+    th = (C.c_double * 2)()
+    ft = {"number": 0, "fraction": 1}[fraction_type]
+    L = load()
+    L.gls_refine_coarsen_pd.argtypes = [C.c_int64, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int64,
+                                        C.c_void_p, C.c_void_p, C.c_void_p]
+    rc = L.gls_refine_coarsen_pd(c.size, c.ctypes.data, int(dim), ft, float(top_fraction), float(bottom_fraction),
+                                 int(max_n_cells), r.ctypes.data, k.ctypes.data, th)
+    check(min(rc, 0), "gls_refine_coarsen_pd")
+    return r, k, (th[0], th[1])
 
 
 def refined_interpolate(dim, n, k, kp, refine, coarse, lo=-1.0, hi=1.0):

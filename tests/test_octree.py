@@ -226,3 +226,95 @@ def test_octree_faces_tile_the_interior(dim):
             if x0[i, d] + h[i, d] < 1.0 - 1e-12:
                 ref += np.prod(np.delete(h[i], d))
     assert abs(area - ref) < 1e-12
+
+
+def _leaves(t):
+    lev, x0, h = t.cells()
+    return [(int(l), tuple(int(round(v)) for v in (x - t.lo) / hh)) for l, x, hh in zip(lev, x0, h)]
+
+
+def test_refine_coarsen_pd_matches_oracle():
+    """gls_refine_coarsen_pd (p::d::GridRefinement with coarsening, navier_stokes_base.cc:654-667) equals
+    the oracle restatement bit for bit: flags and both thresholds, with ties, zeros, the element cap and
+    meshes already above it."""
+    from oracle.oracle import pd_refine_coarsen
+    from softx_2020_200_amd import refine_coarsen_pd
+    rng = np.random.default_rng(1)
+    for t in range(200):
+        n = int(rng.integers(1, 300))
+        dim = int(rng.integers(2, 4))
+        c = (rng.random(n) ** 3).astype(np.float32)
+        if t % 5 == 0:
+            c[rng.integers(0, n, n // 3)] = 0
+        if t % 7 == 0:
+            c = np.round(c * 4) / 4
+        top, bot = float(rng.random() * 0.5), (float(rng.random() * 0.4) if t % 3 else 0.0)
+        ft = ("number", "fraction")[t % 2]
+        mx = int(rng.integers(1, 3 * n + 2))
+        a, b = refine_coarsen_pd(c, dim, top, bot, ft, mx), pd_refine_coarsen(c, dim, top, bot, ft, mx)
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all() and a[2] == b[2], (t, a[2], b[2])
+        assert not (a[0] & a[1]).any()
+    # at the cap, fixed number coarsens (n - max) / (1 - 2^-dim) cells and refines none
+    c = np.arange(1, 101, dtype=np.float32)
+    r, k, _ = refine_coarsen_pd(c, 2, 0.3, 0.0, "number", 76)
+    assert r.sum() == 0 and k.sum() == 32 and k[:32].all()
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+def test_prepare_matches_oracle_and_is_consistent(dim):
+    """gls_octree_prepare (Triangulation::prepare_coarsening_and_refinement with the reference's mesh
+    smoothing, navier_stokes_base.cc:55-60, 682) equals the oracle restatement on random multi-level
+    trees and flags; a second call changes nothing (deal.II's promise); the adaptation then executes
+    exactly the prepared flags (no extra balance refinement) and keeps the vertex 2:1 rule."""
+    from oracle.oracle import prepare_coarsening_and_refinement
+    rng = np.random.default_rng(7 + dim)
+    for case in range(12 if dim == 2 else 5):
+        n = 1 + case % 2
+        t = Octree(dim, n)
+        for _ in range(3 if dim == 2 else 2):
+            t.adapt(np.ones(t.n_cells, np.int32))
+            if dim == 3:
+                break
+        for step in range(3 if dim == 2 else 2):
+            nc = t.n_cells
+            r = (rng.random(nc) < rng.random() * 0.4).astype(np.int32)
+            c = ((rng.random(nc) < rng.random() * 0.7) & (r == 0)).astype(np.int32)
+            pr, pc, loops = t.prepare(r, c)
+            orr, occ = prepare_coarsening_and_refinement(dim, n, _leaves(t), r, c)
+            assert (pr == orr).all() and (pc == occ).all(), (case, step)
+            again = t.prepare(pr, pc)
+            assert (again[0] == pr).all() and (again[1] == pc).all()
+            assert not (pr & pc).any() and pc.sum() % 2 ** dim == 0
+            t.adapt(pr, pc)
+            assert t.n_cells == nc + (2 ** dim - 1) * int(pr.sum()) - (2 ** dim - 1) * int(pc.sum()) // 2 ** dim
+            assert vertex_balanced(t)
+
+
+def test_prepare_islands():
+    """The smoothing rules on a uniform 8x8 mesh: an isolated flagged cell loses its flag
+    (eliminate_refined_inner_islands), and so do four cells that touch only at corners; a cell with
+    three flagged face neighbours is refined too (eliminate_unrefined_islands); a 2x2 block stays as
+    flagged."""
+    t = Octree(2, 1)
+    for _ in range(3):
+        t.adapt(np.ones(t.n_cells, np.int32))
+    lev, x0, h = t.cells()
+    ij = np.round((x0 + 1) / h).astype(int)
+    at = {(int(a), int(b)): i for i, (a, b) in enumerate(ij)}
+    z = np.zeros(t.n_cells, np.int32)
+    r = z.copy()
+    r[at[3, 3]] = 1
+    assert t.prepare(r, z)[0].sum() == 0
+    r = z.copy()
+    for p in [(3, 4), (5, 4), (4, 3), (4, 5)]:
+        r[at[p]] = 1
+    assert t.prepare(r, z)[0].sum() == 0
+    r = z.copy()
+    for p in [(3, 4), (3, 3), (4, 3), (5, 4), (5, 3)]:
+        r[at[p]] = 1
+    pr = t.prepare(r, z)[0]
+    assert pr[at[4, 4]] == 1 and pr.sum() == 6
+    r = z.copy()
+    for p in [(2, 2), (2, 3), (3, 2), (3, 3)]:
+        r[at[p]] = 1
+    assert (t.prepare(r, z)[0] == r).all()
