@@ -11,8 +11,8 @@
 //
 // Usage: gls_navier_stokes [--dim 2|3] [--precond mg|jacobi] file.prm
 // Scope: mesh type dealii / grid type hyper_cube (+ initial refinement; steady "number mesh adapt"
-// with mesh adaptation type uniform, or kelly = one Kelly-driven local refinement with hanging
-// nodes: fraction type number or fraction, no coarsening); bc types noslip, function, periodic, slip.
+// with mesh adaptation type uniform, or kelly = Kelly-driven refinement and coarsening on a forest
+// with hanging nodes, any number of levels); bc types noslip, function, periodic, slip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -169,7 +169,8 @@ struct Params {
   // mesh adaptation (parameters.cc:649-731): uniform, or kelly = one Kelly-driven refinement
   std::string madapt = "none";
   int kelly_variable = 0;  // 0 velocity, 1 pressure
-  double frac_refine = 0.1;
+  double frac_refine = 0.1, frac_coarsen = 0.05;
+  int min_level = 0;
   int frac_type = 0;            // 0 fixed number, 1 fixed fraction (of the summed indicators)
   int64_t max_cells = 100000000;  // max number elements
   int max_level = 10;
@@ -240,7 +241,7 @@ Params read_params(const Prm &p, int dim) {
   if (P.adapt_frequency < 1) die("mesh adaptation/frequency must be >= 1");
   if (P.method == Method::steady && P.mesh_adapt > 0 && madapt != "uniform" && madapt != "kelly")
     die("mesh adaptation type '%s' is not supported (uniform or kelly)", madapt.c_str());
-  if (madapt == "kelly") {  // refine_mesh_kelly (navier_stokes_base.cc:610-780), first adaptation only
+  if (madapt == "kelly") {  // refine_mesh_kelly (navier_stokes_base.cc:610-780)
     const std::string ma = "mesh adaptation/";
     const std::string var = p.get(ma + "variable", "velocity");
     if (var != "velocity" && var != "pressure") die("mesh adaptation variable '%s' is unknown", var.c_str());
@@ -251,11 +252,12 @@ Params read_params(const Prm &p, int dim) {
     P.max_cells = (int64_t)p.d(ma + "max number elements", 100000000);
     P.frac_refine = p.d(ma + "fraction refinement", 0.1);
     P.max_level = p.i(ma + "max refinement level", 10);
-    if (p.d(ma + "fraction coarsening", 0.05) != 0.0)
-      die("mesh adaptation: coarsening is not supported (set fraction coarsening = 0)");
+    P.frac_coarsen = p.d(ma + "fraction coarsening", 0.05);
+    P.min_level = p.i(ma + "min refinement level", 0);
+    if (P.frac_refine < 0 || P.frac_coarsen < 0 || P.frac_refine + P.frac_coarsen > 1)
+      die("mesh adaptation: fractions must be >= 0 with refinement + coarsening <= 1");
     if (P.method != Method::steady) die("kelly mesh adaptation: steady simulations only");
     if (P.general) die("kelly mesh adaptation: hyper_cube meshes only");
-    if (P.mesh_adapt > 1) die("kelly mesh adaptation: one adaptation (one refinement level) at most");
     if (P.k > 2 || P.kp > P.k) die("kelly mesh adaptation: 1 <= pressure order <= velocity order <= 2");
   }
   const int nbc = p.i("boundary conditions/number", 0);
@@ -678,7 +680,8 @@ struct Solver {
   Mesh m;
   Constraints C;
   gls_ctx *ctx = nullptr;
-  gls_refined_mesh *rmesh = nullptr;  // the locally refined mesh m was built from (kelly)
+  gls_refined_mesh *rmesh = nullptr;  // the adapted mesh m was built from (kelly; gls_octree_mesh)
+  gls_octree *tree = nullptr;         // kelly: the forest p4est keeps (created at the first adaptation)
   gls_umesh *um = nullptr;            // general meshes: the triangulation (kept across refinements)
   gls_fe_space *space = nullptr;      // and its current FE space
   std::vector<gls_ctx *> mg_levels;
@@ -711,6 +714,7 @@ struct Solver {
     release();
     if (space) gls_fe_space_destroy(space);
     if (um) gls_umesh_destroy(um);
+    if (tree) gls_octree_destroy(tree);
   }
 
   void release() {
@@ -719,7 +723,7 @@ struct Solver {
     if (ctx) gls_destroy(ctx);
     ilu_ctx = nullptr;
     ctx = nullptr;
-    if (rmesh) gls_mesh_refined_destroy(rmesh);
+    if (rmesh) gls_octree_mesh_destroy(rmesh);
     rmesh = nullptr;
     if (d_cv) (void)hipFree(d_cv);
     for (double *q : {d_h, d_blk}) if (q) (void)hipFree(q);
@@ -829,12 +833,13 @@ struct Solver {
     hk(hipDeviceSynchronize(), "device copy");
   }
 
-  // the hyper_cube(2^refinement) with the flagged cells split once (hanging nodes): mesh,
-  // Dirichlet constraints (hanging nodes excluded), hanging constraint lines on the context.
-  // Per-cell kernels and a Jacobi-preconditioned GMRES (no multigrid on refined meshes).
-  void setup_refined(int n, const std::vector<int32_t> &flags) {
+  // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
+  // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels
+  // and a Jacobi-preconditioned GMRES (no multigrid on locally refined meshes).
+  void setup_refined(gls_refined_mesh *R_new) {
     release();
-    ck(gls_mesh_refined_create(P.dim, n, P.k, P.kp, P.lo, P.hi, flags.data(), &rmesh), "gls_mesh_refined_create");
+    rmesh = R_new;
+    const int n = 1;
     const gls_refined_mesh &R = *rmesh;
     const int dim = P.dim;
     const int nvl = dim == 3 ? (P.k + 1) * (P.k + 1) * (P.k + 1) : (P.k + 1) * (P.k + 1);
@@ -1397,48 +1402,117 @@ struct Solver {
     }
     host_changed();
   }
-  // refine_mesh_kelly (navier_stokes_base.cc:610-780) for the first adaptation of the uniform
-  // mesh: Kelly indicator of the velocity or pressure on the device (gls_kelly_estimate, stored as
-  // float like deal.II's Vector<float>), refine_and_coarsen_fixed_number (refinement part;
-  // coarsening is rejected at parameter time), max refinement level, SolutionTransfer
+  // refine_mesh_kelly (navier_stokes_base.cc:610-780): Kelly indicator of the velocity or pressure
+  // on the device (gls_kelly_estimate on the uniform mesh, gls_kelly_estimate_faces on an adapted
+  // one; stored as float like deal.II's Vector<float>), refine_and_coarsen_fixed_{number,fraction}
+  // with coarsening (:654-667), the max / min refinement level rules (:669-680),
+  // prepare_coarsening_and_refinement with the triangulation's smoothing (:682), execution on the
+  // forest (refine, coarsen complete families, corner balance: p4est) and SolutionTransfer of the
+  // present solution (:684-733). The forest is the hyper_cube's one coarse cell refined
+  // `initial refinement` times, so leaf levels are deal.II's cell levels.
   void refine_kelly() {
     need_host();
-    const Mesh old = m;
-    if (old.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
-    if (!old.vx.empty()) die("kelly mesh adaptation: the mesh is already refined once");
+    if (m.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
+    const int dim = P.dim;
+    const int64_t nc = m.nc;
     upload(present, d_present);
     double *d_eta = nullptr;
-    hk(hipMalloc(&d_eta, sizeof(double) * (size_t)old.nc), "hipMalloc");
-    ck(gls_kelly_estimate(ctx, d_present, P.kelly_variable, d_eta), "gls_kelly_estimate");
+    hk(hipMalloc(&d_eta, sizeof(double) * (size_t)nc), "hipMalloc");
+    if (!rmesh) {
+      ck(gls_kelly_estimate(ctx, d_present, P.kelly_variable, d_eta), "gls_kelly_estimate");
+    } else {
+      int64_t nf = 0;
+      ck(gls_octree_faces(rmesh, &nf, nullptr, nullptr, nullptr, nullptr, nullptr), "gls_octree_faces");
+      std::vector<int32_t> fa((size_t)nf), fb((size_t)nf), fd((size_t)nf);
+      std::vector<double> ra((size_t)nf * 4), rb((size_t)nf * 4);
+      ck(gls_octree_faces(rmesh, &nf, fa.data(), fb.data(), fd.data(), ra.data(), rb.data()), "gls_octree_faces");
+      ck(gls_kelly_estimate_faces(ctx, d_present, P.kelly_variable, nf, fa.data(), fb.data(), fd.data(), ra.data(),
+                                  rb.data(), d_eta),
+         "gls_kelly_estimate_faces");
+    }
     hk(hipDeviceSynchronize(), "kelly estimate");  // the context stream is not the null stream
-    std::vector<double> eta((size_t)old.nc);
+    std::vector<double> eta((size_t)nc);
     download(d_eta, eta);
     (void)hipFree(d_eta);
-    std::vector<float> crit(eta.begin(), eta.end());
-    std::vector<int32_t> cflag((size_t)old.nc, 0), flags((size_t)old.nc, 0);
-    // parallel::distributed::GridRefinement::refine_and_coarsen_fixed_{number,fraction} (:654-667)
-    const int nflag = gls_refine_pd(old.nc, crit.data(), old.dim, P.frac_type, P.frac_refine, P.max_cells,
-                                    cflag.data(), nullptr);
-    ck(nflag, "gls_refine_pd");
-    // cells at max refinement level keep their refine flag cleared (tria.n_levels() > max level)
-    if (P.max_level <= P.refinement) std::fill(cflag.begin(), cflag.end(), 0);
-    // the hyper_cube's cell order -> the lexicographic order gls_mesh_refined_create expects
-    for (int64_t c = 0; c < old.nc; ++c) {
-      int64_t lex = 0, stride = 1;
-      for (int d = 0; d < old.dim; ++d) {
-        const int i = (int)std::lround((old.x0[(size_t)(c * old.dim + d)] - old.lo) / old.hc);
-        lex += (int64_t)i * stride;
-        stride *= old.n;
+    const int64_t n_uniform = (int64_t)1 << P.refinement;
+    if (!tree) {  // GridGenerator::hyper_cube + refine_global(initial refinement)
+      if (rmesh) die("kelly mesh adaptation: internal error (adapted mesh without a forest)");
+      ck(gls_octree_create(dim, 1, &tree), "gls_octree_create");
+      for (int r = 0; r < P.refinement; ++r) {
+        int64_t nl = 0;
+        ck(gls_octree_info(tree, &nl, nullptr), "gls_octree_info");
+        std::vector<int32_t> all((size_t)nl, 1), none((size_t)nl, 0);
+        ck(gls_octree_adapt(tree, all.data(), none.data(), 1 << 20, 0), "gls_octree_adapt");
       }
-      flags[(size_t)lex] = cflag[(size_t)c];
     }
-    std::printf("kelly: %d of %lld cells flagged for refinement\n", P.max_level <= P.refinement ? 0 : nflag,
-                (long long)old.nc);
+    int64_t nl = 0;
+    int max_lev = 0;
+    ck(gls_octree_info(tree, &nl, &max_lev), "gls_octree_info");
+    if (nl != nc) die("kelly mesh adaptation: forest (%lld leaves) and mesh (%lld cells) disagree", (long long)nl, (long long)nc);
+    std::vector<int32_t> lev((size_t)nl);
+    std::vector<double> x0((size_t)nl * dim), hh((size_t)nl * dim);
+    ck(gls_octree_cells(tree, lev.data(), x0.data(), hh.data(), P.lo, P.hi), "gls_octree_cells");
+    std::vector<float> crit((size_t)nc);
+    if (!rmesh) {  // the uniform mesh's cell order -> the forest's leaf order
+      const double hc = (P.hi - P.lo) / (double)n_uniform;
+      std::vector<int64_t> at((size_t)nc);
+      for (int64_t c = 0; c < nc; ++c) {
+        int64_t lex = 0, st = 1;
+        for (int d = 0; d < dim; ++d) {
+          lex += std::lround((m.x0[(size_t)(c * dim + d)] - P.lo) / hc) * st;
+          st *= n_uniform;
+        }
+        at[(size_t)lex] = c;
+      }
+      for (int64_t i = 0; i < nl; ++i) {
+        int64_t lex = 0, st = 1;
+        for (int d = 0; d < dim; ++d) {
+          lex += std::lround((x0[(size_t)(i * dim + d)] - P.lo) / hc) * st;
+          st *= n_uniform;
+        }
+        crit[(size_t)i] = (float)eta[(size_t)at[(size_t)lex]];
+      }
+    } else {
+      for (int64_t i = 0; i < nc; ++i) crit[(size_t)i] = (float)eta[(size_t)i];
+    }
+    std::vector<int32_t> rf((size_t)nc, 0), cf((size_t)nc, 0);
+    ck(gls_refine_coarsen_pd(nc, crit.data(), dim, P.frac_type, P.frac_refine, P.frac_coarsen, P.max_cells,
+                             rf.data(), cf.data(), nullptr),
+       "gls_refine_coarsen_pd");
+    int64_t nr0 = 0, nc0 = 0;
+    for (int64_t i = 0; i < nc; ++i) {
+      nr0 += rf[(size_t)i];
+      nc0 += cf[(size_t)i];
+    }
+    // tria.n_levels() > max refinement level: no refinement from that level up; no coarsening on
+    // the min refinement level
+    for (int64_t i = 0; i < nc; ++i) {
+      if (max_lev + 1 > P.max_level && lev[(size_t)i] >= P.max_level) rf[(size_t)i] = 0;
+      if (lev[(size_t)i] == P.min_level) cf[(size_t)i] = 0;
+    }
+    ck(gls_octree_prepare(tree, rf.data(), cf.data()), "gls_octree_prepare");
+    int64_t nr1 = 0, nc1 = 0;
+    for (int64_t i = 0; i < nc; ++i) {
+      nr1 += rf[(size_t)i];
+      nc1 += cf[(size_t)i];
+    }
+    std::printf("kelly: %lld of %lld cells flagged for refinement, %lld for coarsening (after smoothing: %lld, %lld)\n",
+                (long long)nr0, (long long)nc, (long long)nc0, (long long)nr1, (long long)nc1);
+    ck(gls_octree_adapt(tree, rf.data(), cf.data(), 1 << 20, 0), "gls_octree_adapt");
+    gls_refined_mesh *nm = nullptr;
+    ck(gls_octree_mesh(tree, P.k, P.kp, P.lo, P.hi, &nm), "gls_octree_mesh");
     const std::vector<double> sol = present;
-    setup_refined(old.n, flags);
+    gls_refined_mesh *old_rm = rmesh;
+    rmesh = nullptr;  // kept for the transfer (release() would free it)
+    setup_refined(nm);
     host_changed();  // present is rewritten on the host below
-    ck(gls_mesh_refined_interpolate(rmesh, old.n, P.lo, P.hi, sol.data(), present.data()),
-       "gls_mesh_refined_interpolate");
+    if (old_rm) {
+      ck(gls_octree_transfer(old_rm, rmesh, sol.data(), present.data()), "gls_octree_transfer");
+      gls_octree_mesh_destroy(old_rm);
+    } else {
+      ck(gls_mesh_refined_interpolate(rmesh, (int)n_uniform, P.lo, P.hi, sol.data(), present.data()),
+         "gls_mesh_refined_interpolate");
+    }
   }
   // NavierStokesBase::finish_simulation's error table (navier_stokes_base.cc:382-424): deal.II
   // ConvergenceTable text layout — steady: cells | error_velocity + log2 reduction rate |

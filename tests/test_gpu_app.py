@@ -6,6 +6,7 @@ errors are compared with the numbers the reference printed."""
 import json
 import os
 import subprocess
+import numpy as np
 
 import pytest
 
@@ -246,54 +247,81 @@ def test_app_mms2d_slip_walls_matches_oracle(tmp_path):
     assert abs(rows[0][1] - g["error_velocity"][0]) > 1e-3 * g["error_velocity"][0]
 
 
+def _leaf_lex(tree, n_uniform):
+    """lexicographic hyper_cube(n_uniform) cell index of each leaf of a uniform forest"""
+    lev, x0, h = tree.cells()
+    hc = (tree.hi - tree.lo) / n_uniform
+    ij = np.round((x0 - tree.lo) / hc).astype(np.int64)
+    return sum(ij[:, d] * n_uniform ** d for d in range(tree.dim))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,variable,ftype", [(2, "velocity", "number"), (2, "pressure", "number"),
-                                                (3, "velocity", "number"), (2, "velocity", "fraction")])
-def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable, ftype):
-    """mesh adaptation type = kelly (refine_mesh_kelly, navier_stokes_base.cc:610-780) in the app, first
-    adaptation of the uniform 8^2 (mms2d) / 8^3 (mms3d) Q1 mesh: Kelly indicator on the device, 30 % flagged
-    by parallel::distributed::GridRefinement (fraction type number: cells; fraction: summed indicator; no
-    coarsening), one refinement with hanging nodes, solution transfer,
-    Newton on the refined mesh. The first row equals the reference golden; the refined row equals the
-    oracle's own pipeline (solve -> Kelly -> flag -> refine -> condensed solve). Parity unpinned beyond
-    the oracle: the reference holds no Kelly golden on this mesh."""
-    import numpy as np
-    from oracle.oracle import (Oracle, StructuredProblem, kelly_estimate, muparser_to_numpy, newton_solve,
-                               pd_refine_fixed)
+@pytest.mark.parametrize("dim,variable,ftype,coarsen,adapts", [
+    (2, "velocity", "number", 0.0, 1), (2, "pressure", "number", 0.0, 1), (3, "velocity", "number", 0.0, 1),
+    (2, "velocity", "fraction", 0.0, 1), (2, "velocity", "number", 0.1, 3), (2, "pressure", "fraction", 0.05, 3),
+    (3, "velocity", "number", 0.1, 2)])
+def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable, ftype, coarsen, adapts):
+    """mesh adaptation type = kelly (refine_mesh_kelly, navier_stokes_base.cc:610-780) in the app over
+    `adapts` steady cycles of mms2d (8^2) / mms3d (8^3), Q1: Kelly on the device (conforming kernel on
+    the uniform mesh, face-piece kernel on the adapted ones), p::d::GridRefinement marking with
+    refinement 0.3 and coarsening, max / min level rules, prepare_coarsening_and_refinement smoothing,
+    forest adaptation with hanging nodes, SolutionTransfer, Newton on each mesh. The first row equals
+    the reference golden; every later row equals the oracle's own pipeline (oracle Kelly -> oracle
+    marking -> oracle smoothing -> the forest -> condensed oracle Newton): cell counts exactly, errors
+    at 1e-6. Parity unpinned beyond the oracle: the reference holds no Kelly golden on this mesh."""
+    from oracle.oracle import (Oracle, StructuredProblem, kelly_estimate, kelly_estimate_boxes, muparser_to_numpy,
+                               newton_solve, pd_refine_coarsen, prepare_coarsening_and_refinement)
     import softx_2020_200_amd as sx
     g = G["mms2d_gls" if dim == 2 else "mms3d_gls"]
     n, gi = (8, 0) if dim == 2 else (8, 1)  # 4^3: the discrete velocity is ~0, Kelly is roundoff
-    prm = mms_prm(g, dim, 3, 1).replace("  set type = uniform\n", f"""  set type = kelly
+    prm = mms_prm(g, dim, 3, adapts).replace("  set type = uniform\n", f"""  set type = kelly
   set variable = {variable}
   set fraction type = {ftype}
   set fraction refinement = 0.3
-  set fraction coarsening = 0
+  set fraction coarsening = {coarsen}
 """)
     out = run_app(tmp_path, prm, dim, "--precond", "jacobi")
     rows = table(out)
-    assert len(rows) == 2, out
+    assert len(rows) == adapts + 1, out
     assert int(rows[0][0]) == n ** dim and close(rows[0][1], g["error_velocity"][gi], 5), (rows, out)
-    # the oracle's pipeline on the same mesh
+    # the oracle's pipeline on the same meshes
     F, E = muparser_to_numpy(g["force"]), muparser_to_numpy(g["exact"])
     p = StructuredProblem(dim, n, k=1, viscosity=1.0)
     p.set_force(lambda X: F(X)[:, :dim])
     p.set_dirichlet([("noslip", 0, None)])
     x, _, _ = newton_solve(p, tol=1e-10)
-    eta = kelly_estimate(p, x, 0 if variable == "velocity" else 1)
-    flags, _ = pd_refine_fixed(eta.astype(np.float32), dim, 0.3, ftype)
-    assert int(rows[1][0]) == n ** dim + (2 ** dim - 1) * int(flags.sum()), (rows, int(flags.sum()))
-    mesh = sx.refined_cube(dim, n, 1, 1, flags)
-    q = StructuredProblem.from_refined(mesh, viscosity=1.0)
-    lines = sx.hanging_dof_lines(mesh)
-    q.set_hanging(*lines)
-    q.hang_lines = lines
-    q.set_dirichlet([("noslip", 0, None)])
-    q.set_force(lambda X: F(X)[:, :dim])
-    x0 = q.apply_nonzero_constraints(sx.refined_interpolate(dim, n, 1, 1, flags, x))
-    y, _, _ = newton_solve(q, x0=x0.copy(), tol=1e-10)
-    eu, ep = Oracle(q).l2_error(y, E)
-    assert abs(rows[1][1] - eu) <= 1e-6 * eu, (rows[1], eu)
-    assert abs(rows[1][3] - ep) <= 1e-6 * ep, (rows[1], ep)
-    assert rows[1][1] < rows[0][1]
-    assert f"kelly: {int(flags.sum())} of {n ** dim} cells flagged" in out
-    assert "Hanging node DoFs:            %d" % len(lines[0]) in out
+    tree = sx.Octree(dim, 1)
+    for _ in range(3):
+        tree.adapt(np.ones(tree.n_cells, np.int32))
+    eta = kelly_estimate(p, x, 0 if variable == "velocity" else 1)[_leaf_lex(tree, n)]
+    var = 0 if variable == "velocity" else 1
+    leaves = lambda t: [(int(l), tuple(int(round(v)) for v in (x0 - t.lo) / hh)) for l, x0, hh in zip(*t.cells())]
+    coarsened = 0
+    for a in range(adapts):
+        nc = tree.n_cells
+        r, c, _ = pd_refine_coarsen(eta.astype(np.float32), dim, 0.3, coarsen, ftype)
+        lev = tree.cells()[0]
+        c[lev == 0] = 0  # min refinement level 0; max level 10 is not reached
+        r0 = int(r.sum())
+        c0 = int(c.sum())
+        r, c = prepare_coarsening_and_refinement(dim, 1, leaves(tree), r, c)
+        assert (f"kelly: {r0} of {nc} cells flagged for refinement, {c0} for coarsening (after smoothing: "
+                f"{int(r.sum())}, {int(c.sum())})") in out
+        coarsened += int(c.sum())
+        tree.adapt(r, c)
+        assert int(rows[a + 1][0]) == tree.n_cells == nc + (2 ** dim - 1) * (int(r.sum()) - int(c.sum()) // 2 ** dim), \
+            (a, rows, int(r.sum()), int(c.sum()))
+        mesh = tree.mesh(1, 1)
+        q = StructuredProblem.from_refined(mesh, viscosity=1.0)
+        lines = sx.hanging_dof_lines(mesh)
+        q.set_hanging(*lines)
+        q.hang_lines = lines
+        q.set_dirichlet([("noslip", 0, None)])
+        q.set_force(lambda X: F(X)[:, :dim])
+        y, _, _ = newton_solve(q, tol=1e-10)
+        eu, ep = Oracle(q).l2_error(y, E)
+        assert abs(rows[a + 1][1] - eu) <= 1e-6 * eu, (a, rows[a + 1], eu)
+        assert abs(rows[a + 1][3] - ep) <= 1e-6 * ep, (a, rows[a + 1], ep)
+        eta = kelly_estimate_boxes(mesh, y, var)
+    assert rows[-1][1] < rows[0][1]
+    assert (coarsened > 0) == (coarsen > 0 and adapts > 1), coarsened  # families coarsened from the 2nd cycle on

@@ -190,8 +190,8 @@ def _app(tmp_path, prm_text, *args):
     ("subsection simulation control\n set method = steady\n set number mesh adapt = 1\nend\n"
      "subsection mesh adaptation\n set type = kelly\n set fraction type = banana\nend\n", "fraction type 'banana' is unknown"),
     ("subsection simulation control\n set method = steady\n set number mesh adapt = 1\nend\n"
-     "subsection mesh adaptation\n set type = kelly\n set fraction type = fraction\nend\n",  # default coarsening 0.05
-     "coarsening is not supported"),
+     "subsection mesh adaptation\n set type = kelly\n set fraction refinement = 0.97\nend\n",  # default coarsening 0.05
+     "refinement + coarsening <= 1"),
 ])
 def test_app_rejects_unsupported_input_before_touching_the_gpu(tmp_path, text, msg):
     out = _app(tmp_path, text, "--dim", "3")
