@@ -389,6 +389,12 @@ int gls_kelly_estimate_faces(gls_ctx *ctx, const double *sol, int variable, int6
                              double *eta);
 int gls_octree_faces(const gls_refined_mesh *mesh, int64_t *n_faces, int32_t *fa, int32_t *fb, int32_t *fdir,
                      double *rect_a, double *rect_b);
+/* The same on mapped (MappingQ) meshes, conforming or adapted: pieces and geometry from
+ * gls_fe_space_kelly_faces with nq = n_q + 1 (nqf = nq^(dim-1) points per piece, host arrays),
+ * the jump integrals on the device; eta (DEVICE, n_cells) = sqrt(cell_diam/24 * sum of pieces). */
+int gls_kelly_estimate_mapped(gls_ctx *ctx, const double *sol, int variable, int64_t n_pieces, int nqf,
+                              const int32_t *ca, const int32_t *cb, const double *xi, const double *g,
+                              const double *jxw, const double *cell_diam, double *eta);
 /* GridRefinement::refine_and_coarsen_fixed_number, refinement part (navier_stokes_base.cc:654-661;
  * serial deal.II rule): flags[i] = 1 for the int(top_fraction * n_cells) largest criteria (every
  * cell >= the threshold value). Returns the number of flagged cells. HOST arrays. */
@@ -453,6 +459,14 @@ typedef struct {
   const int32_t *cell_mapping;                /* mapping degree used per cell (1 or k) */
   const double *cell_measure;                 /* cell->measure() */
   double volume;                              /* GridTools::volume (sum of measures) */
+  const int32_t *cell_level;                  /* refinement level of each active cell */
+  int64_t n_vhang;                            /* hanging velocity node vhang_node[i] = sum over j in    */
+  const int64_t *vhang_node, *vhang_off;      /*   [vhang_off[i], vhang_off[i+1]) of vhang_w[j] * node   */
+  const int64_t *vhang_master;                /*   vhang_master[j] (make_hanging_node_constraints +      */
+  const double *vhang_w;                      /*   close(); masters unconstrained)                       */
+  int64_t n_phang;                            /* the same for the pressure nodes */
+  const int64_t *phang_node, *phang_off, *phang_master;
+  const double *phang_w;
   void *impl_;
 } gls_fe_space;
 int gls_umesh_generate(int dim, const char *grid_type, const char *grid_arguments, gls_umesh **out);
@@ -467,6 +481,26 @@ int gls_umesh_fe_space(const gls_umesh *mesh, int k, int kp, int qmapping_all, i
 int gls_fe_space_destroy(gls_fe_space *space);
 int gls_fe_space_transfer(const gls_fe_space *coarse, const gls_fe_space *fine, const double *coarse_vec,
                           double *fine_vec);
+/* Local adaptation of the triangulation (the reference's p::d::Triangulation with
+ * smoothing_on_refinement | smoothing_on_coarsening, navier_stokes_base.cc:55-60, 592-780), on any
+ * mesh above (gmsh, generators, manifolds; new vertices placed as refine_global places them):
+ *   gls_umesh_prepare: prepare_coarsening_and_refinement with that smoothing (the steps of
+ *     gls_octree_prepare, neighbours through shared faces); refine / coarsen are per-active-cell
+ *     flags in the order of gls_umesh_fe_space's cells, updated in place; returns the iterations.
+ *   gls_umesh_adapt: execute_coarsening_and_refinement: flagged cells refined, complete flagged
+ *     families coarsened when the vertex 2:1 balance allows, balance restored by refinement.
+ * A space built afterwards carries the hanging-node lines (gls_fe_space.vhang_* / phang_*) and its
+ * cells' levels; gls_fe_space_transfer then maps vectors from any earlier space of the same mesh
+ * (refinement, coarsening, several levels). */
+int gls_umesh_prepare(const gls_umesh *mesh, int32_t *refine, int32_t *coarsen);
+int gls_umesh_adapt(gls_umesh *mesh, const int32_t *refine, const int32_t *coarsen);
+/* Face pieces for KellyErrorEstimator with MappingQ on such a space (conforming faces one piece,
+ * a face with a refined neighbour one piece per child face; geometry on the coarse side as deal.II's
+ * present cell): cells ca / cb, and per QGauss<dim-1>(nq) point q of piece e the reference
+ * coordinates xi[e][q][side][dim] of both sides, g[e][q][side][dim] = J^-1 n, jxw[e][q];
+ * cell_diam[n_cells] = cell->diameter(). Host arrays; call with ca == NULL for the count. */
+int gls_fe_space_kelly_faces(const gls_fe_space *space, int nq, int64_t *n_pieces, int32_t *ca, int32_t *cb,
+                             double *xi, double *g, double *jxw, double *cell_diam);
 
 /* ------------------------------------------------------------------------------------------
  * Drop-in I/O surface, host side.

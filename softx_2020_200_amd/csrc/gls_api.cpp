@@ -2108,6 +2108,52 @@ int gls_kelly_estimate_faces(gls_ctx *c, const double *sol, int variable, int64_
   return GLS_OK;
 }
 
+// Kelly indicator on mapped (MappingQ) meshes, conforming or with hanging faces: the face pieces
+// and their per-point geometry from gls_fe_space_kelly_faces (host), the jump integrals on the
+// device, eta_K = sqrt(diam(K)/24 * sum of K's pieces) in a fixed order (eta: DEVICE pointer)
+int gls_kelly_estimate_mapped(gls_ctx *c, const double *sol, int variable, int64_t n_pieces, int nqf, const int32_t *ca,
+                              const int32_t *cb, const double *xi, const double *g, const double *jxw,
+                              const double *cell_diam, double *eta) {
+  GLS_TRY(check_ctx(c));
+  if (!sol || !eta || !cell_diam || (variable != 0 && variable != 1) || n_pieces < 0 ||
+      (n_pieces > 0 && (!ca || !cb || !xi || !g || !jxw)))
+    return set_err(GLS_EINVAL, "gls_kelly_estimate_mapped: bad arguments");
+  const int nq = c->nq1d + 1;  // QGauss<dim-1>(n_q + 1)
+  if (nqf != (c->dim == 3 ? nq * nq : nq))
+    return set_err(GLS_EINVAL, "gls_kelly_estimate_mapped: %d face points per piece, the face rule has %d", nqf,
+                   c->dim == 3 ? nq * nq : nq);
+  for (int64_t e = 0; e < n_pieces; ++e)
+    if (ca[e] < 0 || ca[e] >= c->n_cells || cb[e] < 0 || cb[e] >= c->n_cells)
+      return set_err(GLS_EINVAL, "gls_kelly_estimate_mapped: piece %lld out of range", (long long)e);
+  const bool pres = variable == 1;
+  const int m = pres ? c->kp : c->k;
+  const int32_t *nodes = pres && c->cell_pnodes.p ? c->cell_pnodes.p : c->cell_vnodes.p;
+  const gls::KellyTables T = kelly_tables(m, nq);
+  const size_t npts = (size_t)n_pieces * (size_t)nqf;
+  DevBuf<int32_t> dca, dcb;
+  DevBuf<double> dxi, dg, dj, dfi;
+  GLS_TRY(dca.upload(ca, (size_t)n_pieces));
+  GLS_TRY(dcb.upload(cb, (size_t)n_pieces));
+  GLS_TRY(dxi.upload(xi, npts * 2 * c->dim));
+  GLS_TRY(dg.upload(g, npts * 2 * c->dim));
+  GLS_TRY(dj.upload(jxw, npts));
+  GLS_TRY(dfi.alloc((size_t)std::max<int64_t>(n_pieces, 1)));
+  HIP_TRY(gls::launch_kelly_mapped(c->dim, m, nodes, sol, n_pieces, nqf, dca.p, dcb.p, dxi.p, dg.p, dj.p,
+                                   pres ? 1 : c->dim, pres ? (int64_t)c->dim * c->n_vnodes : 0, pres ? 1 : c->dim, T,
+                                   dfi.p, c->stream));
+  std::vector<double> fi((size_t)n_pieces), acc((size_t)c->n_cells, 0.0);
+  HIP_TRY(hipMemcpyAsync(fi.data(), dfi.p, sizeof(double) * fi.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int64_t e = 0; e < n_pieces; ++e) {  // each piece counts for both of its cells
+    acc[(size_t)ca[e]] += fi[(size_t)e];
+    acc[(size_t)cb[e]] += fi[(size_t)e];
+  }
+  for (int64_t k = 0; k < c->n_cells; ++k) acc[(size_t)k] = std::sqrt(cell_diam[k] / 24.0 * acc[(size_t)k]);
+  HIP_TRY(hipMemcpyAsync(eta, acc.data(), sizeof(double) * acc.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GLS_OK;
+}
+
 int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {
   GLS_TRY(check_ctx(c));
   if (c->dim != 3 || n1d < 2 || !l2g) return set_err(GLS_EINVAL, "gls_set_lattice: 3D, n1d >= 2, map required");

@@ -1,4 +1,5 @@
-// gls_kelly.hip — Kelly error indicator on conforming axis-aligned Qk meshes.
+// gls_kelly.hip — Kelly error indicator on Qk meshes: conforming axis-aligned boxes,
+// octree meshes with hanging faces, and mapped (MappingQ) unstructured meshes with hanging faces.
 //
 // Restates KellyErrorEstimator<dim>::estimate as refine_mesh_kelly calls it
 // (navier_stokes_base.cc:612-652: QGauss<dim-1>(n_q + 1) on the faces, no Neumann boundaries, the
@@ -142,6 +143,50 @@ __global__ void __launch_bounds__(256) k_kelly_faces(const int32_t *__restrict__
   fint[e] = integral;
 }
 
+// one thread per face piece of a mapped (MappingQ) mesh: the host lists, per face quadrature point,
+// both sides' reference coordinates xi, the vectors g = J^-1 n (n: the unit normal of the piece)
+// and JxW, so that n . grad u = g . grad_xi u on each side; fint[e] = sum_q JxW sum_c jump_c^2
+template <int DIM, int M>
+__global__ void __launch_bounds__(256) k_kelly_mapped(const int32_t *__restrict__ cell_nodes, const double *__restrict__ sol,
+                                                      int64_t n_pieces, int nqf, const int32_t *__restrict__ ca,
+                                                      const int32_t *__restrict__ cb, const double *__restrict__ xi,
+                                                      const double *__restrict__ gv, const double *__restrict__ jxw,
+                                                      int ncomp, int64_t base, int stride, KellyTables T,
+                                                      double *__restrict__ fint) {
+  constexpr int M1 = M + 1;
+  constexpr int NN = DIM == 3 ? M1 * M1 * M1 : M1 * M1;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_pieces) return;
+  const int cells[2] = {ca[e], cb[e]};
+  double integral = 0.0;
+  for (int q = 0; q < nqf; ++q) {
+    double dn[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    for (int side = 0; side < 2; ++side) {
+      const double *x = xi + ((e * nqf + q) * 2 + side) * DIM;
+      const double *g = gv + ((e * nqf + q) * 2 + side) * DIM;
+      double v[3][M1], dv[3][M1];
+      for (int d = 0; d < DIM; ++d)
+        for (int a = 0; a <= M; ++a) lagr<M>(T.xn, a, x[d], v[d][a], dv[d][a]);
+      for (int a = 0; a < NN; ++a) {
+        const int ai[3] = {a % M1, (a / M1) % M1, DIM == 3 ? a / (M1 * M1) : 0};
+        double phi_n = 0.0;  // g . grad_xi phi_a
+        for (int d = 0; d < DIM; ++d) {
+          double t = g[d] * dv[d][ai[d]];
+          for (int o = 0; o < DIM; ++o)
+            if (o != d) t *= v[o][ai[o]];
+          phi_n += t;
+        }
+        const int64_t node = cell_nodes[(int64_t)cells[side] * NN + a];
+        for (int c = 0; c < ncomp; ++c) dn[side][c] += phi_n * sol[base + node * stride + c];
+      }
+    }
+    double j2 = 0.0;
+    for (int c = 0; c < ncomp; ++c) j2 += (dn[0][c] - dn[1][c]) * (dn[0][c] - dn[1][c]);
+    integral += jxw[e * nqf + q] * j2;
+  }
+  fint[e] = integral;
+}
+
 }  // namespace
 
 hipError_t launch_kelly_faces(int dim, int m, const int32_t *cell_nodes, const double *geo, const double *sol,
@@ -161,6 +206,21 @@ hipError_t launch_kelly_faces(int dim, int m, const int32_t *cell_nodes, const d
   GLS_KELLYF_CASE(3, 1)
   GLS_KELLYF_CASE(3, 2)
 #undef GLS_KELLYF_CASE
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_kelly_mapped(int dim, int m, const int32_t *cell_nodes, const double *sol, int64_t n_pieces, int nqf,
+                               const int32_t *ca, const int32_t *cb, const double *xi, const double *g,
+                               const double *jxw, int ncomp, int64_t base, int stride, const KellyTables &T,
+                               double *fint, hipStream_t s) {
+  if (n_pieces <= 0) return hipSuccess;
+  const dim3 gr((unsigned)((n_pieces + 255) / 256)), b(256);
+#define GLS_KELLYM_CASE(D, MM)                                                                                     if (dim == D && m == MM) {                                                                                         hipLaunchKernelGGL((k_kelly_mapped<D, MM>), gr, b, 0, s, cell_nodes, sol, n_pieces, nqf, ca, cb, xi, g, jxw,                        ncomp, base, stride, T, fint);                                                               return hipGetLastError();                                                                                      }
+  GLS_KELLYM_CASE(2, 1)
+  GLS_KELLYM_CASE(2, 2)
+  GLS_KELLYM_CASE(3, 1)
+  GLS_KELLYM_CASE(3, 2)
+#undef GLS_KELLYM_CASE
   return hipErrorNotSupported;
 }
 

@@ -91,6 +91,11 @@ hipError_t launch_kelly_faces(int dim, int m, const int32_t *cell_nodes, const d
                               int64_t n_faces, const int32_t *fa, const int32_t *fb, const int32_t *fdir,
                               const double *rect_a, const double *rect_b, int ncomp, int64_t base, int stride,
                               const KellyTables &T, double *fint, hipStream_t s);
+// mapped meshes: per piece e and face point q, xi / g [e][q][side][dim] (g = J^-1 n), jxw [e][q]
+hipError_t launch_kelly_mapped(int dim, int m, const int32_t *cell_nodes, const double *sol, int64_t n_pieces, int nqf,
+                               const int32_t *ca, const int32_t *cb, const double *xi, const double *g,
+                               const double *jxw, int ncomp, int64_t base, int stride, const KellyTables &T,
+                               double *fint, hipStream_t s);
 // eta[cell] = sqrt(sum over faces with nbr >= 0 of diam/24 * int_F sum_c [d_n u_c]^2); component c of
 // node n at sol[base + n * stride + c], c < ncomp; cell_nodes [n_cells][(m+1)^dim]; nbr [n_cells][2 dim]
 hipError_t launch_kelly(int dim, int m, const int32_t *cell_nodes, const int32_t *nbr, const double *geo,

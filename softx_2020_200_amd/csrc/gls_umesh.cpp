@@ -82,6 +82,19 @@ struct UMesh {
   std::map<EKey, int> bface;                  // boundary faces -> boundary id
   std::map<EKey, int> line_mf, face_mf;       // manifold ids of lines (and 3D quads)
   std::map<int, ManifoldDesc> mf;
+  // refinement hierarchy (the triangulation's cells on every level): cells / cell_mf above are the
+  // active cells, tree[active[i]] their hierarchy records. Records are never removed (coarsened
+  // children stay as dead records), so hierarchy ids are stable across adaptations.
+  struct HCell {
+    std::array<int64_t, 8> v;
+    int mf, level;
+    int64_t parent;  // -1 on level 0
+    int pos;         // child position in the parent (bit d: upper half in local direction d)
+    int64_t child0;  // first of the 2^dim consecutive children, -1 when active
+  };
+  std::vector<HCell> tree;
+  std::vector<int64_t> roots, active;
+  std::map<EKey, int64_t> line_mid, face_mid;  // refined lines / quads -> their midpoint vertex
 
   int nvc() const { return dim == 2 ? 4 : 8; }
   int mf_of(const std::map<EKey, int> &m, const EKey &k) const {
@@ -224,151 +237,508 @@ void orient(UMesh &m) {
       for (int v = 0; v < m.nvc(); v += 2) std::swap(cv[v], cv[v + 1]);
 }
 
-// ---- refinement (Triangulation::refine_global, deal.II 9.2 vertex placement)
-int refine_once(UMesh &m) {
+// ---- refinement (Triangulation::refine_global / execute_coarsening_and_refinement, deal.II 9.2
+// vertex placement)
+EKey face_key_v(int dim, const std::array<int64_t, 8> &cv, int d, int s) {
+  const auto fv = face_verts(dim, d, s);
+  return dim == 2 ? mkey({cv[fv[0]], cv[fv[1]]}) : mkey({cv[fv[0]], cv[fv[1]], cv[fv[2]], cv[fv[3]]});
+}
+
+// the level-0 records of the hierarchy (once, after the coarse mesh is complete)
+void init_tree(UMesh &m) {
+  if (!m.tree.empty()) return;
+  for (size_t c = 0; c < m.cells.size(); ++c) {
+    m.tree.push_back({m.cells[c], m.cell_mf[c], 0, -1, 0, -1});
+    m.roots.push_back((int64_t)c);
+  }
+  m.active = m.roots;
+}
+
+// active cells in depth-first order (children in lexicographic position order inside their parent):
+// after a global refinement, the children of active cell c are 2^dim c + child
+void sync_active(UMesh &m) {
+  m.active.clear();
+  std::vector<int64_t> st;
+  for (auto r = m.roots.rbegin(); r != m.roots.rend(); ++r) st.push_back(*r);
+  const int nch = 1 << m.dim;
+  while (!st.empty()) {
+    const int64_t id = st.back();
+    st.pop_back();
+    const auto &h = m.tree[(size_t)id];
+    if (h.child0 < 0) {
+      m.active.push_back(id);
+      continue;
+    }
+    for (int ch = nch - 1; ch >= 0; --ch) st.push_back(h.child0 + ch);
+  }
+  m.cells.resize(m.active.size());
+  m.cell_mf.resize(m.active.size());
+  for (size_t i = 0; i < m.active.size(); ++i) {
+    m.cells[i] = m.tree[(size_t)m.active[i]].v;
+    m.cell_mf[i] = m.tree[(size_t)m.active[i]].mf;
+  }
+}
+
+// split hierarchy cell `id` into 2^dim children: line midpoints on the line's manifold, quad / hex
+// centres from the TFI weights; children inherit manifold and boundary ids of the parent object
+// they lie in. Midpoints are shared through m.line_mid / m.face_mid across cells and adaptations.
+void refine_cell(UMesh &m, int64_t id) {
   const int dim = m.dim, nv = m.nvc(), nch = 1 << dim;
   const auto lines = local_lines(dim);
-  std::map<EKey, int64_t> line_mid, face_mid;
-  std::vector<std::array<int64_t, 8>> cells;
-  std::vector<int> cmf;
-  std::map<EKey, int> bface, lmf, fmf;
-  cells.reserve(m.cells.size() * nch);
-  for (size_t c = 0; c < m.cells.size(); ++c) {
-    const auto &cv = m.cells[c];
-    const int cellmf = m.cell_mf[c];
-    // lattice of 3^dim points: index (i, j, l) in {0,1,2}
-    int64_t lat[27];
-    auto L = [&](int i, int j, int l) -> int64_t & { return lat[i + 3 * (j + 3 * l)]; };
-    for (int v = 0; v < nv; ++v) L(2 * (v & 1), 2 * ((v >> 1) & 1), 2 * ((v >> 2) & 1)) = cv[v];
-    // line midpoints
-    std::vector<V3> lmid(lines.size());
+  const std::array<int64_t, 8> cv = m.tree[(size_t)id].v;
+  const int cellmf = m.tree[(size_t)id].mf;
+  // lattice of 3^dim points: index (i, j, l) in {0,1,2}
+  int64_t lat[27];
+  auto L = [&](int i, int j, int l) -> int64_t & { return lat[i + 3 * (j + 3 * l)]; };
+  for (int v = 0; v < nv; ++v) L(2 * (v & 1), 2 * ((v >> 1) & 1), 2 * ((v >> 2) & 1)) = cv[v];
+  // line midpoints
+  std::vector<V3> lmid(lines.size());
+  for (size_t li = 0; li < lines.size(); ++li) {
+    const int a = lines[li][0], b = lines[li][1];
+    const EKey k = mkey({cv[a], cv[b]});
+    auto it = m.line_mid.find(k);
+    int64_t vid;
+    if (it == m.line_mid.end()) {
+      const V3 p = new_point(m, m.mf_of(m.line_mf, k), {m.X[(size_t)cv[a]], m.X[(size_t)cv[b]]}, {0.5, 0.5});
+      vid = (int64_t)m.X.size();
+      m.X.push_back(p);
+      m.line_mid[k] = vid;
+    } else {
+      vid = it->second;
+    }
+    lmid[li] = m.X[(size_t)vid];
+    int q[3];  // lattice: coordinate 1 along the line's direction
+    for (int d = 0; d < 3; ++d) q[d] = ((a >> d) & 1) == ((b >> d) & 1) ? 2 * ((a >> d) & 1) : 1;
+    L(q[0], q[1], dim > 2 ? q[2] : 0) = vid;
+  }
+  auto quad_center = [&](int mfid, const std::array<int, 4> &fv) {  // TFI: vertices -1/4, lines +1/2
+    std::vector<V3> p;
+    std::vector<double> w;
+    for (int i = 0; i < 4; ++i) {
+      p.push_back(m.X[(size_t)cv[fv[i]]]);
+      w.push_back(-0.25);
+    }
     for (size_t li = 0; li < lines.size(); ++li) {
       const int a = lines[li][0], b = lines[li][1];
-      const EKey k = mkey({cv[a], cv[b]});
-      auto it = line_mid.find(k);
-      int64_t id;
-      if (it == line_mid.end()) {
-        const V3 p = new_point(m, m.mf_of(m.line_mf, k), {m.X[(size_t)cv[a]], m.X[(size_t)cv[b]]}, {0.5, 0.5});
-        id = (int64_t)m.X.size();
-        m.X.push_back(p);
-        line_mid[k] = id;
-      } else {
-        id = it->second;
+      if (std::find(fv.begin(), fv.end(), a) != fv.end() && std::find(fv.begin(), fv.end(), b) != fv.end()) {
+        p.push_back(lmid[li]);
+        w.push_back(0.5);
       }
-      lmid[li] = m.X[(size_t)id];
-      int q[3];  // lattice: coordinate 1 along the line's direction
-      for (int d = 0; d < 3; ++d) q[d] = ((a >> d) & 1) == ((b >> d) & 1) ? 2 * ((a >> d) & 1) : 1;
-        L(q[0], q[1], dim > 2 ? q[2] : 0) = id;
     }
-    auto quad_center = [&](int mfid, const std::array<int, 4> &fv) {  // TFI: vertices -1/4, lines +1/2
-      std::vector<V3> p;
-      std::vector<double> w;
-      for (int i = 0; i < 4; ++i) {
-        p.push_back(m.X[(size_t)cv[fv[i]]]);
-        w.push_back(-0.25);
-      }
-      for (size_t li = 0; li < lines.size(); ++li) {
-        const int a = lines[li][0], b = lines[li][1];
-        if (std::find(fv.begin(), fv.end(), a) != fv.end() && std::find(fv.begin(), fv.end(), b) != fv.end()) {
-          p.push_back(lmid[li]);
-          w.push_back(0.5);
-        }
-      }
-      return new_point(m, mfid, p, w);
-    };
+    return new_point(m, mfid, p, w);
+  };
+  if (dim == 3) {
     std::vector<V3> fmid;
-    if (dim == 3) {
-      for (int d = 0; d < 3; ++d)
-        for (int s = 0; s < 2; ++s) {
-          const EKey k = face_key(m, c, d, s);
-          auto it = face_mid.find(k);
-          int64_t id;
-          if (it == face_mid.end()) {
-            const V3 p = quad_center(m.mf_of(m.face_mf, k), face_verts(3, d, s));
-            id = (int64_t)m.X.size();
-            m.X.push_back(p);
-            face_mid[k] = id;
-          } else {
-            id = it->second;
-          }
-          fmid.push_back(m.X[(size_t)id]);
-          int q[3] = {1, 1, 1};
-          q[d] = 2 * s;
-          L(q[0], q[1], q[2]) = id;
-        }
-      // hex centre: TFI weights vertices +1/8, lines -1/4, faces +1/2
-      std::vector<V3> p;
-      std::vector<double> w;
-      for (int v = 0; v < 8; ++v) { p.push_back(m.X[(size_t)cv[v]]); w.push_back(0.125); }
-      for (auto &x : lmid) { p.push_back(x); w.push_back(-0.25); }
-      for (auto &x : fmid) { p.push_back(x); w.push_back(0.5); }
-      L(1, 1, 1) = (int64_t)m.X.size();
-      m.X.push_back(new_point(m, cellmf, p, w));
-    } else {
-      L(1, 1, 0) = (int64_t)m.X.size();
-      m.X.push_back(quad_center(cellmf, {0, 1, 2, 3}));
-    }
-    // children (parent-major, lexicographic child position)
-    for (int ch = 0; ch < nch; ++ch) {
-      const int cx = ch & 1, cy = (ch >> 1) & 1, cz = (ch >> 2) & 1;
-      std::array<int64_t, 8> nc{};
-      for (int v = 0; v < nv; ++v) nc[v] = L(cx + (v & 1), cy + ((v >> 1) & 1), dim == 3 ? cz + ((v >> 2) & 1) : 0);
-      cells.push_back(nc);
-      cmf.push_back(cellmf);
-      // manifold / boundary ids of the child's lines and faces: inherited from the parent object
-      // they lie in (parent line, parent face, or the parent cell's interior)
-      for (auto &ln : lines) {
-        int pa[3], pb[3];
-        for (int d = 0; d < 3; ++d) {
-          pa[d] = (d == 0 ? cx : d == 1 ? cy : cz) + ((ln[0] >> d) & 1);
-          pb[d] = (d == 0 ? cx : d == 1 ? cy : cz) + ((ln[1] >> d) & 1);
-        }
-        int dir = 0;
-        for (int d = 0; d < dim; ++d)
-          if (pa[d] != pb[d]) dir = d;
-        int nend = 0, ends[3], endd[3];
-        for (int d = 0; d < dim; ++d)
-          if (d != dir && (pa[d] == 0 || pa[d] == 2)) { ends[nend] = pa[d]; endd[nend++] = d; }
-        int mfv;
-        if (nend == dim - 1) {  // on a parent line
-          int va = 0, vb = 0;
-          for (int d = 0; d < dim; ++d)
-            if (d != dir) { va |= (pa[d] / 2) << d; vb |= (pa[d] / 2) << d; }
-          vb |= 1 << dir;
-          mfv = m.mf_of(m.line_mf, mkey({cv[va], cv[vb]}));
-        } else if (dim == 3 && nend == 1) {  // inside a parent face
-          mfv = m.mf_of(m.face_mf, face_key(m, c, endd[0], ends[0] / 2));
+    for (int d = 0; d < 3; ++d)
+      for (int s = 0; s < 2; ++s) {
+        const EKey k = face_key_v(3, cv, d, s);
+        auto it = m.face_mid.find(k);
+        int64_t vid;
+        if (it == m.face_mid.end()) {
+          const V3 p = quad_center(m.mf_of(m.face_mf, k), face_verts(3, d, s));
+          vid = (int64_t)m.X.size();
+          m.X.push_back(p);
+          m.face_mid[k] = vid;
         } else {
-          mfv = cellmf;
+          vid = it->second;
         }
-        if (mfv >= 0) lmf[mkey({nc[ln[0]], nc[ln[1]]})] = mfv;
+        fmid.push_back(m.X[(size_t)vid]);
+        int q[3] = {1, 1, 1};
+        q[d] = 2 * s;
+        L(q[0], q[1], q[2]) = vid;
       }
-      for (int d = 0; d < dim; ++d)
-        for (int s = 0; s < 2; ++s) {
-          const int pc = (d == 0 ? cx : d == 1 ? cy : cz) + s;  // parent-lattice coordinate of the face
-          const auto fv = face_verts(dim, d, s);
-          const EKey k = dim == 2 ? mkey({nc[fv[0]], nc[fv[1]]}) : mkey({nc[fv[0]], nc[fv[1]], nc[fv[2]], nc[fv[3]]});
-          if (pc == 0 || pc == 2) {
-            const EKey pk = face_key(m, c, d, pc / 2);
-            auto b = m.bface.find(pk);
-            if (b != m.bface.end()) bface[k] = b->second;
-            if (dim == 3) {
-              const int f = m.mf_of(m.face_mf, pk);
-              if (f >= 0) fmf[k] = f;
-            }
-          } else if (dim == 3 && cellmf >= 0) {
-            fmf[k] = cellmf;
-          }
-        }
-    }
+    // hex centre: TFI weights vertices +1/8, lines -1/4, faces +1/2
+    std::vector<V3> p;
+    std::vector<double> w;
+    for (int v = 0; v < 8; ++v) { p.push_back(m.X[(size_t)cv[v]]); w.push_back(0.125); }
+    for (auto &x : lmid) { p.push_back(x); w.push_back(-0.25); }
+    for (auto &x : fmid) { p.push_back(x); w.push_back(0.5); }
+    L(1, 1, 1) = (int64_t)m.X.size();
+    m.X.push_back(new_point(m, cellmf, p, w));
+  } else {
+    L(1, 1, 0) = (int64_t)m.X.size();
+    m.X.push_back(quad_center(cellmf, {0, 1, 2, 3}));
   }
-  m.cells.swap(cells);
-  m.cell_mf.swap(cmf);
-  m.bface.swap(bface);
-  m.line_mf.swap(lmf);
-  m.face_mf.swap(fmf);
+  // children (lexicographic child position)
+  const int64_t child0 = (int64_t)m.tree.size();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int cx = ch & 1, cy = (ch >> 1) & 1, cz = (ch >> 2) & 1;
+    std::array<int64_t, 8> nc{};
+    for (int v = 0; v < nv; ++v) nc[v] = L(cx + (v & 1), cy + ((v >> 1) & 1), dim == 3 ? cz + ((v >> 2) & 1) : 0);
+    m.tree.push_back({nc, cellmf, m.tree[(size_t)id].level + 1, id, ch, -1});
+    // manifold / boundary ids of the child's lines and faces: inherited from the parent object
+    // they lie in (parent line, parent face, or the parent cell's interior)
+    for (auto &ln : lines) {
+      int pa[3], pb[3];
+      for (int d = 0; d < 3; ++d) {
+        pa[d] = (d == 0 ? cx : d == 1 ? cy : cz) + ((ln[0] >> d) & 1);
+        pb[d] = (d == 0 ? cx : d == 1 ? cy : cz) + ((ln[1] >> d) & 1);
+      }
+      int dir = 0;
+      for (int d = 0; d < dim; ++d)
+        if (pa[d] != pb[d]) dir = d;
+      int nend = 0, ends[3], endd[3];
+      for (int d = 0; d < dim; ++d)
+        if (d != dir && (pa[d] == 0 || pa[d] == 2)) { ends[nend] = pa[d]; endd[nend++] = d; }
+      int mfv;
+      if (nend == dim - 1) {  // on a parent line
+        int va = 0, vb = 0;
+        for (int d = 0; d < dim; ++d)
+          if (d != dir) { va |= (pa[d] / 2) << d; vb |= (pa[d] / 2) << d; }
+        vb |= 1 << dir;
+        mfv = m.mf_of(m.line_mf, mkey({cv[va], cv[vb]}));
+      } else if (dim == 3 && nend == 1) {  // inside a parent face
+        mfv = m.mf_of(m.face_mf, face_key_v(3, cv, endd[0], ends[0] / 2));
+      } else {
+        mfv = cellmf;
+      }
+      if (mfv >= 0) m.line_mf[mkey({nc[ln[0]], nc[ln[1]]})] = mfv;
+    }
+    for (int d = 0; d < dim; ++d)
+      for (int s = 0; s < 2; ++s) {
+        const int pc = (d == 0 ? cx : d == 1 ? cy : cz) + s;  // parent-lattice coordinate of the face
+        const EKey k = face_key_v(dim, nc, d, s);
+        if (pc == 0 || pc == 2) {
+          const EKey pk = face_key_v(dim, cv, d, pc / 2);
+          auto b = m.bface.find(pk);
+          if (b != m.bface.end()) m.bface[k] = b->second;
+          if (dim == 3) {
+            const int f = m.mf_of(m.face_mf, pk);
+            if (f >= 0) m.face_mf[k] = f;
+          }
+        } else if (dim == 3 && cellmf >= 0) {
+          m.face_mf[k] = cellmf;
+        }
+      }
+  }
+  m.tree[(size_t)id].child0 = child0;
+}
+
+// refine_global(1): every active cell. Object maps keep the entries of the parent objects (keys are
+// vertex sets, so an object of any level keeps its own boundary / manifold id).
+int refine_once(UMesh &m) {
+  init_tree(m);
+  const std::vector<int64_t> act = m.active;
+  for (int64_t id : act) refine_cell(m, id);
+  sync_active(m);
   return GLS_OK;
 }
+
+// ---- local adaptation of the hierarchy (the reference's p::d::Triangulation with
+// smoothing_on_refinement | smoothing_on_coarsening, navier_stokes_base.cc:55-60, 592-780)
+
+// highest active level at every vertex
+std::vector<int> vertex_levels(const UMesh &m) {
+  std::vector<int> vl(m.X.size(), -1);
+  for (int64_t id : m.active) {
+    const auto &h = m.tree[(size_t)id];
+    for (int v = 0; v < m.nvc(); ++v) vl[(size_t)h.v[v]] = std::max(vl[(size_t)h.v[v]], h.level);
+  }
+  return vl;
+}
+
+// 2:1 balance over vertices (p4est corner balance): refine every active cell that shares a vertex
+// with an active cell two or more levels finer, until none does
+void balance(UMesh &m) {
+  for (int it = 0; it < 64; ++it) {
+    const std::vector<int> vl = vertex_levels(m);
+    std::vector<int64_t> todo;
+    for (int64_t id : m.active) {
+      const auto &h = m.tree[(size_t)id];
+      for (int v = 0; v < m.nvc(); ++v)
+        if (vl[(size_t)h.v[v]] >= h.level + 2) { todo.push_back(id); break; }
+    }
+    if (todo.empty()) return;
+    for (int64_t id : todo) refine_cell(m, id);
+    sync_active(m);
+  }
+}
+
+// the vertices on the closed boundary of hierarchy cell `id` at its children's resolution: corners,
+// line midpoints and (3D) face centres that exist
+std::vector<int64_t> boundary_half_lattice(const UMesh &m, int64_t id) {
+  const auto &h = m.tree[(size_t)id];
+  std::vector<int64_t> out(h.v.begin(), h.v.begin() + m.nvc());
+  for (auto &ln : local_lines(m.dim)) {
+    auto it = m.line_mid.find(mkey({h.v[ln[0]], h.v[ln[1]]}));
+    if (it != m.line_mid.end()) out.push_back(it->second);
+  }
+  if (m.dim == 3)
+    for (int d = 0; d < 3; ++d)
+      for (int s = 0; s < 2; ++s) {
+        auto it = m.face_mid.find(face_key_v(3, h.v, d, s));
+        if (it != m.face_mid.end()) out.push_back(it->second);
+      }
+  return out;
+}
+
+// execute_coarsening_and_refinement: flagged active cells are refined, complete sibling families
+// whose members are all flagged for coarsening (none for refinement) are coarsened unless a cell
+// two levels finer than the parent touches its boundary after the refinement and balance pass;
+// then the vertex balance is restored by refinement
+int adapt(UMesh &m, const int32_t *ref, const int32_t *crs) {
+  init_tree(m);
+  const size_t na = m.active.size();
+  const int nch = 1 << m.dim;
+  std::map<int64_t, int> fam;  // parent -> flagged children
+  for (size_t i = 0; i < na; ++i) {
+    const auto &h = m.tree[(size_t)m.active[i]];
+    if (crs && crs[i] && !(ref && ref[i]) && h.parent >= 0) ++fam[h.parent];
+  }
+  const std::vector<int64_t> act = m.active;
+  for (size_t i = 0; i < na; ++i)
+    if (ref && ref[i]) refine_cell(m, act[i]);
+  sync_active(m);
+  balance(m);
+  const std::vector<int> vl = vertex_levels(m);
+  std::vector<int64_t> drop;
+  for (auto &kv : fam) {
+    if (kv.second != nch) continue;
+    const auto &p = m.tree[(size_t)kv.first];
+    bool ok = true;
+    for (int ch = 0; ch < nch && ok; ++ch) ok = m.tree[(size_t)(p.child0 + ch)].child0 < 0;
+    for (int64_t v : boundary_half_lattice(m, kv.first)) ok = ok && vl[(size_t)v] <= p.level + 1;
+    if (ok) drop.push_back(kv.first);
+  }
+  for (int64_t id : drop) m.tree[(size_t)id].child0 = -1;
+  sync_active(m);
+  balance(m);
+  return GLS_OK;
+}
+
+// Triangulation::prepare_coarsening_and_refinement (deal.II 9.2 source/grid/tria.cc, third party,
+// not vendored: restated from its published algorithm) with the reference's MeshSmoothing
+// smoothing_on_refinement | smoothing_on_coarsening (navier_stokes_base.cc:55-60, called at :682),
+// on the unstructured hierarchy. The same steps as gls_octree_prepare (gls_octree.cpp), with
+// neighbours found through shared face vertex sets instead of a lattice: cells on each level in
+// hierarchy order (coarse cells, then children of the previous level's refined cells), active cells
+// visited in reverse; isotropic refinement only.
+struct USmoother {
+  const UMesh &m;
+  int dim;
+  std::vector<char> ref, crs;                   // per active cell
+  std::unordered_map<int64_t, int64_t> leaf;    // hierarchy id -> active index
+  std::vector<int64_t> all;                     // live cells, level by level
+  std::vector<int64_t> active_rev;              // active indices, reverse level order
+  std::map<EKey, std::vector<int64_t>> faces;   // face vertex set -> live cells having that face
+  std::unordered_map<int64_t, char> user;       // refined cells to be coarsened (fix_coarsen_flags)
+
+  USmoother(const UMesh &mesh, const int32_t *r, const int32_t *c) : m(mesh), dim(mesh.dim) {
+    const size_t na = m.active.size();
+    ref.resize(na);
+    crs.resize(na);
+    for (size_t i = 0; i < na; ++i) {
+      ref[i] = r[i] != 0;
+      crs[i] = c[i] != 0;
+      leaf[m.active[i]] = (int64_t)i;
+    }
+    std::vector<int64_t> lev = m.roots;
+    while (!lev.empty()) {
+      std::vector<int64_t> next;
+      for (int64_t id : lev) {
+        all.push_back(id);
+        const auto &h = m.tree[(size_t)id];
+        for (int d = 0; d < dim; ++d)
+          for (int s = 0; s < 2; ++s) faces[face_key_v(dim, h.v, d, s)].push_back(id);
+        if (h.child0 >= 0)
+          for (int ch = 0; ch < (1 << dim); ++ch) next.push_back(h.child0 + ch);
+      }
+      lev.swap(next);
+    }
+    for (size_t j = all.size(); j-- > 0;) {
+      auto it = leaf.find(all[j]);
+      if (it != leaf.end()) active_rev.push_back(it->second);
+    }
+  }
+  bool is_active(int64_t id) const { return m.tree[(size_t)id].child0 < 0; }
+  int64_t kid(int64_t id, int ch) const { return m.tree[(size_t)id].child0 + ch; }
+  int nkids() const { return 1 << dim; }
+  // cell->neighbor(f): the live cell of the same level across face f (active or refined), else the
+  // coarser active cell; returns 0 at the boundary, 1 same level, 2 coarser
+  int neighbor(int64_t id, int f, int64_t &nb) const {
+    const auto &h = m.tree[(size_t)id];
+    const int d = f / 2, s = f & 1;
+    auto it = faces.find(face_key_v(dim, h.v, d, s));
+    if (it != faces.end())
+      for (int64_t o : it->second)
+        if (o != id) { nb = o; return 1; }
+    if (h.parent < 0 || ((h.pos >> d) & 1) != s) return 0;  // boundary (a child's inner face is shared)
+    int64_t pn;
+    if (neighbor(h.parent, f, pn) != 1) return 0;
+    nb = pn;
+    return 2;
+  }
+  bool will_be_coarsened(int64_t id) {
+    if (is_active(id)) return false;
+    int n = 0;
+    for (int ch = 0; ch < nkids(); ++ch) {
+      auto it = leaf.find(kid(id, ch));
+      if (it != leaf.end() && crs[(size_t)it->second]) ++n;
+    }
+    if (n == nkids()) return true;
+    for (int ch = 0; ch < nkids(); ++ch) {
+      auto it = leaf.find(kid(id, ch));
+      if (it != leaf.end()) crs[(size_t)it->second] = 0;
+    }
+    return false;
+  }
+  bool face_refined_by_neighbor(int64_t id, int f) {
+    int64_t nb;
+    if (neighbor(id, f, nb) != 1) return false;
+    if (!is_active(nb)) return !will_be_coarsened(nb);
+    return ref[(size_t)leaf.at(nb)] != 0;
+  }
+  void limit_vertex_levels() {
+    std::unordered_map<int64_t, int> vl;
+    const int nv = m.nvc();
+    for (size_t i = 0; i < m.active.size(); ++i) {
+      const auto &h = m.tree[(size_t)m.active[i]];
+      const int lev = ref[i] ? h.level + 1 : crs[i] ? h.level - 1 : h.level;
+      for (int v = 0; v < nv; ++v) {
+        auto it = vl.find(h.v[v]);
+        if (it == vl.end()) vl[h.v[v]] = std::max(0, lev);
+        else it->second = std::max(it->second, lev);
+      }
+    }
+    for (int64_t i : active_rev) {
+      if (ref[(size_t)i]) continue;
+      const auto &h = m.tree[(size_t)m.active[(size_t)i]];
+      for (int v = 0; v < nv; ++v) {
+        const int lv = vl[h.v[v]];
+        if (lv < h.level + 1) continue;
+        crs[(size_t)i] = 0;
+        if (lv > h.level + 1) {
+          ref[(size_t)i] = 1;
+          for (int w = 0; w < nv; ++w) vl[h.v[w]] = std::max(vl[h.v[w]], h.level + 1);
+        }
+      }
+    }
+  }
+  bool coarsening_allowed(int64_t p) const {
+    for (int f = 0; f < 2 * dim; ++f) {
+      int64_t nb;
+      if (neighbor(p, f, nb) == 0) continue;
+      const int d = f / 2;
+      for (int ch = 0; ch < nkids(); ++ch) {
+        if (((ch >> d) & 1) != (f & 1)) continue;  // child not on face f
+        int64_t cn;
+        if (neighbor(kid(p, ch), f, cn) != 1) continue;
+        if (!is_active(cn) && !user.count(cn)) return false;
+        if (is_active(cn) && ref[(size_t)leaf.at(cn)]) return false;
+      }
+    }
+    return true;
+  }
+  void fix_coarsen_flags() {
+    for (int it = 0; it < 1000; ++it) {
+      const std::vector<char> before = crs;
+      limit_vertex_levels();
+      for (size_t i = 0; i < m.active.size(); ++i)
+        if (m.tree[(size_t)m.active[i]].level == 0) crs[i] = 0;
+      user.clear();
+      for (int64_t c : all) {
+        if (is_active(c)) continue;
+        int n = 0;
+        for (int ch = 0; ch < nkids(); ++ch) {
+          auto lt = leaf.find(kid(c, ch));
+          if (lt != leaf.end() && crs[(size_t)lt->second]) {
+            ++n;
+            crs[(size_t)lt->second] = 0;
+          }
+        }
+        if (n == nkids()) user[c] = 1;
+      }
+      for (size_t j = all.size(); j-- > 0;) {
+        const int64_t c = all[j];
+        if (!user.count(c) || !coarsening_allowed(c)) continue;
+        for (int ch = 0; ch < nkids(); ++ch) crs[(size_t)leaf.at(kid(c, ch))] = 1;
+      }
+      user.clear();
+      if (crs == before) break;
+    }
+  }
+  int run() {
+    const int nf = 2 * dim;
+    int loops = 0;
+    while (loops < 1000) {
+      ++loops;
+      const std::vector<char> r0 = ref, c0 = crs;
+      // step 1: do_not_produce_unrefined_islands
+      for (int64_t c : all) {
+        if (is_active(c) || !will_be_coarsened(c)) continue;
+        int n_nb = 0, cnt = 0;
+        for (int f = 0; f < nf; ++f) {
+          int64_t nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          ++n_nb;
+          if (face_refined_by_neighbor(c, f)) ++cnt;
+        }
+        if (cnt == n_nb || (cnt == n_nb - 1 && n_nb == nf))
+          for (int ch = 0; ch < nkids(); ++ch) crs[(size_t)leaf.at(kid(c, ch))] = 0;
+      }
+      // step 2: eliminate_refined_inner_islands | eliminate_refined_boundary_islands
+      for (int64_t c : all) {
+        const bool act = is_active(c);
+        if (act && !ref[(size_t)leaf.at(c)]) continue;
+        bool all_active = true;
+        if (!act)
+          for (int ch = 0; ch < nkids(); ++ch) all_active = all_active && is_active(kid(c, ch));
+        if (!all_active) continue;
+        int total = 0, unrefined = 0;
+        for (int f = 0; f < nf; ++f) {
+          int64_t nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          ++total;
+          if (!face_refined_by_neighbor(c, f)) ++unrefined;
+        }
+        if (unrefined != total || total == 0) continue;
+        if (!act) {
+          for (int ch = 0; ch < nkids(); ++ch) {
+            const size_t k = (size_t)leaf.at(kid(c, ch));
+            ref[k] = 0;
+            crs[k] = 1;
+          }
+        } else {
+          ref[(size_t)leaf.at(c)] = 0;
+        }
+      }
+      // step 3
+      limit_vertex_levels();
+      // step 4: eliminate_unrefined_islands
+      for (int64_t i : active_rev) {
+        if (ref[(size_t)i]) continue;
+        const int64_t c = m.active[(size_t)i];
+        int refined = 0, unrefined = 0;
+        for (int f = 0; f < nf; ++f) {
+          int64_t nb;
+          if (neighbor(c, f, nb) == 0) continue;
+          if (face_refined_by_neighbor(c, f)) ++refined;
+          else ++unrefined;
+        }
+        if (unrefined < refined) {
+          crs[(size_t)i] = 0;
+          ref[(size_t)i] = 1;
+        }
+      }
+      // step 6: no double refinement at a face
+      for (int64_t i : active_rev) {
+        if (!ref[(size_t)i]) continue;
+        const int64_t c = m.active[(size_t)i];
+        for (int f = 0; f < nf; ++f) {
+          int64_t nb;
+          if (neighbor(c, f, nb) != 2) continue;
+          const size_t j = (size_t)leaf.at(nb);
+          crs[j] = 0;
+          ref[j] = 1;
+        }
+      }
+      // step 8
+      fix_coarsen_flags();
+      if (ref == r0 && crs == c0) break;
+    }
+    return loops;
+  }
+};
 
 // ---- generators (GridGenerator::*, deal.II 9.2 geometry and boundary ids)
 std::vector<std::string> split(const std::string &s, char sep) {
@@ -746,10 +1116,163 @@ int read_gmsh(UMesh &m, const std::string &path) {
 // ---- FE space (FE_Q(k) x dim + FE_Q(kp)) on the mesh, k <= 2
 struct FESpaceImpl {
   gls_fe_space pub{};
-  std::vector<int32_t> cell_vnodes, cell_pnodes, cell_mapping;
+  std::vector<int32_t> cell_vnodes, cell_pnodes, cell_mapping, cell_level;
   std::vector<double> vnode_x, pnode_x, cell_support, cell_measure;
   std::vector<uint32_t> vnode_bid, pnode_bid;
+  // hanging lines (node level, chains closed): node = sum_j w_j master_j
+  std::vector<int64_t> vh_node, vh_off, vh_master, ph_node, ph_off, ph_master;
+  std::vector<double> vh_w, ph_w;
+  // hierarchy snapshot for SolutionTransfer: hierarchy id of every active cell, and per record its
+  // parent, child position and first child
+  std::vector<int64_t> hid, t_parent, t_child0;
+  std::vector<int> t_pos;
+  std::vector<std::array<int64_t, 8>> cell_verts, t_verts;  // vertex ids of the active cells / all records
+  std::vector<V3> verts;
+  std::map<EKey, int64_t> line_mid, face_mid;
 };
+
+using HangLines = std::map<int64_t, std::vector<std::pair<int64_t, double>>>;
+double lag1(int k, int a, double x);
+
+// DoFTools::make_hanging_node_constraints (gls_navier_stokes.cc:84, 143) for FE_Q(kk) on the
+// hierarchy: every line (3D: and quad) of an active cell that is refined in the active mesh (its
+// midpoint vertex is a node) carries the nodes of the refined object (midpoint vertex, child lines,
+// child quads); each is constrained to the active cell's Qk interpolant on that object, evaluated
+// at the node's reference position (2kk+1 positions per direction on the refined object). `ids`
+// maps object keys (vertex {-3, v}, line / quad = sorted vertex ids) to node ids; cn = the active
+// cells' node lists. Chains are closed afterwards (AffineConstraints::close).
+int hanging_lines(const UMesh &m, int kk, const std::map<EKey, int64_t> &ids, const std::vector<int32_t> &cn,
+                  HangLines &out) {
+  const int dim = m.dim, kk1 = kk + 1, nn = dim == 2 ? kk1 * kk1 : kk1 * kk1 * kk1, P = 2 * kk;
+  auto vnode = [&](int64_t v) -> int64_t {
+    auto it = ids.find(EKey{{-3, v, -1, -1}});
+    return it == ids.end() ? -1 : it->second;
+  };
+  auto onode = [&](const EKey &k) -> int64_t {
+    auto it = ids.find(k);
+    return it == ids.end() ? -1 : it->second;
+  };
+  auto mid = [&](const std::map<EKey, int64_t> &mp, const EKey &k) -> int64_t {
+    auto it = mp.find(k);
+    return it == mp.end() ? -1 : it->second;
+  };
+  auto local = [&](const int *ia) {
+    return ia[0] + kk1 * (ia[1] + (dim == 3 ? kk1 * ia[2] : 0));
+  };
+  for (size_t c = 0; c < m.cells.size(); ++c) {
+    const auto &cv = m.cells[c];
+    // lines
+    for (auto &ln : local_lines(dim)) {
+      const int la = ln[0], lb = ln[1];
+      int dir = 0;
+      for (int d = 0; d < dim; ++d)
+        if (((la ^ lb) >> d) & 1) dir = d;
+      const int64_t mv = mid(m.line_mid, mkey({cv[la], cv[lb]}));
+      if (mv < 0 || vnode(mv) < 0) continue;
+      const int64_t V[3] = {cv[la], mv, cv[lb]};
+      int64_t kn[4];
+      for (int j = 0; j <= kk; ++j) {
+        int ia[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) ia[d] = d == dir ? j : kk * ((la >> d) & 1);
+        kn[j] = cn[c * nn + (size_t)local(ia)];
+      }
+      for (int p = 0; p <= P; ++p) {
+        const int64_t fn = p % kk == 0 ? vnode(V[p / kk]) : onode(mkey({V[p / kk], V[p / kk + 1]}));
+        if (fn < 0 || out.count(fn)) continue;
+        bool own = false;
+        for (int j = 0; j <= kk; ++j) own = own || kn[j] == fn;
+        if (own) continue;
+        std::vector<std::pair<int64_t, double>> line;
+        for (int j = 0; j <= kk; ++j) {
+          const double w = lag1(kk, j, (double)p / P);
+          if (std::fabs(w) > 1e-13) line.push_back({kn[j], w});
+        }
+        out[fn] = line;
+      }
+    }
+    if (dim != 3) continue;
+    // quads
+    for (int d = 0; d < 3; ++d)
+      for (int s = 0; s < 2; ++s) {
+        const int64_t fv = mid(m.face_mid, face_key_v(3, cv, d, s));
+        if (fv < 0 || vnode(fv) < 0) continue;
+        int t[2], nt = 0;
+        for (int e = 0; e < 3; ++e)
+          if (e != d) t[nt++] = e;
+        int64_t C[2][2];
+        for (int iu = 0; iu < 2; ++iu)
+          for (int iv = 0; iv < 2; ++iv) C[iu][iv] = cv[(s << d) | (iu << t[0]) | (iv << t[1])];
+        int64_t V[3][3];
+        V[1][1] = fv;
+        bool ok = true;
+        for (int i = 0; i < 2; ++i) {
+          V[2 * i][0] = C[i][0];
+          V[2 * i][2] = C[i][1];
+          V[0][2 * i] = C[0][i];
+          V[2][2 * i] = C[1][i];
+          V[1][2 * i] = mid(m.line_mid, mkey({C[0][i], C[1][i]}));
+          V[2 * i][1] = mid(m.line_mid, mkey({C[i][0], C[i][1]}));
+          ok = ok && V[1][2 * i] >= 0 && V[2 * i][1] >= 0;
+        }
+        if (!ok) return gls_io_set_error(GLS_EINVAL, "hanging nodes: refined quad without refined lines");
+        std::vector<int64_t> kn;
+        for (int jv = 0; jv <= kk; ++jv)
+          for (int ju = 0; ju <= kk; ++ju) {
+            int ia[3];
+            ia[d] = s * kk;
+            ia[t[0]] = ju;
+            ia[t[1]] = jv;
+            kn.push_back(cn[c * nn + (size_t)local(ia)]);
+          }
+        for (int pv = 0; pv <= P; ++pv)
+          for (int pu = 0; pu <= P; ++pu) {
+            const int eu = pu / kk, ev = pv / kk;
+            const bool ou = pu % kk != 0, ov = pv % kk != 0;
+            int64_t fn;
+            if (!ou && !ov) fn = vnode(V[eu][ev]);
+            else if (ou && !ov) fn = onode(mkey({V[eu][ev], V[eu + 1][ev]}));
+            else if (!ou && ov) fn = onode(mkey({V[eu][ev], V[eu][ev + 1]}));
+            else fn = onode(mkey({V[eu][ev], V[eu + 1][ev], V[eu][ev + 1], V[eu + 1][ev + 1]}));
+            if (fn < 0 || out.count(fn)) continue;
+            bool own = false;
+            for (int64_t x : kn) own = own || x == fn;
+            if (own) continue;
+            std::vector<std::pair<int64_t, double>> line;
+            for (int jv = 0; jv <= kk; ++jv)
+              for (int ju = 0; ju <= kk; ++ju) {
+                const double w = lag1(kk, ju, (double)pu / P) * lag1(kk, jv, (double)pv / P);
+                if (std::fabs(w) > 1e-13) line.push_back({kn[(size_t)(ju + kk1 * jv)], w});
+              }
+            out[fn] = line;
+          }
+      }
+  }
+  // close the chains: substitute constrained masters by their lines
+  for (int pass = 0; pass < 32; ++pass) {
+    bool changed = false;
+    for (auto &kv : out) {
+      std::map<int64_t, double> acc;
+      bool sub = false;
+      for (auto &mw : kv.second) {
+        auto it = out.find(mw.first);
+        if (it == out.end()) {
+          acc[mw.first] += mw.second;
+        } else {
+          sub = true;
+          for (auto &m2 : it->second) acc[m2.first] += mw.second * m2.second;
+        }
+      }
+      if (sub) {
+        kv.second.clear();
+        for (auto &a : acc)
+          if (std::fabs(a.second) > 1e-14) kv.second.push_back(a);
+        changed = true;
+      }
+    }
+    if (!changed) return GLS_OK;
+  }
+  return gls_io_set_error(GLS_EINVAL, "hanging-node chains do not close");
+}
 
 double lag1(int k, int a, double x) {  // Lagrange basis a of degree k on equidistant nodes (k <= 2)
   double v = 1.0;
@@ -886,7 +1409,9 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
       for (int d = 0; d < dim; ++d) F.cell_support[((size_t)c * nl + a) * dim + d] = S[(size_t)a][d];
   }
   // node numbering: one node per vertex / line / face / cell interior touched by the lattice
-  auto number = [&](int kk, std::vector<int32_t> &cn, std::vector<double> &nx, std::vector<uint32_t> &nb) -> int {
+  auto number = [&](int kk, std::vector<int32_t> &cn, std::vector<double> &nx, std::vector<uint32_t> &nb,
+                    std::vector<int64_t> &hnode, std::vector<int64_t> &hoff, std::vector<int64_t> &hmaster,
+                    std::vector<double> &hw) -> int {
     const int kk1 = kk + 1, nn = dim == 2 ? kk1 * kk1 : kk1 * kk1 * kk1;
     std::map<EKey, int64_t> ids;  // entity key (with a type tag in v[3] for vertices/cells) -> node
     cn.assign((size_t)(nc * nn), -1);
@@ -941,6 +1466,9 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
         }
       }
     }
+    HangLines hang;
+    if (int rc = hanging_lines(m, kk, ids, cn, hang); rc != GLS_OK) return rc;
+    if (!hang.empty() && nper > 0) return gls_io_set_error(GLS_EINVAL, "periodic boundaries on locally refined meshes are not supported");
     // boundary id bits
     std::vector<uint32_t> bits(pos.size(), 0u);
     for (int64_t c = 0; c < nc; ++c)
@@ -1000,19 +1528,53 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
       nb[(size_t)t] |= bits[i];
     }
     for (auto &x : cn) x = (int32_t)compact[(size_t)rep[(size_t)x]];
+    hnode.clear();
+    hoff.assign(1, 0);
+    hmaster.clear();
+    hw.clear();
+    for (auto &kv : hang) {  // (no periodic identification here: ids are compact already)
+      hnode.push_back(compact[(size_t)kv.first]);
+      for (auto &mw : kv.second) {
+        hmaster.push_back(compact[(size_t)mw.first]);
+        hw.push_back(mw.second);
+      }
+      hoff.push_back((int64_t)hmaster.size());
+    }
     if (n > INT32_MAX) return gls_io_set_error(GLS_EINVAL, "too many nodes for int32 ids");
     return GLS_OK;
   };
-  int rc = number(k, F.cell_vnodes, F.vnode_x, F.vnode_bid);
+  int rc = number(k, F.cell_vnodes, F.vnode_x, F.vnode_bid, F.vh_node, F.vh_off, F.vh_master, F.vh_w);
   if (rc) return rc;
   if (kp == k) {
     F.cell_pnodes = F.cell_vnodes;
     F.pnode_x = F.vnode_x;
     F.pnode_bid = F.vnode_bid;
+    F.ph_node = F.vh_node;
+    F.ph_off = F.vh_off;
+    F.ph_master = F.vh_master;
+    F.ph_w = F.vh_w;
   } else {
-    rc = number(kp, F.cell_pnodes, F.pnode_x, F.pnode_bid);
+    rc = number(kp, F.cell_pnodes, F.pnode_x, F.pnode_bid, F.ph_node, F.ph_off, F.ph_master, F.ph_w);
     if (rc) return rc;
   }
+  // hierarchy snapshot (levels, ids, topology for transfers and Kelly faces)
+  F.cell_level.resize((size_t)nc);
+  F.hid.resize((size_t)nc);
+  for (int64_t c = 0; c < nc; ++c) {
+    const int64_t h = m.tree.empty() ? c : m.active[(size_t)c];
+    F.hid[(size_t)c] = h;
+    F.cell_level[(size_t)c] = m.tree.empty() ? 0 : m.tree[(size_t)h].level;
+  }
+  for (const auto &h : m.tree) {
+    F.t_parent.push_back(h.parent);
+    F.t_child0.push_back(h.child0);
+    F.t_pos.push_back(h.pos);
+  }
+  F.cell_verts = m.cells;
+  for (const auto &h : m.tree) F.t_verts.push_back(h.v);
+  F.verts = m.X;
+  F.line_mid = m.line_mid;
+  F.face_mid = m.face_mid;
   auto &P = F.pub;
   P.dim = dim;
   P.k = k;
@@ -1030,10 +1592,95 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
   P.cell_mapping = F.cell_mapping.data();
   P.cell_measure = F.cell_measure.data();
   P.volume = volume;
+  P.cell_level = F.cell_level.data();
+  P.n_vhang = (int64_t)F.vh_node.size();
+  P.vhang_node = F.vh_node.data();
+  P.vhang_off = F.vh_off.data();
+  P.vhang_master = F.vh_master.data();
+  P.vhang_w = F.vh_w.data();
+  P.n_phang = (int64_t)F.ph_node.size();
+  P.phang_node = F.ph_node.data();
+  P.phang_off = F.ph_off.data();
+  P.phang_master = F.ph_master.data();
+  P.phang_w = F.ph_w.data();
   P.impl_ = &F;
   return GLS_OK;
 }
 
+}  // namespace
+
+// ---- Kelly face-piece geometry helpers (gls_fe_space_kelly_faces)
+namespace {
+void gauss01(int n, double *x, double *w) {
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), dp = 1.0;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = 0.0;
+      for (int j = 1; j <= n; ++j) {
+        const double p2 = p1;
+        p1 = p0;
+        p0 = ((2.0 * j - 1.0) * z * p1 - (j - 1.0) * p2) / j;
+      }
+      dp = n * (z * p0 - p1) / (z * z - 1.0);
+      const double dz = p0 / dp;
+      z -= dz;
+      if (std::fabs(dz) < 1e-16) break;
+    }
+    x[n - 1 - i] = 0.5 * (1.0 + z);
+    w[n - 1 - i] = 1.0 / ((1.0 - z * z) * dp * dp);
+  }
+}
+void lagd1(int k, int a, double x, double &v, double &dv) {  // equidistant Lagrange basis and derivative
+  v = 1.0;
+  dv = 0.0;
+  for (int b = 0; b <= k; ++b) {
+    if (b == a) continue;
+    const double inv = 1.0 / ((double)(a - b) / k);
+    dv = dv * (x - (double)b / k) * inv + v * inv;
+    v *= (x - (double)b / k) * inv;
+  }
+}
+// J[i][a] = d x_i / d xi_a of the cell's MappingQ (support points at the FE_Q(k) lattice)
+void jacobian(const gls_fe_space &S, int64_t c, const double *xi, double J[3][3]) {
+  const int dim = S.dim, k = S.k, k1 = k + 1, nl = dim == 2 ? k1 * k1 : k1 * k1 * k1;
+  double v[3][4], dv[3][4];
+  for (int d = 0; d < dim; ++d)
+    for (int a = 0; a <= k; ++a) lagd1(k, a, xi[d], v[d][a], dv[d][a]);
+  for (int i = 0; i < 3; ++i)
+    for (int a = 0; a < 3; ++a) J[i][a] = (i == a && i >= dim) ? 1.0 : 0.0;
+  for (int b = 0; b < nl; ++b) {
+    const int ib[3] = {b % k1, (b / k1) % k1, b / (k1 * k1)};
+    const double *x = S.cell_support + ((size_t)c * nl + b) * dim;
+    for (int a = 0; a < dim; ++a) {
+      double t = dv[a][ib[a]];
+      for (int o = 0; o < dim; ++o)
+        if (o != a) t *= v[o][ib[o]];
+      for (int i = 0; i < dim; ++i) J[i][a] += t * x[i];
+    }
+  }
+}
+// y = J^-1 r
+void solve3(const double J[3][3], const double *r, double *y, int dim) {
+  if (dim == 2) {
+    const double det = J[0][0] * J[1][1] - J[0][1] * J[1][0];
+    y[0] = (J[1][1] * r[0] - J[0][1] * r[1]) / det;
+    y[1] = (-J[1][0] * r[0] + J[0][0] * r[1]) / det;
+    return;
+  }
+  const double det = J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+                     J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+  double inv[3][3];
+  inv[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / det;
+  inv[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / det;
+  inv[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / det;
+  inv[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / det;
+  inv[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / det;
+  inv[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / det;
+  inv[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / det;
+  inv[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / det;
+  inv[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / det;
+  for (int i = 0; i < 3; ++i) y[i] = inv[i][0] * r[0] + inv[i][1] * r[1] + inv[i][2] * r[2];
+}
 }  // namespace
 
 struct gls_umesh {
@@ -1052,6 +1699,7 @@ int gls_umesh_generate(int dim, const char *grid_type, const char *grid_argument
     delete g;
     return rc;
   }
+  init_tree(g->m);
   *out = g;
   return GLS_OK;
 }
@@ -1066,6 +1714,7 @@ int gls_umesh_read_gmsh(int dim, const char *path, gls_umesh **out) {
     delete g;
     return rc;
   }
+  init_tree(g->m);
   *out = g;
   return GLS_OK;
 }
@@ -1152,42 +1801,251 @@ int gls_fe_space_destroy(gls_fe_space *s) {
   return GLS_OK;
 }
 
-// SolutionTransfer::interpolate for one global refinement (navier_stokes_base.cc:737-780): fine
-// cell f is child (f & (2^dim - 1)) of coarse cell f >> dim; each fine node takes the coarse cell's
-// Qk / Qkp interpolant at its reference position in the parent (Qk on the children contains the
-// parent's Qk space, so this is exact)
+// SolutionTransfer::interpolate (navier_stokes_base.cc:689-780) between two FE spaces of the same
+// triangulation (refinement, coarsening, any number of levels). Every new active cell is found in
+// the old mesh through the hierarchy: unchanged (nodal copy), a descendant of an old active cell
+// (the old cell's Qk / Qkp interpolant at the node's reference position in it, exact because Qk on
+// children contains the parent's Qk), or an ancestor of old active cells (each node evaluated in the
+// old descendant that contains its reference position: FE_Q restriction is interpolation).
 int gls_fe_space_transfer(const gls_fe_space *co, const gls_fe_space *fi, const double *cvec, double *fvec) {
-  if (!co || !fi || !cvec || !fvec || co->dim != fi->dim || co->k != fi->k || co->kp != fi->kp ||
-      fi->n_cells != co->n_cells << co->dim)
-    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_transfer: the fine space must be one global refinement of the coarse");
+  if (!co || !fi || !cvec || !fvec || co->dim != fi->dim || co->k != fi->k || co->kp != fi->kp)
+    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_transfer: spaces of different dimension / degree");
+  if (!co->impl_ || !fi->impl_) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_transfer: spaces from gls_umesh_fe_space required");
+  const FESpaceImpl &O = *static_cast<const FESpaceImpl *>(co->impl_);
+  const FESpaceImpl &N = *static_cast<const FESpaceImpl *>(fi->impl_);
+  if (O.t_parent.size() > N.t_parent.size())
+    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_transfer: the new space must come from the same (later) triangulation");
   const int dim = co->dim;
+  std::unordered_map<int64_t, int64_t> old_of;  // hierarchy id -> old active cell
+  for (int64_t c = 0; c < co->n_cells; ++c) old_of[O.hid[(size_t)c]] = c;
   const int64_t voc = (int64_t)dim * co->n_vnodes, vof = (int64_t)dim * fi->n_vnodes;
   for (int pass = 0; pass < 2; ++pass) {
     const int kk = pass == 0 ? co->k : co->kp, kk1 = kk + 1, nn = dim == 2 ? kk1 * kk1 : kk1 * kk1 * kk1;
     const int32_t *cc = pass == 0 ? co->cell_vnodes : co->cell_pnodes, *fc = pass == 0 ? fi->cell_vnodes : fi->cell_pnodes;
     const int ncomp = pass == 0 ? dim : 1;
+    auto eval = [&](int64_t oc, const double *xi, double *val) {
+      for (int e = 0; e < ncomp; ++e) val[e] = 0.0;
+      for (int b = 0; b < nn; ++b) {
+        const int ib[3] = {b % kk1, (b / kk1) % kk1, dim == 3 ? b / (kk1 * kk1) : 0};
+        double w = 1.0;
+        for (int d = 0; d < dim; ++d) w *= lag1(kk, ib[d], xi[d]);
+        if (w == 0.0) continue;
+        const int64_t node = cc[oc * nn + b];
+        for (int e = 0; e < ncomp; ++e) val[e] += w * cvec[pass == 0 ? node * dim + e : voc + node];
+      }
+    };
     for (int64_t f = 0; f < fi->n_cells; ++f) {
-      const int64_t c = f >> dim;
-      const int ch = (int)(f & ((1 << dim) - 1));
+      const int64_t h = N.hid[(size_t)f];
+      // ancestor chain up to an old active cell (refinement or unchanged)
+      int64_t anc = h;
+      std::vector<int> path;
+      while (anc >= 0 && !old_of.count(anc)) {
+        path.push_back(N.t_pos[(size_t)anc]);
+        anc = N.t_parent[(size_t)anc];
+      }
       for (int a = 0; a < nn; ++a) {
         const int ia[3] = {a % kk1, (a / kk1) % kk1, dim == 3 ? a / (kk1 * kk1) : 0};
-        double xp[3];
-        for (int d = 0; d < dim; ++d) xp[d] = 0.5 * ((double)ia[d] / kk + ((ch >> d) & 1));
-        double val[3] = {0, 0, 0};
-        for (int b = 0; b < nn; ++b) {
-          const int ib[3] = {b % kk1, (b / kk1) % kk1, dim == 3 ? b / (kk1 * kk1) : 0};
-          double w = 1.0;
-          for (int d = 0; d < dim; ++d) w *= lag1(kk, ib[d], xp[d]);
-          if (w == 0.0) continue;
-          const int64_t node = cc[c * nn + b];
-          for (int e = 0; e < ncomp; ++e) val[e] += w * cvec[pass == 0 ? node * dim + e : voc + node];
+        double xi[3] = {0, 0, 0}, val[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) xi[d] = (double)ia[d] / kk;
+        int64_t oc;
+        if (anc >= 0) {
+          for (int pos : path)  // child -> parent reference coordinates
+            for (int d = 0; d < dim; ++d) xi[d] = 0.5 * (xi[d] + ((pos >> d) & 1));
+          oc = old_of[anc];
+        } else {  // coarsened: descend the old hierarchy from the new cell
+          int64_t c = h;
+          int guard = 0;
+          while (!old_of.count(c)) {
+            if ((size_t)c >= O.t_child0.size() || O.t_child0[(size_t)c] < 0 || ++guard > 64)
+              return gls_io_set_error(GLS_EINVAL, "gls_fe_space_transfer: cell %lld not found in the old mesh", (long long)h);
+            int ch = 0;
+            for (int d = 0; d < dim; ++d) {
+              const int bit = xi[d] > 0.5 ? 1 : 0;
+              ch |= bit << d;
+              xi[d] = 2 * xi[d] - bit;
+            }
+            c = O.t_child0[(size_t)c] + ch;
+          }
+          oc = old_of[c];
         }
+        eval(oc, xi, val);
         const int64_t fn = fc[f * nn + a];
         for (int e = 0; e < ncomp; ++e) fvec[pass == 0 ? fn * dim + e : vof + fn] = val[e];
       }
     }
   }
   return GLS_OK;
+}
+
+// Face pieces of KellyErrorEstimator::estimate with a MappingQ (navier_stokes_base.cc:612-652;
+// deal.II 9.2 error_estimator.cc, third party, restated): every interior face between two active
+// cells of the same level is one piece; on a face between an active cell and a refined neighbour
+// each child face is a piece (integrate_over_irregular_face), its geometry (normal, JxW) taken on the
+// coarse cell's subface as deal.II's present cell does. QGauss<dim-1>(nq) on each piece; per point,
+// both sides' reference coordinates xi, g = J^-1 n and JxW. cell_diam: cell->diameter() (the longest
+// vertex diagonal). Null arrays: count only.
+int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, int32_t *ca, int32_t *cb, double *xi,
+                             double *g, double *jxw, double *cell_diam) {
+  if (!sp || !sp->impl_ || !n_pieces || nq < 1 || nq > 8) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_kelly_faces: arguments");
+  const FESpaceImpl &F = *static_cast<const FESpaceImpl *>(sp->impl_);
+  const int dim = sp->dim, nqf = dim == 3 ? nq * nq : nq;
+  const int64_t nc = sp->n_cells;
+  if (cell_diam)
+    for (int64_t c = 0; c < nc; ++c) {
+      const auto &cv = F.cell_verts[(size_t)c];
+      const int nd = dim == 2 ? 2 : 4, top = (1 << dim) - 1;
+      double dm = 0;
+      for (int i = 0; i < nd; ++i) dm = std::max(dm, nrm(sub(F.verts[(size_t)cv[i]], F.verts[(size_t)cv[top - i]])));
+      cell_diam[c] = dm;
+    }
+  std::map<EKey, std::vector<std::pair<int64_t, int>>> faces;  // active faces -> (cell, 2d + s)
+  for (int64_t c = 0; c < nc; ++c)
+    for (int f = 0; f < 2 * dim; ++f) faces[face_key_v(dim, F.cell_verts[(size_t)c], f / 2, f & 1)].push_back({c, f});
+  double xq[8], wq[8];
+  gauss01(nq, xq, wq);
+  auto tang = [&](int d, int *t) {
+    int n = 0;
+    for (int e = 0; e < dim; ++e)
+      if (e != d) t[n++] = e;
+  };
+  int64_t cnt = 0;
+  for (int64_t a = 0; a < nc; ++a)
+    for (int fa = 0; fa < 2 * dim; ++fa) {
+      const auto &av = F.cell_verts[(size_t)a];
+      const int da = fa / 2, sa = fa & 1;
+      const auto &lst = faces[face_key_v(dim, av, da, sa)];
+      int64_t b = -1;
+      int fb = -1;
+      bool irregular = false;
+      if (lst.size() == 2) {
+        const auto &o = lst[0].first == a ? lst[1] : lst[0];
+        if (o.first < a) continue;  // emitted from the other side
+        b = o.first;
+        fb = o.second;
+      } else {
+        const int64_t h = F.hid[(size_t)a];
+        const int64_t P = F.t_parent.empty() ? -1 : F.t_parent[(size_t)h];
+        if (P < 0 || ((F.t_pos[(size_t)h] >> da) & 1) != sa) continue;
+        auto it = faces.find(face_key_v(dim, F.t_verts[(size_t)P], da, sa));
+        if (it == faces.end() || it->second.size() != 1) continue;  // boundary
+        b = it->second[0].first;
+        fb = it->second[0].second;
+        irregular = true;
+      }
+      if (!xi) {
+        ++cnt;
+        continue;
+      }
+      const int db = fb / 2, sb = fb & 1;
+      int ta[2] = {0, 0}, tb[2] = {0, 0};
+      tang(da, ta);
+      tang(db, tb);
+      const auto &bv = F.cell_verts[(size_t)b];
+      // b's face lattice: vertex id -> face parameters (corners; with the midpoints when irregular)
+      std::map<int64_t, std::array<double, 2>> par;
+      int64_t C[2][2] = {{-1, -1}, {-1, -1}};
+      for (int iu = 0; iu < 2; ++iu)
+        for (int iv = 0; iv < (dim == 3 ? 2 : 1); ++iv) {
+          C[iu][iv] = bv[(size_t)((sb << db) | (iu << tb[0]) | (dim == 3 ? iv << tb[1] : 0))];
+          par[C[iu][iv]] = {(double)iu, (double)iv};
+        }
+      if (irregular) {
+        if (dim == 2) {
+          auto it = F.line_mid.find(mkey({C[0][0], C[1][0]}));
+          if (it != F.line_mid.end()) par[it->second] = {0.5, 0.0};
+        } else {
+          for (int i = 0; i < 2; ++i) {
+            auto e1 = F.line_mid.find(mkey({C[0][i], C[1][i]}));
+            if (e1 != F.line_mid.end()) par[e1->second] = {0.5, (double)i};
+            auto e2 = F.line_mid.find(mkey({C[i][0], C[i][1]}));
+            if (e2 != F.line_mid.end()) par[e2->second] = {(double)i, 0.5};
+          }
+          auto fc = F.face_mid.find(mkey({C[0][0], C[0][1], C[1][0], C[1][1]}));
+          if (fc != F.face_mid.end()) par[fc->second] = {0.5, 0.5};
+        }
+      }
+      // a's face corners (0,0), (1,0), (0,1) in b's face parameters
+      std::array<double, 2> Pc[3];
+      const int cu[3] = {0, 1, 0}, cvv[3] = {0, 0, 1};
+      for (int i = 0; i < (dim == 3 ? 3 : 2); ++i) {
+        const int64_t vid = av[(size_t)((sa << da) | (cu[i] << ta[0]) | (dim == 3 ? cvv[i] << ta[1] : 0))];
+        auto it = par.find(vid);
+        if (it == par.end()) return gls_io_set_error(GLS_EINVAL, "Kelly faces: cells %lld / %lld do not share a face piece", (long long)a, (long long)b);
+        Pc[i] = it->second;
+      }
+      ca[cnt] = (int32_t)a;
+      cb[cnt] = (int32_t)b;
+      for (int qb = 0; qb < (dim == 3 ? nq : 1); ++qb)
+        for (int qa = 0; qa < nq; ++qa) {
+          const int q = qa + nq * qb;
+          const double u = xq[qa], v = dim == 3 ? xq[qb] : 0.0, w = wq[qa] * (dim == 3 ? wq[qb] : 1.0);
+          double XA[3] = {0, 0, 0}, XB[3] = {0, 0, 0}, TuA[3] = {0, 0, 0}, TvA[3] = {0, 0, 0}, TuB[3] = {0, 0, 0}, TvB[3] = {0, 0, 0};
+          XA[da] = sa;
+          XA[ta[0]] = u;
+          TuA[ta[0]] = 1.0;
+          if (dim == 3) {
+            XA[ta[1]] = v;
+            TvA[ta[1]] = 1.0;
+          }
+          XB[db] = sb;
+          for (int j = 0; j < dim - 1; ++j) {
+            XB[tb[j]] = Pc[0][j] + u * (Pc[1][j] - Pc[0][j]) + v * (dim == 3 ? Pc[2][j] - Pc[0][j] : 0.0);
+            TuB[tb[j]] = Pc[1][j] - Pc[0][j];
+            if (dim == 3) TvB[tb[j]] = Pc[2][j] - Pc[0][j];
+          }
+          double JA[3][3], JB[3][3];
+          jacobian(*sp, a, XA, JA);
+          jacobian(*sp, b, XB, JB);
+          const auto &JG = irregular ? JB : JA;
+          const double *Tu = irregular ? TuB : TuA, *Tv = irregular ? TvB : TvA;
+          V3 tu{0, 0, 0}, tv{0, 0, 0};
+          for (int i = 0; i < dim; ++i)
+            for (int e = 0; e < dim; ++e) {
+              tu[i] += JG[i][e] * Tu[e];
+              tv[i] += JG[i][e] * Tv[e];
+            }
+          V3 n;
+          double area;
+          if (dim == 2) {
+            area = nrm(tu);
+            n = {tu[1] / area, -tu[0] / area, 0.0};
+          } else {
+            n = cross(tu, tv);
+            area = nrm(n);
+            n = scl(n, 1.0 / area);
+          }
+          jxw[cnt * nqf + q] = area * w;
+          double ga[3], gb[3];
+          solve3(JA, n.data(), ga, dim);
+          solve3(JB, n.data(), gb, dim);
+          for (int d = 0; d < dim; ++d) {
+            xi[((cnt * nqf + q) * 2 + 0) * dim + d] = XA[d];
+            xi[((cnt * nqf + q) * 2 + 1) * dim + d] = XB[d];
+            g[((cnt * nqf + q) * 2 + 0) * dim + d] = ga[d];
+            g[((cnt * nqf + q) * 2 + 1) * dim + d] = gb[d];
+          }
+        }
+      ++cnt;
+    }
+  *n_pieces = cnt;
+  return GLS_OK;
+}
+
+int gls_umesh_adapt(gls_umesh *g, const int32_t *refine, const int32_t *coarsen) {
+  if (!g) return gls_io_set_error(GLS_EINVAL, "null mesh");
+  return adapt(g->m, refine, coarsen);
+}
+
+int gls_umesh_prepare(const gls_umesh *g, int32_t *refine, int32_t *coarsen) {
+  if (!g || !refine || !coarsen) return gls_io_set_error(GLS_EINVAL, "gls_umesh_prepare: arguments");
+  init_tree(const_cast<UMesh &>(g->m));
+  USmoother sm(g->m, refine, coarsen);
+  const int loops = sm.run();
+  for (size_t i = 0; i < g->m.active.size(); ++i) {
+    refine[i] = sm.ref[i];
+    coarsen[i] = sm.crs[i];
+  }
+  return loops;
 }
 
 }  // extern "C"

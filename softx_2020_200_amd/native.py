@@ -41,7 +41,8 @@ EXPORTS = [
     "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
-    "gls_fe_space_transfer",
+    "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
+    "gls_kelly_estimate_mapped",
 ]
 
 
@@ -69,7 +70,13 @@ class FESpace(C.Structure):
                 ("vnode_x", C.POINTER(C.c_double)), ("pnode_x", C.POINTER(C.c_double)),
                 ("vnode_bid", C.POINTER(C.c_uint32)), ("pnode_bid", C.POINTER(C.c_uint32)),
                 ("cell_support", C.POINTER(C.c_double)), ("cell_mapping", C.POINTER(C.c_int32)),
-                ("cell_measure", C.POINTER(C.c_double)), ("volume", C.c_double), ("impl_", C.c_void_p)]
+                ("cell_measure", C.POINTER(C.c_double)), ("volume", C.c_double),
+                ("cell_level", C.POINTER(C.c_int32)),
+                ("n_vhang", C.c_int64), ("vhang_node", C.POINTER(C.c_int64)), ("vhang_off", C.POINTER(C.c_int64)),
+                ("vhang_master", C.POINTER(C.c_int64)), ("vhang_w", C.POINTER(C.c_double)),
+                ("n_phang", C.c_int64), ("phang_node", C.POINTER(C.c_int64)), ("phang_off", C.POINTER(C.c_int64)),
+                ("phang_master", C.POINTER(C.c_int64)), ("phang_w", C.POINTER(C.c_double)),
+                ("impl_", C.c_void_p)]
 
 
 class LinearParams(C.Structure):
@@ -178,6 +185,11 @@ def load():
                                      C.POINTER(C.POINTER(FESpace))]
     L.gls_fe_space_destroy.argtypes = [C.POINTER(FESpace)]
     L.gls_fe_space_transfer.argtypes = [C.POINTER(FESpace), C.POINTER(FESpace), d, d]
+    pi32 = C.POINTER(C.c_int32)
+    L.gls_umesh_prepare.argtypes = [vp, pi32, pi32]
+    L.gls_umesh_adapt.argtypes = [vp, pi32, pi32]
+    L.gls_fe_space_kelly_faces.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(i64), pi32, pi32, d, d, d, d]
+    L.gls_kelly_estimate_mapped.argtypes = [vp, vp, C.c_int, i64, C.c_int, pi32, pi32, d, d, d, d, vp]
     _lib = L
     return L
 
@@ -801,15 +813,71 @@ class UMesh:
 
     def fe_space(self, k, kp=None, qmapping_all=False, periodic=()):
         """FE_Q(k)^dim x FE_Q(kp) on this mesh -> dict of numpy arrays (gls_umesh_fe_space)."""
+        return self.fe_space_handle(k, kp, qmapping_all, periodic).data
+
+    def fe_space_handle(self, k, kp=None, qmapping_all=False, periodic=()):
+        """The same as a live FESpaceHandle (transfers, Kelly face pieces)."""
         kp = k if kp is None else kp
         per = np.ascontiguousarray(np.array(periodic, dtype=np.int32).reshape(-1))
         pm = C.POINTER(FESpace)()
         check(self.L.gls_umesh_fe_space(self.h, int(k), int(kp), 1 if qmapping_all else 0, len(per) // 3,
                                         per.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pm)), "gls_umesh_fe_space")
+        return FESpaceHandle(self.L, pm)
+
+    def prepare(self, refine, coarsen):
+        """prepare_coarsening_and_refinement with the reference's smoothing (gls_umesh_prepare);
+        returns the smoothed (refine, coarsen) flags over the active cells."""
+        r = np.ascontiguousarray(refine, dtype=np.int32).copy()
+        c = np.ascontiguousarray(coarsen, dtype=np.int32).copy()
+        check(self.L.gls_umesh_prepare(self.h, r.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       c.ctypes.data_as(C.POINTER(C.c_int32))), "gls_umesh_prepare")
+        return r, c
+
+    def adapt(self, refine, coarsen=None):
+        """execute_coarsening_and_refinement (gls_umesh_adapt) with per-active-cell flags."""
+        r = np.ascontiguousarray(refine, dtype=np.int32)
+        c = np.ascontiguousarray(np.zeros_like(r) if coarsen is None else coarsen, dtype=np.int32)
+        check(self.L.gls_umesh_adapt(self.h, r.ctypes.data_as(C.POINTER(C.c_int32)),
+                                     c.ctypes.data_as(C.POINTER(C.c_int32))), "gls_umesh_adapt")
+
+
+class FESpaceHandle:
+    """A live gls_fe_space: .data (numpy dict), transfer_from (SolutionTransfer from an earlier space
+    of the same mesh), kelly_faces (face pieces with MappingQ geometry)."""
+
+    def __init__(self, L, ptr):
+        self.L, self.ptr = L, ptr
+        self.data = _fe_space_dict(ptr.contents)
+
+    def __del__(self):
         try:
-            return _fe_space_dict(pm.contents)
-        finally:
-            self.L.gls_fe_space_destroy(pm)
+            if getattr(self, "ptr", None):
+                self.L.gls_fe_space_destroy(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+    def transfer_from(self, old, vec):
+        vec = np.ascontiguousarray(vec, dtype=np.float64)
+        out = np.zeros(self.data["dim"] * self.data["n_vnodes"] + self.data["n_pnodes"])
+        check(self.L.gls_fe_space_transfer(old.ptr, self.ptr, _dp(vec), _dp(out)), "gls_fe_space_transfer")
+        return out
+
+    def kelly_faces(self, nq):
+        n = C.c_int64()
+        z32 = C.POINTER(C.c_int32)()
+        zd = C.POINTER(C.c_double)()
+        check(self.L.gls_fe_space_kelly_faces(self.ptr, int(nq), C.byref(n), z32, z32, zd, zd, zd, zd),
+              "gls_fe_space_kelly_faces")
+        dim, ne = self.data["dim"], int(n.value)
+        nqf = nq ** (dim - 1)
+        ca, cb = np.zeros(ne, np.int32), np.zeros(ne, np.int32)
+        xi, g = np.zeros((ne, nqf, 2, dim)), np.zeros((ne, nqf, 2, dim))
+        jxw, diam = np.zeros((ne, nqf)), np.zeros(self.data["n_cells"])
+        p32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
+        check(self.L.gls_fe_space_kelly_faces(self.ptr, int(nq), C.byref(n), p32(ca), p32(cb), _dp(xi), _dp(g),
+                                              _dp(jxw), _dp(diam)), "gls_fe_space_kelly_faces")
+        return dict(ca=ca, cb=cb, xi=xi, g=g, jxw=jxw, diam=diam, nqf=nqf)
 
 
 def _fe_space_dict(m):
@@ -829,4 +897,20 @@ def _fe_space_dict(m):
                 pnode_bid=take(m.pnode_bid, npn, np.uint32, (npn,)),
                 cell_support=take(m.cell_support, nc * nl * dim, np.float64, (nc, nl, dim)),
                 cell_mapping=take(m.cell_mapping, nc, np.int32, (nc,)),
-                cell_measure=take(m.cell_measure, nc, np.float64, (nc,)), volume=float(m.volume))
+                cell_measure=take(m.cell_measure, nc, np.float64, (nc,)), volume=float(m.volume),
+                cell_level=take(m.cell_level, nc, np.int32, (nc,)),
+                vhang=_hang_lines(m.n_vhang, m.vhang_node, m.vhang_off, m.vhang_master, m.vhang_w),
+                phang=_hang_lines(m.n_phang, m.phang_node, m.phang_off, m.phang_master, m.phang_w))
+
+
+def _hang_lines(n, node, off, master, w):
+    """hanging lines as {node: [(master, weight), ...]}"""
+    n = int(n)
+    if n == 0:
+        return {}
+    node = np.ctypeslib.as_array(node, shape=(n,)).copy()
+    off = np.ctypeslib.as_array(off, shape=(n + 1,)).copy()
+    nm = int(off[-1])
+    master = np.ctypeslib.as_array(master, shape=(nm,)).copy()
+    w = np.ctypeslib.as_array(w, shape=(nm,)).copy()
+    return {int(node[i]): [(int(master[j]), float(w[j])) for j in range(off[i], off[i + 1])] for i in range(n)}

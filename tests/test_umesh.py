@@ -76,13 +76,13 @@ def test_fe_space_transfer_is_exact():
                  (UMesh(2, gmsh=os.path.join(MESHES, "square.msh")), 1),
                  (UMesh(3, "cylinder", "1 : 1"), 2)):
         m.refine_global(1)
-        co = m.fe_space(k, 1)
+        coh = m.fe_space_handle(k, 1)
         m.refine_global(1)
-        fi = m.fe_space(k, 1)
-        import softx_2020_200_amd.native as nat
+        fih = m.fe_space_handle(k, 1)
+        co, fi = coh.data, fih.data
         rng = np.random.default_rng(7)
         cvec = rng.uniform(-1, 1, co["dim"] * co["n_vnodes"] + co["n_pnodes"])
-        fvec = transfer(m, co, fi, cvec, nat)
+        fvec = fih.transfer_from(coh, cvec)
         # each fine cell's nodes equal the parent's interpolant: check on the corner (vertex) nodes,
         # which coincide with coarse nodes of the parent
         dim = co["dim"]
@@ -97,31 +97,6 @@ def test_fe_space_transfer_is_exact():
             a_c = sum(idx[d] * k1 ** d for d in range(dim))
             nf, nc_ = fi["cell_vnodes"][f, a_f], co["cell_vnodes"][c, a_c]
             assert np.allclose(fvec[nf * dim:(nf + 1) * dim], cvec[nc_ * dim:(nc_ + 1) * dim], atol=1e-14)
-
-
-def transfer(m, co, fi, cvec, nat):
-    """host-side transfer through the C-ABI (rebuilds the two spaces' structs)."""
-    import ctypes as C
-    L = nat.load()
-    out = np.zeros(fi["dim"] * fi["n_vnodes"] + fi["n_pnodes"])
-    # rebuild owning structs from the same mesh: coarse = parent level (refine_global is parent-major)
-    return _transfer_via_abi(co, fi, cvec, out, L, C)
-
-
-def _transfer_via_abi(co, fi, cvec, out, L, C):
-    from softx_2020_200_amd.native import FESpace, _dp
-    structs = []
-    for s in (co, fi):
-        F = FESpace()
-        F.dim, F.k, F.kp = s["dim"], s["k"], s["kp"]
-        F.n_cells, F.n_vnodes, F.n_pnodes = s["n_cells"], s["n_vnodes"], s["n_pnodes"]
-        F.cell_vnodes = s["cell_vnodes"].ctypes.data_as(C.POINTER(C.c_int32))
-        F.cell_pnodes = s["cell_pnodes"].ctypes.data_as(C.POINTER(C.c_int32))
-        structs.append(F)
-    cv = np.ascontiguousarray(cvec)
-    rc = L.gls_fe_space_transfer(C.byref(structs[0]), C.byref(structs[1]), _dp(cv), _dp(out))
-    assert rc == 0
-    return out
 
 
 def _solve_levels(m, k, qall, bcs, levels, force=None, srf=False, tol=1e-10):
