@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -256,8 +257,8 @@ Params read_params(const Prm &p, int dim) {
     P.min_level = p.i(ma + "min refinement level", 0);
     if (P.frac_refine < 0 || P.frac_coarsen < 0 || P.frac_refine + P.frac_coarsen > 1)
       die("mesh adaptation: fractions must be >= 0 with refinement + coarsening <= 1");
-    if (P.method != Method::steady) die("kelly mesh adaptation: steady simulations only");
-    if (P.general) die("kelly mesh adaptation: hyper_cube meshes only");
+    if (P.method != Method::steady && !P.general)
+      die("kelly mesh adaptation: transient runs on general (gmsh / GridGenerator) meshes only");
     if (P.k > 2 || P.kp > P.k) die("kelly mesh adaptation: 1 <= pressure order <= velocity order <= 2");
   }
   const int nbc = p.i("boundary conditions/number", 0);
@@ -364,6 +365,7 @@ struct Mesh {
   // locally refined mesh (gls_mesh_refined_create): explicit support points, hanging nodes and
   // their DoF-level constraint lines (empty on the uniform lattice)
   std::vector<double> vx, px;
+  std::map<int, std::vector<double>> slip_normals;  // general meshes: boundary id -> node normals [nv][dim]
   std::vector<uint8_t> vhanging;  // per velocity node
   std::vector<int64_t> hang_dofs, hang_off{0}, hang_master;
   std::vector<double> hang_w;
@@ -466,7 +468,12 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
   for (const BC &b : P.bcs) {
     if (b.type == "periodic") continue;
-    if (b.type == "slip" && m.general) die("slip boundaries on curved / unstructured meshes are not supported");
+    const std::vector<double> *sn = nullptr;  // general meshes: node normals of this slip boundary
+    if (b.type == "slip" && m.general) {
+      auto it = m.slip_normals.find(b.id);
+      if (it == m.slip_normals.end()) die("slip boundary %d: no node normals", b.id);
+      sn = &it->second;
+    }
     std::vector<int64_t> sel;
     std::vector<double> X;
     std::vector<unsigned> nrm;
@@ -480,7 +487,17 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       if ((m.general ? m.vbid[(size_t)v] : face_bits(m, x, P.colorize)) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
-        nrm.push_back(face_normals(m, x, P.colorize, b.id));
+        if (sn) {  // n.u = 0 on a straight wall: the normal is an axis, that component is 0
+          unsigned ax = 0;
+          for (int c = 0; c < m.dim; ++c) {
+            const double nc = std::fabs((*sn)[(size_t)(v * m.dim + c)]);
+            if (nc > 1 - 1e-12) ax |= 1u << c;
+            else if (nc > 1e-12) die("slip boundary %d: node normal not along an axis (curved slip walls are not supported)", b.id);
+          }
+          nrm.push_back(ax);
+        } else {
+          nrm.push_back(face_normals(m, x, P.colorize, b.id));
+        }
       }
     }
     std::vector<double> fv[3];
@@ -833,6 +850,38 @@ struct Solver {
     hk(hipDeviceSynchronize(), "device copy");
   }
 
+  // node-level hanging lines -> DoF-level lines: velocity DoF node*dim + c per component, pressure
+  // DoF dim*nv + node
+  static void load_hanging(Mesh &r, int64_t nvh, const int64_t *vn, const int64_t *vo, const int64_t *vm,
+                           const double *vw, int64_t nph, const int64_t *pn, const int64_t *po, const int64_t *pm,
+                           const double *pw) {
+    const int dim = r.dim;
+    r.vhanging.assign((size_t)r.nv, 0);
+    r.hang_dofs.clear();
+    r.hang_off.assign(1, 0);
+    r.hang_master.clear();
+    r.hang_w.clear();
+    for (int64_t i = 0; i < nvh; ++i) {
+      r.vhanging[(size_t)vn[i]] = 1;
+      for (int c = 0; c < dim; ++c) {
+        r.hang_dofs.push_back(vn[i] * dim + c);
+        for (int64_t j = vo[i]; j < vo[i + 1]; ++j) {
+          r.hang_master.push_back(vm[j] * dim + c);
+          r.hang_w.push_back(vw[j]);
+        }
+        r.hang_off.push_back((int64_t)r.hang_master.size());
+      }
+    }
+    for (int64_t i = 0; i < nph; ++i) {
+      r.hang_dofs.push_back(dim * r.nv + pn[i]);
+      for (int64_t j = po[i]; j < po[i + 1]; ++j) {
+        r.hang_master.push_back(dim * r.nv + pm[j]);
+        r.hang_w.push_back(pw[j]);
+      }
+      r.hang_off.push_back((int64_t)r.hang_master.size());
+    }
+  }
+
   // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
   // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels
   // and a Jacobi-preconditioned GMRES (no multigrid on locally refined meshes).
@@ -861,27 +910,8 @@ struct Solver {
     r.h.assign(R.cell_h, R.cell_h + r.nc * dim);
     r.vx.assign(R.vnode_x, R.vnode_x + r.nv * dim);
     r.px.assign(R.pnode_x, R.pnode_x + r.np * dim);
-    r.vhanging.assign((size_t)r.nv, 0);
-    // DoF-level lines: velocity DoF node*dim + c per component, pressure DoF dim*nv + node
-    for (int64_t i = 0; i < R.n_vhang; ++i) {
-      r.vhanging[(size_t)R.vhang_node[i]] = 1;
-      for (int c = 0; c < dim; ++c) {
-        r.hang_dofs.push_back(R.vhang_node[i] * dim + c);
-        for (int64_t j = R.vhang_off[i]; j < R.vhang_off[i + 1]; ++j) {
-          r.hang_master.push_back(R.vhang_master[j] * dim + c);
-          r.hang_w.push_back(R.vhang_w[j]);
-        }
-        r.hang_off.push_back((int64_t)r.hang_master.size());
-      }
-    }
-    for (int64_t i = 0; i < R.n_phang; ++i) {
-      r.hang_dofs.push_back(dim * r.nv + R.phang_node[i]);
-      for (int64_t j = R.phang_off[i]; j < R.phang_off[i + 1]; ++j) {
-        r.hang_master.push_back(dim * r.nv + R.phang_master[j]);
-        r.hang_w.push_back(R.phang_w[j]);
-      }
-      r.hang_off.push_back((int64_t)r.hang_master.size());
-    }
+    load_hanging(r, R.n_vhang, R.vhang_node, R.vhang_off, R.vhang_master, R.vhang_w, R.n_phang, R.phang_node,
+                 R.phang_off, R.phang_master, R.phang_w);
     m = std::move(r);
     C = make_constraints(P, m, time);
     ctx = make_context(m, C);
@@ -969,9 +999,22 @@ struct Solver {
     r.vbid.assign(F.vnode_bid, F.vnode_bid + r.nv);
     r.support.assign(F.cell_support, F.cell_support + r.nc * nvl * P.dim);
     r.measure.assign(F.cell_measure, F.cell_measure + r.nc);
+    load_hanging(r, F.n_vhang, F.vhang_node, F.vhang_off, F.vhang_master, F.vhang_w, F.n_phang, F.phang_node,
+                 F.phang_off, F.phang_master, F.phang_w);
+    // slip boundaries: the averaged face normals at the velocity nodes (compute_no_normal_flux_constraints)
+    for (const BC &b : P.bcs)
+      if (b.type == "slip") {
+        std::vector<double> nrm((size_t)(r.nv * P.dim));
+        ck(gls_fe_space_boundary_normals(space, b.id, nrm.data()), "gls_fe_space_boundary_normals");
+        r.slip_normals[b.id] = std::move(nrm);
+      }
     m = std::move(r);
     C = make_constraints(P, m, time);
     ctx = make_context(m, C);
+    if (!m.hang_dofs.empty())
+      ck(gls_set_hanging(ctx, (int64_t)m.hang_dofs.size(), m.hang_dofs.data(), m.hang_off.data(), m.hang_master.data(),
+                         m.hang_w.data()),
+         "gls_set_hanging");
     alloc_vectors();
     print_setup(F.volume);
   }
@@ -1411,6 +1454,10 @@ struct Solver {
   // present solution (:684-733). The forest is the hyper_cube's one coarse cell refined
   // `initial refinement` times, so leaf levels are deal.II's cell levels.
   void refine_kelly() {
+    if (m.general) {
+      refine_kelly_general();
+      return;
+    }
     need_host();
     if (m.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
     const int dim = P.dim;
@@ -1513,6 +1560,75 @@ struct Solver {
       ck(gls_mesh_refined_interpolate(rmesh, (int)n_uniform, P.lo, P.hi, sol.data(), present.data()),
          "gls_mesh_refined_interpolate");
     }
+  }
+  // refine_mesh_kelly on a general (gmsh / GridGenerator, curved) triangulation: the Kelly indicator
+  // with MappingQ face geometry (gls_fe_space_kelly_faces + gls_kelly_estimate_mapped), the same
+  // thresholds and level rules as above, prepare_coarsening_and_refinement / execution on the
+  // triangulation's hierarchy (gls_umesh_prepare / gls_umesh_adapt), SolutionTransfer of the present
+  // solution and the time history (navier_stokes_base.cc:684-780)
+  void refine_kelly_general() {
+    need_host();
+    const int dim = P.dim;
+    const int64_t nc = m.nc;
+    const int nq = P.k + 2;  // QGauss<dim-1>(n_q + 1), n_q = velocity order + 1
+    const int nqf = dim == 3 ? nq * nq : nq;
+    int64_t np = 0;
+    ck(gls_fe_space_kelly_faces(space, nq, &np, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr), "gls_fe_space_kelly_faces");
+    std::vector<int32_t> ca((size_t)np), cb((size_t)np);
+    std::vector<double> xi((size_t)(np * nqf * 2 * dim)), g(xi.size()), jxw((size_t)(np * nqf)), diam((size_t)nc);
+    ck(gls_fe_space_kelly_faces(space, nq, &np, ca.data(), cb.data(), xi.data(), g.data(), jxw.data(), diam.data()),
+       "gls_fe_space_kelly_faces");
+    upload(present, d_present);
+    double *d_eta = nullptr;
+    hk(hipMalloc(&d_eta, sizeof(double) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
+    ck(gls_kelly_estimate_mapped(ctx, d_present, P.kelly_variable, np, nqf, ca.data(), cb.data(), xi.data(), g.data(),
+                                 jxw.data(), diam.data(), d_eta),
+       "gls_kelly_estimate_mapped");
+    hk(hipDeviceSynchronize(), "kelly estimate");
+    std::vector<double> eta((size_t)nc);
+    download(d_eta, eta);
+    (void)hipFree(d_eta);
+    std::vector<float> crit((size_t)nc);
+    int max_lev = 0;
+    for (int64_t i = 0; i < nc; ++i) {
+      crit[(size_t)i] = (float)eta[(size_t)i];
+      max_lev = std::max(max_lev, (int)space->cell_level[i]);
+    }
+    std::vector<int32_t> rf((size_t)nc, 0), cf((size_t)nc, 0);
+    ck(gls_refine_coarsen_pd(nc, crit.data(), dim, P.frac_type, P.frac_refine, P.frac_coarsen, P.max_cells, rf.data(),
+                             cf.data(), nullptr),
+       "gls_refine_coarsen_pd");
+    int64_t nr0 = 0, nc0 = 0;
+    for (int64_t i = 0; i < nc; ++i) {
+      nr0 += rf[(size_t)i];
+      nc0 += cf[(size_t)i];
+    }
+    for (int64_t i = 0; i < nc; ++i) {  // max / min refinement level rules (:669-680)
+      if (max_lev + 1 > P.max_level && space->cell_level[i] >= P.max_level) rf[(size_t)i] = 0;
+      if (space->cell_level[i] == P.min_level) cf[(size_t)i] = 0;
+    }
+    ck(gls_umesh_prepare(um, rf.data(), cf.data()), "gls_umesh_prepare");
+    int64_t nr1 = 0, nc1 = 0;
+    for (int64_t i = 0; i < nc; ++i) {
+      nr1 += rf[(size_t)i];
+      nc1 += cf[(size_t)i];
+    }
+    if (stats)
+      std::printf("kelly: %lld of %lld cells flagged for refinement, %lld for coarsening (after smoothing: %lld, %lld)\n",
+                  (long long)nr0, (long long)nc, (long long)nc0, (long long)nr1, (long long)nc1);
+    ck(gls_umesh_adapt(um, rf.data(), cf.data()), "gls_umesh_adapt");
+    const std::vector<double> s0 = present, s1 = m1, s2 = m2, s3 = m3;
+    gls_fe_space *old_space = space;
+    space = nullptr;  // keep the old space alive across setup_general
+    setup_general();
+    ck(gls_fe_space_transfer(old_space, space, s0.data(), present.data()), "gls_fe_space_transfer");
+    if (P.method != Method::steady) {
+      ck(gls_fe_space_transfer(old_space, space, s1.data(), m1.data()), "gls_fe_space_transfer");
+      ck(gls_fe_space_transfer(old_space, space, s2.data(), m2.data()), "gls_fe_space_transfer");
+      ck(gls_fe_space_transfer(old_space, space, s3.data(), m3.data()), "gls_fe_space_transfer");
+    }
+    gls_fe_space_destroy(old_space);
+    host_changed();
   }
   // NavierStokesBase::finish_simulation's error table (navier_stokes_base.cc:382-424): deal.II
   // ConvergenceTable text layout — steady: cells | error_velocity + log2 reduction rate |
@@ -1623,9 +1739,9 @@ struct Solver {
       if (step == 1) {
         first_step();
       } else {
-        if (steady && step % P.adapt_frequency == 0) {  // refine_mesh (navier_stokes_base.cc:592-607)
-          if (P.madapt == "kelly") refine_kelly();
-          else refine_uniform();
+        if (step % P.adapt_frequency == 0) {  // refine_mesh (navier_stokes_base.cc:592-607)
+          if (P.madapt == "kelly") refine_kelly();  // steady and transient (gls_navier_stokes.cc:1406-1416)
+          else if (steady) refine_uniform();
         }
         advance();
       }

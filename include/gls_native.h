@@ -493,6 +493,10 @@ int gls_fe_space_transfer(const gls_fe_space *coarse, const gls_fe_space *fine, 
  * cells' levels; gls_fe_space_transfer then maps vectors from any earlier space of the same mesh
  * (refinement, coarsening, several levels). */
 int gls_umesh_prepare(const gls_umesh *mesh, int32_t *refine, int32_t *coarsen);
+/* Unit normals at the velocity nodes of the boundary faces with id boundary_id (the averaged face
+ * normals VectorTools::compute_no_normal_flux_constraints uses for a slip boundary,
+ * gls_navier_stokes.cc:100-110); [n_vnodes][dim], zero off that boundary. Host array. */
+int gls_fe_space_boundary_normals(const gls_fe_space *space, int boundary_id, double *normals);
 int gls_umesh_adapt(gls_umesh *mesh, const int32_t *refine, const int32_t *coarsen);
 /* Face pieces for KellyErrorEstimator with MappingQ on such a space (conforming faces one piece,
  * a face with a refined neighbour one piece per child face; geometry on the coarse side as deal.II's

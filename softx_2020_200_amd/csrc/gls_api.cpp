@@ -295,6 +295,9 @@ struct gls_ctx {
   bool qd_valid = false;  // invalidated with the diagonal by every state / parameter change
   DevBuf<float> qdata32;  // FP32 copy of qdata: the multigrid smoother's J.v (mixed precision)
   bool qd32_valid = false;  // stale whenever qdata is recomputed
+  // per-cell path: element vectors and each node's slots in them (deterministic scatter)
+  DevBuf<double> ev;
+  DevBuf<int64_t> ev_voff, ev_vslot, ev_poff, ev_pslot;
   bool smooth_f32 = false;  // this level's V-cycle J.v runs in FP32 (gls_mg_params.mixed_precision)
   bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
   // solver workspace
@@ -881,6 +884,36 @@ hipError_t slab_sum(gls_ctx *c, double *y) {
                              c->n_vnodes, y, c->stream);
 }
 
+// slots of every node in the per-cell element vectors [n_cells][NV*dim + NP], ascending (cell, local
+// node) order: the fixed summation order of gather_element_vectors
+int ensure_element_maps(gls_ctx *c) {
+  if (c->ev.p || c->n_cells == 0) return GLS_OK;
+  const int dim = c->dim, nv = gls::ipow(c->k + 1, dim), np = gls::ipow(c->kp + 1, dim), el = nv * dim + np;
+  std::vector<int32_t> cv((size_t)c->n_cells * nv), cp;
+  HIP_TRY(hipMemcpy(cv.data(), c->cell_vnodes.p, cv.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (c->cell_pnodes.p) {
+    cp.resize((size_t)c->n_cells * np);
+    HIP_TRY(hipMemcpy(cp.data(), c->cell_pnodes.p, cp.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  const std::vector<int32_t> &pn = c->cell_pnodes.p ? cp : cv;
+  std::vector<int64_t> voff((size_t)c->n_vnodes + 1, 0), poff((size_t)c->n_pnodes + 1, 0);
+  for (int64_t e = 0; e < (int64_t)c->n_cells * nv; ++e) ++voff[(size_t)cv[(size_t)e] + 1];
+  for (int64_t e = 0; e < (int64_t)c->n_cells * np; ++e) ++poff[(size_t)pn[(size_t)e] + 1];
+  for (size_t i = 1; i < voff.size(); ++i) voff[i] += voff[i - 1];
+  for (size_t i = 1; i < poff.size(); ++i) poff[i] += poff[i - 1];
+  std::vector<int64_t> vslot((size_t)voff.back()), pslot((size_t)poff.back());
+  std::vector<int64_t> vf(voff.begin(), voff.end() - 1), pf(poff.begin(), poff.end() - 1);
+  for (int64_t cell = 0; cell < c->n_cells; ++cell) {
+    for (int a = 0; a < nv; ++a) vslot[(size_t)vf[(size_t)cv[(size_t)(cell * nv + a)]]++] = cell * el + (int64_t)a * dim;
+    for (int a = 0; a < np; ++a) pslot[(size_t)pf[(size_t)pn[(size_t)(cell * np + a)]]++] = cell * el + (int64_t)nv * dim + a;
+  }
+  GLS_TRY(c->ev_voff.upload(voff.data(), voff.size()));
+  GLS_TRY(c->ev_vslot.upload(vslot.data(), std::max<size_t>(vslot.size(), 1)));
+  GLS_TRY(c->ev_poff.upload(poff.data(), poff.size()));
+  GLS_TRY(c->ev_pslot.upload(pslot.data(), std::max<size_t>(pslot.size(), 1)));
+  return c->ev.alloc((size_t)c->n_cells * el);
+}
+
 int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
@@ -916,12 +949,19 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   const bool col = brick && c->use_colors;
   if (col) set_colors(c, P, y);  // every node is written exactly once: no zeroing, no slab sum
   else P.slab = brick ? brick_slab(c) : nullptr;
-  if (!col && !P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
+  if (!brick) {  // per-cell kernels: element vectors, then ordered per-node sums (no atomics)
+    GLS_TRY(ensure_element_maps(c));
+    P.ev = c->ev.p;
+  }
+  if (!col && !P.slab && !P.ev) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
     if (brick) HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     else HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
   }
+  if (P.ev)
+    HIP_TRY(gls::gather_element_vectors(y, c->ev.p, c->ev_voff.p, c->ev_vslot.p, c->n_vnodes, c->ev_poff.p,
+                                        c->ev_pslot.p, c->n_pnodes, c->dim, c->stream));
   if (brick && !col && P.slab) {
     TimedLaunch t(c, 5);
     HIP_TRY(slab_sum(c, y));

@@ -10,7 +10,9 @@
 //   3. pointwise: tau, strong residual R_s, S(v) and the test-function coefficients
 //                 (restated from gls_navier_stokes.cc:387-748, Appendix A of SURVEY.md).
 //   4. integrate: one thread per (cell, node): transposed contraction sum_q B^T coef.
-//   5. scatter  : FP64 global atomics into the output vector.
+//   5. scatter  : element vectors stored per cell, then summed per node in a fixed (cell, local node)
+//                 order by gather_element_vectors (bit-reproducible); FP64 global atomics into the
+//                 output vector only when no element-vector buffer is given.
 //
 // Modes: residual (assemble_rhs), Jacobian action (matrix-free assembleGLS<true> . v),
 // Jacobian diagonal (for the Jacobi preconditioner and the deal.II constrained-row diagonal).
@@ -415,8 +417,14 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
           out[c] += s;
         }
       }
+      if (P.ev) {
+        double *e = P.ev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
-      for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], out[c]);
+        for (int c = 0; c < DIM; ++c) e[c] = out[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], out[c]);
+      }
     } else {
       const int cell = c0 + cl;
       const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
@@ -464,8 +472,14 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
       }
       // constrained rows (Dirichlet or hanging) get deal.II's |K_e(i,i)| per cell
       const unsigned m = (P.vmask ? P.vmask[node] : 0u) | (P.hmask ? P.hmask[node] : 0u);
+      if (P.ev) {
+        double *e = P.ev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
-      for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], ((m >> c) & 1u) ? fabs(out[c]) : out[c]);
+        for (int c = 0; c < DIM; ++c) e[c] = ((m >> c) & 1u) ? fabs(out[c]) : out[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], ((m >> c) & 1u) ? fabs(out[c]) : out[c]);
+      }
     }
   }
   for (int i = tid; i < ncb * NP; i += blockDim.x) {
@@ -511,7 +525,8 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
         out += Tq[0] * Tq[1] * (g0 * g0 + g1 * g1 + g2 * g2);
       }
     }
-    atomicAdd(&P.y[voff + pn], out);
+    if (P.ev) P.ev[(int64_t)(c0 + cl) * (NV * DIM + NP) + NV * DIM + a] = out;
+    else atomicAdd(&P.y[voff + pn], out);
   }
 }
 

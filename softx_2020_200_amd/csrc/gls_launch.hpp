@@ -4,6 +4,9 @@
 
 namespace gls {
 
+// deterministic scatter of the per-cell kernels' element vectors (P.ev): y = per-node sums in slot order
+hipError_t gather_element_vectors(double *y, const double *ev, const int64_t *voff, const int64_t *vslot, int64_t nv,
+                                  const int64_t *poff, const int64_t *pslot, int64_t np, int dim, hipStream_t s);
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s);
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);

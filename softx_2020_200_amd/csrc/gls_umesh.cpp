@@ -1129,6 +1129,7 @@ struct FESpaceImpl {
   std::vector<std::array<int64_t, 8>> cell_verts, t_verts;  // vertex ids of the active cells / all records
   std::vector<V3> verts;
   std::map<EKey, int64_t> line_mid, face_mid;
+  std::vector<int> face_bid;  // [n_cells][2 dim] boundary id of each cell face, -1 interior
 };
 
 using HangLines = std::map<int64_t, std::vector<std::pair<int64_t, double>>>;
@@ -1572,6 +1573,12 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
   }
   F.cell_verts = m.cells;
   for (const auto &h : m.tree) F.t_verts.push_back(h.v);
+  F.face_bid.assign((size_t)(nc * 2 * dim), -1);
+  for (int64_t c = 0; c < nc; ++c)
+    for (int f = 0; f < 2 * dim; ++f) {
+      auto b = m.bface.find(face_key_v(dim, m.cells[(size_t)c], f / 2, f & 1));
+      if (b != m.bface.end()) F.face_bid[(size_t)(c * 2 * dim + f)] = b->second;
+    }
   F.verts = m.X;
   F.line_mid = m.line_mid;
   F.face_mid = m.face_mid;
@@ -2028,6 +2035,47 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
       ++cnt;
     }
   *n_pieces = cnt;
+  return GLS_OK;
+}
+
+// Node normals of the boundary faces with id `boundary_id` (VectorTools::
+// compute_no_normal_flux_constraints, gls_navier_stokes.cc:100-110): at every velocity node on such a
+// face, the normalised sum of the adjacent faces' outward unit normals (J^-T e_d of the cell's
+// MappingQ at the node); zero elsewhere. normals: [n_vnodes][dim] host array.
+int gls_fe_space_boundary_normals(const gls_fe_space *sp, int boundary_id, double *normals) {
+  if (!sp || !sp->impl_ || !normals) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_boundary_normals: arguments");
+  const FESpaceImpl &F = *static_cast<const FESpaceImpl *>(sp->impl_);
+  const int dim = sp->dim, k = sp->k, k1 = k + 1, nn = dim == 2 ? k1 * k1 : k1 * k1 * k1;
+  std::fill(normals, normals + sp->n_vnodes * dim, 0.0);
+  for (int64_t c = 0; c < sp->n_cells; ++c)
+    for (int f = 0; f < 2 * dim; ++f) {
+      if (F.face_bid[(size_t)(c * 2 * dim + f)] != boundary_id) continue;
+      const int d = f / 2, s = f & 1;
+      for (int a = 0; a < nn; ++a) {
+        const int ia[3] = {a % k1, (a / k1) % k1, a / (k1 * k1)};
+        if (ia[d] != s * k) continue;
+        double xi[3] = {0, 0, 0}, J[3][3], e[3] = {0, 0, 0}, n[3] = {0, 0, 0};
+        for (int t = 0; t < dim; ++t) xi[t] = (double)ia[t] / k;
+        jacobian(*sp, c, xi, J);
+        // J^-T e_d = (row d of J^-1)^T: solve J^T y = e_d
+        double JT[3][3];
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) JT[i][j] = J[j][i];
+        e[d] = s ? 1.0 : -1.0;
+        solve3(JT, e, n, dim);
+        double l = 0;
+        for (int t = 0; t < dim; ++t) l += n[t] * n[t];
+        l = std::sqrt(l);
+        const int64_t node = sp->cell_vnodes[c * nn + a];
+        for (int t = 0; t < dim; ++t) normals[node * dim + t] += n[t] / l;
+      }
+    }
+  for (int64_t v = 0; v < sp->n_vnodes; ++v) {
+    double l = 0;
+    for (int t = 0; t < dim; ++t) l += normals[v * dim + t] * normals[v * dim + t];
+    if (l > 0)
+      for (int t = 0; t < dim; ++t) normals[v * dim + t] /= std::sqrt(l);
+  }
   return GLS_OK;
 }
 

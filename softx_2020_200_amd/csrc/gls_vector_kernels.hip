@@ -214,6 +214,37 @@ __global__ void k_set_indexed(double *y, const int64_t *idx, const double *vals,
 
 int multidot_work_size() { return (kDotChunk + 1) * kMaxBlocks; }
 
+// y[node] = sum over the node's element-vector slots in ascending order (deterministic scatter of
+// the per-cell kernels): velocity node n, component c: ev[slot + c] for slot in vslot[voff[n]..);
+// pressure node q: ev[slot] for slot in pslot[poff[q]..)
+__global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ ev, const int64_t *__restrict__ voff,
+                            const int64_t *__restrict__ vslot, int64_t nv, const int64_t *__restrict__ poff,
+                            const int64_t *__restrict__ pslot, int64_t np, int dim) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nv) {
+    double acc[3] = {0., 0., 0.};
+    for (int64_t j = voff[i]; j < voff[i + 1]; ++j) {
+      const double *e = ev + vslot[j];
+      for (int c = 0; c < dim; ++c) acc[c] += e[c];
+    }
+    for (int c = 0; c < dim; ++c) y[i * dim + c] = acc[c];
+  } else if (i < nv + np) {
+    const int64_t q = i - nv;
+    double acc = 0.;
+    for (int64_t j = poff[q]; j < poff[q + 1]; ++j) acc += ev[pslot[j]];
+    y[dim * nv + q] = acc;
+  }
+}
+
+hipError_t gather_element_vectors(double *y, const double *ev, const int64_t *voff, const int64_t *vslot, int64_t nv,
+                                  const int64_t *poff, const int64_t *pslot, int64_t np, int dim, hipStream_t s) {
+  const int64_t n = nv + np;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_ev, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, y, ev, voff, vslot, nv, poff,
+                     pslot, np, dim);
+  return hipGetLastError();
+}
+
 hipError_t vec_fill(double *x, int64_t n, double a, hipStream_t s) {
   hipLaunchKernelGGL(k_fill, dim3(grid_for(n)), dim3(kBlock), 0, s, x, n, a);
   return hipGetLastError();

@@ -42,7 +42,7 @@ EXPORTS = [
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
     "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
-    "gls_kelly_estimate_mapped",
+    "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals",
 ]
 
 
@@ -189,6 +189,7 @@ def load():
     L.gls_umesh_prepare.argtypes = [vp, pi32, pi32]
     L.gls_umesh_adapt.argtypes = [vp, pi32, pi32]
     L.gls_fe_space_kelly_faces.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(i64), pi32, pi32, d, d, d, d]
+    L.gls_fe_space_boundary_normals.argtypes = [C.POINTER(FESpace), C.c_int, d]
     L.gls_kelly_estimate_mapped.argtypes = [vp, vp, C.c_int, i64, C.c_int, pi32, pi32, d, d, d, d, vp]
     _lib = L
     return L
@@ -711,6 +712,18 @@ class GLSContext:
               "gls_kelly_estimate_faces")
         return out
 
+    def kelly_estimate_mapped(self, sol, variable, faces, out=None):
+        """Kelly indicator on a mapped mesh (gls_kelly_estimate_mapped); faces from
+        FESpaceHandle.kelly_faces(n_q + 1)."""
+        import torch
+        out = torch.empty(self.n_cells, dtype=torch.float64, device=sol.device) if out is None else out
+        f = {k: np.ascontiguousarray(v) for k, v in faces.items() if isinstance(v, np.ndarray)}
+        p32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
+        check(self.L.gls_kelly_estimate_mapped(self.h, _ptr(sol), int(variable), len(f["ca"]), int(faces["nqf"]),
+                                               p32(f["ca"]), p32(f["cb"]), _dp(f["xi"]), _dp(f["g"]), _dp(f["jxw"]),
+                                               _dp(f["diam"]), _ptr(out)), "gls_kelly_estimate_mapped")
+        return out
+
     def mg_transfer(self, level, direction, v, out):
         """Restrict (direction 0: level -> level+1) or prolongate (1: level+1 -> level) a device vector."""
         check(self.L.gls_mg_transfer(self.h, int(level), int(direction), _ptr(v), _ptr(out)), "gls_mg_transfer")
@@ -861,6 +874,11 @@ class FESpaceHandle:
         vec = np.ascontiguousarray(vec, dtype=np.float64)
         out = np.zeros(self.data["dim"] * self.data["n_vnodes"] + self.data["n_pnodes"])
         check(self.L.gls_fe_space_transfer(old.ptr, self.ptr, _dp(vec), _dp(out)), "gls_fe_space_transfer")
+        return out
+
+    def boundary_normals(self, boundary_id):
+        out = np.zeros((self.data["n_vnodes"], self.data["dim"]))
+        check(self.L.gls_fe_space_boundary_normals(self.ptr, int(boundary_id), _dp(out)), "gls_fe_space_boundary_normals")
         return out
 
     def kelly_faces(self, nq):

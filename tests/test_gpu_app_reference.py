@@ -108,3 +108,17 @@ def test_reference_tgv_sdirk_cases(tmp_path, method):
         assert pick(out.stdout, key) == pick(ref, key), (key, pick(out.stdout, key), pick(ref, key))
     e, r = float(pick(out.stdout, "L2 error velocity")[0]), float(pick(ref, "L2 error velocity")[0])
     assert abs(e - r) <= (3e-4 if method == "sdirk3" else 1e-5) * r, (e, r)
+
+
+@pytest.mark.gpu
+def test_reference_cylinder_kelly_adaptation(tmp_path):
+    """applications_tests/gls_navier_stokes_2d/cylinder_gls (gmsh cylinder_structured.msh, Q1-Q1, slip
+    walls, 3 steady Kelly adaptations: fraction type number, refine 0.3 / coarsen 0.1, max 70000
+    cells, max level 5): Kelly with MappingQ face pieces on hanging faces, the p::d fixed-number
+    thresholds, deal.II mesh smoothing, the unstructured hierarchy's refine / coarsen / balance and
+    the hanging-node DoF count reproduce the reference's active-cell and DoF counts of every cycle
+    (the force summaries are out of scope)."""
+    ref = open(os.path.join(CASES, "cylinder_gls.output")).read()
+    out = run_case(tmp_path, "cylinder_gls", 2)
+    ours, theirs = setup_lines(out), setup_lines(ref)
+    assert ours == theirs, (ours, theirs)
