@@ -1153,7 +1153,7 @@ struct Solver {
     // (the reference's ILU-GMRES; not with hanging nodes) unless --precond jacobi. The reference's
     // iteration caps are tuned for ILU(k) / AMG, so the caps and restart are raised without the
     // V-cycle (ILU(0) is weaker than the reference's ILU(1); Jacobi much weaker).
-    if (mg_levels.empty() && use_ilu && m.hang_dofs.empty() && ilu_ctx != ctx) {
+    if (mg_levels.empty() && use_ilu && ilu_ctx != ctx) {
       ck(gls_ilu_attach(ctx, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;
     }

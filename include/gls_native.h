@@ -212,7 +212,9 @@ int gls_mg_detach(gls_ctx *ctx);
  * reference's 'linear solver/method = gmres' with 'ilu preconditioner absolute / relative tolerance';
  * fill level 0): the Jacobian is probed from the device operator into CSR with distance-2-colored
  * unit vectors once per Jacobian state, its diagonal perturbed like Ifpack (a_ii <- rthresh a_ii +
- * sign(a_ii) athresh) and factored by rocSPARSE. Single rank, no hanging nodes, no multigrid. */
+ * sign(a_ii) athresh) and factored by rocSPARSE. Single rank, no multigrid; with hanging-node lines the
+ * pattern is that of the condensed operator (hanging nodes replaced by their masters, hanging rows
+ * diagonal). */
 int gls_ilu_attach(gls_ctx *ctx, double athresh, double rthresh);
 int gls_ilu_detach(gls_ctx *ctx);
 int gls_ilu_info(const gls_ctx *ctx, int64_t *nnz, int *n_probes);

@@ -379,6 +379,7 @@ struct gls_ctx {
     DevBuf<double> tw;
     DevBuf<uint8_t> hmask;                             // hanging velocity components per node
     DevBuf<double> vbuf;                               // C v for J.v
+    std::vector<int64_t> h_dof, h_off, h_master;       // host copy of the lines (ILU sparsity)
   } hang;
   // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
   struct Lattice {
@@ -1552,6 +1553,10 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
       tdof[(size_t)slot] = dofs[i];
       tw[(size_t)slot] = ow[(size_t)j];
     }
+  c->hang.h_dof.assign(dofs, dofs + n);
+  c->hang.h_off.assign(off, off + n + 1);
+  c->hang.h_master.assign(masters, masters + nm);
+  if (n == 0) c->hang.h_off.assign(1, 0);
   std::vector<uint8_t> hm((size_t)c->n_vnodes, 0);
   std::vector<int64_t> con;  // zero_constraints: Dirichlet + hanging
   for (int64_t d = 0; d < N; ++d) {
@@ -2864,7 +2869,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   GLS_TRY(check_ctx(c));
   auto &I = c->ilu;
   if (c->dist.on) return set_err(GLS_EINVAL, "gls_ilu_attach: single-rank contexts only");
-  if (c->hang.on) return set_err(GLS_EINVAL, "gls_ilu_attach: not with hanging-node constraints");
   if (c->mg.on) return set_err(GLS_EINVAL, "gls_ilu_attach: a multigrid preconditioner is attached");
   const int dim = c->dim, nvc = gls::ipow(c->k + 1, dim);
   const bool sep = c->cell_pnodes.p != nullptr;
@@ -2880,27 +2884,63 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   auto cell_node = [&](int64_t cell, int a) -> int64_t {
     return a < nvc ? cv[(size_t)(cell * nvc + a)] : nv + cp[(size_t)(cell * npc + a - nvc)];
   };
+  // hanging nodes (unified numbering) and their master nodes: the condensed operator C^T K C couples
+  // the masters of a cell's hanging nodes with the cell's other nodes; a hanging row is D_c only
+  const int64_t nvd = (int64_t)dim * nv;
+  std::vector<char> hnode((size_t)nu, 0);
+  std::vector<std::vector<int64_t>> hmas;
+  if (c->hang.on) {
+    hmas.resize((size_t)nu);
+    auto unode = [&](int64_t d) { return d < nvd ? d / dim : (sep ? nv + (d - nvd) : d - nvd); };
+    for (size_t i = 0; i + 1 < c->hang.h_off.size(); ++i) {
+      const int64_t x = unode(c->hang.h_dof[i]);
+      hnode[(size_t)x] = 1;
+      for (int64_t j = c->hang.h_off[i]; j < c->hang.h_off[i + 1]; ++j) {
+        const int64_t y = unode(c->hang.h_master[(size_t)j]);
+        if (std::find(hmas[(size_t)x].begin(), hmas[(size_t)x].end(), y) == hmas[(size_t)x].end()) hmas[(size_t)x].push_back(y);
+      }
+    }
+  }
+  // effective nodes of each cell: its nodes with the hanging ones replaced by their masters
+  std::vector<int64_t> effoff((size_t)nc + 1, 0), eff;
+  {
+    std::vector<int64_t> buf;
+    for (int64_t e = 0; e < nc; ++e) {
+      buf.clear();
+      for (int a = 0; a < ncn; ++a) {
+        const int64_t x = cell_node(e, a);
+        if (!hnode[(size_t)x]) buf.push_back(x);
+        else buf.insert(buf.end(), hmas[(size_t)x].begin(), hmas[(size_t)x].end());
+      }
+      std::sort(buf.begin(), buf.end());
+      buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+      eff.insert(eff.end(), buf.begin(), buf.end());
+      effoff[(size_t)e + 1] = (int64_t)eff.size();
+    }
+  }
   std::vector<int64_t> ncoff((size_t)nu + 1, 0), nccell;
-  for (int64_t e = 0; e < nc; ++e)
-    for (int a = 0; a < ncn; ++a) ++ncoff[(size_t)cell_node(e, a) + 1];
+  for (int64_t t = 0; t < (int64_t)eff.size(); ++t) ++ncoff[(size_t)eff[(size_t)t] + 1];
   for (int64_t x = 0; x < nu; ++x) ncoff[(size_t)x + 1] += ncoff[(size_t)x];
   nccell.resize((size_t)ncoff[(size_t)nu]);
   {
     std::vector<int64_t> fill(ncoff.begin(), ncoff.end() - 1);
     for (int64_t e = 0; e < nc; ++e)
-      for (int a = 0; a < ncn; ++a) nccell[(size_t)fill[(size_t)cell_node(e, a)]++] = e;
+      for (int64_t t = effoff[(size_t)e]; t < effoff[(size_t)e + 1]; ++t) nccell[(size_t)fill[(size_t)eff[(size_t)t]]++] = e;
   }
-  // N1(x): nodes of the cells holding x (sorted, unique)
+  // N1(x): effective nodes of the cells holding x (sorted, unique); a hanging node: itself only
   std::vector<int64_t> n1off((size_t)nu + 1, 0), n1;
   {
     std::vector<int64_t> stamp((size_t)nu, -1), buf;
     for (int64_t x = 0; x < nu; ++x) {
       buf.clear();
-      for (int64_t t = ncoff[(size_t)x]; t < ncoff[(size_t)x + 1]; ++t)
-        for (int a = 0; a < ncn; ++a) {
-          const int64_t y = cell_node(nccell[(size_t)t], a);
+      if (hnode[(size_t)x]) buf.push_back(x);
+      for (int64_t t = ncoff[(size_t)x]; t < ncoff[(size_t)x + 1]; ++t) {
+        const int64_t e = nccell[(size_t)t];
+        for (int64_t u = effoff[(size_t)e]; u < effoff[(size_t)e + 1]; ++u) {
+          const int64_t y = eff[(size_t)u];
           if (stamp[(size_t)y] != x) { stamp[(size_t)y] = x; buf.push_back(y); }
         }
+      }
       std::sort(buf.begin(), buf.end());
       n1.insert(n1.end(), buf.begin(), buf.end());
       n1off[(size_t)x + 1] = (int64_t)n1.size();

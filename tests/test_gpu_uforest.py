@@ -112,3 +112,34 @@ def test_per_cell_operators_bitwise_reproducible():
     for _ in range(3):
         assert np.array_equal(ctx.residual().cpu().numpy(), r0)
         assert np.array_equal(ctx.jacobian_apply(cuda(v)).cpu().numpy(), j0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,k,kp", [("square", 1, 1), ("square", 2, 1), ("rect3d", 2, 1), ("cylshell", 1, 1)])
+def test_ilu_probed_matrix_with_hanging_nodes(name, k, kp):
+    """gls_ilu_attach on an adapted mapped mesh: the probed CSR (the condensed operator's pattern:
+    hanging nodes replaced by their masters, hanging rows diagonal) == the oracle's assembled,
+    hanging-condensed system matrix; ILU(0)-GMRES then solves the Newton step."""
+    case = [c for c in CASES if c[0] == name][0]
+    m, h = adapted_space(*case[:3], k, kp)
+    sp = h.data
+    p = MappedProblem(sp, viscosity=0.05, scheme="bdf1", time_steps=(0.05,) * 4)
+    lines = dof_lines(sp)
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    p.set_dirichlet([("noslip", 0, None)])
+    rng = np.random.default_rng(3)
+    u = p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs))
+    u1 = p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs))
+    A, _ = Oracle(p).matrix_and_rhs(u, u1)
+    ctx = context_for(p)
+    ctx.set_state(cuda(u), cuda(u1))
+    nnz, nprobe = ctx.attach_ilu()
+    M = ctx.ilu_matrix()
+    A = A.tocsr()
+    d = (M - A).tocsr()
+    assert np.abs(d.data).max() <= 1e-12 * np.abs(A.data).max() if d.nnz else True
+    rhs = ctx.residual()
+    x, its, res, ok = ctx.solve_linear(rhs, None, max_iterations=400, restart=60, relative_residual=1e-10,
+                                       minimum_residual=1e-14)
+    assert ok and its < 400, (its, res)
