@@ -339,7 +339,14 @@ struct gls_ctx {
     std::vector<int> nbrs;
     std::vector<int64_t> soff, roff;
     DevBuf<double> own_send, own_recv, own_red;
+    // overlap of the J.v ghost import with the interior bricks (RCCL transport): exchange stream
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   } dist;
+  // brick split for the overlapped J.v: bricks touching a ghost or exported node first
+  // (split[0 .. split_bnd)), then the interior bricks (split[split_bnd .. split_bnd + split_int))
+  DevBuf<int32_t> split;
+  int split_bnd = 0, split_int = 0;
   // assembled ILU(0) preconditioner (gls_ilu_attach; the reference's setup_ILU,
   // gls_navier_stokes.cc:1161-1176): the Jacobian is assembled into CSR by probing the matrix-free
   // operator with distance-2-colored unit vectors, perturbed on the diagonal like Ifpack (athresh,
@@ -483,6 +490,9 @@ struct gls_ctx {
 
   ~gls_ctx() {
     for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+    if (dist.ev_ready) (void)hipEventDestroy(dist.ev_ready);
+    if (dist.ev_done) (void)hipEventDestroy(dist.ev_done);
+    if (dist.xstream) (void)hipStreamDestroy(dist.xstream);
     if (own_stream && stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -885,6 +895,47 @@ hipError_t slab_sum(gls_ctx *c, double *y) {
                              c->n_vnodes, y, c->stream);
 }
 
+int rccl_exchange_on(gls_ctx *c, int phase, hipStream_t stream);  // RCCL transport (below)
+
+// the brick split: a brick is a boundary brick when one of its cells holds a flagged node (ghost or
+// exported); boundary bricks first, then interior ones, each in ascending (Morton) order
+int build_brick_split(gls_ctx *c, const std::vector<char> &flag) {
+  const int nvc = gls::ipow(c->k + 1, 3), nb = c->n_cells / 8;
+  std::vector<int32_t> cv((size_t)c->n_cells * nvc);
+  HIP_TRY(hipMemcpy(cv.data(), c->cell_vnodes.p, cv.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> bnd, inn;
+  for (int b = 0; b < nb; ++b) {
+    bool on = false;
+    for (size_t e = (size_t)b * 8 * nvc; e < (size_t)(b + 1) * 8 * nvc && !on; ++e) on = flag[(size_t)cv[e]] != 0;
+    (on ? bnd : inn).push_back(b);
+  }
+  c->split_bnd = (int)bnd.size();
+  c->split_int = (int)inn.size();
+  bnd.insert(bnd.end(), inn.begin(), inn.end());
+  return c->split.upload(bnd.data(), std::max<size_t>(bnd.size(), 1));
+}
+
+// J.v launched as two brick subsets (boundary, then interior) with the ghost import between them:
+// the RCCL transport imports on the exchange stream while the interior bricks run
+// (GLS_NO_OVERLAP=1: off); GLS_SPLIT_TEST=m on a single-GPU context splits at "bricks b % m == 0"
+// with no exchange, for the bitwise test of the split launch
+bool split_jv_enabled(gls_ctx *c) {
+  if (!c->use_brick || !c->use_qdata || c->use_colors || c->hang.on || !gls::brick_subset_supported(c->k)) return false;
+  if (c->dist.on) return c->dist.comm != nullptr && c->split.p && !std::getenv("GLS_NO_OVERLAP");
+  const char *t = std::getenv("GLS_SPLIT_TEST");
+  if (!t || std::atoi(t) < 1) return false;
+  if (!c->split.p) {
+    const int m = std::atoi(t), nb = c->n_cells / 8;
+    std::vector<int32_t> bnd, inn;
+    for (int b = 0; b < nb; ++b) (b % m == 0 ? bnd : inn).push_back(b);
+    c->split_bnd = (int)bnd.size();
+    c->split_int = (int)inn.size();
+    bnd.insert(bnd.end(), inn.begin(), inn.end());
+    if (c->split.upload(bnd.data(), std::max<size_t>(bnd.size(), 1)) != GLS_OK) return false;
+  }
+  return true;
+}
+
 // slots of every node in the per-cell element vectors [n_cells][NV*dim + NP], ascending (cell, local
 // node) order: the fixed summation order of gather_element_vectors
 int ensure_element_maps(gls_ctx *c) {
@@ -920,7 +971,8 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
-  if (mode == gls::MODE_JV) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
+  const bool split_jv = mode == gls::MODE_JV && split_jv_enabled(c);
+  if (mode == gls::MODE_JV && !split_jv) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
   gls::OpParams P = make_params(c, mode != gls::MODE_RESIDUAL);
   if (mode == gls::MODE_JV && c->use_brick && c->use_qdata) {
     GLS_TRY(ensure_qdata(c));
@@ -957,8 +1009,31 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!col && !P.slab && !P.ev) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
-    if (brick) HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
-    else HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+    if (brick && split_jv && mode == gls::MODE_JVQ) {
+      auto &D = c->dist;
+      double *vv = const_cast<double *>(v);
+      const int64_t voff = 3 * (int64_t)c->n_vnodes;
+      if (D.on) {  // ghost import of v on the exchange stream, ordered after v's producer
+        HIP_TRY(hipEventRecord(D.ev_ready, c->stream));
+        HIP_TRY(hipStreamWaitEvent(D.xstream, D.ev_ready, 0));
+        HIP_TRY(gls::vec_pack_nodes(vv, D.send_nodes.p, D.n_send, voff, D.send_buf, D.xstream));
+        if (rccl_exchange_on(c, 0, D.xstream) != 0) return set_err(GLS_ECOMM, "ghost import exchange failed");
+        HIP_TRY(gls::vec_unpack_nodes(vv, D.recv_nodes.p, D.n_recv, voff, D.recv_buf, 0, D.xstream));
+        HIP_TRY(hipEventRecord(D.ev_done, D.xstream));
+      }
+      gls::OpParams Q = P;  // interior bricks read no ghost value
+      Q.subset = c->split.p + c->split_bnd;
+      Q.subset_n = c->split_int;
+      if (Q.subset_n > 0) HIP_TRY(gls::launch_brick_kernel(c->k, mode, Q, c->tables, c->stream));
+      if (D.on) HIP_TRY(hipStreamWaitEvent(c->stream, D.ev_done, 0));
+      Q.subset = c->split.p;
+      Q.subset_n = c->split_bnd;
+      if (Q.subset_n > 0) HIP_TRY(gls::launch_brick_kernel(c->k, mode, Q, c->tables, c->stream));
+    } else if (brick) {
+      HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
+    } else {
+      HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+    }
   }
   if (P.ev)
     HIP_TRY(gls::gather_element_vectors(y, c->ev.p, c->ev_voff.p, c->ev_vslot.p, c->n_vnodes, c->ev_poff.p,
@@ -1337,6 +1412,12 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  if (c->use_brick && gls::brick_subset_supported(c->k)) {  // boundary / interior bricks (overlapped J.v)
+    std::vector<char> flag((size_t)c->n_vnodes, 0);
+    for (int64_t i = 0; i < ns; ++i) flag[(size_t)send_nodes[i]] = 1;
+    for (int64_t i = 0; i < nr; ++i) flag[(size_t)recv_nodes[i]] = 1;
+    GLS_TRY(build_brick_split(c, flag));
+  }
   return GLS_OK;
 }
 
@@ -3186,8 +3267,12 @@ struct gls_rccl {
   int rank = 0, world = 1;
 };
 namespace {
-int rccl_exchange(void *user, int phase) {
+int rccl_exchange(void *user, int phase) { return rccl_exchange_on(static_cast<gls_ctx *>(user), phase, static_cast<gls_ctx *>(user)->stream); }
+int rccl_allreduce(void *user, double *buf, int n) {
   gls_ctx *c = static_cast<gls_ctx *>(user);
+  return ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, c->dist.comm, c->stream) == ncclSuccess ? 0 : -1;
+}
+int rccl_exchange_on(gls_ctx *c, int phase, hipStream_t stream) {
   auto &D = c->dist;
   // phase 0 (import): send send_buf segments (owned nodes others ghost), receive into recv_buf;
   // phase 1 (export-add): the reverse (ghost partial sums back to their owners)
@@ -3196,14 +3281,10 @@ int rccl_exchange(void *user, int phase) {
   if (ncclGroupStart() != ncclSuccess) return -1;
   for (size_t i = 0; i < D.nbrs.size(); ++i) {
     const size_t ns = (size_t)(4 * (so[i + 1] - so[i])), nr = (size_t)(4 * (ro[i + 1] - ro[i]));
-    if (ns && ncclSend(sb + 4 * so[i], ns, ncclDouble, D.nbrs[i], D.comm, c->stream) != ncclSuccess) return -1;
-    if (nr && ncclRecv(rb + 4 * ro[i], nr, ncclDouble, D.nbrs[i], D.comm, c->stream) != ncclSuccess) return -1;
+    if (ns && ncclSend(sb + 4 * so[i], ns, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
+    if (nr && ncclRecv(rb + 4 * ro[i], nr, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
   }
   return ncclGroupEnd() == ncclSuccess ? 0 : -1;
-}
-int rccl_allreduce(void *user, double *buf, int n) {
-  gls_ctx *c = static_cast<gls_ctx *>(user);
-  return ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, c->dist.comm, c->stream) == ncclSuccess ? 0 : -1;
 }
 }  // namespace
 
@@ -3251,6 +3332,11 @@ extern "C" int gls_dist_attach_rccl(gls_ctx *c, gls_rccl *r, int64_t n_owned_nod
   GLS_TRY(gls_dist_attach(c, n_owned_nodes, n_nbrs, send_offsets, send_nodes, recv_offsets, recv_nodes, D.own_send.p,
                           D.own_recv.p, D.own_red.p, rccl_exchange, rccl_allreduce, c));
   D.comm = r->comm;
+  if (!D.xstream) {
+    HIP_TRY(hipStreamCreateWithFlags(&D.xstream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_ready, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_done, hipEventDisableTiming));
+  }
   D.nbrs.assign(nbr_ranks, nbr_ranks + n_nbrs);
   D.soff.assign(send_offsets, send_offsets + n_nbrs + 1);
   D.roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);

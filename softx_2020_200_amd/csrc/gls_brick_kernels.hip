@@ -243,6 +243,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks)
                     : colored ? P.bricks[P.color_off[P.color] +
                                          xcd_swizzle((int)blockIdx.x, P.color_off[P.color + 1] - P.color_off[P.color])]
+                    : P.subset ? P.subset[xcd_swizzle((int)blockIdx.x, P.subset_n)]
                               : xcd_swizzle((int)blockIdx.x, n_bricks);
   const int64_t unit_dof = (CACHED && P.n_probe > 0) ? P.probe_base + pj : -1;
   double *const Yout = (CACHED && P.n_probe > 0)
@@ -892,7 +893,7 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   if (!colored) Q.bricks = nullptr;
   for (int col = 0; col < nc; ++col) {
     Q.color = col;
-    const int nb = colored ? P.color_off[col + 1] - P.color_off[col] : n_bricks;
+    const int nb = colored ? P.color_off[col + 1] - P.color_off[col] : P.subset ? P.subset_n : n_bricks;
     if (nb <= 0) continue;
     if (mode == MODE_JV)
       hipLaunchKernelGGL((gls_brick_kernel<K, MODE_JV>), dim3(nb), dim3(C::THREADS), lds, s, Q, T);
@@ -1065,6 +1066,7 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
 }
 bool brick_fused_jacobi_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 bool brick_colors_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
+bool brick_subset_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 
 size_t brick_qdata_size(int k, int n_cells) {
   if (brick_impl(k) == 1) return brick_wave_qdata_size(k, n_cells);

@@ -57,6 +57,8 @@ struct OpParams {
   int n_probe;                // MODE_JVQ probing: > 0 -> block b computes J e_(probe_base + b / n_bricks)
   int64_t probe_base;         //   into y + (b / n_bricks) * n_dofs (v unused)
   double *y;                  // output (brick-interior nodes: plain stores; others: slab or atomics)
+  const int32_t *subset;      // brick kernels: launch only bricks subset[0 .. subset_n) (slab scheme), nullptr = all
+  int subset_n;
   double *ev;                 // per-cell kernels: element vectors [n_cells][NV*dim + NP] instead of atomics
                               //   into y (summed per node in a fixed order by gather_element_vectors)
   double *slab;               // brick path: [n_bricks][NBND][4] partial sums of brick-boundary nodes

@@ -35,6 +35,7 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
 bool brick_fused_jacobi_supported(int k);  // the selected brick kernel honours OpParams::jx and ::slabf
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 bool brick_colors_supported(int k);  // colored brick launches (OpParams::bricks) available
+bool brick_subset_supported(int k);  // brick-subset launches (OpParams::subset) available
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s);
 
 // ---- BLAS-1 style kernels on device vectors (gls_vector_kernels.hip)

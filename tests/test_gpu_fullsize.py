@@ -117,3 +117,25 @@ def test_fullsize_f32_smoother_operator(cavity):
     jv = prob.ctx.jacobian_apply(v).clone()
     jf = prob.ctx.jacobian_apply_f32(v)
     assert _relmax(jf, jv) < 2e-5
+
+
+def test_fullsize_split_brick_launch_bitwise(cavity, monkeypatch):
+    """The overlapped multi-GPU J.v launches the bricks as two subsets (bricks touching ghost / exported
+    nodes, then the interior ones, with the ghost import between them). Each brick's partial sums go to
+    its own slab slots and the slab sums run in a fixed order, so the split launch is bitwise the
+    single launch: GLS_SPLIT_TEST=m splits a single-GPU context at bricks b % m == 0."""
+    from softx_2020_200_amd.problem import build_context
+    prob, (u, u1, u2, v, _) = cavity
+    k, n, scheme, nu = prob.cfg
+    if k != 2:
+        pytest.skip("brick subsets: workgroup-per-brick kernel (Q2); Q1 runs the wave kernel")
+    ref = prob.ctx.jacobian_apply(v).clone()
+    monkeypatch.setenv("GLS_SPLIT_TEST", "3")
+    ctx = build_context(prob.mesh, viscosity=nu, vnode_mask=prob.vnode_mask)
+    ctx.set_time(scheme, DT)
+    ctx.set_dirichlet(prob.dir_dofs, prob.dir_vals)
+    ctx.set_state(u, u1, u2)
+    got = ctx.jacobian_apply(v).clone()
+    monkeypatch.delenv("GLS_SPLIT_TEST")
+    del ctx
+    assert bool((got == ref).all())
