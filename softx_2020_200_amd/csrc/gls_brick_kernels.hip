@@ -1015,14 +1015,21 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
   double s[4] = {0., 0., 0., 0.};
-  for (int j = off[i]; j < off[i + 1]; ++j) {
-    double a, b, c, d;
-    SlabQuad<S>::load(slab + (int64_t)slots[j] * 4, a, b, c, d);
-    s[0] += a;
-    s[1] += b;
-    s[2] += c;
-    s[3] += d;
-  }
+  // a node lies on at most 8 bricks: issue every slot load before the (ordered) adds, so a thread
+  // keeps up to 8 independent gathers in flight instead of one dependent chain
+  const int j0 = off[i], nj = off[i + 1] - j0;
+  double q[8][4];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < nj) SlabQuad<S>::load(slab + (int64_t)slots[j0 + t] * 4, q[t][0], q[t][1], q[t][2], q[t][3]);
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < nj) {
+      s[0] += q[t][0];
+      s[1] += q[t][1];
+      s[2] += q[t][2];
+      s[3] += q[t][3];
+    }
   const int64_t node = nodes[i];
   const int64_t gi[4] = {node * 3, node * 3 + 1, node * 3 + 2, voff + node};
   if constexpr (J) {
