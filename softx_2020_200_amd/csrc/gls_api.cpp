@@ -562,8 +562,6 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   }
   std::vector<int32_t> nodes, off{0};
   std::vector<int32_t> start((size_t)d->n_vnodes + 1, 0);
-  for (int64_t n = 0; n < d->n_vnodes; ++n)  // k_slab_sum keeps at most 8 slots of a node in flight
-    if (cnt[(size_t)n + 1] > 8) return GLS_OK;  // (tiny periodic meshes): no slab, FP64 atomics
   for (int64_t n = 0; n < d->n_vnodes; ++n) {
     start[(size_t)n + 1] = start[(size_t)n] + cnt[(size_t)n + 1];
     if (cnt[(size_t)n + 1] > 0) {

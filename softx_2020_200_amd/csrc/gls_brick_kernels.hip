@@ -239,11 +239,18 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   const int pj = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x / n_bricks) : 0;
   // XCD-aware order (blocks b, b+8, b+16, ... share an XCD): each XCD walks a contiguous Morton
   // range of bricks, so the nodes neighbouring bricks share stay in that XCD's L2
+#ifdef GLS_BRICK_COLORS_BUILD
   const bool colored = P.bricks != nullptr && !(CACHED && P.n_probe > 0);
+#else
+  // colored brick launches (the measured-slower experiment, profiles/r02_brick_colors_ab.txt) are
+  // compiled only with -DGLS_BRICK_COLORS_BUILD: their scatter branch costs the FP32 smoother kernel
+  // 4 extra VGPR spills (2.13 -> 2.80 ms at 128^3)
+  constexpr bool colored = false;
+#endif
   const int brick = (CACHED && P.n_probe > 0) ? (int)(blockIdx.x % n_bricks)
                     : colored ? P.bricks[P.color_off[P.color] +
                                          xcd_swizzle((int)blockIdx.x, P.color_off[P.color + 1] - P.color_off[P.color])]
-                    : P.subset ? P.subset[xcd_swizzle((int)blockIdx.x, P.subset_n)]
+                    : (std::is_same<Real, double>::value && P.subset) ? P.subset[xcd_swizzle((int)blockIdx.x, P.subset_n)]
                               : xcd_swizzle((int)blockIdx.x, n_bricks);
   const int64_t unit_dof = (CACHED && P.n_probe > 0) ? P.probe_base + pj : -1;
   double *const Yout = (CACHED && P.n_probe > 0)
@@ -847,6 +854,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     } else if (interior) {
       if (MODE == MODE_JVQ && (P.jx || P.rb)) complete((double)s);
       else Yout[gi] = s;
+#ifdef GLS_BRICK_COLORS_BUILD
     } else if (colored) {  // running sum across colors, in color order
       const unsigned cm = P.ncolor[node];
       const bool first = (cm & ((1u << P.color) - 1u)) == 0u, last = (cm >> (P.color + 1)) == 0u;
@@ -854,6 +862,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       if (!first) tot += P.acc[gi];
       if (last) complete(tot);
       else P.acc[gi] = tot;
+#endif
     } else if (use_slab) {  // brick-boundary node: this brick's partial sum, summed per node by k_slab_sum
       const int64_t si = ((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4 + fld;
       if (std::is_same<Real, float>::value && P.slabf) P.slabf[si] = (float)s;
@@ -1015,21 +1024,14 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
   double s[4] = {0., 0., 0., 0.};
-  // a node lies on at most 8 bricks: issue every slot load before the (ordered) adds, so a thread
-  // keeps up to 8 independent gathers in flight instead of one dependent chain
-  const int j0 = off[i], nj = off[i + 1] - j0;
-  double q[8][4];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-    if (t < nj) SlabQuad<S>::load(slab + (int64_t)slots[j0 + t] * 4, q[t][0], q[t][1], q[t][2], q[t][3]);
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-    if (t < nj) {
-      s[0] += q[t][0];
-      s[1] += q[t][1];
-      s[2] += q[t][2];
-      s[3] += q[t][3];
-    }
+  for (int j = off[i]; j < off[i + 1]; ++j) {
+    double a, b, c, d;
+    SlabQuad<S>::load(slab + (int64_t)slots[j] * 4, a, b, c, d);
+    s[0] += a;
+    s[1] += b;
+    s[2] += c;
+    s[3] += d;
+  }
   const int64_t node = nodes[i];
   const int64_t gi[4] = {node * 3, node * 3 + 1, node * 3 + 2, voff + node};
   if constexpr (J) {
@@ -1072,7 +1074,11 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
   return hipGetLastError();
 }
 bool brick_fused_jacobi_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
+#ifdef GLS_BRICK_COLORS_BUILD
 bool brick_colors_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
+#else
+bool brick_colors_supported(int) { return false; }
+#endif
 bool brick_subset_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 
 size_t brick_qdata_size(int k, int n_cells) {

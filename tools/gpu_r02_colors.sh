@@ -1,5 +1,6 @@
 #!/bin/bash
-# Colored brick launches (GLS_BRICK_COLORS=1) vs the default slab + k_slab_sum path: full GPU suite,
+# Colored brick launches (GLS_BRICK_COLORS=1; build the library with EXTRA=-DGLS_BRICK_COLORS_BUILD, the
+# path is compiled out by default) vs the default slab + k_slab_sum path: full GPU suite,
 # J.v microbench and bench for both.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
