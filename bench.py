@@ -371,11 +371,11 @@ def main():
         "setup_s": t_setup,
     }
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r02_pmc_traffic_pairlayout_128.txt"), 4, N_global) \
+    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r02_pmc_traffic_head_128.txt"), 4, N_global) \
         if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
-        out["roofline"]["traffic_source"] = ("profiles/r02_pmc_traffic_pairlayout_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
+        out["roofline"]["traffic_source"] = ("profiles/r02_pmc_traffic_head_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
                                              "%.2f (k_copy calibration); includes the per-quadrature-point "
                                              "linearization stream (16 doubles/q) the cached J.v reads instead "
                                              "of re-deriving u, grad u, tau, R_s" % (tr[1], tr[2]))
