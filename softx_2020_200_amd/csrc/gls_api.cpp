@@ -354,6 +354,7 @@ struct gls_ctx {
   struct ILU {
     bool on = false, valid = false;
     double athresh = 0., rthresh = 1.;
+    double boost_tol = 0., boost_val = 0.;  // rocsparse keeps these POINTERS and reads them in csrilu0
     int n_probes = 0;
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
@@ -2993,8 +2994,10 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
         if (!hnode[(size_t)x]) buf.push_back(x);
         else buf.insert(buf.end(), hmas[(size_t)x].begin(), hmas[(size_t)x].end());
       }
-      std::sort(buf.begin(), buf.end());
-      buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+      if (c->hang.on) {  // masters shared by several hanging nodes of the cell: once
+        std::sort(buf.begin(), buf.end());
+        buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+      }
       eff.insert(eff.end(), buf.begin(), buf.end());
       effoff[(size_t)e + 1] = (int64_t)eff.size();
     }
@@ -3200,8 +3203,11 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
                                    rocsparse_analysis_policy_reuse, rocsparse_solve_policy_auto, I.work.p));
   // pivots that end below athresh in magnitude are boosted to athresh (enclosed-flow pressure mode)
-  const double btol = athresh > 0 ? athresh : 1e-300, bval = athresh > 0 ? athresh : 1e-12;
-  RS_TRY(rocsparse_dcsrilu0_numeric_boost(I.h, I.info, 1, &btol, &bval));
+  // (rocsparse stores the two pointers and reads them at every csrilu0: they must outlive this call;
+  // stack locals here gave the first factorization whatever the stack later held)
+  I.boost_tol = athresh > 0 ? athresh : 1e-300;
+  I.boost_val = athresh > 0 ? athresh : 1e-12;
+  RS_TRY(rocsparse_dcsrilu0_numeric_boost(I.h, I.info, 1, &I.boost_tol, &I.boost_val));
   I.on = true;
   I.valid = false;
   if (std::getenv("GLS_ILU_VERBOSE"))
