@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--k", type=int, default=2)
     ap.add_argument("--kp", type=int, default=2)
     ap.add_argument("--nu", type=float, default=0.01)
+    ap.add_argument("--scheme", default="bdf2", choices=["bdf2", "steady"],
+                    help="bdf2 (configs[2], the metric) or steady (configs[1]: Q1 64^3, nu = 1)")
     ap.add_argument("--dt", type=float, default=0.01)
     ap.add_argument("--lin-max", type=int, default=200)
     ap.add_argument("--restart", type=int, default=30)
@@ -252,7 +254,7 @@ def main():
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
         m2_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.3), mesh["n_vnodes"])
-    ctx.set_time("bdf2", ts)
+    ctx.set_time(args.scheme, ts)
     if dist is not None:
         dist.barrier()  # first collective before any batched P2P (NCCL requirement)
     m1 = torch.from_numpy(m1_h).to(dev)
@@ -318,7 +320,8 @@ def main():
     nvl = (args.k + 1) ** 3
     n_cells_rank = n_cells // world
     nv_rank = (N // 4) if world > 1 else nv
-    B_jv = 8 * N * 3 + 8 * 2 * 3 * nv_rank + 4 * n_cells_rank * nvl * (1 if args.kp == args.k else 2) + \
+    k_hist = 2 if args.scheme == "bdf2" else 0  # history vectors the scheme reads
+    B_jv = 8 * N * 3 + 8 * k_hist * 3 * nv_rank + 4 * n_cells_rank * nvl * (1 if args.kp == args.k else 2) + \
         32 * n_cells_rank + nv_rank
     jv_launch_ms = jv2_ms / max(jv2_n, 1)
     # the brick kernel writes per-brick surface slabs; the deterministic node sum (k_slab_sum) that
@@ -328,7 +331,7 @@ def main():
     achieved = B_jv / (op_ms * 1e-3) / 1e9
     # dense-contraction FLOP count of the kernel as written (per cell, Q2-Q2 3D): see DESIGN.md §4
     out = {
-        "metric": "nonlinear iters/sec (3D cavity Q2 128^3 BDF2)",
+        "metric": "nonlinear iters/sec (3D cavity Q%d %d^3 %s)" % (args.k, args.n, args.scheme.upper()),
         "value": its_per_s,
         "unit": "nonlinear_iters/s",
         "n_gpus": world,
@@ -339,9 +342,12 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (smooth cavity-like BDF2 history, lid/wall Dirichlet values)",
-        "config": {"workload": "3D lid-driven cavity Q%d-Q%d %d^3 transient BDF2 (BASELINE configs[2])"
-                               % (args.k, args.kp, args.n),
+        "data": "synthetic (smooth cavity-like %s, lid/wall Dirichlet values)" % (
+            "BDF2 history" if args.scheme == "bdf2" else "state"),
+        "config": {"workload": "3D lid-driven cavity Q%d-Q%d %d^3 %s%s"
+                               % (args.k, args.kp, args.n, "transient BDF2" if args.scheme == "bdf2" else "steady",
+                                  {(2, 128, "bdf2"): " (BASELINE configs[2])",
+                                   (1, 64, "steady"): " (BASELINE configs[1])"}.get((args.k, args.n, args.scheme), "")),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
                        args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if -2 in lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
