@@ -444,6 +444,10 @@ struct Constraints {
   std::vector<uint8_t> mask;  // per velocity node, bit c = component c constrained
   std::vector<int64_t> dofs;
   std::vector<double> vals;
+  // slip on curved walls (general meshes): n.u = 0 as the homogeneous line
+  // u_c = -sum_{d != c} (n_d / n_c) u_d on the component c of largest |n_c| (DoF-level, like hanging lines)
+  std::vector<int64_t> line_dofs, line_off{0}, line_master;
+  std::vector<double> line_w;
 };
 
 // normal axes of the faces with boundary id `id` that node idx lies on (bit d = face normal e_d)
@@ -465,6 +469,7 @@ unsigned face_normals(const Mesh &m, const double *x, bool colorize, int id) {
 Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   Constraints C;
   C.mask.assign((size_t)m.nv, 0);
+  std::vector<uint8_t> lined((size_t)m.nv, 0);  // nodes constrained by a slip line (first constraint wins)
   std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
   for (const BC &b : P.bcs) {
     if (b.type == "periodic") continue;
@@ -487,12 +492,30 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       if ((m.general ? m.vbid[(size_t)v] : face_bits(m, x, P.colorize)) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
-        if (sn) {  // n.u = 0 on a straight wall: the normal is an axis, that component is 0
+        if (sn) {  // n.u = 0: on a straight wall the normal is an axis and that component is 0
           unsigned ax = 0;
+          bool axis = true;
           for (int c = 0; c < m.dim; ++c) {
             const double nc = std::fabs((*sn)[(size_t)(v * m.dim + c)]);
             if (nc > 1 - 1e-12) ax |= 1u << c;
-            else if (nc > 1e-12) die("slip boundary %d: node normal not along an axis (curved slip walls are not supported)", b.id);
+            else if (nc > 1e-12) axis = false;
+          }
+          if (!axis) {  // curved wall: a constraint line (unless the node is already constrained)
+            ax = 0;
+            if (!C.mask[(size_t)v] && !lined[(size_t)v]) {
+              const double *n = &(*sn)[(size_t)(v * m.dim)];
+              int cmax = 0;
+              for (int c = 1; c < m.dim; ++c)
+                if (std::fabs(n[c]) > std::fabs(n[cmax])) cmax = c;
+              C.line_dofs.push_back(v * m.dim + cmax);
+              for (int d = 0; d < m.dim; ++d)
+                if (d != cmax && std::fabs(n[d]) > 1e-14) {
+                  C.line_master.push_back(v * m.dim + d);
+                  C.line_w.push_back(-n[d] / n[cmax]);
+                }
+              C.line_off.push_back((int64_t)C.line_master.size());
+              lined[(size_t)v] = 1;
+            }
           }
           nrm.push_back(ax);
         } else {
@@ -507,6 +530,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       for (int c = 0; c < m.dim; ++c) {
         uint8_t &mk = C.mask[(size_t)sel[s]];
         if (mk & (1u << c)) continue;
+        if (lined[(size_t)sel[s]]) continue;  // slip line first: the node keeps it
         if (b.type == "slip" && !((nrm[s] >> c) & 1u)) continue;
         mk |= (uint8_t)(1u << c);
         val[(size_t)(sel[s] * m.dim + c)] = b.type == "function" ? fv[c][s * (size_t)b.f[c].nc] : 0.0;
@@ -1011,10 +1035,19 @@ struct Solver {
     m = std::move(r);
     C = make_constraints(P, m, time);
     ctx = make_context(m, C);
-    if (!m.hang_dofs.empty())
-      ck(gls_set_hanging(ctx, (int64_t)m.hang_dofs.size(), m.hang_dofs.data(), m.hang_off.data(), m.hang_master.data(),
-                         m.hang_w.data()),
-         "gls_set_hanging");
+    // hanging lines + slip lines of curved walls (homogeneous constraint lines on velocity DoFs)
+    std::vector<int64_t> ld = m.hang_dofs, lo = m.hang_off, lm = m.hang_master;
+    std::vector<double> lw = m.hang_w;
+    for (size_t i = 0; i < C.line_dofs.size(); ++i) {
+      ld.push_back(C.line_dofs[i]);
+      for (int64_t j = C.line_off[i]; j < C.line_off[i + 1]; ++j) {
+        lm.push_back(C.line_master[(size_t)j]);
+        lw.push_back(C.line_w[(size_t)j]);
+      }
+      lo.push_back((int64_t)lm.size());
+    }
+    if (!ld.empty())
+      ck(gls_set_hanging(ctx, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging");
     alloc_vectors();
     print_setup(F.volume);
   }
@@ -1153,7 +1186,8 @@ struct Solver {
     // (the reference's ILU-GMRES; not with hanging nodes) unless --precond jacobi. The reference's
     // iteration caps are tuned for ILU(k) / AMG, so the caps and restart are raised without the
     // V-cycle (ILU(0) is weaker than the reference's ILU(1); Jacobi much weaker).
-    if (mg_levels.empty() && use_ilu && ilu_ctx != ctx) {
+    // (not with slip lines on curved walls: ILU(0)-GMRES measured not converging there; Jacobi)
+    if (mg_levels.empty() && use_ilu && C.line_dofs.empty() && ilu_ctx != ctx) {
       ck(gls_ilu_attach(ctx, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;
     }

@@ -326,3 +326,78 @@ def test_app_mms_kelly_adaptation_matches_oracle(tmp_path, dim, variable, ftype,
     assert rows[-1][1] < rows[0][1]
     if coarsen == 0:  # (with coarsening, whether complete families survive the smoothing depends on the case)
         assert coarsened == 0, coarsened
+
+
+SHELL_ROTATION_PRM = """
+subsection simulation control
+  set method            = steady
+  set number mesh adapt = 1
+  set output frequency  = 0
+end
+subsection FEM
+  set velocity order = 2
+  set pressure order = 1
+  set qmapping all   = true
+end
+subsection physical properties
+  set kinematic viscosity = 1.0
+end
+subsection mesh
+  set type           = dealii
+  set grid type      = hyper_shell
+  set grid arguments = 0, 0 : 0.25 : 1 : 8 : true
+  set initial refinement = 1
+end
+subsection boundary conditions
+  set number = 2
+  subsection bc 0
+    set id = 0
+    set type = function
+    subsection u
+      set Function expression = -y
+    end
+    subsection v
+      set Function expression = x
+    end
+  end
+  subsection bc 1
+    set id = 1
+    set type = {outer}
+  end
+end
+subsection mesh adaptation
+  set type = uniform
+end
+subsection analytical solution
+  set enable = true
+  subsection uvw
+    set Function expression = -y*(1+1/(x*x+y*y))/17; x*(1+1/(x*x+y*y))/17; 0
+  end
+end
+subsection non-linear solver
+  set tolerance      = 1e-10
+  set max iterations = 10
+end
+subsection linear solver
+  set max iters         = 5000
+  set relative residual = 1e-12
+  set minimum residual  = 1e-14
+end
+"""
+
+
+@pytest.mark.gpu
+def test_app_slip_on_curved_wall_rigid_rotation(tmp_path):
+    """slip on a curved wall (compute_no_normal_flux_constraints with node normals that are not axes,
+    gls_navier_stokes.cc:100-110): the velocity component of largest |n_c| is constrained by the line
+    u_c = -sum (n_d / n_c) u_d. Inner circle (r = 1/4) rotating with u = (-y, x), outer circle (r = 1)
+    slip: with the reference's Laplacian viscous form the natural condition on the slip wall is
+    d u_theta / dr = 0, so the exact flow is u_theta = (r + 1/r) / 17 (u_theta(1/4) = 1/4,
+    u_theta'(1) = 0) with dp/dr = u_theta^2 / r; the velocity error against it falls with refinement,
+    while a no-slip outer wall gives the Taylor-Couette profile, far from it. Parity unpinned (no
+    reference case uses slip on a curved wall); checked against the analytic solution."""
+    rows = table(run_app(tmp_path, SHELL_ROTATION_PRM.replace("{outer}", "slip"), 2))
+    assert len(rows) == 2, rows
+    assert rows[0][1] < 1e-2 and rows[1][1] < rows[0][1] / 4, rows  # Q2 velocity: ~h^3 on curved cells
+    rows_ns = table(run_app(tmp_path, SHELL_ROTATION_PRM.replace("{outer}", "noslip"), 2))
+    assert rows_ns[-1][1] > 10 * rows[-1][1], (rows, rows_ns)
