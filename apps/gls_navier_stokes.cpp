@@ -164,6 +164,7 @@ struct Params {
   int nl_solver = GLS_NEWTON, skip_iterations = 1;  // non-linear solver/solver, skip iterations
   double lin_rel = 1e-3, lin_min = 1e-8;
   double ilu_atol = 1e-8, ilu_rtol = 1.0;
+  int ilu_fill = 0;
   std::string timer = "none";  // timer/type none | iteration | end (parameters.cc:136-164)
   bool srf = false;
   double omega[3] = {0, 0, 0};
@@ -307,7 +308,14 @@ Params read_params(const Prm &p, int dim) {
   P.lin_max = p.i("linear solver/max iters", 1000);
   P.lin_rel = p.d("linear solver/relative residual", 1e-3);
   P.lin_min = p.d("linear solver/minimum residual", 1e-8);
-  // ILU(k) of the reference's GMRES (parameters.cc:546-560); the level is 0 here (rocSPARSE csrilu0)
+  // ILU(k) of the reference's GMRES (parameters.cc:546-560; a Double entry cast to Ifpack's integer
+  // level of fill): integral values 0..GLS_ILU_MAX_FILL, anything else fails here
+  {
+    const double f = p.d("linear solver/ilu preconditioner fill", 0.0);
+    if (!(f >= 0 && f <= GLS_ILU_MAX_FILL) || f != std::floor(f))
+      die("linear solver/ilu preconditioner fill = %g is not supported (integers 0..%d)", f, GLS_ILU_MAX_FILL);
+    P.ilu_fill = (int)f;
+  }
   P.ilu_atol = p.d("linear solver/ilu preconditioner absolute tolerance", 1e-8);
   P.ilu_rtol = p.d("linear solver/ilu preconditioner relative tolerance", 1.0);
   P.timer = p.get("timer/type", "none");
@@ -1182,16 +1190,15 @@ struct Solver {
     np.tolerance = P.newton_tol;
     np.max_iterations = P.newton_max;
     np.verbosity = P.newton_verbose;
-    // Preconditioner: the multigrid V-cycle on nested hyper_cubes; elsewhere the assembled ILU(0)
-    // (the reference's ILU-GMRES; not with hanging nodes) unless --precond jacobi. The reference's
-    // iteration caps are tuned for ILU(k) / AMG, so the caps and restart are raised without the
-    // V-cycle (ILU(0) is weaker than the reference's ILU(1); Jacobi much weaker).
-    // (not with slip lines on curved walls: ILU(0)-GMRES measured not converging there; Jacobi)
-    if (mg_levels.empty() && use_ilu && C.line_dofs.empty() && ilu_ctx != ctx) {
-      ck(gls_ilu_attach(ctx, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
+    // Preconditioner: the multigrid V-cycle on nested hyper_cubes; elsewhere the reference's
+    // ILU(fill)-GMRES (setup_ILU, gls_navier_stokes.cc:1161-1176) with the prm's restart (30, the
+    // TrilinosWrappers::SolverGMRES default) and iteration cap, unless --precond jacobi. Jacobi is much
+    // weaker than the reference's preconditioners, so its caps and restart are raised.
+    if (mg_levels.empty() && use_ilu && ilu_ctx != ctx) {
+      ck(gls_ilu_attach(ctx, P.ilu_fill, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;
     }
-    const bool jacobi = mg_levels.empty();
+    const bool jacobi = mg_levels.empty() && !use_ilu;
     np.lin.max_iterations = jacobi ? std::max(P.lin_max, 20000) : P.lin_max;
     np.lin.restart = jacobi ? std::max(P.restart, 100) : P.restart;
     np.lin.relative_residual = P.lin_rel;

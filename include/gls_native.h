@@ -208,17 +208,34 @@ int gls_mg_transfer(gls_ctx *ctx, int level, int direction, const double *in, do
  * must fill an axis-aligned box (Morton partitions of a 2^m-cube over 2^j ranks do). */
 int gls_set_lattice(gls_ctx *ctx, int n1d, const int64_t *local_to_global);
 int gls_mg_detach(gls_ctx *ctx);
-/* Assembled ILU(0) preconditioner for GMRES (replaces setup_ILU, gls_navier_stokes.cc:1161-1176, the
- * reference's 'linear solver/method = gmres' with 'ilu preconditioner absolute / relative tolerance';
- * fill level 0): the Jacobian is probed from the device operator into CSR with distance-2-colored
- * unit vectors once per Jacobian state, its diagonal perturbed like Ifpack (a_ii <- rthresh a_ii +
- * sign(a_ii) athresh) and factored by rocSPARSE. Single rank, no multigrid; with hanging-node lines the
- * pattern is that of the condensed operator (hanging nodes replaced by their masters, hanging rows
- * diagonal). */
-int gls_ilu_attach(gls_ctx *ctx, double athresh, double rthresh);
+/* Assembled ILU(fill) preconditioner for GMRES (replaces setup_ILU, gls_navier_stokes.cc:1161-1176:
+ * Trilinos PreconditionILU(ilu_fill, ilu_atol, ilu_rtol, overlap 0) = Ifpack ILU(k), the reference's
+ * 'linear solver/method = gmres' with 'ilu preconditioner fill / absolute / relative tolerance',
+ * parameters.cc:546-560). The Jacobian is probed from the device operator into CSR with
+ * distance-2-colored unit vectors once per Jacobian state; its graph is the reference's system
+ * sparsity (constrained rows / columns hold the diagonal only, lines couple their masters). DoFs are
+ * renumbered like DoFRenumbering::Cuthill_McKee; the ILU(fill) level-of-fill pattern (Ifpack_IlukGraph:
+ * level(i,j) = min_k level(i,k) + level(k,j) + 1 <= fill) is inserted with explicit zeros, the
+ * diagonal perturbed like Ifpack (a_ii <- rthresh a_ii + sign(a_ii) athresh) and factored by rocSPARSE.
+ * fill outside 0..GLS_ILU_MAX_FILL is rejected (GLS_EINVAL). Single rank, no multigrid. */
+#define GLS_ILU_MAX_FILL 10
+int gls_ilu_attach(gls_ctx *ctx, int fill, double athresh, double rthresh);
 int gls_ilu_detach(gls_ctx *ctx);
 int gls_ilu_info(const gls_ctx *ctx, int64_t *nnz, int *n_probes);
 int gls_ilu_matrix(gls_ctx *ctx, int32_t *rowp, int32_t *col, double *val); /* probed CSR (tests) */
+/* factored values in the factorization numbering (perm[dof] = row), for tests */
+int gls_ilu_factors(gls_ctx *ctx, int32_t *perm, int32_t *rowp, int32_t *col, double *val);
+/* Host only (no device): the ILU(fill) level-of-fill pattern of an n x n CSR graph (diagonal always
+ * included, rows sorted), with each entry's level. Call with out_rowp / out_col / out_level all NULL
+ * to get out_nnz; capacity = length of out_col / out_level. */
+int gls_iluk_pattern(int64_t n, const int32_t *rowp, const int32_t *col, int fill, int32_t *out_rowp,
+                     int32_t *out_col, int32_t *out_level, int64_t capacity, int64_t *out_nnz);
+/* Host only: the DoF renumbering gls_ilu_attach uses (deal.II DoFRenumbering::Cuthill_McKee,
+ * gls_navier_stokes.cc:70) on a node graph: node x's row nodes adj[adj_off[x] .. adj_off[x+1]) (itself
+ * included), its DoFs dofs[dof_off[x] .. dof_off[x+1]) (old order = position in dofs);
+ * order[new index] = DoF. */
+int gls_cuthill_mckee(int64_t n_nodes, const int64_t *adj_off, const int64_t *adj, const int64_t *dof_off,
+                      const int64_t *dofs, int64_t *order);
 
 /* ------------------------------------------------------------------------------------------
  * Nonlinear solve: NewtonNonLinearSolver::solve (include/core/newton_non_linear_solver.h:74-139)

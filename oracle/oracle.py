@@ -980,3 +980,104 @@ def muparser_to_numpy(expr: str, constants=None):
         return out
 
     return f
+
+
+# ---------------------------------------------------------------------------------------------------
+# ILU(k) of the reference's GMRES preconditioner (setup_ILU, source/solvers/gls_navier_stokes.cc:
+# 1161-1176: TrilinosWrappers::PreconditionILU(ilu_fill, ilu_atol, ilu_rtol, overlap 0), i.e. Ifpack's
+# ILU on one process). Ifpack (Trilinos, as shipped with the dealii_full_9.2 image; not vendored in the
+# reference) is restated from its published algorithm:
+#   * Ifpack_IlukGraph: original entries (and the diagonal) have level 0; eliminating row k < i from
+#     row i creates (i, j) at level lev(i, k) + lev(k, j) + 1; an entry is kept when its level <= fill.
+#   * Ifpack_ILU::Compute: the diagonal is first replaced by rthresh * a_ii + sign(a_ii) * athresh
+#     (sign(0) = +1), then the row-oriented IKJ incomplete factorisation restricted to that pattern.
+# Plain dict loops: for the small matrices of the tests only.
+# ---------------------------------------------------------------------------------------------------
+def iluk_levels(A, fill):
+    """{(i, j): level} of the ILU(fill) pattern of the square sparse matrix A's graph (explicit
+    entries, whatever their value; the diagonal always included)."""
+    A = A.tocsr()
+    n = A.shape[0]
+    U = [None] * n  # finished rows: {j: level} for j > row
+    out = {}
+    for i in range(n):
+        row = {int(j): 0 for j in A.indices[A.indptr[i]:A.indptr[i + 1]]}
+        row[i] = 0
+        k = -1
+        while True:  # prior rows in increasing order, including fill created on the way
+            cand = [c for c in row if k < c < i]
+            if not cand:
+                break
+            k = min(cand)
+            lik = row[k]
+            for j, lkj in U[k].items():
+                lev = lik + lkj + 1
+                if lev <= fill and lev < row.get(j, fill + 1):
+                    row[j] = lev
+        for j, lev in row.items():
+            out[(i, j)] = lev
+        U[i] = {j: lev for j, lev in row.items() if j > i}
+    return out
+
+
+def ilu_factor(A, pattern, athresh=0.0, rthresh=1.0):
+    """Ifpack-style ILU restricted to `pattern` (iterable of (i, j)): returns the combined factor as a
+    dict {(i, j): value} (strictly lower = L with unit diagonal, upper incl. diagonal = U)."""
+    A = A.tocsr()
+    n = A.shape[0]
+    rows = [dict() for _ in range(n)]
+    for (i, j) in pattern:
+        rows[i][j] = 0.0
+    for i in range(n):
+        for t in range(A.indptr[i], A.indptr[i + 1]):
+            j = int(A.indices[t])
+            if j not in rows[i]:
+                raise ValueError("matrix entry (%d, %d) outside the ILU pattern" % (i, j))
+            rows[i][j] += float(A.data[t])
+        a = rows[i][i]
+        rows[i][i] = rthresh * a + (-athresh if a < 0 else athresh)
+    for i in range(n):
+        r = rows[i]
+        for k in sorted(c for c in r if c < i):
+            lik = r[k] / rows[k][k]
+            r[k] = lik
+            for j, ukj in rows[k].items():
+                if j > k and j in r:
+                    r[j] -= lik * ukj
+    return {(i, j): v for i in range(n) for j, v in rows[i].items()}
+
+
+def cuthill_mckee_dealii(G):
+    """deal.II's SparsityTools::reorder_Cuthill_McKee with no starting indices (used by
+    DoFRenumbering::Cuthill_McKee, gls_navier_stokes.cc:70): start at the first index of least row
+    length; then repeatedly number the not yet numbered neighbours of the last round, ordered by their
+    number of not yet numbered neighbours (stable in index order); a new start per connected
+    component. G: square sparse graph (rows include the diagonal). Returns order[new] = old."""
+    G = G.tocsr()
+    n = G.shape[0]
+    rl = np.diff(G.indptr)
+    new = np.full(n, -1)
+    order = []
+
+    def start():
+        free = np.where(new < 0)[0]
+        return int(free[np.argmin(rl[free])])  # argmin: the first of the least row length
+
+    last = []
+    while len(order) < n:
+        if not last:
+            s = start()
+            new[s] = len(order)
+            order.append(s)
+            last = [s]
+            continue
+        nxt = sorted({int(j) for d in last for j in G.indices[G.indptr[d]:G.indptr[d + 1]] if new[j] < 0})
+        if not nxt:
+            last = []
+            continue
+        coord = {d: sum(1 for j in G.indices[G.indptr[d]:G.indptr[d + 1]] if new[j] < 0) for d in nxt}
+        for d in sorted(nxt, key=lambda d: coord[d]):  # stable: ties in index order
+            new[d] = len(order)
+            order.append(d)
+        last = nxt
+    return np.array(order)

@@ -24,6 +24,7 @@
 #include "../../include/gls_native.h"
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
+#include "gls_sparse.hpp"
 
 namespace {
 
@@ -355,7 +356,7 @@ struct gls_ctx {
     bool on = false, valid = false;
     double athresh = 0., rthresh = 1.;
     double boost_tol = 0., boost_val = 0.;  // rocsparse keeps these POINTERS and reads them in csrilu0
-    int n_probes = 0;
+    int n_probes = 0, fill = 0;
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
     DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
@@ -365,7 +366,7 @@ struct gls_ctx {
     rocsparse_handle h = nullptr;
     rocsparse_mat_descr dA = nullptr, dL = nullptr, dU = nullptr;
     rocsparse_mat_info info = nullptr;
-    int64_t nnz = 0;
+    int64_t nnz = 0, nnz_a = 0;  // entries of the ILU(fill) pattern / of the system matrix
     void release() {
       if (info) rocsparse_destroy_mat_info(info);
       if (dA) rocsparse_destroy_mat_descr(dA);
@@ -2023,6 +2024,7 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
   auto &I = c->ilu;
   const int64_t n = c->n_dofs;
   hipStream_t s = c->stream;
+  if (I.fill > 0) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
   for (int p = 0; p < I.n_probes; ++p) {
     HIP_TRY(gls::vec_fill(I.vbuf.p, n, 0.0, s));
     HIP_TRY(gls::vec_set_const_indexed(I.vbuf.p, I.pdofs.p + I.pdoff[(size_t)p], I.pdoff[(size_t)p + 1] - I.pdoff[(size_t)p],
@@ -2943,15 +2945,22 @@ int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
 // ---------------------------------------------------------------------------------------------
 // gls_ilu_attach: the reference's ILU-preconditioned GMRES (linear solver method gmres with 'ilu
 // preconditioner fill / absolute tolerance / relative tolerance', setup_ILU gls_navier_stokes.cc:
-// 1161-1176, Ifpack ILU(k) with athresh / rthresh) on the assembled Jacobian. The fill level is 0
-// here (rocSPARSE csrilu0); the matrix is never formed by a CPU: it is probed from the device
-// operator with distance-2-colored unit vectors (no two DoFs of a probe share a row).
+// 1161-1176: Ifpack ILU(k) with athresh / rthresh, no overlap) on the assembled Jacobian. The matrix
+// is never formed by a CPU: it is probed from the device operator with distance-2-colored unit
+// vectors (no two DoFs of a probe share a row). Its graph is the reference's system-matrix sparsity
+// (make_sparsity_pattern with nonzero_constraints, keep_constrained_dofs = false,
+// gls_navier_stokes.cc:208-211): a constrained row / column holds its diagonal only, lines
+// (hanging nodes, slip on curved walls) couple their masters. The DoFs are renumbered like
+// DoFRenumbering::Cuthill_McKee (gls_navier_stokes.cc:70), the level-of-fill pattern of ILU(fill)
+// is inserted with explicit zeros, and rocSPARSE csrilu0 on that pattern computes ILU(fill).
 // ---------------------------------------------------------------------------------------------
-extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
+extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthresh) {
   GLS_TRY(check_ctx(c));
   auto &I = c->ilu;
   if (c->dist.on) return set_err(GLS_EINVAL, "gls_ilu_attach: single-rank contexts only");
   if (c->mg.on) return set_err(GLS_EINVAL, "gls_ilu_attach: a multigrid preconditioner is attached");
+  if (fill < 0 || fill > GLS_ILU_MAX_FILL)
+    return set_err(GLS_EINVAL, "gls_ilu_attach: ilu preconditioner fill %d not supported (0..%d)", fill, GLS_ILU_MAX_FILL);
   const int dim = c->dim, nvc = gls::ipow(c->k + 1, dim);
   const bool sep = c->cell_pnodes.p != nullptr;
   const int npc = sep ? gls::ipow(c->kp + 1, dim) : 0;
@@ -2966,65 +2975,105 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   auto cell_node = [&](int64_t cell, int a) -> int64_t {
     return a < nvc ? cv[(size_t)(cell * nvc + a)] : nv + cp[(size_t)(cell * npc + a - nvc)];
   };
-  // hanging nodes (unified numbering) and their master nodes: the condensed operator C^T K C couples
-  // the masters of a cell's hanging nodes with the cell's other nodes; a hanging row is D_c only
+  // DoFs of a unified node and their probe slot (component; dim = pressure)
+  auto node_dofs = [&](int64_t x, int64_t *d, int *slot) -> int {
+    if (x >= nv) { d[0] = dim * nv + (x - nv); slot[0] = dim; return 1; }
+    int m = 0;
+    for (int cc = 0; cc < dim; ++cc) { d[m] = x * dim + cc; slot[m++] = cc; }
+    if (!sep) { d[m] = dim * nv + x; slot[m++] = dim; }
+    return m;
+  };
   const int64_t nvd = (int64_t)dim * nv;
-  std::vector<char> hnode((size_t)nu, 0);
-  std::vector<std::vector<int64_t>> hmas;
-  if (c->hang.on) {
-    hmas.resize((size_t)nu);
-    auto unode = [&](int64_t d) { return d < nvd ? d / dim : (sep ? nv + (d - nvd) : d - nvd); };
-    for (size_t i = 0; i + 1 < c->hang.h_off.size(); ++i) {
-      const int64_t x = unode(c->hang.h_dof[i]);
-      hnode[(size_t)x] = 1;
-      for (int64_t j = c->hang.h_off[i]; j < c->hang.h_off[i + 1]; ++j) {
-        const int64_t y = unode(c->hang.h_master[(size_t)j]);
-        if (std::find(hmas[(size_t)x].begin(), hmas[(size_t)x].end(), y) == hmas[(size_t)x].end()) hmas[(size_t)x].push_back(y);
-      }
-    }
+  auto unode = [&](int64_t d) { return d < nvd ? d / dim : (sep ? nv + (d - nvd) : d - nvd); };
+  // constrained DoFs (zero_constraints: Dirichlet + lines) and the operator lines (Dirichlet masters
+  // drop out, as in the closed AffineConstraints)
+  std::vector<char> cons((size_t)n, 0), isline((size_t)n, 0);
+  {
+    std::vector<int64_t> cd(c->con_dofs.n);
+    if (!cd.empty()) HIP_TRY(hipMemcpy(cd.data(), c->con_dofs.p, cd.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+    for (int64_t d : cd) cons[(size_t)d] = 1;
   }
-  // effective nodes of each cell: its nodes with the hanging ones replaced by their masters
+  std::vector<int64_t> lidx((size_t)n, -1);
+  if (c->hang.on)
+    for (size_t i = 0; i + 1 < c->hang.h_off.size(); ++i) {
+      lidx[(size_t)c->hang.h_dof[i]] = (int64_t)i;
+      isline[(size_t)c->hang.h_dof[i]] = 1;
+    }
+  auto dirichlet = [&](int64_t d) { return cons[(size_t)d] && !isline[(size_t)d]; };
+  // effective DoFs of each cell: its unconstrained DoFs and the (non-Dirichlet) masters of its lines
   std::vector<int64_t> effoff((size_t)nc + 1, 0), eff;
   {
     std::vector<int64_t> buf;
     for (int64_t e = 0; e < nc; ++e) {
       buf.clear();
       for (int a = 0; a < ncn; ++a) {
-        const int64_t x = cell_node(e, a);
-        if (!hnode[(size_t)x]) buf.push_back(x);
-        else buf.insert(buf.end(), hmas[(size_t)x].begin(), hmas[(size_t)x].end());
+        int64_t d[4];
+        int sl[4];
+        const int m = node_dofs(cell_node(e, a), d, sl);
+        for (int j = 0; j < m; ++j) {
+          const int64_t li = lidx[(size_t)d[j]];
+          if (li >= 0) {
+            for (int64_t t = c->hang.h_off[(size_t)li]; t < c->hang.h_off[(size_t)li + 1]; ++t)
+              if (!dirichlet(c->hang.h_master[(size_t)t])) buf.push_back(c->hang.h_master[(size_t)t]);
+          } else if (!cons[(size_t)d[j]]) {
+            buf.push_back(d[j]);
+          }
+        }
       }
-      if (c->hang.on) {  // masters shared by several hanging nodes of the cell: once
-        std::sort(buf.begin(), buf.end());
-        buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
-      }
+      std::sort(buf.begin(), buf.end());
+      buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
       eff.insert(eff.end(), buf.begin(), buf.end());
       effoff[(size_t)e + 1] = (int64_t)eff.size();
     }
   }
-  std::vector<int64_t> ncoff((size_t)nu + 1, 0), nccell;
-  for (int64_t t = 0; t < (int64_t)eff.size(); ++t) ++ncoff[(size_t)eff[(size_t)t] + 1];
-  for (int64_t x = 0; x < nu; ++x) ncoff[(size_t)x + 1] += ncoff[(size_t)x];
-  nccell.resize((size_t)ncoff[(size_t)nu]);
+  // DoF -> cells whose effective list holds it
+  std::vector<int64_t> dcoff((size_t)n + 1, 0), dcell;
+  for (int64_t d : eff) ++dcoff[(size_t)d + 1];
+  for (int64_t i = 0; i < n; ++i) dcoff[(size_t)i + 1] += dcoff[(size_t)i];
+  dcell.resize((size_t)dcoff[(size_t)n]);
   {
-    std::vector<int64_t> fill(ncoff.begin(), ncoff.end() - 1);
+    std::vector<int64_t> f(dcoff.begin(), dcoff.end() - 1);
     for (int64_t e = 0; e < nc; ++e)
-      for (int64_t t = effoff[(size_t)e]; t < effoff[(size_t)e + 1]; ++t) nccell[(size_t)fill[(size_t)eff[(size_t)t]]++] = e;
+      for (int64_t t = effoff[(size_t)e]; t < effoff[(size_t)e + 1]; ++t) dcell[(size_t)f[(size_t)eff[(size_t)t]]++] = e;
   }
-  // N1(x): effective nodes of the cells holding x (sorted, unique); a hanging node: itself only
+  // rows of the system matrix (old numbering, sorted): an unconstrained DoF couples the effective DoFs
+  // of its cells; a constrained DoF only itself
+  std::vector<int64_t> aoff((size_t)n + 1, 0), acol;
+  {
+    std::vector<int64_t> stamp((size_t)n, -1), buf;
+    for (int64_t i = 0; i < n; ++i) {
+      buf.clear();
+      buf.push_back(i);
+      stamp[(size_t)i] = i;
+      if (!cons[(size_t)i])
+        for (int64_t t = dcoff[(size_t)i]; t < dcoff[(size_t)i + 1]; ++t) {
+          const int64_t e = dcell[(size_t)t];
+          for (int64_t u = effoff[(size_t)e]; u < effoff[(size_t)e + 1]; ++u) {
+            const int64_t j = eff[(size_t)u];
+            if (stamp[(size_t)j] != i) { stamp[(size_t)j] = i; buf.push_back(j); }
+          }
+        }
+      std::sort(buf.begin(), buf.end());
+      acol.insert(acol.end(), buf.begin(), buf.end());
+      aoff[(size_t)i + 1] = (int64_t)acol.size();
+    }
+  }
+  // node graph of that pattern (x ~ y when a row of x holds a DoF of y) for the distance-2 coloring
   std::vector<int64_t> n1off((size_t)nu + 1, 0), n1;
   {
     std::vector<int64_t> stamp((size_t)nu, -1), buf;
     for (int64_t x = 0; x < nu; ++x) {
       buf.clear();
-      if (hnode[(size_t)x]) buf.push_back(x);
-      for (int64_t t = ncoff[(size_t)x]; t < ncoff[(size_t)x + 1]; ++t) {
-        const int64_t e = nccell[(size_t)t];
-        for (int64_t u = effoff[(size_t)e]; u < effoff[(size_t)e + 1]; ++u) {
-          const int64_t y = eff[(size_t)u];
+      buf.push_back(x);
+      stamp[(size_t)x] = x;
+      int64_t d[4];
+      int sl[4];
+      const int m = node_dofs(x, d, sl);
+      for (int j = 0; j < m; ++j)
+        for (int64_t t = aoff[(size_t)d[j]]; t < aoff[(size_t)d[j] + 1]; ++t) {
+          const int64_t y = unode(acol[(size_t)t]);
           if (stamp[(size_t)y] != x) { stamp[(size_t)y] = x; buf.push_back(y); }
         }
-      }
       std::sort(buf.begin(), buf.end());
       n1.insert(n1.end(), buf.begin(), buf.end());
       n1off[(size_t)x + 1] = (int64_t)n1.size();
@@ -3049,117 +3098,131 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
     color[(size_t)x] = col;
     ncol = std::max(ncol, col + 1);
   }
-  // DoFs of a unified node and their probe slot (component; dim = pressure)
-  auto node_dofs = [&](int64_t x, int64_t *d, int *slot) -> int {
-    if (x >= nv) { d[0] = dim * nv + (x - nv); slot[0] = dim; return 1; }
-    int m = 0;
-    for (int cc = 0; cc < dim; ++cc) { d[m] = x * dim + cc; slot[m++] = cc; }
-    if (!sep) { d[m] = dim * nv + x; slot[m++] = dim; }
-    return m;
-  };
-  // DoF renumbering for the factorisation: Cuthill-McKee on the node graph (deal.II renumbers the
-  // DoFs with Cuthill_McKee before Trilinos factors, gls_navier_stokes.cc:70), a node's DoFs
-  // consecutive (u, v, [w,] p): the pressure rows sit next to their velocity rows, not in a trailing
-  // block, which keeps ILU(0) of the saddle-point-like GLS matrix away from vanishing pivots
-  std::vector<int32_t> newidx((size_t)n, -1);
-  {
-    std::vector<int64_t> order;
-    order.reserve((size_t)nu);
-    std::vector<char> seen((size_t)nu, 0);
-    auto deg = [&](int64_t x) { return n1off[(size_t)x + 1] - n1off[(size_t)x]; };
-    for (int64_t start = 0; start < nu; ++start) {  // one BFS per connected component
-      if (seen[(size_t)start]) continue;
-      int64_t s0 = start;  // lowest-degree unvisited node of this component's first visit
-      seen[(size_t)s0] = 1;
-      size_t head = order.size();
-      order.push_back(s0);
-      while (head < order.size()) {
-        const int64_t x = order[head++];
-        std::vector<int64_t> nb;
-        for (int64_t t = n1off[(size_t)x]; t < n1off[(size_t)x + 1]; ++t)
-          if (!seen[(size_t)n1[(size_t)t]]) nb.push_back(n1[(size_t)t]);
-        std::stable_sort(nb.begin(), nb.end(), [&](int64_t a, int64_t b) { return deg(a) < deg(b); });
-        for (int64_t y : nb) {
-          seen[(size_t)y] = 1;
-          order.push_back(y);
-        }
+  // Cuthill-McKee (deal.II) on the unconstrained cell-coupling graph of the DoF handler. Its nodes
+  // carry deal.II's per-support-point DoF groups: a velocity node's components followed by the
+  // pressure DoF at the same point (Q(k)-Q(kp) with kp | k: a pressure node sits on the velocity node
+  // of the same lexicographic position in every cell; the map is checked cell by cell)
+  std::vector<int64_t> p_at((size_t)std::max<int64_t>(np, 1), -1);  // pressure node -> velocity node
+  bool p_map = sep && c->k % c->kp == 0;
+  if (p_map) {
+    const int r = c->k / c->kp, k1 = c->k + 1, kp1 = c->kp + 1;
+    for (int64_t e = 0; e < nc && p_map; ++e)
+      for (int a = 0; a < npc; ++a) {
+        const int ax = a % kp1, ay = (a / kp1) % kp1, az = dim == 3 ? a / (kp1 * kp1) : 0;
+        const int va = ax * r + k1 * (ay * r) + (dim == 3 ? k1 * k1 * az * r : 0);
+        const int64_t pn = cp[(size_t)(e * npc + a)], vn = cv[(size_t)(e * nvc + va)];
+        if (p_at[(size_t)pn] < 0) p_at[(size_t)pn] = vn;
+        else if (p_at[(size_t)pn] != vn) { p_map = false; break; }
       }
-    }
-    int32_t next = 0;
-    for (int64_t x : order) {
-      int64_t d[4];
-      int sl[4];
-      const int m2 = node_dofs(x, d, sl);
-      for (int j = 0; j < m2; ++j) newidx[(size_t)d[j]] = next++;
-    }
-    if (next != n) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering covers %d of %lld DoFs", next, (long long)n);
   }
-  std::vector<int32_t> olddof((size_t)n);
-  for (int64_t i = 0; i < n; ++i) olddof[(size_t)newidx[(size_t)i]] = (int32_t)i;
-  // CSR pattern in the new numbering (rows of a node share its N1 column set), diagonal index,
-  // probe of every entry
-  std::vector<int32_t> rowp((size_t)n + 1, 0), col, didx((size_t)n, -1);
-  std::vector<int32_t> rowof_dof_node((size_t)n, 0);
+  // CM nodes: velocity nodes (+ their pressure DoF), then unmapped pressure nodes
+  std::vector<int64_t> cmnode((size_t)nu, -1);  // unified node -> CM node
+  int64_t ncm = 0;
+  for (int64_t x = 0; x < nv; ++x) cmnode[(size_t)x] = ncm++;
+  if (sep)
+    for (int64_t pn = 0; pn < np; ++pn) cmnode[(size_t)(nv + pn)] = p_map ? cmnode[(size_t)p_at[(size_t)pn]] : ncm++;
+  std::vector<int64_t> cm_doff((size_t)ncm + 1, 0), cm_dofs((size_t)n);
   for (int64_t x = 0; x < nu; ++x) {
     int64_t d[4];
     int sl[4];
-    const int m = node_dofs(x, d, sl);
-    for (int i = 0; i < m; ++i) rowof_dof_node[(size_t)d[i]] = (int32_t)x;
+    cm_doff[(size_t)cmnode[(size_t)x] + 1] += node_dofs(x, d, sl);
   }
-  std::vector<int32_t> eprobe;
-  col.reserve((size_t)n * 32);
-  for (int64_t r = 0; r < n; ++r) {  // r: new row; its DoF olddof[r]
+  for (int64_t y = 0; y < ncm; ++y) cm_doff[(size_t)y + 1] += cm_doff[(size_t)y];
+  {
+    std::vector<int64_t> f(cm_doff.begin(), cm_doff.end() - 1);
+    for (int64_t x = 0; x < nu; ++x) {  // velocity nodes come first: their components precede p
+      int64_t d[4];
+      int sl[4];
+      const int m = node_dofs(x, d, sl);
+      for (int j = 0; j < m; ++j) cm_dofs[(size_t)f[(size_t)cmnode[(size_t)x]]++] = d[j];
+    }
+  }
+  std::vector<int64_t> cadj_off((size_t)ncm + 1, 0), cadj;
+  {
+    std::vector<int64_t> ccoff((size_t)ncm + 1, 0), ccell;  // CM node -> cells
+    for (int64_t e = 0; e < nc; ++e)
+      for (int a = 0; a < ncn; ++a) ++ccoff[(size_t)cmnode[(size_t)cell_node(e, a)] + 1];
+    for (int64_t y = 0; y < ncm; ++y) ccoff[(size_t)y + 1] += ccoff[(size_t)y];
+    ccell.resize((size_t)ccoff[(size_t)ncm]);
+    std::vector<int64_t> f(ccoff.begin(), ccoff.end() - 1);
+    for (int64_t e = 0; e < nc; ++e)
+      for (int a = 0; a < ncn; ++a) ccell[(size_t)f[(size_t)cmnode[(size_t)cell_node(e, a)]]++] = e;
+    std::vector<int64_t> stamp((size_t)ncm, -1), buf;
+    for (int64_t y = 0; y < ncm; ++y) {
+      buf.clear();
+      buf.push_back(y);
+      stamp[(size_t)y] = y;
+      for (int64_t t = ccoff[(size_t)y]; t < ccoff[(size_t)y + 1]; ++t)
+        for (int a = 0; a < ncn; ++a) {
+          const int64_t z = cmnode[(size_t)cell_node(ccell[(size_t)t], a)];
+          if (stamp[(size_t)z] != y) { stamp[(size_t)z] = y; buf.push_back(z); }
+        }
+      std::sort(buf.begin(), buf.end());
+      cadj.insert(cadj.end(), buf.begin(), buf.end());
+      cadj_off[(size_t)y + 1] = (int64_t)cadj.size();
+    }
+  }
+  std::vector<int64_t> order;
+  gls::cuthill_mckee_nodes(ncm, cadj_off, cadj, cm_doff, cm_dofs, order);
+  if ((int64_t)order.size() != n) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering covers %lld of %lld DoFs", (long long)order.size(), (long long)n);
+  std::vector<int32_t> newidx((size_t)n, -1), olddof((size_t)n);
+  for (int64_t r = 0; r < n; ++r) {
+    newidx[(size_t)order[(size_t)r]] = (int32_t)r;
+    olddof[(size_t)r] = (int32_t)order[(size_t)r];
+  }
+  // the system matrix's pattern in the new numbering, then its ILU(fill) pattern
+  std::vector<int32_t> arow((size_t)n + 1, 0), acl;
+  acl.reserve(acol.size());
+  for (int64_t r = 0; r < n; ++r) {
     const int64_t i = olddof[(size_t)r];
-    const int64_t x = rowof_dof_node[(size_t)i];
-    std::vector<std::pair<int64_t, int>> cols;
-    for (int64_t t = n1off[(size_t)x]; t < n1off[(size_t)x + 1]; ++t) {
-      int64_t d[4];
-      int sl[4];
-      const int64_t y = n1[(size_t)t];
-      const int m = node_dofs(y, d, sl);
-      for (int j = 0; j < m; ++j) cols.push_back({newidx[(size_t)d[j]], color[(size_t)y] * (dim + 1) + sl[j]});
-    }
-    std::sort(cols.begin(), cols.end());
-    for (auto &cp_ : cols) {
-      if (cp_.first == r) didx[(size_t)r] = (int32_t)col.size();
-      col.push_back((int32_t)cp_.first);
-      eprobe.push_back(cp_.second);
-    }
-    rowp[(size_t)r + 1] = (int32_t)col.size();
-    if (didx[(size_t)r] < 0) return set_err(GLS_EINVAL, "gls_ilu_attach: row %lld has no diagonal", (long long)r);
+    const size_t s0 = acl.size();
+    for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t) acl.push_back(newidx[(size_t)acol[(size_t)t]]);
+    std::sort(acl.begin() + (std::ptrdiff_t)s0, acl.end());
+    arow[(size_t)r + 1] = (int32_t)acl.size();
   }
+  std::vector<int32_t> rowp, col;
+  if (gls::iluk_pattern(n, arow.data(), acl.data(), fill, rowp, col) != GLS_OK)
+    return set_err(GLS_EINVAL, "gls_ilu_attach: ILU(%d) pattern", fill);
+  std::vector<int32_t> didx((size_t)n, -1);
+  for (int64_t r = 0; r < n; ++r) {
+    const auto b = col.begin() + rowp[(size_t)r], e = col.begin() + rowp[(size_t)r + 1];
+    const auto it = std::lower_bound(b, e, (int32_t)r);
+    if (it == e || *it != r) return set_err(GLS_EINVAL, "gls_ilu_attach: row %lld has no diagonal", (long long)r);
+    didx[(size_t)r] = (int32_t)(it - col.begin());
+  }
+  // probes: one per (color, slot); every entry of the system matrix is read from the probe of its
+  // column DoF (entry position in the ILU pattern, row's original DoF)
   const int nprobe = ncol * (dim + 1);
-  // probe lists: unit DoFs per probe; (entry, row) per probe
-  std::vector<int64_t> pdoff((size_t)nprobe + 1, 0), peoff((size_t)nprobe + 1, 0);
-  std::vector<int32_t> pdofs, pent, prow;
+  std::vector<int> dslot((size_t)n, 0);
+  std::vector<int64_t> dnode((size_t)n, 0);
   for (int64_t x = 0; x < nu; ++x) {
     int64_t d[4];
     int sl[4];
     const int m = node_dofs(x, d, sl);
-    for (int j = 0; j < m; ++j) ++pdoff[(size_t)(color[(size_t)x] * (dim + 1) + sl[j]) + 1];
+    for (int j = 0; j < m; ++j) { dslot[(size_t)d[j]] = sl[j]; dnode[(size_t)d[j]] = x; }
   }
-  for (size_t e = 0; e < eprobe.size(); ++e) ++peoff[(size_t)eprobe[e] + 1];
+  auto probe_of = [&](int64_t d) { return color[(size_t)dnode[(size_t)d]] * (dim + 1) + dslot[(size_t)d]; };
+  std::vector<int64_t> pdoff((size_t)nprobe + 1, 0), peoff((size_t)nprobe + 1, 0);
+  for (int64_t d = 0; d < n; ++d) ++pdoff[(size_t)probe_of(d) + 1];
+  for (int64_t r = 0; r < n; ++r)
+    for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) ++peoff[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]]) + 1];
   for (int p = 0; p < nprobe; ++p) {
     pdoff[(size_t)p + 1] += pdoff[(size_t)p];
     peoff[(size_t)p + 1] += peoff[(size_t)p];
   }
-  pdofs.resize((size_t)pdoff[(size_t)nprobe]);
-  pent.resize((size_t)peoff[(size_t)nprobe]);
-  prow.resize(pent.size());
+  std::vector<int32_t> pdofs((size_t)pdoff[(size_t)nprobe]), pent((size_t)peoff[(size_t)nprobe]), prow(pent.size());
   {
     std::vector<int64_t> f1(pdoff.begin(), pdoff.end() - 1), f2(peoff.begin(), peoff.end() - 1);
-    for (int64_t x = 0; x < nu; ++x) {
-      int64_t d[4];
-      int sl[4];
-      const int m = node_dofs(x, d, sl);
-      for (int j = 0; j < m; ++j) pdofs[(size_t)f1[(size_t)(color[(size_t)x] * (dim + 1) + sl[j])]++] = (int32_t)d[j];
-    }
-    for (int64_t r = 0; r < n; ++r)
-      for (int32_t e = rowp[(size_t)r]; e < rowp[(size_t)r + 1]; ++e) {
-        const int64_t k = f2[(size_t)eprobe[(size_t)e]]++;
-        pent[(size_t)k] = e;
+    for (int64_t d = 0; d < n; ++d) pdofs[(size_t)f1[(size_t)probe_of(d)]++] = (int32_t)d;
+    for (int64_t r = 0; r < n; ++r) {
+      int32_t pos = rowp[(size_t)r];
+      for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) {
+        while (col[(size_t)pos] < acl[(size_t)t]) ++pos;  // both rows sorted; A's pattern is a subset
+        const int64_t k = f2[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]])]++;
+        pent[(size_t)k] = pos;
         prow[(size_t)k] = olddof[(size_t)r];  // the probe result is indexed by the original DoF
       }
+    }
   }
   I.release();
   GLS_TRY(I.rowp.upload(rowp.data(), rowp.size()));
@@ -3178,6 +3241,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   I.peoff = peoff;
   I.n_probes = nprobe;
   I.nnz = (int64_t)col.size();
+  I.nnz_a = (int64_t)acl.size();
+  I.fill = fill;
   I.athresh = athresh;
   I.rthresh = rthresh;
   RS_TRY(rocsparse_create_handle(&I.h));
@@ -3211,7 +3276,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, double athresh, double rthresh) {
   I.on = true;
   I.valid = false;
   if (std::getenv("GLS_ILU_VERBOSE"))
-    std::printf("ilu attach: n %lld nnz %lld colors %d probes %d\n", (long long)n, (long long)I.nnz, ncol, nprobe);
+    std::printf("ilu attach: n %lld fill %d nnz(A) %lld nnz(ILU) %lld colors %d probes %d\n", (long long)n, fill,
+                (long long)I.nnz_a, (long long)I.nnz, ncol, nprobe);
   return GLS_OK;
 }
 extern "C" int gls_ilu_detach(gls_ctx *c) {
@@ -3252,6 +3318,22 @@ extern "C" int gls_ilu_matrix(gls_ctx *c, int32_t *rowp, int32_t *col, double *v
     if (rowp) rowp[i + 1] = (int32_t)k;
   }
   I.valid = false;  // the values now hold the unfactored matrix
+  return GLS_OK;
+}
+// the factored ILU(fill) (after the diagonal perturbation) in the factorization's numbering, for
+// tests: perm[dof] = its row; rowp / col / val of gls_ilu_info's nnz entries (unit-diagonal L below
+// the diagonal, U on and above it, as rocSPARSE csrilu0 stores them)
+extern "C" int gls_ilu_factors(gls_ctx *c, int32_t *perm, int32_t *rowp, int32_t *col, double *val) {
+  GLS_TRY(check_ctx(c));
+  auto &I = c->ilu;
+  if (!I.on) return set_err(GLS_EINVAL, "no ILU attached");
+  GLS_TRY(ensure_diag(c));
+  GLS_TRY(ensure_ilu(c));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (perm) HIP_TRY(hipMemcpy(perm, I.perm.p, sizeof(int32_t) * (size_t)c->n_dofs, hipMemcpyDeviceToHost));
+  if (rowp) HIP_TRY(hipMemcpy(rowp, I.rowp.p, sizeof(int32_t) * (size_t)(c->n_dofs + 1), hipMemcpyDeviceToHost));
+  if (col) HIP_TRY(hipMemcpy(col, I.col.p, sizeof(int32_t) * (size_t)I.nnz, hipMemcpyDeviceToHost));
+  if (val) HIP_TRY(hipMemcpy(val, I.val.p, sizeof(double) * (size_t)I.nnz, hipMemcpyDeviceToHost));
   return GLS_OK;
 }
 extern "C" int gls_ilu_info(const gls_ctx *c, int64_t *nnz, int *n_probes) {

@@ -31,7 +31,7 @@ EXPORTS = [
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy",
     "gls_dist_attach_rccl",
-    "gls_mg_attach", "gls_mg_detach", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
+    "gls_mg_attach", "gls_mg_detach", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -738,15 +738,31 @@ class GLSContext:
         check(self.L.gls_mg_detach(self.h), "gls_mg_detach")
         self._mg_levels = None
 
-    def attach_ilu(self, athresh=1e-8, rthresh=1.0):
-        """Assembled ILU(0) preconditioner (the reference's ILU-preconditioned GMRES, setup_ILU); the
-        Jacobian is probed from the device operator. Returns (nnz, n_probes)."""
-        self.L.gls_ilu_attach.argtypes = [C.c_void_p, C.c_double, C.c_double]
-        check(self.L.gls_ilu_attach(self.h, float(athresh), float(rthresh)), "gls_ilu_attach")
+    def attach_ilu(self, athresh=1e-8, rthresh=1.0, fill=0):
+        """Assembled ILU(fill) preconditioner (the reference's ILU-preconditioned GMRES, setup_ILU); the
+        Jacobian is probed from the device operator. Returns (nnz of the ILU pattern, n_probes)."""
+        self.L.gls_ilu_attach.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
+        check(self.L.gls_ilu_attach(self.h, int(fill), float(athresh), float(rthresh)), "gls_ilu_attach")
         nnz, npr = C.c_int64(), C.c_int()
         self.L.gls_ilu_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
         check(self.L.gls_ilu_info(self.h, C.byref(nnz), C.byref(npr)), "gls_ilu_info")
         return nnz.value, npr.value
+
+    def ilu_factors(self):
+        """(perm, scipy CSR of the factored ILU) in the factorization numbering: perm[dof] = its row;
+        strictly lower part = L (unit diagonal), upper part with the diagonal = U."""
+        import scipy.sparse as sp
+        nnz, _ = C.c_int64(), C.c_int()
+        self.L.gls_ilu_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
+        check(self.L.gls_ilu_info(self.h, C.byref(nnz), C.byref(_)), "gls_ilu_info")
+        perm = np.zeros(self.n_dofs, dtype=np.int32)
+        rowp = np.zeros(self.n_dofs + 1, dtype=np.int32)
+        col = np.zeros(nnz.value, dtype=np.int32)
+        val = np.zeros(nnz.value)
+        self.L.gls_ilu_factors.argtypes = [C.c_void_p] * 5
+        check(self.L.gls_ilu_factors(self.h, perm.ctypes.data, rowp.ctypes.data, col.ctypes.data, val.ctypes.data),
+              "gls_ilu_factors")
+        return perm, sp.csr_matrix((val, col, rowp), shape=(self.n_dofs, self.n_dofs))
 
     def ilu_matrix(self):
         """The probed operator matrix (scipy CSR) behind the attached ILU, before perturbation/factoring."""
@@ -932,3 +948,36 @@ def _hang_lines(n, node, off, master, w):
     master = np.ctypeslib.as_array(master, shape=(nm,)).copy()
     w = np.ctypeslib.as_array(w, shape=(nm,)).copy()
     return {int(node[i]): [(int(master[j]), float(w[j])) for j in range(off[i], off[i + 1])] for i in range(n)}
+
+
+def iluk_pattern(A, fill):
+    """Host-only ILU(fill) level-of-fill pattern of the square CSR graph A (scipy sparse): returns
+    (rowp, col, level) of the pattern, diagonal included, rows sorted (gls_iluk_pattern)."""
+    L = load()
+    A = A.tocsr()
+    A.sort_indices()
+    n = A.shape[0]
+    rowp = np.ascontiguousarray(A.indptr, dtype=np.int32)
+    col = np.ascontiguousarray(A.indices, dtype=np.int32)
+    nnz = C.c_int64()
+    L.gls_iluk_pattern.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_int64, C.POINTER(C.c_int64)]
+    check(L.gls_iluk_pattern(n, rowp.ctypes.data, col.ctypes.data, int(fill), None, None, None, 0, C.byref(nnz)),
+          "gls_iluk_pattern")
+    orow = np.zeros(n + 1, dtype=np.int32)
+    ocol = np.zeros(nnz.value, dtype=np.int32)
+    olev = np.zeros(nnz.value, dtype=np.int32)
+    check(L.gls_iluk_pattern(n, rowp.ctypes.data, col.ctypes.data, int(fill), orow.ctypes.data, ocol.ctypes.data,
+                             olev.ctypes.data, nnz.value, C.byref(nnz)), "gls_iluk_pattern")
+    return orow, ocol, olev
+
+
+def cuthill_mckee(adj_off, adj, dof_off, dofs):
+    """Host-only DoF renumbering of gls_ilu_attach (deal.II Cuthill_McKee on a node graph): returns
+    order[new index] = DoF (gls_cuthill_mckee)."""
+    L = load()
+    a = [np.ascontiguousarray(x, dtype=np.int64) for x in (adj_off, adj, dof_off, dofs)]
+    order = np.zeros(len(a[3]), dtype=np.int64)
+    L.gls_cuthill_mckee.argtypes = [C.c_int64] + [C.c_void_p] * 5
+    check(L.gls_cuthill_mckee(len(a[0]) - 1, *(x.ctypes.data for x in a), order.ctypes.data), "gls_cuthill_mckee")
+    return order

@@ -114,20 +114,14 @@ def test_reference_tgv_sdirk_cases(tmp_path, method):
 
 @pytest.mark.gpu
 def test_reference_cylinder_kelly_adaptation(tmp_path):
-    """applications_tests/gls_navier_stokes_2d/cylinder_gls (gmsh cylinder_structured.msh, Q1-Q1, slip
-    walls, 3 steady Kelly adaptations: fraction type number, refine 0.3 / coarsen 0.1, max 70000
-    cells, max level 5): Kelly with MappingQ face pieces on hanging faces, the p::d fixed-number
-    thresholds, deal.II mesh smoothing, the unstructured hierarchy's refine / coarsen / balance and
-    the hanging-node DoF count reproduce the reference's active-cell and DoF counts of every cycle
-    (the force summaries are out of scope). The solves are converged (Newton 1e-10, GMRES rel 1e-12)
-    instead of the prm's 1e-4 / 1e-4: Kelly marks by a threshold on floats, and with this build's
-    ILU(0) stopped at 1e-4 (the reference uses ILU(1)) the second cycle refines 6 cells less (4284 vs
-    4302 cells); the converged discrete solution gives the reference's counts in every cycle (solved
-    here with Jacobi-GMRES: converging ILU(0)-GMRES to 1e-12 costs minutes of triangular solves)."""
+    """applications_tests/gls_navier_stokes_2d/cylinder_gls as shipped (gmsh cylinder_structured.msh,
+    Q1-Q1, slip walls, 3 steady Kelly adaptations: fraction type number, refine 0.3 / coarsen 0.1, max
+    70000 cells, max level 5; Newton 1e-4, GMRES rel 1e-4 with ILU(1)): Kelly with MappingQ face
+    pieces on hanging faces, the p::d fixed-number thresholds, deal.II mesh smoothing, the
+    unstructured hierarchy's refine / coarsen / balance, the hanging-node DoF count and the ILU(1)-GMRES
+    inexact solves reproduce the reference's active-cell and DoF counts of every cycle (the force
+    summaries are out of scope)."""
     ref = open(os.path.join(CASES, "cylinder_gls.output")).read()
-    out = run_case(tmp_path, "cylinder_gls", 2, "--precond", "jacobi", prm_edit=lambda t: t.replace(
-        "set tolerance               = 1e-4", "set tolerance = 1e-10").replace(
-        "set relative residual       = 1e-4", "set relative residual = 1e-12").replace(
-        "set minimum residual        = 1e-9", "set minimum residual = 1e-14"))
+    out = run_case(tmp_path, "cylinder_gls", 2)
     ours, theirs = setup_lines(out), setup_lines(ref)
     assert ours == theirs, (ours, theirs)
