@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iomanip>
 #include <map>
 #include <memory>
 #include <sstream>
@@ -723,9 +724,68 @@ struct CellEval {
 // ---------------------------------------------------------------------------------------------
 // the solver
 // ---------------------------------------------------------------------------------------------
+// TimerOutput(pcout, summary, wall_times) of NavierStokesBase (navier_stokes_base.cc:63-66): named
+// sections with call counts and wall seconds (device work drained at the section boundaries),
+// printed as deal.II's TimerOutput::print_summary table; output disabled for timer/type = none
+// (navier_stokes_base.cc:97-98), per iteration with a reset (:449-455), and at destruction.
+struct SectionTimer {
+  bool on = false;
+  std::map<std::string, std::pair<int, double>> sec;  // name -> (calls, wall seconds), name order
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  struct Scope {
+    SectionTimer &T;
+    std::string name;
+    std::chrono::steady_clock::time_point a;
+    Scope(SectionTimer &t, const char *n) : T(t), name(n) {
+      if (T.on) {
+        (void)hipDeviceSynchronize();
+        a = std::chrono::steady_clock::now();
+      }
+    }
+    ~Scope() {
+      if (!T.on) return;
+      (void)hipDeviceSynchronize();
+      T.add(name, 1, std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count());
+    }
+  };
+  void add(const std::string &name, int calls, double seconds) {
+    auto &e = sec[name];
+    e.first += calls;
+    e.second += seconds;
+  }
+  void reset() {
+    sec.clear();
+    t0 = std::chrono::steady_clock::now();
+  }
+  void print() const {
+    if (!on) return;
+    const double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::ostringstream o;
+    o << "\n\n+---------------------------------------------+------------+------------+\n"
+      << "| Total wallclock time elapsed since start    |";
+    o << std::setw(10) << std::setprecision(3) << std::right << total << "s |            |\n";
+    o << "|                                             |            |            |\n";
+    o << "| Section                         | no. calls |  wall time | % of total |\n";
+    o << "+---------------------------------+-----------+------------+------------+";
+    for (const auto &e : sec) {
+      std::string name = e.first;
+      name.resize(32, ' ');
+      o << "\n| " << name << "| " << std::setw(9) << e.second.first << " |" << std::setw(10) << std::setprecision(3)
+        << e.second.second << "s |" << std::setw(10);
+      const double f = total > 0 ? e.second.second / total : 0.0;
+      if (f > 0.001) o << std::setprecision(2) << f * 100;
+      else o << 0.0;
+      o << "% |";
+    }
+    o << "\n+---------------------------------+-----------+------------+------------+\n\n";
+    std::fputs(o.str().c_str(), stdout);
+  }
+};
+
 struct Solver {
   Params &P;
   bool use_mg;
+  SectionTimer timer;
   Mesh m;
   Constraints C;
   gls_ctx *ctx = nullptr;
@@ -756,7 +816,7 @@ struct Solver {
     std::snprintf(b, sizeof(b), "%g", v);
     return b;
   }
-  Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) {}
+  Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) { timer.on = P.timer != "none"; }
   bool use_ilu;              // assembled ILU(0) where no multigrid hierarchy exists (--precond jacobi: off)
   gls_ctx *ilu_ctx = nullptr;  // the context the ILU was attached to (a new mesh builds a new context)
   ~Solver() {
@@ -918,6 +978,7 @@ struct Solver {
   // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels
   // and a Jacobi-preconditioned GMRES (no multigrid on locally refined meshes).
   void setup_refined(gls_refined_mesh *R_new) {
+    SectionTimer::Scope ts(timer, "setup_dofs");
     release();
     rmesh = R_new;
     const int n = 1;
@@ -956,6 +1017,7 @@ struct Solver {
   }
 
   void setup(int n) {
+    SectionTimer::Scope ts(timer, "setup_dofs");
     release();
     m = build_mesh(P, n, periodic_mask());
     C = make_constraints(P, m, time);
@@ -1002,6 +1064,7 @@ struct Solver {
   // FE space, constraints and context on the current triangulation (per-cell kernels with MappingQ
   // geometry, Jacobi-preconditioned GMRES)
   void setup_general() {
+    SectionTimer::Scope ts(timer, "setup_dofs");
     release();
     if (space) gls_fe_space_destroy(space);
     space = nullptr;
@@ -1207,7 +1270,19 @@ struct Solver {
     np.skip_iterations = P.skip_iterations;
     np.is_initial_step = 0;
     np.force_matrix_renewal = force_renewal ? 1 : 0;
+    if (timer.on) ck(gls_section_timing(ctx, 1), "gls_section_timing");
     ck(gls_newton_solve(ctx, d_present, d_m1, d_m2, d_m3, &np), "gls_newton_solve");
+    if (timer.on) {  // the library's Newton / GMRES sections (gls_navier_stokes.cc:921, 1028, 1165, 1274)
+      static const char *names[GLS_N_SECTIONS] = {"assemble_system", "assemble_rhs", "setup_ILU", "setup_GMG",
+                                                  "solve_linear_system"};
+      for (int sct = 0; sct < GLS_N_SECTIONS; ++sct) {
+        double sec = 0;
+        int calls = 0;
+        ck(gls_section_get(ctx, sct, &sec, &calls), "gls_section_get");
+        if (calls > 0) timer.add(names[sct], calls, sec);
+      }
+      ck(gls_section_timing(ctx, 0), "gls_section_timing");
+    }
     if (np.linear_failures > 0)
       printf("  -Warning: %d linear solve(s) stopped at the iteration limit before the tolerance\n", np.linear_failures);
     dev_changed();
@@ -1267,6 +1342,7 @@ struct Solver {
 
   // ---- post-processing
   std::pair<double, double> l2_error() {  // QGauss(k+2), pressures compared mean-free
+    SectionTimer::Scope ts(timer, "error");
     CellEval ev(m, m.k + 2);
     std::vector<double> X, E;
     for (int64_t c = 0; c < m.nc; ++c)
@@ -1367,6 +1443,7 @@ struct Solver {
     return cmax;
   }
   void write_output() {
+    SectionTimer::Scope ts(timer, "output");
     need_host();
     char tag[32];
     std::snprintf(tag, sizeof(tag), ".%05d", step);
@@ -1408,7 +1485,11 @@ struct Solver {
     if (P.enstrophy || P.kinetic || (!initial && P.analytical)) need_host();
     // post-processing lines of NavierStokesBase::postprocess (navier_stokes_base.cc:791-853)
     if (P.enstrophy && P.pp_verbose) std::printf("Enstrophy  : %s\n", g6(volume_average(true)).c_str());
-    if (P.kinetic && P.pp_verbose) std::printf("Kinetic energy : %s\n", g6(volume_average(false)).c_str());
+    if (P.kinetic) {  // navier_stokes_base.cc:824-839
+      SectionTimer::Scope ts(timer, "kinetic_energy_calculation");
+      const double ke = volume_average(false);
+      if (P.pp_verbose) std::printf("Kinetic energy : %s\n", g6(ke).c_str());
+    }
     if (!initial && P.analytical) {
       const auto e = l2_error();
       if (P.method == Method::steady) errors.push_back({(double)m.nc, e.first, e.second});
@@ -1430,6 +1511,7 @@ struct Solver {
   }
   // uniform refinement with interpolation of the Qk fields onto the refined lattice
   void refine_uniform() {
+    SectionTimer::Scope ts(timer, "refine");
     need_host();
     if (m.general) {  // refine_global + SolutionTransfer (gls_fe_space_transfer)
       const std::vector<double> sol = present;
@@ -1495,6 +1577,7 @@ struct Solver {
   // present solution (:684-733). The forest is the hyper_cube's one coarse cell refined
   // `initial refinement` times, so leaf levels are deal.II's cell levels.
   void refine_kelly() {
+    SectionTimer::Scope ts(timer, "refine");
     if (m.general) {
       refine_kelly_general();
       return;
@@ -1756,11 +1839,8 @@ struct Solver {
     end_of_step();
     postprocess(true);
     const bool steady = P.method == Method::steady;
-    const auto t_start = std::chrono::steady_clock::now();
     while (steady ? step < P.mesh_adapt + 1 : time < P.t_end - 1e-12 * dt_now) {
       ++step;
-      const auto t_step = std::chrono::steady_clock::now();
-      const int nit0 = newton_its, lit0 = linear_its;
       if (steady) {
         time = step;
       } else {
@@ -1788,19 +1868,13 @@ struct Solver {
       }
       postprocess(false);
       end_of_step();
-      if (P.timer == "iteration") {  // the TimerOutput summary per iteration (navier_stokes_base.cc:449-453), condensed
-        hk(hipDeviceSynchronize(), "timer");
-        const double w = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_step).count();
-        std::printf("   Timer: iteration %d wall time %.3f s (Newton iterations %d, linear iterations %d)\n", step, w,
-                    newton_its - nit0, linear_its - lit0);
+      if (P.timer == "iteration") {  // TimerOutput print_summary + reset per iteration (navier_stokes_base.cc:449-455)
+        timer.print();
+        timer.reset();
       }
     }
-    if (P.timer != "none") {
-      const double w = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-      std::printf("   Timer: total wall time %.3f s over %d iterations (Newton iterations %d, linear iterations %d)\n", w,
-                  step, newton_its, linear_its);
-    }
     report();
+    timer.print();  // the TimerOutput destructor's summary (output frequency 'summary')
     if (stats) std::printf("newton_iterations = %d, linear_iterations = %d\n", newton_its, linear_its);
   }
 };

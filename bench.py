@@ -14,8 +14,9 @@ fixed; linear iterations and residual evaluations are reported.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
 Multi-GPU (N>1): the 128^3 mesh is partitioned into contiguous Morton brick ranges (one per GPU,
-p4est-like); ghost import / export-add and the GMRES dot products go over RCCL (torch.distributed
-"nccl") through the C-ABI callbacks (softx_2020_200_amd/dist.py). Fixed total problem ->
+p4est-like); ghost import / export-add and the GMRES dot products go over the library's own RCCL
+communicator (gls_dist_attach_rccl; the ghost import of the J.v overlaps the interior bricks on a
+second stream; --dist-impl torch: torch.distributed callbacks instead). Fixed total problem ->
 "scaling": "strong"; value = nonlinear iterations/s of the whole job.
 """
 from __future__ import annotations
@@ -184,10 +185,13 @@ def main():
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo stages through the host (testing on one GPU)")
-    ap.add_argument("--dist-impl", default="torch", choices=["torch", "native"],
-                    help="ghost exchange / reductions: torch.distributed callbacks (default) or the library's own "
-                         "RCCL communicator (gls_dist_attach_rccl: ncclSend/ncclRecv/ncclAllReduce on the context stream)")
+    ap.add_argument("--dist-impl", default="native", choices=["torch", "native"],
+                    help="ghost exchange / reductions: the library's own RCCL communicator (default; gls_dist_attach_rccl: "
+                         "ncclSend/ncclRecv/ncclAllReduce on the context stream, ghost import overlapped with the "
+                         "interior bricks) or torch.distributed callbacks (host-synchronous; the gloo tests)")
     args = ap.parse_args()
+    if args.dist_backend == "gloo":  # host-staged testing transport: no RCCL communicator
+        args.dist_impl = "torch"
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -242,6 +242,20 @@ int gls_cuthill_mckee(int64_t n_nodes, const int64_t *adj_off, const int64_t *ad
  * on device vectors: present (in/out, DEVICE, length n_dofs). History from gls_set_state's u1..u3
  * slots is given here explicitly.
  * ------------------------------------------------------------------------------------------ */
+/* TimerOutput sections of the Newton / GMRES path (the reference's TimerOutput::Scope names,
+ * gls_navier_stokes.cc:921 assemble_system, :1028 assemble_rhs, :1165 setup_ILU, :1182 setup_AMG (here
+ * the geometric multigrid's setup), :1274 solve_linear_system): while enabled, gls_newton_solve
+ * accumulates each section's host wall time (context stream drained at the section boundaries) and
+ * call count. gls_section_timing(ctx, on) also zeroes the accumulators. */
+#define GLS_SEC_ASSEMBLE_SYSTEM 0
+#define GLS_SEC_ASSEMBLE_RHS 1
+#define GLS_SEC_SETUP_ILU 2
+#define GLS_SEC_SETUP_GMG 3
+#define GLS_SEC_SOLVE_LINEAR 4
+#define GLS_N_SECTIONS 5
+int gls_section_timing(gls_ctx *ctx, int enable);
+int gls_section_get(const gls_ctx *ctx, int section, double *seconds, int *calls);
+
 #define GLS_NEWTON 0
 #define GLS_SKIP_NEWTON 1
 typedef struct {

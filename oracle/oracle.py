@@ -343,9 +343,40 @@ class MappedProblem(StructuredProblem):
         return [set(b for b in range(32) if (int(m) >> b) & 1) for m in self.vnode_bid]
 
     def set_dirichlet(self, bcs):
-        if any(t == "slip" for t, _, _ in bcs):
-            raise ValueError("slip on mapped cells (curved normals) is not restated")
-        return super().set_dirichlet(bcs)
+        """As StructuredProblem.set_dirichlet; 'slip' is restated for axis-aligned planar boundaries
+        only (the id's nodes lie on one or two planes x_d = const: n = +-e_d, u_d = 0, as
+        compute_no_normal_flux_constraints gives there); curved slip walls raise."""
+        X = self.vnode_coords()
+        bids = self.boundary_ids_of_vnodes()
+        self.constrained[:] = 0
+        if self.hang is not None:
+            self.constrained[np.nonzero(self.hang[0][1:] > self.hang[0][:-1])[0]] = 1
+        self.dirichlet = {}
+        scale = max(float(np.abs(X).max()), 1.0)
+        for typ, bid, func in bcs:
+            nodes = np.array([i for i, s in enumerate(bids) if bid in s], dtype=np.int64)
+            if nodes.size == 0:
+                continue
+            comps = np.ones((nodes.size, self.dim), dtype=bool)
+            vals = np.zeros((nodes.size, self.dim))
+            if typ == "function":
+                vals = np.asarray(func(X[nodes]), dtype=np.float64).reshape(nodes.size, self.dim)
+            elif typ == "slip":
+                flat = [d for d in range(self.dim)
+                        if len(np.unique(np.round(X[nodes, d] / (1e-9 * scale)))) <= 2]
+                if len(flat) != 1:
+                    raise ValueError("slip on a curved / oblique boundary (id %d) is not restated" % bid)
+                comps[:] = False
+                comps[:, flat[0]] = True
+            elif typ != "noslip":
+                raise ValueError(typ)
+            for nd, v, cm in zip(nodes, vals, comps):
+                for c in range(self.dim):
+                    dof = nd * self.dim + c
+                    if cm[c] and not self.constrained[dof]:
+                        self.constrained[dof] = 1
+                        self.dirichlet[dof] = float(v[c])
+        return self
 
 
 class Oracle:

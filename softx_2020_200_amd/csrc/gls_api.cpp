@@ -482,6 +482,11 @@ struct gls_ctx {
     int n_hist = 0, scheme = GLS_STEADY;
   } jf;
   int skip_consecutive = 0;  // SkipNewtonNonLinearSolver::consecutive_iters (persists across solves)
+  // TimerOutput sections of the reference's Newton/GMRES path (gls_section_timing): wall seconds and
+  // calls, stream-synchronised at the section boundaries while enabled
+  bool sec_on = false;
+  double sec_t[GLS_N_SECTIONS] = {};
+  int sec_n[GLS_N_SECTIONS] = {};
   // timing
   bool timing = false;
   struct Ev { int which; hipEvent_t a, b; };
@@ -920,10 +925,13 @@ int build_brick_split(gls_ctx *c, const std::vector<char> &flag) {
 // J.v launched as two brick subsets (boundary, then interior) with the ghost import between them:
 // the RCCL transport imports on the exchange stream while the interior bricks run
 // (GLS_NO_OVERLAP=1: off); GLS_SPLIT_TEST=m on a single-GPU context splits at "bricks b % m == 0"
-// with no exchange, for the bitwise test of the split launch
+// with no exchange, for the bitwise test of the split launch; GLS_SPLIT_DIST=1 runs the same split
+// launch with the callback transport (import first, then interior and boundary bricks), so the
+// boundary / interior classification of a real partition is tested without an RCCL communicator
 bool split_jv_enabled(gls_ctx *c) {
   if (!c->use_brick || !c->use_qdata || c->use_colors || c->hang.on || !gls::brick_subset_supported(c->k)) return false;
-  if (c->dist.on) return c->dist.comm != nullptr && c->split.p && !std::getenv("GLS_NO_OVERLAP");
+  if (c->dist.on)
+    return c->split.p && !std::getenv("GLS_NO_OVERLAP") && (c->dist.comm != nullptr || std::getenv("GLS_SPLIT_DIST"));
   const char *t = std::getenv("GLS_SPLIT_TEST");
   if (!t || std::atoi(t) < 1) return false;
   if (!c->split.p) {
@@ -1015,7 +1023,9 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       auto &D = c->dist;
       double *vv = const_cast<double *>(v);
       const int64_t voff = 3 * (int64_t)c->n_vnodes;
-      if (D.on) {  // ghost import of v on the exchange stream, ordered after v's producer
+      if (D.on && !D.comm) {  // callback transport (GLS_SPLIT_DIST): the import completes first
+        GLS_TRY(dist_import(c, vv));
+      } else if (D.on) {  // ghost import of v on the exchange stream, ordered after v's producer
         HIP_TRY(hipEventRecord(D.ev_ready, c->stream));
         HIP_TRY(hipStreamWaitEvent(D.xstream, D.ev_ready, 0));
         HIP_TRY(gls::vec_pack_nodes(vv, D.send_nodes.p, D.n_send, voff, D.send_buf, D.xstream));
@@ -1027,7 +1037,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       Q.subset = c->split.p + c->split_bnd;
       Q.subset_n = c->split_int;
       if (Q.subset_n > 0) HIP_TRY(gls::launch_brick_kernel(c->k, mode, Q, c->tables, c->stream));
-      if (D.on) HIP_TRY(hipStreamWaitEvent(c->stream, D.ev_done, 0));
+      if (D.on && D.comm) HIP_TRY(hipStreamWaitEvent(c->stream, D.ev_done, 0));
       Q.subset = c->split.p;
       Q.subset_n = c->split_bnd;
       if (Q.subset_n > 0) HIP_TRY(gls::launch_brick_kernel(c->k, mode, Q, c->tables, c->stream));
@@ -2695,6 +2705,27 @@ int newton_template(Phys &ph, double tolerance, int max_iterations, int verbosit
   return GLS_OK;
 }
 
+// one TimerOutput::Scope of the reference (gls_navier_stokes.cc:921, 1028, 1165, 1274): host wall
+// time of the section with the context stream drained on entry and exit (the reference's sections
+// are synchronous host code); no cost while the timer is off
+struct SectionScope {
+  gls_ctx *c;
+  int s;
+  std::chrono::steady_clock::time_point t0;
+  SectionScope(gls_ctx *c_, int s_) : c(c_), s(s_) {
+    if (c->sec_on) {
+      (void)hipStreamSynchronize(c->stream);
+      t0 = std::chrono::steady_clock::now();
+    }
+  }
+  ~SectionScope() {
+    if (!c->sec_on) return;
+    (void)hipStreamSynchronize(c->stream);
+    c->sec_t[s] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    ++c->sec_n[s];
+  }
+};
+
 // GLS physics on device vectors (the GLSNavierStokesSolver side of the plugin API)
 struct DevicePhysics {
   gls_ctx *c;
@@ -2709,6 +2740,7 @@ struct DevicePhysics {
     return gls_set_state(c, eval, u1, u2, u3);
   }
   int assemble_matrix_and_rhs() {  // matrix-free: residual + the Jacobian diagonal at this state
+    SectionScope t(c, GLS_SEC_ASSEMBLE_SYSTEM);
     if (skip) {  // renew the frozen Jacobian at this evaluation point
       GLS_TRY(gls_freeze_jacobian(c, 0));
       GLS_TRY(gls_set_state(c, eval, u1, u2, u3));
@@ -2717,7 +2749,10 @@ struct DevicePhysics {
     GLS_TRY(ensure_diag(c));
     return skip ? gls_freeze_jacobian(c, 1) : GLS_OK;
   }
-  int assemble_rhs() { return gls_residual(c, rhs); }
+  int assemble_rhs() {
+    SectionScope t(c, GLS_SEC_ASSEMBLE_RHS);
+    return gls_residual(c, rhs);
+  }
   int rhs_norm(double &r) {
     double r2;
     GLS_TRY(device_dot(c, rhs, rhs, &r2));
@@ -2726,6 +2761,16 @@ struct DevicePhysics {
   }
   int solve_linear_system(int &its) {
     gls_linear_params lp = lin;
+    if (c->mg.on) {  // preconditioner setup first (setup_ILU / setup_AMG, gls_navier_stokes.cc:1165, 1182)
+      SectionScope t(c, GLS_SEC_SETUP_GMG);
+      GLS_TRY(ensure_diag(c));
+      GLS_TRY(mg_prepare(c));
+    } else if (c->ilu.on) {
+      SectionScope t(c, GLS_SEC_SETUP_ILU);
+      GLS_TRY(ensure_diag(c));
+      GLS_TRY(ensure_ilu(c));
+    }
+    SectionScope t(c, GLS_SEC_SOLVE_LINEAR);
     const int rc = gls_solve_linear(c, rhs, update, &lp);
     if (rc < 0 && rc != GLS_ENOCONV) return rc;
     if (rc == GLS_ENOCONV) {
@@ -2807,6 +2852,23 @@ int gls_newton_solve(gls_ctx *c, double *present, const double *u1, const double
   prm->residual_evaluations = st.residuals;
   prm->final_residual = st.final_res;
   prm->linear_failures = ph.linear_failures;
+  return GLS_OK;
+}
+
+int gls_section_timing(gls_ctx *c, int enable) {
+  GLS_TRY(check_ctx(c));
+  c->sec_on = enable != 0;
+  for (int i = 0; i < GLS_N_SECTIONS; ++i) {
+    c->sec_t[i] = 0.;
+    c->sec_n[i] = 0;
+  }
+  return GLS_OK;
+}
+int gls_section_get(const gls_ctx *c, int section, double *seconds, int *calls) {
+  if (!c) return set_err(GLS_EINVAL, "null context");
+  if (section < 0 || section >= GLS_N_SECTIONS) return set_err(GLS_EINVAL, "section %d", section);
+  if (seconds) *seconds = c->sec_t[section];
+  if (calls) *calls = c->sec_n[section];
   return GLS_OK;
 }
 

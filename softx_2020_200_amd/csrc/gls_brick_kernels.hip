@@ -58,6 +58,12 @@
 #define GLS_STAGE_LAYOUT 1
 #endif
 
+#ifndef GLS_QD_PREFETCH
+// 1: the cached J.v issues its linearization loads before the v sweeps (in flight during them,
+// 16 VGPRs live across the sweeps); 0: after the sweeps (short live ranges)
+#define GLS_QD_PREFETCH 0
+#endif
+
 #ifndef GLS_LDS_SPLIT
 #define GLS_LDS_SPLIT 0  // 1 asm / 2 masked: FP64 LDS reads as single ds_read_b64 -- measured slower (profiles/r02_lds_split_ab.txt)
 #endif
@@ -726,6 +732,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     for (int e = 0; e < 3; ++e) Tc[13 + e] = -JxW * tau * R[e] * ih[e];
   } else {
     // ---------------- phase B: the trial function v at this lane's quadrature point
+    if constexpr (CACHED && GLS_QD_PREFETCH && !kQdLite) load_qd();
     Real v[3] = {0., 0., 0.}, gv[3][3] = {}, lv[3] = {0., 0., 0.};
 #pragma unroll
     for (int c = 0; c < 3; ++c) vel_field(FV + c, v[c], gv[c], lv[c]);
@@ -735,7 +742,7 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
 #pragma unroll
       for (int c = 0; c < 3; ++c) scal_fields(c, 0, 0, u[c], gu[c], dummy);
     }
-    if constexpr (CACHED) load_qd();
+    if constexpr (CACHED && !(GLS_QD_PREFETCH && !kQdLite)) load_qd();
     const Real aj = P.alpha_jac;
     Real S[3], A[3];
 #pragma unroll

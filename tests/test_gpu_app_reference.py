@@ -93,10 +93,12 @@ def test_reference_tgv_sdirk_cases(tmp_path, method):
     """The reference's taylor-green-vortex_gls_{sdirk2,sdirk3} application tests as shipped (Q2-Q1,
     periodic, L2-projection IC, one step of 0.1, Newton tol 1e-6, GMRES rel 1e-4 -- an inexact
     Newton): enstrophy and kinetic energy before and after the step match the .output to all printed
-    digits. The L2 error depends on where the inexact linear solves stop: with exact solves the
-    oracle gives 1.38239e-4 (SDIRK3), with this build's ILU(0)-GMRES at the reference's tolerances
-    1.38207e-4; the reference's ILU(1)-GMRES value 1.38223e-4 lies between the two, so the error is
-    checked at the reference's inexact-Newton scale (3e-4 relative; SDIRK2: printed digits)."""
+    digits. The L2 error depends on where the inexact linear solves stop. For SDIRK3, exact solves
+    give 1.38239e-4 (oracle); this build's ILU(1)-GMRES at the reference's tolerances gives
+    1.38249e-4 (ILU(0): 1.38207e-4); the reference printed 1.38223e-4. The values differ by 1.9e-4
+    relative: the DoF order of the ILU factors and AztecOO's GMRES internals decide where the inexact
+    Newton stops. So the error is checked at that scale (3e-4 relative). SDIRK2 is checked at 1e-5
+    relative (1.20259e-3 vs the printed 1.20258e-3)."""
     name = "taylor-green-vortex_gls_" + method
     prm = open(os.path.join(CASES, name + ".prm")).read()
     prm = re.sub(r"set output frequency\s*=\s*1 ", "set output frequency = 1000000 ", prm)
@@ -114,14 +116,41 @@ def test_reference_tgv_sdirk_cases(tmp_path, method):
 
 @pytest.mark.gpu
 def test_reference_cylinder_kelly_adaptation(tmp_path):
-    """applications_tests/gls_navier_stokes_2d/cylinder_gls as shipped (gmsh cylinder_structured.msh,
-    Q1-Q1, slip walls, 3 steady Kelly adaptations: fraction type number, refine 0.3 / coarsen 0.1, max
-    70000 cells, max level 5; Newton 1e-4, GMRES rel 1e-4 with ILU(1)): Kelly with MappingQ face
-    pieces on hanging faces, the p::d fixed-number thresholds, deal.II mesh smoothing, the
-    unstructured hierarchy's refine / coarsen / balance, the hanging-node DoF count and the ILU(1)-GMRES
-    inexact solves reproduce the reference's active-cell and DoF counts of every cycle (the force
-    summaries are out of scope)."""
+    """applications_tests/gls_navier_stokes_2d/cylinder_gls run as shipped (no prm edit): gmsh
+    cylinder_structured.msh, Q1-Q1, slip walls, 3 steady Kelly adaptations (fraction type number,
+    refine 0.3 / coarsen 0.1, max 70000 cells, max level 5), Newton 1e-4 and ILU(1)-GMRES rel 1e-4.
+    The first two meshes reproduce the reference's counts exactly (1167/3750, 2247/7134). The third
+    mesh has 4293 active cells and 13629 DoFs, against the reference's 4302 and 13653. The fourth has
+    8256 and 26040, against 8268 and 26076.
+
+    Remaining cause: the inexact solves. Kelly marks by a float threshold, and the solve stops at
+    GMRES rel 1e-4. Where it stops depends on the ILU(1) factors, which depend on the DoF order:
+    deal.II's Cuthill-McKee runs on deal.II's own initial DoF numbering, which this build cannot
+    reproduce. It also depends on AztecOO's GMRES internals. With ILU(0) the third mesh had 4284
+    cells. With converged solves (Newton 1e-10, GMRES rel 1e-12) all four meshes match the
+    reference exactly (the second test below)."""
     ref = open(os.path.join(CASES, "cylinder_gls.output")).read()
     out = run_case(tmp_path, "cylinder_gls", 2)
+    ours, theirs = setup_lines(out), setup_lines(ref)
+    assert len(ours) == len(theirs) == 12, (ours, theirs)
+    assert ours[:6] == theirs[:6], (ours, theirs)
+    count = lambda l: int(l.split(":")[1])
+    for a, b in zip(ours[6:], theirs[6:]):
+        if a.startswith("Volume"):
+            assert a == b
+        else:  # inexact-solve spread of the Kelly marking (the measured values are in the docstring)
+            assert abs(count(a) - count(b)) <= 0.005 * count(b), (a, b)
+
+
+@pytest.mark.gpu
+def test_reference_cylinder_kelly_adaptation_converged(tmp_path):
+    """The same case with the solves converged (Newton 1e-10, GMRES rel 1e-12): the discrete solution
+    no longer depends on the preconditioner, and every cycle's active-cell and DoF counts equal the
+    reference's (1167/3750, 2247/7134, 4302/13653, 8268/26076)."""
+    ref = open(os.path.join(CASES, "cylinder_gls.output")).read()
+    out = run_case(tmp_path, "cylinder_gls", 2, prm_edit=lambda t: t.replace(
+        "set tolerance               = 1e-4", "set tolerance = 1e-10").replace(
+        "set relative residual       = 1e-4", "set relative residual = 1e-12").replace(
+        "set minimum residual        = 1e-9", "set minimum residual = 1e-14"))
     ours, theirs = setup_lines(out), setup_lines(ref)
     assert ours == theirs, (ours, theirs)

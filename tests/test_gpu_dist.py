@@ -189,3 +189,74 @@ def test_distributed_multigrid_matches_single_rank(world):
         assert e["x_rel"] < 1e-7, (rank, e)
         assert abs(e["newton_lin_its"][0] - e["newton_lin_its"][1]) <= 1, (rank, e)
         assert e["newton_x"] < 1e-7, (rank, e)
+
+
+def _split_worker(rank, world, port, q):
+    """The overlapped J.v's brick split (boundary bricks: a cell holds a ghost or exported node;
+    interior bricks read no ghost value) on a real partition: with the callback transport and
+    GLS_SPLIT_DIST=1 the J.v runs as interior + boundary subset launches after the import; it must be
+    bitwise the single launch, and both must match the single-rank J.v."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import softx_2020_200_amd as sx
+    from softx_2020_200_amd.dist import DistributedProblem, dist_import, local_vector, owned_global_dofs
+    from softx_2020_200_amd.problem import build_context, dirichlet_from_bcs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 8
+        m = sx.hyper_cube(3, n, 2, 2)
+        bcs = [("noslip", b, None) for b in (0, 1, 2, 4, 5)] + [("function", 3, (1.0, 0.0, 0.0))]
+        mask, ddofs, dvals = dirichlet_from_bcs(m, n, -1.0, 1.0, True, bcs)
+        ts = (0.01, 0.012, 0.01, 0.01)
+        g = build_context(m, viscosity=0.05, vnode_mask=mask)
+        g.set_time("bdf2", ts)
+        N = g.n_dofs
+        rng = np.random.default_rng(20200200 + 7)
+        u, u1, u2, v = (rng.uniform(-1, 1, N) for _ in range(4))
+        u[ddofs] = dvals
+        cu = lambda a: torch.tensor(a, dtype=torch.float64, device="cuda")
+        g.set_state(cu(u), cu(u1), cu(u2))
+        jv_g = g.jacobian_apply(cu(v)).cpu().numpy()
+        dp = DistributedProblem(m, rank, world, "cuda", viscosity=0.05, vnode_mask=mask, dirichlet=(ddofs, dvals),
+                                backend="gloo")
+        c = dp.ctx
+        c.set_time("bdf2", ts)
+        lv = lambda a: cu(local_vector(dp.plan, a, m["n_vnodes"]))
+        U, U1, U2 = lv(u), lv(u1), lv(u2)
+        dist_import(c, U1)
+        dist_import(c, U2)
+        c.set_state(U, U1, U2)
+        plain = c.jacobian_apply(lv(v)).cpu().numpy()
+        os.environ["GLS_SPLIT_DIST"] = "1"
+        split = c.jacobian_apply(lv(v)).cpu().numpy()
+        del os.environ["GLS_SPLIT_DIST"]
+        loc, glo = owned_global_dofs(dp.plan, m["n_vnodes"])
+        q.put((rank, {"bitwise": bool(np.array_equal(plain, split)),
+                      "rel": float(np.abs(split[loc] - jv_g[glo]).max() / np.abs(jv_g).max())}))
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_split_jv_on_partition_bitwise(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31300 + 10 * world + os.getpid() % 400
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, e in res:
+        assert "error" not in e, e
+        assert e["bitwise"] and e["rel"] < 1e-12, (rank, e)
