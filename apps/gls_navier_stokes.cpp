@@ -14,8 +14,13 @@
 // with mesh adaptation type uniform, or kelly = Kelly-driven refinement and coarsening on a forest
 // with hanging nodes, any number of levels); bc types noslip, function, periodic, slip.
 #include <hip/hip_runtime.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -35,6 +40,7 @@
 
 namespace {
 
+std::atomic<int> *g_abort = nullptr;  // --np: raised by a failing rank, every other rank stops
 [[noreturn]] void die(const char *fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -42,6 +48,7 @@ namespace {
   std::vfprintf(stderr, fmt, ap);
   std::fprintf(stderr, "\n");
   va_end(ap);
+  if (g_abort) g_abort->store(1);
   std::exit(2);
 }
 void ck(int rc, const char *what) {
@@ -724,6 +731,123 @@ struct CellEval {
 // ---------------------------------------------------------------------------------------------
 // the solver
 // ---------------------------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------------------------
+// `--np N`: the reference's `mpirun -np N gls_navier_stokes_{2d,3d} file.prm`
+// (applications/gls_navier_stokes_3d/gls_navier_stokes_3d.cc:32-33) without MPI: the program forks
+// N processes before any GPU call, one rank each (GPU rank % devices). Every rank holds the same
+// host-side triangulation, constraints and time loop (replicated, deterministic); the GPU work --
+// assembly, Jacobian action, GMRES / Newton, the ILU of its owned rows -- runs on the rank's cells
+// only (gls_gpart_* + gls_dist_attach_dofs, the p::d partition of navier_stokes_base.cc:55-60,
+// re-done after every adaptation). Ghost exchange and dot-product reductions go over RCCL when
+// every rank has its own GPU (gls_dist_attach_dofs_rccl), else through this host shared-memory
+// transport (callbacks: device -> host slot, barrier, peers' slots -> device). Host-side gathers
+// of the global solution (post-processing, Kelly, output) use the same shared memory.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxRanks = 64;
+struct ShmComm {
+  struct Header {
+    std::atomic<int> count, gen, abort;
+    unsigned char rccl_id[GLS_RCCL_ID_BYTES];
+    int64_t table[kMaxRanks][kMaxRanks][2];  // exchange mailbox: (start, count) of rank s's data for rank d
+  };
+  static constexpr size_t kSlot = (size_t)1 << 26;  // doubles per rank slot (virtual, NORESERVE)
+  static constexpr size_t kGlob = (size_t)1 << 27;  // doubles of the shared global vector
+  Header *hdr = nullptr;
+  double *slots = nullptr, *glob = nullptr;
+  int rank = 0, world = 1;
+  void create(int w) {
+    world = w;
+    const size_t bytes = sizeof(Header) + (size_t)w * kSlot * sizeof(double) + kGlob * sizeof(double) + 4096;
+    void *mem = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (mem == MAP_FAILED) die("--np: shared memory of %zu bytes not available", bytes);
+    hdr = new (mem) Header();
+    hdr->count.store(0);
+    hdr->gen.store(0);
+    hdr->abort.store(0);
+    g_abort = &hdr->abort;
+    char *base = static_cast<char *>(mem) + ((sizeof(Header) + 4095) / 4096) * 4096;
+    slots = reinterpret_cast<double *>(base);
+    glob = slots + (size_t)w * kSlot;
+  }
+  double *slot(int r) const { return slots + (size_t)r * kSlot; }
+  void barrier() const {  // sense-reversing; a rank that failed raises abort
+    const int g = hdr->gen.load();
+    if (hdr->count.fetch_add(1) == world - 1) {
+      hdr->count.store(0);
+      hdr->gen.fetch_add(1);
+      return;
+    }
+    while (hdr->gen.load() == g) {
+      if (hdr->abort.load()) _exit(3);
+      sched_yield();
+    }
+  }
+  // every rank writes values[i] at global position idx[i]; all receive the whole vector
+  void allgather(const double *values, const std::vector<int64_t> &idx, std::vector<double> &out) const {
+    if ((size_t)out.size() > kGlob) die("--np: global vector of %zu values exceeds the shared area", out.size());
+    for (size_t i = 0; i < idx.size(); ++i) glob[idx[i]] = values[i];
+    barrier();
+    std::memcpy(out.data(), glob, out.size() * sizeof(double));
+    barrier();
+  }
+  void bcast(std::vector<double> &v, int root) const {  // v sized alike on every rank
+    if (rank == root) std::memcpy(glob, v.data(), v.size() * sizeof(double));
+    barrier();
+    if (rank != root) std::memcpy(v.data(), glob, v.size() * sizeof(double));
+    barrier();
+  }
+};
+ShmComm g_comm;
+
+// host-staged exchange of one distributed context (gls_dist_attach_dofs callbacks)
+struct ShmExchange {
+  std::vector<int> nbrs;
+  std::vector<int64_t> soff, roff;
+  double *send = nullptr, *recv = nullptr, *red = nullptr;  // device buffers
+  std::vector<double> tmp;
+  ~ShmExchange() {
+    for (double *q : {send, recv, red})
+      if (q) (void)hipFree(q);
+  }
+  static int exchange(void *user, int phase) {
+    auto *x = static_cast<ShmExchange *>(user);
+    const ShmComm &C = g_comm;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    const std::vector<int64_t> &so = phase == 0 ? x->soff : x->roff, &ro = phase == 0 ? x->roff : x->soff;
+    double *src = phase == 0 ? x->send : x->recv, *dst = phase == 0 ? x->recv : x->send;
+    const int64_t ns = so.back();
+    if ((size_t)ns > ShmComm::kSlot) return -1;
+    if (ns && hipMemcpy(C.slot(C.rank), src, sizeof(double) * (size_t)ns, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (size_t i = 0; i < x->nbrs.size(); ++i) {
+      C.hdr->table[C.rank][x->nbrs[i]][0] = so[i];
+      C.hdr->table[C.rank][x->nbrs[i]][1] = so[i + 1] - so[i];
+    }
+    C.barrier();
+    for (size_t i = 0; i < x->nbrs.size(); ++i) {
+      const int s = x->nbrs[i];
+      const int64_t start = C.hdr->table[s][C.rank][0], cnt = C.hdr->table[s][C.rank][1];
+      if (cnt != ro[i + 1] - ro[i]) return -1;
+      if (cnt && hipMemcpy(dst + ro[i], C.slot(s) + start, sizeof(double) * (size_t)cnt, hipMemcpyHostToDevice) != hipSuccess)
+        return -1;
+    }
+    C.barrier();
+    return 0;
+  }
+  static int allreduce(void *user, double *dev, int n) {
+    auto *x = static_cast<ShmExchange *>(user);
+    const ShmComm &C = g_comm;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpy(C.slot(C.rank), dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    C.barrier();
+    x->tmp.assign((size_t)n, 0.0);
+    for (int r = 0; r < C.world; ++r)  // rank order: the same sum on every rank
+      for (int i = 0; i < n; ++i) x->tmp[(size_t)i] += C.slot(r)[i];
+    C.barrier();
+    return hipMemcpy(dev, x->tmp.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+  }
+};
+
 // TimerOutput(pcout, summary, wall_times) of NavierStokesBase (navier_stokes_base.cc:63-66): named
 // sections with call counts and wall seconds (device work drained at the section boundaries),
 // printed as deal.II's TimerOutput::print_summary table; output disabled for timer/type = none
@@ -786,6 +910,16 @@ struct Solver {
   Params &P;
   bool use_mg;
   SectionTimer timer;
+  // --np: this process's rank, the rank count, the RCCL communicator (one GPU per rank) and the
+  // rank-local part of the current mesh (local DoF -> global DoF, owned DoFs, transport state)
+  int rank = 0, world = 1;
+  gls_rccl *rccl = nullptr;
+  struct Local {
+    std::vector<int64_t> l2g, g2l, own_l, own_g;
+    std::unique_ptr<ShmExchange> xchg;
+    std::vector<double> tmp;
+  } loc;
+  int64_t ndev() const { return world > 1 ? (int64_t)loc.l2g.size() : m.n_dofs(); }
   Mesh m;
   Constraints C;
   gls_ctx *ctx = nullptr;
@@ -819,6 +953,31 @@ struct Solver {
   Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) { timer.on = P.timer != "none"; }
   bool use_ilu;              // assembled ILU(0) where no multigrid hierarchy exists (--precond jacobi: off)
   gls_ctx *ilu_ctx = nullptr;  // the context the ILU was attached to (a new mesh builds a new context)
+  int64_t ilu_block_dofs = 0;  // block-Jacobi ILU subdomain size (0: one block, the single-rank reference)
+  std::string dump_dir;        // --dump DIR: the state of every iteration's last solve (test hook)
+  int last_scheme = GLS_STEADY;
+  double last_ts[4] = {1, 1, 1, 1};
+  // --dump: after an iteration, the last nonlinear solve's scheme, time steps, mesh size and its
+  // present solution + history (raw little-endian float64, n_dofs each) as DIR/iterNNNN.{meta,bin}
+  void dump_state() {
+    if (dump_dir.empty()) return;
+    need_host();
+    if (rank != 0) return;
+    char b[64];
+    std::snprintf(b, sizeof(b), "/iter%04d", step);
+    const std::string stem = dump_dir + b;
+    FILE *f = std::fopen((stem + ".meta").c_str(), "w");
+    if (!f) die("--dump: cannot write %s.meta", stem.c_str());
+    std::fprintf(f, "step %d\ntime %.17g\nscheme %d\nn_cells %lld\nn_dofs %lld\ntime_steps %.17g %.17g %.17g %.17g\n", step,
+                 time, last_scheme, (long long)m.nc, (long long)m.n_dofs(), last_ts[0], last_ts[1], last_ts[2], last_ts[3]);
+    std::fclose(f);
+    f = std::fopen((stem + ".bin").c_str(), "wb");
+    if (!f) die("--dump: cannot write %s.bin", stem.c_str());
+    for (const std::vector<double> *v : {&present, &m1, &m2, &m3}) std::fwrite(v->data(), sizeof(double), v->size(), f);
+    std::fclose(f);
+  }
+  int ilu_order = -1;  // --ilu-order cm|multicolor (-1: by size, kIluMulticolorDofs)
+  static constexpr int64_t kIluMulticolorDofs = 100000;
   ~Solver() {
     release();
     if (space) gls_fe_space_destroy(space);
@@ -832,6 +991,7 @@ struct Solver {
     if (ctx) gls_destroy(ctx);
     ilu_ctx = nullptr;
     ctx = nullptr;
+    loc.xchg.reset();  // the transport outlives its context
     if (rmesh) gls_octree_mesh_destroy(rmesh);
     rmesh = nullptr;
     if (d_cv) (void)hipFree(d_cv);
@@ -906,11 +1066,104 @@ struct Solver {
     return g;
   }
 
+  // --np: the rank's context on its cells of a general mesh (gls_gpart_*), Dirichlet rows mapped to
+  // local DoFs, attached to RCCL or the shared-memory transport; lines (global DoF ids) decide the
+  // ghosts (their masters) and are set by the caller through loc.g2l
+  gls_ctx *make_context_local(const Mesh &mm, const Constraints &cc, const std::vector<int64_t> &ld,
+                              const std::vector<int64_t> &lo, const std::vector<int64_t> &lm) {
+    const bool sep = mm.kp != mm.k;
+    const int dim = mm.dim, nvc = dim == 3 ? (mm.k + 1) * (mm.k + 1) * (mm.k + 1) : (mm.k + 1) * (mm.k + 1);
+    const int npc = dim == 3 ? (mm.kp + 1) * (mm.kp + 1) * (mm.kp + 1) : (mm.kp + 1) * (mm.kp + 1);
+    gls_gpart *gp = nullptr;
+    ck(gls_gpart_create(dim, mm.k, mm.kp, mm.nc, mm.cv.data(), sep ? mm.cp.data() : nullptr, mm.nv, mm.np,
+                        (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), rank, world, &gp),
+       "gls_gpart_create");
+    int64_t cb, ce, nvl, npl, nov, nop, ns, nr;
+    int nn;
+    ck(gls_gpart_sizes(gp, &cb, &ce, &nvl, &npl, &nov, &nop, &nn, &ns, &nr), "gls_gpart_sizes");
+    const int64_t ncl = ce - cb;
+    std::vector<int32_t> lcv((size_t)(ncl * nvc)), lcp(sep ? (size_t)(ncl * npc) : 0), sd((size_t)ns), rd((size_t)nr);
+    std::vector<int64_t> vl2g((size_t)nvl), pl2g((size_t)npl), soff((size_t)nn + 1, 0), roff((size_t)nn + 1, 0);
+    std::vector<int> nbrs((size_t)nn);
+    ck(gls_gpart_get(gp, lcv.data(), sep ? lcp.data() : nullptr, vl2g.data(), pl2g.data(), nbrs.data(), soff.data(),
+                     sd.data(), roff.data(), rd.data()),
+       "gls_gpart_get");
+    gls_gpart_destroy(gp);
+    const int64_t NVD = (int64_t)dim * mm.nv;
+    loc.l2g.clear();
+    loc.own_l.clear();
+    loc.own_g.clear();
+    for (int64_t i = 0; i < nvl; ++i)
+      for (int c = 0; c < dim; ++c) loc.l2g.push_back(vl2g[(size_t)i] * dim + c);
+    for (int64_t j = 0; j < npl; ++j) loc.l2g.push_back(NVD + pl2g[(size_t)j]);
+    for (int64_t i = 0; i < nov * dim; ++i) loc.own_l.push_back(i);
+    for (int64_t j = 0; j < nop; ++j) loc.own_l.push_back((int64_t)dim * nvl + j);
+    for (int64_t i : loc.own_l) loc.own_g.push_back(loc.l2g[(size_t)i]);
+    loc.g2l.assign((size_t)mm.n_dofs(), -1);
+    for (size_t i = 0; i < loc.l2g.size(); ++i) loc.g2l[(size_t)loc.l2g[i]] = (int64_t)i;
+    std::vector<uint8_t> lmask((size_t)nvl);
+    for (int64_t i = 0; i < nvl; ++i) lmask[(size_t)i] = cc.mask[(size_t)vl2g[(size_t)i]];
+    gls_mesh_desc D;
+    std::memset(&D, 0, sizeof(D));
+    D.dim = dim;
+    D.k = mm.k;
+    D.kp = mm.kp;
+    D.n_cells = (int)ncl;
+    D.n_vnodes = (int)nvl;
+    D.n_pnodes = (int)npl;
+    D.cell_vnodes = lcv.data();
+    D.cell_pnodes = sep ? lcp.data() : nullptr;
+    D.map_degree = mm.k;
+    D.cell_support = mm.support.data() + (size_t)(cb * nvc * dim);
+    D.vnode_mask = lmask.data();
+    D.viscosity = P.nu;
+    D.srf = P.srf ? 1 : 0;
+    for (int i = 0; i < 3; ++i) D.omega[i] = P.omega[i];
+    gls_ctx *g = nullptr;
+    ck(gls_create(&D, &g), "gls_create");
+    if (P.source) {  // forcing at the library's (mapped) quadrature points of the local cells
+      const int nq1 = mm.k + 1, nq = dim == 3 ? nq1 * nq1 * nq1 : nq1 * nq1;
+      std::vector<double> X((size_t)(ncl * nq * dim)), F, fq(X.size());
+      ck(gls_quadrature_points(g, X.data()), "gls_quadrature_points");
+      P.force.eval(X, dim, time, F);
+      for (size_t i = 0; i < fq.size() / dim; ++i)
+        for (int d = 0; d < dim; ++d) fq[i * dim + d] = F[i * (size_t)P.force.nc + d];
+      ck(gls_set_force(g, fq.data()), "gls_set_force");
+    }
+    std::vector<int64_t> dd;
+    std::vector<double> dv;
+    for (size_t i = 0; i < cc.dofs.size(); ++i) {
+      const int64_t l = loc.g2l[(size_t)cc.dofs[i]];
+      if (l >= 0) {
+        dd.push_back(l);
+        dv.push_back(cc.vals[i]);
+      }
+    }
+    ck(gls_set_dirichlet(g, (int64_t)dd.size(), dd.data(), dv.data()), "gls_set_dirichlet");
+    if (rccl) {
+      ck(gls_dist_attach_dofs_rccl(g, rccl, nov, nop, nn, nbrs.data(), soff.data(), sd.data(), roff.data(), rd.data()),
+         "gls_dist_attach_dofs_rccl");
+    } else {
+      loc.xchg.reset(new ShmExchange);
+      ShmExchange &x = *loc.xchg;
+      x.nbrs = nbrs;
+      x.soff = soff;
+      x.roff = roff;
+      hk(hipMalloc(&x.send, sizeof(double) * (size_t)std::max<int64_t>(ns, 1)), "hipMalloc");
+      hk(hipMalloc(&x.recv, sizeof(double) * (size_t)std::max<int64_t>(nr, 1)), "hipMalloc");
+      hk(hipMalloc(&x.red, sizeof(double) * 256), "hipMalloc");
+      ck(gls_dist_attach_dofs(g, nov, nop, nn, soff.data(), sd.data(), roff.data(), rd.data(), x.send, x.recv, x.red,
+                              ShmExchange::exchange, ShmExchange::allreduce, &x),
+         "gls_dist_attach_dofs");
+    }
+    return g;
+  }
+
   void alloc_vectors() {
-    const int64_t N = m.n_dofs();
+    const int64_t N = m.n_dofs(), nd = ndev();
     for (double **q : {&d_present, &d_m1, &d_m2, &d_m3}) {
-      hk(hipMalloc(q, sizeof(double) * (size_t)N), "hipMalloc");
-      hk(hipMemset(*q, 0, sizeof(double) * (size_t)N), "hipMemset");
+      hk(hipMalloc(q, sizeof(double) * (size_t)nd), "hipMalloc");
+      hk(hipMemset(*q, 0, sizeof(double) * (size_t)nd), "hipMemset");
     }
     present.assign((size_t)N, 0.);
     m1 = m2 = m3 = present;
@@ -938,7 +1191,7 @@ struct Solver {
   void dev_changed() { host_ok = false; dev_ok = true; }
   void dcopy(double *dst, const double *src) {  // ordered against the context's own stream: synchronous
     hk(hipDeviceSynchronize(), "device copy");
-    hk(hipMemcpy(dst, src, sizeof(double) * (size_t)m.n_dofs(), hipMemcpyDeviceToDevice), "device copy");
+    hk(hipMemcpy(dst, src, sizeof(double) * (size_t)ndev(), hipMemcpyDeviceToDevice), "device copy");
     hk(hipDeviceSynchronize(), "device copy");
   }
 
@@ -1105,7 +1358,6 @@ struct Solver {
       }
     m = std::move(r);
     C = make_constraints(P, m, time);
-    ctx = make_context(m, C);
     // hanging lines + slip lines of curved walls (homogeneous constraint lines on velocity DoFs)
     std::vector<int64_t> ld = m.hang_dofs, lo = m.hang_off, lm = m.hang_master;
     std::vector<double> lw = m.hang_w;
@@ -1117,8 +1369,29 @@ struct Solver {
       }
       lo.push_back((int64_t)lm.size());
     }
-    if (!ld.empty())
-      ck(gls_set_hanging(ctx, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging");
+    if (world > 1) {  // the rank's cells; its lines in local DoF ids (masters are local by construction)
+      ctx = make_context_local(m, C, ld, lo, lm);
+      std::vector<int64_t> ld2, lo2{0}, lm2;
+      std::vector<double> lw2;
+      for (size_t i = 0; i < ld.size(); ++i) {
+        const int64_t l = loc.g2l[(size_t)ld[i]];
+        if (l < 0) continue;
+        ld2.push_back(l);
+        for (int64_t j = lo[i]; j < lo[i + 1]; ++j) {
+          const int64_t mj = loc.g2l[(size_t)lm[(size_t)j]];
+          if (mj < 0) die("rank %d: a line master is not local", rank);
+          lm2.push_back(mj);
+          lw2.push_back(lw[(size_t)j]);
+        }
+        lo2.push_back((int64_t)lm2.size());
+      }
+      if (!ld2.empty())
+        ck(gls_set_hanging(ctx, (int64_t)ld2.size(), ld2.data(), lo2.data(), lm2.data(), lw2.data()), "gls_set_hanging");
+    } else {
+      ctx = make_context(m, C);
+      if (!ld.empty())
+        ck(gls_set_hanging(ctx, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging");
+    }
     alloc_vectors();
     print_setup(F.volume);
   }
@@ -1129,10 +1402,24 @@ struct Solver {
     std::printf("   Volume of triangulation:      %g\n", volume);
   }
 
-  void upload(const std::vector<double> &h, double *d) {
+  void upload(const std::vector<double> &h, double *d) {  // global host vector -> (rank-local) device vector
+    if (world > 1) {
+      loc.tmp.resize(loc.l2g.size());
+      for (size_t i = 0; i < loc.l2g.size(); ++i) loc.tmp[i] = h[(size_t)loc.l2g[i]];
+      hk(hipMemcpy(d, loc.tmp.data(), sizeof(double) * loc.tmp.size(), hipMemcpyHostToDevice), "upload");
+      return;
+    }
     hk(hipMemcpy(d, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice), "upload");
   }
-  void download(const double *d, std::vector<double> &h) {
+  void download(const double *d, std::vector<double> &h) {  // --np: every rank's owned values, gathered
+    if (world > 1) {
+      loc.tmp.resize(loc.l2g.size());
+      hk(hipMemcpy(loc.tmp.data(), d, sizeof(double) * loc.tmp.size(), hipMemcpyDeviceToHost), "download");
+      std::vector<double> own(loc.own_l.size());
+      for (size_t i = 0; i < own.size(); ++i) own[i] = loc.tmp[(size_t)loc.own_l[i]];
+      g_comm.allgather(own.data(), loc.own_g, h);
+      return;
+    }
     hk(hipMemcpy(h.data(), d, sizeof(double) * h.size(), hipMemcpyDeviceToHost), "download");
   }
 
@@ -1245,6 +1532,8 @@ struct Solver {
     double ts[4];
     for (int i = 0; i < 4; ++i) ts[i] = dts[i] > 0 ? dts[i] : 1.0;
     ck(gls_set_time(ctx, scheme, ts), "gls_set_time");
+    last_scheme = scheme;
+    for (int i = 0; i < 4; ++i) last_ts[i] = ts[i];
     if (nu_override > 0) ck(gls_set_viscosity(ctx, nu_override), "gls_set_viscosity");
     need_dev();
     ck(gls_apply_dirichlet(ctx, d_present), "gls_apply_dirichlet");
@@ -1258,6 +1547,12 @@ struct Solver {
     // TrilinosWrappers::SolverGMRES default) and iteration cap, unless --precond jacobi. Jacobi is much
     // weaker than the reference's preconditioners, so its caps and restart are raised.
     if (mg_levels.empty() && use_ilu && ilu_ctx != ctx) {
+      // ordering: Cuthill-McKee as the reference factors; above kIluMulticolorDofs the multicolor
+      // order, whose triangular solves are ~60x faster on the GPU (profiles/r03_ilu_multicolor_ab.txt)
+      // at the price of more GMRES iterations (--ilu-order overrides)
+      const int order = ilu_order >= 0 ? ilu_order
+                        : (m.n_dofs() > kIluMulticolorDofs ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM);
+      ck(gls_ilu_set_options(ctx, order, ilu_block_dofs), "gls_ilu_set_options");
       ck(gls_ilu_attach(ctx, P.ilu_fill, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;
     }
@@ -1445,6 +1740,7 @@ struct Solver {
   void write_output() {
     SectionTimer::Scope ts(timer, "output");
     need_host();
+    if (rank != 0) return;  // --np: rank 0 writes the (gathered) solution
     char tag[32];
     std::snprintf(tag, sizeof(tag), ".%05d", step);
     const std::string stem = P.output_name + tag, piece = stem + ".00000.vtu", master = stem + ".pvtu";
@@ -1702,16 +1998,25 @@ struct Solver {
     std::vector<double> xi((size_t)(np * nqf * 2 * dim)), g(xi.size()), jxw((size_t)(np * nqf)), diam((size_t)nc);
     ck(gls_fe_space_kelly_faces(space, nq, &np, ca.data(), cb.data(), xi.data(), g.data(), jxw.data(), diam.data()),
        "gls_fe_space_kelly_faces");
-    upload(present, d_present);
-    double *d_eta = nullptr;
-    hk(hipMalloc(&d_eta, sizeof(double) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
-    ck(gls_kelly_estimate_mapped(ctx, d_present, P.kelly_variable, np, nqf, ca.data(), cb.data(), xi.data(), g.data(),
-                                 jxw.data(), diam.data(), d_eta),
-       "gls_kelly_estimate_mapped");
-    hk(hipDeviceSynchronize(), "kelly estimate");
     std::vector<double> eta((size_t)nc);
-    download(d_eta, eta);
-    (void)hipFree(d_eta);
+    if (world == 1 || rank == 0) {  // --np: rank 0 on a context of the whole mesh, eta broadcast
+      gls_ctx *kc = world > 1 ? make_context(m, C) : ctx;
+      double *d_eta = nullptr, *d_sol = d_present;
+      hk(hipMalloc(&d_eta, sizeof(double) * (size_t)std::max<int64_t>(nc, 1)), "hipMalloc");
+      if (world > 1) hk(hipMalloc(&d_sol, sizeof(double) * present.size()), "hipMalloc");
+      hk(hipMemcpy(d_sol, present.data(), sizeof(double) * present.size(), hipMemcpyHostToDevice), "upload");
+      ck(gls_kelly_estimate_mapped(kc, d_sol, P.kelly_variable, np, nqf, ca.data(), cb.data(), xi.data(), g.data(),
+                                   jxw.data(), diam.data(), d_eta),
+         "gls_kelly_estimate_mapped");
+      hk(hipDeviceSynchronize(), "kelly estimate");
+      hk(hipMemcpy(eta.data(), d_eta, sizeof(double) * eta.size(), hipMemcpyDeviceToHost), "download");
+      (void)hipFree(d_eta);
+      if (world > 1) {
+        (void)hipFree(d_sol);
+        gls_destroy(kc);
+      }
+    }
+    if (world > 1) g_comm.bcast(eta, 0);
     std::vector<float> crit((size_t)nc);
     int max_lev = 0;
     for (int64_t i = 0; i < nc; ++i) {
@@ -1819,7 +2124,8 @@ struct Solver {
   void run() {
     dt_now = P.dt;
     dts[0] = P.dt;
-    std::printf("Running on 1 MPI rank(s)...\n");  // navier_stokes_base.cc:115-117 (one rank per GPU)
+    std::printf("Running on %d MPI rank(s)...\n", world);  // navier_stokes_base.cc:115-117 (one rank per GPU)
+    if (world > 1 && !P.general) P.general = true;  // --np: every mesh through the general (partitioned) path
     if (P.general) {
       create_umesh();
       setup_general();
@@ -1867,6 +2173,7 @@ struct Solver {
         advance();
       }
       postprocess(false);
+      dump_state();
       end_of_step();
       if (P.timer == "iteration") {  // TimerOutput print_summary + reset per iteration (navier_stokes_base.cc:449-455)
         timer.print();
@@ -1885,9 +2192,15 @@ int main(int argc, char **argv) {
   // gls_navier_stokes_2d / gls_navier_stokes_3d <file.prm> (applications/gls_navier_stokes_{2d,3d},
   // gls_navier_stokes_3d.cc:22-46): the dimension comes from the program name; the generic
   // binary takes --dim. Extra options: --precond mg|jacobi, --precision N (error table digits),
-  // --stats (solver iteration totals).
+  // --stats (solver iteration totals), --ilu-block-dofs N (block-Jacobi ILU subdomains of N DoFs,
+  // 0 = one block), --ilu-order cm|multicolor (gls_ilu_set_options), --dump DIR (every iteration's
+  // final state for the pipeline tests).
   int dim = 0;
   bool mg = true, stats = false;
+  int64_t ilu_block = -1;
+  int ilu_order = -1;
+  const char *dump = nullptr;
+  int np_ranks = 1;
   int precision = 4;
   const char *file = nullptr;
   const std::string prog = argv[0];
@@ -1898,6 +2211,15 @@ int main(int argc, char **argv) {
     else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) mg = std::strcmp(argv[++i], "jacobi") != 0;
     else if (!std::strcmp(argv[i], "--precision") && i + 1 < argc) precision = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--stats")) stats = true;
+    else if (!std::strcmp(argv[i], "--ilu-block-dofs") && i + 1 < argc) ilu_block = std::atoll(argv[++i]);
+    else if (!std::strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
+    else if (!std::strcmp(argv[i], "--np") && i + 1 < argc) np_ranks = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--ilu-order") && i + 1 < argc) {
+      const char *o = argv[++i];
+      if (!std::strcmp(o, "cm")) ilu_order = GLS_ILU_ORDER_CM;
+      else if (!std::strcmp(o, "multicolor")) ilu_order = GLS_ILU_ORDER_MULTICOLOR;
+      else die("--ilu-order %s: cm or multicolor", o);
+    }
     else if (argv[i][0] != '-') file = argv[i];
     else die("unknown option %s", argv[i]);
   }
@@ -1909,9 +2231,61 @@ int main(int argc, char **argv) {
   if (dim != 2 && dim != 3) die("--dim must be 2 or 3");
   Prm prm(file);
   Params P = read_params(prm, dim);
+  // --np N: N ranks forked here, before any GPU call (the children's stdout is discarded: rank 0
+  // prints, as the reference's pcout does)
+  if (np_ranks < 1 || np_ranks > kMaxRanks) die("--np must be in 1..%d", kMaxRanks);
+  int rank = 0;
+  std::vector<pid_t> kids;
+  if (np_ranks > 1) {
+    g_comm.create(np_ranks);
+    std::fflush(stdout);
+    std::fflush(stderr);
+    for (int r = 1; r < np_ranks; ++r) {
+      const pid_t pid = fork();
+      if (pid < 0) die("--np: fork failed");
+      if (pid == 0) {
+        rank = r;
+        kids.clear();
+        if (!std::freopen("/dev/null", "w", stdout)) die("--np: /dev/null");
+        break;
+      }
+      kids.push_back(pid);
+    }
+    g_comm.rank = rank;
+  }
   Solver s(P, mg);
+  s.rank = rank;
+  s.world = np_ranks;
+  if (np_ranks > 1) {
+    int ndev = 0;
+    hk(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    hk(hipSetDevice(rank % std::max(ndev, 1)), "hipSetDevice");
+    if (ndev >= np_ranks && !std::getenv("GLS_NP_SHM")) {  // one GPU per rank: RCCL over xGMI
+      if (rank == 0) ck(gls_rccl_unique_id(g_comm.hdr->rccl_id), "gls_rccl_unique_id");
+      g_comm.barrier();
+      ck(gls_rccl_create(g_comm.hdr->rccl_id, rank, np_ranks, &s.rccl), "gls_rccl_create");
+    }
+  }
   s.precision = precision;
   s.stats = stats;
+  if (ilu_block >= 0) s.ilu_block_dofs = ilu_block;
+  s.ilu_order = ilu_order;
+  if (dump) s.dump_dir = dump;
   s.run();
+  if (np_ranks > 1) {
+    g_comm.barrier();
+    s.release();
+    if (s.rccl) gls_rccl_destroy(s.rccl);
+    if (rank != 0) {
+      std::fflush(stderr);
+      _exit(0);
+    }
+    int bad = 0;
+    for (pid_t pid : kids) {
+      int st = 0;
+      if (waitpid(pid, &st, 0) < 0 || !WIFEXITED(st) || WEXITSTATUS(st) != 0) ++bad;
+    }
+    if (bad) die("--np: %d rank(s) failed", bad);
+  }
   return 0;
 }

@@ -221,6 +221,18 @@ int gls_mg_detach(gls_ctx *ctx);
 #define GLS_ILU_MAX_FILL 10
 int gls_ilu_attach(gls_ctx *ctx, int fill, double athresh, double rthresh);
 int gls_ilu_detach(gls_ctx *ctx);
+/* Options of the next gls_ilu_attach.
+ * ordering: GLS_ILU_ORDER_CM (default) = DoFRenumbering::Cuthill_McKee as the reference factors;
+ *   GLS_ILU_ORDER_MULTICOLOR = DoFs grouped by a distance-1 coloring of the matrix's node graph
+ *   (Cuthill-McKee inside a color): a different ILU (weaker, more GMRES iterations) whose triangular
+ *   solves have a dependency chain of ~colors x DoFs per node instead of ~the matrix bandwidth.
+ * block_dofs: block-Jacobi subdomains: the cells (in their space-filling order) are cut into
+ *   ceil(n_dofs / block_dofs) contiguous ranges, couplings between the ranges are dropped and every
+ *   block is factored on its own -- Ifpack's additive Schwarz with overlap 0, which is what the
+ *   reference's setup_ILU gives with one block per MPI rank. 0 (default): one block. */
+#define GLS_ILU_ORDER_CM 0
+#define GLS_ILU_ORDER_MULTICOLOR 1
+int gls_ilu_set_options(gls_ctx *ctx, int ordering, int64_t block_dofs);
 int gls_ilu_info(const gls_ctx *ctx, int64_t *nnz, int *n_probes);
 int gls_ilu_matrix(gls_ctx *ctx, int32_t *rowp, int32_t *col, double *val); /* probed CSR (tests) */
 /* factored values in the factorization numbering (perm[dof] = row), for tests */
@@ -328,6 +340,36 @@ int gls_rccl_destroy(gls_rccl *comm);
 int gls_dist_attach_rccl(gls_ctx *ctx, gls_rccl *comm, int64_t n_owned_nodes, int n_nbrs, const int *nbr_ranks,
                          const int64_t *send_offsets, const int32_t *send_nodes, const int64_t *recv_offsets,
                          const int32_t *recv_nodes);
+
+/* General meshes across ranks (adaptive / unstructured forests; the p::d triangulation partition,
+ * navier_stokes_base.cc:55-60, 682-733, ghosted vectors gls_navier_stokes.cc:186-202): any dim,
+ * Qk-Qk' with separate pressure nodes, hanging-node / slip lines (DoF level, global numbering:
+ * velocity node*dim + c, pressure dim*n_vnodes + node). Every rank holds the same global mesh
+ * (replicated host data) and calls gls_gpart_create with its rank: contiguous equal-count ranges of
+ * the given cell order per rank, node ownership by the lowest touching rank, rank-local nodes
+ * owned first then ghosts (ascending (owner, id)); ghosts include the masters of the lines on local
+ * cells. The rank's context is created on the local cells (gls_gpart_get) and attached with
+ * gls_dist_attach_dofs (callbacks, one double per exchanged DoF) or gls_dist_attach_dofs_rccl;
+ * gls_gpart_map_dofs maps global DoF ids (Dirichlet rows, line DoFs and masters) to local ones
+ * (-1 where not local). Hanging lines (gls_set_hanging) are then given in local ids. */
+typedef struct gls_gpart gls_gpart;
+int gls_gpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cell_vnodes, const int32_t *cell_pnodes,
+                     int64_t n_vnodes, int64_t n_pnodes, int64_t n_lines, const int64_t *line_dofs,
+                     const int64_t *line_offsets, const int64_t *line_masters, int rank, int world, gls_gpart **out);
+int gls_gpart_sizes(const gls_gpart *p, int64_t *cell_begin, int64_t *cell_end, int64_t *n_vnodes, int64_t *n_pnodes,
+                    int64_t *n_owned_vnodes, int64_t *n_owned_pnodes, int *n_nbrs, int64_t *n_send, int64_t *n_recv);
+int gls_gpart_get(const gls_gpart *p, int32_t *local_cell_vnodes, int32_t *local_cell_pnodes, int64_t *vnode_l2g,
+                  int64_t *pnode_l2g, int *nbr_ranks, int64_t *send_offsets, int32_t *send_dofs, int64_t *recv_offsets,
+                  int32_t *recv_dofs);
+int gls_gpart_map_dofs(const gls_gpart *p, int64_t n, const int64_t *global_dofs, int64_t *local_dofs);
+int gls_gpart_destroy(gls_gpart *p);
+int gls_dist_attach_dofs(gls_ctx *ctx, int64_t n_owned_vnodes, int64_t n_owned_pnodes, int n_nbrs,
+                         const int64_t *send_offsets, const int32_t *send_dofs, const int64_t *recv_offsets,
+                         const int32_t *recv_dofs, double *send_buf, double *recv_buf, double *red_buf,
+                         gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user);
+int gls_dist_attach_dofs_rccl(gls_ctx *ctx, gls_rccl *comm, int64_t n_owned_vnodes, int64_t n_owned_pnodes,
+                              int n_nbrs, const int *nbr_ranks, const int64_t *send_offsets, const int32_t *send_dofs,
+                              const int64_t *recv_offsets, const int32_t *recv_dofs);
 
 /* ------------------------------------------------------------------------------------------
  * Host-side building blocks (host pointers).

@@ -1065,3 +1065,270 @@ double gls_oracle_time_local_systems(const gls_oracle_problem *p,
   }
   return checksum;
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * One complete CPU Newton iteration on the assembled system (bench.py's cpu_baseline; baseline /
+ * test infrastructure, never the product): NewtonNonLinearSolver::solve's loop body
+ * (newton_non_linear_solver.h:90-137) with
+ *   assemble_matrix_and_rhs into CSR (gls_navier_stokes.cc:916-1022; zero_constraints elimination,
+ *     deal.II's |K_e(i,i)| on constrained rows), cells in parallel on `nthreads` (atomic adds);
+ *   setup_ILU = Ifpack ILU(0) (:1161-1176; diagonal rthresh * a + sign(a) * athresh), serial as
+ *     Ifpack's factorisation of a rank's rows is;
+ *   solve_system_GMRES (:1242-1289): GMRES(restart) right-preconditioned from x0 = 0 to
+ *     max(rel * ||rhs||, minres), modified Gram-Schmidt, serial ILU triangular solves, threaded
+ *     SpMV and vector operations;
+ *   the alpha line search with assemble_rhs (alpha = 1, 1/2, ... while not 0.9 * ||r0||).
+ * Dirichlet constraints only (no hanging lines). x is updated in place.
+ * ------------------------------------------------------------------------------------------------ */
+static int csr_find(const int *col, int b, int e, int j) {
+  while (b < e) {
+    const int m = (b + e) >> 1;
+    if (col[m] < j) b = m + 1;
+    else e = m;
+  }
+  return b;
+}
+static void csr_spmv(int n, const int *rp, const int *ci, const double *v, const double *x, double *y) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    double s = 0.;
+    for (int e = rp[i]; e < rp[i + 1]; ++e) s += v[e] * x[ci[e]];
+    y[i] = s;
+  }
+}
+static double vdot(int n, const double *a, const double *b) {
+  double s = 0.;
+#pragma omp parallel for reduction(+ : s) schedule(static)
+  for (int i = 0; i < n; ++i) s += a[i] * b[i];
+  return s;
+}
+static void ilu_solve(int n, const int *rp, const int *ci, const double *lu, const int *dg, const double *b, double *x) {
+  for (int i = 0; i < n; ++i) {  /* L y = b (unit lower) */
+    double s = b[i];
+    for (int e = rp[i]; e < dg[i]; ++e) s -= lu[e] * x[ci[e]];
+    x[i] = s;
+  }
+  for (int i = n - 1; i >= 0; --i) {  /* U x = y */
+    double s = x[i];
+    for (int e = dg[i] + 1; e < rp[i + 1]; ++e) s -= lu[e] * x[ci[e]];
+    x[i] = s / lu[dg[i]];
+  }
+}
+static void assemble_csr(const gls_oracle_problem *p, const double *u, const double *u1, const double *u2,
+                         const double *u3, const int *rp, const int *ci, const int *dg, double *val, double *rhs,
+                         int with_matrix) {
+  const int N = gls_oracle_n_dofs(p);
+  if (with_matrix) memset(val, 0, sizeof(double) * (size_t)rp[N]);
+  memset(rhs, 0, sizeof(double) * (size_t)N);
+#pragma omp parallel
+  {
+    cell_tab t;
+    tab_alloc(&t, p);
+    const int nd = t.nd;
+    int *dofs = malloc(sizeof(int) * nd);
+    double *Fe = malloc(sizeof(double) * nd);
+    double *Ke = with_matrix ? malloc(sizeof(double) * nd * nd) : NULL;
+#pragma omp for schedule(dynamic, 64)
+    for (int c = 0; c < p->n_cells; ++c) {
+      local_system(p, &t, c, u, u1, u2, u3, Ke, Fe, dofs);
+      for (int i = 0; i < nd; ++i) {
+        const int gi = dofs[i];
+        if (p->constrained[gi]) {
+          if (with_matrix) {
+            const double d = constrained_diag(Ke, nd, i);
+#pragma omp atomic
+            val[dg[gi]] += d;
+          }
+          continue;
+        }
+#pragma omp atomic
+        rhs[gi] += Fe[i];
+        if (!with_matrix) continue;
+        for (int j = 0; j < nd; ++j) {
+          const int gj = dofs[j];
+          if (p->constrained[gj]) continue;
+          const int e = csr_find(ci, rp[gi], rp[gi + 1], gj);
+#pragma omp atomic
+          val[e] += Ke[(size_t)i * nd + j];
+        }
+      }
+    }
+    free(Ke); free(Fe); free(dofs); tab_free(&t);
+  }
+}
+
+int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *u1, const double *u2,
+                          const double *u3, int nthreads, int restart, double rel, double minres, int max_its,
+                          double athresh, double rthresh, gls_oracle_newton_stats *st) {
+  if (p->hang_off) return -1;
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+  memset(st, 0, sizeof(*st));
+  const int N = gls_oracle_n_dofs(p), nd = gls_oracle_dofs_per_cell(p);
+  double t0 = omp_get_wtime();
+  /* sparsity (setup_dofs' make_sparsity_pattern with the constraints, keep_constrained = false) */
+  int *dcnt = calloc((size_t)N + 1, sizeof(int)), *dofs = malloc(sizeof(int) * nd);
+  for (int c = 0; c < p->n_cells; ++c) {
+    gls_oracle_cell_dofs(p, c, dofs);
+    for (int i = 0; i < nd; ++i) ++dcnt[dofs[i] + 1];
+  }
+  for (int i = 0; i < N; ++i) dcnt[i + 1] += dcnt[i];
+  int *dcell = malloc(sizeof(int) * (size_t)dcnt[N]), *fillp = malloc(sizeof(int) * (size_t)N);
+  memcpy(fillp, dcnt, sizeof(int) * (size_t)N);
+  for (int c = 0; c < p->n_cells; ++c) {
+    gls_oracle_cell_dofs(p, c, dofs);
+    for (int i = 0; i < nd; ++i) dcell[fillp[dofs[i]]++] = c;
+  }
+  int *rp = malloc(sizeof(int) * ((size_t)N + 1)), *mark = malloc(sizeof(int) * (size_t)N);
+  for (int i = 0; i < N; ++i) mark[i] = -1;
+  long long nnz = 0;
+  int *ci = NULL;
+  for (int pass = 0; pass < 2; ++pass) {  /* count, then fill */
+    nnz = 0;
+    rp[0] = 0;
+    for (int r = 0; r < N; ++r) {
+      const long long b = nnz;
+      if (pass) ci[nnz] = r;
+      ++nnz;
+      mark[r] = r;
+      if (!p->constrained[r])
+        for (int t = dcnt[r]; t < dcnt[r + 1]; ++t) {
+          gls_oracle_cell_dofs(p, dcell[t], dofs);
+          for (int i = 0; i < nd; ++i) {
+            const int j = dofs[i];
+            if (p->constrained[j] || mark[j] == r) continue;
+            mark[j] = r;
+            if (pass) ci[nnz] = j;
+            ++nnz;
+          }
+        }
+      if (pass) { /* sort the row (insertion: short rows) */
+        for (long long a = b + 1; a < nnz; ++a) {
+          const int v = ci[a];
+          long long q = a - 1;
+          while (q >= b && ci[q] > v) { ci[q + 1] = ci[q]; --q; }
+          ci[q + 1] = v;
+        }
+      }
+      rp[r + 1] = (int)nnz;
+    }
+    for (int i = 0; i < N; ++i) mark[i] = -1;
+    if (!pass) ci = malloc(sizeof(int) * (size_t)nnz);
+  }
+  int *dg = malloc(sizeof(int) * (size_t)N);
+  for (int r = 0; r < N; ++r) dg[r] = csr_find(ci, rp[r], rp[r + 1], r);
+  st->nnz = nnz;
+  st->t_pattern = omp_get_wtime() - t0;
+  double *val = malloc(sizeof(double) * (size_t)nnz), *lu = malloc(sizeof(double) * (size_t)nnz);
+  double *rhs = malloc(sizeof(double) * (size_t)N), *dx = calloc((size_t)N, sizeof(double));
+  const int m = restart > 0 ? restart : 30;
+  double *V = malloc(sizeof(double) * (size_t)N * (size_t)(m + 1)), *Z = malloc(sizeof(double) * (size_t)N * (size_t)m);
+  double *w = malloc(sizeof(double) * (size_t)N), *H = calloc((size_t)(m + 1) * m, sizeof(double));
+  double *g = malloc(sizeof(double) * (size_t)(m + 1)), *cs = malloc(sizeof(double) * (size_t)m), *sn = malloc(sizeof(double) * (size_t)m);
+  double *yv = malloc(sizeof(double) * (size_t)m), *xt = malloc(sizeof(double) * (size_t)N);
+  /* assemble_matrix_and_rhs */
+  t0 = omp_get_wtime();
+  assemble_csr(p, x, u1, u2, u3, rp, ci, dg, val, rhs, 1);
+  st->t_assemble = omp_get_wtime() - t0;
+  const double res0 = sqrt(vdot(N, rhs, rhs));
+  st->res0 = res0;
+  /* setup_ILU: ILU(0) */
+  t0 = omp_get_wtime();
+  memcpy(lu, val, sizeof(double) * (size_t)nnz);
+  for (int r = 0; r < N; ++r) {
+    const double a = lu[dg[r]];
+    lu[dg[r]] = rthresh * a + (a < 0 ? -athresh : athresh);
+  }
+  for (int i = 0; i < N; ++i) {
+    for (int e = rp[i]; e < rp[i + 1]; ++e) mark[ci[e]] = e;
+    for (int e = rp[i]; e < dg[i]; ++e) {
+      const int k = ci[e];
+      const double lik = lu[e] / lu[dg[k]];
+      lu[e] = lik;
+      for (int f = dg[k] + 1; f < rp[k + 1]; ++f) {
+        const int q = mark[ci[f]];
+        if (q >= 0) lu[q] -= lik * lu[f];
+      }
+    }
+    for (int e = rp[i]; e < rp[i + 1]; ++e) mark[ci[e]] = -1;
+  }
+  st->t_ilu = omp_get_wtime() - t0;
+  /* solve_system_GMRES: right-preconditioned GMRES(m), x0 = 0 */
+  t0 = omp_get_wtime();
+  const double tol = fmax(rel * res0, minres);
+  double beta = res0;
+  int its = 0;
+  memset(dx, 0, sizeof(double) * (size_t)N);
+  memcpy(w, rhs, sizeof(double) * (size_t)N);
+  while (beta > tol && its < max_its) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < N; ++i) V[i] = w[i] / beta;
+    for (int i = 0; i <= m; ++i) g[i] = 0.;
+    g[0] = beta;
+    int j = 0;
+    for (; j < m && its < max_its; ++j) {
+      double *zj = Z + (size_t)j * N, *vj = V + (size_t)j * N, *vn = V + (size_t)(j + 1) * N;
+      ilu_solve(N, rp, ci, lu, dg, vj, zj);
+      csr_spmv(N, rp, ci, val, zj, vn);
+      for (int i = 0; i <= j; ++i) {  /* modified Gram-Schmidt */
+        const double *vi = V + (size_t)i * N;
+        const double h = vdot(N, vn, vi);
+        H[(size_t)i * m + j] = h;
+#pragma omp parallel for schedule(static)
+        for (int q = 0; q < N; ++q) vn[q] -= h * vi[q];
+      }
+      const double hn = sqrt(vdot(N, vn, vn));
+      H[(size_t)(j + 1) * m + j] = hn;
+      if (hn > 0) {
+#pragma omp parallel for schedule(static)
+        for (int q = 0; q < N; ++q) vn[q] /= hn;
+      }
+      for (int i = 0; i < j; ++i) {
+        const double a = H[(size_t)i * m + j], b = H[(size_t)(i + 1) * m + j];
+        H[(size_t)i * m + j] = cs[i] * a + sn[i] * b;
+        H[(size_t)(i + 1) * m + j] = -sn[i] * a + cs[i] * b;
+      }
+      const double a = H[(size_t)j * m + j], b = H[(size_t)(j + 1) * m + j], rr = hypot(a, b);
+      cs[j] = rr > 0 ? a / rr : 1.;
+      sn[j] = rr > 0 ? b / rr : 0.;
+      H[(size_t)j * m + j] = rr;
+      H[(size_t)(j + 1) * m + j] = 0.;
+      g[j + 1] = -sn[j] * g[j];
+      g[j] *= cs[j];
+      ++its;
+      if (fabs(g[j + 1]) <= tol) { ++j; break; }
+    }
+    for (int i = j - 1; i >= 0; --i) {
+      double s = g[i];
+      for (int l = i + 1; l < j; ++l) s -= H[(size_t)i * m + l] * yv[l];
+      yv[i] = H[(size_t)i * m + i] != 0. ? s / H[(size_t)i * m + i] : 0.;
+    }
+    for (int i = 0; i < j; ++i) {
+      const double *zi = Z + (size_t)i * N;
+#pragma omp parallel for schedule(static)
+      for (int q = 0; q < N; ++q) dx[q] += yv[i] * zi[q];
+    }
+    csr_spmv(N, rp, ci, val, dx, w);  /* true residual at the restart */
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < N; ++q) w[q] = rhs[q] - w[q];
+    beta = sqrt(vdot(N, w, w));
+  }
+  st->gmres_its = its;
+  st->t_gmres = omp_get_wtime() - t0;
+  /* line search with assemble_rhs (zero_constraints: the update vanishes on constrained rows) */
+  t0 = omp_get_wtime();
+  double res = res0;
+  for (double alpha = 1.0; alpha > 1e-3; alpha *= 0.5) {
+#pragma omp parallel for schedule(static)
+    for (int q = 0; q < N; ++q) xt[q] = x[q] + (p->constrained[q] ? 0. : alpha * dx[q]);
+    assemble_csr(p, xt, u1, u2, u3, rp, ci, dg, NULL, rhs, 0);
+    ++st->line_search_rhs;
+    res = sqrt(vdot(N, rhs, rhs));
+    if (res < 0.9 * res0) break;
+  }
+  memcpy(x, xt, sizeof(double) * (size_t)N);
+  st->res1 = res;
+  st->t_linesearch = omp_get_wtime() - t0;
+  free(dcnt); free(dofs); free(dcell); free(fillp); free(rp); free(mark); free(ci); free(dg); free(val); free(lu);
+  free(rhs); free(dx); free(V); free(Z); free(w); free(H); free(g); free(cs); free(sn); free(yv); free(xt);
+  return 0;
+}

@@ -122,6 +122,17 @@ int gls_oracle_sdirk_coefficients(int order, double dt, double *out);
 /* CPU baseline: compute local systems of cells [c0, c0+count) with nthreads OpenMP threads;
  * returns a checksum so the work cannot be elided. */
 void gls_oracle_set_fast_tables(int on); /* timing path: reference-cell tables (bit-identical) */
+/* one complete CPU Newton iteration on the assembled CSR system (bench.py's cpu_baseline): see
+ * gls_oracle.c; times in seconds on omp_get_wtime */
+typedef struct {
+  double t_pattern, t_assemble, t_ilu, t_gmres, t_linesearch;
+  int gmres_its, line_search_rhs;
+  double res0, res1;
+  long long nnz;
+} gls_oracle_newton_stats;
+int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *u1, const double *u2,
+                          const double *u3, int nthreads, int restart, double rel, double minres, int max_its,
+                          double athresh, double rthresh, gls_oracle_newton_stats *st);
 double gls_oracle_time_local_systems(const gls_oracle_problem *p,
                                      const double *u, const double *u1, const double *u2, const double *u3,
                                      int c0, int count, int with_matrix, int nthreads);

@@ -36,6 +36,12 @@ SCHEMES = {
 }
 
 
+class _NewtonStats(C.Structure):
+    _fields_ = [("t_pattern", C.c_double), ("t_assemble", C.c_double), ("t_ilu", C.c_double), ("t_gmres", C.c_double),
+                ("t_linesearch", C.c_double), ("gmres_its", C.c_int), ("line_search_rhs", C.c_int),
+                ("res0", C.c_double), ("res1", C.c_double), ("nnz", C.c_longlong)]
+
+
 class _Problem(C.Structure):
     _fields_ = [
         ("dim", C.c_int), ("k", C.c_int), ("kp", C.c_int), ("nq1d", C.c_int), ("n_cells", C.c_int),
@@ -84,6 +90,8 @@ def lib():
         _lib.gls_oracle_time_local_systems.restype = C.c_double
         _lib.gls_oracle_coo_size.argtypes = [P]
         _lib.gls_oracle_coo_size.restype = C.c_longlong
+        _lib.gls_oracle_newton_csr.argtypes = [P, d, d, d, d, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                               C.c_double, C.c_double, C.POINTER(_NewtonStats)]
     return _lib
 
 
@@ -1112,3 +1120,79 @@ def cuthill_mckee_dealii(G):
             order.append(d)
         last = nxt
     return np.array(order)
+
+
+def kelly_from_face_pieces(sp, faces, nodal, variable=0):
+    """KellyErrorEstimator::estimate (deal.II 9.2, called by refine_mesh_kelly,
+    navier_stokes_base.cc:610-652) evaluated from face pieces: eta_K^2 = diam_K / 24 *
+    sum over the pieces of K's faces of sum_q JxW |grad u_a . g_a - grad u_b . g_b|^2, where each
+    piece holds, per face quadrature point, both sides' reference points xi and reference-space
+    normal-derivative weights g (the mapped normal), as gls_fe_space_kelly_faces lays them out (the
+    face geometry is shared input, like the mesh). Vectorised numpy over pieces x points x sides."""
+    dim = sp["dim"]
+    k = sp["k"] if variable == 0 else sp["kp"]
+    cn = np.asarray(sp["cell_vnodes"] if variable == 0 else sp["cell_pnodes"])
+    nv = sp["n_vnodes"]
+    ncomp = dim if variable == 0 else 1
+    loc = np.indices((k + 1,) * dim).reshape(dim, -1)[::-1].T  # local node a -> (i_x, i_y, i_z)
+    pts = np.linspace(0.0, 1.0, k + 1) if k <= 2 else None
+    if pts is None:  # Gauss-Lobatto support points for k >= 3
+        from numpy.polynomial import legendre
+        inner = np.sort(np.real(legendre.Legendre.basis(k).deriv().roots()))
+        pts = np.concatenate([[0.0], 0.5 * (inner + 1.0), [1.0]])
+    xi, g = faces["xi"], faces["g"]  # (ne, nqf, 2, dim)
+    L = np.ones(xi.shape + (k + 1,))
+    dL = np.zeros(xi.shape + (k + 1,))
+    for a in range(k + 1):
+        for b in range(k + 1):
+            if b == a:
+                continue
+            L[..., a] *= (xi - pts[b]) / (pts[a] - pts[b])
+        for c in range(k + 1):  # derivative: sum over the dropped factor
+            if c == a:
+                continue
+            t = np.full(xi.shape, 1.0 / (pts[a] - pts[c]))
+            for b in range(k + 1):
+                if b != a and b != c:
+                    t = t * (xi - pts[b]) / (pts[a] - pts[b])
+            dL[..., a] += t
+    # gphi[e, q, side, a] = sum_d g_d dphi_a/dxi_d
+    gphi = np.zeros(xi.shape[:3] + (len(loc),))
+    for a, ia in enumerate(loc):
+        for d in range(dim):
+            t = g[..., d] * dL[..., d, ia[d]]
+            for o in range(dim):
+                if o != d:
+                    t = t * L[..., o, ia[o]]
+            gphi[..., a] += t
+    cells = np.stack([faces["ca"], faces["cb"]], axis=1)  # (ne, 2)
+    nodes = cn[cells]  # (ne, 2, nloc)
+    if variable == 0:
+        vals = np.asarray(nodal)[:dim * nv].reshape(nv, dim)[nodes]  # (ne, 2, nloc, dim)
+    else:
+        vals = np.asarray(nodal)[dim * nv:][nodes][..., None]
+    dn = np.einsum("eqsa,esac->eqsc", gphi, vals)  # (ne, nqf, 2, ncomp)
+    jump = ((dn[:, :, 0] - dn[:, :, 1]) ** 2).sum(axis=-1)  # (ne, nqf)
+    tot = (faces["jxw"] * jump).sum(axis=1)
+    acc = np.zeros(sp["n_cells"])
+    np.add.at(acc, faces["ca"], tot)
+    np.add.at(acc, faces["cb"], tot)
+    assert ncomp >= 1
+    return np.sqrt(faces["diam"] / 24.0 * acc)
+
+
+def newton_csr(prob: StructuredProblem, x, u1=None, u2=None, u3=None, threads=1, restart=30, rel=1e-4, minres=1e-12,
+               max_its=5000, athresh=1e-8, rthresh=1.0):
+    """One complete Newton iteration of the reference's CPU path on the assembled system
+    (gls_oracle_newton_csr: CSR assembly on `threads`, ILU(0), GMRES(restart) with ILU(0), line
+    search); x (numpy, float64) is updated in place. Returns the timing / iteration dict."""
+    L = lib()
+    P = prob.struct()
+    orc = Oracle(prob)
+    h = orc._hist(u1, u2, u3)
+    st = _NewtonStats()
+    assert x.dtype == np.float64 and x.flags["C_CONTIGUOUS"]
+    rc = L.gls_oracle_newton_csr(C.byref(P), _dp(x), _dp(h[0]), _dp(h[1]), _dp(h[2]), int(threads), int(restart),
+                                 float(rel), float(minres), int(max_its), float(athresh), float(rthresh), C.byref(st))
+    assert rc == 0, rc
+    return {f: getattr(st, f) for f, _ in _NewtonStats._fields_}

@@ -328,7 +328,13 @@ struct gls_ctx {
   // distributed (rank-local mesh): owned nodes [0, n_owned), ghosts after; exchange via callbacks
   struct Dist {
     bool on = false;
-    int64_t n_owned = 0, n_send = 0, n_recv = 0;
+    // dofs: DoF-level exchange of a general mesh (gls_dist_attach_dofs: one double per DoF, owned
+    // velocity nodes [0, n_owned) and owned pressure nodes [0, n_owned_p) first); else node-level
+    // exchange of a Morton brick mesh (4 doubles per node)
+    bool dofs = false;
+    int width = 4;  // doubles per exchange entry
+    int64_t n_owned = 0, n_owned_p = 0, n_send = 0, n_recv = 0;
+    DevBuf<int32_t> add_u, add_off, add_slot;  // export-add of the DoF exchange in a fixed order
     DevBuf<int32_t> send_nodes, recv_nodes;
     double *send_buf = nullptr, *recv_buf = nullptr, *red_buf = nullptr;
     gls_exchange_fn xchg = nullptr;
@@ -357,6 +363,14 @@ struct gls_ctx {
     double athresh = 0., rthresh = 1.;
     double boost_tol = 0., boost_val = 0.;  // rocsparse keeps these POINTERS and reads them in csrilu0
     int n_probes = 0, fill = 0;
+    int64_t block_dofs = 0;  // subdomain size of the block-Jacobi ILU (gls_ilu_set_options); 0: one block
+    int ordering = GLS_ILU_ORDER_CM, n_blocks = 1, n_order_colors = 0;
+    // multicolor order with a pattern whose same-color entries stay inside a node (fill 0): the
+    // color-by-color solves of gls_ilu_kernels.hip replace rocSPARSE csrsv
+    bool mc_solve = false;
+    std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
+    DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
+    DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
     DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
@@ -482,6 +496,7 @@ struct gls_ctx {
     int n_hist = 0, scheme = GLS_STEADY;
   } jf;
   int skip_consecutive = 0;  // SkipNewtonNonLinearSolver::consecutive_iters (persists across solves)
+  bool probe_local = false;  // ILU probe across ranks: J.v on the rank's cells only (no ghost exchange)
   // TimerOutput sections of the reference's Newton/GMRES path (gls_section_timing): wall seconds and
   // calls, stream-synchronised at the section boundaries while enabled
   bool sec_on = false;
@@ -839,6 +854,12 @@ struct TimedLaunch {
 // ---- distributed hooks (no-ops on a single rank)
 int dist_import(gls_ctx *c, double *x) {
   if (!c->dist.on) return GLS_OK;
+  if (c->dist.dofs) {
+    HIP_TRY(gls::vec_pack_dofs(x, c->dist.send_nodes.p, c->dist.n_send, c->dist.send_buf, c->stream));
+    if (c->dist.xchg(c->dist.user, 0) != 0) return set_err(GLS_ECOMM, "ghost import exchange failed");
+    HIP_TRY(gls::vec_unpack_dofs(x, c->dist.recv_nodes.p, c->dist.n_recv, c->dist.recv_buf, c->stream));
+    return GLS_OK;
+  }
   const int64_t voff = 3 * (int64_t)c->n_vnodes;
   HIP_TRY(gls::vec_pack_nodes(x, c->dist.send_nodes.p, c->dist.n_send, voff, c->dist.send_buf, c->stream));
   if (c->dist.xchg(c->dist.user, 0) != 0) return set_err(GLS_ECOMM, "ghost import exchange failed");
@@ -847,6 +868,13 @@ int dist_import(gls_ctx *c, double *x) {
 }
 int dist_export_add(gls_ctx *c, double *y) {
   if (!c->dist.on) return GLS_OK;
+  if (c->dist.dofs) {
+    HIP_TRY(gls::vec_pack_dofs(y, c->dist.recv_nodes.p, c->dist.n_recv, c->dist.recv_buf, c->stream));
+    if (c->dist.xchg(c->dist.user, 1) != 0) return set_err(GLS_ECOMM, "ghost export exchange failed");
+    HIP_TRY(gls::vec_add_dofs_ordered(y, c->dist.add_u.p, c->dist.add_off.p, c->dist.add_slot.p, (int64_t)c->dist.add_u.n,
+                                      c->dist.send_buf, c->stream));
+    return GLS_OK;
+  }
   const int64_t voff = 3 * (int64_t)c->n_vnodes;
   HIP_TRY(gls::vec_pack_nodes(y, c->dist.recv_nodes.p, c->dist.n_recv, voff, c->dist.recv_buf, c->stream));
   if (c->dist.xchg(c->dist.user, 1) != 0) return set_err(GLS_ECOMM, "ghost export exchange failed");
@@ -855,9 +883,9 @@ int dist_export_add(gls_ctx *c, double *y) {
 }
 // out[k] = sum over OWNED DoFs of A[k] . w, reduced over ranks (host result)
 int dist_multidot(gls_ctx *c, const double *A, int64_t lda, int nk, const double *w, double *host_out) {
-  const int64_t n1 = c->dist.on ? 3 * c->dist.n_owned : c->n_dofs;
-  const int64_t off2 = c->dist.on ? 3 * (int64_t)c->n_vnodes : 0;
-  const int64_t n2 = c->dist.on ? c->dist.n_owned : 0;
+  const int64_t n1 = c->dist.on ? (int64_t)c->dim * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? (int64_t)c->dim * c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned_p : 0;
   HIP_TRY(gls::vec_multidot2(A, lda, nk, w, n1, off2, n2, c->scal.p, c->work.p, c->stream));
   if (c->dist.on) {
     HIP_TRY(hipMemcpyAsync(c->dist.red_buf, c->scal.p, sizeof(double) * nk, hipMemcpyDeviceToDevice, c->stream));
@@ -982,7 +1010,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
   const bool split_jv = mode == gls::MODE_JV && split_jv_enabled(c);
-  if (mode == gls::MODE_JV && !split_jv) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
+  if (mode == gls::MODE_JV && !split_jv && !c->probe_local) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
   gls::OpParams P = make_params(c, mode != gls::MODE_RESIDUAL);
   if (mode == gls::MODE_JV && c->use_brick && c->use_qdata) {
     GLS_TRY(ensure_qdata(c));
@@ -1054,10 +1082,13 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     TimedLaunch t(c, 5);
     HIP_TRY(slab_sum(c, y));
   }
-  GLS_TRY(dist_export_add(c, y));  // ghost contributions -> owners (compress(add))
-  if (c->hang.on && (mode == gls::MODE_RESIDUAL || mode == gls::MODE_JV))  // C^T y: rows onto masters
+  // C^T y: the local cells' hanging rows onto their masters (masters across the partition are local
+  // ghosts), then the ghost contributions to their owners (compress(add)); condensing the partial
+  // rows before the export equals condensing the summed rows after it
+  if (c->hang.on && (mode == gls::MODE_RESIDUAL || mode == gls::MODE_JV))
     HIP_TRY(gls::vec_csr_condense(y, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
                                   (int64_t)c->hang.tm.n, c->stream));
+  if (!c->probe_local) GLS_TRY(dist_export_add(c, y));
   if (lin_diag) {  // the same launch stored the J.v linearization
     c->qd_valid = true;
     c->qd32_valid = P.qdf != nullptr;
@@ -1069,9 +1100,9 @@ int ensure_diag(gls_ctx *c) {
   if (c->diag_valid) return GLS_OK;
   GLS_TRY(run_cell(c, gls::MODE_DIAG, nullptr, c->diag.p));
   if (c->dist.on) {  // ghost rows are not owned here: keep the Jacobi division finite
-    const int64_t nl = c->n_vnodes, no = c->dist.n_owned;
-    HIP_TRY(gls::vec_fill(c->diag.p + 3 * no, 3 * (nl - no), 1.0, c->stream));
-    HIP_TRY(gls::vec_fill(c->diag.p + 3 * nl + no, nl - no, 1.0, c->stream));
+    const int64_t d = c->dim, nl = c->n_vnodes, no = c->dist.n_owned, npl = c->n_dofs - d * nl, nop = c->dist.n_owned_p;
+    HIP_TRY(gls::vec_fill(c->diag.p + d * no, d * (nl - no), 1.0, c->stream));
+    HIP_TRY(gls::vec_fill(c->diag.p + d * nl + nop, npl - nop, 1.0, c->stream));
   }
   c->diag_valid = true;
   return GLS_OK;
@@ -1081,9 +1112,9 @@ int ensure_diag(gls_ctx *c) {
 // host_out[dots ? nk : 0] = ||w_new||^2 over owned DoFs, reduced over ranks
 int dist_multiaxpy_dots(gls_ctx *c, double *w, const double *V, int64_t lda, int nk, const double *h, bool dots,
                         double *host_out, double scale = 1.0) {
-  const int64_t n1 = c->dist.on ? 3 * c->dist.n_owned : c->n_dofs;
-  const int64_t off2 = c->dist.on ? 3 * (int64_t)c->n_vnodes : 0;
-  const int64_t n2 = c->dist.on ? c->dist.n_owned : 0;
+  const int64_t n1 = c->dist.on ? (int64_t)c->dim * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? (int64_t)c->dim * c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned_p : 0;
   const int nd = dots ? nk + 1 : 1;
   HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, scale, c->scal.p, c->work.p,
                                   c->stream));
@@ -1412,6 +1443,9 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   GLS_TRY(c->dist.send_nodes.upload(send_nodes, (size_t)ns));
   GLS_TRY(c->dist.recv_nodes.upload(recv_nodes, (size_t)nr));
   c->dist.n_owned = n_owned_nodes;
+  c->dist.n_owned_p = n_owned_nodes;
+  c->dist.dofs = false;
+  c->dist.width = 4;
   c->dist.n_send = ns;
   c->dist.n_recv = nr;
   c->dist.send_buf = send_buf;
@@ -1430,6 +1464,64 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
     for (int64_t i = 0; i < nr; ++i) flag[(size_t)recv_nodes[i]] = 1;
     GLS_TRY(build_brick_split(c, flag));
   }
+  return GLS_OK;
+}
+
+int gls_dist_attach_dofs(gls_ctx *c, int64_t n_owned_vnodes, int64_t n_owned_pnodes, int n_nbrs,
+                         const int64_t *send_offsets, const int32_t *send_dofs, const int64_t *recv_offsets,
+                         const int32_t *recv_dofs, double *send_buf, double *recv_buf, double *red_buf,
+                         gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user) {
+  GLS_TRY(check_ctx(c));
+  const int64_t nvd = (int64_t)c->dim * c->n_vnodes, npn = c->n_dofs - nvd;
+  if (n_owned_vnodes < 0 || n_owned_vnodes > c->n_vnodes || n_owned_pnodes < 0 || n_owned_pnodes > npn || n_nbrs < 0 ||
+      !xchg || !allreduce || !red_buf)
+    return set_err(GLS_EINVAL, "gls_dist_attach_dofs: bad arguments");
+  if (c->mg.on) return set_err(GLS_EINVAL, "gls_dist_attach_dofs: no multigrid");
+  const int64_t ns = n_nbrs ? send_offsets[n_nbrs] : 0, nr = n_nbrs ? recv_offsets[n_nbrs] : 0;
+  auto owned = [&](int64_t d) { return d < nvd ? d / c->dim < n_owned_vnodes : d - nvd < n_owned_pnodes; };
+  for (int64_t i = 0; i < ns; ++i)
+    if (send_dofs[i] < 0 || send_dofs[i] >= c->n_dofs || !owned(send_dofs[i])) return set_err(GLS_EINVAL, "send DoF not owned");
+  for (int64_t i = 0; i < nr; ++i)
+    if (recv_dofs[i] < 0 || recv_dofs[i] >= c->n_dofs || owned(recv_dofs[i])) return set_err(GLS_EINVAL, "recv DoF not a ghost");
+  if ((ns && !send_buf) || (nr && !recv_buf)) return set_err(GLS_EINVAL, "exchange buffers missing");
+  // export-add: every owned DoF's incoming slots in neighbour order (deterministic sums)
+  std::vector<std::pair<int32_t, int32_t>> ds;
+  ds.reserve((size_t)ns);
+  for (int64_t j = 0; j < ns; ++j) ds.push_back({send_dofs[j], (int32_t)j});
+  std::stable_sort(ds.begin(), ds.end(), [](const std::pair<int32_t, int32_t> &a, const std::pair<int32_t, int32_t> &b) {
+    return a.first < b.first;
+  });
+  std::vector<int32_t> au, aoff{0}, aslot;
+  for (size_t t = 0; t < ds.size(); ++t) {
+    if (t == 0 || ds[t].first != ds[t - 1].first) {
+      if (t) aoff.push_back((int32_t)aslot.size());
+      au.push_back(ds[t].first);
+    }
+    aslot.push_back(ds[t].second);
+  }
+  if (!au.empty()) aoff.push_back((int32_t)aslot.size());
+  auto &D = c->dist;
+  GLS_TRY(D.send_nodes.upload(send_dofs, (size_t)ns));
+  GLS_TRY(D.recv_nodes.upload(recv_dofs, (size_t)nr));
+  GLS_TRY(D.add_u.upload(au.data(), au.size()));
+  GLS_TRY(D.add_off.upload(aoff.data(), au.empty() ? 0 : aoff.size()));
+  GLS_TRY(D.add_slot.upload(aslot.data(), aslot.size()));
+  D.dofs = true;
+  D.width = 1;
+  D.n_owned = n_owned_vnodes;
+  D.n_owned_p = n_owned_pnodes;
+  D.n_send = ns;
+  D.n_recv = nr;
+  D.send_buf = send_buf;
+  D.recv_buf = recv_buf;
+  D.red_buf = red_buf;
+  D.xchg = xchg;
+  D.allreduce = allreduce;
+  D.user = user;
+  D.on = true;
+  c->diag_valid = false;
+  c->ilu.valid = false;
+  c->qd_valid = false;
   return GLS_OK;
 }
 
@@ -1581,9 +1673,12 @@ int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *
 int gls_apply_dirichlet(gls_ctx *c, double *x) {
   GLS_TRY(check_ctx(c));
   HIP_TRY(gls::vec_set_indexed(x, c->dir_dofs.p, c->dir_vals.p, (int64_t)c->dir_dofs.n, c->stream));
-  if (c->hang.on)  // hanging values from their masters (all masters: Dirichlet values included)
+  if (c->hang.on) {  // hanging values from their masters (all masters: Dirichlet values included)
+    // across ranks the masters may be ghosts: their owners' values first
+    if (c->dist.on) GLS_TRY(dist_import(c, x));
     HIP_TRY(gls::vec_csr_gather_set(x, x, c->hang.dof.p, c->hang.off.p, c->hang.master.p, c->hang.w.p,
                                     (int64_t)c->hang.dof.n, c->stream));
+  }
   if (!c->jf.on && (x == c->u || x == c->u1 || x == c->u2 || x == c->u3)) {  // the captured state changed
     c->diag_valid = false;
     c->ilu.valid = false;
@@ -1597,7 +1692,8 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
                     const double *w) {
   GLS_TRY(check_ctx(c));
   if (n < 0 || (n > 0 && (!dofs || !off || !masters || !w))) return set_err(GLS_EINVAL, "gls_set_hanging: arrays");
-  if (c->dist.on || c->mg.on) return set_err(GLS_EINVAL, "hanging constraints: single GPU, no multigrid");
+  if (c->mg.on) return set_err(GLS_EINVAL, "hanging constraints: no multigrid");
+  if (c->dist.on && !c->dist.dofs) return set_err(GLS_EINVAL, "hanging constraints across ranks: gls_dist_attach_dofs");
   HIP_TRY(hipStreamSynchronize(c->stream));
   const int dim = c->dim;
   const int64_t N = c->n_dofs, nvd = (int64_t)dim * c->n_vnodes;
@@ -2034,7 +2130,8 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
   auto &I = c->ilu;
   const int64_t n = c->n_dofs;
   hipStream_t s = c->stream;
-  if (I.fill > 0) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
+  if (I.fill > 0 || c->dist.on) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
+  c->probe_local = c->dist.on;  // owned block: the probe's J.v skips the ghost exchange (ghost v = 0)
   for (int p = 0; p < I.n_probes; ++p) {
     HIP_TRY(gls::vec_fill(I.vbuf.p, n, 0.0, s));
     HIP_TRY(gls::vec_set_const_indexed(I.vbuf.p, I.pdofs.p + I.pdoff[(size_t)p], I.pdoff[(size_t)p + 1] - I.pdoff[(size_t)p],
@@ -2043,6 +2140,8 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
     HIP_TRY(gls::csr_probe_extract(I.val.p, I.pent.p + I.peoff[(size_t)p], I.prow.p + I.peoff[(size_t)p],
                                    I.peoff[(size_t)p + 1] - I.peoff[(size_t)p], I.ybuf.p, s));
   }
+  c->probe_local = false;
+  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
   return GLS_OK;
 }
 static int apply_ilu(gls_ctx *c, const double *v, double *z);
@@ -2084,6 +2183,12 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   RS_TRY(rocsparse_set_stream(I.h, c->stream));
   // z = P^T U^-1 L^-1 P v (P: the Cuthill-McKee renumbering the factors live in)
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
+  if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
+    HIP_TRY(gls::ilu_mc_solve(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
+                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, c->stream));
+    HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
+    return GLS_OK;
+  }
   RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dL, I.val.p, I.rowp.p, I.col.p, I.info,
                                 I.vbuf.p, I.tbuf.p, rocsparse_solve_policy_auto, I.work.p));
   RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
@@ -3019,7 +3124,7 @@ int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
 extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthresh) {
   GLS_TRY(check_ctx(c));
   auto &I = c->ilu;
-  if (c->dist.on) return set_err(GLS_EINVAL, "gls_ilu_attach: single-rank contexts only");
+  if (c->dist.on && !c->dist.dofs) return set_err(GLS_EINVAL, "gls_ilu_attach: brick-partitioned contexts use the multigrid");
   if (c->mg.on) return set_err(GLS_EINVAL, "gls_ilu_attach: a multigrid preconditioner is attached");
   if (fill < 0 || fill > GLS_ILU_MAX_FILL)
     return set_err(GLS_EINVAL, "gls_ilu_attach: ilu preconditioner fill %d not supported (0..%d)", fill, GLS_ILU_MAX_FILL);
@@ -3061,7 +3166,15 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       lidx[(size_t)c->hang.h_dof[i]] = (int64_t)i;
       isline[(size_t)c->hang.h_dof[i]] = 1;
     }
-  auto dirichlet = [&](int64_t d) { return cons[(size_t)d] && !isline[(size_t)d]; };
+  // across ranks (Ifpack additive Schwarz, overlap 0, as the reference runs with MPI): each rank
+  // factors its owned rows and columns; ghost DoFs are identity rows and drop out of the pattern
+  auto ghost = [&](int64_t d) {
+    if (!c->dist.on) return false;
+    return d < nvd ? d / dim >= c->dist.n_owned : d - nvd >= c->dist.n_owned_p;
+  };
+  for (int64_t d = 0; d < n; ++d)
+    if (ghost(d)) cons[(size_t)d] = 1;
+  auto dirichlet = [&](int64_t d) { return (cons[(size_t)d] && !isline[(size_t)d]) || ghost(d); };
   // effective DoFs of each cell: its unconstrained DoFs and the (non-Dirichlet) masters of its lines
   std::vector<int64_t> effoff((size_t)nc + 1, 0), eff;
   {
@@ -3074,7 +3187,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
         const int m = node_dofs(cell_node(e, a), d, sl);
         for (int j = 0; j < m; ++j) {
           const int64_t li = lidx[(size_t)d[j]];
-          if (li >= 0) {
+          if (li >= 0 && !ghost(d[j])) {
             for (int64_t t = c->hang.h_off[(size_t)li]; t < c->hang.h_off[(size_t)li + 1]; ++t)
               if (!dirichlet(c->hang.h_master[(size_t)t])) buf.push_back(c->hang.h_master[(size_t)t]);
           } else if (!cons[(size_t)d[j]]) {
@@ -3227,6 +3340,75 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int64_t> order;
   gls::cuthill_mckee_nodes(ncm, cadj_off, cadj, cm_doff, cm_dofs, order);
   if ((int64_t)order.size() != n) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering covers %lld of %lld DoFs", (long long)order.size(), (long long)n);
+  // subdomains (Ifpack's additive Schwarz with overlap 0, which the reference runs with one block per
+  // MPI rank): contiguous ranges of the cell order (space-filling: leaf order of the forest / Morton
+  // bricks), a DoF in the block of its lowest cell; couplings between blocks are dropped, each block
+  // is factored on its own, the blocks' triangular solves run side by side
+  const int nblk = I.block_dofs > 0 ? (int)std::min<int64_t>(std::max<int64_t>((n + I.block_dofs - 1) / I.block_dofs, 1), nc) : 1;
+  std::vector<int32_t> dblk((size_t)n, 0);
+  std::vector<int64_t> dnode_((size_t)n, 0);  // DoF -> unified node
+  for (int64_t x = 0; x < nu; ++x) {
+    int64_t d[4];
+    int sl[4];
+    const int m = node_dofs(x, d, sl);
+    for (int j = 0; j < m; ++j) dnode_[(size_t)d[j]] = x;
+  }
+  if (nblk > 1) {
+    std::vector<int32_t> nodeblk((size_t)nu, INT32_MAX);
+    for (int64_t e = 0; e < nc; ++e) {
+      const int32_t b = (int32_t)(e * nblk / nc);
+      for (int a = 0; a < ncn; ++a) {
+        int32_t &nb_ = nodeblk[(size_t)cell_node(e, a)];
+        nb_ = std::min(nb_, b);
+      }
+    }
+    for (int64_t d = 0; d < n; ++d) {
+      const int32_t b = nodeblk[(size_t)dnode_[(size_t)d]];
+      dblk[(size_t)d] = b == INT32_MAX ? 0 : b;
+    }
+  }
+  std::vector<int32_t> dcolor;  // multicolor: each DoF's color (its node's)
+  if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
+    // multicolor order: a greedy distance-1 coloring of the node graph of the system matrix (nodes
+    // visited in Cuthill-McKee order); DoFs sorted by (color, node's first Cuthill-McKee position,
+    // position), so a node's DoFs stay consecutive. Same-colored nodes share no matrix entry: each
+    // color's diagonal block is block-diagonal by node, and the triangular solves' dependency chain
+    // is ~colors x DoFs per node. (Blocks only drop couplings here: the colors stay outermost.)
+    std::vector<int> c1((size_t)nu, -1), used;
+    int ncl = 0;
+    for (int64_t t = 0; t < n; ++t) {
+      const int64_t x = dnode_[(size_t)order[(size_t)t]];
+      if (c1[(size_t)x] >= 0) continue;
+      for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) {
+        const int cy = c1[(size_t)n1[(size_t)u]];
+        if (cy >= 0) {
+          if ((int)used.size() <= cy) used.resize((size_t)cy + 1, -1);
+          used[(size_t)cy] = (int)x;
+        }
+      }
+      int col = 0;
+      while (col < (int)used.size() && used[(size_t)col] == (int)x) ++col;
+      c1[(size_t)x] = col;
+      ncl = std::max(ncl, col + 1);
+    }
+    I.n_order_colors = ncl;
+    std::vector<int64_t> npos((size_t)nu, INT64_MAX), pos((size_t)n);
+    for (int64_t t = 0; t < n; ++t) {
+      pos[(size_t)order[(size_t)t]] = t;
+      int64_t &np_ = npos[(size_t)dnode_[(size_t)order[(size_t)t]]];
+      np_ = std::min(np_, t);
+    }
+    dcolor.assign((size_t)n, 0);
+    for (int64_t d = 0; d < n; ++d) dcolor[(size_t)d] = c1[(size_t)dnode_[(size_t)d]];
+    std::sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      if (dcolor[(size_t)a] != dcolor[(size_t)b]) return dcolor[(size_t)a] < dcolor[(size_t)b];
+      const int64_t pa = npos[(size_t)dnode_[(size_t)a]], pb = npos[(size_t)dnode_[(size_t)b]];
+      if (pa != pb) return pa < pb;
+      return pos[(size_t)a] < pos[(size_t)b];
+    });
+  } else if (nblk > 1) {
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return dblk[(size_t)a] < dblk[(size_t)b]; });
+  }
   std::vector<int32_t> newidx((size_t)n, -1), olddof((size_t)n);
   for (int64_t r = 0; r < n; ++r) {
     newidx[(size_t)order[(size_t)r]] = (int32_t)r;
@@ -3238,7 +3420,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   for (int64_t r = 0; r < n; ++r) {
     const int64_t i = olddof[(size_t)r];
     const size_t s0 = acl.size();
-    for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t) acl.push_back(newidx[(size_t)acol[(size_t)t]]);
+    for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t)
+      if (dblk[(size_t)acol[(size_t)t]] == dblk[(size_t)i]) acl.push_back(newidx[(size_t)acol[(size_t)t]]);
     std::sort(acl.begin() + (std::ptrdiff_t)s0, acl.end());
     arow[(size_t)r + 1] = (int32_t)acl.size();
   }
@@ -3251,6 +3434,43 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     const auto it = std::lower_bound(b, e, (int32_t)r);
     if (it == e || *it != r) return set_err(GLS_EINVAL, "gls_ilu_attach: row %lld has no diagonal", (long long)r);
     didx[(size_t)r] = (int32_t)(it - col.begin());
+  }
+  // multicolor solves: node groups (consecutive rows of one node), per color their range, per row
+  // the split of its entries into other colors / own node; valid while no entry couples two nodes of
+  // one color (fill 0; fill-in can create such entries: then rocSPARSE csrsv solves)
+  I.mc_solve = false;
+  if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
+    const int ncl = I.n_order_colors;
+    std::vector<int32_t> cstart((size_t)ncl + 2, (int32_t)n), grow, cg((size_t)ncl + 1, 0), lsp((size_t)n), usp((size_t)n);
+    for (int64_t r = n - 1; r >= 0; --r) cstart[(size_t)dcolor[(size_t)olddof[(size_t)r]]] = (int32_t)r;
+    for (int c = ncl - 1; c >= 0; --c) cstart[(size_t)c] = std::min(cstart[(size_t)c], cstart[(size_t)c + 1]);
+    bool ok = true;
+    for (int64_t r = 0; r < n && ok; ++r) {
+      const int64_t x = dnode_[(size_t)olddof[(size_t)r]];
+      if (r == 0 || x != dnode_[(size_t)olddof[(size_t)r - 1]]) grow.push_back((int32_t)r);
+      if (r + 1 - grow.back() > gls::kMaxGroupRows) ok = false;
+      const int cr = dcolor[(size_t)olddof[(size_t)r]];
+      int32_t e = rowp[(size_t)r];
+      while (e < rowp[(size_t)r + 1] && col[(size_t)e] < cstart[(size_t)cr]) ++e;
+      lsp[(size_t)r] = e;
+      while (e < rowp[(size_t)r + 1] && col[(size_t)e] < cstart[(size_t)cr + 1]) {
+        if (dnode_[(size_t)olddof[(size_t)col[(size_t)e]]] != x) ok = false;  // same color, other node
+        ++e;
+      }
+      usp[(size_t)r] = e;
+    }
+    if (ok) {
+      grow.push_back((int32_t)n);
+      for (int c = 0, g = 0; c <= ncl; ++c) {
+        while (g + 1 < (int)grow.size() && grow[(size_t)g] < cstart[(size_t)c]) ++g;
+        cg[(size_t)c] = c == ncl ? (int)grow.size() - 1 : g;
+      }
+      GLS_TRY(I.mc_grow.upload(grow.data(), grow.size()));
+      GLS_TRY(I.mc_lsp.upload(lsp.data(), lsp.size()));
+      GLS_TRY(I.mc_usp.upload(usp.data(), usp.size()));
+      I.mc_cg = cg;
+      I.mc_solve = true;
+    }
   }
   // probes: one per (color, slot); every entry of the system matrix is read from the probe of its
   // column DoF (entry position in the ILU pattern, row's original DoF)
@@ -3275,7 +3495,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int32_t> pdofs((size_t)pdoff[(size_t)nprobe]), pent((size_t)peoff[(size_t)nprobe]), prow(pent.size());
   {
     std::vector<int64_t> f1(pdoff.begin(), pdoff.end() - 1), f2(peoff.begin(), peoff.end() - 1);
-    for (int64_t d = 0; d < n; ++d) pdofs[(size_t)f1[(size_t)probe_of(d)]++] = (int32_t)d;
+    for (int64_t d = 0; d < n; ++d) pdofs[(size_t)f1[(size_t)probe_of(d)]++] = ghost(d) ? -1 : (int32_t)d;
     for (int64_t r = 0; r < n; ++r) {
       int32_t pos = rowp[(size_t)r];
       for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) {
@@ -3291,6 +3511,22 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   GLS_TRY(I.col.upload(col.data(), col.size()));
   GLS_TRY(I.didx.upload(didx.data(), didx.size()));
   GLS_TRY(I.perm.upload(newidx.data(), newidx.size()));
+  // ghost DoFs are not probed (identity rows): drop them from the unit lists, remember their diagonals
+  {
+    std::vector<int32_t> pd2;
+    std::vector<int64_t> pdoff2((size_t)nprobe + 1, 0);
+    for (int p = 0; p < nprobe; ++p) {
+      for (int64_t t = pdoff[(size_t)p]; t < pdoff[(size_t)p + 1]; ++t)
+        if (pdofs[(size_t)t] >= 0) pd2.push_back(pdofs[(size_t)t]);
+      pdoff2[(size_t)p + 1] = (int64_t)pd2.size();
+    }
+    pdofs.swap(pd2);
+    pdoff.swap(pdoff2);
+    std::vector<int32_t> gd;
+    for (int64_t r = 0; r < n; ++r)
+      if (ghost(olddof[(size_t)r])) gd.push_back(didx[(size_t)r]);
+    GLS_TRY(I.ghost_diag.upload(gd.data(), gd.size()));
+  }
   GLS_TRY(I.pdofs.upload(pdofs.data(), pdofs.size()));
   GLS_TRY(I.pent.upload(pent.data(), pent.size()));
   GLS_TRY(I.prow.upload(prow.data(), prow.size()));
@@ -3305,6 +3541,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   I.nnz = (int64_t)col.size();
   I.nnz_a = (int64_t)acl.size();
   I.fill = fill;
+  I.n_blocks = nblk;
   I.athresh = athresh;
   I.rthresh = rthresh;
   RS_TRY(rocsparse_create_handle(&I.h));
@@ -3338,8 +3575,18 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   I.on = true;
   I.valid = false;
   if (std::getenv("GLS_ILU_VERBOSE"))
-    std::printf("ilu attach: n %lld fill %d nnz(A) %lld nnz(ILU) %lld colors %d probes %d\n", (long long)n, fill,
-                (long long)I.nnz_a, (long long)I.nnz, ncol, nprobe);
+    std::printf("ilu attach: n %lld fill %d blocks %d ordering %s (%d colors%s) nnz(A) %lld nnz(ILU) %lld probe colors "
+                "%d probes %d\n", (long long)n, fill, nblk, I.ordering == GLS_ILU_ORDER_CM ? "cuthill-mckee" : "multicolor",
+                I.n_order_colors, I.mc_solve ? ", color solves" : "", (long long)I.nnz_a, (long long)I.nnz, ncol, nprobe);
+  return GLS_OK;
+}
+extern "C" int gls_ilu_set_options(gls_ctx *c, int ordering, int64_t block_dofs) {
+  GLS_TRY(check_ctx(c));
+  if (block_dofs < 0) return set_err(GLS_EINVAL, "gls_ilu_set_options: negative block size");
+  if (ordering != GLS_ILU_ORDER_CM && ordering != GLS_ILU_ORDER_MULTICOLOR)
+    return set_err(GLS_EINVAL, "gls_ilu_set_options: ordering %d", ordering);
+  c->ilu.block_dofs = block_dofs;
+  c->ilu.ordering = ordering;
   return GLS_OK;
 }
 extern "C" int gls_ilu_detach(gls_ctx *c) {
@@ -3430,9 +3677,10 @@ int rccl_exchange_on(gls_ctx *c, int phase, hipStream_t stream) {
   const std::vector<int64_t> &so = phase == 0 ? D.soff : D.roff, &ro = phase == 0 ? D.roff : D.soff;
   if (ncclGroupStart() != ncclSuccess) return -1;
   for (size_t i = 0; i < D.nbrs.size(); ++i) {
-    const size_t ns = (size_t)(4 * (so[i + 1] - so[i])), nr = (size_t)(4 * (ro[i + 1] - ro[i]));
-    if (ns && ncclSend(sb + 4 * so[i], ns, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
-    if (nr && ncclRecv(rb + 4 * ro[i], nr, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
+    const int w = D.width;
+    const size_t ns = (size_t)(w * (so[i + 1] - so[i])), nr = (size_t)(w * (ro[i + 1] - ro[i]));
+    if (ns && ncclSend(sb + w * so[i], ns, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
+    if (nr && ncclRecv(rb + w * ro[i], nr, ncclDouble, D.nbrs[i], D.comm, stream) != ncclSuccess) return -1;
   }
   return ncclGroupEnd() == ncclSuccess ? 0 : -1;
 }
@@ -3487,6 +3735,33 @@ extern "C" int gls_dist_attach_rccl(gls_ctx *c, gls_rccl *r, int64_t n_owned_nod
     HIP_TRY(hipEventCreateWithFlags(&D.ev_ready, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&D.ev_done, hipEventDisableTiming));
   }
+  D.nbrs.assign(nbr_ranks, nbr_ranks + n_nbrs);
+  D.soff.assign(send_offsets, send_offsets + n_nbrs + 1);
+  D.roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);
+  if (n_nbrs == 0) {
+    D.soff.assign(1, 0);
+    D.roff.assign(1, 0);
+  }
+  return GLS_OK;
+}
+
+extern "C" int gls_dist_attach_dofs_rccl(gls_ctx *c, gls_rccl *r, int64_t n_owned_vnodes, int64_t n_owned_pnodes,
+                                         int n_nbrs, const int *nbr_ranks, const int64_t *send_offsets,
+                                         const int32_t *send_dofs, const int64_t *recv_offsets, const int32_t *recv_dofs) {
+  GLS_TRY(check_ctx(c));
+  if (!r || !r->comm || n_nbrs < 0 || (n_nbrs > 0 && (!nbr_ranks || !send_offsets || !recv_offsets)))
+    return set_err(GLS_EINVAL, "gls_dist_attach_dofs_rccl: bad arguments");
+  auto &D = c->dist;
+  const int64_t ns = n_nbrs ? send_offsets[n_nbrs] : 0, nr = n_nbrs ? recv_offsets[n_nbrs] : 0;
+  for (int i = 0; i < n_nbrs; ++i)
+    if (nbr_ranks[i] < 0 || nbr_ranks[i] >= r->world || nbr_ranks[i] == r->rank)
+      return set_err(GLS_EINVAL, "gls_dist_attach_dofs_rccl: neighbour rank %d", nbr_ranks[i]);
+  GLS_TRY(D.own_send.alloc((size_t)std::max<int64_t>(ns, 1)));
+  GLS_TRY(D.own_recv.alloc((size_t)std::max<int64_t>(nr, 1)));
+  GLS_TRY(D.own_red.alloc(256));
+  GLS_TRY(gls_dist_attach_dofs(c, n_owned_vnodes, n_owned_pnodes, n_nbrs, send_offsets, send_dofs, recv_offsets, recv_dofs,
+                               D.own_send.p, D.own_recv.p, D.own_red.p, rccl_exchange, rccl_allreduce, c));
+  D.comm = r->comm;
   D.nbrs.assign(nbr_ranks, nbr_ranks + n_nbrs);
   D.soff.assign(send_offsets, send_offsets + n_nbrs + 1);
   D.roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);

@@ -161,3 +161,286 @@ int gls_part_destroy(gls_part *p) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// General meshes (row e2 of SURVEY §8: adaptive / unstructured forests across ranks, the p::d
+// triangulation partition of navier_stokes_base.cc:55-60 re-done after every adaptation,
+// :682-733): any dim, Qk-Qk' with separate pressure nodes, hanging-node (and slip) lines.
+//  * cells: contiguous, equal-count ranges of the given cell order (the space-filling leaf order of
+//    the adapted forest), one per rank;
+//  * a node is owned by the lowest rank whose cells touch it; rank-local nodes are owned first
+//    (ascending global id), then ghosts (ascending (owner, global id)) -- velocity and pressure
+//    nodes separately;
+//  * ghosts also include the masters of every line whose DoF sits on a local cell and that no
+//    local cell touches (the coarse side of a hanging face across the partition), so C v and the
+//    condensation C^T y of the local cells need only local values;
+//  * exchange lists are DoF-level (one double per DoF): both sides derive them from the same
+//    replicated global mesh, ordered by global DoF id (velocity node*dim+c, pressure dim*NV+p).
+// ---------------------------------------------------------------------------------------------
+struct gls_gpart {
+  int dim = 0, nvl = 0, npl = 0;
+  bool sep = false;
+  int64_t cell_begin = 0, cell_end = 0;
+  int64_t n_owned_v = 0, n_owned_p = 0;
+  std::vector<int64_t> vl2g, pl2g;                  // local -> global node
+  std::vector<int32_t> local_cv, local_cp;          // local cell node maps
+  std::vector<int> nbrs;
+  std::vector<int64_t> send_off, recv_off;
+  std::vector<int32_t> send_dofs, recv_dofs;        // local DoF ids
+  std::vector<int64_t> gdof2l_keys, gdof2l_vals;    // sorted global DoF -> local DoF (local DoFs only)
+  int64_t n_local_dofs() const { return (int64_t)dim * (int64_t)vl2g.size() + (int64_t)(sep ? pl2g.size() : vl2g.size()); }
+};
+
+extern "C" {
+
+int gls_gpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cell_vnodes, const int32_t *cell_pnodes,
+                     int64_t n_vnodes, int64_t n_pnodes, int64_t n_lines, const int64_t *line_dofs,
+                     const int64_t *line_off, const int64_t *line_masters, int rank, int world, gls_gpart **out) {
+  if (!out || (dim != 2 && dim != 3) || k < 1 || kp < 1 || n_cells < 0 || !cell_vnodes || n_vnodes <= 0 || world < 1 ||
+      rank < 0 || rank >= world || n_lines < 0 || (n_lines > 0 && (!line_dofs || !line_off || !line_masters)))
+    return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: bad arguments");
+  std::unique_ptr<gls_gpart> p(new gls_gpart);
+  p->dim = dim;
+  p->nvl = 1;
+  p->npl = 1;
+  for (int d = 0; d < dim; ++d) {
+    p->nvl *= k + 1;
+    p->npl *= kp + 1;
+  }
+  p->sep = cell_pnodes != nullptr;
+  if (!p->sep && (kp != k || n_pnodes != n_vnodes))
+    return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: equal-order meshes share their nodes");
+  const int nvl = p->nvl, npl = p->npl;
+  const int64_t NV = n_vnodes, NP = p->sep ? n_pnodes : n_vnodes, NVD = (int64_t)dim * NV;
+  std::vector<int64_t> cb((size_t)world + 1);
+  for (int r = 0; r <= world; ++r) cb[(size_t)r] = n_cells * r / world;
+  p->cell_begin = cb[(size_t)rank];
+  p->cell_end = cb[(size_t)rank + 1];
+  auto rank_of_cell = [&](int64_t c) {
+    int r = (int)std::min<int64_t>(world - 1, c * world / std::max<int64_t>(n_cells, 1));
+    while (r > 0 && c < cb[(size_t)r]) --r;
+    while (r < world - 1 && c >= cb[(size_t)r + 1]) ++r;
+    return r;
+  };
+  // owners: the lowest rank touching the node
+  std::vector<int32_t> vown((size_t)NV, INT32_MAX), pown;
+  for (int64_t c = 0; c < n_cells; ++c) {
+    const int r = rank_of_cell(c);
+    for (int a = 0; a < nvl; ++a) {
+      const int32_t nd = cell_vnodes[c * nvl + a];
+      if (nd < 0 || nd >= NV) return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: node out of range");
+      vown[(size_t)nd] = std::min(vown[(size_t)nd], (int32_t)r);
+    }
+  }
+  if (p->sep) {
+    pown.assign((size_t)NP, INT32_MAX);
+    for (int64_t c = 0; c < n_cells; ++c) {
+      const int r = rank_of_cell(c);
+      for (int a = 0; a < npl; ++a) {
+        const int32_t nd = cell_pnodes[c * npl + a];
+        if (nd < 0 || nd >= NP) return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: pressure node out of range");
+        pown[(size_t)nd] = std::min(pown[(size_t)nd], (int32_t)r);
+      }
+    }
+  }
+  for (int64_t i = 0; i < NV; ++i)
+    if (vown[(size_t)i] == INT32_MAX) return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: a velocity node lies in no cell");
+  auto dof_owner = [&](int64_t g) -> int32_t {
+    if (g < NVD) return vown[(size_t)(g / dim)];
+    return p->sep ? pown[(size_t)(g - NVD)] : vown[(size_t)(g - NVD)];
+  };
+  // the lines of a global DoF
+  std::vector<int64_t> lidx((size_t)(NVD + NP), -1);
+  for (int64_t i = 0; i < n_lines; ++i) {
+    if (line_dofs[i] < 0 || line_dofs[i] >= NVD + NP) return gls_internal_set_err(GLS_EINVAL, "gls_gpart_create: line DoF");
+    lidx[(size_t)line_dofs[i]] = i;
+  }
+  // the global DoFs a rank needs: those of its cells and the masters of their lines
+  auto needed = [&](int r, std::vector<int64_t> &dofs) {
+    dofs.clear();
+    for (int64_t c = cb[(size_t)r]; c < cb[(size_t)r + 1]; ++c) {
+      for (int a = 0; a < nvl; ++a) {
+        const int64_t nd = cell_vnodes[c * nvl + a];
+        for (int cc = 0; cc < dim; ++cc) dofs.push_back(nd * dim + cc);
+        if (!p->sep) dofs.push_back(NVD + nd);
+      }
+      if (p->sep)
+        for (int a = 0; a < npl; ++a) dofs.push_back(NVD + cell_pnodes[c * npl + a]);
+    }
+    std::sort(dofs.begin(), dofs.end());
+    dofs.erase(std::unique(dofs.begin(), dofs.end()), dofs.end());
+    const size_t nc = dofs.size();
+    for (size_t t = 0; t < nc; ++t) {
+      const int64_t li = lidx[(size_t)dofs[t]];
+      if (li < 0) continue;
+      for (int64_t j = line_off[li]; j < line_off[li + 1]; ++j) dofs.push_back(line_masters[j]);
+    }
+    std::sort(dofs.begin(), dofs.end());
+    dofs.erase(std::unique(dofs.begin(), dofs.end()), dofs.end());
+  };
+  std::vector<int64_t> mine;
+  needed(rank, mine);
+  // local nodes: the nodes of the needed DoFs (a node's DoFs come together), owned first
+  std::vector<int64_t> vown_l, vgh_l, pown_l, pgh_l;
+  {
+    std::vector<char> vseen((size_t)NV, 0), pseen((size_t)NP, 0);
+    for (int64_t g : mine) {
+      if (g < NVD || !p->sep) {
+        const int64_t nd = g < NVD ? g / dim : g - NVD;
+        if (!vseen[(size_t)nd]) {
+          vseen[(size_t)nd] = 1;
+          (vown[(size_t)nd] == rank ? vown_l : vgh_l).push_back(nd);
+        }
+      } else {
+        const int64_t nd = g - NVD;
+        if (!pseen[(size_t)nd]) {
+          pseen[(size_t)nd] = 1;
+          (pown[(size_t)nd] == rank ? pown_l : pgh_l).push_back(nd);
+        }
+      }
+    }
+  }
+  auto order_nodes = [&](std::vector<int64_t> &own, std::vector<int64_t> &gh, const std::vector<int32_t> &ow,
+                         std::vector<int64_t> &l2g) {
+    std::sort(own.begin(), own.end());
+    std::sort(gh.begin(), gh.end(), [&](int64_t a, int64_t b) {
+      return ow[(size_t)a] != ow[(size_t)b] ? ow[(size_t)a] < ow[(size_t)b] : a < b;
+    });
+    l2g = own;
+    l2g.insert(l2g.end(), gh.begin(), gh.end());
+  };
+  order_nodes(vown_l, vgh_l, vown, p->vl2g);
+  p->n_owned_v = (int64_t)vown_l.size();
+  if (p->sep) {
+    order_nodes(pown_l, pgh_l, pown, p->pl2g);
+    p->n_owned_p = (int64_t)pown_l.size();
+  } else {
+    p->n_owned_p = p->n_owned_v;
+  }
+  const int64_t nvloc = (int64_t)p->vl2g.size();
+  std::vector<int32_t> vg2l((size_t)NV, -1), pg2l;
+  for (int64_t i = 0; i < nvloc; ++i) vg2l[(size_t)p->vl2g[(size_t)i]] = (int32_t)i;
+  if (p->sep) {
+    pg2l.assign((size_t)NP, -1);
+    for (size_t i = 0; i < p->pl2g.size(); ++i) pg2l[(size_t)p->pl2g[i]] = (int32_t)i;
+  }
+  auto g2l_dof = [&](int64_t g) -> int64_t {
+    if (g < NVD) {
+      const int32_t l = vg2l[(size_t)(g / dim)];
+      return l < 0 ? -1 : (int64_t)l * dim + g % dim;
+    }
+    const int32_t l = p->sep ? pg2l[(size_t)(g - NVD)] : vg2l[(size_t)(g - NVD)];
+    return l < 0 ? -1 : (int64_t)dim * nvloc + l;
+  };
+  // local cells
+  const int64_t ncl = p->cell_end - p->cell_begin;
+  p->local_cv.resize((size_t)(ncl * nvl));
+  for (int64_t c = 0; c < ncl; ++c)
+    for (int a = 0; a < nvl; ++a) p->local_cv[(size_t)(c * nvl + a)] = vg2l[(size_t)cell_vnodes[(p->cell_begin + c) * nvl + a]];
+  if (p->sep) {
+    p->local_cp.resize((size_t)(ncl * npl));
+    for (int64_t c = 0; c < ncl; ++c)
+      for (int a = 0; a < npl; ++a) p->local_cp[(size_t)(c * npl + a)] = pg2l[(size_t)cell_pnodes[(p->cell_begin + c) * npl + a]];
+  }
+  // global -> local DoF map of the local DoFs (sorted pairs, for gls_gpart_map_dofs)
+  {
+    const int64_t nl = p->n_local_dofs();
+    std::vector<std::pair<int64_t, int64_t>> kv;
+    kv.reserve((size_t)nl);
+    for (int64_t i = 0; i < nvloc; ++i)
+      for (int cc = 0; cc < dim; ++cc) kv.push_back({p->vl2g[(size_t)i] * dim + cc, i * dim + cc});
+    if (p->sep)
+      for (size_t i = 0; i < p->pl2g.size(); ++i) kv.push_back({NVD + p->pl2g[i], (int64_t)dim * nvloc + (int64_t)i});
+    else
+      for (int64_t i = 0; i < nvloc; ++i) kv.push_back({NVD + p->vl2g[(size_t)i], (int64_t)dim * nvloc + i});
+    std::sort(kv.begin(), kv.end());
+    for (auto &e : kv) {
+      p->gdof2l_keys.push_back(e.first);
+      p->gdof2l_vals.push_back(e.second);
+    }
+  }
+  // exchange lists: recv = my ghost DoFs by owner; send = my owned DoFs each other rank needs
+  std::map<int, std::vector<int32_t>> send, recv;
+  for (int64_t g : mine) {
+    const int32_t o = dof_owner(g);
+    if (o != rank) recv[o].push_back((int32_t)g2l_dof(g));
+  }
+  std::vector<int64_t> theirs;
+  for (int s = 0; s < world; ++s) {
+    if (s == rank) continue;
+    needed(s, theirs);
+    std::vector<int32_t> lst;
+    for (int64_t g : theirs)
+      if (dof_owner(g) == rank) lst.push_back((int32_t)g2l_dof(g));
+    if (!lst.empty()) send[s] = lst;
+  }
+  std::vector<int> nb;
+  for (auto &kv : send) nb.push_back(kv.first);
+  for (auto &kv : recv) nb.push_back(kv.first);
+  std::sort(nb.begin(), nb.end());
+  nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+  p->nbrs = nb;
+  p->send_off.assign(1, 0);
+  p->recv_off.assign(1, 0);
+  for (int r : nb) {
+    auto its = send.find(r);
+    if (its != send.end()) p->send_dofs.insert(p->send_dofs.end(), its->second.begin(), its->second.end());
+    p->send_off.push_back((int64_t)p->send_dofs.size());
+    auto itr = recv.find(r);
+    if (itr != recv.end()) p->recv_dofs.insert(p->recv_dofs.end(), itr->second.begin(), itr->second.end());
+    p->recv_off.push_back((int64_t)p->recv_dofs.size());
+  }
+  *out = p.release();
+  return GLS_OK;
+}
+
+int gls_gpart_sizes(const gls_gpart *p, int64_t *cell_begin, int64_t *cell_end, int64_t *n_vnodes, int64_t *n_pnodes,
+                    int64_t *n_owned_vnodes, int64_t *n_owned_pnodes, int *n_nbrs, int64_t *n_send, int64_t *n_recv) {
+  if (!p) return gls_internal_set_err(GLS_EINVAL, "null partition");
+  if (cell_begin) *cell_begin = p->cell_begin;
+  if (cell_end) *cell_end = p->cell_end;
+  if (n_vnodes) *n_vnodes = (int64_t)p->vl2g.size();
+  if (n_pnodes) *n_pnodes = p->sep ? (int64_t)p->pl2g.size() : (int64_t)p->vl2g.size();
+  if (n_owned_vnodes) *n_owned_vnodes = p->n_owned_v;
+  if (n_owned_pnodes) *n_owned_pnodes = p->n_owned_p;
+  if (n_nbrs) *n_nbrs = (int)p->nbrs.size();
+  if (n_send) *n_send = (int64_t)p->send_dofs.size();
+  if (n_recv) *n_recv = (int64_t)p->recv_dofs.size();
+  return GLS_OK;
+}
+
+int gls_gpart_get(const gls_gpart *p, int32_t *local_cell_vnodes, int32_t *local_cell_pnodes, int64_t *vnode_l2g,
+                  int64_t *pnode_l2g, int *nbr_ranks, int64_t *send_offsets, int32_t *send_dofs, int64_t *recv_offsets,
+                  int32_t *recv_dofs) {
+  if (!p) return gls_internal_set_err(GLS_EINVAL, "null partition");
+  if (local_cell_vnodes) std::memcpy(local_cell_vnodes, p->local_cv.data(), p->local_cv.size() * sizeof(int32_t));
+  if (local_cell_pnodes && p->sep) std::memcpy(local_cell_pnodes, p->local_cp.data(), p->local_cp.size() * sizeof(int32_t));
+  if (vnode_l2g) std::memcpy(vnode_l2g, p->vl2g.data(), p->vl2g.size() * sizeof(int64_t));
+  if (pnode_l2g) {
+    const std::vector<int64_t> &src = p->sep ? p->pl2g : p->vl2g;
+    std::memcpy(pnode_l2g, src.data(), src.size() * sizeof(int64_t));
+  }
+  if (nbr_ranks) std::memcpy(nbr_ranks, p->nbrs.data(), p->nbrs.size() * sizeof(int));
+  if (send_offsets) std::memcpy(send_offsets, p->send_off.data(), p->send_off.size() * sizeof(int64_t));
+  if (send_dofs) std::memcpy(send_dofs, p->send_dofs.data(), p->send_dofs.size() * sizeof(int32_t));
+  if (recv_offsets) std::memcpy(recv_offsets, p->recv_off.data(), p->recv_off.size() * sizeof(int64_t));
+  if (recv_dofs) std::memcpy(recv_dofs, p->recv_dofs.data(), p->recv_dofs.size() * sizeof(int32_t));
+  return GLS_OK;
+}
+
+// global DoF ids -> local DoF ids (-1: not local to this rank)
+int gls_gpart_map_dofs(const gls_gpart *p, int64_t n, const int64_t *global_dofs, int64_t *local_dofs) {
+  if (!p || n < 0 || (n > 0 && (!global_dofs || !local_dofs))) return gls_internal_set_err(GLS_EINVAL, "gls_gpart_map_dofs");
+  for (int64_t i = 0; i < n; ++i) {
+    auto it = std::lower_bound(p->gdof2l_keys.begin(), p->gdof2l_keys.end(), global_dofs[i]);
+    local_dofs[i] = (it != p->gdof2l_keys.end() && *it == global_dofs[i]) ? p->gdof2l_vals[(size_t)(it - p->gdof2l_keys.begin())] : -1;
+  }
+  return GLS_OK;
+}
+
+int gls_gpart_destroy(gls_gpart *p) {
+  delete p;
+  return GLS_OK;
+}
+
+}  // extern "C"

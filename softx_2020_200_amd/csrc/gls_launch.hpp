@@ -75,6 +75,16 @@ hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, doubl
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
                              hipStream_t s);
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s);
+// multicolor ILU triangular solves (gls_ilu_kernels.hip): y = L^-1 b, x = U^-1 y on node groups of <=
+// kMaxGroupRows rows, colors in order (forward) / reverse order (backward)
+constexpr int kMaxGroupRows = 4;
+hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
+                        const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
+                        const int32_t *didx, const double *b, double *y, double *x, hipStream_t s);
+hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
+hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
+hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                                const double *buf, hipStream_t s);
 hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh, hipStream_t s);
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();

@@ -360,6 +360,42 @@ hipError_t vec_unpack_nodes(double *x, const int32_t *nodes, int64_t m, int64_t 
   hipLaunchKernelGGL(k_unpack_nodes, dim3(grid_for(m)), dim3(kBlock), 0, s, x, nodes, m, voff, buf, add);
   return hipGetLastError();
 }
+// DoF-level ghost exchange (general meshes): buf[j] = x[dofs[j]]; x[dofs[j]] = buf[j]; and the
+// export-add x[u[i]] += sum_{j in [off[i], off[i+1])} buf[slot[j]] in a fixed (neighbour) order
+__global__ void k_pack_dofs(const double *__restrict__ x, const int32_t *__restrict__ dofs, int64_t m,
+                            double *__restrict__ buf) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
+    buf[j] = x[dofs[j]];
+}
+__global__ void k_unpack_dofs(double *__restrict__ x, const int32_t *__restrict__ dofs, int64_t m,
+                              const double *__restrict__ buf) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x)
+    x[dofs[j]] = buf[j];
+}
+__global__ void k_add_dofs_ordered(double *__restrict__ x, const int32_t *__restrict__ u, const int32_t *__restrict__ off,
+                                   const int32_t *__restrict__ slot, int64_t n, const double *__restrict__ buf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = x[u[i]];
+    for (int j = off[i]; j < off[i + 1]; ++j) s += buf[slot[j]];
+    x[u[i]] = s;
+  }
+}
+hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_dofs, dim3(grid_for(m)), dim3(kBlock), 0, s, x, dofs, m, buf);
+  return hipGetLastError();
+}
+hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unpack_dofs, dim3(grid_for(m)), dim3(kBlock), 0, s, x, dofs, m, buf);
+  return hipGetLastError();
+}
+hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                                const double *buf, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_add_dofs_ordered, dim3(grid_for(n)), dim3(kBlock), 0, s, x, u, off, slot, n, buf);
+  return hipGetLastError();
+}
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_indexed, dim3(grid_for(m)), dim3(kBlock), 0, s, y, idx, vals, m);

@@ -39,6 +39,16 @@ def _bind(L):
     L.gls_rccl_destroy.argtypes = [vp]
     L.gls_dist_attach_rccl.argtypes = [vp, vp, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int32),
                                        C.POINTER(i64), C.POINTER(C.c_int32)]
+    i32p, i64p = C.POINTER(C.c_int32), C.POINTER(i64)
+    L.gls_gpart_create.argtypes = [C.c_int, C.c_int, C.c_int, i64, i32p, i32p, i64, i64, i64, i64p, i64p, i64p, C.c_int,
+                                   C.c_int, C.POINTER(vp)]
+    L.gls_gpart_sizes.argtypes = [vp] + [i64p] * 6 + [C.POINTER(C.c_int)] + [i64p] * 2
+    L.gls_gpart_get.argtypes = [vp, i32p, i32p, i64p, i64p, C.POINTER(C.c_int), i64p, i32p, i64p, i32p]
+    L.gls_gpart_map_dofs.argtypes = [vp, i64, i64p, i64p]
+    L.gls_gpart_destroy.argtypes = [vp]
+    L.gls_dist_attach_dofs.argtypes = [vp, i64, i64, C.c_int, i64p, i32p, i64p, i32p, vp, vp, vp, EXCHANGE_FN,
+                                       ALLREDUCE_FN, vp]
+    L.gls_dist_attach_dofs_rccl.argtypes = [vp, vp, i64, i64, C.c_int, C.POINTER(C.c_int), i64p, i32p, i64p, i32p]
     L._dist_bound = True
     return L
 
@@ -80,16 +90,17 @@ def partition(cell_vnodes, n_vnodes, rank, world):
 class Exchanger:
     """Device exchange buffers + the C callbacks (torch.distributed point-to-point / all-reduce)."""
 
-    def __init__(self, plan, device, backend="nccl", group=None):
+    def __init__(self, plan, device, backend="nccl", group=None, width=4):
         import torch
         self.torch = torch
         self.dist = torch.distributed
         self.plan = plan
         self.backend = backend
         self.group = group
+        self.width = width  # doubles per exchange entry: 4 per node (brick meshes), 1 per DoF (general meshes)
         ns, nr = int(plan["send_off"][-1]), int(plan["recv_off"][-1])
-        self.send_buf = torch.zeros(max(ns, 1) * 4, dtype=torch.float64, device=device)
-        self.recv_buf = torch.zeros(max(nr, 1) * 4, dtype=torch.float64, device=device)
+        self.send_buf = torch.zeros(max(ns, 1) * width, dtype=torch.float64, device=device)
+        self.recv_buf = torch.zeros(max(nr, 1) * width, dtype=torch.float64, device=device)
         self.red_buf = torch.zeros(256, dtype=torch.float64, device=device)
         self._xchg = EXCHANGE_FN(self._exchange)
         self._allred = ALLREDUCE_FN(self._allreduce)
@@ -98,8 +109,9 @@ class Exchanger:
         p = self.plan
         sb, rb = (self.send_buf, self.recv_buf) if phase == 0 else (self.recv_buf, self.send_buf)
         so, ro = (p["send_off"], p["recv_off"]) if phase == 0 else (p["recv_off"], p["send_off"])
+        w = self.width
         for i, nbr in enumerate(p["nbrs"]):
-            yield int(nbr), sb[4 * so[i]:4 * so[i + 1]], rb[4 * ro[i]:4 * ro[i + 1]]
+            yield int(nbr), sb[w * so[i]:w * so[i + 1]], rb[w * ro[i]:w * ro[i + 1]]
 
     def _exchange(self, user, phase):
         try:
@@ -286,3 +298,126 @@ def attach_distributed_multigrid(levels, **mg_opts):
         lv.set_lattice()
     levels[0].ctx.attach_multigrid([lv.ctx for lv in levels[1:]], **mg_opts)
     levels[0]._mg_levels = levels
+
+
+
+# ---------------------------------------------------------------------------------------------------
+# General meshes (adaptive / unstructured / curved forests, row e2): DoF-level partition and exchange
+# ---------------------------------------------------------------------------------------------------
+def gpartition(space, rank, world, lines=None):
+    """gls_gpart_create on a (replicated) global mesh description: space = gls_fe_space-style dict
+    (dim, k, kp, n_cells, cell_vnodes, cell_pnodes, n_vnodes, n_pnodes); lines = global DoF-level
+    lines (dofs, offsets, masters[, weights]) or None. Returns the plan dict (local cells, node maps,
+    owned counts, DoF exchange lists) and the C handle's global -> local DoF map as a function."""
+    L = _bind(load())
+    dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])
+    cv = np.ascontiguousarray(space["cell_vnodes"], dtype=np.int32)
+    sep = kp != k
+    cp = np.ascontiguousarray(space["cell_pnodes"], dtype=np.int32) if sep else None
+    nv, npn = int(space["n_vnodes"]), int(space["n_pnodes"])
+    if lines is None or len(lines[0]) == 0:
+        ld, lo, lm = np.zeros(0, np.int64), np.zeros(1, np.int64), np.zeros(0, np.int64)
+    else:
+        ld, lo, lm = (np.ascontiguousarray(a, dtype=np.int64) for a in lines[:3])
+    p64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    p32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else C.POINTER(C.c_int32)()  # noqa: E731
+    h = C.c_void_p()
+    check(L.gls_gpart_create(dim, k, kp, cv.shape[0], p32(cv), p32(cp), nv, npn, len(ld), p64(ld), p64(lo), p64(lm),
+                             rank, world, C.byref(h)), "gls_gpart_create")
+    try:
+        cb, ce, nvl, npl, nov, nop, ns, nr = (C.c_int64() for _ in range(8))
+        nn = C.c_int()
+        check(L.gls_gpart_sizes(h, C.byref(cb), C.byref(ce), C.byref(nvl), C.byref(npl), C.byref(nov), C.byref(nop),
+                                C.byref(nn), C.byref(ns), C.byref(nr)), "gls_gpart_sizes")
+        nc = ce.value - cb.value
+        out = dict(cell_begin=cb.value, cell_end=ce.value, n_vnodes=nvl.value, n_pnodes=npl.value,
+                   n_owned_v=nov.value, n_owned_p=nop.value, dim=dim,
+                   local_cv=np.zeros((nc, cv.shape[1]), np.int32),
+                   local_cp=np.zeros((nc, cp.shape[1]), np.int32) if sep else None,
+                   vl2g=np.zeros(nvl.value, np.int64), pl2g=np.zeros(npl.value, np.int64),
+                   nbrs=np.zeros(nn.value, np.int32), send_off=np.zeros(nn.value + 1, np.int64),
+                   send_dofs=np.zeros(ns.value, np.int32), recv_off=np.zeros(nn.value + 1, np.int64),
+                   recv_dofs=np.zeros(nr.value, np.int32))
+        check(L.gls_gpart_get(h, p32(out["local_cv"]), p32(out["local_cp"]), p64(out["vl2g"]), p64(out["pl2g"]),
+                              out["nbrs"].ctypes.data_as(C.POINTER(C.c_int)), p64(out["send_off"]),
+                              p32(out["send_dofs"]), p64(out["recv_off"]), p32(out["recv_dofs"])), "gls_gpart_get")
+        if nn.value == 0:
+            out["send_off"] = np.zeros(1, np.int64)
+            out["recv_off"] = np.zeros(1, np.int64)
+        if not sep:
+            out["local_cp"] = out["local_cv"]
+        # global DoF ids of the local DoFs (velocity node*dim + c, pressure dim*NV + p)
+        g = np.concatenate([(out["vl2g"][:, None] * dim + np.arange(dim)[None, :]).reshape(-1), dim * nv + out["pl2g"]])
+        out["l2g_dofs"] = g
+        out["n_global_dofs"] = dim * nv + npn
+        return out
+    finally:
+        L.gls_gpart_destroy(h)
+
+
+def owned_dofs(plan):
+    """(local ids, global ids) of the rank's owned DoFs (velocity of owned nodes, pressure of owned nodes)"""
+    d = plan["dim"]
+    nvl = plan["n_vnodes"]
+    loc = np.concatenate([np.arange(d * plan["n_owned_v"]), d * nvl + np.arange(plan["n_owned_p"])])
+    return loc, plan["l2g_dofs"][loc]
+
+
+def attach_dofs(ctx: GLSContext, plan, exchanger: Exchanger):
+    L = _bind(load())
+    p = plan
+    p64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    p32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))  # noqa: E731
+    check(L.gls_dist_attach_dofs(ctx.h, int(p["n_owned_v"]), int(p["n_owned_p"]), len(p["nbrs"]), p64(p["send_off"]),
+                                 p32(p["send_dofs"]), p64(p["recv_off"]), p32(p["recv_dofs"]),
+                                 C.c_void_p(exchanger.send_buf.data_ptr()), C.c_void_p(exchanger.recv_buf.data_ptr()),
+                                 C.c_void_p(exchanger.red_buf.data_ptr()), exchanger._xchg, exchanger._allred, None),
+          "gls_dist_attach_dofs")
+    ctx._exchanger = exchanger
+    ctx._plan = plan
+
+
+class DistributedGeneralProblem:
+    """Rank-local GLS context on a general (mapped, adapted) mesh: the rank's cells of the global
+    space, Dirichlet rows and hanging lines mapped to local DoFs, DoF-level ghost exchange through
+    torch.distributed (gloo / nccl callbacks)."""
+
+    def __init__(self, space, rank, world, device, viscosity=1.0, vnode_mask=None, dirichlet=None, lines=None,
+                 backend="gloo", group=None, qmapping=True, force_q=None):
+        plan = gpartition(space, rank, world, lines)
+        self.plan = plan
+        cb, ce = plan["cell_begin"], plan["cell_end"]
+        dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])
+        lmask = np.ascontiguousarray(vnode_mask[plan["vl2g"]]) if vnode_mask is not None else None
+        self.ctx = GLSContext(dim, k, kp, plan["local_cv"], plan["local_cp"] if kp != k else None, None,
+                              plan["n_vnodes"], plan["n_pnodes"], viscosity=viscosity, vnode_mask=lmask,
+                              map_degree=k, cell_support=np.ascontiguousarray(space["cell_support"][cb:ce]),
+                              force_q=None if force_q is None else np.ascontiguousarray(force_q[cb:ce]))
+        g2l = np.full(plan["n_global_dofs"], -1, np.int64)
+        g2l[plan["l2g_dofs"]] = np.arange(len(plan["l2g_dofs"]))
+        self.g2l = g2l
+        if lines is not None and len(lines[0]):
+            ld, lo, lm, lw = (np.asarray(a) for a in lines)
+            keep = np.nonzero(g2l[ld] >= 0)[0]
+            dofs, offs, mas, ws = [], [0], [], []
+            for i in keep:
+                m = g2l[lm[lo[i]:lo[i + 1]]]
+                if (m < 0).any():
+                    raise GLSError("line master not local on rank %d" % rank)
+                dofs.append(g2l[ld[i]])
+                mas.extend(m.tolist())
+                ws.extend(lw[lo[i]:lo[i + 1]].tolist())
+                offs.append(len(mas))
+            if dofs:
+                self.ctx.set_hanging(np.array(dofs, np.int64), np.array(offs, np.int64), np.array(mas, np.int64),
+                                     np.array(ws))
+        if dirichlet is not None:
+            gd, gv = (np.asarray(a) for a in dirichlet)
+            ld_ = g2l[gd]
+            sel = ld_ >= 0
+            self.ctx.set_dirichlet(ld_[sel], gv[sel])
+        self.exchanger = Exchanger(plan, device, backend=backend, group=group, width=1)
+        attach_dofs(self.ctx, plan, self.exchanger)
+
+    def local(self, global_vec):
+        return np.ascontiguousarray(np.asarray(global_vec)[self.plan["l2g_dofs"]])

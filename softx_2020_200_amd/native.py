@@ -31,7 +31,7 @@ EXPORTS = [
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy",
     "gls_dist_attach_rccl",
-    "gls_mg_attach", "gls_mg_detach", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
+    "gls_mg_attach", "gls_mg_detach", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -738,9 +738,14 @@ class GLSContext:
         check(self.L.gls_mg_detach(self.h), "gls_mg_detach")
         self._mg_levels = None
 
-    def attach_ilu(self, athresh=1e-8, rthresh=1.0, fill=0):
+    def attach_ilu(self, athresh=1e-8, rthresh=1.0, fill=0, block_dofs=0, ordering="cm"):
         """Assembled ILU(fill) preconditioner (the reference's ILU-preconditioned GMRES, setup_ILU); the
-        Jacobian is probed from the device operator. Returns (nnz of the ILU pattern, n_probes)."""
+        Jacobian is probed from the device operator; ordering "cm" (the reference's Cuthill-McKee) or
+        "multicolor"; block_dofs > 0: block-Jacobi subdomains of that size (gls_ilu_set_options).
+        Returns (nnz of the ILU pattern, n_probes)."""
+        self.L.gls_ilu_set_options.argtypes = [C.c_void_p, C.c_int, C.c_int64]
+        check(self.L.gls_ilu_set_options(self.h, {"cm": 0, "multicolor": 1}[ordering], int(block_dofs)),
+              "gls_ilu_set_options")
         self.L.gls_ilu_attach.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double]
         check(self.L.gls_ilu_attach(self.h, int(fill), float(athresh), float(rthresh)), "gls_ilu_attach")
         nnz, npr = C.c_int64(), C.c_int()

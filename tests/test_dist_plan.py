@@ -146,3 +146,62 @@ def test_distributed_residual_equals_global_gloo(world):
         pr.join(timeout=60)
     for rank, err in res:
         assert err < 1e-13, (rank, err)
+
+
+# ---- general meshes (row e2): gls_gpart_* on adapted mapped meshes with hanging-node lines
+def _adapted_space(dim, k, kp):
+    from tests.test_uforest import make_mesh, random_adapt
+    spec = dict(grid=("hyper_shell", "0, 0 : 0.25 : 1 : 6 : true")) if dim == 2 else \
+        dict(grid=("cylinder_shell", "1 : 0.25 : 1 : 8 : 2"))
+    m = make_mesh(dim, spec)
+    m.refine_global(1)
+    random_adapt(m, 2 if dim == 2 else 1, seed=5, k=k)
+    return m.fe_space(k, kp, qmapping_all=True)
+
+
+@pytest.mark.parametrize("dim,k,kp", [(2, 2, 1), (2, 1, 1), (3, 2, 1)])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_general_partition_covers_and_closes(dim, k, kp, world):
+    """Every global DoF is owned by exactly one rank; each rank's local DoFs hold its cells' DoFs and
+    the masters of every hanging line on them; a rank's send list to a neighbour equals (as global
+    DoFs, in order) the neighbour's receive list from it, and receives only ghost DoFs."""
+    from softx_2020_200_amd.dist import gpartition, owned_dofs
+    from tests.test_gpu_uforest import dof_lines
+    sp = _adapted_space(dim, k, kp)
+    lines = dof_lines(sp)
+    assert len(lines[0]) > 0
+    plans = [gpartition(sp, r, world, lines) for r in range(world)]
+    ndof = plans[0]["n_global_dofs"]
+    owned = np.concatenate([owned_dofs(p)[1] for p in plans])
+    assert np.array_equal(np.sort(owned), np.arange(ndof))
+    ld, lo, lm = (np.asarray(a) for a in lines[:3])
+    line_of = {int(d): i for i, d in enumerate(ld)}
+    for r, p in enumerate(plans):
+        loc = set(p["l2g_dofs"].tolist())
+        cells = range(p["cell_begin"], p["cell_end"])
+        nvg = sp["n_vnodes"]
+        for c in cells:
+            for nd in sp["cell_vnodes"][c]:
+                for cc in range(dim):
+                    g = int(nd) * dim + cc
+                    assert g in loc
+                    if g in line_of:
+                        i = line_of[g]
+                        assert set(lm[lo[i]:lo[i + 1]].tolist()) <= loc, (r, g)
+            for pn in (sp["cell_pnodes"][c] if kp != k else sp["cell_vnodes"][c]):
+                assert dim * nvg + int(pn) in loc
+        # local cell maps agree with the global ones
+        lv = p["vl2g"][p["local_cv"]]
+        assert np.array_equal(lv, sp["cell_vnodes"][p["cell_begin"]:p["cell_end"]])
+        # owned-first numbering
+        n_own = p["n_owned_v"]
+        assert np.all(np.diff(p["vl2g"][:n_own]) > 0)
+    for a, pa in enumerate(plans):
+        for i, b in enumerate(pa["nbrs"]):
+            pb = plans[int(b)]
+            j = list(pb["nbrs"]).index(a)
+            sent = pa["l2g_dofs"][pa["send_dofs"][pa["send_off"][i]:pa["send_off"][i + 1]]]
+            got = pb["l2g_dofs"][pb["recv_dofs"][pb["recv_off"][j]:pb["recv_off"][j + 1]]]
+            assert np.array_equal(sent, got), (a, int(b))
+            own_b = set(owned_dofs(pb)[1].tolist())
+            assert not (set(got.tolist()) & own_b)

@@ -1,0 +1,95 @@
+"""Row e2 (multi-GPU on adaptive / unstructured forests) through the C-ABI: an adapted, curved
+(MappingQ2) cylinder_shell Q2-Q1 mesh with hanging-node lines partitioned over 2 / 4 ranks on the
+box's one GPU (gls_gpart_* + gls_dist_attach_dofs, DoF-level ghost exchange through
+torch.distributed gloo). The distributed residual, Jacobian action and Jacobian diagonal equal the
+single-rank operators at 1e-12 on the owned DoFs, and a Newton solve (Jacobi-GMRES) reaches the
+single-rank solution (reference: the p::d triangulation partition and Trilinos ghosted vectors,
+navier_stokes_base.cc:55-60, gls_navier_stokes.cc:186-202, 774-776)."""
+import os
+
+import numpy as np
+import pytest
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from oracle.oracle import MappedProblem
+    from softx_2020_200_amd.dist import DistributedGeneralProblem, owned_dofs
+    from tests.gpu_util import context_for, vnode_mask_of
+    from tests.test_dist_plan import _adapted_space
+    from tests.test_gpu_uforest import continuous_field, dof_lines
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sp = _adapted_space(3, 2, 1)
+        lines = dof_lines(sp)
+        p = MappedProblem(sp, viscosity=0.2, scheme="bdf2", time_steps=(0.1, 0.12, 0.1, 0.1))
+        p.set_hanging(*lines)
+        p.hang_lines = lines
+        rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)
+        p.set_dirichlet([("function", 0, rot), ("noslip", 1, None)])
+        cu = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device="cuda")
+        rng = np.random.default_rng(20200200 + 11)
+        u, u1, u2, v = (continuous_field(sp, rng) for _ in range(4))
+        u = p.apply_nonzero_constraints(u)
+        g = context_for(p)
+        g.set_time("bdf2", p.time_steps)
+        g.set_state(cu(u), cu(u1), cu(u2))
+        r_g = g.residual().cpu().numpy()
+        jv_g = g.jacobian_apply(cu(v)).cpu().numpy()
+        d_g = g.jacobian_diagonal().cpu().numpy()
+        dirs = np.array(sorted(p.dirichlet), np.int64)
+        dp = DistributedGeneralProblem(sp, rank, world, "cuda", viscosity=0.2, vnode_mask=vnode_mask_of(p),
+                                       dirichlet=(dirs, np.array([p.dirichlet[d] for d in dirs])), lines=lines)
+        c = dp.ctx
+        c.set_time("bdf2", p.time_steps)
+        c.set_state(cu(dp.local(u)), cu(dp.local(u1)), cu(dp.local(u2)))
+        loc, glo = owned_dofs(dp.plan)
+        rel = lambda a, b: float(np.abs(a - b).max() / np.abs(b).max())
+        errs = {"res": rel(c.residual().cpu().numpy()[loc], r_g[glo]),
+                "jv": rel(c.jacobian_apply(cu(dp.local(v))).cpu().numpy()[loc], jv_g[glo]),
+                "diag": rel(c.jacobian_diagonal().cpu().numpy()[loc], d_g[glo]),
+                "n_owned": len(loc), "n_ghost_recv": int(dp.plan["recv_off"][-1])}
+        # one BDF2 time step by Newton with Jacobi-GMRES to a tight tolerance
+        kw = dict(tolerance=1e-10, max_iterations=8, lin_max_iterations=20000, restart=200, relative_residual=1e-11,
+                  minimum_residual=1e-14)
+        x0 = p.apply_nonzero_constraints(u1.copy())
+        xg = cu(x0)
+        stg = g.newton(xg, cu(u1), cu(u2), **kw)
+        xd = cu(dp.local(x0))
+        std = c.newton(xd, cu(dp.local(u1)), cu(dp.local(u2)), **kw)
+        xgn, xdn = xg.cpu().numpy(), xd.cpu().numpy()
+        vel = glo < 3 * sp["n_vnodes"]
+        errs["newton_u"] = float(np.abs(xdn[loc][vel] - xgn[glo][vel]).max() / np.abs(xgn[:3 * sp["n_vnodes"]]).max())
+        errs["newton_res"] = (stg["final_residual"], std["final_residual"])
+        q.put((rank, errs))
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_adapted_mapped_mesh_across_ranks_matches_single_rank(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32300 + 10 * world + os.getpid() % 400
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, e in res:
+        assert "error" not in e, e
+        assert e["n_ghost_recv"] > 0, e
+        assert e["res"] < 1e-12 and e["jv"] < 1e-12 and e["diag"] < 1e-12, (rank, e)
+        assert e["newton_res"][0] < 1e-10 and e["newton_res"][1] < 1e-10, (rank, e)
+        assert e["newton_u"] < 1e-8, (rank, e)

@@ -62,9 +62,11 @@ def test_ilu_gmres_newton(dim, n, k, kp):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,n,k,kp,fill,rthresh", [(2, 4, 1, 1, 0, 1.0), (2, 4, 1, 1, 1, 1.0), (2, 4, 1, 1, 4, 1.02),
-                                                     (2, 3, 2, 1, 1, 1.0), (3, 2, 1, 1, 1, 1.0), (3, 2, 2, 2, 2, 1.0)])
-def test_iluk_factors_match_oracle(dim, n, k, kp, fill, rthresh):
+@pytest.mark.parametrize("dim,n,k,kp,fill,rthresh,order,blk", [
+    (2, 4, 1, 1, 0, 1.0, "cm", 0), (2, 4, 1, 1, 1, 1.0, "cm", 0), (2, 4, 1, 1, 4, 1.02, "cm", 0),
+    (2, 3, 2, 1, 1, 1.0, "cm", 0), (3, 2, 1, 1, 1, 1.0, "cm", 0), (3, 2, 2, 2, 2, 1.0, "cm", 0),
+    (2, 4, 2, 1, 0, 1.0, "multicolor", 0), (3, 2, 2, 2, 0, 1.0, "multicolor", 200), (2, 6, 1, 1, 1, 1.0, "cm", 40)])
+def test_iluk_factors_match_oracle(dim, n, k, kp, fill, rthresh, order, blk):
     """ILU(fill) factors computed on the device (probe -> level-of-fill pattern -> Ifpack diagonal
     perturbation -> rocSPARSE csrilu0) equal the oracle's Ifpack restatement (ilu_factor) of the
     oracle's assembled matrix in the factorization's numbering, on the device's pattern; that pattern
@@ -77,13 +79,19 @@ def test_iluk_factors_match_oracle(dim, n, k, kp, fill, rthresh):
     ctx.set_time("bdf1", p.time_steps)
     ctx.set_state(cuda(u), cuda(u1))
     athresh = 1e-5
-    ctx.attach_ilu(athresh, rthresh, fill=fill)
+    ctx.attach_ilu(athresh, rthresh, fill=fill, ordering=order, block_dofs=blk)
     perm, F = ctx.ilu_factors()
     A = A.tocoo()
     B = sp.csr_matrix((A.data, (perm[A.row], perm[A.col])), shape=A.shape)
     B.eliminate_zeros()
     F = F.tocsr()
     pattern = [(i, int(j)) for i in range(F.shape[0]) for j in F.indices[F.indptr[i]:F.indptr[i + 1]]]
+    if blk:  # block-Jacobi: the couplings between subdomains are dropped before the factorisation
+        S = set(pattern)
+        B = B.tocoo()
+        keep = np.array([(int(i), int(j)) in S for i, j in zip(B.row, B.col)], dtype=bool)
+        assert (~keep).any()
+        B = sp.csr_matrix((B.data[keep], (B.row[keep], B.col[keep])), shape=B.shape)
     assert set(iluk_levels(B, fill)) <= set(pattern)
     ref = ilu_factor(B, pattern, athresh=athresh, rthresh=rthresh)
     got = {(i, int(j)): v for i in range(F.shape[0]) for j, v in zip(F.indices[F.indptr[i]:F.indptr[i + 1]],
@@ -119,3 +127,32 @@ def test_ilu_fill_out_of_range_fails_loudly():
     for bad in (-1, 11):
         with pytest.raises(Exception, match="fill"):
             ctx.attach_ilu(1e-8, 1.0, fill=bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,n,k,kp,order,blk", [(2, 6, 2, 1, "multicolor", 0), (3, 3, 2, 2, "multicolor", 0),
+                                                  (3, 3, 2, 1, "multicolor", 500), (2, 6, 1, 1, "cm", 100)])
+def test_ilu_apply_is_the_factored_solve(dim, n, k, kp, order, blk):
+    """gls_apply_preconditioner with the ILU attached (multicolor: the color-by-color solves of
+    gls_ilu_kernels.hip; Cuthill-McKee: rocSPARSE csrsv) equals P^T U^-1 L^-1 P v computed from the
+    returned factors by scipy's triangular solves."""
+    import scipy.sparse.linalg as spla
+    p = _cavity(dim, n, k, kp, "bdf1", 0.05)
+    rng = np.random.default_rng(SEED + 3)
+    u, u1 = (p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs)) for _ in range(2))
+    ctx = context_for(p)
+    ctx.set_time("bdf1", p.time_steps)
+    ctx.set_state(cuda(u), cuda(u1))
+    ctx.attach_ilu(1e-5, 1.0, fill=0, ordering=order, block_dofs=blk)
+    v = rng.uniform(-1, 1, p.n_dofs)
+    z = ctx.apply_preconditioner(cuda(v)).cpu().numpy()
+    perm, F = ctx.ilu_factors()
+    F = F.tocsr()
+    L = (sp.tril(F, -1) + sp.identity(F.shape[0])).tocsr()
+    U = sp.triu(F).tocsr()
+    pv = np.zeros_like(v)
+    pv[perm] = v
+    y = spla.spsolve_triangular(L, pv, lower=True)
+    x = spla.spsolve_triangular(U, y, lower=False)
+    zref = x[perm]
+    assert np.abs(z - zref).max() <= 1e-10 * np.abs(zref).max(), np.abs(z - zref).max()

@@ -266,3 +266,22 @@ def test_kelly_faces_match_box_oracle(dim, k, kp):
         ref = kelly_estimate_boxes(sp, nodal, variable)
         got = _numpy_kelly(sp, faces, nodal, variable, dim)
         assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), variable
+
+
+@pytest.mark.parametrize("name,dim,spec,flat", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("k,kp", [(2, 1)])
+def test_vectorised_kelly_equals_loop_restatement(name, dim, spec, flat, k, kp):
+    """oracle.kelly_from_face_pieces (used by the app pipeline tests on larger meshes) equals the
+    plain-loop evaluation of the same face pieces on adapted meshes, for velocity and pressure."""
+    from oracle.oracle import kelly_from_face_pieces
+    m = make_mesh(dim, spec)
+    m.refine_global(1)
+    random_adapt(m, 1, seed=3, k=k)
+    h = m.fe_space_handle(k, kp, qmapping_all=True)
+    sp = h.data
+    faces = h.kelly_faces(k + 2)
+    x = np.random.default_rng(9).uniform(-1, 1, dim * sp["n_vnodes"] + sp["n_pnodes"])
+    for variable in (0, 1):
+        a = kelly_from_face_pieces(sp, faces, x, variable)
+        b = _numpy_kelly(sp, faces, x, variable, dim)
+        assert np.abs(a - b).max() <= 1e-12 * np.abs(b).max(), variable
