@@ -1089,16 +1089,17 @@ static int csr_find(const int *col, int b, int e, int j) {
   return b;
 }
 static void csr_spmv(int n, const int *rp, const int *ci, const double *v, const double *x, double *y) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (n >= (1 << 15))
   for (int i = 0; i < n; ++i) {
     double s = 0.;
     for (int e = rp[i]; e < rp[i + 1]; ++e) s += v[e] * x[ci[e]];
     y[i] = s;
   }
 }
+#define PAR_N (1 << 20) /* vector operations below this length run on one thread (team start-up costs more) */
 static double vdot(int n, const double *a, const double *b) {
   double s = 0.;
-#pragma omp parallel for reduction(+ : s) schedule(static)
+#pragma omp parallel for reduction(+ : s) schedule(static) if (n >= PAR_N)
   for (int i = 0; i < n; ++i) s += a[i] * b[i];
   return s;
 }
@@ -1260,7 +1261,7 @@ int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *
   memset(dx, 0, sizeof(double) * (size_t)N);
   memcpy(w, rhs, sizeof(double) * (size_t)N);
   while (beta > tol && its < max_its) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
     for (int i = 0; i < N; ++i) V[i] = w[i] / beta;
     for (int i = 0; i <= m; ++i) g[i] = 0.;
     g[0] = beta;
@@ -1273,13 +1274,13 @@ int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *
         const double *vi = V + (size_t)i * N;
         const double h = vdot(N, vn, vi);
         H[(size_t)i * m + j] = h;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
         for (int q = 0; q < N; ++q) vn[q] -= h * vi[q];
       }
       const double hn = sqrt(vdot(N, vn, vn));
       H[(size_t)(j + 1) * m + j] = hn;
       if (hn > 0) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
         for (int q = 0; q < N; ++q) vn[q] /= hn;
       }
       for (int i = 0; i < j; ++i) {
@@ -1304,11 +1305,11 @@ int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *
     }
     for (int i = 0; i < j; ++i) {
       const double *zi = Z + (size_t)i * N;
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
       for (int q = 0; q < N; ++q) dx[q] += yv[i] * zi[q];
     }
     csr_spmv(N, rp, ci, val, dx, w);  /* true residual at the restart */
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
     for (int q = 0; q < N; ++q) w[q] = rhs[q] - w[q];
     beta = sqrt(vdot(N, w, w));
   }
@@ -1318,7 +1319,7 @@ int gls_oracle_newton_csr(const gls_oracle_problem *p, double *x, const double *
   t0 = omp_get_wtime();
   double res = res0;
   for (double alpha = 1.0; alpha > 1e-3; alpha *= 0.5) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (N >= PAR_N)
     for (int q = 0; q < N; ++q) xt[q] = x[q] + (p->constrained[q] ? 0. : alpha * dx[q]);
     assemble_csr(p, xt, u1, u2, u3, rp, ci, dg, NULL, rhs, 0);
     ++st->line_search_rhs;

@@ -1543,7 +1543,7 @@ int gls_jacobian_diagonal(gls_ctx *c, double *d) {
 int gls_jacobian_apply(gls_ctx *c, const double *v, double *y) {
   GLS_TRY(check_ctx(c));
   if (!v || !y || v == y) return set_err(GLS_EINVAL, "v/y null or aliased");
-  if (c->con_dofs.n) GLS_TRY(ensure_diag(c));
+  if (c->con_dofs.n || c->dist.on) GLS_TRY(ensure_diag(c));  // (collective across ranks: on every rank)
   GLS_TRY(run_cell(c, gls::MODE_JV, v, y));
   HIP_TRY(gls::vec_gather_scale_set(y, c->diag.p, v, c->con_dofs.p, (int64_t)c->con_dofs.n, c->stream));
   return GLS_OK;
@@ -1673,12 +1673,12 @@ int gls_set_dirichlet(gls_ctx *c, int64_t n, const int64_t *dofs, const double *
 int gls_apply_dirichlet(gls_ctx *c, double *x) {
   GLS_TRY(check_ctx(c));
   HIP_TRY(gls::vec_set_indexed(x, c->dir_dofs.p, c->dir_vals.p, (int64_t)c->dir_dofs.n, c->stream));
-  if (c->hang.on) {  // hanging values from their masters (all masters: Dirichlet values included)
-    // across ranks the masters may be ghosts: their owners' values first
-    if (c->dist.on) GLS_TRY(dist_import(c, x));
+  // across ranks the masters of the lines below may be ghosts: their owners' values first (on every
+  // rank, whether or not it holds lines: the exchange is collective)
+  if (c->dist.on && c->dist.dofs) GLS_TRY(dist_import(c, x));
+  if (c->hang.on)  // hanging values from their masters (all masters: Dirichlet values included)
     HIP_TRY(gls::vec_csr_gather_set(x, x, c->hang.dof.p, c->hang.off.p, c->hang.master.p, c->hang.w.p,
                                     (int64_t)c->hang.dof.n, c->stream));
-  }
   if (!c->jf.on && (x == c->u || x == c->u1 || x == c->u2 || x == c->u3)) {  // the captured state changed
     c->diag_valid = false;
     c->ilu.valid = false;

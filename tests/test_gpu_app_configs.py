@@ -64,7 +64,7 @@ def run_app(tmp_path, prm_text, files=(), extra=()):
     if not os.path.exists(app):
         pytest.fail("apps/gls_navier_stokes_3d is not built (run __graft_entry__.build())")
     r = subprocess.run([app, "--stats", *extra, "--dump", str(dump), "case.prm"], cwd=str(tmp_path), capture_output=True,
-                       text=True, timeout=600)
+                       text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout, read_dumps(str(dump))
 
