@@ -31,6 +31,7 @@
 #include <fstream>
 #include <iomanip>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -478,14 +479,18 @@ unsigned face_normals(const Mesh &m, const double *x, bool colorize, int id) {
 }
 
 // Dirichlet data of the noslip / function / slip boundary conditions at the velocity support
-// points; a component already set by an earlier bc keeps its value (deal.II's first-constraint
-// rule). slip = VectorTools::compute_no_normal_flux_constraints (gls_navier_stokes.cc:100-110,
-// 149-160) on the box's axis-aligned faces: n.u = 0 constrains the normal component(s) to 0
-// (every face normal of this boundary at edges / corners).
+// points; a DoF already constrained by an earlier bc keeps its constraint (deal.II's first-constraint
+// rule, per DoF: a slip line takes u_cmax only, later bcs still set the node's other components).
+// slip = VectorTools::compute_no_normal_flux_constraints (gls_navier_stokes.cc:100-110, 149-160): on
+// axis-aligned faces n.u = 0 constrains the normal component(s) to 0 (every face normal of this
+// boundary at edges / corners); on curved walls it is the line u_cmax = -sum (n_d / n_cmax) u_d,
+// added unless u_cmax is already constrained (masters that end up Dirichlet drop out of the closed
+// operator lines, gls_set_hanging; a line whose master is itself a slip line is skipped, which
+// keeps the lines free of cycles).
 Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   Constraints C;
   C.mask.assign((size_t)m.nv, 0);
-  std::vector<uint8_t> lined((size_t)m.nv, 0);  // nodes constrained by a slip line (first constraint wins)
+  std::vector<uint8_t> lined((size_t)(m.nv * m.dim), 0);  // DoFs constrained by a slip line
   std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
   for (const BC &b : P.bcs) {
     if (b.type == "periodic") continue;
@@ -516,13 +521,16 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
             if (nc > 1 - 1e-12) ax |= 1u << c;
             else if (nc > 1e-12) axis = false;
           }
-          if (!axis) {  // curved wall: a constraint line (unless the node is already constrained)
+          if (!axis) {  // curved wall: a constraint line on u_cmax (unless that DoF is already constrained)
             ax = 0;
-            if (!C.mask[(size_t)v] && !lined[(size_t)v]) {
-              const double *n = &(*sn)[(size_t)(v * m.dim)];
-              int cmax = 0;
-              for (int c = 1; c < m.dim; ++c)
-                if (std::fabs(n[c]) > std::fabs(n[cmax])) cmax = c;
+            const double *n = &(*sn)[(size_t)(v * m.dim)];
+            int cmax = 0;
+            for (int c = 1; c < m.dim; ++c)
+              if (std::fabs(n[c]) > std::fabs(n[cmax])) cmax = c;
+            bool free_line = !((C.mask[(size_t)v] >> cmax) & 1u) && !lined[(size_t)(v * m.dim + cmax)];
+            for (int d = 0; d < m.dim; ++d)
+              if (d != cmax && std::fabs(n[d]) > 1e-14 && lined[(size_t)(v * m.dim + d)]) free_line = false;
+            if (free_line) {
               C.line_dofs.push_back(v * m.dim + cmax);
               for (int d = 0; d < m.dim; ++d)
                 if (d != cmax && std::fabs(n[d]) > 1e-14) {
@@ -530,7 +538,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
                   C.line_w.push_back(-n[d] / n[cmax]);
                 }
               C.line_off.push_back((int64_t)C.line_master.size());
-              lined[(size_t)v] = 1;
+              lined[(size_t)(v * m.dim + cmax)] = 1;
             }
           }
           nrm.push_back(ax);
@@ -546,7 +554,7 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       for (int c = 0; c < m.dim; ++c) {
         uint8_t &mk = C.mask[(size_t)sel[s]];
         if (mk & (1u << c)) continue;
-        if (lined[(size_t)sel[s]]) continue;  // slip line first: the node keeps it
+        if (lined[(size_t)(sel[s] * m.dim + c)]) continue;  // slip line first: the DoF keeps it
         if (b.type == "slip" && !((nrm[s] >> c) & 1u)) continue;
         mk |= (uint8_t)(1u << c);
         val[(size_t)(sel[s] * m.dim + c)] = b.type == "function" ? fv[c][s * (size_t)b.f[c].nc] : 0.0;
@@ -559,6 +567,49 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
         C.vals.push_back(val[(size_t)(v * m.dim + c)]);
       }
   return C;
+}
+
+// AffineConstraints::close() for the homogeneous lines: a master that is itself a constrained line
+// (a hanging node's master vertex on a curved slip wall, whose u_cmax carries the slip line) is
+// replaced by that line's masters with the weights multiplied; repeated masters are merged. Lines
+// are acyclic (make_constraints), so the substitution ends after at most #lines rounds.
+void close_lines(std::vector<int64_t> &ld, std::vector<int64_t> &lo, std::vector<int64_t> &lm,
+                 std::vector<double> &lw) {
+  std::unordered_map<int64_t, size_t> line_of;
+  for (size_t i = 0; i < ld.size(); ++i) line_of[ld[i]] = i;
+  bool chained = false;
+  for (int64_t mj : lm) chained = chained || line_of.count(mj);
+  if (!chained) return;
+  std::vector<int64_t> no{0}, nm;
+  std::vector<double> nw;
+  for (size_t i = 0; i < ld.size(); ++i) {
+    std::vector<std::pair<int64_t, double>> row, next;
+    for (int64_t j = lo[i]; j < lo[i + 1]; ++j) row.emplace_back(lm[(size_t)j], lw[(size_t)j]);
+    for (size_t round = 0;; ++round) {
+      if (round > ld.size()) die("constraint lines: a cycle through DoF %lld", (long long)ld[i]);
+      bool again = false;
+      next.clear();
+      for (auto [mj, w] : row) {
+        auto it = line_of.find(mj);
+        if (it == line_of.end()) { next.emplace_back(mj, w); continue; }
+        again = true;
+        const size_t l = it->second;
+        for (int64_t j = lo[l]; j < lo[l + 1]; ++j) next.emplace_back(lm[(size_t)j], w * lw[(size_t)j]);
+      }
+      row.swap(next);
+      if (!again) break;
+    }
+    std::map<int64_t, double> merged;
+    for (auto [mj, w] : row) merged[mj] += w;
+    for (auto [mj, w] : merged) {
+      nm.push_back(mj);
+      nw.push_back(w);
+    }
+    no.push_back((int64_t)nm.size());
+  }
+  lo.swap(no);
+  lm.swap(nm);
+  lw.swap(nw);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1369,6 +1420,7 @@ struct Solver {
       }
       lo.push_back((int64_t)lm.size());
     }
+    close_lines(ld, lo, lm, lw);
     if (world > 1) {  // the rank's cells; its lines in local DoF ids (masters are local by construction)
       ctx = make_context_local(m, C, ld, lo, lm);
       std::vector<int64_t> ld2, lo2{0}, lm2;

@@ -401,3 +401,23 @@ def test_app_slip_on_curved_wall_rigid_rotation(tmp_path):
     assert rows[0][1] < 1e-2 and rows[1][1] < rows[0][1] / 4, rows  # Q2 velocity: ~h^3 on curved cells
     rows_ns = table(run_app(tmp_path, SHELL_ROTATION_PRM.replace("{outer}", "noslip"), 2))
     assert rows_ns[-1][1] > 10 * rows[-1][1], (rows, rows_ns)
+
+
+@pytest.mark.gpu
+def test_app_slip_on_curved_wall_kelly_hanging_chains(tmp_path):
+    """Kelly adaptation next to a curved slip wall: a hanging node on the outer circle has master
+    vertices whose u_cmax carries the slip line, so the hanging line's masters are themselves
+    constrained; the app closes the chain (AffineConstraints::close(): the slip line's masters
+    substituted with the weights multiplied) instead of aborting. Two Kelly cycles of the rigid
+    rotation case above (fixed fraction 0.4 of the cells refined, so the refined region ends on the
+    wall): it runs and the error against the analytic profile stays at the uniform runs' level and
+    falls. Parity unpinned (no reference case uses slip on a curved wall); checked against the
+    analytic solution."""
+    prm = (SHELL_ROTATION_PRM.replace("{outer}", "slip").replace("number mesh adapt = 1", "number mesh adapt = 2")
+           .replace("set type = uniform", "set type = kelly\n  set fraction type = number\n"
+                    "  set fraction refinement = 0.4\n  set fraction coarsening = 0.0\n  set variable = velocity"))
+    rows = table(run_app(tmp_path, prm, 2))
+    assert len(rows) == 3, rows
+    assert rows[0][1] < 1e-2 and rows[-1][1] < rows[0][1], rows
+    # not uniform: the adapted meshes have fewer cells than 4^cycles x the initial mesh
+    assert int(rows[-1][0]) < 16 * int(rows[0][0]), rows
