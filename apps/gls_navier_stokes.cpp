@@ -800,6 +800,8 @@ struct ShmComm {
   struct Header {
     std::atomic<int> count, gen, abort;
     unsigned char rccl_id[GLS_RCCL_ID_BYTES];
+    int64_t nbar[kMaxRanks];   // barriers entered per rank and the tag of the last one (watchdog report)
+    char tag[kMaxRanks][24];
     int64_t table[kMaxRanks][kMaxRanks][2];  // exchange mailbox: (start, count) of rank s's data for rank d
   };
   static constexpr size_t kSlot = (size_t)1 << 26;  // doubles per rank slot (virtual, NORESERVE)
@@ -822,31 +824,47 @@ struct ShmComm {
     glob = slots + (size_t)w * kSlot;
   }
   double *slot(int r) const { return slots + (size_t)r * kSlot; }
-  void barrier() const {  // sense-reversing; a rank that failed raises abort
+  // sense-reversing; a rank that failed raises abort. Watchdog: a rank left waiting longer than
+  // GLS_NP_WATCHDOG seconds (default 60) reports every rank's barrier count and last tag -- ranks
+  // that disagree name the collective one of them skipped -- and aborts the run.
+  void barrier(const char *tag = "") const {
+    ++hdr->nbar[rank];
+    std::snprintf(hdr->tag[rank], sizeof(hdr->tag[rank]), "%s", tag);
     const int g = hdr->gen.load();
     if (hdr->count.fetch_add(1) == world - 1) {
       hdr->count.store(0);
       hdr->gen.fetch_add(1);
       return;
     }
-    while (hdr->gen.load() == g) {
+    static const double limit = std::getenv("GLS_NP_WATCHDOG") ? std::atof(std::getenv("GLS_NP_WATCHDOG")) : 60.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0; hdr->gen.load() == g; ++spin) {
       if (hdr->abort.load()) _exit(3);
       sched_yield();
+      if ((spin & 4095) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+        std::fprintf(stderr, "--np watchdog: rank %d waited %.0f s at barrier #%lld (%s); ranks:", rank, limit,
+                     (long long)hdr->nbar[rank], tag);
+        for (int r = 0; r < world; ++r) std::fprintf(stderr, " [%d] #%lld %s", r, (long long)hdr->nbar[r], hdr->tag[r]);
+        std::fprintf(stderr, "\n");
+        hdr->abort.store(1);
+        _exit(3);
+      }
     }
   }
   // every rank writes values[i] at global position idx[i]; all receive the whole vector
   void allgather(const double *values, const std::vector<int64_t> &idx, std::vector<double> &out) const {
     if ((size_t)out.size() > kGlob) die("--np: global vector of %zu values exceeds the shared area", out.size());
     for (size_t i = 0; i < idx.size(); ++i) glob[idx[i]] = values[i];
-    barrier();
+    barrier("allgather");
     std::memcpy(out.data(), glob, out.size() * sizeof(double));
-    barrier();
+    barrier("allgather-done");
   }
   void bcast(std::vector<double> &v, int root) const {  // v sized alike on every rank
     if (rank == root) std::memcpy(glob, v.data(), v.size() * sizeof(double));
-    barrier();
+    barrier("bcast");
     if (rank != root) std::memcpy(v.data(), glob, v.size() * sizeof(double));
-    barrier();
+    barrier("bcast-done");
   }
 };
 ShmComm g_comm;
@@ -874,7 +892,7 @@ struct ShmExchange {
       C.hdr->table[C.rank][x->nbrs[i]][0] = so[i];
       C.hdr->table[C.rank][x->nbrs[i]][1] = so[i + 1] - so[i];
     }
-    C.barrier();
+    C.barrier(phase == 0 ? "import" : "export-add");
     for (size_t i = 0; i < x->nbrs.size(); ++i) {
       const int s = x->nbrs[i];
       const int64_t start = C.hdr->table[s][C.rank][0], cnt = C.hdr->table[s][C.rank][1];
@@ -882,7 +900,7 @@ struct ShmExchange {
       if (cnt && hipMemcpy(dst + ro[i], C.slot(s) + start, sizeof(double) * (size_t)cnt, hipMemcpyHostToDevice) != hipSuccess)
         return -1;
     }
-    C.barrier();
+    C.barrier(phase == 0 ? "import-done" : "export-add-done");
     return 0;
   }
   static int allreduce(void *user, double *dev, int n) {
@@ -890,11 +908,11 @@ struct ShmExchange {
     const ShmComm &C = g_comm;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpy(C.slot(C.rank), dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    C.barrier();
+    C.barrier("allreduce");
     x->tmp.assign((size_t)n, 0.0);
     for (int r = 0; r < C.world; ++r)  // rank order: the same sum on every rank
       for (int i = 0; i < n; ++i) x->tmp[(size_t)i] += C.slot(r)[i];
-    C.barrier();
+    C.barrier("allreduce-done");
     return hipMemcpy(dev, x->tmp.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
   }
 };
@@ -973,6 +991,8 @@ struct Solver {
   int64_t ndev() const { return world > 1 ? (int64_t)loc.l2g.size() : m.n_dofs(); }
   Mesh m;
   Constraints C;
+  std::vector<std::vector<int64_t>> g_lines;  // the current mesh's global constraint lines (dofs, offsets, masters)
+  std::vector<double> g_lines_w;
   gls_ctx *ctx = nullptr;
   gls_refined_mesh *rmesh = nullptr;  // the adapted mesh m was built from (kelly; gls_octree_mesh)
   gls_octree *tree = nullptr;         // kelly: the forest p4est keeps (created at the first adaptation)
@@ -1421,6 +1441,8 @@ struct Solver {
       lo.push_back((int64_t)lm.size());
     }
     close_lines(ld, lo, lm, lw);
+    g_lines = {ld, lo, lm};
+    g_lines_w = lw;
     if (world > 1) {  // the rank's cells; its lines in local DoF ids (masters are local by construction)
       ctx = make_context_local(m, C, ld, lo, lm);
       std::vector<int64_t> ld2, lo2{0}, lm2;
@@ -1578,6 +1600,65 @@ struct Solver {
     }
   }
 
+  // --np diagnostics (GLS_NP_CHECK): the gathered distributed residual at the current state against
+  // the residual of a whole-mesh context on rank 0; the largest differences are printed to stderr
+  void check_distributed_residual(const double ts[4]) {
+    const int64_t N = m.n_dofs(), nd = ndev();
+    double *d_r = nullptr;
+    hk(hipMalloc(&d_r, sizeof(double) * (size_t)nd), "hipMalloc");
+    ck(gls_set_state(ctx, d_present, d_m1, d_m2, d_m3), "gls_set_state");
+    ck(gls_residual(ctx, d_r), "gls_residual");
+    hk(hipDeviceSynchronize(), "residual");
+    std::vector<double> rd((size_t)N), x((size_t)N), h1((size_t)N), h2((size_t)N), h3((size_t)N);
+    download(d_r, rd);
+    download(d_present, x);
+    download(d_m1, h1);
+    download(d_m2, h2);
+    download(d_m3, h3);
+    (void)hipFree(d_r);
+    if (rank != 0) return;
+    gls_ctx *g = make_context(m, C);
+    if (!g_lines[0].empty())
+      ck(gls_set_hanging(g, (int64_t)g_lines[0].size(), g_lines[0].data(), g_lines[1].data(), g_lines[2].data(),
+                         g_lines_w.data()),
+         "gls_set_hanging");
+    ck(gls_set_time(g, last_scheme, ts), "gls_set_time");
+    double *dv[5];
+    for (double *&q : dv) hk(hipMalloc(&q, sizeof(double) * (size_t)N), "hipMalloc");
+    const std::vector<double> *hv[4] = {&x, &h1, &h2, &h3};
+    for (int i = 0; i < 4; ++i) hk(hipMemcpy(dv[i], hv[i]->data(), sizeof(double) * (size_t)N, hipMemcpyHostToDevice), "upload");
+    ck(gls_set_state(g, dv[0], dv[1], dv[2], dv[3]), "gls_set_state");
+    ck(gls_residual(g, dv[4]), "gls_residual");
+    std::vector<double> rg((size_t)N);
+    hk(hipMemcpy(rg.data(), dv[4], sizeof(double) * (size_t)N, hipMemcpyDeviceToHost), "download");
+    for (double *q : dv) (void)hipFree(q);
+    gls_destroy(g);
+    std::vector<int64_t> idx((size_t)N);
+    double nr = 0, nd2 = 0, ps = 0, psg = 0;
+    const int64_t nvd = (int64_t)m.dim * m.nv;
+    for (int64_t i = 0; i < N; ++i) {
+      idx[(size_t)i] = i;
+      nr += rg[(size_t)i] * rg[(size_t)i];
+      nd2 += (rd[(size_t)i] - rg[(size_t)i]) * (rd[(size_t)i] - rg[(size_t)i]);
+      if (i >= nvd) { ps += rd[(size_t)i]; psg += rg[(size_t)i]; }
+    }
+    std::partial_sort(idx.begin(), idx.begin() + std::min<int64_t>(N, 8), idx.end(), [&](int64_t a, int64_t b) {
+      return std::fabs(rd[(size_t)a] - rg[(size_t)a]) > std::fabs(rd[(size_t)b] - rg[(size_t)b]);
+    });
+    std::fprintf(stderr, "np-check: |r| %.6e |r_dist - r| %.6e  sum r_p: dist %.6e whole %.6e\n", std::sqrt(nr),
+                 std::sqrt(nd2), ps, psg);
+    std::vector<char> isline((size_t)N, 0);
+    for (int64_t d : g_lines[0]) isline[(size_t)d] = 1;
+    for (int t = 0; t < std::min<int64_t>(N, 8); ++t) {
+      const int64_t i = idx[(size_t)t];
+      const bool vel = i < nvd;
+      const int64_t node = vel ? i / m.dim : i - nvd;
+      std::fprintf(stderr, "  dof %lld (%s node %lld%s%s) dist %.6e whole %.6e\n", (long long)i, vel ? "u" : "p",
+                   (long long)node, isline[(size_t)i] ? ", line" : "",
+                   vel && ((C.mask[(size_t)node] >> (i % m.dim)) & 1) ? ", dirichlet" : "", rd[(size_t)i], rg[(size_t)i]);
+    }
+  }
+
   // ---- one nonlinear solve of `scheme` from the current present solution and history
   // solve_non_linear_system(method, first_iteration = false, force_matrix_renewal)
   void solve_nonlinear(int scheme, double nu_override = -1.0, bool force_renewal = false) {
@@ -1589,6 +1670,7 @@ struct Solver {
     if (nu_override > 0) ck(gls_set_viscosity(ctx, nu_override), "gls_set_viscosity");
     need_dev();
     ck(gls_apply_dirichlet(ctx, d_present), "gls_apply_dirichlet");
+    if (world > 1 && std::getenv("GLS_NP_CHECK")) check_distributed_residual(ts);
     gls_newton_params np;
     std::memset(&np, 0, sizeof(np));
     np.tolerance = P.newton_tol;
@@ -2281,6 +2363,7 @@ int main(int argc, char **argv) {
   }
   if (dim == 0) dim = 3;
   if (dim != 2 && dim != 3) die("--dim must be 2 or 3");
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // progress visible in a log while the run goes on
   Prm prm(file);
   Params P = read_params(prm, dim);
   // --np N: N ranks forked here, before any GPU call (the children's stdout is discarded: rank 0
@@ -2314,7 +2397,7 @@ int main(int argc, char **argv) {
     hk(hipSetDevice(rank % std::max(ndev, 1)), "hipSetDevice");
     if (ndev >= np_ranks && !std::getenv("GLS_NP_SHM")) {  // one GPU per rank: RCCL over xGMI
       if (rank == 0) ck(gls_rccl_unique_id(g_comm.hdr->rccl_id), "gls_rccl_unique_id");
-      g_comm.barrier();
+      g_comm.barrier("rccl-id");
       ck(gls_rccl_create(g_comm.hdr->rccl_id, rank, np_ranks, &s.rccl), "gls_rccl_create");
     }
   }
@@ -2325,7 +2408,7 @@ int main(int argc, char **argv) {
   if (dump) s.dump_dir = dump;
   s.run();
   if (np_ranks > 1) {
-    g_comm.barrier();
+    g_comm.barrier("end");
     s.release();
     if (s.rccl) gls_rccl_destroy(s.rccl);
     if (rank != 0) {

@@ -3295,7 +3295,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   int64_t ncm = 0;
   for (int64_t x = 0; x < nv; ++x) cmnode[(size_t)x] = ncm++;
   if (sep)
-    for (int64_t pn = 0; pn < np; ++pn) cmnode[(size_t)(nv + pn)] = p_map ? cmnode[(size_t)p_at[(size_t)pn]] : ncm++;
+    for (int64_t pn = 0; pn < np; ++pn)  // (a ghost pressure node in no local cell -- a line master only -- is its own node)
+      cmnode[(size_t)(nv + pn)] = p_map && p_at[(size_t)pn] >= 0 ? cmnode[(size_t)p_at[(size_t)pn]] : ncm++;
   std::vector<int64_t> cm_doff((size_t)ncm + 1, 0), cm_dofs((size_t)n);
   for (int64_t x = 0; x < nu; ++x) {
     int64_t d[4];
@@ -3340,6 +3341,11 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int64_t> order;
   gls::cuthill_mckee_nodes(ncm, cadj_off, cadj, cm_doff, cm_dofs, order);
   if ((int64_t)order.size() != n) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering covers %lld of %lld DoFs", (long long)order.size(), (long long)n);
+  {
+    std::vector<char> seen((size_t)n, 0);
+    for (int64_t d : order)
+      if (d < 0 || d >= n || seen[(size_t)d]++) return set_err(GLS_EINVAL, "gls_ilu_attach: renumbering is not a permutation");
+  }
   // subdomains (Ifpack's additive Schwarz with overlap 0, which the reference runs with one block per
   // MPI rank): contiguous ranges of the cell order (space-filling: leaf order of the forest / Morton
   // bricks), a DoF in the block of its lowest cell; couplings between blocks are dropped, each block

@@ -63,10 +63,15 @@ def run_app(tmp_path, prm_text, files=(), extra=()):
     app = os.path.join(ROOT, "apps", "gls_navier_stokes_3d")
     if not os.path.exists(app):
         pytest.fail("apps/gls_navier_stokes_3d is not built (run __graft_entry__.build())")
-    r = subprocess.run([app, "--stats", *extra, "--dump", str(dump), "case.prm"], cwd=str(tmp_path), capture_output=True,
-                       text=True, timeout=170)
-    assert r.returncode == 0, r.stderr[-3000:]
-    return r.stdout, read_dumps(str(dump))
+    fo, fe = tmp_path / "stdout.txt", tmp_path / "stderr.txt"
+    with open(fo, "w") as o, open(fe, "w") as e:
+        try:  # the app line-buffers stdout: a run cut off at the limit still shows how far it got
+            r = subprocess.run([app, "--stats", *extra, "--dump", str(dump), "case.prm"], cwd=str(tmp_path), stdout=o,
+                               stderr=e, timeout=float(os.environ.get("GLS_APP_TIMEOUT", "170")))
+        except subprocess.TimeoutExpired:
+            pytest.fail("app timed out; stdout tail:\n%s\nstderr tail:\n%s" % (fo.read_text()[-3000:], fe.read_text()[-2000:]))
+    assert r.returncode == 0, fe.read_text()[-3000:] + "\nstdout tail:\n" + fo.read_text()[-2000:]
+    return fo.read_text(), read_dumps(str(dump))
 
 
 def setprm(text, key, value):

@@ -93,3 +93,79 @@ def test_adapted_mapped_mesh_across_ranks_matches_single_rank(world):
         assert e["res"] < 1e-12 and e["jv"] < 1e-12 and e["diag"] < 1e-12, (rank, e)
         assert e["newton_res"][0] < 1e-10 and e["newton_res"][1] < 1e-10, (rank, e)
         assert e["newton_u"] < 1e-8, (rank, e)
+
+
+def _worker_enclosed(rank, world, port, q, precond):
+    """configs[3]'s constraint set on the adapted shell (inner wall rotating, outer noslip, slip end
+    caps: an enclosed flow, pressure fixed only up to a constant), steady Newton across ranks with
+    the rank-local ILU (additive Schwarz, overlap 0) or Jacobi."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from oracle.oracle import MappedProblem
+    from softx_2020_200_amd.dist import DistributedGeneralProblem, owned_dofs
+    from tests.gpu_util import context_for, vnode_mask_of
+    from tests.test_dist_plan import _adapted_space
+    from tests.test_gpu_uforest import dof_lines
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sp = _adapted_space(3, 2, 1)
+        lines = dof_lines(sp)
+        p = MappedProblem(sp, viscosity=1.0, scheme="steady")
+        p.set_hanging(*lines)
+        p.hang_lines = lines
+        rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)
+        p.set_dirichlet([("function", 0, rot), ("noslip", 1, None), ("slip", 2, None), ("slip", 3, None)])
+        cu = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device="cuda")
+        kw = dict(tolerance=1e-8, max_iterations=8, lin_max_iterations=3000, restart=100, relative_residual=1e-10,
+                  minimum_residual=1e-13)
+        x0 = p.apply_nonzero_constraints(np.zeros(p.n_dofs))
+        out = {}
+        if world == 1 or rank == 0:
+            g = context_for(p)
+            if precond == "ilu":
+                g.attach_ilu(1e-12, 1.0)
+            xg = cu(x0)
+            out["single"] = g.newton(xg, **kw)
+        dirs = np.array(sorted(p.dirichlet), np.int64)
+        dp = DistributedGeneralProblem(sp, rank, world, "cuda", viscosity=1.0, vnode_mask=vnode_mask_of(p),
+                                       dirichlet=(dirs, np.array([p.dirichlet[d] for d in dirs])), lines=lines)
+        c = dp.ctx
+        c.set_time("steady")
+        if precond == "ilu":
+            c.attach_ilu(1e-12, 1.0)
+        xd = cu(dp.local(x0))
+        out["dist"] = c.newton(xd, **kw)
+        q.put((rank, out))
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precond", ["ilu", "jacobi"])
+def test_enclosed_steady_flow_with_hanging_lines_across_ranks(precond):
+    """The enclosed steady flow (configs[3]'s constraints) on the adapted shell converges across 4
+    ranks as on one: the distributed residual keeps the single-rank problem's compatibility (no
+    residual floor from the pressure null space)."""
+    import torch.multiprocessing as mp
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32500 + (11 if precond == "ilu" else 23) + os.getpid() % 400
+    procs = [ctx.Process(target=_worker_enclosed, args=(r, world, port, q, precond)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=400) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, e in res.items():
+        assert "error" not in e, (rank, e)
+    print(res[0])
+    assert res[0]["single"]["final_residual"] < 1e-8, res[0]
+    assert res[0]["dist"]["final_residual"] < 1e-8, res[0]
