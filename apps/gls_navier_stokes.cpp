@@ -1609,8 +1609,21 @@ struct Solver {
     ck(gls_set_state(ctx, d_present, d_m1, d_m2, d_m3), "gls_set_state");
     ck(gls_residual(ctx, d_r), "gls_residual");
     hk(hipDeviceSynchronize(), "residual");
-    std::vector<double> rd((size_t)N), x((size_t)N), h1((size_t)N), h2((size_t)N), h3((size_t)N);
+    std::vector<double> rd((size_t)N), x((size_t)N), h1((size_t)N), h2((size_t)N), h3((size_t)N), vv((size_t)N),
+        jd((size_t)N);
     download(d_r, rd);
+    for (int64_t i = 0; i < N; ++i) vv[(size_t)i] = std::sin(0.37 * (double)i + 0.1) + 0.5 * std::cos(1.3 * (double)i);
+    {
+      double *d_v = nullptr, *d_j = nullptr;
+      hk(hipMalloc(&d_v, sizeof(double) * (size_t)nd), "hipMalloc");
+      hk(hipMalloc(&d_j, sizeof(double) * (size_t)nd), "hipMalloc");
+      upload(vv, d_v);
+      ck(gls_jacobian_apply(ctx, d_v, d_j), "gls_jacobian_apply");
+      hk(hipDeviceSynchronize(), "jv");
+      download(d_j, jd);
+      (void)hipFree(d_v);
+      (void)hipFree(d_j);
+    }
     download(d_present, x);
     download(d_m1, h1);
     download(d_m2, h2);
@@ -1623,14 +1636,31 @@ struct Solver {
                          g_lines_w.data()),
          "gls_set_hanging");
     ck(gls_set_time(g, last_scheme, ts), "gls_set_time");
-    double *dv[5];
+    double *dv[6];
     for (double *&q : dv) hk(hipMalloc(&q, sizeof(double) * (size_t)N), "hipMalloc");
     const std::vector<double> *hv[4] = {&x, &h1, &h2, &h3};
     for (int i = 0; i < 4; ++i) hk(hipMemcpy(dv[i], hv[i]->data(), sizeof(double) * (size_t)N, hipMemcpyHostToDevice), "upload");
     ck(gls_set_state(g, dv[0], dv[1], dv[2], dv[3]), "gls_set_state");
     ck(gls_residual(g, dv[4]), "gls_residual");
-    std::vector<double> rg((size_t)N);
+    hk(hipDeviceSynchronize(), "residual");
+    std::vector<double> rg((size_t)N), jg((size_t)N);
     hk(hipMemcpy(rg.data(), dv[4], sizeof(double) * (size_t)N, hipMemcpyDeviceToHost), "download");
+    hk(hipMemcpy(dv[5], vv.data(), sizeof(double) * (size_t)N, hipMemcpyHostToDevice), "upload");
+    ck(gls_jacobian_apply(g, dv[5], dv[4]), "gls_jacobian_apply");
+    hk(hipDeviceSynchronize(), "jv");
+    hk(hipMemcpy(jg.data(), dv[4], sizeof(double) * (size_t)N, hipMemcpyDeviceToHost), "download");
+    {
+      double dj = 0, nj = 0;
+      int64_t worst = 0;
+      for (int64_t i = 0; i < N; ++i) {
+        nj += jg[(size_t)i] * jg[(size_t)i];
+        const double e = std::fabs(jd[(size_t)i] - jg[(size_t)i]);
+        dj += e * e;
+        if (e > std::fabs(jd[(size_t)worst] - jg[(size_t)worst])) worst = i;
+      }
+      std::fprintf(stderr, "np-check: |Jv| %.6e |Jv_dist - Jv| %.6e worst dof %lld dist %.6e whole %.6e\n", std::sqrt(nj),
+                   std::sqrt(dj), (long long)worst, jd[(size_t)worst], jg[(size_t)worst]);
+    }
     for (double *q : dv) (void)hipFree(q);
     gls_destroy(g);
     std::vector<int64_t> idx((size_t)N);
@@ -1681,11 +1711,12 @@ struct Solver {
     // TrilinosWrappers::SolverGMRES default) and iteration cap, unless --precond jacobi. Jacobi is much
     // weaker than the reference's preconditioners, so its caps and restart are raised.
     if (mg_levels.empty() && use_ilu && ilu_ctx != ctx) {
-      // ordering: Cuthill-McKee as the reference factors; above kIluMulticolorDofs the multicolor
-      // order, whose triangular solves are ~60x faster on the GPU (profiles/r03_ilu_multicolor_ab.txt)
-      // at the price of more GMRES iterations (--ilu-order overrides)
+      // ordering: Cuthill-McKee as the reference factors; above kIluMulticolorDofs, and across ranks
+      // (where the block-Jacobi ILU does not reproduce the single-rank iteration counts anyway), the
+      // multicolor order, whose triangular solves are ~60x faster on the GPU
+      // (profiles/r03_ilu_multicolor_ab.txt) at the price of more GMRES iterations (--ilu-order overrides)
       const int order = ilu_order >= 0 ? ilu_order
-                        : (m.n_dofs() > kIluMulticolorDofs ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM);
+                        : (m.n_dofs() > kIluMulticolorDofs || world > 1 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM);
       ck(gls_ilu_set_options(ctx, order, ilu_block_dofs), "gls_ilu_set_options");
       ck(gls_ilu_attach(ctx, P.ilu_fill, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;

@@ -345,6 +345,8 @@ struct gls_ctx {
     ncclComm_t comm = nullptr;
     std::vector<int> nbrs;
     std::vector<int64_t> soff, roff;
+    std::vector<int32_t> h_send, h_recv;  // host copies of the DoF exchange lists (gls_dist_attach_dofs)
+    std::vector<int64_t> h_soff, h_roff;
     DevBuf<double> own_send, own_recv, own_red;
     // overlap of the J.v ghost import with the interior bricks (RCCL transport): exchange stream
     hipStream_t xstream = nullptr;
@@ -371,6 +373,13 @@ struct gls_ctx {
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
     DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
     DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
+    // across ranks, complete owned rows: the neighbours' cell contributions to the owned x owned block
+    // arrive per probe round through the export exchange (n_rounds = the largest probe count of any
+    // rank); round p adds send_buf slots into CSR entries ru[rr[p] .. rr[p+1]) in a fixed order
+    bool complete = false;
+    int n_rounds = 0;
+    std::vector<int64_t> rr;
+    DevBuf<int32_t> ru, ruoff, rslot;
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
     DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
@@ -1503,6 +1512,14 @@ int gls_dist_attach_dofs(gls_ctx *c, int64_t n_owned_vnodes, int64_t n_owned_pno
   auto &D = c->dist;
   GLS_TRY(D.send_nodes.upload(send_dofs, (size_t)ns));
   GLS_TRY(D.recv_nodes.upload(recv_dofs, (size_t)nr));
+  D.h_send.assign(send_dofs, send_dofs + ns);
+  D.h_recv.assign(recv_dofs, recv_dofs + nr);
+  D.h_soff.assign(1, 0);
+  D.h_roff.assign(1, 0);
+  if (n_nbrs > 0) {
+    D.h_soff.assign(send_offsets, send_offsets + n_nbrs + 1);
+    D.h_roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);
+  }
   GLS_TRY(D.add_u.upload(au.data(), au.size()));
   GLS_TRY(D.add_off.upload(aoff.data(), au.empty() ? 0 : aoff.size()));
   GLS_TRY(D.add_slot.upload(aslot.data(), aslot.size()));
@@ -2131,14 +2148,30 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
   const int64_t n = c->n_dofs;
   hipStream_t s = c->stream;
   if (I.fill > 0 || c->dist.on) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
-  c->probe_local = c->dist.on;  // owned block: the probe's J.v skips the ghost exchange (ghost v = 0)
-  for (int p = 0; p < I.n_probes; ++p) {
-    HIP_TRY(gls::vec_fill(I.vbuf.p, n, 0.0, s));
-    HIP_TRY(gls::vec_set_const_indexed(I.vbuf.p, I.pdofs.p + I.pdoff[(size_t)p], I.pdoff[(size_t)p + 1] - I.pdoff[(size_t)p],
-                                       1.0, s));
-    GLS_TRY(gls_jacobian_apply(c, I.vbuf.p, I.ybuf.p));
-    HIP_TRY(gls::csr_probe_extract(I.val.p, I.pent.p + I.peoff[(size_t)p], I.prow.p + I.peoff[(size_t)p],
-                                   I.peoff[(size_t)p + 1] - I.peoff[(size_t)p], I.ybuf.p, s));
+  // across ranks the constrained rows' diagonal is the exchanged one: computed before the local probes
+  if (c->dist.on && (c->con_dofs.n || I.complete)) GLS_TRY(ensure_diag(c));
+  c->probe_local = c->dist.on;  // the probe's J.v: the rank's cells only, no ghost exchange
+  auto &D = c->dist;
+  const int rounds = I.complete ? I.n_rounds : I.n_probes;
+  for (int p = 0; p < rounds; ++p) {
+    if (p < I.n_probes) {
+      HIP_TRY(gls::vec_fill(I.vbuf.p, n, 0.0, s));
+      HIP_TRY(gls::vec_set_const_indexed(I.vbuf.p, I.pdofs.p + I.pdoff[(size_t)p],
+                                         I.pdoff[(size_t)p + 1] - I.pdoff[(size_t)p], 1.0, s));
+      GLS_TRY(gls_jacobian_apply(c, I.vbuf.p, I.ybuf.p));
+      HIP_TRY(gls::csr_probe_extract(I.val.p, I.pent.p + I.peoff[(size_t)p], I.prow.p + I.peoff[(size_t)p],
+                                     I.peoff[(size_t)p + 1] - I.peoff[(size_t)p], I.ybuf.p, s, c->dist.on));
+    }
+    if (!I.complete) continue;
+    // ghost rows of this probe (the local cells' part of a neighbour's owned rows) to their owners
+    if (p < I.n_probes) HIP_TRY(gls::vec_pack_dofs(I.ybuf.p, D.recv_nodes.p, D.n_recv, D.recv_buf, s));
+    else if (D.n_recv) HIP_TRY(gls::vec_fill(D.recv_buf, D.n_recv, 0.0, s));
+    if (D.xchg(D.user, 1) != 0) {
+      c->probe_local = false;
+      return set_err(GLS_ECOMM, "ILU probe exchange failed");
+    }
+    const int64_t a = I.rr[(size_t)p], b = I.rr[(size_t)p + 1];
+    if (b > a) HIP_TRY(gls::vec_add_dofs_ordered(I.val.p, I.ru.p + a, I.ruoff.p + a, I.rslot.p, b - a, D.send_buf, s));
   }
   c->probe_local = false;
   if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
@@ -3172,6 +3205,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     if (!c->dist.on) return false;
     return d < nvd ? d / dim >= c->dist.n_owned : d - nvd >= c->dist.n_owned_p;
   };
+  const std::vector<char> fcons = cons;  // constrained DoFs before the ghosts join them (complete rows)
   for (int64_t d = 0; d < n; ++d)
     if (ghost(d)) cons[(size_t)d] = 1;
   auto dirichlet = [&](int64_t d) { return (cons[(size_t)d] && !isline[(size_t)d]) || ghost(d); };
@@ -3272,6 +3306,185 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     while (col < (int)mark.size() && mark[(size_t)col] == (int)x) ++col;
     color[(size_t)x] = col;
     ncol = std::max(ncol, col + 1);
+  }
+  // Across ranks, complete owned rows (the rows of Ifpack's distributed matrix, restricted to the owned
+  // columns as its additive Schwarz with overlap 0 does): the owned x owned block also receives the
+  // neighbours' cells. Every rank probes its cells' operator on ALL its DoFs (owned and ghost) with a
+  // distance-2 coloring of that full local pattern; the ghost rows of each probe go to their owners
+  // through the export exchange, tagged once (here) with the column as its position in the owner's
+  // send list. Probe rounds run to the largest probe count of any rank (collective).
+  std::vector<char> aown;  // per system-matrix entry: probed on this rank (else a neighbour's entry only)
+  struct RemoteEntry {
+    int32_t round, slot;
+    int64_t i, j;
+  };
+  std::vector<RemoteEntry> remote;
+  int n_rounds = 0;
+  const bool cmpl = c->dist.on && c->dist.dofs && std::getenv("GLS_ILU_LOCAL_ROWS") == nullptr;
+  if (cmpl) {
+    auto fdir = [&](int64_t d) { return fcons[(size_t)d] && !isline[(size_t)d]; };
+    std::vector<int64_t> feoff((size_t)nc + 1, 0), feff, buf;
+    for (int64_t e = 0; e < nc; ++e) {
+      buf.clear();
+      for (int a = 0; a < ncn; ++a) {
+        int64_t d[4];
+        int sl[4];
+        const int m = node_dofs(cell_node(e, a), d, sl);
+        for (int j = 0; j < m; ++j) {
+          const int64_t li = lidx[(size_t)d[j]];
+          if (li >= 0) {
+            for (int64_t t = c->hang.h_off[(size_t)li]; t < c->hang.h_off[(size_t)li + 1]; ++t)
+              if (!fdir(c->hang.h_master[(size_t)t])) buf.push_back(c->hang.h_master[(size_t)t]);
+          } else if (!fcons[(size_t)d[j]]) {
+            buf.push_back(d[j]);
+          }
+        }
+      }
+      std::sort(buf.begin(), buf.end());
+      buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+      feff.insert(feff.end(), buf.begin(), buf.end());
+      feoff[(size_t)e + 1] = (int64_t)feff.size();
+    }
+    std::vector<int64_t> fdoff((size_t)n + 1, 0), fdcell;
+    for (int64_t d : feff) ++fdoff[(size_t)d + 1];
+    for (int64_t i = 0; i < n; ++i) fdoff[(size_t)i + 1] += fdoff[(size_t)i];
+    fdcell.resize((size_t)fdoff[(size_t)n]);
+    {
+      std::vector<int64_t> f(fdoff.begin(), fdoff.end() - 1);
+      for (int64_t e = 0; e < nc; ++e)
+        for (int64_t t = feoff[(size_t)e]; t < feoff[(size_t)e + 1]; ++t) fdcell[(size_t)f[(size_t)feff[(size_t)t]]++] = e;
+    }
+    std::vector<int64_t> faoff((size_t)n + 1, 0), facol;
+    {
+      std::vector<int64_t> stamp((size_t)n, -1);
+      for (int64_t i = 0; i < n; ++i) {
+        buf.clear();
+        buf.push_back(i);
+        stamp[(size_t)i] = i;
+        if (!fcons[(size_t)i])
+          for (int64_t t = fdoff[(size_t)i]; t < fdoff[(size_t)i + 1]; ++t) {
+            const int64_t e = fdcell[(size_t)t];
+            for (int64_t u = feoff[(size_t)e]; u < feoff[(size_t)e + 1]; ++u) {
+              const int64_t j = feff[(size_t)u];
+              if (stamp[(size_t)j] != i) { stamp[(size_t)j] = i; buf.push_back(j); }
+            }
+          }
+        std::sort(buf.begin(), buf.end());
+        facol.insert(facol.end(), buf.begin(), buf.end());
+        faoff[(size_t)i + 1] = (int64_t)facol.size();
+      }
+    }
+    // distance-2 coloring of the full pattern's node graph (replaces the owned-block coloring)
+    std::vector<int64_t> g1off((size_t)nu + 1, 0), g1;
+    {
+      std::vector<int64_t> stamp((size_t)nu, -1);
+      for (int64_t x = 0; x < nu; ++x) {
+        buf.clear();
+        buf.push_back(x);
+        stamp[(size_t)x] = x;
+        int64_t d[4];
+        int sl[4];
+        const int m = node_dofs(x, d, sl);
+        for (int j = 0; j < m; ++j)
+          for (int64_t t = faoff[(size_t)d[j]]; t < faoff[(size_t)d[j] + 1]; ++t) {
+            const int64_t y = unode(facol[(size_t)t]);
+            if (stamp[(size_t)y] != x) { stamp[(size_t)y] = x; buf.push_back(y); }
+          }
+        std::sort(buf.begin(), buf.end());
+        g1.insert(g1.end(), buf.begin(), buf.end());
+        g1off[(size_t)x + 1] = (int64_t)g1.size();
+      }
+    }
+    std::fill(color.begin(), color.end(), -1);
+    mark.clear();
+    ncol = 0;
+    for (int64_t x = 0; x < nu; ++x) {
+      for (int64_t t = g1off[(size_t)x]; t < g1off[(size_t)x + 1]; ++t) {
+        const int64_t z = g1[(size_t)t];
+        for (int64_t u = g1off[(size_t)z]; u < g1off[(size_t)z + 1]; ++u) {
+          const int cy = color[(size_t)g1[(size_t)u]];
+          if (cy >= 0) {
+            if ((int)mark.size() <= cy) mark.resize((size_t)cy + 1, -1);
+            mark[(size_t)cy] = (int)x;
+          }
+        }
+      }
+      int col = 0;
+      while (col < (int)mark.size() && mark[(size_t)col] == (int)x) ++col;
+      color[(size_t)x] = col;
+      ncol = std::max(ncol, col + 1);
+    }
+    auto pof = [&](int64_t d) { return color[(size_t)unode(d)] * (dim + 1) + (d < nvd ? (int)(d % dim) : dim); };
+    const int nprobe_local = ncol * (dim + 1);
+    // the column tags: per round, each ghost row's probed column as its position in the owner's list
+    auto &D = c->dist;
+    const int nn = (int)D.h_soff.size() - 1;
+    const int64_t ns = D.n_send, nr = D.n_recv;
+    std::vector<int32_t> gnb((size_t)n, -1), gk((size_t)n, -1);
+    for (int t = 0; t < nn; ++t)
+      for (int64_t q = D.h_roff[(size_t)t]; q < D.h_roff[(size_t)t + 1]; ++q) {
+        gnb[(size_t)D.h_recv[(size_t)q]] = t;
+        gk[(size_t)D.h_recv[(size_t)q]] = (int32_t)(q - D.h_roff[(size_t)t]);
+      }
+    std::vector<double> hpos((size_t)std::max<int64_t>(nr, 1)), hin((size_t)std::max<int64_t>(ns, 1));
+    for (int p = 0;; ++p) {
+      double flag = p < nprobe_local ? 1.0 : 0.0;
+      HIP_TRY(hipMemcpy(D.red_buf, &flag, sizeof(double), hipMemcpyHostToDevice));
+      if (D.allreduce(D.user, D.red_buf, 1) != 0) return set_err(GLS_ECOMM, "gls_ilu_attach: allreduce failed");
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipMemcpy(&flag, D.red_buf, sizeof(double), hipMemcpyDeviceToHost));
+      if (flag == 0.0) break;
+      ++n_rounds;
+      for (int64_t q = 0; q < nr; ++q) {
+        const int64_t i = D.h_recv[(size_t)q];
+        double pos = -1.0;
+        if (p < nprobe_local && !fcons[(size_t)i])
+          for (int64_t t = faoff[(size_t)i]; t < faoff[(size_t)i + 1]; ++t) {
+            const int64_t j = facol[(size_t)t];
+            if (pof(j) != p) continue;
+            if (gnb[(size_t)j] == gnb[(size_t)i]) pos = (double)gk[(size_t)j];
+            break;
+          }
+        hpos[(size_t)q] = pos;
+      }
+      if (nr) HIP_TRY(hipMemcpy(D.recv_buf, hpos.data(), sizeof(double) * (size_t)nr, hipMemcpyHostToDevice));
+      HIP_TRY(hipDeviceSynchronize());
+      if (D.xchg(D.user, 1) != 0) return set_err(GLS_ECOMM, "gls_ilu_attach: exchange failed");
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (ns) HIP_TRY(hipMemcpy(hin.data(), D.send_buf, sizeof(double) * (size_t)ns, hipMemcpyDeviceToHost));
+      for (int t = 0; t < nn; ++t)
+        for (int64_t q = D.h_soff[(size_t)t]; q < D.h_soff[(size_t)t + 1]; ++q) {
+          const int64_t pos = (int64_t)hin[(size_t)q];
+          if (pos < 0) continue;
+          if (pos >= D.h_soff[(size_t)t + 1] - D.h_soff[(size_t)t]) return set_err(GLS_ECOMM, "gls_ilu_attach: bad column tag");
+          const int64_t i = D.h_send[(size_t)q], j = D.h_send[(size_t)(D.h_soff[(size_t)t] + pos)];
+          if (cons[(size_t)i] || cons[(size_t)j]) continue;
+          remote.push_back({p, (int32_t)q, i, j});
+        }
+    }
+    // the system matrix's rows gain the neighbours' couplings
+    std::vector<std::vector<int64_t>> extra((size_t)n);
+    for (const auto &r : remote) extra[(size_t)r.i].push_back(r.j);
+    std::vector<int64_t> noff((size_t)n + 1, 0), ncl_;
+    for (int64_t i = 0; i < n; ++i) {
+      const size_t s0 = ncl_.size();
+      for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t) ncl_.push_back(acol[(size_t)t]);
+      auto &x = extra[(size_t)i];
+      std::sort(x.begin(), x.end());
+      for (int64_t j : x)
+        if (!std::binary_search(acol.begin() + aoff[(size_t)i], acol.begin() + aoff[(size_t)i + 1], j)) ncl_.push_back(j);
+      std::sort(ncl_.begin() + (std::ptrdiff_t)s0, ncl_.end());
+      ncl_.erase(std::unique(ncl_.begin() + (std::ptrdiff_t)s0, ncl_.end()), ncl_.end());
+      noff[(size_t)i + 1] = (int64_t)ncl_.size();
+    }
+    aown.assign(ncl_.size(), 0);
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t t = noff[(size_t)i]; t < noff[(size_t)i + 1]; ++t)
+        aown[(size_t)t] = std::binary_search(acol.begin() + aoff[(size_t)i], acol.begin() + aoff[(size_t)i + 1], ncl_[(size_t)t]);
+    aoff.swap(noff);
+    acol.swap(ncl_);
+  } else {
+    aown.assign(acol.size(), 1);
   }
   // Cuthill-McKee (deal.II) on the unconstrained cell-coupling graph of the DoF handler. Its nodes
   // carry deal.II's per-support-point DoF groups: a velocity node's components followed by the
@@ -3422,14 +3635,22 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   }
   // the system matrix's pattern in the new numbering, then its ILU(fill) pattern
   std::vector<int32_t> arow((size_t)n + 1, 0), acl;
+  std::vector<char> aclown;  // entry probed on this rank (pent / prow); else filled by the neighbours only
   acl.reserve(acol.size());
-  for (int64_t r = 0; r < n; ++r) {
-    const int64_t i = olddof[(size_t)r];
-    const size_t s0 = acl.size();
-    for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t)
-      if (dblk[(size_t)acol[(size_t)t]] == dblk[(size_t)i]) acl.push_back(newidx[(size_t)acol[(size_t)t]]);
-    std::sort(acl.begin() + (std::ptrdiff_t)s0, acl.end());
-    arow[(size_t)r + 1] = (int32_t)acl.size();
+  {
+    std::vector<std::pair<int32_t, char>> rowbuf;
+    for (int64_t r = 0; r < n; ++r) {
+      const int64_t i = olddof[(size_t)r];
+      rowbuf.clear();
+      for (int64_t t = aoff[(size_t)i]; t < aoff[(size_t)i + 1]; ++t)
+        if (dblk[(size_t)acol[(size_t)t]] == dblk[(size_t)i]) rowbuf.push_back({newidx[(size_t)acol[(size_t)t]], aown[(size_t)t]});
+      std::sort(rowbuf.begin(), rowbuf.end());
+      for (const auto &e : rowbuf) {
+        acl.push_back(e.first);
+        aclown.push_back(e.second);
+      }
+      arow[(size_t)r + 1] = (int32_t)acl.size();
+    }
   }
   std::vector<int32_t> rowp, col;
   if (gls::iluk_pattern(n, arow.data(), acl.data(), fill, rowp, col) != GLS_OK)
@@ -3493,7 +3714,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int64_t> pdoff((size_t)nprobe + 1, 0), peoff((size_t)nprobe + 1, 0);
   for (int64_t d = 0; d < n; ++d) ++pdoff[(size_t)probe_of(d) + 1];
   for (int64_t r = 0; r < n; ++r)
-    for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) ++peoff[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]]) + 1];
+    for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t)
+      if (aclown[(size_t)t]) ++peoff[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]]) + 1];
   for (int p = 0; p < nprobe; ++p) {
     pdoff[(size_t)p + 1] += pdoff[(size_t)p];
     peoff[(size_t)p + 1] += peoff[(size_t)p];
@@ -3501,11 +3723,14 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int32_t> pdofs((size_t)pdoff[(size_t)nprobe]), pent((size_t)peoff[(size_t)nprobe]), prow(pent.size());
   {
     std::vector<int64_t> f1(pdoff.begin(), pdoff.end() - 1), f2(peoff.begin(), peoff.end() - 1);
-    for (int64_t d = 0; d < n; ++d) pdofs[(size_t)f1[(size_t)probe_of(d)]++] = ghost(d) ? -1 : (int32_t)d;
+    // (complete rows: the unconstrained ghost DoFs are probed too)
+    for (int64_t d = 0; d < n; ++d)
+      pdofs[(size_t)f1[(size_t)probe_of(d)]++] = ghost(d) && !(cmpl && !fcons[(size_t)d]) ? -1 : (int32_t)d;
     for (int64_t r = 0; r < n; ++r) {
       int32_t pos = rowp[(size_t)r];
       for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) {
         while (col[(size_t)pos] < acl[(size_t)t]) ++pos;  // both rows sorted; A's pattern is a subset
+        if (!aclown[(size_t)t]) continue;
         const int64_t k = f2[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]])]++;
         pent[(size_t)k] = pos;
         prow[(size_t)k] = olddof[(size_t)r];  // the probe result is indexed by the original DoF
@@ -3532,6 +3757,43 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     for (int64_t r = 0; r < n; ++r)
       if (ghost(olddof[(size_t)r])) gd.push_back(didx[(size_t)r]);
     GLS_TRY(I.ghost_diag.upload(gd.data(), gd.size()));
+  }
+  // the neighbours' entries: per round, each CSR entry's send_buf slots in (round, neighbour, slot) order
+  {
+    std::vector<std::pair<int64_t, int64_t>> key;  // (round * nnz + entry, record) sorted stably
+    const int64_t nnz = (int64_t)col.size();
+    for (size_t q = 0; q < remote.size(); ++q) {
+      const auto &e = remote[q];
+      if (dblk[(size_t)e.i] != dblk[(size_t)e.j]) continue;
+      const int32_t r = newidx[(size_t)e.i], cj = newidx[(size_t)e.j];
+      const auto b = col.begin() + rowp[(size_t)r], en = col.begin() + rowp[(size_t)r + 1];
+      const auto it = std::lower_bound(b, en, cj);
+      if (it == en || *it != cj) return set_err(GLS_EINVAL, "gls_ilu_attach: a neighbour's entry is not in the pattern");
+      key.push_back({(int64_t)e.round * nnz + (int64_t)(it - col.begin()), (int64_t)q});
+    }
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<int64_t, int64_t> &a, const std::pair<int64_t, int64_t> &b) {
+      return a.first < b.first;
+    });
+    std::vector<int32_t> ru, ruoff{0}, rslot;
+    std::vector<int64_t> rr((size_t)std::max(n_rounds, 0) + 1, 0);
+    for (size_t t = 0; t < key.size(); ++t) {
+      if (t == 0 || key[t].first != key[t - 1].first) {
+        if (t) ruoff.push_back((int32_t)rslot.size());
+        ru.push_back((int32_t)(key[t].first % nnz));
+        ++rr[(size_t)(key[t].first / nnz) + 1];
+      }
+      rslot.push_back(remote[(size_t)key[t].second].slot);
+    }
+    if (!key.empty()) ruoff.push_back((int32_t)rslot.size());
+    for (int p = 0; p < n_rounds; ++p) rr[(size_t)p + 1] += rr[(size_t)p];
+    ru.push_back(0);  // (padding: no zero-sized device buffers)
+    rslot.push_back(0);
+    GLS_TRY(I.ru.upload(ru.data(), ru.size()));
+    GLS_TRY(I.ruoff.upload(ruoff.data(), ruoff.size()));
+    GLS_TRY(I.rslot.upload(rslot.data(), rslot.size()));
+    I.rr = rr;
+    I.complete = cmpl;
+    I.n_rounds = n_rounds;
   }
   GLS_TRY(I.pdofs.upload(pdofs.data(), pdofs.size()));
   GLS_TRY(I.pent.upload(pent.data(), pent.size()));

@@ -70,10 +70,11 @@ hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, c
                             int64_t n, hipStream_t s);
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
                                 hipStream_t s, const double *rb = nullptr);  // y[idx] = d[idx]*v[idx] (rb: rb[idx] - d v)
-// assembled-ILU helpers: x[idx] = a; val[ent] = y[row] (probe extraction); a_ii <- r a_ii + sign(a_ii) t
+// assembled-ILU helpers: x[idx] = a; val[ent] = y[row] (probe extraction; add: val[ent] += y[row]);
+// a_ii <- r a_ii + sign(a_ii) t
 hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s);
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
-                             hipStream_t s);
+                             hipStream_t s, bool add = false);
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s);
 // multicolor ILU triangular solves (gls_ilu_kernels.hip): y = L^-1 b, x = U^-1 y on node groups of <=
 // kMaxGroupRows rows, colors in order (forward) / reverse order (backward)

@@ -412,9 +412,10 @@ __global__ void k_set_const_indexed(double *x, const int32_t *idx, int64_t m, do
   if (i < m) x[idx[i]] = a;
 }
 // CSR values of the entries whose column belongs to one probe: val[ent[i]] = y[row[i]]
-__global__ void k_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y) {
+__global__ void k_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
+                                int add) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) val[ent[i]] = y[row[i]];
+  if (i < m) val[ent[i]] = add ? val[ent[i]] + y[row[i]] : y[row[i]];
 }
 // Ifpack-style diagonal perturbation before the factorisation: a_ii <- rthresh a_ii + sign(a_ii) athresh
 __global__ void k_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh) {
@@ -442,9 +443,10 @@ hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, doubl
   return hipGetLastError();
 }
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
-                             hipStream_t s) {
+                             hipStream_t s, bool add) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_probe_extract, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, m, y);
+  hipLaunchKernelGGL(k_probe_extract, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, m, y,
+                     add ? 1 : 0);
   return hipGetLastError();
 }
 hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh,
