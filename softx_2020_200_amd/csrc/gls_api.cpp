@@ -334,7 +334,7 @@ struct gls_ctx {
     bool dofs = false;
     int width = 4;  // doubles per exchange entry
     int64_t n_owned = 0, n_owned_p = 0, n_send = 0, n_recv = 0;
-    DevBuf<int32_t> add_u, add_off, add_slot;  // export-add of the DoF exchange in a fixed order
+    DevBuf<int32_t> add_u, add_off, add_slot;  // export-add (node or DoF exchange) in a fixed order
     DevBuf<int32_t> send_nodes, recv_nodes;
     double *send_buf = nullptr, *recv_buf = nullptr, *red_buf = nullptr;
     gls_exchange_fn xchg = nullptr;
@@ -875,6 +875,28 @@ int dist_import(gls_ctx *c, double *x) {
   HIP_TRY(gls::vec_unpack_nodes(x, c->dist.recv_nodes.p, c->dist.n_recv, voff, c->dist.recv_buf, 0, c->stream));
   return GLS_OK;
 }
+// export-add order: every owned entry's incoming exchange slots in ascending slot (= neighbour) order,
+// so the sums over several neighbours are deterministic
+int upload_export_order(gls_ctx::Dist &D, const int32_t *send, int64_t ns) {
+  std::vector<std::pair<int32_t, int32_t>> ds;
+  ds.reserve((size_t)ns);
+  for (int64_t j = 0; j < ns; ++j) ds.push_back({send[j], (int32_t)j});
+  std::stable_sort(ds.begin(), ds.end(), [](const std::pair<int32_t, int32_t> &a, const std::pair<int32_t, int32_t> &b) {
+    return a.first < b.first;
+  });
+  std::vector<int32_t> au, aoff{0}, aslot;
+  for (size_t t = 0; t < ds.size(); ++t) {
+    if (t == 0 || ds[t].first != ds[t - 1].first) {
+      if (t) aoff.push_back((int32_t)aslot.size());
+      au.push_back(ds[t].first);
+    }
+    aslot.push_back(ds[t].second);
+  }
+  if (!au.empty()) aoff.push_back((int32_t)aslot.size());
+  GLS_TRY(D.add_u.upload(au.data(), au.size()));
+  GLS_TRY(D.add_off.upload(aoff.data(), au.empty() ? 0 : aoff.size()));
+  return D.add_slot.upload(aslot.data(), aslot.size());
+}
 int dist_export_add(gls_ctx *c, double *y) {
   if (!c->dist.on) return GLS_OK;
   if (c->dist.dofs) {
@@ -887,7 +909,8 @@ int dist_export_add(gls_ctx *c, double *y) {
   const int64_t voff = 3 * (int64_t)c->n_vnodes;
   HIP_TRY(gls::vec_pack_nodes(y, c->dist.recv_nodes.p, c->dist.n_recv, voff, c->dist.recv_buf, c->stream));
   if (c->dist.xchg(c->dist.user, 1) != 0) return set_err(GLS_ECOMM, "ghost export exchange failed");
-  HIP_TRY(gls::vec_unpack_nodes(y, c->dist.send_nodes.p, c->dist.n_send, voff, c->dist.send_buf, 1, c->stream));
+  HIP_TRY(gls::vec_add_nodes_ordered(y, c->dist.add_u.p, c->dist.add_off.p, c->dist.add_slot.p, (int64_t)c->dist.add_u.n,
+                                     voff, c->dist.send_buf, c->stream));
   return GLS_OK;
 }
 // out[k] = sum over OWNED DoFs of A[k] . w, reduced over ranks (host result)
@@ -1449,6 +1472,7 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   for (int64_t i = 0; i < nr; ++i)
     if (recv_nodes[i] < n_owned_nodes || recv_nodes[i] >= c->n_vnodes) return set_err(GLS_EINVAL, "recv node not a ghost");
   if ((ns && !send_buf) || (nr && !recv_buf)) return set_err(GLS_EINVAL, "exchange buffers missing");
+  GLS_TRY(upload_export_order(c->dist, send_nodes, ns));
   GLS_TRY(c->dist.send_nodes.upload(send_nodes, (size_t)ns));
   GLS_TRY(c->dist.recv_nodes.upload(recv_nodes, (size_t)nr));
   c->dist.n_owned = n_owned_nodes;
@@ -1493,23 +1517,8 @@ int gls_dist_attach_dofs(gls_ctx *c, int64_t n_owned_vnodes, int64_t n_owned_pno
   for (int64_t i = 0; i < nr; ++i)
     if (recv_dofs[i] < 0 || recv_dofs[i] >= c->n_dofs || owned(recv_dofs[i])) return set_err(GLS_EINVAL, "recv DoF not a ghost");
   if ((ns && !send_buf) || (nr && !recv_buf)) return set_err(GLS_EINVAL, "exchange buffers missing");
-  // export-add: every owned DoF's incoming slots in neighbour order (deterministic sums)
-  std::vector<std::pair<int32_t, int32_t>> ds;
-  ds.reserve((size_t)ns);
-  for (int64_t j = 0; j < ns; ++j) ds.push_back({send_dofs[j], (int32_t)j});
-  std::stable_sort(ds.begin(), ds.end(), [](const std::pair<int32_t, int32_t> &a, const std::pair<int32_t, int32_t> &b) {
-    return a.first < b.first;
-  });
-  std::vector<int32_t> au, aoff{0}, aslot;
-  for (size_t t = 0; t < ds.size(); ++t) {
-    if (t == 0 || ds[t].first != ds[t - 1].first) {
-      if (t) aoff.push_back((int32_t)aslot.size());
-      au.push_back(ds[t].first);
-    }
-    aslot.push_back(ds[t].second);
-  }
-  if (!au.empty()) aoff.push_back((int32_t)aslot.size());
   auto &D = c->dist;
+  GLS_TRY(upload_export_order(D, send_dofs, ns));
   GLS_TRY(D.send_nodes.upload(send_dofs, (size_t)ns));
   GLS_TRY(D.recv_nodes.upload(recv_dofs, (size_t)nr));
   D.h_send.assign(send_dofs, send_dofs + ns);
@@ -1520,9 +1529,6 @@ int gls_dist_attach_dofs(gls_ctx *c, int64_t n_owned_vnodes, int64_t n_owned_pno
     D.h_soff.assign(send_offsets, send_offsets + n_nbrs + 1);
     D.h_roff.assign(recv_offsets, recv_offsets + n_nbrs + 1);
   }
-  GLS_TRY(D.add_u.upload(au.data(), au.size()));
-  GLS_TRY(D.add_off.upload(aoff.data(), au.empty() ? 0 : aoff.size()));
-  GLS_TRY(D.add_slot.upload(aslot.data(), aslot.size()));
   D.dofs = true;
   D.width = 1;
   D.n_owned = n_owned_vnodes;

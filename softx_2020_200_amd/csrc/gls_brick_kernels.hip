@@ -64,6 +64,10 @@
 #define GLS_QD_PREFETCH 0
 #endif
 
+#ifndef GLS_SLAB_INFLIGHT
+#define GLS_SLAB_INFLIGHT 0  // k_slab_sum: 1 = every slot of a node loaded at once (A/B candidate)
+#endif
+
 #ifndef GLS_LDS_SPLIT
 #define GLS_LDS_SPLIT 0  // 1 asm / 2 masked: FP64 LDS reads as single ds_read_b64 -- measured slower (profiles/r02_lds_split_ab.txt)
 #endif
@@ -1031,6 +1035,34 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
   double s[4] = {0., 0., 0., 0.};
+#if GLS_SLAB_INFLIGHT
+  // a hex-mesh node lies in at most 8 bricks: all slot indices, then all slab entries in flight at
+  // once (one dependent-load round trip instead of one per slot); summed in the same slot order
+  const int j0 = off[i], cnt = off[i + 1] - j0;
+  int sl[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) sl[t] = t < cnt ? slots[j0 + t] : 0;
+  double e[8][4];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < cnt) SlabQuad<S>::load(slab + (int64_t)sl[t] * 4, e[t][0], e[t][1], e[t][2], e[t][3]);
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < cnt) {
+      s[0] += e[t][0];
+      s[1] += e[t][1];
+      s[2] += e[t][2];
+      s[3] += e[t][3];
+    }
+  for (int j = j0 + 8; j < j0 + cnt; ++j) {  // not reached on hex meshes
+    double a, b, c, d;
+    SlabQuad<S>::load(slab + (int64_t)slots[j] * 4, a, b, c, d);
+    s[0] += a;
+    s[1] += b;
+    s[2] += c;
+    s[3] += d;
+  }
+#else
   for (int j = off[i]; j < off[i + 1]; ++j) {
     double a, b, c, d;
     SlabQuad<S>::load(slab + (int64_t)slots[j] * 4, a, b, c, d);
@@ -1039,6 +1071,7 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
     s[2] += c;
     s[3] += d;
   }
+#endif
   const int64_t node = nodes[i];
   const int64_t gi[4] = {node * 3, node * 3 + 1, node * 3 + 2, voff + node};
   if constexpr (J) {

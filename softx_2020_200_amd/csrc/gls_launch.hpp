@@ -86,6 +86,8 @@ hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double
 hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
 hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
                                 const double *buf, hipStream_t s);
+hipError_t vec_add_nodes_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                                 int64_t voff, const double *buf, hipStream_t s);  // 4 values per node slot
 hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh, hipStream_t s);
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();

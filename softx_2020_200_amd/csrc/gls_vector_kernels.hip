@@ -396,6 +396,34 @@ hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off,
   hipLaunchKernelGGL(k_add_dofs_ordered, dim3(grid_for(n)), dim3(kBlock), 0, s, x, u, off, slot, n, buf);
   return hipGetLastError();
 }
+// node export-add in a fixed order: x[(u[i], c)] += buf[slot[j]*4 + c] for j in [off[i], off[i+1])
+// (a corner node of a 4- or 8-rank partition receives from several neighbours; atomics would make
+// the sum order, and the last bit, depend on the schedule)
+__global__ void k_add_nodes_ordered(double *__restrict__ x, const int32_t *__restrict__ u, const int32_t *__restrict__ off,
+                                    const int32_t *__restrict__ slot, int64_t n, int64_t voff,
+                                    const double *__restrict__ buf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t nd = u[i];
+    double s0 = x[nd * 3 + 0], s1 = x[nd * 3 + 1], s2 = x[nd * 3 + 2], s3 = x[voff + nd];
+    for (int j = off[i]; j < off[i + 1]; ++j) {
+      const double *b = buf + (int64_t)slot[j] * 4;
+      s0 += b[0];
+      s1 += b[1];
+      s2 += b[2];
+      s3 += b[3];
+    }
+    x[nd * 3 + 0] = s0;
+    x[nd * 3 + 1] = s1;
+    x[nd * 3 + 2] = s2;
+    x[voff + nd] = s3;
+  }
+}
+hipError_t vec_add_nodes_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                                 int64_t voff, const double *buf, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_add_nodes_ordered, dim3(grid_for(n)), dim3(kBlock), 0, s, x, u, off, slot, n, voff, buf);
+  return hipGetLastError();
+}
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_indexed, dim3(grid_for(m)), dim3(kBlock), 0, s, y, idx, vals, m);
