@@ -64,8 +64,12 @@
 #define GLS_QD_PREFETCH 0
 #endif
 
+#ifndef GLS_REDUCE_NODE
+#define GLS_REDUCE_NODE 1  // brick reduction: one thread per node (4 fields) instead of per (node, field)
+#endif
+
 #ifndef GLS_SLAB_INFLIGHT
-#define GLS_SLAB_INFLIGHT 0  // k_slab_sum: 1 = every slot of a node loaded at once (A/B candidate)
+#define GLS_SLAB_INFLIGHT 1  // k_slab_sum: every slot of a node loaded at once (0.583 -> 0.548 ms at 128^3, profiles/r03_ab_reduce_node.txt)
 #endif
 
 #ifndef GLS_LDS_SPLIT
@@ -316,14 +320,15 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
       BF(5)[n] = h[1];
       BF(6)[n] = h[2];
     } else if (JV) {
-      const unsigned m = P.vmask ? P.vmask[node] : 0u;
       if (unit_dof >= 0) {
+        const unsigned m = P.vmask ? P.vmask[node] : 0u;
         BF(FV)[n] = (m & 1u) ? 0.0 : (i3 == unit_dof ? 1.0 : 0.0);
         BF(FV + 1)[n] = (m & 2u) ? 0.0 : (i3 + 1 == unit_dof ? 1.0 : 0.0);
         BF(FV + 2)[n] = (m & 4u) ? 0.0 : (i3 + 2 == unit_dof ? 1.0 : 0.0);
         BF(FV + 3)[n] = voff + node == unit_dof ? 1.0 : 0.0;
-      } else {  // unconditional loads (all in flight together), masked afterwards
+      } else {  // v and the mask loaded together (all in flight: one round trip), masked afterwards
         const double v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
+        const unsigned m = P.vmask ? P.vmask[node] : 0u;
         BF(FV)[n] = (m & 1u) ? 0.0 : v0;
         BF(FV + 1)[n] = (m & 2u) ? 0.0 : v1;
         BF(FV + 2)[n] = (m & 4u) ? 0.0 : v2;
@@ -332,7 +337,6 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
     }
   }
   __syncthreads();
-
   // ---------------- per-wave: cells 2*wave, 2*wave+1 of the brick
   auto Out = [&](int ci, int f) { return sO + (ci * C::NO + f) * N3; };
   const int cbase = wave * CPW;
@@ -826,6 +830,70 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   __syncthreads();
 
   // ---------------- brick reduction (fixed order) + scatter
+#if GLS_REDUCE_NODE && !defined(GLS_BRICK_COLORS_BUILD)
+  // one thread per brick node, all 4 fields: the node's cell / offset bookkeeping is done once, the
+  // slab entry goes out as one vector store. Same cell order per field as the per-(node, field) loop.
+  {
+    if (!(GLS_ABL & 2)) {
+      for (int n = tid; n < BN3; n += blockDim.x) {
+        const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
+        Real s[4] = {0., 0., 0., 0.};
+#pragma unroll
+        for (int cz = 0; cz < 2; ++cz) {
+          const int az = Zn - K * cz;
+          if (az < 0 || az > K) continue;
+#pragma unroll
+          for (int cy = 0; cy < 2; ++cy) {
+            const int ay = Yn - K * cy;
+            if (ay < 0 || ay > K) continue;
+#pragma unroll
+            for (int cx = 0; cx < 2; ++cx) {
+              const int ax = Xn - K * cx;
+              if (ax < 0 || ax > K) continue;
+              const Real *o = Out(cx + 2 * cy + 4 * cz, 0) + ax + K1 * (ay + K1 * az);
+#pragma unroll
+              for (int f = 0; f < 4; ++f) s[f] += lds(o + f * N3, zm);
+            }
+          }
+        }
+        const int node = sNode[n];
+        const int64_t gi[4] = {(int64_t)node * 3, (int64_t)node * 3 + 1, (int64_t)node * 3 + 2, voff + node};
+        const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
+        if (interior) {
+          if (MODE == MODE_JVQ && P.jx) {  // fused damped-Jacobi sweep
+            const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              const bool con = f < 3 && ((m >> f) & 1u);
+              const double x = P.jx[gi[f]], dd = P.jd[gi[f]];
+              P.jx[gi[f]] = x + P.jomega * (P.jb[gi[f]] - (con ? dd * x : (double)s[f])) / dd;
+            }
+          } else if (MODE == MODE_JVQ && P.rb) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) Yout[gi[f]] = P.rb[gi[f]] - (double)s[f];
+          } else {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) Yout[gi[f]] = s[f];
+          }
+        } else if (use_slab) {  // this brick's partial sums of a brick-boundary node (k_slab_sum)
+          const int64_t si = ((int64_t)brick * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4;
+          if (std::is_same<Real, float>::value && P.slabf) {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<f4 *>(P.slabf + si) = f4{(float)s[0], (float)s[1], (float)s[2], (float)s[3]};
+          } else {
+            typedef double d2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<d2 *>(P.slab + si) = d2{(double)s[0], (double)s[1]};
+            *reinterpret_cast<d2 *>(P.slab + si + 2) = d2{(double)s[2], (double)s[3]};
+          }
+        } else {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) atomicAdd(&Yout[gi[f]], (double)s[f]);
+        }
+      }
+      return;
+    }
+  }
+#endif
   for (int t = tid; t < BN3 * 4; t += blockDim.x) {
     const int n = t >> 2, fld = t & 3;
     const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
