@@ -383,6 +383,8 @@ struct Mesh {
   // their DoF-level constraint lines (empty on the uniform lattice)
   std::vector<double> vx, px;
   std::map<int, std::vector<double>> slip_normals;  // general meshes: boundary id -> node normals [nv][dim]
+  std::map<int, std::vector<int32_t>> slip_rank;    // ... -> independent normal directions per node (edges, corners)
+  std::map<int, std::vector<double>> slip_sets;     // ... -> the grouped normals [nv][3][dim]
   std::vector<uint8_t> vhanging;  // per velocity node
   std::vector<int64_t> hang_dofs, hang_off{0}, hang_master;
   std::vector<double> hang_w;
@@ -494,11 +496,14 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
   std::vector<double> val((size_t)(m.nv * m.dim), 0.0);
   for (const BC &b : P.bcs) {
     if (b.type == "periodic") continue;
-    const std::vector<double> *sn = nullptr;  // general meshes: node normals of this slip boundary
+    const std::vector<double> *sn = nullptr, *ss = nullptr;  // general meshes: node normals of this slip boundary
+    const std::vector<int32_t> *sr = nullptr;
     if (b.type == "slip" && m.general) {
       auto it = m.slip_normals.find(b.id);
       if (it == m.slip_normals.end()) die("slip boundary %d: no node normals", b.id);
       sn = &it->second;
+      sr = &m.slip_rank.at(b.id);
+      ss = &m.slip_sets.at(b.id);
     }
     std::vector<int64_t> sel;
     std::vector<double> X;
@@ -513,7 +518,40 @@ Constraints make_constraints(const Params &P, const Mesh &m, double t) {
       if ((m.general ? m.vbid[(size_t)v] : face_bits(m, x, P.colorize)) & (1u << b.id)) {
         sel.push_back(v);
         X.insert(X.end(), x, x + m.dim);
-        if (sn) {  // n.u = 0: on a straight wall the normal is an axis and that component is 0
+        const int rk = sr ? (*sr)[(size_t)v] : 0;
+        if (sn && rk >= m.dim) {  // as many independent normals as components (a corner): u = 0
+          nrm.push_back((1u << m.dim) - 1u);
+        } else if (sn && rk == 2) {  // an edge in 3D: u parallel to t = n0 x n1, two constraints
+          const double *g = &(*ss)[(size_t)(v * 3 * m.dim)];
+          double t[3] = {0, 0, 0}, tl = 0;
+          for (int j = 1; j < 3 && tl <= 1e-3; ++j) {
+            const double *h = g + j * m.dim;
+            t[0] = g[1] * h[2] - g[2] * h[1];
+            t[1] = g[2] * h[0] - g[0] * h[2];
+            t[2] = g[0] * h[1] - g[1] * h[0];
+            tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+          }
+          int cm = 0;
+          for (int c = 1; c < 3; ++c)
+            if (std::fabs(t[c]) > std::fabs(t[cm])) cm = c;
+          unsigned ax = 0;
+          for (int a = 0; a < 3; ++a) {
+            if (a == cm) continue;
+            const double w = t[a] / t[cm];
+            if (std::fabs(w) < 1e-12) {  // t has no a-component: u_a = 0
+              ax |= 1u << a;
+              continue;
+            }
+            // u_a = (t_a / t_cm) u_cm, unless u_a is already constrained or u_cm carries a line
+            if ((C.mask[(size_t)v] >> a) & 1u || lined[(size_t)(v * 3 + a)] || lined[(size_t)(v * 3 + cm)]) continue;
+            C.line_dofs.push_back(v * 3 + a);
+            C.line_master.push_back(v * 3 + cm);
+            C.line_w.push_back(w);
+            C.line_off.push_back((int64_t)C.line_master.size());
+            lined[(size_t)(v * 3 + a)] = 1;
+          }
+          nrm.push_back(ax);
+        } else if (sn) {  // n.u = 0: on a straight wall the normal is an axis and that component is 0
           unsigned ax = 0;
           bool axis = true;
           for (int c = 0; c < m.dim; ++c) {
@@ -1423,9 +1461,13 @@ struct Solver {
     // slip boundaries: the averaged face normals at the velocity nodes (compute_no_normal_flux_constraints)
     for (const BC &b : P.bcs)
       if (b.type == "slip") {
-        std::vector<double> nrm((size_t)(r.nv * P.dim));
+        std::vector<double> nrm((size_t)(r.nv * P.dim)), sets((size_t)(r.nv * 3 * P.dim));
+        std::vector<int32_t> rank_((size_t)r.nv);
         ck(gls_fe_space_boundary_normals(space, b.id, nrm.data()), "gls_fe_space_boundary_normals");
+        ck(gls_fe_space_boundary_normal_sets(space, b.id, rank_.data(), sets.data()), "gls_fe_space_boundary_normal_sets");
         r.slip_normals[b.id] = std::move(nrm);
+        r.slip_rank[b.id] = std::move(rank_);
+        r.slip_sets[b.id] = std::move(sets);
       }
     m = std::move(r);
     C = make_constraints(P, m, time);

@@ -75,7 +75,7 @@ def pmc_traffic(path, kernel_mode, n_dofs):
             vals.setdefault(cur, {})[f[0]] = float(f[1]) * 1024.0
     copy = next((v for k_, v in vals.items() if "k_copy" in k_), None)
     kern = next((v for k_, v in vals.items() if "gls_brick_kernel<2, %d, double>" % kernel_mode in k_), None)
-    slab = next((v for k_, v in vals.items() if "k_slab_sum" in k_), {})
+    slab = next((v for k_, v in vals.items() if "k_slab_sum<double" in k_), {})
     if not copy or not kern or len(copy) < 2 or len(kern) < 2:
         return None
     fetch_corr = 8.0 * n_dofs / copy["FETCH_SIZE"]
@@ -309,8 +309,9 @@ def main():
                          "GMRES operator, Newton residual and all vectors stay FP64)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-full-1core", action="store_true", help="with --cpu-full: also the 1-thread Newton")
     ap.add_argument("--cpu-full", action="store_true",
-                    help="cpu_baseline = complete CPU Newton iterations on the full workload (threads and 1 thread; "
+                    help="cpu_baseline = a complete CPU Newton iteration on the full workload (the job threads; "
                          "minutes at configs[1]); default: the bounded extrapolated sample")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -515,11 +516,11 @@ def main():
         "setup_s": t_setup,
     }
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r02_pmc_traffic_head_128.txt"), 4, N_global) \
+    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r03_pmc_traffic_head_128.txt"), 4, N_global) \
         if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
-        out["roofline"]["traffic_source"] = ("profiles/r02_pmc_traffic_head_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
+        out["roofline"]["traffic_source"] = ("profiles/r03_pmc_traffic_head_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
                                              "%.2f (k_copy calibration); includes the per-quadrature-point "
                                              "linearization stream (16 doubles/q) the cached J.v reads instead "
                                              "of re-deriving u, grad u, tau, R_s" % (tr[1], tr[2]))
@@ -527,10 +528,11 @@ def main():
         # the reference's CPU path measured end to end on this very workload (1 Newton iteration)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
         full = cpu_newton(args.k, args.kp, args.n, args.nu, args.scheme, args.dt, threads)
-        full1 = cpu_newton(args.k, args.kp, args.n, args.nu, args.scheme, args.dt, 1)
+        # the 1-thread leg only on request (--cpu-full-1core): at Q1 64^3 it is ~5 min of host time
+        full1 = cpu_newton(args.k, args.kp, args.n, args.nu, args.scheme, args.dt, 1) if args.cpu_full_1core else None
         out["cpu_baseline"] = {
             "value": 1.0 / full["seconds"], "unit": "nonlinear_iters/s", "cores": threads, "kind": "port",
-            "value_1core": 1.0 / full1["seconds"], "cpu": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "value_1core": 1.0 / full1["seconds"] if full1 else None, "cpu": _cpu_model(), "host_cpus_visible": os.cpu_count(),
             "affinity": len(os.sched_getaffinity(0)),
             "sample": ("MEASURED: one complete Newton iteration of the reference's CPU path on the full workload "
                        "(%d DoFs, same synthetic state): oracle/gls_oracle.c assembly of the CSR system (%d nnz) on %d "
@@ -540,7 +542,7 @@ def main():
                           full["t_pattern"])),
             "seconds_per_iter": {key: full[key] for key in ("t_assemble", "t_ilu", "t_gmres", "t_linesearch", "seconds")},
             "seconds_per_iter_1core": {key: full1[key] for key in ("t_assemble", "t_ilu", "t_gmres", "t_linesearch",
-                                                                   "seconds")},
+                                                                   "seconds")} if full1 else None,
         }
     elif rank == 0 and world == 1 and not args.no_cpu:
         # the OpenMP threads this process may use (OMP_NUM_THREADS; on the GPU box the job's CPU share)

@@ -572,6 +572,12 @@ int gls_umesh_prepare(const gls_umesh *mesh, int32_t *refine, int32_t *coarsen);
  * normals VectorTools::compute_no_normal_flux_constraints uses for a slip boundary,
  * gls_navier_stokes.cc:100-110); [n_vnodes][dim], zero off that boundary. Host array. */
 int gls_fe_space_boundary_normals(const gls_fe_space *space, int boundary_id, double *normals);
+/* Edges and corners of a slip boundary (compute_no_normal_flux_constraints constrains as many
+ * velocity components as independent normal directions meet at a node): the node's face normals
+ * grouped by direction (groups within 60 degrees merge: a smooth curved wall gives one), count[v] =
+ * the rank of the group means (0 off the boundary, 1, 2 = an edge in 3D, dim = all components);
+ * normals: [n_vnodes][3][dim], row i = unit mean of group i (row 0 = the node normal when count = 1). */
+int gls_fe_space_boundary_normal_sets(const gls_fe_space *space, int boundary_id, int32_t *count, double *normals);
 int gls_umesh_adapt(gls_umesh *mesh, const int32_t *refine, const int32_t *coarsen);
 /* Face pieces for KellyErrorEstimator with MappingQ on such a space (conforming faces one piece,
  * a face with a refined neighbour one piece per child face; geometry on the coarse side as deal.II's

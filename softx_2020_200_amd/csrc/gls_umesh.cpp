@@ -2079,6 +2079,88 @@ int gls_fe_space_boundary_normals(const gls_fe_space *sp, int boundary_id, doubl
   return GLS_OK;
 }
 
+// The independent normal directions at every velocity node of the boundary faces with id
+// `boundary_id`, for compute_no_normal_flux_constraints at edges and corners (gls_navier_stokes.cc:
+// 100-110): the faces' outward unit normals at the node are grouped (a normal joins the first group
+// whose mean direction is within 60 degrees, else it opens a group -- adjacent faces of a smooth
+// curved wall share one group, the faces meeting at a box edge or corner do not); the group means
+// are orthogonalised (Gram-Schmidt, tolerance 1e-3) and count[v] = the rank (0 off the boundary,
+// 1 = one normal, 2 = an edge in 3D, dim = every component constrained). normals: [n_vnodes][3][dim],
+// row 0 = the unit mean of the first group (the node normal of gls_fe_space_boundary_normals when
+// count = 1), rows 1.. = the other group means (unit, not orthogonalised).
+int gls_fe_space_boundary_normal_sets(const gls_fe_space *sp, int boundary_id, int32_t *count, double *normals) {
+  if (!sp || !sp->impl_ || !count || !normals)
+    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_boundary_normal_sets: arguments");
+  const FESpaceImpl &F = *static_cast<const FESpaceImpl *>(sp->impl_);
+  const int dim = sp->dim, k = sp->k, k1 = k + 1, nn = dim == 2 ? k1 * k1 : k1 * k1 * k1;
+  struct Group {
+    double s[3];
+  };
+  std::vector<std::vector<Group>> groups((size_t)sp->n_vnodes);
+  for (int64_t c = 0; c < sp->n_cells; ++c)
+    for (int f = 0; f < 2 * dim; ++f) {
+      if (F.face_bid[(size_t)(c * 2 * dim + f)] != boundary_id) continue;
+      const int d = f / 2, s = f & 1;
+      for (int a = 0; a < nn; ++a) {
+        const int ia[3] = {a % k1, (a / k1) % k1, a / (k1 * k1)};
+        if (ia[d] != s * k) continue;
+        double xi[3] = {0, 0, 0}, J[3][3], e[3] = {0, 0, 0}, n[3] = {0, 0, 0}, JT[3][3];
+        for (int t = 0; t < dim; ++t) xi[t] = (double)ia[t] / k;
+        jacobian(*sp, c, xi, J);
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) JT[i][j] = J[j][i];
+        e[d] = s ? 1.0 : -1.0;
+        solve3(JT, e, n, dim);
+        double l = 0;
+        for (int t = 0; t < dim; ++t) l += n[t] * n[t];
+        l = std::sqrt(l);
+        for (int t = 0; t < dim; ++t) n[t] /= l;
+        auto &G = groups[(size_t)sp->cell_vnodes[c * nn + a]];
+        bool joined = false;
+        for (Group &g : G) {
+          double gl = 0, dot = 0;
+          for (int t = 0; t < dim; ++t) gl += g.s[t] * g.s[t];
+          for (int t = 0; t < dim; ++t) dot += g.s[t] * n[t];
+          if (dot > 0.5 * std::sqrt(gl)) {
+            for (int t = 0; t < dim; ++t) g.s[t] += n[t];
+            joined = true;
+            break;
+          }
+        }
+        if (!joined) G.push_back(Group{{n[0], n[1], dim == 3 ? n[2] : 0.0}});
+      }
+    }
+  std::fill(normals, normals + sp->n_vnodes * 3 * dim, 0.0);
+  for (int64_t v = 0; v < sp->n_vnodes; ++v) {
+    const auto &G = groups[(size_t)v];
+    double q[3][3] = {};  // orthonormal basis of the group means (rank)
+    int r = 0;
+    for (size_t i = 0; i < G.size(); ++i) {
+      double m[3] = {0, 0, 0}, l = 0;
+      for (int t = 0; t < dim; ++t) l += G[i].s[t] * G[i].s[t];
+      l = std::sqrt(l);
+      for (int t = 0; t < dim; ++t) m[t] = G[i].s[t] / l;
+      if (i < 3)
+        for (int t = 0; t < dim; ++t) normals[(v * 3 + (int64_t)i) * dim + t] = m[t];
+      double w[3] = {m[0], m[1], m[2]};
+      for (int j = 0; j < r; ++j) {
+        double p = 0;
+        for (int t = 0; t < dim; ++t) p += q[j][t] * w[t];
+        for (int t = 0; t < dim; ++t) w[t] -= p * q[j][t];
+      }
+      double wl = 0;
+      for (int t = 0; t < dim; ++t) wl += w[t] * w[t];
+      wl = std::sqrt(wl);
+      if (wl > 1e-3 && r < dim) {
+        for (int t = 0; t < dim; ++t) q[r][t] = w[t] / wl;
+        ++r;
+      }
+    }
+    count[v] = r;
+  }
+  return GLS_OK;
+}
+
 int gls_umesh_adapt(gls_umesh *g, const int32_t *refine, const int32_t *coarsen) {
   if (!g) return gls_io_set_error(GLS_EINVAL, "null mesh");
   return adapt(g->m, refine, coarsen);

@@ -42,7 +42,7 @@ EXPORTS = [
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
     "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
-    "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals",
+    "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals", "gls_fe_space_boundary_normal_sets",
 ]
 
 
@@ -190,6 +190,7 @@ def load():
     L.gls_umesh_adapt.argtypes = [vp, pi32, pi32]
     L.gls_fe_space_kelly_faces.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(i64), pi32, pi32, d, d, d, d]
     L.gls_fe_space_boundary_normals.argtypes = [C.POINTER(FESpace), C.c_int, d]
+    L.gls_fe_space_boundary_normal_sets.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(C.c_int32), d]
     L.gls_kelly_estimate_mapped.argtypes = [vp, vp, C.c_int, i64, C.c_int, pi32, pi32, d, d, d, d, vp]
     _lib = L
     return L
@@ -901,6 +902,14 @@ class FESpaceHandle:
         out = np.zeros((self.data["n_vnodes"], self.data["dim"]))
         check(self.L.gls_fe_space_boundary_normals(self.ptr, int(boundary_id), _dp(out)), "gls_fe_space_boundary_normals")
         return out
+
+    def boundary_normal_sets(self, boundary_id):
+        """(rank per node, grouped unit normals [n_vnodes][3][dim]) of a slip boundary's edges / corners"""
+        nv, dim = self.data["n_vnodes"], self.data["dim"]
+        cnt, out = np.zeros(nv, np.int32), np.zeros((nv, 3, dim))
+        check(self.L.gls_fe_space_boundary_normal_sets(self.ptr, int(boundary_id), cnt.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                       _dp(out)), "gls_fe_space_boundary_normal_sets")
+        return cnt, out
 
     def kelly_faces(self, nq):
         n = C.c_int64()

@@ -151,3 +151,34 @@ def test_slip_newton_2d_cell_kernel():
     left = np.nonzero(np.abs(X[:, 0] + 1) < 1e-12)[0]
     inner = left[(np.abs(X[left, 1]) < 0.9)]
     assert np.abs(xs[2 * inner]).max() == 0.0 and np.abs(xs[2 * inner + 1]).max() > 1e-4
+
+
+def test_slip_normal_sets_edges_and_corners():
+    """compute_no_normal_flux_constraints at edges / corners (gls_navier_stokes.cc:100-110): the
+    face normals meeting at a node are grouped by direction and constrain as many components as
+    independent directions meet -- box corners all components (2D: 2, 3D: 3), 3D box edges two, face
+    nodes one (the axis normal); a smooth curved wall (hyper_shell, MappingQ2) one normal per node,
+    equal to the averaged node normal of gls_fe_space_boundary_normals."""
+    from softx_2020_200_amd.native import UMesh
+    for dim, k in ((2, 2), (3, 1)):
+        m = UMesh(dim, "hyper_cube", "-1 : 1 : false")
+        m.refine_global(2)
+        h = m.fe_space_handle(k, k)
+        X = h.data["vnode_x"].reshape(-1, dim)
+        cnt, nrm = h.boundary_normal_sets(0)
+        on = (np.abs(np.abs(X) - 1) < 1e-12).sum(1)  # number of box faces the node lies on
+        assert np.array_equal(cnt, on), (dim, np.unique(cnt), np.unique(on))
+        one = on == 1
+        n0 = nrm[one, 0]
+        assert np.allclose(np.abs(n0).max(1), 1) and np.allclose(np.abs(n0).sum(1), 1)  # axis normals
+        ax = np.argmax(np.abs(n0), 1)
+        assert np.allclose(n0[np.arange(len(ax)), ax], np.sign(X[one][np.arange(len(ax)), ax]))
+    m = UMesh(2, "hyper_shell", "0, 0 : 0.25 : 1 : 4 : true")
+    m.refine_global(2)
+    h = m.fe_space_handle(2, 2, qmapping_all=True)
+    for bid in (0, 1):
+        cnt, nrm = h.boundary_normal_sets(bid)
+        avg = h.boundary_normals(bid)
+        on = np.abs(avg).sum(1) > 0
+        assert on.any() and np.array_equal(cnt[on], np.ones(on.sum(), np.int32)) and not cnt[~on].any()
+        assert np.allclose(nrm[on, 0], avg[on], atol=1e-12)
