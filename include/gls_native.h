@@ -216,7 +216,8 @@ int gls_mg_detach(gls_ctx *ctx);
  * sparsity (constrained rows / columns hold the diagonal only, lines couple their masters). DoFs are
  * renumbered like DoFRenumbering::Cuthill_McKee; the ILU(fill) level-of-fill pattern (Ifpack_IlukGraph:
  * level(i,j) = min_k level(i,k) + level(k,j) + 1 <= fill) is inserted with explicit zeros, the
- * diagonal perturbed like Ifpack (a_ii <- rthresh a_ii + sign(a_ii) athresh) and factored by rocSPARSE.
+ * diagonal perturbed like Ifpack (a_ii <- rthresh a_ii + sign(a_ii) athresh) and factored by rocSPARSE
+ * (multicolor order: by the color-by-color device factorization, same IKJ update order).
  * fill outside 0..GLS_ILU_MAX_FILL is rejected (GLS_EINVAL). Single rank, no multigrid. */
 #define GLS_ILU_MAX_FILL 10
 int gls_ilu_attach(gls_ctx *ctx, int fill, double athresh, double rthresh);

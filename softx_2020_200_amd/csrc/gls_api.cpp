@@ -298,6 +298,8 @@ struct gls_ctx {
   bool qd32_valid = false;  // stale whenever qdata is recomputed
   // per-cell path: element vectors and each node's slots in them (deterministic scatter)
   DevBuf<double> ev;
+  DevBuf<double> bev;  // batched ILU probing: element vectors of a batch of probe vectors
+  DevBuf<uint8_t> bact;  // ... and which (probe, cell batch) blocks computed them
   DevBuf<int64_t> ev_voff, ev_vslot, ev_poff, ev_pslot;
   bool smooth_f32 = false;  // this level's V-cycle J.v runs in FP32 (gls_mg_params.mixed_precision)
   bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
@@ -370,6 +372,7 @@ struct gls_ctx {
     // multicolor order with a pattern whose same-color entries stay inside a node (fill 0): the
     // color-by-color solves of gls_ilu_kernels.hip replace rocSPARSE csrsv
     bool mc_solve = false;
+    bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
     DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
     DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
@@ -382,6 +385,8 @@ struct gls_ctx {
     DevBuf<int32_t> ru, ruoff, rslot;
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
+    DevBuf<int32_t> pdpid, pepid;        // probe of each unit DoF / each extracted entry (batched probing)
+    DevBuf<double> bV, bC, bY;           // batched probing: probe vectors, C V (hanging lines), results [batch][n_dofs]
     DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
     DevBuf<int32_t> perm;                // DoF -> its row in the factored (renumbered) matrix
     DevBuf<double> val, vbuf, ybuf, tbuf;
@@ -2149,10 +2154,76 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
 
 // assembled ILU(0): probe the operator into the CSR values (one J.v per color and DoF slot), perturb
 // the diagonal, factor in place; once per Jacobian state (invalidated with the diagonal)
+// the per-cell path on one rank: all probes in batches of B vectors, each step one launch over the batch
+// (unit vectors, hanging-line values, the per-cell J.v with zero cell batches skipped, the ordered
+// element-vector sums, condensation, constrained rows, extraction) -- the same operations per probe as
+// gls_jacobian_apply, without one launch sequence per probe
+static int ilu_probe_batched(gls_ctx *c) {
+  auto &I = c->ilu;
+  const int64_t n = c->n_dofs;
+  hipStream_t s = c->stream;
+  if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  GLS_TRY(ensure_element_maps(c));
+  if (c->con_dofs.n) GLS_TRY(ensure_diag(c));
+  const int dim = c->dim, nv = gls::ipow(c->k + 1, dim), np = gls::ipow(c->kp + 1, dim);
+  const int64_t el = (int64_t)nv * dim + np, evs = (int64_t)c->n_cells * el;
+  const char *bs = std::getenv("GLS_ILU_PROBE_BATCH");
+  const int64_t budget = (int64_t)1 << 31;  // bytes of V, C V, Y and the element vectors per batch
+  int B = bs ? std::atoi(bs) : (int)std::min<int64_t>(I.n_probes, std::max<int64_t>(1, budget / (8 * (3 * n + evs))));
+  B = std::max(1, std::min(B, I.n_probes));
+  if (I.bV.n < (size_t)B * n) {
+    GLS_TRY(I.bV.alloc((size_t)B * n));
+    GLS_TRY(I.bY.alloc((size_t)B * n));
+  }
+  if (c->hang.on && I.bC.n < (size_t)B * n) GLS_TRY(I.bC.alloc((size_t)B * n));
+  if (c->bev.n < (size_t)B * evs) GLS_TRY(c->bev.alloc((size_t)B * evs));
+  const int cb = gls::cell_kernel_cells_per_block(dim, c->k, c->nq1d), nblk = (c->n_cells + cb - 1) / cb;
+  if (c->bact.n < (size_t)B * nblk) GLS_TRY(c->bact.alloc((size_t)B * nblk));
+  if (I.fill > 0) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
+  for (int p0 = 0; p0 < I.n_probes; p0 += B) {
+    const int nb = std::min(B, I.n_probes - p0);
+    HIP_TRY(gls::vec_fill(I.bV.p, (int64_t)nb * n, 0.0, s));
+    const int64_t d0 = I.pdoff[(size_t)p0], d1 = I.pdoff[(size_t)(p0 + nb)];
+    HIP_TRY(gls::probe_set_batched(I.bV.p, n, I.pdofs.p + d0, I.pdpid.p + d0, p0, d1 - d0, s));
+    const double *Cv = I.bV.p;
+    if (c->hang.on) {  // C v (hanging entries interpolated from their masters) in a copy: the constrained
+      // rows below take the probe vector itself, as gls_jacobian_apply does
+      HIP_TRY(gls::vec_copy(I.bC.p, I.bV.p, (int64_t)nb * n, s));
+      HIP_TRY(gls::vec_csr_gather_set_b(I.bC.p, c->hang.dof.p, c->hang.ooff.p, c->hang.omaster.p, c->hang.ow.p,
+                                        (int64_t)c->hang.dof.n, nb, n, s));
+      Cv = I.bC.p;
+    }
+    gls::OpParams P = make_params(c, true);
+    P.v = Cv;
+    P.y = I.bY.p;
+    P.hmask = c->hang.on ? c->hang.hmask.p : nullptr;
+    P.ev = c->bev.p;
+    P.bv_stride = n;
+    P.bev_stride = evs;
+    P.n_probe = nb;
+    P.bact = c->bact.p;
+    {
+      TimedLaunch t(c, (int)gls::MODE_JV);
+      HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, gls::MODE_JV, P, c->tables, s));
+    }
+    HIP_TRY(gls::gather_element_vectors_b(I.bY.p, c->bev.p, c->ev_voff.p, c->ev_vslot.p, c->n_vnodes, c->ev_poff.p,
+                                          c->ev_pslot.p, c->n_pnodes, c->dim, nb, n, evs, c->bact.p, el, cb, nblk, s));
+    if (c->hang.on)
+      HIP_TRY(gls::vec_csr_condense_b(I.bY.p, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
+                                      (int64_t)c->hang.tm.n, nb, n, s));
+    HIP_TRY(gls::vec_gather_scale_set_b(I.bY.p, c->diag.p, I.bV.p, c->con_dofs.p, (int64_t)c->con_dofs.n, nb, n, s));
+    const int64_t e0 = I.peoff[(size_t)p0], e1 = I.peoff[(size_t)(p0 + nb)];
+    HIP_TRY(gls::probe_extract_batched(I.val.p, I.pent.p + e0, I.prow.p + e0, I.pepid.p + e0, p0, e1 - e0, I.bY.p, n, s));
+  }
+  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
+  return GLS_OK;
+}
+
 static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_jacobian_apply)
   auto &I = c->ilu;
   const int64_t n = c->n_dofs;
   hipStream_t s = c->stream;
+  if (!c->dist.on && !c->use_brick && !std::getenv("GLS_ILU_PROBE_LOOP")) return ilu_probe_batched(c);
   if (I.fill > 0 || c->dist.on) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
   // across ranks the constrained rows' diagonal is the exchanged one: computed before the local probes
   if (c->dist.on && (c->con_dofs.n || I.complete)) GLS_TRY(ensure_diag(c));
@@ -2200,7 +2271,11 @@ static int ensure_ilu(gls_ctx *c) {
   const auto t1 = now();
   const rocsparse_int m = (rocsparse_int)n, nnz = (rocsparse_int)I.nnz;
   RS_TRY(rocsparse_set_stream(I.h, s));
-  RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
+  if (I.mc_factor)
+    HIP_TRY(gls::ilu_mc_factor(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
+                               I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, s));
+  else
+    RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
   I.valid = true;
   if (verbose) {
     const auto t2 = now();
@@ -3672,6 +3747,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   // the split of its entries into other colors / own node; valid while no entry couples two nodes of
   // one color (fill 0; fill-in can create such entries: then rocSPARSE csrsv solves)
   I.mc_solve = false;
+  I.mc_factor = false;
   if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
     const int ncl = I.n_order_colors;
     std::vector<int32_t> cstart((size_t)ncl + 2, (int32_t)n), grow, cg((size_t)ncl + 1, 0), lsp((size_t)n), usp((size_t)n);
@@ -3703,6 +3779,9 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       GLS_TRY(I.mc_usp.upload(usp.data(), usp.size()));
       I.mc_cg = cg;
       I.mc_solve = true;
+      int32_t maxrow = 0;
+      for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
+      I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
     }
   }
   // probes: one per (color, slot); every entry of the system matrix is read from the probe of its
@@ -3804,6 +3883,15 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   GLS_TRY(I.pdofs.upload(pdofs.data(), pdofs.size()));
   GLS_TRY(I.pent.upload(pent.data(), pent.size()));
   GLS_TRY(I.prow.upload(prow.data(), prow.size()));
+  {  // probe of every unit DoF and every extracted entry (batched probing)
+    std::vector<int32_t> pdp(std::max<size_t>(pdofs.size(), 1)), pep(std::max<size_t>(pent.size(), 1));
+    for (int p = 0; p < nprobe; ++p) {
+      for (int64_t t = pdoff[(size_t)p]; t < pdoff[(size_t)p + 1]; ++t) pdp[(size_t)t] = p;
+      for (int64_t t = peoff[(size_t)p]; t < peoff[(size_t)p + 1]; ++t) pep[(size_t)t] = p;
+    }
+    GLS_TRY(I.pdpid.upload(pdp.data(), pdp.size()));
+    GLS_TRY(I.pepid.upload(pep.data(), pep.size()));
+  }
   GLS_TRY(I.val.alloc(col.size()));
   HIP_TRY(hipMemset(I.val.p, 0, col.size() * sizeof(double)));
   GLS_TRY(I.vbuf.alloc((size_t)n));

@@ -63,6 +63,29 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
   const int ncb = min(CB, P.n_cells - c0);
   const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
 
+  // batched J.v (probing): this block's vector; J is linear, so a batch of cells on which the vector
+  // vanishes has zero element vectors (most (probe, cell batch) pairs of a distance-2 colored probe set)
+  const double *Pv = P.v;
+  double *Pev = P.ev;
+  if constexpr (MODE == MODE_JV) {
+    if (P.bv_stride) {
+      Pv += (int64_t)blockIdx.y * P.bv_stride;
+      Pev += (int64_t)blockIdx.y * P.bev_stride;
+      int any = 0;
+      for (int i = tid; i < ncb * NV; i += blockDim.x) {
+        const int64_t b = (int64_t)P.cell_vnodes[(int64_t)c0 * NV + i] * DIM;
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) any |= Pv[b + c] != 0.0;
+      }
+      for (int i = tid; i < ncb * NP; i += blockDim.x) {
+        const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+        any |= Pv[voff + pn] != 0.0;
+      }
+      const int act = __syncthreads_or(any);
+      if (tid == 0) P.bact[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = act ? 1 : 0;
+      if (!act) return;  // the batched gather reads these element vectors as zero
+    }
+  }
   // ---- stage tables
   {
     const double *src = reinterpret_cast<const double *>(&T);
@@ -89,13 +112,13 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
     if constexpr (MODE == MODE_JV) {
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
 #pragma unroll
-      for (int c = 0; c < DIM; ++c) sV[i * DIM + c] = ((m >> c) & 1u) ? 0.0 : P.v[b + c];
+      for (int c = 0; c < DIM; ++c) sV[i * DIM + c] = ((m >> c) & 1u) ? 0.0 : Pv[b + c];
     }
   }
   for (int i = tid; i < ncb * NP; i += blockDim.x) {
     const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
     sP[i] = P.u[voff + pn];
-    if constexpr (MODE == MODE_JV) sVP[i] = P.v[voff + pn];
+    if constexpr (MODE == MODE_JV) sVP[i] = Pv[voff + pn];
   }
   __syncthreads();
 
@@ -417,8 +440,8 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
           out[c] += s;
         }
       }
-      if (P.ev) {
-        double *e = P.ev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
+      if (Pev) {
+        double *e = Pev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
         for (int c = 0; c < DIM; ++c) e[c] = out[c];
       } else {
@@ -472,8 +495,8 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
       }
       // constrained rows (Dirichlet or hanging) get deal.II's |K_e(i,i)| per cell
       const unsigned m = (P.vmask ? P.vmask[node] : 0u) | (P.hmask ? P.hmask[node] : 0u);
-      if (P.ev) {
-        double *e = P.ev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
+      if (Pev) {
+        double *e = Pev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
         for (int c = 0; c < DIM; ++c) e[c] = ((m >> c) & 1u) ? fabs(out[c]) : out[c];
       } else {
@@ -525,7 +548,7 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
         out += Tq[0] * Tq[1] * (g0 * g0 + g1 * g1 + g2 * g2);
       }
     }
-    if (P.ev) P.ev[(int64_t)(c0 + cl) * (NV * DIM + NP) + NV * DIM + a] = out;
+    if (Pev) Pev[(int64_t)(c0 + cl) * (NV * DIM + NP) + NV * DIM + a] = out;
     else atomicAdd(&P.y[voff + pn], out);
   }
 }
@@ -558,7 +581,8 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
       hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
       break;
     case MODE_JV:
-      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
+      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks, P.bv_stride ? P.n_probe : 1),
+                         dim3(256), lds, s, P, T);
       break;
     default:
       hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
@@ -586,6 +610,13 @@ hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const 
   GLS_CASE(3, 2, 2)
 #undef GLS_CASE
   return hipErrorNotSupported;
+}
+
+int cell_kernel_cells_per_block(int dim, int k, int nq1d) {
+  (void)k;
+  int nq = 1;
+  for (int d = 0; d < dim; ++d) nq *= nq1d;
+  return 256 / nq;  // Cfg<>::CB
 }
 
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d) {

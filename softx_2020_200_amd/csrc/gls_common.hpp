@@ -61,6 +61,9 @@ struct OpParams {
   int subset_n;
   double *ev;                 // per-cell kernels: element vectors [n_cells][NV*dim + NP] instead of atomics
                               //   into y (summed per node in a fixed order by gather_element_vectors)
+  int64_t bv_stride;          // per-cell MODE_JV batch (probing): blockIdx.y = vector, v / ev at these strides;
+  int64_t bev_stride;         //   cell batches on which the vector vanishes skip their element vectors and
+  uint8_t *bact;              //   exit, flagged 0 in bact[vector * gridDim.x + block] (1 = computed)
   double *slab;               // brick path: [n_bricks][NBND][4] partial sums of brick-boundary nodes
                               //   (nullptr -> FP64 atomics into y, which the caller zeroes)
   float *slabf;               // FP32 kernels: the same slab in FP32 when set (takes precedence)

@@ -10,6 +10,7 @@ hipError_t gather_element_vectors(double *y, const double *ev, const int64_t *vo
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s);
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
+int cell_kernel_cells_per_block(int dim, int k, int nq1d);  // cells of one per-cell kernel workgroup
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
@@ -76,9 +77,29 @@ hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, doubl
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
                              hipStream_t s, bool add = false);
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s);
+// batched probing of the per-cell operator (nb probe vectors at stride bs / ys, element vectors at evs;
+// pid[e] = probe of entry e, p0 = the batch's first probe)
+hipError_t probe_set_batched(double *V, int64_t n, const int32_t *dofs, const int32_t *pid, int p0, int64_t m,
+                             hipStream_t s);
+hipError_t probe_extract_batched(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+                                 int64_t m, const double *Y, int64_t n, hipStream_t s);
+hipError_t vec_csr_gather_set_b(double *x, const int64_t *dof, const int64_t *off, const int64_t *master,
+                                const double *w, int64_t n, int nb, int64_t bs, hipStream_t s);
+hipError_t vec_csr_condense_b(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
+                              int64_t n, int nb, int64_t bs, hipStream_t s);
+hipError_t vec_gather_scale_set_b(double *y, const double *d, const double *v, const int64_t *idx, int64_t m, int nb,
+                                  int64_t bs, hipStream_t s);
+hipError_t gather_element_vectors_b(double *y, const double *ev, const int64_t *voff, const int64_t *vslot, int64_t nv,
+                                    const int64_t *poff, const int64_t *pslot, int64_t np, int dim, int nb, int64_t ys,
+                                    int64_t evs, const uint8_t *act, int64_t el, int cb, int nblk, hipStream_t s);
 // multicolor ILU triangular solves (gls_ilu_kernels.hip): y = L^-1 b, x = U^-1 y on node groups of <=
 // kMaxGroupRows rows, colors in order (forward) / reverse order (backward)
 constexpr int kMaxGroupRows = 4;
+// multicolor ILU numeric factorization in place (same structures; rows of <= kIluMaxRow entries)
+constexpr int kIluMaxRow = 640;
+hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
+                         const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
+                         double boost_val, hipStream_t s);
 hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                         const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
                         const int32_t *didx, const double *b, double *y, double *x, hipStream_t s);

@@ -154,7 +154,9 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
 // (masters are never constrained lines themselves, so src may alias x)
 __global__ void k_csr_gather_set(double *x, const double *src, const int64_t *__restrict__ dof,
                                  const int64_t *__restrict__ off, const int64_t *__restrict__ master,
-                                 const double *__restrict__ w, int64_t n) {
+                                 const double *__restrict__ w, int64_t n, int64_t bs = 0) {
+  x += blockIdx.y * bs;  // batched (probe) vectors: blockIdx.y selects the vector
+  src += blockIdx.y * bs;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.;
     for (int64_t j = off[i]; j < off[i + 1]; ++j) s += w[j] * src[master[j]];
@@ -164,7 +166,8 @@ __global__ void k_csr_gather_set(double *x, const double *src, const int64_t *__
 // condensation onto masters: y[tm[i]] += sum_{j in [toff[i], toff[i+1])} tw[j] * y[tdof[j]]
 // (one thread per master, fixed order: deterministic)
 __global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const int64_t *__restrict__ toff,
-                               const int64_t *__restrict__ tdof, const double *__restrict__ tw, int64_t n) {
+                               const int64_t *__restrict__ tdof, const double *__restrict__ tw, int64_t n, int64_t bs = 0) {
+  y += blockIdx.y * bs;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     double s = 0.;
     for (int64_t j = toff[i]; j < toff[i + 1]; ++j) s += tw[j] * y[tdof[j]];
@@ -173,7 +176,9 @@ __global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const 
 }
 
 __global__ void k_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
-                                   const double *rb) {
+                                   const double *rb, int64_t bs = 0) {
+  y += blockIdx.y * bs;
+  v += blockIdx.y * bs;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = idx[j];
     y[i] = rb ? rb[i] - d[i] * v[i] : d[i] * v[i];
@@ -219,11 +224,17 @@ int multidot_work_size() { return (kDotChunk + 1) * kMaxBlocks; }
 // pressure node q: ev[slot] for slot in pslot[poff[q]..)
 __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ ev, const int64_t *__restrict__ voff,
                             const int64_t *__restrict__ vslot, int64_t nv, const int64_t *__restrict__ poff,
-                            const int64_t *__restrict__ pslot, int64_t np, int dim) {
+                            const int64_t *__restrict__ pslot, int64_t np, int dim, int64_t ys = 0, int64_t evs = 0,
+                            const uint8_t *__restrict__ act = nullptr, int64_t el = 1, int cb = 1, int nblk = 0) {
+  y += blockIdx.y * ys;
+  ev += blockIdx.y * evs;
+  if (act) act += (int64_t)blockIdx.y * nblk;  // batched probing: cell batches the kernel skipped hold 0
+  auto live = [&](int64_t slot) { return !act || act[slot / el / cb]; };
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nv) {
     double acc[3] = {0., 0., 0.};
     for (int64_t j = voff[i]; j < voff[i + 1]; ++j) {
+      if (!live(vslot[j])) continue;
       const double *e = ev + vslot[j];
       for (int c = 0; c < dim; ++c) acc[c] += e[c];
     }
@@ -231,7 +242,8 @@ __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ e
   } else if (i < nv + np) {
     const int64_t q = i - nv;
     double acc = 0.;
-    for (int64_t j = poff[q]; j < poff[q + 1]; ++j) acc += ev[pslot[j]];
+    for (int64_t j = poff[q]; j < poff[q + 1]; ++j)
+      if (live(pslot[j])) acc += ev[pslot[j]];
     y[dim * nv + q] = acc;
   }
 }
@@ -439,6 +451,17 @@ __global__ void k_set_const_indexed(double *x, const int32_t *idx, int64_t m, do
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < m) x[idx[i]] = a;
 }
+// batched probes p0 .. : V[(pid[e] - p0) * n + dofs[e]] = 1 (V zeroed) and the extraction
+// val[ent[e]] = Y[(pid[e] - p0) * n + row[e]]
+__global__ void k_probe_set_b(double *V, int64_t n, const int32_t *dofs, const int32_t *pid, int p0, int64_t m) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < m) V[(int64_t)(pid[e] - p0) * n + dofs[e]] = 1.0;
+}
+__global__ void k_probe_extract_b(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+                                  int64_t m, const double *Y, int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < m) val[ent[e]] = Y[(int64_t)(pid[e] - p0) * n + row[e]];
+}
 // CSR values of the entries whose column belongs to one probe: val[ent[i]] = y[row[i]]
 __global__ void k_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
                                 int add) {
@@ -468,6 +491,45 @@ hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_
 hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_const_indexed, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, x, idx, m, a);
+  return hipGetLastError();
+}
+hipError_t probe_set_batched(double *V, int64_t n, const int32_t *dofs, const int32_t *pid, int p0, int64_t m,
+                             hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_set_b, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, V, n, dofs, pid, p0, m);
+  return hipGetLastError();
+}
+hipError_t probe_extract_batched(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+                                 int64_t m, const double *Y, int64_t n, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_probe_extract_b, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, pid, p0, m, Y, n);
+  return hipGetLastError();
+}
+hipError_t vec_csr_gather_set_b(double *x, const int64_t *dof, const int64_t *off, const int64_t *master,
+                                const double *w, int64_t n, int nb, int64_t bs, hipStream_t s) {
+  if (n <= 0 || nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_csr_gather_set, dim3(grid_for(n), nb), dim3(kBlock), 0, s, x, x, dof, off, master, w, n, bs);
+  return hipGetLastError();
+}
+hipError_t vec_csr_condense_b(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
+                              int64_t n, int nb, int64_t bs, hipStream_t s) {
+  if (n <= 0 || nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_csr_condense, dim3(grid_for(n), nb), dim3(kBlock), 0, s, y, tm, toff, tdof, tw, n, bs);
+  return hipGetLastError();
+}
+hipError_t vec_gather_scale_set_b(double *y, const double *d, const double *v, const int64_t *idx, int64_t m, int nb,
+                                  int64_t bs, hipStream_t s) {
+  if (m <= 0 || nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_scale_set, dim3(grid_for(m), nb), dim3(kBlock), 0, s, y, d, v, idx, m, nullptr, bs);
+  return hipGetLastError();
+}
+hipError_t gather_element_vectors_b(double *y, const double *ev, const int64_t *voff, const int64_t *vslot, int64_t nv,
+                                    const int64_t *poff, const int64_t *pslot, int64_t np, int dim, int nb, int64_t ys,
+                                    int64_t evs, const uint8_t *act, int64_t el, int cb, int nblk, hipStream_t s) {
+  const int64_t n = nv + np;
+  if (n <= 0 || nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_ev, dim3((unsigned)((n + 255) / 256), nb), dim3(256), 0, s, y, ev, voff, vslot, nv, poff,
+                     pslot, np, dim, ys, evs, act, el, cb, nblk);
   return hipGetLastError();
 }
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,

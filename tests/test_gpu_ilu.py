@@ -3,6 +3,8 @@ setup_ILU gls_navier_stokes.cc:1161-1176): the CSR matrix it probes from the dev
 the oracle's assembled, constraint-eliminated system matrix (assemble_matrix_and_rhs, the matrix
 Trilinos factors in the reference), and ILU-preconditioned GMRES reaches the Jacobi-preconditioned
 Newton solution in far fewer iterations."""
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -65,10 +67,12 @@ def test_ilu_gmres_newton(dim, n, k, kp):
 @pytest.mark.parametrize("dim,n,k,kp,fill,rthresh,order,blk", [
     (2, 4, 1, 1, 0, 1.0, "cm", 0), (2, 4, 1, 1, 1, 1.0, "cm", 0), (2, 4, 1, 1, 4, 1.02, "cm", 0),
     (2, 3, 2, 1, 1, 1.0, "cm", 0), (3, 2, 1, 1, 1, 1.0, "cm", 0), (3, 2, 2, 2, 2, 1.0, "cm", 0),
-    (2, 4, 2, 1, 0, 1.0, "multicolor", 0), (3, 2, 2, 2, 0, 1.0, "multicolor", 200), (2, 6, 1, 1, 1, 1.0, "cm", 40)])
+    (2, 4, 2, 1, 0, 1.0, "multicolor", 0), (3, 2, 2, 2, 0, 1.0, "multicolor", 200), (2, 6, 1, 1, 1, 1.0, "cm", 40),
+    (3, 2, 2, 1, 0, 1.02, "multicolor", 0), (2, 4, 1, 1, 1, 1.0, "multicolor", 0)])
 def test_iluk_factors_match_oracle(dim, n, k, kp, fill, rthresh, order, blk):
     """ILU(fill) factors computed on the device (probe -> level-of-fill pattern -> Ifpack diagonal
-    perturbation -> rocSPARSE csrilu0) equal the oracle's Ifpack restatement (ilu_factor) of the
+    perturbation -> rocSPARSE csrilu0, or in multicolor order the color-by-color factorization
+    kernel) equal the oracle's Ifpack restatement (ilu_factor) of the
     oracle's assembled matrix in the factorization's numbering, on the device's pattern; that pattern
     holds the oracle's ILU(fill) graph of the matrix."""
     p = _cavity(dim, n, k, kp, "bdf1", 0.05)
@@ -156,3 +160,64 @@ def test_ilu_apply_is_the_factored_solve(dim, n, k, kp, order, blk):
     x = spla.spsolve_triangular(U, y, lower=False)
     zref = x[perm]
     assert np.abs(z - zref).max() <= 1e-10 * np.abs(zref).max(), np.abs(z - zref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,n,k,kp", [(3, 3, 2, 1), (2, 8, 2, 2)])
+def test_multicolor_factorization_equals_rocsparse(dim, n, k, kp):
+    """The multicolor order's color-by-color factorization (k_mc_ilu0: rows of earlier colors in
+    parallel, the node's own rows in order) and rocSPARSE csrilu0 on the same pattern and values
+    (GLS_ILU_ROCSPARSE_FACTOR=1) give the same factors."""
+    p = _cavity(dim, n, k, kp, "bdf1", 0.05)
+    rng = np.random.default_rng(SEED + 3)
+    u, u1 = (p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs)) for _ in range(2))
+    out = []
+    for env in ("1", None):
+        if env:
+            os.environ["GLS_ILU_ROCSPARSE_FACTOR"] = env
+        try:
+            ctx = context_for(p)
+            ctx.set_time("bdf1", p.time_steps)
+            ctx.set_state(cuda(u), cuda(u1))
+            ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
+            out.append(ctx.ilu_factors())
+        finally:
+            os.environ.pop("GLS_ILU_ROCSPARSE_FACTOR", None)
+    (p0, F0), (p1, F1) = out
+    assert np.array_equal(p0, p1)
+    F0, F1 = F0.tocsr(), F1.tocsr()
+    assert np.array_equal(F0.indptr, F1.indptr) and np.array_equal(F0.indices, F1.indices)
+    assert np.abs(F0.data - F1.data).max() <= 1e-12 * np.abs(F0.data).max()
+
+
+@pytest.mark.gpu
+def test_batched_probing_equals_probe_loop_with_hanging_and_slip_lines():
+    """The batched probe launches (per-cell path) give the same probed matrix as one
+    gls_jacobian_apply per probe (GLS_ILU_PROBE_LOOP=1) on an adapted mapped shell with hanging-node
+    and curved-slip constraint lines."""
+    from oracle.oracle import MappedProblem
+    from tests.test_dist_plan import _adapted_space
+    from tests.test_gpu_uforest import dof_lines
+    sp_ = _adapted_space(3, 2, 1)
+    lines = dof_lines(sp_)
+    p = MappedProblem(sp_, viscosity=1.0, scheme="steady")
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)
+    p.set_dirichlet([("function", 0, rot), ("noslip", 1, None), ("slip", 2, None), ("slip", 3, None)])
+    rng = np.random.default_rng(SEED + 5)
+    x0 = p.apply_nonzero_constraints(0.1 * rng.standard_normal(p.n_dofs))
+    out = []
+    for env in (None, "1"):
+        if env:
+            os.environ["GLS_ILU_PROBE_LOOP"] = env
+        try:
+            g = context_for(p)
+            g.attach_ilu(1e-12, 1.0)
+            g.set_state(cuda(x0))
+            out.append(g.ilu_matrix().tocsr())
+        finally:
+            os.environ.pop("GLS_ILU_PROBE_LOOP", None)
+    a, b = out
+    assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
+    assert np.abs(a.data - b.data).max() <= 1e-14 * np.abs(b.data).max()
