@@ -2177,7 +2177,7 @@ static int ilu_probe_batched(gls_ctx *c) {
   }
   if (c->hang.on && I.bC.n < (size_t)B * n) GLS_TRY(I.bC.alloc((size_t)B * n));
   if (c->bev.n < (size_t)B * evs) GLS_TRY(c->bev.alloc((size_t)B * evs));
-  const int cb = gls::cell_kernel_cells_per_block(dim, c->k, c->nq1d), nblk = (c->n_cells + cb - 1) / cb;
+  const int cb = gls::cell_kernel_cells_per_block(dim, c->k, c->nq1d, true), nblk = (c->n_cells + cb - 1) / cb;
   if (c->bact.n < (size_t)B * nblk) GLS_TRY(c->bact.alloc((size_t)B * nblk));
   if (I.fill > 0) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
   for (int p0 = 0; p0 < I.n_probes; p0 += B) {

@@ -64,6 +64,11 @@
 #define GLS_QD_PREFETCH 0
 #endif
 
+#ifndef GLS_TEST_PAIR
+#define GLS_TEST_PAIR 1  // StageLayout bits (1 FP64 cached J.v, 2 FP32): two test fields per integration pass
+                         // (FP64 J.v 2.96 -> 2.89 ms at 128^3; FP32 no change, profiles/r03_ab_test_pair.txt)
+#endif
+
 #ifndef GLS_REDUCE_NODE
 #define GLS_REDUCE_NODE 1  // brick reduction: one thread per node (4 fields) instead of per (node, field)
 #endif
@@ -132,8 +137,10 @@ struct StageLayout {
   static constexpr int BIT = CACHED ? (sizeof(Real) == 8 ? 1 : 2) : (MODE == MODE_RESIDUAL ? 4 : 8);
   static constexpr bool ORIENTED = (GLS_STAGE_LAYOUT & BIT) != 0;  // else natural arrays
   static constexpr bool PAIR = ORIENTED && sizeof(Real) == 8 && K1 == 3;
+  // two test fields integrated side by side (their z / y / x stages share the LDS round trips)
+  static constexpr bool TPAIR = CACHED && (GLS_TEST_PAIR & BIT) != 0;
   static constexpr int LP = K1 == 3 ? 4 : K1;            // padded line length (non-pair layouts)
-  static constexpr int NXA = CACHED ? 4 : 5, NYA = CACHED ? 4 : 6;  // X / Y arrays in flight
+  static constexpr int NXA = CACHED ? (TPAIR ? 8 : 4) : 5, NYA = CACHED ? (TPAIR ? 6 : 4) : 6;  // X / Y arrays
   static constexpr int XP = (NXA + 1) / 2, YP = (NYA + 1) / 2;
   static constexpr int YB = PAIR ? 2 * XP : NXA;        // slot of Y array 0
   static constexpr int A0 = 18, H1 = 44, PB = 62;       // pair block: halves at 0 / A0, e2 plane at H1
@@ -788,41 +795,62 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   row(4, i1, cd1);
   row(3, i0, cb0);
   row(4, i0, cd0);
+  // FS test fields per pass (SL::TPAIR: 2, slots 4u.., YB + 3u.., 2u.. for field f0 + u)
+  constexpr int FS = SL::TPAIR ? 2 : 1;
 #pragma unroll
-  for (int fld = 0; fld < 4; ++fld) {
-    if (GLS_ABL & 4) { if (pact) Out(pci, fld)[me] = Tc[4 * fld] + Tc[4 * fld + 1] + Tc[4 * fld + 2] + Tc[4 * fld + 3]; continue; }
+  for (int f0 = 0; f0 < 4; f0 += FS) {
+    if (GLS_ABL & 4) {
+      for (int u = 0; u < FS; ++u) {
+        const int fld = f0 + u;
+        if (pact) Out(pci, fld)[me] = Tc[4 * fld] + Tc[4 * fld + 1] + Tc[4 * fld + 2] + Tc[4 * fld + 3];
+      }
+      continue;
+    }
     if (pact) {
-      wr(0, 2, Tc[4 * fld]);
-      wr(1, 2, Tc[4 * fld + 1]);
-      wr(2, 2, Tc[4 * fld + 2]);
-      wr(3, 2, Tc[4 * fld + 3]);
+#pragma unroll
+      for (int u = 0; u < FS; ++u) {
+        const int fld = f0 + u;
+        wr(4 * u + 0, 2, Tc[4 * fld]);
+        wr(4 * u + 1, 2, Tc[4 * fld + 1]);
+        wr(4 * u + 2, 2, Tc[4 * fld + 2]);
+        wr(4 * u + 3, 2, Tc[4 * fld + 3]);
+      }
     }
     wave_sync();
     if (pact) {  // transposed z (output index az = i2): Z0 = B^T Tv + D^T Tz, Z1 = B^T Tx, Z2 = B^T Ty
-      Real tv[K1], tx[K1], ty[K1], tz[K1];
-      rdl(0, 2, tv);
-      rdl(1, 2, tx);
-      rdl(2, 2, ty);
-      rdl(3, 2, tz);
-      wr(SL::YB + 0, 1, dot(cb2, tv) + dot(cd2, tz));
-      wr(SL::YB + 1, 1, dot(cb2, tx));
-      wr(SL::YB + 2, 1, dot(cb2, ty));
+#pragma unroll
+      for (int u = 0; u < FS; ++u) {
+        Real tv[K1], tx[K1], ty[K1], tz[K1];
+        rdl(4 * u + 0, 2, tv);
+        rdl(4 * u + 1, 2, tx);
+        rdl(4 * u + 2, 2, ty);
+        rdl(4 * u + 3, 2, tz);
+        wr(SL::YB + 3 * u + 0, 1, dot(cb2, tv) + dot(cd2, tz));
+        wr(SL::YB + 3 * u + 1, 1, dot(cb2, tx));
+        wr(SL::YB + 3 * u + 2, 1, dot(cb2, ty));
+      }
     }
     wave_sync();
     if (pact) {  // transposed y (ay = i1): W0 = B^T Z0 + D^T Z2, W1 = B^T Z1
-      Real z0[K1], z1[K1], z2[K1];
-      rdl(SL::YB + 0, 1, z0);
-      rdl(SL::YB + 1, 1, z1);
-      rdl(SL::YB + 2, 1, z2);
-      wr(0, 0, dot(cb1, z0) + dot(cd1, z2));
-      wr(1, 0, dot(cb1, z1));
+#pragma unroll
+      for (int u = 0; u < FS; ++u) {
+        Real z0[K1], z1[K1], z2[K1];
+        rdl(SL::YB + 3 * u + 0, 1, z0);
+        rdl(SL::YB + 3 * u + 1, 1, z1);
+        rdl(SL::YB + 3 * u + 2, 1, z2);
+        wr(2 * u + 0, 0, dot(cb1, z0) + dot(cd1, z2));
+        wr(2 * u + 1, 0, dot(cb1, z1));
+      }
     }
     wave_sync();
     if (pact) {  // transposed x (ax = i0): out = B^T W0 + D^T W1
-      Real w0[K1], w1[K1];
-      rdl(0, 0, w0);
-      rdl(1, 0, w1);
-      Out(pci, fld)[me] = dot(cb0, w0) + dot(cd0, w1);
+#pragma unroll
+      for (int u = 0; u < FS; ++u) {
+        Real w0[K1], w1[K1];
+        rdl(2 * u + 0, 0, w0);
+        rdl(2 * u + 1, 0, w1);
+        Out(pci, f0 + u)[me] = dot(cb0, w0) + dot(cd0, w1);
+      }
     }
     wave_sync();
   }

@@ -26,20 +26,20 @@
 
 namespace gls {
 
-template <int DIM, int K, int KP, int NQ1>
+template <int DIM, int K, int KP, int NQ1, int TPB = 256>
 struct Cfg {
   static constexpr int NV = ipow(K + 1, DIM);
   static constexpr int NP = ipow(KP + 1, DIM);
   static constexpr int NQ = ipow(NQ1, DIM);
-  static constexpr int CB = 256 / NQ;
+  static constexpr int CB = TPB / NQ;  // cells per workgroup (TPB = 64: the batched probe launches)
   static constexpr int NT = DIM * (DIM + 1) + DIM + 1;  // test coefficients per q
   static constexpr int K1 = K + 1, KP1 = KP + 1;
   static constexpr int TABN = 5 * kMaxQ1D * kMaxNodes1D + 2 * kMaxQ1D;
 };
 
-template <int DIM, int K, int KP, int NQ1, int MODE, bool GEN = false>
-__global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const Tables1D T) {
-  using C = Cfg<DIM, K, KP, NQ1>;
+template <int DIM, int K, int KP, int NQ1, int MODE, bool GEN = false, int TPB = 256>
+__global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const Tables1D T) {
+  using C = Cfg<DIM, K, KP, NQ1, TPB>;
   constexpr int NV = C::NV, NP = C::NP, NQ = C::NQ, CB = C::CB, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *sTab = smem;                              // Tables1D copy
@@ -553,9 +553,9 @@ __global__ void __launch_bounds__(256) gls_cell_kernel(const OpParams P, const T
   }
 }
 
-template <int DIM, int K, int KP, int NQ1>
+template <int DIM, int K, int KP, int NQ1, int TPB = 256>
 size_t cell_kernel_lds_bytes() {
-  using C = Cfg<DIM, K, KP, NQ1>;
+  using C = Cfg<DIM, K, KP, NQ1, TPB>;
   size_t n = ((C::TABN + 1) & ~1) + C::CB * C::NV * DIM + C::CB * C::NP + 3 * C::CB * C::NV * DIM +
              C::CB * C::NV * DIM + C::CB * C::NP + C::CB * C::NQ * C::NT;
   return n * sizeof(double);
@@ -581,6 +581,15 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
       hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_RESIDUAL, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
       break;
     case MODE_JV:
+      if (P.bv_stride) {  // batched probes: small workgroups, so that more (probe, cell batch) pairs skip
+        using C64 = Cfg<DIM, K, KP, NQ1, 64>;
+        if constexpr (C64::CB >= 1) {
+          hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64>),
+                             dim3((P.n_cells + C64::CB - 1) / C64::CB, P.n_probe), dim3(64),
+                             (cell_kernel_lds_bytes<DIM, K, KP, NQ1, 64>()), s, P, T);
+          break;
+        }
+      }
       hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks, P.bv_stride ? P.n_probe : 1),
                          dim3(256), lds, s, P, T);
       break;
@@ -612,11 +621,11 @@ hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const 
   return hipErrorNotSupported;
 }
 
-int cell_kernel_cells_per_block(int dim, int k, int nq1d) {
+int cell_kernel_cells_per_block(int dim, int k, int nq1d, bool probe) {
   (void)k;
   int nq = 1;
   for (int d = 0; d < dim; ++d) nq *= nq1d;
-  return 256 / nq;  // Cfg<>::CB
+  return probe && nq <= 64 ? 64 / nq : 256 / nq;  // Cfg<>::CB of the launch launch_cell_g picks
 }
 
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d) {

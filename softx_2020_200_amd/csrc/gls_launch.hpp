@@ -10,7 +10,7 @@ hipError_t gather_element_vectors(double *y, const double *ev, const int64_t *vo
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s);
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
-int cell_kernel_cells_per_block(int dim, int k, int nq1d);  // cells of one per-cell kernel workgroup
+int cell_kernel_cells_per_block(int dim, int k, int nq1d, bool probe = false);  // cells per workgroup
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
