@@ -1756,7 +1756,7 @@ struct Solver {
       // ordering: Cuthill-McKee as the reference factors; above kIluMulticolorDofs, and across ranks
       // (where the block-Jacobi ILU does not reproduce the single-rank iteration counts anyway), the
       // multicolor order, whose triangular solves are ~60x faster on the GPU
-      // (profiles/r03_ilu_multicolor_ab.txt) at the price of more GMRES iterations (--ilu-order overrides)
+      // (profiles/r03_app_cylinder3d_ilu_timing.log vs r03_app_cylinder3d_multicolor_ilu.log) at the price of more GMRES iterations (--ilu-order overrides)
       const int order = ilu_order >= 0 ? ilu_order
                         : (m.n_dofs() > kIluMulticolorDofs || world > 1 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM);
       ck(gls_ilu_set_options(ctx, order, ilu_block_dofs), "gls_ilu_set_options");

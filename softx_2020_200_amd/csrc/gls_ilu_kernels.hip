@@ -7,7 +7,7 @@
 // row's entries of the other colors (a gather-dot, HBM / L2 bound), then lane 0 resolves the <= 4
 // rows of the node in order. The dependency chain of a solve is the number of colors, where the
 // general level-scheduled csrsv of a Cuthill-McKee-ordered 3D Q2 matrix waits on thousands of
-// levels (profiles/r03_ilu_multicolor_ab.txt).
+// levels (profiles/r03_app_cylinder3d_ilu_timing.log vs r03_app_cylinder3d_multicolor_ilu.log).
 #include "gls_launch.hpp"
 
 namespace gls {
