@@ -15,6 +15,7 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include <set>
 
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -373,6 +374,7 @@ struct gls_ctx {
     // color-by-color solves of gls_ilu_kernels.hip replace rocSPARSE csrsv
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
+    int mc_waves = 1;        // wavefronts per node group in the color solves (4 for long rows)
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
     DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
     DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
@@ -2299,7 +2301,8 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
   if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
     HIP_TRY(gls::ilu_mc_solve(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
-                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, c->stream));
+                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_waves,
+                              c->stream));
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
@@ -3676,8 +3679,45 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     // is ~colors x DoFs per node. (Blocks only drop couplings here: the colors stay outermost.)
     std::vector<int> c1((size_t)nu, -1), used;
     int ncl = 0;
-    for (int64_t t = 0; t < n; ++t) {
-      const int64_t x = dnode_[(size_t)order[(size_t)t]];
+    // visit order of the greedy coloring: Cuthill-McKee (default) or smallest-last (GLS_ILU_COLORING=sl:
+    // nodes removed by minimum remaining degree, colored in reverse removal order -- fewer colors)
+    std::vector<int64_t> visit;
+    visit.reserve((size_t)nu);
+    const char *cm_env = std::getenv("GLS_ILU_COLORING");
+    if (cm_env && !std::strcmp(cm_env, "sl")) {
+      std::vector<int64_t> deg((size_t)nu, 0);
+      for (int64_t x = 0; x < nu; ++x)
+        for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) deg[(size_t)x] += n1[(size_t)u] != x;
+      std::set<std::pair<int64_t, int64_t>> q;
+      for (int64_t x = 0; x < nu; ++x) q.insert({deg[(size_t)x], x});
+      std::vector<char> gone((size_t)nu, 0);
+      std::vector<int64_t> removal;
+      removal.reserve((size_t)nu);
+      while (!q.empty()) {
+        const auto it = q.begin();
+        const int64_t x = it->second;
+        q.erase(it);
+        gone[(size_t)x] = 1;
+        removal.push_back(x);
+        for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) {
+          const int64_t y = n1[(size_t)u];
+          if (y == x || gone[(size_t)y]) continue;
+          q.erase({deg[(size_t)y], y});
+          q.insert({--deg[(size_t)y], y});
+        }
+      }
+      visit.assign(removal.rbegin(), removal.rend());
+    } else {
+      std::vector<char> seen((size_t)nu, 0);
+      for (int64_t t = 0; t < n; ++t) {
+        const int64_t x = dnode_[(size_t)order[(size_t)t]];
+        if (!seen[(size_t)x]) {
+          seen[(size_t)x] = 1;
+          visit.push_back(x);
+        }
+      }
+    }
+    for (const int64_t x : visit) {
       if (c1[(size_t)x] >= 0) continue;
       for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) {
         const int cy = c1[(size_t)n1[(size_t)u]];
@@ -3782,6 +3822,10 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       int32_t maxrow = 0;
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
       I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
+      // a group's entries over one wave's lanes: 4 waves once a group has more than a few hundred
+      const double per_group = (double)rowp[(size_t)n] / (double)std::max<size_t>(1, grow.size() - 1);
+      I.mc_waves = per_group > 320.0 ? 4 : 1;
+      if (const char *e = std::getenv("GLS_ILU_SOLVE_WAVES")) I.mc_waves = std::atoi(e) >= 4 ? 4 : 1;
     }
   }
   // probes: one per (color, slot); every entry of the system matrix is read from the probe of its

@@ -3,9 +3,9 @@
 //
 // In that order the DoFs of one color belong to nodes that share no matrix entry, so inside a color
 // a row depends on rows of earlier colors (forward) / later colors (backward) and on the rows of its
-// own node only. One launch per color, one wavefront per node group: the 64 lanes stride over the
-// row's entries of the other colors (a gather-dot, HBM / L2 bound), then lane 0 resolves the <= 4
-// rows of the node in order. The dependency chain of a solve is the number of colors, where the
+// own node only. One launch per color, one or four wavefronts per node group: the group's threads
+// stride over its rows' entries of the other colors (a gather-dot), then one thread resolves the
+// <= 4 rows of the node in order. The dependency chain of a solve is the number of colors, where the
 // general level-scheduled csrsv of a Cuthill-McKee-ordered 3D Q2 matrix waits on thousands of
 // levels (profiles/r03_app_cylinder3d_ilu_timing.log vs r03_app_cylinder3d_multicolor_ilu.log).
 #include "gls_launch.hpp"
@@ -13,7 +13,6 @@
 namespace gls {
 
 namespace {
-constexpr int kGroupsPerBlock = 4;  // 256 threads = 4 wavefronts = 4 node groups
 
 __device__ __forceinline__ double wave_sum(double s) {
 #pragma unroll
@@ -21,67 +20,133 @@ __device__ __forceinline__ double wave_sum(double s) {
   return s;
 }
 
-// forward: y_i = b_i - sum_{j < i} L_ij y_j (unit lower); entries [rowp_i, lsp_i) lie in earlier colors,
-// [lsp_i, didx_i) in the row's own node
-__global__ void __launch_bounds__(256) k_mc_lower(const int32_t *__restrict__ grow, int g0, int g1,
-                                                  const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
-                                                  const double *__restrict__ val, const int32_t *__restrict__ lsp,
-                                                  const int32_t *__restrict__ didx, const double *__restrict__ b,
-                                                  double *__restrict__ y) {
-  const int lane = threadIdx.x & 63;
-  const int g = g0 + (int)blockIdx.x * kGroupsPerBlock + (int)(threadIdx.x >> 6);
-  if (g >= g1) return;
-  const int r0 = grow[g], r1 = grow[g + 1];
-  double part[kMaxGroupRows];
+// One launch per color; WPG wavefronts per node group (1 for short rows, 4 for the ~200-entry rows
+// of 3D Q2 matrices, where a single wave would walk each row's other-color entries in several
+// dependent load rounds). The rows of a group are contiguous in the CSR, so the group's threads
+// stride over its whole entry range at once (all <= 4 rows, kGatherUnroll entries per thread in
+// flight) and mask entries outside a row's other-color segment before the x gather. Thread 0 of the
+// group loads its serial-part operands (right-hand sides, the <= 3 own-node entries per row, the
+// diagonal) before the gather so they are in flight with it, and keeps the rows it has resolved in
+// registers: the only dependent global traffic left is the gather.
+constexpr int kGatherUnroll = 4;
+constexpr int kOwnMax = kMaxGroupRows - 1;  // own-node entries per row besides the diagonal
+
+__device__ __forceinline__ double pick4(const double *a, int j) {
+  return j == 0 ? a[0] : j == 1 ? a[1] : j == 2 ? a[2] : a[3];
+}
+
+// LOWER: y_i = b_i - sum_{j < i} L_ij y_j (unit lower); entries [rowp_i, sp_i) lie in earlier colors,
+//        [sp_i, didx_i) in the row's own node (sp = lsp).
+// upper: x_i = (y_i - sum_{j > i} U_ij x_j) / U_ii; entries [sp_i, rowp_{i+1}) lie in later colors,
+//        (didx_i, sp_i) in the row's own node (sp = usp).
+// In both, the gathered vector is the output (x / y of the other colors, already final).
+template <int WPG, bool LOWER>
+__global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow, int g0, int g1,
+                                                const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
+                                                const double *__restrict__ val, const int32_t *__restrict__ sp,
+                                                const int32_t *__restrict__ didx, const double *__restrict__ rhs,
+                                                double *__restrict__ out) {
+  constexpr int GPB = 4 / WPG;  // node groups per 256-thread block
+  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int gl = w / WPG, tig = (w % WPG) * 64 + lane;
+  const int g = g0 + (int)blockIdx.x * GPB + gl;
+  const bool live = g < g1;
+  __shared__ double red[4][kMaxGroupRows];
+  int r0 = 0, nr = 0;
+  if (live) {
+    r0 = grow[g];
+    nr = grow[g + 1] - r0;
+  }
+  int32_t bnd[kMaxGroupRows], lo[kMaxGroupRows], hi[kMaxGroupRows];
 #pragma unroll
   for (int t = 0; t < kMaxGroupRows; ++t) {
-    double s = 0.0;
-    if (r0 + t < r1) {
-      const int i = r0 + t;
-      for (int e = rowp[i] + lane; e < lsp[i]; e += 64) s += val[e] * y[col[e]];
-    }
-    part[t] = wave_sum(s);
+    const bool in = t < nr;
+    bnd[t] = in ? rowp[r0 + t] : INT32_MAX;
+    lo[t] = !in ? 0 : LOWER ? rowp[r0 + t] : sp[r0 + t];
+    hi[t] = !in ? 0 : LOWER ? sp[r0 + t] : rowp[r0 + t + 1];
   }
-  if (lane == 0) {
-    for (int t = 0; t < r1 - r0; ++t) {
+  // serial-part operands (thread 0 of the group)
+  double rb[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0}, dg[kMaxGroupRows] = {1.0, 1.0, 1.0, 1.0};
+  double ov[kMaxGroupRows][kOwnMax];
+  int oc[kMaxGroupRows][kOwnMax];
+  if (tig == 0) {
+#pragma unroll
+    for (int t = 0; t < kMaxGroupRows; ++t) {
       const int i = r0 + t;
-      double s = b[i] - part[t];
-      for (int e = lsp[i]; e < didx[i]; ++e) s -= val[e] * y[col[e]];
-      y[i] = s;
+      const bool in = t < nr;
+      const int d = in ? didx[i] : 0;
+      const int ob = !in ? 0 : LOWER ? sp[i] : d + 1, oe = !in ? 0 : LOWER ? d : sp[i];
+      rb[t] = in ? rhs[i] : 0.0;
+      if (!LOWER) dg[t] = in ? val[d] : 1.0;
+#pragma unroll
+      for (int k = 0; k < kOwnMax; ++k) {
+        const bool ok = ob + k < oe;
+        ov[t][k] = ok ? val[ob + k] : 0.0;
+        oc[t][k] = ok ? col[ob + k] - r0 : 0;
+      }
     }
+  }
+  // other-color gather-dot
+  double acc[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0};
+  const int eb = live ? rowp[r0] : 0, ee = live ? rowp[r0 + nr] : 0;
+  for (int e0 = eb + tig; e0 < ee; e0 += 64 * WPG * kGatherUnroll) {
+    int c[kGatherUnroll], tt[kGatherUnroll];
+    double v[kGatherUnroll], xv[kGatherUnroll];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int e = e0 + 64 * WPG * u;
+      const int t = (e >= bnd[1]) + (e >= bnd[2]) + (e >= bnd[3]);
+      const int l = t == 0 ? lo[0] : t == 1 ? lo[1] : t == 2 ? lo[2] : lo[3];
+      const int h = t == 0 ? hi[0] : t == 1 ? hi[1] : t == 2 ? hi[2] : hi[3];
+      const bool ok = e < ee && e >= l && e < h;
+      tt[u] = ok ? t : -1;
+      c[u] = ok ? col[e] : 0;
+      v[u] = ok ? val[e] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) xv[u] = tt[u] >= 0 ? out[c[u]] : 0.0;
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const double p = v[u] * xv[u];
+#pragma unroll
+      for (int r = 0; r < kMaxGroupRows; ++r) acc[r] += tt[u] == r ? p : 0.0;
+    }
+  }
+  double part[kMaxGroupRows];
+#pragma unroll
+  for (int r = 0; r < kMaxGroupRows; ++r) part[r] = wave_sum(acc[r]);
+  if (WPG > 1) {
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < kMaxGroupRows; ++r) red[w][r] = part[r];
+    }
+    __syncthreads();
+    if (tig == 0) {
+#pragma unroll
+      for (int r = 0; r < kMaxGroupRows; ++r) {
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < WPG; ++k) sum += red[gl * WPG + k][r];
+        part[r] = sum;
+      }
+    }
+  }
+  if (tig != 0 || !live) return;
+  // the node's own rows (forward in order, backward in reverse), resolved values kept in registers
+  double res[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < kMaxGroupRows; ++q) {
+    const int t = LOWER ? q : kMaxGroupRows - 1 - q;
+    if (t >= nr) continue;
+    double s = rb[t] - part[t];
+#pragma unroll
+    for (int k = 0; k < kOwnMax; ++k) s -= ov[t][k] * pick4(res, oc[t][k]);
+    const double r = LOWER ? s : s / dg[t];
+    res[t] = r;
+    out[r0 + t] = r;
   }
 }
 
-// backward: x_i = (y_i - sum_{j > i} U_ij x_j) / U_ii; entries [usp_i, rowp_{i+1}) lie in later colors,
-// (didx_i, usp_i) in the row's own node
-__global__ void __launch_bounds__(256) k_mc_upper(const int32_t *__restrict__ grow, int g0, int g1,
-                                                  const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
-                                                  const double *__restrict__ val, const int32_t *__restrict__ usp,
-                                                  const int32_t *__restrict__ didx, const double *__restrict__ y,
-                                                  double *__restrict__ x) {
-  const int lane = threadIdx.x & 63;
-  const int g = g0 + (int)blockIdx.x * kGroupsPerBlock + (int)(threadIdx.x >> 6);
-  if (g >= g1) return;
-  const int r0 = grow[g], r1 = grow[g + 1];
-  double part[kMaxGroupRows];
-#pragma unroll
-  for (int t = 0; t < kMaxGroupRows; ++t) {
-    double s = 0.0;
-    if (r0 + t < r1) {
-      const int i = r0 + t;
-      for (int e = usp[i] + lane; e < rowp[i + 1]; e += 64) s += val[e] * x[col[e]];
-    }
-    part[t] = wave_sum(s);
-  }
-  if (lane == 0) {
-    for (int t = r1 - r0 - 1; t >= 0; --t) {
-      const int i = r0 + t;
-      double s = y[i] - part[t];
-      for (int e = didx[i] + 1; e < usp[i]; ++e) s -= val[e] * x[col[e]];
-      x[i] = s / val[didx[i]];
-    }
-  }
-}
 constexpr int kIluPrefetch = 4;
 // first position q in [lo, hi) of the sorted column list c with c[q] == j, else -1
 __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_t j) {
@@ -236,18 +301,22 @@ hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n
 
 hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                         const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, hipStream_t s) {
+                        const int32_t *didx, const double *b, double *y, double *x, int waves_per_group,
+                        hipStream_t s) {
+  const int wpg = waves_per_group >= 4 ? 4 : 1, gpb = 4 / wpg;
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
-    const unsigned nb = (unsigned)((g1 - g0 + kGroupsPerBlock - 1) / kGroupsPerBlock);
-    hipLaunchKernelGGL(k_mc_lower, dim3(nb), dim3(64 * kGroupsPerBlock), 0, s, grow, g0, g1, rowp, col, val, lsp, didx, b, y);
+    const unsigned nb = (unsigned)((g1 - g0 + gpb - 1) / gpb);
+    if (wpg == 4) hipLaunchKernelGGL((k_mc_tri<4, true>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, lsp, didx, b, y);
+    else hipLaunchKernelGGL((k_mc_tri<1, true>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, lsp, didx, b, y);
   }
   for (int c = n_colors - 1; c >= 0; --c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
-    const unsigned nb = (unsigned)((g1 - g0 + kGroupsPerBlock - 1) / kGroupsPerBlock);
-    hipLaunchKernelGGL(k_mc_upper, dim3(nb), dim3(64 * kGroupsPerBlock), 0, s, grow, g0, g1, rowp, col, val, usp, didx, y, x);
+    const unsigned nb = (unsigned)((g1 - g0 + gpb - 1) / gpb);
+    if (wpg == 4) hipLaunchKernelGGL((k_mc_tri<4, false>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, usp, didx, y, x);
+    else hipLaunchKernelGGL((k_mc_tri<1, false>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, usp, didx, y, x);
   }
   return hipGetLastError();
 }

@@ -102,7 +102,8 @@ hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n
                          double boost_val, hipStream_t s);
 hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                         const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, hipStream_t s);
+                        const int32_t *didx, const double *b, double *y, double *x, int waves_per_group,
+                        hipStream_t s);
 hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
 hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
 hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
