@@ -374,7 +374,10 @@ struct gls_ctx {
     // color-by-color solves of gls_ilu_kernels.hip replace rocSPARSE csrsv
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
-    int mc_waves = 1;        // wavefronts per node group in the color solves (4 for long rows)
+    std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
+    int mc_stages = 6;                  // factorization: pivot rows in flight (MAP kernel)
+    DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
+    DevBuf<uint16_t> mc_map;   // per (row, pivot, upper entry of the pivot row): position in the row
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
     DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
     DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
@@ -2275,7 +2278,8 @@ static int ensure_ilu(gls_ctx *c) {
   RS_TRY(rocsparse_set_stream(I.h, s));
   if (I.mc_factor)
     HIP_TRY(gls::ilu_mc_factor(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
-                               I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, s));
+                               I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, I.mc_moff.p,
+                               I.mc_map.n ? I.mc_map.p : nullptr, I.mc_stages, s));
   else
     RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
   I.valid = true;
@@ -2301,8 +2305,8 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
   if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
     HIP_TRY(gls::ilu_mc_solve(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
-                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_waves,
-                              c->stream));
+                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_wl.data(),
+                              I.mc_wu.data(), c->stream));
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
@@ -3788,6 +3792,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   // one color (fill 0; fill-in can create such entries: then rocSPARSE csrsv solves)
   I.mc_solve = false;
   I.mc_factor = false;
+  std::vector<int64_t> mc_moff_h;  // position map offsets (empty: no map)
   if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
     const int ncl = I.n_order_colors;
     std::vector<int32_t> cstart((size_t)ncl + 2, (int32_t)n), grow, cg((size_t)ncl + 1, 0), lsp((size_t)n), usp((size_t)n);
@@ -3822,10 +3827,41 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       int32_t maxrow = 0;
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
       I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
-      // a group's entries over one wave's lanes: 4 waves once a group has more than a few hundred
-      const double per_group = (double)rowp[(size_t)n] / (double)std::max<size_t>(1, grow.size() - 1);
-      I.mc_waves = per_group > 320.0 ? 4 : 1;
-      if (const char *e = std::getenv("GLS_ILU_SOLVE_WAVES")) I.mc_waves = std::atoi(e) >= 4 ? 4 : 1;
+      if (I.mc_factor) {  // the position map (uint16 per entry), when it fits a quarter of free memory
+        mc_moff_h.assign((size_t)n + 1, 0);
+        for (int64_t r = 0; r < n; ++r) {
+          int64_t m = 0;
+          for (int32_t e = rowp[(size_t)r]; e < lsp[(size_t)r]; ++e) {
+            const int32_t k = col[(size_t)e];
+            m += rowp[(size_t)k + 1] - didx[(size_t)k] - 1;
+          }
+          mc_moff_h[(size_t)r + 1] = mc_moff_h[(size_t)r] + m;
+        }
+        size_t fr = 0, tot = 0;
+        const char *me = std::getenv("GLS_ILU_FACTOR_MAP");
+        if ((me && std::atoi(me) == 0) || hipMemGetInfo(&fr, &tot) != hipSuccess ||
+            (double)mc_moff_h[(size_t)n] * 2.0 > 0.25 * (double)fr)
+          mc_moff_h.clear();
+      }
+      // per color and direction: one wavefront per node group while a group's other-color entries
+      // fit a few passes of 64 lanes, else four (long rows: the late colors' L parts, the early
+      // colors' U parts)
+      I.mc_wl.assign((size_t)ncl, 1);
+      I.mc_wu.assign((size_t)ncl, 1);
+      const char *we = std::getenv("GLS_ILU_SOLVE_WAVES");
+      for (int c = 0; c < ncl; ++c) {
+        const int32_t ra = grow[(size_t)cg[(size_t)c]], rb = grow[(size_t)cg[(size_t)c + 1]];
+        const int ng = cg[(size_t)c + 1] - cg[(size_t)c];
+        int64_t nlo = 0, nup = 0;
+        for (int32_t r = ra; r < rb; ++r) {
+          nlo += lsp[(size_t)r] - rowp[(size_t)r];
+          nup += rowp[(size_t)r + 1] - usp[(size_t)r];
+        }
+        I.mc_wl[(size_t)c] = (uint8_t)(ng && nlo > 256 * (int64_t)ng ? 4 : 1);
+        I.mc_wu[(size_t)c] = (uint8_t)(ng && nup > 256 * (int64_t)ng ? 4 : 1);
+        if (we) I.mc_wl[(size_t)c] = I.mc_wu[(size_t)c] = (uint8_t)(std::atoi(we) >= 4 ? 4 : 1);
+      }
+      if (const char *se = std::getenv("GLS_ILU_STAGES")) I.mc_stages = std::atoi(se);
     }
   }
   // probes: one per (color, slot); every entry of the system matrix is read from the probe of its
@@ -3871,6 +3907,13 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   GLS_TRY(I.col.upload(col.data(), col.size()));
   GLS_TRY(I.didx.upload(didx.data(), didx.size()));
   GLS_TRY(I.perm.upload(newidx.data(), newidx.size()));
+  I.mc_map.release();
+  I.mc_moff.release();
+  if (!mc_moff_h.empty()) {
+    GLS_TRY(I.mc_moff.upload(mc_moff_h.data(), mc_moff_h.size()));
+    GLS_TRY(I.mc_map.alloc((size_t)mc_moff_h.back() + 256));  // + the clamped index of empty stages
+    HIP_TRY(gls::ilu_mc_factor_map(n, I.rowp.p, I.col.p, I.mc_lsp.p, I.didx.p, I.mc_moff.p, I.mc_map.p, c->stream));
+  }
   // ghost DoFs are not probed (identity rows): drop them from the unit lists, remember their diagonals
   {
     std::vector<int32_t> pd2;

@@ -148,6 +148,8 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow
 }
 
 constexpr int kIluPrefetch = 4;
+// pivot rows in flight in the factorization (template NS): 3 for the searching kernel, whose step is
+// long; more for the MAP kernel, whose step is a few LDS operations
 // first position q in [lo, hi) of the sorted column list c with c[q] == j, else -1
 __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_t j) {
   while (lo < hi) {
@@ -165,14 +167,26 @@ __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_
 // the rows of earlier colors are final, so each row's updates from them run in parallel (phase 1, the
 // bulk); the couplings inside the node (own-node rows, lower than i) follow row by row (phase 2) from
 // the workgroup's LDS copy of the group. Rows of up to kIluMaxRow entries (the caller checks).
+//
+// MAP: the row positions the upper entries of each pivot row land on (found by the column searches)
+// depend on the pattern only; gls_ilu_attach precomputes them once (k_mc_ilu0_map, uint16 per
+// (row, pivot, upper entry), 0xffff where the entry is outside the row's pattern), and the
+// factorization streams them with the upper values instead of searching: the step's LDS chain
+// shrinks to sv[p] / U_kk and one read-modify-write per lane. Same updates in the same order, so the
+// factors are bitwise those of the searching kernel.
+constexpr uint16_t kMapMiss = 0xffff;
+template <bool MAP, int NS>
 __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *__restrict__ grow, int g0, int g1,
                                                                 const int32_t *__restrict__ rowp,
                                                                 const int32_t *__restrict__ col, double *__restrict__ val,
                                                                 const int32_t *__restrict__ lsp,
                                                                 const int32_t *__restrict__ didx, double boost_tol,
-                                                                double boost_val) {
+                                                                double boost_val, const int64_t *__restrict__ moff,
+                                                                const uint16_t *__restrict__ map) {
   __shared__ int32_t sc[kMaxGroupRows][kIluMaxRow + 1];
   __shared__ double sv[kMaxGroupRows][kIluMaxRow];
+  __shared__ int32_t sdk[kMaxGroupRows][kIluMaxRow], se1[kMaxGroupRows][kIluMaxRow];  // pivot-row extents
+  __shared__ int32_t smo[MAP ? kMaxGroupRows : 1][MAP ? kIluMaxRow : 1];  // per pivot: map offset in the row
   const int g = g0 + (int)blockIdx.x;
   if (g >= g1) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -186,81 +200,124 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
   if (lane == 0) sc[w][len] = 0x7fffffff;  // search sentinel
   __builtin_amdgcn_wave_barrier();
   __syncthreads();
-  // phase 1: the pivots of earlier colors (entries [rowp_i, lsp_i)), in ascending column order
+  // phase 1: the pivots of earlier colors (entries [rowp_i, lsp_i)), in ascending column order.
+  // Every pivot row k_p belongs to an earlier color and is final, so its upper entries can be loaded
+  // any number of steps ahead: the extents [didx_k, rowp_{k+1}) of all pivot rows are staged in LDS
+  // first (one gather for the row), then a ring of NS register stages keeps the upper
+  // entries of k_{p+1} .. k_{p+NS-1} in flight while step p searches and updates the row.
+  // The ring is unrolled (stage j serves the pivots p = j mod NS), so no register copies wait
+  // on loads in flight. The step itself is the LDS chain: sv[p] / U_kk, the column searches, the
+  // updates. (An LDS hash of the row's columns measured slower, 47 vs 23 ms: most lookups miss.)
   if (w < nr) {
-    // software pipeline over the pivot rows k_p = sc[w][p]: while step p updates the row from k_p's
-    // upper entries (held in registers), the upper entries of k_{p+1} and the indices of k_{p+2} are in
-    // flight. (A two-step-deep rotation of four register stages measured slower, 27 vs 23 ms per
-    // factorization at 121 k DoFs: the step is bound by its LDS search chain, and the extra VGPRs cost
-    // occupancy.)
     constexpr int PF = kIluPrefetch;  // upper entries per lane held in registers (64 * PF per pivot row)
     const int nl = lsp[i] - rp;
-    int dk1 = 0, e11 = 0, dk2 = 0, e12 = 0;  // indices of k_{p+1}, k_{p+2}
-    double piv0 = 1.0, piv1 = 1.0, v0[PF], v1[PF];
-    int c0[PF], c1[PF];
-    auto load_upper = [&](int dk, int e1, double &piv, int (&c)[PF], double (&v)[PF]) {
-      piv = val[dk];
+    int mrun = 0;  // MAP: running offset of the pivot's map segment in the row's
+    for (int p0 = 0; p0 < nl; p0 += 64) {
+      const int p = p0 + lane;
+      int m = 0;
+      if (p < nl) {
+        const int k = sc[w][p];
+        const int dk = didx[k], e1 = rowp[k + 1];
+        sdk[w][p] = dk;
+        se1[w][p] = e1;
+        m = e1 - dk - 1;
+      }
+      if (MAP) {  // exclusive prefix sum of the upper-entry counts over the wave
+        int x = m;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (p < nl) smo[w][p] = mrun + x - m;
+        mrun += __shfl(x, 63, 64);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int64_t mbase = MAP ? moff[i] : 0;
+    struct Stage {
+      double piv, v[PF];
+      int c[PF], dk, e1, mo;  // c: the upper entries' columns (MAP: their row positions)
+    } S[NS];
+    // branchless: every load is issued (clamped to the diagonal entry when out of range) so that the
+    // waitcnt pass sees straight-line code and waits for exactly the stage in use, not vmcnt(0)
+    auto issue = [&](int p, Stage &st) {
+      const bool in = p < nl;
+      st.dk = in ? sdk[w][p] : rp;
+      st.e1 = in ? se1[w][p] : rp;
+      st.mo = MAP && in ? smo[w][p] : 0;
+      st.piv = val[st.dk];
 #pragma unroll
       for (int t = 0; t < PF; ++t) {
-        const int e = dk + 1 + lane + 64 * t;
-        c[t] = e < e1 ? col[e] : -1;
-        v[t] = e < e1 ? val[e] : 0.0;
+        const int e = st.dk + 1 + lane + 64 * t;
+        const bool ok = e < st.e1;
+        const int ec = ok ? e : st.dk;
+        // raw; validity (e < e1) is applied where the stage is used, so no instruction touches these
+        // registers before the stage's step
+        st.c[t] = MAP ? (int)map[mbase + (ok ? st.mo + lane + 64 * t : 0)] : col[ec];
+        st.v[t] = val[ec];
       }
     };
-    int dk0 = 0, e10 = 0;
-    if (nl > 0) {
-      dk0 = didx[sc[w][0]];
-      e10 = rowp[sc[w][0] + 1];
-      load_upper(dk0, e10, piv0, c0, v0);
-    }
-    if (nl > 1) {
-      dk1 = didx[sc[w][1]];
-      e11 = rowp[sc[w][1] + 1];
-    }
-    for (int p = 0; p < nl; ++p) {
-      if (p + 1 < nl) load_upper(dk1, e11, piv1, c1, v1);
-      if (p + 2 < nl) {
-        dk2 = didx[sc[w][p + 2]];
-        e12 = rowp[sc[w][p + 2] + 1];
+    auto step = [&](int p, const Stage &st) {
+      const double lik = sv[w][p] / st.piv;
+      if (MAP) {
+#pragma unroll
+        for (int t = 0; t < PF; ++t) {
+          const int q = st.c[t];
+          if (st.dk + 1 + lane + 64 * t < st.e1 && q != kMapMiss) sv[w][q] -= lik * st.v[t];
+        }
+        for (int e = lane + 64 * PF; e < st.e1 - st.dk - 1; e += 64) {  // longer pivot rows
+          const int q = map[mbase + st.mo + e];
+          if (q != kMapMiss) sv[w][q] -= lik * val[st.dk + 1 + e];
+        }
+        if (lane == 0) sv[w][p] = lik;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        return;
       }
-      const double lik = sv[w][p] / piv0;
-      {  // PF branchless lower_bound searches in [p+1, len) side by side (the trip count is uniform;
-         // an LDS hash of the row's columns measured slower, 47 vs 23 ms: most lookups miss)
+      int cs[PF];
+#pragma unroll
+      for (int t = 0; t < PF; ++t) cs[t] = st.dk + 1 + lane + 64 * t < st.e1 ? st.c[t] : -1;
+      {  // PF branchless lower_bound searches in [p+1, len) side by side (the trip count is uniform)
         int b[PF], n = len - (p + 1);
 #pragma unroll
         for (int t = 0; t < PF; ++t) b[t] = p + 1;
         while (n > 1) {
           const int half = n >> 1;
 #pragma unroll
-          for (int t = 0; t < PF; ++t) b[t] = sc[w][b[t] + half] < c0[t] ? b[t] + half : b[t];
+          for (int t = 0; t < PF; ++t) b[t] = sc[w][b[t] + half] < cs[t] ? b[t] + half : b[t];
           n -= half;
         }
         if (n > 0) {
 #pragma unroll
           for (int t = 0; t < PF; ++t) {
-            const int q = b[t] + (sc[w][b[t]] < c0[t] ? 1 : 0);
-            if (c0[t] >= 0 && sc[w][q] == c0[t]) sv[w][q] -= lik * v0[t];  // sc[w][len]: sentinel
+            const int q = b[t] + (sc[w][b[t]] < cs[t] ? 1 : 0);
+            if (cs[t] >= 0 && sc[w][q] == cs[t]) sv[w][q] -= lik * st.v[t];  // sc[w][len]: sentinel
           }
         }
       }
-      for (int e = dk0 + 1 + lane + 64 * PF; e < e10; e += 64) {  // longer pivot rows: the rest directly
+      for (int e = st.dk + 1 + lane + 64 * PF; e < st.e1; e += 64) {  // longer pivot rows: the rest directly
         const int q = lds_find(sc[w], p + 1, len, col[e]);
         if (q >= 0) sv[w][q] -= lik * val[e];
       }
       if (lane == 0) sv[w][p] = lik;
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      dk0 = dk1;
-      e10 = e11;
-      piv0 = piv1;
+    };
 #pragma unroll
-      for (int t = 0; t < PF; ++t) {
-        c0[t] = c1[t];
-        v0[t] = v1[t];
+    for (int j = 0; j < NS; ++j) issue(j, S[j]);
+    int p = 0;
+    for (; p + NS <= nl; p += NS) {  // full rounds: no branch between the stages
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        step(p + j, S[j]);
+        issue(p + j + NS, S[j]);
       }
-      dk1 = dk2;
-      e11 = e12;
     }
+#pragma unroll
+    for (int j = 0; j < NS; ++j)  // the last < NS pivots, already in flight
+      if (p + j < nl) step(p + j, S[j]);
   }
   __syncthreads();
   // phase 2: the own-node pivots (entries [lsp_i, didx_i): rows r0 .. i-1 of this group), row by row
@@ -285,38 +342,86 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
   }
   for (int e = lane; e < len; e += 64) val[rp + e] = sv[w][e];
 }
+
+// the MAP positions: one wavefront per row, its columns staged in LDS; for every pivot k_p (entries
+// [rowp_i, lsp_i)) and every upper entry of row k_p, the position of that column in row i (> p) or
+// kMapMiss. Segments follow the pivots in order from moff[i].
+__global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int32_t *__restrict__ rowp,
+                                                     const int32_t *__restrict__ col, const int32_t *__restrict__ lsp,
+                                                     const int32_t *__restrict__ didx,
+                                                     const int64_t *__restrict__ moff, uint16_t *__restrict__ map) {
+  __shared__ int32_t sc[4][kIluMaxRow + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 4 + w;
+  if (i >= n) return;
+  const int rp = rowp[i], len = rowp[i + 1] - rp, nl = lsp[i] - rp;
+  for (int e = lane; e < len; e += 64) sc[w][e] = col[rp + e];
+  if (lane == 0) sc[w][len] = 0x7fffffff;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  int64_t o = moff[i];
+  for (int p = 0; p < nl; ++p) {
+    const int k = sc[w][p];
+    const int dk = didx[k], m = rowp[k + 1] - dk - 1;
+    for (int e = lane; e < m; e += 64) {
+      const int q = lds_find(sc[w], p + 1, len, col[dk + 1 + e]);
+      map[o + e] = q >= 0 ? (uint16_t)q : kMapMiss;
+    }
+    o += m;
+  }
+}
 }  // namespace
+
+hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col, const int32_t *lsp,
+                             const int32_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mc_ilu0_map, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, n, rowp, col, lsp, didx, moff, map);
+  return hipGetLastError();
+}
 
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                          const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
-                         double boost_val, hipStream_t s) {
+                         double boost_val, const int64_t *moff, const uint16_t *map, int stages, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
-    hipLaunchKernelGGL(k_mc_ilu0, dim3((unsigned)(g1 - g0)), dim3(64 * kMaxGroupRows), 0, s, grow, g0, g1, rowp, col, val,
-                       lsp, didx, boost_tol, boost_val);
+    const dim3 gr((unsigned)(g1 - g0)), bl(64 * kMaxGroupRows);
+    if (map && stages >= 6)
+      hipLaunchKernelGGL((k_mc_ilu0<true, 6>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
+                         boost_val, moff, map);
+    else if (map)
+      hipLaunchKernelGGL((k_mc_ilu0<true, 3>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
+                         boost_val, moff, map);
+    else
+      hipLaunchKernelGGL((k_mc_ilu0<false, 3>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
+                         boost_val, moff, map);
   }
   return hipGetLastError();
 }
 
 hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                         const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, int waves_per_group,
-                        hipStream_t s) {
-  const int wpg = waves_per_group >= 4 ? 4 : 1, gpb = 4 / wpg;
+                        const int32_t *didx, const double *b, double *y, double *x, const uint8_t *waves_lower,
+                        const uint8_t *waves_upper, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
-    const unsigned nb = (unsigned)((g1 - g0 + gpb - 1) / gpb);
-    if (wpg == 4) hipLaunchKernelGGL((k_mc_tri<4, true>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, lsp, didx, b, y);
-    else hipLaunchKernelGGL((k_mc_tri<1, true>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, lsp, didx, b, y);
+    if (waves_lower[c] >= 4)
+      hipLaunchKernelGGL((k_mc_tri<4, true>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, grow, g0, g1, rowp, col, val,
+                         lsp, didx, b, y);
+    else
+      hipLaunchKernelGGL((k_mc_tri<1, true>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, grow, g0, g1, rowp,
+                         col, val, lsp, didx, b, y);
   }
   for (int c = n_colors - 1; c >= 0; --c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
-    const unsigned nb = (unsigned)((g1 - g0 + gpb - 1) / gpb);
-    if (wpg == 4) hipLaunchKernelGGL((k_mc_tri<4, false>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, usp, didx, y, x);
-    else hipLaunchKernelGGL((k_mc_tri<1, false>), dim3(nb), dim3(256), 0, s, grow, g0, g1, rowp, col, val, usp, didx, y, x);
+    if (waves_upper[c] >= 4)
+      hipLaunchKernelGGL((k_mc_tri<4, false>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, grow, g0, g1, rowp, col, val,
+                         usp, didx, y, x);
+    else
+      hipLaunchKernelGGL((k_mc_tri<1, false>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, grow, g0, g1, rowp,
+                         col, val, usp, didx, y, x);
   }
   return hipGetLastError();
 }

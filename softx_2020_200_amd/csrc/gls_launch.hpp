@@ -99,11 +99,14 @@ constexpr int kMaxGroupRows = 4;
 constexpr int kIluMaxRow = 640;
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                          const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
-                         double boost_val, hipStream_t s);
+                         double boost_val, const int64_t *moff, const uint16_t *map, int stages, hipStream_t s);
+// the factorization's row-position map (map == nullptr in ilu_mc_factor: column searches instead)
+hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col, const int32_t *lsp,
+                             const int32_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s);
 hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                         const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, int waves_per_group,
-                        hipStream_t s);
+                        const int32_t *didx, const double *b, double *y, double *x, const uint8_t *waves_lower,
+                        const uint8_t *waves_upper, hipStream_t s);
 hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
 hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
 hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,

@@ -167,14 +167,14 @@ def test_ilu_apply_is_the_factored_solve(dim, n, k, kp, order, blk):
 def test_multicolor_factorization_equals_rocsparse(dim, n, k, kp):
     """The multicolor order's color-by-color factorization (k_mc_ilu0: rows of earlier colors in
     parallel, the node's own rows in order) and rocSPARSE csrilu0 on the same pattern and values
-    (GLS_ILU_ROCSPARSE_FACTOR=1) give the same factors."""
+    (GLS_ILU_ROCSPARSE_FACTOR=1) give the same factors; the kernel with the precomputed row-position
+    map (default) and with column searches (GLS_ILU_FACTOR_MAP=0) give bitwise the same factors."""
     p = _cavity(dim, n, k, kp, "bdf1", 0.05)
     rng = np.random.default_rng(SEED + 3)
     u, u1 = (p.apply_nonzero_constraints(rng.uniform(-1, 1, p.n_dofs)) for _ in range(2))
     out = []
-    for env in ("1", None):
-        if env:
-            os.environ["GLS_ILU_ROCSPARSE_FACTOR"] = env
+    for env in ({"GLS_ILU_ROCSPARSE_FACTOR": "1"}, {"GLS_ILU_FACTOR_MAP": "0"}, {}):
+        os.environ.update(env)
         try:
             ctx = context_for(p)
             ctx.set_time("bdf1", p.time_steps)
@@ -182,12 +182,14 @@ def test_multicolor_factorization_equals_rocsparse(dim, n, k, kp):
             ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
             out.append(ctx.ilu_factors())
         finally:
-            os.environ.pop("GLS_ILU_ROCSPARSE_FACTOR", None)
-    (p0, F0), (p1, F1) = out
-    assert np.array_equal(p0, p1)
-    F0, F1 = F0.tocsr(), F1.tocsr()
+            for key in env:
+                os.environ.pop(key, None)
+    (p0, F0), (p1, F1), (p2, F2) = out
+    assert np.array_equal(p0, p1) and np.array_equal(p0, p2)
+    F0, F1, F2 = F0.tocsr(), F1.tocsr(), F2.tocsr()
     assert np.array_equal(F0.indptr, F1.indptr) and np.array_equal(F0.indices, F1.indices)
     assert np.abs(F0.data - F1.data).max() <= 1e-12 * np.abs(F0.data).max()
+    assert np.array_equal(F1.indices, F2.indices) and np.array_equal(F1.data, F2.data)
 
 
 @pytest.mark.gpu
