@@ -375,7 +375,7 @@ struct gls_ctx {
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
     std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
-    int mc_stages = 6;                  // factorization: pivot rows in flight (MAP kernel)
+    DevBuf<int32_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc ints)
     DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
     DevBuf<uint16_t> mc_map;   // per (row, pivot, upper entry of the pivot row): position in the row
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
@@ -2279,7 +2279,7 @@ static int ensure_ilu(gls_ctx *c) {
   if (I.mc_factor)
     HIP_TRY(gls::ilu_mc_factor(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
                                I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, I.mc_moff.p,
-                               I.mc_map.n ? I.mc_map.p : nullptr, I.mc_stages, s));
+                               I.mc_map.n ? I.mc_map.p : nullptr, s));
   else
     RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
   I.valid = true;
@@ -2304,9 +2304,8 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   // z = P^T U^-1 L^-1 P v (P: the Cuthill-McKee renumbering the factors live in)
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
   if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
-    HIP_TRY(gls::ilu_mc_solve(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
-                              I.mc_lsp.p, I.mc_usp.p, I.didx.p, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_wl.data(),
-                              I.mc_wu.data(), c->stream));
+    HIP_TRY(gls::ilu_mc_solve(I.mc_desc.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.col.p, I.val.p, I.vbuf.p,
+                              I.tbuf.p, I.vbuf.p, I.mc_wl.data(), I.mc_wu.data(), c->stream));
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
@@ -3822,6 +3821,26 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       GLS_TRY(I.mc_grow.upload(grow.data(), grow.size()));
       GLS_TRY(I.mc_lsp.upload(lsp.data(), lsp.size()));
       GLS_TRY(I.mc_usp.upload(usp.data(), usp.size()));
+      {
+        const size_t ng = grow.size() - 1;
+        std::vector<int32_t> desc(ng * gls::kGroupDesc, 0);
+        for (size_t g = 0; g < ng; ++g) {
+          int32_t *d = &desc[g * gls::kGroupDesc];
+          const int32_t r0 = grow[g], nr = grow[g + 1] - r0;
+          d[0] = r0;
+          d[1] = nr;
+          d[2] = rowp[(size_t)r0];
+          d[3] = rowp[(size_t)(r0 + nr)];
+          for (int t = 1; t < 4; ++t) d[3 + t] = t < nr ? rowp[(size_t)(r0 + t)] : INT32_MAX;
+          for (int t = 0; t < nr; ++t) {
+            d[8 + t] = lsp[(size_t)(r0 + t)];
+            d[12 + t] = usp[(size_t)(r0 + t)];
+            d[16 + t] = didx[(size_t)(r0 + t)];
+            d[20 + t] = rowp[(size_t)(r0 + t) + 1];
+          }
+        }
+        GLS_TRY(I.mc_desc.upload(desc.data(), desc.size()));
+      }
       I.mc_cg = cg;
       I.mc_solve = true;
       int32_t maxrow = 0;
@@ -3861,7 +3880,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
         I.mc_wu[(size_t)c] = (uint8_t)(ng && nup > 256 * (int64_t)ng ? 4 : 1);
         if (we) I.mc_wl[(size_t)c] = I.mc_wu[(size_t)c] = (uint8_t)(std::atoi(we) >= 4 ? 4 : 1);
       }
-      if (const char *se = std::getenv("GLS_ILU_STAGES")) I.mc_stages = std::atoi(se);
     }
   }
   // probes: one per (color, slot); every entry of the system matrix is read from the probe of its

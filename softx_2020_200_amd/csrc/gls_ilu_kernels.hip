@@ -22,9 +22,9 @@ __device__ __forceinline__ double wave_sum(double s) {
 
 // One launch per color; WPG wavefronts per node group (1 for short rows, 4 for the ~200-entry rows
 // of 3D Q2 matrices, where a single wave would walk each row's other-color entries in several
-// dependent load rounds). The rows of a group are contiguous in the CSR, so the group's threads
-// stride over its whole entry range at once (all <= 4 rows, kGatherUnroll entries per thread in
-// flight) and mask entries outside a row's other-color segment before the x gather. Thread 0 of the
+// dependent load rounds). The group's threads stride over the concatenation of its rows'
+// other-color segments at once (all <= 4 rows, kGatherUnroll entries per thread in flight; no lane
+// walks the other triangle's entries). Thread 0 of the
 // group loads its serial-part operands (right-hand sides, the <= 3 own-node entries per row, the
 // diagonal) before the gather so they are in flight with it, and keeps the rows it has resolved in
 // registers: the only dependent global traffic left is the gather.
@@ -40,30 +40,40 @@ __device__ __forceinline__ double pick4(const double *a, int j) {
 // upper: x_i = (y_i - sum_{j > i} U_ij x_j) / U_ii; entries [sp_i, rowp_{i+1}) lie in later colors,
 //        (didx_i, sp_i) in the row's own node (sp = usp).
 // In both, the gathered vector is the output (x / y of the other colors, already final).
+// Each node group's row extents come from one 96-byte descriptor (kGroupDesc ints, built at attach:
+// r0, nr, entry range, row boundaries, lsp, usp, didx, row ends), so the first dependent load round
+// of a launch is the descriptor itself rather than grow -> rowp / lsp / usp / didx.
 template <int WPG, bool LOWER>
-__global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow, int g0, int g1,
-                                                const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
-                                                const double *__restrict__ val, const int32_t *__restrict__ sp,
-                                                const int32_t *__restrict__ didx, const double *__restrict__ rhs,
-                                                double *__restrict__ out) {
+__global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdesc, int g0, int g1,
+                                                const int32_t *__restrict__ col, const double *__restrict__ val,
+                                                const double *__restrict__ rhs, double *__restrict__ out) {
   constexpr int GPB = 4 / WPG;  // node groups per 256-thread block
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
   const int gl = w / WPG, tig = (w % WPG) * 64 + lane;
   const int g = g0 + (int)blockIdx.x * GPB + gl;
   const bool live = g < g1;
   __shared__ double red[4][kMaxGroupRows];
-  int r0 = 0, nr = 0;
-  if (live) {
-    r0 = grow[g];
-    nr = grow[g + 1] - r0;
+  int32_t dsc[kGroupDesc];
+  {
+    const int4 *d4 = reinterpret_cast<const int4 *>(gdesc + (int64_t)(live ? g : g0) * kGroupDesc);
+#pragma unroll
+    for (int k = 0; k < kGroupDesc / 4; ++k) {
+      const int4 q = d4[k];
+      dsc[4 * k] = q.x;
+      dsc[4 * k + 1] = q.y;
+      dsc[4 * k + 2] = q.z;
+      dsc[4 * k + 3] = q.w;
+    }
   }
-  int32_t bnd[kMaxGroupRows], lo[kMaxGroupRows], hi[kMaxGroupRows];
+  const int r0 = dsc[0], nr = live ? dsc[1] : 0;
+  int32_t bnd[kMaxGroupRows], lo[kMaxGroupRows], hi[kMaxGroupRows], dix[kMaxGroupRows];
 #pragma unroll
   for (int t = 0; t < kMaxGroupRows; ++t) {
     const bool in = t < nr;
-    bnd[t] = in ? rowp[r0 + t] : INT32_MAX;
-    lo[t] = !in ? 0 : LOWER ? rowp[r0 + t] : sp[r0 + t];
-    hi[t] = !in ? 0 : LOWER ? sp[r0 + t] : rowp[r0 + t + 1];
+    bnd[t] = t == 0 ? dsc[2] : dsc[3 + t];
+    lo[t] = !in ? 0 : LOWER ? bnd[t] : dsc[12 + t];
+    hi[t] = !in ? 0 : LOWER ? dsc[8 + t] : dsc[20 + t];
+    dix[t] = dsc[16 + t];
   }
   // serial-part operands (thread 0 of the group)
   double rb[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0}, dg[kMaxGroupRows] = {1.0, 1.0, 1.0, 1.0};
@@ -74,8 +84,8 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow
     for (int t = 0; t < kMaxGroupRows; ++t) {
       const int i = r0 + t;
       const bool in = t < nr;
-      const int d = in ? didx[i] : 0;
-      const int ob = !in ? 0 : LOWER ? sp[i] : d + 1, oe = !in ? 0 : LOWER ? d : sp[i];
+      const int d = in ? dix[t] : 0;
+      const int ob = !in ? 0 : LOWER ? dsc[8 + t] : d + 1, oe = !in ? 0 : LOWER ? d : dsc[12 + t];
       rb[t] = in ? rhs[i] : 0.0;
       if (!LOWER) dg[t] = in ? val[d] : 1.0;
 #pragma unroll
@@ -86,19 +96,19 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow
       }
     }
   }
-  // other-color gather-dot
+  // other-color gather-dot over the rows' segments [lo_t, hi_t) concatenated (virtual index v:
+  // row t = number of segment prefix sums <= v), so no lane walks entries of the other triangle
   double acc[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0};
-  const int eb = live ? rowp[r0] : 0, ee = live ? rowp[r0 + nr] : 0;
-  for (int e0 = eb + tig; e0 < ee; e0 += 64 * WPG * kGatherUnroll) {
+  const int P1 = hi[0] - lo[0], P2 = P1 + hi[1] - lo[1], P3 = P2 + hi[2] - lo[2], tot = P3 + hi[3] - lo[3];
+  for (int v0 = tig; v0 < tot; v0 += 64 * WPG * kGatherUnroll) {
     int c[kGatherUnroll], tt[kGatherUnroll];
     double v[kGatherUnroll], xv[kGatherUnroll];
 #pragma unroll
     for (int u = 0; u < kGatherUnroll; ++u) {
-      const int e = e0 + 64 * WPG * u;
-      const int t = (e >= bnd[1]) + (e >= bnd[2]) + (e >= bnd[3]);
-      const int l = t == 0 ? lo[0] : t == 1 ? lo[1] : t == 2 ? lo[2] : lo[3];
-      const int h = t == 0 ? hi[0] : t == 1 ? hi[1] : t == 2 ? hi[2] : hi[3];
-      const bool ok = e < ee && e >= l && e < h;
+      const int vi = v0 + 64 * WPG * u;
+      const int t = (vi >= P1) + (vi >= P2) + (vi >= P3);
+      const int e = vi + (t == 0 ? lo[0] : t == 1 ? lo[1] - P1 : t == 2 ? lo[2] - P2 : lo[3] - P3);
+      const bool ok = vi < tot;
       tt[u] = ok ? t : -1;
       c[u] = ok ? col[e] : 0;
       v[u] = ok ? val[e] : 0.0;
@@ -148,8 +158,10 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ grow
 }
 
 constexpr int kIluPrefetch = 4;
-// pivot rows in flight in the factorization (template NS): 3 for the searching kernel, whose step is
-// long; more for the MAP kernel, whose step is a few LDS operations
+// pivot rows in flight in the factorization (template NS): 3; 6 measured the same with the MAP kernel
+// (10.5 ms per factorization at 121 k DoFs either way): its step is bound by the wave's own
+// instruction stream (loads' address arithmetic, the division, four predicated updates), not by
+// the loads
 // first position q in [lo, hi) of the sorted column list c with c[q] == j, else -1
 __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_t j) {
   while (lo < hi) {
@@ -238,7 +250,9 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     const int64_t mbase = MAP ? moff[i] : 0;
     struct Stage {
       double piv, v[PF];
-      int c[PF], dk, e1, mo;  // c: the upper entries' columns (MAP: their row positions)
+      int c[PF], dk, e1, mo;  // c: the upper entries' columns
+      uint16_t mq[PF];        // MAP: their row positions (kept 16-bit until used: a widening of a
+                              // register still in flight would wait for its load)
     } S[NS];
     // branchless: every load is issued (clamped to the diagonal entry when out of range) so that the
     // waitcnt pass sees straight-line code and waits for exactly the stage in use, not vmcnt(0)
@@ -255,7 +269,8 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
         const int ec = ok ? e : st.dk;
         // raw; validity (e < e1) is applied where the stage is used, so no instruction touches these
         // registers before the stage's step
-        st.c[t] = MAP ? (int)map[mbase + (ok ? st.mo + lane + 64 * t : 0)] : col[ec];
+        if (MAP) st.mq[t] = map[mbase + (ok ? st.mo + lane + 64 * t : 0)];
+        else st.c[t] = col[ec];
         st.v[t] = val[ec];
       }
     };
@@ -264,7 +279,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
       if (MAP) {
 #pragma unroll
         for (int t = 0; t < PF; ++t) {
-          const int q = st.c[t];
+          const int q = st.mq[t];
           if (st.dk + 1 + lane + 64 * t < st.e1 && q != kMapMiss) sv[w][q] -= lik * st.v[t];
         }
         for (int e = lane + 64 * PF; e < st.e1 - st.dk - 1; e += 64) {  // longer pivot rows
@@ -381,15 +396,12 @@ hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col,
 
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                          const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
-                         double boost_val, const int64_t *moff, const uint16_t *map, int stages, hipStream_t s) {
+                         double boost_val, const int64_t *moff, const uint16_t *map, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     const dim3 gr((unsigned)(g1 - g0)), bl(64 * kMaxGroupRows);
-    if (map && stages >= 6)
-      hipLaunchKernelGGL((k_mc_ilu0<true, 6>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
-                         boost_val, moff, map);
-    else if (map)
+    if (map)
       hipLaunchKernelGGL((k_mc_ilu0<true, 3>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
                          boost_val, moff, map);
     else
@@ -399,29 +411,26 @@ hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n
   return hipGetLastError();
 }
 
-hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
-                        const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, const uint8_t *waves_lower,
+hipError_t ilu_mc_solve(const int32_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+                        const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
                         const uint8_t *waves_upper, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_lower[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, true>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, grow, g0, g1, rowp, col, val,
-                         lsp, didx, b, y);
+      hipLaunchKernelGGL((k_mc_tri<4, true>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, b, y);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, true>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, grow, g0, g1, rowp,
-                         col, val, lsp, didx, b, y);
+      hipLaunchKernelGGL((k_mc_tri<1, true>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
+                         val, b, y);
   }
   for (int c = n_colors - 1; c >= 0; --c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_upper[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, false>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, grow, g0, g1, rowp, col, val,
-                         usp, didx, y, x);
+      hipLaunchKernelGGL((k_mc_tri<4, false>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, y, x);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, false>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, grow, g0, g1, rowp,
-                         col, val, usp, didx, y, x);
+      hipLaunchKernelGGL((k_mc_tri<1, false>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
+                         val, y, x);
   }
   return hipGetLastError();
 }

@@ -99,13 +99,15 @@ constexpr int kMaxGroupRows = 4;
 constexpr int kIluMaxRow = 640;
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
                          const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
-                         double boost_val, const int64_t *moff, const uint16_t *map, int stages, hipStream_t s);
+                         double boost_val, const int64_t *moff, const uint16_t *map, hipStream_t s);
 // the factorization's row-position map (map == nullptr in ilu_mc_factor: column searches instead)
 hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col, const int32_t *lsp,
                              const int32_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s);
-hipError_t ilu_mc_solve(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
-                        const int32_t *col, const double *val, const int32_t *lsp, const int32_t *usp,
-                        const int32_t *didx, const double *b, double *y, double *x, const uint8_t *waves_lower,
+// per node group: r0, nr, rowp[r0], rowp[r0 + nr], rowp[r0 + 1..3] (INT32_MAX past nr), 0, lsp[4], usp[4],
+// didx[4], rowp[r0 + 1..4] (the solves' group descriptor)
+constexpr int kGroupDesc = 24;
+hipError_t ilu_mc_solve(const int32_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+                        const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
                         const uint8_t *waves_upper, hipStream_t s);
 hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
 hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
