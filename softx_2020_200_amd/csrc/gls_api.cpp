@@ -3852,7 +3852,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
           int64_t m = 0;
           for (int32_t e = rowp[(size_t)r]; e < lsp[(size_t)r]; ++e) {
             const int32_t k = col[(size_t)e];
-            m += rowp[(size_t)k + 1] - didx[(size_t)k] - 1;
+            m += (rowp[(size_t)k + 1] - didx[(size_t)k] - 1 + 3) & ~3;  // segments padded to quads
           }
           mc_moff_h[(size_t)r + 1] = mc_moff_h[(size_t)r] + m;
         }
@@ -3997,7 +3997,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     GLS_TRY(I.pdpid.upload(pdp.data(), pdp.size()));
     GLS_TRY(I.pepid.upload(pep.data(), pep.size()));
   }
-  GLS_TRY(I.val.alloc(col.size()));
+  GLS_TRY(I.val.alloc(col.size() + 256));  // + the factorization's whole-quad loads past a row's end
   HIP_TRY(hipMemset(I.val.p, 0, col.size() * sizeof(double)));
   GLS_TRY(I.vbuf.alloc((size_t)n));
   GLS_TRY(I.ybuf.alloc((size_t)n));

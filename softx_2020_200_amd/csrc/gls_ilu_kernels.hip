@@ -182,7 +182,8 @@ __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_
 //
 // MAP: the row positions the upper entries of each pivot row land on (found by the column searches)
 // depend on the pattern only; gls_ilu_attach precomputes them once (k_mc_ilu0_map, uint16 per
-// (row, pivot, upper entry), 0xffff where the entry is outside the row's pattern), and the
+// (row, pivot, upper entry), 0xffff where the entry is outside the row's pattern, each pivot's
+// segment padded to a multiple of 4 so a lane reads its quad of positions in one load), and the
 // factorization streams them with the upper values instead of searching: the step's LDS chain
 // shrinks to sv[p] / U_kk and one read-modify-write per lane. Same updates in the same order, so the
 // factors are bitwise those of the searching kernel.
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
                                                                 double boost_val, const int64_t *__restrict__ moff,
                                                                 const uint16_t *__restrict__ map) {
   __shared__ int32_t sc[kMaxGroupRows][kIluMaxRow + 1];
-  __shared__ double sv[kMaxGroupRows][kIluMaxRow];
+  __shared__ double sv[kMaxGroupRows][kIluMaxRow + 1];  // + a dummy slot for the MAP step's idle lanes
   __shared__ int32_t sdk[kMaxGroupRows][kIluMaxRow], se1[kMaxGroupRows][kIluMaxRow];  // pivot-row extents
   __shared__ int32_t smo[MAP ? kMaxGroupRows : 1][MAP ? kIluMaxRow : 1];  // per pivot: map offset in the row
   const int g = g0 + (int)blockIdx.x;
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
         const int dk = didx[k], e1 = rowp[k + 1];
         sdk[w][p] = dk;
         se1[w][p] = e1;
-        m = e1 - dk - 1;
+        m = MAP ? (e1 - dk - 1 + 3) & ~3 : e1 - dk - 1;  // MAP segments are padded to quads
       }
       if (MAP) {  // exclusive prefix sum of the upper-entry counts over the wave
         int x = m;
@@ -251,8 +252,8 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     struct Stage {
       double piv, v[PF];
       int c[PF], dk, e1, mo;  // c: the upper entries' columns
-      uint16_t mq[PF];        // MAP: their row positions (kept 16-bit until used: a widening of a
-                              // register still in flight would wait for its load)
+      uint64_t mq;            // MAP: the row positions of the lane's quad, 4 x 16 bit (unpacked only
+                              // when used: touching a register still in flight waits for its load)
     } S[NS];
     // branchless: every load is issued (clamped to the diagonal entry when out of range) so that the
     // waitcnt pass sees straight-line code and waits for exactly the stage in use, not vmcnt(0)
@@ -260,29 +261,44 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
       const bool in = p < nl;
       st.dk = in ? sdk[w][p] : rp;
       st.e1 = in ? se1[w][p] : rp;
-      st.mo = MAP && in ? smo[w][p] : 0;
       st.piv = val[st.dk];
+      if (MAP) {  // lane l: the quad of upper entries 4l .. 4l+3 (one 8-byte map load, one address
+                  // for the values; past the row's end they are masked in the step, and the value
+                  // array is padded for the last rows)
+        st.mo = in ? smo[w][p] : 0;
+        const bool ok = 4 * lane < st.e1 - st.dk - 1;
+        st.mq = reinterpret_cast<const uint64_t *>(map + mbase + st.mo)[ok ? lane : 0];
+        const double *vp = val + st.dk + 1 + 4 * lane;
+#pragma unroll
+        for (int t = 0; t < PF; ++t) st.v[t] = vp[t];
+        return;
+      }
 #pragma unroll
       for (int t = 0; t < PF; ++t) {
         const int e = st.dk + 1 + lane + 64 * t;
-        const bool ok = e < st.e1;
-        const int ec = ok ? e : st.dk;
+        const int ec = e < st.e1 ? e : st.dk;
         // raw; validity (e < e1) is applied where the stage is used, so no instruction touches these
         // registers before the stage's step
-        if (MAP) st.mq[t] = map[mbase + (ok ? st.mo + lane + 64 * t : 0)];
-        else st.c[t] = col[ec];
+        st.c[t] = col[ec];
         st.v[t] = val[ec];
       }
     };
     auto step = [&](int p, const Stage &st) {
       const double lik = sv[w][p] / st.piv;
-      if (MAP) {
+      if (MAP) {  // branchless: all four reads, then all four writes (idle lanes on the dummy slot)
+        const int m = st.e1 - st.dk - 1;
+        int qa[PF];
+        double r[PF];
 #pragma unroll
         for (int t = 0; t < PF; ++t) {
-          const int q = st.mq[t];
-          if (st.dk + 1 + lane + 64 * t < st.e1 && q != kMapMiss) sv[w][q] -= lik * st.v[t];
+          const int q = (int)((st.mq >> (16 * t)) & 0xffffu);
+          qa[t] = 4 * lane + t < m && q != kMapMiss ? q : kIluMaxRow;
         }
-        for (int e = lane + 64 * PF; e < st.e1 - st.dk - 1; e += 64) {  // longer pivot rows
+#pragma unroll
+        for (int t = 0; t < PF; ++t) r[t] = sv[w][qa[t]];
+#pragma unroll
+        for (int t = 0; t < PF; ++t) sv[w][qa[t]] = r[t] - lik * st.v[t];
+        for (int e = 4 * 64 + lane; e < m; e += 64) {  // longer pivot rows: the rest directly
           const int q = map[mbase + st.mo + e];
           if (q != kMapMiss) sv[w][q] -= lik * val[st.dk + 1 + e];
         }
@@ -377,12 +393,12 @@ __global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int32_t *_
   int64_t o = moff[i];
   for (int p = 0; p < nl; ++p) {
     const int k = sc[w][p];
-    const int dk = didx[k], m = rowp[k + 1] - dk - 1;
-    for (int e = lane; e < m; e += 64) {
-      const int q = lds_find(sc[w], p + 1, len, col[dk + 1 + e]);
+    const int dk = didx[k], m = rowp[k + 1] - dk - 1, mp = (m + 3) & ~3;  // segments padded to quads
+    for (int e = lane; e < mp; e += 64) {
+      const int q = e < m ? lds_find(sc[w], p + 1, len, col[dk + 1 + e]) : -1;
       map[o + e] = q >= 0 ? (uint16_t)q : kMapMiss;
     }
-    o += m;
+    o += mp;
   }
 }
 }  // namespace
