@@ -518,6 +518,18 @@ def main():
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
     tr = pmc_traffic(os.path.join(ROOT, "profiles", "r03_pmc_traffic_head_128.txt"), 4, N_global) \
         if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
+    if tr is not None and args.k == 2 and world == 1:
+        # the roof that actually binds the brick J.v: the LDS pipe (DESIGN §4 "What bounds the J.v").
+        # Cycles per wave = the kernel's LDS instruction stream priced by MI355X_MICROARCH.md §LDS
+        # (tools/isa_mix.py: 1248 static, x 234/248 executed per the PMC instruction count) inflated by
+        # the measured bank-conflict share (16.5 % of LDS-array cycles), profiles/r03_lds_roof_model.txt
+        lds_cyc_wave = 1248 * 234 / 248 / (1 - 0.165)
+        waves_per_cu = (n_cells // 8) * 4 / 256
+        lds_ms = waves_per_cu * lds_cyc_wave / 2.4e9 * 1e3  # at the 2400 MHz peak clock
+        out["roofline"]["lds"] = {"kernel": "gls_brick_kernel<2,MODE_JVQ,double>", "lds_cycles_per_wave": lds_cyc_wave,
+                                  "waves_per_cu": waves_per_cu, "floor_ms_at_2400MHz": lds_ms,
+                                  "launch_ms": jv_launch_ms, "frac": lds_ms / jv_launch_ms,
+                                  "source": "profiles/r03_lds_roof_model.txt"}
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
         out["roofline"]["traffic_source"] = ("profiles/r03_pmc_traffic_head_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "

@@ -306,6 +306,9 @@ struct gls_ctx {
   bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
   // solver workspace
   DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
+  DevBuf<double> scal2;  // GMRES: the projection pass's dots (scal holds the coefficients it reads)
+  double *hpin = nullptr;  // pinned host copy of the Gram-Schmidt dots (async D2H, one wait per pass pair)
+  size_t hpin_n = 0;
   DevBuf<double> krylov;      // (restart+1) x n_dofs
   DevBuf<double> zbasis;      // restart x n_dofs: M^-1 v_j when the preconditioner is the V-cycle
   int krylov_m = 0;
@@ -530,6 +533,7 @@ struct gls_ctx {
   int64_t t_n[6] = {0, 0, 0, 0, 0, 0};
 
   ~gls_ctx() {
+    if (hpin) (void)hipHostFree(hpin);
     for (auto &e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
     if (dist.ev_ready) (void)hipEventDestroy(dist.ev_ready);
     if (dist.ev_done) (void)hipEventDestroy(dist.ev_done);
@@ -1173,6 +1177,52 @@ int dist_multiaxpy_dots(gls_ctx *c, double *w, const double *V, int64_t lda, int
 
 int device_dot(gls_ctx *c, const double *a, const double *b, double *host_out) {
   return dist_multidot(c, a, 0, 1, b, host_out);
+}
+
+// Stream-ordered variants for GMRES (no host wait): the dots land in `out` (device), are reduced over
+// ranks, and are copied to the pinned host buffer `hp` (read after the caller's next wait). The return
+// value is the device address of the reduced dots, which the next projection reads as its
+// coefficients directly (no host round trip, no H2D copy).
+const double *reduce_dots_async(gls_ctx *c, const double *out, int nd, double *hp, int *err) {
+  const double *res = out;
+  *err = GLS_OK;
+  if (c->dist.on) {
+    if (hipMemcpyAsync(c->dist.red_buf, out, sizeof(double) * nd, hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
+      *err = set_err(GLS_EHIP, "reduce_dots_async: D2D copy");
+      return nullptr;
+    }
+    if (c->dist.allreduce(c->dist.user, c->dist.red_buf, nd) != 0) {
+      *err = set_err(GLS_ECOMM, "allreduce failed");
+      return nullptr;
+    }
+    res = c->dist.red_buf;
+  }
+  if (hipMemcpyAsync(hp, res, sizeof(double) * nd, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+    *err = set_err(GLS_EHIP, "reduce_dots_async: D2H copy");
+    return nullptr;
+  }
+  return res;
+}
+int multidot_async(gls_ctx *c, const double *A, int64_t lda, int nk, const double *w, double *out, double *hp,
+                   const double **dev_res) {
+  const int64_t n1 = c->dist.on ? (int64_t)c->dim * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? (int64_t)c->dim * c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned_p : 0;
+  HIP_TRY(gls::vec_multidot2(A, lda, nk, w, n1, off2, n2, out, c->work.p, c->stream));
+  int err;
+  *dev_res = reduce_dots_async(c, out, nk, hp, &err);
+  return err;
+}
+int multiaxpy_dots_async(gls_ctx *c, double *w, const double *V, int64_t lda, int nk, const double *h, bool dots,
+                         double *out, double *hp, const double **dev_res, double scale = 1.0) {
+  const int64_t n1 = c->dist.on ? (int64_t)c->dim * c->dist.n_owned : c->n_dofs;
+  const int64_t off2 = c->dist.on ? (int64_t)c->dim * c->n_vnodes : 0;
+  const int64_t n2 = c->dist.on ? c->dist.n_owned_p : 0;
+  HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, scale, out, c->work.p,
+                                  c->stream));
+  int err;
+  *dev_res = reduce_dots_async(c, out, dots ? nk + 1 : 1, hp, &err);
+  return err;
 }
 
 }  // namespace
@@ -2697,6 +2747,14 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     GLS_TRY(c->krylov.alloc((size_t)(m + 1) * n));
     GLS_TRY(c->coef.alloc((size_t)m + 8));
     if (c->scal.n < (size_t)m + 8) GLS_TRY(c->scal.alloc((size_t)m + 8));
+    if (c->scal2.n < (size_t)m + 8) GLS_TRY(c->scal2.alloc((size_t)m + 8));
+    if (c->hpin_n < 3 * ((size_t)m + 8)) {
+      if (c->hpin) HIP_TRY(hipHostFree(c->hpin));
+      c->hpin = nullptr;
+      c->hpin_n = 0;
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->hpin), sizeof(double) * 3 * ((size_t)m + 8)));
+      c->hpin_n = 3 * ((size_t)m + 8);
+    }
     c->krylov_m = m;
   }
   if (!c->tmp1.p) {
@@ -2719,7 +2777,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   HIP_TRY(gls::vec_copy(r, b, n, s));
   double beta = std::sqrt(bnorm2);
   int it = 0;
-  std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hcol(m + 2), hc2(m + 2), y(m);
+  std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hc2(m + 2), y(m);
   bool converged = beta <= tol;
   const bool lverbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
   while (!converged && it < prm->max_iterations) {
@@ -2734,20 +2792,25 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       double *zj = keepz ? c->zbasis.p + (int64_t)j * n : z;
       GLS_TRY(apply_prec(c, vj, zj));
       GLS_TRY(gls_jacobian_apply(c, zj, w));
-      // h = V[0..j]^T w and ||w||^2 in one pass
-      GLS_TRY(dist_multidot(c, V, n, j + 2, w, hcol.data()));
-      const double wnorm0 = std::sqrt(std::max(hcol[j + 1], 0.0));
-      for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hcol[i];
-      HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
-      double wn2, wnorm;
+      // h = V[0..j]^T w and ||w||^2 in one pass. The Gram-Schmidt passes are chained on the stream:
+      // each projection reads the previous pass's dots from device memory (scal / scal2 alternate),
+      // the host copies arrive in pinned memory, and the host waits once per pass pair (after the
+      // projection, and after the DGKS correction when it is taken) instead of once per pass.
+      double *hp1 = c->hpin, *hp2 = c->hpin + (m + 8), *hp3 = c->hpin + 2 * (m + 8);
+      const double *hdev = nullptr, *h2dev = nullptr, *h3dev = nullptr;
+      GLS_TRY(multidot_async(c, V, n, j + 2, w, c->scal.p, hp1, &hdev));
+      double wn2, wnorm, wnorm0;
       bool normalized = false;  // w already scaled to v_{j+1} (H(j+1, j) set) by the fused DGKS pass
       if (j + 1 <= 8) {
         // projection fused with the DGKS dots and the norm: one pass over V instead of three
-        GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, true, hc2.data()));
+        GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, hdev, true, c->scal2.p, hp2, &h2dev));
+        HIP_TRY(hipStreamSynchronize(s));
+        wnorm0 = std::sqrt(std::max(hp1[j + 1], 0.0));
+        for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hp1[i];
+        std::copy(hp2, hp2 + j + 2, hc2.begin());
         wnorm = std::sqrt(std::max(hc2[j + 1], 0.0));
         if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation with the dots of the fused pass
           for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hc2[i];
-          HIP_TRY(hipMemcpyAsync(c->coef.p, hc2.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
           // ||w''||^2 = ||w'||^2 - |V^T w'|^2 (V orthonormal): the correction pass also normalises,
           // v_{j+1} = w'' / est, and H(j+1, j) = est keeps A z_j = V H exactly (|v_{j+1}| = 1 + O(eps))
           double h2 = 0.;
@@ -2755,25 +2818,34 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
           const double est2 = wnorm * wnorm - h2;
           if (est2 > 0.25 * wnorm * wnorm && est2 > 0.) {
             const double est = std::sqrt(est2);
-            GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2, 1.0 / est));
+            GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, h2dev, false, c->scal.p, hp3, &h3dev, 1.0 / est));
+            HIP_TRY(hipStreamSynchronize(s));
+            wn2 = hp3[0];
             H[(size_t)(j + 1) * m + j] = est;
             normalized = true;
             wnorm = est * std::sqrt(std::max(wn2, 0.0));
           } else {
-            GLS_TRY(dist_multiaxpy_dots(c, w, V, n, j + 1, c->coef.p, false, &wn2));
+            GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, h2dev, false, c->scal.p, hp3, &h3dev));
+            HIP_TRY(hipStreamSynchronize(s));
+            wn2 = hp3[0];
             wnorm = std::sqrt(std::max(wn2, 0.0));
           }
         }
       } else {
-        HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
-        GLS_TRY(device_dot(c, w, w, &wn2));
+        HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, hdev, 1.0, n, s));
+        GLS_TRY(multidot_async(c, w, 0, 1, w, c->scal2.p, hp2, &h2dev));
+        HIP_TRY(hipStreamSynchronize(s));
+        wnorm0 = std::sqrt(std::max(hp1[j + 1], 0.0));
+        for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hp1[i];
+        wn2 = hp2[0];
         wnorm = std::sqrt(std::max(wn2, 0.0));
         if (wnorm < 0.7071 * wnorm0) {  // DGKS re-orthogonalisation
-          GLS_TRY(dist_multidot(c, V, n, j + 1, w, hcol.data()));
-          for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hcol[i];
-          HIP_TRY(hipMemcpyAsync(c->coef.p, hcol.data(), sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
-          HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
-          GLS_TRY(device_dot(c, w, w, &wn2));
+          GLS_TRY(multidot_async(c, V, n, j + 1, w, c->scal.p, hp1, &hdev));
+          HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, hdev, 1.0, n, s));
+          GLS_TRY(multidot_async(c, w, 0, 1, w, c->scal2.p, hp2, &h2dev));
+          HIP_TRY(hipStreamSynchronize(s));
+          for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += hp1[i];
+          wn2 = hp2[0];
           wnorm = std::sqrt(std::max(wn2, 0.0));
         }
       }
