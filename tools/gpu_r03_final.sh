@@ -15,4 +15,8 @@ rc=$?; echo "bench rc $rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 150 python3 bench.py --workload cylinder3d --steps 5 --warmup 1 > gpurun_out/bench_cyl3d_final.json 2> gpurun_out/bench_cyl3d_final.err
 rc=$?; echo "cyl3d rc $rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 150 python3 bench.py --cells 64 --k 1 --kp 1 --nu 1 --scheme steady --steps 10 --warmup 3 --no-cpu > gpurun_out/bench_q1_final.json 2> gpurun_out/bench_q1_final.err
-rc=$?; echo "q1 rc $rc"; exit $rc
+rc=$?; echo "q1 rc $rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cyl3d_final -o run --output-format csv -- python3 bench.py --workload cylinder3d --steps 3 --warmup 1 > gpurun_out/bench_cyl3d_prof_final.json 2> gpurun_out/bench_cyl3d_prof_final.err
+rc=$?; echo "cyl3d prof rc $rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_final.log 2>&1
+rc=$?; echo "smoke rc $rc"; exit $rc
