@@ -491,7 +491,9 @@ def main():
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
                        args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if -2 in lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
-                   "parallelism": "domain decomposition x%d (RCCL P2P ghosts)" % world if world > 1 else "single"},
+                   "parallelism": ("domain decomposition x%d (%s)" % (world, "in-library RCCL P2P ghosts" if args.dist_impl == "native"
+                                                                     else "torch.distributed %s ghosts" % args.dist_backend))
+                   if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean(lin_its)),
         "residual_evaluations_per_step": float(np.mean(nres)),
