@@ -518,7 +518,7 @@ def main():
         "setup_s": t_setup,
     }
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r03_pmc_traffic_head_128.txt"), 4, N_global) \
+    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r03_pmc_traffic_head_s3_128.txt"), 4, N_global) \
         if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
     if tr is not None and args.k == 2 and world == 1:
         # the roof that actually binds the brick J.v: the LDS pipe (DESIGN §4 "What bounds the J.v").
@@ -534,7 +534,7 @@ def main():
                                   "source": "profiles/r03_lds_roof_model.txt"}
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
-        out["roofline"]["traffic_source"] = ("profiles/r03_pmc_traffic_head_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
+        out["roofline"]["traffic_source"] = ("profiles/r03_pmc_traffic_head_s3_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
                                              "%.2f (k_copy calibration); includes the per-quadrature-point "
                                              "linearization stream (16 doubles/q) the cached J.v reads instead "
                                              "of re-deriving u, grad u, tau, R_s" % (tr[1], tr[2]))
