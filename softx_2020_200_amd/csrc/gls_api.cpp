@@ -2778,11 +2778,16 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   double beta = std::sqrt(bnorm2);
   int it = 0;
   std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hc2(m + 2), y(m);
+  // Gram-corrected single-pass orthogonalisation (default; GLS_GMRES_CGS2=1: classical Gram-Schmidt with
+  // the DGKS second pass); Gm: measured off-diagonal part of V^T V of the current restart cycle
+  static const bool gram = [] { const char *e = std::getenv("GLS_GMRES_CGS2"); return !(e && std::atoi(e) != 0); }();
+  std::vector<double> Gm((size_t)(m + 1) * (m + 1), 0.0);
   bool converged = beta <= tol;
   const bool lverbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
   while (!converged && it < prm->max_iterations) {
     if (lverbose) std::printf("gmres: it %d residual %.6e (tol %.3e)\n", it, beta, tol);
     HIP_TRY(gls::vec_axpby(V, 1.0 / beta, r, 0.0, n, s));
+    std::fill(Gm.begin(), Gm.end(), 0.);
     std::fill(g.begin(), g.end(), 0.);
     g[0] = beta;
     int j = 0;
@@ -2801,7 +2806,72 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
       GLS_TRY(multidot_async(c, V, n, j + 2, w, c->scal.p, hp1, &hdev));
       double wn2, wnorm, wnorm0;
       bool normalized = false;  // w already scaled to v_{j+1} (H(j+1, j) set) by the fused DGKS pass
-      if (j + 1 <= 8) {
+      bool done = false;        // the Gram-corrected single projection below handled this column
+      if (gram) {
+        // Gram-corrected classical Gram-Schmidt: ONE projection pass with h = (2I - G) h1, where
+        // h1 = V^T w and G = V^T V (unit diagonal, off-diagonal part Gm measured by the previous
+        // projections' fused dots) -- the first-order inverse of G, so w - V h is orthogonal to the
+        // basis up to O(|G - I|^2) and rounding, as after CGS2's second pass, without that pass over
+        // V. The projection also normalises (est^2 = |w|^2 - 2 h.h1 + h^T G h) and returns V^T v_{j+1}
+        // (the next column of Gm) and |v_{j+1}|^2; a DGKS pass repairs the rare column whose measured
+        // orthogonality or norm is off by more than 1e-8 (catastrophic cancellation).
+        HIP_TRY(hipStreamSynchronize(s));
+        const double wn0sq = std::max(hp1[j + 1], 0.0);
+        wnorm0 = std::sqrt(wn0sq);
+        auto G = [&](int a, int b) { return Gm[(size_t)std::min(a, b) * (m + 1) + std::max(a, b)]; };
+        double *hc = hp3;
+        for (int i = 0; i <= j; ++i) {
+          double t = hp1[i];
+          for (int k = 0; k <= j; ++k)
+            if (k != i) t -= G(i, k) * hp1[k];
+          hc[i] = t;
+        }
+        double q = wn0sq;
+        for (int i = 0; i <= j; ++i) q += hc[i] * hc[i] - 2.0 * hc[i] * hp1[i];
+        for (int i = 0; i <= j; ++i)
+          for (int k = i + 1; k <= j; ++k) q += 2.0 * hc[i] * hc[k] * G(i, k);
+        if (q > 1e-20 * wn0sq && q > 0.) {
+          const double est = std::sqrt(q);
+          HIP_TRY(hipMemcpyAsync(c->coef.p, hc, sizeof(double) * (j + 1), hipMemcpyHostToDevice, s));
+          if (j + 1 <= 8) {
+            GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, c->coef.p, true, c->scal2.p, hp2, &h2dev, 1.0 / est));
+          } else {
+            HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, c->coef.p, 1.0, n, s));
+            HIP_TRY(gls::vec_scale(w, 1.0 / est, n, s));
+            GLS_TRY(multidot_async(c, V, n, j + 2, w, c->scal2.p, hp2, &h2dev));
+          }
+          HIP_TRY(hipStreamSynchronize(s));
+          for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] = hc[i];
+          H[(size_t)(j + 1) * m + j] = est;
+          double gmax = 0., gg = 0.;
+          for (int i = 0; i <= j; ++i) {
+            gmax = std::max(gmax, std::fabs(hp2[i]));
+            gg += hp2[i] * hp2[i];
+          }
+          const double nrm2 = hp2[j + 1];
+          const double est2 = std::sqrt(std::max(nrm2 - gg, 0.0));
+          if ((gmax > 1e-8 || std::fabs(nrm2 - 1.0) > 1e-8) && est2 > 0.) {
+            // v = V g + est2 v', v' = (v - V g) / est2: H column += est g, H(j+1, j) = est est2
+            for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += est * hp2[i];
+            H[(size_t)(j + 1) * m + j] = est * est2;
+            if (j + 1 <= 8) {
+              GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, h2dev, true, c->scal.p, hp1, &hdev, 1.0 / est2));
+            } else {
+              HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, h2dev, 1.0, n, s));
+              HIP_TRY(gls::vec_scale(w, 1.0 / est2, n, s));
+              GLS_TRY(multidot_async(c, V, n, j + 2, w, c->scal.p, hp1, &hdev));
+            }
+            HIP_TRY(hipStreamSynchronize(s));
+            for (int i = 0; i <= j; ++i) Gm[(size_t)i * (m + 1) + j + 1] = hp1[i];
+          } else {
+            for (int i = 0; i <= j; ++i) Gm[(size_t)i * (m + 1) + j + 1] = hp2[i];
+          }
+          wnorm = H[(size_t)(j + 1) * m + j];
+          normalized = done = true;
+        }
+      }
+      if (done) {
+      } else if (j + 1 <= 8) {
         // projection fused with the DGKS dots and the norm: one pass over V instead of three
         GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, hdev, true, c->scal2.p, hp2, &h2dev));
         HIP_TRY(hipStreamSynchronize(s));
