@@ -1154,27 +1154,6 @@ int ensure_diag(gls_ctx *c) {
   return GLS_OK;
 }
 
-// w -= V[0..nk) h (h on device, nk <= 8) fused with host_out[k] = V_k . w_new (k < nk, when dots) and
-// host_out[dots ? nk : 0] = ||w_new||^2 over owned DoFs, reduced over ranks
-int dist_multiaxpy_dots(gls_ctx *c, double *w, const double *V, int64_t lda, int nk, const double *h, bool dots,
-                        double *host_out, double scale = 1.0) {
-  const int64_t n1 = c->dist.on ? (int64_t)c->dim * c->dist.n_owned : c->n_dofs;
-  const int64_t off2 = c->dist.on ? (int64_t)c->dim * c->n_vnodes : 0;
-  const int64_t n2 = c->dist.on ? c->dist.n_owned_p : 0;
-  const int nd = dots ? nk + 1 : 1;
-  HIP_TRY(gls::vec_multiaxpy_dots(w, V, lda, nk, h, 1.0, c->n_dofs, n1, off2, n2, dots, scale, c->scal.p, c->work.p,
-                                  c->stream));
-  if (c->dist.on) {
-    HIP_TRY(hipMemcpyAsync(c->dist.red_buf, c->scal.p, sizeof(double) * nd, hipMemcpyDeviceToDevice, c->stream));
-    if (c->dist.allreduce(c->dist.user, c->dist.red_buf, nd) != 0) return set_err(GLS_ECOMM, "allreduce failed");
-    HIP_TRY(hipMemcpyAsync(host_out, c->dist.red_buf, sizeof(double) * nd, hipMemcpyDeviceToHost, c->stream));
-  } else {
-    HIP_TRY(hipMemcpyAsync(host_out, c->scal.p, sizeof(double) * nd, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  return GLS_OK;
-}
-
 int device_dot(gls_ctx *c, const double *a, const double *b, double *host_out) {
   return dist_multidot(c, a, 0, 1, b, host_out);
 }
@@ -2733,9 +2712,10 @@ int gls_mg_detach(gls_ctx *c) {
 }
 
 // --------------------------------------------------------------------------------------------
-// GMRES(m), right preconditioned by the Jacobian diagonal. Classical Gram–Schmidt with one
-// DGKS re-orthogonalisation pass; fused multi-dot / multi-axpy kernels (one pass over the
-// Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
+// GMRES(m), right preconditioned (Jacobi, the V-cycle or the assembled ILU). Orthogonalisation:
+// Gram-corrected classical Gram–Schmidt (one projection pass per iteration, see the loop) or, with
+// GLS_GMRES_CGS2=1, classical Gram–Schmidt with one DGKS re-orthogonalisation pass; fused multi-dot /
+// multi-axpy kernels (one pass over the Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
 // ||b - A x|| <= max(rel*||b||, abs) (deal.II SolverControl / AztecOO AZ_noscaled).
 // --------------------------------------------------------------------------------------------
 int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *prm) {
