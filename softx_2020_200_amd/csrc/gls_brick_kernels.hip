@@ -713,12 +713,14 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
             const Real Rq[3] = {lds(Nat(7) + qq, zm), lds(Nat(8) + qq, zm), lds(Nat(9) + qq, zm)};
             const Real av = uq[0] * g[0] + uq[1] * g[1] + uq[2] * g[2];
             const Real g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
+            // the same sum with the component-independent part factored out (A = gc_c phi + av):
+            // jw [av phi + nu g2 + tq av (av - nu lap)] + gc_c jw phi (phi + tq av) + Rq_c g_c jw tq phi
+            const Real jt = jw * tq;
+            const Real c0 = jw * (av * phi + nu * g2) + jt * av * (av - nu * lap);
+            const Real k1 = jw * phi * (phi + tq * av), k2 = jt * phi;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const Real A = gc[c] * phi + av;
-              acc[c] += jw * (A * phi + nu * g2 + tq * (A - nu * lap) * av + tq * Rq[c] * phi * g[c]);
-            }
-            acc[3] += jw * tq * g2;
+            for (int c = 0; c < 3; ++c) acc[c] += c0 + gc[c] * k1 + k2 * Rq[c] * g[c];
+            acc[3] += jt * g2;
           }
         }
       }
