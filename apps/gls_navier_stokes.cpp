@@ -50,7 +50,7 @@ std::atomic<int> *g_abort = nullptr;  // --np: raised by a failing rank, every o
   std::fprintf(stderr, "\n");
   va_end(ap);
   if (g_abort) g_abort->store(1);
-  std::exit(2);
+  std::exit(1);
 }
 void ck(int rc, const char *what) {
   if (rc < 0 && rc != GLS_ENOCONV) die("%s failed (%d): %s", what, rc, gls_last_error());
@@ -174,6 +174,10 @@ struct Params {
   double lin_rel = 1e-3, lin_min = 1e-8;
   double ilu_atol = 1e-8, ilu_rtol = 1.0;
   int ilu_fill = 0;
+  int lin_method = 0;  // linear solver/method: 0 gmres, 1 bicgstab, 2 amg
+  int amg_ilu_fill = 0, amg_n_cycles = 1, amg_sweeps = 2, amg_overlap = 1;
+  double amg_ilu_atol = 1e-12, amg_ilu_rtol = 1.0, amg_threshold = 1e-14;
+  bool amg_w_cycles = false;
   std::string timer = "none";  // timer/type none | iteration | end (parameters.cc:136-164)
   bool srf = false;
   double omega[3] = {0, 0, 0};
@@ -327,6 +331,40 @@ Params read_params(const Prm &p, int dim) {
   }
   P.ilu_atol = p.d("linear solver/ilu preconditioner absolute tolerance", 1e-8);
   P.ilu_rtol = p.d("linear solver/ilu preconditioner relative tolerance", 1.0);
+  // linear solver/method (parameters.cc:519-532, 616-626; dispatch gls_navier_stokes.cc:1140-1157):
+  // gmres and bicgstab with the ILU(fill) of the entries above (or the geometric multigrid V-cycle where
+  // the nested hyper_cube hierarchy exists); amg = GMRES + ML AMG with ILU smoother / coarsener
+  // (setup_AMG, :1180-1240), which this library substitutes explicitly (announced at setup, see
+  // Solver::announce_linear_solver): the geometric multigrid V-cycle on nested hyper_cubes, elsewhere
+  // the ILU(amg preconditioner ilu fill / absolute / relative tolerance) that ML would smooth with.
+  // The amg entries are validated (parameters.cc:562-595, 627-644) even where they do not act.
+  {
+    const std::string m = p.get("linear solver/method", "gmres");
+    if (m == "gmres") P.lin_method = 0;
+    else if (m == "bicgstab") P.lin_method = 1;
+    else if (m == "amg") P.lin_method = 2;
+    else die("linear solver/method '%s' is invalid (amg | gmres | bicgstab)", m.c_str());
+    const double af = p.d("linear solver/amg preconditioner ilu fill", 0.0);
+    if (!(af >= 0 && af <= GLS_ILU_MAX_FILL) || af != std::floor(af))
+      die("linear solver/amg preconditioner ilu fill = %g is not supported (integers 0..%d)", af, GLS_ILU_MAX_FILL);
+    P.amg_ilu_fill = (int)af;
+    P.amg_ilu_atol = p.d("linear solver/amg preconditioner ilu absolute tolerance", 1e-12);
+    P.amg_ilu_rtol = p.d("linear solver/amg preconditioner ilu relative tolerance", 1.0);
+    P.amg_threshold = p.d("linear solver/amg aggregation threshold", 1e-14);
+    P.amg_n_cycles = p.i("linear solver/amg n cycles", 1);
+    P.amg_w_cycles = p.b("linear solver/amg w cycles", false);
+    P.amg_sweeps = p.i("linear solver/amg smoother sweeps", 2);
+    P.amg_overlap = p.i("linear solver/amg smoother overlap", 1);
+    if (P.amg_n_cycles < 1) die("linear solver/amg n cycles must be >= 1");
+    if (P.amg_sweeps < 0 || P.amg_overlap < 0) die("linear solver/amg smoother sweeps / overlap must be >= 0");
+    if (P.amg_threshold < 0) die("linear solver/amg aggregation threshold must be >= 0");
+    const std::string v = p.get("linear solver/verbosity", "verbose");
+    if (v != "verbose" && v != "quiet") die("Unknown verbosity mode for the linear solver");
+  }
+  // restart (parameters.cc:759-798): checkpoint / restart files are out of scope; a prm
+  // that asks for either fails here instead of silently running without it
+  if (p.b("restart/restart", false)) die("restart/restart = true: restarting from a checkpoint is not supported");
+  if (p.b("restart/checkpoint", false)) die("restart/checkpoint = true: checkpointing is not supported");
   P.timer = p.get("timer/type", "none");
   if (P.timer != "none" && P.timer != "iteration" && P.timer != "end") die("timer/type '%s' is unknown", P.timer.c_str());
   P.srf = p.get("velocity source/type", "none") == "srf";
@@ -862,9 +900,10 @@ struct ShmComm {
     glob = slots + (size_t)w * kSlot;
   }
   double *slot(int r) const { return slots + (size_t)r * kSlot; }
-  // sense-reversing; a rank that failed raises abort. Watchdog: a rank left waiting longer than
-  // GLS_NP_WATCHDOG seconds (default 60) reports every rank's barrier count and last tag -- ranks
-  // that disagree name the collective one of them skipped -- and aborts the run.
+  // sense-reversing; a rank that failed raises abort. Watchdog: when NO rank has entered a barrier for
+  // GLS_NP_WATCHDOG seconds (default 600) while this one waits -- a stall, not merely long rank-local
+  // work (output, Kelly, ILU setup on big meshes) -- it reports every rank's barrier count and last
+  // tag (ranks that disagree name the collective one of them skipped) and aborts the run.
   void barrier(const char *tag = "") const {
     ++hdr->nbar[rank];
     std::snprintf(hdr->tag[rank], sizeof(hdr->tag[rank]), "%s", tag);
@@ -874,11 +913,21 @@ struct ShmComm {
       hdr->gen.fetch_add(1);
       return;
     }
-    static const double limit = std::getenv("GLS_NP_WATCHDOG") ? std::atof(std::getenv("GLS_NP_WATCHDOG")) : 60.0;
-    const auto t0 = std::chrono::steady_clock::now();
+    static const double limit = std::getenv("GLS_NP_WATCHDOG") ? std::atof(std::getenv("GLS_NP_WATCHDOG")) : 600.0;
+    auto progress = [&]() {
+      int64_t t = 0;
+      for (int r = 0; r < world; ++r) t += hdr->nbar[r];
+      return t;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    int64_t seen = progress();
     for (uint64_t spin = 0; hdr->gen.load() == g; ++spin) {
       if (hdr->abort.load()) _exit(3);
       sched_yield();
+      if ((spin & 4095) == 0 && progress() != seen) {  // another rank reached a barrier: not stalled
+        seen = progress();
+        t0 = std::chrono::steady_clock::now();
+      }
       if ((spin & 4095) == 0 &&
           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
         std::fprintf(stderr, "--np watchdog: rank %d waited %.0f s at barrier #%lld (%s); ranks:", rank, limit,
@@ -1731,6 +1780,30 @@ struct Solver {
     }
   }
 
+  // the linear solver and preconditioner actually used for the prm's 'linear solver/method', once per
+  // run on stderr (stdout stays the reference's): the substitutions are explicit, never silent
+  bool lin_announced = false;
+  void announce_linear_solver() {
+    if (lin_announced || rank != 0) return;
+    lin_announced = true;
+    const char *meth[3] = {"gmres", "bicgstab", "amg"};
+    const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
+    char prec[256];
+    if (!mg_levels.empty())
+      std::snprintf(prec, sizeof prec, "geometric multigrid V(1,1)-cycle on the nested hyper_cubes");
+    else if (use_ilu && P.lin_method == 2)
+      std::snprintf(prec, sizeof prec, "ILU(%d) atol %g rtol %g (the amg smoother's ILU on the fine level)",
+                    P.amg_ilu_fill, P.amg_ilu_atol, P.amg_ilu_rtol);
+    else if (use_ilu)
+      std::snprintf(prec, sizeof prec, "ILU(%d) atol %g rtol %g", P.ilu_fill, P.ilu_atol, P.ilu_rtol);
+    else
+      std::snprintf(prec, sizeof prec, "Jacobi (--precond jacobi)");
+    std::fprintf(stderr, "linear solver: method = %s -> %s + %s%s\n", meth[P.lin_method], krylov, prec,
+                 P.lin_method == 2 ? (P.amg_w_cycles ? "; ML AMG substituted (amg w cycles = true: V-cycle used)"
+                                                     : "; ML AMG substituted")
+                                   : "");
+  }
+
   // ---- one nonlinear solve of `scheme` from the current present solution and history
   // solve_non_linear_system(method, first_iteration = false, force_matrix_renewal)
   void solve_nonlinear(int scheme, double nu_override = -1.0, bool force_renewal = false) {
@@ -1760,14 +1833,19 @@ struct Solver {
       const int order = ilu_order >= 0 ? ilu_order
                         : (m.n_dofs() > kIluMulticolorDofs || world > 1 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM);
       ck(gls_ilu_set_options(ctx, order, ilu_block_dofs), "gls_ilu_set_options");
-      ck(gls_ilu_attach(ctx, P.ilu_fill, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
+      if (P.lin_method == 2)  // amg: the ILU ML would smooth / coarsen with (setup_AMG, :1225-1233)
+        ck(gls_ilu_attach(ctx, P.amg_ilu_fill, P.amg_ilu_atol, P.amg_ilu_rtol), "gls_ilu_attach");
+      else
+        ck(gls_ilu_attach(ctx, P.ilu_fill, P.ilu_atol, P.ilu_rtol), "gls_ilu_attach");
       ilu_ctx = ctx;
     }
+    announce_linear_solver();
     const bool jacobi = mg_levels.empty() && !use_ilu;
     np.lin.max_iterations = jacobi ? std::max(P.lin_max, 20000) : P.lin_max;
     np.lin.restart = jacobi ? std::max(P.restart, 100) : P.restart;
     np.lin.relative_residual = P.lin_rel;
     np.lin.minimum_residual = P.lin_min;
+    np.lin.method = P.lin_method == 1 ? GLS_LIN_BICGSTAB : GLS_LIN_GMRES;
     np.solver = P.nl_solver;
     np.skip_iterations = P.skip_iterations;
     np.is_initial_step = 0;

@@ -151,12 +151,24 @@ int gls_apply_dirichlet(gls_ctx *ctx, double *x);
  * Jacobi (diagonal) preconditioner; tolerance = max(rel*||rhs||, abs) as the reference.
  * x and rhs are DEVICE pointers. Returns GLS_OK or GLS_ENOCONV (x holds the last iterate).
  * ------------------------------------------------------------------------------------------ */
+#define GLS_LIN_GMRES 0     /* solve_system_GMRES (gls_navier_stokes.cc:1242-1289) */
+#define GLS_LIN_BICGSTAB 1  /* solve_system_BiCGStab (gls_navier_stokes.cc:1293-1340): right-preconditioned
+                               BiCGStab, same preconditioner and tolerance rule; an iteration = one
+                               BiCGStab step (two operator applications), as AztecOO counts them */
+#define GLS_ORTHO_GRAM 0    /* GMRES: Gram-corrected single-pass classical Gram-Schmidt (default) */
+#define GLS_ORTHO_CGS2 1    /* GMRES: classical Gram-Schmidt + DGKS re-orthogonalisation pass */
 typedef struct {
   int max_iterations;     /* linear solver/max iters */
   int restart;            /* GMRES restart (deal.II default 30) */
   double relative_residual, minimum_residual;
   int iterations;         /* out */
   double final_residual;  /* out */
+  int method;             /* GLS_LIN_GMRES (0, default) | GLS_LIN_BICGSTAB ('linear solver/method',
+                             parameters.cc:519-532; 'amg' is GMRES with the caller's preconditioner) */
+  int orthogonalization;  /* GMRES only: GLS_ORTHO_GRAM (0) | GLS_ORTHO_CGS2; the environment variable
+                             GLS_GMRES_CGS2=1 forces CGS2 for every call */
+  int true_residual;      /* in: 1 = on convergence recompute ||b - A x|| into final_residual (one extra
+                             operator application); 0 = the Krylov recurrence estimate (deal.II) */
 } gls_linear_params;
 int gls_solve_linear(gls_ctx *ctx, const double *rhs, double *x, gls_linear_params *prm);
 

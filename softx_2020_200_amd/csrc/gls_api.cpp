@@ -311,6 +311,7 @@ struct gls_ctx {
   size_t hpin_n = 0;
   DevBuf<double> krylov;      // (restart+1) x n_dofs
   DevBuf<double> zbasis;      // restart x n_dofs: M^-1 v_j when the preconditioner is the V-cycle
+  DevBuf<double> bicg;        // 7 x n_dofs BiCGStab work vectors (when the GMRES basis is smaller)
   int krylov_m = 0;
   DevBuf<double> tmp1, tmp2, tmp3, tmp4, tmp5;
   bool use_brick = false;  // sum-factorized brick kernels (3D Qk-Qk, Morton 2x2x2 bricks)
@@ -2262,6 +2263,10 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
   // across ranks the constrained rows' diagonal is the exchanged one: computed before the local probes
   if (c->dist.on && (c->con_dofs.n || I.complete)) GLS_TRY(ensure_diag(c));
   c->probe_local = c->dist.on;  // the probe's J.v: the rank's cells only, no ghost exchange
+  struct ProbeLocalGuard {      // every exit path (errors included) restores the exchanging operator
+    gls_ctx *c;
+    ~ProbeLocalGuard() { c->probe_local = false; }
+  } guard{c};
   auto &D = c->dist;
   const int rounds = I.complete ? I.n_rounds : I.n_probes;
   for (int p = 0; p < rounds; ++p) {
@@ -2277,10 +2282,7 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
     // ghost rows of this probe (the local cells' part of a neighbour's owned rows) to their owners
     if (p < I.n_probes) HIP_TRY(gls::vec_pack_dofs(I.ybuf.p, D.recv_nodes.p, D.n_recv, D.recv_buf, s));
     else if (D.n_recv) HIP_TRY(gls::vec_fill(D.recv_buf, D.n_recv, 0.0, s));
-    if (D.xchg(D.user, 1) != 0) {
-      c->probe_local = false;
-      return set_err(GLS_ECOMM, "ILU probe exchange failed");
-    }
+    if (D.xchg(D.user, 1) != 0) return set_err(GLS_ECOMM, "ILU probe exchange failed");
     const int64_t a = I.rr[(size_t)p], b = I.rr[(size_t)p + 1];
     if (b > a) HIP_TRY(gls::vec_add_dofs_ordered(I.val.p, I.ru.p + a, I.ruoff.p + a, I.rslot.p, b - a, D.send_buf, s));
   }
@@ -2718,6 +2720,89 @@ int gls_mg_detach(gls_ctx *c) {
 // multi-axpy kernels (one pass over the Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
 // ||b - A x|| <= max(rel*||b||, abs) (deal.II SolverControl / AztecOO AZ_noscaled).
 // --------------------------------------------------------------------------------------------
+// BiCGStab (solve_system_BiCGStab, gls_navier_stokes.cc:1293-1340: TrilinosWrappers::SolverBicgstab =
+// AztecOO AZ_bicgstab with the same ILU, here with whatever preconditioner gls_solve_linear applies),
+// right preconditioned (van der Vorst's BiCGStab on A M^-1, x = M^-1 y), so the recursively updated
+// residual is the unpreconditioned b - A x the reference's tolerance rule tests:
+// ||r|| <= max(rel ||b||, abs). One iteration = one BiCGStab step (two operator applications), as
+// AztecOO counts. Breakdown (rho or (rhat, v) or (t, t) vanishing) stops with the current iterate.
+static int solve_bicgstab(gls_ctx *c, const double *b, double *x, gls_linear_params *prm) {
+  const int64_t n = c->n_dofs;
+  hipStream_t s = c->stream;
+  // work vectors: r, rhat, p, v, phat, shat, t (the GMRES basis storage when it is large enough)
+  double *w[7];
+  if (c->krylov.p && c->krylov.n >= (size_t)7 * n) {
+    for (int i = 0; i < 7; ++i) w[i] = c->krylov.p + (int64_t)i * n;
+  } else {
+    if (c->bicg.n != (size_t)7 * n) GLS_TRY(c->bicg.alloc((size_t)7 * n));
+    for (int i = 0; i < 7; ++i) w[i] = c->bicg.p + (int64_t)i * n;
+  }
+  double *r = w[0], *rh = w[1], *p = w[2], *v = w[3], *ph = w[4], *sh = w[5], *t = w[6];
+  double bn2;
+  GLS_TRY(device_dot(c, b, b, &bn2));
+  const double tol = std::max(prm->relative_residual * std::sqrt(bn2), prm->minimum_residual);
+  HIP_TRY(gls::vec_fill(x, n, 0.0, s));
+  HIP_TRY(gls::vec_copy(r, b, n, s));
+  HIP_TRY(gls::vec_copy(rh, b, n, s));
+  HIP_TRY(gls::vec_fill(p, n, 0.0, s));
+  HIP_TRY(gls::vec_fill(v, n, 0.0, s));
+  double res = std::sqrt(bn2), rho = 1.0, alpha = 1.0, omega = 1.0;
+  int it = 0;
+  bool converged = res <= tol;
+  while (!converged && it < prm->max_iterations) {
+    double rho1;
+    GLS_TRY(device_dot(c, rh, r, &rho1));
+    if (rho1 == 0.0 || omega == 0.0) break;  // breakdown
+    const double beta = (rho1 / rho) * (alpha / omega);
+    rho = rho1;
+    // p = r + beta (p - omega v)
+    HIP_TRY(gls::vec_axpy(p, -omega, v, n, s));
+    HIP_TRY(gls::vec_axpby(p, 1.0, r, beta, n, s));
+    GLS_TRY(apply_prec(c, p, ph));
+    GLS_TRY(gls_jacobian_apply(c, ph, v));
+    double rhv;
+    GLS_TRY(device_dot(c, rh, v, &rhv));
+    if (rhv == 0.0) break;
+    alpha = rho / rhv;
+    HIP_TRY(gls::vec_axpy(r, -alpha, v, n, s));  // r <- s = r - alpha v
+    HIP_TRY(gls::vec_axpy(x, alpha, ph, n, s));  // x += alpha M^-1 p
+    ++it;
+    double sn2;
+    GLS_TRY(device_dot(c, r, r, &sn2));
+    res = std::sqrt(sn2);
+    if (res <= tol) {
+      converged = true;
+      break;
+    }
+    GLS_TRY(apply_prec(c, r, sh));
+    GLS_TRY(gls_jacobian_apply(c, sh, t));
+    double tt, ts;
+    GLS_TRY(device_dot(c, t, t, &tt));
+    GLS_TRY(device_dot(c, t, r, &ts));
+    if (tt == 0.0) break;
+    omega = ts / tt;
+    HIP_TRY(gls::vec_axpy(x, omega, sh, n, s));  // x += omega M^-1 s
+    HIP_TRY(gls::vec_axpy(r, -omega, t, n, s));  // r = s - omega t
+    double rn2;
+    GLS_TRY(device_dot(c, r, r, &rn2));
+    res = std::sqrt(rn2);
+    converged = res <= tol;
+    if (getenv("GLS_GMRES_VERBOSE") && (it % 10 == 0 || it == 1))
+      printf("  bicgstab it %d  res %.6e  (tol %.3e)\n", it, res, tol);
+  }
+  if (converged && prm->true_residual) {
+    GLS_TRY(gls_jacobian_apply(c, x, t));
+    HIP_TRY(gls::vec_axpby(t, 1.0, b, -1.0, n, s));
+    double rn2;
+    GLS_TRY(device_dot(c, t, t, &rn2));
+    res = std::sqrt(rn2);
+  }
+  prm->iterations = it;
+  prm->final_residual = res;
+  if (!converged) return set_err(GLS_ENOCONV, "BiCGStab: %d iterations, residual %.3e > %.3e", it, res, tol);
+  return GLS_OK;
+}
+
 int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *prm) {
   GLS_TRY(check_ctx(c));
   if (!b || !x || !prm) return set_err(GLS_EINVAL, "null argument");
@@ -2744,6 +2829,8 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   GLS_TRY(ensure_diag(c));
   if (c->mg.on) GLS_TRY(mg_prepare(c));
   GLS_TRY(ensure_ilu(c));
+  if (prm->method == GLS_LIN_BICGSTAB) return solve_bicgstab(c, b, x, prm);
+  if (prm->method != GLS_LIN_GMRES) return set_err(GLS_EINVAL, "linear solver method %d unknown", prm->method);
   // with the V-cycle, keep Z = M^-1 V (flexible-GMRES storage): the update x += Z y then needs no
   // extra preconditioner application per restart cycle
   const bool keepz = c->mg.on;
@@ -2758,9 +2845,16 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   double beta = std::sqrt(bnorm2);
   int it = 0;
   std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hc2(m + 2), y(m);
-  // Gram-corrected single-pass orthogonalisation (default; GLS_GMRES_CGS2=1: classical Gram-Schmidt with
-  // the DGKS second pass); Gm: measured off-diagonal part of V^T V of the current restart cycle
-  static const bool gram = [] { const char *e = std::getenv("GLS_GMRES_CGS2"); return !(e && std::atoi(e) != 0); }();
+  // Gram-corrected single-pass orthogonalisation (default; prm->orthogonalization = GLS_ORTHO_CGS2 or
+  // GLS_GMRES_CGS2=1: classical Gram-Schmidt with the DGKS second pass); Gm: measured off-diagonal part
+  // of V^T V of the current restart cycle
+  static const bool env_cgs2 = [] { const char *e = std::getenv("GLS_GMRES_CGS2"); return e && std::atoi(e) != 0; }();
+  const bool gram = !env_cgs2 && prm->orthogonalization != GLS_ORTHO_CGS2;
+  int ortho_repairs = 0;
+  // test knobs (read per call): GLS_GMRES_REPAIR_TOL (default 1e-8; 0 repairs every column) and
+  // GLS_GMRES_REPAIR_MEASURED=1 (the repair pass always normalises by the measured norm)
+  const double repair_tol = std::getenv("GLS_GMRES_REPAIR_TOL") ? std::atof(std::getenv("GLS_GMRES_REPAIR_TOL")) : 1e-8;
+  const bool repair_measured = std::getenv("GLS_GMRES_REPAIR_MEASURED") != nullptr;
   std::vector<double> Gm((size_t)(m + 1) * (m + 1), 0.0);
   bool converged = beta <= tol;
   const bool lverbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
@@ -2829,20 +2923,36 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
             gg += hp2[i] * hp2[i];
           }
           const double nrm2 = hp2[j + 1];
-          const double est2 = std::sqrt(std::max(nrm2 - gg, 0.0));
-          if ((gmax > 1e-8 || std::fabs(nrm2 - 1.0) > 1e-8) && est2 > 0.) {
-            // v = V g + est2 v', v' = (v - V g) / est2: H column += est g, H(j+1, j) = est est2
+          const double est2sq = nrm2 - gg;  // |v - V g|^2 if V were exactly orthonormal
+          if (gmax > repair_tol || std::fabs(nrm2 - 1.0) > repair_tol) {
+            // repair pass v' = (v - V g) / s: H column += est g, H(j+1, j) = est s. The first-order
+            // estimate s = sqrt(|v|^2 - |g|^2) is used only when the cancellation leaves it well
+            // above rounding (est2sq > 1e-4); otherwise the pass runs unscaled and s is the MEASURED
+            // norm of its result. Either way the measured |v'|^2 returned by the pass decides: a
+            // vector off unit length by more than 1e-8 is rescaled (with its H entry and Gram
+            // column), and a vanishing one is a breakdown (the Krylov space is exhausted).
+            const bool use_est = est2sq > 1e-4 && !repair_measured;
+            const double est2 = use_est ? std::sqrt(est2sq) : 1.0;
             for (int i = 0; i <= j; ++i) H[(size_t)i * m + j] += est * hp2[i];
-            H[(size_t)(j + 1) * m + j] = est * est2;
             if (j + 1 <= 8) {
               GLS_TRY(multiaxpy_dots_async(c, w, V, n, j + 1, h2dev, true, c->scal.p, hp1, &hdev, 1.0 / est2));
             } else {
               HIP_TRY(gls::vec_multiaxpy(w, V, n, j + 1, h2dev, 1.0, n, s));
-              HIP_TRY(gls::vec_scale(w, 1.0 / est2, n, s));
+              if (use_est) HIP_TRY(gls::vec_scale(w, 1.0 / est2, n, s));
               GLS_TRY(multidot_async(c, V, n, j + 2, w, c->scal.p, hp1, &hdev));
             }
             HIP_TRY(hipStreamSynchronize(s));
-            for (int i = 0; i <= j; ++i) Gm[(size_t)i * (m + 1) + j + 1] = hp1[i];
+            const double nn = std::max(hp1[j + 1], 0.0);  // measured |v'|^2
+            double sc = 1.0;                               // v_{j+1} = v' / sc
+            if (nn <= 1e-28 * (use_est ? 1.0 : std::max(nrm2, 1e-300))) {
+              sc = 0.0;  // breakdown: w lies in span(V) to rounding
+            } else if (!use_est || std::fabs(nn - 1.0) > 1e-8) {
+              sc = std::sqrt(nn);
+              HIP_TRY(gls::vec_scale(w, 1.0 / sc, n, s));
+            }
+            H[(size_t)(j + 1) * m + j] = est * est2 * sc;
+            for (int i = 0; i <= j; ++i) Gm[(size_t)i * (m + 1) + j + 1] = sc > 0. ? hp1[i] / sc : 0.;
+            ++ortho_repairs;
           } else {
             for (int i = 0; i <= j; ++i) Gm[(size_t)i * (m + 1) + j + 1] = hp2[i];
           }
@@ -2944,6 +3054,13 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     if (res <= tol) {
       beta = res;
       converged = true;
+      if (prm->true_residual) {  // the caller asked for ||b - A x|| instead of the recurrence estimate
+        GLS_TRY(gls_jacobian_apply(c, x, r));
+        HIP_TRY(gls::vec_axpby(r, 1.0, b, -1.0, n, s));
+        double rn2;
+        GLS_TRY(device_dot(c, r, r, &rn2));
+        beta = std::sqrt(rn2);
+      }
       break;
     }
     // true residual r = b - A x
@@ -2957,6 +3074,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   }
   prm->iterations = it;
   prm->final_residual = beta;
+  if (ortho_repairs && std::getenv("GLS_GMRES_VERBOSE")) printf("  gmres: %d orthogonality repair passes\n", ortho_repairs);
   if (!converged) return set_err(GLS_ENOCONV, "GMRES: %d iterations, residual %.3e > %.3e", it, beta, tol);
   return GLS_OK;
 }

@@ -81,7 +81,12 @@ class FESpace(C.Structure):
 
 class LinearParams(C.Structure):
     _fields_ = [("max_iterations", C.c_int), ("restart", C.c_int), ("relative_residual", C.c_double),
-                ("minimum_residual", C.c_double), ("iterations", C.c_int), ("final_residual", C.c_double)]
+                ("minimum_residual", C.c_double), ("iterations", C.c_int), ("final_residual", C.c_double),
+                ("method", C.c_int), ("orthogonalization", C.c_int), ("true_residual", C.c_int)]
+
+
+LIN_METHODS = {"gmres": 0, "bicgstab": 1}
+ORTHO = {"gram": 0, "cgs2": 1}
 
 
 class MGParams(C.Structure):
@@ -641,9 +646,13 @@ class GLSContext:
         return x
 
     def solve_linear(self, rhs, x=None, max_iterations=1000, restart=30, relative_residual=1e-4,
-                     minimum_residual=1e-12):
+                     minimum_residual=1e-12, method="gmres", orthogonalization="gram", true_residual=False):
+        """solve_system_GMRES / solve_system_BiCGStab (method="bicgstab") with the attached preconditioner.
+        orthogonalization: GMRES's "gram" (Gram-corrected single pass) or "cgs2"; true_residual: report
+        ||b - A x|| at convergence instead of the Krylov recurrence estimate."""
         x = self.zeros() if x is None else x
-        p = LinearParams(max_iterations, restart, relative_residual, minimum_residual, 0, 0.0)
+        p = LinearParams(max_iterations, restart, relative_residual, minimum_residual, 0, 0.0,
+                         LIN_METHODS[method], ORTHO[orthogonalization], int(bool(true_residual)))
         rc = self.L.gls_solve_linear(self.h, _ptr(rhs), _ptr(x), C.byref(p))
         if rc < 0 and rc != GLS_ENOCONV:
             check(rc, "gls_solve_linear")
@@ -651,10 +660,13 @@ class GLSContext:
 
     def newton(self, present, u1=None, u2=None, u3=None, tolerance=1e-8, max_iterations=10, verbosity=0,
                lin_max_iterations=1000, restart=30, relative_residual=1e-4, minimum_residual=1e-12,
-               solver="newton", skip_iterations=1, is_initial_step=False, force_matrix_renewal=False):
-        """NewtonNonLinearSolver::solve / SkipNewtonNonLinearSolver::solve (solver="skip_newton")."""
+               solver="newton", skip_iterations=1, is_initial_step=False, force_matrix_renewal=False,
+               lin_method="gmres", orthogonalization="gram"):
+        """NewtonNonLinearSolver::solve / SkipNewtonNonLinearSolver::solve (solver="skip_newton");
+        lin_method: the linear solver ("gmres" | "bicgstab")."""
         self._state = (present, u1, u2, u3)
-        lp = LinearParams(lin_max_iterations, restart, relative_residual, minimum_residual, 0, 0.0)
+        lp = LinearParams(lin_max_iterations, restart, relative_residual, minimum_residual, 0, 0.0,
+                          LIN_METHODS[lin_method], ORTHO[orthogonalization], 0)
         p = NewtonParams(tolerance, max_iterations, verbosity, lp, 0, 0, 0, 0.0,
                          {"newton": 0, "skip_newton": 1}[solver], int(skip_iterations), int(is_initial_step),
                          int(force_matrix_renewal), 0)

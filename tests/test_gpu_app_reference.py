@@ -154,3 +154,26 @@ def test_reference_cylinder_kelly_adaptation_converged(tmp_path):
         "set minimum residual        = 1e-9", "set minimum residual = 1e-14"))
     ours, theirs = setup_lines(out), setup_lines(ref)
     assert ours == theirs, (ours, theirs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["gmres", "bicgstab", "amg"])
+def test_reference_mms2d_every_linear_solver_method(tmp_path, method):
+    """'linear solver/method' (parameters.cc:519-532) is honoured, not ignored: the reference's mms2d_gls
+    with each of gmres, bicgstab (solve_system_BiCGStab, gls_navier_stokes.cc:1293-1340) and amg
+    (solve_system_AMG, :1344-1391; the ML hierarchy is substituted explicitly, announced on stderr)
+    reproduces the golden error table; the app states the solver / preconditioner it used."""
+    app = os.path.join(ROOT, "apps", "gls_navier_stokes_2d")
+    prm = open(os.path.join(CASES, "mms2d_gls.prm")).read()
+    prm, n = re.subn(r"(subsection linear solver.*?set method\s*=\s*)\w+", r"\g<1>" + method, prm, flags=re.S)
+    assert n == 1
+    (tmp_path / "case.prm").write_text(prm)
+    out = subprocess.run([app, "case.prm"], cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    want = {"gmres": "-> GMRES + ILU(", "bicgstab": "-> BiCGStab + ILU(", "amg": "-> GMRES + ILU("}[method]
+    line = [l for l in out.stderr.splitlines() if l.startswith("linear solver: method = " + method)]
+    assert len(line) == 1 and want in line[0], out.stderr[-2000:]
+    if method == "amg":
+        assert "ML AMG substituted" in line[0]
+    ref = open(os.path.join(CASES, "mms2d_gls.output")).read()
+    assert error_rows(out.stdout) == error_rows(ref), (error_rows(out.stdout), error_rows(ref))

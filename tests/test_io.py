@@ -192,7 +192,16 @@ def _app(tmp_path, prm_text, *args):
     ("subsection simulation control\n set method = steady\n set number mesh adapt = 1\nend\n"
      "subsection mesh adaptation\n set type = kelly\n set fraction refinement = 0.97\nend\n",  # default coarsening 0.05
      "refinement + coarsening <= 1"),
+    # linear solver/method (parameters.cc:519-532): only amg | gmres | bicgstab; the amg entries validated
+    ("subsection linear solver\n set method = direct\nend\n", "method 'direct' is invalid"),
+    ("subsection linear solver\n set method = amg\n set amg n cycles = 0\nend\n", "amg n cycles must be >= 1"),
+    ("subsection linear solver\n set method = amg\n set amg preconditioner ilu fill = 1.5\nend\n",
+     "amg preconditioner ilu fill = 1.5 is not supported"),
+    ("subsection linear solver\n set verbosity = loud\nend\n", "Unknown verbosity mode"),
+    # restart (parameters.cc:759-798): checkpoint / restart out of scope, never silently ignored
+    ("subsection restart\n set restart = true\nend\n", "restart/restart = true"),
+    ("subsection restart\n set checkpoint = true\n set frequency = 5\nend\n", "restart/checkpoint = true"),
 ])
 def test_app_rejects_unsupported_input_before_touching_the_gpu(tmp_path, text, msg):
     out = _app(tmp_path, text, "--dim", "3")
-    assert out.returncode == 2 and msg in out.stderr, out.stderr
+    assert out.returncode == 1 and msg in out.stderr, out.stderr
