@@ -7,8 +7,9 @@ One "step" = one Newton iteration of NewtonNonLinearSolver::solve
 diagonal (matrix-free "assemble_matrix_and_rhs"); GMRES(30) on the matrix-free Jacobian, right
 preconditioned by a geometric-multigrid V-cycle (levels 64^3..2^3, FP32 damped-Jacobi smoothing,
 2+2 sweeps on the 4^3 level, exact LU solve of the 2^3 level's 500 DoFs; Jacobi with --precond
-jacobi; on N GPUs every level is partitioned like the fine mesh and the 4^3 coarsest level gets
-100 Jacobi sweeps), relative residual 1e-4, max `--lin-max` iterations; alpha line search with
+jacobi; on N GPUs the levels down to 4^3 are partitioned like the fine mesh and every rank runs the
+rest of the same cycle -- 4^3 sweeps, LU on 2^3 -- on a replica of the 4^3 level from the all-reduced
+right-hand side), relative residual 1e-4, max `--lin-max` iterations; alpha line search with
 residual re-assembly. Every step restarts from the same synthetic state so the work per step is
 fixed; linear iterations and residual evaluations are reported.
 
@@ -348,7 +349,11 @@ def main():
 
     from softx_2020_200_amd.problem import CavityProblem
     if args.mg_coarsest == 0:
-        args.mg_coarsest = 2 if world == 1 else 4
+        args.mg_coarsest = 2
+    # N > 1 with the exact coarsest solve: the distributed levels stop at 4^3 (whole bricks per rank), and
+    # below them every rank runs the one-GPU cycle's remainder on a replica of the 4^3 level (2 + 2
+    # sweeps, exact LU on 2^3; gls_mg_set_coarse_replica): the same V-cycle as N = 1
+    replica = world > 1 and args.precond == "mg" and args.mg_coarsest == 2 and args.mg_coarse_direct >= 0
     lsweeps = {-2: (args.mg_coarse_level_sweeps,) * 2} if world == 1 and args.mg_coarse_direct >= 0 else {}
     if args.mg_fine_sweeps:
         lsweeps[0] = tuple(args.mg_fine_sweeps)
@@ -379,16 +384,26 @@ def main():
         ctx = dp.ctx
         if args.precond == "mg":  # the same V-cycle on nested per-rank boxes (RCCL ghosts per level)
             from softx_2020_200_amd.dist import attach_distributed_multigrid, multigrid_levels
-            lv = [dp]
-            for m in multigrid_levels(args.n, world, args.mg_coarsest):
+            lv, m_last = [dp], args.n
+            for m in multigrid_levels(args.n, world, 4 if replica else args.mg_coarsest):
+                m_last = m
                 mm = sx.hyper_cube(3, m, args.k, args.kp, -1.0, 1.0)
                 mk, dd, dv = dirichlet_from_bcs(mm, m, -1.0, 1.0, True, bcs)
                 lv.append(DistributedProblem(mm, rank, world, dev, viscosity=args.nu, vnode_mask=mk,
                                              dirichlet=(dd, dv), backend=args.dist_backend, impl=args.dist_impl))
-            attach_distributed_multigrid(lv, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
+            rep = None
+            if replica:  # the 4^3 level's whole mesh on every rank, with the one-GPU cycle below it
+                rep = CavityProblem(dim=3, n=m_last, k=args.k,
+                                    kp=args.kp, viscosity=args.nu, multigrid=True, mg_coarsest=2,
+                                    pre_smooth=args.mg_coarse_level_sweeps, post_smooth=args.mg_coarse_level_sweeps,
+                                    omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
+                                    coarse_omega=args.mg_coarse_omega, mixed_precision=args.mg_precision == "f32",
+                                    coarse_direct=args.mg_coarse_direct)
+            attach_distributed_multigrid(lv, replica=rep, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
                                          omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
                                          coarse_omega=args.mg_coarse_omega,
-                                         mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct)
+                                         mixed_precision=args.mg_precision == "f32",
+                                         coarse_direct=-1 if replica else args.mg_coarse_direct)
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
@@ -489,7 +504,7 @@ def main():
                                    (1, 64, "steady"): " (BASELINE configs[1])"}.get((args.k, args.n, args.scheme), "")),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
-                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if -2 in lsweeps else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
+                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if (-2 in lsweeps or replica) else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
                    "parallelism": ("domain decomposition x%d (%s)" % (world, "in-library RCCL P2P ghosts" if args.dist_impl == "native"
                                                                      else "torch.distributed %s ghosts" % args.dist_backend))

@@ -220,6 +220,15 @@ int gls_mg_transfer(gls_ctx *ctx, int level, int direction, const double *in, do
  * must fill an axis-aligned box (Morton partitions of a 2^m-cube over 2^j ranks do). */
 int gls_set_lattice(gls_ctx *ctx, int n1d, const int64_t *local_to_global);
 int gls_mg_detach(gls_ctx *ctx);
+/* Multi-GPU: the V-cycle below the coarsest DISTRIBUTED level is the single-GPU one, computed
+ * redundantly on every rank. replica = a single-rank context of that level's WHOLE mesh (same problem
+ * and boundary data) with its own gls_mg_attach hierarchy below it (e.g. the exact LU level of the
+ * one-GPU cycle); local_to_replica[i] = the replica row of the coarsest level's local row i (n_local =
+ * its n_dofs). The coarsest level's correction becomes: all-reduce its owned right-hand-side rows into
+ * the replica numbering, apply the replica's preconditioner, take back the local rows. Its state, time
+ * data and viscosity follow the hierarchy's (gathered at every Jacobian state). With the replica the
+ * N-rank cycle performs the operations of the 1-rank cycle (bench.py --gpus N). */
+int gls_mg_set_coarse_replica(gls_ctx *ctx, gls_ctx *replica, int64_t n_local, const int64_t *local_to_replica);
 /* Assembled ILU(fill) preconditioner for GMRES (replaces setup_ILU, gls_navier_stokes.cc:1161-1176:
  * Trilinos PreconditionILU(ilu_fill, ilu_atol, ilu_rtol, overlap 0) = Ifpack ILU(k), the reference's
  * 'linear solver/method = gmres' with 'ilu preconditioner fill / absolute / relative tolerance',

@@ -320,6 +320,8 @@ struct gls_ctx {
   bool use_slab = false;
   DevBuf<double> slab;
   DevBuf<int32_t> sum_nodes, sum_off, sum_slots;
+  int cube_nb1 = 0;  // > 0: the mesh is the structured hyper_cube with cube_nb1 bricks per direction
+                     // (k_slab_sum_cube computes the slab slots from the lattice; GLS_SLAB_CSR=1: off)
   // colored brick launches (opt-in GLS_BRICK_COLORS=1): bricks greedily colored in Morton order so
   // that no two bricks of a color share a node (the 2x2x2 parity classes on a brick lattice: 8
   // colors); surface-node sums carried across colors in acc, no slab and no k_slab_sum. Measured
@@ -505,6 +507,13 @@ struct gls_ctx {
     std::vector<unsigned char> cgraph_key;  // launch parameters the graph was captured with
     bool cgraph_failed = false;  // capture refused once: stay on plain launches
     bool dirty = true;
+    // multi-GPU (gls_mg_set_coarse_replica): the coarsest DISTRIBUTED level's correction is computed
+    // by a replica -- a single-rank context of that level's whole mesh with its own hierarchy below
+    // it -- identically on every rank, from the all-reduced (gathered) right-hand side
+    gls_ctx *replica = nullptr;
+    DevBuf<int32_t> rep_own_loc, rep_own_glob;  // owned local rows of the coarsest level -> replica rows
+    DevBuf<int32_t> rep_map;                    // every local row -> replica row
+    DevBuf<double> rep_b, rep_x, rep_tmp, rep_u[4];
   } mg;
   double time_steps[4] = {1, 1, 1, 1};
   // frozen Jacobian (skip_newton: the matrix and its preconditioner are reused across Newton
@@ -642,6 +651,30 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   GLS_TRY(c->sum_off.upload(off.data(), off.size()));
   GLS_TRY(c->sum_slots.upload(slots.data(), slots.size()));
   c->use_slab = true;
+  // structured hyper_cube (gls_mesh_hyper_cube: lexicographic node lattice, cells in Morton order, no
+  // periodic wrap): verified cell by cell, then the slab sums run without the index arrays
+  c->cube_nb1 = 0;
+  if (!std::getenv("GLS_SLAB_CSR")) {
+    int64_t n = (int64_t)std::llround(std::cbrt((double)d->n_cells));
+    const int64_t NX = K * n + 1;
+    bool ok = n >= 2 && n % 2 == 0 && n * n * n == d->n_cells && NX * NX * NX == d->n_vnodes && n <= 2048;
+    for (int64_t cl = 0; ok && cl < d->n_cells; ++cl) {
+      const int64_t b = cl / 8, ci = cl % 8;
+      int64_t bx = 0, by = 0, bz = 0;
+      for (int bit = 0; bit < 21; ++bit) {
+        bx |= ((b >> (3 * bit)) & 1) << bit;
+        by |= ((b >> (3 * bit + 1)) & 1) << bit;
+        bz |= ((b >> (3 * bit + 2)) & 1) << bit;
+      }
+      if (bx >= n / 2 || by >= n / 2 || bz >= n / 2) { ok = false; break; }
+      const int64_t x0 = K * (2 * bx + (ci & 1)), y0 = K * (2 * by + ((ci >> 1) & 1)), z0 = K * (2 * bz + (ci >> 2));
+      for (int a = 0; a < N3 && ok; ++a) {
+        const int ax = a % K1, ay = (a / K1) % K1, az = a / (K1 * K1);
+        ok = d->cell_vnodes[(size_t)cl * N3 + a] == (int32_t)((x0 + ax) + NX * ((y0 + ay) + NX * (z0 + az)));
+      }
+    }
+    if (ok) c->cube_nb1 = (int)(n / 2);
+  }
   // brick coloring: greedy in brick (Morton) order over the bricks sharing a surface node
   if (!gls::brick_colors_supported(K) || !std::getenv("GLS_BRICK_COLORS")) return GLS_OK;
   std::vector<int> color((size_t)nb, -1);
@@ -972,7 +1005,18 @@ int ensure_qdata(gls_ctx *c) {
   return GLS_OK;
 }
 
+// the slab node sums with an FP32 slab and / or the fused damped-Jacobi sweep / residual form
+hipError_t slab_sum_ex(gls_ctx *g, const double *slab, const float *slabf, double *y, const uint8_t *vmask,
+                       const double *jb, const double *jd, double omega, const double *rb) {
+  if (g->cube_nb1 > 0)
+    return gls::brick_slab_sum_cube(g->k, g->cube_nb1, slab, slabf, g->n_vnodes, y, vmask, jb, jd, omega, g->stream, rb);
+  return gls::brick_slab_sum_ex(slab, slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p, (int64_t)g->sum_nodes.n,
+                                g->n_vnodes, y, vmask, jb, jd, omega, g->stream, rb);
+}
 hipError_t slab_sum(gls_ctx *c, double *y) {
+  if (c->cube_nb1 > 0)
+    return gls::brick_slab_sum_cube(c->k, c->cube_nb1, c->slab.p, nullptr, c->n_vnodes, y, nullptr, nullptr, nullptr, 0.0,
+                                    c->stream);
   return gls::brick_slab_sum(c->slab.p, c->sum_nodes.p, c->sum_off.p, c->sum_slots.p, (int64_t)c->sum_nodes.n,
                              c->n_vnodes, y, c->stream);
 }
@@ -1652,9 +1696,7 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
   }
   if (P.slab) {
     TimedLaunch t(g, 5);
-    HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
-                                   (int64_t)g->sum_nodes.n, g->n_vnodes, y, nullptr, nullptr, nullptr, 0.0,
-                                   g->stream, P.rb));
+    HIP_TRY(slab_sum_ex(g, P.slab, P.slabf, y, nullptr, nullptr, nullptr, 0.0, P.rb));
   }
   GLS_TRY(dist_export_add(g, y));
   HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream, P.rb));
@@ -1709,8 +1751,7 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   }
   if (g->use_colors) return GLS_OK;
   TimedLaunch t(g, 5);
-  HIP_TRY(gls::brick_slab_sum_ex(P.slab, P.slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p,
-                                 (int64_t)g->sum_nodes.n, g->n_vnodes, x, g->vmask.p, b, g->diag.p, omega, g->stream));
+  HIP_TRY(slab_sum_ex(g, P.slab, P.slabf, x, g->vmask.p, b, g->diag.p, omega, nullptr));
   return GLS_OK;
 }
 }  // namespace
@@ -1879,6 +1920,7 @@ int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
   return mg_from_box(c, l, coarse);
 }
 
+int replica_gather(gls_ctx *c, const double *loc, double *glob);
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
@@ -1918,6 +1960,16 @@ int mg_prepare(gls_ctx *c) {
     GLS_TRY(gls_set_time(g, jscheme, jts));
     GLS_TRY(gls_set_state(g, mgbuf(c, l, MB_U), gh[0], gh[1], gh[2]));
     GLS_TRY(ensure_diag(g));
+  }
+  if (mg.replica) {  // the replica takes the coarsest distributed level's state (gathered) and time data
+    gls_ctx *g = mg.lev[(size_t)L - 1], *r = mg.replica;
+    const double *st[4] = {g->u, g->u1, g->u2, g->u3};
+    for (int i = 0; i < 4; ++i)
+      if (st[i]) GLS_TRY(replica_gather(c, st[i], mg.rep_u[i].p));
+    r->viscosity = c->viscosity;
+    GLS_TRY(gls_set_time(r, jscheme, jts));
+    GLS_TRY(gls_set_state(r, mg.rep_u[0].p, st[1] ? mg.rep_u[1].p : nullptr, st[2] ? mg.rep_u[2].p : nullptr,
+                          st[3] ? mg.rep_u[3].p : nullptr));
   }
   mg.direct_ok = false;
   if (mg.direct) {  // probe A = J_coarse column by column, then invert on the device
@@ -2114,6 +2166,33 @@ int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, dou
   return GLS_OK;
 }
 
+// glob (replica numbering, every rank) = the coarsest distributed level's vector loc: each rank scatters
+// its owned rows into a zeroed copy, then one sum all-reduce (RCCL: in place; callback transports
+// through their reduction buffer in chunks of 256 values)
+int replica_gather(gls_ctx *c, const double *loc, double *glob) {
+  auto &mg = c->mg;
+  gls_ctx *g = mg.lev.back();
+  auto &D = g->dist;
+  const int64_t ng = mg.replica->n_dofs, no = (int64_t)mg.rep_own_loc.n;
+  hipStream_t s = c->stream;
+  HIP_TRY(gls::vec_fill(glob, ng, 0.0, s));
+  if (no) {
+    HIP_TRY(gls::vec_pack_dofs(loc, mg.rep_own_loc.p, no, mg.rep_tmp.p, s));
+    HIP_TRY(gls::vec_unpack_dofs(glob, mg.rep_own_glob.p, no, mg.rep_tmp.p, s));
+  }
+  if (D.comm) {
+    if (D.allreduce(D.user, glob, (int)ng) != 0) return set_err(GLS_ECOMM, "replica all-reduce failed");
+    return GLS_OK;
+  }
+  for (int64_t o = 0; o < ng; o += 256) {
+    const int len = (int)std::min<int64_t>(256, ng - o);
+    HIP_TRY(hipMemcpyAsync(D.red_buf, glob + o, sizeof(double) * len, hipMemcpyDeviceToDevice, s));
+    if (D.allreduce(D.user, D.red_buf, len) != 0) return set_err(GLS_ECOMM, "replica all-reduce failed");
+    HIP_TRY(hipMemcpyAsync(glob + o, D.red_buf, sizeof(double) * len, hipMemcpyDeviceToDevice, s));
+  }
+  return GLS_OK;
+}
+
 // x = V-cycle(b) on level l (x, b are level-l vectors)
 int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   auto &mg = c->mg;
@@ -2124,6 +2203,12 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   double *y = mgbuf(c, l, MB_Y);
   const double *d = g->diag.p;
   hipStream_t s = c->stream;
+  if (l == L - 1 && mg.replica) {  // the replica's cycle on the gathered right-hand side, every rank
+    GLS_TRY(replica_gather(c, b, mg.rep_b.p));
+    GLS_TRY(gls_apply_preconditioner(mg.replica, mg.rep_b.p, mg.rep_x.p));
+    HIP_TRY(gls::vec_pack_dofs(mg.rep_x.p, mg.rep_map.p, n, x, c->stream));
+    return GLS_OK;
+  }
   if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
     if (mg.lu) {
       const double one = 1.0, zero = 0.0;
@@ -2703,6 +2788,42 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   // one stream for the whole V-cycle: the coarse levels' kernels are ordered with the transfers
   for (size_t l = 1; l < mg.lev.size(); ++l)
     if (mg.lev[l]->stream != c->stream) GLS_TRY(gls_set_stream(mg.lev[l], c->stream));
+  return GLS_OK;
+}
+
+int gls_mg_set_coarse_replica(gls_ctx *c, gls_ctx *replica, int64_t n_local, const int64_t *local_to_replica) {
+  GLS_TRY(check_ctx(c));
+  auto &mg = c->mg;
+  if (!mg.on || mg.lev.size() < 2) return set_err(GLS_EINVAL, "coarse replica: attach the multigrid hierarchy first");
+  gls_ctx *g = mg.lev.back();
+  if (!replica || replica == c || replica->dist.on) return set_err(GLS_EINVAL, "coarse replica: a single-rank context");
+  if (!g->dist.on) return set_err(GLS_EINVAL, "coarse replica: the coarsest level is not distributed");
+  if (n_local != g->n_dofs || !local_to_replica) return set_err(GLS_EINVAL, "coarse replica: map of %lld rows expected",
+                                                                (long long)g->n_dofs);
+  const int64_t ng = replica->n_dofs;
+  if (ng >= INT32_MAX) return set_err(GLS_EINVAL, "coarse replica too large");
+  std::vector<int32_t> all((size_t)n_local), own_l, own_g;
+  const int64_t dv = (int64_t)g->dim * g->n_vnodes;
+  for (int64_t i = 0; i < n_local; ++i) {
+    const int64_t t = local_to_replica[i];
+    if (t < 0 || t >= ng) return set_err(GLS_EINVAL, "coarse replica: row %lld maps outside", (long long)i);
+    all[(size_t)i] = (int32_t)t;
+    const bool owned = i < dv ? i < (int64_t)g->dim * g->dist.n_owned : i - dv < g->dist.n_owned_p;
+    if (owned) {
+      own_l.push_back((int32_t)i);
+      own_g.push_back((int32_t)t);
+    }
+  }
+  GLS_TRY(mg.rep_map.upload(all.data(), all.size()));
+  GLS_TRY(mg.rep_own_loc.upload(own_l.data(), own_l.size()));
+  GLS_TRY(mg.rep_own_glob.upload(own_g.data(), own_g.size()));
+  GLS_TRY(mg.rep_b.alloc((size_t)ng));
+  GLS_TRY(mg.rep_x.alloc((size_t)ng));
+  GLS_TRY(mg.rep_tmp.alloc(std::max<size_t>(own_l.size(), 1)));
+  for (auto &u : mg.rep_u) GLS_TRY(u.alloc((size_t)ng));
+  if (replica->stream != c->stream) GLS_TRY(gls_set_stream(replica, c->stream));
+  mg.replica = replica;
+  mg.dirty = true;
   return GLS_OK;
 }
 

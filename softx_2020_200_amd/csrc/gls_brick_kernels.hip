@@ -23,6 +23,7 @@
 //   J.v    : v (value, grad, Laplacian) x 3 comps, then v_p (value, grad)
 //   test   : per test field, transposed z/y/x sweeps of (value, grad) coefficients -> node array
 // The pointwise algebra restates gls_navier_stokes.cc:387-748.
+#include "gls_brick_common.hpp"
 #include "gls_common.hpp"
 #include "gls_launch.hpp"
 
@@ -155,26 +156,6 @@ struct StageLayout {
   static constexpr int CS = stride(SR);  // per-cell stride (elements)
 };
 
-// rank of brick-lattice node (X, Y, Z) among the brick-boundary nodes (lexicographic, x fastest):
-// its index minus the interior nodes that precede it
-template <int BN>
-__device__ __forceinline__ int bnd_index(int X, int Y, int Z) {
-  constexpr int I = BN - 2;
-  const int n = X + BN * (Y + BN * Z);
-  int before = min(max(Z - 1, 0), I) * I * I;
-  if (Z >= 1 && Z <= I) {
-    before += min(max(Y - 1, 0), I) * I;
-    if (Y >= 1 && Y <= I) before += min(max(X - 1, 0), I);
-  }
-  return n - before;
-}
-
-// bijective XCD swizzle of n work items: orig % 8 labels the blocks that share an XCD
-__device__ __forceinline__ int xcd_swizzle(int orig, int n) {
-  const int q = n / 8, r = n % 8, x = orig % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + orig / 8;
-}
-
 // offset of element e of line l in a [K1][K1][K1] array ([z][y][x], x fastest), sweep dim D
 template <int D, int K1>
 __device__ __forceinline__ int loff(int l, int e) {
@@ -213,17 +194,6 @@ __device__ __forceinline__ void bwd_add(const double (&M)[kMaxQ1D][kMaxNodes1D],
     for (int j = 0; j < K1; ++j) s += M[j][i] * in[j];
     out[i] = s;
   }
-}
-
-// LDS hand-off between lanes of ONE wave: LDS ops of a wave execute in order; the asm keeps the
-// compiler from moving LDS accesses across this point.
-__device__ __forceinline__ void wave_sync() {
-#ifdef GLS_WAVE_SYNC_DRAIN
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  asm volatile("" ::: "memory");
-#endif
-  __builtin_amdgcn_wave_barrier();
 }
 
 template <int K, int MODE, typename Real = double>
@@ -551,11 +521,15 @@ __global__ void __launch_bounds__(BrickCfg<K>::THREADS,
   const Real JxW = sM[80 + qx] * sM[80 + qy] * sM[80 + qz] * hx * hy * hz;
   // linearization storage: per wave CPW*N3 lanes x kQDataBrick values, value-major (coalesced)
   constexpr int QW = CPW * N3;
+  // K = 2: the pencil layout (qdp_base, gls_brick_common.hpp: the pencil J.v's rows; value stride 54 =
+  // QW); K = 1: wave-major per brick
+  static_assert(K != 2 || (QW == kQdpRow && !kQdLite), "pencil layout: 54-entry rows, full linearization");
+  const int64_t qoff = K == 2 ? qdp_base(brick, pci, q) : ((int64_t)brick * C::WAVES + wave) * kQDataBrick * QW + lane;
   Real *qdw = nullptr;
   if constexpr (std::is_same<Real, double>::value) {
-    if (P.qd) qdw = P.qd + ((int64_t)brick * C::WAVES + wave) * kQDataBrick * QW + lane;
+    if (P.qd) qdw = P.qd + qoff;
   } else {
-    if (P.qdf) qdw = P.qdf + ((int64_t)brick * C::WAVES + wave) * kQDataBrick * QW + lane;
+    if (P.qdf) qdw = P.qdf + qoff;
   }
 
   // ---------------- phase A: state at this lane's quadrature point
@@ -996,6 +970,7 @@ size_t brick_lds_bytes(int mode) {
 template <int K>
 size_t brick_qdata_doubles(int n_cells) {
   using C = BrickCfg<K>;
+  if (K == 2) return (size_t)((n_cells / 8 + 2) / 3) * kQdpTriple;  // pencil layout: whole brick triples
   return (size_t)(n_cells / 8) * C::WAVES * kQDataBrick * C::CPW * C::N3;
 }
 
@@ -1009,6 +984,11 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   const int nc = colored ? P.n_colors : 1;
   OpParams Q = P;
   if (!colored) Q.bricks = nullptr;
+  // the Q2 J.v from the linearization: the pencil-dataflow kernel (gls_brick_pencil.hip)
+  if (K == 2 && (mode == MODE_JVQ || mode == MODE_RESIDUAL) && !colored && pencil_enabled()) {
+    const hipError_t e = mode == MODE_JVQ ? launch_pencil_jv(Q, T, s, false) : launch_pencil_residual(Q, T, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   for (int col = 0; col < nc; ++col) {
     Q.color = col;
     const int nb = colored ? P.color_off[col + 1] - P.color_off[col] : P.subset ? P.subset_n : n_bricks;
@@ -1069,6 +1049,10 @@ hipError_t launch_brick_jv_f32_t(const OpParams &P, const Tables1D &T, hipStream
   const int n_bricks = P.n_cells / 8;
   if (n_bricks <= 0) return hipSuccess;
   if (!P.qdf || P.n_probe > 0) return hipErrorInvalidValue;
+  if (K == 2 && !P.bricks && pencil_enabled()) {
+    const hipError_t e = launch_pencil_jv(P, T, s, true);
+    if (e != hipErrorNotSupported) return e;
+  }
   const int nc = P.bricks ? P.n_colors : 1;
   OpParams Q = P;
   for (int col = 0; col < nc; ++col) {
@@ -1211,6 +1195,151 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
   }
   return hipGetLastError();
 }
+// The same node sums on the uniform hyper_cube (structured lattice: lexicographic nodes, Morton
+// bricks, no periodic wrap; checked by the host, build_slab_map): no node / offset / slot arrays. A
+// thread's node follows from its (plane, index) and its slots from the node's lattice coordinates:
+// per direction the brick(s) whose surface holds it (two where the coordinate is a brick boundary),
+// slot = brick * NBND + bnd_index(local coordinates). The <= 8 slots are sorted so that the sum runs
+// in ascending slot order, exactly the order of the CSR map (bitwise equal results). One dependent
+// load round (the slab entries) instead of three, and y stored row by row.
+__device__ __forceinline__ uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
+  uint32_t m = 0;
+  for (int b = 0; b < 10; ++b)
+    m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
+  return m;
+}
+template <typename S, bool J, int K>
+__global__ void __launch_bounds__(256) k_slab_sum_cube(const S *__restrict__ slab, int nb1, int64_t voff,
+                                                       double *__restrict__ y, const uint8_t *__restrict__ vmask,
+                                                       const double *__restrict__ jb, const double *__restrict__ jd,
+                                                       double jomega, const double *__restrict__ rb) {
+  constexpr int BN = 2 * K + 1, P2 = 2 * K, NBND = BN * BN * BN - (BN - 2) * (BN - 2) * (BN - 2);
+  const int NX = P2 * nb1 + 1;
+  const int Z = blockIdx.y;
+  const bool zs = Z % P2 == 0;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // surface nodes of plane Z: all of it when Z is a brick boundary, else the full rows Y % 2K == 0
+  // followed by the brick-boundary columns X % 2K == 0 of the other rows
+  int X, Y;
+  const int ns = nb1 + 1;  // brick-boundary coordinates per direction
+  if (zs) {
+    if (t >= (int64_t)NX * NX) return;
+    X = (int)(t % NX);
+    Y = (int)(t / NX);
+  } else {
+    const int64_t full = (int64_t)ns * NX, sparse = (int64_t)(NX - ns) * ns;
+    if (t >= full + sparse) return;
+    if (t < full) {
+      X = (int)(t % NX);
+      Y = (int)(t / NX) * P2;
+    } else {
+      const int64_t u = t - full;
+      const int r = (int)(u / ns);  // r-th row that is not a brick boundary
+      X = (int)(u % ns) * P2;
+      Y = (r / (P2 - 1)) * P2 + 1 + r % (P2 - 1);
+    }
+  }
+  // per direction: (brick coordinate, local coordinate) pairs holding the lattice coordinate
+  int bc[3][2], lc[3][2], nc[3];
+  const int co[3] = {X, Y, Z};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int x = co[d];
+    if (x % P2 == 0 && x > 0 && x < NX - 1) {
+      nc[d] = 2;
+      bc[d][0] = x / P2 - 1;
+      lc[d][0] = P2;
+      bc[d][1] = x / P2;
+      lc[d][1] = 0;
+    } else {
+      nc[d] = 1;
+      bc[d][0] = min(x / P2, nb1 - 1);
+      lc[d][0] = x - P2 * bc[d][0];
+      bc[d][1] = bc[d][0];
+      lc[d][1] = lc[d][0];
+    }
+  }
+  int64_t sl[8];
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool on = i < nc[0] && j < nc[1] && k < nc[2];
+        const int64_t s = (int64_t)morton3(bc[0][i], bc[1][j], bc[2][k]) * NBND + bnd_index<BN>(lc[0][i], lc[1][j], lc[2][k]);
+        sl[i + 2 * j + 4 * k] = on ? s : INT64_MAX;
+        cnt += on;
+      }
+  // ascending slot order (sorting network on 8 keys; absent slots sort last)
+  auto cs = [&](int a, int b) {
+    const int64_t lo = min(sl[a], sl[b]), hi = max(sl[a], sl[b]);
+    sl[a] = lo;
+    sl[b] = hi;
+  };
+  cs(0, 1); cs(2, 3); cs(4, 5); cs(6, 7);
+  cs(0, 2); cs(1, 3); cs(4, 6); cs(5, 7);
+  cs(1, 2); cs(5, 6); cs(0, 4); cs(3, 7);
+  cs(1, 5); cs(2, 6);
+  cs(1, 4); cs(3, 6);
+  cs(2, 4); cs(3, 5);
+  cs(3, 4);
+  double e[8][4];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < cnt) SlabQuad<S>::load(slab + sl[q] * 4, e[q][0], e[q][1], e[q][2], e[q][3]);
+  double s[4] = {0., 0., 0., 0.};
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < cnt) {
+      s[0] += e[q][0];
+      s[1] += e[q][1];
+      s[2] += e[q][2];
+      s[3] += e[q][3];
+    }
+  const int64_t node = X + (int64_t)NX * (Y + (int64_t)NX * Z);
+  const int64_t gi[4] = {node * 3, node * 3 + 1, node * 3 + 2, voff + node};
+  if constexpr (J) {
+    const unsigned m = vmask ? vmask[node] : 0u;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const double x = y[gi[f]], dd = jd[gi[f]];
+      y[gi[f]] = x + jomega * (jb[gi[f]] - ((f < 3 && ((m >> f) & 1u)) ? dd * x : s[f])) / dd;
+    }
+  } else if (rb) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) y[gi[f]] = rb[gi[f]] - s[f];
+  } else {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) y[gi[f]] = s[f];
+  }
+}
+// nb1 > 0: the structured form (nb1 bricks per direction) instead of the node / offset / slot map
+hipError_t brick_slab_sum_cube(int k, int nb1, const double *slab, const float *slabf, int64_t n_vnodes, double *y,
+                               const uint8_t *vmask, const double *jb, const double *jd, double jomega, hipStream_t s,
+                               const double *rb) {
+  if (nb1 <= 0 || (k != 1 && k != 2)) return hipErrorInvalidValue;
+  const int NX = 2 * k * nb1 + 1;
+  const dim3 g((unsigned)(((int64_t)NX * NX + 255) / 256), (unsigned)NX), b(256);
+  const int64_t voff = 3 * n_vnodes;
+#define GLS_SLAB_CUBE(KK)                                                                                                   \
+  if (slabf) {                                                                                                              \
+    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<float, true, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb);  \
+    else hipLaunchKernelGGL((k_slab_sum_cube<float, false, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb);   \
+  } else {                                                                                                                  \
+    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<double, true, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb); \
+    else hipLaunchKernelGGL((k_slab_sum_cube<double, false, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb);  \
+  }
+  if (k == 1) {
+    GLS_SLAB_CUBE(1)
+  } else {
+    GLS_SLAB_CUBE(2)
+  }
+#undef GLS_SLAB_CUBE
+  return hipGetLastError();
+}
+
 bool brick_fused_jacobi_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }
 #ifdef GLS_BRICK_COLORS_BUILD
 bool brick_colors_supported(int k) { return brick_impl(k) == 0 && (k == 1 || k == 2); }

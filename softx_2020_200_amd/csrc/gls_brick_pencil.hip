@@ -1,0 +1,581 @@
+// gls_brick_pencil.hip — the Q2 brick J.v (MODE_JVQ, FP64 outer operator and FP32 smoother) in the
+// "pencil" dataflow: one lane holds a line of 3 values along z for every field it works on.
+//
+// Why: the lane-per-point brick kernel (gls_brick_kernels.hip) is bound by its LDS
+// stream -- every stage array is written once (ds_write_b64, ~6 LDS cycles per wave instruction) and
+// read three times (each lane reads the whole line its output needs). Here a lane owns the z-line of
+// its (qx, qy) column of a cell (9 lanes per cell, 6 cells per wave, 54 of 64 lanes):
+//   forward : x sweep from the brick array (uniform coefficients; per lane one x-line of the node
+//             lattice, all 3 qx outputs) -> LDS -> y sweep (each lane reads its qx slab, 9 values per
+//             array) -> kept in REGISTERS -> z sweep in registers at each qz;
+//   backward: z-transposed contraction accumulated in registers while the pointwise runs over qz ->
+//             LDS -> y-transposed -> LDS -> x-transposed -> per-cell node values (Out) -> brick sums.
+// The Y stage (4 arrays per velocity field) and the test coefficients (16 values per point) never go
+// through LDS, and no element is read three times: per cell ~945 LDS element writes and ~1540 reads
+// against ~1780 and ~5350 for the lane-per-point kernel. The sweeps' coefficients are uniform over the
+// wave except in the y sweep (row of the lane's qy, from an LDS table).
+//
+// Workgroup = 3 consecutive (XCD-swizzled) bricks = 24 cells, 4 waves of 6 cells; the brick-interior
+// nodes are stored directly, brick-surface nodes go to the brick's slab (k_slab_sum), exactly as the
+// lane-per-point kernel does (same slab slots, same fixed per-node summation order: bitwise equal
+// sums per brick node). The linearization is read from the pencil layout (qdp_base) that MODE_LIN
+// writes: per (qz, value) one contiguous row of 54 entries per wave.
+//
+// The pointwise algebra restates gls_navier_stokes.cc:548-622 (the Jacobian's action, SURVEY.md
+// Appendix A) with the same operation order per term as gls_brick_kernels.hip MODE_JVQ.
+#include "gls_brick_common.hpp"
+#include "gls_common.hpp"
+#include "gls_launch.hpp"
+
+#include <cstdlib>
+#include <type_traits>
+
+#ifndef GLS_PENCIL_WPE64
+#define GLS_PENCIL_WPE64 2  // FP64: ~230 VGPRs -> 2 waves / SIMD (2 workgroups per CU)
+#endif
+#ifndef GLS_PENCIL_WPE32
+#define GLS_PENCIL_WPE32 4  // FP32: <= 128 VGPRs -> 4 waves / SIMD
+#endif
+
+namespace gls {
+
+template <typename Real>
+struct PencilCfg {
+  static constexpr int K1 = 3, N3 = 27, BN = 5, BN3 = 125, BN3P = 128, NBND = 98;
+  static constexpr int CPW = 6, WAVES = 4, THREADS = 256, CPG = 24, BPG = 3;
+  static constexpr bool F64 = sizeof(Real) == 8;
+  // forward X arrays: [qx][k][j] slabs of 9 (+ pad: 16-B aligned slabs), read as one slab per lane
+  static constexpr int XS = F64 ? 10 : 12, XA = 3 * XS;
+  // backward Z arrays: [qx][az][qy] slabs of 9, W arrays [az][ay][qx] (27)
+  static constexpr int ZS = F64 ? 10 : 12, ZA = 3 * ZS, WA = F64 ? 28 : 28;
+  static constexpr int CSF = 3 * XA, CSB = 3 * ZA + 2 * WA;
+  static constexpr int CS0 = CSF > CSB ? CSF : CSB;
+  static constexpr int CS = F64 ? CS0 + 4 : CS0 + 4;  // per-cell stage stride (Reals)
+  static constexpr int NO = 4;                          // test fields
+};
+
+// brick fields gathered per brick: J.v: v (3) + v_p; residual: u (3), p, the history H = sum_k alpha_k u^(k) (3)
+constexpr int pencil_fields(int mode) { return mode == MODE_RESIDUAL ? 7 : 4; }
+template <typename Real>
+size_t pencil_lds_bytes(int mode) {
+  using C = PencilCfg<Real>;
+  return sizeof(Real) * ((size_t)C::BPG * pencil_fields(mode) * C::BN3P + (size_t)C::WAVES * C::CPW * C::CS +
+                         (size_t)C::CPG * C::NO * C::N3) +
+         sizeof(int) * (size_t)C::BPG * C::BN3P;
+}
+
+// the Q2 1D tables in the kernel's precision (kernel argument -> scalar registers): [q][node]
+template <typename Real>
+struct PencilTab {
+  Real V[3][3], D[3][3], S[3][3], w[3], xi[3];
+};
+
+// GEN: the forcing term and the SRF source are compiled in (an instantiation without them is the hot
+// path: their per-point loads and terms cost the residual ~50 VGPRs of spills)
+template <typename Real, int MODE, bool GEN>
+__global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
+    gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
+  using C = PencilCfg<Real>;
+  constexpr bool RES = MODE == MODE_RESIDUAL;  // else MODE_JVQ
+  constexpr int BN = C::BN, BN3 = C::BN3, BN3P = C::BN3P, NF = pencil_fields(MODE);
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  Real *const sB = reinterpret_cast<Real *>(smem_raw);            // [3 bricks][NF fields][BN3P]
+  Real *const sS = sB + C::BPG * NF * BN3P;                        // [4 waves][6 cells][CS] stage arrays
+  Real *const sO = sS + C::WAVES * C::CPW * C::CS;                 // [24 cells][4 fields][27] cell node values
+  int *const sNode = reinterpret_cast<int *>(sO + C::CPG * C::NO * C::N3);  // [3][BN3P]
+  __shared__ Real sRow[3 * 16];  // V, D, S rows [mat][q][4] for the y sweep's per-lane coefficients
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n_bricks = P.n_cells / 8;
+  // brick-subset launches (the distributed split: interior / boundary bricks) for the FP64 operator,
+  // as the lane-per-point kernel honours them
+  const int32_t *const subset = std::is_same<Real, double>::value ? P.subset : nullptr;
+  const int n_items = subset ? P.subset_n : n_bricks;       // bricks of this launch
+  const int n_groups = (n_items + 2) / 3;
+  const int g = xcd_swizzle((int)blockIdx.x, n_groups);      // XCD-aware: contiguous Morton triples per XCD
+  const int nbg = min(3, n_items - 3 * g);                   // bricks in this group (last one may be short)
+  auto brick_of = [&](int bi) { return subset ? subset[3 * g + bi] : 3 * g + bi; };
+  const int64_t voff = (int64_t)3 * P.n_vnodes;
+
+  if (tid < 48) {
+    const int mat = tid >> 4, r = (tid >> 2) & 3, cc = tid & 3;
+    Real v = 0;
+    if (r < 3 && cc < 3) v = mat == 0 ? T.V[r][cc] : mat == 1 ? T.D[r][cc] : T.S[r][cc];
+    sRow[tid] = v;
+  }
+  // ---------------- gather the group's brick nodes: v (masked: P v) or u, p, H, and the node ids
+  for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
+    const int bi = t / BN3, n = t % BN3;
+    if (bi >= nbg) break;
+    const int brick = brick_of(bi);
+    const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
+    const int cx = min(X / 2, 1), cy = min(Y / 2, 1), cz = min(Z / 2, 1);
+    const int a = (X - 2 * cx) + 3 * ((Y - 2 * cy) + 3 * (Z - 2 * cz));
+    const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * 27 + a];
+    const int64_t i3 = (int64_t)node * 3;
+    Real *b = sB + bi * NF * BN3P + n;
+    if constexpr (RES) {
+      double h[3] = {0., 0., 0.};
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        if (P.n_hist > 0) h[cc] += P.alpha[1] * P.h1[i3 + cc];
+        if (P.n_hist > 1) h[cc] += P.alpha[2] * P.h2[i3 + cc];
+        if (P.n_hist > 2) h[cc] += P.alpha[3] * P.h3[i3 + cc];
+      }
+      b[0] = (Real)P.u[i3];
+      b[BN3P] = (Real)P.u[i3 + 1];
+      b[2 * BN3P] = (Real)P.u[i3 + 2];
+      b[3 * BN3P] = (Real)P.u[voff + node];
+      b[4 * BN3P] = (Real)h[0];
+      b[5 * BN3P] = (Real)h[1];
+      b[6 * BN3P] = (Real)h[2];
+    } else {
+      const double v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
+      const unsigned m = P.vmask ? P.vmask[node] : 0u;
+      b[0] = (m & 1u) ? Real(0) : (Real)v0;
+      b[BN3P] = (m & 2u) ? Real(0) : (Real)v1;
+      b[2 * BN3P] = (m & 4u) ? Real(0) : (Real)v2;
+      b[3 * BN3P] = (Real)vp;
+    }
+    sNode[bi * BN3P + n] = node;
+  }
+  __syncthreads();
+
+  // ---------------- per lane: cell c of this wave, (a, b) position in the cell's 3 x 3 pencil grid
+  const bool act = lane < 9 * C::CPW;
+  const int c = act ? lane / 9 : 0, rr = act ? lane % 9 : 0, pa = rr % 3, pb = rr / 3;
+  const int cw = wave * C::CPW + c, bi = cw >> 3, ci = cw & 7;
+  const bool valid = act && bi < nbg;
+  const int brick = brick_of(valid ? bi : 0);
+  const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
+  const int64_t gcell = (int64_t)brick * 8 + (valid ? ci : 0);
+  const Real hx = (Real)P.geo[gcell * 4 + 0], hy = (Real)P.geo[gcell * 4 + 1], hz = (Real)P.geo[gcell * 4 + 2];
+  const Real ihx = Real(1) / hx, ihy = Real(1) / hy, ihz = Real(1) / hz;
+  const Real wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
+  Real *const cellS = sS + (wave * C::CPW + c) * C::CS;
+
+  // ---------------- forward sweeps of brick field f into Y registers ([k]: BB, BD, DB, L). kind 0: the
+  // value only (BB); 1: value and gradient (BB, BD, DB; pressure); 2: velocity (+ L for the Laplacian)
+  auto forward = [&](int f, int kind, Real (&BB)[3], Real (&BD)[3], Real (&DB)[3], Real (&LL)[3]) {
+    const bool grad = kind >= 1, vel = kind == 2;
+    // x sweep, lane (a, b) = (y node j, z node k): the brick's x-line of this cell at (j, k)
+    {
+      const Real *F = sB + (bi < 3 ? bi : 0) * NF * BN3P + f * BN3P + 2 * cx + BN * (2 * cy + pa) + BN * BN * (2 * cz + pb);
+      const Real f0 = F[0], f1 = F[1], f2 = F[2];
+#pragma unroll
+      for (int qx = 0; qx < 3; ++qx) {
+        const Real xb = T.V[qx][0] * f0 + T.V[qx][1] * f1 + T.V[qx][2] * f2;
+        const Real xd = grad ? T.D[qx][0] * f0 + T.D[qx][1] * f1 + T.D[qx][2] * f2 : Real(0);
+        const int o = qx * C::XS + pa + 3 * pb;  // slab qx, entry (j, k) at j + 3 k
+        const Real xs = vel ? T.S[qx][0] * f0 + T.S[qx][1] * f1 + T.S[qx][2] * f2 : Real(0);
+        if (act) {  // lanes 54..63 mirror lane 0 and store nothing
+          cellS[0 * C::XA + o] = xb;
+          if (grad) cellS[1 * C::XA + o] = xd;
+          if (vel) cellS[2 * C::XA + o] = xs;
+        }
+      }
+    }
+    wave_sync();
+    // y sweep, lane (a, b) = (qx, qy): slab qx of each X array, all (j, k); the lane's V / D / S rows
+    {
+      const Real *rowp = sRow + pb * 4;
+      const Real v0 = rowp[0], v1 = rowp[1], v2 = rowp[2];
+      const Real d0 = rowp[16], d1 = rowp[17], d2 = rowp[18];
+      const Real s0 = rowp[32], s1 = rowp[33], s2 = rowp[34];
+      Real xb[9], xd[9], xs[9];
+      const Real *sl = cellS + pa * C::XS;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) {
+        xb[e] = sl[e];
+        if (grad) xd[e] = sl[C::XA + e];
+        if (vel) xs[e] = sl[2 * C::XA + e];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const Real b0 = xb[3 * k], b1 = xb[3 * k + 1], b2 = xb[3 * k + 2];
+        BB[k] = v0 * b0 + v1 * b1 + v2 * b2;
+        if (grad) {
+          BD[k] = d0 * b0 + d1 * b1 + d2 * b2;
+          DB[k] = v0 * xd[3 * k] + v1 * xd[3 * k + 1] + v2 * xd[3 * k + 2];
+        }
+        if (vel)
+          LL[k] = wyy * (s0 * b0 + s1 * b1 + s2 * b2) + wxx * (v0 * xs[3 * k] + v1 * xs[3 * k + 1] + v2 * xs[3 * k + 2]);
+      }
+    }
+    wave_sync();  // the X arrays are rewritten by the next field
+  };
+
+  // z sweep helpers (uniform coefficients: qz, k are compile-time after unrolling)
+  auto zval = [&](const Real (&y)[3], int qz) { return T.V[qz][0] * y[0] + T.V[qz][1] * y[1] + T.V[qz][2] * y[2]; };
+  auto zder = [&](const Real (&y)[3], int qz) { return T.D[qz][0] * y[0] + T.D[qz][1] * y[1] + T.D[qz][2] * y[2]; };
+  auto zsec = [&](const Real (&y)[3], int qz) { return T.S[qz][0] * y[0] + T.S[qz][1] * y[1] + T.S[qz][2] * y[2]; };
+
+  const Real nu = (Real)P.nu, aj = (Real)P.alpha_jac;
+  auto wsel = [&](int i) { return i == 0 ? T.w[0] : i == 1 ? T.w[1] : T.w[2]; };  // lane-varying index
+  const Real wxy = wsel(pa) * wsel(pb) * hx * hy * hz;  // JxW / w[qz]
+  const Real ihv[3] = {ihx, ihy, ihz};
+  Real om[3] = {0, 0, 0};
+  if (GEN && P.srf) { om[0] = (Real)P.omega[0]; om[1] = (Real)P.omega[1]; om[2] = (Real)P.omega[2]; }
+
+  // backward stages of test field f from its z-transposed sums Z[m][az] (lane (qx, qy)):
+  // LDS -> y-transposed (lane (qx, az)) -> LDS -> x-transposed (lane (ay, az)) -> Out
+  Real *const outc = sO + cw * C::NO * C::N3;
+  auto backward = [&](int f, const Real (&Z)[3][3]) {
+    Real *Zs = cellS;                    // [m][qx][az][qy]: m * ZA + qx * ZS + 3 az + qy
+    Real *Ws = cellS + 3 * C::ZA;        // [m][az][ay][qx]: m * WA + 3 (ay + 3 az) + qx
+    if (act) {
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int az = 0; az < 3; ++az) Zs[m * C::ZA + pa * C::ZS + 3 * az + pb] = Z[m][az];
+    }
+    wave_sync();
+    {  // lane (a, b) = (qx, az)
+      Real z[3][3];
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int qy = 0; qy < 3; ++qy) z[m][qy] = Zs[m * C::ZA + pa * C::ZS + 3 * pb + qy];
+#pragma unroll
+      for (int ay = 0; ay < 3; ++ay) {
+        const Real w0 = T.V[0][ay] * z[0][0] + T.V[1][ay] * z[0][1] + T.V[2][ay] * z[0][2] +
+                        (T.D[0][ay] * z[2][0] + T.D[1][ay] * z[2][1] + T.D[2][ay] * z[2][2]);
+        const Real w1 = T.V[0][ay] * z[1][0] + T.V[1][ay] * z[1][1] + T.V[2][ay] * z[1][2];
+        if (act) {
+          Ws[0 * C::WA + 3 * (ay + 3 * pb) + pa] = w0;
+          Ws[1 * C::WA + 3 * (ay + 3 * pb) + pa] = w1;
+        }
+      }
+    }
+    wave_sync();
+    {  // lane (a, b) = (ay, az)
+      Real w0[3], w1[3];
+#pragma unroll
+      for (int qx = 0; qx < 3; ++qx) {
+        w0[qx] = Ws[3 * (pa + 3 * pb) + qx];
+        w1[qx] = Ws[C::WA + 3 * (pa + 3 * pb) + qx];
+      }
+      if (valid) {
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax)
+          outc[f * C::N3 + 9 * pb + 3 * pa + ax] =
+              T.V[0][ax] * w0[0] + T.V[1][ax] * w0[1] + T.V[2][ax] * w0[2] +
+              (T.D[0][ax] * w1[0] + T.D[1][ax] * w1[1] + T.D[2][ax] * w1[2]);
+      }
+    }
+    wave_sync();  // the stage area is rewritten by the next field
+  };
+
+  if constexpr (RES) {
+    // ---------------- residual (assemble_rhs, gls_navier_stokes.cc:391-516): values of u, H and p, grad p
+    Real uq[3][3], Ttq[3][3], pq[3], gp[3][3];
+    {
+      Real dz[3];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        Real bb[3], hb[3];
+        forward(cc, 0, bb, dz, dz, dz);
+        forward(4 + cc, 0, hb, dz, dz, dz);
+#pragma unroll
+        for (int qz = 0; qz < 3; ++qz) {
+          uq[cc][qz] = zval(bb, qz);
+          Ttq[cc][qz] = (Real)P.alpha[0] * uq[cc][qz] + zval(hb, qz);  // time term alpha_0 u + H
+        }
+      }
+      Real pb_[3], pbd[3], pdb[3];
+      forward(3, 1, pb_, pbd, pdb, dz);
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+        pq[qz] = zval(pb_, qz);
+        gp[0][qz] = zval(pdb, qz) * ihx;
+        gp[1][qz] = zval(pbd, qz) * ihy;
+        gp[2][qz] = zder(pb_, qz) * ihz;
+      }
+    }
+    // tau (gls_navier_stokes.cc:401-408), per point
+    const Real hst = (Real)P.geo[gcell * 4 + 3];
+    Real tauq[3];
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+      const Real un2 = uq[0][qz] * uq[0][qz] + uq[1][qz] * uq[1][qz] + uq[2][qz] * uq[2][qz];
+      const Real u_mag = fmax(sqrt(un2), Real(1e-12));
+      const Real t1 = Real(2) * u_mag / hst, t2 = Real(4) * nu / (hst * hst);
+      tauq[qz] = Real(1) / sqrt((Real)P.sdt2 + t1 * t1 + Real(9) * (t2 * t2));
+    }
+    // SRF: the lane's point coordinates x0 + h xi (z per point)
+    Real xl = 0, yl = 0, zl = 0;
+    if (GEN && P.srf) {
+      auto xsel = [&](int i) { return i == 0 ? T.xi[0] : i == 1 ? T.xi[1] : T.xi[2]; };
+      xl = (Real)P.x0[gcell * 3 + 0] + hx * xsel(pa);
+      yl = (Real)P.x0[gcell * 3 + 1] + hy * xsel(pb);
+      zl = (Real)P.x0[gcell * 3 + 2];
+    }
+    Real Rq[3][3], divu[3] = {0, 0, 0};
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      Real Yc[4][3];
+      forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
+      Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+        const Real g0 = zval(Yc[2], qz) * ihx, g1 = zval(Yc[1], qz) * ihy, g2 = zder(Yc[0], qz) * ihz;
+        const Real lu = zval(Yc[3], qz) + wzz * zsec(Yc[0], qz);
+        const Real u0 = uq[0][qz], u1 = uq[1][qz], u2 = uq[2][qz];
+        const Real Gu = g0 * u0 + g1 * u1 + g2 * u2;
+        Real f = 0;
+        if (GEN && P.force_q && valid) f = (Real)P.force_q[(gcell * 27 + pa + 3 * pb + 9 * qz) * 3 + cc];
+        Real R = Gu + gp[cc][qz] - nu * lu - f;
+        Real srf = 0;
+        if (GEN && P.srf) {
+          const Real uu[3] = {u0, u1, u2}, xx[3] = {xl, yl, zl + hz * T.xi[qz]};
+          const int c1 = (cc + 1) % 3, c2 = (cc + 2) % 3;
+          const Real cxu = om[c1] * uu[c2] - om[c2] * uu[c1];
+          const Real ox1 = om[(c1 + 1) % 3] * xx[(c1 + 2) % 3] - om[(c1 + 2) % 3] * xx[(c1 + 1) % 3];
+          const Real ox2 = om[(c2 + 1) % 3] * xx[(c2 + 2) % 3] - om[(c2 + 2) % 3] * xx[(c2 + 1) % 3];
+          srf = 2 * cxu + (om[c1] * ox2 - om[c2] * ox1);
+          R += srf;
+        }
+        const Real Tt = Ttq[cc][qz];
+        R += Tt;
+        Rq[cc][qz] = R;
+        divu[qz] += cc == 0 ? g0 : cc == 1 ? g1 : g2;
+        const Real JxW = wxy * T.w[qz], tau = tauq[qz];
+        const Real gg[3] = {g0, g1, g2}, uu[3] = {u0, u1, u2};
+        Real Te[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          Te[e] = JxW * (-nu * gg[e] + (cc == e ? pq[qz] : Real(0)) - tau * R * uu[e]) * ihv[e];
+        const Real Tv = JxW * (-Gu + f - Tt - srf);
+#pragma unroll
+        for (int az = 0; az < 3; ++az) {
+          Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Te[2];
+          Z[1][az] += T.V[qz][az] * Te[0];
+          Z[2][az] += T.V[qz][az] * Te[1];
+        }
+      }
+      backward(cc, Z);
+    }
+    {  // pressure test field: -JxW div u, -JxW tau R_e / h_e
+      Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+        const Real JxW = wxy * T.w[qz], jt = JxW * tauq[qz];
+        const Real Tv = -JxW * divu[qz];
+        const Real Tx = -jt * Rq[0][qz] * ihx, Ty = -jt * Rq[1][qz] * ihy, Tz = -jt * Rq[2][qz] * ihz;
+#pragma unroll
+        for (int az = 0; az < 3; ++az) {
+          Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Tz;
+          Z[1][az] += T.V[qz][az] * Tx;
+          Z[2][az] += T.V[qz][az] * Ty;
+        }
+      }
+      backward(3, Z);
+    }
+  } else {
+  // values of v (all components) and vp, grad vp at the lane's three points: every test field needs
+  // them; each velocity component's gradient / Laplacian sweeps run later, next to its test field, so
+  // that only one component's Y stage is live at a time
+  Real vq[3][3], vpq[3], gvp[3][3];
+  {
+    Real dz[3];
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      Real bb[3];
+      forward(cc, 0, bb, dz, dz, dz);
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) vq[cc][qz] = zval(bb, qz);
+    }
+    Real pb_[3], pbd[3], pdb[3];
+    forward(3, 1, pb_, pbd, pdb, dz);
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+      vpq[qz] = zval(pb_, qz);
+      gvp[0][qz] = zval(pdb, qz) * ihx;
+      gvp[1][qz] = zval(pbd, qz) * ihy;
+      gvp[2][qz] = zder(pb_, qz) * ihz;
+    }
+  }
+
+  // linearization rows of this lane (pencil layout: value v of point qz at + (qz * 16 + v) * 54)
+  const Real *qrow = nullptr;
+  {
+    const Real *base = std::is_same<Real, double>::value ? reinterpret_cast<const Real *>(P.qd)
+                                                          : reinterpret_cast<const Real *>(P.qdf);
+    qrow = base + qdp_base(brick, valid ? ci : 0, pa + 3 * pb);
+  }
+  auto ld = [&](int qz, int v) { return __builtin_nontemporal_load(qrow + (qz * kQData + v) * kQdpRow); };
+  Real uq[3][3], tauq[3];
+#pragma unroll
+  for (int qz = 0; qz < 3; ++qz) {
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) uq[cc][qz] = ld(qz, cc);
+    tauq[qz] = ld(qz, 12);
+  }
+
+  // ---------------- pointwise + backward, one velocity test field (= trial component) at a time
+  Real Sq[3][3], divv[3] = {0, 0, 0};
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    Real Yc[4][3];  // this component's Y stage: BB, BD, DB, L
+    forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
+    Real gu[3][3], Rq[3];  // grad u_cc (by e) and R_cc at the lane's three points
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) gu[e][qz] = ld(qz, 3 + 3 * cc + e);
+      Rq[qz] = ld(qz, 13 + cc);
+    }
+    Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+      const Real gv0 = zval(Yc[2], qz) * ihx, gv1 = zval(Yc[1], qz) * ihy, gv2 = zder(Yc[0], qz) * ihz;
+      const Real lv = zval(Yc[3], qz) + wzz * zsec(Yc[0], qz);
+      const Real v0 = vq[0][qz], v1 = vq[1][qz], v2 = vq[2][qz];
+      const Real u0 = uq[0][qz], u1 = uq[1][qz], u2 = uq[2][qz];
+      const Real guv = gu[0][qz] * v0 + gu[1][qz] * v1 + gu[2][qz] * v2;
+      const Real gvu = gv0 * u0 + gv1 * u1 + gv2 * u2;
+      Real A = guv + gvu + aj * vq[cc][qz];
+      Real S = guv + gvu + gvp[cc][qz] - nu * lv + aj * vq[cc][qz];
+      if (GEN && P.srf) {
+        const Real cj = cc == 0 ? 2 * (om[1] * v2 - om[2] * v1) : cc == 1 ? 2 * (om[2] * v0 - om[0] * v2)
+                                                                         : 2 * (om[0] * v1 - om[1] * v0);
+        A += cj;
+        S += cj;
+      }
+      Sq[cc][qz] = S;
+      divv[qz] += cc == 0 ? gv0 : cc == 1 ? gv1 : gv2;
+      const Real JxW = wxy * T.w[qz], tau = tauq[qz];
+      const Real gv[3] = {gv0, gv1, gv2}, uu[3] = {u0, u1, u2}, vv[3] = {v0, v1, v2};
+      Real Te[3];
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        Te[e] = JxW * (nu * gv[e] - (cc == e ? vpq[qz] : Real(0)) + tau * S * uu[e] + tau * Rq[qz] * vv[e]) * ihv[e];
+      const Real Tv = JxW * A;
+#pragma unroll
+      for (int az = 0; az < 3; ++az) {
+        Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Te[2];
+        Z[1][az] += T.V[qz][az] * Te[0];
+        Z[2][az] += T.V[qz][az] * Te[1];
+      }
+    }
+    backward(cc, Z);
+  }
+  {  // pressure test field: Tv = JxW div v, Te = JxW tau S_e / h_e
+    Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+      const Real JxW = wxy * T.w[qz], jt = JxW * tauq[qz];
+      const Real Tv = JxW * divv[qz];
+      const Real Tx = jt * Sq[0][qz] * ihx, Ty = jt * Sq[1][qz] * ihy, Tz = jt * Sq[2][qz] * ihz;
+#pragma unroll
+      for (int az = 0; az < 3; ++az) {
+        Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Tz;
+        Z[1][az] += T.V[qz][az] * Tx;
+        Z[2][az] += T.V[qz][az] * Ty;
+      }
+    }
+    backward(3, Z);
+  }
+  }  // MODE_JVQ
+  __syncthreads();
+
+  // ---------------- brick reduction (fixed cell order per node) + scatter: one thread per brick node
+  for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
+    const int rb_ = t / BN3, n = t % BN3;
+    if (rb_ >= nbg) break;
+    const int bk = brick_of(rb_);
+    const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
+    Real s[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int kz = 0; kz < 2; ++kz) {
+      const int az = Zn - 2 * kz;
+      if (az < 0 || az > 2) continue;
+#pragma unroll
+      for (int ky = 0; ky < 2; ++ky) {
+        const int ay = Yn - 2 * ky;
+        if (ay < 0 || ay > 2) continue;
+#pragma unroll
+        for (int kx = 0; kx < 2; ++kx) {
+          const int ax = Xn - 2 * kx;
+          if (ax < 0 || ax > 2) continue;
+          const Real *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::NO * C::N3 + ax + 3 * (ay + 3 * az);
+#pragma unroll
+          for (int f = 0; f < 4; ++f) s[f] += o[f * C::N3];
+        }
+      }
+    }
+    const int node = sNode[rb_ * BN3P + n];
+    const int64_t gi[4] = {(int64_t)node * 3, (int64_t)node * 3 + 1, (int64_t)node * 3 + 2, voff + node};
+    const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
+    if (interior) {
+      if (P.jx) {  // fused damped-Jacobi sweep (interior nodes: no other brick reads this x)
+        const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const bool con = f < 3 && ((m >> f) & 1u);
+          const double x = P.jx[gi[f]], dd = P.jd[gi[f]];
+          P.jx[gi[f]] = x + P.jomega * (P.jb[gi[f]] - (con ? dd * x : (double)s[f])) / dd;
+        }
+      } else if (P.rb) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) P.y[gi[f]] = P.rb[gi[f]] - (double)s[f];
+      } else {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) P.y[gi[f]] = s[f];
+      }
+    } else {  // this brick's partial sums of a brick-boundary node (summed per node by k_slab_sum)
+      const int64_t si = ((int64_t)bk * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4;
+      if (std::is_same<Real, float>::value && P.slabf) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<f4 *>(P.slabf + si) = f4{(float)s[0], (float)s[1], (float)s[2], (float)s[3]};
+      } else {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<d2 *>(P.slab + si) = d2{(double)s[0], (double)s[1]};
+        *reinterpret_cast<d2 *>(P.slab + si + 2) = d2{(double)s[2], (double)s[3]};
+      }
+    }
+  }
+}
+
+// Selection: on by default for the Q2 brick J.v with a slab (the launch contract of the
+// lane-per-point kernel); GLS_PENCIL=0 keeps the lane-per-point kernel (A/B, fallback)
+bool pencil_enabled() {  // read per launch: tests compare both kernels in one process
+  const char *e = std::getenv("GLS_PENCIL");
+  return !(e && std::atoi(e) == 0);
+}
+
+template <typename Real, int MODE>
+hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
+  const bool gen = P.srf || (MODE == MODE_RESIDUAL && P.force_q);
+  const int n_items = (std::is_same<Real, double>::value && P.subset) ? P.subset_n : P.n_cells / 8;
+  if (n_items <= 0) return hipSuccess;
+  const int n_groups = (n_items + 2) / 3;
+  PencilTab<Real> tab;
+  for (int q = 0; q < 3; ++q) {
+    tab.w[q] = (Real)T.w[q];
+    for (int i = 0; i < 3; ++i) {
+      tab.V[q][i] = (Real)T.V[q][i];
+      tab.D[q][i] = (Real)T.D[q][i];
+      tab.S[q][i] = (Real)T.S[q][i];
+    }
+    tab.xi[q] = (Real)T.xi[q];
+  }
+  if (gen)
+    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, true>), dim3((unsigned)n_groups), dim3(256),
+                       pencil_lds_bytes<Real>(MODE), s, P, tab);
+  else
+    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, false>), dim3((unsigned)n_groups), dim3(256),
+                       pencil_lds_bytes<Real>(MODE), s, P, tab);
+  return hipGetLastError();
+}
+hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32) {
+  if (P.n_probe > 0 || P.bricks || !(f32 ? (P.slabf != nullptr || P.slab != nullptr) : P.slab != nullptr))
+    return hipErrorNotSupported;
+  return f32 ? launch_pencil_t<float, MODE_JVQ>(P, T, s) : launch_pencil_t<double, MODE_JVQ>(P, T, s);
+}
+hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (P.bricks || !P.slab || P.subset) return hipErrorNotSupported;
+  return launch_pencil_t<double, MODE_RESIDUAL>(P, T, s);
+}
+
+}  // namespace gls

@@ -17,6 +17,12 @@ size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
 // J.v in FP32 arithmetic from P.qdf (FP32 linearization); v, y FP64 (multigrid smoother operator)
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
+// Q2 brick J.v in the pencil dataflow (gls_brick_pencil.hip; FP64 from P.qd or FP32 from P.qdf), same
+// contract as the lane-per-point MODE_JVQ launch with a slab; hipErrorNotSupported when not applicable
+// (probing, colored launches, no slab). GLS_PENCIL=0 disables it.
+hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32);
+hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_RESIDUAL, FP64
+bool pencil_enabled();
 // persistent wave-per-brick versions (gls_brick_wave.hip), selected by the launchers above
 hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t launch_brick_wave_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
@@ -33,6 +39,11 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
                              const int32_t *slots, int64_t n_sum, int64_t n_vnodes, double *y, const uint8_t *vmask,
                              const double *jb, const double *jd, double jomega, hipStream_t s,
                              const double *rb = nullptr);  // rb (no jb): y = rb - A x
+// the same sums on the structured hyper_cube (nb1 bricks per direction, lexicographic nodes, Morton
+// bricks, no periodic wrap): slots computed from the lattice coordinates, no index arrays
+hipError_t brick_slab_sum_cube(int k, int nb1, const double *slab, const float *slabf, int64_t n_vnodes, double *y,
+                               const uint8_t *vmask, const double *jb, const double *jd, double jomega, hipStream_t s,
+                               const double *rb = nullptr);
 bool brick_fused_jacobi_supported(int k);  // the selected brick kernel honours OpParams::jx and ::slabf
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 bool brick_colors_supported(int k);  // colored brick launches (OpParams::bricks) available

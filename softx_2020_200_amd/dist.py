@@ -292,12 +292,23 @@ def multigrid_levels(n, world, coarsest=4):
     return out
 
 
-def attach_distributed_multigrid(levels, **mg_opts):
-    """levels: [DistributedProblem] on nested hyper_cubes (fine first), same ranks / boundary data."""
+def attach_distributed_multigrid(levels, replica=None, **mg_opts):
+    """levels: [DistributedProblem] on nested hyper_cubes (fine first), same ranks / boundary data.
+    replica: optional single-rank problem object (``.ctx``, ``.mesh``; e.g. a CavityProblem with its own
+    multigrid) on the WHOLE mesh of the coarsest distributed level: below that level every rank runs the
+    replica's cycle on the gathered right-hand side (gls_mg_set_coarse_replica), so that the N-rank
+    V-cycle is the one-rank one."""
     for lv in levels:
         lv.set_lattice()
     levels[0].ctx.attach_multigrid([lv.ctx for lv in levels[1:]], **mg_opts)
     levels[0]._mg_levels = levels
+    if replica is not None:
+        cl = levels[-1]
+        l2g = cl.plan["local_to_global"].astype(np.int64)
+        nvg = cl.n_vnodes_global
+        loc = np.concatenate([(l2g[:, None] * 3 + np.arange(3)[None, :]).reshape(-1), 3 * nvg + l2g])
+        levels[0].ctx.set_coarse_replica(replica.ctx, loc)
+        levels[0]._replica = replica
 
 
 

@@ -701,6 +701,15 @@ class GLSContext:
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
 
+    def set_coarse_replica(self, replica, local_to_replica):
+        """Multi-GPU V-cycle below the coarsest distributed level = the single-GPU one, run redundantly on
+        every rank by `replica` (a single-rank GLSContext of that level's whole mesh with its own
+        attach_multigrid hierarchy); local_to_replica: replica row of each local row of that level."""
+        m = np.ascontiguousarray(local_to_replica, dtype=np.int64)
+        check(self.L.gls_mg_set_coarse_replica(self.h, replica.h, len(m), m.ctypes.data_as(C.POINTER(C.c_int64))),
+              "gls_mg_set_coarse_replica")
+        self._coarse_replica = replica
+
     def apply_preconditioner(self, v, out=None):
         out = self.zeros() if out is None else out
         check(self.L.gls_apply_preconditioner(self.h, _ptr(v), _ptr(out)), "gls_apply_preconditioner")

@@ -177,3 +177,63 @@ def test_reference_mms2d_every_linear_solver_method(tmp_path, method):
         assert "ML AMG substituted" in line[0]
     ref = open(os.path.join(CASES, "mms2d_gls.output")).read()
     assert error_rows(out.stdout) == error_rows(ref), (error_rows(out.stdout), error_rows(ref))
+
+
+@pytest.mark.gpu
+def test_reference_cylinder_kelly_flag_flips_are_within_the_inexact_solve_perturbation(tmp_path):
+    """Why the shipped cylinder_gls run (Newton 1e-4, GMRES rel 1e-4) does not reproduce the reference's
+    third and fourth meshes exactly while the converged run does: run both with --dump, recompute on the
+    oracle side, for each cycle on the common mesh, the Kelly indicator of each run's solution
+    (kelly_from_face_pieces: MappingQ1 face pieces, QGauss(3)) and the p::d fixed-number marking
+    (pd_refine_coarsen: refine 0.3 / coarsen 0.1, max 70000 cells). At the first cycle whose flags
+    differ, EVERY differing cell K must satisfy |eta_conv(K) - theta_conv| <= |eta_ship(K) - eta_conv(K)|
+    + |theta_ship - theta_conv| (theta: that flag's threshold): the flip is explained by how far the
+    inexact solve moved that cell's indicator and the threshold, not by a difference in the
+    estimator, the marking or the mesh. The measured perturbation and the flipped cells are printed."""
+    from oracle.oracle import kelly_from_face_pieces, pd_refine_coarsen
+    from softx_2020_200_amd.native import UMesh
+    from tests.test_gpu_app_configs import read_dumps
+    converged = lambda t: t.replace("set tolerance               = 1e-4", "set tolerance = 1e-10").replace(  # noqa: E731
+        "set relative residual       = 1e-4", "set relative residual = 1e-12").replace(
+        "set minimum residual        = 1e-9", "set minimum residual = 1e-14")
+    runs = {}
+    for tag, edit in (("shipped", None), ("converged", converged)):
+        d = tmp_path / tag
+        d.mkdir()
+        (d / "dump").mkdir()
+        run_case(d, "cylinder_gls", 2, "--dump", str(d / "dump"), prm_edit=edit)
+        runs[tag] = read_dumps(str(d / "dump"))
+    assert len(runs["shipped"]) == len(runs["converged"]) == 4
+    m = UMesh(2, gmsh=os.path.join(MESHES, "cylinder_structured.msh"))
+    first_diff = None
+    for cyc in range(3):
+        h = m.fe_space_handle(1, 1)
+        sp = h.data
+        ds, dc = runs["shipped"][cyc], runs["converged"][cyc]
+        assert int(ds["n_cells"]) == int(dc["n_cells"]) == sp["n_cells"], cyc
+        faces = h.kelly_faces(3)
+        es = np.asarray(kelly_from_face_pieces(sp, faces, ds["x"], 0), dtype=np.float32).astype(np.float64)
+        ec = np.asarray(kelly_from_face_pieces(sp, faces, dc["x"], 0), dtype=np.float32).astype(np.float64)
+        rs, cs, (ts, bs) = pd_refine_coarsen(es, 2, 0.3, 0.1, "number", 70000)
+        rc, cc, (tc, bc) = pd_refine_coarsen(ec, 2, 0.3, 0.1, "number", 70000)
+        lev = np.asarray(sp["cell_level"])
+        for r_ in (rs, rc):
+            r_[lev >= 5] = 0  # max refinement level
+        flip_r, flip_c = np.nonzero(rs != rc)[0], np.nonzero(cs != cc)[0]
+        if len(flip_r) or len(flip_c):
+            d_eta = np.abs(es - ec)
+            slack = 1e-6 * max(abs(tc), abs(bc), 1e-30)  # float32 indicators
+            print("cycle %d: %d cells, %d refine / %d coarsen flags differ; max |eta_s - eta_c| %.3e (eta max %.3e), "
+                  "refine threshold %.6e vs %.6e, coarsen threshold %.6e vs %.6e"
+                  % (cyc, sp["n_cells"], len(flip_r), len(flip_c), d_eta.max(), ec.max(), ts, tc, bs, bc))
+            for K in flip_r:
+                assert abs(ec[K] - tc) <= d_eta[K] + abs(ts - tc) + slack, (cyc, K, ec[K], es[K], tc, ts)
+            for K in flip_c:
+                assert abs(ec[K] - bc) <= d_eta[K] + abs(bs - bc) + slack, (cyc, K, ec[K], es[K], bc, bs)
+            first_diff = cyc
+            break
+        r, c = m.prepare(rc, cc)
+        m.adapt(r, c)
+    # the shipped run's third mesh differs from the reference's (4293 vs 4302 cells): the flags differ
+    # at cycle 1 at the latest
+    assert first_diff is not None and first_diff <= 1, first_diff

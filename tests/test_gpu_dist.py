@@ -97,9 +97,12 @@ def test_two_ranks_one_gpu_matches_single_rank():
         assert e["newton_u"] < 1e-7, (rank, e)
 
 
-def _mg_worker(rank, world, port, q):
+def _mg_worker(rank, world, port, q, replica=False):
     """Distributed multigrid (every level partitioned, nested rank boxes) vs the single-rank V-cycle:
-    the preconditioned GMRES and one Newton step must agree (same iterations, same solution)."""
+    the preconditioned GMRES and one Newton step must agree (same iterations, same solution).
+    replica: the bench's cycle -- 2 + 2 sweeps on 4^3 and an exact LU on 2^3 -- on one rank, and on N
+    ranks the distributed levels down to 4^3 with that remainder run on a replica of the 4^3 level
+    (gls_mg_set_coarse_replica)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -112,7 +115,12 @@ def _mg_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n, nu, ts = 8, 0.02, (0.01, 0.01, 0.01, 0.01)
-        single = CavityProblem(dim=3, n=n, k=2, viscosity=nu, multigrid=True, mg_coarsest=4)
+        opts = dict(pre_smooth=1, post_smooth=1, omega=0.9, mixed_precision=True) if replica else {}
+        if replica:
+            single = CavityProblem(dim=3, n=n, k=2, viscosity=nu, multigrid=True, mg_coarsest=2,
+                                   level_sweeps={-2: (2, 2)}, **opts)
+        else:
+            single = CavityProblem(dim=3, n=n, k=2, viscosity=nu, multigrid=True, mg_coarsest=4)
         g = single.ctx
         g.set_time("bdf2", ts)
         m = single.mesh
@@ -135,8 +143,14 @@ def _mg_worker(rank, world, port, q):
             mk, dd, dv = dirichlet_from_bcs(mm, mm_n, -1.0, 1.0, True, bcs)
             levels.append(DistributedProblem(mm, rank, world, "cuda", viscosity=nu, vnode_mask=mk, dirichlet=(dd, dv),
                                              backend="gloo"))
-        assert len(levels) == 1 + len(single.levels)
-        attach_distributed_multigrid(levels)
+        if replica:
+            assert len(levels) == len(single.levels)  # the 2^3 level lives in the replica
+            rep = CavityProblem(dim=3, n=4, k=2, viscosity=nu, multigrid=True, mg_coarsest=2, pre_smooth=2,
+                                post_smooth=2, omega=0.9, mixed_precision=True)
+            attach_distributed_multigrid(levels, replica=rep, coarse_direct=-1, **opts)
+        else:
+            assert len(levels) == 1 + len(single.levels)
+            attach_distributed_multigrid(levels)
         dp = levels[0]
         c = dp.ctx
         c.set_time("bdf2", ts)
@@ -170,13 +184,13 @@ def _mg_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_distributed_multigrid_matches_single_rank(world):
+@pytest.mark.parametrize("world,replica", [(2, False), (4, False), (2, True), (4, True)])
+def test_distributed_multigrid_matches_single_rank(world, replica):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 30300 + 10 * world + os.getpid() % 400
-    procs = [ctx.Process(target=_mg_worker, args=(r, world, port, q)) for r in range(world)]
+    port = 30300 + 10 * world + 5 * int(replica) + os.getpid() % 400
+    procs = [ctx.Process(target=_mg_worker, args=(r, world, port, q, replica)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -185,9 +199,10 @@ def test_distributed_multigrid_matches_single_rank(world):
     for rank, e in res:
         assert "error" not in e, e
         assert e["ok"] == (True, True), (rank, e)
-        assert abs(e["lin_its"][0] - e["lin_its"][1]) <= 1, (rank, e)
+        tol_its = 0 if replica else 1  # the replica's cycle is the one-rank cycle: identical counts
+        assert abs(e["lin_its"][0] - e["lin_its"][1]) <= tol_its, (rank, e)
         assert e["x_rel"] < 1e-7, (rank, e)
-        assert abs(e["newton_lin_its"][0] - e["newton_lin_its"][1]) <= 1, (rank, e)
+        assert abs(e["newton_lin_its"][0] - e["newton_lin_its"][1]) <= tol_its, (rank, e)
         assert e["newton_x"] < 1e-7, (rank, e)
 
 

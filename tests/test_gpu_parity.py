@@ -243,3 +243,34 @@ def test_brick_jv_f32_vs_oracle(case):
     e2 = relerr(ctx.jacobian_apply_f32(cuda(v)).cpu().numpy(), orc.jacobian_apply(u3, v, u1, u2, u))
     print("FP32 J.v rel err %.2e %.2e" % (e1, e2))
     assert e1 < TOL_F32 and e2 < TOL_F32, (e1, e2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4, 6])
+def test_pencil_kernel_and_structured_slab_sum(monkeypatch, n):
+    """The Q2 J.v's two brick kernels and two slab-sum forms agree: the pencil-dataflow kernel
+    (gls_brick_pencil.hip, default) and the lane-per-point kernel (GLS_PENCIL=0) to FP64 rounding
+    (1e-13; FP32 smoother operator to FP32 rounding), and the structured hyper_cube slab sum
+    (k_slab_sum_cube, default on the cube) BITWISE equal to the node/offset/slot-map form
+    (GLS_SLAB_CSR=1, read at context creation): the same slots in the same ascending order. n = 2, 4
+    leave the last brick triple short (1 and 2 of 3 bricks)."""
+    p = _morton_problem(n, 2, "bdf2", 0.01)
+    u, u1, u2, u3, v = _states(p)
+    ctx = context_for(p)
+    monkeypatch.setenv("GLS_SLAB_CSR", "1")
+    csr = context_for(p)
+    monkeypatch.delenv("GLS_SLAB_CSR")
+    for c in (ctx, csr):
+        c.set_state(cuda(u), cuda(u1), cuda(u2))
+    V = cuda(v)
+    a = ctx.jacobian_apply(V).cpu().numpy()
+    assert np.array_equal(a, csr.jacobian_apply(V).cpu().numpy())
+    af = ctx.jacobian_apply_f32(V).cpu().numpy()
+    assert np.array_equal(af, csr.jacobian_apply_f32(V).cpu().numpy())
+    monkeypatch.setenv("GLS_PENCIL", "0")
+    b = ctx.jacobian_apply(V).cpu().numpy()
+    bf = ctx.jacobian_apply_f32(V).cpu().numpy()
+    monkeypatch.delenv("GLS_PENCIL")
+    assert relerr(a, b) < 1e-13, relerr(a, b)
+    assert relerr(af, bf) < 2e-6, relerr(af, bf)
+    assert relerr(a, Oracle(p).jacobian_apply(u, v, u1, u2)) < TOL

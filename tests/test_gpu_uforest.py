@@ -69,8 +69,6 @@ def test_mapped_kelly_kernel_matches_host(name, dim, spec, flat, k, kp):
 @pytest.mark.parametrize("name,dim,spec,flat", CASES, ids=[c[0] for c in CASES])
 @pytest.mark.parametrize("k,kp,scheme", [(1, 1, "bdf2"), (2, 1, "steady"), (2, 2, "bdf1")])
 def test_adapted_mapped_operators_match_oracle(name, dim, spec, flat, k, kp, scheme):
-    if dim == 3 and k == 2 and kp == 2:
-        pytest.skip("3D Q2-Q2 covered by Q2-Q1")
     m, h = adapted_space(name, dim, spec, k, kp)
     sp = h.data
     p = MappedProblem(sp, viscosity=0.05, scheme=scheme, time_steps=(0.01, 0.012, 0.011, 0.01))
