@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+PMC_TRAFFIC_FILE = "r04_pmc_traffic_pencil_128.txt"  # tools/pmc_traffic.sh summary of the pencil J.v
 FP64_PEAK_TFS = 78.6        # MI355X FP64 (vector = matrix) spec; measured 61-64 TF (profiles/r01_microbench_fp64.txt)
 
 
@@ -75,7 +76,8 @@ def pmc_traffic(path, kernel_mode, n_dofs):
         if cur and f and f[0] in ("FETCH_SIZE", "WRITE_SIZE"):
             vals.setdefault(cur, {})[f[0]] = float(f[1]) * 1024.0
     copy = next((v for k_, v in vals.items() if "k_copy" in k_), None)
-    kern = next((v for k_, v in vals.items() if "gls_brick_kernel<2, %d, double>" % kernel_mode in k_), None)
+    kern = next((v for k_, v in vals.items() if ("gls_pencil_kernel<double, %d" % kernel_mode in k_
+                                                 or "gls_brick_kernel<2, %d, double>" % kernel_mode in k_)), None)
     slab = next((v for k_, v in vals.items() if "k_slab_sum<double" in k_), {})
     if not copy or not kern or len(copy) < 2 or len(kern) < 2:
         return None
@@ -94,6 +96,18 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def cpu_threads():
+    """Host threads of the CPU legs and why: OMP_NUM_THREADS when set -- on the GPU box the pool sets it to
+    this job's CPU share (16 host threads per GPU; the affinity mask shows the whole machine, whose other
+    cores belong to other jobs) -- else every CPU in the process's affinity."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    aff = len(os.sched_getaffinity(0))
+    if env:
+        return env, ("OMP_NUM_THREADS=%d: the job's CPU share (the affinity mask lists %d CPUs of the whole "
+                     "machine, shared with other jobs)" % (env, aff))
+    return aff, "every CPU in the process's affinity mask (%d)" % aff
 
 
 def cpu_baseline(k, kp, nu, seconds, threads):
@@ -533,34 +547,40 @@ def main():
         "setup_s": t_setup,
     }
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    tr = pmc_traffic(os.path.join(ROOT, "profiles", "r03_pmc_traffic_head_s3_128.txt"), 4, N_global) \
-        if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels) else None
-    if tr is not None and args.k == 2 and world == 1:
-        # the roof that actually binds the brick J.v: the LDS pipe (DESIGN §4 "What bounds the J.v").
-        # Cycles per wave = the kernel's LDS instruction stream priced by MI355X_MICROARCH.md §LDS
-        # (tools/isa_mix.py: 1248 static, x 234/248 executed per the PMC instruction count) inflated by
-        # the measured bank-conflict share (16.5 % of LDS-array cycles), profiles/r03_lds_roof_model.txt
-        lds_cyc_wave = 1248 * 234 / 248 / (1 - 0.165)
-        waves_per_cu = (n_cells // 8) * 4 / 256
-        lds_ms = waves_per_cu * lds_cyc_wave / 2.4e9 * 1e3  # at the 2400 MHz peak clock
-        out["roofline"]["lds"] = {"kernel": "gls_brick_kernel<2,MODE_JVQ,double>", "lds_cycles_per_wave": lds_cyc_wave,
-                                  "waves_per_cu": waves_per_cu, "floor_ms_at_2400MHz": lds_ms,
+    pencil = os.environ.get("GLS_PENCIL", "1") != "0"
+    tr = pmc_traffic(os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE), 4, N_global) \
+        if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil) else None
+    model_path = os.path.join(ROOT, "profiles", "r04_lds_model.json")
+    if world == 1 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil and os.path.exists(model_path):
+        # the LDS and VALU issue floors of the pencil J.v from a STATIC model of its compiled instruction
+        # stream (tools/lds_model.py: LDS instructions priced conflict-free by MI355X_MICROARCH.md §LDS,
+        # FP64 VALU at 4 cycles per wave instruction), not a measurement; the commit it was derived from
+        # is in the file
+        mdl = json.load(open(model_path))
+        km = next(v for k_, v in mdl["kernels"].items() if "gls_pencil_kernelIdLi4ELb0" in k_)
+        waves_per_cu = -(-(n_cells // 8) // 3) * 4 / 256
+        lds_ms = waves_per_cu * km["lds_cycles_per_wave"] / 2.4e9 * 1e3  # the CU's LDS pipe at 2400 MHz
+        valu_ms = waves_per_cu / 4 * (4 * km["valu_f64"] + 2 * km["valu_other"]) / 2.4e9 * 1e3  # per SIMD
+        out["roofline"]["lds"] = {"kernel": "gls_pencil_kernel<double,MODE_JVQ>", "model": "static",
+                                  "lds_cycles_per_wave": km["lds_cycles_per_wave"], "waves_per_cu": waves_per_cu,
+                                  "floor_ms_at_2400MHz": lds_ms, "valu_floor_ms_at_2400MHz": valu_ms,
                                   "launch_ms": jv_launch_ms, "frac": lds_ms / jv_launch_ms,
-                                  "source": "profiles/r03_lds_roof_model.txt"}
+                                  "source": "profiles/r04_lds_model.json (%s)" % mdl.get("commit")}
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
-        out["roofline"]["traffic_source"] = ("profiles/r03_pmc_traffic_head_s3_128.txt: FETCH_SIZE x %.2f + WRITE_SIZE x "
+        out["roofline"]["traffic_source"] = ("profiles/%s: FETCH_SIZE x %.2f + WRITE_SIZE x "
                                              "%.2f (k_copy calibration); includes the per-quadrature-point "
                                              "linearization stream (16 doubles/q) the cached J.v reads instead "
-                                             "of re-deriving u, grad u, tau, R_s" % (tr[1], tr[2]))
+                                             "of re-deriving u, grad u, tau, R_s" % (PMC_TRAFFIC_FILE, tr[1], tr[2]))
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_full:
         # the reference's CPU path measured end to end on this very workload (1 Newton iteration)
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        threads, cores_note = cpu_threads()
         full = cpu_newton(args.k, args.kp, args.n, args.nu, args.scheme, args.dt, threads)
         # the 1-thread leg only on request (--cpu-full-1core): at Q1 64^3 it is ~5 min of host time
         full1 = cpu_newton(args.k, args.kp, args.n, args.nu, args.scheme, args.dt, 1) if args.cpu_full_1core else None
         out["cpu_baseline"] = {
-            "value": 1.0 / full["seconds"], "unit": "nonlinear_iters/s", "cores": threads, "kind": "port",
+            "value": 1.0 / full["seconds"], "unit": "nonlinear_iters/s", "cores": threads, "cores_note": cores_note,
+            "kind": "port",
             "value_1core": 1.0 / full1["seconds"] if full1 else None, "cpu": _cpu_model(), "host_cpus_visible": os.cpu_count(),
             "affinity": len(os.sched_getaffinity(0)),
             "sample": ("MEASURED: one complete Newton iteration of the reference's CPU path on the full workload "
@@ -575,7 +595,7 @@ def main():
         }
     elif rank == 0 and world == 1 and not args.no_cpu:
         # the OpenMP threads this process may use (OMP_NUM_THREADS; on the GPU box the job's CPU share)
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        threads, cores_note = cpu_threads()
         cb = cpu_baseline(args.k, args.kp, args.nu, args.cpu_seconds, threads)
         per_cell = {key: cb[key][1] / cb[key][0] for key in ("matrix", "rhs", "matrix_1core", "rhs_1core")}
         L_ = float(np.mean(nres)) - 1.0    # line-search residuals per Newton step (GPU run's count)
@@ -590,7 +610,7 @@ def main():
         t_all = t_iter((per_cell["matrix"], per_cell["rhs"]))
         t_one = t_iter((per_cell["matrix_1core"], per_cell["rhs_1core"]), spmv_scale=threads)
         out["cpu_baseline"] = {
-            "value": 1.0 / t_all, "unit": "nonlinear_iters/s", "cores": threads, "kind": "port",
+            "value": 1.0 / t_all, "unit": "nonlinear_iters/s", "cores": threads, "cores_note": cores_note, "kind": "port",
             "value_1core": 1.0 / t_one,
             "cpu": _cpu_model(), "host_cpus_visible": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
             "sample": ("EXTRAPOLATED from measured samples to one Newton step of the GPU run (m = %.1f GMRES its, "

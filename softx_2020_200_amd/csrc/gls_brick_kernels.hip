@@ -985,8 +985,9 @@ hipError_t launch_brick_t(int mode, const OpParams &P, const Tables1D &T, hipStr
   OpParams Q = P;
   if (!colored) Q.bricks = nullptr;
   // the Q2 J.v from the linearization: the pencil-dataflow kernel (gls_brick_pencil.hip)
-  if (K == 2 && (mode == MODE_JVQ || mode == MODE_RESIDUAL) && !colored && pencil_enabled()) {
-    const hipError_t e = mode == MODE_JVQ ? launch_pencil_jv(Q, T, s, false) : launch_pencil_residual(Q, T, s);
+  if (K == 2 && (mode == MODE_JVQ || mode == MODE_RESIDUAL || mode == MODE_LIN) && !colored && pencil_enabled()) {
+    const hipError_t e = mode == MODE_JVQ ? launch_pencil_jv(Q, T, s, false)
+                         : mode == MODE_RESIDUAL ? launch_pencil_residual(Q, T, s) : launch_pencil_lin(Q, T, s);
     if (e != hipErrorNotSupported) return e;
   }
   for (int col = 0; col < nc; ++col) {

@@ -55,7 +55,7 @@ struct PencilCfg {
 };
 
 // brick fields gathered per brick: J.v: v (3) + v_p; residual: u (3), p, the history H = sum_k alpha_k u^(k) (3)
-constexpr int pencil_fields(int mode) { return mode == MODE_RESIDUAL ? 7 : 4; }
+constexpr int pencil_fields(int mode) { return mode == MODE_JVQ ? 4 : 7; }
 template <typename Real>
 size_t pencil_lds_bytes(int mode) {
   using C = PencilCfg<Real>;
@@ -76,7 +76,8 @@ template <typename Real, int MODE, bool GEN>
 __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
     gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
   using C = PencilCfg<Real>;
-  constexpr bool RES = MODE == MODE_RESIDUAL;  // else MODE_JVQ
+  constexpr bool RES = MODE == MODE_RESIDUAL, LIN = MODE == MODE_LIN;  // else MODE_JVQ
+  constexpr bool ST = RES || LIN;  // state sweeps (u, p, H) instead of the cached linearization
   constexpr int BN = C::BN, BN3 = C::BN3, BN3P = C::BN3P, NF = pencil_fields(MODE);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Real *const sB = reinterpret_cast<Real *>(smem_raw);            // [3 bricks][NF fields][BN3P]
@@ -114,7 +115,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * 27 + a];
     const int64_t i3 = (int64_t)node * 3;
     Real *b = sB + bi * NF * BN3P + n;
-    if constexpr (RES) {
+    if constexpr (ST) {
       double h[3] = {0., 0., 0.};
 #pragma unroll
       for (int cc = 0; cc < 3; ++cc) {
@@ -266,8 +267,10 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     wave_sync();  // the stage area is rewritten by the next field
   };
 
-  if constexpr (RES) {
-    // ---------------- residual (assemble_rhs, gls_navier_stokes.cc:391-516): values of u, H and p, grad p
+  if constexpr (ST) {
+    // ---------------- residual (assemble_rhs, gls_navier_stokes.cc:391-516) / linearization (MODE_LIN:
+    // u, grad u, tau, R_s per point into the pencil rows, then the Jacobian diagonal): values of u, H
+    // and p, grad p
     Real uq[3][3], Ttq[3][3], pq[3], gp[3][3];
     {
       Real dz[3];
@@ -302,6 +305,23 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       const Real t1 = Real(2) * u_mag / hst, t2 = Real(4) * nu / (hst * hst);
       tauq[qz] = Real(1) / sqrt((Real)P.sdt2 + t1 * t1 + Real(9) * (t2 * t2));
     }
+    // MODE_LIN: the lane's linearization rows (pencil layout, qdp_base), FP64 and the FP32 copy
+    double *const lrow = LIN && P.qd ? P.qd + qdp_base(brick, valid ? ci : 0, pa + 3 * pb) : nullptr;
+    float *const lrowf = LIN && P.qdf ? P.qdf + qdp_base(brick, valid ? ci : 0, pa + 3 * pb) : nullptr;
+    auto st_lin = [&](int qz, int v, Real x) {
+      if (!valid) return;
+      if (lrow) lrow[(qz * kQData + v) * kQdpRow] = (double)x;
+      if (lrowf) __builtin_nontemporal_store((float)x, lrowf + (qz * kQData + v) * kQdpRow);
+    };
+    if constexpr (LIN) {
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) st_lin(qz, cc, uq[cc][qz]);
+        st_lin(qz, 12, tauq[qz]);
+      }
+    }
+    Real gcq[3][3];  // MODE_LIN: d u_c / d x_c + alpha_jac per point (the diagonal's mass-like factor)
     // SRF: the lane's point coordinates x0 + h xi (z per point)
     Real xl = 0, yl = 0, zl = 0;
     if (GEN && P.srf) {
@@ -339,6 +359,14 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
         R += Tt;
         Rq[cc][qz] = R;
         divu[qz] += cc == 0 ? g0 : cc == 1 ? g1 : g2;
+        if constexpr (LIN) {
+          st_lin(qz, 3 + 3 * cc + 0, g0);
+          st_lin(qz, 3 + 3 * cc + 1, g1);
+          st_lin(qz, 3 + 3 * cc + 2, g2);
+          st_lin(qz, 13 + cc, R);
+          gcq[cc][qz] = (cc == 0 ? g0 : cc == 1 ? g1 : g2) + aj;
+          continue;
+        }
         const Real JxW = wxy * T.w[qz], tau = tauq[qz];
         const Real gg[3] = {g0, g1, g2}, uu[3] = {u0, u1, u2};
         Real Te[3];
@@ -353,9 +381,90 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
           Z[2][az] += T.V[qz][az] * Te[1];
         }
       }
-      backward(cc, Z);
+      if constexpr (RES) backward(cc, Z);
     }
-    {  // pressure test field: -JxW div u, -JxW tau R_e / h_e
+    if constexpr (LIN) {
+      // ---------------- Jacobian diagonal at this state (the lane-per-point MODE_LIN restated): for
+      // the trial / test pair phi_i e_c (gls_navier_stokes.cc:548-622 with v = phi_i e_c)
+      //   J_ii(c) = sum_q JxW [A phi + nu |grad phi|^2 + tau (A - nu lap phi) a + tau R_c phi d_c phi],
+      //   A = (du_c/dx_c + alpha_jac) phi + a, a = u . grad phi;  J_ii(p) = sum_q JxW tau |grad psi|^2,
+      // deal.II's |K_e(i,i)| on constrained rows. Lane (a, b) = node column (ix, iy), nodes iz = 0..2;
+      // the points' data go through the stage area one qz plane at a time.
+      if (P.y == nullptr) return;  // linearization only (uniform over the workgroup)
+      Real Vx[3], Dx[3], Sx[3], Vy[3], Dy[3], Sy[3];  // the lane's node columns of the 1D tables
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const Real *rx = sRow + q * 4, *ry = sRow + q * 4;
+        Vx[q] = rx[pa];
+        Dx[q] = rx[16 + pa] * ihx;
+        Sx[q] = rx[32 + pa] * wxx;
+        Vy[q] = ry[pb];
+        Dy[q] = ry[16 + pb] * ihy;
+        Sy[q] = ry[32 + pb] * wyy;
+      }
+      Real acc[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+        // plane qz: [value][qx + 3 qy] = u0 u1 u2 gc0 gc1 gc2 tau R0 R1 R2 JxW
+        if (act) {
+          const int o = pa + 3 * pb;
+          cellS[0 * 9 + o] = uq[0][qz];
+          cellS[1 * 9 + o] = uq[1][qz];
+          cellS[2 * 9 + o] = uq[2][qz];
+          cellS[3 * 9 + o] = gcq[0][qz];
+          cellS[4 * 9 + o] = gcq[1][qz];
+          cellS[5 * 9 + o] = gcq[2][qz];
+          cellS[6 * 9 + o] = tauq[qz];
+          cellS[7 * 9 + o] = Rq[0][qz];
+          cellS[8 * 9 + o] = Rq[1][qz];
+          cellS[9 * 9 + o] = Rq[2][qz];
+          cellS[10 * 9 + o] = wxy * T.w[qz];
+        }
+        wave_sync();
+#pragma nounroll
+        for (int qy = 0; qy < 3; ++qy) {
+#pragma unroll
+          for (int qx = 0; qx < 3; ++qx) {
+            const int o = qx + 3 * qy;
+            const Real u0 = cellS[o], u1 = cellS[9 + o], u2 = cellS[18 + o];
+            const Real gc[3] = {cellS[27 + o], cellS[36 + o], cellS[45 + o]};
+            const Real tq = cellS[54 + o], jw = cellS[90 + o];
+            const Real Rr[3] = {cellS[63 + o], cellS[72 + o], cellS[81 + o]};
+            const Real jt = jw * tq;
+            const Real bxy = Vx[qx] * Vy[qy], dxy = Dx[qx] * Vy[qy], xdy = Vx[qx] * Dy[qy];
+            const Real lxy = Sx[qx] * Vy[qy] + Vx[qx] * Sy[qy];
+#pragma unroll
+            for (int iz = 0; iz < 3; ++iz) {
+              const Real b2 = T.V[qz][iz], d2 = T.D[qz][iz] * ihz, s2 = T.S[qz][iz] * wzz;
+              const Real phi = bxy * b2;
+              const Real g[3] = {dxy * b2, xdy * b2, bxy * d2};
+              const Real lap = lxy * b2 + bxy * s2;
+              const Real av = u0 * g[0] + u1 * g[1] + u2 * g[2];
+              const Real g2 = g[0] * g[0] + g[1] * g[1] + g[2] * g[2];
+              const Real c0 = jw * (av * phi + nu * g2) + jt * av * (av - nu * lap);
+              const Real k1 = jw * phi * (phi + tq * av), k2 = jt * phi;
+#pragma unroll
+              for (int c3 = 0; c3 < 3; ++c3) acc[iz][c3] += c0 + gc[c3] * k1 + k2 * Rr[c3] * g[c3];
+              acc[iz][3] += jt * g2;
+            }
+          }
+        }
+        wave_sync();  // the plane is rewritten by the next qz
+      }
+      // deal.II's constrained-row rule: |K_e(i,i)| summed over cells
+      if (valid) {
+#pragma unroll
+        for (int iz = 0; iz < 3; ++iz) {
+          const int bn = (2 * cx + pa) + BN * ((2 * cy + pb) + BN * (2 * cz + iz));
+          const unsigned msk = P.vmask ? P.vmask[sNode[bi * BN3P + bn]] : 0u;
+#pragma unroll
+          for (int c3 = 0; c3 < 3; ++c3)
+            outc[c3 * C::N3 + 9 * iz + 3 * pb + pa] = (msk >> c3) & 1u ? fabs(acc[iz][c3]) : acc[iz][c3];
+          outc[3 * C::N3 + 9 * iz + 3 * pb + pa] = acc[iz][3];
+        }
+      }
+    }
+    if constexpr (RES) {  // pressure test field: -JxW div u, -JxW tau R_e / h_e
       Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
 #pragma unroll
       for (int qz = 0; qz < 3; ++qz) {
@@ -546,7 +655,7 @@ bool pencil_enabled() {  // read per launch: tests compare both kernels in one p
 
 template <typename Real, int MODE>
 hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
-  const bool gen = P.srf || (MODE == MODE_RESIDUAL && P.force_q);
+  const bool gen = P.srf || (MODE != MODE_JVQ && P.force_q);
   const int n_items = (std::is_same<Real, double>::value && P.subset) ? P.subset_n : P.n_cells / 8;
   if (n_items <= 0) return hipSuccess;
   const int n_groups = (n_items + 2) / 3;
@@ -576,6 +685,10 @@ hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s,
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (P.bricks || !P.slab || P.subset) return hipErrorNotSupported;
   return launch_pencil_t<double, MODE_RESIDUAL>(P, T, s);
+}
+hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (P.bricks || (P.y && !P.slab) || P.subset || !P.qd) return hipErrorNotSupported;
+  return launch_pencil_t<double, MODE_LIN>(P, T, s);
 }
 
 }  // namespace gls

@@ -22,6 +22,7 @@ hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
 // (probing, colored launches, no slab). GLS_PENCIL=0 disables it.
 hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32);
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_RESIDUAL, FP64
+hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_LIN (+ diagonal into P.y)
 bool pencil_enabled();
 // persistent wave-per-brick versions (gls_brick_wave.hip), selected by the launchers above
 hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);

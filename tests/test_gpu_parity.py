@@ -246,31 +246,36 @@ def test_brick_jv_f32_vs_oracle(case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 4, 6])
-def test_pencil_kernel_and_structured_slab_sum(monkeypatch, n):
-    """The Q2 J.v's two brick kernels and two slab-sum forms agree: the pencil-dataflow kernel
-    (gls_brick_pencil.hip, default) and the lane-per-point kernel (GLS_PENCIL=0) to FP64 rounding
-    (1e-13; FP32 smoother operator to FP32 rounding), and the structured hyper_cube slab sum
-    (k_slab_sum_cube, default on the cube) BITWISE equal to the node/offset/slot-map form
-    (GLS_SLAB_CSR=1, read at context creation): the same slots in the same ascending order. n = 2, 4
-    leave the last brick triple short (1 and 2 of 3 bricks)."""
-    p = _morton_problem(n, 2, "bdf2", 0.01)
+@pytest.mark.parametrize("n,scheme,srf", [(2, "bdf2", False), (4, "bdf2", False), (6, "bdf1", False),
+                                          (4, "steady", True)])
+def test_pencil_kernels_and_structured_slab_sum(monkeypatch, n, scheme, srf):
+    """The Q2 brick operators in the two dataflows agree: the pencil kernels (gls_brick_pencil.hip,
+    default: residual, linearization + Jacobian diagonal, J.v, FP32 smoother J.v) and the lane-per-point
+    kernels (GLS_PENCIL=0) to FP64 rounding (1e-13; the FP32 operator to FP32 rounding), both equal to the
+    oracle; and the structured hyper_cube slab sum (k_slab_sum_cube, default on the cube) is BITWISE the
+    node/offset/slot-map form (GLS_SLAB_CSR=1, read at context creation): same slots, same ascending
+    order. n = 2, 4 leave the last brick triple short (1 and 2 of 3 bricks); the forcing and (case 4)
+    the SRF source run the general instantiation."""
+    p = _morton_problem(n, 2, scheme, 0.01, srf=srf)
     u, u1, u2, u3, v = _states(p)
     ctx = context_for(p)
     monkeypatch.setenv("GLS_SLAB_CSR", "1")
     csr = context_for(p)
     monkeypatch.delenv("GLS_SLAB_CSR")
-    for c in (ctx, csr):
-        c.set_state(cuda(u), cuda(u1), cuda(u2))
     V = cuda(v)
-    a = ctx.jacobian_apply(V).cpu().numpy()
-    assert np.array_equal(a, csr.jacobian_apply(V).cpu().numpy())
-    af = ctx.jacobian_apply_f32(V).cpu().numpy()
-    assert np.array_equal(af, csr.jacobian_apply_f32(V).cpu().numpy())
-    monkeypatch.setenv("GLS_PENCIL", "0")
-    b = ctx.jacobian_apply(V).cpu().numpy()
-    bf = ctx.jacobian_apply_f32(V).cpu().numpy()
+    out = {}
+    for tag, c, pencil in (("pencil", ctx, "1"), ("csr", csr, "1"), ("lpp", ctx, "0")):
+        monkeypatch.setenv("GLS_PENCIL", pencil)
+        c.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))  # drops the cached linearization / diagonal
+        out[tag] = [c.residual().cpu().numpy(), c.jacobian_diagonal().cpu().numpy(),
+                    c.jacobian_apply(V).cpu().numpy(), c.jacobian_apply_f32(V).cpu().numpy()]
     monkeypatch.delenv("GLS_PENCIL")
-    assert relerr(a, b) < 1e-13, relerr(a, b)
-    assert relerr(af, bf) < 2e-6, relerr(af, bf)
-    assert relerr(a, Oracle(p).jacobian_apply(u, v, u1, u2)) < TOL
+    for a, b in zip(out["pencil"], out["csr"]):
+        assert np.array_equal(a, b)
+    names = ("residual", "diagonal", "J.v", "J.v f32")
+    for i, (a, b) in enumerate(zip(out["pencil"], out["lpp"])):
+        assert relerr(a, b) < (2e-6 if i == 3 else 1e-13), (names[i], relerr(a, b))
+    orc = Oracle(p)
+    assert relerr(out["pencil"][0], orc.residual(u, u1, u2, u3)) < TOL
+    assert relerr(out["pencil"][1], orc.jacobian_diagonal(u, u1, u2, u3)) < TOL
+    assert relerr(out["pencil"][2], orc.jacobian_apply(u, v, u1, u2, u3)) < TOL

@@ -9,7 +9,7 @@ mkdir -p $OUT
 i=0
 for CTR in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-include-regex "gls_brick_kernel|k_copy|k_slab_sum" -d $OUT/p$i -o run \
+  timeout -k 10 300 rocprofv3 --pmc $CTR --kernel-include-regex "gls_brick_kernel|gls_pencil_kernel|k_copy|k_slab_sum" -d $OUT/p$i -o run \
       --output-format csv -- python3 tools/jv_bench.py $N 4 > $OUT/p$i.log 2>&1 || exit 1
 done
 python3 - "$OUT" << 'PY'
