@@ -104,6 +104,26 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     if (r < 3 && cc < 3) v = mat == 0 ? T.V[r][cc] : mat == 1 ? T.D[r][cc] : T.S[r][cc];
     sRow[tid] = v;
   }
+  // ---------------- per lane: cell c of this wave, (a, b) position in the cell's 3 x 3 pencil grid
+  const bool act = lane < 9 * C::CPW;
+  const int c = act ? lane / 9 : 0, rr = act ? lane % 9 : 0, pa = rr % 3, pb = rr / 3;
+  const int cw = wave * C::CPW + c, bi = cw >> 3, ci = cw & 7;
+  const bool valid = act && bi < nbg;
+  const int brick = brick_of(valid ? bi : 0);
+  const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
+  const int64_t gcell = (int64_t)brick * 8 + (valid ? ci : 0);
+  const Real hx = (Real)P.geo[gcell * 4 + 0], hy = (Real)P.geo[gcell * 4 + 1], hz = (Real)P.geo[gcell * 4 + 2];
+  const Real ihx = Real(1) / hx, ihy = Real(1) / hy, ihz = Real(1) / hz;
+  const Real wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
+  Real *const cellS = sS + (wave * C::CPW + c) * C::CS;
+  // J.v: the lane's linearization rows (issued after the sweeps of each component: loading all 48
+  // values up front was measured slower, it needs ~96 more VGPRs or spills)
+  const Real *qrow = nullptr;
+  if constexpr (!ST) {
+    const Real *base = std::is_same<Real, double>::value ? reinterpret_cast<const Real *>(P.qd)
+                                                          : reinterpret_cast<const Real *>(P.qdf);
+    qrow = base + qdp_base(brick, valid ? ci : 0, pa + 3 * pb);
+  }
   // ---------------- gather the group's brick nodes: v (masked: P v) or u, p, H, and the node ids
   for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
     const int bi = t / BN3, n = t % BN3;
@@ -142,18 +162,6 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   }
   __syncthreads();
 
-  // ---------------- per lane: cell c of this wave, (a, b) position in the cell's 3 x 3 pencil grid
-  const bool act = lane < 9 * C::CPW;
-  const int c = act ? lane / 9 : 0, rr = act ? lane % 9 : 0, pa = rr % 3, pb = rr / 3;
-  const int cw = wave * C::CPW + c, bi = cw >> 3, ci = cw & 7;
-  const bool valid = act && bi < nbg;
-  const int brick = brick_of(valid ? bi : 0);
-  const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
-  const int64_t gcell = (int64_t)brick * 8 + (valid ? ci : 0);
-  const Real hx = (Real)P.geo[gcell * 4 + 0], hy = (Real)P.geo[gcell * 4 + 1], hz = (Real)P.geo[gcell * 4 + 2];
-  const Real ihx = Real(1) / hx, ihy = Real(1) / hy, ihz = Real(1) / hz;
-  const Real wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
-  Real *const cellS = sS + (wave * C::CPW + c) * C::CS;
 
   // ---------------- forward sweeps of brick field f into Y registers ([k]: BB, BD, DB, L). kind 0: the
   // value only (BB); 1: value and gradient (BB, BD, DB; pressure); 2: velocity (+ L for the Laplacian)
@@ -505,13 +513,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     }
   }
 
-  // linearization rows of this lane (pencil layout: value v of point qz at + (qz * 16 + v) * 54)
-  const Real *qrow = nullptr;
-  {
-    const Real *base = std::is_same<Real, double>::value ? reinterpret_cast<const Real *>(P.qd)
-                                                          : reinterpret_cast<const Real *>(P.qdf);
-    qrow = base + qdp_base(brick, valid ? ci : 0, pa + 3 * pb);
-  }
+  // linearization rows of this lane (pencil layout: value v of point qz), loaded at the start
   auto ld = [&](int qz, int v) { return __builtin_nontemporal_load(qrow + (qz * kQData + v) * kQdpRow); };
   Real uq[3][3], tauq[3];
 #pragma unroll
