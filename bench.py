@@ -78,7 +78,7 @@ def pmc_traffic(path, kernel_mode, n_dofs):
     copy = next((v for k_, v in vals.items() if "k_copy" in k_), None)
     kern = next((v for k_, v in vals.items() if ("gls_pencil_kernel<double, %d" % kernel_mode in k_
                                                  or "gls_brick_kernel<2, %d, double>" % kernel_mode in k_)), None)
-    slab = next((v for k_, v in vals.items() if "k_slab_sum<double" in k_), {})
+    slab = next((v for k_, v in vals.items() if "k_slab_sum<double" in k_ or "k_slab_sum_cube<double, false" in k_), {})
     if not copy or not kern or len(copy) < 2 or len(kern) < 2:
         return None
     fetch_corr = 8.0 * n_dofs / copy["FETCH_SIZE"]
@@ -497,6 +497,8 @@ def main():
     slab_launch_ms = sl2_ms / max(jv2_n, 1)
     op_ms = jv_launch_ms + slab_launch_ms
     achieved = B_jv / (op_ms * 1e-3) / 1e9
+    pencil = os.environ.get("GLS_PENCIL", "1") != "0"
+    pencil_jv = pencil and args.k == 2  # the Q2 brick J.v runs in the pencil dataflow (gls_brick_pencil.hip)
     # dense-contraction FLOP count of the kernel as written (per cell, Q2-Q2 3D): see DESIGN.md §4
     out = {
         "metric": "nonlinear iters/sec (3D cavity Q%d %d^3 %s)" % (args.k, args.n, args.scheme.upper()),
@@ -539,15 +541,16 @@ def main():
                                         "jv_linearization": lin_ms / (1e3 * elapsed_instr),
                                         "smoother_jv_f32": f32_ms / (1e3 * elapsed_instr),
                                         "slab_sum": sl_ms / (1e3 * elapsed_instr)}},
-        "roofline": {"bound": "hbm", "kernel": "gls_brick_kernel<%d,MODE_JVQ> + k_slab_sum" % args.k if ctx.uses_brick_kernels
+        "roofline": {"bound": "hbm", "kernel": ("gls_pencil_kernel<double,MODE_JVQ> + slab sum" if pencil_jv else
+                                                "gls_brick_kernel<%d,MODE_JVQ> + k_slab_sum" % args.k) if ctx.uses_brick_kernels
                      else "gls_cell_kernel<3,%d,%d,%d,MODE_JV>" % (args.k, args.kp, args.k + 1), "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "algorithmic_bytes_per_launch": B_jv, "launch_ms": op_ms,
-                     "launch_ms_by_kernel": {"gls_brick_kernel": jv_launch_ms, "k_slab_sum": slab_launch_ms}},
+                     "launch_ms_by_kernel": {"gls_pencil_kernel" if pencil_jv else "gls_brick_kernel": jv_launch_ms,
+                                             "k_slab_sum": slab_launch_ms}},
         "setup_s": t_setup,
     }
     # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    pencil = os.environ.get("GLS_PENCIL", "1") != "0"
     tr = pmc_traffic(os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE), 4, N_global) \
         if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil) else None
     model_path = os.path.join(ROOT, "profiles", "r04_lds_model.json")

@@ -75,6 +75,12 @@
 #endif
 
 #ifndef GLS_SLAB_INFLIGHT
+#ifndef GLS_SLAB_NT
+#define GLS_SLAB_NT 0  // 1: slab entries read non-temporally (0.55 vs 0.31 ms at 128^3: a slab line serves up to 4 nodes)
+#endif
+#ifndef GLS_SLAB_XCD
+#define GLS_SLAB_XCD 0  // 1: consecutive slab-sum blocks on one XCD (measured no gain, 0.31 vs 0.32 ms)
+#endif
 #define GLS_SLAB_INFLIGHT 1  // k_slab_sum: every slot of a node loaded at once (0.583 -> 0.548 ms at 128^3, profiles/r03_ab_reduce_node.txt)
 #endif
 
@@ -1097,7 +1103,11 @@ struct SlabQuad<double> {
   typedef double d2 __attribute__((ext_vector_type(2)));
   __device__ static void load(const double *p, double &a, double &b, double &c, double &d) {
     const d2 *e = reinterpret_cast<const d2 *>(p);
+#if GLS_SLAB_NT
     const d2 u = __builtin_nontemporal_load(e), v = __builtin_nontemporal_load(e + 1);
+#else
+    const d2 u = e[0], v = e[1];
+#endif
     a = u.x, b = u.y, c = v.x, d = v.y;
   }
 };
@@ -1105,7 +1115,11 @@ template <>
 struct SlabQuad<float> {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __device__ static void load(const float *p, double &a, double &b, double &c, double &d) {
+#if GLS_SLAB_NT
     const f4 u = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
+#else
+    const f4 u = *reinterpret_cast<const f4 *>(p);
+#endif
     a = u.x, b = u.y, c = u.z, d = u.w;
   }
 };
@@ -1115,7 +1129,8 @@ __global__ void k_slab_sum(const S *__restrict__ slab, const int32_t *__restrict
                            int64_t voff, double *__restrict__ y, const uint8_t *__restrict__ vmask,
                            const double *__restrict__ jb, const double *__restrict__ jd, double jomega,
                            const double *__restrict__ rb) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = GLS_SLAB_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int64_t i = (int64_t)blk * blockDim.x + threadIdx.x;
   if (i >= n_sum) return;
   double s[4] = {0., 0., 0., 0.};
 #if GLS_SLAB_INFLIGHT
@@ -1216,9 +1231,14 @@ __global__ void __launch_bounds__(256) k_slab_sum_cube(const S *__restrict__ sla
                                                        double jomega, const double *__restrict__ rb) {
   constexpr int BN = 2 * K + 1, P2 = 2 * K, NBND = BN * BN * BN - (BN - 2) * (BN - 2) * (BN - 2);
   const int NX = P2 * nb1 + 1;
-  const int Z = blockIdx.y;
+  int bx = blockIdx.x, Z = blockIdx.y;
+  if (GLS_SLAB_XCD) {  // XCD-aware: each XCD walks a contiguous range of planes
+    const int lin = xcd_swizzle((int)(blockIdx.x + gridDim.x * blockIdx.y), (int)(gridDim.x * gridDim.y));
+    bx = lin % (int)gridDim.x;
+    Z = lin / (int)gridDim.x;
+  }
   const bool zs = Z % P2 == 0;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = (int64_t)bx * blockDim.x + threadIdx.x;
   // surface nodes of plane Z: all of it when Z is a brick boundary, else the full rows Y % 2K == 0
   // followed by the brick-boundary columns X % 2K == 0 of the other rows
   int X, Y;

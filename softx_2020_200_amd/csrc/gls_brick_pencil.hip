@@ -33,6 +33,12 @@
 #ifndef GLS_PENCIL_WPE64
 #define GLS_PENCIL_WPE64 2  // FP64: ~230 VGPRs -> 2 waves / SIMD (2 workgroups per CU)
 #endif
+#ifndef GLS_PENCIL_PIPE
+#define GLS_PENCIL_PIPE 1  // J.v linearization batches requested one component ahead: bit 0 FP64, bit 1 FP32
+#endif
+#ifndef GLS_PENCIL_NT
+#define GLS_PENCIL_NT 0  // 1: J.v linearization rows read non-temporally (measured slower: 2.61 / 1.36 ms FP64 / FP32 plain vs 2.65 / 1.44 NT)
+#endif
 #ifndef GLS_PENCIL_WPE32
 #define GLS_PENCIL_WPE32 4  // FP32: <= 128 VGPRs -> 4 waves / SIMD
 #endif
@@ -82,7 +88,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Real *const sB = reinterpret_cast<Real *>(smem_raw);            // [3 bricks][NF fields][BN3P]
   Real *const sS = sB + C::BPG * NF * BN3P;                        // [4 waves][6 cells][CS] stage arrays
-  Real *const sO = sS + C::WAVES * C::CPW * C::CS;                 // [24 cells][4 fields][27] cell node values
+  constexpr int CS = C::CS;
+  Real *const sO = sS + C::WAVES * C::CPW * CS;                    // [24 cells][4 fields][27] cell node values
   int *const sNode = reinterpret_cast<int *>(sO + C::CPG * C::NO * C::N3);  // [3][BN3P]
   __shared__ Real sRow[3 * 16];  // V, D, S rows [mat][q][4] for the y sweep's per-lane coefficients
 
@@ -115,9 +122,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   const Real hx = (Real)P.geo[gcell * 4 + 0], hy = (Real)P.geo[gcell * 4 + 1], hz = (Real)P.geo[gcell * 4 + 2];
   const Real ihx = Real(1) / hx, ihy = Real(1) / hy, ihz = Real(1) / hz;
   const Real wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
-  Real *const cellS = sS + (wave * C::CPW + c) * C::CS;
-  // J.v: the lane's linearization rows (issued after the sweeps of each component: loading all 48
-  // values up front was measured slower, it needs ~96 more VGPRs or spills)
+  Real *const cellS = sS + (wave * C::CPW + c) * CS;
+  // J.v: the lane's linearization rows (loaded in batches below)
   const Real *qrow = nullptr;
   if constexpr (!ST) {
     const Real *base = std::is_same<Real, double>::value ? reinterpret_cast<const Real *>(P.qd)
@@ -165,52 +171,58 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
 
   // ---------------- forward sweeps of brick field f into Y registers ([k]: BB, BD, DB, L). kind 0: the
   // value only (BB); 1: value and gradient (BB, BD, DB; pressure); 2: velocity (+ L for the Laplacian)
-  auto forward = [&](int f, int kind, Real (&BB)[3], Real (&BD)[3], Real (&DB)[3], Real (&LL)[3]) {
+  auto xsweep = [&](int f, int kind, int base) {
     const bool grad = kind >= 1, vel = kind == 2;
     // x sweep, lane (a, b) = (y node j, z node k): the brick's x-line of this cell at (j, k)
-    {
-      const Real *F = sB + (bi < 3 ? bi : 0) * NF * BN3P + f * BN3P + 2 * cx + BN * (2 * cy + pa) + BN * BN * (2 * cz + pb);
-      const Real f0 = F[0], f1 = F[1], f2 = F[2];
+    const Real *F = sB + (bi < 3 ? bi : 0) * NF * BN3P + f * BN3P + 2 * cx + BN * (2 * cy + pa) + BN * BN * (2 * cz + pb);
+    const Real f0 = F[0], f1 = F[1], f2 = F[2];
+    Real *const X = cellS + base;
 #pragma unroll
-      for (int qx = 0; qx < 3; ++qx) {
-        const Real xb = T.V[qx][0] * f0 + T.V[qx][1] * f1 + T.V[qx][2] * f2;
-        const Real xd = grad ? T.D[qx][0] * f0 + T.D[qx][1] * f1 + T.D[qx][2] * f2 : Real(0);
-        const int o = qx * C::XS + pa + 3 * pb;  // slab qx, entry (j, k) at j + 3 k
-        const Real xs = vel ? T.S[qx][0] * f0 + T.S[qx][1] * f1 + T.S[qx][2] * f2 : Real(0);
-        if (act) {  // lanes 54..63 mirror lane 0 and store nothing
-          cellS[0 * C::XA + o] = xb;
-          if (grad) cellS[1 * C::XA + o] = xd;
-          if (vel) cellS[2 * C::XA + o] = xs;
-        }
+    for (int qx = 0; qx < 3; ++qx) {
+      const Real xb = T.V[qx][0] * f0 + T.V[qx][1] * f1 + T.V[qx][2] * f2;
+      const Real xd = grad ? T.D[qx][0] * f0 + T.D[qx][1] * f1 + T.D[qx][2] * f2 : Real(0);
+      const int o = qx * C::XS + pa + 3 * pb;  // slab qx, entry (j, k) at j + 3 k
+      const Real xs = vel ? T.S[qx][0] * f0 + T.S[qx][1] * f1 + T.S[qx][2] * f2 : Real(0);
+      if (act) {  // lanes 54..63 mirror lane 0 and store nothing
+        X[0 * C::XA + o] = xb;
+        if (grad) X[1 * C::XA + o] = xd;
+        if (vel) X[2 * C::XA + o] = xs;
       }
     }
+  };
+  // y sweep, lane (a, b) = (qx, qy): slab qx of each X array, all (j, k); the lane's V / D / S rows
+  auto ysweep = [&](int kind, int base, Real (&BB)[3], Real (&BD)[3], Real (&DB)[3], Real (&LL)[3]) {
+    const bool grad = kind >= 1, vel = kind == 2;
+    const Real *rowp = sRow + pb * 4;
+    const Real v0 = rowp[0], v1 = rowp[1], v2 = rowp[2];
+    const Real d0 = rowp[16], d1 = rowp[17], d2 = rowp[18];
+    const Real s0 = rowp[32], s1 = rowp[33], s2 = rowp[34];
+    Real xb[9], xd[9], xs[9];
+    const Real *sl = cellS + base + pa * C::XS;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      xb[e] = sl[e];
+      if (grad) xd[e] = sl[C::XA + e];
+      if (vel) xs[e] = sl[2 * C::XA + e];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const Real b0 = xb[3 * k], b1 = xb[3 * k + 1], b2 = xb[3 * k + 2];
+      BB[k] = v0 * b0 + v1 * b1 + v2 * b2;
+      if (grad) {
+        BD[k] = d0 * b0 + d1 * b1 + d2 * b2;
+        DB[k] = v0 * xd[3 * k] + v1 * xd[3 * k + 1] + v2 * xd[3 * k + 2];
+      }
+      if (vel)
+        LL[k] = wyy * (s0 * b0 + s1 * b1 + s2 * b2) + wxx * (v0 * xs[3 * k] + v1 * xs[3 * k + 1] + v2 * xs[3 * k + 2]);
+    }
+  };
+  // forward sweeps of brick field f into Y registers ([k]: BB, BD, DB, L). kind 0: the value only (BB);
+  // 1: value and gradient (BB, BD, DB; pressure); 2: velocity (+ L for the Laplacian)
+  auto forward = [&](int f, int kind, Real (&BB)[3], Real (&BD)[3], Real (&DB)[3], Real (&LL)[3]) {
+    xsweep(f, kind, 0);
     wave_sync();
-    // y sweep, lane (a, b) = (qx, qy): slab qx of each X array, all (j, k); the lane's V / D / S rows
-    {
-      const Real *rowp = sRow + pb * 4;
-      const Real v0 = rowp[0], v1 = rowp[1], v2 = rowp[2];
-      const Real d0 = rowp[16], d1 = rowp[17], d2 = rowp[18];
-      const Real s0 = rowp[32], s1 = rowp[33], s2 = rowp[34];
-      Real xb[9], xd[9], xs[9];
-      const Real *sl = cellS + pa * C::XS;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) {
-        xb[e] = sl[e];
-        if (grad) xd[e] = sl[C::XA + e];
-        if (vel) xs[e] = sl[2 * C::XA + e];
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const Real b0 = xb[3 * k], b1 = xb[3 * k + 1], b2 = xb[3 * k + 2];
-        BB[k] = v0 * b0 + v1 * b1 + v2 * b2;
-        if (grad) {
-          BD[k] = d0 * b0 + d1 * b1 + d2 * b2;
-          DB[k] = v0 * xd[3 * k] + v1 * xd[3 * k + 1] + v2 * xd[3 * k + 2];
-        }
-        if (vel)
-          LL[k] = wyy * (s0 * b0 + s1 * b1 + s2 * b2) + wxx * (v0 * xs[3 * k] + v1 * xs[3 * k + 1] + v2 * xs[3 * k + 2]);
-      }
-    }
+    ysweep(kind, 0, BB, BD, DB, LL);
     wave_sync();  // the X arrays are rewritten by the next field
   };
 
@@ -229,49 +241,58 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   // backward stages of test field f from its z-transposed sums Z[m][az] (lane (qx, qy)):
   // LDS -> y-transposed (lane (qx, az)) -> LDS -> x-transposed (lane (ay, az)) -> Out
   Real *const outc = sO + cw * C::NO * C::N3;
-  auto backward = [&](int f, const Real (&Z)[3][3]) {
-    Real *Zs = cellS;                    // [m][qx][az][qy]: m * ZA + qx * ZS + 3 az + qy
-    Real *Ws = cellS + 3 * C::ZA;        // [m][az][ay][qx]: m * WA + 3 (ay + 3 az) + qx
+  // Z[m][az] -> Zs at cellS + zb: [m][qx][az][qy] = m * ZA + qx * ZS + 3 az + qy
+  auto bwd_z = [&](const Real (&Z)[3][3], int zb) {
     if (act) {
 #pragma unroll
       for (int m = 0; m < 3; ++m)
 #pragma unroll
-        for (int az = 0; az < 3; ++az) Zs[m * C::ZA + pa * C::ZS + 3 * az + pb] = Z[m][az];
+        for (int az = 0; az < 3; ++az) cellS[zb + m * C::ZA + pa * C::ZS + 3 * az + pb] = Z[m][az];
     }
+  };
+  // lane (a, b) = (qx, az): y-transposed contraction of Zs (at zb) into Ws at wb: [m][az][ay][qx]
+  auto bwd_w = [&](int zb, int wb) {
+    const Real *Zs = cellS + zb;
+    Real *Ws = cellS + wb;
+    Real z[3][3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int qy = 0; qy < 3; ++qy) z[m][qy] = Zs[m * C::ZA + pa * C::ZS + 3 * pb + qy];
+#pragma unroll
+    for (int ay = 0; ay < 3; ++ay) {
+      const Real w0 = T.V[0][ay] * z[0][0] + T.V[1][ay] * z[0][1] + T.V[2][ay] * z[0][2] +
+                      (T.D[0][ay] * z[2][0] + T.D[1][ay] * z[2][1] + T.D[2][ay] * z[2][2]);
+      const Real w1 = T.V[0][ay] * z[1][0] + T.V[1][ay] * z[1][1] + T.V[2][ay] * z[1][2];
+      if (act) {
+        Ws[0 * C::WA + 3 * (ay + 3 * pb) + pa] = w0;
+        Ws[1 * C::WA + 3 * (ay + 3 * pb) + pa] = w1;
+      }
+    }
+  };
+  // lane (a, b) = (ay, az): x-transposed contraction of Ws (at wb) into the cell's node values of field f
+  auto bwd_out = [&](int f, int wb) {
+    const Real *Ws = cellS + wb;
+    Real w0[3], w1[3];
+#pragma unroll
+    for (int qx = 0; qx < 3; ++qx) {
+      w0[qx] = Ws[3 * (pa + 3 * pb) + qx];
+      w1[qx] = Ws[C::WA + 3 * (pa + 3 * pb) + qx];
+    }
+    if (valid) {
+#pragma unroll
+      for (int ax = 0; ax < 3; ++ax)
+        outc[f * C::N3 + 9 * pb + 3 * pa + ax] =
+            T.V[0][ax] * w0[0] + T.V[1][ax] * w0[1] + T.V[2][ax] * w0[2] +
+            (T.D[0][ax] * w1[0] + T.D[1][ax] * w1[1] + T.D[2][ax] * w1[2]);
+    }
+  };
+  auto backward = [&](int f, const Real (&Z)[3][3]) {
+    bwd_z(Z, 0);
     wave_sync();
-    {  // lane (a, b) = (qx, az)
-      Real z[3][3];
-#pragma unroll
-      for (int m = 0; m < 3; ++m)
-#pragma unroll
-        for (int qy = 0; qy < 3; ++qy) z[m][qy] = Zs[m * C::ZA + pa * C::ZS + 3 * pb + qy];
-#pragma unroll
-      for (int ay = 0; ay < 3; ++ay) {
-        const Real w0 = T.V[0][ay] * z[0][0] + T.V[1][ay] * z[0][1] + T.V[2][ay] * z[0][2] +
-                        (T.D[0][ay] * z[2][0] + T.D[1][ay] * z[2][1] + T.D[2][ay] * z[2][2]);
-        const Real w1 = T.V[0][ay] * z[1][0] + T.V[1][ay] * z[1][1] + T.V[2][ay] * z[1][2];
-        if (act) {
-          Ws[0 * C::WA + 3 * (ay + 3 * pb) + pa] = w0;
-          Ws[1 * C::WA + 3 * (ay + 3 * pb) + pa] = w1;
-        }
-      }
-    }
+    bwd_w(0, 3 * C::ZA);
     wave_sync();
-    {  // lane (a, b) = (ay, az)
-      Real w0[3], w1[3];
-#pragma unroll
-      for (int qx = 0; qx < 3; ++qx) {
-        w0[qx] = Ws[3 * (pa + 3 * pb) + qx];
-        w1[qx] = Ws[C::WA + 3 * (pa + 3 * pb) + qx];
-      }
-      if (valid) {
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax)
-          outc[f * C::N3 + 9 * pb + 3 * pa + ax] =
-              T.V[0][ax] * w0[0] + T.V[1][ax] * w0[1] + T.V[2][ax] * w0[2] +
-              (T.D[0][ax] * w1[0] + T.D[1][ax] * w1[1] + T.D[2][ax] * w1[2]);
-      }
-    }
+    bwd_out(f, 3 * C::ZA);
     wave_sync();  // the stage area is rewritten by the next field
   };
 
@@ -489,6 +510,35 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       backward(3, Z);
     }
   } else {
+  // linearization rows of this lane (pencil layout: value v of point qz). Full: u, tau and component 0's
+  // grad u_0, R_0 are requested here, behind the gather's loads (vmcnt retires in order, so a load issued
+  // before the gather would be waited for at the gather), and component cc + 1's batch while component
+  // cc is swept (GLS_PENCIL_PIPE), one batch (12 values) in flight at a time. (Streaming R_s only and
+  // re-deriving u, grad u, tau from a u gather was measured slower: DESIGN §4)
+  auto ld = [&](int qz, int v) {
+#if GLS_PENCIL_NT
+    return __builtin_nontemporal_load(qrow + (qz * kQData + v) * kQdpRow);
+#else
+    return qrow[(qz * kQData + v) * kQdpRow];
+#endif
+  };
+  Real uq[3][3], tauq[3], lnx[3][4];
+#pragma unroll
+  for (int qz = 0; qz < 3; ++qz) {
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) uq[cc][qz] = ld(qz, cc);
+    tauq[qz] = ld(qz, 12);
+  }
+  auto ld_comp = [&](int cc) {
+#pragma unroll
+    for (int qz = 0; qz < 3; ++qz) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) lnx[qz][e] = ld(qz, 3 + 3 * cc + e);
+      lnx[qz][3] = ld(qz, 13 + cc);
+    }
+  };
+  constexpr bool PIPE = (GLS_PENCIL_PIPE & (std::is_same<Real, double>::value ? 1 : 2)) != 0;
+  if (PIPE) ld_comp(0);
   // values of v (all components) and vp, grad vp at the lane's three points: every test field needs
   // them; each velocity component's gradient / Laplacian sweeps run later, next to its test field, so
   // that only one component's Y stage is live at a time
@@ -513,28 +563,22 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     }
   }
 
-  // linearization rows of this lane (pencil layout: value v of point qz), loaded at the start
-  auto ld = [&](int qz, int v) { return __builtin_nontemporal_load(qrow + (qz * kQData + v) * kQdpRow); };
-  Real uq[3][3], tauq[3];
-#pragma unroll
-  for (int qz = 0; qz < 3; ++qz) {
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) uq[cc][qz] = ld(qz, cc);
-    tauq[qz] = ld(qz, 12);
-  }
-
   // ---------------- pointwise + backward, one velocity test field (= trial component) at a time
   Real Sq[3][3], divv[3] = {0, 0, 0};
 #pragma unroll
   for (int cc = 0; cc < 3; ++cc) {
-    Real Yc[4][3];  // this component's Y stage: BB, BD, DB, L
-    forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
     Real gu[3][3], Rq[3];  // grad u_cc (by e) and R_cc at the lane's three points
+    Real Yc[4][3];         // this component's Y stage: BB, BD, DB, L
+    {
+      if (!PIPE) ld_comp(cc);
 #pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
+      for (int qz = 0; qz < 3; ++qz) {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) gu[e][qz] = ld(qz, 3 + 3 * cc + e);
-      Rq[qz] = ld(qz, 13 + cc);
+        for (int e = 0; e < 3; ++e) gu[e][qz] = lnx[qz][e];
+        Rq[qz] = lnx[qz][3];
+      }
+      if (PIPE && cc < 2) ld_comp(cc + 1);
+      forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
     }
     Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
 #pragma unroll

@@ -66,6 +66,16 @@ __global__ void __launch_bounds__(256) k_transfer3d(const double *__restrict__ i
 // so the traffic is 1.6x the single-pass bytes with ~8x fewer loads than the 125-tap gather above.
 // A tile of OX x OY outputs reads the input x range [min first tap, max last tap] over its outputs,
 // <= IXM x IYM (checked on the host when the tables are built).
+#ifndef GLS_XFER_NT
+#define GLS_XFER_NT 1  // input tiles read non-temporally (neighbouring tiles share only their halo)
+#endif
+__device__ __forceinline__ double xfer_load(const double *p) {
+#if GLS_XFER_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 template <int OX, int OY, int IXM, int IYM>
 __global__ void __launch_bounds__(256) k_transfer_xy(const double *__restrict__ in, double *__restrict__ out, int i0,
                                                      int i1, int o0, int o1, int nz, int zb,
@@ -128,9 +138,9 @@ __global__ void __launch_bounds__(256) k_transfer_xy(const double *__restrict__ 
   auto load_plane = [&](int z) {
     const double *pv = in + 3 * (int64_t)z * i1 * i0, *pp = in + 3 * nin + (int64_t)z * i1 * i0;
 #pragma unroll
-    for (int u = 0; u < NV; ++u) rv[u] = offv[u] >= 0 ? __builtin_nontemporal_load(pv + offv[u]) : 0.0;
+    for (int u = 0; u < NV; ++u) rv[u] = offv[u] >= 0 ? xfer_load(pv + offv[u]) : 0.0;
 #pragma unroll
-    for (int u = 0; u < NP; ++u) rp[u] = offp[u] >= 0 ? __builtin_nontemporal_load(pp + offp[u]) : 0.0;
+    for (int u = 0; u < NP; ++u) rp[u] = offp[u] >= 0 ? xfer_load(pp + offp[u]) : 0.0;
   };
   if (z0 < z1) load_plane(z0);
   for (int z = z0; z < z1; ++z) {
