@@ -45,29 +45,43 @@
 
 namespace gls {
 
-template <typename Real>
+template <typename Real, bool JV>
 struct PencilCfg {
   static constexpr int K1 = 3, N3 = 27, BN = 5, BN3 = 125, BN3P = 128, NBND = 98;
   static constexpr int CPW = 6, WAVES = 4, THREADS = 256, CPG = 24, BPG = 3;
   static constexpr bool F64 = sizeof(Real) == 8;
-  // forward X arrays: [qx][k][j] slabs of 9 (+ pad: 16-B aligned slabs), read as one slab per lane
-  static constexpr int XS = F64 ? 10 : 12, XA = 3 * XS;
-  // backward Z arrays: [qx][az][qy] slabs of 9, W arrays [az][ay][qx] (27)
-  static constexpr int ZS = F64 ? 10 : 12, ZA = 3 * ZS, WA = F64 ? 28 : 28;
-  static constexpr int CSF = 3 * XA, CSB = 3 * ZA + 2 * WA;
+  // LDS layout (strides in Reals). The J.v's (JV) are chosen against bank conflicts by
+  // tools/lds_bank_sim.py (the MI355X_MICROARCH.md §LDS lane groups; modelled LDS-array cycles per wave
+  // J.v FP64 2296 -> 1594, FP32 1282 -> 1043, conflict-free 1049 / 601: J.v 2.61 -> 2.53 ms, FP32
+  // 1.37 -> 1.35 ms). The residual / linearization keep the first layout: the model's best within the
+  // 80 KB of 2 workgroups per CU (2554 -> 1828) measured no faster (profiles/r04_ab_lds_layout.txt).
+  // brick arrays: node (X, Y, Z) at X + SY Y + SZ Z, field stride FB
+  static constexpr int SY = 5, SZ = 25, FB = JV ? (F64 ? 131 : 129) : 128;
+  // forward X arrays: [arr * XA + qx * XS + j + 3 k] (slabs 16-B aligned: read as one slab per lane)
+  static constexpr int XS = JV ? (F64 ? 12 : 16) : 10, XA = 3 * XS;
+  // backward Z arrays [m * ZA + qx * ZS + az * ZAZ + qy], W arrays at WB: [m * WA + az * WAZ + 3 ay + qx]
+  static constexpr int ZS = JV ? (F64 ? 12 : 10) : 10, ZAZ = 3, ZA = 3 * ZS, WB = 3 * ZA, WAZ = 9,
+                       WA = 28;
+  static constexpr int CSF = 3 * XA, CSB = WB + 2 * WA;
   static constexpr int CS0 = CSF > CSB ? CSF : CSB;
-  static constexpr int CS = F64 ? CS0 + 4 : CS0 + 4;  // per-cell stage stride (Reals)
-  static constexpr int NO = 4;                          // test fields
+  static constexpr int CS = JV ? (F64 ? 190 : 164) : CS0 + 4;  // per-cell stage stride
+  static constexpr int NO = 4;                                 // test fields
+  static constexpr int OF = 27, OC = JV ? 123 : NO * OF;  // cell node values: [cell * OC + f * OF + 9 az + 3 ay + ax]
+  static_assert(CS >= CS0 && OC >= NO * OF && FB >= 4 * SZ + 4 * SY + 5, "pencil LDS layout");
 };
 
 // brick fields gathered per brick: J.v: v (3) + v_p; residual: u (3), p, the history H = sum_k alpha_k u^(k) (3)
 constexpr int pencil_fields(int mode) { return mode == MODE_JVQ ? 4 : 7; }
+template <typename Real, bool JV>
+size_t pencil_lds_bytes_t(int mode) {
+  using C = PencilCfg<Real, JV>;
+  return sizeof(Real) * ((size_t)C::BPG * pencil_fields(mode) * C::FB + (size_t)C::WAVES * C::CPW * C::CS +
+                         (size_t)C::CPG * C::OC) +
+         sizeof(int) * (size_t)C::BPG * C::BN3P;
+}
 template <typename Real>
 size_t pencil_lds_bytes(int mode) {
-  using C = PencilCfg<Real>;
-  return sizeof(Real) * ((size_t)C::BPG * pencil_fields(mode) * C::BN3P + (size_t)C::WAVES * C::CPW * C::CS +
-                         (size_t)C::CPG * C::NO * C::N3) +
-         sizeof(int) * (size_t)C::BPG * C::BN3P;
+  return mode == MODE_JVQ ? pencil_lds_bytes_t<Real, true>(mode) : pencil_lds_bytes_t<Real, false>(mode);
 }
 
 // the Q2 1D tables in the kernel's precision (kernel argument -> scalar registers): [q][node]
@@ -81,16 +95,17 @@ struct PencilTab {
 template <typename Real, int MODE, bool GEN>
 __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
     gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
-  using C = PencilCfg<Real>;
+  using C = PencilCfg<Real, MODE == MODE_JVQ>;
   constexpr bool RES = MODE == MODE_RESIDUAL, LIN = MODE == MODE_LIN;  // else MODE_JVQ
   constexpr bool ST = RES || LIN;  // state sweeps (u, p, H) instead of the cached linearization
   constexpr int BN = C::BN, BN3 = C::BN3, BN3P = C::BN3P, NF = pencil_fields(MODE);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  Real *const sB = reinterpret_cast<Real *>(smem_raw);            // [3 bricks][NF fields][BN3P]
-  Real *const sS = sB + C::BPG * NF * BN3P;                        // [4 waves][6 cells][CS] stage arrays
+  constexpr int FB = C::FB, SY = C::SY, SZ = C::SZ;
+  Real *const sB = reinterpret_cast<Real *>(smem_raw);            // [3 bricks][NF fields][FB]
+  Real *const sS = sB + C::BPG * NF * FB;                          // [4 waves][6 cells][CS] stage arrays
   constexpr int CS = C::CS;
-  Real *const sO = sS + C::WAVES * C::CPW * CS;                    // [24 cells][4 fields][27] cell node values
-  int *const sNode = reinterpret_cast<int *>(sO + C::CPG * C::NO * C::N3);  // [3][BN3P]
+  Real *const sO = sS + C::WAVES * C::CPW * CS;                    // [24 cells][OC] cell node values
+  int *const sNode = reinterpret_cast<int *>(sO + C::CPG * C::OC);  // [3][BN3P]
   __shared__ Real sRow[3 * 16];  // V, D, S rows [mat][q][4] for the y sweep's per-lane coefficients
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -140,7 +155,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     const int a = (X - 2 * cx) + 3 * ((Y - 2 * cy) + 3 * (Z - 2 * cz));
     const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * 27 + a];
     const int64_t i3 = (int64_t)node * 3;
-    Real *b = sB + bi * NF * BN3P + n;
+    Real *b = sB + bi * NF * FB + X + SY * Y + SZ * Z;
     if constexpr (ST) {
       double h[3] = {0., 0., 0.};
 #pragma unroll
@@ -150,19 +165,19 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
         if (P.n_hist > 2) h[cc] += P.alpha[3] * P.h3[i3 + cc];
       }
       b[0] = (Real)P.u[i3];
-      b[BN3P] = (Real)P.u[i3 + 1];
-      b[2 * BN3P] = (Real)P.u[i3 + 2];
-      b[3 * BN3P] = (Real)P.u[voff + node];
-      b[4 * BN3P] = (Real)h[0];
-      b[5 * BN3P] = (Real)h[1];
-      b[6 * BN3P] = (Real)h[2];
+      b[FB] = (Real)P.u[i3 + 1];
+      b[2 * FB] = (Real)P.u[i3 + 2];
+      b[3 * FB] = (Real)P.u[voff + node];
+      b[4 * FB] = (Real)h[0];
+      b[5 * FB] = (Real)h[1];
+      b[6 * FB] = (Real)h[2];
     } else {
       const double v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
       b[0] = (m & 1u) ? Real(0) : (Real)v0;
-      b[BN3P] = (m & 2u) ? Real(0) : (Real)v1;
-      b[2 * BN3P] = (m & 4u) ? Real(0) : (Real)v2;
-      b[3 * BN3P] = (Real)vp;
+      b[FB] = (m & 2u) ? Real(0) : (Real)v1;
+      b[2 * FB] = (m & 4u) ? Real(0) : (Real)v2;
+      b[3 * FB] = (Real)vp;
     }
     sNode[bi * BN3P + n] = node;
   }
@@ -174,7 +189,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   auto xsweep = [&](int f, int kind, int base) {
     const bool grad = kind >= 1, vel = kind == 2;
     // x sweep, lane (a, b) = (y node j, z node k): the brick's x-line of this cell at (j, k)
-    const Real *F = sB + (bi < 3 ? bi : 0) * NF * BN3P + f * BN3P + 2 * cx + BN * (2 * cy + pa) + BN * BN * (2 * cz + pb);
+    const Real *F = sB + (bi < 3 ? bi : 0) * NF * FB + f * FB + 2 * cx + SY * (2 * cy + pa) + SZ * (2 * cz + pb);
     const Real f0 = F[0], f1 = F[1], f2 = F[2];
     Real *const X = cellS + base;
 #pragma unroll
@@ -240,14 +255,14 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
 
   // backward stages of test field f from its z-transposed sums Z[m][az] (lane (qx, qy)):
   // LDS -> y-transposed (lane (qx, az)) -> LDS -> x-transposed (lane (ay, az)) -> Out
-  Real *const outc = sO + cw * C::NO * C::N3;
+  Real *const outc = sO + cw * C::OC;
   // Z[m][az] -> Zs at cellS + zb: [m][qx][az][qy] = m * ZA + qx * ZS + 3 az + qy
   auto bwd_z = [&](const Real (&Z)[3][3], int zb) {
     if (act) {
 #pragma unroll
       for (int m = 0; m < 3; ++m)
 #pragma unroll
-        for (int az = 0; az < 3; ++az) cellS[zb + m * C::ZA + pa * C::ZS + 3 * az + pb] = Z[m][az];
+        for (int az = 0; az < 3; ++az) cellS[zb + m * C::ZA + pa * C::ZS + C::ZAZ * az + pb] = Z[m][az];
     }
   };
   // lane (a, b) = (qx, az): y-transposed contraction of Zs (at zb) into Ws at wb: [m][az][ay][qx]
@@ -258,15 +273,15 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
 #pragma unroll
     for (int m = 0; m < 3; ++m)
 #pragma unroll
-      for (int qy = 0; qy < 3; ++qy) z[m][qy] = Zs[m * C::ZA + pa * C::ZS + 3 * pb + qy];
+      for (int qy = 0; qy < 3; ++qy) z[m][qy] = Zs[m * C::ZA + pa * C::ZS + C::ZAZ * pb + qy];
 #pragma unroll
     for (int ay = 0; ay < 3; ++ay) {
       const Real w0 = T.V[0][ay] * z[0][0] + T.V[1][ay] * z[0][1] + T.V[2][ay] * z[0][2] +
                       (T.D[0][ay] * z[2][0] + T.D[1][ay] * z[2][1] + T.D[2][ay] * z[2][2]);
       const Real w1 = T.V[0][ay] * z[1][0] + T.V[1][ay] * z[1][1] + T.V[2][ay] * z[1][2];
       if (act) {
-        Ws[0 * C::WA + 3 * (ay + 3 * pb) + pa] = w0;
-        Ws[1 * C::WA + 3 * (ay + 3 * pb) + pa] = w1;
+        Ws[0 * C::WA + C::WAZ * pb + 3 * ay + pa] = w0;
+        Ws[1 * C::WA + C::WAZ * pb + 3 * ay + pa] = w1;
       }
     }
   };
@@ -276,13 +291,13 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     Real w0[3], w1[3];
 #pragma unroll
     for (int qx = 0; qx < 3; ++qx) {
-      w0[qx] = Ws[3 * (pa + 3 * pb) + qx];
-      w1[qx] = Ws[C::WA + 3 * (pa + 3 * pb) + qx];
+      w0[qx] = Ws[C::WAZ * pb + 3 * pa + qx];
+      w1[qx] = Ws[C::WA + C::WAZ * pb + 3 * pa + qx];
     }
     if (valid) {
 #pragma unroll
       for (int ax = 0; ax < 3; ++ax)
-        outc[f * C::N3 + 9 * pb + 3 * pa + ax] =
+        outc[f * C::OF + 9 * pb + 3 * pa + ax] =
             T.V[0][ax] * w0[0] + T.V[1][ax] * w0[1] + T.V[2][ax] * w0[2] +
             (T.D[0][ax] * w1[0] + T.D[1][ax] * w1[1] + T.D[2][ax] * w1[2]);
     }
@@ -290,9 +305,9 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   auto backward = [&](int f, const Real (&Z)[3][3]) {
     bwd_z(Z, 0);
     wave_sync();
-    bwd_w(0, 3 * C::ZA);
+    bwd_w(0, C::WB);
     wave_sync();
-    bwd_out(f, 3 * C::ZA);
+    bwd_out(f, C::WB);
     wave_sync();  // the stage area is rewritten by the next field
   };
 
@@ -488,8 +503,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
           const unsigned msk = P.vmask ? P.vmask[sNode[bi * BN3P + bn]] : 0u;
 #pragma unroll
           for (int c3 = 0; c3 < 3; ++c3)
-            outc[c3 * C::N3 + 9 * iz + 3 * pb + pa] = (msk >> c3) & 1u ? fabs(acc[iz][c3]) : acc[iz][c3];
-          outc[3 * C::N3 + 9 * iz + 3 * pb + pa] = acc[iz][3];
+            outc[c3 * C::OF + 9 * iz + 3 * pb + pa] = (msk >> c3) & 1u ? fabs(acc[iz][c3]) : acc[iz][c3];
+          outc[3 * C::OF + 9 * iz + 3 * pb + pa] = acc[iz][3];
         }
       }
     }
@@ -653,9 +668,9 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
         for (int kx = 0; kx < 2; ++kx) {
           const int ax = Xn - 2 * kx;
           if (ax < 0 || ax > 2) continue;
-          const Real *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::NO * C::N3 + ax + 3 * (ay + 3 * az);
+          const Real *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::OC + ax + 3 * (ay + 3 * az);
 #pragma unroll
-          for (int f = 0; f < 4; ++f) s[f] += o[f * C::N3];
+          for (int f = 0; f < 4; ++f) s[f] += o[f * C::OF];
         }
       }
     }
