@@ -1416,6 +1416,7 @@ struct Solver {
     r.px.assign(R.pnode_x, R.pnode_x + r.np * dim);
     load_hanging(r, R.n_vhang, R.vhang_node, R.vhang_off, R.vhang_master, R.vhang_w, R.n_phang, R.phang_node,
                  R.phang_off, R.phang_master, R.phang_w);
+    r.pmask = m.pmask;  // periodic faces identified by the forest mesh
     m = std::move(r);
     C = make_constraints(P, m, time);
     ctx = make_context(m, C);
@@ -2164,7 +2165,6 @@ struct Solver {
       return;
     }
     need_host();
-    if (m.pmask) die("kelly mesh adaptation: periodic boundaries are not supported");
     const int dim = P.dim;
     const int64_t nc = m.nc;
     upload(present, d_present);
@@ -2187,14 +2187,27 @@ struct Solver {
     download(d_eta, eta);
     (void)hipFree(d_eta);
     const int64_t n_uniform = (int64_t)1 << P.refinement;
+    gls_refined_mesh *um = nullptr;  // periodic: the uniform mesh as the forest numbers it (SolutionTransfer source)
     if (!tree) {  // GridGenerator::hyper_cube + refine_global(initial refinement)
       if (rmesh) die("kelly mesh adaptation: internal error (adapted mesh without a forest)");
       ck(gls_octree_create(dim, 1, &tree), "gls_octree_create");
+      ck(gls_octree_set_periodic(tree, m.pmask), "gls_octree_set_periodic");  // add_periodicity
       for (int r = 0; r < P.refinement; ++r) {
         int64_t nl = 0;
         ck(gls_octree_info(tree, &nl, nullptr), "gls_octree_info");
         std::vector<int32_t> all((size_t)nl, 1), none((size_t)nl, 0);
         ck(gls_octree_adapt(tree, all.data(), none.data(), 1 << 20, 0), "gls_octree_adapt");
+      }
+      if (m.pmask) {  // the wrapped uniform lattice in lexicographic order is the forest mesh's numbering
+        ck(gls_octree_mesh(tree, P.k, P.kp, P.lo, P.hi, &um), "gls_octree_mesh");
+        bool same = um->n_vnodes == m.nv && um->n_pnodes == m.np;
+        for (int64_t v = 0; same && v < m.nv; ++v) {
+          double x[3];
+          int idx[3];
+          m.coord(v, true, x, idx);
+          for (int d = 0; d < dim; ++d) same = same && std::fabs(x[d] - um->vnode_x[v * dim + d]) < 1e-12 * (P.hi - P.lo);
+        }
+        if (!same) die("kelly mesh adaptation: periodic uniform mesh and forest numbering disagree");
       }
     }
     int64_t nl = 0;
@@ -2261,6 +2274,9 @@ struct Solver {
     if (old_rm) {
       ck(gls_octree_transfer(old_rm, rmesh, sol.data(), present.data()), "gls_octree_transfer");
       gls_octree_mesh_destroy(old_rm);
+    } else if (um) {
+      ck(gls_octree_transfer(um, rmesh, sol.data(), present.data()), "gls_octree_transfer");
+      gls_octree_mesh_destroy(um);
     } else {
       ck(gls_mesh_refined_interpolate(rmesh, (int)n_uniform, P.lo, P.hi, sol.data(), present.data()),
          "gls_mesh_refined_interpolate");

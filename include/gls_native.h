@@ -140,6 +140,13 @@ int gls_set_hanging(gls_ctx *ctx, int64_t n_lines, const int64_t *dofs, const in
 /* Diagonal of that assembled Jacobian (DEVICE pointer). */
 int gls_jacobian_diagonal(gls_ctx *ctx, double *diag);
 
+/* assemble_matrix_and_rhs (gls_navier_stokes.cc:917-1000, assembleGLS<true>: the matrix and the rhs in
+ * one pass over the cells): the residual into rhs (as gls_residual) and the Jacobian's diagonal (as
+ * gls_jacobian_diagonal; diag may be NULL) at the current state, with the J.v linearization cached.
+ * On the 3D Q2 brick path one fused launch computes all three; the values equal those of the separate
+ * calls bitwise. DEVICE pointers. */
+int gls_residual_and_diagonal(gls_ctx *ctx, double *rhs, double *diag);
+
 /* Apply nonzero_constraints.distribute to a DEVICE vector: x[dof] = value for listed DoFs
  * (PhysicsSolver::apply_constraints, physics_solver.h:98-102). Host arrays, copied. */
 int gls_set_dirichlet(gls_ctx *ctx, int64_t n, const int64_t *dofs, const double *values);
@@ -456,6 +463,11 @@ int gls_mesh_refined_destroy(gls_refined_mesh *mesh);
 typedef struct gls_octree gls_octree;
 int gls_octree_create(int dim, int n, gls_octree **out);
 void gls_octree_destroy(gls_octree *tree);
+/* Periodic directions (bit d of mask; before adapting): the balance, the smoothing's neighbourhoods and
+ * the Kelly faces wrap around them, and gls_octree_mesh identifies the max face's nodes with the min
+ * face's, hanging lines included (periodicity under local refinement, gls_navier_stokes.cc:130-134,
+ * 164-168: make_periodicity_constraints closed together with the hanging-node constraints). */
+int gls_octree_set_periodic(gls_octree *tree, int mask);
 int gls_octree_info(const gls_octree *tree, int64_t *n_cells, int *max_level);
 int gls_octree_cells(const gls_octree *tree, int32_t *level, double *x0, double *h, double lo, double hi);
 int gls_octree_adapt(gls_octree *tree, const int32_t *refine, const int32_t *coarsen, int max_level, int min_level);

@@ -196,6 +196,8 @@ class StructuredProblem:
         tol = 1e-12 * (self.hi - self.lo)
         ids = [set() for _ in range(X.shape[0])]
         for d in range(self.dim):
+            if d in getattr(self, "periodic", ()):  # identified faces carry no boundary id
+                continue
             lo_ = np.nonzero(np.abs(X[:, d] - self.lo) < tol)[0]
             hi_ = np.nonzero(np.abs(X[:, d] - self.hi) < tol)[0]
             for i in lo_:

@@ -319,6 +319,7 @@ struct gls_ctx {
   // surface nodes into a slab; k_slab_sum adds a node's slots in a fixed order (CSR node -> slots)
   bool use_slab = false;
   DevBuf<double> slab;
+  DevBuf<double> slab2;  // the fused residual + linearization pass: the residual's brick-surface slab
   DevBuf<int32_t> sum_nodes, sum_off, sum_slots;
   int cube_nb1 = 0;  // > 0: the mesh is the structured hyper_cube with cube_nb1 bricks per direction
                      // (k_slab_sum_cube computes the slab slots from the lattice; GLS_SLAB_CSR=1: off)
@@ -1007,9 +1008,11 @@ int ensure_qdata(gls_ctx *c) {
 
 // the slab node sums with an FP32 slab and / or the fused damped-Jacobi sweep / residual form
 hipError_t slab_sum_ex(gls_ctx *g, const double *slab, const float *slabf, double *y, const uint8_t *vmask,
-                       const double *jb, const double *jd, double omega, const double *rb) {
+                       const double *jb, const double *jd, double omega, const double *rb, double *x0 = nullptr) {
   if (g->cube_nb1 > 0)
-    return gls::brick_slab_sum_cube(g->k, g->cube_nb1, slab, slabf, g->n_vnodes, y, vmask, jb, jd, omega, g->stream, rb);
+    return gls::brick_slab_sum_cube(g->k, g->cube_nb1, slab, slabf, g->n_vnodes, y, vmask, jb, jd, omega, g->stream, rb,
+                                    x0);
+  if (x0) return hipErrorInvalidValue;
   return gls::brick_slab_sum_ex(slab, slabf, g->sum_nodes.p, g->sum_off.p, g->sum_slots.p, (int64_t)g->sum_nodes.n,
                                 g->n_vnodes, y, vmask, jb, jd, omega, g->stream, rb);
 }
@@ -1640,6 +1643,59 @@ int gls_residual(gls_ctx *c, double *rhs) {
   return GLS_OK;
 }
 
+// assemble_matrix_and_rhs (gls_navier_stokes.cc:917-1000: assembleGLS<true>, the matrix and the rhs in
+// one cell loop): on
+// the Q2 brick path one pencil launch (MODE_RESLIN) computes the residual, the J.v linearization and
+// the Jacobian diagonal at the current state (the residual's and the diagonal's node sums are bitwise
+// those of the separate launches); elsewhere -- and with a frozen Jacobian, hanging nodes, colored or
+// distributed launches, GLS_NO_RESLIN=1 -- the residual and the diagonal separately
+int gls_residual_and_diagonal(gls_ctx *c, double *rhs, double *d) {
+  GLS_TRY(check_ctx(c));
+  if (!rhs) return set_err(GLS_EINVAL, "rhs is null");
+  if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
+  if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
+  if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
+  if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
+  const bool fuse = !c->diag_valid && c->use_brick && c->use_qdata && c->use_slab && !c->use_colors && !c->hang.on &&
+                    !c->dist.on && !c->jf.on && c->k == 2 && c->cube_nb1 > 0 && gls::pencil_enabled() &&
+                    std::getenv("GLS_NO_RESLIN") == nullptr;
+  if (fuse) {
+    const size_t nq = gls::brick_qdata_size(c->k, c->n_cells);
+    if (c->qdata.n != nq) GLS_TRY(c->qdata.alloc(nq));
+    double *slab = brick_slab(c);
+    if (!slab) return set_err(GLS_ENOMEM, "slab allocation failed");
+    if (c->slab2.n != c->slab.n) GLS_TRY(c->slab2.alloc(c->slab.n));
+    gls::OpParams P = make_params(c, true);
+    P.qd = c->qdata.p;
+    GLS_TRY(lin_f32_target(c, P));
+    P.y = c->diag.p;
+    P.slab = slab;
+    P.res_y = rhs;
+    P.res_slab = c->slab2.p;
+    {
+      TimedLaunch t(c, gls::MODE_DIAG);
+      HIP_TRY(gls::launch_pencil_reslin(P, c->tables, c->stream));
+    }
+    {
+      TimedLaunch t(c, 5);
+      HIP_TRY(slab_sum_ex(c, c->slab2.p, nullptr, rhs, nullptr, nullptr, nullptr, 0.0, nullptr));
+    }
+    {
+      TimedLaunch t(c, 5);
+      HIP_TRY(slab_sum(c, c->diag.p));
+    }
+    HIP_TRY(gls::vec_set_indexed(rhs, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, c->stream));
+    c->qd_valid = true;
+    c->qd32_valid = P.qdf != nullptr;
+    c->diag_valid = true;
+  } else {
+    GLS_TRY(gls_residual(c, rhs));
+    GLS_TRY(ensure_diag(c));
+  }
+  if (d && d != c->diag.p) HIP_TRY(gls::vec_copy(d, c->diag.p, c->n_dofs, c->stream));
+  return GLS_OK;
+}
+
 int gls_jacobian_diagonal(gls_ctx *c, double *d) {
   GLS_TRY(check_ctx(c));
   GLS_TRY(ensure_diag(c));
@@ -1671,8 +1727,16 @@ int ensure_qdata32(gls_ctx *g) {
 }
 // FP32 kernels write their brick-surface partial sums in FP32 (half the slab traffic; summed in FP64)
 bool slab_f32() { return std::getenv("GLS_SLAB_F64") == nullptr; }
-// rb != nullptr: y = rb - A v (the V-cycle's residual), fused into the kernels' stores on one rank
-int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr) {
+// rb != nullptr: y = rb - A v (the V-cycle's residual), fused into the kernels' stores on one rank.
+// first_omega > 0 (only where first_sweep_fusable): v is not read but formed as the first damped-Jacobi
+// sweep from 0, v = 0 + first_omega rb / D (mg_jacobi_update's arithmetic), in the J.v's gather and
+// stored to v by the J.v (brick-interior nodes) and the slab sum (surface nodes)
+bool first_sweep_fusable(gls_ctx *g) {
+  return g->smooth_f32 && g->use_brick && g->use_qdata && !g->use_colors && !g->dist.on && !g->hang.on && g->k == 2 &&
+         g->cube_nb1 > 0 && g->use_slab && gls::pencil_enabled() && std::getenv("GLS_MG_NO_FUSE") == nullptr &&
+         std::getenv("GLS_MG_NO_FIRST_FUSE") == nullptr;
+}
+int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr, double first_omega = 0.0) {
   if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   GLS_TRY(ensure_diag(g));
   GLS_TRY(ensure_qdata32(g));
@@ -1688,6 +1752,12 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
   P.rb = fuse_rb ? rb : nullptr;
   P.slabf = P.slab && slab_f32() && gls::brick_fused_jacobi_supported(g->k) ? reinterpret_cast<float *>(P.slab)
                                                                              : nullptr;
+  if (first_omega > 0.0) {
+    if (!fuse_rb || !first_sweep_fusable(g)) return set_err(GLS_EINVAL, "fused first sweep not applicable");
+    P.jx0 = const_cast<double *>(v);
+    P.jd = g->diag.p;
+    P.jomega = first_omega;
+  }
   if (col) set_colors(g, P, y);
   if (!col && !P.slab) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * g->n_dofs, g->stream));
   {
@@ -1696,7 +1766,7 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
   }
   if (P.slab) {
     TimedLaunch t(g, 5);
-    HIP_TRY(slab_sum_ex(g, P.slab, P.slabf, y, nullptr, nullptr, nullptr, 0.0, P.rb));
+    HIP_TRY(slab_sum_ex(g, P.slab, P.slabf, y, nullptr, nullptr, P.jx0 ? g->diag.p : nullptr, P.jomega, P.rb, P.jx0));
   }
   GLS_TRY(dist_export_add(g, y));
   HIP_TRY(gls::vec_gather_scale_set(y, g->diag.p, v, g->con_dofs.p, (int64_t)g->con_dofs.n, g->stream, P.rb));
@@ -2233,15 +2303,19 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
       return GLS_OK;
     }
   }
-  if (pre > 0) {
+  // one pre-sweep from 0 on a fused level: x = omega D^-1 b is formed inside the residual's J.v
+  const bool first_fused = pre == 1 && l < L - 1 && first_sweep_fusable(g);
+  if (pre > 0 && !first_fused) {
     HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
     for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
-  } else {
+  } else if (pre == 0) {
     HIP_TRY(gls::vec_fill(x, n, 0.0, s));
   }
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
-  if (pre > 0) {
+  if (first_fused) {
+    GLS_TRY(jacobian_apply_f32(g, x, y, b, om));  // x = omega D^-1 b, y = b - A x
+  } else if (pre > 0) {
     GLS_TRY(smoother_apply(g, x, y, b));  // y = b - A x
   } else {
     HIP_TRY(gls::vec_copy(y, b, n, s));  // x = 0: the residual is b
@@ -3331,8 +3405,7 @@ struct DevicePhysics {
       GLS_TRY(gls_freeze_jacobian(c, 0));
       GLS_TRY(gls_set_state(c, eval, u1, u2, u3));
     }
-    GLS_TRY(gls_residual(c, rhs));
-    GLS_TRY(ensure_diag(c));
+    GLS_TRY(gls_residual_and_diagonal(c, rhs, nullptr));
     return skip ? gls_freeze_jacobian(c, 1) : GLS_OK;
   }
   int assemble_rhs() {

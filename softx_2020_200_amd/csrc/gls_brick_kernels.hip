@@ -1228,7 +1228,8 @@ template <typename S, bool J, int K>
 __global__ void __launch_bounds__(256) k_slab_sum_cube(const S *__restrict__ slab, int nb1, int64_t voff,
                                                        double *__restrict__ y, const uint8_t *__restrict__ vmask,
                                                        const double *__restrict__ jb, const double *__restrict__ jd,
-                                                       double jomega, const double *__restrict__ rb) {
+                                                       double jomega, const double *__restrict__ rb,
+                                                       double *__restrict__ x0) {
   constexpr int BN = 2 * K + 1, P2 = 2 * K, NBND = BN * BN * BN - (BN - 2) * (BN - 2) * (BN - 2);
   const int NX = P2 * nb1 + 1;
   int bx = blockIdx.x, Z = blockIdx.y;
@@ -1331,6 +1332,10 @@ __global__ void __launch_bounds__(256) k_slab_sum_cube(const S *__restrict__ sla
   } else if (rb) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) y[gi[f]] = rb[gi[f]] - s[f];
+    if (x0) {  // the fused first Jacobi sweep's x at this surface node (pencil J.v, OpParams::jx0)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) x0[gi[f]] = 0.0 + jomega * rb[gi[f]] / jd[gi[f]];
+    }
   } else {
 #pragma unroll
     for (int f = 0; f < 4; ++f) y[gi[f]] = s[f];
@@ -1339,18 +1344,19 @@ __global__ void __launch_bounds__(256) k_slab_sum_cube(const S *__restrict__ sla
 // nb1 > 0: the structured form (nb1 bricks per direction) instead of the node / offset / slot map
 hipError_t brick_slab_sum_cube(int k, int nb1, const double *slab, const float *slabf, int64_t n_vnodes, double *y,
                                const uint8_t *vmask, const double *jb, const double *jd, double jomega, hipStream_t s,
-                               const double *rb) {
+                               const double *rb, double *x0) {
   if (nb1 <= 0 || (k != 1 && k != 2)) return hipErrorInvalidValue;
+  if (x0 && (!rb || !jd || jb)) return hipErrorInvalidValue;
   const int NX = 2 * k * nb1 + 1;
   const dim3 g((unsigned)(((int64_t)NX * NX + 255) / 256), (unsigned)NX), b(256);
   const int64_t voff = 3 * n_vnodes;
 #define GLS_SLAB_CUBE(KK)                                                                                                   \
   if (slabf) {                                                                                                              \
-    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<float, true, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb);  \
-    else hipLaunchKernelGGL((k_slab_sum_cube<float, false, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb);   \
+    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<float, true, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb, x0);  \
+    else hipLaunchKernelGGL((k_slab_sum_cube<float, false, KK>), g, b, 0, s, slabf, nb1, voff, y, vmask, jb, jd, jomega, rb, x0);   \
   } else {                                                                                                                  \
-    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<double, true, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb); \
-    else hipLaunchKernelGGL((k_slab_sum_cube<double, false, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb);  \
+    if (jb) hipLaunchKernelGGL((k_slab_sum_cube<double, true, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb, x0); \
+    else hipLaunchKernelGGL((k_slab_sum_cube<double, false, KK>), g, b, 0, s, slab, nb1, voff, y, vmask, jb, jd, jomega, rb, x0);  \
   }
   if (k == 1) {
     GLS_SLAB_CUBE(1)

@@ -96,7 +96,8 @@ template <typename Real, int MODE, bool GEN>
 __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
     gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
   using C = PencilCfg<Real, MODE == MODE_JVQ>;
-  constexpr bool RES = MODE == MODE_RESIDUAL, LIN = MODE == MODE_LIN;  // else MODE_JVQ
+  // MODE_RESLIN = MODE_RESIDUAL + MODE_LIN at one state (assemble_matrix_and_rhs); else MODE_JVQ
+  constexpr bool RL = MODE == MODE_RESLIN, RES = MODE == MODE_RESIDUAL || RL, LIN = MODE == MODE_LIN || RL;
   constexpr bool ST = RES || LIN;  // state sweeps (u, p, H) instead of the cached linearization
   constexpr int BN = C::BN, BN3 = C::BN3, BN3P = C::BN3P, NF = pencil_fields(MODE);
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -172,7 +173,15 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       b[5 * FB] = (Real)h[1];
       b[6 * FB] = (Real)h[2];
     } else {
-      const double v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
+      double v0, v1, v2, vp;
+      if (P.jx0) {  // the first Jacobi sweep from 0: v = 0 + omega b / d (mg_jacobi_update's arithmetic)
+        v0 = 0.0 + P.jomega * P.rb[i3] / P.jd[i3];
+        v1 = 0.0 + P.jomega * P.rb[i3 + 1] / P.jd[i3 + 1];
+        v2 = 0.0 + P.jomega * P.rb[i3 + 2] / P.jd[i3 + 2];
+        vp = 0.0 + P.jomega * P.rb[voff + node] / P.jd[voff + node];
+      } else {
+        v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
+      }
       const unsigned m = P.vmask ? P.vmask[node] : 0u;
       b[0] = (m & 1u) ? Real(0) : (Real)v0;
       b[FB] = (m & 2u) ? Real(0) : (Real)v1;
@@ -311,6 +320,70 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     wave_sync();  // the stage area is rewritten by the next field
   };
 
+  // ---------------- brick reduction (fixed cell order per node) + scatter: one thread per brick node;
+  // fused: the launch's damped-Jacobi / residual-form / FP32-slab options apply
+  auto reduce_scatter = [&](double *yo, double *slo, bool fused) {
+    for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
+      const int rb_ = t / BN3, n = t % BN3;
+      if (rb_ >= nbg) break;
+      const int bk = brick_of(rb_);
+      const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
+      Real s[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int kz = 0; kz < 2; ++kz) {
+        const int az = Zn - 2 * kz;
+        if (az < 0 || az > 2) continue;
+#pragma unroll
+        for (int ky = 0; ky < 2; ++ky) {
+          const int ay = Yn - 2 * ky;
+          if (ay < 0 || ay > 2) continue;
+#pragma unroll
+          for (int kx = 0; kx < 2; ++kx) {
+            const int ax = Xn - 2 * kx;
+            if (ax < 0 || ax > 2) continue;
+            const Real *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::OC + ax + 3 * (ay + 3 * az);
+#pragma unroll
+            for (int f = 0; f < 4; ++f) s[f] += o[f * C::OF];
+          }
+        }
+      }
+      const int node = sNode[rb_ * BN3P + n];
+      const int64_t gi[4] = {(int64_t)node * 3, (int64_t)node * 3 + 1, (int64_t)node * 3 + 2, voff + node};
+      const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
+      if (interior) {
+        if (fused && P.jx) {  // fused damped-Jacobi sweep (interior nodes: no other brick reads this x)
+          const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            const bool con = f < 3 && ((m >> f) & 1u);
+            const double x = P.jx[gi[f]], dd = P.jd[gi[f]];
+            P.jx[gi[f]] = x + P.jomega * (P.jb[gi[f]] - (con ? dd * x : (double)s[f])) / dd;
+          }
+        } else if (fused && P.rb) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) yo[gi[f]] = P.rb[gi[f]] - (double)s[f];
+          if (P.jx0) {
+#pragma unroll
+            for (int f = 0; f < 4; ++f) P.jx0[gi[f]] = 0.0 + P.jomega * P.rb[gi[f]] / P.jd[gi[f]];
+          }
+        } else {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) yo[gi[f]] = s[f];
+        }
+      } else {  // this brick's partial sums of a brick-boundary node (summed per node by k_slab_sum)
+        const int64_t si = ((int64_t)bk * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4;
+        if (fused && std::is_same<Real, float>::value && P.slabf) {
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<f4 *>(P.slabf + si) = f4{(float)s[0], (float)s[1], (float)s[2], (float)s[3]};
+        } else {
+          typedef double d2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<d2 *>(slo + si) = d2{(double)s[0], (double)s[1]};
+          *reinterpret_cast<d2 *>(slo + si + 2) = d2{(double)s[2], (double)s[3]};
+        }
+      }
+    }
+  };
+
   if constexpr (ST) {
     // ---------------- residual (assemble_rhs, gls_navier_stokes.cc:391-516) / linearization (MODE_LIN:
     // u, grad u, tau, R_s per point into the pencil rows, then the Jacobian diagonal): values of u, H
@@ -409,7 +482,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
           st_lin(qz, 3 + 3 * cc + 2, g2);
           st_lin(qz, 13 + cc, R);
           gcq[cc][qz] = (cc == 0 ? g0 : cc == 1 ? g1 : g2) + aj;
-          continue;
+          if constexpr (!RES) continue;
         }
         const Real JxW = wxy * T.w[qz], tau = tauq[qz];
         const Real gg[3] = {g0, g1, g2}, uu[3] = {u0, u1, u2};
@@ -426,6 +499,27 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
         }
       }
       if constexpr (RES) backward(cc, Z);
+    }
+    if constexpr (RES) {  // pressure test field: -JxW div u, -JxW tau R_e / h_e
+      Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+      for (int qz = 0; qz < 3; ++qz) {
+        const Real JxW = wxy * T.w[qz], jt = JxW * tauq[qz];
+        const Real Tv = -JxW * divu[qz];
+        const Real Tx = -jt * Rq[0][qz] * ihx, Ty = -jt * Rq[1][qz] * ihy, Tz = -jt * Rq[2][qz] * ihz;
+#pragma unroll
+        for (int az = 0; az < 3; ++az) {
+          Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Tz;
+          Z[1][az] += T.V[qz][az] * Tx;
+          Z[2][az] += T.V[qz][az] * Ty;
+        }
+      }
+      backward(3, Z);
+    }
+    if constexpr (RL) {  // the residual's node sums first; the diagonal then reuses the cell-value area
+      __syncthreads();
+      reduce_scatter(P.res_y, P.res_slab, false);
+      __syncthreads();
     }
     if constexpr (LIN) {
       // ---------------- Jacobian diagonal at this state (the lane-per-point MODE_LIN restated): for
@@ -507,22 +601,6 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
           outc[3 * C::OF + 9 * iz + 3 * pb + pa] = acc[iz][3];
         }
       }
-    }
-    if constexpr (RES) {  // pressure test field: -JxW div u, -JxW tau R_e / h_e
-      Real Z[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-#pragma unroll
-      for (int qz = 0; qz < 3; ++qz) {
-        const Real JxW = wxy * T.w[qz], jt = JxW * tauq[qz];
-        const Real Tv = -JxW * divu[qz];
-        const Real Tx = -jt * Rq[0][qz] * ihx, Ty = -jt * Rq[1][qz] * ihy, Tz = -jt * Rq[2][qz] * ihz;
-#pragma unroll
-        for (int az = 0; az < 3; ++az) {
-          Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Tz;
-          Z[1][az] += T.V[qz][az] * Tx;
-          Z[2][az] += T.V[qz][az] * Ty;
-        }
-      }
-      backward(3, Z);
     }
   } else {
   // linearization rows of this lane (pencil layout: value v of point qz). Full: u, tau and component 0's
@@ -649,62 +727,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   }  // MODE_JVQ
   __syncthreads();
 
-  // ---------------- brick reduction (fixed cell order per node) + scatter: one thread per brick node
-  for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
-    const int rb_ = t / BN3, n = t % BN3;
-    if (rb_ >= nbg) break;
-    const int bk = brick_of(rb_);
-    const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
-    Real s[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int kz = 0; kz < 2; ++kz) {
-      const int az = Zn - 2 * kz;
-      if (az < 0 || az > 2) continue;
-#pragma unroll
-      for (int ky = 0; ky < 2; ++ky) {
-        const int ay = Yn - 2 * ky;
-        if (ay < 0 || ay > 2) continue;
-#pragma unroll
-        for (int kx = 0; kx < 2; ++kx) {
-          const int ax = Xn - 2 * kx;
-          if (ax < 0 || ax > 2) continue;
-          const Real *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::OC + ax + 3 * (ay + 3 * az);
-#pragma unroll
-          for (int f = 0; f < 4; ++f) s[f] += o[f * C::OF];
-        }
-      }
-    }
-    const int node = sNode[rb_ * BN3P + n];
-    const int64_t gi[4] = {(int64_t)node * 3, (int64_t)node * 3 + 1, (int64_t)node * 3 + 2, voff + node};
-    const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
-    if (interior) {
-      if (P.jx) {  // fused damped-Jacobi sweep (interior nodes: no other brick reads this x)
-        const unsigned m = P.vmask ? P.vmask[node] : 0u;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const bool con = f < 3 && ((m >> f) & 1u);
-          const double x = P.jx[gi[f]], dd = P.jd[gi[f]];
-          P.jx[gi[f]] = x + P.jomega * (P.jb[gi[f]] - (con ? dd * x : (double)s[f])) / dd;
-        }
-      } else if (P.rb) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) P.y[gi[f]] = P.rb[gi[f]] - (double)s[f];
-      } else {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) P.y[gi[f]] = s[f];
-      }
-    } else {  // this brick's partial sums of a brick-boundary node (summed per node by k_slab_sum)
-      const int64_t si = ((int64_t)bk * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4;
-      if (std::is_same<Real, float>::value && P.slabf) {
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<f4 *>(P.slabf + si) = f4{(float)s[0], (float)s[1], (float)s[2], (float)s[3]};
-      } else {
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<d2 *>(P.slab + si) = d2{(double)s[0], (double)s[1]};
-        *reinterpret_cast<d2 *>(P.slab + si + 2) = d2{(double)s[2], (double)s[3]};
-      }
-    }
-  }
+  reduce_scatter(P.y, P.slab, true);
 }
 
 // Selection: on by default for the Q2 brick J.v with a slab (the launch contract of the
@@ -746,6 +769,11 @@ hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s,
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (P.bricks || !P.slab || P.subset) return hipErrorNotSupported;
   return launch_pencil_t<double, MODE_RESIDUAL>(P, T, s);
+}
+// residual (into res_y / res_slab) + linearization + diagonal (into y / slab) at one state
+hipError_t launch_pencil_reslin(const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if (P.bricks || P.subset || !P.qd || !P.y || !P.slab || !P.res_y || !P.res_slab) return hipErrorNotSupported;
+  return launch_pencil_t<double, MODE_RESLIN>(P, T, s);
 }
 hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (P.bricks || (P.y && !P.slab) || P.subset || !P.qd) return hipErrorNotSupported;

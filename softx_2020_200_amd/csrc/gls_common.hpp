@@ -13,7 +13,8 @@ constexpr int ipow(int b, int e) { return e == 0 ? 1 : b * ipow(b, e - 1); }
 
 // MODE_LIN / MODE_JVQ (brick kernels only): MODE_LIN stores the linearization at every quadrature
 // point (u, grad u, tau, R_s: kQData doubles) once per state; MODE_JVQ applies J.v from it.
-enum Mode { MODE_RESIDUAL = 0, MODE_JV = 1, MODE_DIAG = 2, MODE_LIN = 3, MODE_JVQ = 4 };
+enum Mode { MODE_RESIDUAL = 0, MODE_JV = 1, MODE_DIAG = 2, MODE_LIN = 3, MODE_JVQ = 4,
+            MODE_RESLIN = 5 /* pencil kernel: residual + linearization + diagonal in one pass */ };
 constexpr int kQData = 16;  // u[3], grad u[3][3], tau, R_s[3]
 
 // Reference-cell 1D tables on [0,1] (deal.II unit cell): Lagrange basis on Gauss–Lobatto
@@ -75,6 +76,14 @@ struct OpParams {
   double jomega;
   // residual form (MODE_JVQ brick kernels, no jx): y = rb - A v instead of y = A v (nullptr: off)
   const double *rb;
+  // with rb (pencil J.v, hyper_cube slab sum): the first damped-Jacobi sweep from x = 0 fused in front of
+  // the residual: v = 0 + jomega rb / jd is formed in the gather and stored to jx0 (interior nodes here,
+  // surface nodes by the slab sum), y = rb - A v
+  double *jx0;
+  // MODE_RESLIN: the residual's node sums (brick-interior nodes, and the brick-surface slab summed by
+  // the slab sum) next to the diagonal's in y / slab
+  double *res_y;
+  double *res_slab;
   // colored brick launches (replace the slab + k_slab_sum): bricks are launched one color at a time
   // (no two bricks of a color share a node); a brick-surface node's running sum lives in acc[] and
   // is carried across colors in color order (deterministic): the node's first-color brick writes,

@@ -23,6 +23,8 @@ hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
 hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32);
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_RESIDUAL, FP64
 hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_LIN (+ diagonal into P.y)
+// MODE_RESLIN: residual (res_y / res_slab) + linearization (qd, qdf) + diagonal (y / slab) in one pass
+hipError_t launch_pencil_reslin(const OpParams &P, const Tables1D &T, hipStream_t s);
 bool pencil_enabled();
 // persistent wave-per-brick versions (gls_brick_wave.hip), selected by the launchers above
 hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);
@@ -44,7 +46,7 @@ hipError_t brick_slab_sum_ex(const double *slab, const float *slabf, const int32
 // bricks, no periodic wrap): slots computed from the lattice coordinates, no index arrays
 hipError_t brick_slab_sum_cube(int k, int nb1, const double *slab, const float *slabf, int64_t n_vnodes, double *y,
                                const uint8_t *vmask, const double *jb, const double *jd, double jomega, hipStream_t s,
-                               const double *rb = nullptr);
+                               const double *rb = nullptr, double *x0 = nullptr);  // x0: OpParams::jx0's surface nodes
 bool brick_fused_jacobi_supported(int k);  // the selected brick kernel honours OpParams::jx and ::slabf
 // batched probing: Y[(j - j0) * n_dofs + i] += (J_cell-sum e_j)_i for nprobe unit vectors (MODE_JVQ)
 bool brick_colors_supported(int k);  // colored brick launches (OpParams::bricks) available

@@ -11,6 +11,13 @@
 // order (children lexicographic, x fastest), which is p4est's order for a single tree.
 // gls_octree_mesh builds the FE_Q(k) / FE_Q(kp) node spaces on the finest node lattice with
 // hanging lines whose masters are all unconstrained (chains resolved).
+// Periodic directions (gls_octree_set_periodic; GridTools::collect_periodic_faces +
+// add_periodicity, gls_navier_stokes.cc:130-134, 164-168): the forest's neighbourhoods wrap around
+// them -- the 2:1 vertex balance, the smoothing's face neighbours and vertex levels, the Kelly faces --
+// and the node lattice identifies the max face with the min face, so the hanging lines of a coarse
+// cell also constrain a finer periodic neighbour's face nodes (periodicity and hanging constraints
+// together, as make_periodicity_constraints + make_hanging_node_constraints close them). Restated, no
+// reference golden covers it (no reference case combines periodicity with adaptation).
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -27,6 +34,7 @@ int gls_io_set_error(int code, const char *fmt, ...);  // gls_api.cpp
 
 struct gls_octree {
   int dim = 3, n = 1;
+  int pmask = 0;  // periodic directions (bit d)
   struct Leaf {
     int level;
     int64_t x[3];  // origin in units of its own level's cells
@@ -67,15 +75,16 @@ void sort_leaves(gls_octree &t) {
 
 // level of the leaf covering every finest-level cell (a dense grid: small trees only)
 struct LevelGrid {
-  int dim, L;
+  int dim, L, pmask = 0;
   int64_t N;  // finest cells per direction
   std::vector<int8_t> lev;
   int at(const int64_t *p) const {
-    for (int d = 0; d < dim; ++d)
-      if (p[d] < 0 || p[d] >= N) return -1;
     int64_t id = 0, st = 1;
     for (int d = 0; d < dim; ++d) {
-      id += p[d] * st;
+      int64_t q = p[d];
+      if ((pmask >> d) & 1) q = ((q % N) + N) % N;  // periodic: the neighbourhood wraps
+      else if (q < 0 || q >= N) return -1;
+      id += q * st;
       st *= N;
     }
     return lev[(size_t)id];
@@ -84,6 +93,7 @@ struct LevelGrid {
 int make_grid(const gls_octree &t, int L, LevelGrid &g) {
   g.dim = t.dim;
   g.L = L;
+  g.pmask = t.pmask;
   g.N = (int64_t)t.n << L;
   int64_t tot = 1;
   for (int d = 0; d < t.dim; ++d) tot *= g.N;
@@ -176,7 +186,7 @@ struct MeshImpl {
   std::vector<int64_t> vh_node, vh_off, vh_master, ph_node, ph_off, ph_master;
   std::vector<double> vh_w, ph_w;
   // for transfers: the tree geometry
-  int n = 1, L = 0;
+  int n = 1, L = 0, pmask = 0;
   double lo = 0, hi = 1;
 };
 
@@ -189,10 +199,10 @@ int build_space(const gls_octree &t, int L, int kk, double lo, double hf, std::v
   int64_t npts = 1;
   for (int d = 0; d < dim; ++d) npts *= np1;
   if (npts > ((int64_t)1 << 31)) return gls_io_set_error(GLS_EINVAL, "octree mesh lattice too large");
-  auto lat = [&](const int64_t *p) {
+  auto lat = [&](const int64_t *p) {  // periodic directions: the max face is the min face
     int64_t id = 0, st = 1;
     for (int d = 0; d < dim; ++d) {
-      id += p[d] * st;
+      id += (((t.pmask >> d) & 1) ? p[d] % (np1 - 1) : p[d]) * st;
       st *= np1;
     }
     return id;
@@ -377,7 +387,10 @@ struct Smoother {
     const int d = f / 2;
     nb = c;
     nb.x[d] += (f & 1) ? 1 : -1;
-    if (nb.x[d] < 0 || nb.x[d] >= extent(c.level)) return 0;
+    if (nb.x[d] < 0 || nb.x[d] >= extent(c.level)) {
+      if (!((t.pmask >> d) & 1)) return 0;
+      nb.x[d] = (nb.x[d] + extent(c.level)) % extent(c.level);  // periodic neighbour
+    }
     if (find(nb.level, nb.x) != -2) return 1;
     nb.level -= 1;
     for (int e = 0; e < 3; ++e) nb.x[e] /= 2;
@@ -412,7 +425,10 @@ struct Smoother {
   }
   uint64_t vkey(const Leaf &c, int corner) const {  // vertex on the lattice of level LM + 1
     int64_t v[3] = {0, 0, 0};
-    for (int d = 0; d < dim; ++d) v[d] = (c.x[d] + ((corner >> d) & 1)) << (LM + 1 - c.level);
+    for (int d = 0; d < dim; ++d) {
+      v[d] = (c.x[d] + ((corner >> d) & 1)) << (LM + 1 - c.level);
+      if ((t.pmask >> d) & 1) v[d] %= extent(LM + 1);  // periodic: the max vertex is the min vertex
+    }
     return ((uint64_t)v[0] << 42) | ((uint64_t)v[1] << 21) | (uint64_t)v[2];
   }
   // limit_level_difference_at_vertices (step 3, repeated in fix_coarsen_flags): the highest future
@@ -596,6 +612,12 @@ int gls_octree_create(int dim, int n, gls_octree **out) {
 }
 void gls_octree_destroy(gls_octree *t) { delete t; }
 
+int gls_octree_set_periodic(gls_octree *t, int mask) {
+  if (!t || mask < 0 || mask >= (1 << t->dim)) return gls_io_set_error(GLS_EINVAL, "gls_octree_set_periodic: bad mask");
+  t->pmask = mask;
+  return GLS_OK;
+}
+
 int gls_octree_info(const gls_octree *t, int64_t *n_cells, int *max_level) {
   if (!t) return gls_io_set_error(GLS_EINVAL, "null octree");
   if (n_cells) *n_cells = (int64_t)t->leaves.size();
@@ -715,6 +737,7 @@ int gls_octree_mesh(const gls_octree *t, int k, int kp, double lo, double hi, gl
   }
   M->n = t->n;
   M->L = L;
+  M->pmask = t->pmask;
   M->lo = lo;
   M->hi = hi;
   gls_refined_mesh &p = M->pub;
@@ -844,9 +867,12 @@ int gls_octree_faces(const gls_refined_mesh *m, int64_t *n_faces, int32_t *fa, i
   for (int64_t c = 0; c < m->n_cells; ++c)
     for (int d = 0; d < dim; ++d) low[{d, box[(size_t)c][d]}].push_back((int32_t)c);
   int64_t cnt = 0;
+  const int64_t NL = (int64_t)M->n << M->L;
   for (int64_t a = 0; a < m->n_cells; ++a)
     for (int d = 0; d < dim; ++d) {
-      auto it = low.find({d, box[(size_t)a][3 + d]});
+      int64_t hi = box[(size_t)a][3 + d];
+      if (((M->pmask >> d) & 1) && hi == NL) hi = 0;  // periodic face pair: a at the max, b at the min face
+      auto it = low.find({d, hi});
       if (it == low.end()) continue;
       for (int32_t b : it->second) {
         int64_t olo[3], ohi[3];

@@ -31,7 +31,7 @@ EXPORTS = [
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy",
     "gls_dist_attach_rccl",
-    "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
+    "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_residual_and_diagonal", "gls_octree_set_periodic", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",
@@ -145,6 +145,7 @@ def load():
     L.gls_jacobian_apply.argtypes = [vp, vp, vp]
     L.gls_jacobian_apply_f32.argtypes = [vp, vp, vp]
     L.gls_jacobian_diagonal.argtypes = [vp, vp]
+    L.gls_residual_and_diagonal.argtypes = [vp, vp, vp]
     L.gls_set_dirichlet.argtypes = [vp, i64, C.POINTER(i64), d]
     L.gls_apply_dirichlet.argtypes = [vp, vp]
     L.gls_solve_linear.argtypes = [vp, vp, vp, C.POINTER(LinearParams)]
@@ -312,6 +313,7 @@ class Octree:
         self.L = load()
         self.L.gls_octree_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
         self.L.gls_octree_destroy.argtypes = [C.c_void_p]
+        self.L.gls_octree_set_periodic.argtypes = [C.c_void_p, C.c_int]
         self.L.gls_octree_info.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int)]
         self.L.gls_octree_cells.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_double]
         self.L.gls_octree_adapt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
@@ -326,6 +328,10 @@ class Octree:
     def __del__(self):
         if getattr(self, "h", None):
             self.L.gls_octree_destroy(self.h)
+
+    def set_periodic(self, mask):
+        """periodic directions (bit d), before adapting: neighbourhoods wrap, mesh() identifies the faces"""
+        check(self.L.gls_octree_set_periodic(self.h, int(mask)), "gls_octree_set_periodic")
 
     @property
     def n_cells(self):
@@ -629,6 +635,14 @@ class GLSContext:
         out = self.zeros() if out is None else out
         check(self.L.gls_jacobian_apply_f32(self.h, _ptr(v), _ptr(out)), "gls_jacobian_apply_f32")
         return out
+
+    def residual_and_diagonal(self, out=None, diag=None):
+        """assemble_matrix_and_rhs: the residual and the Jacobian diagonal at the current state (one
+        fused launch on the Q2 brick path); returns (residual, diagonal)."""
+        out = self.zeros() if out is None else out
+        diag = self.zeros() if diag is None else diag
+        check(self.L.gls_residual_and_diagonal(self.h, _ptr(out), _ptr(diag)), "gls_residual_and_diagonal")
+        return out, diag
 
     def jacobian_diagonal(self, out=None):
         out = self.zeros() if out is None else out

@@ -279,3 +279,30 @@ def test_pencil_kernels_and_structured_slab_sum(monkeypatch, n, scheme, srf):
     assert relerr(out["pencil"][0], orc.residual(u, u1, u2, u3)) < TOL
     assert relerr(out["pencil"][1], orc.jacobian_diagonal(u, u1, u2, u3)) < TOL
     assert relerr(out["pencil"][2], orc.jacobian_apply(u, v, u1, u2, u3)) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,scheme,srf", [(2, "bdf2", False), (4, "bdf2", False), (4, "steady", True)])
+def test_fused_residual_linearization_diagonal(monkeypatch, n, scheme, srf):
+    """assemble_matrix_and_rhs as one pencil launch (MODE_RESLIN: residual, J.v linearization and Jacobian
+    diagonal, gls_residual_and_diagonal) is BITWISE the separate residual / diagonal launches: the
+    residual, the diagonal, and the J.v / FP32 J.v from the linearization it cached. Case 3 runs the
+    forcing + SRF instantiation; GLS_NO_RESLIN=1 (the separate calls behind the same entry) agrees too."""
+    p = _morton_problem(n, 2, scheme, 0.01, srf=srf)
+    u, u1, u2, u3, v = _states(p)
+    ctx = context_for(p)
+    V = cuda(v)
+    ctx.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))
+    sep = [ctx.residual().cpu().numpy(), ctx.jacobian_diagonal().cpu().numpy(),
+           ctx.jacobian_apply(V).cpu().numpy(), ctx.jacobian_apply_f32(V).cpu().numpy()]
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("GLS_NO_RESLIN", env)
+        ctx.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))  # drops the linearization / diagonal
+        r, d = ctx.residual_and_diagonal()
+        fused = [r.cpu().numpy(), d.cpu().numpy(), ctx.jacobian_apply(V).cpu().numpy(),
+                 ctx.jacobian_apply_f32(V).cpu().numpy()]
+        for name, a, b in zip(("residual", "diagonal", "J.v", "J.v f32"), fused, sep):
+            assert np.array_equal(a, b), (env, name, relerr(a, b))
+    orc = Oracle(p)
+    assert relerr(sep[0], orc.residual(u, u1, u2, u3)) < TOL

@@ -307,3 +307,36 @@ def test_skip_newton_reaches_newton_solution():
     assert ss["newton_iterations"] > sn["newton_iterations"]
     nu_ = p.dim * p.n_vnodes
     assert np.abs(xs[:nu_] - xn[:nu_]).max() < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [8, 16])
+def test_fused_first_sweep_is_bitwise(n, monkeypatch):
+    """V(1,1) with the FP32 smoother: the first pre-sweep from x = 0 formed inside the residual's pencil
+    J.v (x = omega D^-1 b in the gather, stored by the J.v and the slab sum; no separate mg_jacobi_update)
+    gives the BITWISE same preconditioner application as the separate update + residual
+    (GLS_MG_NO_FIRST_FUSE=1), and GMRES the same iterations and solution."""
+    import torch
+    import bench
+    from softx_2020_200_amd.problem import CavityProblem
+    prob = CavityProblem(dim=3, n=n, k=2, viscosity=0.01, multigrid=True, pre_smooth=1, post_smooth=1,
+                         omega=0.9, coarse_sweeps=20, coarse_omega=0.7, mixed_precision=1)
+    ctx = prob.ctx
+    ctx.set_time("bdf2", (0.01,) * 4)
+    m1 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.0)).cuda()
+    m2 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.3)).cuda()
+    ctx.set_state(m1, m1, m2)
+    v = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, ctx.n_dofs)).cuda()
+    b = ctx.residual()
+    out = {}
+    for tag, env in (("fused", None), ("plain", "1")):
+        if env:
+            monkeypatch.setenv("GLS_MG_NO_FIRST_FUSE", env)
+        z = ctx.apply_preconditioner(v).cpu().numpy()
+        x, its, _, ok = ctx.solve_linear(b, max_iterations=200, relative_residual=1e-8)
+        assert ok
+        out[tag] = (z, x.cpu().numpy(), its)
+    assert np.array_equal(out["fused"][0], out["plain"][0])
+    assert np.array_equal(out["fused"][1], out["plain"][1])
+    assert out["fused"][2] == out["plain"][2]
+    assert np.abs(out["plain"][0]).max() > 0

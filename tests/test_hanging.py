@@ -238,3 +238,112 @@ def test_hanging_newton_mms3d():
     assert np.abs(xs[:nvd] - x_ref[:nvd]).max() < 1e-8
     eu, ep = Oracle(p).l2_error(xs, E)
     assert g["error_velocity"][1] < eu < g["error_velocity"][0], (eu, g["error_velocity"])
+
+
+# ---------------------------------------------------------------------------------------------------
+# periodic directions under local refinement (gls_octree_set_periodic; gls_navier_stokes.cc:130-134,
+# 164-168: periodicity and hanging constraints closed together). No reference case combines the two:
+# pinned by the constraint algebra below and by the oracle.
+PERIODIC_CASES = [  # dim, n, k, kp, periodic mask
+    (2, 2, 2, 1, 1),
+    (2, 2, 1, 1, 3),
+    (3, 2, 2, 2, 1),
+    (3, 2, 1, 1, 5),
+]
+
+
+def periodic_octree_mesh(dim, n, k, kp, pmask, steps=3, seed=5):
+    """refine around (0.85, ...), next to the periodic max faces, coarsen half of the rest at random"""
+    t = sx.Octree(dim, n)
+    t.set_periodic(pmask)
+    rng = np.random.default_rng(seed)
+    for _ in range(steps):
+        lev, x0, h = t.cells()
+        near = np.linalg.norm(x0 + 0.5 * h - 0.85, axis=1) < 0.7
+        t.adapt(refine=near.astype(np.int32), coarsen=(~near & (rng.uniform(size=len(lev)) < 0.5)).astype(np.int32),
+                max_level=4)
+    return t, t.mesh(k, kp)
+
+
+def periodic_octree_problem(dim, n, k, kp, pmask, scheme="bdf2", nu=0.05):
+    _, mesh = periodic_octree_mesh(dim, n, k, kp, pmask)
+    per = tuple(d for d in range(dim) if (pmask >> d) & 1)
+    p = StructuredProblem.from_refined(mesh, viscosity=nu, scheme=scheme, time_steps=(0.01, 0.013, 0.011, 0.009),
+                                       periodic=per)
+    lines = sx.hanging_dof_lines(mesh)
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    p.set_dirichlet([("noslip", 0, None)])
+    p.set_force(lambda X: np.stack([np.sin(np.pi * X[:, 0]) * np.cos(np.pi * X[:, 1]) for _ in range(dim)], 1))
+    return p, mesh
+
+
+@pytest.mark.parametrize("case", PERIODIC_CASES, ids=lambda c: "d%d_n%d_Q%dQ%d_p%d" % c)
+def test_periodic_octree_balance_and_constraints(case):
+    """Periodic directions wrap the forest and the node lattice: no node on a periodic max face; the
+    vertex 2:1 balance holds across the periodic boundary; hanging lines are partitions of unity whose
+    masters are free and reproduce every field that is Q_k in the tangential coordinates and continuous
+    across the periodic faces, g(x_p) P(x) with g(lo) = g(hi); and some hanging nodes lie on the
+    periodic min face, constrained by the coarser cell on the other side."""
+    dim, n, k, kp, pm = case
+    t, m = periodic_octree_mesh(dim, n, k, kp, pm)
+    lo, hi = -1.0, 1.0
+    per = [d for d in range(dim) if (pm >> d) & 1]
+    assert m["cell_level"].max() >= 3
+    # vertex balance with wrap: levels at every vertex of the finest lattice differ by <= 1
+    lev, x0, h = t.cells()
+    L = int(lev.max())
+    N = n << L
+    hf = (hi - lo) / N
+    vmin, vmax = {}, {}
+    for c in range(len(lev)):
+        o = np.rint((x0[c] - lo) / hf).astype(np.int64)
+        s = 1 << (L - int(lev[c]))
+        for corner in np.ndindex(*(2,) * dim):
+            v = tuple(int((o[d] + corner[d] * s) % N) if d in per else int(o[d] + corner[d] * s) for d in range(dim))
+            vmin[v] = min(vmin.get(v, 99), int(lev[c]))
+            vmax[v] = max(vmax.get(v, -1), int(lev[c]))
+    assert max(vmax[v] - vmin[v] for v in vmax) <= 1
+    rng = np.random.default_rng(SEED)
+    on_face = 0
+    for tag, deg, X in (("vhang", k, m["vnode_x"]), ("phang", kp, m["pnode_x"])):
+        for d in per:
+            assert np.abs(X[:, d] - hi).min() > 1e-9  # identified with the min face
+        nodes, off, mas, w = m[tag]
+        assert len(nodes) > 0
+        f = np.ones(X.shape[0])
+        for d in range(dim):
+            if d in per:  # a periodic-compatible factor g(lo) = g(hi) = 1 of degree <= deg
+                f *= 1.0 + (0.3 * (X[:, d] - lo) * (hi - X[:, d]) if deg >= 2 else 0.0)
+            else:
+                f *= np.polynomial.polynomial.polyval(X[:, d], rng.normal(size=deg + 1))
+        for i, nd in enumerate(nodes):
+            sl = slice(off[i], off[i + 1])
+            assert abs(np.sum(w[sl]) - 1.0) < 1e-13
+            assert abs(np.dot(w[sl], f[mas[sl]]) - f[nd]) < 1e-12 * max(1.0, np.abs(f).max())
+            assert len(set(mas[sl].tolist()) & set(nodes.tolist())) == 0
+            on_face += any(abs(X[nd, d] - lo) < 1e-12 for d in per)
+    assert on_face > 0
+
+
+@pytest.mark.parametrize("case", PERIODIC_CASES[1:2] + PERIODIC_CASES[3:], ids=lambda c: "d%d_n%d_Q%dQ%d_p%d" % c)
+def test_periodic_octree_oracle_condensation_matches_numpy(case):
+    """The oracle's condensed operators on the periodic adapted meshes == C^T K C in numpy."""
+    p, mesh = periodic_octree_problem(*case)
+    _check_condensation(p, mesh)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PERIODIC_CASES, ids=lambda c: "d%d_n%d_Q%dQ%d_p%d" % c)
+def test_periodic_octree_gpu_vs_oracle(case):
+    """Periodic adapted meshes: HIP residual, J.v and constraint distribution == the oracle at 1e-12."""
+    from tests.gpu_util import context_for, cuda, relerr
+    p, mesh = periodic_octree_problem(*case)
+    rng = np.random.default_rng(SEED)
+    u, u1, u2, v = (rng.uniform(-1, 1, p.n_dofs) for _ in range(4))
+    p.apply_nonzero_constraints(u)
+    orc = Oracle(p)
+    ctx = context_for(p)
+    ctx.set_state(cuda(u), cuda(u1), cuda(u2))
+    assert relerr(ctx.residual().cpu().numpy(), orc.residual(u, u1, u2)) < 1e-12
+    assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1, u2)) < 1e-12
