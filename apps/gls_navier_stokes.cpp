@@ -271,8 +271,6 @@ Params read_params(const Prm &p, int dim) {
     P.min_level = p.i(ma + "min refinement level", 0);
     if (P.frac_refine < 0 || P.frac_coarsen < 0 || P.frac_refine + P.frac_coarsen > 1)
       die("mesh adaptation: fractions must be >= 0 with refinement + coarsening <= 1");
-    if (P.method != Method::steady && !P.general)
-      die("kelly mesh adaptation: transient runs on general (gmsh / GridGenerator) meshes only");
     if (P.k > 2 || P.kp > P.k) die("kelly mesh adaptation: 1 <= pressure order <= velocity order <= 2");
   }
   const int nbc = p.i("boundary conditions/number", 0);
@@ -2266,21 +2264,27 @@ struct Solver {
     ck(gls_octree_adapt(tree, rf.data(), cf.data(), 1 << 20, 0), "gls_octree_adapt");
     gls_refined_mesh *nm = nullptr;
     ck(gls_octree_mesh(tree, P.k, P.kp, P.lo, P.hi, &nm), "gls_octree_mesh");
-    const std::vector<double> sol = present;
+    // SolutionTransfer of the present solution and, transient, the time history (:684-733)
+    const bool transient = P.method != Method::steady;
+    const std::vector<double> sol = present, s1 = m1, s2 = m2, s3 = m3;
     gls_refined_mesh *old_rm = rmesh;
     rmesh = nullptr;  // kept for the transfer (release() would free it)
     setup_refined(nm);
-    host_changed();  // present is rewritten on the host below
-    if (old_rm) {
-      ck(gls_octree_transfer(old_rm, rmesh, sol.data(), present.data()), "gls_octree_transfer");
-      gls_octree_mesh_destroy(old_rm);
-    } else if (um) {
-      ck(gls_octree_transfer(um, rmesh, sol.data(), present.data()), "gls_octree_transfer");
-      gls_octree_mesh_destroy(um);
-    } else {
-      ck(gls_mesh_refined_interpolate(rmesh, (int)n_uniform, P.lo, P.hi, sol.data(), present.data()),
-         "gls_mesh_refined_interpolate");
+    host_changed();  // present (and the history) are rewritten on the host below
+    auto move = [&](const std::vector<double> &from, std::vector<double> &to) {
+      if (old_rm) ck(gls_octree_transfer(old_rm, rmesh, from.data(), to.data()), "gls_octree_transfer");
+      else if (um) ck(gls_octree_transfer(um, rmesh, from.data(), to.data()), "gls_octree_transfer");
+      else ck(gls_mesh_refined_interpolate(rmesh, (int)n_uniform, P.lo, P.hi, from.data(), to.data()),
+              "gls_mesh_refined_interpolate");
+    };
+    move(sol, present);
+    if (transient) {
+      move(s1, m1);
+      move(s2, m2);
+      move(s3, m3);
     }
+    if (old_rm) gls_octree_mesh_destroy(old_rm);
+    if (um) gls_octree_mesh_destroy(um);
   }
   // refine_mesh_kelly on a general (gmsh / GridGenerator, curved) triangulation: the Kelly indicator
   // with MappingQ face geometry (gls_fe_space_kelly_faces + gls_kelly_estimate_mapped), the same

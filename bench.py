@@ -234,7 +234,7 @@ def bench_cylinder3d(args):
     ctx, sp, x = cylinder3d_context()
     dev = torch.device("cuda", 0)
     ctx.set_time("bdf2", (0.05,) * 4)
-    ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
+    ctx.attach_ilu(1e-5, 1.0, fill=args.ilu_fill, ordering="multicolor" if args.ilu_fill == 0 else "cm")
     m1 = torch.from_numpy(x).to(dev)
     m2 = m1.clone()
     present = m1.clone()
@@ -242,7 +242,7 @@ def bench_cylinder3d(args):
     def one_step():
         present.copy_(m1)
         return ctx.newton(present, m1, m2, tolerance=1e-30, max_iterations=1, lin_max_iterations=args.lin_max,
-                          restart=30, relative_residual=1e-4, minimum_residual=1e-9)
+                          restart=args.restart, relative_residual=1e-4, minimum_residual=1e-9)
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
@@ -275,7 +275,8 @@ def bench_cylinder3d(args):
         "dtype": "f64", "data": "synthetic (free stream with a smooth wake-like perturbation, prm boundary values)",
         "config": {"workload": "BASELINE configs[4] problem on one GPU: apps/cases/cylinder3d_extruded.msh "
                                "(unadapted), Q2-Q1 MappingQ2, nu 0.005, BDF2 dt 0.05",
-                   "n_dofs": N, "n_cells": nc, "linear_solver": "GMRES(30)+ILU(0) multicolor, rel 1e-4"},
+                   "n_dofs": N, "n_cells": nc, "linear_solver": "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
+                       args.restart, args.ilu_fill, "multicolor" if args.ilu_fill == 0 else "Cuthill-McKee")},
         "mdof_per_s": N * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
         "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,1,3,MODE_JV,GEN>", "achieved": B / (ms * 1e-3) / 1e9,
@@ -302,6 +303,7 @@ def main():
     ap.add_argument("--dt", type=float, default=0.01)
     ap.add_argument("--lin-max", type=int, default=200)
     ap.add_argument("--restart", type=int, default=30)
+    ap.add_argument("--ilu-fill", type=int, default=0, help="cylinder3d: ILU level of fill (0: multicolor order)")
     ap.add_argument("--rel", type=float, default=1e-4)
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
                     help="GMRES right preconditioner: geometric multigrid V-cycle (default) or Jacobi")
@@ -532,6 +534,9 @@ def main():
                       "diagonal": dg_ms / max(dg_n, 1), "jv_linearization": lin_ms / max(lin_n, 1),
                       "smoother_jv_f32": f32_ms / max(f32_n, 1), "slab_sum": sl_ms / max(sl_n, 1),
                       "source": "one extra instrumented step after the timed region (HIP events per launch)",
+                      "note": ("diagonal = the Newton step's fused residual + linearization + Jacobian-diagonal launch "
+                               "(assemble_matrix_and_rhs, gls_residual_and_diagonal); residual = the line search's"
+                               if pencil_jv and world == 1 else ""),
                       "instrumented_step_ms": 1e3 * elapsed_instr,
                       "launches_per_step": {"jacobian_apply": jv_n, "residual": res_n, "diagonal": dg_n,
                                             "jv_linearization": lin_n, "smoother_jv_f32": f32_n, "slab_sum": sl_n},

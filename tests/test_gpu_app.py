@@ -484,3 +484,37 @@ end""")
     hang = [int(l.split(":")[1]) for l in out.splitlines() if "Hanging node DoFs" in l]
     assert hang and max(hang) > 0, out[-3000:]
     assert "kelly:" in out
+
+
+@pytest.mark.gpu
+def test_app_transient_kelly_periodic_tgv(tmp_path):
+    """Transient Kelly adaptation on a periodic hyper_cube (refine_mesh_kelly every step with the time
+    history transferred, navier_stokes_base.cc:684-733): the reference's 2D Taylor-Green vortex prm
+    (Q2-Q1, SDIRK2, periodic in x and y) on 16^2 cells, 3 steps of 0.05 with Kelly every step, against
+    the same run on the uniform mesh: the adapted meshes carry hanging DoFs across the periodic faces and
+    the velocity error vs the analytic decay stays at or below the uniform run's every step. Parity
+    unpinned (no reference golden for an adapted TGV)."""
+    base = open(os.path.join(os.path.dirname(__file__), "golden", "app_cases", "taylor-green-vortex_gls_sdirk2.prm")).read()
+    prm = (base.replace("set time step               = 0.100", "set time step = 0.05")
+               .replace("set time end                = 0.10", "set time end = 0.15")
+               .replace("set output frequency        = 1 ", "set output frequency = 0 ")
+               .replace("set initial refinement   = 6", "set initial refinement = 4")
+               .replace("set tolerance               = 1e-6", "set tolerance = 1e-9")
+               .replace("set relative residual                     = 1e-4", "set relative residual = 1e-10")
+               .replace("set minimum residual                      = 1e-9", "set minimum residual = 1e-13"))
+    assert "time step = 0.05" in prm and "initial refinement = 4" in prm and "tolerance = 1e-9" in prm, prm
+    errs = {}
+    for tag, adapt in (("uniform", "  set type                    = none"),
+                       ("kelly", "  set type = kelly\n  set frequency = 1\n  set variable = velocity\n"
+                                 "  set fraction type = number\n  set fraction refinement = 0.2\n"
+                                 "  set fraction coarsening = 0.0\n  set max refinement level = 6")):
+        d = tmp_path / tag
+        d.mkdir()
+        out = run_app(d, prm.replace("  set type                    = none", adapt), 2)
+        errs[tag] = [float(l.split(":")[1]) for l in out.splitlines() if l.startswith("L2 error velocity")]
+        if tag == "kelly":
+            hang = [int(l.split(":")[1]) for l in out.splitlines() if "Hanging node DoFs" in l]
+            assert hang and max(hang) > 0, out[-3000:]
+    assert len(errs["uniform"]) == len(errs["kelly"]) == 3, errs
+    for a, b in zip(errs["kelly"], errs["uniform"]):
+        assert 0 < a <= 1.0001 * b, errs

@@ -347,3 +347,29 @@ def test_periodic_octree_gpu_vs_oracle(case):
     ctx.set_state(cuda(u), cuda(u1), cuda(u2))
     assert relerr(ctx.residual().cpu().numpy(), orc.residual(u, u1, u2)) < 1e-12
     assert relerr(ctx.jacobian_apply(cuda(v)).cpu().numpy(), orc.jacobian_apply(u, v, u1, u2)) < 1e-12
+
+
+@pytest.mark.parametrize("case", PERIODIC_CASES, ids=lambda c: "d%d_n%d_Q%dQ%d_p%d" % c)
+def test_periodic_octree_kelly_faces_tile_every_face(case):
+    """gls_octree_faces on a periodic forest: the face pieces of every cell tile its faces exactly
+    (reference-coordinate areas sum to 1 per face), the periodic boundary faces included -- they are
+    interior faces for the Kelly jump, as for deal.II's periodic neighbours -- and only the faces on
+    non-periodic boundaries stay uncovered."""
+    dim, n, k, kp, pm = case
+    t, m = periodic_octree_mesh(dim, n, k, kp, pm)
+    fa, fb, fd, ra, rb = t.faces(k, kp)
+    nc = int(m["n_cells"])
+    cover = np.zeros((nc, 2 * dim))
+    for a, b, d, qa, qb in zip(fa, fb, fd, ra, rb):
+        ar_a = (qa[1] - qa[0]) * ((qa[3] - qa[2]) if dim == 3 else 1.0)
+        ar_b = (qb[1] - qb[0]) * ((qb[3] - qb[2]) if dim == 3 else 1.0)
+        cover[a, 2 * d + 1] += ar_a  # a's face at xi_d = 1
+        cover[b, 2 * d] += ar_b      # b's face at xi_d = 0
+    x0, h = m["cell_x0"], m["cell_h"]
+    lo, hi = -1.0, 1.0
+    for c in range(nc):
+        for d in range(dim):
+            for side in (0, 1):
+                on_bnd = abs((x0[c, d] + side * h[c, d]) - (hi if side else lo)) < 1e-12
+                want = 0.0 if (on_bnd and not (pm >> d) & 1) else 1.0
+                assert abs(cover[c, 2 * d + side] - want) < 1e-12, (c, d, side, cover[c, 2 * d + side])
