@@ -1730,11 +1730,15 @@ bool slab_f32() { return std::getenv("GLS_SLAB_F64") == nullptr; }
 // rb != nullptr: y = rb - A v (the V-cycle's residual), fused into the kernels' stores on one rank.
 // first_omega > 0 (only where first_sweep_fusable): v is not read but formed as the first damped-Jacobi
 // sweep from 0, v = 0 + first_omega rb / D (mg_jacobi_update's arithmetic), in the J.v's gather and
-// stored to v by the J.v (brick-interior nodes) and the slab sum (surface nodes)
+// stored to v by the J.v (brick-interior nodes) and the slab sum (surface nodes). Opt-in
+// (GLS_MG_FIRST_FUSE=1): bitwise the separate update, but measured slower at Q2 128^3 (99.5 vs 96.0 ms per
+// Newton step, profiles/r04_ab_env_switches.txt: the gather's two extra FP64 loads and FP64 divisions per
+// node cost the J.v more than the update pass it saves)
 bool first_sweep_fusable(gls_ctx *g) {
-  return g->smooth_f32 && g->use_brick && g->use_qdata && !g->use_colors && !g->dist.on && !g->hang.on && g->k == 2 &&
-         g->cube_nb1 > 0 && g->use_slab && gls::pencil_enabled() && std::getenv("GLS_MG_NO_FUSE") == nullptr &&
-         std::getenv("GLS_MG_NO_FIRST_FUSE") == nullptr;
+  const char *e = std::getenv("GLS_MG_FIRST_FUSE");
+  return e && std::atoi(e) != 0 && g->smooth_f32 && g->use_brick && g->use_qdata && !g->use_colors && !g->dist.on &&
+         !g->hang.on && g->k == 2 && g->cube_nb1 > 0 && g->use_slab && gls::pencil_enabled() &&
+         std::getenv("GLS_MG_NO_FUSE") == nullptr;
 }
 int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr, double first_omega = 0.0) {
   if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
