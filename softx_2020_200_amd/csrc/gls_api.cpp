@@ -460,6 +460,7 @@ struct gls_ctx {
     // the first pressure DoF pinned (enclosed-flow gauge); falls back to the one-workgroup
     // Gauss-Jordan (mg_dense_invert) for small levels or when the LU reports a zero pivot
     bool lu = false;
+    int64_t npvt_ipiv_n = -1;  // ipiv holds the identity permutation of this size (unpivoted LU)
     struct Blas {  // owning rocBLAS handle (movable, destroyed with the MG state)
       rocblas_handle h = nullptr;
       Blas() = default;
@@ -481,6 +482,7 @@ struct gls_ctx {
     } blas;
     DevBuf<int> ipiv, info;
     DevBuf<double> probe, aug, unit;
+    DevBuf<double> probe_bak;  // the probed coarse matrix kept for the pivoted retry of an unpivoted LU
     DevBuf<int> status;
     // coarsest-level Jacobi sweeps (single rank, fused brick path) replayed as one HIP graph: the
     // ~2×csweeps tiny launches per V-cycle are captured once per state (mg_prepare) and launched
@@ -2073,26 +2075,42 @@ int mg_prepare(gls_ctx *c) {
     }
     const auto t1 = tick();
     mg.lu = false;
-    const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");  // gj | lu | lu_npvt (default lu)
+    // gj | lu | lu_npvt. Default: LU without pivoting (rocSOLVER's pivoted panel factorization is ~1 ms of
+    // a Newton step at n = 500, profiles/r04_ab_env_switches.txt) with a pivoted retry when a pivot vanishes
+    const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");
     const bool use_lu = cs ? std::strncmp(cs, "lu", 2) == 0 : true;  // LU: 1.5-3 ms at n = 500 vs the one-workgroup GJ's ~15
-    const bool npvt = cs && std::strcmp(cs, "lu_npvt") == 0;
+    bool npvt = cs ? std::strcmp(cs, "lu_npvt") == 0 : true;
     if (use_lu) {  // LU with the pressure gauge pinned
       const int64_t pin = 3 * (int64_t)g->n_vnodes;
       HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
-      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-          (npvt ? rocsolver_dgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.info.p)
-                : rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p,
-                                   mg.info.p)) != rocblas_status_success)
-        return set_err(GLS_EHIP, "rocsolver_dgetrf failed");
-      if (npvt) {  // identity permutation for getri
-        std::vector<int> id((size_t)n);
-        for (int64_t i = 0; i < n; ++i) id[(size_t)i] = (int)(i + 1);
-        HIP_TRY(hipMemcpyAsync(mg.ipiv.p, id.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+      if (npvt && !cs) {  // keep the matrix for a pivoted retry
+        if (mg.probe_bak.n != (size_t)(n * n)) GLS_TRY(mg.probe_bak.alloc((size_t)(n * n)));
+        HIP_TRY(gls::vec_copy(mg.probe_bak.p, mg.probe.p, n * n, c->stream));
       }
       int inf = -1;
-      HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
+      for (int attempt = 0; attempt < 2; ++attempt) {
+        if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+            (npvt ? rocsolver_dgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.info.p)
+                  : rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p,
+                                     mg.info.p)) != rocblas_status_success)
+          return set_err(GLS_EHIP, "rocsolver_dgetrf failed");
+        if (npvt) {  // identity permutation for getri
+          if (mg.npvt_ipiv_n != n) {
+            std::vector<int> id((size_t)n);
+            for (int64_t i = 0; i < n; ++i) id[(size_t)i] = (int)(i + 1);
+            HIP_TRY(hipMemcpyAsync(mg.ipiv.p, id.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            mg.npvt_ipiv_n = n;
+          }
+        }
+        HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (inf == 0 || !npvt || cs) break;
+        if (verbose) std::printf("mg: unpivoted coarse LU hit pivot %d, retrying with pivoting\n", inf);
+        HIP_TRY(gls::vec_copy(mg.probe.p, mg.probe_bak.p, n * n, c->stream));  // the pinned matrix again
+        npvt = false;
+        mg.npvt_ipiv_n = -1;  // getrf overwrites ipiv with its permutation
+      }
       const auto t2 = tick();
       if (verbose) std::printf("mg: levels+probe %.2f ms, getrf %.2f ms\n", ms(t0, t1), ms(t1, t2));
       if (inf == 0) {

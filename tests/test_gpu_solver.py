@@ -339,3 +339,32 @@ def test_fused_first_sweep_is_bitwise(n, monkeypatch):
     assert np.array_equal(out["fused"][1], out["plain"][1])
     assert out["fused"][2] == out["plain"][2]
     assert np.abs(out["plain"][0]).max() > 0
+
+
+@pytest.mark.gpu
+def test_coarse_lu_unpivoted_default_matches_pivoted(monkeypatch):
+    """The coarsest-level LU defaults to rocSOLVER's unpivoted factorization (a pivoted retry when a pivot
+    vanishes): bench.py's hierarchy gives the same Newton / GMRES iteration counts and the same solution
+    to 1e-10 as the pivoted LU (GLS_MG_COARSE_SOLVER=lu)."""
+    import torch
+    import bench
+    from softx_2020_200_amd.problem import CavityProblem
+    n = 16
+    out = {}
+    for env in (None, "lu"):
+        if env:
+            monkeypatch.setenv("GLS_MG_COARSE_SOLVER", env)
+        prob = CavityProblem(dim=3, n=n, k=2, viscosity=0.01, multigrid=True, mg_coarsest=2, pre_smooth=1,
+                             post_smooth=1, omega=0.9, mixed_precision=True, level_sweeps={-2: (2, 2)})
+        ctx = prob.ctx
+        ctx.set_time("bdf2", (0.01,) * 4)
+        m1 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.0)).cuda()
+        m2 = torch.from_numpy(bench.smooth_state(prob.mesh, n, 3, prob.dir_dofs, prob.dir_vals, 0.3)).cuda()
+        x = m1.clone()
+        st = ctx.newton(x, m1, m2, tolerance=1e-9, max_iterations=8, lin_max_iterations=500, restart=30,
+                        relative_residual=1e-6, minimum_residual=1e-14)
+        out[env] = (x.cpu().numpy(), st)
+    a, b = out[None], out["lu"]
+    assert a[1]["final_residual"] < 1e-9 and b[1]["final_residual"] < 1e-9
+    assert a[1]["linear_iterations"] == b[1]["linear_iterations"], (a[1], b[1])
+    assert np.abs(a[0] - b[0]).max() < 1e-10 * max(1.0, np.abs(b[0]).max())

@@ -14,14 +14,9 @@ print('%-14s ms/step %7.2f  its %5.1f  %s' % (sys.argv[2], d['ms_per_step'], d['
       ' '.join('%s=%.3f' % (n, k[n]) for n in ('jacobian_apply','smoother_jv_f32','slab_sum','residual','diagonal') if n in k)))" gpurun_out/envab_$tag.json $tag >> $O
 }
 B="--steps 8 --warmup 2 --no-cpu"
-run base X=1 -- $B || exit 1
-run nofirst GLS_MG_NO_FIRST_FUSE=1 -- $B || exit 1
-run noreslin GLS_NO_RESLIN=1 -- $B || exit 1
-run base2 X=1 -- $B || exit 1
-run gj GLS_MG_COARSE_SOLVER=gj -- $B || exit 1
-run lunpvt GLS_MG_COARSE_SOLVER=lu_npvt -- $B || exit 1
-C="--workload cylinder3d --steps 6 --warmup 2"
-run cyl30 X=1 -- $C || exit 1
-run cyl60 X=1 -- $C --restart 60 || exit 1
-run cyl100 X=1 -- $C --restart 100 || exit 1
+VARIANTS=("base X=1" "lupiv GLS_MG_COARSE_SOLVER=lu" "base2 X=1" "lupiv2 GLS_MG_COARSE_SOLVER=lu")
+for v in "${VARIANTS[@]}"; do
+  set -- $v
+  run $1 $2 -- $B || exit 1
+done
 cat $O
