@@ -212,6 +212,17 @@ typedef struct {
                                                  the coarsest level are ignored) */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
+/* The same V-cycle on a general level hierarchy with the caller's grid transfers: levels of an adaptive
+ * (octree) mesh with hanging-node constraints (gls_set_hanging before attaching), e.g. the global
+ * coarsening gls_octree_coarsen_to / gls_octree_mg_transfer builds. For l = 0 .. n_levels-2:
+ * p_off[l] (n_dofs(l)+1), p_col[l], p_w[l] = the prolongation from level l+1 to level l as CSR (rows of
+ * constrained fine DoFs may be empty), inject[l] (n_dofs(l+1)) = the level-l DoF whose value the
+ * level-(l+1) state takes (hanging values are then distributed from their lines). Restriction = P^T;
+ * the V-cycle zeroes constrained rows (Dirichlet and hanging) after each transfer. Smoothing: damped
+ * Jacobi with each level's own operator (per-cell kernels on hanging levels, FP64). One GPU. Host arrays
+ * (copied). */
+int gls_mg_attach_transfers(gls_ctx *ctx, const gls_mg_params *prm, const int64_t *const *p_off,
+                            const int32_t *const *p_col, const double *const *p_w, const int64_t *const *inject);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
  * attached, else Jacobi): the reference's preconditioner vmult (DEVICE pointers, no aliasing). */
 int gls_apply_preconditioner(gls_ctx *ctx, const double *v, double *z);
@@ -498,6 +509,18 @@ int gls_kelly_estimate_faces(gls_ctx *ctx, const double *sol, int variable, int6
                              double *eta);
 int gls_octree_faces(const gls_refined_mesh *mesh, int64_t *n_faces, int32_t *fa, int32_t *fb, int32_t *fdir,
                      double *rect_a, double *rect_b);
+/* Level meshes of a geometric multigrid on the refinement hierarchy (global coarsening; the reference's
+ * level hierarchy of the p4est forest, not a reference interface -- its GLS solver uses ILU / ML-AMG,
+ * gls_navier_stokes.cc:1161-1240): a copy of the forest with every leaf finer than `level` replaced by
+ * its ancestor on `level` (2:1 balance preserved). Free with gls_octree_destroy. */
+int gls_octree_coarsen_to(const gls_octree *tree, int level, gls_octree **out);
+/* Prolongation between two nested octree meshes (coarse = a coarsening of fine): DoF-level CSR over the
+ * fine DoFs, fine DoF i = sum_j P_ij coarse DoF j = the conforming coarse field (hanging nodes from their
+ * lines) interpolated at the fine node; rows of fine hanging DoFs are empty, columns are coarse masters.
+ * off: n_dofs(fine)+1, col / w: nnz; inject: n_dofs(coarse), the fine DoF at each coarse DoF's position.
+ * off == NULL: nnz only. Host arrays; non-periodic. */
+int gls_octree_mg_transfer(const gls_refined_mesh *fine, const gls_refined_mesh *coarse, int64_t *nnz, int64_t *off,
+                           int32_t *col, double *w, int64_t *inject);
 /* The same on mapped (MappingQ) meshes, conforming or adapted: pieces and geometry from
  * gls_fe_space_kelly_faces with nq = n_q + 1 (nqf = nq^(dim-1) points per piece, host arrays),
  * the jump integrals on the device; eta (DEVICE, n_cells) = sqrt(cell_diam/24 * sum of pieces). */

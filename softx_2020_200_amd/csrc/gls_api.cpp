@@ -453,6 +453,16 @@ struct gls_ctx {
       bool two_pass = false;  // the xy tiles of mg_transfer_2pass fit these tables
     };
     std::vector<std::unique_ptr<Taps>> taps;
+    // general hierarchies (gls_mg_attach_transfers): per level pair the prolongation P (fine rows), the
+    // restriction R = P^T (coarse rows) as CSR, and the state injection (coarse DoF <- fine DoF)
+    bool csr = false;
+    struct Csr {
+      DevBuf<int64_t> poff, roff;
+      DevBuf<int32_t> pcol, rcol, inj;
+      DevBuf<double> pw, rw;
+      int64_t nf = 0, nc = 0;
+    };
+    std::vector<std::unique_ptr<Csr>> xfer;
     DevBuf<double> xwork;  // two-pass transfer intermediate (coarse xy x fine z, 4 fields)
     // coarsest level: direct solve with the probed, regularised, inverted Jacobian
     bool direct = false, direct_ok = false;
@@ -1989,6 +1999,15 @@ int mg_from_box(gls_ctx *c, int l, double *loc) {
 
 // injected coarse state (every second lattice node); history likewise
 int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
+  if (c->mg.csr) {  // general hierarchy: the fine value at each coarse DoF's position (hanging values follow)
+    const auto &X = *c->mg.xfer[(size_t)l - 1];
+    HIP_TRY(gls::vec_pack_dofs(fine, X.inj.p, X.nc, coarse, c->stream));
+    gls_ctx *g = c->mg.lev[(size_t)l];
+    if (g->hang.on)
+      HIP_TRY(gls::vec_csr_gather_set(coarse, coarse, g->hang.dof.p, g->hang.off.p, g->hang.master.p, g->hang.w.p,
+                                      (int64_t)g->hang.dof.n, c->stream));
+    return GLS_OK;
+  }
   const double *fb = mg_to_box(c, l - 1, fine, false);
   if (!fb) return set_err(GLS_EHIP, "mg box gather failed");
   HIP_TRY(gls::mg_inject(fb, mg_box_target(c, l, coarse), c->mg.dims[(size_t)l - 1].data(), c->mg.dims[(size_t)l].data(),
@@ -2146,6 +2165,12 @@ int mg_restrict(gls_ctx *c, int l, const double *y, double *bc) {
   auto &mg = c->mg;
   gls_ctx *h = mg.lev[(size_t)l + 1];
   hipStream_t s = c->stream;
+  if (mg.csr) {
+    const auto &X = *mg.xfer[(size_t)l];
+    HIP_TRY(gls::vec_csr_spmv(bc, y, X.roff.p, X.rcol.p, X.rw.p, X.nc, false, s));
+    (void)h;
+    return GLS_OK;
+  }
   const double *yb = mg_to_box(c, l, y, true);
   if (!yb) return set_err(GLS_EHIP, "mg box gather failed");
   {
@@ -2167,12 +2192,18 @@ int mg_restrict(gls_ctx *c, int l, const double *y, double *bc) {
 // y (level l) = P xc (xc on level l+1; its ghost values are imported first); add: y += P xc
 // (single rank, two-pass transfer only: the caller checks mg_prolong_add_ok)
 bool mg_prolong_add_ok(gls_ctx *c, int l) {
+  if (c->mg.csr) return false;  // general hierarchies: P xc, constrained rows zeroed, then added
   return !c->mg.boxed && c->mg.taps[(size_t)l]->two_pass && std::getenv("GLS_MG_NO_FUSE") == nullptr;
 }
 int mg_prolong(gls_ctx *c, int l, double *xc, double *y, bool add = false) {
   auto &mg = c->mg;
   gls_ctx *h = mg.lev[(size_t)l + 1];
   hipStream_t s = c->stream;
+  if (mg.csr) {
+    const auto &X = *mg.xfer[(size_t)l];
+    HIP_TRY(gls::vec_csr_spmv(y, xc, X.poff.p, X.pcol.p, X.pw.p, X.nf, add, s));
+    return GLS_OK;
+  }
   GLS_TRY(dist_import(h, xc));
   const double *xb = mg_to_box(c, l + 1, xc, false);
   if (!xb) return set_err(GLS_EHIP, "mg box gather failed");
@@ -2759,6 +2790,56 @@ int gls_set_lattice(gls_ctx *c, int n1d, const int64_t *l2g) {
   return GLS_OK;
 }
 
+// the sweep parameters, level buffers and the coarsest-level direct solve of an attached hierarchy
+static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
+  auto &mg = c->mg;
+  mg.k = c->k;
+  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : (p->pre_smooth < 0 ? 0 : 2);
+  mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
+  mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
+  mg.omega = p->omega > 0 ? p->omega : 0.6;
+  mg.comega = p->coarse_omega > 0 ? p->coarse_omega : mg.omega;
+  mg.lpre.assign((size_t)p->n_levels, mg.pre);
+  mg.lpost.assign((size_t)p->n_levels, mg.post);
+  if (p->level_sweeps)
+    for (int l = 0; l < p->n_levels; ++l) {
+      if (p->level_sweeps[2 * l] < 0 || p->level_sweeps[2 * l + 1] < 0) return set_err(GLS_EINVAL, "mg: negative level sweeps");
+      mg.lpre[(size_t)l] = p->level_sweeps[2 * l];
+      mg.lpost[(size_t)l] = p->level_sweeps[2 * l + 1];
+    }
+  for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
+  for (int l = 0; l < p->n_levels; ++l)
+    for (int b = 0; b < MB_N; ++b) {
+      mg.bufs.emplace_back(new DevBuf<double>());
+      const bool need = b == MB_BOX ? mg.boxed : (l > 0 || b == MB_Y);
+      if (need) GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
+    }
+  // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
+  {
+    const int64_t nco = mg.lev.back()->n_dofs;
+    const int want = p->coarse_direct;
+    if (want > 0 && (mg.boxed || nco > 8192)) return set_err(GLS_EINVAL, "mg: direct coarse solve needs one GPU, <= 8192 DoFs");
+    mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
+    if (mg.direct) {
+      GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
+      if (std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));  // gj experiments
+      GLS_TRY(mg.ipiv.alloc((size_t)nco));
+      GLS_TRY(mg.info.alloc(1));
+      if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)
+        return set_err(GLS_EHIP, "rocblas_create_handle failed");
+      rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
+      GLS_TRY(mg.unit.alloc((size_t)nco));
+      GLS_TRY(mg.status.alloc(1));
+    }
+  }
+  mg.on = true;
+  mg.dirty = true;
+  // one stream for the whole V-cycle: the coarse levels' kernels are ordered with the transfers
+  for (size_t l = 1; l < mg.lev.size(); ++l)
+    if (mg.lev[l]->stream != c->stream) GLS_TRY(gls_set_stream(mg.lev[l], c->stream));
+  return GLS_OK;
+}
+
 int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   GLS_TRY(check_ctx(c));
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
@@ -2792,27 +2873,6 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.lev.push_back(g);
     mg.dims.push_back(dm);
   }
-  mg.k = c->k;
-  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : (p->pre_smooth < 0 ? 0 : 2);
-  mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
-  mg.csweeps = p->coarse_sweeps > 0 ? p->coarse_sweeps : 30;
-  mg.omega = p->omega > 0 ? p->omega : 0.6;
-  mg.comega = p->coarse_omega > 0 ? p->coarse_omega : mg.omega;
-  mg.lpre.assign((size_t)p->n_levels, mg.pre);
-  mg.lpost.assign((size_t)p->n_levels, mg.post);
-  if (p->level_sweeps)
-    for (int l = 0; l < p->n_levels; ++l) {
-      if (p->level_sweeps[2 * l] < 0 || p->level_sweeps[2 * l + 1] < 0) return set_err(GLS_EINVAL, "mg: negative level sweeps");
-      mg.lpre[(size_t)l] = p->level_sweeps[2 * l];
-      mg.lpost[(size_t)l] = p->level_sweeps[2 * l + 1];
-    }
-  for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
-  for (int l = 0; l < p->n_levels; ++l)
-    for (int b = 0; b < MB_N; ++b) {
-      mg.bufs.emplace_back(new DevBuf<double>());
-      const bool need = b == MB_BOX ? mg.boxed : (l > 0 || b == MB_Y);
-      if (need) GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
-    }
   // 1D transfer taps: fine lattice index i sits at x = i / (2k) coarse cells from the box origin;
   // prolongation interpolates the coarse Qk field of the parent cell (equidistant nodes, k <= 2)
   const int K = c->k;
@@ -2861,30 +2921,66 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
     mg.taps.push_back(std::move(T));
   }
   if (xwork) GLS_TRY(mg.xwork.alloc(xwork));
-  // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
-  {
-    const int64_t nco = mg.lev.back()->n_dofs;
-    const int want = p->coarse_direct;
-    if (want > 0 && (mg.boxed || nco > 8192)) return set_err(GLS_EINVAL, "mg: direct coarse solve needs one GPU, <= 8192 DoFs");
-    mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
-    if (mg.direct) {
-      GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
-      if (std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));  // gj experiments
-      GLS_TRY(mg.ipiv.alloc((size_t)nco));
-      GLS_TRY(mg.info.alloc(1));
-      if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)
-        return set_err(GLS_EHIP, "rocblas_create_handle failed");
-      rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
-      GLS_TRY(mg.unit.alloc((size_t)nco));
-      GLS_TRY(mg.status.alloc(1));
-    }
+  return mg_attach_common(c, p);
+}
+
+int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *const *p_off, const int32_t *const *p_col,
+                            const double *const *p_w, const int64_t *const *inject) {
+  GLS_TRY(check_ctx(c));
+  if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
+  if (!p_off || !p_col || !p_w || !inject) return set_err(GLS_EINVAL, "mg: transfer arrays missing");
+  if (p->mixed_precision) return set_err(GLS_EINVAL, "mg transfers: FP64 smoothing only (per-cell levels)");
+  auto &mg = c->mg;
+  mg = gls_ctx::MG();
+  mg.csr = true;
+  for (int l = 0; l < p->n_levels; ++l) {
+    gls_ctx *g = p->levels[l];
+    if (!g || g->dim != c->dim || g->k != c->k || g->kp != c->kp || g->dist.on)
+      return set_err(GLS_EINVAL, "mg level %d: dimension / order differs from level 0, or distributed", l);
+    mg.lev.push_back(g);
+    mg.dims.push_back({0, 0, 0});
   }
-  mg.on = true;
-  mg.dirty = true;
-  // one stream for the whole V-cycle: the coarse levels' kernels are ordered with the transfers
-  for (size_t l = 1; l < mg.lev.size(); ++l)
-    if (mg.lev[l]->stream != c->stream) GLS_TRY(gls_set_stream(mg.lev[l], c->stream));
-  return GLS_OK;
+  for (int l = 0; l + 1 < p->n_levels; ++l) {
+    const int64_t nf = mg.lev[(size_t)l]->n_dofs, nc = mg.lev[(size_t)l + 1]->n_dofs;
+    const int64_t *off = p_off[l];
+    if (!off || !p_col[l] || !p_w[l] || !inject[l] || off[0] != 0) return set_err(GLS_EINVAL, "mg transfer %d: arrays", l);
+    for (int64_t i = 0; i < nf; ++i)
+      if (off[i + 1] < off[i]) return set_err(GLS_EINVAL, "mg transfer %d: offsets not monotone", l);
+    const int64_t nnz = off[nf];
+    std::vector<int64_t> rcnt((size_t)nc + 1, 0);
+    for (int64_t j = 0; j < nnz; ++j) {
+      if (p_col[l][j] < 0 || p_col[l][j] >= nc) return set_err(GLS_EINVAL, "mg transfer %d: column out of range", l);
+      ++rcnt[(size_t)p_col[l][j] + 1];
+    }
+    for (int64_t j = 0; j < nc; ++j) rcnt[(size_t)j + 1] += rcnt[(size_t)j];
+    // R = P^T, each coarse row's terms in ascending fine row order (deterministic sums)
+    std::vector<int32_t> rcol((size_t)nnz);
+    std::vector<double> rw((size_t)nnz);
+    std::vector<int64_t> fill(rcnt.begin(), rcnt.end() - 1);
+    for (int64_t i = 0; i < nf; ++i)
+      for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+        const int64_t slot = fill[(size_t)p_col[l][j]]++;
+        rcol[(size_t)slot] = (int32_t)i;
+        rw[(size_t)slot] = p_w[l][j];
+      }
+    std::vector<int32_t> inj((size_t)nc);
+    for (int64_t j = 0; j < nc; ++j) {
+      if (inject[l][j] < 0 || inject[l][j] >= nf) return set_err(GLS_EINVAL, "mg transfer %d: injection out of range", l);
+      inj[(size_t)j] = (int32_t)inject[l][j];
+    }
+    std::unique_ptr<gls_ctx::MG::Csr> X(new gls_ctx::MG::Csr);
+    X->nf = nf;
+    X->nc = nc;
+    GLS_TRY(X->poff.upload(off, (size_t)nf + 1));
+    GLS_TRY(X->pcol.upload(p_col[l], (size_t)std::max<int64_t>(nnz, 1)));
+    GLS_TRY(X->pw.upload(p_w[l], (size_t)std::max<int64_t>(nnz, 1)));
+    GLS_TRY(X->roff.upload(rcnt.data(), rcnt.size()));
+    GLS_TRY(X->rcol.upload(rcol.data(), std::max<size_t>(rcol.size(), 1)));
+    GLS_TRY(X->rw.upload(rw.data(), std::max<size_t>(rw.size(), 1)));
+    GLS_TRY(X->inj.upload(inj.data(), inj.size()));
+    mg.xfer.push_back(std::move(X));
+  }
+  return mg_attach_common(c, p);
 }
 
 int gls_mg_set_coarse_replica(gls_ctx *c, gls_ctx *replica, int64_t n_local, const int64_t *local_to_replica) {

@@ -911,4 +911,190 @@ int gls_octree_faces(const gls_refined_mesh *m, int64_t *n_faces, int32_t *fa, i
   return GLS_OK;
 }
 
+// Level meshes of a multigrid on the refinement hierarchy (global coarsening): the forest with every leaf
+// finer than `level` replaced by its ancestor on `level`. Truncation keeps the vertex 2:1 balance (two
+// truncated leaves that touch have ancestors-or-selves that touched, whose levels differed by <= 1).
+int gls_octree_coarsen_to(const gls_octree *t, int level, gls_octree **out) {
+  if (!t || !out || level < 0) return gls_io_set_error(GLS_EINVAL, "gls_octree_coarsen_to: bad arguments");
+  auto r = std::make_unique<gls_octree>(*t);
+  r->leaves.clear();
+  std::map<std::array<int64_t, 4>, char> seen;
+  for (const Leaf &c : t->leaves) {
+    Leaf a = c;
+    if (a.level > level) {
+      for (int d = 0; d < t->dim; ++d) a.x[d] >>= (a.level - level);
+      a.level = level;
+    }
+    if (seen.emplace(std::array<int64_t, 4>{a.level, a.x[0], a.x[1], a.x[2]}, 1).second) r->leaves.push_back(a);
+  }
+  sort_leaves(*r);
+  *out = r.release();
+  return GLS_OK;
+}
+
+// Grid transfer between two nested octree meshes of the same cube (coarse = a coarsening of fine, e.g.
+// gls_octree_coarsen_to): the prolongation P as a DoF-level CSR over the fine DoFs ([velocity node-major |
+// pressure]), fine DoF i = sum_j P_ij coarse DoF j -- the coarse FE field (its hanging nodes replaced by
+// their lines, so a conforming field) evaluated at the fine node: the Qk interpolant of the coarse cell
+// holding it, in exact lattice arithmetic. Rows of fine hanging DoFs are empty (their values follow from
+// the fine lines); columns are coarse masters only. inject[j] = the fine DoF at coarse DoF j's position
+// (the state injection of the coarse levels). Call with off == NULL for nnz only. Non-periodic meshes.
+int gls_octree_mg_transfer(const gls_refined_mesh *fm, const gls_refined_mesh *cm, int64_t *nnz, int64_t *off,
+                           int32_t *col, double *w, int64_t *inject) {
+  if (!fm || !cm || !nnz || fm->dim != cm->dim || fm->k != cm->k || fm->kp != cm->kp)
+    return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: incompatible meshes");
+  const MeshImpl *F = static_cast<const MeshImpl *>(fm->impl_), *Cm = static_cast<const MeshImpl *>(cm->impl_);
+  if (F->n != Cm->n || F->lo != Cm->lo || F->hi != Cm->hi || F->pmask || Cm->pmask || Cm->L > F->L)
+    return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: not nested meshes of one cube (or periodic)");
+  const int dim = fm->dim;
+  const int64_t Nc = (int64_t)Cm->n << Cm->L;  // coarse-finest cells per direction
+  int64_t tot = 1;
+  for (int d = 0; d < dim; ++d) tot *= Nc;
+  if (tot > ((int64_t)1 << 28)) return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: grid too large");
+  const double hff = (F->hi - F->lo) / ((double)F->n * (double)((int64_t)1 << F->L));  // fine-finest cell
+  std::vector<int64_t> rows_v, rows_p;                                                  // per space
+  std::vector<int32_t> cols_acc;
+  std::vector<double> w_acc;
+  std::vector<int64_t> row_off{0};
+  const int64_t nvf = fm->n_vnodes, nvc = cm->n_vnodes;
+  std::vector<int64_t> inj((size_t)(dim * nvc + cm->n_pnodes), -1);
+  for (int sp = 0; sp < 2; ++sp) {
+    const bool vel = sp == 0;
+    const int kk = vel ? fm->k : fm->kp, K1 = kk + 1;
+    int npc = 1;
+    for (int d = 0; d < dim; ++d) npc *= K1;
+    const double u = hff / kk;                                    // fine lattice spacing of this space
+    const int64_t sc = (int64_t)kk << (F->L - Cm->L);              // coarse-finest cell in lattice units
+    auto lattice = [&](const double *x, int64_t *p) {
+      for (int d = 0; d < dim; ++d) p[d] = (int64_t)std::llround((x[d] - F->lo) / u);
+    };
+    // coarse cells: integer boxes, owner grid at the coarse-finest resolution
+    std::vector<int32_t> owner((size_t)tot, -1);
+    std::vector<std::array<int64_t, 4>> cbox((size_t)cm->n_cells);  // origin[3], size
+    for (int64_t c = 0; c < cm->n_cells; ++c) {
+      int64_t o[3] = {0, 0, 0};
+      lattice(cm->cell_x0 + c * dim, o);
+      const int64_t S = (int64_t)std::llround(cm->cell_h[c * dim] / u);
+      cbox[(size_t)c] = {o[0], o[1], o[2], S};
+      const int64_t s = S / sc;
+      int64_t nb = 1;
+      for (int d = 0; d < dim; ++d) nb *= s;
+      for (int64_t b = 0; b < nb; ++b) {
+        int64_t r = b, id = 0, st = 1;
+        for (int d = 0; d < dim; ++d) {
+          id += (o[d] / sc + r % s) * st;
+          r /= s;
+          st *= Nc;
+        }
+        owner[(size_t)id] = (int32_t)c;
+      }
+    }
+    // hanging lines (node level) of both meshes
+    const int64_t nh_c = vel ? cm->n_vhang : cm->n_phang, nh_f = vel ? fm->n_vhang : fm->n_phang;
+    const int64_t *hc_node = vel ? cm->vhang_node : cm->phang_node, *hc_off = vel ? cm->vhang_off : cm->phang_off;
+    const int64_t *hc_mas = vel ? cm->vhang_master : cm->phang_master;
+    const double *hc_w = vel ? cm->vhang_w : cm->phang_w;
+    const int64_t *hf_node = vel ? fm->vhang_node : fm->phang_node;
+    std::unordered_map<int64_t, int64_t> cline;  // coarse hanging node -> line index
+    for (int64_t i = 0; i < nh_c; ++i) cline[hc_node[i]] = i;
+    const int64_t nnf = vel ? nvf : fm->n_pnodes, nnc = vel ? nvc : cm->n_pnodes;
+    std::vector<char> fhang((size_t)nnf, 0);
+    for (int64_t i = 0; i < nh_f; ++i) fhang[(size_t)hf_node[i]] = 1;
+    const double *fx = vel ? fm->vnode_x : fm->pnode_x, *cx = vel ? cm->vnode_x : cm->pnode_x;
+    const int32_t *cnodes = vel ? cm->cell_vnodes : cm->cell_pnodes;
+    // fine lattice position -> fine node (injection)
+    std::unordered_map<int64_t, int64_t> fpos;
+    fpos.reserve((size_t)nnf);
+    const int64_t span = kk * ((int64_t)F->n << F->L) + 1;
+    auto key = [&](const int64_t *p) {
+      int64_t k = 0, st = 1;
+      for (int d = 0; d < dim; ++d) {
+        k += p[d] * st;
+        st *= span;
+      }
+      return k;
+    };
+    for (int64_t v = 0; v < nnf; ++v) {
+      int64_t p[3] = {0, 0, 0};
+      lattice(fx + v * dim, p);
+      fpos[key(p)] = v;
+    }
+    for (int64_t j = 0; j < nnc; ++j) {
+      int64_t p[3] = {0, 0, 0};
+      lattice(cx + j * dim, p);
+      auto it = fpos.find(key(p));
+      if (it == fpos.end()) return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: coarse node %lld not a fine node",
+                                                    (long long)j);
+      if (vel)
+        for (int c = 0; c < dim; ++c) inj[(size_t)(j * dim + c)] = it->second * dim + c;
+      else
+        inj[(size_t)(dim * nvc + j)] = dim * nvf + it->second;
+    }
+    std::vector<std::pair<int32_t, double>> acc;
+    for (int64_t v = 0; v < nnf; ++v) {
+      acc.clear();
+      if (!fhang[(size_t)v]) {
+        int64_t p[3] = {0, 0, 0}, id = 0, st = 1;
+        lattice(fx + v * dim, p);
+        for (int d = 0; d < dim; ++d) {
+          id += std::min(p[d] / sc, Nc - 1) * st;
+          st *= Nc;
+        }
+        const int32_t c = owner[(size_t)id];
+        if (c < 0) return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: fine node outside the coarse mesh");
+        const auto &B = cbox[(size_t)c];
+        double xi[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) xi[d] = (double)(p[d] - B[d]) / (double)B[3];
+        for (int a = 0; a < npc; ++a) {
+          double wa = 1.0;
+          int r = a;
+          for (int d = 0; d < dim; ++d) {
+            wa *= lagrange(kk, r % K1, xi[d]);
+            r /= K1;
+          }
+          if (std::fabs(wa) < 1e-14) continue;
+          const int32_t cn = cnodes[(size_t)c * npc + a];
+          auto it = cline.find(cn);
+          if (it == cline.end()) {
+            acc.push_back({cn, wa});
+          } else {
+            for (int64_t q = hc_off[it->second]; q < hc_off[it->second + 1]; ++q)
+              acc.push_back({(int32_t)hc_mas[q], wa * hc_w[q]});
+          }
+        }
+        std::sort(acc.begin(), acc.end(), [](const std::pair<int32_t, double> &x, const std::pair<int32_t, double> &y) {
+          return x.first < y.first;
+        });
+        size_t m = 0;  // merge duplicate masters (fixed order: ascending node, then the order of the terms)
+        for (size_t i = 0; i < acc.size(); ++i) {
+          if (m > 0 && acc[m - 1].first == acc[i].first) acc[m - 1].second += acc[i].second;
+          else acc[m++] = acc[i];
+        }
+        acc.resize(m);
+        acc.erase(std::remove_if(acc.begin(), acc.end(), [](const std::pair<int32_t, double> &e) {
+                    return std::fabs(e.second) < 1e-14;
+                  }),
+                  acc.end());
+      }
+      const int nrow = vel ? dim : 1;
+      for (int c = 0; c < nrow; ++c) {
+        for (auto &e : acc) {
+          cols_acc.push_back(vel ? (int32_t)(e.first * dim + c) : (int32_t)(dim * nvc + e.first));
+          w_acc.push_back(e.second);
+        }
+        row_off.push_back((int64_t)cols_acc.size());
+      }
+    }
+  }
+  *nnz = (int64_t)cols_acc.size();
+  if (off) {
+    if (!col || !w) return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: col / w missing");
+    std::memcpy(off, row_off.data(), sizeof(int64_t) * row_off.size());
+    std::memcpy(col, cols_acc.data(), sizeof(int32_t) * cols_acc.size());
+    std::memcpy(w, w_acc.data(), sizeof(double) * w_acc.size());
+  }
+  if (inject) std::memcpy(inject, inj.data(), sizeof(int64_t) * inj.size());
+  return GLS_OK;
+}
+
 }  // extern "C"

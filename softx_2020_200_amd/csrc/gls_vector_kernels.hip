@@ -163,6 +163,16 @@ __global__ void k_csr_gather_set(double *x, const double *src, const int64_t *__
     x[dof[i]] = s;
   }
 }
+// y = A x (add: y += A x) for a CSR matrix A of n rows: the multigrid transfers of general hierarchies
+// (prolongation P and restriction P^T). One thread per row, terms in stored order (deterministic).
+__global__ void k_csr_spmv(double *__restrict__ y, const double *__restrict__ x, const int64_t *__restrict__ off,
+                           const int32_t *__restrict__ col, const double *__restrict__ w, int64_t n, int add) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.;
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) s += w[j] * x[col[j]];
+    y[i] = add ? y[i] + s : s;
+  }
+}
 // condensation onto masters: y[tm[i]] += sum_{j in [toff[i], toff[i+1])} tw[j] * y[tdof[j]]
 // (one thread per master, fixed order: deterministic)
 __global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const int64_t *__restrict__ toff,
@@ -346,6 +356,12 @@ hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, 
                               const int64_t *master, const double *w, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_csr_gather_set, dim3(grid_for(n)), dim3(kBlock), 0, s, x, src, dof, off, master, w, n);
+  return hipGetLastError();
+}
+hipError_t vec_csr_spmv(double *y, const double *x, const int64_t *off, const int32_t *col, const double *w, int64_t n,
+                        bool add, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(n)), dim3(kBlock), 0, s, y, x, off, col, w, n, add ? 1 : 0);
   return hipGetLastError();
 }
 hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,

@@ -43,6 +43,7 @@ EXPORTS = [
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
     "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
     "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals", "gls_fe_space_boundary_normal_sets",
+    "gls_octree_coarsen_to", "gls_octree_mg_transfer", "gls_mg_attach_transfers",
 ]
 
 
@@ -165,6 +166,11 @@ def load():
     L.gls_mg_attach.argtypes = [vp, C.POINTER(MGParams)]
     L.gls_mg_detach.argtypes = [vp]
     L.gls_mg_set_coarse_replica.argtypes = [vp, vp, i64, C.POINTER(i64)]
+    L.gls_mg_attach_transfers.argtypes = [vp, C.POINTER(MGParams), C.POINTER(C.POINTER(i64)),
+                                          C.POINTER(C.POINTER(C.c_int32)), C.POINTER(C.POINTER(C.c_double)),
+                                          C.POINTER(C.POINTER(i64))]
+    L.gls_octree_coarsen_to.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.gls_octree_mg_transfer.argtypes = [C.POINTER(RefinedMesh), C.POINTER(RefinedMesh), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
     L.gls_mg_transfer.argtypes = [vp, C.c_int, C.c_int, vp, vp]
@@ -329,6 +335,15 @@ class Octree:
         if getattr(self, "h", None):
             self.L.gls_octree_destroy(self.h)
 
+    def coarsen_to(self, level):
+        """The forest with every leaf finer than `level` replaced by its ancestor on `level`
+        (gls_octree_coarsen_to): a level mesh of the multigrid on the refinement hierarchy."""
+        out = Octree.__new__(Octree)
+        out.L, out.dim, out.n, out.lo, out.hi = self.L, self.dim, self.n, self.lo, self.hi
+        out.h = C.c_void_p()
+        check(self.L.gls_octree_coarsen_to(self.h, int(level), C.byref(out.h)), "gls_octree_coarsen_to")
+        return out
+
     def set_periodic(self, mask):
         """periodic directions (bit d), before adapting: neighbourhoods wrap, mesh() identifies the faces"""
         check(self.L.gls_octree_set_periodic(self.h, int(mask)), "gls_octree_set_periodic")
@@ -404,6 +419,25 @@ class Octree:
             return _refined_mesh_dict(pm, self.dim, k, kp)
         finally:
             self.free_mesh_handle(pm)
+
+
+def octree_mg_transfer(fine_handle, coarse_handle):
+    """Prolongation CSR (off, col, w) over the fine DoFs and the state injection (coarse DoF -> fine DoF)
+    between two nested octree meshes (gls_octree_mg_transfer; handles from Octree.mesh_handle)."""
+    L = load()
+    nnz = C.c_int64()
+    check(L.gls_octree_mg_transfer(fine_handle, coarse_handle, C.byref(nnz), None, None, None, None),
+          "gls_octree_mg_transfer")
+    f, c = fine_handle.contents, coarse_handle.contents
+    nf = f.dim * f.n_vnodes + f.n_pnodes
+    nc = c.dim * c.n_vnodes + c.n_pnodes
+    off = np.zeros(nf + 1, np.int64)
+    col = np.zeros(max(nnz.value, 1), np.int32)
+    w = np.zeros(max(nnz.value, 1))
+    inj = np.zeros(nc, np.int64)
+    check(L.gls_octree_mg_transfer(fine_handle, coarse_handle, C.byref(nnz), off.ctypes.data, col.ctypes.data,
+                                   w.ctypes.data, inj.ctypes.data), "gls_octree_mg_transfer")
+    return off, col[:nnz.value], w[:nnz.value], inj
 
 
 def octree_transfer(old_handle, new_handle, vec, n_new):
@@ -714,6 +748,35 @@ class GLSContext:
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
                      coarse_omega, coarse_direct, int(mixed_precision), ls)
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
+        self._mg_levels = levels
+
+    def attach_multigrid_transfers(self, coarse_levels, transfers, pre_smooth=2, post_smooth=2, coarse_sweeps=30,
+                                   omega=0.6, coarse_omega=0.0, coarse_direct=0, level_sweeps=None):
+        """The V-cycle on a general hierarchy (gls_mg_attach_transfers): levels [self] + coarse_levels
+        (hanging lines set on each), transfers[l] = (off, col, w, inject) from level l+1 to level l
+        (octree_mg_transfer). FP64 smoothing."""
+        levels = [self] + list(coarse_levels)
+        if len(transfers) != len(levels) - 1:
+            raise GLSError("attach_multigrid_transfers: one transfer per level pair")
+        arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
+        ls = None
+        if level_sweeps:
+            pre0 = pre_smooth if pre_smooth > 0 else (0 if pre_smooth < 0 else 2)
+            post0 = post_smooth if post_smooth >= 0 else 2
+            flat = [pre0, post0] * len(levels)
+            for lv, (a, b) in level_sweeps.items():
+                flat[2 * (lv % len(levels))], flat[2 * (lv % len(levels)) + 1] = a, b
+            ls = (C.c_int * len(flat))(*flat)
+        keep = [(np.ascontiguousarray(o, np.int64), np.ascontiguousarray(c, np.int32), np.ascontiguousarray(w, np.float64),
+                 np.ascontiguousarray(j, np.int64)) for o, c, w, j in transfers]
+        P64, P32, PD = C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.POINTER(C.c_double)
+        offs = (P64 * len(keep))(*[k[0].ctypes.data_as(P64) for k in keep])
+        cols = (P32 * len(keep))(*[k[1].ctypes.data_as(P32) for k in keep])
+        ws = (PD * len(keep))(*[k[2].ctypes.data_as(PD) for k in keep])
+        injs = (P64 * len(keep))(*[k[3].ctypes.data_as(P64) for k in keep])
+        p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
+                     coarse_omega, coarse_direct, 0, ls)
+        check(self.L.gls_mg_attach_transfers(self.h, C.byref(p), offs, cols, ws, injs), "gls_mg_attach_transfers")
         self._mg_levels = levels
 
     def set_coarse_replica(self, replica, local_to_replica):
