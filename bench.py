@@ -286,10 +286,85 @@ def bench_cylinder3d(args):
     print(json.dumps(out))
 
 
+def bench_octree(args):
+    """--workload octree: the lid-driven cavity on an adapted octree forest (hanging-node constraints;
+    base --cells^3, --octree-steps levels of lid / edge refinement, softx_2020_200_amd.problem.octree_lid_tree),
+    Q2-Q2 BDF2, one Newton iteration per step: residual + diagonal, preconditioner setup, GMRES(--restart) to
+    rel 1e-4, line search. --precond mg: the V-cycle on the refinement hierarchy (gls_mg_attach_transfers;
+    per-cell FP64 smoothing on the hanging levels, exact LU on the uniform level 0); --precond ilu: the
+    assembled multicolor ILU(0) (the adaptive path's default before)."""
+    import torch
+    from softx_2020_200_amd.problem import AdaptiveCavityProblem, octree_lid_tree
+    dev = torch.device("cuda", 0)
+    tree = octree_lid_tree(args.n, args.octree_steps)
+    mg = args.precond == "mg"
+    prob = AdaptiveCavityProblem(tree, k=args.k, kp=args.kp, viscosity=args.nu, multigrid=mg,
+                                 pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
+                                 coarse_direct=1)
+    ctx = prob.ctx
+    if not mg:
+        ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
+    ctx.set_time("bdf2", (args.dt,) * 4)
+    X = prob.mesh["vnode_x"]
+    vel = np.zeros((len(X), 3))
+    vel[:, 0] = ((X[:, 1] + 1.0) / 2.0) ** 2 * (1.0 - X[:, 0] ** 2) * (1.0 - X[:, 2] ** 2)
+    vel[:, 1] = 0.1 * np.sin(np.pi * X[:, 0]) * (1.0 - X[:, 1] ** 2)
+    m1 = torch.from_numpy(np.concatenate([vel.reshape(-1), np.zeros(prob.mesh["n_pnodes"])])).to(dev)
+    ctx.apply_dirichlet(m1)
+    m2 = m1.clone()
+    present = m1.clone()
+
+    def one_step():
+        present.copy_(m1)
+        return ctx.newton(present, m1, m2, tolerance=1e-30, max_iterations=1, lin_max_iterations=args.lin_max,
+                          restart=args.restart, relative_residual=args.rel, minimum_residual=1e-12)
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [one_step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ctx.set_state(present, m1, m2)
+    v = torch.rand(ctx.n_dofs, dtype=torch.float64, device=dev)
+    y = torch.empty_like(v)
+    ctx.jacobian_apply(v, y)
+    ctx.timing(True)
+    for _ in range(args.jv_reps):
+        ctx.jacobian_apply(v, y)
+    jv_ms, jv_n = ctx.timing_get(1)
+    ctx.timing(False)
+    N, nc = ctx.n_dofs, prob.mesh["n_cells"]
+    # algorithmic bytes of one per-cell J.v launch on box cells (gls_cell_kernel MODE_JV): v and u (8N
+    # each), node maps (4 B x 2 x 27 per cell), the cell box (48 B), the element vectors (8 B x 4 x 27)
+    B = 16 * N + 4 * nc * 54 + 48 * nc + 8 * nc * 4 * 27
+    ms = jv_ms / max(jv_n, 1)
+    its_per_s = args.steps / el
+    lev = [int(v_) for v_ in np.bincount(prob.mesh["cell_level"])]
+    out = {
+        "metric": "nonlinear iters/sec (3D lid-driven cavity, adapted octree, Q%d-Q%d, BDF2)" % (args.k, args.kp),
+        "value": its_per_s, "unit": "nonlinear_iters/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (smooth lid-driven profile, prm-style boundary values)",
+        "config": {"workload": "cavity on an adapted octree: base %d^3, %d lid/edge refinement levels "
+                               "(hanging-node constraints), nu %g, BDF2 dt %g" % (args.n, args.octree_steps, args.nu, args.dt),
+                   "n_dofs": N, "n_cells": nc, "cells_per_level": lev,
+                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels), rel %g"
+                                     % (args.restart, args.mg_smooth[0], args.mg_smooth[1], len(prob.levels), args.rel))
+                   if mg else "GMRES(%d)+ILU(0) multicolor, rel %g" % (args.restart, args.rel)},
+        "mdof_per_s": N * its_per_s / 1e6,
+        "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
+        "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,2,3,MODE_JV>", "achieved": B / (ms * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": B, "launch_ms": ms},
+    }
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="cavity", choices=["cavity", "cylinder3d"],
+    ap.add_argument("--workload", default="cavity", choices=["cavity", "cylinder3d", "octree"],
                     help="cavity: the BASELINE metric (configs[1] / [2]); cylinder3d: configs[4]'s adaptive-path "
                          "problem on one GPU (per-cell mapped kernels + ILU-GMRES)")
     ap.add_argument("--steps", type=int, default=3)
@@ -305,7 +380,8 @@ def main():
     ap.add_argument("--restart", type=int, default=30)
     ap.add_argument("--ilu-fill", type=int, default=0, help="cylinder3d: ILU level of fill (0: multicolor order)")
     ap.add_argument("--rel", type=float, default=1e-4)
-    ap.add_argument("--precond", default="mg", choices=["mg", "jacobi"],
+    ap.add_argument("--octree-steps", type=int, default=3, help="octree: lid / edge refinement levels")
+    ap.add_argument("--precond", default="mg", choices=["mg", "jacobi", "ilu"],
                     help="GMRES right preconditioner: geometric multigrid V-cycle (default) or Jacobi")
     ap.add_argument("--mg-coarsest", type=int, default=0,
                     help="cells per direction of the coarsest level (0: 2 on one GPU -- exact LU solve of its "
@@ -340,10 +416,10 @@ def main():
     args = ap.parse_args()
     if args.dist_backend == "gloo":  # host-staged testing transport: no RCCL communicator
         args.dist_impl = "torch"
-    if args.workload == "cylinder3d":
+    if args.workload in ("cylinder3d", "octree"):
         import torch
         torch.cuda.set_device(0)
-        return bench_cylinder3d(args)
+        return bench_cylinder3d(args) if args.workload == "cylinder3d" else bench_octree(args)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))

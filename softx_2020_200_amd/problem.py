@@ -95,3 +95,88 @@ class CavityProblem:
                 m //= 2
                 self.levels.append(CavityProblem(dim, m, k, kp, viscosity, stream))
             self.ctx.attach_multigrid([lv.ctx for lv in self.levels], **mg_opts)
+
+
+def octree_lid_tree(n=4, steps=3, dim=3):
+    """An adapted forest for the cavity: `steps` refinements of the cells next to the lid (y = +1) and
+    its two upper edges, each step one level deeper and one half thinner (a Kelly-like boundary-layer
+    grading: gls_octree_adapt with the vertex 2:1 balance)."""
+    from .native import Octree
+    t = Octree(dim, n)
+    for s in range(steps):
+        lev, x0, h = t.cells()
+        c = x0 + 0.5 * h
+        band = 1.0 - 2.0 ** -s
+        near = (c[:, 1] > band) | ((c[:, 1] > 0.0) & (np.abs(c[:, 0]) > band))
+        t.adapt(refine=near.astype(np.int32), max_level=s + 1)
+    return t
+
+
+def octree_dirichlet(mesh, lo=-1.0, hi=1.0):
+    """CavityProblem's boundary conditions on an octree mesh (walls noslip, lid y = hi u = (1, 0, 0),
+    wall edges keep u = 0): (vnode_mask, dofs, values); hanging nodes carry no mask bit (their lines
+    give their values)."""
+    dim, X = mesh["dim"], mesh["vnode_x"]
+    tol = 1e-12 * (hi - lo)
+    on = [(np.abs(X[:, d] - lo) < tol, np.abs(X[:, d] - hi) < tol) for d in range(dim)]
+    wall = np.zeros(len(X), bool)
+    for d in range(dim):
+        wall |= on[d][0] | (on[d][1] if d != 1 else False)
+    lid = on[1][1] & ~wall
+    bnd = wall | lid
+    hang = np.zeros(len(X), bool)
+    hang[mesh["vhang"][0]] = True
+    bnd &= ~hang
+    mask = np.where(bnd, (1 << dim) - 1, 0).astype(np.uint8)
+    nodes = np.nonzero(bnd)[0]
+    dofs = (nodes[:, None] * dim + np.arange(dim)[None]).reshape(-1).astype(np.int64)
+    vals = np.zeros((len(nodes), dim))
+    vals[lid[nodes], 0] = 1.0
+    return mask, dofs, vals.reshape(-1)
+
+
+class AdaptiveCavityProblem:
+    """CavityProblem's lid-driven cavity on an adapted octree forest (hanging-node constraints,
+    gls_set_hanging; per-cell kernels). multigrid=True: the GMRES preconditioner is the V-cycle on the
+    refinement hierarchy (gls_mg_attach_transfers) -- levels = the forest coarsened one level at a time
+    (gls_octree_coarsen_to), transfers = gls_octree_mg_transfer, and the uniform level-0 mesh as the
+    brick context of a CavityProblem (the same lexicographic node numbering) with an exact LU solve."""
+
+    def __init__(self, tree, k=2, kp=None, viscosity=0.01, stream=None, multigrid=False, **mg_opts):
+        from .native import hanging_dof_lines, octree_mg_transfer
+        kp = k if kp is None else kp
+        self.dim, self.k, self.kp, self.tree = tree.dim, k, kp, tree
+        L = tree.max_level
+        self.trees = [tree.coarsen_to(L - l) for l in range(L + 1)] if multigrid else [tree]
+        self.levels, self.meshes = [], []
+        for l, t in enumerate(self.trees):
+            mesh = t.mesh(k, kp)
+            self.meshes.append(mesh)
+            lines = hanging_dof_lines(mesh)
+            if multigrid and l == len(self.trees) - 1 and len(lines[0]) == 0:
+                base = CavityProblem(tree.dim, tree.n, k, kp, viscosity, stream)
+                nx = k * tree.n + 1
+                idx = np.indices((nx,) * tree.dim).reshape(tree.dim, -1)[::-1].T
+                if not np.allclose(mesh["vnode_x"], -1.0 + idx * (2.0 / (k * tree.n)), atol=1e-13):
+                    raise RuntimeError("level-0 numbering differs from the hyper_cube's")
+                self.levels.append(base.ctx)
+                continue
+            mask, dofs, vals = octree_dirichlet(mesh)
+            ctx = build_context(mesh, viscosity=viscosity, vnode_mask=mask, stream=stream)
+            if len(lines[0]):
+                ctx.set_hanging(*lines)
+            ctx.set_dirichlet(dofs, vals)
+            self.levels.append(ctx)
+        self.ctx = self.levels[0]
+        self.mesh = self.meshes[0]
+        self.n_dofs = self.ctx.n_dofs
+        if multigrid:
+            xfer = []
+            for l in range(len(self.trees) - 1):
+                hf, hc = self.trees[l].mesh_handle(k, kp), self.trees[l + 1].mesh_handle(k, kp)
+                try:
+                    xfer.append(octree_mg_transfer(hf, hc))
+                finally:
+                    self.trees[l].free_mesh_handle(hf)
+                    self.trees[l + 1].free_mesh_handle(hc)
+            self.ctx.attach_multigrid_transfers(self.levels[1:], xfer, **mg_opts)
