@@ -944,10 +944,12 @@ int gls_octree_mg_transfer(const gls_refined_mesh *fm, const gls_refined_mesh *c
   if (!fm || !cm || !nnz || fm->dim != cm->dim || fm->k != cm->k || fm->kp != cm->kp)
     return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: incompatible meshes");
   const MeshImpl *F = static_cast<const MeshImpl *>(fm->impl_), *Cm = static_cast<const MeshImpl *>(cm->impl_);
-  if (F->n != Cm->n || F->lo != Cm->lo || F->hi != Cm->hi || F->pmask || Cm->pmask || Cm->L > F->L)
+  // nested: the coarse mesh's finest cells are unions of the fine mesh's finest cells (the two forests may
+  // have different level-0 grids, e.g. a uniform level below an adapted forest's base)
+  const int64_t Nf = (int64_t)F->n << F->L, Nc = (int64_t)Cm->n << Cm->L;  // finest cells per direction
+  if (F->lo != Cm->lo || F->hi != Cm->hi || F->pmask || Cm->pmask || Nf % Nc != 0)
     return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: not nested meshes of one cube (or periodic)");
   const int dim = fm->dim;
-  const int64_t Nc = (int64_t)Cm->n << Cm->L;  // coarse-finest cells per direction
   int64_t tot = 1;
   for (int d = 0; d < dim; ++d) tot *= Nc;
   if (tot > ((int64_t)1 << 28)) return gls_io_set_error(GLS_EINVAL, "gls_octree_mg_transfer: grid too large");
@@ -964,7 +966,7 @@ int gls_octree_mg_transfer(const gls_refined_mesh *fm, const gls_refined_mesh *c
     int npc = 1;
     for (int d = 0; d < dim; ++d) npc *= K1;
     const double u = hff / kk;                                    // fine lattice spacing of this space
-    const int64_t sc = (int64_t)kk << (F->L - Cm->L);              // coarse-finest cell in lattice units
+    const int64_t sc = (int64_t)kk * (Nf / Nc);                    // coarse-finest cell in lattice units
     auto lattice = [&](const double *x, int64_t *p) {
       for (int d = 0; d < dim; ++d) p[d] = (int64_t)std::llround((x[d] - F->lo) / u);
     };

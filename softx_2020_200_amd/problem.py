@@ -97,18 +97,24 @@ class CavityProblem:
             self.ctx.attach_multigrid([lv.ctx for lv in self.levels], **mg_opts)
 
 
-def octree_lid_tree(n=4, steps=3, dim=3):
-    """An adapted forest for the cavity: `steps` refinements of the cells next to the lid (y = +1) and
-    its two upper edges, each step one level deeper and one half thinner (a Kelly-like boundary-layer
-    grading: gls_octree_adapt with the vertex 2:1 balance)."""
+def octree_lid_tree(n=4, steps=3, dim=3, base=2):
+    """An adapted forest for the cavity: n^dim cells (a base^dim forest refined globally to n per
+    direction, so the multigrid hierarchy reaches down to base^dim cells), then `steps` refinements of
+    the cells next to the lid (y = +1) and its two upper edges, each step one level deeper and one half
+    thinner (a Kelly-like boundary-layer grading: gls_octree_adapt with the vertex 2:1 balance)."""
     from .native import Octree
-    t = Octree(dim, n)
+    base = base if n % base == 0 and (n // base) & (n // base - 1) == 0 else n
+    t = Octree(dim, base)
+    g = 0
+    while base << g < n:
+        t.adapt(refine=np.ones(t.n_cells, np.int32))
+        g += 1
     for s in range(steps):
         lev, x0, h = t.cells()
         c = x0 + 0.5 * h
         band = 1.0 - 2.0 ** -s
         near = (c[:, 1] > band) | ((c[:, 1] > 0.0) & (np.abs(c[:, 0]) > band))
-        t.adapt(refine=near.astype(np.int32), max_level=s + 1)
+        t.adapt(refine=near.astype(np.int32), max_level=g + s + 1)
     return t
 
 

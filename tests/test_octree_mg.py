@@ -103,3 +103,24 @@ def test_mg_transfer_reproduces_qk(dim, k, kp, gap):
     assert np.abs(np.asarray(P.sum(1)).ravel()[rows] - 1.0).max() < 1e-12
     # injection: the coincident fine DoF
     assert np.abs(uf[inj] - uc).max() < 1e-12 * max(1.0, np.abs(uf).max())
+
+
+@pytest.mark.parametrize("dim,k", [(2, 2), (3, 2), (3, 1)])
+def test_mg_transfer_below_the_base(dim, k):
+    """a uniform level below an adapted forest's level-0 grid (two forests, bases 4 and 2): the
+    transfer between the base-4 level-0 mesh and the 2^dim mesh is the same exact interpolation"""
+    fine, coarse = sx.Octree(dim, 4), sx.Octree(dim, 2)
+    hf, hc = fine.mesh_handle(k, k), coarse.mesh_handle(k, k)
+    try:
+        off, col, w, inj = sx.octree_mg_transfer(hf, hc)
+    finally:
+        fine.free_mesh_handle(hf)
+        coarse.free_mesh_handle(hc)
+    mf, mc = fine.mesh(k, k), coarse.mesh(k, k)
+    nf, nc = dim * mf["n_vnodes"] + mf["n_pnodes"], dim * mc["n_vnodes"] + mc["n_pnodes"]
+    rng = np.random.default_rng(SEED + 11 * dim + k)
+    cv, cp = rng.normal(size=(dim,) + (k + 1,) * dim), rng.normal(size=(k + 1,) * dim)
+    uf, uc = field(mf, dim, k, k, cv, cp), field(mc, dim, k, k, cv, cp)
+    P = sps.csr_matrix((w, col, off), shape=(nf, nc))
+    assert np.abs(P @ uc - uf).max() < 1e-11 * max(1.0, np.abs(uf).max())
+    assert np.abs(uf[inj] - uc).max() < 1e-12 * max(1.0, np.abs(uf).max())
