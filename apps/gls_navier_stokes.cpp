@@ -1108,6 +1108,7 @@ struct Solver {
   }
   Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) { timer.on = P.timer != "none"; }
   bool use_ilu;              // assembled ILU(0) where no multigrid hierarchy exists (--precond jacobi: off)
+  bool forest_ilu = false;   // --precond ilu: ILU instead of the multigrid on adapted hyper_cubes
   gls_ctx *ilu_ctx = nullptr;  // the context the ILU was attached to (a new mesh builds a new context)
   int64_t ilu_block_dofs = 0;  // block-Jacobi ILU subdomain size (0: one block, the single-rank reference)
   std::string dump_dir;        // --dump DIR: the state of every iteration's last solve (test hook)
@@ -1144,6 +1145,8 @@ struct Solver {
   void release() {
     for (gls_ctx *g : mg_levels) gls_destroy(g);
     mg_levels.clear();
+    for (gls_refined_mesh *R : mg_meshes) gls_octree_mesh_destroy(R);
+    mg_meshes.clear();
     if (ctx) gls_destroy(ctx);
     ilu_ctx = nullptr;
     ctx = nullptr;
@@ -1383,26 +1386,19 @@ struct Solver {
     }
   }
 
-  // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
-  // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels
-  // and a Jacobi-preconditioned GMRES (no multigrid on locally refined meshes).
-  void setup_refined(gls_refined_mesh *R_new) {
-    SectionTimer::Scope ts(timer, "setup_dofs");
-    release();
-    rmesh = R_new;
-    const int n = 1;
-    const gls_refined_mesh &R = *rmesh;
+  // the app's Mesh of a forest mesh (gls_octree_mesh): cells, node maps and coordinates, hanging lines
+  Mesh mesh_of_refined(const gls_refined_mesh &R) const {
     const int dim = P.dim;
     const int nvl = dim == 3 ? (P.k + 1) * (P.k + 1) * (P.k + 1) : (P.k + 1) * (P.k + 1);
     const int npl = dim == 3 ? (P.kp + 1) * (P.kp + 1) * (P.kp + 1) : (P.kp + 1) * (P.kp + 1);
     Mesh r;
     r.dim = dim;
-    r.n = n;
+    r.n = 1;
     r.k = P.k;
     r.kp = P.kp;
     r.lo = P.lo;
     r.hi = P.hi;
-    r.hc = (P.hi - P.lo) / n;
+    r.hc = P.hi - P.lo;
     r.nc = R.n_cells;
     r.nv = R.n_vnodes;
     r.np = R.n_pnodes;
@@ -1414,6 +1410,18 @@ struct Solver {
     r.px.assign(R.pnode_x, R.pnode_x + r.np * dim);
     load_hanging(r, R.n_vhang, R.vhang_node, R.vhang_off, R.vhang_master, R.vhang_w, R.n_phang, R.phang_node,
                  R.phang_off, R.phang_master, R.phang_w);
+    return r;
+  }
+
+  // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
+  // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels;
+  // 3D equal-order non-periodic: the multigrid V-cycle on the forest's refinement hierarchy
+  // (attach_forest_mg), else ILU / Jacobi-preconditioned GMRES.
+  void setup_refined(gls_refined_mesh *R_new) {
+    SectionTimer::Scope ts(timer, "setup_dofs");
+    release();
+    rmesh = R_new;
+    Mesh r = mesh_of_refined(*rmesh);
     r.pmask = m.pmask;  // periodic faces identified by the forest mesh
     m = std::move(r);
     C = make_constraints(P, m, time);
@@ -1422,8 +1430,76 @@ struct Solver {
                        m.hang_master.data(), m.hang_w.data()),
        "gls_set_hanging");
     alloc_vectors();
+    if (use_mg && !forest_ilu && world == 1 && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && tree)
+      attach_forest_mg();
     print_setup(std::pow(P.hi - P.lo, P.dim));
     std::printf("   Hanging node DoFs:            %lld\n", (long long)m.hang_dofs.size());
+  }
+
+  // Geometric multigrid on the forest's refinement hierarchy (gls_mg_attach_transfers): the levels are
+  // the forest coarsened one level at a time (gls_octree_coarsen_to) down to 2^dim cells, each with its
+  // Dirichlet constraints and hanging lines, the transfers the nested-space interpolation
+  // (gls_octree_mg_transfer); FP64 damped-Jacobi V(2,2) at 0.6 (the per-cell levels), exact LU on the
+  // coarsest level. The reference preconditions with ILU / ML-AMG (gls_navier_stokes.cc:1161-1240);
+  // the substitution is announced (announce_linear_solver).
+  std::vector<gls_refined_mesh *> mg_meshes;
+  void attach_forest_mg() {
+    int L = 0;
+    ck(gls_octree_info(tree, nullptr, &L), "gls_octree_info");
+    if (L < 2) return;
+    std::vector<gls_ctx *> lv{ctx};
+    std::vector<const gls_refined_mesh *> meshes{rmesh};
+    for (int l = L - 1; l >= 1; --l) {
+      gls_octree *tc = nullptr;
+      ck(gls_octree_coarsen_to(tree, l, &tc), "gls_octree_coarsen_to");
+      gls_refined_mesh *R = nullptr;
+      const int rc = gls_octree_mesh(tc, P.k, P.kp, P.lo, P.hi, &R);
+      gls_octree_destroy(tc);
+      ck(rc, "gls_octree_mesh");
+      mg_meshes.push_back(R);
+      meshes.push_back(R);
+      const Mesh r = mesh_of_refined(*R);
+      const Constraints cc = make_constraints(P, r, time);
+      gls_ctx *g = make_context(r, cc);
+      mg_levels.push_back(g);
+      lv.push_back(g);
+      if (!r.hang_dofs.empty())
+        ck(gls_set_hanging(g, (int64_t)r.hang_dofs.size(), r.hang_dofs.data(), r.hang_off.data(), r.hang_master.data(),
+                           r.hang_w.data()),
+           "gls_set_hanging (multigrid level)");
+    }
+    const size_t np = lv.size() - 1;
+    std::vector<std::vector<int64_t>> off(np), inj(np);
+    std::vector<std::vector<int32_t>> col(np);
+    std::vector<std::vector<double>> w(np);
+    std::vector<const int64_t *> po(np), pi(np);
+    std::vector<const int32_t *> pc(np);
+    std::vector<const double *> pw(np);
+    for (size_t l = 0; l < np; ++l) {
+      int64_t nnz = 0, nf = 0, nco = 0;
+      ck(gls_octree_mg_transfer(meshes[l], meshes[l + 1], &nnz, nullptr, nullptr, nullptr, nullptr), "gls_octree_mg_transfer");
+      ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
+      ck(gls_n_dofs(lv[l + 1], &nco), "gls_n_dofs");
+      off[l].resize((size_t)nf + 1);
+      col[l].resize((size_t)std::max<int64_t>(nnz, 1));
+      w[l].resize((size_t)std::max<int64_t>(nnz, 1));
+      inj[l].resize((size_t)nco);
+      ck(gls_octree_mg_transfer(meshes[l], meshes[l + 1], &nnz, off[l].data(), col[l].data(), w[l].data(), inj[l].data()),
+         "gls_octree_mg_transfer");
+      po[l] = off[l].data();
+      pc[l] = col[l].data();
+      pw[l] = w[l].data();
+      pi[l] = inj[l].data();
+    }
+    gls_mg_params mp;
+    std::memset(&mp, 0, sizeof(mp));
+    mp.n_levels = (int)lv.size();
+    mp.levels = lv.data();
+    mp.pre_smooth = 2;
+    mp.post_smooth = 2;
+    mp.omega = 0.6;
+    mp.coarse_direct = 1;
+    ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
   }
 
   void setup(int n) {
@@ -1788,7 +1864,10 @@ struct Solver {
     const char *meth[3] = {"gmres", "bicgstab", "amg"};
     const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
     char prec[256];
-    if (!mg_levels.empty())
+    if (!mg_levels.empty() && rmesh)
+      std::snprintf(prec, sizeof prec, "geometric multigrid V(2,2)-cycle on the forest's refinement hierarchy (%zu levels)",
+                    mg_levels.size() + 1);
+    else if (!mg_levels.empty())
       std::snprintf(prec, sizeof prec, "geometric multigrid V(1,1)-cycle on the nested hyper_cubes");
     else if (use_ilu && P.lin_method == 2)
       std::snprintf(prec, sizeof prec, "ILU(%d) atol %g rtol %g (the amg smoother's ILU on the fine level)",
@@ -2496,7 +2575,8 @@ struct Solver {
 int main(int argc, char **argv) {
   // gls_navier_stokes_2d / gls_navier_stokes_3d <file.prm> (applications/gls_navier_stokes_{2d,3d},
   // gls_navier_stokes_3d.cc:22-46): the dimension comes from the program name; the generic
-  // binary takes --dim. Extra options: --precond mg|jacobi, --precision N (error table digits),
+  // binary takes --dim. Extra options: --precond mg|ilu|jacobi (ilu: ILU instead of the multigrid on adapted
+  // hyper_cubes), --precision N (error table digits),
   // --stats (solver iteration totals), --ilu-block-dofs N (block-Jacobi ILU subdomains of N DoFs,
   // 0 = one block), --ilu-order cm|multicolor (gls_ilu_set_options), --dump DIR (every iteration's
   // final state for the pipeline tests).
@@ -2506,6 +2586,7 @@ int main(int argc, char **argv) {
   int ilu_order = -1;
   const char *dump = nullptr;
   int np_ranks = 1;
+  bool forest_ilu = false;
   int precision = 4;
   const char *file = nullptr;
   const std::string prog = argv[0];
@@ -2513,7 +2594,12 @@ int main(int argc, char **argv) {
   if (prog.size() >= 2 && prog.compare(prog.size() - 2, 2, "3d") == 0) dim = 3;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--dim") && i + 1 < argc) dim = std::atoi(argv[++i]);
-    else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) mg = std::strcmp(argv[++i], "jacobi") != 0;
+    else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) {
+      const char *pc = argv[++i];
+      if (std::strcmp(pc, "mg") && std::strcmp(pc, "jacobi") && std::strcmp(pc, "ilu")) die("--precond %s: mg, ilu or jacobi", pc);
+      mg = std::strcmp(pc, "jacobi") != 0;
+      forest_ilu = !std::strcmp(pc, "ilu");
+    }
     else if (!std::strcmp(argv[i], "--precision") && i + 1 < argc) precision = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--stats")) stats = true;
     else if (!std::strcmp(argv[i], "--ilu-block-dofs") && i + 1 < argc) ilu_block = std::atoll(argv[++i]);
@@ -2560,6 +2646,7 @@ int main(int argc, char **argv) {
     g_comm.rank = rank;
   }
   Solver s(P, mg);
+  s.forest_ilu = forest_ilu;
   s.rank = rank;
   s.world = np_ranks;
   if (np_ranks > 1) {
