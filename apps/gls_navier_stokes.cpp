@@ -1415,8 +1415,8 @@ struct Solver {
 
   // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
   // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels;
-  // 3D equal-order non-periodic: the multigrid V-cycle on the forest's refinement hierarchy
-  // (attach_forest_mg), else ILU / Jacobi-preconditioned GMRES.
+  // one rank, non-periodic: the multigrid V-cycle on the forest's refinement hierarchy (attach_forest_mg),
+  // else ILU / Jacobi-preconditioned GMRES.
   void setup_refined(gls_refined_mesh *R_new) {
     SectionTimer::Scope ts(timer, "setup_dofs");
     release();
@@ -1430,8 +1430,7 @@ struct Solver {
                        m.hang_master.data(), m.hang_w.data()),
        "gls_set_hanging");
     alloc_vectors();
-    if (use_mg && !forest_ilu && world == 1 && P.dim == 3 && P.k == P.kp && P.k <= 2 && m.pmask == 0 && tree)
-      attach_forest_mg();
+    if (use_mg && !forest_ilu && world == 1 && m.pmask == 0 && tree) attach_forest_mg();
     print_setup(std::pow(P.hi - P.lo, P.dim));
     std::printf("   Hanging node DoFs:            %lld\n", (long long)m.hang_dofs.size());
   }
@@ -1857,10 +1856,9 @@ struct Solver {
 
   // the linear solver and preconditioner actually used for the prm's 'linear solver/method', once per
   // run on stderr (stdout stays the reference's): the substitutions are explicit, never silent
-  bool lin_announced = false;
+  std::string lin_announced;  // the last announcement (a new one when the preconditioner changes)
   void announce_linear_solver() {
-    if (lin_announced || rank != 0) return;
-    lin_announced = true;
+    if (rank != 0) return;
     const char *meth[3] = {"gmres", "bicgstab", "amg"};
     const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
     char prec[256];
@@ -1876,10 +1874,14 @@ struct Solver {
       std::snprintf(prec, sizeof prec, "ILU(%d) atol %g rtol %g", P.ilu_fill, P.ilu_atol, P.ilu_rtol);
     else
       std::snprintf(prec, sizeof prec, "Jacobi (--precond jacobi)");
-    std::fprintf(stderr, "linear solver: method = %s -> %s + %s%s\n", meth[P.lin_method], krylov, prec,
-                 P.lin_method == 2 ? (P.amg_w_cycles ? "; ML AMG substituted (amg w cycles = true: V-cycle used)"
-                                                     : "; ML AMG substituted")
-                                   : "");
+    char line[512];
+    std::snprintf(line, sizeof line, "linear solver: method = %s -> %s + %s%s\n", meth[P.lin_method], krylov, prec,
+                  P.lin_method == 2 ? (P.amg_w_cycles ? "; ML AMG substituted (amg w cycles = true: V-cycle used)"
+                                                      : "; ML AMG substituted")
+                                    : "");
+    if (lin_announced == line) return;
+    lin_announced = line;
+    std::fputs(line, stderr);
   }
 
   // ---- one nonlinear solve of `scheme` from the current present solution and history

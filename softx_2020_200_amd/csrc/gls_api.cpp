@@ -461,6 +461,7 @@ struct gls_ctx {
       DevBuf<int32_t> pcol, rcol, inj;
       DevBuf<double> pw, rw;
       int64_t nf = 0, nc = 0;
+      int plane = 1, rlane = 1;  // SpMV lanes per row (from the mean row length)
     };
     std::vector<std::unique_ptr<Csr>> xfer;
     DevBuf<double> xwork;  // two-pass transfer intermediate (coarse xy x fine z, 4 fields)
@@ -2167,7 +2168,7 @@ int mg_restrict(gls_ctx *c, int l, const double *y, double *bc) {
   hipStream_t s = c->stream;
   if (mg.csr) {
     const auto &X = *mg.xfer[(size_t)l];
-    HIP_TRY(gls::vec_csr_spmv(bc, y, X.roff.p, X.rcol.p, X.rw.p, X.nc, false, s));
+    HIP_TRY(gls::vec_csr_spmv(bc, y, X.roff.p, X.rcol.p, X.rw.p, X.nc, false, s, X.rlane));
     (void)h;
     return GLS_OK;
   }
@@ -2201,7 +2202,7 @@ int mg_prolong(gls_ctx *c, int l, double *xc, double *y, bool add = false) {
   hipStream_t s = c->stream;
   if (mg.csr) {
     const auto &X = *mg.xfer[(size_t)l];
-    HIP_TRY(gls::vec_csr_spmv(y, xc, X.poff.p, X.pcol.p, X.pw.p, X.nf, add, s));
+    HIP_TRY(gls::vec_csr_spmv(y, xc, X.poff.p, X.pcol.p, X.pw.p, X.nf, add, s, X.plane));
     return GLS_OK;
   }
   GLS_TRY(dist_import(h, xc));
@@ -2971,6 +2972,14 @@ int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *c
     std::unique_ptr<gls_ctx::MG::Csr> X(new gls_ctx::MG::Csr);
     X->nf = nf;
     X->nc = nc;
+    auto lanes = [](double mean) {  // ~2 entries per lane
+      int L = 1;
+      while (L < 16 && 2.0 * L < mean) L *= 2;
+      return L;
+    };
+    X->plane = lanes((double)nnz / (double)std::max<int64_t>(nf, 1));
+    X->rlane = lanes((double)nnz / (double)std::max<int64_t>(nc, 1));
+    if (const char *e = std::getenv("GLS_MG_SPMV_LANES")) X->plane = X->rlane = std::atoi(e);
     GLS_TRY(X->poff.upload(off, (size_t)nf + 1));
     GLS_TRY(X->pcol.upload(p_col[l], (size_t)std::max<int64_t>(nnz, 1)));
     GLS_TRY(X->pw.upload(p_w[l], (size_t)std::max<int64_t>(nnz, 1)));

@@ -84,7 +84,7 @@ hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, 
 hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
                             int64_t n, hipStream_t s);
 hipError_t vec_csr_spmv(double *y, const double *x, const int64_t *off, const int32_t *col, const double *w, int64_t n,
-                        bool add, hipStream_t s);  // y (+)= A x, CSR
+                        bool add, hipStream_t s, int lanes = 1);  // y (+)= A x, CSR; lanes (1, 2, 4, 8, 16) per row
 hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, const int64_t *idx, int64_t m,
                                 hipStream_t s, const double *rb = nullptr);  // y[idx] = d[idx]*v[idx] (rb: rb[idx] - d v)
 // assembled-ILU helpers: x[idx] = a; val[ent] = y[row] (probe extraction; add: val[ent] += y[row]);

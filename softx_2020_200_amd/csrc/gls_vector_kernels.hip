@@ -1,3 +1,4 @@
+#include <algorithm>
 // gls_vector_kernels.hip — Krylov vector kernels (HBM-bound; 16-byte accesses where aligned).
 #include "gls_launch.hpp"
 
@@ -358,10 +359,37 @@ hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, 
   hipLaunchKernelGGL(k_csr_gather_set, dim3(grid_for(n)), dim3(kBlock), 0, s, x, src, dof, off, master, w, n);
   return hipGetLastError();
 }
+// the same with L lanes per row (CSR-vector): lane r of a row sums its entries r, r + L, ... in order, then a
+// fixed xor butterfly over the L lanes (deterministic); coalesced col / w reads for long rows (the
+// restriction P^T of a Q2 hierarchy: up to 125 terms per coarse row)
+template <int L>
+__global__ void __launch_bounds__(256) k_csr_spmv_v(double *__restrict__ y, const double *__restrict__ x,
+                                                    const int64_t *__restrict__ off, const int32_t *__restrict__ col,
+                                                    const double *__restrict__ w, int64_t n, int add) {
+  const int r = threadIdx.x % L;
+  for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / L; i < n;
+       i += (int64_t)gridDim.x * blockDim.x / L) {
+    double s = 0.;
+    const int64_t e = off[i + 1];
+    for (int64_t j = off[i] + r; j < e; j += L) s += w[j] * x[col[j]];
+#pragma unroll
+    for (int m = L / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, L);
+    if (r == 0) y[i] = add ? y[i] + s : s;
+  }
+}
 hipError_t vec_csr_spmv(double *y, const double *x, const int64_t *off, const int32_t *col, const double *w, int64_t n,
-                        bool add, hipStream_t s) {
+                        bool add, hipStream_t s, int lanes) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(n)), dim3(kBlock), 0, s, y, x, off, col, w, n, add ? 1 : 0);
+  const int a = add ? 1 : 0;
+  const int64_t th = n * (lanes < 1 ? 1 : lanes);
+  const dim3 g((unsigned)std::min<int64_t>((th + 255) / 256, 65535 * 8)), b(256);
+  switch (lanes) {
+    case 2: hipLaunchKernelGGL(k_csr_spmv_v<2>, g, b, 0, s, y, x, off, col, w, n, a); break;
+    case 4: hipLaunchKernelGGL(k_csr_spmv_v<4>, g, b, 0, s, y, x, off, col, w, n, a); break;
+    case 8: hipLaunchKernelGGL(k_csr_spmv_v<8>, g, b, 0, s, y, x, off, col, w, n, a); break;
+    case 16: hipLaunchKernelGGL(k_csr_spmv_v<16>, g, b, 0, s, y, x, off, col, w, n, a); break;
+    default: hipLaunchKernelGGL(k_csr_spmv, dim3(grid_for(n)), dim3(kBlock), 0, s, y, x, off, col, w, n, a);
+  }
   return hipGetLastError();
 }
 hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,

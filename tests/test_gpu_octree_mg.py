@@ -15,13 +15,14 @@ from test_octree_mg import adapted_tree
 
 def level_problem(tree, k, kp, nu, scheme="steady"):
     mesh = tree.mesh(k, kp)
+    dim = mesh["dim"]
     p = StructuredProblem.from_refined(mesh, viscosity=nu, scheme=scheme, time_steps=(0.05, 0.05, 0.05, 0.05))
     lines = sx.hanging_dof_lines(mesh)
     if len(lines[0]):
         p.set_hanging(*lines)
         p.hang_lines = lines
     p.set_dirichlet([("noslip", 0, None)])
-    p.set_force(lambda X: np.stack([np.sin(X[:, 0] + 2 * X[:, 1]) * (1.0 + X[:, 2]) for _ in range(3)], 1))
+    p.set_force(lambda X: np.stack([np.sin(X[:, 0] + 2 * X[:, 1]) * (1.0 + X[:, dim - 1]) for _ in range(dim)], 1))
     return p
 
 
@@ -42,11 +43,11 @@ def octree_hierarchy(tree, k, kp, nu, scheme="steady"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,steps", [(1, 3), (2, 2)])
-def test_octree_multigrid_newton(k, steps):
-    tree = adapted_tree(3, 2, steps)
+@pytest.mark.parametrize("dim,k,kp,steps", [(3, 1, 1, 3), (3, 2, 2, 2), (3, 2, 1, 2), (2, 2, 2, 4), (2, 2, 1, 4)])
+def test_octree_multigrid_newton(dim, k, kp, steps):
+    tree = adapted_tree(dim, 2, steps)
     assert tree.max_level >= 2
-    trees, probs, xfer = octree_hierarchy(tree, k, k, nu=0.1)
+    trees, probs, xfer = octree_hierarchy(tree, k, kp, nu=0.1)
     p = probs[0]
     x_ref, _, _ = newton_solve(p, tol=1e-10)
     out = {}
@@ -60,11 +61,12 @@ def test_octree_multigrid_newton(k, steps):
                             relative_residual=1e-10, minimum_residual=1e-13)
         out[mg] = (x.cpu().numpy(), st)
         assert st["final_residual"] < 1e-10, (mg, st)
-    nvd = 3 * p.n_vnodes
+    nvd = dim * p.n_vnodes
     for mg in (False, True):
         assert np.abs(out[mg][0][:nvd] - x_ref[:nvd]).max() < 1e-8, mg
     its_mg, its_j = out[True][1]["linear_iterations"], out[False][1]["linear_iterations"]
-    print("octree GMG: %d levels, %d DoFs, GMRES its %d (Jacobi %d)" % (len(probs), p.n_dofs, its_mg, its_j))
+    print("octree GMG %dD Q%dQ%d: %d levels, %d DoFs, GMRES its %d (Jacobi %d)" % (dim, k, kp, len(probs), p.n_dofs,
+                                                                                 its_mg, its_j))
     assert its_mg * 4 < its_j, (out[True][1], out[False][1])
 
 
