@@ -1108,7 +1108,8 @@ struct Solver {
   }
   Solver(Params &p, bool mg) : P(p), use_mg(mg), use_ilu(mg) { timer.on = P.timer != "none"; }
   bool use_ilu;              // assembled ILU(0) where no multigrid hierarchy exists (--precond jacobi: off)
-  bool forest_ilu = false;   // --precond ilu: ILU instead of the multigrid on adapted hyper_cubes
+  int forest_mode = 0;       // adapted meshes: 0 default, 1 --precond ilu (never the hierarchy multigrid),
+                             // 2 --precond hmg (the hierarchy multigrid for every method and order)
   gls_ctx *ilu_ctx = nullptr;  // the context the ILU was attached to (a new mesh builds a new context)
   int64_t ilu_block_dofs = 0;  // block-Jacobi ILU subdomain size (0: one block, the single-rank reference)
   std::string dump_dir;        // --dump DIR: the state of every iteration's last solve (test hook)
@@ -1415,8 +1416,8 @@ struct Solver {
 
   // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
   // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels;
-  // one rank, non-periodic: the multigrid V-cycle on the forest's refinement hierarchy (attach_forest_mg),
-  // else ILU / Jacobi-preconditioned GMRES.
+  // one rank, equal order, non-periodic: the multigrid V-cycle on the forest's refinement hierarchy
+  // (attach_forest_mg; Q2-Q1 cuts the iterations only ~3x against Jacobi, so ILU there), else ILU / Jacobi.
   void setup_refined(gls_refined_mesh *R_new) {
     SectionTimer::Scope ts(timer, "setup_dofs");
     release();
@@ -1430,7 +1431,8 @@ struct Solver {
                        m.hang_master.data(), m.hang_w.data()),
        "gls_set_hanging");
     alloc_vectors();
-    if (use_mg && !forest_ilu && world == 1 && m.pmask == 0 && tree) attach_forest_mg();
+    if (use_mg && forest_mode != 1 && world == 1 && (P.k == P.kp || forest_mode == 2) && m.pmask == 0 && tree)
+      attach_forest_mg();
     print_setup(std::pow(P.hi - P.lo, P.dim));
     std::printf("   Hanging node DoFs:            %lld\n", (long long)m.hang_dofs.size());
   }
@@ -1546,22 +1548,9 @@ struct Solver {
     }
     ck(gls_umesh_refine_global(um, P.refinement), "refine_global");
   }
-  // FE space, constraints and context on the current triangulation (per-cell kernels with MappingQ
-  // geometry, Jacobi-preconditioned GMRES)
-  void setup_general() {
-    SectionTimer::Scope ts(timer, "setup_dofs");
-    release();
-    if (space) gls_fe_space_destroy(space);
-    space = nullptr;
-    std::vector<int32_t> per;
-    for (const BC &b : P.bcs)
-      if (b.type == "periodic") {  // make_periodicity_constraints(id, periodic_id, direction)
-        per.push_back(b.id);
-        per.push_back(b.periodic_id);
-        per.push_back(b.periodic_direction);
-      }
-    ck(gls_umesh_fe_space(um, P.k, P.kp, P.qmapping_all ? 1 : 0, (int)per.size() / 3, per.data(), &space), "gls_umesh_fe_space");
-    const gls_fe_space &F = *space;
+  // the app's Mesh of an FE space of the triangulation (cells, nodes, MappingQ support points, hanging
+  // lines, the slip boundaries' averaged node normals)
+  Mesh mesh_of_space(const gls_fe_space &F) {
     Mesh r;
     r.dim = P.dim;
     r.k = P.k;
@@ -1586,26 +1575,122 @@ struct Solver {
       if (b.type == "slip") {
         std::vector<double> nrm((size_t)(r.nv * P.dim)), sets((size_t)(r.nv * 3 * P.dim));
         std::vector<int32_t> rank_((size_t)r.nv);
-        ck(gls_fe_space_boundary_normals(space, b.id, nrm.data()), "gls_fe_space_boundary_normals");
-        ck(gls_fe_space_boundary_normal_sets(space, b.id, rank_.data(), sets.data()), "gls_fe_space_boundary_normal_sets");
+        ck(gls_fe_space_boundary_normals(&F, b.id, nrm.data()), "gls_fe_space_boundary_normals");
+        ck(gls_fe_space_boundary_normal_sets(&F, b.id, rank_.data(), sets.data()), "gls_fe_space_boundary_normal_sets");
         r.slip_normals[b.id] = std::move(nrm);
         r.slip_rank[b.id] = std::move(rank_);
         r.slip_sets[b.id] = std::move(sets);
       }
-    m = std::move(r);
-    C = make_constraints(P, m, time);
-    // hanging lines + slip lines of curved walls (homogeneous constraint lines on velocity DoFs)
-    std::vector<int64_t> ld = m.hang_dofs, lo = m.hang_off, lm = m.hang_master;
-    std::vector<double> lw = m.hang_w;
-    for (size_t i = 0; i < C.line_dofs.size(); ++i) {
-      ld.push_back(C.line_dofs[i]);
-      for (int64_t j = C.line_off[i]; j < C.line_off[i + 1]; ++j) {
-        lm.push_back(C.line_master[(size_t)j]);
-        lw.push_back(C.line_w[(size_t)j]);
+    return r;
+  }
+  // the context's constraint lines: hanging lines + slip lines of curved walls, chains closed
+  void constraint_lines(const Mesh &mm, const Constraints &cc, std::vector<int64_t> &ld, std::vector<int64_t> &lo,
+                        std::vector<int64_t> &lm, std::vector<double> &lw) {
+    ld = mm.hang_dofs;
+    lo = mm.hang_off;
+    lm = mm.hang_master;
+    lw = mm.hang_w;
+    for (size_t i = 0; i < cc.line_dofs.size(); ++i) {
+      ld.push_back(cc.line_dofs[i]);
+      for (int64_t j = cc.line_off[i]; j < cc.line_off[i + 1]; ++j) {
+        lm.push_back(cc.line_master[(size_t)j]);
+        lw.push_back(cc.line_w[(size_t)j]);
       }
       lo.push_back((int64_t)lm.size());
     }
     close_lines(ld, lo, lm, lw);
+  }
+
+  // Geometric multigrid on the triangulation's refinement hierarchy (gls_mg_attach_transfers): levels =
+  // the triangulation coarsened one level at a time (gls_umesh_coarsen_to) down to the coarse mesh, each
+  // with its FE space, MappingQ geometry, Dirichlet / slip constraints and hanging lines; transfers =
+  // FE_Q's embedding (gls_fe_space_mg_transfer); FP64 damped-Jacobi V(2,2) at 0.6, exact LU on the
+  // coarsest level when it is small enough (<= 8192 DoFs), else 30 Jacobi sweeps there.
+  void attach_umesh_mg() {
+    int L = 0;
+    for (int64_t c = 0; c < space->n_cells; ++c) L = std::max(L, (int)space->cell_level[c]);
+    if (L < 1) return;
+    std::vector<gls_ctx *> lv{ctx};
+    std::vector<gls_fe_space *> spaces;
+    std::vector<const gls_fe_space *> sp{space};
+    int64_t n_coarse = 0;
+    for (int l = L - 1; l >= 0; --l) {
+      gls_umesh *uc = nullptr;
+      ck(gls_umesh_coarsen_to(um, l, &uc), "gls_umesh_coarsen_to");
+      gls_fe_space *s_ = nullptr;
+      const int rc = gls_umesh_fe_space(uc, P.k, P.kp, P.qmapping_all ? 1 : 0, 0, nullptr, &s_);
+      gls_umesh_destroy(uc);
+      ck(rc, "gls_umesh_fe_space (multigrid level)");
+      spaces.push_back(s_);
+      sp.push_back(s_);
+      const Mesh r = mesh_of_space(*s_);
+      const Constraints cc = make_constraints(P, r, time);
+      std::vector<int64_t> ld, lo, lm;
+      std::vector<double> lw;
+      constraint_lines(r, cc, ld, lo, lm, lw);
+      gls_ctx *g = make_context(r, cc);
+      mg_levels.push_back(g);
+      lv.push_back(g);
+      if (!ld.empty()) ck(gls_set_hanging(g, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging (multigrid level)");
+      n_coarse = r.n_dofs();
+    }
+    const size_t np = lv.size() - 1;
+    std::vector<std::vector<int64_t>> off(np), inj(np);
+    std::vector<std::vector<int32_t>> col(np);
+    std::vector<std::vector<double>> w(np);
+    std::vector<const int64_t *> po(np), pi(np);
+    std::vector<const int32_t *> pc(np);
+    std::vector<const double *> pw(np);
+    for (size_t l = 0; l < np; ++l) {
+      int64_t nnz = 0, nf = 0, nco = 0;
+      ck(gls_fe_space_mg_transfer(sp[l], sp[l + 1], &nnz, nullptr, nullptr, nullptr, nullptr), "gls_fe_space_mg_transfer");
+      ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
+      ck(gls_n_dofs(lv[l + 1], &nco), "gls_n_dofs");
+      off[l].resize((size_t)nf + 1);
+      col[l].resize((size_t)std::max<int64_t>(nnz, 1));
+      w[l].resize((size_t)std::max<int64_t>(nnz, 1));
+      inj[l].resize((size_t)nco);
+      ck(gls_fe_space_mg_transfer(sp[l], sp[l + 1], &nnz, off[l].data(), col[l].data(), w[l].data(), inj[l].data()),
+         "gls_fe_space_mg_transfer");
+      po[l] = off[l].data();
+      pc[l] = col[l].data();
+      pw[l] = w[l].data();
+      pi[l] = inj[l].data();
+    }
+    for (gls_fe_space *s_ : spaces) gls_fe_space_destroy(s_);
+    gls_mg_params mp;
+    std::memset(&mp, 0, sizeof(mp));
+    mp.n_levels = (int)lv.size();
+    mp.levels = lv.data();
+    mp.pre_smooth = 2;
+    mp.post_smooth = 2;
+    mp.omega = 0.6;
+    mp.coarse_direct = n_coarse <= 8192 ? 1 : -1;
+    ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
+  }
+
+  // FE space, constraints and context on the current triangulation (per-cell kernels with MappingQ
+  // geometry, Jacobi-preconditioned GMRES)
+  void setup_general() {
+    SectionTimer::Scope ts(timer, "setup_dofs");
+    release();
+    if (space) gls_fe_space_destroy(space);
+    space = nullptr;
+    std::vector<int32_t> per;
+    for (const BC &b : P.bcs)
+      if (b.type == "periodic") {  // make_periodicity_constraints(id, periodic_id, direction)
+        per.push_back(b.id);
+        per.push_back(b.periodic_id);
+        per.push_back(b.periodic_direction);
+      }
+    ck(gls_umesh_fe_space(um, P.k, P.kp, P.qmapping_all ? 1 : 0, (int)per.size() / 3, per.data(), &space), "gls_umesh_fe_space");
+    const gls_fe_space &F = *space;
+    m = mesh_of_space(F);
+    C = make_constraints(P, m, time);
+    // hanging lines + slip lines of curved walls (homogeneous constraint lines on velocity DoFs)
+    std::vector<int64_t> ld, lo, lm;
+    std::vector<double> lw;
+    constraint_lines(m, C, ld, lo, lm, lw);
     g_lines = {ld, lo, lm};
     g_lines_w = lw;
     if (world > 1) {  // the rank's cells; its lines in local DoF ids (masters are local by construction)
@@ -1630,6 +1715,10 @@ struct Solver {
       ctx = make_context(m, C);
       if (!ld.empty())
         ck(gls_set_hanging(ctx, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging");
+      // method = amg (ML's multilevel hierarchy): the geometric one of the triangulation; gmres keeps the
+      // reference's ILU (--precond hmg: the hierarchy multigrid for every method and order)
+      if (use_mg && per.empty() && ((P.lin_method == 2 && P.k == P.kp && forest_mode != 1) || forest_mode == 2))
+        attach_umesh_mg();
     }
     alloc_vectors();
     print_setup(F.volume);
@@ -1862,9 +1951,9 @@ struct Solver {
     const char *meth[3] = {"gmres", "bicgstab", "amg"};
     const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
     char prec[256];
-    if (!mg_levels.empty() && rmesh)
-      std::snprintf(prec, sizeof prec, "geometric multigrid V(2,2)-cycle on the forest's refinement hierarchy (%zu levels)",
-                    mg_levels.size() + 1);
+    if (!mg_levels.empty() && (rmesh || space))
+      std::snprintf(prec, sizeof prec, "geometric multigrid V(2,2)-cycle on the %s refinement hierarchy (%zu levels)",
+                    rmesh ? "forest's" : "triangulation's", mg_levels.size() + 1);
     else if (!mg_levels.empty())
       std::snprintf(prec, sizeof prec, "geometric multigrid V(1,1)-cycle on the nested hyper_cubes");
     else if (use_ilu && P.lin_method == 2)
@@ -2577,8 +2666,8 @@ struct Solver {
 int main(int argc, char **argv) {
   // gls_navier_stokes_2d / gls_navier_stokes_3d <file.prm> (applications/gls_navier_stokes_{2d,3d},
   // gls_navier_stokes_3d.cc:22-46): the dimension comes from the program name; the generic
-  // binary takes --dim. Extra options: --precond mg|ilu|jacobi (ilu: ILU instead of the multigrid on adapted
-  // hyper_cubes), --precision N (error table digits),
+  // binary takes --dim. Extra options: --precond mg|ilu|hmg|jacobi (ilu: never the refinement-hierarchy
+  // multigrid on adapted meshes; hmg: that multigrid for every method and order), --precision N (error table digits),
   // --stats (solver iteration totals), --ilu-block-dofs N (block-Jacobi ILU subdomains of N DoFs,
   // 0 = one block), --ilu-order cm|multicolor (gls_ilu_set_options), --dump DIR (every iteration's
   // final state for the pipeline tests).
@@ -2588,7 +2677,7 @@ int main(int argc, char **argv) {
   int ilu_order = -1;
   const char *dump = nullptr;
   int np_ranks = 1;
-  bool forest_ilu = false;
+  int forest_mode = 0;
   int precision = 4;
   const char *file = nullptr;
   const std::string prog = argv[0];
@@ -2598,9 +2687,10 @@ int main(int argc, char **argv) {
     if (!std::strcmp(argv[i], "--dim") && i + 1 < argc) dim = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--precond") && i + 1 < argc) {
       const char *pc = argv[++i];
-      if (std::strcmp(pc, "mg") && std::strcmp(pc, "jacobi") && std::strcmp(pc, "ilu")) die("--precond %s: mg, ilu or jacobi", pc);
+      if (std::strcmp(pc, "mg") && std::strcmp(pc, "jacobi") && std::strcmp(pc, "ilu") && std::strcmp(pc, "hmg"))
+        die("--precond %s: mg, ilu, hmg or jacobi", pc);
       mg = std::strcmp(pc, "jacobi") != 0;
-      forest_ilu = !std::strcmp(pc, "ilu");
+      forest_mode = !std::strcmp(pc, "ilu") ? 1 : !std::strcmp(pc, "hmg") ? 2 : 0;
     }
     else if (!std::strcmp(argv[i], "--precision") && i + 1 < argc) precision = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--stats")) stats = true;
@@ -2648,7 +2738,7 @@ int main(int argc, char **argv) {
     g_comm.rank = rank;
   }
   Solver s(P, mg);
-  s.forest_ilu = forest_ilu;
+  s.forest_mode = forest_mode;
   s.rank = rank;
   s.world = np_ranks;
   if (np_ranks > 1) {

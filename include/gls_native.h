@@ -636,6 +636,18 @@ int gls_fe_space_boundary_normals(const gls_fe_space *space, int boundary_id, do
  * normals: [n_vnodes][3][dim], row i = unit mean of group i (row 0 = the node normal when count = 1). */
 int gls_fe_space_boundary_normal_sets(const gls_fe_space *space, int boundary_id, int32_t *count, double *normals);
 int gls_umesh_adapt(gls_umesh *mesh, const int32_t *refine, const int32_t *coarsen);
+/* Level meshes of a geometric multigrid on the triangulation's refinement hierarchy (global coarsening):
+ * a copy whose active cells are the current ones with every cell finer than `level` replaced by its
+ * ancestor on `level` (free with gls_umesh_destroy). gls_fe_space_mg_transfer: the prolongation between
+ * the FE spaces of two such levels (coarse = a coarsening of fine's triangulation) as a DoF-level CSR over
+ * the fine DoFs -- FE_Q's embedding of the coarse cell's field (hanging nodes from their lines) at the fine
+ * node's reference position, whatever the mapping; fine hanging rows empty, coarse masters as columns --
+ * and inject (n_dofs(coarse)): the fine DoF at each coarse DoF's node. off == NULL: nnz only. Feed both to
+ * gls_mg_attach_transfers (the reference preconditions these meshes with ILU / ML-AMG,
+ * gls_navier_stokes.cc:1161-1240). */
+int gls_umesh_coarsen_to(const gls_umesh *mesh, int level, gls_umesh **out);
+int gls_fe_space_mg_transfer(const gls_fe_space *fine, const gls_fe_space *coarse, int64_t *nnz, int64_t *off,
+                             int32_t *col, double *w, int64_t *inject);
 /* Face pieces for KellyErrorEstimator with MappingQ on such a space (conforming faces one piece,
  * a face with a refined neighbour one piece per child face; geometry on the coarse side as deal.II's
  * present cell): cells ca / cb, and per QGauss<dim-1>(nq) point q of piece e the reference

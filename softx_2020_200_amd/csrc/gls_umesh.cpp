@@ -1884,6 +1884,180 @@ int gls_fe_space_transfer(const gls_fe_space *co, const gls_fe_space *fi, const 
   return GLS_OK;
 }
 
+// Level meshes of a geometric multigrid on the triangulation's refinement hierarchy (global coarsening):
+// a copy whose active cells are the current ones with every cell finer than `level` replaced by its
+// ancestor on `level` (depth-first order kept; the 2:1 balance survives truncation). Its FE spaces
+// (gls_umesh_fe_space) share the hierarchy ids of the original's, which gls_fe_space_mg_transfer uses.
+int gls_umesh_coarsen_to(const gls_umesh *g, int level, gls_umesh **out) {
+  if (!g || !out || level < 0) return gls_io_set_error(GLS_EINVAL, "gls_umesh_coarsen_to: arguments");
+  auto *r = new gls_umesh(*g);
+  UMesh &m = r->m;
+  if (!m.tree.empty()) {
+    std::vector<int64_t> act;
+    std::unordered_map<int64_t, char> seen;
+    for (int64_t h : g->m.active) {
+      int64_t a = h;
+      while (m.tree[(size_t)a].level > level && m.tree[(size_t)a].parent >= 0) a = m.tree[(size_t)a].parent;
+      if (seen.emplace(a, 1).second) act.push_back(a);
+    }
+    m.active = act;
+    m.cells.resize(act.size());
+    m.cell_mf.resize(act.size());
+    for (size_t i = 0; i < act.size(); ++i) {
+      m.cells[i] = m.tree[(size_t)act[i]].v;
+      m.cell_mf[i] = m.tree[(size_t)act[i]].mf;
+    }
+  }
+  *out = r;
+  return GLS_OK;
+}
+
+// Prolongation between the FE spaces of two levels of one hierarchy (coarse from gls_umesh_coarsen_to of
+// the fine space's triangulation): fine DoF i = sum_j P_ij coarse DoF j = the coarse field (its hanging
+// nodes replaced by their lines) at the fine node's reference position in its coarse ancestor cell --
+// FE_Q's embedding (child -> parent reference coordinates), independent of the mapping, as
+// SolutionTransfer interpolates (gls_fe_space_transfer). Rows of fine hanging DoFs are empty; columns are
+// coarse masters. inject[j] = the fine DoF at coarse DoF j's node (descending the hierarchy to the fine
+// cell holding it). off == NULL: nnz only.
+int gls_fe_space_mg_transfer(const gls_fe_space *fi, const gls_fe_space *co, int64_t *nnz, int64_t *off, int32_t *col,
+                             double *w, int64_t *inject) {
+  if (!fi || !co || !nnz || fi->dim != co->dim || fi->k != co->k || fi->kp != co->kp || !fi->impl_ || !co->impl_)
+    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: spaces of different dimension / degree");
+  const FESpaceImpl &N = *static_cast<const FESpaceImpl *>(fi->impl_);
+  const FESpaceImpl &O = *static_cast<const FESpaceImpl *>(co->impl_);
+  if (N.t_parent.size() != O.t_parent.size())
+    return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: the spaces are not levels of one hierarchy");
+  const int dim = fi->dim;
+  std::unordered_map<int64_t, int64_t> cof, fof;  // hierarchy id -> active cell
+  for (int64_t c = 0; c < co->n_cells; ++c) cof[O.hid[(size_t)c]] = c;
+  for (int64_t f = 0; f < fi->n_cells; ++f) fof[N.hid[(size_t)f]] = f;
+  const int64_t nvf = fi->n_vnodes, nvc = co->n_vnodes;
+  std::vector<int64_t> inj((size_t)(dim * nvc + co->n_pnodes), -1);
+  std::vector<int32_t> cols;
+  std::vector<double> ws;
+  std::vector<int64_t> roff{0};
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool vel = pass == 0;
+    const int kk = vel ? fi->k : fi->kp, kk1 = kk + 1, nn = dim == 2 ? kk1 * kk1 : kk1 * kk1 * kk1;
+    const int32_t *ccn = vel ? co->cell_vnodes : co->cell_pnodes, *fcn = vel ? fi->cell_vnodes : fi->cell_pnodes;
+    const int64_t nnf = vel ? nvf : fi->n_pnodes, nnc = vel ? nvc : co->n_pnodes;
+    const int64_t nh_c = vel ? co->n_vhang : co->n_phang, nh_f = vel ? fi->n_vhang : fi->n_phang;
+    const int64_t *hc_node = vel ? co->vhang_node : co->phang_node, *hc_off = vel ? co->vhang_off : co->phang_off;
+    const int64_t *hc_mas = vel ? co->vhang_master : co->phang_master;
+    const double *hc_w = vel ? co->vhang_w : co->phang_w;
+    const int64_t *hf_node = vel ? fi->vhang_node : fi->phang_node;
+    std::unordered_map<int64_t, int64_t> cline;
+    for (int64_t i = 0; i < nh_c; ++i) cline[hc_node[i]] = i;
+    std::vector<char> fh((size_t)nnf, 0), seen((size_t)nnf, 0);
+    for (int64_t i = 0; i < nh_f; ++i) fh[(size_t)hf_node[i]] = 1;
+    std::vector<std::vector<std::pair<int32_t, double>>> rows((size_t)nnf);
+    for (int64_t f = 0; f < fi->n_cells; ++f) {
+      int64_t anc = N.hid[(size_t)f];
+      std::vector<int> path;
+      while (anc >= 0 && !cof.count(anc)) {
+        path.push_back(N.t_pos[(size_t)anc]);
+        anc = N.t_parent[(size_t)anc];
+      }
+      if (anc < 0) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: fine cell %lld has no coarse ancestor", (long long)f);
+      const int64_t oc = cof[anc];
+      for (int a = 0; a < nn; ++a) {
+        const int64_t node = fcn[f * nn + a];
+        if (seen[(size_t)node] || fh[(size_t)node]) continue;
+        seen[(size_t)node] = 1;
+        const int ia[3] = {a % kk1, (a / kk1) % kk1, dim == 3 ? a / (kk1 * kk1) : 0};
+        double xi[3] = {0, 0, 0};
+        for (int d = 0; d < dim; ++d) xi[d] = (double)ia[d] / kk;
+        for (int pos : path)
+          for (int d = 0; d < dim; ++d) xi[d] = 0.5 * (xi[d] + ((pos >> d) & 1));
+        auto &acc = rows[(size_t)node];
+        for (int b = 0; b < nn; ++b) {
+          const int ib[3] = {b % kk1, (b / kk1) % kk1, dim == 3 ? b / (kk1 * kk1) : 0};
+          double wb = 1.0;
+          for (int d = 0; d < dim; ++d) wb *= lag1(kk, ib[d], xi[d]);
+          if (std::fabs(wb) < 1e-14) continue;
+          const int64_t cn = ccn[oc * nn + b];
+          auto it = cline.find(cn);
+          if (it == cline.end()) {
+            acc.push_back({(int32_t)cn, wb});
+          } else {
+            for (int64_t q = hc_off[it->second]; q < hc_off[it->second + 1]; ++q) acc.push_back({(int32_t)hc_mas[q], wb * hc_w[q]});
+          }
+        }
+        std::sort(acc.begin(), acc.end(), [](const std::pair<int32_t, double> &x, const std::pair<int32_t, double> &y) {
+          return x.first < y.first;
+        });
+        size_t m = 0;
+        for (size_t i = 0; i < acc.size(); ++i) {
+          if (m > 0 && acc[m - 1].first == acc[i].first) acc[m - 1].second += acc[i].second;
+          else acc[m++] = acc[i];
+        }
+        acc.resize(m);
+        acc.erase(std::remove_if(acc.begin(), acc.end(), [](const std::pair<int32_t, double> &e) {
+                    return std::fabs(e.second) < 1e-14;
+                  }),
+                  acc.end());
+      }
+    }
+    for (int64_t v = 0; v < nnf; ++v) {
+      const int nrow = vel ? dim : 1;
+      for (int c = 0; c < nrow; ++c) {
+        for (auto &e : rows[(size_t)v]) {
+          cols.push_back(vel ? (int32_t)(e.first * dim + c) : (int32_t)(dim * nvc + e.first));
+          ws.push_back(e.second);
+        }
+        roff.push_back((int64_t)cols.size());
+      }
+    }
+    // injection: each coarse node's position, descended to the fine active cell holding it
+    std::vector<char> done((size_t)nnc, 0);
+    for (int64_t oc = 0; oc < co->n_cells; ++oc)
+      for (int b = 0; b < nn; ++b) {
+        const int64_t cnode = ccn[oc * nn + b];
+        if (done[(size_t)cnode]) continue;
+        done[(size_t)cnode] = 1;
+        double xi[3] = {0, 0, 0};
+        const int ib[3] = {b % kk1, (b / kk1) % kk1, dim == 3 ? b / (kk1 * kk1) : 0};
+        for (int d = 0; d < dim; ++d) xi[d] = (double)ib[d] / kk;
+        int64_t c = O.hid[(size_t)oc];
+        int guard = 0;
+        while (!fof.count(c)) {
+          if ((size_t)c >= N.t_child0.size() || N.t_child0[(size_t)c] < 0 || ++guard > 64)
+            return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: coarse cell %lld not refined into the fine mesh", (long long)oc);
+          int ch = 0;
+          for (int d = 0; d < dim; ++d) {
+            const int bit = xi[d] > 0.5 ? 1 : 0;
+            ch |= bit << d;
+            xi[d] = 2 * xi[d] - bit;
+          }
+          c = N.t_child0[(size_t)c] + ch;
+        }
+        const int64_t f = fof[c];
+        int la = 0, st = 1;
+        for (int d = 0; d < dim; ++d) {
+          const double q = xi[d] * kk;
+          const int iq = (int)std::lround(q);
+          if (std::fabs(q - iq) > 1e-9) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: coarse node not a fine node");
+          la += iq * st;
+          st *= kk1;
+        }
+        const int64_t fnode = fcn[f * nn + la];
+        if (vel)
+          for (int e = 0; e < dim; ++e) inj[(size_t)(cnode * dim + e)] = fnode * dim + e;
+        else
+          inj[(size_t)(dim * nvc + cnode)] = dim * nvf + fnode;
+      }
+  }
+  *nnz = (int64_t)cols.size();
+  if (off) {
+    if (!col || !w) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: col / w missing");
+    std::memcpy(off, roff.data(), sizeof(int64_t) * roff.size());
+    std::memcpy(col, cols.data(), sizeof(int32_t) * cols.size());
+    std::memcpy(w, ws.data(), sizeof(double) * ws.size());
+  }
+  if (inject) std::memcpy(inject, inj.data(), sizeof(int64_t) * inj.size());
+  return GLS_OK;
+}
+
 // Face pieces of KellyErrorEstimator::estimate with a MappingQ (navier_stokes_base.cc:612-652;
 // deal.II 9.2 error_estimator.cc, third party, restated): every interior face between two active
 // cells of the same level is one piece; on a face between an active cell and a refined neighbour

@@ -43,7 +43,8 @@ EXPORTS = [
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
     "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
     "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals", "gls_fe_space_boundary_normal_sets",
-    "gls_octree_coarsen_to", "gls_octree_mg_transfer", "gls_mg_attach_transfers",
+    "gls_octree_coarsen_to", "gls_octree_mg_transfer", "gls_mg_attach_transfers", "gls_umesh_coarsen_to",
+    "gls_fe_space_mg_transfer",
 ]
 
 
@@ -170,6 +171,8 @@ def load():
                                           C.POINTER(C.POINTER(C.c_int32)), C.POINTER(C.POINTER(C.c_double)),
                                           C.POINTER(C.POINTER(i64))]
     L.gls_octree_coarsen_to.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.gls_umesh_coarsen_to.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.gls_fe_space_mg_transfer.argtypes = [C.POINTER(FESpace), C.POINTER(FESpace), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_octree_mg_transfer.argtypes = [C.POINTER(RefinedMesh), C.POINTER(RefinedMesh), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
@@ -958,6 +961,15 @@ class UMesh:
                                         per.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pm)), "gls_umesh_fe_space")
         return FESpaceHandle(self.L, pm)
 
+    def coarsen_to(self, level):
+        """A copy with every active cell finer than `level` replaced by its ancestor (gls_umesh_coarsen_to):
+        a level mesh of the multigrid on the refinement hierarchy."""
+        out = UMesh.__new__(UMesh)
+        out.L, out.dim = self.L, self.dim
+        out.h = C.c_void_p()
+        check(self.L.gls_umesh_coarsen_to(self.h, int(level), C.byref(out.h)), "gls_umesh_coarsen_to")
+        return out
+
     def prepare(self, refine, coarsen):
         """prepare_coarsening_and_refinement with the reference's smoothing (gls_umesh_prepare);
         returns the smoothed (refine, coarsen) flags over the active cells."""
@@ -990,6 +1002,23 @@ class FESpaceHandle:
                 self.ptr = None
         except Exception:
             pass
+
+    def mg_transfer_from(self, coarse):
+        """Prolongation CSR (off, col, w) from the space `coarse` of a coarser level of the same hierarchy and
+        the state injection (gls_fe_space_mg_transfer)."""
+        nnz = C.c_int64()
+        check(self.L.gls_fe_space_mg_transfer(self.ptr, coarse.ptr, C.byref(nnz), None, None, None, None),
+              "gls_fe_space_mg_transfer")
+        d, c = self.data, coarse.data
+        nf = d["dim"] * d["n_vnodes"] + d["n_pnodes"]
+        nc = c["dim"] * c["n_vnodes"] + c["n_pnodes"]
+        off = np.zeros(nf + 1, np.int64)
+        col = np.zeros(max(nnz.value, 1), np.int32)
+        w = np.zeros(max(nnz.value, 1))
+        inj = np.zeros(nc, np.int64)
+        check(self.L.gls_fe_space_mg_transfer(self.ptr, coarse.ptr, C.byref(nnz), off.ctypes.data, col.ctypes.data,
+                                              w.ctypes.data, inj.ctypes.data), "gls_fe_space_mg_transfer")
+        return off, col[:nnz.value], w[:nnz.value], inj
 
     def transfer_from(self, old, vec):
         vec = np.ascontiguousarray(vec, dtype=np.float64)

@@ -196,3 +196,29 @@ def test_configs4_cylinder3d_re200_bdf2_kelly_pipeline(tmp_path, np_ranks):
         assert res <= 1.01 * tol, (it, scheme, res)
         h_prev, prev = h, d
     assert adapted == 1 and dumps[1]["n_cells"] > dumps[0]["n_cells"], [x["n_cells"] for x in dumps]
+
+
+@pytest.mark.gpu
+def test_configs3_taylor_couette3d_kelly_hierarchy_multigrid(tmp_path):
+    """configs[3]'s adaptive pipeline with the geometric multigrid on the triangulation's refinement
+    hierarchy as the GMRES preconditioner (--precond hmg: gls_umesh_coarsen_to levels, gls_fe_space_mg_transfer,
+    gls_mg_attach_transfers; MappingQ2 per-cell kernels on every level, hanging and slip lines) instead of the
+    reference's ILU: the same meshes and error table as the ILU run (converged Newton, 1e-8), the
+    preconditioner announced on stderr, the GMRES iteration totals printed."""
+    prm = open(os.path.join(CASES, "taylor-couette3d_q2q1_kelly.prm")).read()
+    res = {}
+    for pc in ("mg", "hmg"):
+        d = tmp_path / pc
+        d.mkdir()
+        out, dumps = run_app(d, prm, extra=("--precision", "9", "--precond", pc))
+        err = (d / "stderr.txt").read_text()
+        rows = [l.split() for l in out.splitlines() if re.match(r"^\s*\d+\s+\d\.\d+e[-+]\d+", l)]
+        its = [l for l in out.splitlines() if "linear_iterations =" in l]
+        res[pc] = (rows, err, its, dumps)
+    assert "triangulation's refinement hierarchy" in res["hmg"][1], res["hmg"][1][-1500:]
+    assert "refinement hierarchy" not in res["mg"][1]
+    ra, rb = res["mg"][0], res["hmg"][0]
+    assert len(ra) == len(rb) == 3 and [r[0] for r in ra] == [r[0] for r in rb], (ra, rb)
+    for a, b in zip(ra, rb):
+        assert abs(float(a[1]) - float(b[1])) <= 1e-6 * float(a[1]), (a, b)
+    print("configs[3] GMRES totals: ILU %s, hierarchy GMG %s" % (res["mg"][2], res["hmg"][2]))
