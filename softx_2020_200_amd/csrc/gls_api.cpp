@@ -2101,7 +2101,8 @@ int mg_prepare(gls_ctx *c) {
     const bool use_lu = cs ? std::strncmp(cs, "lu", 2) == 0 : true;  // LU: 1.5-3 ms at n = 500 vs the one-workgroup GJ's ~15
     bool npvt = cs ? std::strcmp(cs, "lu_npvt") == 0 : true;
     if (use_lu) {  // LU with the pressure gauge pinned
-      const int64_t pin = 3 * (int64_t)g->n_vnodes;
+      const int64_t pin = (int64_t)g->dim * g->n_vnodes;  // the first pressure DoF
+      if (pin >= n) return set_err(GLS_EINVAL, "mg: coarsest level without pressure DoFs");
       HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
       if (npvt && !cs) {  // keep the matrix for a pivoted retry
         if (mg.probe_bak.n != (size_t)(n * n)) GLS_TRY(mg.probe_bak.alloc((size_t)(n * n)));
