@@ -1,7 +1,7 @@
 """GPU: the geometric multigrid V-cycle on the refinement hierarchy of adapted unstructured / curved meshes
 (gls_umesh_coarsen_to + gls_fe_space_mg_transfer levels, gls_mg_attach_transfers; MappingQ per-cell
 kernels on every level, hanging-node lines) as the GMRES preconditioner of the device Newton. A linearized
-solve (the Newton step at a smooth state) reaches the Jacobi-preconditioned GMRES's solution (1e-8) in
+solve (the Newton step at a smooth state) reaches the Jacobi-preconditioned GMRES's solution (1e-6 relative, both at residual 1e-11) in
 fewer GMRES iterations; the level operators are the per-cell ones the oracle pins at 1e-12
 (tests/test_gpu_uforest.py). Parity pinned by the oracle
 only (the reference holds no multigrid)."""
@@ -62,7 +62,8 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k):
         out[mg] = (x.cpu().numpy(), its)
         assert ok and res <= 1e-11 * float(rhs.norm()) * 1.01, (mg, its, res)
     nvd = dim * p.n_vnodes
-    assert np.abs(out[True][0][:nvd] - out[False][0][:nvd]).max() < 1e-8 * max(1.0, np.abs(out[False][0][:nvd]).max())
+    # both at rel. residual 1e-11; the difference is that times the conditioning (~1e4 on the shells)
+    assert np.abs(out[True][0][:nvd] - out[False][0][:nvd]).max() < 1e-6 * max(1.0, np.abs(out[False][0][:nvd]).max())
     its_mg, its_j = out[True][1], out[False][1]
     print("umesh GMG %s Q%d: %d levels %s DoFs, GMRES its %d (Jacobi %d)" % (name, k, len(probs),
                                                                            [q.n_dofs for q in probs], its_mg, its_j))
