@@ -110,13 +110,19 @@ SCHEME_NAMES = {0: "steady", 1: "bdf1", 2: "bdf2", 3: "bdf3"}
 @pytest.mark.gpu
 @pytest.mark.parametrize("np_ranks", [1, 4])
 def test_configs3_taylor_couette3d_kelly_pipeline(tmp_path, np_ranks):
-    from oracle.oracle import Oracle, kelly_from_face_pieces
-    from softx_2020_200_amd.native import UMesh
     prm = open(os.path.join(CASES, "taylor-couette3d_q2q1_kelly.prm")).read()
     tol = 1e-8
     out, dumps = run_app(tmp_path, prm, extra=("--precision", "9", "--np", str(np_ranks)))
-    assert len(dumps) == 3, out
     assert "Running on %d MPI rank(s)" % np_ranks in out
+    check_configs3_pipeline(out, dumps, tol)
+
+
+def check_configs3_pipeline(out, dumps, tol):
+    """every cycle's dump: the oracle's residual at it <= tol on the oracle's own copy of the mesh, the
+    printed error = the oracle's, the Kelly marking = the oracle's (then the oracle adapts its copy)"""
+    from oracle.oracle import Oracle, kelly_from_face_pieces
+    from softx_2020_200_amd.native import UMesh
+    assert len(dumps) == 3, out
     rows = [l.split() for l in out.splitlines() if re.match(r"^\s*\d+\s+\d\.\d+e[-+]\d+", l)]
     m = UMesh(3, "cylinder_shell", "1 : 0.25 : 1 : 8 : 2")
     m.refine_global(1)
@@ -203,22 +209,21 @@ def test_configs3_taylor_couette3d_kelly_hierarchy_multigrid(tmp_path):
     """configs[3]'s adaptive pipeline with the geometric multigrid on the triangulation's refinement
     hierarchy as the GMRES preconditioner (--precond hmg: gls_umesh_coarsen_to levels, gls_fe_space_mg_transfer,
     gls_mg_attach_transfers; MappingQ2 per-cell kernels on every level, hanging and slip lines) instead of the
-    reference's ILU: the same meshes and error table as the ILU run (converged Newton, 1e-8), the
-    preconditioner announced on stderr, the GMRES iteration totals printed."""
+    reference's ILU: the same oracle checks as the ILU pipeline above (converged residual at every cycle's
+    state, error table, Kelly marking), the preconditioner announced on stderr, the GMRES iteration totals
+    of both runs printed (the two runs' meshes may differ from the third cycle on: the marking of cells at
+    the refinement threshold depends on the inexact solves, as with the shipped cylinder_gls settings)."""
     prm = open(os.path.join(CASES, "taylor-couette3d_q2q1_kelly.prm")).read()
-    res = {}
+    its = {}
     for pc in ("mg", "hmg"):
         d = tmp_path / pc
         d.mkdir()
         out, dumps = run_app(d, prm, extra=("--precision", "9", "--precond", pc))
         err = (d / "stderr.txt").read_text()
-        rows = [l.split() for l in out.splitlines() if re.match(r"^\s*\d+\s+\d\.\d+e[-+]\d+", l)]
-        its = [l for l in out.splitlines() if "linear_iterations =" in l]
-        res[pc] = (rows, err, its, dumps)
-    assert "triangulation's refinement hierarchy" in res["hmg"][1], res["hmg"][1][-1500:]
-    assert "refinement hierarchy" not in res["mg"][1]
-    ra, rb = res["mg"][0], res["hmg"][0]
-    assert len(ra) == len(rb) == 3 and [r[0] for r in ra] == [r[0] for r in rb], (ra, rb)
-    for a, b in zip(ra, rb):
-        assert abs(float(a[1]) - float(b[1])) <= 1e-6 * float(a[1]), (a, b)
-    print("configs[3] GMRES totals: ILU %s, hierarchy GMG %s" % (res["mg"][2], res["hmg"][2]))
+        if pc == "hmg":
+            assert "triangulation's refinement hierarchy" in err, err[-1500:]
+            check_configs3_pipeline(out, dumps, 1e-8)
+        else:
+            assert "refinement hierarchy" not in err
+        its[pc] = [l for l in out.splitlines() if "linear_iterations =" in l]
+    print("configs[3] GMRES totals: ILU %s, hierarchy GMG %s" % (its["mg"], its["hmg"]))
