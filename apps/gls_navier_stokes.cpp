@@ -1496,8 +1496,9 @@ struct Solver {
     std::memset(&mp, 0, sizeof(mp));
     mp.n_levels = (int)lv.size();
     mp.levels = lv.data();
-    mp.pre_smooth = 2;
-    mp.post_smooth = 2;
+    mp.smoother = P.k != P.kp ? 1 : 0;  // Q2-Q1: ILU(0) sweeps (point Jacobi sees only the PSPG pressure diagonal)
+    mp.pre_smooth = mp.smoother ? 1 : 2;
+    mp.post_smooth = mp.smoother ? 1 : 2;
     mp.omega = 0.6;
     mp.coarse_direct = 1;
     ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
@@ -1662,8 +1663,9 @@ struct Solver {
     std::memset(&mp, 0, sizeof(mp));
     mp.n_levels = (int)lv.size();
     mp.levels = lv.data();
-    mp.pre_smooth = 2;
-    mp.post_smooth = 2;
+    mp.smoother = P.k != P.kp ? 1 : 0;  // Q2-Q1: ILU(0) sweeps (point Jacobi sees only the PSPG pressure diagonal)
+    mp.pre_smooth = mp.smoother ? 1 : 2;
+    mp.post_smooth = mp.smoother ? 1 : 2;
     mp.omega = 0.6;
     mp.coarse_direct = n_coarse <= 8192 ? 1 : -1;
     ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
@@ -1952,7 +1954,8 @@ struct Solver {
     const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
     char prec[256];
     if (!mg_levels.empty() && (rmesh || space))
-      std::snprintf(prec, sizeof prec, "geometric multigrid V(2,2)-cycle on the %s refinement hierarchy (%zu levels)",
+      std::snprintf(prec, sizeof prec, "geometric multigrid %s on the %s refinement hierarchy (%zu levels)",
+                    P.k != P.kp ? "V(1,1)-cycle with ILU(0) smoothing" : "V(2,2)-cycle with damped-Jacobi smoothing",
                     rmesh ? "forest's" : "triangulation's", mg_levels.size() + 1);
     else if (!mg_levels.empty())
       std::snprintf(prec, sizeof prec, "geometric multigrid V(1,1)-cycle on the nested hyper_cubes");

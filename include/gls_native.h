@@ -210,6 +210,11 @@ typedef struct {
   const int *level_sweeps;                    /* optional (NULL: uniform): 2*n_levels ints, the
                                                  pre / post sweep counts of each level (the entries of
                                                  the coarsest level are ignored) */
+  int smoother;                               /* 0: damped Jacobi (omega); 1: ILU(0) of each level's
+                                                 probed Jacobian, undamped (the smoother Trilinos ML
+                                                 uses under the reference's AMG, gls_navier_stokes.cc:
+                                                 1208-1226); levels with hanging nodes only
+                                                 (gls_mg_attach_transfers) */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
 /* The same V-cycle on a general level hierarchy with the caller's grid transfers: levels of an adaptive

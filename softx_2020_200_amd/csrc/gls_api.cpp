@@ -456,6 +456,7 @@ struct gls_ctx {
     // general hierarchies (gls_mg_attach_transfers): per level pair the prolongation P (fine rows), the
     // restriction R = P^T (coarse rows) as CSR, and the state injection (coarse DoF <- fine DoF)
     bool csr = false;
+    bool ilu_smooth = false;  // gls_mg_params.smoother = 1: ILU(0) sweeps on the levels above the coarsest
     struct Csr {
       DevBuf<int64_t> poff, roff;
       DevBuf<int32_t> pcol, rcol, inj;
@@ -1800,7 +1801,21 @@ int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nu
 // one damped-Jacobi sweep x <- x + omega D^-1 (b - A x) with the smoother's operator A (constrained
 // rows D_c x). Single rank on the brick path: fused into the J.v (brick-interior nodes) and the slab
 // sum (brick-surface nodes), so A x is never stored; otherwise smoother_apply + mg_jacobi_update.
-int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double omega) {
+}  // namespace
+static int ensure_ilu(gls_ctx *c);
+static int apply_ilu(gls_ctx *c, const double *v, double *z);
+namespace {
+// one ILU(0) smoothing sweep x <- x + M^-1 (b - A x) (M = the level's ILU(0), undamped; z: scratch)
+int ilu_sweep(gls_ctx *g, double *x, const double *b, double *y, double *z) {
+  GLS_TRY(ensure_ilu(g));
+  GLS_TRY(gls_jacobian_apply(g, x, y));
+  HIP_TRY(gls::vec_axpby(y, 1.0, b, -1.0, g->n_dofs, g->stream));  // y = b - A x
+  GLS_TRY(apply_ilu(g, y, z));
+  HIP_TRY(gls::vec_axpy(x, 1.0, z, g->n_dofs, g->stream));
+  return GLS_OK;
+}
+int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double omega, double *z = nullptr) {
+  if (z && g->ilu.on) return ilu_sweep(g, x, b, y, z);
   const bool nofuse = std::getenv("GLS_MG_NO_FUSE") != nullptr;
   const bool brick = g->use_brick && g->use_qdata && (g->use_colors || brick_slab(g)) && !g->dist.on &&
                      !g->hang.on && gls::brick_fused_jacobi_supported(g->k);
@@ -2360,7 +2375,12 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   }
   // one pre-sweep from 0 on a fused level: x = omega D^-1 b is formed inside the residual's J.v
   const bool first_fused = pre == 1 && l < L - 1 && first_sweep_fusable(g);
-  if (pre > 0 && !first_fused) {
+  double *zs = mg.ilu_smooth && g->ilu.on ? mgbuf(c, l, MB_BOX) : nullptr;  // ILU smoothing scratch
+  if (pre > 0 && !first_fused && zs) {
+    GLS_TRY(ensure_ilu(g));
+    GLS_TRY(apply_ilu(g, b, x));  // first sweep from x = 0: x = M^-1 b
+    for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om, zs));
+  } else if (pre > 0 && !first_fused) {
     HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, d, om, n, 1, s));  // first sweep from x = 0
     for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(g, x, b, y, om));
   } else if (pre == 0) {
@@ -2391,7 +2411,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
     HIP_TRY(gls::vec_set_indexed(y, g->con_dofs.p, nullptr, (int64_t)g->con_dofs.n, s));
     HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
   }
-  for (int it = 0; it < mg.lpost[(size_t)l]; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega));
+  for (int it = 0; it < mg.lpost[(size_t)l]; ++it) GLS_TRY(smoother_sweep(g, x, b, y, mg.omega, zs));
   return GLS_OK;
 }
 
@@ -2810,11 +2830,21 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       mg.lpost[(size_t)l] = p->level_sweeps[2 * l + 1];
     }
   for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
+  mg.ilu_smooth = p->smoother == 1;
+  if (p->smoother < 0 || p->smoother > 1 || (mg.ilu_smooth && !mg.csr))
+    return set_err(GLS_EINVAL, "mg: smoother 0 (Jacobi) or 1 (ILU, gls_mg_attach_transfers hierarchies)");
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
-      const bool need = b == MB_BOX ? mg.boxed : (l > 0 || b == MB_Y);
-      if (need) GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
+      const bool need = b == MB_BOX ? (mg.boxed || mg.ilu_smooth) : (l > 0 || b == MB_Y);
+      if (need)
+        GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX && mg.boxed ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
+    }
+  if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (Cuthill-McKee order; multicolor above 1e5 DoFs)
+    for (int l = 0; l + 1 < p->n_levels; ++l) {
+      gls_ctx *g = mg.lev[(size_t)l];
+      GLS_TRY(gls_ilu_set_options(g, g->n_dofs > 100000 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM, 0));
+      GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
     }
   // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
   {

@@ -95,7 +95,7 @@ class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
                 ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
                 ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int),
-                ("level_sweeps", C.POINTER(C.c_int))]
+                ("level_sweeps", C.POINTER(C.c_int)), ("smoother", C.c_int)]
 
 
 class RefinedMesh(C.Structure):
@@ -754,10 +754,10 @@ class GLSContext:
         self._mg_levels = levels
 
     def attach_multigrid_transfers(self, coarse_levels, transfers, pre_smooth=2, post_smooth=2, coarse_sweeps=30,
-                                   omega=0.6, coarse_omega=0.0, coarse_direct=0, level_sweeps=None):
+                                   omega=0.6, coarse_omega=0.0, coarse_direct=0, level_sweeps=None, smoother="jacobi"):
         """The V-cycle on a general hierarchy (gls_mg_attach_transfers): levels [self] + coarse_levels
         (hanging lines set on each), transfers[l] = (off, col, w, inject) from level l+1 to level l
-        (octree_mg_transfer). FP64 smoothing."""
+        (octree_mg_transfer). FP64 smoothing: damped Jacobi, or smoother="ilu" (ILU(0) per level)."""
         levels = [self] + list(coarse_levels)
         if len(transfers) != len(levels) - 1:
             raise GLSError("attach_multigrid_transfers: one transfer per level pair")
@@ -778,7 +778,7 @@ class GLSContext:
         ws = (PD * len(keep))(*[k[2].ctypes.data_as(PD) for k in keep])
         injs = (P64 * len(keep))(*[k[3].ctypes.data_as(P64) for k in keep])
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct, 0, ls)
+                     coarse_omega, coarse_direct, 0, ls, {"jacobi": 0, "ilu": 1}[smoother])
         check(self.L.gls_mg_attach_transfers(self.h, C.byref(p), offs, cols, ws, injs), "gls_mg_attach_transfers")
         self._mg_levels = levels
 

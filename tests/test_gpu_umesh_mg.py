@@ -30,14 +30,14 @@ def mapped_level(sp, nu):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,dim,spec,flat", [c for c in CASES if c[0] in ("shell", "cylshell", "rect3d")],
                          ids=["shell", "rect3d", "cylshell"])
-@pytest.mark.parametrize("k", [1, 2])
-def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k):
+@pytest.mark.parametrize("k,kp,smoother", [(1, 1, "jacobi"), (2, 2, "jacobi"), (2, 1, "ilu")])
+def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k, kp, smoother):
     m = make_mesh(dim, spec)
     m.refine_global(1)
     random_adapt(m, 2 if dim == 2 else 1, seed=5, k=k)
-    hf = m.fe_space_handle(k, k, qmapping_all=True)
+    hf = m.fe_space_handle(k, kp, qmapping_all=True)
     L = int(hf.data["cell_level"].max())
-    handles = [hf] + [m.coarsen_to(L - l).fe_space_handle(k, k, qmapping_all=True) for l in range(1, L + 1)]
+    handles = [hf] + [m.coarsen_to(L - l).fe_space_handle(k, kp, qmapping_all=True) for l in range(1, L + 1)]
     probs = [mapped_level(h.data, 0.1) for h in handles]
     xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(L)]
     p = probs[0]
@@ -52,7 +52,9 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k):
     for mg in (False, True):
         ctxs = [context_for(q) for q in (probs if mg else probs[:1])]
         if mg:
-            ctxs[0].attach_multigrid_transfers(ctxs[1:], xfer, pre_smooth=2, post_smooth=2, omega=0.6, coarse_direct=1)
+            sw = 2 if smoother == "jacobi" else 1
+            ctxs[0].attach_multigrid_transfers(ctxs[1:], xfer, pre_smooth=sw, post_smooth=sw, omega=0.6, coarse_direct=1,
+                                               smoother=smoother)
         U, U1 = cuda(u), cuda(np.zeros(p.n_dofs))
         ctxs[0].apply_dirichlet(U)
         ctxs[0].set_state(U, U1)
@@ -65,6 +67,6 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k):
     # both at rel. residual 1e-11; the difference is that times the conditioning (~1e4 on the shells)
     assert np.abs(out[True][0][:nvd] - out[False][0][:nvd]).max() < 1e-6 * max(1.0, np.abs(out[False][0][:nvd]).max())
     its_mg, its_j = out[True][1], out[False][1]
-    print("umesh GMG %s Q%d: %d levels %s DoFs, GMRES its %d (Jacobi %d)" % (name, k, len(probs),
+    print("umesh GMG %s Q%dQ%d %s: %d levels %s DoFs, GMRES its %d (Jacobi %d)" % (name, k, kp, smoother, len(probs),
                                                                            [q.n_dofs for q in probs], its_mg, its_j))
     assert its_mg * 2 < its_j, (its_mg, its_j)
