@@ -137,6 +137,12 @@ int gls_jacobian_apply_f32(gls_ctx *ctx, const double *v, double *Jv);
 int gls_set_hanging(gls_ctx *ctx, int64_t n_lines, const int64_t *dofs, const int64_t *offsets,
                     const int64_t *masters, const double *weights);
 
+/* Adapted forests (after gls_set_hanging on 3D Q2-Q2 box cells): the number of complete sibling groups
+ * of leaves (8 consecutive cells forming a 2x2x2 brick) whose J.v / diagonal run the sum-factorised pencil
+ * kernel (cached linearization, element-vector output summed with the per-cell kernel's); 0 = per-cell
+ * kernels only (GLS_OCT_BRICKS=0 in the environment forces it). */
+int gls_forest_bricks(const gls_ctx *ctx);
+
 /* Diagonal of that assembled Jacobian (DEVICE pointer). */
 int gls_jacobian_diagonal(gls_ctx *ctx, double *diag);
 

@@ -430,6 +430,14 @@ struct gls_ctx {
     DevBuf<double> vbuf;                               // C v for J.v
     std::vector<int64_t> h_dof, h_off, h_master;       // host copy of the lines (ILU sparsity)
   } hang;
+  // adapted forests (hanging contexts, 3D Q2-Q2 boxes): the complete sibling groups of leaves run the
+  // pencil kernel (cached linearization, element-vector output), the other cells the per-cell kernel
+  struct Oct {
+    bool on = false;
+    int nb = 0;
+    DevBuf<int32_t> cell0, list;  // first cell of each brick; 0..nb-1 (the launch's brick list)
+    DevBuf<uint8_t> skip;         // per-cell kernel batches made only of brick cells
+  } oct;
   // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
   struct Lattice {
     bool set = false;
@@ -1152,6 +1160,26 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     GLS_TRY(ensure_element_maps(c));
     P.ev = c->ev.p;
   }
+  // adapted forest: the sibling-group bricks by the pencil kernel (J.v from the cached linearization; the
+  // diagonal pass computes that cache), the per-cell kernel skips the batches made only of brick cells
+  const bool oct = c->oct.on && (mode == gls::MODE_JV || mode == gls::MODE_DIAG) && !brick;
+  if (oct) {
+    const size_t nq = gls::brick_qdata_size(c->k, 8 * c->oct.nb);
+    if (c->qdata.n != nq) {
+      GLS_TRY(c->qdata.alloc(nq));
+      c->qd_valid = false;
+    }
+    if (mode == gls::MODE_JV && !c->qd_valid) {  // linearization only (no output), at the current state
+      gls::OpParams L = make_params(c, true);
+      L.qd = c->qdata.p;
+      L.subset = c->oct.list.p;
+      L.subset_n = c->oct.nb;
+      L.brick_cell0 = c->oct.cell0.p;
+      HIP_TRY(gls::launch_pencil_ev(gls::MODE_LIN, L, c->tables, c->stream));
+      c->qd_valid = true;
+    }
+    P.blk_skip = c->oct.skip.p;
+  }
   if (!col && !P.slab && !P.ev) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
     TimedLaunch t(c, mode == gls::MODE_JVQ ? (int)gls::MODE_JV : (lin_diag ? (int)gls::MODE_DIAG : mode));
@@ -1181,6 +1209,17 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     } else {
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
+      if (oct) {  // after the per-cell launch: the bricks' element vectors overwrite its mixed batches' ones
+        gls::OpParams Q = P;
+        Q.blk_skip = nullptr;
+        Q.y = nullptr;  // element vectors only
+        Q.qd = c->qdata.p;
+        Q.subset = c->oct.list.p;
+        Q.subset_n = c->oct.nb;
+        Q.brick_cell0 = c->oct.cell0.p;
+        HIP_TRY(gls::launch_pencil_ev(mode == gls::MODE_JV ? gls::MODE_JVQ : gls::MODE_LIN, Q, c->tables, c->stream));
+        if (mode == gls::MODE_DIAG) c->qd_valid = true;
+      }
     }
   }
   if (P.ev)
@@ -1894,6 +1933,73 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
   return GLS_OK;
 }
 
+}  // extern "C"
+// sibling groups of an adapted forest's leaves that form 2x2x2 bricks: 8 consecutive cells (the forest's
+// depth-first order keeps a complete family together, children x fastest) of equal extents whose node
+// maps agree on the 5^3 brick lattice (a node shared by two cells sits at the same brick position in
+// both). GLS_OCT_BRICKS=0: per-cell kernels only.
+static int detect_oct_bricks(gls_ctx *c) {
+  auto &O = c->oct;
+  O = gls_ctx::Oct();
+  const char *e = std::getenv("GLS_OCT_BRICKS");
+  if ((e && std::atoi(e) == 0) || c->dim != 3 || c->k != 2 || c->kp != 2 || c->map_degree > 0 || c->dist.on ||
+      c->cell_pnodes.p || c->host_h.empty() || !gls::pencil_enabled() || c->n_cells < 8)
+    return GLS_OK;
+  const int64_t nc = c->n_cells;
+  std::vector<int32_t> cv((size_t)nc * 27);
+  HIP_TRY(hipMemcpy(cv.data(), c->cell_vnodes.p, cv.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> cell0;
+  std::vector<char> in((size_t)nc, 0);
+  int32_t lat[125];
+  for (int64_t i = 0; i + 8 <= nc;) {
+    bool ok = true;
+    for (int ci = 1; ci < 8 && ok; ++ci)
+      for (int d = 0; d < 3; ++d) ok = ok && c->host_h[(size_t)(i + ci) * 3 + d] == c->host_h[(size_t)i * 3 + d];
+    for (int t = 0; t < 125 && ok; ++t) lat[t] = -1;
+    for (int ci = 0; ci < 8 && ok; ++ci) {
+      const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
+      for (int a = 0; a < 27 && ok; ++a) {
+        const int X = 2 * cx + a % 3, Y = 2 * cy + (a / 3) % 3, Z = 2 * cz + a / 9;
+        int32_t &slot = lat[X + 5 * (Y + 5 * Z)];
+        const int32_t nd = cv[(size_t)(i + ci) * 27 + a];
+        if (slot < 0) slot = nd;
+        else ok = slot == nd;
+      }
+    }
+    if (ok) {  // 125 distinct nodes
+      std::vector<int32_t> u(lat, lat + 125);
+      std::sort(u.begin(), u.end());
+      ok = std::adjacent_find(u.begin(), u.end()) == u.end();
+    }
+    if (ok) {
+      cell0.push_back((int32_t)i);
+      for (int ci = 0; ci < 8; ++ci) in[(size_t)(i + ci)] = 1;
+      i += 8;
+    } else {
+      ++i;
+    }
+  }
+  if (cell0.empty()) return GLS_OK;
+  const int CB = gls::cell_kernel_cells_per_block(3, 2, 3, false);
+  const int64_t nblk = (nc + CB - 1) / CB;
+  std::vector<uint8_t> skip((size_t)nblk, 0);
+  for (int64_t b = 0; b < nblk; ++b) {
+    bool all = true;
+    for (int64_t q = b * CB; q < std::min<int64_t>(nc, (b + 1) * CB); ++q) all = all && in[(size_t)q];
+    skip[(size_t)b] = all ? 1 : 0;
+  }
+  std::vector<int32_t> list(cell0.size());
+  for (size_t b = 0; b < list.size(); ++b) list[b] = (int32_t)b;
+  GLS_TRY(O.cell0.upload(cell0.data(), cell0.size()));
+  GLS_TRY(O.list.upload(list.data(), list.size()));
+  GLS_TRY(O.skip.upload(skip.data(), skip.size()));
+  O.nb = (int)cell0.size();
+  O.on = true;
+  return GLS_OK;
+}
+extern "C" {
+int gls_forest_bricks(const gls_ctx *c) { return c && c->oct.on ? c->oct.nb : 0; }
+
 int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *off, const int64_t *masters,
                     const double *w) {
   GLS_TRY(check_ctx(c));
@@ -1979,7 +2085,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
-  return GLS_OK;
+  return detect_oct_bricks(c);
 }
 
 // --------------------------------------------------------------------------------------------

@@ -119,6 +119,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   const int g = xcd_swizzle((int)blockIdx.x, n_groups);      // XCD-aware: contiguous Morton triples per XCD
   const int nbg = min(3, n_items - 3 * g);                   // bricks in this group (last one may be short)
   auto brick_of = [&](int bi) { return subset ? subset[3 * g + bi] : 3 * g + bi; };
+  // first cell of a brick: 8 b on the cube; the listed cell on an adapted forest's sibling groups
+  auto cell0 = [&](int b) -> int64_t { return P.brick_cell0 ? (int64_t)P.brick_cell0[b] : (int64_t)b * 8; };
   const int64_t voff = (int64_t)3 * P.n_vnodes;
 
   if (tid < 48) {
@@ -134,7 +136,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   const bool valid = act && bi < nbg;
   const int brick = brick_of(valid ? bi : 0);
   const int cx = ci & 1, cy = (ci >> 1) & 1, cz = ci >> 2;
-  const int64_t gcell = (int64_t)brick * 8 + (valid ? ci : 0);
+  const int64_t gcell = cell0(brick) + (valid ? ci : 0);
   const Real hx = (Real)P.geo[gcell * 4 + 0], hy = (Real)P.geo[gcell * 4 + 1], hz = (Real)P.geo[gcell * 4 + 2];
   const Real ihx = Real(1) / hx, ihy = Real(1) / hy, ihz = Real(1) / hz;
   const Real wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
@@ -154,7 +156,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
     const int cx = min(X / 2, 1), cy = min(Y / 2, 1), cz = min(Z / 2, 1);
     const int a = (X - 2 * cx) + 3 * ((Y - 2 * cy) + 3 * (Z - 2 * cz));
-    const int node = P.cell_vnodes[((int64_t)brick * 8 + cx + 2 * cy + 4 * cz) * 27 + a];
+    const int node = P.cell_vnodes[(cell0(brick) + cx + 2 * cy + 4 * cz) * 27 + a];
     const int64_t i3 = (int64_t)node * 3;
     Real *b = sB + bi * NF * FB + X + SY * Y + SZ * Z;
     if constexpr (ST) {
@@ -384,6 +386,20 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     }
   };
 
+  // element-vector output (adapted forests: the ordered per-node sums of gather_element_vectors include
+  // these cells' 27-node vectors with the per-cell kernel's; layout [cell][a * 3 + c | 81 + a])
+  auto write_ev = [&]() {
+    for (int t = tid; t < nbg * 8 * 27; t += C::THREADS) {
+      const int rb_ = t / 216, r = t - rb_ * 216, ci_ = r / 27, a = r - ci_ * 27;
+      const Real *o = sO + (rb_ * 8 + ci_) * C::OC + a;
+      double *e = P.ev + (cell0(brick_of(rb_)) + ci_) * 108;
+      e[a * 3] = (double)o[0];
+      e[a * 3 + 1] = (double)o[C::OF];
+      e[a * 3 + 2] = (double)o[2 * C::OF];
+      e[81 + a] = (double)o[3 * C::OF];
+    }
+  };
+
   if constexpr (ST) {
     // ---------------- residual (assemble_rhs, gls_navier_stokes.cc:391-516) / linearization (MODE_LIN:
     // u, grad u, tau, R_s per point into the pencil rows, then the Jacobian diagonal): values of u, H
@@ -528,7 +544,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       //   A = (du_c/dx_c + alpha_jac) phi + a, a = u . grad phi;  J_ii(p) = sum_q JxW tau |grad psi|^2,
       // deal.II's |K_e(i,i)| on constrained rows. Lane (a, b) = node column (ix, iy), nodes iz = 0..2;
       // the points' data go through the stage area one qz plane at a time.
-      if (P.y == nullptr) return;  // linearization only (uniform over the workgroup)
+      if (P.y == nullptr && P.ev == nullptr) return;  // linearization only (uniform over the workgroup)
       Real Vx[3], Dx[3], Sx[3], Vy[3], Dy[3], Sy[3];  // the lane's node columns of the 1D tables
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -594,7 +610,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
 #pragma unroll
         for (int iz = 0; iz < 3; ++iz) {
           const int bn = (2 * cx + pa) + BN * ((2 * cy + pb) + BN * (2 * cz + iz));
-          const unsigned msk = P.vmask ? P.vmask[sNode[bi * BN3P + bn]] : 0u;
+          const int nd = sNode[bi * BN3P + bn];  // constrained: Dirichlet or hanging (per-cell kernel's rule)
+          const unsigned msk = (P.vmask ? P.vmask[nd] : 0u) | (P.hmask ? P.hmask[nd] : 0u);
 #pragma unroll
           for (int c3 = 0; c3 < 3; ++c3)
             outc[c3 * C::OF + 9 * iz + 3 * pb + pa] = (msk >> c3) & 1u ? fabs(acc[iz][c3]) : acc[iz][c3];
@@ -727,7 +744,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   }  // MODE_JVQ
   __syncthreads();
 
-  reduce_scatter(P.y, P.slab, true);
+  if (P.ev) write_ev();
+  else reduce_scatter(P.y, P.slab, true);
 }
 
 // Selection: on by default for the Q2 brick J.v with a slab (the launch contract of the
@@ -774,6 +792,16 @@ hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStrea
 hipError_t launch_pencil_reslin(const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (P.bricks || P.subset || !P.qd || !P.y || !P.slab || !P.res_y || !P.res_slab) return hipErrorNotSupported;
   return launch_pencil_t<double, MODE_RESLIN>(P, T, s);
+}
+// adapted forests: the listed sibling-group bricks (P.subset over P.brick_cell0), element-vector output
+// (P.ev); mode MODE_JVQ (FP64) or MODE_LIN (linearization rows + the diagonal's element vectors)
+hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
+  if ((!P.ev && mode != MODE_LIN) || P.y || !P.brick_cell0 || !P.subset || P.subset_n <= 0 || !P.qd || P.slab ||
+      P.bricks || P.n_probe > 0 || P.rb || P.jx || P.jx0)
+    return hipErrorNotSupported;
+  if (mode == MODE_JVQ) return launch_pencil_t<double, MODE_JVQ>(P, T, s);
+  if (mode == MODE_LIN) return launch_pencil_t<double, MODE_LIN>(P, T, s);
+  return hipErrorNotSupported;
 }
 hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (P.bricks || (P.y && !P.slab) || P.subset || !P.qd) return hipErrorNotSupported;

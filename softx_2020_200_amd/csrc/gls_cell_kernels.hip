@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * CB;
   const int ncb = min(CB, P.n_cells - c0);
+  if (P.blk_skip && P.blk_skip[blockIdx.x]) return;  // every cell of the batch is in a pencil brick (uniform)
   const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
 
   // batched J.v (probing): this block's vector; J is linear, so a batch of cells on which the vector

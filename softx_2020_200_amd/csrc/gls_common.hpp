@@ -50,6 +50,10 @@ struct OpParams {
   const double *force_q;      // [n_cells][nq][dim] or nullptr
   const uint8_t *vmask;       // [n_vnodes] zero_constraints bits, nullptr = none
   const uint8_t *hmask;       // [n_vnodes] hanging velocity components (MODE_DIAG: |K_ii| per cell)
+  // pencil kernel on the complete sibling groups of an adapted forest: first cell of each (compact)
+  // brick; the launch writes element vectors (ev) instead of node sums
+  const int32_t *brick_cell0;
+  const uint8_t *blk_skip;  // per-cell kernels: blocks (CB-cell batches) to skip (cells the pencil covers)
   const double *u;
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input

@@ -44,7 +44,7 @@ EXPORTS = [
     "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
     "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals", "gls_fe_space_boundary_normal_sets",
     "gls_octree_coarsen_to", "gls_octree_mg_transfer", "gls_mg_attach_transfers", "gls_umesh_coarsen_to",
-    "gls_fe_space_mg_transfer",
+    "gls_fe_space_mg_transfer", "gls_forest_bricks",
 ]
 
 
@@ -172,6 +172,7 @@ def load():
                                           C.POINTER(C.POINTER(i64))]
     L.gls_octree_coarsen_to.argtypes = [vp, C.c_int, C.POINTER(vp)]
     L.gls_umesh_coarsen_to.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.gls_forest_bricks.argtypes = [vp]
     L.gls_fe_space_mg_transfer.argtypes = [C.POINTER(FESpace), C.POINTER(FESpace), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_octree_mg_transfer.argtypes = [C.POINTER(RefinedMesh), C.POINTER(RefinedMesh), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
@@ -641,6 +642,10 @@ class GLSContext:
     def set_state(self, u, u1=None, u2=None, u3=None):
         self._state = (u, u1, u2, u3)  # keep tensors alive while borrowed
         check(self.L.gls_set_state(self.h, _ptr(u), _ptr(u1), _ptr(u2), _ptr(u3)), "gls_set_state")
+
+    def forest_bricks(self):
+        """sibling-group bricks of an adapted forest that run the pencil kernel (gls_forest_bricks)"""
+        return int(self.L.gls_forest_bricks(self.h))
 
     def set_hanging(self, dofs, offsets, masters, weights):
         """Hanging-node constraint lines (gls_set_hanging): DoF dofs[i] = sum w * masters."""
