@@ -436,7 +436,8 @@ struct gls_ctx {
     bool on = false;
     int nb = 0;
     DevBuf<int32_t> cell0, list;  // first cell of each brick; 0..nb-1 (the launch's brick list)
-    DevBuf<uint8_t> skip;         // per-cell kernel batches made only of brick cells
+    DevBuf<int32_t> rest;         // the cells outside the bricks (the per-cell kernel's list)
+    int n_rest = 0;
   } oct;
   // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
   struct Lattice {
@@ -1161,7 +1162,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     P.ev = c->ev.p;
   }
   // adapted forest: the sibling-group bricks by the pencil kernel (J.v from the cached linearization; the
-  // diagonal pass computes that cache), the per-cell kernel skips the batches made only of brick cells
+  // diagonal pass computes that cache), the other cells by the per-cell kernel (its cell list)
   const bool oct = c->oct.on && (mode == gls::MODE_JV || mode == gls::MODE_DIAG) && !brick;
   if (oct) {
     const size_t nq = gls::brick_qdata_size(c->k, 8 * c->oct.nb);
@@ -1178,7 +1179,8 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       HIP_TRY(gls::launch_pencil_ev(gls::MODE_LIN, L, c->tables, c->stream));
       c->qd_valid = true;
     }
-    P.blk_skip = c->oct.skip.p;
+    P.cell_list = c->oct.rest.p;  // the per-cell kernel runs the cells outside the bricks only
+    P.cell_list_n = c->oct.n_rest;
   }
   if (!col && !P.slab && !P.ev) HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * c->n_dofs, c->stream));
   {
@@ -1209,9 +1211,10 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     } else {
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
-      if (oct) {  // after the per-cell launch: the bricks' element vectors overwrite its mixed batches' ones
+      if (oct) {  // the bricks' cells: element vectors from the pencil kernel
         gls::OpParams Q = P;
-        Q.blk_skip = nullptr;
+        Q.cell_list = nullptr;
+        Q.cell_list_n = 0;
         Q.y = nullptr;  // element vectors only
         Q.qd = c->qdata.p;
         Q.subset = c->oct.list.p;
@@ -1980,19 +1983,15 @@ static int detect_oct_bricks(gls_ctx *c) {
     }
   }
   if (cell0.empty()) return GLS_OK;
-  const int CB = gls::cell_kernel_cells_per_block(3, 2, 3, false);
-  const int64_t nblk = (nc + CB - 1) / CB;
-  std::vector<uint8_t> skip((size_t)nblk, 0);
-  for (int64_t b = 0; b < nblk; ++b) {
-    bool all = true;
-    for (int64_t q = b * CB; q < std::min<int64_t>(nc, (b + 1) * CB); ++q) all = all && in[(size_t)q];
-    skip[(size_t)b] = all ? 1 : 0;
-  }
+  std::vector<int32_t> rest;
+  for (int64_t q = 0; q < nc; ++q)
+    if (!in[(size_t)q]) rest.push_back((int32_t)q);
   std::vector<int32_t> list(cell0.size());
   for (size_t b = 0; b < list.size(); ++b) list[b] = (int32_t)b;
   GLS_TRY(O.cell0.upload(cell0.data(), cell0.size()));
   GLS_TRY(O.list.upload(list.data(), list.size()));
-  GLS_TRY(O.skip.upload(skip.data(), skip.size()));
+  GLS_TRY(O.rest.upload(rest.data(), std::max<size_t>(rest.size(), 1)));
+  O.n_rest = (int)rest.size();
   O.nb = (int)cell0.size();
   O.on = true;
   return GLS_OK;

@@ -60,8 +60,9 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
 
   const int tid = threadIdx.x;
   const int c0 = blockIdx.x * CB;
-  const int ncb = min(CB, P.n_cells - c0);
-  if (P.blk_skip && P.blk_skip[blockIdx.x]) return;  // every cell of the batch is in a pencil brick (uniform)
+  // cell list (adapted forests: the cells outside the pencil's sibling-group bricks), else all cells
+  const int ncb = min(CB, (P.cell_list ? P.cell_list_n : P.n_cells) - c0);
+  auto cid = [&](int cl) -> int64_t { return P.cell_list ? (int64_t)P.cell_list[c0 + cl] : (int64_t)(c0 + cl); };
   const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
 
   // batched J.v (probing): this block's vector; J is linear, so a batch of cells on which the vector
@@ -74,12 +75,12 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
       Pev += (int64_t)blockIdx.y * P.bev_stride;
       int any = 0;
       for (int i = tid; i < ncb * NV; i += blockDim.x) {
-        const int64_t b = (int64_t)P.cell_vnodes[(int64_t)c0 * NV + i] * DIM;
+        const int64_t b = (int64_t)P.cell_vnodes[cid(i / NV) * NV + i % NV] * DIM;
 #pragma unroll
         for (int c = 0; c < DIM; ++c) any |= Pv[b + c] != 0.0;
       }
       for (int i = tid; i < ncb * NP; i += blockDim.x) {
-        const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+        const int pn = P.cell_pnodes ? P.cell_pnodes[cid(i / NP) * NP + i % NP] : P.cell_vnodes[cid(i / NV) * NV + i % NV];
         any |= Pv[voff + pn] != 0.0;
       }
       const int act = __syncthreads_or(any);
@@ -94,7 +95,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   }
   // ---- 1. gather (velocity-type fields)
   for (int i = tid; i < ncb * NV; i += blockDim.x) {
-    const int node = P.cell_vnodes[(int64_t)c0 * NV + i];
+    const int node = P.cell_vnodes[cid(i / NV) * NV + i % NV];
     const int64_t b = (int64_t)node * DIM;
 #pragma unroll
     for (int c = 0; c < DIM; ++c) sU[i * DIM + c] = P.u[b + c];
@@ -117,7 +118,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     }
   }
   for (int i = tid; i < ncb * NP; i += blockDim.x) {
-    const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+    const int pn = P.cell_pnodes ? P.cell_pnodes[cid(i / NP) * NP + i % NP] : P.cell_vnodes[cid(i / NV) * NV + i % NV];
     sP[i] = P.u[voff + pn];
     if constexpr (MODE == MODE_JV) sVP[i] = Pv[voff + pn];
   }
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   // ---- 2./3. evaluate + pointwise, one thread per (cell, q)
   if (tid < ncb * NQ) {
     const int cl = tid / NQ, q = tid % NQ;
-    const int cell = c0 + cl;
+    const int cell = (int)cid(cl);
     const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
     const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
     const double hst = P.geo[cell * 4 + 3];
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     const int cl = i / NV, a = i % NV;
     const int ax = a % C::K1, ay = (a / C::K1) % C::K1, az = DIM == 3 ? a / (C::K1 * C::K1) : 0;
     const double *Tc = sT + cl * NQ * NT;
-    const int node = P.cell_vnodes[(int64_t)c0 * NV + i];
+    const int node = P.cell_vnodes[cid(i / NV) * NV + i % NV];
     if constexpr (MODE != MODE_DIAG) {
       double out[DIM] = {};
 #pragma nounroll
@@ -442,7 +443,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
         }
       }
       if (Pev) {
-        double *e = Pev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
+        double *e = Pev + cid(cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
         for (int c = 0; c < DIM; ++c) e[c] = out[c];
       } else {
@@ -450,7 +451,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
         for (int c = 0; c < DIM; ++c) atomicAdd(&P.y[(int64_t)node * DIM + c], out[c]);
       }
     } else {
-      const int cell = c0 + cl;
+      const int cell = (int)cid(cl);
       const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
       const double ih[3] = {1.0 / hx, 1.0 / hy, 1.0 / hz};
       const double nu = P.nu, aj = P.alpha_jac;
@@ -497,7 +498,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
       // constrained rows (Dirichlet or hanging) get deal.II's |K_e(i,i)| per cell
       const unsigned m = (P.vmask ? P.vmask[node] : 0u) | (P.hmask ? P.hmask[node] : 0u);
       if (Pev) {
-        double *e = Pev + (int64_t)(c0 + cl) * (NV * DIM + NP) + a * DIM;
+        double *e = Pev + cid(cl) * (NV * DIM + NP) + a * DIM;
 #pragma unroll
         for (int c = 0; c < DIM; ++c) e[c] = ((m >> c) & 1u) ? fabs(out[c]) : out[c];
       } else {
@@ -510,7 +511,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     const int cl = i / NP, a = i % NP;
     const int ax = a % C::KP1, ay = (a / C::KP1) % C::KP1, az = DIM == 3 ? a / (C::KP1 * C::KP1) : 0;
     const double *Tc = sT + cl * NQ * NT;
-    const int pn = P.cell_pnodes ? P.cell_pnodes[(int64_t)c0 * NP + i] : P.cell_vnodes[(int64_t)c0 * NV + i];
+    const int pn = P.cell_pnodes ? P.cell_pnodes[cid(i / NP) * NP + i % NP] : P.cell_vnodes[cid(i / NV) * NV + i % NV];
     double out = 0.;
     if constexpr (MODE != MODE_DIAG) {
 #pragma nounroll
@@ -525,7 +526,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
         out += s;
       }
     } else {
-      const int cell = c0 + cl;
+      const int cell = (int)cid(cl);
       const double hx = P.geo[cell * 4 + 0], hy = P.geo[cell * 4 + 1], hz = DIM == 3 ? P.geo[cell * 4 + 2] : 1.0;
 #pragma nounroll
       for (int q = 0; q < NQ; ++q) {
@@ -549,7 +550,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
         out += Tq[0] * Tq[1] * (g0 * g0 + g1 * g1 + g2 * g2);
       }
     }
-    if (Pev) Pev[(int64_t)(c0 + cl) * (NV * DIM + NP) + NV * DIM + a] = out;
+    if (Pev) Pev[cid(cl) * (NV * DIM + NP) + NV * DIM + a] = out;
     else atomicAdd(&P.y[voff + pn], out);
   }
 }
@@ -565,7 +566,7 @@ size_t cell_kernel_lds_bytes() {
 template <int DIM, int K, int KP, int NQ1, bool GEN>
 hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
   using C = Cfg<DIM, K, KP, NQ1>;
-  const int blocks = (P.n_cells + C::CB - 1) / C::CB;
+  const int blocks = ((P.cell_list ? P.cell_list_n : P.n_cells) + C::CB - 1) / C::CB;
   const size_t lds = cell_kernel_lds_bytes<DIM, K, KP, NQ1>();
   static bool attr_set = false;  // allow > 64 KiB dynamic LDS (gfx950 has 160 KiB per CU)
   if (!attr_set) {
@@ -601,7 +602,8 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
 }
 template <int DIM, int K, int KP, int NQ1>
 hipError_t launch_cell_t(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
-  if (P.n_cells <= 0) return hipSuccess;
+  if (P.n_cells <= 0 || (P.cell_list && P.cell_list_n <= 0)) return hipSuccess;
+  if (P.cell_list && P.bv_stride) return hipErrorNotSupported;  // probes run over all cells
   if (P.gq) return launch_cell_g<DIM, K, KP, NQ1, true>(mode, P, T, s);
   return launch_cell_g<DIM, K, KP, NQ1, false>(mode, P, T, s);
 }

@@ -53,7 +53,8 @@ struct OpParams {
   // pencil kernel on the complete sibling groups of an adapted forest: first cell of each (compact)
   // brick; the launch writes element vectors (ev) instead of node sums
   const int32_t *brick_cell0;
-  const uint8_t *blk_skip;  // per-cell kernels: blocks (CB-cell batches) to skip (cells the pencil covers)
+  const int32_t *cell_list;  // per-cell kernels: the cells to run (NULL: all), e.g. those outside forest bricks
+  int cell_list_n;
   const double *u;
   const double *h1, *h2, *h3; // history (solution_m1..m3)
   const double *v;            // JV input

@@ -6,7 +6,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method threa
   > gpurun_out/fb_tests.log 2>&1 || { tail -40 gpurun_out/fb_tests.log; exit 1; }
 grep -E "PASSED|FAILED|forest bricks" gpurun_out/fb_tests.log
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_hanging.py \
-  tests/test_gpu_octree_mg.py tests/test_gpu_parity.py > gpurun_out/fb_regress.log 2>&1 || { tail -40 gpurun_out/fb_regress.log; exit 1; }
+  tests/test_gpu_octree_mg.py tests/test_gpu_parity.py tests/test_gpu_uforest.py tests/test_gpu_mapped.py > gpurun_out/fb_regress.log 2>&1 || { tail -40 gpurun_out/fb_regress.log; exit 1; }
 tail -2 gpurun_out/fb_regress.log
 timeout -k 10 300 python3 bench.py --workload octree --cells 4 --octree-steps 4 --steps 5 --warmup 1 --mg-smooth 2 2 --mg-omega 0.6 > gpurun_out/fb_oct.json 2> gpurun_out/fb_oct.err || { tail -5 gpurun_out/fb_oct.err; exit 1; }
 cut -c1-300 gpurun_out/fb_oct.json
