@@ -1990,8 +1990,9 @@ static int detect_oct_bricks(gls_ctx *c) {
   for (size_t b = 0; b < list.size(); ++b) list[b] = (int32_t)b;
   GLS_TRY(O.cell0.upload(cell0.data(), cell0.size()));
   GLS_TRY(O.list.upload(list.data(), list.size()));
-  GLS_TRY(O.rest.upload(rest.data(), std::max<size_t>(rest.size(), 1)));
   O.n_rest = (int)rest.size();
+  if (rest.empty()) rest.push_back(0);  // (no per-cell launch when n_rest == 0)
+  GLS_TRY(O.rest.upload(rest.data(), rest.size()));
   O.nb = (int)cell0.size();
   O.on = true;
   return GLS_OK;
