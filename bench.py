@@ -300,7 +300,7 @@ def bench_octree(args):
     mg = args.precond == "mg"
     prob = AdaptiveCavityProblem(tree, k=args.k, kp=args.kp, viscosity=args.nu, multigrid=mg,
                                  pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
-                                 coarse_direct=1)
+                                 coarse_direct=1, mixed_precision=int(args.mg_precision == "f32"))
     ctx = prob.ctx
     if not mg:
         ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
@@ -350,8 +350,9 @@ def bench_octree(args):
         "config": {"workload": "cavity on an adapted octree: base %d^3, %d lid/edge refinement levels "
                                "(hanging-node constraints), nu %g, BDF2 dt %g" % (args.n, args.octree_steps, args.nu, args.dt),
                    "n_dofs": N, "n_cells": nc, "cells_per_level": lev,
-                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels), rel %g"
-                                     % (args.restart, args.mg_smooth[0], args.mg_smooth[1], len(prob.levels), args.rel))
+                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing), rel %g"
+                                     % (args.restart, args.mg_smooth[0], args.mg_smooth[1], len(prob.levels),
+                                        "FP32 brick" if args.mg_precision == "f32" else "FP64", args.rel))
                    if mg else "GMRES(%d)+ILU(0) multicolor, rel %g" % (args.restart, args.rel)},
         "mdof_per_s": N * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),

@@ -438,6 +438,7 @@ struct gls_ctx {
     DevBuf<int32_t> cell0, list;  // first cell of each brick; 0..nb-1 (the launch's brick list)
     DevBuf<int32_t> rest;         // the cells outside the bricks (the per-cell kernel's list)
     int n_rest = 0;
+    bool f32_next = false;        // the next J.v: the bricks in FP32 from qdata32 (the V-cycle's smoother)
   } oct;
   // embedding in the global hyper_cube node lattice (gls_set_lattice): box of local nodes
   struct Lattice {
@@ -1121,6 +1122,18 @@ int ensure_element_maps(gls_ctx *c) {
   return c->ev.alloc((size_t)c->n_cells * el);
 }
 
+// adapted forest bricks: the pencil linearization (no output) at the current state
+int oct_lin(gls_ctx *c) {
+  gls::OpParams L = make_params(c, true);
+  L.qd = c->qdata.p;
+  L.subset = c->oct.list.p;
+  L.subset_n = c->oct.nb;
+  L.brick_cell0 = c->oct.cell0.p;
+  HIP_TRY(gls::launch_pencil_ev(gls::MODE_LIN, L, c->tables, c->stream));
+  c->qd_valid = true;
+  c->qd32_valid = false;
+  return GLS_OK;
+}
 int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!c->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
@@ -1170,14 +1183,11 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
       GLS_TRY(c->qdata.alloc(nq));
       c->qd_valid = false;
     }
-    if (mode == gls::MODE_JV && !c->qd_valid) {  // linearization only (no output), at the current state
-      gls::OpParams L = make_params(c, true);
-      L.qd = c->qdata.p;
-      L.subset = c->oct.list.p;
-      L.subset_n = c->oct.nb;
-      L.brick_cell0 = c->oct.cell0.p;
-      HIP_TRY(gls::launch_pencil_ev(gls::MODE_LIN, L, c->tables, c->stream));
-      c->qd_valid = true;
+    if (mode == gls::MODE_JV && !c->qd_valid) GLS_TRY(oct_lin(c));  // linearization only, current state
+    if (mode == gls::MODE_JV && c->oct.f32_next && !c->qd32_valid) {
+      if (c->qdata32.n != c->qdata.n) GLS_TRY(c->qdata32.alloc(c->qdata.n));
+      HIP_TRY(gls::vec_to_f32(c->qdata.p, c->qdata32.p, (int64_t)c->qdata.n, c->stream));
+      c->qd32_valid = true;
     }
     P.cell_list = c->oct.rest.p;  // the per-cell kernel runs the cells outside the bricks only
     P.cell_list_n = c->oct.n_rest;
@@ -1220,8 +1230,13 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
         Q.subset = c->oct.list.p;
         Q.subset_n = c->oct.nb;
         Q.brick_cell0 = c->oct.cell0.p;
-        HIP_TRY(gls::launch_pencil_ev(mode == gls::MODE_JV ? gls::MODE_JVQ : gls::MODE_LIN, Q, c->tables, c->stream));
-        if (mode == gls::MODE_DIAG) c->qd_valid = true;
+        const bool f32 = mode == gls::MODE_JV && c->oct.f32_next;
+        if (f32) Q.qdf = c->qdata32.p;
+        HIP_TRY(gls::launch_pencil_ev(mode == gls::MODE_JV ? gls::MODE_JVQ : gls::MODE_LIN, Q, c->tables, c->stream, f32));
+        if (mode == gls::MODE_DIAG) {
+          c->qd_valid = true;
+          c->qd32_valid = false;
+        }
       }
     }
   }
@@ -1836,7 +1851,10 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
 // y = A v with the level's smoothing operator; rb != nullptr: y = rb - A v
 int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nullptr) {
   if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y, rb);
-  GLS_TRY(gls_jacobian_apply(g, v, y));
+  g->oct.f32_next = g->smooth_f32 && g->oct.on;  // adapted forest: its bricks in FP32, the other cells FP64
+  const int rc = gls_jacobian_apply(g, v, y);
+  g->oct.f32_next = false;
+  GLS_TRY(rc);
   if (rb) HIP_TRY(gls::vec_axpby(y, 1.0, rb, -1.0, g->n_dofs, g->stream));
   return GLS_OK;
 }
@@ -3067,7 +3085,7 @@ int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *c
   GLS_TRY(check_ctx(c));
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
   if (!p_off || !p_col || !p_w || !inject) return set_err(GLS_EINVAL, "mg: transfer arrays missing");
-  if (p->mixed_precision) return set_err(GLS_EINVAL, "mg transfers: FP64 smoothing only (per-cell levels)");
+
   auto &mg = c->mg;
   mg = gls_ctx::MG();
   mg.csr = true;

@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   const int n_bricks = P.n_cells / 8;
   // brick-subset launches (the distributed split: interior / boundary bricks) for the FP64 operator,
   // as the lane-per-point kernel honours them
-  const int32_t *const subset = std::is_same<Real, double>::value ? P.subset : nullptr;
+  const int32_t *const subset = (std::is_same<Real, double>::value || P.brick_cell0) ? P.subset : nullptr;
   const int n_items = subset ? P.subset_n : n_bricks;       // bricks of this launch
   const int n_groups = (n_items + 2) / 3;
   const int g = xcd_swizzle((int)blockIdx.x, n_groups);      // XCD-aware: contiguous Morton triples per XCD
@@ -758,7 +758,7 @@ bool pencil_enabled() {  // read per launch: tests compare both kernels in one p
 template <typename Real, int MODE>
 hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
   const bool gen = P.srf || (MODE != MODE_JVQ && P.force_q);
-  const int n_items = (std::is_same<Real, double>::value && P.subset) ? P.subset_n : P.n_cells / 8;
+  const int n_items = ((std::is_same<Real, double>::value || P.brick_cell0) && P.subset) ? P.subset_n : P.n_cells / 8;
   if (n_items <= 0) return hipSuccess;
   const int n_groups = (n_items + 2) / 3;
   PencilTab<Real> tab;
@@ -795,10 +795,11 @@ hipError_t launch_pencil_reslin(const OpParams &P, const Tables1D &T, hipStream_
 }
 // adapted forests: the listed sibling-group bricks (P.subset over P.brick_cell0), element-vector output
 // (P.ev); mode MODE_JVQ (FP64) or MODE_LIN (linearization rows + the diagonal's element vectors)
-hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipStream_t s) {
+hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipStream_t s, bool f32) {
   if ((!P.ev && mode != MODE_LIN) || P.y || !P.brick_cell0 || !P.subset || P.subset_n <= 0 || !P.qd || P.slab ||
-      P.bricks || P.n_probe > 0 || P.rb || P.jx || P.jx0)
+      P.bricks || P.n_probe > 0 || P.rb || P.jx || P.jx0 || (f32 && (mode != MODE_JVQ || !P.qdf)))
     return hipErrorNotSupported;
+  if (mode == MODE_JVQ && f32) return launch_pencil_t<float, MODE_JVQ>(P, T, s);  // the smoother's operator
   if (mode == MODE_JVQ) return launch_pencil_t<double, MODE_JVQ>(P, T, s);
   if (mode == MODE_LIN) return launch_pencil_t<double, MODE_LIN>(P, T, s);
   return hipErrorNotSupported;

@@ -25,7 +25,7 @@ hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStrea
 hipError_t launch_pencil_lin(const OpParams &P, const Tables1D &T, hipStream_t s);  // MODE_LIN (+ diagonal into P.y)
 // MODE_RESLIN: residual (res_y / res_slab) + linearization (qd, qdf) + diagonal (y / slab) in one pass
 hipError_t launch_pencil_reslin(const OpParams &P, const Tables1D &T, hipStream_t s);
-hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipStream_t s);  // forest sibling-group bricks -> element vectors
+hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipStream_t s, bool f32 = false);  // forest sibling-group bricks -> element vectors
 bool pencil_enabled();
 // persistent wave-per-brick versions (gls_brick_wave.hip), selected by the launchers above
 hipError_t launch_brick_wave(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);

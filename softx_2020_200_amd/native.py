@@ -759,10 +759,12 @@ class GLSContext:
         self._mg_levels = levels
 
     def attach_multigrid_transfers(self, coarse_levels, transfers, pre_smooth=2, post_smooth=2, coarse_sweeps=30,
-                                   omega=0.6, coarse_omega=0.0, coarse_direct=0, level_sweeps=None, smoother="jacobi"):
+                                   omega=0.6, coarse_omega=0.0, coarse_direct=0, level_sweeps=None, smoother="jacobi",
+                                   mixed_precision=0):
         """The V-cycle on a general hierarchy (gls_mg_attach_transfers): levels [self] + coarse_levels
         (hanging lines set on each), transfers[l] = (off, col, w, inject) from level l+1 to level l
-        (octree_mg_transfer). FP64 smoothing: damped Jacobi, or smoother="ilu" (ILU(0) per level)."""
+        (octree_mg_transfer). Smoothing: damped Jacobi, or smoother="ilu" (ILU(0) per level); mixed_precision=1:
+        the levels' forest bricks apply the pencil J.v in FP32 (the other cells stay FP64)."""
         levels = [self] + list(coarse_levels)
         if len(transfers) != len(levels) - 1:
             raise GLSError("attach_multigrid_transfers: one transfer per level pair")
@@ -783,7 +785,7 @@ class GLSContext:
         ws = (PD * len(keep))(*[k[2].ctypes.data_as(PD) for k in keep])
         injs = (P64 * len(keep))(*[k[3].ctypes.data_as(P64) for k in keep])
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct, 0, ls, {"jacobi": 0, "ilu": 1}[smoother])
+                     coarse_omega, coarse_direct, int(mixed_precision), ls, {"jacobi": 0, "ilu": 1}[smoother])
         check(self.L.gls_mg_attach_transfers(self.h, C.byref(p), offs, cols, ws, injs), "gls_mg_attach_transfers")
         self._mg_levels = levels
 

@@ -93,3 +93,26 @@ def test_octree_multigrid_transfers_match_host():
         yc = ctxs[0].mg_transfer(l, 0, cuda(xf), cuda(np.zeros(nc)))
         assert np.abs(yf.cpu().numpy() - P @ xc).max() < 1e-13 * np.abs(P @ xc).max()
         assert np.abs(yc.cpu().numpy() - P.T @ xf).max() < 1e-13 * np.abs(P.T @ xf).max()
+
+
+@pytest.mark.gpu
+def test_octree_multigrid_mixed_precision():
+    """the levels' forest bricks smooth with the FP32 pencil J.v (gls_mg_params.mixed_precision): the outer FP64
+    Newton / GMRES reach the oracle's solution (1e-8), iterations within a few of the FP64 V-cycle's"""
+    tree = adapted_tree(3, 2, 2)
+    trees, probs, xfer = octree_hierarchy(tree, 2, 2, nu=0.1)
+    p = probs[0]
+    x_ref, _, _ = newton_solve(p, tol=1e-10)
+    its = {}
+    for mp in (0, 1):
+        ctxs = [context_for(q) for q in probs]
+        assert ctxs[0].forest_bricks() > 0
+        ctxs[0].attach_multigrid_transfers(ctxs[1:], xfer, coarse_direct=1, mixed_precision=mp)
+        x = cuda(p.apply_nonzero_constraints(np.zeros(p.n_dofs)))
+        st = ctxs[0].newton(x, tolerance=1e-10, max_iterations=10, lin_max_iterations=5000, restart=200,
+                            relative_residual=1e-10, minimum_residual=1e-13)
+        assert st["final_residual"] < 1e-10, (mp, st)
+        assert np.abs(x.cpu().numpy()[:3 * p.n_vnodes] - x_ref[:3 * p.n_vnodes]).max() < 1e-8, mp
+        its[mp] = st["linear_iterations"]
+    print("octree GMG FP64 / mixed: %d / %d GMRES its" % (its[0], its[1]))
+    assert its[1] <= its[0] + 10
