@@ -92,7 +92,7 @@ struct PencilTab {
 
 // GEN: the forcing term and the SRF source are compiled in (an instantiation without them is the hot
 // path: their per-point loads and terms cost the residual ~50 VGPRs of spills)
-template <typename Real, int MODE, bool GEN>
+template <typename Real, int MODE, bool GEN, bool FOREST = false>  // FOREST: an FP32 launch on forest bricks (subset list)
 __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
     gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
   using C = PencilCfg<Real, MODE == MODE_JVQ>;
@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   const int n_bricks = P.n_cells / 8;
   // brick-subset launches (the distributed split: interior / boundary bricks) for the FP64 operator,
   // as the lane-per-point kernel honours them
-  const int32_t *const subset = (std::is_same<Real, double>::value || P.brick_cell0) ? P.subset : nullptr;
+  const int32_t *const subset = (std::is_same<Real, double>::value || FOREST) ? P.subset : nullptr;
   const int n_items = subset ? P.subset_n : n_bricks;       // bricks of this launch
   const int n_groups = (n_items + 2) / 3;
   const int g = xcd_swizzle((int)blockIdx.x, n_groups);      // XCD-aware: contiguous Morton triples per XCD
@@ -755,7 +755,7 @@ bool pencil_enabled() {  // read per launch: tests compare both kernels in one p
   return !(e && std::atoi(e) == 0);
 }
 
-template <typename Real, int MODE>
+template <typename Real, int MODE, bool FB = false>
 hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
   const bool gen = P.srf || (MODE != MODE_JVQ && P.force_q);
   const int n_items = ((std::is_same<Real, double>::value || P.brick_cell0) && P.subset) ? P.subset_n : P.n_cells / 8;
@@ -772,10 +772,10 @@ hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) 
     tab.xi[q] = (Real)T.xi[q];
   }
   if (gen)
-    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, true>), dim3((unsigned)n_groups), dim3(256),
+    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, true, FB>), dim3((unsigned)n_groups), dim3(256),
                        pencil_lds_bytes<Real>(MODE), s, P, tab);
   else
-    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, false>), dim3((unsigned)n_groups), dim3(256),
+    hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, false, FB>), dim3((unsigned)n_groups), dim3(256),
                        pencil_lds_bytes<Real>(MODE), s, P, tab);
   return hipGetLastError();
 }
@@ -799,7 +799,7 @@ hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipS
   if ((!P.ev && mode != MODE_LIN) || P.y || !P.brick_cell0 || !P.subset || P.subset_n <= 0 || !P.qd || P.slab ||
       P.bricks || P.n_probe > 0 || P.rb || P.jx || P.jx0 || (f32 && (mode != MODE_JVQ || !P.qdf)))
     return hipErrorNotSupported;
-  if (mode == MODE_JVQ && f32) return launch_pencil_t<float, MODE_JVQ>(P, T, s);  // the smoother's operator
+  if (mode == MODE_JVQ && f32) return launch_pencil_t<float, MODE_JVQ, true>(P, T, s);  // the smoother's operator
   if (mode == MODE_JVQ) return launch_pencil_t<double, MODE_JVQ>(P, T, s);
   if (mode == MODE_LIN) return launch_pencil_t<double, MODE_LIN>(P, T, s);
   return hipErrorNotSupported;
