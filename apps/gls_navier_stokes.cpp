@@ -1416,8 +1416,9 @@ struct Solver {
 
   // an adapted hyper_cube (gls_octree_mesh, hanging nodes; rmesh already set): mesh, Dirichlet
   // constraints (hanging nodes excluded), hanging constraint lines on the context. Per-cell kernels;
-  // one rank, non-periodic: the multigrid V-cycle on the forest's refinement hierarchy (attach_forest_mg;
-  // damped-Jacobi smoothing for equal order, ILU(0) smoothing for Q2-Q1), else ILU / Jacobi.
+  // one rank, non-periodic, method = amg or --precond hmg: the multigrid V-cycle on the forest's refinement
+  // hierarchy (attach_forest_mg; damped-Jacobi smoothing for equal order, ILU(0) smoothing for Q2-Q1), else
+  // ILU / Jacobi.
   void setup_refined(gls_refined_mesh *R_new) {
     SectionTimer::Scope ts(timer, "setup_dofs");
     release();
@@ -1431,7 +1432,10 @@ struct Solver {
                        m.hang_master.data(), m.hang_w.data()),
        "gls_set_hanging");
     alloc_vectors();
-    if (use_mg && forest_mode != 1 && world == 1 && m.pmask == 0 && tree) attach_forest_mg();
+    // as on general meshes: method = amg (ML's hierarchy -> the forest's) or --precond hmg; gmres / bicgstab
+    // keep the reference's ILU (setup_ILU, gls_navier_stokes.cc:1161-1176)
+    if (use_mg && world == 1 && m.pmask == 0 && tree && ((P.lin_method == 2 && forest_mode != 1) || forest_mode == 2))
+      attach_forest_mg();
     print_setup(std::pow(P.hi - P.lo, P.dim));
     std::printf("   Hanging node DoFs:            %lld\n", (long long)m.hang_dofs.size());
   }

@@ -13,12 +13,18 @@ right-hand side), relative residual 1e-4, max `--lin-max` iterations; alpha line
 residual re-assembly. Every step restarts from the same synthetic state so the work per step is
 fixed; linear iterations and residual evaluations are reported.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under torch.distributed.run.
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under torch.distributed.run
+(WORLD_SIZE must equal --gpus, else exit 1) or directly: without WORLD_SIZE the process starts N fresh
+rank processes itself (before anything touches the GPU; RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+127.0.0.1), waits for them, exits non-zero if one fails and re-prints rank 0's JSON line.
 Multi-GPU (N>1): the 128^3 mesh is partitioned into contiguous Morton brick ranges (one per GPU,
 p4est-like); ghost import / export-add and the GMRES dot products go over the library's own RCCL
 communicator (gls_dist_attach_rccl; the ghost import of the J.v overlaps the interior bricks on a
-second stream; --dist-impl torch: torch.distributed callbacks instead). Fixed total problem ->
-"scaling": "strong"; value = nonlinear iterations/s of the whole job.
+second stream; --dist-impl torch: torch.distributed callbacks instead). Before the warm-up a pre-flight
+checks the N-rank residual and J.v of a 16^3 cavity (same transport) against a single-rank context on
+rank 0 (abort above 1e-12; `preflight_relerr`). Fixed total problem -> "scaling": "strong"; value =
+nonlinear iterations/s of the whole job; `rccl_ranks` = the in-library communicator's size as RCCL
+reports it, `devices` = distinct GPUs behind the ranks.
 """
 from __future__ import annotations
 
@@ -366,6 +372,117 @@ def bench_octree(args):
     print(json.dumps(out))
 
 
+def spawn_ranks(n):
+    """Launcher-less N-rank run: start N fresh processes of this script with the torch.distributed.run
+    environment (this parent never imports torch or touches the GPU), forward their output, and return
+    the exit status: the first failing rank's code (the others are then terminated), else 0 after
+    re-printing rank 0's JSON line as the only line on stdout."""
+    import socket
+    import subprocess
+    import threading
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs, lines = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLS_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE, text=True))
+
+    def pump(r, f):  # keep rank 0's JSON line; everything else goes on to stderr
+        for line in f:
+            if r == 0 and line.lstrip().startswith("{"):
+                lines.append(line)
+            else:
+                sys.stderr.write(line)
+    ths = [threading.Thread(target=pump, args=(r, p.stdout), daemon=True) for r, p in enumerate(procs)]
+    for th in ths:
+        th.start()
+    rc = 0
+    while True:
+        st = [p.poll() for p in procs]  # every rank polled (not short-circuited), so failures are seen
+        if all(x is not None for x in st):
+            break
+        bad = [x for x in st if x not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        time.sleep(0.2)
+    if rc:
+        sys.stderr.write("bench.py: a rank exited with status %d; terminating the others\n" % rc)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    for th in ths:
+        th.join(timeout=10)
+    rc = rc or next((p.returncode for p in procs if p.returncode), 0)
+    if rc:
+        return rc if rc > 0 else 1
+    if not lines:
+        sys.stderr.write("bench.py: rank 0 printed no result line\n")
+        return 1
+    sys.stdout.write(lines[-1])
+    sys.stdout.flush()
+    return 0
+
+
+def preflight(args, rank, world, dev, dist):
+    """N-rank residual and J.v of a 16^3 cavity (the bench's boundary data, state and scheme; the same
+    transport as the timed run) against a single-rank context of the whole mesh on rank 0. Returns the
+    max relative difference (every rank gets rank 0's number)."""
+    import torch
+
+    import softx_2020_200_amd as sx
+    from softx_2020_200_amd.dist import DistributedProblem, local_vector, owned_global_dofs
+    from softx_2020_200_amd.problem import build_context, dirichlet_from_bcs
+    n = 16
+    mesh = sx.hyper_cube(3, n, args.k, args.kp, -1.0, 1.0)
+    bcs = [("noslip", b, None) for b in (0, 1, 2, 4, 5)] + [("function", 3, (1.0, 0.0, 0.0))]
+    mask, dd, dv = dirichlet_from_bcs(mesh, n, -1.0, 1.0, True, bcs)
+    nv = mesh["n_vnodes"]
+    u = smooth_state(mesh, n, 3, dd, dv, 0.0)
+    u2 = smooth_state(mesh, n, 3, dd, dv, 0.3)
+    v = np.random.default_rng(20200200).uniform(-1.0, 1.0, len(u))
+    dp = DistributedProblem(mesh, rank, world, dev, viscosity=args.nu, vnode_mask=mask, dirichlet=(dd, dv),
+                            backend=args.dist_backend, impl=args.dist_impl)
+    dist.barrier()  # first collective before any batched P2P (NCCL requirement)
+    loc = lambda g: torch.from_numpy(local_vector(dp.plan, g, nv)).to(dev)  # noqa: E731
+    dp.ctx.set_time(args.scheme, (args.dt,) * 4)
+    dp.ctx.set_state(loc(u), loc(u), loc(u2))
+    r = dp.ctx.residual().cpu().numpy()
+    jv = dp.ctx.jacobian_apply(loc(v)).cpu().numpy()
+    li, gi = owned_global_dofs(dp.plan, nv)
+    parts = [None] * world
+    dist.all_gather_object(parts, (gi, r[li], jv[li]))
+    err = torch.zeros(1, dtype=torch.float64)
+    if rank == 0:
+        R, J = np.full(len(u), np.nan), np.full(len(u), np.nan)
+        for g_, r_, j_ in parts:
+            R[g_], J[g_] = r_, j_
+        one = build_context(mesh, viscosity=args.nu, vnode_mask=mask)
+        one.set_dirichlet(dd, dv)
+        one.set_time(args.scheme, (args.dt,) * 4)
+        t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+        one.set_state(t(u), t(u), t(u2))
+        r1 = one.residual().cpu().numpy()
+        j1 = one.jacobian_apply(t(v)).cpu().numpy()
+        one.close()
+        e = max(np.abs(R - r1).max() / np.abs(r1).max(), np.abs(J - j1).max() / np.abs(j1).max())
+        err[0] = e if np.isfinite(e) else np.inf  # a DoF no rank owns leaves a NaN
+    if args.dist_backend == "nccl":
+        err = err.to(dev)
+    dist.broadcast(err, 0)
+    dp.ctx.close()
+    return float(err.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -421,6 +538,18 @@ def main():
     args = ap.parse_args()
     if args.dist_backend == "gloo":  # host-staged testing transport: no RCCL communicator
         args.dist_impl = "torch"
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.stderr.write("bench.py: WORLD_SIZE=%s but --gpus %d: launch one rank per GPU (torch.distributed.run "
+                         "--nproc-per-node %d ... --gpus %d) or run without a launcher\n"
+                         % (env_world, args.gpus, args.gpus, args.gpus))
+        sys.exit(1)
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.workload in ("cylinder3d", "octree") and args.gpus > 1:
+        sys.exit("bench.py: --workload %s runs on one GPU" % args.workload)
     if args.workload in ("cylinder3d", "octree"):
         import torch
         torch.cuda.set_device(0)
@@ -443,6 +572,23 @@ def main():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
+
+    devices, rccl_ranks, pre_err = 1, None, None
+    if dist is not None:
+        props = torch.cuda.get_device_properties(local)
+        ids = [None] * world
+        dist.all_gather_object(ids, str(getattr(props, "uuid", None) or "%s:%d" % (os.uname().nodename, local)))
+        devices = len(set(ids))
+        pre_err = preflight(args, rank, world, torch.device("cuda", local), dist)
+        if not pre_err <= 1e-12:
+            if rank == 0:
+                sys.stderr.write("bench.py: pre-flight FAILED: %d-rank residual / J.v differ from one rank by %.3e "
+                                 "(16^3 cavity, %s transport)\n" % (world, pre_err, args.dist_impl))
+            dist.destroy_process_group()
+            sys.exit(3)
+        if args.dist_impl == "native":
+            from softx_2020_200_amd.dist import rccl_comm, rccl_info
+            rccl_ranks = rccl_info(rccl_comm(rank, world))[1]
 
     from softx_2020_200_amd.problem import CavityProblem
     if args.mg_coarsest == 0:
@@ -609,6 +755,7 @@ def main():
                                                                      else "torch.distributed %s ghosts" % args.dist_backend))
                    if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,
+        "devices": devices, "rccl_ranks": rccl_ranks, "preflight_relerr": pre_err,
         "linear_iterations_per_step": float(np.mean(lin_its)),
         "residual_evaluations_per_step": float(np.mean(nres)),
         "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),

@@ -206,9 +206,12 @@ typedef struct {
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
                                                  with <= 2048 DoFs), 1 exact solve (<= 8192 DoFs), -1
                                                  Jacobi sweeps. The exact solve probes the coarsest
-                                                 Jacobian and inverts it by rocSOLVER LU (partial
-                                                 pivoting) with the first pressure DoF pinned (the
-                                                 enclosed-flow gauge) */
+                                                 Jacobian and inverts it by rocSOLVER LU with the
+                                                 first pressure DoF pinned (the enclosed-flow gauge):
+                                                 unpivoted by default, the inverse checked by
+                                                 max|A (A^-1 e) - e| and finiteness; a zero pivot or a
+                                                 failed check refactors with partial pivoting
+                                                 (GLS_MG_COARSE_SOLVER=lu: always pivoted) */
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
                                                  arithmetic from an FP32 copy of the linearization
                                                  (brick path; vectors, transfers and the outer GMRES
@@ -372,6 +375,10 @@ int gls_part_destroy(gls_part *p);
 
 typedef int (*gls_exchange_fn)(void *user, int phase);
 typedef int (*gls_allreduce_fn)(void *user, double *dev_buf, int n);
+/* red_buf: a DEVICE buffer of at least GLS_RED_BUF_MIN doubles. Every reduction the library makes
+ * through the callback goes through it in pieces of at most that many values (GMRES dots: restart+1
+ * <= 256, the multigrid replica's right-hand side in chunks of 256). */
+#define GLS_RED_BUF_MIN 256
 int gls_dist_attach(gls_ctx *ctx, int64_t n_owned_nodes, int n_nbrs, const int64_t *send_offsets,
                     const int32_t *send_nodes, const int64_t *recv_offsets, const int32_t *recv_nodes, double *send_buf,
                     double *recv_buf, double *red_buf, gls_exchange_fn xchg, gls_allreduce_fn allreduce, void *user);
@@ -388,6 +395,8 @@ typedef struct gls_rccl gls_rccl;
 int gls_rccl_unique_id(unsigned char *id_out);
 int gls_rccl_create(const unsigned char *id, int rank, int world, gls_rccl **out);
 int gls_rccl_destroy(gls_rccl *comm);
+/* the communicator's rank and size as RCCL reports them (ncclCommUserRank / ncclCommCount) */
+int gls_rccl_info(const gls_rccl *comm, int *rank, int *world);
 int gls_dist_attach_rccl(gls_ctx *ctx, gls_rccl *comm, int64_t n_owned_nodes, int n_nbrs, const int *nbr_ranks,
                          const int64_t *send_offsets, const int32_t *send_nodes, const int64_t *recv_offsets,
                          const int32_t *recv_nodes);

@@ -475,6 +475,7 @@ struct gls_ctx {
       int plane = 1, rlane = 1;  // SpMV lanes per row (from the mean row length)
     };
     std::vector<std::unique_ptr<Csr>> xfer;
+    std::vector<gls_ctx *> ilu_levels;  // levels whose ILU(0) smoother this attach created (smoother = 1)
     DevBuf<double> xwork;  // two-pass transfer intermediate (coarse xy x fine z, 4 fields)
     // coarsest level: direct solve with the probed, regularised, inverted Jacobian
     bool direct = false, direct_ok = false;
@@ -505,6 +506,7 @@ struct gls_ctx {
     DevBuf<int> ipiv, info;
     DevBuf<double> probe, aug, unit;
     DevBuf<double> probe_bak;  // the probed coarse matrix kept for the pivoted retry of an unpivoted LU
+    DevBuf<double> chk;        // coarse_inverse_check's y = A^-1 e and z = A y
     DevBuf<int> status;
     // coarsest-level Jacobi sweeps (single rank, fused brick path) replayed as one HIP graph: the
     // ~2×csweeps tiny launches per V-cycle are captured once per state (mg_prepare) and launched
@@ -1446,8 +1448,11 @@ int gls_set_stream(gls_ctx *c, void *s) {
   c->own_stream = false;
   c->stream = (hipStream_t)s;
   // multigrid levels run on the fine level's stream (the V-cycle interleaves their kernels)
-  if (c->mg.on)
+  if (c->mg.on) {
     for (size_t l = 1; l < c->mg.lev.size(); ++l) GLS_TRY(gls_set_stream(c->mg.lev[l], s));
+    // the replica's V-cycle is ordered with replica_gather / vec_pack_dofs on this stream
+    if (c->mg.replica) GLS_TRY(gls_set_stream(c->mg.replica, s));
+  }
   return GLS_OK;
 }
 
@@ -2156,6 +2161,43 @@ int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
 }
 
 int replica_gather(gls_ctx *c, const double *loc, double *glob);
+// The explicit coarse inverse (mg.probe) against the pinned matrix it came from (mg.probe_bak): y = A^-1 e,
+// z = A y for e = (1, ..., 1); good = y finite and max|z - e| <= 1e-8 max(1, max|A| max|y|) (a backward-stable
+// factorization leaves ~n eps there; an unpivoted LU through a tiny pivot leaves O(1) or non-finite values)
+static int coarse_inverse_check(gls_ctx *c, int64_t n, bool *good) {
+  auto &mg = c->mg;
+  *good = false;
+  if (mg.chk.n < (size_t)(2 * n)) GLS_TRY(mg.chk.alloc((size_t)(2 * n)));
+  double *y = mg.chk.p, *z = mg.chk.p + n;
+  HIP_TRY(gls::vec_fill(mg.unit.p, n, 1.0, c->stream));
+  const double one = 1.0, zero = 0.0;
+  rocblas_int imax = 0;
+  if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+      rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe.p, (rocblas_int)n,
+                    mg.unit.p, 1, &zero, y, 1) != rocblas_status_success ||
+      rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe_bak.p,
+                    (rocblas_int)n, y, 1, &zero, z, 1) != rocblas_status_success ||
+      rocblas_idamax(mg.blas, (rocblas_int)(n * n), mg.probe_bak.p, 1, &imax) != rocblas_status_success)
+    return set_err(GLS_EHIP, "coarse inverse check: rocBLAS failed");
+  std::vector<double> h((size_t)(2 * n));
+  double amax = 0.0;
+  HIP_TRY(hipMemcpyAsync(h.data(), mg.chk.p, sizeof(double) * (size_t)(2 * n), hipMemcpyDeviceToHost, c->stream));
+  if (imax > 0)
+    HIP_TRY(hipMemcpyAsync(&amax, mg.probe_bak.p + (imax - 1), sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  double ymax = 0.0, err = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (!std::isfinite(h[(size_t)i]) || !std::isfinite(h[(size_t)(n + i)])) return GLS_OK;
+    ymax = std::max(ymax, std::fabs(h[(size_t)i]));
+    err = std::max(err, std::fabs(h[(size_t)(n + i)] - 1.0));
+  }
+  *good = err <= 1e-8 * std::max(1.0, std::fabs(amax) * ymax);
+  if (std::getenv("GLS_MG_VERBOSE"))
+    std::printf("mg: coarse inverse check n=%lld max|Ay-e| %.3e max|A| %.3e max|y| %.3e -> %s\n", (long long)n, err,
+                std::fabs(amax), ymax, *good ? "ok" : "FAILED");
+  return GLS_OK;
+}
+
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
@@ -2277,9 +2319,34 @@ int mg_prepare(gls_ctx *c) {
         if (rocsolver_dgetri(mg.blas, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
             rocblas_status_success)
           return set_err(GLS_EHIP, "rocsolver_dgetri failed");
-        HIP_TRY(gls::mg_zero_row(mg.probe.p, n, pin, c->stream));  // pinned unknown: zero correction
         HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        // an unpivoted LU of the indefinite velocity-pressure Jacobian passes getrf with a tiny nonzero
+        // pivot and can return a wildly wrong (or non-finite) inverse: check A (A^-1 e) = e and redo the
+        // factorization with partial pivoting when it fails
+        if (inf == 0 && npvt && !cs) {
+          bool good = false;
+          GLS_TRY(coarse_inverse_check(c, n, &good));
+          if (!good) {
+            if (verbose) std::printf("mg: unpivoted coarse inverse failed its check, refactoring with pivoting\n");
+            HIP_TRY(gls::vec_copy(mg.probe.p, mg.probe_bak.p, n * n, c->stream));
+            mg.npvt_ipiv_n = -1;
+            npvt = false;
+            if (rocsolver_dgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p,
+                                 mg.info.p) != rocblas_status_success)
+              return set_err(GLS_EHIP, "rocsolver_dgetrf failed");
+            HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (inf == 0) {
+              if (rocsolver_dgetri(mg.blas, (rocblas_int)n, mg.probe.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+                  rocblas_status_success)
+                return set_err(GLS_EHIP, "rocsolver_dgetri failed");
+              HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+              HIP_TRY(hipStreamSynchronize(c->stream));
+            }
+          }
+        }
+        if (inf == 0) HIP_TRY(gls::mg_zero_row(mg.probe.p, n, pin, c->stream));  // pinned unknown: zero correction
       }
       mg.lu = mg.direct_ok = inf == 0;
       if (verbose) std::printf("mg: coarse LU n=%lld info=%d, getri done at %.2f ms\n", (long long)n, inf, ms(t0, tick()));
@@ -2969,6 +3036,7 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       gls_ctx *g = mg.lev[(size_t)l];
       GLS_TRY(gls_ilu_set_options(g, g->n_dofs > 100000 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM, 0));
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
+      mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
   // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
   {
@@ -3002,8 +3070,8 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   if (c->dim != 3 || c->k > 2 || c->k != c->kp) return set_err(GLS_EINVAL, "mg: 3D Q1-Q1 / Q2-Q2 only");
   if (c->hang.on) return set_err(GLS_EINVAL, "mg: not with hanging-node constraints");
   if (c->map_degree > 0) return set_err(GLS_EINVAL, "mg: nested hyper_cube levels only (not mapped cells)");
+  GLS_TRY(gls_mg_detach(c));  // a previous attach's levels / smoother ILUs
   auto &mg = c->mg;
-  mg = gls_ctx::MG();
   mg.boxed = c->dist.on;
   for (int l = 0; l < p->n_levels; ++l) {
     gls_ctx *g = p->levels[l];
@@ -3086,8 +3154,8 @@ int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *c
   if (!p || p->n_levels < 2 || !p->levels || p->levels[0] != c) return set_err(GLS_EINVAL, "mg: levels[0] must be ctx");
   if (!p_off || !p_col || !p_w || !inject) return set_err(GLS_EINVAL, "mg: transfer arrays missing");
 
+  GLS_TRY(gls_mg_detach(c));  // a previous attach's levels / smoother ILUs
   auto &mg = c->mg;
-  mg = gls_ctx::MG();
   mg.csr = true;
   for (int l = 0; l < p->n_levels; ++l) {
     gls_ctx *g = p->levels[l];
@@ -3186,6 +3254,9 @@ int gls_mg_set_coarse_replica(gls_ctx *c, gls_ctx *replica, int64_t n_local, con
 int gls_mg_detach(gls_ctx *c) {
   GLS_TRY(check_ctx(c));
   for (auto *g : c->mg.lev) g->smooth_f32 = false;
+  // the ILU(0) smoothers the attach put on the levels (level 0 is this context) go with the multigrid, so
+  // the preconditioner falls back to Jacobi (gls_native.h) and not to a leftover smoother ILU
+  for (auto *g : c->mg.ilu_levels) GLS_TRY(gls_ilu_detach(g));
   c->mg = gls_ctx::MG();
   return GLS_OK;
 }
@@ -4888,6 +4959,16 @@ extern "C" int gls_rccl_create(const unsigned char *id_in, int rank, int world, 
   r->rank = rank;
   r->world = world;
   *out = r.release();
+  return GLS_OK;
+}
+// the communicator's own view (ncclCommUserRank / ncclCommCount): what bench.py reports as rccl_ranks
+extern "C" int gls_rccl_info(const gls_rccl *r, int *rank, int *world) {
+  if (!r || !r->comm) return set_err(GLS_EINVAL, "gls_rccl_info: no communicator");
+  int rk = -1, n = 0;
+  if (ncclCommUserRank(r->comm, &rk) != ncclSuccess || ncclCommCount(r->comm, &n) != ncclSuccess)
+    return set_err(GLS_ECOMM, "gls_rccl_info: ncclCommUserRank / ncclCommCount failed");
+  if (rank) *rank = rk;
+  if (world) *world = n;
   return GLS_OK;
 }
 extern "C" int gls_rccl_destroy(gls_rccl *r) {

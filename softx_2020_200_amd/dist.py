@@ -37,6 +37,7 @@ def _bind(L):
     L.gls_rccl_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
     L.gls_rccl_create.argtypes = [C.POINTER(C.c_ubyte), C.c_int, C.c_int, C.POINTER(vp)]
     L.gls_rccl_destroy.argtypes = [vp]
+    L.gls_rccl_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.gls_dist_attach_rccl.argtypes = [vp, vp, i64, C.c_int, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(C.c_int32),
                                        C.POINTER(i64), C.POINTER(C.c_int32)]
     i32p, i64p = C.POINTER(C.c_int32), C.POINTER(i64)
@@ -198,6 +199,14 @@ def rccl_comm(rank, world, group=None):
         check(L.gls_rccl_create(idb, rank, world, C.byref(h)), "gls_rccl_create")
         _RCCL[key] = h
     return _RCCL[key]
+
+
+def rccl_info(comm):
+    """(rank, size) of an in-library RCCL communicator as RCCL itself reports them."""
+    L = _bind(load())
+    r, w = C.c_int(), C.c_int()
+    check(L.gls_rccl_info(comm, C.byref(r), C.byref(w)), "gls_rccl_info")
+    return r.value, w.value
 
 
 def attach_rccl(ctx: GLSContext, plan, comm):

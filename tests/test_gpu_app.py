@@ -522,10 +522,11 @@ def test_app_transient_kelly_periodic_tgv(tmp_path):
 
 @pytest.mark.gpu
 def test_app_kelly_forest_multigrid(tmp_path):
-    """3D Kelly adaptation of mms3d (Q1-Q1, two cycles with coarsening) with the app's default preconditioner on
-    the adapted hyper_cubes: the V-cycle on the forest's refinement hierarchy (gls_mg_attach_transfers,
-    announced on stderr) gives the error table of the ILU-preconditioned run (--precond ilu, the reference's
-    setup_ILU, gls_navier_stokes.cc:1161-1176): same cell counts, errors at 1e-6 (converged solves)."""
+    """3D Kelly adaptation of mms3d (Q1-Q1, two cycles with coarsening) with the hierarchy multigrid on the
+    adapted hyper_cubes (--precond hmg; method = amg picks it too): the V-cycle on the forest's refinement
+    hierarchy (gls_mg_attach_transfers, announced on stderr) gives the error table of the ILU-preconditioned run
+    (method = gmres, the app's default there as the reference's setup_ILU, gls_navier_stokes.cc:1161-1176):
+    same cell counts, errors at 1e-6 (converged solves)."""
     import subprocess
     g = G["mms3d_gls"]
     prm = mms_prm(g, 3, 3, 2).replace("  set type = uniform\n", """  set type = kelly
@@ -535,7 +536,7 @@ def test_app_kelly_forest_multigrid(tmp_path):
   set fraction coarsening = 0.1
 """)
     res = {}
-    for pc in ("mg", "ilu"):
+    for pc in ("hmg", "mg"):
         f = tmp_path / ("%s.prm" % pc)
         f.write_text(prm)
         out = subprocess.run([APP, "--dim", "3", "--precision", "9", "--stats", "--precond", pc, str(f)],
@@ -543,10 +544,10 @@ def test_app_kelly_forest_multigrid(tmp_path):
         assert out.returncode == 0, out.stderr[-2000:]
         its = [int(l.split("linear_iterations =")[1]) for l in out.stdout.splitlines() if "linear_iterations =" in l]
         res[pc] = (table(out.stdout), out.stderr, its)
-    assert "refinement hierarchy" in res["mg"][1], res["mg"][1][-800:]
-    assert "refinement hierarchy" not in res["ilu"][1]
-    rm, ri = res["mg"][0], res["ilu"][0]
+    assert "refinement hierarchy" in res["hmg"][1], res["hmg"][1][-800:]
+    assert "refinement hierarchy" not in res["mg"][1] and "ILU(" in res["mg"][1], res["mg"][1][-800:]
+    rm, ri = res["hmg"][0], res["mg"][0]
     assert len(rm) == len(ri) == 3 and [r[0] for r in rm] == [r[0] for r in ri], (rm, ri)
     for a, b in zip(rm, ri):
         assert abs(a[1] - b[1]) <= 1e-6 * b[1] and abs(a[3] - b[3]) <= 1e-6 * b[3], (a, b)
-    print("forest GMG linear iterations %s, ILU %s" % (res["mg"][2], res["ilu"][2]))
+    print("forest GMG linear iterations %s, ILU %s" % (res["hmg"][2], res["mg"][2]))
