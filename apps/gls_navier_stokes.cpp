@@ -430,6 +430,9 @@ struct Mesh {
   std::vector<double> support, measure;
   std::vector<uint32_t> vbid;
   int64_t n_dofs() const { return (int64_t)dim * nv + np; }
+  // the DoFHandler's count deal.II prints on periodic meshes: periodicity is a constraint there, so the
+  // nodes this build identifies are counted on both faces (-1: not periodic, n_dofs())
+  int64_t n_dofs_dealii = -1;
   void coord(int64_t node, bool vel, double *x, int *idx) const {
     if (!vx.empty()) {  // refined mesh: no lattice index
       const double *src = &(vel ? vx : px)[(size_t)(node * dim)];
@@ -476,6 +479,14 @@ Mesh build_mesh(const Params &P, int n, int pmask) {
   m.h.resize((size_t)(m.nc * P.dim));
   ck(gls_mesh_hyper_cube(P.dim, n, P.k, P.kp, P.lo, P.hi, pmask, m.cv.data(), m.cp.data(), m.x0.data(), m.h.data()),
      "gls_mesh_hyper_cube");
+  if (pmask) {  // deal.II's count: the unwrapped lattices
+    int64_t nvf = 1, npf = 1;
+    for (int d = 0; d < P.dim; ++d) {
+      nvf *= (int64_t)P.k * n + 1;
+      npf *= (int64_t)P.kp * n + 1;
+    }
+    m.n_dofs_dealii = (int64_t)P.dim * nvf + npf;
+  }
   return m;
 }
 
@@ -1550,6 +1561,16 @@ struct Solver {
       ck(gls_umesh_set_manifold(um, mp.id, 1, mp.arg, nullptr), "gls_umesh_set_manifold");
       ck(gls_umesh_boundary_manifold(um, mp.id, mp.id), "gls_umesh_boundary_manifold");
     }
+    // periodic pairs of the triangulation (attach_grid_to_triangulation's add_periodicity, grids.cc:41-58):
+    // the Kelly adaptation keeps the levels across them within one of each other
+    std::vector<int32_t> per;
+    for (const BC &b : P.bcs)
+      if (b.type == "periodic") {
+        per.push_back(b.id);
+        per.push_back(b.periodic_id);
+        per.push_back(b.periodic_direction);
+      }
+    if (!per.empty()) ck(gls_umesh_set_periodic(um, (int)per.size() / 3, per.data()), "gls_umesh_set_periodic");
     ck(gls_umesh_refine_global(um, P.refinement), "refine_global");
   }
   // the app's Mesh of an FE space of the triangulation (cells, nodes, MappingQ support points, hanging
@@ -1691,6 +1712,12 @@ struct Solver {
     ck(gls_umesh_fe_space(um, P.k, P.kp, P.qmapping_all ? 1 : 0, (int)per.size() / 3, per.data(), &space), "gls_umesh_fe_space");
     const gls_fe_space &F = *space;
     m = mesh_of_space(F);
+    if (!per.empty()) {  // deal.II's DoF count: the same space without the periodic identification
+      gls_fe_space *raw = nullptr;
+      ck(gls_umesh_fe_space(um, P.k, P.kp, P.qmapping_all ? 1 : 0, 0, nullptr, &raw), "gls_umesh_fe_space");
+      m.n_dofs_dealii = (int64_t)P.dim * raw->n_vnodes + raw->n_pnodes;
+      gls_fe_space_destroy(raw);
+    }
     C = make_constraints(P, m, time);
     // hanging lines + slip lines of curved walls (homogeneous constraint lines on velocity DoFs)
     std::vector<int64_t> ld, lo, lm;
@@ -1731,7 +1758,7 @@ struct Solver {
   // setup_dofs' summary lines (gls_navier_stokes.cc:220-227)
   void print_setup(double volume) {
     std::printf("   Number of active cells:       %lld\n   Number of degrees of freedom: %lld\n", (long long)m.nc,
-                (long long)m.n_dofs());
+                (long long)(m.n_dofs_dealii >= 0 ? m.n_dofs_dealii : m.n_dofs()));
     std::printf("   Volume of triangulation:      %g\n", volume);
   }
 

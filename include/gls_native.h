@@ -656,6 +656,15 @@ int gls_fe_space_boundary_normals(const gls_fe_space *space, int boundary_id, do
  * normals: [n_vnodes][3][dim], row i = unit mean of group i (row 0 = the node normal when count = 1). */
 int gls_fe_space_boundary_normal_sets(const gls_fe_space *space, int boundary_id, int32_t *count, double *normals);
 int gls_umesh_adapt(gls_umesh *mesh, const int32_t *refine, const int32_t *coarsen);
+/* Periodic boundary pairs of the triangulation (the reference's add_periodicity after
+ * collect_periodic_faces, grids.cc:41-58): n_periodic triples (id a, id b, direction). gls_umesh_prepare
+ * then treats the faces across them as neighbours (mesh smoothing) and gls_umesh_adapt / the vertex 2:1
+ * balance identify the translated vertices, so refinement levels differ by at most one across a periodic
+ * boundary. A space built with the same pairs (gls_umesh_fe_space) identifies the partnered nodes and
+ * constrains the nodes of a finer face to the coarser face across the boundary
+ * (make_periodicity_constraints, gls_navier_stokes.cc:128-134, 162-168), and its Kelly faces
+ * (gls_fe_space_kelly_faces) include the periodic face pieces. */
+int gls_umesh_set_periodic(gls_umesh *mesh, int n_periodic, const int32_t *periodic);
 /* Level meshes of a geometric multigrid on the triangulation's refinement hierarchy (global coarsening):
  * a copy whose active cells are the current ones with every cell finer than `level` replaced by its
  * ancestor on `level` (free with gls_umesh_destroy). gls_fe_space_mg_transfer: the prolongation between

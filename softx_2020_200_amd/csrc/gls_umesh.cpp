@@ -26,7 +26,9 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
+#include <set>
 #include <sstream>
 #include <string>
 #include <unordered_map>
@@ -95,6 +97,9 @@ struct UMesh {
   std::vector<HCell> tree;
   std::vector<int64_t> roots, active;
   std::map<EKey, int64_t> line_mid, face_mid;  // refined lines / quads -> their midpoint vertex
+  // periodic boundary pairs (id a, id b, direction) of the triangulation (add_periodicity, grids.cc:41-58):
+  // the mesh smoothing and the vertex 2:1 balance see across them
+  std::vector<std::array<int, 3>> periodic;
 
   int nvc() const { return dim == 2 ? 4 : 8; }
   int mf_of(const std::map<EKey, int> &m, const EKey &k) const {
@@ -427,12 +432,112 @@ int refine_once(UMesh &m) {
 // ---- local adaptation of the hierarchy (the reference's p::d::Triangulation with
 // smoothing_on_refinement | smoothing_on_coarsening, navier_stokes_base.cc:55-60, 592-780)
 
-// highest active level at every vertex
+// ---- periodicity under local refinement (add_periodicity, grids.cc:41-58; make_periodicity_constraints,
+// gls_navier_stokes.cc:128-134, 162-168): per pair (id a, id b, direction d) the vertices of the boundary
+// faces with id b are matched onto those of id a by the translation along d (every other coordinate
+// equal). A vertex without a partner lies on a face finer than the one across the periodic boundary.
+// `rep` joins matched vertices into classes (smallest id) for the level rules of the smoothing / balance.
+struct PeriodicVerts {
+  std::vector<std::array<int, 3>> pairs;
+  std::vector<std::map<int64_t, int64_t>> b2a, a2b;  // per pair
+  std::vector<int64_t> rep;
+  bool on() const { return !pairs.empty(); }
+  int64_t cls(int64_t v) const { return rep.empty() ? v : rep[(size_t)v]; }
+};
+double periodic_tol(const std::vector<V3> &X) {
+  double scale = 0;
+  for (auto &x : X) scale = std::max(scale, std::fabs(x[0]) + std::fabs(x[1]) + std::fabs(x[2]));
+  return 1e-8 * std::max(scale, 1e-300);
+}
+PeriodicVerts periodic_vertices(const UMesh &m, const std::vector<std::array<int, 3>> &pairs) {
+  PeriodicVerts P;
+  if (pairs.empty()) return P;
+  P.pairs = pairs;
+  const double tol = periodic_tol(m.X);
+  P.rep.resize(m.X.size());
+  for (size_t i = 0; i < P.rep.size(); ++i) P.rep[i] = (int64_t)i;
+  std::function<int64_t(int64_t)> root = [&](int64_t v) {
+    while (P.rep[(size_t)v] != v) v = P.rep[(size_t)v] = P.rep[(size_t)P.rep[(size_t)v]];
+    return v;
+  };
+  for (const auto &pr : pairs) {
+    std::set<int64_t> A, B;
+    for (const auto &kv : m.bface) {
+      if (kv.second != pr[0] && kv.second != pr[1]) continue;
+      for (int i = 0; i < 4; ++i)
+        if (kv.first.v[i] >= 0) (kv.second == pr[0] ? A : B).insert(kv.first.v[i]);
+    }
+    const int o1 = (pr[2] + 1) % 3, o2 = (pr[2] + 2) % 3;
+    auto cellk = [&](const V3 &x) {
+      return std::array<long long, 2>{std::llround(x[o1] / (100 * tol)), std::llround(x[o2] / (100 * tol))};
+    };
+    std::map<std::array<long long, 2>, std::vector<int64_t>> grid;
+    for (int64_t i : A) grid[cellk(m.X[(size_t)i])].push_back(i);
+    std::map<int64_t, int64_t> b2a, a2b;
+    for (int64_t j : B) {
+      const auto ck = cellk(m.X[(size_t)j]);
+      int64_t match = -1;
+      for (long long dx = -1; dx <= 1 && match < 0; ++dx)
+        for (long long dy = -1; dy <= 1 && match < 0; ++dy) {
+          auto g = grid.find({ck[0] + dx, ck[1] + dy});
+          if (g == grid.end()) continue;
+          for (int64_t i : g->second)
+            if (i != j && std::fabs(m.X[(size_t)i][o1] - m.X[(size_t)j][o1]) < tol &&
+                std::fabs(m.X[(size_t)i][o2] - m.X[(size_t)j][o2]) < tol) {
+              match = i;
+              break;
+            }
+        }
+      if (match < 0) continue;
+      b2a[j] = match;
+      a2b[match] = j;
+      const int64_t ra = root(match), rb = root(j);
+      if (ra != rb) P.rep[(size_t)std::max(ra, rb)] = std::min(ra, rb);
+    }
+    P.b2a.push_back(std::move(b2a));
+    P.a2b.push_back(std::move(a2b));
+  }
+  for (size_t i = 0; i < P.rep.size(); ++i) P.rep[i] = root((int64_t)i);
+  return P;
+}
+// the face across the periodic boundary with the same vertices (translated); false when `key` is not a
+// periodic boundary face or its translate is not a face of vertices that exist
+bool periodic_partner(const UMesh &m, const PeriodicVerts &P, const EKey &key, EKey &out) {
+  if (!P.on()) return false;
+  auto b = m.bface.find(key);
+  if (b == m.bface.end()) return false;
+  for (size_t p = 0; p < P.pairs.size(); ++p) {
+    const bool onA = b->second == P.pairs[p][0], onB = b->second == P.pairs[p][1];
+    if (!onA && !onB) continue;
+    const auto &mp = onA ? P.a2b[p] : P.b2a[p];
+    EKey k{{-1, -1, -1, -1}};
+    int n = 0;
+    bool ok = true;
+    for (int i = 0; i < 4 && ok; ++i) {
+      if (key.v[i] < 0) continue;
+      auto it = mp.find(key.v[i]);
+      if (it == mp.end()) ok = false;
+      else k.v[n++] = it->second;
+    }
+    if (!ok) continue;
+    std::sort(k.v, k.v + n);
+    out = k;
+    return true;
+  }
+  return false;
+}
+
+// highest active level at every vertex (periodic partners share it)
 std::vector<int> vertex_levels(const UMesh &m) {
   std::vector<int> vl(m.X.size(), -1);
   for (int64_t id : m.active) {
     const auto &h = m.tree[(size_t)id];
     for (int v = 0; v < m.nvc(); ++v) vl[(size_t)h.v[v]] = std::max(vl[(size_t)h.v[v]], h.level);
+  }
+  if (!m.periodic.empty()) {
+    const PeriodicVerts P = periodic_vertices(m, m.periodic);
+    for (size_t v = 0; v < vl.size(); ++v) vl[(size_t)P.cls((int64_t)v)] = std::max(vl[(size_t)P.cls((int64_t)v)], vl[v]);
+    for (size_t v = 0; v < vl.size(); ++v) vl[v] = vl[(size_t)P.cls((int64_t)v)];
   }
   return vl;
 }
@@ -522,8 +627,10 @@ struct USmoother {
   std::vector<int64_t> active_rev;              // active indices, reverse level order
   std::map<EKey, std::vector<int64_t>> faces;   // face vertex set -> live cells having that face
   std::unordered_map<int64_t, char> user;       // refined cells to be coarsened (fix_coarsen_flags)
+  PeriodicVerts pv;                             // faces across periodic boundaries are neighbours
 
-  USmoother(const UMesh &mesh, const int32_t *r, const int32_t *c) : m(mesh), dim(mesh.dim) {
+  USmoother(const UMesh &mesh, const int32_t *r, const int32_t *c)
+      : m(mesh), dim(mesh.dim), pv(periodic_vertices(mesh, mesh.periodic)) {
     const size_t na = m.active.size();
     ref.resize(na);
     crs.resize(na);
@@ -558,10 +665,16 @@ struct USmoother {
   int neighbor(int64_t id, int f, int64_t &nb) const {
     const auto &h = m.tree[(size_t)id];
     const int d = f / 2, s = f & 1;
-    auto it = faces.find(face_key_v(dim, h.v, d, s));
+    const EKey key = face_key_v(dim, h.v, d, s);
+    auto it = faces.find(key);
     if (it != faces.end())
       for (int64_t o : it->second)
         if (o != id) { nb = o; return 1; }
+    EKey pk;  // across a periodic boundary: the live cell of this level on the translated face
+    if (periodic_partner(m, pv, key, pk)) {
+      auto jt = faces.find(pk);
+      if (jt != faces.end() && !jt->second.empty()) { nb = jt->second[0]; return 1; }
+    }
     if (h.parent < 0 || ((h.pos >> d) & 1) != s) return 0;  // boundary (a child's inner face is shared)
     int64_t pn;
     if (neighbor(h.parent, f, pn) != 1) return 0;
@@ -595,8 +708,8 @@ struct USmoother {
       const auto &h = m.tree[(size_t)m.active[i]];
       const int lev = ref[i] ? h.level + 1 : crs[i] ? h.level - 1 : h.level;
       for (int v = 0; v < nv; ++v) {
-        auto it = vl.find(h.v[v]);
-        if (it == vl.end()) vl[h.v[v]] = std::max(0, lev);
+        auto it = vl.find(pv.cls(h.v[v]));
+        if (it == vl.end()) vl[pv.cls(h.v[v])] = std::max(0, lev);
         else it->second = std::max(it->second, lev);
       }
     }
@@ -604,12 +717,12 @@ struct USmoother {
       if (ref[(size_t)i]) continue;
       const auto &h = m.tree[(size_t)m.active[(size_t)i]];
       for (int v = 0; v < nv; ++v) {
-        const int lv = vl[h.v[v]];
+        const int lv = vl[pv.cls(h.v[v])];
         if (lv < h.level + 1) continue;
         crs[(size_t)i] = 0;
         if (lv > h.level + 1) {
           ref[(size_t)i] = 1;
-          for (int w = 0; w < nv; ++w) vl[h.v[w]] = std::max(vl[h.v[w]], h.level + 1);
+          for (int w = 0; w < nv; ++w) vl[pv.cls(h.v[w])] = std::max(vl[pv.cls(h.v[w])], h.level + 1);
         }
       }
     }
@@ -1130,10 +1243,13 @@ struct FESpaceImpl {
   std::vector<V3> verts;
   std::map<EKey, int64_t> line_mid, face_mid;
   std::vector<int> face_bid;  // [n_cells][2 dim] boundary id of each cell face, -1 interior
+  std::vector<std::array<int, 3>> periodic;  // the space's periodic pairs (id a, id b, direction)
 };
 
 using HangLines = std::map<int64_t, std::vector<std::pair<int64_t, double>>>;
 double lag1(int k, int a, double x);
+int close_lines(HangLines &out);
+bool periodic_face_params(int dim, int dir, const V3 (&C)[2][2], const V3 &x, double tol, double uv[2]);
 
 // DoFTools::make_hanging_node_constraints (gls_navier_stokes.cc:84, 143) for FE_Q(kk) on the
 // hierarchy: every line (3D: and quad) of an active cell that is refined in the active mesh (its
@@ -1248,7 +1364,11 @@ int hanging_lines(const UMesh &m, int kk, const std::map<EKey, int64_t> &ids, co
           }
       }
   }
-  // close the chains: substitute constrained masters by their lines
+  return close_lines(out);
+}
+
+// AffineConstraints::close: substitute constrained masters by their lines until none is left
+int close_lines(HangLines &out) {
   for (int pass = 0; pass < 32; ++pass) {
     bool changed = false;
     for (auto &kv : out) {
@@ -1280,6 +1400,52 @@ double lag1(int k, int a, double x) {  // Lagrange basis a of degree k on equidi
   for (int b = 0; b <= k; ++b)
     if (b != a) v *= (x - (double)b / k) / ((double)(a - b) / k);
   return v;
+}
+
+// (u, v) on a straight periodic face with corners C[iu][iv] (2D: a line, v = 0) of the point x, in the
+// coordinates across the periodic direction `dir` (x and the face may sit on either side of the
+// boundary); false when x is off the face. Snapped to multiples of 1/16 (the positions of nodes of
+// finer faces of the hierarchy) when within 1e-10.
+bool periodic_face_params(int dim, int dir, const V3 (&C)[2][2], const V3 &x, double tol, double uv[2]) {
+  auto pr = [&](V3 a) {
+    a[dir] = 0.0;
+    return a;
+  };
+  const V3 c00 = pr(C[0][0]), c10 = pr(C[1][0]), xx = pr(x);
+  double u = 0.5, v = 0.0;
+  if (dim == 2) {
+    const V3 t = sub(c10, c00);
+    const double tt = dot3(t, t);
+    if (tt <= 0) return false;
+    u = dot3(sub(xx, c00), t) / tt;
+    if (nrm(sub(add(c00, scl(t, u)), xx)) > tol) return false;
+  } else {
+    const V3 c01 = pr(C[0][1]), c11 = pr(C[1][1]);
+    const int o1 = (dir + 1) % 3, o2 = (dir + 2) % 3;
+    v = 0.5;
+    for (int it = 0; it < 40; ++it) {
+      V3 F = sub(add(add(scl(c00, (1 - u) * (1 - v)), scl(c10, u * (1 - v))), add(scl(c01, (1 - u) * v), scl(c11, u * v))), xx);
+      const V3 Fu = add(scl(sub(c10, c00), 1 - v), scl(sub(c11, c01), v));
+      const V3 Fv = add(scl(sub(c01, c00), 1 - u), scl(sub(c11, c10), u));
+      const double det = Fu[o1] * Fv[o2] - Fu[o2] * Fv[o1];
+      if (std::fabs(det) < 1e-300) return false;
+      const double du = -(F[o1] * Fv[o2] - F[o2] * Fv[o1]) / det, dv = -(Fu[o1] * F[o2] - Fu[o2] * F[o1]) / det;
+      u += du;
+      v += dv;
+      if (std::fabs(du) + std::fabs(dv) < 1e-15) break;
+    }
+    const V3 F = sub(add(add(scl(c00, (1 - u) * (1 - v)), scl(c10, u * (1 - v))), add(scl(c01, (1 - u) * v), scl(c11, u * v))), xx);
+    if (nrm(F) > tol) return false;
+  }
+  const double e = 1e-9;
+  if (u < -e || u > 1 + e || v < -e || v > 1 + e) return false;
+  for (double *w : {&u, &v}) {
+    const double r = std::round(*w * 16.0) / 16.0;
+    if (std::fabs(r - *w) < 1e-10) *w = r;
+  }
+  uv[0] = u;
+  uv[1] = v;
+  return true;
 }
 
 // deal.II cell->measure(): exact area / volume of the bilinear / trilinear cell (2-point Gauss of
@@ -1469,7 +1635,6 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
     }
     HangLines hang;
     if (int rc = hanging_lines(m, kk, ids, cn, hang); rc != GLS_OK) return rc;
-    if (!hang.empty() && nper > 0) return gls_io_set_error(GLS_EINVAL, "periodic boundaries on locally refined meshes are not supported");
     // boundary id bits
     std::vector<uint32_t> bits(pos.size(), 0u);
     for (int64_t c = 0; c < nc; ++c)
@@ -1482,9 +1647,14 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
             if (ia[d] == s * kk) bits[(size_t)cn[(size_t)(c * nn + a)]] |= 1u << b->second;
           }
         }
-    // periodic identification: nodes on faces of id b map onto the translated nodes of id a
+    // periodic identification (make_periodicity_constraints): nodes on faces of id b map onto the
+    // translated nodes of id a. Under local refinement a node without a partner lies on a face finer than
+    // the one across the boundary; it is constrained to that coarser face's Q_kk interpolant at its
+    // position (deal.II constrains the finer side's DoFs to the coarser side's), like a hanging node.
     std::vector<int64_t> rep(pos.size());
     for (size_t i = 0; i < rep.size(); ++i) rep[i] = (int64_t)i;
+    HangLines phang;  // pre-identification node ids
+    const double tol = periodic_tol(pos);
     for (int p = 0; p < nper; ++p) {
       const int ida = per[3 * p], idb = per[3 * p + 1], dir = per[3 * p + 2];
       std::vector<int64_t> A, B;
@@ -1492,13 +1662,12 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
         if ((bits[i] >> ida) & 1) A.push_back((int64_t)i);
         if ((bits[i] >> idb) & 1) B.push_back((int64_t)i);
       }
-      double scale = 0;
-      for (auto &x : pos) scale = std::max(scale, std::fabs(x[0]) + std::fabs(x[1]) + std::fabs(x[2]));
-      const double tol = 1e-8 * std::max(scale, 1e-300);
       std::map<std::array<long long, 2>, std::vector<int64_t>> grid;
       const int o1 = (dir + 1) % 3, o2 = (dir + 2) % 3;
       auto cellk = [&](const V3 &x) { return std::array<long long, 2>{std::llround(x[o1] / (100 * tol)), std::llround(x[o2] / (100 * tol))}; };
       for (auto i : A) grid[cellk(pos[(size_t)i])].push_back(i);
+      std::set<int64_t> hitA;
+      std::vector<int64_t> loneB;
       for (auto j : B) {
         int64_t match = -1;
         const auto ck = cellk(pos[(size_t)j]);
@@ -1510,8 +1679,76 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
               if (std::fabs(pos[(size_t)i][o1] - pos[(size_t)j][o1]) < tol &&
                   std::fabs(pos[(size_t)i][o2] - pos[(size_t)j][o2]) < tol) { match = i; break; }
           }
-        if (match < 0) return gls_io_set_error(GLS_EINVAL, "periodic boundaries %d / %d: node without a partner", ida, idb);
+        if (match < 0) {
+          loneB.push_back(j);
+          continue;
+        }
         rep[(size_t)j] = match;
+        hitA.insert(match);
+      }
+      std::vector<int64_t> loneA;
+      for (auto i : A)
+        if (!hitA.count(i)) loneA.push_back(i);
+      if (loneA.empty() && loneB.empty()) continue;
+      // the active cells' faces on a side: corners (lexicographic in the two tangential directions) + nodes
+      struct PFace {
+        V3 C[2][2];
+        std::vector<int64_t> kn;
+      };
+      auto side_faces = [&](int bid) {
+        std::vector<PFace> out;
+        for (int64_t c = 0; c < nc; ++c)
+          for (int d = 0; d < dim; ++d)
+            for (int s2 = 0; s2 < 2; ++s2) {
+              auto bf = m.bface.find(face_key(m, (size_t)c, d, s2));
+              if (bf == m.bface.end() || bf->second != bid) continue;
+              int t[2] = {0, 0}, nt = 0;
+              for (int e = 0; e < dim; ++e)
+                if (e != d) t[nt++] = e;
+              PFace f;
+              const auto &cv = m.cells[(size_t)c];
+              for (int iu = 0; iu < 2; ++iu)
+                for (int iv = 0; iv < 2; ++iv)
+                  f.C[iu][iv] = m.X[(size_t)cv[(size_t)((s2 << d) | (iu << t[0]) | (dim == 3 ? iv << t[1] : 0))]];
+              for (int jv = 0; jv <= (dim == 3 ? kk : 0); ++jv)
+                for (int ju = 0; ju <= kk; ++ju) {
+                  int ia[3] = {0, 0, 0};
+                  ia[d] = s2 * kk;
+                  ia[t[0]] = ju;
+                  if (dim == 3) ia[t[1]] = jv;
+                  f.kn.push_back(cn[(size_t)(c * nn + ia[0] + kk1 * (ia[1] + (dim == 3 ? kk1 * ia[2] : 0)))]);
+                }
+              out.push_back(std::move(f));
+            }
+        return out;
+      };
+      auto constrain = [&](const std::vector<int64_t> &lone, const std::vector<PFace> &across, int ida_, int idb_) -> int {
+        for (int64_t j : lone) {
+          if (hang.count(j) || phang.count(j)) continue;  // already a hanging node of its own side
+          bool done = false;
+          for (const auto &f : across) {
+            double uv[2];
+            if (!periodic_face_params(dim, dir, f.C, pos[(size_t)j], tol, uv)) continue;
+            std::vector<std::pair<int64_t, double>> line;
+            for (int jv = 0; jv <= (dim == 3 ? kk : 0); ++jv)
+              for (int ju = 0; ju <= kk; ++ju) {
+                const double w = lag1(kk, ju, uv[0]) * (dim == 3 ? lag1(kk, jv, uv[1]) : 1.0);
+                if (std::fabs(w) > 1e-13) line.push_back({f.kn[(size_t)(ju + kk1 * jv)], w});
+              }
+            phang[j] = line;
+            done = true;
+            break;
+          }
+          if (!done)
+            return gls_io_set_error(GLS_EINVAL, "periodic boundaries %d / %d: node without a partner face", ida_, idb_);
+        }
+        return GLS_OK;
+      };
+      if (!loneB.empty()) {
+        if (int rc = constrain(loneB, side_faces(ida), ida, idb); rc != GLS_OK) return rc;
+      }
+      if (!loneA.empty()) {
+        if (int rc = constrain(loneA, side_faces(idb), ida, idb); rc != GLS_OK) return rc;
       }
     }
     for (size_t i = 0; i < rep.size(); ++i)  // chains (corner nodes of several periodic pairs)
@@ -1529,14 +1766,33 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
       nb[(size_t)t] |= bits[i];
     }
     for (auto &x : cn) x = (int32_t)compact[(size_t)rep[(size_t)x]];
+    // constraint lines in the identified numbering: the hanging lines of each side, then the periodic
+    // lines of unpartnered nodes (a node keeps its first line), chains closed together
+    HangLines all;
+    auto put = [&](const HangLines &H) {
+      for (auto &kv : H) {
+        const int64_t nd = compact[(size_t)rep[(size_t)kv.first]];
+        if (all.count(nd)) continue;
+        std::map<int64_t, double> acc;
+        for (auto &mw : kv.second) acc[compact[(size_t)rep[(size_t)mw.first]]] += mw.second;
+        std::vector<std::pair<int64_t, double>> line;
+        for (auto &a : acc)
+          if (std::fabs(a.second) > 1e-14 && a.first != nd) line.push_back(a);
+        all[nd] = line;
+      }
+    };
+    put(hang);
+    put(phang);
+    if (!phang.empty())
+      if (int rc = close_lines(all); rc != GLS_OK) return rc;
     hnode.clear();
     hoff.assign(1, 0);
     hmaster.clear();
     hw.clear();
-    for (auto &kv : hang) {  // (no periodic identification here: ids are compact already)
-      hnode.push_back(compact[(size_t)kv.first]);
+    for (auto &kv : all) {
+      hnode.push_back(kv.first);
       for (auto &mw : kv.second) {
-        hmaster.push_back(compact[(size_t)mw.first]);
+        hmaster.push_back(mw.first);
         hw.push_back(mw.second);
       }
       hoff.push_back((int64_t)hmaster.size());
@@ -1580,6 +1836,8 @@ int build_fe_space(const UMesh &m, int k, int kp, int qall, int nper, const int3
       if (b != m.bface.end()) F.face_bid[(size_t)(c * 2 * dim + f)] = b->second;
     }
   F.verts = m.X;
+  F.periodic.clear();
+  for (int p = 0; p < nper; ++p) F.periodic.push_back({per[3 * p], per[3 * p + 1], per[3 * p + 2]});
   F.line_mid = m.line_mid;
   F.face_mid = m.face_mid;
   auto &P = F.pub;
@@ -2089,6 +2347,33 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
     for (int e = 0; e < dim; ++e)
       if (e != d) t[n++] = e;
   };
+  // periodic boundaries (KellyErrorEstimator's periodic neighbours): the active faces on each periodic id
+  struct PFace {
+    int64_t c;
+    int f;
+    V3 C[2][2];
+  };
+  auto face_corners = [&](int64_t c, int f, V3 (&C)[2][2]) {
+    const auto &cv = F.cell_verts[(size_t)c];
+    const int d = f / 2, s = f & 1;
+    int t[2] = {0, 0}, nt = 0;
+    for (int e = 0; e < dim; ++e)
+      if (e != d) t[nt++] = e;
+    for (int iu = 0; iu < 2; ++iu)
+      for (int iv = 0; iv < 2; ++iv)
+        C[iu][iv] = F.verts[(size_t)cv[(size_t)((s << d) | (iu << t[0]) | (dim == 3 ? iv << t[1] : 0))]];
+  };
+  std::map<int, std::vector<PFace>> pfaces;
+  const double ptol = F.periodic.empty() ? 0.0 : periodic_tol(F.verts);
+  for (const auto &pr : F.periodic)
+    for (int64_t c = 0; c < nc; ++c)
+      for (int f = 0; f < 2 * dim; ++f) {
+        const int bid = F.face_bid[(size_t)(c * 2 * dim + f)];
+        if (bid != pr[0] && bid != pr[1]) continue;
+        PFace pf{c, f, {}};
+        face_corners(c, f, pf.C);
+        pfaces[bid].push_back(pf);
+      }
   int64_t cnt = 0;
   for (int64_t a = 0; a < nc; ++a)
     for (int fa = 0; fa < 2 * dim; ++fa) {
@@ -2097,7 +2382,8 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
       const auto &lst = faces[face_key_v(dim, av, da, sa)];
       int64_t b = -1;
       int fb = -1;
-      bool irregular = false;
+      bool irregular = false, periodic = false;
+      std::array<double, 2> Pc[3];  // periodic pieces: a's face corners in b's face parameters
       if (lst.size() == 2) {
         const auto &o = lst[0].first == a ? lst[1] : lst[0];
         if (o.first < a) continue;  // emitted from the other side
@@ -2106,12 +2392,49 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
       } else {
         const int64_t h = F.hid[(size_t)a];
         const int64_t P = F.t_parent.empty() ? -1 : F.t_parent[(size_t)h];
-        if (P < 0 || ((F.t_pos[(size_t)h] >> da) & 1) != sa) continue;
-        auto it = faces.find(face_key_v(dim, F.t_verts[(size_t)P], da, sa));
-        if (it == faces.end() || it->second.size() != 1) continue;  // boundary
-        b = it->second[0].first;
-        fb = it->second[0].second;
-        irregular = true;
+        std::map<EKey, std::vector<std::pair<int64_t, int>>>::const_iterator it = faces.end();
+        if (P >= 0 && ((F.t_pos[(size_t)h] >> da) & 1) == sa) it = faces.find(face_key_v(dim, F.t_verts[(size_t)P], da, sa));
+        if (it != faces.end() && it->second.size() == 1) {
+          b = it->second[0].first;
+          fb = it->second[0].second;
+          irregular = true;
+        } else {  // a boundary face: a piece only across a periodic boundary
+          const int bid = F.face_bid[(size_t)(a * 2 * dim + fa)];
+          int other = -1, dir = 0;
+          for (const auto &pr : F.periodic)
+            if (bid == pr[0] || bid == pr[1]) {
+              other = bid == pr[0] ? pr[1] : pr[0];
+              dir = pr[2];
+            }
+          if (other < 0) continue;
+          V3 Ca[2][2];
+          face_corners(a, fa, Ca);
+          V3 xc{0, 0, 0};
+          for (int iu = 0; iu < 2; ++iu)
+            for (int iv = 0; iv < (dim == 3 ? 2 : 1); ++iv) xc = add(xc, scl(Ca[iu][iv], dim == 3 ? 0.25 : 0.5));
+          const PFace *hit = nullptr;
+          double uv[2];
+          for (const auto &pf : pfaces[other])
+            if (periodic_face_params(dim, dir, pf.C, xc, ptol, uv)) {
+              hit = &pf;
+              break;
+            }
+          if (!hit) return gls_io_set_error(GLS_EINVAL, "Kelly faces: periodic face of cell %lld without a partner", (long long)a);
+          b = hit->c;
+          fb = hit->f;
+          const int la = F.cell_level[(size_t)a], lb = F.cell_level[(size_t)b];
+          if (lb > la) continue;                                             // the finer side emits the pieces
+          if (lb == la && (b < a || (b == a && fb < fa))) continue;          // emitted from the other side
+          irregular = lb < la;
+          periodic = true;
+          const int cu[3] = {0, 1, 0}, cvv[3] = {0, 0, 1};
+          for (int i = 0; i < (dim == 3 ? 3 : 2); ++i) {
+            if (!periodic_face_params(dim, dir, hit->C, Ca[cu[i]][cvv[i]], ptol, uv))
+              return gls_io_set_error(GLS_EINVAL, "Kelly faces: periodic cells %lld / %lld do not share a face piece",
+                                      (long long)a, (long long)b);
+            Pc[i] = {uv[0], uv[1]};
+          }
+        }
       }
       if (!xi) {
         ++cnt;
@@ -2122,7 +2445,8 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
       tang(da, ta);
       tang(db, tb);
       const auto &bv = F.cell_verts[(size_t)b];
-      // b's face lattice: vertex id -> face parameters (corners; with the midpoints when irregular)
+      // b's face lattice: vertex id -> face parameters (corners; with the midpoints when irregular);
+      // periodic pieces have theirs from the geometry already
       std::map<int64_t, std::array<double, 2>> par;
       int64_t C[2][2] = {{-1, -1}, {-1, -1}};
       for (int iu = 0; iu < 2; ++iu)
@@ -2146,9 +2470,8 @@ int gls_fe_space_kelly_faces(const gls_fe_space *sp, int nq, int64_t *n_pieces, 
         }
       }
       // a's face corners (0,0), (1,0), (0,1) in b's face parameters
-      std::array<double, 2> Pc[3];
       const int cu[3] = {0, 1, 0}, cvv[3] = {0, 0, 1};
-      for (int i = 0; i < (dim == 3 ? 3 : 2); ++i) {
+      for (int i = 0; i < (dim == 3 ? 3 : 2) && !periodic; ++i) {
         const int64_t vid = av[(size_t)((sa << da) | (cu[i] << ta[0]) | (dim == 3 ? cvv[i] << ta[1] : 0))];
         auto it = par.find(vid);
         if (it == par.end()) return gls_io_set_error(GLS_EINVAL, "Kelly faces: cells %lld / %lld do not share a face piece", (long long)a, (long long)b);
@@ -2331,6 +2654,18 @@ int gls_fe_space_boundary_normal_sets(const gls_fe_space *sp, int boundary_id, i
       }
     }
     count[v] = r;
+  }
+  return GLS_OK;
+}
+
+int gls_umesh_set_periodic(gls_umesh *g, int n_periodic, const int32_t *periodic) {
+  if (!g || n_periodic < 0 || (n_periodic > 0 && !periodic)) return gls_io_set_error(GLS_EINVAL, "gls_umesh_set_periodic: arguments");
+  g->m.periodic.clear();
+  for (int p = 0; p < n_periodic; ++p) {
+    const int d = periodic[3 * p + 2];
+    if (d < 0 || d >= g->m.dim || periodic[3 * p] == periodic[3 * p + 1])
+      return gls_io_set_error(GLS_EINVAL, "gls_umesh_set_periodic: pair %d", p);
+    g->m.periodic.push_back({periodic[3 * p], periodic[3 * p + 1], d});
   }
   return GLS_OK;
 }

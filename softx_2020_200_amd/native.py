@@ -41,7 +41,7 @@ EXPORTS = [
     "gls_freeze_jacobian", "gls_skip_newton_selftest", "gls_quadrature_points",
     "gls_umesh_generate", "gls_umesh_read_gmsh", "gls_umesh_set_manifold", "gls_umesh_boundary_manifold",
     "gls_umesh_refine_global", "gls_umesh_info", "gls_umesh_destroy", "gls_umesh_fe_space", "gls_fe_space_destroy",
-    "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_fe_space_kelly_faces",
+    "gls_fe_space_transfer", "gls_umesh_prepare", "gls_umesh_adapt", "gls_umesh_set_periodic", "gls_fe_space_kelly_faces",
     "gls_kelly_estimate_mapped", "gls_fe_space_boundary_normals", "gls_fe_space_boundary_normal_sets",
     "gls_octree_coarsen_to", "gls_octree_mg_transfer", "gls_mg_attach_transfers", "gls_umesh_coarsen_to",
     "gls_fe_space_mg_transfer", "gls_forest_bricks",
@@ -205,6 +205,7 @@ def load():
     pi32 = C.POINTER(C.c_int32)
     L.gls_umesh_prepare.argtypes = [vp, pi32, pi32]
     L.gls_umesh_adapt.argtypes = [vp, pi32, pi32]
+    L.gls_umesh_set_periodic.argtypes = [vp, C.c_int, pi32]
     L.gls_fe_space_kelly_faces.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(i64), pi32, pi32, d, d, d, d]
     L.gls_fe_space_boundary_normals.argtypes = [C.POINTER(FESpace), C.c_int, d]
     L.gls_fe_space_boundary_normal_sets.argtypes = [C.POINTER(FESpace), C.c_int, C.POINTER(C.c_int32), d]
@@ -967,6 +968,13 @@ class UMesh:
         check(self.L.gls_umesh_fe_space(self.h, int(k), int(kp), 1 if qmapping_all else 0, len(per) // 3,
                                         per.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pm)), "gls_umesh_fe_space")
         return FESpaceHandle(self.L, pm)
+
+    def set_periodic(self, periodic):
+        """Periodic pairs (id a, id b, direction) of the triangulation (gls_umesh_set_periodic): the mesh
+        smoothing and the 2:1 balance see across them."""
+        per = np.ascontiguousarray(np.array(periodic, dtype=np.int32).reshape(-1))
+        check(self.L.gls_umesh_set_periodic(self.h, len(per) // 3, per.ctypes.data_as(C.POINTER(C.c_int32))),
+              "gls_umesh_set_periodic")
 
     def coarsen_to(self, level):
         """A copy with every active cell finer than `level` replaced by its ancestor (gls_umesh_coarsen_to):

@@ -487,6 +487,66 @@ end""")
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_app_periodic_kelly_adaptation_general_mesh(tmp_path, k):
+    """The same periodic manufactured flow on the GENERAL mesh path (GridGenerator
+    subdivided_hyper_rectangle -> gls_umesh: MappingQ geometry, per-cell kernels): the triangulation
+    carries the periodic pair (gls_umesh_set_periodic: the smoothing and the 2:1 balance see across it),
+    the space identifies the partnered nodes and constrains the nodes of a finer periodic face to the
+    coarser face across it, the Kelly faces include the periodic pieces. Three Kelly cycles refine and the
+    velocity error falls every cycle. Parity unpinned (no reference case combines periodicity with
+    adaptation; the constraint algebra is checked on the CPU in tests/test_umesh_periodic.py)."""
+    prm = mms_prm({"force": PERIODIC_MMS_FORCE, "exact": PERIODIC_MMS_EXACT}, 2, 3, 2)
+    prm = prm.replace("  set grid type          = hyper_cube\n  set grid arguments     = -1 : 1 : false",
+                      "  set grid type          = subdivided_hyper_rectangle\n"
+                      "  set grid arguments     = 1,1 : -1,-1 : 1,1 : true")
+    assert "subdivided_hyper_rectangle" in prm
+    prm = prm.replace("  set velocity order = 1\n  set pressure order = 1", f"  set velocity order = {k}\n  set pressure order = 1")
+    prm = prm.replace("  set type = uniform\n", """  set type = kelly
+  set variable = velocity
+  set fraction type = number
+  set fraction refinement = 0.3
+  set fraction coarsening = 0.0
+""")
+    prm = prm.replace("""subsection boundary conditions
+  set number = 1
+  subsection bc 0
+    set type = noslip
+  end
+end""", """subsection boundary conditions
+  set number = 3
+  subsection bc 0
+    set type = periodic
+    set id = 0
+    set periodic_id = 1
+    set periodic_direction = 0
+  end
+  subsection bc 1
+    set type = noslip
+    set id = 2
+  end
+  subsection bc 2
+    set type = noslip
+    set id = 3
+  end
+end""")
+    out = run_app(tmp_path, prm, 2, "--precond", "jacobi")
+    rows = table(out)
+    assert len(rows) == 3, out
+    cells = [int(r[0]) for r in rows]
+    assert cells[0] == 64 and cells[1] > cells[0] and cells[2] > cells[1], cells
+    errs = [r[1] for r in rows]
+    assert errs[1] < errs[0] and errs[2] < errs[1], errs
+    # the uniform first mesh equals the hyper_cube path's (same cells, same periodic identification)
+    ref = run_app(tmp_path, prm.replace("  set grid type          = subdivided_hyper_rectangle\n"
+                                        "  set grid arguments     = 1,1 : -1,-1 : 1,1 : true",
+                                        "  set grid type          = hyper_cube\n  set grid arguments     = -1 : 1 : true"),
+                  2, "--precond", "jacobi")
+    r0 = table(ref)[0]
+    assert abs(rows[0][1] - r0[1]) <= 1e-6 * r0[1], (rows[0], r0)
+
+
+@pytest.mark.gpu
 def test_app_transient_kelly_periodic_tgv(tmp_path):
     """Transient Kelly adaptation on a periodic hyper_cube (refine_mesh_kelly every step with the time
     history transferred, navier_stokes_base.cc:684-733): the reference's 2D Taylor-Green vortex prm
