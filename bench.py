@@ -40,7 +40,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
-PMC_TRAFFIC_FILE = "r04_pmc_traffic_pencil_128.txt"  # tools/pmc_traffic.sh summary of the pencil J.v
+PMC_TRAFFIC_FILE = "r04_pmc_traffic_pencil_128.txt"  # tools/pmc_traffic.sh summary of the pencil J.v (fallback)
+LDS_MODEL_FILE = "r05_lds_model.json"                # tools/lds_model.py (static model, source-hash tagged)
 FP64_PEAK_TFS = 78.6        # MI355X FP64 (vector = matrix) spec; measured 61-64 TF (profiles/r01_microbench_fp64.txt)
 
 
@@ -92,6 +93,72 @@ def pmc_traffic(path, kernel_mode, n_dofs):
     # the J.v's slab node sum (one k_slab_sum per brick launch, same size for every mode)
     t = sum(d.get("FETCH_SIZE", 0.0) * fetch_corr + d.get("WRITE_SIZE", 0.0) * write_corr for d in (kern, slab))
     return t, fetch_corr, write_corr
+
+
+def live_pmc_traffic(n, k, n_dofs, timeout=180):
+    """HBM bytes per launch of the J.v (pencil kernel + its slab sum) MEASURED NOW: two separate
+    `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes (MI355X_MICROARCH.md "HBM": one TCC counter
+    group per pass) over tools/jv_bench.py in a child process (this process keeps its GPU state; nothing is
+    exec'ed), calibrated on the k_copy of n_dofs doubles in the same run (gfx950 counts half of a
+    streaming read in FETCH_SIZE). Returns (bytes, fetch_corr, write_corr) or raises."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    out = tempfile.mkdtemp(prefix="gls_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    vals = {}
+    for i, ctr in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+        cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "gls_pencil_kernel|gls_brick_kernel|k_copy|k_slab_sum",
+               "-d", os.path.join(out, "p%d" % i), "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "tools", "jv_bench.py"), str(n), "4"]
+        subprocess.run(cmd, timeout=timeout, capture_output=True, check=True, cwd=out, env=dict(os.environ, GLS_K=str(k)))
+        for f in glob.glob(os.path.join(out, "p%d" % i, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                vals.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]) * 1024.0)
+    shutil.rmtree(out, ignore_errors=True)
+    mean = {kn: {c: sum(v) / len(v) for c, v in d.items()} for kn, d in vals.items()}
+    copy = next(v for kn, v in mean.items() if "k_copy" in kn)
+    kern = next(v for kn, v in mean.items() if "gls_pencil_kernel<double, 4" in kn or "gls_brick_kernel<%d, 4, double>" % k in kn)
+    slab = next((v for kn, v in mean.items() if "k_slab_sum_cube<double, false" in kn or "k_slab_sum<double" in kn), {})
+    fc, wc = 8.0 * n_dofs / copy["FETCH_SIZE"], 8.0 * n_dofs / copy["WRITE_SIZE"]
+    t = sum(d.get("FETCH_SIZE", 0.0) * fc + d.get("WRITE_SIZE", 0.0) * wc for d in (kern, slab))
+    return t, fc, wc
+
+
+def step_bytes_model(n, k, m, L, f32_fine, k_hist=2):
+    """Algorithmic HBM bytes of one Newton iteration of the cube (SURVEY §8d formulas, every array touched
+    once per operator call): assemble_matrix_and_rhs (B_res + the diagonal's 8N), L line-search residuals
+    (B_res), m FP64 J.v (B_Jv), the V-cycles' smoother J.v (B_Jv at the level's size: `f32_fine` measured
+    launches on the fine level, 2 per V-cycle on each coarser level), their transfers (restriction reads the
+    fine and writes the coarse vector, prolongation reads the coarse one and updates the fine x: 8 (3 N_l + 2
+    N_l+1)) and first Jacobi sweeps (b, D, x: 24 N_l), and the Gram-Schmidt passes (multi-dot over j + 1
+    vectors and the projection over j + 2 at step j, the final update over m + 2)."""
+    def sz(c):  # (velocity nodes, DoFs) of the Qk-Qk c^3 cube
+        nv = (k * c + 1) ** 3
+        return nv, 4 * nv
+    def b_jv(c):
+        nv, N = sz(c)
+        return 8 * N * 3 + 8 * k_hist * 3 * nv + 4 * c ** 3 * (k + 1) ** 3 + 32 * c ** 3 + nv
+    def b_res(c):
+        nv, N = sz(c)
+        return 8 * N * 2 + 8 * k_hist * 3 * nv + 4 * c ** 3 * (k + 1) ** 3 + 32 * c ** 3
+    N = sz(n)[1]
+    levels = []
+    c = n
+    while c > 2:
+        levels.append(c)
+        c //= 2
+    levels.append(2)
+    vcyc = max(f32_fine // 2, 1)
+    parts = {"assemble_matrix_and_rhs": b_res(n) + 8 * N, "line_search_residuals": L * b_res(n),
+             "jacobian_apply_fp64": m * b_jv(n), "smoother_jv_fine": f32_fine * b_jv(n),
+             "smoother_jv_coarse": vcyc * sum(2 * b_jv(c) for c in levels[1:-1]),
+             "transfers": vcyc * sum(8 * (3 * sz(a)[1] + 2 * sz(b)[1]) for a, b in zip(levels[:-1], levels[1:])),
+             "jacobi_first_sweeps": vcyc * sum(24 * sz(c)[1] for c in levels[:-1]),
+             "orthogonalisation": 8 * N * (sum(2 * j + 3 for j in range(1, int(m) + 1)) + int(m) + 2)}
+    return sum(parts.values()), parts
 
 
 def _cpu_model():
@@ -529,6 +596,9 @@ def main():
                     help="cpu_baseline = a complete CPU Newton iteration on the full workload (the job threads; "
                          "minutes at configs[1]); default: the bounded extrapolated sample")
     ap.add_argument("--jv-reps", type=int, default=10, help="extra back-to-back J.v launches timed for the roofline")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 --pmc traffic passes (roofline.traffic then replays the committed "
+                         "summary, labelled)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo stages through the host (testing on one GPU)")
     ap.add_argument("--dist-impl", default="native", choices=["torch", "native"],
@@ -783,16 +853,46 @@ def main():
                                              "k_slab_sum": slab_launch_ms}},
         "setup_s": t_setup,
     }
-    # measured HBM traffic of the same kernel (committed PMC summary of this build at this size)
-    tr = pmc_traffic(os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE), 4, N_global) \
-        if (world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil) else None
-    model_path = os.path.join(ROOT, "profiles", "r04_lds_model.json")
+    # the whole Newton iteration against the HBM roof: algorithmic bytes of every operator / vector pass of the
+    # step (model, step_bytes_model) over the measured step time
+    if world == 1 and ctx.uses_brick_kernels and args.precond == "mg" and args.scheme == "bdf2":
+        bs, parts = step_bytes_model(args.n, args.k, float(np.mean(lin_its)), float(np.mean(nres)) - 1.0, f32_n)
+        ach = bs / (t_max / args.steps) / 1e9
+        out["step_roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes_per_step": bs,
+                                "bytes_by_part": parts, "ms_per_step": 1e3 * t_max / args.steps,
+                                "model": "SURVEY §8d per-operator formulas x the step's measured counts (GMRES "
+                                         "iterations, line-search residuals, fine smoother launches); kernel time "
+                                         "and PMC bytes per class: profiles/r05_step_budget.txt"}
+    # measured HBM traffic of the same kernel: live PMC passes (child rocprofv3 runs over tools/jv_bench.py),
+    # else the committed summary, labelled as replayed
+    tr, tr_src = None, None
+    if world == 1 and args.n == 128 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil:
+        if not args.no_pmc:
+            try:
+                del v, y
+                torch.cuda.empty_cache()
+                tr = live_pmc_traffic(args.n, args.k, N_global)
+                tr_src = ("MEASURED in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
+                          "tools/jv_bench.py %d, FETCH_SIZE x %.2f + WRITE_SIZE x %.2f (k_copy calibration of the same "
+                          "run)" % (args.n, tr[1], tr[2]))
+            except Exception as e:  # noqa: BLE001 (report, fall back)
+                tr_src = "live PMC failed (%s: %s); " % (type(e).__name__, str(e)[:120])
+        if tr is None:
+            tr = pmc_traffic(os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE), 4, N_global)
+            if tr is not None:
+                tr_src = (tr_src or "") + ("REPLAYED from the committed profiles/%s (FETCH_SIZE x %.2f + WRITE_SIZE x "
+                                           "%.2f), not measured in this run" % (PMC_TRAFFIC_FILE, tr[1], tr[2]))
+    model_path = os.path.join(ROOT, "profiles", LDS_MODEL_FILE)
     if world == 1 and args.k == 2 and args.kp == 2 and ctx.uses_brick_kernels and pencil and os.path.exists(model_path):
         # the LDS and VALU issue floors of the pencil J.v from a STATIC model of its compiled instruction
         # stream (tools/lds_model.py: LDS instructions priced conflict-free by MI355X_MICROARCH.md §LDS,
         # FP64 VALU at 4 cycles per wave instruction), not a measurement; the commit it was derived from
         # is in the file
+        import hashlib
         mdl = json.load(open(model_path))
+        src = os.path.join(ROOT, mdl.get("source", "softx_2020_200_amd/csrc/gls_brick_pencil.hip"))
+        stale = mdl.get("source_sha256") != hashlib.sha256(open(src, "rb").read()).hexdigest()
         km = next(v for k_, v in mdl["kernels"].items() if "gls_pencil_kernelIdLi4ELb0" in k_)
         waves_per_cu = -(-(n_cells // 8) // 3) * 4 / 256
         lds_ms = waves_per_cu * km["lds_cycles_per_wave"] / 2.4e9 * 1e3  # the CU's LDS pipe at 2400 MHz
@@ -801,13 +901,17 @@ def main():
                                   "lds_cycles_per_wave": km["lds_cycles_per_wave"], "waves_per_cu": waves_per_cu,
                                   "floor_ms_at_2400MHz": lds_ms, "valu_floor_ms_at_2400MHz": valu_ms,
                                   "launch_ms": jv_launch_ms, "frac": lds_ms / jv_launch_ms,
-                                  "source": "profiles/r04_lds_model.json (%s)" % mdl.get("commit")}
+                                  "source": "profiles/%s (%s)" % (LDS_MODEL_FILE, mdl.get("commit")),
+                                  "stale": stale,
+                                  "stale_note": "the kernel source changed since the model was made: rerun "
+                                                "tools/lds_model.py" if stale else "model made from this source"}
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
-        out["roofline"]["traffic_source"] = ("profiles/%s: FETCH_SIZE x %.2f + WRITE_SIZE x "
-                                             "%.2f (k_copy calibration); includes the per-quadrature-point "
-                                             "linearization stream (16 doubles/q) the cached J.v reads instead "
-                                             "of re-deriving u, grad u, tau, R_s" % (PMC_TRAFFIC_FILE, tr[1], tr[2]))
+        out["roofline"]["traffic_source"] = (tr_src + "; includes the per-quadrature-point linearization stream "
+                                             "(16 doubles/q) the cached J.v reads instead of re-deriving u, grad u, "
+                                             "tau, R_s")
+    elif tr_src:
+        out["roofline"]["traffic_source"] = tr_src
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_full:
         # the reference's CPU path measured end to end on this very workload (1 Newton iteration)
         threads, cores_note = cpu_threads()

@@ -2117,11 +2117,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
 // state (Galerkin-free, matrix-free), smoothed by damped Jacobi on their own diagonals.
 // --------------------------------------------------------------------------------------------
 namespace {
-enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_BOX, MB_R, MB_E, MB_N };
-int mg_gamma() {  // coarse-grid visits per level (1: V-cycle, 2: W-cycle), GLS_MG_GAMMA
-  static const int g = std::getenv("GLS_MG_GAMMA") ? std::max(1, std::atoi(std::getenv("GLS_MG_GAMMA"))) : 1;
-  return g;
-}
+enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_BOX, MB_N };
 double *mgbuf(gls_ctx *c, int l, int which) { return c->mg.bufs[(size_t)l * MB_N + which]->p; }
 int64_t mg_nbox(const gls_ctx *c, int l) {
   const auto &d = c->mg.dims[(size_t)l];
@@ -2595,16 +2591,6 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   GLS_TRY(mg_restrict(c, l, y, bc));
   HIP_TRY(gls::vec_set_indexed(bc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
   GLS_TRY(mg_vcycle(c, l + 1, bc, xc));
-  // W-cycle (GLS_MG_GAMMA = 2, measurement option): further coarse-grid visits on the coarse residual,
-  // x_c += V(b_c - A_c x_c); the exact coarsest solve needs none
-  if (!(l + 1 == L - 1 && mg.direct_ok) && !mg.boxed && !mg.csr)
-    for (int gm = 1; gm < mg_gamma(); ++gm) {
-      double *rc = mgbuf(c, l + 1, MB_R), *ec = mgbuf(c, l + 1, MB_E);
-      GLS_TRY(smoother_apply(h, xc, rc, bc));  // rc = bc - A_c xc
-      HIP_TRY(gls::vec_set_indexed(rc, h->con_dofs.p, nullptr, (int64_t)h->con_dofs.n, s));
-      GLS_TRY(mg_vcycle(c, l + 1, rc, ec));
-      HIP_TRY(gls::vec_axpy(xc, 1.0, ec, h->n_dofs, s));
-    }
   // prolongate the coarse correction (ghost values imported first). x += P xc in the transfer's
   // store on one rank: the coarse correction vanishes on the coarse Dirichlet rows (zero rhs rows,
   // D_c-scaled sweeps) and the nested Qk interpolation maps them onto the fine Dirichlet rows, so
@@ -3041,9 +3027,7 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
-      const bool need = b == MB_BOX ? (mg.boxed || mg.ilu_smooth)
-                        : (b == MB_R || b == MB_E) ? (l > 0 && mg_gamma() > 1)
-                                                   : (l > 0 || b == MB_Y);
+      const bool need = b == MB_BOX ? (mg.boxed || mg.ilu_smooth) : (l > 0 || b == MB_Y);
       if (need)
         GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX && mg.boxed ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
     }

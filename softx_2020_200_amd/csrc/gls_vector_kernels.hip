@@ -1,4 +1,6 @@
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 // gls_vector_kernels.hip — Krylov vector kernels (HBM-bound; 16-byte accesses where aligned).
 #include "gls_launch.hpp"
 
@@ -151,6 +153,106 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
   }
 }
 
+// 16-byte variants of the Gram-Schmidt passes (one row pair per thread and trip, double2 loads / stores,
+// non-temporal basis loads; single-rank vectors: all rows owned). Default; GLS_VEC16=0 keeps the 8-byte
+// kernels. Orthogonalisation 11.9 -> 11.0 ms per Newton step at configs[2] (4.9 -> 5.3 TB/s,
+// profiles/r05_ab_vec16.txt)
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+template <int NK>
+__global__ void __launch_bounds__(kBlock) k_multidot16(const double *__restrict__ A, int64_t lda,
+                                                       const double *__restrict__ w, int64_t n, double *work) {
+  double acc[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) acc[k] = 0.;
+  const int64_t np = n / 2;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
+    const dbl2 wi = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(w) + p);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const dbl2 a = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(A + k * lda) + p);
+      acc[k] += a.x * wi.x;
+      acc[k] += a.y * wi.y;
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < NK; ++k) acc[k] += A[k * lda + n - 1] * w[n - 1];
+  __shared__ double red[NK][kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const double t = wave_sum(acc[k]);
+    if (lane == 0) red[k][wv] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < NK) {
+    double t = 0.;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; ++j) t += red[threadIdx.x][j];
+    work[threadIdx.x * gridDim.x + blockIdx.x] = t;
+  }
+}
+template <int NK, bool DOTS>
+__global__ void __launch_bounds__(kBlock) k_multiaxpy_dot16(double *__restrict__ w, const double *__restrict__ A,
+                                                            int64_t lda, const double *__restrict__ h, double sign,
+                                                            int64_t n, double scale, double *work) {
+  constexpr int ND = (DOTS ? NK : 0) + 1;
+  double hk[NK], acc[ND];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) hk[k] = sign * h[k];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) acc[d] = 0.;
+  auto row = [&](double wi, const double *a) {
+    double s = wi;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s -= hk[k] * a[k];
+    s *= scale;
+    if constexpr (DOTS) {
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc[k] += a[k] * s;
+    }
+    acc[ND - 1] += s * s;
+    return s;
+  };
+  const int64_t np = n / 2;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
+    double a0[NK], a1[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const dbl2 a = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(A + k * lda) + p);
+      a0[k] = a.x;
+      a1[k] = a.y;
+    }
+    const dbl2 wi = reinterpret_cast<const dbl2 *>(w)[p];
+    const double o0 = row(wi.x, a0), o1 = row(wi.y, a1);
+    reinterpret_cast<dbl2 *>(w)[p] = dbl2{o0, o1};
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    double a[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) a[k] = A[k * lda + n - 1];
+    w[n - 1] = row(w[n - 1], a);
+  }
+  __shared__ double red[ND][kBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const double t = wave_sum(acc[d]);
+    if (lane == 0) red[d][wv] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < ND) {
+    double t = 0.;
+#pragma unroll
+    for (int j = 0; j < kBlock / 64; ++j) t += red[threadIdx.x][j];
+    work[threadIdx.x * gridDim.x + blockIdx.x] = t;
+  }
+}
+bool vec16(const double *A, int64_t lda, const double *w, int64_t n, int64_t n1, int64_t n2) {
+  static const bool on = !(std::getenv("GLS_VEC16") && std::atoi(std::getenv("GLS_VEC16")) == 0);
+  return on && n2 == 0 && n1 == n && (lda % 2) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)w % 16) == 0;
+}
+
 // constraint lines: x[dof[i]] = sum_{j in [off[i], off[i+1])} w[j] * src[master[j]]
 // (masters are never constrained lines themselves, so src may alias x)
 __global__ void k_csr_gather_set(double *x, const double *src, const int64_t *__restrict__ dof,
@@ -301,12 +403,16 @@ hipError_t vec_multidot(const double *A, int64_t lda, int nk, const double *w, i
 hipError_t vec_multidot2(const double *A, int64_t lda, int nk, const double *w, int64_t n1, int64_t off2, int64_t n2,
                          double *out, double *work, hipStream_t s) {
   const int nb = grid_for(n1 + n2);
+  const bool v16 = vec16(A, lda, w, n1 + n2, n1, n2);
   for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
     const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;
     const double *Ak = A + (int64_t)k0 * lda;
     switch (m) {
-#define MD(M) \
-  case M: hipLaunchKernelGGL(k_multidot<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n1, off2, n2, work); break;
+#define MD(M)                                                                                                  \
+  case M:                                                                                                      \
+    if (v16) hipLaunchKernelGGL(k_multidot16<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n1, work);          \
+    else hipLaunchKernelGGL(k_multidot<M>, dim3(nb), dim3(kBlock), 0, s, Ak, lda, w, n1, off2, n2, work);      \
+    break;
       MD(1) MD(2) MD(3) MD(4) MD(5) MD(6) MD(7) MD(8)
 #undef MD
     }
@@ -336,15 +442,22 @@ hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, c
                               hipStream_t s) {
   if (nk < 1 || nk > kDotChunk) return hipErrorInvalidValue;
   const int nb = grid_for(n);
+  const bool v16 = vec16(A, lda, w, n, n1, n2);
   switch (nk * 2 + (dots ? 1 : 0)) {
 #define MX(M)                                                                                                         \
   case 2 * M:                                                                                                         \
-    hipLaunchKernelGGL((k_multiaxpy_dot<M, false>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2, \
-                       scale, work);                                                                                         \
+    if (v16)                                                                                                          \
+      hipLaunchKernelGGL((k_multiaxpy_dot16<M, false>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, scale, work); \
+    else                                                                                                              \
+      hipLaunchKernelGGL((k_multiaxpy_dot<M, false>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2, \
+                         scale, work);                                                                                \
     break;                                                                                                            \
   case 2 * M + 1:                                                                                                     \
-    hipLaunchKernelGGL((k_multiaxpy_dot<M, true>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2,  \
-                       scale, work);                                                                                         \
+    if (v16)                                                                                                          \
+      hipLaunchKernelGGL((k_multiaxpy_dot16<M, true>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, scale, work); \
+    else                                                                                                              \
+      hipLaunchKernelGGL((k_multiaxpy_dot<M, true>), dim3(nb), dim3(kBlock), 0, s, w, A, lda, h, sign, n, n1, off2, n2, \
+                         scale, work);                                                                                \
     break;
     MX(1) MX(2) MX(3) MX(4) MX(5) MX(6) MX(7) MX(8)
 #undef MX

@@ -5,8 +5,9 @@ instructions priced with MI355X_MICROARCH.md §LDS (ds_read_b64 2, ds_read_b128 
 ds_write_b64 ~6, ds_write2_b64 13, ...), the FP64 / FP32 VALU instructions and the VGPR count, and
 writes profiles/<out>.json with the git commit of the source. bench.py reads it for its
 roofline["lds"] block and labels that block a static model (conflict-free, straight-line count).
-Usage: python tools/lds_model.py [out_name]   (default r04_lds_model)"""
+Usage: python tools/lds_model.py [out_name]   (default r05_lds_model)"""
 import collections
+import hashlib
 import json
 import os
 import re
@@ -22,7 +23,7 @@ LDS_CYCLES = {'ds_read_b32': 2, 'ds_read_b64': 2, 'ds_read_b128': 4, 'ds_read_b9
 
 
 def main():
-    out_name = sys.argv[1] if len(sys.argv) > 1 else "r04_lds_model"
+    out_name = sys.argv[1] if len(sys.argv) > 1 else "r05_lds_model"
     asm = "/tmp/gls_brick_pencil_model.s"
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics",
                            "-fno-slp-vectorize", "--cuda-device-only", "-S", SRC, "-o", asm],
@@ -70,6 +71,7 @@ def main():
                     "conflict-free by MI355X_MICROARCH.md §LDS; every wave of the pencil kernel runs the whole "
                     "stream once (no loops except the diagonal's qy loop, x3)",
            "source": os.path.relpath(SRC, ROOT), "commit": commit + ("+dirty" if dirty else ""),
+           "source_sha256": hashlib.sha256(open(SRC, "rb").read()).hexdigest(),
            "cells_per_wave": 6, "kernels": kernels}
     path = os.path.join(ROOT, "profiles", out_name + ".json")
     with open(path, "w") as f:

@@ -19,6 +19,7 @@ import collections
 import csv
 import json
 import math
+import re
 
 FETCH_CORR, WRITE_CORR = 2.0, 1.0
 
@@ -66,12 +67,12 @@ def classify(name, blocks, threads, n_fine):
         return "brick kernel (other)", n, 0
     if "k_slab_sum" in nm:
         return "slab sums", None, 0  # folded into their J.v's algorithmic bytes (the J.v's y write)
-    if "k_multidot<" in nm:
-        M = int(nm.split("k_multidot<")[1].split(">")[0])
-        return "GMRES orthogonalisation", None, (M + 1) * 8 * Nf
-    if "k_multiaxpy_dot<" in nm or "k_multiaxpy<" in nm:
-        M = int(nm.split("k_multiaxpy")[1].split("<")[1].split(",")[0].split(">")[0])
-        return "GMRES orthogonalisation", None, (M + 2) * 8 * Nf
+    m = re.search(r"k_multidot(?:16)?<(\d+)", nm)
+    if m:
+        return "GMRES orthogonalisation", None, (int(m.group(1)) + 1) * 8 * Nf
+    m = re.search(r"k_multiaxpy(?:_dot)?(?:16)?<(\d+)", nm)
+    if m:
+        return "GMRES orthogonalisation", None, (int(m.group(1)) + 2) * 8 * Nf
     if "transfer" in nm or "k_inject" in nm or "box" in nm:
         return "MG transfers", None, None
     if "jacobi" in nm:
