@@ -1545,6 +1545,8 @@ struct Solver {
       mp.coarse_sweeps = 100;
       mp.omega = 0.9;
       mp.coarse_omega = 0.7;
+      mp.mixed_precision = 1;    // FP32 smoothing J.v (the outer GMRES operator stays the FP64 Jacobian)
+      mp.smoother_operator = 1;  // ... with the Oseen (Picard) linearization (bench.py's V-cycle)
       ck(gls_mg_attach(ctx, &mp), "gls_mg_attach");
     }
     (void)N;

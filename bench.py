@@ -586,6 +586,10 @@ def main():
     ap.add_argument("--mg-coarse-omega", type=float, default=0.7, help="0 = --mg-omega")
     ap.add_argument("--mg-coarse-direct", type=int, default=0,
                     help="coarsest level: 0 auto (exact solve on one GPU when <= 2048 DoFs), 1 exact (LU above 2048), -1 Jacobi sweeps")
+    ap.add_argument("--mg-operator", default="oseen", choices=["oseen", "newton"],
+                    help="operator of the V-cycle's FP32 smoothing J.v: the Oseen (Picard) linearization (default; "
+                         "gls_mg_params.smoother_operator = 1) or Newton's Jacobian; the outer GMRES operator is the "
+                         "exact FP64 Jacobian either way")
     ap.add_argument("--mg-precision", default="f32", choices=["f32", "f64"],
                     help="arithmetic of the V-cycle's J.v (f32: FP32 linearization + FP32 sweeps; the outer "
                          "GMRES operator, Newton residual and all vectors stay FP64)")
@@ -679,7 +683,7 @@ def main():
                              pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
                              coarse_sweeps=args.mg_coarse_sweeps, coarse_omega=args.mg_coarse_omega,
                              mixed_precision=args.mg_precision == "f32", coarse_direct=args.mg_coarse_direct,
-                             level_sweeps=lsweeps)
+                             level_sweeps=lsweeps, smoother_operator=int(args.mg_operator == "oseen"))
         ctx = prob.ctx
         mesh = prob.mesh
         N = N_global = ctx.n_dofs
@@ -711,12 +715,14 @@ def main():
                                     pre_smooth=args.mg_coarse_level_sweeps, post_smooth=args.mg_coarse_level_sweeps,
                                     omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
                                     coarse_omega=args.mg_coarse_omega, mixed_precision=args.mg_precision == "f32",
-                                    coarse_direct=args.mg_coarse_direct)
+                                    coarse_direct=args.mg_coarse_direct,
+                                    smoother_operator=int(args.mg_operator == "oseen"))
             attach_distributed_multigrid(lv, replica=rep, pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1],
                                          omega=args.mg_omega, coarse_sweeps=args.mg_coarse_sweeps,
                                          coarse_omega=args.mg_coarse_omega,
                                          mixed_precision=args.mg_precision == "f32",
-                                         coarse_direct=-1 if replica else args.mg_coarse_direct)
+                                         coarse_direct=-1 if replica else args.mg_coarse_direct,
+                                         smoother_operator=int(args.mg_operator == "oseen"))
         N = ctx.n_dofs
         N_global = 3 * mesh["n_vnodes"] + mesh["n_pnodes"]
         m1_h = local_vector(dp.plan, smooth_state(mesh, args.n, 3, ddofs, dvals, 0.0), mesh["n_vnodes"])
@@ -819,7 +825,12 @@ def main():
                                    (1, 64, "steady"): " (BASELINE configs[1])"}.get((args.k, args.n, args.scheme), "")),
                    "n_dofs": N_global, "n_cells": n_cells, "viscosity": args.nu, "dt": args.dt,
                    "linear_solver": "GMRES(%d)+%s, rel %.0e, max %d" % (
-                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s)" % (tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if (-2 in lsweeps or replica) else "%d Jacobi sweeps" % args.mg_coarse_sweeps)) if args.precond == "mg" else "Jacobi",
+                       args.restart, "GMG V(%d,%d)-cycle to %d^3 (%s; %s %s smoothing J.v)" % (
+                           tuple(args.mg_smooth) + (args.mg_coarsest, "exact LU" if (-2 in lsweeps or replica)
+                                                    else "%d Jacobi sweeps" % args.mg_coarse_sweeps,
+                                                    args.mg_precision.upper(),
+                                                    "Oseen" if args.mg_operator == "oseen" else "Newton"))
+                       if args.precond == "mg" else "Jacobi",
                        args.rel, args.lin_max),
                    "parallelism": ("domain decomposition x%d (%s)" % (world, "in-library RCCL P2P ghosts" if args.dist_impl == "native"
                                                                      else "torch.distributed %s ghosts" % args.dist_backend))

@@ -224,6 +224,11 @@ typedef struct {
                                                  uses under the reference's AMG, gls_navier_stokes.cc:
                                                  1208-1226); levels with hanging nodes only
                                                  (gls_mg_attach_transfers) */
+  int smoother_operator;                      /* 0: the levels' Newton Jacobian; 1: its Oseen (Picard)
+                                                 linearization on the FP32 brick levels (no (grad u) v
+                                                 terms, no SUPG tau (v . grad phi) R_s term): cheaper
+                                                 smoothing J.v; the outer GMRES operator is the exact
+                                                 Jacobian either way */
 } gls_mg_params;
 int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
 /* The same V-cycle on a general level hierarchy with the caller's grid transfers: levels of an adaptive
@@ -240,6 +245,9 @@ int gls_mg_attach_transfers(gls_ctx *ctx, const gls_mg_params *prm, const int64_
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
  * attached, else Jacobi): the reference's preconditioner vmult (DEVICE pointers, no aliasing). */
 int gls_apply_preconditioner(gls_ctx *ctx, const double *v, double *z);
+/* y = A_s v: the operator the attached V-cycle smooths this level with (the Jacobian, in FP32 with
+ * gls_mg_params.mixed_precision, its Oseen part with smoother_operator = 1); DEVICE pointers. */
+int gls_mg_smoother_apply(gls_ctx *ctx, const double *v, double *y);
 /* Multigrid grid transfer between levels `level` and `level`+1 of the attached hierarchy (DEVICE
  * pointers): direction 0 restricts a level-`level` vector into level `level`+1 (transpose of the
  * Qk interpolation, the reference's MGTransfer restrict_and_add into a zeroed vector), direction 1

@@ -297,12 +297,14 @@ struct gls_ctx {
   bool qd_valid = false;  // invalidated with the diagonal by every state / parameter change
   DevBuf<float> qdata32;  // FP32 copy of qdata: the multigrid smoother's J.v (mixed precision)
   bool qd32_valid = false;  // stale whenever qdata is recomputed
+  bool qd32_partial = false;  // the FP32 copy holds only u and tau (written for the Oseen smoother operator)
   // per-cell path: element vectors and each node's slots in them (deterministic scatter)
   DevBuf<double> ev;
   DevBuf<double> bev;  // batched ILU probing: element vectors of a batch of probe vectors
   DevBuf<uint8_t> bact;  // ... and which (probe, cell batch) blocks computed them
   DevBuf<int64_t> ev_voff, ev_vslot, ev_poff, ev_pslot;
   bool smooth_f32 = false;  // this level's V-cycle J.v runs in FP32 (gls_mg_params.mixed_precision)
+  bool smooth_oseen = false;  // ... with the Oseen (Picard) operator (gls_mg_params.smoother_operator = 1)
   bool use_qdata = true;  // GLS_JV_RECOMPUTE=1 -> J.v recomputes the state per call (MODE_JV)
   // solver workspace
   DevBuf<double> work, scal, coef;  // multidot partials, device dot results, GMRES coefficients
@@ -1012,6 +1014,7 @@ int lin_f32_target(gls_ctx *c, gls::OpParams &P) {
   if (!c->smooth_f32 || !gls::brick_fused_jacobi_supported(c->k) || std::getenv("GLS_LIN_NO_F32")) return GLS_OK;
   if (c->qdata32.n != c->qdata.n) GLS_TRY(c->qdata32.alloc(c->qdata.n));
   P.qdf = c->qdata32.p;
+  P.oseen = c->smooth_oseen ? 1 : 0;  // the Oseen smoother reads u and tau only: the other FP32 rows are not written
   return GLS_OK;
 }
 
@@ -1029,6 +1032,7 @@ int ensure_qdata(gls_ctx *c) {
   }
   c->qd_valid = true;
   c->qd32_valid = P.qdf != nullptr;
+  c->qd32_partial = P.qdf != nullptr && P.oseen;
   return GLS_OK;
 }
 
@@ -1259,6 +1263,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (lin_diag) {  // the same launch stored the J.v linearization
     c->qd_valid = true;
     c->qd32_valid = P.qdf != nullptr;
+    c->qd32_partial = P.qdf != nullptr && P.oseen;
   }
   return GLS_OK;
 }
@@ -1763,6 +1768,7 @@ int gls_residual_and_diagonal(gls_ctx *c, double *rhs, double *d) {
     HIP_TRY(gls::vec_set_indexed(rhs, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, c->stream));
     c->qd_valid = true;
     c->qd32_valid = P.qdf != nullptr;
+  c->qd32_partial = P.qdf != nullptr && P.oseen;
     c->diag_valid = true;
   } else {
     GLS_TRY(gls_residual(c, rhs));
@@ -1792,12 +1798,14 @@ namespace {
 // the V-cycle's operator on level g: J.v in FP32 arithmetic from the FP32 linearization when the
 // level smooths in mixed precision (brick path), else the FP64 gls_jacobian_apply. Same
 // constraint handling (constrained rows D_c v) and ghost exchange as gls_jacobian_apply.
-int ensure_qdata32(gls_ctx *g) {
+// full = false: u and tau suffice (the Oseen smoother operator); else every row of the FP32 copy
+int ensure_qdata32(gls_ctx *g, bool full = true) {
   GLS_TRY(ensure_qdata(g));
-  if (!g->qd32_valid) {
+  if (!g->qd32_valid || (full && g->qd32_partial)) {
     if (g->qdata32.n != g->qdata.n) GLS_TRY(g->qdata32.alloc(g->qdata.n));
     HIP_TRY(gls::vec_to_f32(g->qdata.p, g->qdata32.p, (int64_t)g->qdata.n, g->stream));
     g->qd32_valid = true;
+    g->qd32_partial = false;
   }
   return GLS_OK;
 }
@@ -1816,13 +1824,15 @@ bool first_sweep_fusable(gls_ctx *g) {
          !g->hang.on && g->k == 2 && g->cube_nb1 > 0 && g->use_slab && gls::pencil_enabled() &&
          std::getenv("GLS_MG_NO_FUSE") == nullptr;
 }
-int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr, double first_omega = 0.0) {
+int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb = nullptr, double first_omega = 0.0,
+                       bool oseen = false) {
   if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   GLS_TRY(ensure_diag(g));
-  GLS_TRY(ensure_qdata32(g));
+  GLS_TRY(ensure_qdata32(g, !oseen));
   GLS_TRY(dist_import(g, const_cast<double *>(v)));
   gls::OpParams P = make_params(g, true);
   P.qdf = g->qdata32.p;
+  P.oseen = oseen ? 1 : 0;
   P.v = v;
   P.y = y;
   const bool col = g->use_colors;
@@ -1855,7 +1865,7 @@ int jacobian_apply_f32(gls_ctx *g, const double *v, double *y, const double *rb 
 }
 // y = A v with the level's smoothing operator; rb != nullptr: y = rb - A v
 int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nullptr) {
-  if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y, rb);
+  if (g->smooth_f32 && g->use_brick && g->use_qdata) return jacobian_apply_f32(g, v, y, rb, 0.0, g->smooth_oseen);
   g->oct.f32_next = g->smooth_f32 && g->oct.on;  // adapted forest: its bricks in FP32, the other cells FP64
   const int rc = gls_jacobian_apply(g, v, y);
   g->oct.f32_next = false;
@@ -1892,7 +1902,7 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   if (!g->u) return set_err(GLS_EINVAL, "gls_set_state was not called");
   GLS_TRY(ensure_diag(g));
   const bool f32 = g->smooth_f32;
-  GLS_TRY(f32 ? ensure_qdata32(g) : ensure_qdata(g));
+  GLS_TRY(f32 ? ensure_qdata32(g, !g->smooth_oseen) : ensure_qdata(g));
   gls::OpParams P = make_params(g, true);
   P.v = x;
   P.y = x;
@@ -1908,6 +1918,7 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   }
   if (f32) {
     P.qdf = g->qdata32.p;
+    P.oseen = g->smooth_oseen ? 1 : 0;
     P.slabf = P.slab && slab_f32() ? reinterpret_cast<float *>(P.slab) : nullptr;
     TimedLaunch t(g, 4);
     HIP_TRY(gls::launch_brick_jv_f32(g->k, P, g->tables, g->stream));
@@ -1922,6 +1933,13 @@ int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double ome
   return GLS_OK;
 }
 }  // namespace
+
+// y = A_s v with the operator the attached V-cycle smooths this level with (FP32 / Oseen per gls_mg_params)
+int gls_mg_smoother_apply(gls_ctx *c, const double *v, double *y) {
+  GLS_TRY(check_ctx(c));
+  if (!v || !y || v == y) return set_err(GLS_EINVAL, "v/y null or aliased");
+  return smoother_apply(c, v, y);
+}
 
 int gls_jacobian_apply_f32(gls_ctx *c, const double *v, double *y) {
   GLS_TRY(check_ctx(c));
@@ -2467,7 +2485,7 @@ int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, dou
   auto &mg = c->mg;
   hipStream_t s = c->stream;
   GLS_TRY(ensure_diag(g));
-  GLS_TRY(g->smooth_f32 ? ensure_qdata32(g) : ensure_qdata(g));
+  GLS_TRY(g->smooth_f32 ? ensure_qdata32(g, !g->smooth_oseen) : ensure_qdata(g));
   if (g->use_colors && g->acc.n != (size_t)g->n_dofs) GLS_TRY(g->acc.alloc((size_t)g->n_dofs));  // no malloc in capture
   const bool tim = g->timing;
   g->timing = false;  // no event records inside the capture
@@ -2556,7 +2574,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   const double om = l == L - 1 ? mg.comega : mg.omega;
   if (l == L - 1 && l > 0 && pre > 1 && coarse_graph_eligible(c, g, b, x)) {
     GLS_TRY(ensure_diag(g));  // contents the replay reads: current for this state
-    GLS_TRY(g->smooth_f32 ? ensure_qdata32(g) : ensure_qdata(g));
+    GLS_TRY(g->smooth_f32 ? ensure_qdata32(g, !g->smooth_oseen) : ensure_qdata(g));
     if (mg.cgraph.h && mg.cgraph_key != coarse_graph_key(g, b, x, y, pre, om)) mg.cgraph.reset();
     if (!mg.cgraph.h) GLS_TRY(coarse_graph_capture(c, g, b, x, y, pre, om));
     if (mg.cgraph.h) {
@@ -2580,7 +2598,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   if (l == L - 1) return GLS_OK;
   // residual -> coarse right-hand side: restrict the owned rows, export-add coarse ghost rows
   if (first_fused) {
-    GLS_TRY(jacobian_apply_f32(g, x, y, b, om));  // x = omega D^-1 b, y = b - A x
+    GLS_TRY(jacobian_apply_f32(g, x, y, b, om, g->smooth_oseen));  // x = omega D^-1 b, y = b - A x
   } else if (pre > 0) {
     GLS_TRY(smoother_apply(g, x, y, b));  // y = b - A x
   } else {
@@ -3021,6 +3039,14 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       mg.lpost[(size_t)l] = p->level_sweeps[2 * l + 1];
     }
   for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
+  // the smoother's operator: Newton's Jacobian, or its Oseen (Picard) part (FP32 brick levels only: the
+  // pencil J.v drops the (grad u) v terms; GLS_MG_OSEEN=0/1 overrides for A/B)
+  {
+    const char *e = std::getenv("GLS_MG_OSEEN");
+    const bool os = e ? std::atoi(e) != 0 : p->smoother_operator == 1;
+    if (p->smoother_operator < 0 || p->smoother_operator > 1) return set_err(GLS_EINVAL, "mg: smoother_operator 0 or 1");
+    for (auto *g : mg.lev) g->smooth_oseen = os && g->smooth_f32;
+  }
   mg.ilu_smooth = p->smoother == 1;
   if (p->smoother < 0 || p->smoother > 1 || (mg.ilu_smooth && !mg.csr))
     return set_err(GLS_EINVAL, "mg: smoother 0 (Jacobi) or 1 (ILU, gls_mg_attach_transfers hierarchies)");
@@ -3253,7 +3279,7 @@ int gls_mg_set_coarse_replica(gls_ctx *c, gls_ctx *replica, int64_t n_local, con
 
 int gls_mg_detach(gls_ctx *c) {
   GLS_TRY(check_ctx(c));
-  for (auto *g : c->mg.lev) g->smooth_f32 = false;
+  for (auto *g : c->mg.lev) g->smooth_f32 = g->smooth_oseen = false;
   // the ILU(0) smoothers the attach put on the levels (level 0 is this context) go with the multigrid, so
   // the preconditioner falls back to Jacobi (gls_native.h) and not to a leftover smoother ILU
   for (auto *g : c->mg.ilu_levels) GLS_TRY(gls_ilu_detach(g));

@@ -92,9 +92,12 @@ struct PencilTab {
 
 // GEN: the forcing term and the SRF source are compiled in (an instantiation without them is the hot
 // path: their per-point loads and terms cost the residual ~50 VGPRs of spills)
-template <typename Real, int MODE, bool GEN, bool FOREST = false>  // FOREST: an FP32 launch on forest bricks (subset list)
+// FOREST: an FP32 launch on forest bricks (subset list); OS: the Oseen (Picard) operator of the FP32 smoother
+// (MODE_JVQ: no (grad u) v terms, no tau (v . grad phi) R_s term; reads u and tau of the linearization only)
+template <typename Real, int MODE, bool GEN, bool FOREST = false, bool OS = false>
 __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_PENCIL_WPE32 : GLS_PENCIL_WPE64))
     gls_pencil_kernel(const OpParams P, const PencilTab<Real> T) {
+  static_assert(!OS || (MODE == MODE_JVQ && std::is_same<Real, float>::value), "Oseen operator: FP32 J.v only");
   using C = PencilCfg<Real, MODE == MODE_JVQ>;
   // MODE_RESLIN = MODE_RESIDUAL + MODE_LIN at one state (assemble_matrix_and_rhs); else MODE_JVQ
   constexpr bool RL = MODE == MODE_RESLIN, RES = MODE == MODE_RESIDUAL || RL, LIN = MODE == MODE_LIN || RL;
@@ -441,10 +444,11 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     // MODE_LIN: the lane's linearization rows (pencil layout, qdp_base), FP64 and the FP32 copy
     double *const lrow = LIN && P.qd ? P.qd + qdp_base(brick, valid ? ci : 0, pa + 3 * pb) : nullptr;
     float *const lrowf = LIN && P.qdf ? P.qdf + qdp_base(brick, valid ? ci : 0, pa + 3 * pb) : nullptr;
+    const bool f32_all = !P.oseen;  // the Oseen smoother reads only u (0..2) and tau (12) of the FP32 copy
     auto st_lin = [&](int qz, int v, Real x) {
       if (!valid) return;
       if (lrow) lrow[(qz * kQData + v) * kQdpRow] = (double)x;
-      if (lrowf) __builtin_nontemporal_store((float)x, lrowf + (qz * kQData + v) * kQdpRow);
+      if (lrowf && (f32_all || v < 3 || v == 12)) __builtin_nontemporal_store((float)x, lrowf + (qz * kQData + v) * kQdpRow);
     };
     if constexpr (LIN) {
 #pragma unroll
@@ -640,11 +644,13 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
     tauq[qz] = ld(qz, 12);
   }
   auto ld_comp = [&](int cc) {
+    if constexpr (!OS) {
 #pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
+      for (int qz = 0; qz < 3; ++qz) {
 #pragma unroll
-      for (int e = 0; e < 3; ++e) lnx[qz][e] = ld(qz, 3 + 3 * cc + e);
-      lnx[qz][3] = ld(qz, 13 + cc);
+        for (int e = 0; e < 3; ++e) lnx[qz][e] = ld(qz, 3 + 3 * cc + e);
+        lnx[qz][3] = ld(qz, 13 + cc);
+      }
     }
   };
   constexpr bool PIPE = (GLS_PENCIL_PIPE & (std::is_same<Real, double>::value ? 1 : 2)) != 0;
@@ -684,8 +690,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
 #pragma unroll
       for (int qz = 0; qz < 3; ++qz) {
 #pragma unroll
-        for (int e = 0; e < 3; ++e) gu[e][qz] = lnx[qz][e];
-        Rq[qz] = lnx[qz][3];
+        for (int e = 0; e < 3; ++e) gu[e][qz] = OS ? Real(0) : lnx[qz][e];
+        Rq[qz] = OS ? Real(0) : lnx[qz][3];
       }
       if (PIPE && cc < 2) ld_comp(cc + 1);
       forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
@@ -697,10 +703,10 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       const Real lv = zval(Yc[3], qz) + wzz * zsec(Yc[0], qz);
       const Real v0 = vq[0][qz], v1 = vq[1][qz], v2 = vq[2][qz];
       const Real u0 = uq[0][qz], u1 = uq[1][qz], u2 = uq[2][qz];
-      const Real guv = gu[0][qz] * v0 + gu[1][qz] * v1 + gu[2][qz] * v2;
+      const Real guv = OS ? Real(0) : gu[0][qz] * v0 + gu[1][qz] * v1 + gu[2][qz] * v2;
       const Real gvu = gv0 * u0 + gv1 * u1 + gv2 * u2;
-      Real A = guv + gvu + aj * vq[cc][qz];
-      Real S = guv + gvu + gvp[cc][qz] - nu * lv + aj * vq[cc][qz];
+      Real A = OS ? gvu + aj * vq[cc][qz] : guv + gvu + aj * vq[cc][qz];
+      Real S = OS ? gvu + gvp[cc][qz] - nu * lv + aj * vq[cc][qz] : guv + gvu + gvp[cc][qz] - nu * lv + aj * vq[cc][qz];
       if (GEN && P.srf) {
         const Real cj = cc == 0 ? 2 * (om[1] * v2 - om[2] * v1) : cc == 1 ? 2 * (om[2] * v0 - om[0] * v2)
                                                                          : 2 * (om[0] * v1 - om[1] * v0);
@@ -714,7 +720,8 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
       Real Te[3];
 #pragma unroll
       for (int e = 0; e < 3; ++e)
-        Te[e] = JxW * (nu * gv[e] - (cc == e ? vpq[qz] : Real(0)) + tau * S * uu[e] + tau * Rq[qz] * vv[e]) * ihv[e];
+        Te[e] = OS ? JxW * (nu * gv[e] - (cc == e ? vpq[qz] : Real(0)) + tau * S * uu[e]) * ihv[e]
+                   : JxW * (nu * gv[e] - (cc == e ? vpq[qz] : Real(0)) + tau * S * uu[e] + tau * Rq[qz] * vv[e]) * ihv[e];
       const Real Tv = JxW * A;
 #pragma unroll
       for (int az = 0; az < 3; ++az) {
@@ -1216,6 +1223,17 @@ hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) 
     }
     tab.xi[q] = (Real)T.xi[q];
   }
+  if constexpr (std::is_same<Real, float>::value && MODE == MODE_JVQ && !FB) {
+    if (P.oseen) {  // the multigrid smoother's Oseen operator
+      if (gen)
+        hipLaunchKernelGGL((gls_pencil_kernel<float, MODE_JVQ, true, false, true>), dim3((unsigned)n_groups), dim3(256),
+                           pencil_lds_bytes<float>(MODE), s, P, tab);
+      else
+        hipLaunchKernelGGL((gls_pencil_kernel<float, MODE_JVQ, false, false, true>), dim3((unsigned)n_groups),
+                           dim3(256), pencil_lds_bytes<float>(MODE), s, P, tab);
+      return hipGetLastError();
+    }
+  }
   if (gen)
     hipLaunchKernelGGL((gls_pencil_kernel<Real, MODE, true, FB>), dim3((unsigned)n_groups), dim3(256),
                        pencil_lds_bytes<Real>(MODE), s, P, tab);
@@ -1227,7 +1245,7 @@ hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) 
 hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32) {
   if (P.n_probe > 0 || P.bricks || !(f32 ? (P.slabf != nullptr || P.slab != nullptr) : P.slab != nullptr))
     return hipErrorNotSupported;
-  if (f32 && pencil_pair_enabled()) return launch_pencil_pair<false>(P, T, s);
+  if (f32 && pencil_pair_enabled() && !P.oseen) return launch_pencil_pair<false>(P, T, s);
   return f32 ? launch_pencil_t<float, MODE_JVQ>(P, T, s) : launch_pencil_t<double, MODE_JVQ>(P, T, s);
 }
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s) {

@@ -105,6 +105,10 @@ struct OpParams {
   double sdt2;                // (1/dt)^2 for transient tau, 0 when steady
   int srf;
   double omega[3];
+  // FP32 smoother J.v on the cube's bricks: the Oseen (Picard) linearization instead of Newton's, i.e. without
+  // the (grad u) v terms and the SUPG term tau (v . grad phi) R_s (the multigrid smoother's operator,
+  // gls_mg_params.smoother_operator = 1); the outer GMRES operator is never affected
+  int oseen;
 };
 
 }  // namespace gls

@@ -29,7 +29,7 @@ EXPORTS = [
     "gls_jacobian_diagonal", "gls_set_dirichlet", "gls_apply_dirichlet", "gls_solve_linear", "gls_newton_solve",
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
-    "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy", "gls_rccl_info",
+    "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy", "gls_rccl_info", "gls_mg_smoother_apply",
     "gls_dist_attach_rccl",
     "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_residual_and_diagonal", "gls_octree_set_periodic", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
@@ -95,7 +95,7 @@ class MGParams(C.Structure):
     _fields_ = [("n_levels", C.c_int), ("levels", C.POINTER(C.c_void_p)), ("pre_smooth", C.c_int),
                 ("post_smooth", C.c_int), ("coarse_sweeps", C.c_int), ("omega", C.c_double),
                 ("coarse_omega", C.c_double), ("coarse_direct", C.c_int), ("mixed_precision", C.c_int),
-                ("level_sweeps", C.POINTER(C.c_int)), ("smoother", C.c_int)]
+                ("level_sweeps", C.POINTER(C.c_int)), ("smoother", C.c_int), ("smoother_operator", C.c_int)]
 
 
 class RefinedMesh(C.Structure):
@@ -177,6 +177,7 @@ def load():
     L.gls_octree_mg_transfer.argtypes = [C.POINTER(RefinedMesh), C.POINTER(RefinedMesh), C.POINTER(i64), vp, vp, vp, vp]
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
+    L.gls_mg_smoother_apply.argtypes = [vp, vp, vp]
     L.gls_mg_transfer.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     P64 = C.POINTER(i64)
     L.gls_set_hanging.argtypes = [vp, i64, P64, P64, P64, d]
@@ -739,11 +740,12 @@ class GLSContext:
         check(self.L.gls_freeze_jacobian(self.h, 1 if freeze else 0), "gls_freeze_jacobian")
 
     def attach_multigrid(self, coarse_levels, pre_smooth=2, post_smooth=2, coarse_sweeps=30, omega=0.6,
-                         coarse_omega=0.0, coarse_direct=0, mixed_precision=0, level_sweeps=None):
+                         coarse_omega=0.0, coarse_direct=0, mixed_precision=0, level_sweeps=None, smoother_operator=0):
         """GMRES right preconditioner = geometric multigrid V-cycle over [self] + coarse_levels
         (GLSContext objects of the same problem on hyper_cube(n/2^l)). Keeps references alive.
         level_sweeps: optional {level: (pre, post)} overriding pre_smooth / post_smooth per level
-        (negative level indices count from the coarsest)."""
+        (negative level indices count from the coarsest). smoother_operator=1: the FP32 smoothing J.v
+        applies the Oseen (Picard) linearization (gls_mg_params.smoother_operator)."""
         levels = [self] + list(coarse_levels)
         arr = (C.c_void_p * len(levels))(*[lv.h for lv in levels])
         ls = None
@@ -755,7 +757,7 @@ class GLSContext:
                 flat[2 * (lv % len(levels))], flat[2 * (lv % len(levels)) + 1] = a, b
             ls = (C.c_int * len(flat))(*flat)
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct, int(mixed_precision), ls)
+                     coarse_omega, coarse_direct, int(mixed_precision), ls, 0, int(smoother_operator))
         check(self.L.gls_mg_attach(self.h, C.byref(p)), "gls_mg_attach")
         self._mg_levels = levels
 
@@ -798,6 +800,12 @@ class GLSContext:
         check(self.L.gls_mg_set_coarse_replica(self.h, replica.h, len(m), m.ctypes.data_as(C.POINTER(C.c_int64))),
               "gls_mg_set_coarse_replica")
         self._coarse_replica = replica
+
+    def mg_smoother_apply(self, v, out=None):
+        """y = A_s v with the operator the attached V-cycle smooths this level with (gls_mg_smoother_apply)."""
+        out = self.zeros() if out is None else out
+        check(self.L.gls_mg_smoother_apply(self.h, _ptr(v), _ptr(out)), "gls_mg_smoother_apply")
+        return out
 
     def apply_preconditioner(self, v, out=None):
         out = self.zeros() if out is None else out

@@ -143,6 +143,58 @@ def test_multigrid_mixed_precision():
     assert np.abs(out[1][0][:nv] - out[0][0][:nv]).max() < 1e-7
 
 
+@pytest.mark.gpu
+def test_multigrid_oseen_smoother_operator():
+    """The V-cycle's FP32 smoothing J.v with the Oseen (Picard) linearization (gls_mg_params.smoother_operator =
+    1: no (grad u) v terms, no SUPG tau (v . grad phi) R_s term). (a) The operator: at a state with grad u = 0 and
+    R_s = 0 (constant velocity, constant pressure, steady, no force) it is the FP32 Newton operator to FP32
+    rounding; at the bench's state it differs by far more (the dropped terms act). (b) The outer FP64 GMRES /
+    Newton is untouched: the same converged solution as with the Newton smoothing operator, GMRES iterations
+    within one per Newton iteration."""
+    import torch
+    import bench
+    from softx_2020_200_amd.problem import CavityProblem
+    n = 16
+    probs = {}
+    for so in (0, 1):
+        probs[so] = CavityProblem(dim=3, n=n, k=2, viscosity=0.01, multigrid=True, pre_smooth=1, post_smooth=1,
+                                  omega=0.9, coarse_sweeps=100, coarse_omega=0.7, mixed_precision=1,
+                                  smoother_operator=so)
+    mesh = probs[0].mesh
+    nv = mesh["n_vnodes"]
+    v = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, probs[0].ctx.n_dofs)).cuda()
+    const = np.zeros(probs[0].ctx.n_dofs)
+    const[:3 * nv] = np.tile([0.3, -0.2, 0.1], nv)
+    const[3 * nv:] = 0.7
+    smooth = bench.smooth_state(mesh, n, 3, probs[0].dir_dofs, probs[0].dir_vals, 0.0)
+    res = {}
+    for tag, state, scheme in (("const", const, "steady"), ("bench", smooth, "bdf2")):
+        ys = []
+        for so in (0, 1):
+            ctx = probs[so].ctx
+            ctx.set_time(scheme, (0.01,) * 4)
+            u = torch.from_numpy(state).cuda()
+            ctx.set_state(u, u, u)
+            ys.append(ctx.mg_smoother_apply(v).cpu().numpy())
+        res[tag] = np.abs(ys[1] - ys[0]).max() / np.abs(ys[0]).max()
+    print("Oseen vs Newton smoothing operator: constant state %.2e, bench state %.2e" % (res["const"], res["bench"]))
+    assert res["const"] < 2e-6 and res["bench"] > 1e-4, res
+    out = {}
+    for so in (0, 1):
+        ctx = probs[so].ctx
+        ctx.set_time("bdf2", (0.01,) * 4)
+        m1 = torch.from_numpy(smooth).cuda()
+        m2 = torch.from_numpy(bench.smooth_state(mesh, n, 3, probs[so].dir_dofs, probs[so].dir_vals, 0.3)).cuda()
+        x = m1.clone()
+        st = ctx.newton(x, m1, m2, tolerance=1e-9, max_iterations=8, lin_max_iterations=500, restart=60,
+                        relative_residual=1e-6, minimum_residual=1e-14)
+        out[so] = (x.cpu().numpy(), st)
+    assert out[1][1]["final_residual"] < 1e-9, out[1][1]
+    assert out[1][1]["linear_iterations"] <= out[0][1]["linear_iterations"] + out[0][1]["newton_iterations"], (
+        out[0][1], out[1][1])
+    assert np.abs(out[1][0][:3 * nv] - out[0][0][:3 * nv]).max() < 1e-7
+
+
 def _interp_1d(nf, nc, k):
     """Qk interpolation on nested equidistant node lattices (numpy, independent of the C++ tap
     tables): fine lattice node i sits at x = i / (2k) coarse cells."""
