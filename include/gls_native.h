@@ -242,6 +242,18 @@ int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
  * (copied). */
 int gls_mg_attach_transfers(gls_ctx *ctx, const gls_mg_params *prm, const int64_t *const *p_off,
                             const int32_t *const *p_col, const double *const *p_w, const int64_t *const *inject);
+/* The refinement-hierarchy V-cycle ACROSS RANKS on general meshes (the reference's AMG is global,
+ * gls_navier_stokes.cc:1180-1240): ctx is the rank-local fine context (distributed with
+ * gls_dist_attach_dofs[_rccl]); every coarser level runs as a REPLICA on every rank: `replica` is a
+ * single-rank context of the level-1 mesh (the whole of it) with its own hierarchy attached (e.g.
+ * gls_mg_attach_transfers), so the N-rank V-cycle is the one-rank V-cycle up to the fine level's smoother.
+ * p_off (n_local + 1) / p_col / p_w: the prolongation from level 1 (replica DoFs) onto the rank's local fine
+ * DoFs, owned and ghost rows; inject (replica n_dofs): the local fine DoF whose value the replica's state
+ * takes, on the one rank that owns it (-1 elsewhere). The restriction sums P^T over each rank's owned rows
+ * and all-reduces in the replica numbering. prm: pre / post smooth, omega, smoother (0 damped Jacobi, 1
+ * ILU(0) per rank = Ifpack additive Schwarz, overlap 0); levels / coarse entries are not used. Host arrays. */
+int gls_mg_attach_replica(gls_ctx *ctx, const gls_mg_params *prm, gls_ctx *replica, const int64_t *p_off,
+                          const int32_t *p_col, const double *p_w, const int64_t *inject);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when
  * attached, else Jacobi): the reference's preconditioner vmult (DEVICE pointers, no aliasing). */
 int gls_apply_preconditioner(gls_ctx *ctx, const double *v, double *z);

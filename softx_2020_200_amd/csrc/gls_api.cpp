@@ -540,6 +540,16 @@ struct gls_ctx {
     // by a replica -- a single-rank context of that level's whole mesh with its own hierarchy below
     // it -- identically on every rank, from the all-reduced (gathered) right-hand side
     gls_ctx *replica = nullptr;
+    // general hierarchies across ranks (gls_mg_attach_replica): the distributed fine level smooths its own
+    // rows, every coarser level is a replica on every rank (rep2, with its own hierarchy); restriction over the
+    // rank's OWNED fine rows into the replica numbering + a sum all-reduce, prolongation onto all local rows
+    bool rep_csr = false;
+    gls_ctx *rep2 = nullptr;
+    DevBuf<int64_t> r2p_off, r2r_off;  // P (local fine rows x replica DoFs), R = P_owned^T (replica rows)
+    DevBuf<int32_t> r2p_col, r2r_col;
+    DevBuf<double> r2p_w, r2r_w;
+    int r2p_lane = 1, r2r_lane = 1;
+    DevBuf<int32_t> r2inj_c, r2inj_f;  // replica DoF <- owned local fine DoF (state injection pairs)
     DevBuf<int32_t> rep_own_loc, rep_own_glob;  // owned local rows of the coarsest level -> replica rows
     DevBuf<int32_t> rep_map;                    // every local row -> replica row
     DevBuf<double> rep_b, rep_x, rep_tmp, rep_u[4];
@@ -1457,6 +1467,7 @@ int gls_set_stream(gls_ctx *c, void *s) {
     for (size_t l = 1; l < c->mg.lev.size(); ++l) GLS_TRY(gls_set_stream(c->mg.lev[l], s));
     // the replica's V-cycle is ordered with replica_gather / vec_pack_dofs on this stream
     if (c->mg.replica) GLS_TRY(gls_set_stream(c->mg.replica, s));
+    if (c->mg.rep2) GLS_TRY(gls_set_stream(c->mg.rep2, s));
   }
   return GLS_OK;
 }
@@ -2179,6 +2190,7 @@ int mg_inject_level(gls_ctx *c, int l, const double *fine, double *coarse) {
 }
 
 int replica_gather(gls_ctx *c, const double *loc, double *glob);
+int rep2_inject(gls_ctx *c, const double *loc, double *glob);
 // The explicit coarse inverse (mg.probe) against the pinned matrix it came from (mg.probe_bak): y = A^-1 e,
 // z = A y for e = (1, ..., 1); good = y finite and max|z - e| <= 1e-8 max(1, max|A| max|y|) (a backward-stable
 // factorization leaves ~n eps there; an unpivoted LU through a tiny pivot leaves O(1) or non-finite values)
@@ -2255,6 +2267,19 @@ int mg_prepare(gls_ctx *c) {
     GLS_TRY(gls_set_time(g, jscheme, jts));
     GLS_TRY(gls_set_state(g, mgbuf(c, l, MB_U), gh[0], gh[1], gh[2]));
     GLS_TRY(ensure_diag(g));
+  }
+  if (mg.rep_csr) {  // the replica hierarchy takes the fine state (injected, summed over ranks) and time data
+    gls_ctx *r = mg.rep2;
+    const double *st[4] = {ju, jh[0], jh[1], jh[2]};
+    for (int i = 0; i < 4; ++i)
+      if (st[i]) GLS_TRY(rep2_inject(c, st[i], mg.rep_u[i].p));
+    GLS_TRY(gls_apply_dirichlet(r, mg.rep_u[0].p));
+    r->viscosity = c->viscosity;
+    GLS_TRY(gls_set_time(r, jscheme, jts));
+    GLS_TRY(gls_set_state(r, mg.rep_u[0].p, st[1] ? mg.rep_u[1].p : nullptr, st[2] ? mg.rep_u[2].p : nullptr,
+                          st[3] ? mg.rep_u[3].p : nullptr));
+    mg.dirty = false;
+    return GLS_OK;
   }
   if (mg.replica) {  // the replica takes the coarsest distributed level's state (gathered) and time data
     gls_ctx *g = mg.lev[(size_t)L - 1], *r = mg.replica;
@@ -2512,6 +2537,70 @@ int coarse_graph_capture(gls_ctx *c, gls_ctx *g, const double *b, double *x, dou
   }
   mg.cgraph.h = ex;
   mg.cgraph_key = coarse_graph_key(g, b, x, y, pre, om);
+  return GLS_OK;
+}
+
+// in-place sum over ranks of a device vector through c's transport (RCCL: one call; callback transports
+// through their reduction buffer in chunks of GLS_RED_BUF_MIN values)
+int dist_allreduce_vector(gls_ctx *c, double *v, int64_t n) {
+  auto &D = c->dist;
+  if (!D.on) return GLS_OK;
+  if (D.comm) {
+    if (D.allreduce(D.user, v, (int)n) != 0) return set_err(GLS_ECOMM, "vector all-reduce failed");
+    return GLS_OK;
+  }
+  hipStream_t s = c->stream;
+  for (int64_t o = 0; o < n; o += GLS_RED_BUF_MIN) {
+    const int len = (int)std::min<int64_t>(GLS_RED_BUF_MIN, n - o);
+    HIP_TRY(hipMemcpyAsync(D.red_buf, v + o, sizeof(double) * len, hipMemcpyDeviceToDevice, s));
+    if (D.allreduce(D.user, D.red_buf, len) != 0) return set_err(GLS_ECOMM, "vector all-reduce failed");
+    HIP_TRY(hipMemcpyAsync(v + o, D.red_buf, sizeof(double) * len, hipMemcpyDeviceToDevice, s));
+  }
+  return GLS_OK;
+}
+// the replica's copy of a fine-level state vector: each replica DoF takes its injection source's value on
+// the one rank that owns that fine DoF (0 elsewhere), then the sum over ranks
+int rep2_inject(gls_ctx *c, const double *loc, double *glob) {
+  auto &mg = c->mg;
+  const int64_t ng = mg.rep2->n_dofs, ni = (int64_t)mg.r2inj_c.n;
+  HIP_TRY(gls::vec_fill(glob, ng, 0.0, c->stream));
+  if (ni) {
+    HIP_TRY(gls::vec_pack_dofs(loc, mg.r2inj_f.p, ni, mg.rep_tmp.p, c->stream));
+    HIP_TRY(gls::vec_unpack_dofs(glob, mg.r2inj_c.p, ni, mg.rep_tmp.p, c->stream));
+  }
+  return dist_allreduce_vector(c, glob, ng);
+}
+// one V-cycle with the replica hierarchy below the distributed fine level (gls_mg_attach_replica)
+int mg_vcycle_rep2(gls_ctx *c, const double *b, double *x) {
+  auto &mg = c->mg;
+  gls_ctx *r = mg.rep2;
+  const int64_t n = c->n_dofs, ng = r->n_dofs;
+  hipStream_t s = c->stream;
+  GLS_TRY(ensure_diag(c));
+  double *y = mgbuf(c, 0, MB_Y);
+  double *zs = mg.ilu_smooth && c->ilu.on ? mgbuf(c, 0, MB_BOX) : nullptr;
+  const int pre = mg.lpre[0], post = mg.lpost[0];
+  if (pre > 0 && zs) {
+    GLS_TRY(ensure_ilu(c));
+    GLS_TRY(apply_ilu(c, b, x));
+    for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(c, x, b, y, mg.omega, zs));
+  } else if (pre > 0) {
+    HIP_TRY(gls::mg_jacobi_update(x, b, nullptr, c->diag.p, mg.omega, n, 1, s));
+    for (int it = 1; it < pre; ++it) GLS_TRY(smoother_sweep(c, x, b, y, mg.omega));
+  } else {
+    HIP_TRY(gls::vec_fill(x, n, 0.0, s));
+  }
+  if (pre > 0) GLS_TRY(smoother_apply(c, x, y, b));  // y = b - A x
+  else HIP_TRY(gls::vec_copy(y, b, n, s));
+  // restriction: the owned rows' part of P^T y on this rank, summed over ranks
+  HIP_TRY(gls::vec_csr_spmv(mg.rep_b.p, y, mg.r2r_off.p, mg.r2r_col.p, mg.r2r_w.p, ng, false, s, mg.r2r_lane));
+  GLS_TRY(dist_allreduce_vector(c, mg.rep_b.p, ng));
+  HIP_TRY(gls::vec_set_indexed(mg.rep_b.p, r->con_dofs.p, nullptr, (int64_t)r->con_dofs.n, s));
+  GLS_TRY(gls_apply_preconditioner(r, mg.rep_b.p, mg.rep_x.p));  // the replica's own V-cycle, every rank
+  HIP_TRY(gls::vec_csr_spmv(y, mg.rep_x.p, mg.r2p_off.p, mg.r2p_col.p, mg.r2p_w.p, n, false, s, mg.r2p_lane));
+  HIP_TRY(gls::vec_set_indexed(y, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, s));
+  HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
+  for (int it = 0; it < post; ++it) GLS_TRY(smoother_sweep(c, x, b, y, mg.omega, zs));
   return GLS_OK;
 }
 
@@ -2793,6 +2882,7 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
 
 // z = M^{-1} v : Jacobi, assembled ILU(0) or a multigrid V-cycle when attached
 int apply_prec(gls_ctx *c, const double *v, double *z) {
+  if (c->mg.on && c->mg.rep_csr) return mg_vcycle_rep2(c, v, z);
   if (c->mg.on) return mg_vcycle(c, 0, v, z);
   if (c->ilu.on) return apply_ilu(c, v, z);
   HIP_TRY(gls::vec_div(z, v, c->diag.p, c->n_dofs, c->stream));
@@ -3273,6 +3363,99 @@ int gls_mg_set_coarse_replica(gls_ctx *c, gls_ctx *replica, int64_t n_local, con
   for (auto &u : mg.rep_u) GLS_TRY(u.alloc((size_t)ng));
   if (replica->stream != c->stream) GLS_TRY(gls_set_stream(replica, c->stream));
   mg.replica = replica;
+  mg.dirty = true;
+  return GLS_OK;
+}
+
+int gls_mg_attach_replica(gls_ctx *c, const gls_mg_params *p, gls_ctx *replica, const int64_t *p_off,
+                          const int32_t *p_col, const double *p_w, const int64_t *inject) {
+  GLS_TRY(check_ctx(c));
+  if (!p || !replica || replica == c || replica->dist.on || !p_off || !p_col || !p_w || !inject)
+    return set_err(GLS_EINVAL, "mg replica attach: arguments");
+  if (!c->dist.on) return set_err(GLS_EINVAL, "mg replica attach: the fine context is not distributed");
+  if (replica->dim != c->dim || replica->k != c->k || replica->kp != c->kp)
+    return set_err(GLS_EINVAL, "mg replica attach: replica order / dimension differs");
+  if (p->smoother < 0 || p->smoother > 1) return set_err(GLS_EINVAL, "mg replica attach: smoother 0 or 1");
+  GLS_TRY(gls_mg_detach(c));
+  auto &mg = c->mg;
+  const int64_t n = c->n_dofs, ng = replica->n_dofs;
+  if (ng >= INT32_MAX) return set_err(GLS_EINVAL, "mg replica attach: replica too large");
+  const int64_t dv = (int64_t)c->dim * c->n_vnodes;
+  auto owned = [&](int64_t i) { return i < dv ? i < (int64_t)c->dim * c->dist.n_owned : i - dv < c->dist.n_owned_p; };
+  // P on the local rows; R = the owned rows' P^T (rows = replica DoFs, local fine columns in ascending order)
+  const int64_t nnz = p_off[n];
+  std::vector<int64_t> roff((size_t)ng + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (p_off[i + 1] < p_off[i]) return set_err(GLS_EINVAL, "mg replica attach: P offsets");
+    for (int64_t e = p_off[i]; e < p_off[i + 1]; ++e) {
+      if (p_col[e] < 0 || p_col[e] >= ng) return set_err(GLS_EINVAL, "mg replica attach: P column %d", p_col[e]);
+      if (owned(i)) ++roff[(size_t)p_col[e] + 1];
+    }
+  }
+  for (int64_t r = 0; r < ng; ++r) roff[(size_t)r + 1] += roff[(size_t)r];
+  std::vector<int32_t> rcol((size_t)roff[(size_t)ng]);
+  std::vector<double> rw(rcol.size());
+  std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
+  for (int64_t i = 0; i < n; ++i)
+    if (owned(i))
+      for (int64_t e = p_off[i]; e < p_off[i + 1]; ++e) {
+        const int64_t at = fill[(size_t)p_col[e]]++;
+        rcol[(size_t)at] = (int32_t)i;
+        rw[(size_t)at] = p_w[e];
+      }
+  std::vector<int32_t> ic, iff;
+  for (int64_t r = 0; r < ng; ++r)
+    if (inject[r] >= 0) {
+      if (inject[r] >= n || !owned(inject[r])) return set_err(GLS_EINVAL, "mg replica attach: inject[%lld] not owned", (long long)r);
+      ic.push_back((int32_t)r);
+      iff.push_back((int32_t)inject[r]);
+    }
+  GLS_TRY(mg.r2p_off.upload(p_off, (size_t)n + 1));
+  GLS_TRY(mg.r2p_col.upload(p_col, std::max<size_t>((size_t)nnz, 1)));
+  GLS_TRY(mg.r2p_w.upload(p_w, std::max<size_t>((size_t)nnz, 1)));
+  GLS_TRY(mg.r2r_off.upload(roff.data(), roff.size()));
+  if (rcol.empty()) {
+    rcol.push_back(0);
+    rw.push_back(0.0);
+  }
+  GLS_TRY(mg.r2r_col.upload(rcol.data(), rcol.size()));
+  GLS_TRY(mg.r2r_w.upload(rw.data(), rw.size()));
+  auto lanes = [](double mean) { return mean > 24 ? 16 : mean > 6 ? 4 : 1; };
+  mg.r2p_lane = lanes(n ? (double)nnz / (double)n : 0.0);
+  mg.r2r_lane = lanes(ng ? (double)(roff[(size_t)ng]) / (double)ng : 0.0);
+  if (ic.empty()) {
+    ic.push_back(0);
+    iff.push_back(0);
+  }
+  GLS_TRY(mg.r2inj_c.upload(ic.data(), ic.size()));
+  GLS_TRY(mg.r2inj_f.upload(iff.data(), iff.size()));
+  if (ic.size() == 1 && inject[ic[0]] < 0) mg.r2inj_c.n = mg.r2inj_f.n = 0;  // no owned source on this rank
+  GLS_TRY(mg.rep_b.alloc((size_t)ng));
+  GLS_TRY(mg.rep_x.alloc((size_t)ng));
+  GLS_TRY(mg.rep_tmp.alloc(std::max<size_t>(ic.size(), 1)));
+  for (auto &u : mg.rep_u) GLS_TRY(u.alloc((size_t)ng));
+  // smoothing on the distributed fine level: damped Jacobi or ILU(0) (per-rank blocks, Ifpack overlap 0)
+  mg.lev.assign(1, c);
+  mg.pre = p->pre_smooth > 0 ? p->pre_smooth : (p->pre_smooth < 0 ? 0 : 2);
+  mg.post = p->post_smooth >= 0 ? p->post_smooth : 2;
+  mg.lpre.assign(1, mg.pre);
+  mg.lpost.assign(1, mg.post);
+  mg.omega = p->omega > 0 ? p->omega : 0.6;
+  mg.comega = mg.omega;
+  mg.ilu_smooth = p->smoother == 1;
+  for (int b = 0; b < MB_N; ++b) {
+    mg.bufs.emplace_back(new DevBuf<double>());
+    if (b == MB_Y || (b == MB_BOX && mg.ilu_smooth)) GLS_TRY(mg.bufs.back()->alloc((size_t)n));
+  }
+  if (mg.ilu_smooth) {
+    GLS_TRY(gls_ilu_set_options(c, GLS_ILU_ORDER_MULTICOLOR, 0));
+    GLS_TRY(gls_ilu_attach(c, 0, 1e-12, 1.0));
+    mg.ilu_levels.push_back(c);
+  }
+  if (replica->stream != c->stream) GLS_TRY(gls_set_stream(replica, c->stream));
+  mg.rep2 = replica;
+  mg.rep_csr = true;
+  mg.on = true;
   mg.dirty = true;
   return GLS_OK;
 }

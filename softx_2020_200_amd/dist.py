@@ -441,3 +441,28 @@ class DistributedGeneralProblem:
 
     def local(self, global_vec):
         return np.ascontiguousarray(np.asarray(global_vec)[self.plan["l2g_dofs"]])
+
+
+def replica_transfer(plan, p_off, p_col, p_w, inject):
+    """gls_mg_attach_replica's arrays for this rank from the GLOBAL prolongation (fine DoFs x level-1 DoFs, CSR)
+    and injection (level-1 DoF -> fine DoF): P restricted to the rank's local fine rows (owned and ghost, local
+    order), and for every level-1 DoF the local fine DoF it takes its state from where this rank owns that DoF
+    (-1 elsewhere)."""
+    l2g = np.asarray(plan["l2g_dofs"], np.int64)
+    p_off, p_col, p_w = (np.asarray(a) for a in (p_off, p_col, p_w))
+    lens = p_off[l2g + 1] - p_off[l2g]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    idx = np.repeat(p_off[l2g], lens) + (np.arange(off[-1]) - np.repeat(off[:-1], lens))
+    loc, glo = owned_dofs(plan)
+    g2l_own = np.full(int(plan["n_global_dofs"]), -1, np.int64)
+    g2l_own[glo] = loc
+    return off, p_col[idx].astype(np.int32), p_w[idx].astype(np.float64), g2l_own[np.asarray(inject, np.int64)]
+
+
+def attach_replica_multigrid(dp, replica_ctx, p_global, **opts):
+    """The refinement-hierarchy V-cycle across ranks: dp (DistributedGeneralProblem of the fine level) smooths
+    its rows, replica_ctx (single-rank context of the whole level-1 mesh with its own hierarchy attached) runs
+    the coarser levels on every rank (gls_mg_attach_replica); p_global = (off, col, w, inject) from level 1 to
+    the fine level, global numbering (FESpaceHandle.mg_transfer_from / octree transfers)."""
+    off, col, w, inj = replica_transfer(dp.plan, *p_global)
+    dp.ctx.attach_multigrid_replica(replica_ctx, off, col, w, inj, **opts)

@@ -29,7 +29,7 @@ EXPORTS = [
     "gls_jacobian_diagonal", "gls_set_dirichlet", "gls_apply_dirichlet", "gls_solve_linear", "gls_newton_solve",
     "gls_bdf_coefficients", "gls_sdirk_coefficients", "gls_newton_selftest", "gls_mesh_hyper_cube_sizes",
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
-    "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy", "gls_rccl_info", "gls_mg_smoother_apply",
+    "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy", "gls_rccl_info", "gls_mg_smoother_apply", "gls_mg_attach_replica",
     "gls_dist_attach_rccl",
     "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_residual_and_diagonal", "gls_octree_set_periodic", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
@@ -178,6 +178,8 @@ def load():
     L.gls_set_lattice.argtypes = [vp, C.c_int, C.POINTER(i64)]
     L.gls_apply_preconditioner.argtypes = [vp, vp, vp]
     L.gls_mg_smoother_apply.argtypes = [vp, vp, vp]
+    L.gls_mg_attach_replica.argtypes = [vp, C.POINTER(MGParams), vp, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_double), C.POINTER(C.c_int64)]
     L.gls_mg_transfer.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     P64 = C.POINTER(i64)
     L.gls_set_hanging.argtypes = [vp, i64, P64, P64, P64, d]
@@ -791,6 +793,23 @@ class GLSContext:
                      coarse_omega, coarse_direct, int(mixed_precision), ls, {"jacobi": 0, "ilu": 1}[smoother])
         check(self.L.gls_mg_attach_transfers(self.h, C.byref(p), offs, cols, ws, injs), "gls_mg_attach_transfers")
         self._mg_levels = levels
+
+    def attach_multigrid_replica(self, replica, p_off, p_col, p_w, inject_local, pre_smooth=2, post_smooth=2,
+                                 omega=0.6, smoother="jacobi"):
+        """The refinement-hierarchy V-cycle across ranks (gls_mg_attach_replica): this distributed fine
+        context smooths its rows, `replica` (a single-rank context of the whole level-1 mesh with its own
+        hierarchy attached) runs the coarser levels on every rank; P on the local fine rows (replica columns),
+        inject_local = the local fine DoF a replica DoF's state comes from where this rank owns it, else -1."""
+        keep = (np.ascontiguousarray(p_off, np.int64), np.ascontiguousarray(p_col, np.int32),
+                np.ascontiguousarray(p_w, np.float64), np.ascontiguousarray(inject_local, np.int64))
+        arr = (C.c_void_p * 1)(self.h)
+        p = MGParams(1, C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, 0, omega, 0.0, 0, 0, None,
+                     {"jacobi": 0, "ilu": 1}[smoother], 0)
+        check(self.L.gls_mg_attach_replica(self.h, C.byref(p), replica.h, keep[0].ctypes.data_as(C.POINTER(C.c_int64)),
+                                           keep[1].ctypes.data_as(C.POINTER(C.c_int32)),
+                                           keep[2].ctypes.data_as(C.POINTER(C.c_double)),
+                                           keep[3].ctypes.data_as(C.POINTER(C.c_int64))), "gls_mg_attach_replica")
+        self._mg_replica = (replica, keep)
 
     def set_coarse_replica(self, replica, local_to_replica):
         """Multi-GPU V-cycle below the coarsest distributed level = the single-GPU one, run redundantly on
