@@ -205,3 +205,38 @@ def test_general_partition_covers_and_closes(dim, k, kp, world):
             assert np.array_equal(sent, got), (a, int(b))
             own_b = set(owned_dofs(pb)[1].tolist())
             assert not (set(got.tolist()) & own_b)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_replica_transfer_rows_and_injection(world):
+    """gls_mg_attach_replica's per-rank arrays (dist.replica_transfer): every rank's local fine rows carry the
+    global prolongation's rows (replica columns unchanged), and each level-1 DoF's state is injected by exactly
+    one rank, the owner of the fine DoF it is taken from."""
+    from softx_2020_200_amd.dist import gpartition, owned_dofs, replica_transfer
+    from tests.test_gpu_uforest import dof_lines
+    from tests.test_uforest import make_mesh, random_adapt
+    m = make_mesh(3, dict(grid=("cylinder_shell", "1 : 0.25 : 1 : 8 : 2")))
+    m.refine_global(1)
+    random_adapt(m, 1, seed=5, k=2)
+    hf = m.fe_space_handle(2, 1, qmapping_all=True)
+    L = int(hf.data["cell_level"].max())
+    hc = m.coarsen_to(L - 1).fe_space_handle(2, 1, qmapping_all=True)
+    off, col, w, inj = hf.mg_transfer_from(hc)
+    lines = dof_lines(hf.data)
+    nc = len(inj)
+    hits = np.zeros(nc, np.int64)
+    for r in range(world):
+        plan = gpartition(hf.data, r, world, lines)
+        lo, lc, lw, li = replica_transfer(plan, off, col, w, inj)
+        l2g = np.asarray(plan["l2g_dofs"])
+        assert len(lo) == len(l2g) + 1
+        for i in range(0, len(l2g), max(1, len(l2g) // 200)):
+            g = l2g[i]
+            assert np.array_equal(lc[lo[i]:lo[i + 1]], col[off[g]:off[g + 1]])
+            assert np.array_equal(lw[lo[i]:lo[i + 1]], w[off[g]:off[g + 1]])
+        loc, glo = owned_dofs(plan)
+        sel = li >= 0
+        assert np.isin(li[sel], loc).all()
+        assert np.array_equal(l2g[li[sel]], inj[sel])
+        hits += sel
+    assert (hits == 1).all()
