@@ -1493,7 +1493,10 @@ struct Solver {
     for (size_t l = 0; l < np; ++l) {
       int64_t nnz = 0, nf = 0, nco = 0;
       ck(gls_octree_mg_transfer(meshes[l], meshes[l + 1], &nnz, nullptr, nullptr, nullptr, nullptr), "gls_octree_mg_transfer");
-      ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
+      if (l == 0)
+        nf = m.n_dofs();  // the fine space's (global) DoFs: with --np, lv[0] is the rank-local context
+      else
+        ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
       ck(gls_n_dofs(lv[l + 1], &nco), "gls_n_dofs");
       off[l].resize((size_t)nf + 1);
       col[l].resize((size_t)std::max<int64_t>(nnz, 1));
@@ -1671,7 +1674,10 @@ struct Solver {
     for (size_t l = 0; l < np; ++l) {
       int64_t nnz = 0, nf = 0, nco = 0;
       ck(gls_fe_space_mg_transfer(sp[l], sp[l + 1], &nnz, nullptr, nullptr, nullptr, nullptr), "gls_fe_space_mg_transfer");
-      ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
+      if (l == 0)
+        nf = m.n_dofs();  // the fine space's (global) DoFs: with --np, lv[0] is the rank-local context
+      else
+        ck(gls_n_dofs(lv[l], &nf), "gls_n_dofs");
       ck(gls_n_dofs(lv[l + 1], &nco), "gls_n_dofs");
       off[l].resize((size_t)nf + 1);
       col[l].resize((size_t)std::max<int64_t>(nnz, 1));
@@ -1694,7 +1700,43 @@ struct Solver {
     mp.post_smooth = mp.smoother ? 1 : 2;
     mp.omega = 0.6;
     mp.coarse_direct = n_coarse <= 8192 ? 1 : -1;
-    ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
+    if (world == 1) {
+      ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
+      return;
+    }
+    // --np: the fine level is this rank's cells; levels 1..L (whole meshes) run on every rank as one replica
+    // hierarchy fed by the all-reduced restriction of the owned rows (gls_mg_attach_replica). P's rows of the
+    // rank's local fine DoFs; a level-1 DoF's state comes from the fine DoF it injects, on the rank owning it.
+    gls_ctx *replica = lv[1];
+    if (lv.size() > 2) {
+      gls_mg_params rp = mp;
+      rp.n_levels = (int)lv.size() - 1;
+      rp.levels = lv.data() + 1;
+      ck(gls_mg_attach_transfers(replica, &rp, po.data() + 1, pc.data() + 1, pw.data() + 1, pi.data() + 1),
+         "gls_mg_attach_transfers (replica)");
+    }
+    std::vector<int64_t> loff{0};
+    std::vector<int32_t> lcol;
+    std::vector<double> lwt;
+    for (int64_t g : loc.l2g) {
+      for (int64_t j = off[0][(size_t)g]; j < off[0][(size_t)g + 1]; ++j) {
+        lcol.push_back(col[0][(size_t)j]);
+        lwt.push_back(w[0][(size_t)j]);
+      }
+      loff.push_back((int64_t)lcol.size());
+    }
+    std::vector<uint8_t> owned(loc.l2g.size(), 0);
+    for (int64_t i : loc.own_l) owned[(size_t)i] = 1;
+    std::vector<int64_t> linj(inj[0].size(), -1);
+    for (size_t j = 0; j < inj[0].size(); ++j) {
+      const int64_t l = loc.g2l[(size_t)inj[0][j]];
+      if (l >= 0 && owned[(size_t)l]) linj[j] = l;
+    }
+    if (lcol.empty()) lcol.push_back(0), lwt.push_back(0.0);
+    gls_mg_params fp = mp;
+    fp.n_levels = 1;
+    fp.levels = lv.data();
+    ck(gls_mg_attach_replica(ctx, &fp, replica, loff.data(), lcol.data(), lwt.data(), linj.data()), "gls_mg_attach_replica");
   }
 
   // FE space, constraints and context on the current triangulation (per-cell kernels with MappingQ
@@ -1745,6 +1787,9 @@ struct Solver {
       }
       if (!ld2.empty())
         ck(gls_set_hanging(ctx, (int64_t)ld2.size(), ld2.data(), lo2.data(), lm2.data(), lw2.data()), "gls_set_hanging");
+      // --precond hmg (or method = amg on Q2-Q2): the one-rank V-cycle with a replicated coarse hierarchy
+      if (use_mg && per.empty() && ((P.lin_method == 2 && P.k == P.kp && forest_mode != 1) || forest_mode == 2))
+        attach_umesh_mg();
     } else {
       ctx = make_context(m, C);
       if (!ld.empty())

@@ -251,7 +251,9 @@ int gls_mg_attach_transfers(gls_ctx *ctx, const gls_mg_params *prm, const int64_
  * DoFs, owned and ghost rows; inject (replica n_dofs): the local fine DoF whose value the replica's state
  * takes, on the one rank that owns it (-1 elsewhere). The restriction sums P^T over each rank's owned rows
  * and all-reduces in the replica numbering. prm: pre / post smooth, omega, smoother (0 damped Jacobi, 1
- * ILU(0) per rank = Ifpack additive Schwarz, overlap 0); levels / coarse entries are not used. Host arrays. */
+ * ILU(0) per rank = Ifpack additive Schwarz, overlap 0); coarse_direct > 0 with a replica WITHOUT a hierarchy
+ * of its own (two-level case): the replica level is solved exactly (probed, LU-inverted, <= 8192 DoFs) on
+ * every rank; levels / other coarse entries are not used. Host arrays. */
 int gls_mg_attach_replica(gls_ctx *ctx, const gls_mg_params *prm, gls_ctx *replica, const int64_t *p_off,
                           const int32_t *p_col, const double *p_w, const int64_t *inject);
 /* z = M^-1 v with the preconditioner gls_solve_linear uses at the current state (the V-cycle when

@@ -2278,8 +2278,10 @@ int mg_prepare(gls_ctx *c) {
     GLS_TRY(gls_set_time(r, jscheme, jts));
     GLS_TRY(gls_set_state(r, mg.rep_u[0].p, st[1] ? mg.rep_u[1].p : nullptr, st[2] ? mg.rep_u[2].p : nullptr,
                           st[3] ? mg.rep_u[3].p : nullptr));
-    mg.dirty = false;
-    return GLS_OK;
+    if (!mg.direct) {
+      mg.dirty = false;
+      return GLS_OK;
+    }
   }
   if (mg.replica) {  // the replica takes the coarsest distributed level's state (gathered) and time data
     gls_ctx *g = mg.lev[(size_t)L - 1], *r = mg.replica;
@@ -2293,7 +2295,8 @@ int mg_prepare(gls_ctx *c) {
   }
   mg.direct_ok = false;
   if (mg.direct) {  // probe A = J_coarse column by column, then invert on the device
-    gls_ctx *g = mg.lev[(size_t)L - 1];
+    // coarsest level: the last one, or the whole-mesh replica below a distributed fine level (rep_csr)
+    gls_ctx *g = mg.rep_csr ? mg.rep2 : mg.lev[(size_t)L - 1];
     const int64_t n = g->n_dofs;
     if (g->use_brick && g->use_qdata) {  // all unit vectors in one launch per batch
       GLS_TRY(ensure_diag(g));
@@ -2596,7 +2599,15 @@ int mg_vcycle_rep2(gls_ctx *c, const double *b, double *x) {
   HIP_TRY(gls::vec_csr_spmv(mg.rep_b.p, y, mg.r2r_off.p, mg.r2r_col.p, mg.r2r_w.p, ng, false, s, mg.r2r_lane));
   GLS_TRY(dist_allreduce_vector(c, mg.rep_b.p, ng));
   HIP_TRY(gls::vec_set_indexed(mg.rep_b.p, r->con_dofs.p, nullptr, (int64_t)r->con_dofs.n, s));
-  GLS_TRY(gls_apply_preconditioner(r, mg.rep_b.p, mg.rep_x.p));  // the replica's own V-cycle, every rank
+  if (mg.direct_ok) {  // the replica level is the coarsest: its exact solve, every rank
+    const double one = 1.0, zero = 0.0;
+    if (rocblas_set_stream(mg.blas, s) != rocblas_status_success ||
+        rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)ng, (rocblas_int)ng, &one, mg.probe.p,
+                      (rocblas_int)ng, mg.rep_b.p, 1, &zero, mg.rep_x.p, 1) != rocblas_status_success)
+      return set_err(GLS_EHIP, "rocblas_dgemv failed");
+  } else {
+    GLS_TRY(gls_apply_preconditioner(r, mg.rep_b.p, mg.rep_x.p));  // the replica's own V-cycle, every rank
+  }
   HIP_TRY(gls::vec_csr_spmv(y, mg.rep_x.p, mg.r2p_off.p, mg.r2p_col.p, mg.r2p_w.p, n, false, s, mg.r2p_lane));
   HIP_TRY(gls::vec_set_indexed(y, c->con_dofs.p, nullptr, (int64_t)c->con_dofs.n, s));
   HIP_TRY(gls::vec_axpy(x, 1.0, y, n, s));
@@ -3451,6 +3462,19 @@ int gls_mg_attach_replica(gls_ctx *c, const gls_mg_params *p, gls_ctx *replica, 
     GLS_TRY(gls_ilu_set_options(c, GLS_ILU_ORDER_MULTICOLOR, 0));
     GLS_TRY(gls_ilu_attach(c, 0, 1e-12, 1.0));
     mg.ilu_levels.push_back(c);
+  }
+  // a replica without a hierarchy of its own is the coarsest level: exact LU when asked (coarse_direct > 0)
+  if (p->coarse_direct > 0 && !replica->mg.on) {
+    if (ng > 8192) return set_err(GLS_EINVAL, "mg replica attach: direct coarse solve needs <= 8192 DoFs");
+    mg.direct = true;
+    GLS_TRY(mg.probe.alloc((size_t)(ng * ng)));
+    GLS_TRY(mg.ipiv.alloc((size_t)ng));
+    GLS_TRY(mg.info.alloc(1));
+    if (!mg.blas.h && rocblas_create_handle(&mg.blas.h) != rocblas_status_success)
+      return set_err(GLS_EHIP, "rocblas_create_handle failed");
+    rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
+    GLS_TRY(mg.unit.alloc((size_t)ng));
+    GLS_TRY(mg.status.alloc(1));
   }
   if (replica->stream != c->stream) GLS_TRY(gls_set_stream(replica, c->stream));
   mg.rep2 = replica;

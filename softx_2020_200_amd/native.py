@@ -795,16 +795,17 @@ class GLSContext:
         self._mg_levels = levels
 
     def attach_multigrid_replica(self, replica, p_off, p_col, p_w, inject_local, pre_smooth=2, post_smooth=2,
-                                 omega=0.6, smoother="jacobi"):
+                                 omega=0.6, smoother="jacobi", coarse_direct=0):
         """The refinement-hierarchy V-cycle across ranks (gls_mg_attach_replica): this distributed fine
         context smooths its rows, `replica` (a single-rank context of the whole level-1 mesh with its own
         hierarchy attached) runs the coarser levels on every rank; P on the local fine rows (replica columns),
-        inject_local = the local fine DoF a replica DoF's state comes from where this rank owns it, else -1."""
+        inject_local = the local fine DoF a replica DoF's state comes from where this rank owns it, else -1;
+        coarse_direct=1 with a replica without its own hierarchy: the exact solve on it (two-level cycle)."""
         keep = (np.ascontiguousarray(p_off, np.int64), np.ascontiguousarray(p_col, np.int32),
                 np.ascontiguousarray(p_w, np.float64), np.ascontiguousarray(inject_local, np.int64))
         arr = (C.c_void_p * 1)(self.h)
-        p = MGParams(1, C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, 0, omega, 0.0, 0, 0, None,
-                     {"jacobi": 0, "ilu": 1}[smoother], 0)
+        p = MGParams(1, C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, 0, omega, 0.0, int(coarse_direct), 0,
+                     None, {"jacobi": 0, "ilu": 1}[smoother], 0)
         check(self.L.gls_mg_attach_replica(self.h, C.byref(p), replica.h, keep[0].ctypes.data_as(C.POINTER(C.c_int64)),
                                            keep[1].ctypes.data_as(C.POINTER(C.c_int32)),
                                            keep[2].ctypes.data_as(C.POINTER(C.c_double)),

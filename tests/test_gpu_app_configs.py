@@ -227,3 +227,25 @@ def test_configs3_taylor_couette3d_kelly_hierarchy_multigrid(tmp_path):
             assert "refinement hierarchy" not in err
         its[pc] = [l for l in out.splitlines() if "linear_iterations =" in l]
     print("configs[3] GMRES totals: ILU %s, hierarchy GMG %s" % (its["mg"], its["hmg"]))
+
+
+@pytest.mark.gpu
+def test_configs3_hierarchy_multigrid_across_ranks(tmp_path):
+    """configs[3] at --np 4 with --precond hmg: the fine level partitioned over the ranks, the coarser levels of
+    the triangulation's hierarchy replicated on every rank (gls_mg_attach_replica; the exact LU on the coarsest
+    when the replica is the only coarser level), the same oracle checks as the one-rank pipeline. The GMRES
+    totals of the 4-rank run stay within 2x of the one-rank run's (the fine level's ILU(0) smoother becomes one
+    block per rank, as the reference's Ifpack additive Schwarz)."""
+    prm = open(os.path.join(CASES, "taylor-couette3d_q2q1_kelly.prm")).read()
+    its = {}
+    for npr in (1, 4):
+        d = tmp_path / ("np%d" % npr)
+        d.mkdir()
+        out, dumps = run_app(d, prm, extra=("--precision", "9", "--precond", "hmg", "--np", str(npr), "--stats"))
+        err = (d / "stderr.txt").read_text()
+        assert "Running on %d MPI rank(s)" % npr in out
+        assert "triangulation's refinement hierarchy" in err, err[-1500:]
+        check_configs3_pipeline(out, dumps, 1e-8)
+        its[npr] = [int(x) for x in re.findall(r"linear_iterations = (\d+)", out)]
+    print("configs[3] hmg GMRES totals: 1 rank %s, 4 ranks %s" % (its[1], its[4]))
+    assert its[1] and its[4] and sum(its[4]) <= 2 * sum(its[1]) + 10, its

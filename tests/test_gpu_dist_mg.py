@@ -28,14 +28,16 @@ def _worker(rank, world, port, q, case):
     from tests.test_uforest import CASES, make_mesh, random_adapt
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        name, k, kp, smoother = case
+        name, k, kp, smoother, two_level = case
         _, dim, spec, _ = [c for c in CASES if c[0] == name][0]
         m = make_mesh(dim, spec)
         m.refine_global(1)
         random_adapt(m, 2 if dim == 2 else 1, seed=5, k=k)
         hf = m.fe_space_handle(k, kp, qmapping_all=True)
-        L = int(hf.data["cell_level"].max())
-        handles = [hf] + [m.coarsen_to(L - l).fe_space_handle(k, kp, qmapping_all=True) for l in range(1, L + 1)]
+        L = L0 = int(hf.data["cell_level"].max())
+        if two_level:  # fine + one coarser level: the replica is the coarsest, solved exactly on every rank
+            L = 1
+        handles = [hf] + [m.coarsen_to(L0 - l).fe_space_handle(k, kp, qmapping_all=True) for l in range(1, L + 1)]
         probs = [mapped_level(h.data, 0.1) for h in handles]
         xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(L)]
         p = probs[0]
@@ -70,7 +72,7 @@ def _worker(rank, world, port, q, case):
         c = dp.ctx
         c.set_time(p.scheme, p.time_steps)
         replica = coarse_hierarchy(probs[1:])
-        attach_replica_multigrid(dp, replica[0], xfer[0], **mg)
+        attach_replica_multigrid(dp, replica[0], xfer[0], coarse_direct=int(two_level), **mg)
         Ud = cuda(dp.local(u))
         c.apply_dirichlet(Ud)
         c.set_state(Ud, cuda(np.zeros(len(dp.plan["l2g_dofs"]))))
@@ -100,8 +102,9 @@ def _worker(rank, world, port, q, case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("case", [("shell", 2, 2, "jacobi"), ("cylshell", 2, 1, "jacobi"), ("cylshell", 2, 1, "ilu")],
-                         ids=["shell-q2q2-jacobi", "cylshell-q2q1-jacobi", "cylshell-q2q1-ilu"])
+@pytest.mark.parametrize("case", [("shell", 2, 2, "jacobi", False), ("cylshell", 2, 1, "jacobi", False),
+                                  ("cylshell", 2, 1, "ilu", False), ("cylshell", 2, 1, "jacobi", True)],
+                         ids=["shell-q2q2-jacobi", "cylshell-q2q1-jacobi", "cylshell-q2q1-ilu", "cylshell-q2q1-two-level"])
 def test_hierarchy_multigrid_across_ranks_matches_single_rank(world, case):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
