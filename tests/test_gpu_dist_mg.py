@@ -16,19 +16,25 @@ import pytest
 SOLVE = dict(max_iterations=3000, restart=200, relative_residual=1e-10, minimum_residual=1e-300, true_residual=True)
 
 
-def _worker(rank, world, port, q, case):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    import torch.distributed as dist
-
-    from softx_2020_200_amd.dist import DistributedGeneralProblem, attach_replica_multigrid, owned_dofs
-    from tests.gpu_util import context_for, cuda, vnode_mask_of
+def _levels(case):
+    """(fine space dict for the partition, level problems fine -> coarsest, transfers, fine hanging lines, state)"""
+    import softx_2020_200_amd as sx
     from tests.test_gpu_umesh_mg import mapped_level
     from tests.test_gpu_uforest import dof_lines
     from tests.test_uforest import CASES, make_mesh, random_adapt
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        name, k, kp, smoother, two_level = case
+    name, k, kp, smoother, two_level = case
+    if name == "octree3d":  # adapted hyper_cube forest: affine per-cell levels; the ranks see its mapped form
+        from tests.test_gpu_octree_mg import octree_hierarchy
+        from tests.test_octree_mg import adapted_tree
+        tree = adapted_tree(3, 2, 2)
+        trees, probs, xfer = octree_hierarchy(tree, k, kp, nu=0.1)
+        if two_level:
+            raise ValueError("octree: full hierarchy only")
+        mesh = trees[0].mesh(k, kp)
+        space = dict(mesh, cell_support=np.ascontiguousarray(mesh["vnode_x"][mesh["cell_vnodes"]]))
+        lines = sx.hanging_dof_lines(mesh)
+        Xv, Xp, dim = mesh["vnode_x"], mesh["pnode_x"], 3
+    else:
         _, dim, spec, _ = [c for c in CASES if c[0] == name][0]
         m = make_mesh(dim, spec)
         m.refine_global(1)
@@ -40,11 +46,27 @@ def _worker(rank, world, port, q, case):
         handles = [hf] + [m.coarsen_to(L0 - l).fe_space_handle(k, kp, qmapping_all=True) for l in range(1, L + 1)]
         probs = [mapped_level(h.data, 0.1) for h in handles]
         xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(L)]
+        space = handles[0].data
+        lines = dof_lines(space) if (space["vhang"] or space["phang"]) else None
+        Xv, Xp = space["vnode_x"], space["pnode_x"]
+    u = np.concatenate([np.stack([np.sin(Xv[:, 0] + Xv[:, d]) for d in range(dim)], 1).reshape(-1), np.cos(Xp[:, 0])])
+    probs[0].apply_nonzero_constraints(u)
+    return space, probs, xfer, lines, u, dim
+
+
+def _worker(rank, world, port, q, case):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from softx_2020_200_amd.dist import DistributedGeneralProblem, attach_replica_multigrid, owned_dofs
+    from tests.gpu_util import context_for, cuda, vnode_mask_of
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        smoother, two_level = case[3], case[4]
+        space, probs, xfer, lines, u, dim = _levels(case)
+        L = len(probs) - 1
         p = probs[0]
-        Xv = handles[0].data["vnode_x"]
-        u = np.concatenate([np.stack([np.sin(Xv[:, 0] + Xv[:, d]) for d in range(dim)], 1).reshape(-1),
-                            np.cos(handles[0].data["pnode_x"][:, 0])])
-        p.apply_nonzero_constraints(u)
         sw = 2 if smoother == "jacobi" else 1
         mg = dict(pre_smooth=sw, post_smooth=sw, omega=0.6, smoother=smoother)
 
@@ -64,9 +86,8 @@ def _worker(rank, world, port, q, case):
         xs, its_s, res_s, ok_s = ctxs[0].solve_linear(rhs, ctxs[0].zeros(), **SOLVE)
         out["single"] = (its_s, ok_s, res_s / float(rhs.norm()))
         # ranks: fine level partitioned, levels 1..L replicated on every rank
-        lines = dof_lines(handles[0].data) if (handles[0].data["vhang"] or handles[0].data["phang"]) else None
         dirs = np.array(sorted(p.dirichlet), np.int64)
-        dp = DistributedGeneralProblem(handles[0].data, rank, world, "cuda", viscosity=0.1, vnode_mask=vnode_mask_of(p),
+        dp = DistributedGeneralProblem(space, rank, world, "cuda", viscosity=0.1, vnode_mask=vnode_mask_of(p),
                                        dirichlet=(dirs, np.array([p.dirichlet[d] for d in dirs])), lines=lines,
                                        force_q=p.force_q)
         c = dp.ctx
@@ -103,8 +124,10 @@ def _worker(rank, world, port, q, case):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", [("shell", 2, 2, "jacobi", False), ("cylshell", 2, 1, "jacobi", False),
-                                  ("cylshell", 2, 1, "ilu", False), ("cylshell", 2, 1, "jacobi", True)],
-                         ids=["shell-q2q2-jacobi", "cylshell-q2q1-jacobi", "cylshell-q2q1-ilu", "cylshell-q2q1-two-level"])
+                                  ("cylshell", 2, 1, "ilu", False), ("cylshell", 2, 1, "jacobi", True),
+                                  ("octree3d", 2, 2, "jacobi", False)],
+                         ids=["shell-q2q2-jacobi", "cylshell-q2q1-jacobi", "cylshell-q2q1-ilu", "cylshell-q2q1-two-level",
+                              "octree3d-q2q2-jacobi"])
 def test_hierarchy_multigrid_across_ranks_matches_single_rank(world, case):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
