@@ -3621,8 +3621,11 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   double bnorm2;
   GLS_TRY(device_dot(c, b, b, &bnorm2));
   const double tol = std::max(prm->relative_residual * std::sqrt(bnorm2), prm->minimum_residual);
-  HIP_TRY(gls::vec_fill(x, n, 0.0, s));
-  HIP_TRY(gls::vec_copy(r, b, n, s));
+  // x = 0: with the Z basis the first update writes x = Z y without reading it (x_zero), and the first
+  // restart cycle starts from r = b itself (no copy)
+  bool x_zero = keepz;
+  if (!keepz) HIP_TRY(gls::vec_fill(x, n, 0.0, s));
+  const double *rcur = b;
   double beta = std::sqrt(bnorm2);
   int it = 0;
   std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hc2(m + 2), y(m);
@@ -3641,7 +3644,7 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   const bool lverbose = std::getenv("GLS_ILU_VERBOSE") != nullptr;
   while (!converged && it < prm->max_iterations) {
     if (lverbose) std::printf("gmres: it %d residual %.6e (tol %.3e)\n", it, beta, tol);
-    HIP_TRY(gls::vec_axpby(V, 1.0 / beta, r, 0.0, n, s));
+    HIP_TRY(gls::vec_axpby(V, 1.0 / beta, rcur, 0.0, n, s));
     std::fill(Gm.begin(), Gm.end(), 0.);
     std::fill(g.begin(), g.end(), 0.);
     g[0] = beta;
@@ -3823,7 +3826,8 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     }
     HIP_TRY(hipMemcpyAsync(c->coef.p, y.data(), sizeof(double) * kdim, hipMemcpyHostToDevice, s));
     if (keepz) {
-      HIP_TRY(gls::vec_multiaxpy(x, c->zbasis.p, n, kdim, c->coef.p, -1.0, n, s));  // x += Z y
+      HIP_TRY(gls::vec_multiaxpy(x, c->zbasis.p, n, kdim, c->coef.p, -1.0, n, s, x_zero));  // x += Z y
+      x_zero = false;
     } else {
       HIP_TRY(gls::vec_fill(r, n, 0.0, s));
       HIP_TRY(gls::vec_multiaxpy(r, V, n, kdim, c->coef.p, -1.0, n, s));  // r = V y
@@ -3847,12 +3851,14 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
     // true residual r = b - A x
     GLS_TRY(gls_jacobian_apply(c, x, r));
     HIP_TRY(gls::vec_axpby(r, 1.0, b, -1.0, n, s));
+    rcur = r;
     double rn2;
     GLS_TRY(device_dot(c, r, r, &rn2));
     beta = std::sqrt(rn2);
     converged = beta <= tol;
     if (beta == 0.) break;
   }
+  if (x_zero) HIP_TRY(gls::vec_fill(x, n, 0.0, s));  // no update was made (b below the tolerance)
   prm->iterations = it;
   prm->final_residual = beta;
   if (ortho_repairs && std::getenv("GLS_GMRES_VERBOSE")) printf("  gmres: %d orthogonality repair passes\n", ortho_repairs);
@@ -3982,6 +3988,9 @@ struct DevicePhysics {
   bool skip = false;  // skip_newton: the Jacobian is frozen between assemblies (gls_freeze_jacobian)
   int linear_failures = 0;
   int evaluation_point_from_present() {
+    // the state IS present (no copy): the assembly reads it, the line search writes eval; the frozen-
+    // Jacobian renewal (skip) re-states eval, so it keeps the reference's copy
+    if (!skip) return gls_set_state(c, present, u1, u2, u3);
     HIP_TRY(gls::vec_copy(eval, present, c->n_dofs, c->stream));
     return gls_set_state(c, eval, u1, u2, u3);
   }
@@ -4029,8 +4038,7 @@ struct DevicePhysics {
     return GLS_OK;
   }
   int line_point(double alpha) {
-    HIP_TRY(gls::vec_copy(eval, present, c->n_dofs, c->stream));
-    HIP_TRY(gls::vec_axpy(eval, alpha, update, c->n_dofs, c->stream));
+    HIP_TRY(gls::vec_waxpy(eval, present, alpha, update, c->n_dofs, c->stream));  // eval = present + alpha update
     GLS_TRY(gls_apply_dirichlet(c, eval));  // nonzero_constraints.distribute
     return gls_set_state(c, eval, u1, u2, u3);
   }

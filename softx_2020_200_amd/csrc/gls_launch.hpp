@@ -71,9 +71,11 @@ hipError_t vec_multidot2(const double *A, int64_t lda, int nk, const double *w, 
 hipError_t vec_pack_nodes(const double *x, const int32_t *nodes, int64_t m, int64_t voff, double *buf, hipStream_t s);
 hipError_t vec_unpack_nodes(double *x, const int32_t *nodes, int64_t m, int64_t voff, const double *buf, int add,
                             hipStream_t s);
-// w -= sum_k h[k] * A[k]  (h on device)
+// w -= sum_k h[k] * A[k]  (h on device); zero_init: w starts at 0 (not read)
 hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
-                         hipStream_t s);
+                         hipStream_t s, bool zero_init = false);
+// w = y + a x
+hipError_t vec_waxpy(double *w, const double *y, double a, const double *x, int64_t n, hipStream_t s);
 // w -= sign * sum_k h[k] A[k] (nk <= 8, h on device), fused with out[k] = A[k] . w_new (k < nk, when
 // dots) and out[dots ? nk : 0] = ||w_new||^2, both over the owned rows [0, n1) U [off2, off2 + n2)
 hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,

@@ -26,6 +26,12 @@ __global__ void k_axpy(double *__restrict__ y, double a, const double *__restric
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     y[i] += a * x[i];
 }
+// w = y + a x (the copy + k_axpy pair in one pass, same arithmetic)
+__global__ void k_waxpy(double *__restrict__ w, const double *__restrict__ y, double a, const double *__restrict__ x,
+                        int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    w[i] = y[i] + a * x[i];
+}
 __global__ void k_axpby(double *__restrict__ y, double a, const double *__restrict__ x, double b, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = a * x[i] + b * y[i];
@@ -158,6 +164,33 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
 // kernels. Orthogonalisation 11.9 -> 11.0 ms per Newton step at configs[2] (4.9 -> 5.3 TB/s,
 // profiles/r05_ab_vec16.txt)
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+// k_multiaxpy with 16-byte loads / stores (two rows per lane); ZERO: w starts at 0 and is not read
+// (same arithmetic as a fill + k_multiaxpy: s = 0.0 - h0 a0 - ...)
+template <int NK, bool ZERO>
+__global__ void __launch_bounds__(kBlock) k_multiaxpy16(double *__restrict__ w, const double *__restrict__ A, int64_t lda,
+                                                        const double *__restrict__ h, double sign, int64_t n) {
+  double hk[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) hk[k] = sign * h[k];
+  const int64_t np = n / 2;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < np; p += (int64_t)gridDim.x * blockDim.x) {
+    dbl2 s = ZERO ? dbl2{0.0, 0.0} : reinterpret_cast<const dbl2 *>(w)[p];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const dbl2 a = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(A + k * lda) + p);
+      s.x -= hk[k] * a.x;
+      s.y -= hk[k] * a.y;
+    }
+    reinterpret_cast<dbl2 *>(w)[p] = s;
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    double s = ZERO ? 0.0 : w[n - 1];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) s -= hk[k] * A[k * lda + n - 1];
+    w[n - 1] = s;
+  }
+}
+
 template <int NK>
 __global__ void __launch_bounds__(kBlock) k_multidot16(const double *__restrict__ A, int64_t lda,
                                                        const double *__restrict__ w, int64_t n, double *work) {
@@ -422,18 +455,36 @@ hipError_t vec_multidot2(const double *A, int64_t lda, int nk, const double *w, 
 }
 
 hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const double *h, double sign, int64_t n,
-                         hipStream_t s) {
+                         hipStream_t s, bool zero_init) {
   const int nb = grid_for(n);
+  const bool v16 = vec16(A, lda, w, n, n, 0);
+  if (zero_init && !v16) {
+    const hipError_t e = vec_fill(w, n, 0.0, s);
+    if (e != hipSuccess) return e;
+  }
   for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
     const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;
     const double *Ak = A + (int64_t)k0 * lda;
+    const bool z = zero_init && v16 && k0 == 0;
     switch (m) {
-#define MA(M) \
-  case M: hipLaunchKernelGGL(k_multiaxpy<M>, dim3(nb), dim3(kBlock), 0, s, w, Ak, lda, h + k0, sign, n); break;
+#define MA(M)                                                                                                    \
+  case M:                                                                                                        \
+    if (z)                                                                                                       \
+      hipLaunchKernelGGL((k_multiaxpy16<M, true>), dim3(nb), dim3(kBlock), 0, s, w, Ak, lda, h + k0, sign, n);   \
+    else if (v16)                                                                                                \
+      hipLaunchKernelGGL((k_multiaxpy16<M, false>), dim3(nb), dim3(kBlock), 0, s, w, Ak, lda, h + k0, sign, n);  \
+    else                                                                                                         \
+      hipLaunchKernelGGL(k_multiaxpy<M>, dim3(nb), dim3(kBlock), 0, s, w, Ak, lda, h + k0, sign, n);             \
+    break;
       MA(1) MA(2) MA(3) MA(4) MA(5) MA(6) MA(7) MA(8)
 #undef MA
     }
   }
+  return hipGetLastError();
+}
+
+hipError_t vec_waxpy(double *w, const double *y, double a, const double *x, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_waxpy, dim3(grid_for(n)), dim3(kBlock), 0, s, w, y, a, x, n);
   return hipGetLastError();
 }
 
