@@ -259,15 +259,20 @@ def cpu_newton(k, kp, n, nu, scheme, dt, threads):
     return st
 
 
-def cylinder3d_context(k=2, kp=1, nu=0.005):
+def cylinder3d_context(k=2, kp=1, nu=0.005, refine=0, space=None):
     """BASELINE configs[4]'s discrete problem on one GPU (apps/cases/cylinder3d_q2q1_re200_kelly.prm):
     the reference's cylinder_structured.msh extruded to 3D (4 layers, apps/cases/cylinder3d_extruded.msh),
     Q2-Q1 with MappingQ2 on the boundary cells, nu = 0.005 (Re 200); boundary conditions in the prm's
     order: id 0 noslip (cylinder), id 1 u = (1, 0, 0) (inlet), slip on the planar ids 2, 4, 5 (n.u = 0,
-    the normal component; compute_no_normal_flux_constraints on axis-aligned walls)."""
+    the normal component; compute_no_normal_flux_constraints on axis-aligned walls). refine: global
+    refinements of the mesh (flat: no manifold on the extruded gmsh mesh); space: that FE space given."""
     from softx_2020_200_amd.native import GLSContext, UMesh
-    m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
-    sp = m.fe_space(k, kp)
+    if space is None:
+        m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
+        if refine:
+            m.refine_global(refine)
+        space = m.fe_space(k, kp)
+    sp = space
     nv, X, bid = sp["n_vnodes"], sp["vnode_x"], sp["vnode_bid"].astype(np.int64)
     con = np.zeros((nv, 3), dtype=bool)
     val = np.zeros((nv, 3))
@@ -304,10 +309,32 @@ def bench_cylinder3d(args):
     GPU, unadapted extruded mesh): residual, ILU(0) setup (probe + factor, multicolor order) and
     GMRES(30)+ILU to rel 1e-4, line search; the per-cell J.v kernel's roofline."""
     import torch
-    ctx, sp, x = cylinder3d_context()
+    t_setup = time.perf_counter()
+    levels, sw = None, 0
+    if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh (--cyl-refine >= 1)
+        from softx_2020_200_amd.native import UMesh
+        if args.cyl_refine < 1:
+            sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 (a hierarchy below the fine mesh)")
+        m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
+        m.refine_global(args.cyl_refine)
+        handles = [m.fe_space_handle(2, 1)] + [m.coarsen_to(args.cyl_refine - l).fe_space_handle(2, 1)
+                                               for l in range(1, args.cyl_refine + 1)]
+        xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(args.cyl_refine)]
+        levels = [cylinder3d_context(space=h.data) for h in handles]
+        ctx, sp, x = levels[0]
+        for c_, _, _ in levels:
+            c_.set_time("bdf2", (0.05,) * 4)
+        sw = 1 if args.cyl_smoother == "ilu" else 2
+        ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
+                                       coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=0.6, coarse_direct=-1,
+                                       smoother=args.cyl_smoother)
+    else:
+        ctx, sp, x = cylinder3d_context(refine=args.cyl_refine)
+        ctx.set_time("bdf2", (0.05,) * 4)
+        ctx.attach_ilu(1e-5, 1.0, fill=args.ilu_fill, ordering="multicolor" if args.ilu_fill == 0 else "cm")
     dev = torch.device("cuda", 0)
     ctx.set_time("bdf2", (0.05,) * 4)
-    ctx.attach_ilu(1e-5, 1.0, fill=args.ilu_fill, ordering="multicolor" if args.ilu_fill == 0 else "cm")
+    t_setup = time.perf_counter() - t_setup
     m1 = torch.from_numpy(x).to(dev)
     m2 = m1.clone()
     present = m1.clone()
@@ -347,9 +374,17 @@ def bench_cylinder3d(args):
         "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (free stream with a smooth wake-like perturbation, prm boundary values)",
         "config": {"workload": "BASELINE configs[4] problem on one GPU: apps/cases/cylinder3d_extruded.msh "
-                               "(unadapted), Q2-Q1 MappingQ2, nu 0.005, BDF2 dt 0.05",
-                   "n_dofs": N, "n_cells": nc, "linear_solver": "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
+                               "(unadapted%s), Q2-Q1 MappingQ2, nu 0.005, BDF2 dt 0.05" % (
+                                   ", %d global refinements (flat)" % args.cyl_refine if args.cyl_refine else ""),
+                   "n_dofs": N, "n_cells": nc,
+                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing, "
+                                     "%d sweeps on the base mesh), rel 1e-4" % (
+                                         args.restart, sw, sw, len(levels),
+                                         "ILU(0)" if args.cyl_smoother == "ilu" else "damped-Jacobi",
+                                         args.mg_coarse_sweeps_cyl))
+                   if levels else "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
                        args.restart, args.ilu_fill, "multicolor" if args.ilu_fill == 0 else "Cuthill-McKee")},
+        "setup_s": t_setup,
         "mdof_per_s": N * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
         "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,1,3,MODE_JV,GEN>", "achieved": B / (ms * 1e-3) / 1e9,
@@ -568,6 +603,13 @@ def main():
     ap.add_argument("--lin-max", type=int, default=200)
     ap.add_argument("--restart", type=int, default=30)
     ap.add_argument("--ilu-fill", type=int, default=0, help="cylinder3d: ILU level of fill (0: multicolor order)")
+    ap.add_argument("--cyl-refine", type=int, default=0, help="cylinder3d: global refinements of the mesh")
+    ap.add_argument("--cyl-precond", default="ilu", choices=["ilu", "hmg"],
+                    help="cylinder3d: ILU(fill) or the multigrid on the refinement hierarchy (needs --cyl-refine)")
+    ap.add_argument("--cyl-smoother", default="ilu", choices=["ilu", "jacobi"],
+                    help="cylinder3d --cyl-precond hmg: level smoother (ILU(0) V(1,1) or damped Jacobi V(2,2))")
+    ap.add_argument("--mg-coarse-sweeps-cyl", type=int, default=10,
+                    help="cylinder3d --cyl-precond hmg: ILU sweeps on the base (coarsest) mesh")
     ap.add_argument("--rel", type=float, default=1e-4)
     ap.add_argument("--octree-steps", type=int, default=3, help="octree: lid / edge refinement levels")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi", "ilu"],

@@ -295,6 +295,10 @@ struct gls_ctx {
   bool diag_valid = false;
   DevBuf<double> qdata;   // brick J.v linearization at the quadrature points (MODE_LIN output)
   bool qd_valid = false;  // invalidated with the diagonal by every state / parameter change
+  // per-cell kernels: linearization cache (u, grad u, tau, R_s per quadrature point) written by the diagonal
+  // pass and read by the J.v (OpParams::cq); valid with qd_valid's rules
+  DevBuf<double> cq;
+  bool cq_valid = false;
   DevBuf<float> qdata32;  // FP32 copy of qdata: the multigrid smoother's J.v (mixed precision)
   bool qd32_valid = false;  // stale whenever qdata is recomputed
   bool qd32_partial = false;  // the FP32 copy holds only u and tau (written for the Oseen smoother operator)
@@ -1138,6 +1142,17 @@ int ensure_element_maps(gls_ctx *c) {
   return c->ev.alloc((size_t)c->n_cells * el);
 }
 
+int ensure_diag(gls_ctx *c);
+// the per-cell linearization cache: on for contexts that run the per-cell kernels
+bool cell_cache_on(const gls_ctx *c) {
+  static const bool off = [] { const char *e = std::getenv("GLS_CELL_CACHE"); return e && std::atoi(e) == 0; }();
+  return !off && !c->use_brick && c->n_cells > 0;
+}
+size_t cell_cache_size(const gls_ctx *c) {
+  const int dim = c->dim;
+  return (size_t)c->n_cells * (size_t)gls::ipow(c->nq1d, dim) * (size_t)(dim + dim * dim + 1 + dim);
+}
+
 // adapted forest bricks: the pencil linearization (no output) at the current state
 int oct_lin(gls_ctx *c) {
   gls::OpParams L = make_params(c, true);
@@ -1155,6 +1170,19 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
+  // per-cell J.v from the diagonal pass's linearization cache (GLS_CELL_CACHE=0: re-derived every time)
+  const bool cq_on = cell_cache_on(c) && (mode == gls::MODE_JV || mode == gls::MODE_DIAG);
+  if (cq_on) {
+    const size_t need = cell_cache_size(c);
+    if (c->cq.n != need) {
+      GLS_TRY(c->cq.alloc(need));
+      c->cq_valid = false;
+    }
+    if (mode == gls::MODE_JV && !c->cq_valid) {  // the diagonal pass at this state writes it
+      c->diag_valid = false;
+      GLS_TRY(ensure_diag(c));
+    }
+  }
   const bool split_jv = mode == gls::MODE_JV && split_jv_enabled(c);
   if (mode == gls::MODE_JV && !split_jv && !c->probe_local) GLS_TRY(dist_import(c, const_cast<double *>(v)));  // ghost values of v
   gls::OpParams P = make_params(c, mode != gls::MODE_RESIDUAL);
@@ -1189,6 +1217,10 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (!brick) {  // per-cell kernels: element vectors, then ordered per-node sums (no atomics)
     GLS_TRY(ensure_element_maps(c));
     P.ev = c->ev.p;
+    if (cq_on) {
+      P.cq = c->cq.p;
+      P.cq_mode = mode == gls::MODE_DIAG ? 1 : 2;
+    }
   }
   // adapted forest: the sibling-group bricks by the pencil kernel (J.v from the cached linearization; the
   // diagonal pass computes that cache), the other cells by the per-cell kernel (its cell list)
@@ -1198,6 +1230,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     if (c->qdata.n != nq) {
       GLS_TRY(c->qdata.alloc(nq));
       c->qd_valid = false;
+      c->cq_valid = false;
     }
     if (mode == gls::MODE_JV && !c->qd_valid) GLS_TRY(oct_lin(c));  // linearization only, current state
     if (mode == gls::MODE_JV && c->oct.f32_next && !c->qd32_valid) {
@@ -1265,11 +1298,15 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   }
   // C^T y: the local cells' hanging rows onto their masters (masters across the partition are local
   // ghosts), then the ghost contributions to their owners (compress(add)); condensing the partial
-  // rows before the export equals condensing the summed rows after it
+  // rows before the export equals condensing the summed rows after it. (Folding this pass into the
+  // element-vector gather -- each master re-summing its hanging rows' slots -- measured 6.6 ms per Newton
+  // step SLOWER on the 1.28 M-DoF octree line: dependent slot-load chains per master stall whole waves,
+  // profiles/r05_ab_cell_cache_fold.txt.)
   if (c->hang.on && (mode == gls::MODE_RESIDUAL || mode == gls::MODE_JV))
     HIP_TRY(gls::vec_csr_condense(y, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
                                   (int64_t)c->hang.tm.n, c->stream));
   if (!c->probe_local) GLS_TRY(dist_export_add(c, y));
+  if (P.cq_mode == 1) c->cq_valid = true;
   if (lin_diag) {  // the same launch stored the J.v linearization
     c->qd_valid = true;
     c->qd32_valid = P.qdf != nullptr;
@@ -1515,6 +1552,7 @@ int gls_set_force(gls_ctx *c, const double *f) {
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  c->cq_valid = false;
   return GLS_OK;
 }
 
@@ -1524,6 +1562,7 @@ int gls_set_viscosity(gls_ctx *c, double nu) {
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  c->cq_valid = false;
   return GLS_OK;
 }
 
@@ -1570,6 +1609,7 @@ int gls_set_time(gls_ctx *c, int scheme, const double ts[4]) {
     c->diag_valid = false;
     c->ilu.valid = false;
     c->qd_valid = false;
+    c->cq_valid = false;
   }
   return GLS_OK;
 }
@@ -1585,6 +1625,7 @@ int gls_set_state(gls_ctx *c, const double *u, const double *u1, const double *u
     c->diag_valid = false;
     c->ilu.valid = false;
     c->qd_valid = false;
+    c->cq_valid = false;
     c->mg.dirty = true;
   }
   // distributed: refresh the ghost values of the evaluation point (history vectors are imported
@@ -1605,6 +1646,7 @@ int gls_freeze_jacobian(gls_ctx *c, int freeze) {
       c->diag_valid = false;
       c->ilu.valid = false;
       c->qd_valid = false;
+      c->cq_valid = false;
       c->mg.dirty = true;
     }
     return GLS_OK;
@@ -1670,6 +1712,7 @@ int gls_dist_attach(gls_ctx *c, int64_t n_owned_nodes, int n_nbrs, const int64_t
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  c->cq_valid = false;
   if (c->use_brick && gls::brick_subset_supported(c->k)) {  // boundary / interior bricks (overlapped J.v)
     std::vector<char> flag((size_t)c->n_vnodes, 0);
     for (int64_t i = 0; i < ns; ++i) flag[(size_t)send_nodes[i]] = 1;
@@ -1724,6 +1767,7 @@ int gls_dist_attach_dofs(gls_ctx *c, int64_t n_owned_vnodes, int64_t n_owned_pno
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  c->cq_valid = false;
   return GLS_OK;
 }
 
@@ -1983,6 +2027,7 @@ int gls_apply_dirichlet(gls_ctx *c, double *x) {
     c->diag_valid = false;
     c->ilu.valid = false;
     c->qd_valid = false;
+    c->cq_valid = false;
     c->mg.dirty = true;
   }
   return GLS_OK;
@@ -2137,6 +2182,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   c->diag_valid = false;
   c->ilu.valid = false;
   c->qd_valid = false;
+  c->cq_valid = false;
   return detect_oct_bricks(c);
 }
 
@@ -2776,6 +2822,8 @@ static int ilu_probe_batched(gls_ctx *c) {
     P.y = I.bY.p;
     P.hmask = c->hang.on ? c->hang.hmask.p : nullptr;
     P.ev = c->bev.p;
+    // (the probes re-derive the linearization: reading the cache per (probe, cell batch) moves more bytes than
+    // the state gathers -- configs[4]'s ILU setup ran 1.4 ms per Newton step slower with it)
     P.bv_stride = n;
     P.bev_stride = evs;
     P.n_probe = nb;

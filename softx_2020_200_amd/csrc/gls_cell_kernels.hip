@@ -64,6 +64,9 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   const int ncb = min(CB, (P.cell_list ? P.cell_list_n : P.n_cells) - c0);
   auto cid = [&](int cl) -> int64_t { return P.cell_list ? (int64_t)P.cell_list[c0 + cl] : (int64_t)(c0 + cl); };
   const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
+  constexpr int NCQ = DIM + DIM * DIM + 1 + DIM;    // linearization cache values per q (u, grad u, tau, R_s)
+  const bool cqr = MODE == MODE_JV && P.cq && P.cq_mode == 2;   // J.v from the cache
+  const bool cqw = MODE == MODE_DIAG && P.cq && P.cq_mode == 1;  // the diagonal pass fills it
 
   // batched J.v (probing): this block's vector; J is linear, so a batch of cells on which the vector
   // vanishes has zero element vectors (most (probe, cell batch) pairs of a distance-2 colored probe set)
@@ -97,6 +100,12 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   for (int i = tid; i < ncb * NV; i += blockDim.x) {
     const int node = P.cell_vnodes[cid(i / NV) * NV + i % NV];
     const int64_t b = (int64_t)node * DIM;
+    if constexpr (MODE == MODE_JV) {
+      const unsigned m = P.vmask ? P.vmask[node] : 0u;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) sV[i * DIM + c] = ((m >> c) & 1u) ? 0.0 : Pv[b + c];
+      if (cqr) continue;  // u and its history come from the cache
+    }
 #pragma unroll
     for (int c = 0; c < DIM; ++c) sU[i * DIM + c] = P.u[b + c];
     if (P.n_hist > 0) {
@@ -111,15 +120,10 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
 #pragma unroll
       for (int c = 0; c < DIM; ++c) sH[2 * CB * NV * DIM + i * DIM + c] = P.h3[b + c];
     }
-    if constexpr (MODE == MODE_JV) {
-      const unsigned m = P.vmask ? P.vmask[node] : 0u;
-#pragma unroll
-      for (int c = 0; c < DIM; ++c) sV[i * DIM + c] = ((m >> c) & 1u) ? 0.0 : Pv[b + c];
-    }
   }
   for (int i = tid; i < ncb * NP; i += blockDim.x) {
     const int pn = P.cell_pnodes ? P.cell_pnodes[cid(i / NP) * NP + i % NP] : P.cell_vnodes[cid(i / NV) * NV + i % NV];
-    sP[i] = P.u[voff + pn];
+    if (!cqr) sP[i] = P.u[voff + pn];
     if constexpr (MODE == MODE_JV) sVP[i] = Pv[voff + pn];
   }
   __syncthreads();
@@ -203,11 +207,13 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
           const double gr[3] = {g0, g1, g2};
 #pragma unroll
           for (int c = 0; c < DIM; ++c) {
-            const double val = cu[a * DIM + c];
-            u[c] += val * N;
-            lu[c] += val * L;
+            if (!cqr) {
+              const double val = cu[a * DIM + c];
+              u[c] += val * N;
+              lu[c] += val * L;
 #pragma unroll
-            for (int e = 0; e < DIM; ++e) gu[c][e] += val * gr[e];
+              for (int e = 0; e < DIM; ++e) gu[c][e] += val * gr[e];
+            }
             if constexpr (MODE == MODE_JV) {
               const double vv = cv[a * DIM + c];
               v[c] += vv * N;
@@ -215,9 +221,11 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
 #pragma unroll
               for (int e = 0; e < DIM; ++e) gv[c][e] += vv * gr[e];
             }
-            if (nh > 0) h1[c] += ch[a * DIM + c] * N;
-            if (nh > 1) h2[c] += ch[CB * NV * DIM + a * DIM + c] * N;
-            if (nh > 2) h3[c] += ch[2 * CB * NV * DIM + a * DIM + c] * N;
+            if (!cqr) {
+              if (nh > 0) h1[c] += ch[a * DIM + c] * N;
+              if (nh > 1) h2[c] += ch[CB * NV * DIM + a * DIM + c] * N;
+              if (nh > 2) h3[c] += ch[2 * CB * NV * DIM + a * DIM + c] * N;
+            }
           }
         }
       }
@@ -237,10 +245,12 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
             const int a = ax + C::KP1 * (ay + C::KP1 * az);
             const double N = vx * vy * vz;
             const double gr[3] = {dx * vy * vz, vx * dy * vz, vx * vy * dz};
-            const double pv = cp[a];
-            if constexpr (MODE == MODE_RESIDUAL) pq += pv * N;
+            if (!cqr) {
+              const double pv = cp[a];
+              if constexpr (MODE == MODE_RESIDUAL) pq += pv * N;
 #pragma unroll
-            for (int e = 0; e < DIM; ++e) gp[e] += pv * gr[e];
+              for (int e = 0; e < DIM; ++e) gp[e] += pv * gr[e];
+            }
             if constexpr (MODE == MODE_JV) {
               const double w = cvp[a];
               vp += w * N;
@@ -274,6 +284,15 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
       for (int e = 0; e < DIM; ++e) { gp[e] *= ih[e]; gvp[e] *= ih[e]; }
     }
 
+    const int64_t cqb = ((int64_t)cell * NCQ) * NQ + q;  // cache entry k of this point at cqb + k * NQ
+    if (cqr) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) u[c] = P.cq[cqb + (int64_t)c * NQ];
+#pragma unroll
+      for (int c = 0; c < DIM; ++c)
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) gu[c][e] = P.cq[cqb + (int64_t)(DIM + DIM * c + e) * NQ];
+    }
     // ---- pointwise (gls_navier_stokes.cc:391-516)
     const double nu = P.nu;
     double un2 = 0.;
@@ -281,7 +300,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     for (int c = 0; c < DIM; ++c) un2 += u[c] * u[c];
     const double u_mag = fmax(sqrt(un2), 1e-12);
     const double t1 = 2. * u_mag / hst, t2 = 4 * nu / (hst * hst);
-    const double tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
+    double tau = 1. / sqrt(P.sdt2 + t1 * t1 + 9 * (t2 * t2));
     double f[DIM] = {};
     if (P.force_q) {
 #pragma unroll
@@ -336,6 +355,22 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
       if (nh > 2) s += P.alpha[3] * h3[c];
       Tt[c] = s;
       R[c] += s;
+    }
+    if (cqr) {  // tau and R_s as the diagonal pass computed them (the state's gathers were skipped)
+      tau = P.cq[cqb + (int64_t)(DIM + DIM * DIM) * NQ];
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) R[c] = P.cq[cqb + (int64_t)(DIM + DIM * DIM + 1 + c) * NQ];
+    }
+    if (cqw) {
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) P.cq[cqb + (int64_t)c * NQ] = u[c];
+#pragma unroll
+      for (int c = 0; c < DIM; ++c)
+#pragma unroll
+        for (int e = 0; e < DIM; ++e) P.cq[cqb + (int64_t)(DIM + DIM * c + e) * NQ] = gu[c][e];
+      P.cq[cqb + (int64_t)(DIM + DIM * DIM) * NQ] = tau;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) P.cq[cqb + (int64_t)(DIM + DIM * DIM + 1 + c) * NQ] = R[c];
     }
 
     double *Tq = sT + (cl * NQ + q) * NT;

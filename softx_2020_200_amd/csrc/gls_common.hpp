@@ -109,6 +109,12 @@ struct OpParams {
   // the (grad u) v terms and the SUPG term tau (v . grad phi) R_s (the multigrid smoother's operator,
   // gls_mg_params.smoother_operator = 1); the outer GMRES operator is never affected
   int oseen;
+  // per-cell kernels: the linearization cache [cell][NCQ][NQ] (u, grad u, tau, R_s at every quadrature point,
+  // NCQ = dim + dim^2 + 1 + dim): cq_mode 1 = MODE_DIAG writes it, 2 = MODE_JV reads it instead of re-deriving
+  // u, its derivatives, the history terms and R_s from the state (same values: the diagonal pass computes them
+  // with the same code)
+  double *cq;
+  int cq_mode;
 };
 
 }  // namespace gls

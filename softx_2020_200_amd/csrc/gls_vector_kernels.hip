@@ -32,7 +32,13 @@ __global__ void k_waxpy(double *__restrict__ w, const double *__restrict__ y, do
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     w[i] = y[i] + a * x[i];
 }
+// y = a x + b y; b == 0 does not read y (a fresh buffer may hold NaN bit patterns: 0 * NaN is NaN)
 __global__ void k_axpby(double *__restrict__ y, double a, const double *__restrict__ x, double b, int64_t n) {
+  if (b == 0.0) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+      y[i] = a * x[i];
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = a * x[i] + b * y[i];
 }

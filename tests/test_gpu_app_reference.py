@@ -67,6 +67,7 @@ def test_reference_application_case(tmp_path, name, dim, periodic, pressure):
     for a, b in zip(ours, theirs):  # periodic cases too: deal.II's DoF count (periodicity as a constraint)
         assert a == b, (a, b)
     ro, rr = error_rows(out), error_rows(ref)
+    print(name, "ours", ro, "reference", rr)
     assert len(ro) == len(rr), out
     roundoff = name in ("rigid-body-rotation_gls", "cylinder-rigid-body_gls")  # exact solution: errors ~1e-11
     for a, b in zip(ro, rr):
