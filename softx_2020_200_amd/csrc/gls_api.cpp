@@ -1299,9 +1299,10 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   // C^T y: the local cells' hanging rows onto their masters (masters across the partition are local
   // ghosts), then the ghost contributions to their owners (compress(add)); condensing the partial
   // rows before the export equals condensing the summed rows after it. (Folding this pass into the
-  // element-vector gather -- each master re-summing its hanging rows' slots -- measured 6.6 ms per Newton
-  // step SLOWER on the 1.28 M-DoF octree line: dependent slot-load chains per master stall whole waves,
-  // profiles/r05_ab_cell_cache_fold.txt.)
+  // element-vector gather measured slower on the 1.28 M-DoF octree line both ways: each master re-summing
+  // its hanging rows' slots through their node maps +6.6 ms per Newton step, flattened (slot, weight) lists
+  // per master DoF +1.6 ms -- the gather is bound by its dependent load chain, which either form lengthens;
+  // profiles/r05_ab_cell_cache_fold.txt, r05_ab_condense_fold2.txt.)
   if (c->hang.on && (mode == gls::MODE_RESIDUAL || mode == gls::MODE_JV))
     HIP_TRY(gls::vec_csr_condense(y, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
                                   (int64_t)c->hang.tm.n, c->stream));
