@@ -485,6 +485,10 @@ struct gls_ctx {
     DevBuf<double> xwork;  // two-pass transfer intermediate (coarse xy x fine z, 4 fields)
     // coarsest level: direct solve with the probed, regularised, inverted Jacobian
     bool direct = false, direct_ok = false;
+    // per-cell coarsest level: its matrix for the direct solve assembled by the ILU's colored batched probes
+    // (a structure-only ILU(0) on that level, never factored) instead of one J.v per column
+    gls_ctx *probe_ilu = nullptr;
+    DevBuf<int32_t> pinv;
     // direct solve by LU (rocSOLVER getrf + getri -> explicit inverse, applied by rocBLAS gemv) with
     // the first pressure DoF pinned (enclosed-flow gauge); falls back to the one-workgroup
     // Gauss-Jordan (mg_dense_invert) for small levels or when the LU reports a zero pivot
@@ -1934,6 +1938,7 @@ int smoother_apply(gls_ctx *g, const double *v, double *y, const double *rb = nu
 // sum (brick-surface nodes), so A x is never stored; otherwise smoother_apply + mg_jacobi_update.
 }  // namespace
 static int ensure_ilu(gls_ctx *c);
+static int ilu_probe(gls_ctx *c);
 static int apply_ilu(gls_ctx *c, const double *v, double *z);
 namespace {
 // one ILU(0) smoothing sweep x <- x + M^-1 (b - A x) (M = the level's ILU(0), undamped; z: scratch)
@@ -2275,6 +2280,21 @@ static int coarse_inverse_check(gls_ctx *c, int64_t n, bool *good) {
   return GLS_OK;
 }
 
+// the direct coarse solve's matrix by colored probing on a per-cell level (mg.probe_ilu; GLS_MG_PROBE_LOOP=1:
+// one J.v per column as before): the ILU structure (CM order, fill 0, one block) is attached once
+int mg_probe_setup(gls_ctx *c, gls_ctx *g) {
+  auto &mg = c->mg;
+  mg.probe_ilu = nullptr;
+  if (std::getenv("GLS_MG_PROBE_LOOP") || (g->use_brick && g->use_qdata) || g->dist.on || g->mg.on || g->ilu.on)
+    return GLS_OK;
+  GLS_TRY(gls_ilu_set_options(g, GLS_ILU_ORDER_CM, 0));
+  GLS_TRY(gls_ilu_attach(g, 0, 0.0, 1.0));
+  mg.ilu_levels.push_back(g);  // detached with the multigrid
+  GLS_TRY(mg.pinv.alloc((size_t)g->n_dofs));
+  mg.probe_ilu = g;
+  return GLS_OK;
+}
+
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
@@ -2360,6 +2380,12 @@ int mg_prepare(gls_ctx *c) {
         HIP_TRY(gls::mg_probe_fix(mg.probe.p + j0 * n, n, j0, nb, g->con_dofs.p, (int64_t)g->con_dofs.n, g->diag.p,
                                   c->stream));
       }
+    } else if (mg.probe_ilu == g && g->ilu.on) {  // colored batched probes into the ILU's CSR, then dense
+      GLS_TRY(ensure_diag(g));
+      GLS_TRY(ilu_probe(g));
+      HIP_TRY(hipMemsetAsync(mg.probe.p, 0, sizeof(double) * (size_t)(n * n), c->stream));
+      const auto &I = g->ilu;
+      HIP_TRY(gls::csr_to_dense(mg.probe.p, I.rowp.p, I.col.p, I.val.p, I.perm.p, mg.pinv.p, n, c->stream));
     } else {
       HIP_TRY(gls::vec_fill(mg.unit.p, n, 0.0, c->stream));
       for (int64_t j = 0; j < n; ++j) {
@@ -3230,6 +3256,7 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
       GLS_TRY(mg.unit.alloc((size_t)nco));
       GLS_TRY(mg.status.alloc(1));
+      GLS_TRY(mg_probe_setup(c, mg.lev.back()));
     }
   }
   mg.on = true;
@@ -3524,6 +3551,7 @@ int gls_mg_attach_replica(gls_ctx *c, const gls_mg_params *p, gls_ctx *replica, 
     rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
     GLS_TRY(mg.unit.alloc((size_t)ng));
     GLS_TRY(mg.status.alloc(1));
+    GLS_TRY(mg_probe_setup(c, replica));
   }
   if (replica->stream != c->stream) GLS_TRY(gls_set_stream(replica, c->stream));
   mg.rep2 = replica;

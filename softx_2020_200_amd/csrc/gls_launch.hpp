@@ -95,6 +95,10 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
 hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s);
 hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
                              hipStream_t s, bool add = false);
+// dense column-major A (n x n, A[j * n + i] = A_ij, DoF numbering) from the ILU's probed CSR (rows / columns
+// in its renumbered order, perm: DoF -> row); inv (n ints, scratch) receives row -> DoF. A is not zeroed here
+hipError_t csr_to_dense(double *A, const int32_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
+                        const int32_t *inv, int64_t n, hipStream_t s);
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s);
 // batched probing of the per-cell operator (nb probe vectors at stride bs / ys, element vectors at evs;
 // pid[e] = probe of entry e, p0 = the batch's first probe)

@@ -690,6 +690,20 @@ __global__ void k_diag_perturb(double *val, const int32_t *didx, int64_t n, doub
   val[didx[i]] = rthresh * a + (a < 0 ? -athresh : athresh);
 }
 // out[idx[i]] = in[i] (scatter, dir 0) or out[i] = in[idx[i]] (gather, dir 1)
+// dense column-major A (A[j * n + i] = A_ij in DoF numbering) from a CSR in a renumbered order (perm: DoF -> CSR
+// row, inv: CSR row -> DoF); positions outside the pattern are left as they are (the caller zeroes A)
+__global__ void k_csr_to_dense(double *__restrict__ A, const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
+                               const double *__restrict__ val, const int32_t *__restrict__ perm,
+                               const int32_t *__restrict__ inv, int64_t n) {
+  for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
+    const int r = perm[d];
+    for (int e = rowp[r]; e < rowp[r + 1]; ++e) A[(int64_t)inv[col[e]] * n + d] = val[e];
+  }
+}
+__global__ void k_invert_perm(int32_t *__restrict__ inv, const int32_t *__restrict__ perm, int64_t n) {
+  for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x)
+    inv[perm[d]] = (int32_t)d;
+}
 __global__ void k_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -697,6 +711,12 @@ __global__ void k_permute(double *out, const double *in, const int32_t *idx, int
   else out[i] = in[idx[i]];
 }
 }  // namespace
+hipError_t csr_to_dense(double *A, const int32_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
+                        const int32_t *inv, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_invert_perm, dim3(grid_for(n)), dim3(kBlock), 0, s, const_cast<int32_t *>(inv), perm, n);
+  hipLaunchKernelGGL(k_csr_to_dense, dim3(grid_for(n)), dim3(kBlock), 0, s, A, rowp, col, val, perm, inv, n);
+  return hipGetLastError();
+}
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_permute, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, in, idx, n, dir);
