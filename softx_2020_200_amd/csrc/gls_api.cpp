@@ -3233,10 +3233,15 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       if (need)
         GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX && mg.boxed ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
     }
-  if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (Cuthill-McKee order; multicolor above 1e5 DoFs)
+  if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (multicolor order)
     for (int l = 0; l + 1 < p->n_levels; ++l) {
       gls_ctx *g = mg.lev[(size_t)l];
-      GLS_TRY(gls_ilu_set_options(g, g->n_dofs > 100000 ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM, 0));
+      // multicolor order on every level (GLS_MG_ILU_MC_MIN: the level size from which it is used; Cuthill-McKee
+      // below). As a smoother the color-by-color ILU(0) is both faster per sweep (no level-scheduled csrsv) and
+      // stronger: configs[3] --precond hmg 38 -> 26 GMRES iterations, 3.97 -> 1.37 s wall, the linear solves
+      // 1.72 -> 0.08 s (profiles/r05_app_configs3_hmg_ilu_order.txt)
+      static const int64_t mc_min = std::getenv("GLS_MG_ILU_MC_MIN") ? std::atoll(std::getenv("GLS_MG_ILU_MC_MIN")) : 0;
+      GLS_TRY(gls_ilu_set_options(g, g->n_dofs > mc_min ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM, 0));
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
       mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
