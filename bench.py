@@ -408,7 +408,8 @@ def bench_octree(args):
     mg = args.precond == "mg"
     prob = AdaptiveCavityProblem(tree, k=args.k, kp=args.kp, viscosity=args.nu, multigrid=mg,
                                  pre_smooth=args.mg_smooth[0], post_smooth=args.mg_smooth[1], omega=args.mg_omega,
-                                 coarse_direct=1, mixed_precision=int(args.mg_precision == "f32"))
+                                 coarse_direct=1, mixed_precision=int(args.mg_precision == "f32"),
+                                 smoother=args.oct_smoother)
     ctx = prob.ctx
     if not mg:
         ctx.attach_ilu(1e-5, 1.0, fill=0, ordering="multicolor")
@@ -460,7 +461,9 @@ def bench_octree(args):
                    "n_dofs": N, "n_cells": nc, "cells_per_level": lev,
                    "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing), rel %g"
                                      % (args.restart, args.mg_smooth[0], args.mg_smooth[1], len(prob.levels),
-                                        "FP32 brick" if args.mg_precision == "f32" else "FP64", args.rel))
+                                        "multicolor ILU(0)" if args.oct_smoother == "ilu" else
+                                        ("damped-Jacobi, FP32 brick J.v" if args.mg_precision == "f32" else "damped-Jacobi FP64"),
+                                        args.rel))
                    if mg else "GMRES(%d)+ILU(0) multicolor, rel %g" % (args.restart, args.rel)},
         "mdof_per_s": N * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
@@ -606,6 +609,8 @@ def main():
     ap.add_argument("--cyl-refine", type=int, default=0, help="cylinder3d: global refinements of the mesh")
     ap.add_argument("--cyl-precond", default="ilu", choices=["ilu", "hmg"],
                     help="cylinder3d: ILU(fill) or the multigrid on the refinement hierarchy (needs --cyl-refine)")
+    ap.add_argument("--oct-smoother", default="jacobi", choices=["jacobi", "ilu"],
+                    help="octree --precond mg: level smoother (damped Jacobi with FP32 brick J.v, or multicolor ILU(0))")
     ap.add_argument("--cyl-smoother", default="ilu", choices=["ilu", "jacobi"],
                     help="cylinder3d --cyl-precond hmg: level smoother (ILU(0) V(1,1) or damped Jacobi V(2,2))")
     ap.add_argument("--mg-coarse-sweeps-cyl", type=int, default=10,
