@@ -1787,16 +1787,17 @@ struct Solver {
       }
       if (!ld2.empty())
         ck(gls_set_hanging(ctx, (int64_t)ld2.size(), ld2.data(), lo2.data(), lm2.data(), lw2.data()), "gls_set_hanging");
-      // --precond hmg (or method = amg on Q2-Q2): the one-rank V-cycle with a replicated coarse hierarchy
-      if (use_mg && per.empty() && ((P.lin_method == 2 && P.k == P.kp && forest_mode != 1) || forest_mode == 2))
+      // --precond hmg (or method = amg): the one-rank V-cycle with a replicated coarse hierarchy
+      if (use_mg && per.empty() && ((P.lin_method == 2 && forest_mode != 1) || forest_mode == 2))
         attach_umesh_mg();
     } else {
       ctx = make_context(m, C);
       if (!ld.empty())
         ck(gls_set_hanging(ctx, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging");
-      // method = amg (ML's multilevel hierarchy): the geometric one of the triangulation; gmres keeps the
-      // reference's ILU (--precond hmg: the hierarchy multigrid for every method and order)
-      if (use_mg && per.empty() && ((P.lin_method == 2 && P.k == P.kp && forest_mode != 1) || forest_mode == 2))
+      // method = amg (ML's multilevel hierarchy): the geometric one of the triangulation, every order (Q2-Q1
+      // levels smooth with multicolor ILU(0), equal order with damped Jacobi); gmres keeps the reference's ILU
+      // (--precond hmg: the hierarchy multigrid for every method)
+      if (use_mg && per.empty() && ((P.lin_method == 2 && forest_mode != 1) || forest_mode == 2))
         attach_umesh_mg();
     }
     alloc_vectors();

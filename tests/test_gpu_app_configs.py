@@ -215,18 +215,20 @@ def test_configs3_taylor_couette3d_kelly_hierarchy_multigrid(tmp_path):
     the refinement threshold depends on the inexact solves, as with the shipped cylinder_gls settings)."""
     prm = open(os.path.join(CASES, "taylor-couette3d_q2q1_kelly.prm")).read()
     its = {}
-    for pc in ("mg", "hmg"):
+    # the prm's method = amg runs the hierarchy multigrid by default (the ML hierarchy substituted);
+    # --precond ilu forces the ILU that ML would smooth with, for the comparison
+    for pc in ("ilu", "mg", "hmg"):
         d = tmp_path / pc
         d.mkdir()
         out, dumps = run_app(d, prm, extra=("--precision", "9", "--precond", pc))
         err = (d / "stderr.txt").read_text()
-        if pc == "hmg":
-            assert "triangulation's refinement hierarchy" in err, err[-1500:]
-            check_configs3_pipeline(out, dumps, 1e-8)
-        else:
+        if pc == "ilu":
             assert "refinement hierarchy" not in err
+        else:
+            assert "triangulation's refinement hierarchy" in err and "ML AMG substituted" in err, err[-1500:]
+            check_configs3_pipeline(out, dumps, 1e-8)
         its[pc] = [l for l in out.splitlines() if "linear_iterations =" in l]
-    print("configs[3] GMRES totals: ILU %s, hierarchy GMG %s" % (its["mg"], its["hmg"]))
+    print("configs[3] GMRES totals: ILU %s, amg -> hierarchy GMG %s, --precond hmg %s" % (its["ilu"], its["mg"], its["hmg"]))
 
 
 @pytest.mark.gpu
