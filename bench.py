@@ -462,6 +462,8 @@ def bench_octree(args):
                    "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing), rel %g"
                                      % (args.restart, args.mg_smooth[0], args.mg_smooth[1], len(prob.levels),
                                         "multicolor ILU(0)" if args.oct_smoother == "ilu" else
+                                        "multicolor ILU(0) below the finest, damped-Jacobi FP32 brick J.v on it"
+                                        if args.oct_smoother == "ilu-coarse" else
                                         ("damped-Jacobi, FP32 brick J.v" if args.mg_precision == "f32" else "damped-Jacobi FP64"),
                                         args.rel))
                    if mg else "GMRES(%d)+ILU(0) multicolor, rel %g" % (args.restart, args.rel)},
@@ -609,7 +611,7 @@ def main():
     ap.add_argument("--cyl-refine", type=int, default=0, help="cylinder3d: global refinements of the mesh")
     ap.add_argument("--cyl-precond", default="ilu", choices=["ilu", "hmg"],
                     help="cylinder3d: ILU(fill) or the multigrid on the refinement hierarchy (needs --cyl-refine)")
-    ap.add_argument("--oct-smoother", default="jacobi", choices=["jacobi", "ilu"],
+    ap.add_argument("--oct-smoother", default="jacobi", choices=["jacobi", "ilu", "ilu-coarse"],
                     help="octree --precond mg: level smoother (damped Jacobi with FP32 brick J.v, or multicolor ILU(0))")
     ap.add_argument("--cyl-smoother", default="ilu", choices=["ilu", "jacobi"],
                     help="cylinder3d --cyl-precond hmg: level smoother (ILU(0) V(1,1) or damped Jacobi V(2,2))")

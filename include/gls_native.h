@@ -223,7 +223,9 @@ typedef struct {
                                                  probed Jacobian, undamped (the smoother Trilinos ML
                                                  uses under the reference's AMG, gls_navier_stokes.cc:
                                                  1208-1226); levels with hanging nodes only
-                                                 (gls_mg_attach_transfers) */
+                                                 (gls_mg_attach_transfers); 2: ILU(0) on the coarser
+                                                 levels, damped Jacobi on the finest (its FP32 brick
+                                                 J.v with mixed_precision) */
   int smoother_operator;                      /* 0: the levels' Newton Jacobian; 1: its Oseen (Picard)
                                                  linearization on the FP32 brick levels (no (grad u) v
                                                  terms, no SUPG tau (v . grad phi) R_s term): cheaper

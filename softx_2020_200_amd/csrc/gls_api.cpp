@@ -3223,9 +3223,9 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
     if (p->smoother_operator < 0 || p->smoother_operator > 1) return set_err(GLS_EINVAL, "mg: smoother_operator 0 or 1");
     for (auto *g : mg.lev) g->smooth_oseen = os && g->smooth_f32;
   }
-  mg.ilu_smooth = p->smoother == 1;
-  if (p->smoother < 0 || p->smoother > 1 || (mg.ilu_smooth && !mg.csr))
-    return set_err(GLS_EINVAL, "mg: smoother 0 (Jacobi) or 1 (ILU, gls_mg_attach_transfers hierarchies)");
+  mg.ilu_smooth = p->smoother == 1 || p->smoother == 2;
+  if (p->smoother < 0 || p->smoother > 2 || (mg.ilu_smooth && !mg.csr))
+    return set_err(GLS_EINVAL, "mg: smoother 0 (Jacobi), 1 (ILU) or 2 (ILU below the finest level; gls_mg_attach_transfers hierarchies)");
   for (int l = 0; l < p->n_levels; ++l)
     for (int b = 0; b < MB_N; ++b) {
       mg.bufs.emplace_back(new DevBuf<double>());
@@ -3233,8 +3233,8 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       if (need)
         GLS_TRY(mg.bufs.back()->alloc(b == MB_BOX && mg.boxed ? (size_t)(4 * mg_nbox(c, l)) : (size_t)mg.lev[l]->n_dofs));
     }
-  if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (multicolor order)
-    for (int l = 0; l + 1 < p->n_levels; ++l) {
+  if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (multicolor order); smoother 2: not the finest
+    for (int l = p->smoother == 2 ? 1 : 0; l + 1 < p->n_levels; ++l) {
       gls_ctx *g = mg.lev[(size_t)l];
       // multicolor order on every level (GLS_MG_ILU_MC_MIN: the level size from which it is used; Cuthill-McKee
       // below). As a smoother the color-by-color ILU(0) is both faster per sweep (no level-scheduled csrsv) and

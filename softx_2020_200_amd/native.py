@@ -790,7 +790,7 @@ class GLSContext:
         ws = (PD * len(keep))(*[k[2].ctypes.data_as(PD) for k in keep])
         injs = (P64 * len(keep))(*[k[3].ctypes.data_as(P64) for k in keep])
         p = MGParams(len(levels), C.cast(arr, C.POINTER(C.c_void_p)), pre_smooth, post_smooth, coarse_sweeps, omega,
-                     coarse_omega, coarse_direct, int(mixed_precision), ls, {"jacobi": 0, "ilu": 1}[smoother])
+                     coarse_omega, coarse_direct, int(mixed_precision), ls, {"jacobi": 0, "ilu": 1, "ilu-coarse": 2}[smoother])
         check(self.L.gls_mg_attach_transfers(self.h, C.byref(p), offs, cols, ws, injs), "gls_mg_attach_transfers")
         self._mg_levels = levels
 
