@@ -259,6 +259,46 @@ def cpu_newton(k, kp, n, nu, scheme, dt, threads):
     return st
 
 
+def general_context(sp, bcs, nu, state, k=2, kp=1):
+    """A GLS context on a general (mapped) FE space: bcs = [(type, boundary id, values)] in prm order, type
+    noslip / function (values: X -> (n, 3)) / slip on an axis-aligned wall (the normal component, as
+    compute_no_normal_flux_constraints there); state: X -> (n, 3) synthetic velocity, Dirichlet values applied."""
+    from softx_2020_200_amd.native import GLSContext
+    nv, X, bid = sp["n_vnodes"], sp["vnode_x"], sp["vnode_bid"].astype(np.int64)
+    con = np.zeros((nv, 3), dtype=bool)
+    val = np.zeros((nv, 3))
+    scale = float(np.abs(X).max())
+    for typ, b, fn in bcs:
+        on = ((bid >> b) & 1).astype(bool)
+        comps = np.ones(3, dtype=bool)
+        if typ == "slip":
+            flat = [d for d in range(3) if len(np.unique(np.round(X[on, d] / (1e-9 * scale)))) <= 2]
+            comps = np.array([d == flat[0] for d in range(3)])
+        vals = fn(X) if typ == "function" else np.zeros((nv, 3))
+        for c in range(3):
+            if not comps[c]:
+                continue
+            sel = on & ~con[:, c]
+            con[sel, c] = True
+            val[sel, c] = vals[sel, c]
+    mask = (con[:, 0] * 1 + con[:, 1] * 2 + con[:, 2] * 4).astype(np.uint8)
+    ctx = GLSContext(3, k, kp, sp["cell_vnodes"], sp["cell_pnodes"], None, nv, sp["n_pnodes"], viscosity=nu,
+                     vnode_mask=mask, map_degree=k, cell_support=sp["cell_support"])
+    dofs = np.nonzero(con.reshape(-1))[0].astype(np.int64)
+    ctx.set_dirichlet(dofs, val.reshape(-1)[dofs])
+    x = np.concatenate([state(X).reshape(-1), np.zeros(sp["n_pnodes"])])
+    x[dofs] = val.reshape(-1)[dofs]
+    return ctx, sp, x
+
+
+def cylinder3d_mesh(refine=0):
+    from softx_2020_200_amd.native import UMesh
+    m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
+    if refine:
+        m.refine_global(refine)
+    return m
+
+
 def cylinder3d_context(k=2, kp=1, nu=0.005, refine=0, space=None):
     """BASELINE configs[4]'s discrete problem on one GPU (apps/cases/cylinder3d_q2q1_re200_kelly.prm):
     the reference's cylinder_structured.msh extruded to 3D (4 layers, apps/cases/cylinder3d_extruded.msh),
@@ -266,74 +306,78 @@ def cylinder3d_context(k=2, kp=1, nu=0.005, refine=0, space=None):
     order: id 0 noslip (cylinder), id 1 u = (1, 0, 0) (inlet), slip on the planar ids 2, 4, 5 (n.u = 0,
     the normal component; compute_no_normal_flux_constraints on axis-aligned walls). refine: global
     refinements of the mesh (flat: no manifold on the extruded gmsh mesh); space: that FE space given."""
-    from softx_2020_200_amd.native import GLSContext, UMesh
-    if space is None:
-        m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
-        if refine:
-            m.refine_global(refine)
-        space = m.fe_space(k, kp)
-    sp = space
-    nv, X, bid = sp["n_vnodes"], sp["vnode_x"], sp["vnode_bid"].astype(np.int64)
-    con = np.zeros((nv, 3), dtype=bool)
-    val = np.zeros((nv, 3))
-    scale = float(np.abs(X).max())
-    for typ, b in (("noslip", 0), ("function", 1), ("slip", 2), ("slip", 4), ("slip", 5)):
-        on = ((bid >> b) & 1).astype(bool)
-        comps = np.ones(3, dtype=bool)
-        if typ == "slip":
-            flat = [d for d in range(3) if len(np.unique(np.round(X[on, d] / (1e-9 * scale)))) <= 2]
-            comps = np.array([d == flat[0] for d in range(3)])
-        for c in range(3):
-            if not comps[c]:
-                continue
-            sel = on & ~con[:, c]
-            con[sel, c] = True
-            val[sel, c] = 1.0 if (typ == "function" and c == 0) else 0.0
-    mask = (con[:, 0] * 1 + con[:, 1] * 2 + con[:, 2] * 4).astype(np.uint8)
-    ctx = GLSContext(3, k, kp, sp["cell_vnodes"], sp["cell_pnodes"], None, nv, sp["n_pnodes"], viscosity=nu,
-                     vnode_mask=mask, map_degree=k, cell_support=sp["cell_support"])
-    dofs = np.nonzero(con.reshape(-1))[0].astype(np.int64)
-    ctx.set_dirichlet(dofs, val.reshape(-1)[dofs])
-    # synthetic state: the free stream with a smooth wake-like perturbation, Dirichlet values applied
-    r2 = X[:, 0] ** 2 + X[:, 1] ** 2
-    vel = np.zeros((nv, 3))
-    vel[:, 0] = 1.0 - np.exp(-r2 / 4.0) * (1.0 + 0.2 * np.sin(X[:, 2]))
-    vel[:, 1] = 0.1 * np.exp(-r2 / 4.0) * X[:, 1]
-    x = np.concatenate([vel.reshape(-1), np.zeros(sp["n_pnodes"])])
-    x[dofs] = val.reshape(-1)[dofs]
-    return ctx, sp, x
+    sp = space if space is not None else cylinder3d_mesh(refine).fe_space(k, kp)
+    inlet = lambda X: np.stack([np.ones(len(X)), 0 * X[:, 0], 0 * X[:, 0]], 1)  # noqa: E731
+
+    def state(X):  # the free stream with a smooth wake-like perturbation
+        r2 = X[:, 0] ** 2 + X[:, 1] ** 2
+        vel = np.zeros((len(X), 3))
+        vel[:, 0] = 1.0 - np.exp(-r2 / 4.0) * (1.0 + 0.2 * np.sin(X[:, 2]))
+        vel[:, 1] = 0.1 * np.exp(-r2 / 4.0) * X[:, 1]
+        return vel
+    return general_context(sp, [("noslip", 0, None), ("function", 1, inlet), ("slip", 2, None), ("slip", 4, None),
+                                ("slip", 5, None)], nu, state, k, kp)
+
+
+def taylorcouette3d_mesh(refine=1):
+    from softx_2020_200_amd.native import UMesh
+    m = UMesh(3, "cylinder_shell", "1 : 0.25 : 1 : 8 : 2")
+    m.refine_global(refine)
+    return m
+
+
+def taylorcouette3d_context(space, k=2, kp=1, nu=1.0):
+    """BASELINE configs[3]'s discrete problem (apps/cases/taylor-couette3d_q2q1_kelly.prm): cylinder_shell
+    (inner radius 0.25, outer 1, length 1) with its cylindrical manifold, Q2-Q1 with MappingQ2 on every cell
+    (qmapping all), nu = 1, steady; id 0 (inner) u = (-y, x, 0), id 1 noslip, slip end caps ids 2, 3."""
+    rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)  # noqa: E731
+
+    def state(X):  # the Couette profile u_theta(r) with an axial modulation
+        r = np.sqrt(X[:, 0] ** 2 + X[:, 1] ** 2)
+        eta, ri = 0.25, 0.25
+        ut = (-(eta ** 2) / (1 - eta ** 2) * r + ri ** 2 / (1 - eta ** 2) / r) * (1.0 + 0.1 * np.sin(np.pi * X[:, 2]))
+        th = np.arctan2(X[:, 1], X[:, 0])
+        return np.stack([-np.sin(th) * ut, np.cos(th) * ut, 0.02 * np.sin(np.pi * X[:, 2]) * (1 - r)], 1)
+    return general_context(space, [("function", 0, rot), ("noslip", 1, None), ("slip", 2, None), ("slip", 3, None)],
+                           nu, state, k, kp)
 
 
 def bench_cylinder3d(args):
     """--workload cylinder3d: one Newton iteration per step of BDF2 on configs[4]'s problem (single
     GPU, unadapted extruded mesh): residual, ILU(0) setup (probe + factor, multicolor order) and
-    GMRES(30)+ILU to rel 1e-4, line search; the per-cell J.v kernel's roofline."""
+    GMRES(30)+ILU to rel 1e-4, line search; the per-cell J.v kernel's roofline. --workload taylorcouette3d:
+    the same on configs[3]'s problem (steady, cylinder_shell refined --cyl-refine + 1 times)."""
     import torch
     t_setup = time.perf_counter()
+    tc = args.workload == "taylorcouette3d"
+    scheme, ts = ("steady", (0.0,) * 4) if tc else ("bdf2", (0.05,) * 4)
+    refine = args.cyl_refine + (1 if tc else 0)  # configs[3]'s prm starts from one global refinement
+    mesh = (lambda r: taylorcouette3d_mesh(r)) if tc else (lambda r: cylinder3d_mesh(r))
+    make = (lambda sp_: taylorcouette3d_context(sp_)) if tc else (lambda sp_: cylinder3d_context(space=sp_))
+    qall = tc  # configs[3]: MappingQ2 on every cell
     levels, sw = None, 0
-    if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh (--cyl-refine >= 1)
-        from softx_2020_200_amd.native import UMesh
-        if args.cyl_refine < 1:
+    if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh
+        if refine < 1:
             sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 (a hierarchy below the fine mesh)")
-        m = UMesh(3, gmsh=os.path.join(ROOT, "apps", "cases", "cylinder3d_extruded.msh"))
-        m.refine_global(args.cyl_refine)
-        handles = [m.fe_space_handle(2, 1)] + [m.coarsen_to(args.cyl_refine - l).fe_space_handle(2, 1)
-                                               for l in range(1, args.cyl_refine + 1)]
-        xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(args.cyl_refine)]
-        levels = [cylinder3d_context(space=h.data) for h in handles]
+        m = mesh(refine)
+        handles = [m.fe_space_handle(2, 1, qmapping_all=qall)] + [
+            m.coarsen_to(refine - l).fe_space_handle(2, 1, qmapping_all=qall) for l in range(1, refine + 1)]
+        xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(refine)]
+        levels = [make(h.data) for h in handles]
         ctx, sp, x = levels[0]
         for c_, _, _ in levels:
-            c_.set_time("bdf2", (0.05,) * 4)
+            c_.set_time(scheme, ts)
         sw = 1 if args.cyl_smoother == "ilu" else 2
+        nco = levels[-1][0].n_dofs
         ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
-                                       coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=0.6, coarse_direct=-1,
-                                       smoother=args.cyl_smoother)
+                                       coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=0.6,
+                                       coarse_direct=1 if nco <= 8192 else -1, smoother=args.cyl_smoother)
     else:
-        ctx, sp, x = cylinder3d_context(refine=args.cyl_refine)
-        ctx.set_time("bdf2", (0.05,) * 4)
+        ctx, sp, x = make(mesh(refine).fe_space(2, 1, qmapping_all=qall))
+        ctx.set_time(scheme, ts)
         ctx.attach_ilu(1e-5, 1.0, fill=args.ilu_fill, ordering="multicolor" if args.ilu_fill == 0 else "cm")
     dev = torch.device("cuda", 0)
-    ctx.set_time("bdf2", (0.05,) * 4)
+    ctx.set_time(scheme, ts)
     t_setup = time.perf_counter() - t_setup
     m1 = torch.from_numpy(x).to(dev)
     m2 = m1.clone()
@@ -369,19 +413,25 @@ def bench_cylinder3d(args):
     ms = jv_ms / max(jv_n, 1)
     its_per_s = args.steps / el
     out = {
-        "metric": "nonlinear iters/sec (3D cylinder Re 200, Q2-Q1 mapped, BDF2)", "value": its_per_s,
+        "metric": ("nonlinear iters/sec (3D Taylor-Couette, Q2-Q1 mapped, steady)" if tc else
+                   "nonlinear iters/sec (3D cylinder Re 200, Q2-Q1 mapped, BDF2)"), "value": its_per_s,
         "unit": "nonlinear_iters/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (free stream with a smooth wake-like perturbation, prm boundary values)",
-        "config": {"workload": "BASELINE configs[4] problem on one GPU: apps/cases/cylinder3d_extruded.msh "
+        "dtype": "f64", "data": ("synthetic (Couette profile with an axial modulation, prm boundary values)" if tc else
+                                 "synthetic (free stream with a smooth wake-like perturbation, prm boundary values)"),
+        "config": {"workload": ("BASELINE configs[3] problem on one GPU: cylinder_shell 1:0.25:1:8:2 refined %d times "
+                                "globally (cylindrical manifold), Q2-Q1 MappingQ2 on every cell, nu 1, steady" % refine)
+                   if tc else ("BASELINE configs[4] problem on one GPU: apps/cases/cylinder3d_extruded.msh "
                                "(unadapted%s), Q2-Q1 MappingQ2, nu 0.005, BDF2 dt 0.05" % (
-                                   ", %d global refinements (flat)" % args.cyl_refine if args.cyl_refine else ""),
+                                   ", %d global refinements (flat)" % args.cyl_refine if args.cyl_refine else "")),
                    "n_dofs": N, "n_cells": nc,
                    "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing, "
-                                     "%d sweeps on the base mesh), rel 1e-4" % (
+                                     "%s on the base mesh), rel 1e-4" % (
                                          args.restart, sw, sw, len(levels),
-                                         "ILU(0)" if args.cyl_smoother == "ilu" else "damped-Jacobi",
-                                         args.mg_coarse_sweeps_cyl))
+                                         {"ilu": "multicolor ILU(0)", "jacobi": "damped-Jacobi",
+                                          "ilu-coarse": "damped-Jacobi on the finest, multicolor ILU(0) below"}[
+                                             args.cyl_smoother],
+                                         "exact LU" if levels[-1][0].n_dofs <= 8192 else "%d sweeps" % args.mg_coarse_sweeps_cyl))
                    if levels else "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
                        args.restart, args.ilu_fill, "multicolor" if args.ilu_fill == 0 else "Cuthill-McKee")},
         "setup_s": t_setup,
@@ -593,7 +643,7 @@ def preflight(args, rank, world, dev, dist):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="cavity", choices=["cavity", "cylinder3d", "octree"],
+    ap.add_argument("--workload", default="cavity", choices=["cavity", "cylinder3d", "taylorcouette3d", "octree"],
                     help="cavity: the BASELINE metric (configs[1] / [2]); cylinder3d: configs[4]'s adaptive-path "
                          "problem on one GPU (per-cell mapped kernels + ILU-GMRES)")
     ap.add_argument("--steps", type=int, default=3)
@@ -613,7 +663,7 @@ def main():
                     help="cylinder3d: ILU(fill) or the multigrid on the refinement hierarchy (needs --cyl-refine)")
     ap.add_argument("--oct-smoother", default="jacobi", choices=["jacobi", "ilu", "ilu-coarse"],
                     help="octree --precond mg: level smoother (damped Jacobi with FP32 brick J.v, or multicolor ILU(0))")
-    ap.add_argument("--cyl-smoother", default="ilu", choices=["ilu", "jacobi"],
+    ap.add_argument("--cyl-smoother", default="ilu", choices=["ilu", "jacobi", "ilu-coarse"],
                     help="cylinder3d --cyl-precond hmg: level smoother (ILU(0) V(1,1) or damped Jacobi V(2,2))")
     ap.add_argument("--mg-coarse-sweeps-cyl", type=int, default=10,
                     help="cylinder3d --cyl-precond hmg: ILU sweeps on the base (coarsest) mesh")
@@ -671,12 +721,12 @@ def main():
         sys.exit(1)
     if env_world is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
-    if args.workload in ("cylinder3d", "octree") and args.gpus > 1:
+    if args.workload in ("cylinder3d", "taylorcouette3d", "octree") and args.gpus > 1:
         sys.exit("bench.py: --workload %s runs on one GPU" % args.workload)
-    if args.workload in ("cylinder3d", "octree"):
+    if args.workload in ("cylinder3d", "taylorcouette3d", "octree"):
         import torch
         torch.cuda.set_device(0)
-        return bench_cylinder3d(args) if args.workload == "cylinder3d" else bench_octree(args)
+        return bench_octree(args) if args.workload == "octree" else bench_cylinder3d(args)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -4462,6 +4462,9 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       std::sort(buf.begin(), buf.end());
       acol.insert(acol.end(), buf.begin(), buf.end());
       aoff[(size_t)i + 1] = (int64_t)acol.size();
+      if (aoff[(size_t)i + 1] >= INT32_MAX)  // the factored CSR is 32-bit (rocSPARSE / the multicolor kernels)
+        return set_err(GLS_EINVAL, "gls_ilu_attach: the matrix has more than %d entries (32-bit CSR): use the "
+                                   "multigrid (or damped-Jacobi smoothing on this level)", INT32_MAX);
     }
   }
   // node graph of that pattern (x ~ y when a row of x holds a DoF of y) for the distance-2 coloring
