@@ -447,6 +447,19 @@ int gls_gpart_get(const gls_gpart *p, int32_t *local_cell_vnodes, int32_t *local
                   int32_t *recv_dofs);
 int gls_gpart_map_dofs(const gls_gpart *p, int64_t n, const int64_t *global_dofs, int64_t *local_dofs);
 int gls_gpart_destroy(gls_gpart *p);
+/* The same plan from the rank's LOCAL PART only (distributed forest: no rank holds the global mesh;
+ * the p::d triangulation's locally relevant cells, navier_stokes_base.cc:55-60): the owned cells
+ * (cell_owner == rank, in the given order) plus the ghost layer -- every cell sharing a node with an
+ * owned cell or linked to one through a hanging line (a line DoF on one cell, a master on the other) --
+ * each with its owner; the lines whose DoF lies on a provided cell. Nodes are 64-bit keys unique over
+ * the forest (no global numbering needed); DoF keys are key * (dim + 1) + c with c = dim for pressure
+ * (line_dofs / line_masters and gls_gpart_map_dofs use DoF keys). cell_pkeys = NULL for equal order.
+ * vnode_l2g / pnode_l2g of gls_gpart_get return the local nodes' keys; the exchange lists are those of
+ * gls_gpart_create for the same partition (identical arrays when the keys are the global node ids).
+ * A global numbering, if wanted, is one exclusive scan of the owned counts plus one exchange. */
+int gls_dpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cell_owner, const int64_t *cell_vkeys,
+                     const int64_t *cell_pkeys, int64_t n_lines, const int64_t *line_dofs, const int64_t *line_offsets,
+                     const int64_t *line_masters, int rank, int world, gls_gpart **out);
 int gls_dist_attach_dofs(gls_ctx *ctx, int64_t n_owned_vnodes, int64_t n_owned_pnodes, int n_nbrs,
                          const int64_t *send_offsets, const int32_t *send_dofs, const int64_t *recv_offsets,
                          const int32_t *recv_dofs, double *send_buf, double *recv_buf, double *red_buf,

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/gls_native.h"
@@ -377,6 +378,214 @@ int gls_gpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cel
   std::vector<int> nb;
   for (auto &kv : send) nb.push_back(kv.first);
   for (auto &kv : recv) nb.push_back(kv.first);
+  std::sort(nb.begin(), nb.end());
+  nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+  p->nbrs = nb;
+  p->send_off.assign(1, 0);
+  p->recv_off.assign(1, 0);
+  for (int r : nb) {
+    auto its = send.find(r);
+    if (its != send.end()) p->send_dofs.insert(p->send_dofs.end(), its->second.begin(), its->second.end());
+    p->send_off.push_back((int64_t)p->send_dofs.size());
+    auto itr = recv.find(r);
+    if (itr != recv.end()) p->recv_dofs.insert(p->recv_dofs.end(), itr->second.begin(), itr->second.end());
+    p->recv_off.push_back((int64_t)p->recv_dofs.size());
+  }
+  *out = p.release();
+  return GLS_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same plan from the rank's LOCAL PART of a distributed forest (no global mesh on the rank):
+// the owned cells plus the ghost layer -- every cell coupled to an owned cell, where two cells are
+// coupled when they share a node or one carries a hanging line whose master is a node of the other
+// (p4est's ghost layer with corner connectivity, extended by the line closure; the p::d triangulation's
+// locally relevant cells, navier_stokes_base.cc:55-60) -- each with its owner rank, and the lines whose
+// DoF sits on a provided cell. Nodes are named by 64-bit keys unique across the forest (the global
+// node id, or a lattice / vertex key; no global numbering is needed); a DoF is key * (dim + 1) + c,
+// c = dim for pressure. Why the part is enough: a node an owned cell touches has all its cells coupled
+// to that owned cell, so "lowest rank touching it" is exact for every DoF this rank holds, and any other
+// rank's cell needing a DoF this rank owns is coupled to the owned cell touching that DoF, so both
+// exchange lists come out of the part alone, in the same order on both sides ((velocity before
+// pressure, key, component) order, which equals gls_gpart_create's global-id order when keys are global
+// ids). Owned cells are the provided cells with owner == rank, in the given order. The result is a
+// gls_gpart handle: gls_gpart_sizes / _get (vnode_l2g / pnode_l2g hold keys) / _map_dofs (DoF keys).
+// ---------------------------------------------------------------------------------------------
+int gls_dpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cell_owner, const int64_t *cell_vkeys,
+                     const int64_t *cell_pkeys, int64_t n_lines, const int64_t *line_dofs, const int64_t *line_off,
+                     const int64_t *line_masters, int rank, int world, gls_gpart **out) {
+  if (!out || (dim != 2 && dim != 3) || k < 1 || kp < 1 || n_cells < 0 || (n_cells > 0 && (!cell_owner || !cell_vkeys)) ||
+      world < 1 || rank < 0 || rank >= world || n_lines < 0 || (n_lines > 0 && (!line_dofs || !line_off || !line_masters)))
+    return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: bad arguments");
+  std::unique_ptr<gls_gpart> p(new gls_gpart);
+  p->dim = dim;
+  p->nvl = 1;
+  p->npl = 1;
+  for (int d = 0; d < dim; ++d) {
+    p->nvl *= k + 1;
+    p->npl *= kp + 1;
+  }
+  p->sep = cell_pkeys != nullptr;
+  if (!p->sep && kp != k) return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: equal-order meshes share their nodes");
+  const int nvl = p->nvl, npl = p->npl, D1 = dim + 1;
+  const int64_t kmax = INT64_MAX / D1 - 1;
+  // owners of every node on a provided cell: the lowest rank touching it
+  std::unordered_map<int64_t, int32_t> vown, pown;
+  vown.reserve((size_t)(n_cells * 4 + 16));
+  auto touch = [](std::unordered_map<int64_t, int32_t> &m, int64_t key, int32_t r) {
+    auto it = m.find(key);
+    if (it == m.end()) m.emplace(key, r);
+    else if (r < it->second) it->second = r;
+  };
+  int64_t n_owned_cells = 0;
+  for (int64_t c = 0; c < n_cells; ++c) {
+    const int32_t r = cell_owner[c];
+    if (r < 0 || r >= world) return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: cell owner out of range");
+    n_owned_cells += r == rank;
+    for (int a = 0; a < nvl; ++a) {
+      const int64_t key = cell_vkeys[c * nvl + a];
+      if (key < 0 || key > kmax) return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: node key out of range");
+      touch(vown, key, r);
+    }
+    if (p->sep)
+      for (int a = 0; a < npl; ++a) {
+        const int64_t key = cell_pkeys[c * npl + a];
+        if (key < 0 || key > kmax) return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: pressure key out of range");
+        touch(pown, key, r);
+      }
+  }
+  // DoF order: velocity before pressure, then key, then component (= DoF key order within each kind)
+  auto is_p = [D1, dim](int64_t g) { return g % D1 == dim; };
+  auto dof_less = [&](int64_t a, int64_t b) { return is_p(a) != is_p(b) ? !is_p(a) : a < b; };
+  // owner of a DoF (-1: no provided cell touches its node -- not this rank's, whoever owns it)
+  auto dof_owner = [&](int64_t g) -> int32_t {
+    const std::unordered_map<int64_t, int32_t> &m = (is_p(g) && p->sep) ? pown : vown;
+    auto it = m.find(g / D1);
+    return it == m.end() ? -1 : it->second;
+  };
+  std::unordered_map<int64_t, int64_t> lidx;
+  for (int64_t i = 0; i < n_lines; ++i) {
+    if (line_dofs[i] < 0) return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: line DoF key");
+    lidx[line_dofs[i]] = i;
+  }
+  // the DoFs the cells of rank r (among the provided ones) need: their own and their lines' masters
+  auto needed = [&](int r, std::vector<int64_t> &dofs) {
+    dofs.clear();
+    for (int64_t c = 0; c < n_cells; ++c) {
+      if (cell_owner[c] != r) continue;
+      for (int a = 0; a < nvl; ++a) {
+        const int64_t key = cell_vkeys[c * nvl + a];
+        for (int cc = 0; cc < dim; ++cc) dofs.push_back(key * D1 + cc);
+        if (!p->sep) dofs.push_back(key * D1 + dim);
+      }
+      if (p->sep)
+        for (int a = 0; a < npl; ++a) dofs.push_back(cell_pkeys[c * npl + a] * D1 + dim);
+    }
+    std::sort(dofs.begin(), dofs.end());
+    dofs.erase(std::unique(dofs.begin(), dofs.end()), dofs.end());
+    const size_t nc = dofs.size();
+    for (size_t t = 0; t < nc; ++t) {
+      auto it = lidx.find(dofs[t]);
+      if (it == lidx.end()) continue;
+      for (int64_t j = line_off[it->second]; j < line_off[it->second + 1]; ++j) dofs.push_back(line_masters[j]);
+    }
+    std::sort(dofs.begin(), dofs.end(), dof_less);
+    dofs.erase(std::unique(dofs.begin(), dofs.end()), dofs.end());
+  };
+  std::vector<int64_t> mine;
+  needed(rank, mine);
+  for (int64_t g : mine)
+    if (dof_owner(g) < 0)
+      return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: a line master lies on no provided cell (the ghost "
+                                              "layer must include the cells coupled through hanging lines)");
+  // local nodes (a node's DoFs come together): owned first by key, then ghosts by (owner, key)
+  std::vector<int64_t> vown_l, vgh_l, pown_l, pgh_l;
+  {
+    std::unordered_map<int64_t, char> vseen, pseen;
+    for (int64_t g : mine) {
+      const int64_t key = g / D1;
+      const bool pres = is_p(g) && p->sep;
+      auto &seen = pres ? pseen : vseen;
+      if (seen.emplace(key, 1).second) {
+        const bool own = dof_owner(g) == rank;
+        (pres ? (own ? pown_l : pgh_l) : (own ? vown_l : vgh_l)).push_back(key);
+      }
+    }
+  }
+  auto order_nodes = [&](std::vector<int64_t> &own, std::vector<int64_t> &gh, const std::unordered_map<int64_t, int32_t> &ow,
+                         std::vector<int64_t> &l2k) {
+    std::sort(own.begin(), own.end());
+    std::sort(gh.begin(), gh.end(), [&](int64_t a, int64_t b) {
+      const int32_t oa = ow.at(a), ob = ow.at(b);
+      return oa != ob ? oa < ob : a < b;
+    });
+    l2k = own;
+    l2k.insert(l2k.end(), gh.begin(), gh.end());
+  };
+  order_nodes(vown_l, vgh_l, vown, p->vl2g);
+  p->n_owned_v = (int64_t)vown_l.size();
+  if (p->sep) {
+    order_nodes(pown_l, pgh_l, pown, p->pl2g);
+    p->n_owned_p = (int64_t)pown_l.size();
+  } else {
+    p->n_owned_p = p->n_owned_v;
+  }
+  const int64_t nvloc = (int64_t)p->vl2g.size();
+  if (nvloc > INT32_MAX || n_owned_cells * nvl > INT32_MAX)
+    return gls_internal_set_err(GLS_EINVAL, "gls_dpart_create: the local part exceeds 32-bit node ids");
+  std::unordered_map<int64_t, int32_t> vk2l, pk2l;
+  for (int64_t i = 0; i < nvloc; ++i) vk2l[p->vl2g[(size_t)i]] = (int32_t)i;
+  for (size_t i = 0; i < p->pl2g.size(); ++i) pk2l[p->pl2g[i]] = (int32_t)i;
+  auto k2l_dof = [&](int64_t g) -> int64_t {
+    const int64_t key = g / D1;
+    const int c = (int)(g % D1);
+    if (c < dim) return (int64_t)vk2l.at(key) * dim + c;
+    return (int64_t)dim * nvloc + (p->sep ? pk2l.at(key) : vk2l.at(key));
+  };
+  // owned cells, in the given order
+  p->cell_begin = 0;
+  p->cell_end = n_owned_cells;
+  p->local_cv.reserve((size_t)(n_owned_cells * nvl));
+  if (p->sep) p->local_cp.reserve((size_t)(n_owned_cells * npl));
+  for (int64_t c = 0; c < n_cells; ++c) {
+    if (cell_owner[c] != rank) continue;
+    for (int a = 0; a < nvl; ++a) p->local_cv.push_back(vk2l.at(cell_vkeys[c * nvl + a]));
+    if (p->sep)
+      for (int a = 0; a < npl; ++a) p->local_cp.push_back(pk2l.at(cell_pkeys[c * npl + a]));
+  }
+  // DoF key -> local DoF (for gls_gpart_map_dofs)
+  {
+    std::vector<std::pair<int64_t, int64_t>> kv;
+    kv.reserve(mine.size());
+    for (int64_t g : mine) kv.push_back({g, k2l_dof(g)});
+    std::sort(kv.begin(), kv.end());
+    for (auto &e : kv) {
+      p->gdof2l_keys.push_back(e.first);
+      p->gdof2l_vals.push_back(e.second);
+    }
+  }
+  // exchange lists: recv = my ghost DoFs by owner; send = my owned DoFs the provided cells of each other rank need
+  std::map<int, std::vector<int32_t>> send, recv;
+  for (int64_t g : mine) {
+    const int32_t o = dof_owner(g);
+    if (o != rank) recv[o].push_back((int32_t)k2l_dof(g));
+  }
+  std::vector<int> others;
+  for (int64_t c = 0; c < n_cells; ++c)
+    if (cell_owner[c] != rank) others.push_back(cell_owner[c]);
+  std::sort(others.begin(), others.end());
+  others.erase(std::unique(others.begin(), others.end()), others.end());
+  std::vector<int64_t> theirs;
+  for (int s : others) {
+    needed(s, theirs);
+    std::vector<int32_t> lst;
+    for (int64_t g : theirs)
+      if (dof_owner(g) == rank) lst.push_back((int32_t)k2l_dof(g));
+    if (!lst.empty()) send[s] = lst;
+  }
+  std::vector<int> nb;
+  for (auto &e : send) nb.push_back(e.first);
+  for (auto &e : recv) nb.push_back(e.first);
   std::sort(nb.begin(), nb.end());
   nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
   p->nbrs = nb;

@@ -47,6 +47,8 @@ def _bind(L):
     L.gls_gpart_get.argtypes = [vp, i32p, i32p, i64p, i64p, C.POINTER(C.c_int), i64p, i32p, i64p, i32p]
     L.gls_gpart_map_dofs.argtypes = [vp, i64, i64p, i64p]
     L.gls_gpart_destroy.argtypes = [vp]
+    L.gls_dpart_create.argtypes = [C.c_int, C.c_int, C.c_int, i64, i32p, i64p, i64p, i64, i64p, i64p, i64p, C.c_int,
+                                   C.c_int, C.POINTER(vp)]
     L.gls_dist_attach_dofs.argtypes = [vp, i64, i64, C.c_int, i64p, i32p, i64p, i32p, vp, vp, vp, EXCHANGE_FN,
                                        ALLREDUCE_FN, vp]
     L.gls_dist_attach_dofs_rccl.argtypes = [vp, vp, i64, i64, C.c_int, C.POINTER(C.c_int), i64p, i32p, i64p, i32p]
@@ -344,16 +346,29 @@ def gpartition(space, rank, world, lines=None):
     h = C.c_void_p()
     check(L.gls_gpart_create(dim, k, kp, cv.shape[0], p32(cv), p32(cp), nv, npn, len(ld), p64(ld), p64(lo), p64(lm),
                              rank, world, C.byref(h)), "gls_gpart_create")
+    out = _plan_from_handle(L, h, dim, cv.shape[1], cp.shape[1] if sep else None)
+    # global DoF ids of the local DoFs (velocity node*dim + c, pressure dim*NV + p)
+    g = np.concatenate([(out["vl2g"][:, None] * dim + np.arange(dim)[None, :]).reshape(-1), dim * nv + out["pl2g"]])
+    out["l2g_dofs"] = g
+    out["n_global_dofs"] = dim * nv + npn
+    return out
+
+
+def _plan_from_handle(L, h, dim, nvpc, npc):
+    """gls_gpart_sizes / _get into a plan dict (and destroy the handle); npc None = equal order"""
+    p64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64))  # noqa: E731
+    p32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else C.POINTER(C.c_int32)()  # noqa: E731
     try:
         cb, ce, nvl, npl, nov, nop, ns, nr = (C.c_int64() for _ in range(8))
         nn = C.c_int()
         check(L.gls_gpart_sizes(h, C.byref(cb), C.byref(ce), C.byref(nvl), C.byref(npl), C.byref(nov), C.byref(nop),
                                 C.byref(nn), C.byref(ns), C.byref(nr)), "gls_gpart_sizes")
         nc = ce.value - cb.value
+        sep = npc is not None
         out = dict(cell_begin=cb.value, cell_end=ce.value, n_vnodes=nvl.value, n_pnodes=npl.value,
                    n_owned_v=nov.value, n_owned_p=nop.value, dim=dim,
-                   local_cv=np.zeros((nc, cv.shape[1]), np.int32),
-                   local_cp=np.zeros((nc, cp.shape[1]), np.int32) if sep else None,
+                   local_cv=np.zeros((nc, nvpc), np.int32),
+                   local_cp=np.zeros((nc, npc), np.int32) if sep else None,
                    vl2g=np.zeros(nvl.value, np.int64), pl2g=np.zeros(npl.value, np.int64),
                    nbrs=np.zeros(nn.value, np.int32), send_off=np.zeros(nn.value + 1, np.int64),
                    send_dofs=np.zeros(ns.value, np.int32), recv_off=np.zeros(nn.value + 1, np.int64),
@@ -366,13 +381,154 @@ def gpartition(space, rank, world, lines=None):
             out["recv_off"] = np.zeros(1, np.int64)
         if not sep:
             out["local_cp"] = out["local_cv"]
-        # global DoF ids of the local DoFs (velocity node*dim + c, pressure dim*NV + p)
-        g = np.concatenate([(out["vl2g"][:, None] * dim + np.arange(dim)[None, :]).reshape(-1), dim * nv + out["pl2g"]])
-        out["l2g_dofs"] = g
-        out["n_global_dofs"] = dim * nv + npn
         return out
     finally:
         L.gls_gpart_destroy(h)
+
+
+# ---------------------------------------------------------------------------------------------------
+# Distributed forest: a rank's plan from its local part only (gls_dpart_create)
+# ---------------------------------------------------------------------------------------------------
+def _dof_node(g, dim, nv, sep):
+    """unified node id of global DoF ids (velocity nodes [0, nv), pressure nodes nv + p when separate)"""
+    g = np.asarray(g, np.int64)
+    nvd = dim * nv
+    return np.where(g < nvd, g // dim, (nv if sep else 0) + g - nvd)
+
+
+def _dof_key(g, dim, nv):
+    """DoF key (node key * (dim + 1) + c, c = dim for pressure) of global DoF ids, keys = global node ids"""
+    g = np.asarray(g, np.int64)
+    nvd = dim * nv
+    return np.where(g < nvd, (g // dim) * (dim + 1) + g % dim, (g - nvd) * (dim + 1) + dim)
+
+
+def local_part(space, rank, world, lines=None, dirichlet=None, vnode_mask=None, force_q=None):
+    """What a p::d triangulation hands rank `rank` of the forest `space` (the partitioner's hand-off; the rank
+    itself never sees the global arrays): its owned cells (the equal-count range of the space-filling cell
+    order) plus the ghost layer (every cell sharing a node with an owned cell or linked to one through a hanging
+    line), with owners, node keys (= global node ids), the lines on those cells in DoF keys, and the per-cell /
+    per-node data the rank's context needs (cell_support and force_q of the owned cells, vnode_mask and Dirichlet
+    rows on the provided nodes). Feeds dpartition / DistributedGeneralProblem(part=...)."""
+    dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])
+    sep = kp != k
+    cv = np.asarray(space["cell_vnodes"], np.int64)
+    cp = np.asarray(space["cell_pnodes"], np.int64) if sep else None
+    nv = int(space["n_vnodes"])
+    npn = int(space["n_pnodes"]) if sep else nv
+    nc = cv.shape[0]
+    cb = [nc * r // world for r in range(world + 1)]
+    owner = np.searchsorted(np.asarray(cb[1:]), np.arange(nc), side="right").astype(np.int32)
+    U = np.concatenate([cv, cp + nv], 1) if sep else cv
+    nun = nv + (npn if sep else 0)
+    S = np.zeros(nun, bool)
+    S[U[cb[rank]:cb[rank + 1]].ravel()] = True
+    if lines is not None and len(lines[0]):
+        ld, lo, lm = (np.asarray(a, np.int64) for a in lines[:3])
+        dn = _dof_node(ld, dim, nv, sep)
+        mn = _dof_node(lm, dim, nv, sep)
+        mline = np.repeat(np.arange(len(ld)), np.diff(lo))
+        add = np.zeros(nun, bool)
+        add[mn[S[dn[mline]]]] = True   # masters of the lines on the owned cells' nodes
+        add[dn[mline[S[mn]]]] = True   # DoF nodes of the lines whose master an owned cell touches
+        S |= add
+    prov = np.nonzero(S[U].any(1))[0]
+    nodes = np.zeros(nun, bool)
+    nodes[U[prov].ravel()] = True
+    part = dict(dim=dim, k=k, kp=kp, cell_owner=owner[prov], cell_vkeys=np.ascontiguousarray(cv[prov]),
+                cell_pkeys=np.ascontiguousarray(cp[prov]) if sep else None)
+    own = slice(cb[rank], cb[rank + 1])
+    if "cell_support" in space:
+        part["cell_support"] = np.ascontiguousarray(space["cell_support"][own])
+    if force_q is not None:
+        part["force_q"] = np.ascontiguousarray(np.asarray(force_q)[own])
+    if lines is not None and len(lines[0]):
+        ld, lo, lm = (np.asarray(a, np.int64) for a in lines[:3])
+        lw = np.asarray(lines[3]) if len(lines) > 3 else np.ones(len(lm))
+        keep = np.nonzero(nodes[_dof_node(ld, dim, nv, sep)])[0]
+        lens = np.diff(lo)[keep]
+        idx = np.repeat(lo[keep], lens) + (np.arange(lens.sum()) - np.repeat(np.cumsum(lens) - lens, lens))
+        part["lines"] = (_dof_key(ld[keep], dim, nv), np.concatenate([[0], np.cumsum(lens)]).astype(np.int64),
+                         _dof_key(lm[idx], dim, nv), lw[idx])
+    vk = np.nonzero(nodes[:nv])[0]
+    part["vnode_keys"] = vk
+    if vnode_mask is not None:
+        part["vnode_mask"] = np.ascontiguousarray(np.asarray(vnode_mask)[vk])
+    if dirichlet is not None:
+        gd, gv = (np.asarray(a) for a in dirichlet)
+        sel = nodes[_dof_node(gd, dim, nv, sep)]
+        part["dirichlet"] = (_dof_key(gd[sel], dim, nv), gv[sel])
+    return part
+
+
+def part_dof_keys(part):
+    """sorted DoF keys of every DoF on the part's provided cells"""
+    d1 = part["dim"] + 1
+    vk = np.unique(part["cell_vkeys"])
+    pk = np.unique(part["cell_pkeys"]) if part["cell_pkeys"] is not None else vk
+    return np.unique(np.concatenate([(vk[:, None] * d1 + np.arange(part["dim"])[None, :]).ravel(), pk * d1 + part["dim"]]))
+
+
+def dplan(part, rank, world):
+    """gls_dpart_create on the rank's local part: plan dict as gpartition's with the local nodes' keys (vl2k,
+    pl2k, l2k_dofs) in place of global ids."""
+    L = _bind(load())
+    dim, k, kp = int(part["dim"]), int(part["k"]), int(part["kp"])
+    owner = np.ascontiguousarray(part["cell_owner"], np.int32)
+    cv = np.ascontiguousarray(part["cell_vkeys"], np.int64)
+    cp = part["cell_pkeys"]
+    cp = np.ascontiguousarray(cp, np.int64) if cp is not None else None
+    lines = part.get("lines")
+    if lines is None or len(lines[0]) == 0:
+        ld, lo, lm = np.zeros(0, np.int64), np.zeros(1, np.int64), np.zeros(0, np.int64)
+    else:
+        ld, lo, lm = (np.ascontiguousarray(a, dtype=np.int64) for a in lines[:3])
+    p64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int64)) if a is not None else C.POINTER(C.c_int64)()  # noqa: E731
+    h = C.c_void_p()
+    check(L.gls_dpart_create(dim, k, kp, cv.shape[0], owner.ctypes.data_as(C.POINTER(C.c_int32)), p64(cv), p64(cp),
+                             len(ld), p64(ld), p64(lo), p64(lm), rank, world, C.byref(h)), "gls_dpart_create")
+    out = _plan_from_handle(L, h, dim, cv.shape[1], cp.shape[1] if cp is not None else None)
+    out["vl2k"], out["pl2k"] = out.pop("vl2g"), out.pop("pl2g")
+    d1 = dim + 1
+    out["l2k_dofs"] = np.concatenate([(out["vl2k"][:, None] * d1 + np.arange(dim)[None, :]).reshape(-1),
+                                      out["pl2k"] * d1 + dim])
+    return out
+
+
+def dpartition(part, rank, world, device="cpu", backend="gloo", group=None):
+    """dplan, then the distributed global numbering (deal.II's: each rank's owned DoFs one contiguous range, by an
+    all-reduce of the owned counts and one owner -> ghost exchange of the ghost DoFs' ids): adds l2g_dofs,
+    n_global_dofs (velocity node * dim + c, pressure dim * NV + node, as gpartition's)."""
+    import torch
+    out = dplan(part, rank, world)
+    dim = out["dim"]
+    # distributed numbering: owned counts -> offsets; owners send their ids to the ghosting ranks
+    dev = device if backend == "nccl" else "cpu"
+    cnt = torch.zeros(2 * world, dtype=torch.int64, device=dev)
+    cnt[2 * rank], cnt[2 * rank + 1] = out["n_owned_v"], out["n_owned_p"]
+    torch.distributed.all_reduce(cnt, group=group)
+    cnt = cnt.cpu().numpy().reshape(world, 2)
+    nv_g, np_g = int(cnt[:, 0].sum()), int(cnt[:, 1].sum())
+    voff, poff = int(cnt[:rank, 0].sum()), int(cnt[:rank, 1].sum())
+    nvl = out["n_vnodes"]
+    g = np.full(len(out["l2k_dofs"]), -1, np.int64)
+    nov, nop = out["n_owned_v"], out["n_owned_p"]
+    g[:dim * nov] = ((voff + np.arange(nov))[:, None] * dim + np.arange(dim)[None, :]).ravel()
+    g[dim * nvl:dim * nvl + nop] = dim * nv_g + poff + np.arange(nop)
+    ex = Exchanger(out, dev, backend=backend, group=group, width=1)
+    ns, nr = int(out["send_off"][-1]), int(out["recv_off"][-1])
+    if ns:
+        ex.send_buf[:ns] = torch.as_tensor(g[out["send_dofs"]].astype(np.float64), device=dev)
+    if ex._exchange(None, 0) != 0:
+        raise GLSError("dpartition: the numbering exchange failed")
+    if nr:
+        g[out["recv_dofs"]] = ex.recv_buf[:nr].cpu().numpy().astype(np.int64)
+    if (g < 0).any():
+        raise GLSError("dpartition: rank %d holds DoFs no exchange numbered" % rank)
+    out["l2g_dofs"] = g
+    out["n_global_dofs"] = dim * nv_g + np_g
+    out["n_global_vnodes"] = nv_g
+    return out
 
 
 def owned_dofs(plan):
@@ -403,28 +559,55 @@ class DistributedGeneralProblem:
     torch.distributed (gloo / nccl callbacks)."""
 
     def __init__(self, space, rank, world, device, viscosity=1.0, vnode_mask=None, dirichlet=None, lines=None,
-                 backend="gloo", group=None, qmapping=True, force_q=None):
-        plan = gpartition(space, rank, world, lines)
+                 backend="gloo", group=None, qmapping=True, force_q=None, part=None):
+        """space = the replicated global mesh (gpartition), or part = this rank's local part only (local_part's
+        dict; space, vnode_mask, dirichlet, lines and force_q then come from the part, in node / DoF keys)."""
+        if part is not None:  # distributed forest: nothing global on this rank
+            plan = dpartition(part, rank, world, device, backend, group)
+            dim, k, kp = int(part["dim"]), int(part["k"]), int(part["kp"])
+            vk = np.asarray(part["vnode_keys"])
+            lmask = np.ascontiguousarray(part["vnode_mask"][np.searchsorted(vk, plan["vl2k"])]) \
+                if "vnode_mask" in part else None
+            support, fq = part["cell_support"], part.get("force_q")
+            lines, dirichlet = part.get("lines"), part.get("dirichlet")
+            keys = plan["l2k_dofs"]
+            order = np.argsort(keys)
+
+            def to_local(ids):
+                ids = np.asarray(ids, np.int64)
+                pos = np.minimum(np.searchsorted(keys, ids, sorter=order), len(keys) - 1)
+                loc = order[pos]
+                return np.where(keys[loc] == ids, loc, -1)
+        else:
+            plan = gpartition(space, rank, world, lines)
+            cb, ce = plan["cell_begin"], plan["cell_end"]
+            dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])
+            lmask = np.ascontiguousarray(vnode_mask[plan["vl2g"]]) if vnode_mask is not None else None
+            support = space["cell_support"][cb:ce]
+            fq = None if force_q is None else force_q[cb:ce]
+            g2l = np.full(plan["n_global_dofs"], -1, np.int64)
+            g2l[plan["l2g_dofs"]] = np.arange(len(plan["l2g_dofs"]))
+            self.g2l = g2l
+
+            def to_local(ids):
+                return g2l[np.asarray(ids, np.int64)]
         self.plan = plan
-        cb, ce = plan["cell_begin"], plan["cell_end"]
-        dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])
-        lmask = np.ascontiguousarray(vnode_mask[plan["vl2g"]]) if vnode_mask is not None else None
         self.ctx = GLSContext(dim, k, kp, plan["local_cv"], plan["local_cp"] if kp != k else None, None,
                               plan["n_vnodes"], plan["n_pnodes"], viscosity=viscosity, vnode_mask=lmask,
-                              map_degree=k, cell_support=np.ascontiguousarray(space["cell_support"][cb:ce]),
-                              force_q=None if force_q is None else np.ascontiguousarray(force_q[cb:ce]))
-        g2l = np.full(plan["n_global_dofs"], -1, np.int64)
-        g2l[plan["l2g_dofs"]] = np.arange(len(plan["l2g_dofs"]))
-        self.g2l = g2l
+                              map_degree=k, cell_support=np.ascontiguousarray(support),
+                              force_q=None if fq is None else np.ascontiguousarray(fq))
         if lines is not None and len(lines[0]):
-            ld, lo, lm, lw = (np.asarray(a) for a in lines)
-            keep = np.nonzero(g2l[ld] >= 0)[0]
+            ld, lo, lm = (np.asarray(a) for a in lines[:3])
+            lw = np.asarray(lines[3])
+            lloc = to_local(ld)
+            keep = np.nonzero(lloc >= 0)[0]
+            mloc = to_local(lm)
             dofs, offs, mas, ws = [], [0], [], []
             for i in keep:
-                m = g2l[lm[lo[i]:lo[i + 1]]]
+                m = mloc[lo[i]:lo[i + 1]]
                 if (m < 0).any():
                     raise GLSError("line master not local on rank %d" % rank)
-                dofs.append(g2l[ld[i]])
+                dofs.append(lloc[i])
                 mas.extend(m.tolist())
                 ws.extend(lw[lo[i]:lo[i + 1]].tolist())
                 offs.append(len(mas))
@@ -433,7 +616,7 @@ class DistributedGeneralProblem:
                                      np.array(ws))
         if dirichlet is not None:
             gd, gv = (np.asarray(a) for a in dirichlet)
-            ld_ = g2l[gd]
+            ld_ = to_local(gd)
             sel = ld_ >= 0
             self.ctx.set_dirichlet(ld_[sel], gv[sel])
         self.exchanger = Exchanger(plan, device, backend=backend, group=group, width=1)

@@ -240,3 +240,122 @@ def test_replica_transfer_rows_and_injection(world):
         assert np.array_equal(l2g[li[sel]], inj[sel])
         hits += sel
     assert (hits == 1).all()
+
+
+# ---- distributed forest: gls_dpart_create from each rank's local part only
+@pytest.mark.parametrize("dim,k,kp", [(2, 2, 1), (2, 1, 1), (3, 2, 1)])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_local_part_plan_equals_replicated_plan(dim, k, kp, world):
+    """A rank's plan from its local part alone (owned cells + ghost layer, node keys = global ids) is the plan
+    the replicated global mesh gives: same local cells, node order, owned counts, neighbours and exchange lists."""
+    from softx_2020_200_amd.dist import dplan, gpartition, local_part
+    from tests.test_gpu_uforest import dof_lines
+    sp = _adapted_space(dim, k, kp)
+    lines = dof_lines(sp)
+    for r in range(world):
+        g = gpartition(sp, r, world, lines)
+        part = local_part(sp, r, world, lines)
+        assert len(part["cell_owner"]) < sp["n_cells"] or world == 1
+        d = dplan(part, r, world)
+        assert np.array_equal(d["vl2k"], g["vl2g"]) and np.array_equal(d["pl2k"], g["pl2g"]), r
+        for key in ("local_cv", "local_cp", "nbrs", "send_off", "send_dofs", "recv_off", "recv_dofs"):
+            assert np.array_equal(d[key], g[key]), (r, key)
+        assert (d["n_owned_v"], d["n_owned_p"]) == (g["n_owned_v"], g["n_owned_p"])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_part_plan_with_sparse_keys(world):
+    """Node keys need not be a numbering: with scattered 64-bit keys the plans still pair up (a rank's send list to
+    a neighbour is, as DoF keys and in order, that neighbour's receive list), owned cells map back to their keys,
+    and every DoF is owned by exactly one rank."""
+    from softx_2020_200_amd.dist import dplan, local_part
+    from tests.test_gpu_uforest import dof_lines
+    sp = _adapted_space(3, 2, 1)
+    lines = dof_lines(sp)
+    rng = np.random.default_rng(3)
+    vkey = rng.choice(2 ** 40, sp["n_vnodes"], replace=False) * 7 + 5
+    pkey = rng.choice(2 ** 40, sp["n_pnodes"], replace=False) * 3 + 1
+
+    def rekey(part):
+        d1 = part["dim"] + 1
+        def kv(dk):
+            pres = dk % d1 == part["dim"]
+            out = np.empty_like(dk)
+            out[pres] = pkey[dk[pres] // d1]
+            out[~pres] = vkey[dk[~pres] // d1]
+            return out * d1 + dk % d1
+        q = dict(part, cell_vkeys=vkey[part["cell_vkeys"]], cell_pkeys=pkey[part["cell_pkeys"]])
+        ld, lo, lm, lw = part["lines"]
+        q["lines"] = (kv(ld), lo, kv(lm), lw)
+        return q
+    plans, parts = [], []
+    for r in range(world):
+        part = rekey(local_part(sp, r, world, lines))
+        parts.append(part)
+        plans.append(dplan(part, r, world))
+    owned = []
+    for r, (pl, pa) in enumerate(zip(plans, parts)):
+        own = pa["cell_owner"] == r
+        assert np.array_equal(pl["vl2k"][pl["local_cv"]], pa["cell_vkeys"][own])
+        assert np.array_equal(pl["pl2k"][pl["local_cp"]], pa["cell_pkeys"][own])
+        n = pl["n_vnodes"]
+        owned.append(np.concatenate([pl["l2k_dofs"][:3 * pl["n_owned_v"]], pl["l2k_dofs"][3 * n:3 * n + pl["n_owned_p"]]]))
+    allown = np.concatenate(owned)
+    assert len(np.unique(allown)) == len(allown) == 3 * sp["n_vnodes"] + sp["n_pnodes"]
+    for a, pa in enumerate(plans):
+        for i, b in enumerate(pa["nbrs"]):
+            pb = plans[int(b)]
+            j = list(pb["nbrs"]).index(a)
+            sent = pa["l2k_dofs"][pa["send_dofs"][pa["send_off"][i]:pa["send_off"][i + 1]]]
+            got = pb["l2k_dofs"][pb["recv_dofs"][pb["recv_off"][j]:pb["recv_off"][j + 1]]]
+            assert np.array_equal(sent, got), (a, int(b))
+
+
+def _numbering_worker(rank, world, port, q, part):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from softx_2020_200_amd.dist import dpartition
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pl = dpartition(part, rank, world)
+        q2 = dict(l2k=pl["l2k_dofs"], l2g=pl["l2g_dofs"], n=pl["n_global_dofs"], no=(pl["n_owned_v"], pl["n_owned_p"]),
+                  nv=pl["n_vnodes"])
+        q.put((rank, q2))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_numbering_gloo(world):
+    """dpartition's global numbering (owned counts all-reduced, ghost ids from their owners): every rank's owned
+    DoFs are one contiguous range, the ranges tile [0, n), and a DoF key has the same global id on every rank that
+    holds it. Each worker process receives only its local part."""
+    from softx_2020_200_amd.dist import local_part
+    from tests.test_gpu_uforest import dof_lines
+    sp = _adapted_space(3, 2, 1)
+    lines = dof_lines(sp)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + world * 11 + os.getpid() % 400
+    procs = [ctx.Process(target=_numbering_worker, args=(r, world, port, q, local_part(sp, r, world, lines)))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for r in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+    n = 3 * sp["n_vnodes"] + sp["n_pnodes"]
+    key2g = {}
+    ranges = []
+    for r in range(world):
+        e = res[r]
+        assert e["n"] == n
+        nov, nop = e["no"]
+        own = np.concatenate([e["l2g"][:3 * nov], e["l2g"][3 * e["nv"]:3 * e["nv"] + nop]])
+        ranges.append(np.sort(own))
+        for kk, gg in zip(e["l2k"].tolist(), e["l2g"].tolist()):
+            assert key2g.setdefault(kk, gg) == gg
+    allown = np.concatenate(ranges)
+    assert np.array_equal(np.sort(allown), np.arange(n))
+    assert len(set(key2g.values())) == len(key2g)

@@ -190,3 +190,113 @@ def test_enclosed_steady_flow_with_hanging_lines_across_ranks(precond):
             assert e["block_err"] < 1e-12 and e["block_missing"] == 0, (rank, e)
         # Ifpack-like rows: the block-Jacobi ILU over 4 ranks stays within a few x the single-rank count
         assert res[0]["dist"]["linear_iterations"] <= 4 * res[0]["single"]["linear_iterations"], res[0]
+
+
+def _worker_part(rank, world, port, q, part, data):
+    """a rank that never holds the global mesh: its context, Dirichlet rows, hanging lines and global numbering
+    come from its local part (owned cells + ghost layer) alone; data = values at the part's DoF keys"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    from softx_2020_200_amd.dist import DistributedGeneralProblem, owned_dofs
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dp = DistributedGeneralProblem(None, rank, world, "cuda", viscosity=0.2, part=part)
+        pos = np.searchsorted(data["keys"], dp.plan["l2k_dofs"])
+        assert np.array_equal(data["keys"][pos], dp.plan["l2k_dofs"])
+        loc_v = lambda name: data[name][pos]  # noqa: E731
+        cu = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device="cuda")  # noqa: E731
+        c = dp.ctx
+        c.set_time("bdf2", data["time_steps"])
+        c.set_state(cu(loc_v("u")), cu(loc_v("u1")), cu(loc_v("u2")))
+        loc, _ = owned_dofs(dp.plan)
+        rel = lambda a, b, s: float(np.abs(a - b).max() / s)  # noqa: E731
+        errs = {"res": rel(c.residual().cpu().numpy()[loc], loc_v("r")[loc], data["scale_r"]),
+                "jv": rel(c.jacobian_apply(cu(loc_v("v"))).cpu().numpy()[loc], loc_v("jv")[loc], data["scale_jv"]),
+                "diag": rel(c.jacobian_diagonal().cpu().numpy()[loc], loc_v("d")[loc], data["scale_d"]),
+                "n_ghost_recv": int(dp.plan["recv_off"][-1]), "n_cells_local": len(part["cell_owner"]),
+                "n_global_dofs": int(dp.plan["n_global_dofs"])}
+        xd = cu(loc_v("x0"))
+        std = c.newton(xd, cu(loc_v("u1")), cu(loc_v("u2")), **data["kw"])
+        vel = (dp.plan["l2k_dofs"] % 4 != 3)[loc]
+        errs["newton_u"] = rel(xd.cpu().numpy()[loc][vel], loc_v("x")[loc][vel], data["scale_x"])
+        errs["newton_res"] = std["final_residual"]
+        q.put((rank, errs))
+    except Exception as e:
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_forest_ranks_hold_only_their_local_part(world):
+    """Distributed forest (gls_dpart_create): each rank process receives only its local part of the adapted,
+    curved Q2-Q1 shell -- owned cells plus the ghost layer, node keys, the hanging lines and Dirichlet rows on those
+    cells -- builds its plan, numbers the global DoFs by an all-reduce of owned counts plus one exchange, and its
+    residual, J.v, diagonal and Newton solve equal the single-rank ones on its owned DoFs (the test process holds
+    the global mesh only to cut the parts and to compute the single-rank answers)."""
+    import torch
+    import torch.multiprocessing as mp
+
+    from oracle.oracle import MappedProblem
+    from softx_2020_200_amd.dist import local_part, part_dof_keys
+    from tests.gpu_util import context_for, vnode_mask_of
+    from tests.test_dist_plan import _adapted_space
+    from tests.test_gpu_uforest import continuous_field, dof_lines
+    sp = _adapted_space(3, 2, 1)
+    lines = dof_lines(sp)
+    p = MappedProblem(sp, viscosity=0.2, scheme="bdf2", time_steps=(0.1, 0.12, 0.1, 0.1))
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)  # noqa: E731
+    p.set_dirichlet([("function", 0, rot), ("noslip", 1, None)])
+    cu = lambda a: torch.tensor(np.asarray(a), dtype=torch.float64, device="cuda")  # noqa: E731
+    rng = np.random.default_rng(20200200 + 11)
+    u, u1, u2, v = (continuous_field(sp, rng) for _ in range(4))
+    u = p.apply_nonzero_constraints(u)
+    g = context_for(p)
+    g.set_time("bdf2", p.time_steps)
+    g.set_state(cu(u), cu(u1), cu(u2))
+    vals = {"r": g.residual().cpu().numpy(), "jv": g.jacobian_apply(cu(v)).cpu().numpy(),
+            "d": g.jacobian_diagonal().cpu().numpy(), "u": u, "u1": u1, "u2": u2, "v": v}
+    kw = dict(tolerance=1e-10, max_iterations=8, lin_max_iterations=20000, restart=200, relative_residual=1e-11,
+              minimum_residual=1e-14)
+    x0 = p.apply_nonzero_constraints(u1.copy())
+    xg = cu(x0)
+    stg = g.newton(xg, cu(u1), cu(u2), **kw)
+    assert stg["final_residual"] < 1e-10
+    vals["x0"], vals["x"] = x0, xg.cpu().numpy()
+    nv = sp["n_vnodes"]
+    dirs = np.array(sorted(p.dirichlet), np.int64)
+    common = {"time_steps": p.time_steps, "kw": kw, "scale_r": np.abs(vals["r"]).max(),
+              "scale_jv": np.abs(vals["jv"]).max(), "scale_d": np.abs(vals["d"]).max(),
+              "scale_x": np.abs(vals["x"][:3 * nv]).max()}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32700 + 13 * world + os.getpid() % 400
+    procs = []
+    for r in range(world):
+        part = local_part(sp, r, world, lines, dirichlet=(dirs, np.array([p.dirichlet[d] for d in dirs])),
+                          vnode_mask=vnode_mask_of(p))
+        keys = part_dof_keys(part)
+        gid = np.where(keys % 4 == 3, 3 * nv + keys // 4, (keys // 4) * 3 + keys % 4)
+        data = dict(common, keys=keys, **{n: np.asarray(a)[gid] for n, a in vals.items()})
+        procs.append(ctx.Process(target=_worker_part, args=(r, world, port, q, part, data)))
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+    print(world, res)
+    for rank, e in res.items():
+        assert "error" not in e, (rank, e)
+        assert e["n_cells_local"] < sp["n_cells"], (rank, e)
+        assert e["n_global_dofs"] == p.n_dofs
+        assert e["res"] < 1e-12 and e["jv"] < 1e-12 and e["diag"] < 1e-12, (rank, e)
+        assert e["newton_res"] < 1e-10 and e["newton_u"] < 1e-8, (rank, e)
+    assert sum(e["n_ghost_recv"] for e in res.values()) > 0
