@@ -31,7 +31,7 @@ EXPORTS = [
     "gls_mesh_hyper_cube", "gls_timing_reset", "gls_timing_get", "gls_timing_enable", "gls_uses_brick_kernels",
     "gls_part_create", "gls_part_sizes", "gls_part_get", "gls_part_destroy", "gls_dist_attach", "gls_dist_import", "gls_rccl_unique_id", "gls_rccl_create", "gls_rccl_destroy", "gls_rccl_info", "gls_mg_smoother_apply", "gls_mg_attach_replica",
     "gls_dist_attach_rccl",
-    "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_residual_and_diagonal", "gls_octree_set_periodic", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
+    "gls_mg_attach", "gls_mg_detach", "gls_mg_set_coarse_replica", "gls_residual_and_diagonal", "gls_octree_set_periodic", "gls_ilu_attach", "gls_ilu_detach", "gls_ilu_info", "gls_ilu_matrix", "gls_ilu_factors", "gls_ilu_set_options", "gls_iluk_pattern", "gls_cuthill_mckee", "gls_section_timing", "gls_section_get", "gls_dist_attach_dofs", "gls_dist_attach_dofs_rccl", "gls_gpart_create", "gls_gpart_sizes", "gls_gpart_get", "gls_gpart_map_dofs", "gls_gpart_destroy", "gls_dpart_create", "gls_set_lattice", "gls_apply_preconditioner", "gls_mg_transfer",
     "gls_prm_parse", "gls_prm_get", "gls_prm_n_entries", "gls_prm_entry", "gls_prm_destroy",
     "gls_expr_create", "gls_expr_n_components", "gls_expr_eval", "gls_expr_destroy",
     "gls_vtu_write", "gls_pvtu_write", "gls_pvd_write",

@@ -85,6 +85,14 @@ def test_reference_application_case(tmp_path, name, dim, periodic, pressure):
             assert a[2] == b[2], (name, a, b)
         if pressure:
             assert a[3:] == b[3:], (name, a, b)
+        elif name.startswith("poiseuille"):
+            # the exact pressure (linear) lies in the Q1 space: both columns are the inexact solve's noise
+            # (reference 2.5e-09..1.6e-08); bounded at the same scale instead of diffed
+            assert float(a[3]) < 1e-7 and float(b[3]) < 1e-7, (name, a, b)
+        elif name == "taylorcouette_gls":
+            # the reference's column carries its solver's free pressure constant (pressure_note): ours,
+            # without it, stays below the reference's on every level
+            assert float(a[3]) < float(b[3]), (name, a, b)
 
 
 @pytest.mark.gpu
