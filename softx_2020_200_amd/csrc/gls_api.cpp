@@ -433,6 +433,7 @@ struct gls_ctx {
     DevBuf<int64_t> tm, toff, tdof;                     // operator lines transposed: master -> (hanging dof, w)
     DevBuf<double> tw;
     DevBuf<uint8_t> hmask;                             // hanging velocity components per node
+    DevBuf<uint8_t> dmask;                             // 1 on the hanging DoFs (C v in one pass)
     DevBuf<double> vbuf;                               // C v for J.v
     std::vector<int64_t> h_dof, h_off, h_master;       // host copy of the lines (ILU sparsity)
   } hang;
@@ -1206,9 +1207,14 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   }
   if (mode == gls::MODE_JV && c->hang.on) {  // C v: hanging entries interpolated from their masters
     if (c->hang.vbuf.n != (size_t)c->n_dofs) GLS_TRY(c->hang.vbuf.alloc((size_t)c->n_dofs));
-    HIP_TRY(gls::vec_copy(c->hang.vbuf.p, v, c->n_dofs, c->stream));
-    HIP_TRY(gls::vec_csr_gather_set(c->hang.vbuf.p, c->hang.vbuf.p, c->hang.dof.p, c->hang.ooff.p, c->hang.omaster.p,
-                                    c->hang.ow.p, (int64_t)c->hang.dof.n, c->stream));
+    if (c->hang.dmask.n == (size_t)c->n_dofs) {  // one pass: copy the free DoFs, interpolate the hanging ones
+      HIP_TRY(gls::vec_copy_gather_set(c->hang.vbuf.p, v, c->hang.dmask.p, c->n_dofs, c->hang.dof.p, c->hang.ooff.p,
+                                       c->hang.omaster.p, c->hang.ow.p, (int64_t)c->hang.dof.n, c->stream));
+    } else {
+      HIP_TRY(gls::vec_copy(c->hang.vbuf.p, v, c->n_dofs, c->stream));
+      HIP_TRY(gls::vec_csr_gather_set(c->hang.vbuf.p, c->hang.vbuf.p, c->hang.dof.p, c->hang.ooff.p, c->hang.omaster.p,
+                                      c->hang.ow.p, (int64_t)c->hang.dof.n, c->stream));
+    }
     v = c->hang.vbuf.p;
   }
   P.v = v;
@@ -1273,6 +1279,9 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
     } else if (brick) {
       HIP_TRY(gls::launch_brick_kernel(c->k, mode, P, c->tables, c->stream));
     } else {
+      // (the bricks' pencil launch forked onto a side stream, concurrent with this one and joined before the
+      // gather, measured 1.0-1.4 ms per Newton step SLOWER on the 1.28 M-DoF octree line: the cross-stream event
+      // pair costs more than the overlap of two ~20 us launches gains; profiles/r05_ab_octree_overlap.txt)
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, mode, P, c->tables, c->stream));
       if (oct) {  // the bricks' cells: element vectors from the pencil kernel
         gls::OpParams Q = P;
@@ -2161,10 +2170,11 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   c->hang.h_off.assign(off, off + n + 1);
   c->hang.h_master.assign(masters, masters + nm);
   if (n == 0) c->hang.h_off.assign(1, 0);
-  std::vector<uint8_t> hm((size_t)c->n_vnodes, 0);
+  std::vector<uint8_t> hm((size_t)c->n_vnodes, 0), dm((size_t)N, 0);
   std::vector<int64_t> con;  // zero_constraints: Dirichlet + hanging
   for (int64_t d = 0; d < N; ++d) {
     if (is_h[(size_t)d] && d < nvd) hm[(size_t)(d / dim)] |= (uint8_t)(1u << (d % dim));
+    dm[(size_t)d] = is_h[(size_t)d] ? 1 : 0;
     if (is_h[(size_t)d] || dirichlet(d)) con.push_back(d);
   }
   auto &h = c->hang;
@@ -2180,6 +2190,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
   GLS_TRY(h.tdof.upload(tdof.data(), tdof.size()));
   GLS_TRY(h.tw.upload(tw.data(), tw.size()));
   GLS_TRY(h.hmask.upload(hm.data(), hm.size()));
+  GLS_TRY(h.dmask.upload(dm.data(), dm.size()));
   GLS_TRY(c->con_dofs.upload(con.data(), con.size()));
   h.on = n > 0;
   c->use_brick = false;  // mixed cell sizes: the general per-cell kernels

@@ -84,6 +84,8 @@ hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, c
 // hanging-node constraint lines (CSR): distribute x[dof] = sum w src[master]; condense onto masters
 hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, const int64_t *off,
                               const int64_t *master, const double *w, int64_t n, hipStream_t s);
+hipError_t vec_copy_gather_set(double *x, const double *v, const uint8_t *dmask, int64_t n, const int64_t *dof,
+                               const int64_t *off, const int64_t *master, const double *w, int64_t nl, hipStream_t s);
 hipError_t vec_csr_condense(double *y, const int64_t *tm, const int64_t *toff, const int64_t *tdof, const double *tw,
                             int64_t n, hipStream_t s);
 hipError_t vec_csr_spmv(double *y, const double *x, const int64_t *off, const int32_t *col, const double *w, int64_t n,

@@ -523,6 +523,30 @@ hipError_t vec_multiaxpy_dots(double *w, const double *A, int64_t lda, int nk, c
   return hipGetLastError();
 }
 
+// x = C v in one pass: the free DoFs copied, the hanging ones interpolated from their masters' values in v (masters
+// are never hanging, so reading them from v equals the copy-then-interpolate order)
+__global__ void k_copy_gather_set(double *__restrict__ x, const double *__restrict__ v, const uint8_t *__restrict__ dmask,
+                                  int64_t n, const int64_t *__restrict__ dof, const int64_t *__restrict__ off,
+                                  const int64_t *__restrict__ master, const double *__restrict__ w, int64_t nl) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n + nl; i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n) {
+      if (!dmask[i]) x[i] = v[i];
+    } else {
+      const int64_t l = i - n;
+      double s = 0.;
+      for (int64_t j = off[l]; j < off[l + 1]; ++j) s += w[j] * v[master[j]];
+      x[dof[l]] = s;
+    }
+  }
+}
+hipError_t vec_copy_gather_set(double *x, const double *v, const uint8_t *dmask, int64_t n, const int64_t *dof,
+                               const int64_t *off, const int64_t *master, const double *w, int64_t nl, hipStream_t s) {
+  if (n + nl <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_gather_set, dim3(grid_for(n + nl)), dim3(kBlock), 0, s, x, v, dmask, n, dof, off, master, w,
+                     nl);
+  return hipGetLastError();
+}
+
 hipError_t vec_csr_gather_set(double *x, const double *src, const int64_t *dof, const int64_t *off,
                               const int64_t *master, const double *w, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
