@@ -709,7 +709,10 @@ def main():
                          "ncclSend/ncclRecv/ncclAllReduce on the context stream, ghost import overlapped with the "
                          "interior bricks) or torch.distributed callbacks (host-synchronous; the gloo tests)")
     args = ap.parse_args()
-    if args.dist_backend == "gloo":  # host-staged testing transport: no RCCL communicator
+    # GLS_BENCH_FAIL_NATIVE_PREFLIGHT=1 (test hook): the native transport's pre-flight raises on every rank, so the
+    # fallback to the torch.distributed transport runs (on one GPU with gloo)
+    fail_native = os.environ.get("GLS_BENCH_FAIL_NATIVE_PREFLIGHT") == "1"
+    if args.dist_backend == "gloo" and not fail_native:  # host-staged testing transport: no RCCL communicator
         args.dist_impl = "torch"
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus < 1:
@@ -752,7 +755,25 @@ def main():
         ids = [None] * world
         dist.all_gather_object(ids, str(getattr(props, "uuid", None) or "%s:%d" % (os.uname().nodename, local)))
         devices = len(set(ids))
-        pre_err = preflight(args, rank, world, torch.device("cuda", local), dist)
+        try:
+            if fail_native and args.dist_impl == "native":
+                raise RuntimeError("GLS_BENCH_FAIL_NATIVE_PREFLIGHT")
+            pre_err = preflight(args, rank, world, torch.device("cuda", local), dist)
+            failed = 0.0 if pre_err <= 1e-12 else 1.0
+        except Exception as e:  # noqa: BLE001 -- reported, and the ranks agree on it below
+            sys.stderr.write("bench.py: rank %d pre-flight with the %s transport raised: %r\n" % (rank, args.dist_impl, e))
+            pre_err, failed = float("nan"), 1.0
+        flag = torch.tensor([failed], dtype=torch.float64, device=torch.device("cuda", local) if args.dist_backend == "nccl"
+                            else "cpu")
+        dist.all_reduce(flag)
+        if flag.item() > 0 and args.dist_impl == "native":
+            # the in-library RCCL transport failed its check on some rank: the timed run takes torch.distributed's
+            # RCCL (callbacks) instead, after the same pre-flight, and the line says so
+            if rank == 0:
+                sys.stderr.write("bench.py: in-library RCCL pre-flight failed (%s); falling back to the torch.distributed "
+                                 "transport\n" % pre_err)
+            args.dist_impl, args.dist_impl_fallback = "torch", "native pre-flight failed (%s)" % pre_err
+            pre_err = preflight(args, rank, world, torch.device("cuda", local), dist)
         if not pre_err <= 1e-12:
             if rank == 0:
                 sys.stderr.write("bench.py: pre-flight FAILED: %d-rank residual / J.v differ from one rank by %.3e "
@@ -936,6 +957,8 @@ def main():
                    if world > 1 else "single"},
         "mdof_per_s": N_global * its_per_s / 1e6,
         "devices": devices, "rccl_ranks": rccl_ranks, "preflight_relerr": pre_err,
+        "dist_impl": args.dist_impl if world > 1 else None,
+        "dist_impl_fallback": getattr(args, "dist_impl_fallback", None),
         "linear_iterations_per_step": float(np.mean(lin_its)),
         "residual_evaluations_per_step": float(np.mean(nres)),
         "kernel_ms": {"jacobian_apply": jv_ms / max(jv_n, 1), "residual": res_ms / max(res_n, 1),
