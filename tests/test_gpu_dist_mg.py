@@ -1,5 +1,5 @@
 """Row e2 + f1: the refinement-hierarchy multigrid across ranks (gls_mg_attach_replica). The fine level of an
-adapted, curved unstructured mesh with hanging-node lines is partitioned over 2 / 3 ranks on the box's one GPU
+adapted, curved unstructured mesh with hanging-node lines is partitioned over 2 / 3 / 4 ranks on the box's one GPU
 (gls_gpart_* + gls_dist_attach_dofs, gloo ghost exchange); the coarser levels run on every rank as one
 single-rank context with its own hierarchy (the replica), fed by the all-reduced restriction of the owned rows.
 With Jacobi smoothing the distributed V-cycle is the single-rank one (the distributed diagonal and J.v equal the
@@ -122,7 +122,7 @@ def _worker(rank, world, port, q, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("case", [("shell", 2, 2, "jacobi", False), ("cylshell", 2, 1, "jacobi", False),
                                   ("cylshell", 2, 1, "ilu", False), ("cylshell", 2, 1, "jacobi", True),
                                   ("octree3d", 2, 2, "jacobi", False)],
