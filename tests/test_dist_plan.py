@@ -244,7 +244,7 @@ def test_replica_transfer_rows_and_injection(world):
 
 # ---- distributed forest: gls_dpart_create from each rank's local part only
 @pytest.mark.parametrize("dim,k,kp", [(2, 2, 1), (2, 1, 1), (3, 2, 1)])
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_local_part_plan_equals_replicated_plan(dim, k, kp, world):
     """A rank's plan from its local part alone (owned cells + ghost layer, node keys = global ids) is the plan
     the replicated global mesh gives: same local cells, node order, owned counts, neighbours and exchange lists."""
@@ -359,3 +359,22 @@ def test_distributed_numbering_gloo(world):
     allown = np.concatenate(ranges)
     assert np.array_equal(np.sort(allown), np.arange(n))
     assert len(set(key2g.values())) == len(key2g)
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_local_part_plan_on_an_adapted_octree(world):
+    """The same equality on an adapted hyper_cube forest (octree leaves with hanging faces, Q2-Q2): the local part's
+    ghost layer closes over the hanging lines, and the plan equals the replicated one."""
+    import softx_2020_200_amd as sx
+    from softx_2020_200_amd.dist import dplan, gpartition, local_part
+    from tests.test_octree_mg import adapted_tree
+    mesh = adapted_tree(3, 2, 2).mesh(2, 2)
+    space = dict(mesh, cell_support=np.ascontiguousarray(mesh["vnode_x"][mesh["cell_vnodes"]]))
+    lines = sx.hanging_dof_lines(mesh)
+    assert len(lines[0]) > 0
+    for r in range(world):
+        g = gpartition(space, r, world, lines)
+        d = dplan(local_part(space, r, world, lines), r, world)
+        assert np.array_equal(d["vl2k"], g["vl2g"]), r
+        for key in ("local_cv", "nbrs", "send_off", "send_dofs", "recv_off", "recv_dofs"):
+            assert np.array_equal(d[key], g[key]), (r, key)
