@@ -462,7 +462,9 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     const int node = P.cell_vnodes[cid(i / NV) * NV + i % NV];
     if constexpr (MODE != MODE_DIAG) {
       double out[DIM] = {};
-#pragma nounroll
+      // unrolled by 3: three points' table and coefficient loads in flight (same VGPRs and occupancy; the small
+      // latency-bound leaf launches of forests 2.5 % faster per Newton step, profiles/r05_ab_cell_unroll.txt)
+#pragma unroll 3
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tV[qx][ax], vy = tV[qy][ay], vz = DIM == 3 ? tV[qz][az] : 1.0;
@@ -549,7 +551,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     const int pn = P.cell_pnodes ? P.cell_pnodes[cid(i / NP) * NP + i % NP] : P.cell_vnodes[cid(i / NV) * NV + i % NV];
     double out = 0.;
     if constexpr (MODE != MODE_DIAG) {
-#pragma nounroll
+#pragma unroll 3
       for (int q = 0; q < NQ; ++q) {
         const int qx = q % NQ1, qy = (q / NQ1) % NQ1, qz = DIM == 3 ? q / (NQ1 * NQ1) : 0;
         const double vx = tVp[qx][ax], vy = tVp[qy][ay], vz = DIM == 3 ? tVp[qz][az] : 1.0;
