@@ -320,9 +320,26 @@ __global__ void k_csr_spmv(double *__restrict__ y, const double *__restrict__ x,
 __global__ void k_csr_condense(double *y, const int64_t *__restrict__ tm, const int64_t *__restrict__ toff,
                                const int64_t *__restrict__ tdof, const double *__restrict__ tw, int64_t n, int64_t bs = 0) {
   y += blockIdx.y * bs;
+  constexpr int kIn = 8;  // hanging rows gathered at once: all row ids and weights, then all values, then the sum
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = toff[i], nj = toff[i + 1] - j0;
     double s = 0.;
-    for (int64_t j = toff[i]; j < toff[i + 1]; ++j) s += tw[j] * y[tdof[j]];
+    if (nj <= kIn) {
+      int64_t r[kIn];
+      double w[kIn], v[kIn];
+#pragma unroll
+      for (int t = 0; t < kIn; ++t) {
+        r[t] = t < nj ? tdof[j0 + t] : -1;
+        w[t] = t < nj ? tw[j0 + t] : 0.;
+      }
+#pragma unroll
+      for (int t = 0; t < kIn; ++t) v[t] = r[t] >= 0 ? y[r[t]] : 0.;
+#pragma unroll
+      for (int t = 0; t < kIn; ++t)  // the stored order, as the general loop
+        if (t < nj) s += w[t] * v[t];
+    } else {
+      for (int64_t j = j0; j < j0 + nj; ++j) s += tw[j] * y[tdof[j]];
+    }
     y[tm[i]] += s;
   }
 }
@@ -383,7 +400,25 @@ __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ e
   if (act) act += (int64_t)blockIdx.y * nblk;  // batched probing: cell batches the kernel skipped hold 0
   auto live = [&](int64_t slot) { return !act || act[slot / el / cb]; };
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nv) {
+  constexpr int kIn = 8;  // incidences gathered at once (all slots, then all values: one dependent round each)
+  if (i < nv && !act && voff[i + 1] - voff[i] <= kIn) {
+    const int64_t j0 = voff[i], nj = voff[i + 1] - j0;
+    int64_t sl[kIn];
+#pragma unroll
+    for (int t = 0; t < kIn; ++t) sl[t] = t < nj ? vslot[j0 + t] : -1;
+    double e[kIn][3];
+#pragma unroll
+    for (int t = 0; t < kIn; ++t)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) e[t][c] = (sl[t] >= 0 && c < dim) ? ev[sl[t] + c] : 0.;
+    double acc[3] = {0., 0., 0.};
+#pragma unroll
+    for (int t = 0; t < kIn; ++t)  // ascending slot order, as the general loop below
+      if (t < nj)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] += e[t][c];
+    for (int c = 0; c < dim; ++c) y[i * dim + c] = acc[c];
+  } else if (i < nv) {
     double acc[3] = {0., 0., 0.};
     for (int64_t j = voff[i]; j < voff[i + 1]; ++j) {
       if (!live(vslot[j])) continue;
@@ -531,10 +566,26 @@ __global__ void k_copy_gather_set(double *__restrict__ x, const double *__restri
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n + nl; i += (int64_t)gridDim.x * blockDim.x) {
     if (i < n) {
       if (!dmask[i]) x[i] = v[i];
-    } else {
-      const int64_t l = i - n;
+    } else {  // a line: its masters (<= 9 on Q2 faces) and weights first, then their values, then the ordered sum
+      const int64_t l = i - n, j0 = off[l], nj = off[l + 1] - j0;
+      constexpr int kIn = 9;
       double s = 0.;
-      for (int64_t j = off[l]; j < off[l + 1]; ++j) s += w[j] * v[master[j]];
+      if (nj <= kIn) {
+        int64_t m[kIn];
+        double wt[kIn], vv[kIn];
+#pragma unroll
+        for (int t = 0; t < kIn; ++t) {
+          m[t] = t < nj ? master[j0 + t] : -1;
+          wt[t] = t < nj ? w[j0 + t] : 0.;
+        }
+#pragma unroll
+        for (int t = 0; t < kIn; ++t) vv[t] = m[t] >= 0 ? v[m[t]] : 0.;
+#pragma unroll
+        for (int t = 0; t < kIn; ++t)
+          if (t < nj) s += wt[t] * vv[t];
+      } else {
+        for (int64_t j = j0; j < j0 + nj; ++j) s += w[j] * v[master[j]];
+      }
       x[dof[l]] = s;
     }
   }
