@@ -37,8 +37,12 @@ struct Cfg {
   static constexpr int TABN = 5 * kMaxQ1D * kMaxNodes1D + 2 * kMaxQ1D;
 };
 
-template <int DIM, int K, int KP, int NQ1, int MODE, bool GEN = false, int TPB = 256>
+// CQ: J.v from the linearization cache the diagonal pass wrote (P.cq, cq_mode 2) -- its own instantiation, so the
+// state-field sums drop out at compile time and the evaluation rows unroll at the old register count (198 / 248
+// VGPRs on boxes / mapped cells; profiles/r05_ab_cell_cache_instantiation.txt: taylorcouette3d -7 % per Newton step)
+template <int DIM, int K, int KP, int NQ1, int MODE, bool GEN = false, int TPB = 256, bool CQ = false>
 __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const Tables1D T) {
+  static_assert(!CQ || MODE == MODE_JV, "the cache feeds J.v only");
   using C = Cfg<DIM, K, KP, NQ1, TPB>;
   constexpr int NV = C::NV, NP = C::NP, NQ = C::NQ, CB = C::CB, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -65,7 +69,7 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   auto cid = [&](int cl) -> int64_t { return P.cell_list ? (int64_t)P.cell_list[c0 + cl] : (int64_t)(c0 + cl); };
   const int64_t voff = (int64_t)DIM * P.n_vnodes;  // first pressure DoF
   constexpr int NCQ = DIM + DIM * DIM + 1 + DIM;    // linearization cache values per q (u, grad u, tau, R_s)
-  const bool cqr = MODE == MODE_JV && P.cq && P.cq_mode == 2;   // J.v from the cache
+  constexpr bool cqr = CQ;                                      // J.v from the cache (launch_cell_g picks it)
   const bool cqw = MODE == MODE_DIAG && P.cq && P.cq_mode == 1;  // the diagonal pass fills it
 
   // batched J.v (probing): this block's vector; J is linear, so a batch of cells on which the vector
@@ -186,12 +190,10 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
     const double *cv = sV + cl * NV * DIM;
     const double *ch = sH + cl * NV * DIM;
     const int nh = P.n_hist;
-#pragma nounroll
-    for (int az = 0; az < (DIM == 3 ? C::K1 : 1); ++az) {
+    auto eval_row = [&](int az, int ay) {
       const double vz = DIM == 3 ? tV[qz][az] : 1.0, dz = DIM == 3 ? tD[qz][az] : 0.0,
                    sz = DIM == 3 ? tS[qz][az] : 0.0;
-#pragma nounroll
-      for (int ay = 0; ay < C::K1; ++ay) {
+      {
         const double vy = tV[qy][ay], dy = tD[qy][ay], sy = tS[qy][ay];
 #pragma unroll
         for (int ax = 0; ax < C::K1; ++ax) {
@@ -229,6 +231,17 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
           }
         }
       }
+    };
+    if constexpr (CQ) {  // v only: a plane's rows unroll (their table and node loads in flight together)
+#pragma nounroll
+      for (int az = 0; az < (DIM == 3 ? C::K1 : 1); ++az)
+#pragma unroll
+        for (int ay = 0; ay < C::K1; ++ay) eval_row(az, ay);
+    } else {
+#pragma nounroll
+      for (int az = 0; az < (DIM == 3 ? C::K1 : 1); ++az)
+#pragma nounroll
+        for (int ay = 0; ay < C::K1; ++ay) eval_row(az, ay);
     }
     {
       const double *cp = sP + cl * NP;
@@ -611,6 +624,8 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 256, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipFuncSetAttribute((const void *)gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG, GEN>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
@@ -629,8 +644,12 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
           break;
         }
       }
-      hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks, P.bv_stride ? P.n_probe : 1),
-                         dim3(256), lds, s, P, T);
+      if (P.cq && P.cq_mode == 2 && !P.bv_stride)  // from the linearization cache
+        hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 256, true>), dim3(blocks), dim3(256), lds, s,
+                           P, T);
+      else
+        hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN>), dim3(blocks, P.bv_stride ? P.n_probe : 1),
+                           dim3(256), lds, s, P, T);
       break;
     default:
       hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_DIAG, GEN>), dim3(blocks), dim3(256), lds, s, P, T);
