@@ -405,6 +405,14 @@ struct gls_ctx {
     DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
     DevBuf<int32_t> pdpid, pepid;        // probe of each unit DoF / each extracted entry (batched probing)
     DevBuf<double> bV, bC, bY;           // batched probing: probe vectors, C V (hanging lines), results [batch][n_dofs]
+    // batched probing's activity: which (probe, cell batch) pairs have a nonzero C e_p on their cells depends on
+    // the pattern and the hanging lines only, so the first probing records it (the kernel's flags, wact) and the
+    // later ones launch just the active pairs (wlist, per chunk from woff; chunk size wB, batches wnblk)
+    DevBuf<uint8_t> wact;
+    DevBuf<int32_t> wlist;
+    std::vector<int64_t> woff;
+    int wB = 0;
+    int64_t wnblk = 0;
     DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
     DevBuf<int32_t> perm;                // DoF -> its row in the factored (renumbered) matrix
     DevBuf<double> val, vbuf, ybuf, tbuf;
@@ -2842,6 +2850,18 @@ static int ilu_probe_batched(gls_ctx *c) {
   const int cb = gls::cell_kernel_cells_per_block(dim, c->k, c->nq1d, true), nblk = (c->n_cells + cb - 1) / cb;
   if (c->bact.n < (size_t)B * nblk) GLS_TRY(c->bact.alloc((size_t)B * nblk));
   if (I.fill > 0) HIP_TRY(gls::vec_fill(I.val.p, I.nnz, 0.0, s));  // fill-in positions start at 0
+  // recorded activity (GLS_ILU_PROBE_LIST=0: every (probe, batch) block tests its vector, every time)
+  const char *wl_env = std::getenv("GLS_ILU_PROBE_LIST");
+  const bool wl_on = !(wl_env && wl_env[0] == '0');
+  const bool use_list = wl_on && !I.woff.empty() && I.wB == B && I.wnblk == nblk;
+  const bool record = wl_on && !use_list;
+  std::vector<int32_t> hlist;
+  std::vector<int64_t> hoff;
+  std::vector<uint8_t> hact;
+  if (record) {
+    GLS_TRY(I.wact.alloc((size_t)I.n_probes * nblk));
+    hoff.push_back(0);
+  }
   for (int p0 = 0; p0 < I.n_probes; p0 += B) {
     const int nb = std::min(B, I.n_probes - p0);
     HIP_TRY(gls::vec_fill(I.bV.p, (int64_t)nb * n, 0.0, s));
@@ -2865,13 +2885,31 @@ static int ilu_probe_batched(gls_ctx *c) {
     P.bv_stride = n;
     P.bev_stride = evs;
     P.n_probe = nb;
-    P.bact = c->bact.p;
-    {
+    const int chunk = p0 / B;
+    P.bact = use_list ? I.wact.p + (size_t)p0 * nblk : c->bact.p;
+    if (use_list) {
+      P.work = I.wlist.p + 2 * I.woff[(size_t)chunk];
+      P.n_work = (int)(I.woff[(size_t)chunk + 1] - I.woff[(size_t)chunk]);
+    }
+    if (!use_list || P.n_work > 0) {
       TimedLaunch t(c, (int)gls::MODE_JV);
       HIP_TRY(gls::launch_cell_kernel(c->dim, c->k, c->kp, c->nq1d, gls::MODE_JV, P, c->tables, s));
     }
+    if (record) {  // this chunk's flags: kept on the device for the gathers, listed on the host
+      HIP_TRY(hipMemcpyAsync(I.wact.p + (size_t)p0 * nblk, c->bact.p, (size_t)nb * nblk, hipMemcpyDeviceToDevice, s));
+      hact.resize((size_t)nb * nblk);
+      HIP_TRY(hipMemcpyAsync(hact.data(), c->bact.p, hact.size(), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      for (int v = 0; v < nb; ++v)
+        for (int64_t b = 0; b < nblk; ++b)
+          if (hact[(size_t)v * nblk + b]) {
+            hlist.push_back(v);
+            hlist.push_back((int32_t)b);
+          }
+      hoff.push_back((int64_t)hlist.size() / 2);
+    }
     HIP_TRY(gls::gather_element_vectors_b(I.bY.p, c->bev.p, c->ev_voff.p, c->ev_vslot.p, c->n_vnodes, c->ev_poff.p,
-                                          c->ev_pslot.p, c->n_pnodes, c->dim, nb, n, evs, c->bact.p, el, cb, nblk, s));
+                                          c->ev_pslot.p, c->n_pnodes, c->dim, nb, n, evs, P.bact, el, cb, nblk, s));
     if (c->hang.on)
       HIP_TRY(gls::vec_csr_condense_b(I.bY.p, c->hang.tm.p, c->hang.toff.p, c->hang.tdof.p, c->hang.tw.p,
                                       (int64_t)c->hang.tm.n, nb, n, s));
@@ -2880,6 +2918,12 @@ static int ilu_probe_batched(gls_ctx *c) {
     HIP_TRY(gls::probe_extract_batched(I.val.p, I.pent.p + e0, I.prow.p + e0, I.pepid.p + e0, p0, e1 - e0, I.bY.p, n, s));
   }
   if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
+  if (record) {
+    GLS_TRY(I.wlist.upload(hlist.data(), hlist.size()));
+    I.woff.swap(hoff);
+    I.wB = B;
+    I.wnblk = nblk;
+  }
   return GLS_OK;
 }
 
@@ -5127,6 +5171,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   GLS_TRY(I.ybuf.alloc((size_t)n));
   GLS_TRY(I.tbuf.alloc((size_t)n));
   I.pdoff = pdoff;
+  I.woff.clear();  // new probes: their activity is recorded again
   I.peoff = peoff;
   I.n_probes = nprobe;
   I.nnz = (int64_t)col.size();

@@ -63,7 +63,11 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   const double *tXi = tW + kMaxQ1D;
 
   const int tid = threadIdx.x;
-  const int c0 = blockIdx.x * CB;
+  // batched probing from a recorded work list: this block's (vector, cell batch) pair, known active
+  const bool listed = MODE == MODE_JV && P.work != nullptr;
+  const int bx = listed ? P.work[2 * blockIdx.x + 1] : (int)blockIdx.x;
+  const int by = listed ? P.work[2 * blockIdx.x] : (int)blockIdx.y;
+  const int c0 = bx * CB;
   // cell list (adapted forests: the cells outside the pencil's sibling-group bricks), else all cells
   const int ncb = min(CB, (P.cell_list ? P.cell_list_n : P.n_cells) - c0);
   auto cid = [&](int cl) -> int64_t { return P.cell_list ? (int64_t)P.cell_list[c0 + cl] : (int64_t)(c0 + cl); };
@@ -78,8 +82,10 @@ __global__ void __launch_bounds__(TPB) gls_cell_kernel(const OpParams P, const T
   double *Pev = P.ev;
   if constexpr (MODE == MODE_JV) {
     if (P.bv_stride) {
-      Pv += (int64_t)blockIdx.y * P.bv_stride;
-      Pev += (int64_t)blockIdx.y * P.bev_stride;
+      Pv += (int64_t)by * P.bv_stride;
+      Pev += (int64_t)by * P.bev_stride;
+    }
+    if (P.bv_stride && !listed) {
       int any = 0;
       for (int i = tid; i < ncb * NV; i += blockDim.x) {
         const int64_t b = (int64_t)P.cell_vnodes[cid(i / NV) * NV + i % NV] * DIM;
@@ -638,11 +644,12 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
       if (P.bv_stride) {  // batched probes: small workgroups, so that more (probe, cell batch) pairs skip
         using C64 = Cfg<DIM, K, KP, NQ1, 64>;
         if constexpr (C64::CB >= 1) {
-          hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64>),
-                             dim3((P.n_cells + C64::CB - 1) / C64::CB, P.n_probe), dim3(64),
+          const dim3 grid = P.work ? dim3((unsigned)P.n_work) : dim3((P.n_cells + C64::CB - 1) / C64::CB, P.n_probe);
+          hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64>), grid, dim3(64),
                              (cell_kernel_lds_bytes<DIM, K, KP, NQ1, 64>()), s, P, T);
           break;
         }
+        if (P.work) return hipErrorNotSupported;  // work lists pair with the 64-lane batches only
       }
       if (P.cq && P.cq_mode == 2 && !P.bv_stride)  // from the linearization cache
         hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 256, true>), dim3(blocks), dim3(256), lds, s,

@@ -70,6 +70,8 @@ struct OpParams {
   int64_t bv_stride;          // per-cell MODE_JV batch (probing): blockIdx.y = vector, v / ev at these strides;
   int64_t bev_stride;         //   cell batches on which the vector vanishes skip their element vectors and
   uint8_t *bact;              //   exit, flagged 0 in bact[vector * gridDim.x + block] (1 = computed)
+  const int32_t *work;        //   or: the (vector, block) pairs known to be active, one block each (bact read only)
+  int n_work;
   double *slab;               // brick path: [n_bricks][NBND][4] partial sums of brick-boundary nodes
                               //   (nullptr -> FP64 atomics into y, which the caller zeroes)
   float *slabf;               // FP32 kernels: the same slab in FP32 when set (takes precedence)

@@ -223,3 +223,41 @@ def test_batched_probing_equals_probe_loop_with_hanging_and_slip_lines():
     a, b = out
     assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
     assert np.abs(a.data - b.data).max() <= 1e-14 * np.abs(b.data).max()
+
+
+@pytest.mark.gpu
+def test_recorded_probe_activity_gives_the_same_matrix():
+    """Batched probing records which (probe, cell batch) pairs are active at its first run and launches only those
+    afterwards: at a second state the probed matrix equals the one of a context that tests every pair
+    (GLS_ILU_PROBE_LIST=0), in chunks of 7 probes, on the adapted mapped shell with hanging and slip lines."""
+    from oracle.oracle import MappedProblem
+    from tests.test_dist_plan import _adapted_space
+    from tests.test_gpu_uforest import dof_lines
+    sp_ = _adapted_space(3, 2, 1)
+    lines = dof_lines(sp_)
+    p = MappedProblem(sp_, viscosity=1.0, scheme="steady")
+    p.set_hanging(*lines)
+    p.hang_lines = lines
+    rot = lambda X: np.stack([-X[:, 1], X[:, 0], 0 * X[:, 0]], 1)  # noqa: E731
+    p.set_dirichlet([("function", 0, rot), ("noslip", 1, None), ("slip", 2, None), ("slip", 3, None)])
+    rng = np.random.default_rng(SEED + 6)
+    x0 = p.apply_nonzero_constraints(0.1 * rng.standard_normal(p.n_dofs))
+    x1 = p.apply_nonzero_constraints(0.1 * rng.standard_normal(p.n_dofs))
+    os.environ["GLS_ILU_PROBE_BATCH"] = "7"
+    try:
+        g = context_for(p)
+        g.attach_ilu(1e-12, 1.0)
+        g.set_state(cuda(x0))
+        g.ilu_matrix()  # first probing: records the activity
+        g.set_state(cuda(x1))
+        listed = g.ilu_matrix().tocsr()
+        os.environ["GLS_ILU_PROBE_LIST"] = "0"
+        h = context_for(p)
+        h.attach_ilu(1e-12, 1.0)
+        h.set_state(cuda(x1))
+        tested = h.ilu_matrix().tocsr()
+    finally:
+        os.environ.pop("GLS_ILU_PROBE_BATCH", None)
+        os.environ.pop("GLS_ILU_PROBE_LIST", None)
+    assert np.array_equal(listed.indptr, tested.indptr) and np.array_equal(listed.indices, tested.indices)
+    assert np.array_equal(listed.data, tested.data)
