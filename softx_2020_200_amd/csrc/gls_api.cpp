@@ -2855,6 +2855,14 @@ static int ilu_probe_batched(gls_ctx *c) {
   const bool wl_on = !(wl_env && wl_env[0] == '0');
   const bool use_list = wl_on && !I.woff.empty() && I.wB == B && I.wnblk == nblk;
   const bool record = wl_on && !use_list;
+  // listed blocks read u, grad u, tau and R_s from the linearization cache of this state (the diagonal pass writes
+  // it for every cell; not on forests, whose cache covers the cells outside the bricks only; GLS_ILU_PROBE_CACHE=0)
+  const char *pc_env = std::getenv("GLS_ILU_PROBE_CACHE");
+  bool cq_probe = use_list && cell_cache_on(c) && !c->oct.on && !(pc_env && pc_env[0] == '0');
+  if (cq_probe) {
+    GLS_TRY(ensure_diag(c));
+    cq_probe = c->cq_valid && c->cq.n == cell_cache_size(c);
+  }
   std::vector<int32_t> hlist;
   std::vector<int64_t> hoff;
   std::vector<uint8_t> hact;
@@ -2880,8 +2888,9 @@ static int ilu_probe_batched(gls_ctx *c) {
     P.y = I.bY.p;
     P.hmask = c->hang.on ? c->hang.hmask.p : nullptr;
     P.ev = c->bev.p;
-    // (the probes re-derive the linearization: reading the cache per (probe, cell batch) moves more bytes than
-    // the state gathers -- configs[4]'s ILU setup ran 1.4 ms per Newton step slower with it)
+    // (the first, recording run re-derives the linearization in every (probe, cell batch) block: with all blocks
+    // launched, reading the cache moved more bytes than the state gathers -- configs[4]'s ILU setup ran 1.4 ms per
+    // Newton step slower; the listed runs read it, profiles/r05_ab_probe_cache.txt)
     P.bv_stride = n;
     P.bev_stride = evs;
     P.n_probe = nb;
@@ -2890,6 +2899,10 @@ static int ilu_probe_batched(gls_ctx *c) {
     if (use_list) {
       P.work = I.wlist.p + 2 * I.woff[(size_t)chunk];
       P.n_work = (int)(I.woff[(size_t)chunk + 1] - I.woff[(size_t)chunk]);
+      if (cq_probe) {
+        P.cq = c->cq.p;
+        P.cq_mode = 2;
+      }
     }
     if (!use_list || P.n_work > 0) {
       TimedLaunch t(c, (int)gls::MODE_JV);

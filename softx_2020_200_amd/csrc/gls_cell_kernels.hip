@@ -645,8 +645,12 @@ hipError_t launch_cell_g(int mode, const OpParams &P, const Tables1D &T, hipStre
         using C64 = Cfg<DIM, K, KP, NQ1, 64>;
         if constexpr (C64::CB >= 1) {
           const dim3 grid = P.work ? dim3((unsigned)P.n_work) : dim3((P.n_cells + C64::CB - 1) / C64::CB, P.n_probe);
-          hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64>), grid, dim3(64),
-                             (cell_kernel_lds_bytes<DIM, K, KP, NQ1, 64>()), s, P, T);
+          if (P.work && P.cq && P.cq_mode == 2)  // listed blocks from the linearization cache
+            hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64, true>), grid, dim3(64),
+                               (cell_kernel_lds_bytes<DIM, K, KP, NQ1, 64>()), s, P, T);
+          else
+            hipLaunchKernelGGL((gls_cell_kernel<DIM, K, KP, NQ1, MODE_JV, GEN, 64>), grid, dim3(64),
+                               (cell_kernel_lds_bytes<DIM, K, KP, NQ1, 64>()), s, P, T);
           break;
         }
         if (P.work) return hipErrorNotSupported;  // work lists pair with the 64-lane batches only

@@ -228,8 +228,9 @@ def test_batched_probing_equals_probe_loop_with_hanging_and_slip_lines():
 @pytest.mark.gpu
 def test_recorded_probe_activity_gives_the_same_matrix():
     """Batched probing records which (probe, cell batch) pairs are active at its first run and launches only those
-    afterwards: at a second state the probed matrix equals the one of a context that tests every pair
-    (GLS_ILU_PROBE_LIST=0), in chunks of 7 probes, on the adapted mapped shell with hanging and slip lines."""
+    afterwards (from the cached linearization where the state has one): at a second state the probed matrix equals the
+    one of a context that tests every pair (GLS_ILU_PROBE_LIST=0), in chunks of 7 probes, on the adapted mapped shell
+    with hanging and slip lines."""
     from oracle.oracle import MappedProblem
     from tests.test_dist_plan import _adapted_space
     from tests.test_gpu_uforest import dof_lines
@@ -260,4 +261,5 @@ def test_recorded_probe_activity_gives_the_same_matrix():
         os.environ.pop("GLS_ILU_PROBE_BATCH", None)
         os.environ.pop("GLS_ILU_PROBE_LIST", None)
     assert np.array_equal(listed.indptr, tested.indptr) and np.array_equal(listed.indices, tested.indices)
-    assert np.array_equal(listed.data, tested.data)
+    # the listed blocks read the linearization the diagonal pass cached (its own FMA contraction): rounding only
+    assert np.abs(listed.data - tested.data).max() <= 1e-14 * np.abs(tested.data).max()
