@@ -357,13 +357,20 @@ def bench_cylinder3d(args):
     qall = tc  # configs[3]: MappingQ2 on every cell
     levels, sw = None, 0
     if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh
-        if refine < 1:
-            sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 (a hierarchy below the fine mesh)")
+        if refine < 1 and not args.cyl_plevel:
+            sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 or the p-level (a level below the fine mesh)")
         m = mesh(refine)
+        base = m.coarsen_to(0)
         handles = [m.fe_space_handle(2, 1, qmapping_all=qall)] + [
-            m.coarsen_to(refine - l).fe_space_handle(2, 1, qmapping_all=qall) for l in range(1, refine + 1)]
-        xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(refine)]
-        levels = [make(h.data) for h in handles]
+            m.coarsen_to(refine - l).fe_space_handle(2, 1, qmapping_all=qall) for l in range(1, refine)] + (
+            [base.fe_space_handle(2, 1, qmapping_all=qall)] if refine >= 1 else [])
+        kps = [(2, 1)] * len(handles)
+        if args.cyl_plevel:  # p-level below the base mesh: Q1-Q1 on the same cells, solved exactly
+            handles.append(base.fe_space_handle(1, 1, qmapping_all=qall))
+            kps.append((1, 1))
+        xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(len(handles) - 1)]
+        levels = [(taylorcouette3d_context(h.data, k=k_, kp=kp_) if tc else cylinder3d_context(k=k_, kp=kp_, space=h.data))
+                  for h, (k_, kp_) in zip(handles, kps)]
         ctx, sp, x = levels[0]
         for c_, _, _ in levels:
             c_.set_time(scheme, ts)
@@ -371,7 +378,7 @@ def bench_cylinder3d(args):
         nco = levels[-1][0].n_dofs
         ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
                                        coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=0.6,
-                                       coarse_direct=1 if nco <= 8192 else -1, smoother=args.cyl_smoother)
+                                       coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother)
     else:
         ctx, sp, x = make(mesh(refine).fe_space(2, 1, qmapping_all=qall))
         ctx.set_time(scheme, ts)
@@ -431,7 +438,8 @@ def bench_cylinder3d(args):
                                          {"ilu": "multicolor ILU(0)", "jacobi": "damped-Jacobi",
                                           "ilu-coarse": "damped-Jacobi on the finest, multicolor ILU(0) below"}[
                                              args.cyl_smoother],
-                                         "exact LU" if levels[-1][0].n_dofs <= 8192 else "%d sweeps" % args.mg_coarse_sweeps_cyl))
+                                         ("exact LU of the Q1-Q1 p-level" if args.cyl_plevel else "exact LU")
+                                         if levels[-1][0].n_dofs <= args.direct_max else "%d sweeps" % args.mg_coarse_sweeps_cyl))
                    if levels else "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
                        args.restart, args.ilu_fill, "multicolor" if args.ilu_fill == 0 else "Cuthill-McKee")},
         "setup_s": t_setup,
@@ -590,10 +598,33 @@ def spawn_ranks(n):
     return 0
 
 
-def preflight(args, rank, world, dev, dist):
+def preflight_agreement(dist, ctl, world, failed, late):
+    """The ranks' pre-flight outcomes, agreed over the gloo control group `ctl` (created with a timeout), never
+    over the data-path transport that a failed rank may have left inside a collective. failed: this rank's
+    pre-flight raised or missed the tolerance; late: it raised after the transport's first collective.
+    Returns "ok"; "fallback" when no rank can be stuck in the native transport (every failure came before its
+    first collective, or every rank failed); "abort" when a rank failed after the first collective while
+    another did not, or a peer never reached the agreement (the control group's timeout)."""
+    import torch
+    t = torch.tensor([float(bool(failed)), float(bool(failed) and bool(late))], dtype=torch.float64)
+    try:
+        dist.all_reduce(t, group=ctl)
+    except Exception as e:  # noqa: BLE001 -- a peer is stuck in the data-path transport
+        sys.stderr.write("bench.py: pre-flight agreement failed (%r): a rank did not reach it\n" % (e,))
+        return "abort"
+    nfail, nlate = t.tolist()
+    if nfail == 0:
+        return "ok"
+    if nlate == 0 or nfail == world:
+        return "fallback"
+    return "abort"
+
+
+def preflight(args, rank, world, dev, dist, stage=None):
     """N-rank residual and J.v of a 16^3 cavity (the bench's boundary data, state and scheme; the same
     transport as the timed run) against a single-rank context of the whole mesh on rank 0. Returns the
-    max relative difference (every rank gets rank 0's number)."""
+    max relative difference (every rank gets rank 0's number). stage["s"] becomes "collective" when the
+    transport's first collective (the communicator's creation) starts."""
     import torch
 
     import softx_2020_200_amd as sx
@@ -607,9 +638,13 @@ def preflight(args, rank, world, dev, dist):
     u = smooth_state(mesh, n, 3, dd, dv, 0.0)
     u2 = smooth_state(mesh, n, 3, dd, dv, 0.3)
     v = np.random.default_rng(20200200).uniform(-1.0, 1.0, len(u))
+    if stage is not None:
+        stage["s"] = "collective"
     dp = DistributedProblem(mesh, rank, world, dev, viscosity=args.nu, vnode_mask=mask, dirichlet=(dd, dv),
                             backend=args.dist_backend, impl=args.dist_impl)
     dist.barrier()  # first collective before any batched P2P (NCCL requirement)
+    if os.environ.get("GLS_BENCH_FAIL_NATIVE_PREFLIGHT") == "late%d" % rank and args.dist_impl == "native":
+        raise RuntimeError("GLS_BENCH_FAIL_NATIVE_PREFLIGHT (after the first collective)")
     loc = lambda g: torch.from_numpy(local_vector(dp.plan, g, nv)).to(dev)  # noqa: E731
     dp.ctx.set_time(args.scheme, (args.dt,) * 4)
     dp.ctx.set_state(loc(u), loc(u), loc(u2))
@@ -667,6 +702,11 @@ def main():
                     help="cylinder3d --cyl-precond hmg: level smoother (ILU(0) V(1,1) or damped Jacobi V(2,2))")
     ap.add_argument("--mg-coarse-sweeps-cyl", type=int, default=10,
                     help="cylinder3d --cyl-precond hmg: ILU sweeps on the base (coarsest) mesh")
+    ap.add_argument("--cyl-plevel", type=int, default=1,
+                    help="cylinder3d / taylorcouette3d --cyl-precond hmg: 1 = a Q1-Q1 p-level below the base mesh "
+                         "(gls_fe_space_mg_transfer's p-level pair), solved by the dense LU")
+    ap.add_argument("--direct-max", type=int, default=40000,
+                    help="hmg: the coarsest level is factored (dense LU) up to this many DoFs, else smoothed")
     ap.add_argument("--rel", type=float, default=1e-4)
     ap.add_argument("--octree-steps", type=int, default=3, help="octree: lid / edge refinement levels")
     ap.add_argument("--precond", default="mg", choices=["mg", "jacobi", "ilu"],
@@ -709,9 +749,11 @@ def main():
                          "ncclSend/ncclRecv/ncclAllReduce on the context stream, ghost import overlapped with the "
                          "interior bricks) or torch.distributed callbacks (host-synchronous; the gloo tests)")
     args = ap.parse_args()
-    # GLS_BENCH_FAIL_NATIVE_PREFLIGHT=1 (test hook): the native transport's pre-flight raises on every rank, so the
-    # fallback to the torch.distributed transport runs (on one GPU with gloo)
-    fail_native = os.environ.get("GLS_BENCH_FAIL_NATIVE_PREFLIGHT") == "1"
+    # GLS_BENCH_FAIL_NATIVE_PREFLIGHT (test hooks): "1" -- the native transport's pre-flight raises on every rank
+    # before its first collective, so the fallback to the torch.distributed transport runs (on one GPU with gloo);
+    # "late<r>" -- rank r raises after the first collective, so the run aborts instead of falling back
+    fail_env = os.environ.get("GLS_BENCH_FAIL_NATIVE_PREFLIGHT", "")
+    fail_native = fail_env == "1" or fail_env.startswith("late")
     if args.dist_backend == "gloo" and not fail_native:  # host-staged testing transport: no RCCL communicator
         args.dist_impl = "torch"
     env_world = os.environ.get("WORLD_SIZE")
@@ -755,18 +797,27 @@ def main():
         ids = [None] * world
         dist.all_gather_object(ids, str(getattr(props, "uuid", None) or "%s:%d" % (os.uname().nodename, local)))
         devices = len(set(ids))
+        from datetime import timedelta
+        ctl = dist.new_group(backend="gloo", timeout=timedelta(seconds=180))  # control plane of the pre-flight
+        stage = {"s": "local"}
         try:
-            if fail_native and args.dist_impl == "native":
+            if fail_env == "1" and args.dist_impl == "native":
                 raise RuntimeError("GLS_BENCH_FAIL_NATIVE_PREFLIGHT")
-            pre_err = preflight(args, rank, world, torch.device("cuda", local), dist)
-            failed = 0.0 if pre_err <= 1e-12 else 1.0
+            pre_err = preflight(args, rank, world, torch.device("cuda", local), dist, stage)
+            failed = not pre_err <= 1e-12
         except Exception as e:  # noqa: BLE001 -- reported, and the ranks agree on it below
-            sys.stderr.write("bench.py: rank %d pre-flight with the %s transport raised: %r\n" % (rank, args.dist_impl, e))
-            pre_err, failed = float("nan"), 1.0
-        flag = torch.tensor([failed], dtype=torch.float64, device=torch.device("cuda", local) if args.dist_backend == "nccl"
-                            else "cpu")
-        dist.all_reduce(flag)
-        if flag.item() > 0 and args.dist_impl == "native":
+            sys.stderr.write("bench.py: rank %d pre-flight with the %s transport raised (%s stage): %r\n"
+                             % (rank, args.dist_impl, stage["s"], e))
+            pre_err, failed = float("nan"), True
+        verdict = preflight_agreement(dist, ctl, world, failed, stage["s"] == "collective" and pre_err != pre_err)
+        if verdict == "abort":
+            sys.stderr.write("bench.py: rank %d: pre-flight failed after the transport's first collective; no fallback "
+                             "(a peer may be inside a collective)\n" % rank)
+            sys.stderr.flush()
+            os._exit(4)
+        if verdict == "fallback" and args.dist_impl == "native":
+            from softx_2020_200_amd.dist import drop_rccl
+            drop_rccl()
             # the in-library RCCL transport failed its check on some rank: the timed run takes torch.distributed's
             # RCCL (callbacks) instead, after the same pre-flight, and the line says so
             if rank == 0:

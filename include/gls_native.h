@@ -450,8 +450,13 @@ int gls_gpart_destroy(gls_gpart *p);
 /* The same plan from the rank's LOCAL PART only (distributed forest: no rank holds the global mesh;
  * the p::d triangulation's locally relevant cells, navier_stokes_base.cc:55-60): the owned cells
  * (cell_owner == rank, in the given order) plus the ghost layer -- every cell sharing a node with an
- * owned cell or linked to one through a hanging line (a line DoF on one cell, a master on the other) --
- * each with its owner; the lines whose DoF lies on a provided cell. Nodes are 64-bit keys unique over
+ * owned cell, and every cell touching a MASTER node of a hanging line whose DoF lies on an owned cell
+ * (e.g. the far corner / edge midpoints of a coarse face) -- each with its owner; the lines whose DoF
+ * lies on a provided cell. A node is owned by the lowest rank among ALL cells touching it, so each node
+ * the rank needs must come with every cell touching it: with a thinner layer (p4est's one-cell ghost
+ * layer alone) two ranks can disagree on an owner and on the exchange lists. A needed master node that
+ * lies on no provided cell is rejected (GLS_EINVAL); a missing cell of a provided node cannot be seen
+ * locally -- dist.local_part() builds the layer by this rule. Nodes are 64-bit keys unique over
  * the forest (no global numbering needed); DoF keys are key * (dim + 1) + c with c = dim for pressure
  * (line_dofs / line_masters and gls_gpart_map_dofs use DoF keys). cell_pkeys = NULL for equal order.
  * vnode_l2g / pnode_l2g of gls_gpart_get return the local nodes' keys; the exchange lists are those of

@@ -378,6 +378,9 @@ struct gls_ctx {
   // rthresh) and factored in place by rocSPARSE; M^-1 v = U^-1 L^-1 v (two sparse triangular solves)
   struct ILU {
     bool on = false, valid = false;
+    // attached by the multigrid for its coarse matrix's probing pattern only (mg_probe_setup): never factored or
+    // applied as a preconditioner / smoother of this context
+    bool probe_only = false;
     double athresh = 0., rthresh = 1.;
     double boost_tol = 0., boost_val = 0.;  // rocsparse keeps these POINTERS and reads them in csrilu0
     int n_probes = 0, fill = 0;
@@ -686,7 +689,7 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
   // sum order: nodes by their first (lowest) slot, i.e. in slab order of their lowest brick, so
   // that consecutive threads of k_slab_sum read consecutive slab entries (node order would leave
   // the x-face nodes of every brick row 4 lattice points apart: 2.3x read amplification, PMC)
-  if (!std::getenv("GLS_SLAB_NODE_ORDER")) {
+  {
     const size_t m = nodes.size();
     std::vector<int32_t> perm(m);
     for (size_t i = 0; i < m; ++i) perm[i] = (int32_t)i;
@@ -732,7 +735,7 @@ int build_slab_map(gls_ctx *c, const gls_mesh_desc *d) {
     if (ok) c->cube_nb1 = (int)(n / 2);
   }
   // brick coloring: greedy in brick (Morton) order over the bricks sharing a surface node
-  if (!gls::brick_colors_supported(K) || !std::getenv("GLS_BRICK_COLORS")) return GLS_OK;
+  if (!gls::brick_colors_supported(K)) return GLS_OK;  // only in a -DGLS_BRICK_COLORS_BUILD library (A/B)
   std::vector<int> color((size_t)nb, -1);
   int ncol = 0;
   for (int64_t b = 0; b < nb; ++b) {
@@ -1038,7 +1041,7 @@ int dist_multidot(gls_ctx *c, const double *A, int64_t lda, int nk, const double
 // launch (workgroup brick kernel): no separate FP64 -> FP32 conversion pass over the linearization
 int lin_f32_target(gls_ctx *c, gls::OpParams &P) {
   P.qdf = nullptr;
-  if (!c->smooth_f32 || !gls::brick_fused_jacobi_supported(c->k) || std::getenv("GLS_LIN_NO_F32")) return GLS_OK;
+  if (!c->smooth_f32 || !gls::brick_fused_jacobi_supported(c->k)) return GLS_OK;
   if (c->qdata32.n != c->qdata.n) GLS_TRY(c->qdata32.alloc(c->qdata.n));
   P.qdf = c->qdata32.p;
   P.oseen = c->smooth_oseen ? 1 : 0;  // the Oseen smoother reads u and tau only: the other FP32 rows are not written
@@ -1103,14 +1106,14 @@ int build_brick_split(gls_ctx *c, const std::vector<char> &flag) {
 
 // J.v launched as two brick subsets (boundary, then interior) with the ghost import between them:
 // the RCCL transport imports on the exchange stream while the interior bricks run
-// (GLS_NO_OVERLAP=1: off); GLS_SPLIT_TEST=m on a single-GPU context splits at "bricks b % m == 0"
+// GLS_SPLIT_TEST=m on a single-GPU context splits at "bricks b % m == 0"
 // with no exchange, for the bitwise test of the split launch; GLS_SPLIT_DIST=1 runs the same split
 // launch with the callback transport (import first, then interior and boundary bricks), so the
 // boundary / interior classification of a real partition is tested without an RCCL communicator
 bool split_jv_enabled(gls_ctx *c) {
   if (!c->use_brick || !c->use_qdata || c->use_colors || c->hang.on || !gls::brick_subset_supported(c->k)) return false;
   if (c->dist.on)
-    return c->split.p && !std::getenv("GLS_NO_OVERLAP") && (c->dist.comm != nullptr || std::getenv("GLS_SPLIT_DIST"));
+    return c->split.p && (c->dist.comm != nullptr || std::getenv("GLS_SPLIT_DIST"));
   const char *t = std::getenv("GLS_SPLIT_TEST");
   if (!t || std::atoi(t) < 1) return false;
   if (!c->split.p) {
@@ -1158,8 +1161,7 @@ int ensure_element_maps(gls_ctx *c) {
 int ensure_diag(gls_ctx *c);
 // the per-cell linearization cache: on for contexts that run the per-cell kernels
 bool cell_cache_on(const gls_ctx *c) {
-  static const bool off = [] { const char *e = std::getenv("GLS_CELL_CACHE"); return e && std::atoi(e) == 0; }();
-  return !off && !c->use_brick && c->n_cells > 0;
+  return !c->use_brick && c->n_cells > 0;
 }
 size_t cell_cache_size(const gls_ctx *c) {
   const int dim = c->dim;
@@ -1183,7 +1185,7 @@ int run_cell(gls_ctx *c, int mode, const double *v, double *y) {
   if (c->n_hist > 0 && !c->u1) return set_err(GLS_EINVAL, "scheme needs solution_m1");
   if (c->n_hist > 1 && !c->u2) return set_err(GLS_EINVAL, "scheme needs solution_m2");
   if (c->n_hist > 2 && !c->u3) return set_err(GLS_EINVAL, "scheme needs solution_m3");
-  // per-cell J.v from the diagonal pass's linearization cache (GLS_CELL_CACHE=0: re-derived every time)
+  // per-cell J.v from the diagonal pass's linearization cache
   const bool cq_on = cell_cache_on(c) && (mode == gls::MODE_JV || mode == gls::MODE_DIAG);
   if (cq_on) {
     const size_t need = cell_cache_size(c);
@@ -1442,7 +1444,7 @@ int gls_create(const gls_mesh_desc *d, gls_ctx **out) {
 
   GLS_TRY(c->cell_vnodes.upload(d->cell_vnodes, (size_t)d->n_cells * nv));
   c->use_brick = !mapped && detect_bricks(d, nq1d);
-  if (c->use_brick && !std::getenv("GLS_BRICK_ATOMICS")) GLS_TRY(build_slab_map(c.get(), d));
+  if (c->use_brick) GLS_TRY(build_slab_map(c.get(), d));
   if (const char *e = std::getenv("GLS_JV_RECOMPUTE")) c->use_qdata = std::atoi(e) == 0;
   if (d->cell_pnodes) GLS_TRY(c->cell_pnodes.upload(d->cell_pnodes, (size_t)d->n_cells * np));
   std::vector<double> geo((size_t)d->n_cells * 4);
@@ -1968,7 +1970,7 @@ int ilu_sweep(gls_ctx *g, double *x, const double *b, double *y, double *z) {
   return GLS_OK;
 }
 int smoother_sweep(gls_ctx *g, double *x, const double *b, double *y, double omega, double *z = nullptr) {
-  if (z && g->ilu.on) return ilu_sweep(g, x, b, y, z);
+  if (z && g->ilu.on && !g->ilu.probe_only) return ilu_sweep(g, x, b, y, z);
   const bool nofuse = std::getenv("GLS_MG_NO_FUSE") != nullptr;
   const bool brick = g->use_brick && g->use_qdata && (g->use_colors || brick_slab(g)) && !g->dist.on &&
                      !g->hang.on && gls::brick_fused_jacobi_supported(g->k);
@@ -2299,15 +2301,16 @@ static int coarse_inverse_check(gls_ctx *c, int64_t n, bool *good) {
   return GLS_OK;
 }
 
-// the direct coarse solve's matrix by colored probing on a per-cell level (mg.probe_ilu; GLS_MG_PROBE_LOOP=1:
-// one J.v per column as before): the ILU structure (CM order, fill 0, one block) is attached once
+// the direct coarse solve's matrix by colored probing on a per-cell level (mg.probe_ilu; brick levels and
+// distributed or nested contexts: one J.v per column): the ILU structure (CM order, fill 0, one block) is attached once
 int mg_probe_setup(gls_ctx *c, gls_ctx *g) {
   auto &mg = c->mg;
   mg.probe_ilu = nullptr;
-  if (std::getenv("GLS_MG_PROBE_LOOP") || (g->use_brick && g->use_qdata) || g->dist.on || g->mg.on || g->ilu.on)
+  if ((g->use_brick && g->use_qdata) || g->dist.on || g->mg.on || g->ilu.on)
     return GLS_OK;
   GLS_TRY(gls_ilu_set_options(g, GLS_ILU_ORDER_CM, 0));
   GLS_TRY(gls_ilu_attach(g, 0, 0.0, 1.0));
+  g->ilu.probe_only = true;
   mg.ilu_levels.push_back(g);  // detached with the multigrid
   GLS_TRY(mg.pinv.alloc((size_t)g->n_dofs));
   mg.probe_ilu = g;
@@ -2673,7 +2676,7 @@ int mg_vcycle_rep2(gls_ctx *c, const double *b, double *x) {
   hipStream_t s = c->stream;
   GLS_TRY(ensure_diag(c));
   double *y = mgbuf(c, 0, MB_Y);
-  double *zs = mg.ilu_smooth && c->ilu.on ? mgbuf(c, 0, MB_BOX) : nullptr;
+  double *zs = mg.ilu_smooth && c->ilu.on && !c->ilu.probe_only ? mgbuf(c, 0, MB_BOX) : nullptr;
   const int pre = mg.lpre[0], post = mg.lpost[0];
   if (pre > 0 && zs) {
     GLS_TRY(ensure_ilu(c));
@@ -2776,7 +2779,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   }
   // one pre-sweep from 0 on a fused level: x = omega D^-1 b is formed inside the residual's J.v
   const bool first_fused = pre == 1 && l < L - 1 && first_sweep_fusable(g);
-  double *zs = mg.ilu_smooth && g->ilu.on ? mgbuf(c, l, MB_BOX) : nullptr;  // ILU smoothing scratch
+  double *zs = mg.ilu_smooth && g->ilu.on && !g->ilu.probe_only ? mgbuf(c, l, MB_BOX) : nullptr;  // ILU smoothing scratch
   if (pre > 0 && !first_fused && zs) {
     GLS_TRY(ensure_ilu(g));
     GLS_TRY(apply_ilu(g, b, x));  // first sweep from x = 0: x = M^-1 b
@@ -2856,9 +2859,8 @@ static int ilu_probe_batched(gls_ctx *c) {
   const bool use_list = wl_on && !I.woff.empty() && I.wB == B && I.wnblk == nblk;
   const bool record = wl_on && !use_list;
   // listed blocks read u, grad u, tau and R_s from the linearization cache of this state (the diagonal pass writes
-  // it for every cell; not on forests, whose cache covers the cells outside the bricks only; GLS_ILU_PROBE_CACHE=0)
-  const char *pc_env = std::getenv("GLS_ILU_PROBE_CACHE");
-  bool cq_probe = use_list && cell_cache_on(c) && !c->oct.on && !(pc_env && pc_env[0] == '0');
+  // it for every cell; not on forests, whose cache covers the cells outside the bricks only)
+  bool cq_probe = use_list && cell_cache_on(c) && !c->oct.on;
   if (cq_probe) {
     GLS_TRY(ensure_diag(c));
     cq_probe = c->cq_valid && c->cq.n == cell_cache_size(c);
@@ -3038,7 +3040,7 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
 int apply_prec(gls_ctx *c, const double *v, double *z) {
   if (c->mg.on && c->mg.rep_csr) return mg_vcycle_rep2(c, v, z);
   if (c->mg.on) return mg_vcycle(c, 0, v, z);
-  if (c->ilu.on) return apply_ilu(c, v, z);
+  if (c->ilu.on && !c->ilu.probe_only) return apply_ilu(c, v, z);
   HIP_TRY(gls::vec_div(z, v, c->diag.p, c->n_dofs, c->stream));
   return GLS_OK;
 }
@@ -3284,10 +3286,9 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
     }
   for (auto *g : mg.lev) g->smooth_f32 = p->mixed_precision != 0;
   // the smoother's operator: Newton's Jacobian, or its Oseen (Picard) part (FP32 brick levels only: the
-  // pencil J.v drops the (grad u) v terms; GLS_MG_OSEEN=0/1 overrides for A/B)
+  // pencil J.v drops the (grad u) v terms)
   {
-    const char *e = std::getenv("GLS_MG_OSEEN");
-    const bool os = e ? std::atoi(e) != 0 : p->smoother_operator == 1;
+    const bool os = p->smoother_operator == 1;
     if (p->smoother_operator < 0 || p->smoother_operator > 1) return set_err(GLS_EINVAL, "mg: smoother_operator 0 or 1");
     for (auto *g : mg.lev) g->smooth_oseen = os && g->smooth_f32;
   }
@@ -3304,12 +3305,10 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
   if (mg.ilu_smooth)  // ILU(0) on every level above the coarsest (multicolor order); smoother 2: not the finest
     for (int l = p->smoother == 2 ? 1 : 0; l + 1 < p->n_levels; ++l) {
       gls_ctx *g = mg.lev[(size_t)l];
-      // multicolor order on every level (GLS_MG_ILU_MC_MIN: the level size from which it is used; Cuthill-McKee
-      // below). As a smoother the color-by-color ILU(0) is both faster per sweep (no level-scheduled csrsv) and
+      // multicolor order on every level. As a smoother the color-by-color ILU(0) is both faster per sweep (no level-scheduled csrsv) and
       // stronger: configs[3] --precond hmg 38 -> 26 GMRES iterations, 3.97 -> 1.37 s wall, the linear solves
       // 1.72 -> 0.08 s (profiles/r05_app_configs3_hmg_ilu_order.txt)
-      static const int64_t mc_min = std::getenv("GLS_MG_ILU_MC_MIN") ? std::atoll(std::getenv("GLS_MG_ILU_MC_MIN")) : 0;
-      GLS_TRY(gls_ilu_set_options(g, g->n_dofs > mc_min ? GLS_ILU_ORDER_MULTICOLOR : GLS_ILU_ORDER_CM, 0));
+      GLS_TRY(gls_ilu_set_options(g, GLS_ILU_ORDER_MULTICOLOR, 0));
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
       mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
@@ -3376,11 +3375,10 @@ int gls_mg_attach(gls_ctx *c, const gls_mg_params *p) {
   // 1D transfer taps: fine lattice index i sits at x = i / (2k) coarse cells from the box origin;
   // prolongation interpolates the coarse Qk field of the parent cell (equidistant nodes, k <= 2)
   const int K = c->k;
-  const bool two_pass_ok = !std::getenv("GLS_MG_ONEPASS");
   size_t xwork = 0;
   for (int l = 0; l + 1 < p->n_levels; ++l) {
     std::unique_ptr<gls_ctx::MG::Taps> T(new gls_ctx::MG::Taps);
-    T->two_pass = two_pass_ok;
+    T->two_pass = true;
     xwork = std::max(xwork, (size_t)4 * mg.dims[l + 1][0] * mg.dims[l + 1][1] * mg.dims[l][2]);
     for (int a = 0; a < 3; ++a) {
       const int nf = mg.dims[l][a], nc = mg.dims[l + 1][a], ncc = (nf - 1) / (2 * K);
@@ -3478,7 +3476,6 @@ int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *c
     };
     X->plane = lanes((double)nnz / (double)std::max<int64_t>(nf, 1));
     X->rlane = lanes((double)nnz / (double)std::max<int64_t>(nc, 1));
-    if (const char *e = std::getenv("GLS_MG_SPMV_LANES")) X->plane = X->rlane = std::atoi(e);
     GLS_TRY(X->poff.upload(off, (size_t)nf + 1));
     GLS_TRY(X->pcol.upload(p_col[l], (size_t)std::max<int64_t>(nnz, 1)));
     GLS_TRY(X->pw.upload(p_w[l], (size_t)std::max<int64_t>(nnz, 1)));
@@ -3779,11 +3776,9 @@ int gls_solve_linear(gls_ctx *c, const double *b, double *x, gls_linear_params *
   double beta = std::sqrt(bnorm2);
   int it = 0;
   std::vector<double> H((size_t)(m + 1) * m), cs(m), sn(m), g(m + 1), hc2(m + 2), y(m);
-  // Gram-corrected single-pass orthogonalisation (default; prm->orthogonalization = GLS_ORTHO_CGS2 or
-  // GLS_GMRES_CGS2=1: classical Gram-Schmidt with the DGKS second pass); Gm: measured off-diagonal part
-  // of V^T V of the current restart cycle
-  static const bool env_cgs2 = [] { const char *e = std::getenv("GLS_GMRES_CGS2"); return e && std::atoi(e) != 0; }();
-  const bool gram = !env_cgs2 && prm->orthogonalization != GLS_ORTHO_CGS2;
+  // Gram-corrected single-pass orthogonalisation (default; prm->orthogonalization = GLS_ORTHO_CGS2: classical
+  // Gram-Schmidt with the DGKS second pass); Gm: measured off-diagonal part of V^T V of the current restart cycle
+  const bool gram = prm->orthogonalization != GLS_ORTHO_CGS2;
   int ortho_repairs = 0;
   // test knobs (read per call): GLS_GMRES_REPAIR_TOL (default 1e-8; 0 repairs every column) and
   // GLS_GMRES_REPAIR_MEASURED=1 (the repair pass always normalises by the measured norm)
@@ -4169,7 +4164,7 @@ struct DevicePhysics {
       SectionScope t(c, GLS_SEC_SETUP_GMG);
       GLS_TRY(ensure_diag(c));
       GLS_TRY(mg_prepare(c));
-    } else if (c->ilu.on) {
+    } else if (c->ilu.on && !c->ilu.probe_only) {
       SectionScope t(c, GLS_SEC_SETUP_ILU);
       GLS_TRY(ensure_diag(c));
       GLS_TRY(ensure_ilu(c));
@@ -4422,6 +4417,7 @@ int gls_timing_get(gls_ctx *c, int which, double *ms, int64_t *cnt) {
 extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthresh) {
   GLS_TRY(check_ctx(c));
   auto &I = c->ilu;
+  I.probe_only = false;  // a caller's attach: a preconditioner (mg_probe_setup marks its own afterwards)
   if (c->dist.on && !c->dist.dofs) return set_err(GLS_EINVAL, "gls_ilu_attach: brick-partitioned contexts use the multigrid");
   if (c->mg.on) return set_err(GLS_EINVAL, "gls_ilu_attach: a multigrid preconditioner is attached");
   if (fill < 0 || fill > GLS_ILU_MAX_FILL)
@@ -4588,7 +4584,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   };
   std::vector<RemoteEntry> remote;
   int n_rounds = 0;
-  const bool cmpl = c->dist.on && c->dist.dofs && std::getenv("GLS_ILU_LOCAL_ROWS") == nullptr;
+  const bool cmpl = c->dist.on && c->dist.dofs;
   if (cmpl) {
     auto fdir = [&](int64_t d) { return fcons[(size_t)d] && !isline[(size_t)d]; };
     std::vector<int64_t> feoff((size_t)nc + 1, 0), feff, buf;
@@ -4863,42 +4859,16 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     // is ~colors x DoFs per node. (Blocks only drop couplings here: the colors stay outermost.)
     std::vector<int> c1((size_t)nu, -1), used;
     int ncl = 0;
-    // visit order of the greedy coloring: Cuthill-McKee (default) or smallest-last (GLS_ILU_COLORING=sl:
-    // nodes removed by minimum remaining degree, colored in reverse removal order -- fewer colors)
+    // visit order of the greedy coloring: Cuthill-McKee (smallest-last ordering gave 36 instead of 46 colors but
+    // 104 instead of 60 GMRES iterations, profiles/r03_ilu_coloring_ab.txt)
     std::vector<int64_t> visit;
     visit.reserve((size_t)nu);
-    const char *cm_env = std::getenv("GLS_ILU_COLORING");
-    if (cm_env && !std::strcmp(cm_env, "sl")) {
-      std::vector<int64_t> deg((size_t)nu, 0);
-      for (int64_t x = 0; x < nu; ++x)
-        for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) deg[(size_t)x] += n1[(size_t)u] != x;
-      std::set<std::pair<int64_t, int64_t>> q;
-      for (int64_t x = 0; x < nu; ++x) q.insert({deg[(size_t)x], x});
-      std::vector<char> gone((size_t)nu, 0);
-      std::vector<int64_t> removal;
-      removal.reserve((size_t)nu);
-      while (!q.empty()) {
-        const auto it = q.begin();
-        const int64_t x = it->second;
-        q.erase(it);
-        gone[(size_t)x] = 1;
-        removal.push_back(x);
-        for (int64_t u = n1off[(size_t)x]; u < n1off[(size_t)x + 1]; ++u) {
-          const int64_t y = n1[(size_t)u];
-          if (y == x || gone[(size_t)y]) continue;
-          q.erase({deg[(size_t)y], y});
-          q.insert({--deg[(size_t)y], y});
-        }
-      }
-      visit.assign(removal.rbegin(), removal.rend());
-    } else {
-      std::vector<char> seen((size_t)nu, 0);
-      for (int64_t t = 0; t < n; ++t) {
-        const int64_t x = dnode_[(size_t)order[(size_t)t]];
-        if (!seen[(size_t)x]) {
-          seen[(size_t)x] = 1;
-          visit.push_back(x);
-        }
+    std::vector<char> seen((size_t)nu, 0);
+    for (int64_t t = 0; t < n; ++t) {
+      const int64_t x = dnode_[(size_t)order[(size_t)t]];
+      if (!seen[(size_t)x]) {
+        seen[(size_t)x] = 1;
+        visit.push_back(x);
       }
     }
     for (const int64_t x : visit) {
@@ -5048,7 +5018,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       // colors' U parts)
       I.mc_wl.assign((size_t)ncl, 1);
       I.mc_wu.assign((size_t)ncl, 1);
-      const char *we = std::getenv("GLS_ILU_SOLVE_WAVES");
       for (int c = 0; c < ncl; ++c) {
         const int32_t ra = grow[(size_t)cg[(size_t)c]], rb = grow[(size_t)cg[(size_t)c + 1]];
         const int ng = cg[(size_t)c + 1] - cg[(size_t)c];
@@ -5059,7 +5028,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
         }
         I.mc_wl[(size_t)c] = (uint8_t)(ng && nlo > 256 * (int64_t)ng ? 4 : 1);
         I.mc_wu[(size_t)c] = (uint8_t)(ng && nup > 256 * (int64_t)ng ? 4 : 1);
-        if (we) I.mc_wl[(size_t)c] = I.mc_wu[(size_t)c] = (uint8_t)(std::atoi(we) >= 4 ? 4 : 1);
       }
     }
   }
@@ -5241,6 +5209,7 @@ extern "C" int gls_ilu_set_options(gls_ctx *c, int ordering, int64_t block_dofs)
 extern "C" int gls_ilu_detach(gls_ctx *c) {
   GLS_TRY(check_ctx(c));
   c->ilu.on = false;
+  c->ilu.probe_only = false;
   c->ilu.release();
   return GLS_OK;
 }

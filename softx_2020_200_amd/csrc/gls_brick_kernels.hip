@@ -1031,15 +1031,8 @@ hipError_t launch_brick_probe_t(const OpParams &P0, const Tables1D &T, int64_t j
 //       64 lanes) for every mode;
 //   Q2: the workgroup-per-brick kernel here (the wave kernel at 3 waves / SIMD, and a variant
 //       interleaving two fields per sweep stage, both measured slower: LDS-issue bound).
-// Timing-only overrides: GLS_BRICK_V1=1 (this file's kernel everywhere), GLS_BRICK_WAVE=1 (the
-// wave kernel everywhere). The Q2 linearization layout is the same in all three kernels.
-static int brick_impl(int k) {  // 0 this file, 1 wave kernel
-  static const int v1 = std::getenv("GLS_BRICK_V1") != nullptr ? 1 : 0;
-  static const int wv = std::getenv("GLS_BRICK_WAVE") != nullptr ? 1 : 0;
-  if (v1) return 0;
-  if (wv) return 1;
-  return k == 1 ? 1 : 0;
-}
+// The Q2 linearization layout is the same in all three kernels.
+static int brick_impl(int k) { return k == 1 ? 1 : 0; }  // 0 this file, 1 wave kernel
 
 hipError_t launch_brick_probe(int k, const OpParams &P, const Tables1D &T, int64_t j0, int nprobe, hipStream_t s) {
   if (brick_impl(k) == 1) return launch_brick_wave_probe(k, P, T, j0, nprobe, s);

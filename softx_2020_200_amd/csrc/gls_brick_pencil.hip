@@ -755,450 +755,9 @@ __global__ void __launch_bounds__(256, (std::is_same<Real, float>::value ? GLS_P
   else reduce_scatter(P.y, P.slab, true);
 }
 
-// ==============================================================================================
-// The FP32 smoother J.v in PACKED FP32 ("pair" pencil). The FP32 pencil kernel above is VALU-issue
-// bound (~0.94 of its SIMDs' VALU slots): FP32 and FP64 VALU instructions issue at the same rate on
-// gfx950 unless they are packed (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two FP32 lanes per
-// instruction). Here every lane carries TWO cells -- the z-neighbours j and j + 4 of a brick, same
-// (qx, qy) column -- as one float2, so every sweep, the pointwise algebra and the test contractions
-// map one-to-one onto packed instructions (the 1D coefficients are scalar: op_sel broadcast, no
-// moves). A wave holds 6 cell pairs (54 lanes) = 12 cells, a workgroup 2 waves = 3 bricks = 24 cells;
-// the stage arrays hold 8-byte pairs in the FP64 J.v's bank-tuned layout (same element size, same lane
-// map), the brick arrays and the per-cell node values stay FP32 scalars, and the brick reduction /
-// slab / fused Jacobi options are the FP32 pencil kernel's (same slots, same per-node summation order:
-// bitwise the FP32 pencil kernel's sums of the same cell values).
-// ==============================================================================================
-typedef float pf2 __attribute__((ext_vector_type(2)));
-
-#ifndef GLS_PAIR_PIPE
-#define GLS_PAIR_PIPE 1  // linearization batch of component cc + 1 requested while cc is swept
-#endif
-
-struct PairCfg {
-  static constexpr int BN = 5, BN3 = 125, BN3P = 128, NBND = 98;
-  static constexpr int PPW = 6, WAVES = 2, THREADS = 128, CPG = 24, BPG = 3, NF = 4;
-  static constexpr int SY = 5, SZ = 25, FB = 129;  // brick arrays (FP32): node (X, Y, Z) at X + SY Y + SZ Z
-  // stage arrays in pf2 (8-byte) units: the FP64 J.v's layout (PencilCfg<double, true>)
-  static constexpr int XS = 12, XA = 3 * XS, ZS = 12, ZAZ = 3, ZA = 3 * ZS, WB = 3 * ZA, WAZ = 9, WA = 28;
-  static constexpr int CS = 190;
-  static constexpr int OF = 27, OC = 123;  // per-cell node values (FP32): [cell * OC + f * OF + 9 az + 3 ay + ax]
-  static_assert(CS >= 3 * XA && CS >= WB + 2 * WA && OC >= 4 * OF, "pair pencil LDS layout");
-};
-size_t pencil_pair_lds_bytes() {
-  using C = PairCfg;
-  return sizeof(float) * (size_t)C::BPG * C::NF * C::FB + sizeof(pf2) * (size_t)C::WAVES * C::PPW * C::CS +
-         sizeof(float) * (size_t)C::CPG * C::OC + sizeof(int) * (size_t)C::BPG * C::BN3P;
-}
-
-template <bool GEN, bool FOREST>
-__global__ void __launch_bounds__(128, 2) gls_pencil_pair_kernel(const OpParams P, const PencilTab<float> T) {
-  using C = PairCfg;
-  constexpr int BN = C::BN, BN3 = C::BN3, BN3P = C::BN3P, NF = C::NF, FB = C::FB, SY = C::SY, SZ = C::SZ;
-  constexpr int CS = C::CS;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  float *const sB = reinterpret_cast<float *>(smem_raw);                   // [3 bricks][4 fields][FB]
-  pf2 *const sS = reinterpret_cast<pf2 *>(sB + C::BPG * NF * FB);           // [2 waves][6 pairs][CS]
-  float *const sO = reinterpret_cast<float *>(sS + C::WAVES * C::PPW * CS);  // [24 cells][OC]
-  int *const sNode = reinterpret_cast<int *>(sO + C::CPG * C::OC);          // [3][BN3P]
-  __shared__ float sRow[3 * 16];
-  const pf2 Z0 = {0.f, 0.f};
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n_bricks = P.n_cells / 8;
-  const int32_t *const subset = FOREST ? P.subset : nullptr;  // as the FP32 pencil kernel
-  const int n_items = subset ? P.subset_n : n_bricks;
-  const int n_groups = (n_items + 2) / 3;
-  const int g = xcd_swizzle((int)blockIdx.x, n_groups);
-  const int nbg = min(3, n_items - 3 * g);
-  auto brick_of = [&](int bi) { return subset ? subset[3 * g + bi] : 3 * g + bi; };
-  auto cell0 = [&](int b) -> int64_t { return P.brick_cell0 ? (int64_t)P.brick_cell0[b] : (int64_t)b * 8; };
-  const int64_t voff = (int64_t)3 * P.n_vnodes;
-
-  if (tid < 48) {
-    const int mat = tid >> 4, r = (tid >> 2) & 3, cc = tid & 3;
-    float v = 0;
-    if (r < 3 && cc < 3) v = mat == 0 ? T.V[r][cc] : mat == 1 ? T.D[r][cc] : T.S[r][cc];
-    sRow[tid] = v;
-  }
-  // ---------------- per lane: cell pair pp (cells j, j + 4 of brick bi), (a, b) in the 3 x 3 pencil grid
-  const bool act = lane < 9 * C::PPW;
-  const int cp = act ? lane / 9 : 0, rr = act ? lane % 9 : 0, pa = rr % 3, pb = rr / 3;
-  const int pp = wave * C::PPW + cp, bi = pp >> 2, j = pp & 3;
-  const bool valid = act && bi < nbg;
-  const int brick = brick_of(valid ? bi : 0);
-  const int cx = j & 1, cy = j >> 1;
-  const int jj = valid ? j : 0;
-  const int64_t gc0 = cell0(brick) + jj, gc1 = gc0 + 4;
-  const pf2 hx = {(float)P.geo[gc0 * 4 + 0], (float)P.geo[gc1 * 4 + 0]};
-  const pf2 hy = {(float)P.geo[gc0 * 4 + 1], (float)P.geo[gc1 * 4 + 1]};
-  const pf2 hz = {(float)P.geo[gc0 * 4 + 2], (float)P.geo[gc1 * 4 + 2]};
-  const pf2 one = {1.f, 1.f};
-  const pf2 ihx = one / hx, ihy = one / hy, ihz = one / hz;
-  const pf2 wxx = ihx * ihx, wyy = ihy * ihy, wzz = ihz * ihz;
-  pf2 *const cellS = sS + (wave * C::PPW + cp) * CS;
-  const float *const qrow0 = P.qdf + qdp_base(brick, jj, pa + 3 * pb);
-  const float *const qrow1 = P.qdf + qdp_base(brick, jj + 4, pa + 3 * pb);
-
-  // ---------------- gather v (masked: P v) into the brick arrays, and the node ids
-  for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
-    const int bi_ = t / BN3, n = t % BN3;
-    if (bi_ >= nbg) break;
-    const int bk = brick_of(bi_);
-    const int X = n % BN, Y = (n / BN) % BN, Z = n / (BN * BN);
-    const int ccx = min(X / 2, 1), ccy = min(Y / 2, 1), ccz = min(Z / 2, 1);
-    const int a = (X - 2 * ccx) + 3 * ((Y - 2 * ccy) + 3 * (Z - 2 * ccz));
-    const int node = P.cell_vnodes[(cell0(bk) + ccx + 2 * ccy + 4 * ccz) * 27 + a];
-    const int64_t i3 = (int64_t)node * 3;
-    float *b = sB + bi_ * NF * FB + X + SY * Y + SZ * Z;
-    double v0, v1, v2, vp;
-    if (P.jx0) {  // the first Jacobi sweep from 0: v = 0 + omega b / d (mg_jacobi_update's arithmetic)
-      v0 = 0.0 + P.jomega * P.rb[i3] / P.jd[i3];
-      v1 = 0.0 + P.jomega * P.rb[i3 + 1] / P.jd[i3 + 1];
-      v2 = 0.0 + P.jomega * P.rb[i3 + 2] / P.jd[i3 + 2];
-      vp = 0.0 + P.jomega * P.rb[voff + node] / P.jd[voff + node];
-    } else {
-      v0 = P.v[i3], v1 = P.v[i3 + 1], v2 = P.v[i3 + 2], vp = P.v[voff + node];
-    }
-    const unsigned m = P.vmask ? P.vmask[node] : 0u;
-    b[0] = (m & 1u) ? 0.f : (float)v0;
-    b[FB] = (m & 2u) ? 0.f : (float)v1;
-    b[2 * FB] = (m & 4u) ? 0.f : (float)v2;
-    b[3 * FB] = (float)vp;
-    sNode[bi_ * BN3P + n] = node;
-  }
-  __syncthreads();
-
-  // ---------------- forward sweeps (the FP32 pencil kernel's, two cells per lane)
-  auto xsweep = [&](int f, int kind) {
-    const bool grad = kind >= 1, vel = kind == 2;
-    const float *F = sB + (bi < 3 ? bi : 0) * NF * FB + f * FB + 2 * cx + SY * (2 * cy + pa) + SZ * pb;
-    const pf2 f0 = {F[0], F[2 * SZ]}, f1 = {F[1], F[2 * SZ + 1]}, f2 = {F[2], F[2 * SZ + 2]};
-#pragma unroll
-    for (int qx = 0; qx < 3; ++qx) {
-      const pf2 xb = T.V[qx][0] * f0 + T.V[qx][1] * f1 + T.V[qx][2] * f2;
-      const int o = qx * C::XS + pa + 3 * pb;
-      if (act) {
-        cellS[o] = xb;
-        if (grad) cellS[C::XA + o] = T.D[qx][0] * f0 + T.D[qx][1] * f1 + T.D[qx][2] * f2;
-        if (vel) cellS[2 * C::XA + o] = T.S[qx][0] * f0 + T.S[qx][1] * f1 + T.S[qx][2] * f2;
-      }
-    }
-  };
-  auto ysweep = [&](int kind, pf2 (&BB)[3], pf2 (&BD)[3], pf2 (&DB)[3], pf2 (&LL)[3]) {
-    const bool grad = kind >= 1, vel = kind == 2;
-    const float *rowp = sRow + pb * 4;
-    const float v0 = rowp[0], v1 = rowp[1], v2 = rowp[2];
-    const float d0 = rowp[16], d1 = rowp[17], d2 = rowp[18];
-    const float s0 = rowp[32], s1 = rowp[33], s2 = rowp[34];
-    pf2 xb[9], xd[9], xs[9];
-    const pf2 *sl = cellS + pa * C::XS;
-#pragma unroll
-    for (int e = 0; e < 9; ++e) {
-      xb[e] = sl[e];
-      if (grad) xd[e] = sl[C::XA + e];
-      if (vel) xs[e] = sl[2 * C::XA + e];
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const pf2 b0 = xb[3 * k], b1 = xb[3 * k + 1], b2 = xb[3 * k + 2];
-      BB[k] = v0 * b0 + v1 * b1 + v2 * b2;
-      if (grad) {
-        BD[k] = d0 * b0 + d1 * b1 + d2 * b2;
-        DB[k] = v0 * xd[3 * k] + v1 * xd[3 * k + 1] + v2 * xd[3 * k + 2];
-      }
-      if (vel)
-        LL[k] = wyy * (s0 * b0 + s1 * b1 + s2 * b2) + wxx * (v0 * xs[3 * k] + v1 * xs[3 * k + 1] + v2 * xs[3 * k + 2]);
-    }
-  };
-  auto forward = [&](int f, int kind, pf2 (&BB)[3], pf2 (&BD)[3], pf2 (&DB)[3], pf2 (&LL)[3]) {
-    xsweep(f, kind);
-    wave_sync();
-    ysweep(kind, BB, BD, DB, LL);
-    wave_sync();
-  };
-  auto zval = [&](const pf2 (&y)[3], int qz) { return T.V[qz][0] * y[0] + T.V[qz][1] * y[1] + T.V[qz][2] * y[2]; };
-  auto zder = [&](const pf2 (&y)[3], int qz) { return T.D[qz][0] * y[0] + T.D[qz][1] * y[1] + T.D[qz][2] * y[2]; };
-  auto zsec = [&](const pf2 (&y)[3], int qz) { return T.S[qz][0] * y[0] + T.S[qz][1] * y[1] + T.S[qz][2] * y[2]; };
-
-  const float nu = (float)P.nu, aj = (float)P.alpha_jac;
-  auto wsel = [&](int i) { return i == 0 ? T.w[0] : i == 1 ? T.w[1] : T.w[2]; };
-  const pf2 wxy = (wsel(pa) * wsel(pb)) * hx * hy * hz;
-  const pf2 ihv[3] = {ihx, ihy, ihz};
-  float om[3] = {0, 0, 0};
-  if (GEN && P.srf) { om[0] = (float)P.omega[0]; om[1] = (float)P.omega[1]; om[2] = (float)P.omega[2]; }
-
-  // ---------------- backward stages (the FP32 pencil kernel's), the two cells' node values split at the end
-  float *const outc0 = sO + (bi * 8 + j) * C::OC, *const outc1 = outc0 + 4 * C::OC;
-  auto bwd_z = [&](const pf2 (&Z)[3][3]) {
-    if (act) {
-#pragma unroll
-      for (int m = 0; m < 3; ++m)
-#pragma unroll
-        for (int az = 0; az < 3; ++az) cellS[m * C::ZA + pa * C::ZS + C::ZAZ * az + pb] = Z[m][az];
-    }
-  };
-  auto bwd_w = [&]() {
-    pf2 z[3][3];
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-#pragma unroll
-      for (int qy = 0; qy < 3; ++qy) z[m][qy] = cellS[m * C::ZA + pa * C::ZS + C::ZAZ * pb + qy];
-    pf2 *Ws = cellS + C::WB;
-#pragma unroll
-    for (int ay = 0; ay < 3; ++ay) {
-      const pf2 w0 = T.V[0][ay] * z[0][0] + T.V[1][ay] * z[0][1] + T.V[2][ay] * z[0][2] +
-                     (T.D[0][ay] * z[2][0] + T.D[1][ay] * z[2][1] + T.D[2][ay] * z[2][2]);
-      const pf2 w1 = T.V[0][ay] * z[1][0] + T.V[1][ay] * z[1][1] + T.V[2][ay] * z[1][2];
-      if (act) {
-        Ws[C::WAZ * pb + 3 * ay + pa] = w0;
-        Ws[C::WA + C::WAZ * pb + 3 * ay + pa] = w1;
-      }
-    }
-  };
-  auto bwd_out = [&](int f) {
-    const pf2 *Ws = cellS + C::WB;
-    pf2 w0[3], w1[3];
-#pragma unroll
-    for (int qx = 0; qx < 3; ++qx) {
-      w0[qx] = Ws[C::WAZ * pb + 3 * pa + qx];
-      w1[qx] = Ws[C::WA + C::WAZ * pb + 3 * pa + qx];
-    }
-    if (valid) {
-#pragma unroll
-      for (int ax = 0; ax < 3; ++ax) {
-        const pf2 r = T.V[0][ax] * w0[0] + T.V[1][ax] * w0[1] + T.V[2][ax] * w0[2] +
-                      (T.D[0][ax] * w1[0] + T.D[1][ax] * w1[1] + T.D[2][ax] * w1[2]);
-        outc0[f * C::OF + 9 * pb + 3 * pa + ax] = r.x;
-        outc1[f * C::OF + 9 * pb + 3 * pa + ax] = r.y;
-      }
-    }
-  };
-  auto backward = [&](int f, const pf2 (&Z)[3][3]) {
-    bwd_z(Z);
-    wave_sync();
-    bwd_w();
-    wave_sync();
-    bwd_out(f);
-    wave_sync();
-  };
-
-  // ---------------- J.v from the FP32 linearization (the FP32 pencil kernel's MODE_JVQ, packed)
-  auto ld = [&](int qz, int v) {
-    const int o = (qz * kQData + v) * kQdpRow;
-    return pf2{qrow0[o], qrow1[o]};
-  };
-  pf2 uq[3][3], tauq[3], lnx[3][4];
-#pragma unroll
-  for (int qz = 0; qz < 3; ++qz) {
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) uq[cc][qz] = ld(qz, cc);
-    tauq[qz] = ld(qz, 12);
-  }
-  auto ld_comp = [&](int cc) {
-#pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e) lnx[qz][e] = ld(qz, 3 + 3 * cc + e);
-      lnx[qz][3] = ld(qz, 13 + cc);
-    }
-  };
-  constexpr bool PIPE = GLS_PAIR_PIPE != 0;
-  if (PIPE) ld_comp(0);
-  pf2 vq[3][3], vpq[3], gvp[3][3];
-  {
-    pf2 dz[3];
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) {
-      pf2 bb[3];
-      forward(cc, 0, bb, dz, dz, dz);
-#pragma unroll
-      for (int qz = 0; qz < 3; ++qz) vq[cc][qz] = zval(bb, qz);
-    }
-    pf2 pb_[3], pbd[3], pdb[3];
-    forward(3, 1, pb_, pbd, pdb, dz);
-#pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
-      vpq[qz] = zval(pb_, qz);
-      gvp[0][qz] = zval(pdb, qz) * ihx;
-      gvp[1][qz] = zval(pbd, qz) * ihy;
-      gvp[2][qz] = zder(pb_, qz) * ihz;
-    }
-  }
-  pf2 Sq[3][3], divv[3] = {Z0, Z0, Z0};
-#pragma unroll
-  for (int cc = 0; cc < 3; ++cc) {
-    pf2 gu[3][3], Rq[3];
-    pf2 Yc[4][3];
-    {
-      if (!PIPE) ld_comp(cc);
-#pragma unroll
-      for (int qz = 0; qz < 3; ++qz) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) gu[e][qz] = lnx[qz][e];
-        Rq[qz] = lnx[qz][3];
-      }
-      if (PIPE && cc < 2) ld_comp(cc + 1);
-      forward(cc, 2, Yc[0], Yc[1], Yc[2], Yc[3]);
-    }
-    pf2 Z[3][3] = {{Z0, Z0, Z0}, {Z0, Z0, Z0}, {Z0, Z0, Z0}};
-#pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
-      const pf2 gv0 = zval(Yc[2], qz) * ihx, gv1 = zval(Yc[1], qz) * ihy, gv2 = zder(Yc[0], qz) * ihz;
-      const pf2 lv = zval(Yc[3], qz) + wzz * zsec(Yc[0], qz);
-      const pf2 v0 = vq[0][qz], v1 = vq[1][qz], v2 = vq[2][qz];
-      const pf2 u0 = uq[0][qz], u1 = uq[1][qz], u2 = uq[2][qz];
-      const pf2 guv = gu[0][qz] * v0 + gu[1][qz] * v1 + gu[2][qz] * v2;
-      const pf2 gvu = gv0 * u0 + gv1 * u1 + gv2 * u2;
-      pf2 A = guv + gvu + aj * vq[cc][qz];
-      pf2 S = guv + gvu + gvp[cc][qz] - nu * lv + aj * vq[cc][qz];
-      if (GEN && P.srf) {
-        const pf2 cj = cc == 0 ? 2.f * (om[1] * v2 - om[2] * v1)
-                               : cc == 1 ? 2.f * (om[2] * v0 - om[0] * v2) : 2.f * (om[0] * v1 - om[1] * v0);
-        A += cj;
-        S += cj;
-      }
-      Sq[cc][qz] = S;
-      divv[qz] += cc == 0 ? gv0 : cc == 1 ? gv1 : gv2;
-      const pf2 JxW = wxy * T.w[qz], tau = tauq[qz];
-      const pf2 gv[3] = {gv0, gv1, gv2}, uu[3] = {u0, u1, u2}, vv[3] = {v0, v1, v2};
-      pf2 Te[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        Te[e] = JxW * (nu * gv[e] - (cc == e ? vpq[qz] : Z0) + tau * S * uu[e] + tau * Rq[qz] * vv[e]) * ihv[e];
-      const pf2 Tv = JxW * A;
-#pragma unroll
-      for (int az = 0; az < 3; ++az) {
-        Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Te[2];
-        Z[1][az] += T.V[qz][az] * Te[0];
-        Z[2][az] += T.V[qz][az] * Te[1];
-      }
-    }
-    backward(cc, Z);
-  }
-  {  // pressure test field: Tv = JxW div v, Te = JxW tau S_e / h_e
-    pf2 Z[3][3] = {{Z0, Z0, Z0}, {Z0, Z0, Z0}, {Z0, Z0, Z0}};
-#pragma unroll
-    for (int qz = 0; qz < 3; ++qz) {
-      const pf2 JxW = wxy * T.w[qz], jt = JxW * tauq[qz];
-      const pf2 Tv = JxW * divv[qz];
-      const pf2 Tx = jt * Sq[0][qz] * ihx, Ty = jt * Sq[1][qz] * ihy, Tz = jt * Sq[2][qz] * ihz;
-#pragma unroll
-      for (int az = 0; az < 3; ++az) {
-        Z[0][az] += T.V[qz][az] * Tv + T.D[qz][az] * Tz;
-        Z[1][az] += T.V[qz][az] * Tx;
-        Z[2][az] += T.V[qz][az] * Ty;
-      }
-    }
-    backward(3, Z);
-  }
-  __syncthreads();
-
-  if (FOREST && P.ev) {  // element vectors [cell][a * 3 + c | 81 + a] (gather_element_vectors sums them)
-    for (int t = tid; t < nbg * 8 * 27; t += C::THREADS) {
-      const int rb_ = t / 216, r = t - rb_ * 216, ci_ = r / 27, a = r - ci_ * 27;
-      const float *o = sO + (rb_ * 8 + ci_) * C::OC + a;
-      double *e = P.ev + (cell0(brick_of(rb_)) + ci_) * 108;
-      e[a * 3] = (double)o[0];
-      e[a * 3 + 1] = (double)o[C::OF];
-      e[a * 3 + 2] = (double)o[2 * C::OF];
-      e[81 + a] = (double)o[3 * C::OF];
-    }
-    return;
-  }
-  // ---------------- brick reduction (fixed cell order per node) + scatter, the FP32 pencil kernel's
-  for (int t = tid; t < C::BPG * BN3; t += C::THREADS) {
-    const int rb_ = t / BN3, n = t % BN3;
-    if (rb_ >= nbg) break;
-    const int bk = brick_of(rb_);
-    const int Xn = n % BN, Yn = (n / BN) % BN, Zn = n / (BN * BN);
-    float s[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int kz = 0; kz < 2; ++kz) {
-      const int az = Zn - 2 * kz;
-      if (az < 0 || az > 2) continue;
-#pragma unroll
-      for (int ky = 0; ky < 2; ++ky) {
-        const int ay = Yn - 2 * ky;
-        if (ay < 0 || ay > 2) continue;
-#pragma unroll
-        for (int kx = 0; kx < 2; ++kx) {
-          const int ax = Xn - 2 * kx;
-          if (ax < 0 || ax > 2) continue;
-          const float *o = sO + (rb_ * 8 + kx + 2 * ky + 4 * kz) * C::OC + ax + 3 * (ay + 3 * az);
-#pragma unroll
-          for (int f = 0; f < 4; ++f) s[f] += o[f * C::OF];
-        }
-      }
-    }
-    const int node = sNode[rb_ * BN3P + n];
-    const int64_t gi[4] = {(int64_t)node * 3, (int64_t)node * 3 + 1, (int64_t)node * 3 + 2, voff + node};
-    const bool interior = Xn > 0 && Xn < BN - 1 && Yn > 0 && Yn < BN - 1 && Zn > 0 && Zn < BN - 1;
-    if (interior) {
-      if (P.jx) {  // fused damped-Jacobi sweep (interior nodes: no other brick reads this x)
-        const unsigned m = P.vmask ? P.vmask[node] : 0u;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          const bool con = f < 3 && ((m >> f) & 1u);
-          const double x = P.jx[gi[f]], dd = P.jd[gi[f]];
-          P.jx[gi[f]] = x + P.jomega * (P.jb[gi[f]] - (con ? dd * x : (double)s[f])) / dd;
-        }
-      } else if (P.rb) {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) P.y[gi[f]] = P.rb[gi[f]] - (double)s[f];
-        if (P.jx0) {
-#pragma unroll
-          for (int f = 0; f < 4; ++f) P.jx0[gi[f]] = 0.0 + P.jomega * P.rb[gi[f]] / P.jd[gi[f]];
-        }
-      } else {
-#pragma unroll
-        for (int f = 0; f < 4; ++f) P.y[gi[f]] = s[f];
-      }
-    } else {  // this brick's partial sums of a brick-boundary node (summed per node by the slab sum)
-      const int64_t si = ((int64_t)bk * C::NBND + bnd_index<BN>(Xn, Yn, Zn)) * 4;
-      if (P.slabf) {
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<f4 *>(P.slabf + si) = f4{s[0], s[1], s[2], s[3]};
-      } else {
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<d2 *>(P.slab + si) = d2{(double)s[0], (double)s[1]};
-        *reinterpret_cast<d2 *>(P.slab + si + 2) = d2{(double)s[2], (double)s[3]};
-      }
-    }
-  }
-}
-
-// the packed kernel for the FP32 smoother J.v: opt-in (GLS_PENCIL_PAIR=1). Measured SLOWER than the scalar
-// FP32 pencil kernel at Q2 128^3 (1.56 vs 1.37 ms per launch, 99.6 vs 94.3 ms per Newton step on one box,
-// profiles/r05_ab_pair_kernel.txt): 240 VGPRs and 38 KB of LDS per 2-wave workgroup hold it at 2 waves per
-// SIMD, where it is latency-bound (VALU ~45 % busy) like the FP64 J.v, instead of VALU-bound at 4
-bool pencil_pair_enabled() {
-  const char *e = std::getenv("GLS_PENCIL_PAIR");
-  return e && std::atoi(e) != 0;
-}
-template <bool FOREST>
-hipError_t launch_pencil_pair(const OpParams &P, const Tables1D &T, hipStream_t s) {
-  const int n_items = (FOREST && P.subset) ? P.subset_n : P.n_cells / 8;
-  if (n_items <= 0) return hipSuccess;
-  if (!P.qdf) return hipErrorInvalidValue;
-  const int n_groups = (n_items + 2) / 3;
-  PencilTab<float> tab;
-  for (int q = 0; q < 3; ++q) {
-    tab.w[q] = (float)T.w[q];
-    for (int i = 0; i < 3; ++i) {
-      tab.V[q][i] = (float)T.V[q][i];
-      tab.D[q][i] = (float)T.D[q][i];
-      tab.S[q][i] = (float)T.S[q][i];
-    }
-    tab.xi[q] = (float)T.xi[q];
-  }
-  if (P.srf)
-    hipLaunchKernelGGL((gls_pencil_pair_kernel<true, FOREST>), dim3((unsigned)n_groups), dim3(PairCfg::THREADS),
-                       pencil_pair_lds_bytes(), s, P, tab);
-  else
-    hipLaunchKernelGGL((gls_pencil_pair_kernel<false, FOREST>), dim3((unsigned)n_groups), dim3(PairCfg::THREADS),
-                       pencil_pair_lds_bytes(), s, P, tab);
-  return hipGetLastError();
-}
+// (A packed-FP32 variant of the FP32 smoother J.v -- two cells per lane as float2 -- was measured slower than
+// the scalar FP32 kernel above, 1.56 vs 1.37 ms per launch at Q2 128^3, profiles/r05_ab_pair_kernel.txt, and was
+// removed in round 6.)
 
 // Selection: on by default for the Q2 brick J.v with a slab (the launch contract of the
 // lane-per-point kernel); GLS_PENCIL=0 keeps the lane-per-point kernel (A/B, fallback)
@@ -1245,7 +804,6 @@ hipError_t launch_pencil_t(const OpParams &P, const Tables1D &T, hipStream_t s) 
 hipError_t launch_pencil_jv(const OpParams &P, const Tables1D &T, hipStream_t s, bool f32) {
   if (P.n_probe > 0 || P.bricks || !(f32 ? (P.slabf != nullptr || P.slab != nullptr) : P.slab != nullptr))
     return hipErrorNotSupported;
-  if (f32 && pencil_pair_enabled() && !P.oseen) return launch_pencil_pair<false>(P, T, s);
   return f32 ? launch_pencil_t<float, MODE_JVQ>(P, T, s) : launch_pencil_t<double, MODE_JVQ>(P, T, s);
 }
 hipError_t launch_pencil_residual(const OpParams &P, const Tables1D &T, hipStream_t s) {
@@ -1263,7 +821,6 @@ hipError_t launch_pencil_ev(int mode, const OpParams &P, const Tables1D &T, hipS
   if ((!P.ev && mode != MODE_LIN) || P.y || !P.brick_cell0 || !P.subset || P.subset_n <= 0 || !P.qd || P.slab ||
       P.bricks || P.n_probe > 0 || P.rb || P.jx || P.jx0 || (f32 && (mode != MODE_JVQ || !P.qdf)))
     return hipErrorNotSupported;
-  if (mode == MODE_JVQ && f32 && pencil_pair_enabled()) return launch_pencil_pair<true>(P, T, s);  // the smoother's operator
   if (mode == MODE_JVQ && f32) return launch_pencil_t<float, MODE_JVQ, true>(P, T, s);
   if (mode == MODE_JVQ) return launch_pencil_t<double, MODE_JVQ>(P, T, s);
   if (mode == MODE_LIN) return launch_pencil_t<double, MODE_LIN>(P, T, s);

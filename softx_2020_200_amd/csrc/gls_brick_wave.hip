@@ -658,17 +658,9 @@ hipError_t launch_wave_wpb(const OpParams &P, const Tables1D &T, hipStream_t s) 
 
 // waves per brick: Q1 (one round of 8 cells) -> 1; Q2 (four rounds of 2 cells) -> 4, the
 // workgroup shares the brick (LDS per wave would otherwise cap occupancy at 3 waves / SIMD).
-// GLS_WPB=1|4 overrides for A/B timing.
 template <int K, int MODE, typename Real>
 hipError_t launch_wave_t(const OpParams &P, const Tables1D &T, hipStream_t s) {
-  static const int wpb = [] {
-    const char *e = std::getenv("GLS_WPB");
-    const int w = e ? std::atoi(e) : (K == 2 ? 4 : 1);
-    return (w == 4 && WaveCfg<K>::ROUNDS % 4 == 0) ? 4 : 1;
-  }();
-  if (wpb == 4) {
-    if constexpr (WaveCfg<K>::ROUNDS % 4 == 0) return launch_wave_wpb<K, MODE, 4, Real>(P, T, s);
-  }
+  if constexpr (K == 2 && WaveCfg<K>::ROUNDS % 4 == 0) return launch_wave_wpb<K, MODE, 4, Real>(P, T, s);
   return launch_wave_wpb<K, MODE, 1, Real>(P, T, s);
 }
 

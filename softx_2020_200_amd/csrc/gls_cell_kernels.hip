@@ -678,6 +678,10 @@ hipError_t launch_cell_t(int mode, const OpParams &P, const Tables1D &T, hipStre
 // Supported element families (dim, k, kp) with the reference quadrature QGauss(k+1).
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s) {
+  if (mode == MODE_JV && !(P.cell_list && P.cell_list_n <= 0)) {  // sum-factorized J.v where it applies
+    const hipError_t e = launch_cell_sf_jv(dim, k, kp, nq1d, P, T, s);
+    if (e != hipErrorNotSupported) return e;
+  }
 #define GLS_CASE(D, KK, KKP)                                                         \
   if (dim == D && k == KK && kp == KKP && nq1d == KK + 1) return launch_cell_t<D, KK, KKP, KK + 1>(mode, P, T, s);
   GLS_CASE(2, 1, 1)

@@ -457,7 +457,8 @@ int gls_dpart_create(int dim, int k, int kp, int64_t n_cells, const int32_t *cel
   // DoF order: velocity before pressure, then key, then component (= DoF key order within each kind)
   auto is_p = [D1, dim](int64_t g) { return g % D1 == dim; };
   auto dof_less = [&](int64_t a, int64_t b) { return is_p(a) != is_p(b) ? !is_p(a) : a < b; };
-  // owner of a DoF (-1: no provided cell touches its node -- not this rank's, whoever owns it)
+  // owner of a DoF (-1: no provided cell touches its node -- not this rank's, whoever owns it). Exact because the
+  // caller provides EVERY cell touching each node this rank needs, line masters included (the header's contract)
   auto dof_owner = [&](int64_t g) -> int32_t {
     const std::unordered_map<int64_t, int32_t> &m = (is_p(g) && p->sep) ? pown : vown;
     auto it = m.find(g / D1);

@@ -10,6 +10,10 @@ hipError_t gather_element_vectors(double *y, const double *ev, const int64_t *vo
 hipError_t launch_cell_kernel(int dim, int k, int kp, int nq1d, int mode, const OpParams &P, const Tables1D &T,
                               hipStream_t s);
 bool cell_kernel_supported(int dim, int k, int kp, int nq1d);
+// sum-factorized J.v of 3D Q2-Q1 / Q2-Q2 cells from the linearization cache (gls_cell_sf.hip); hipErrorNotSupported
+// when the launch is not its case (launch_cell_kernel then runs the dense kernel). GLS_CELL_SF=0: dense (A/B, tests)
+hipError_t launch_cell_sf_jv(int dim, int k, int kp, int nq1d, const OpParams &P, const Tables1D &T, hipStream_t s);
+bool cell_sf_enabled();
 int cell_kernel_cells_per_block(int dim, int k, int nq1d, bool probe = false);  // cells per workgroup
 // sum-factorized 3D Qk-Qk kernels on 2x2x2 Morton bricks (residual, J.v); k in {1,2}
 hipError_t launch_brick_kernel(int k, int mode, const OpParams &P, const Tables1D &T, hipStream_t s);

@@ -208,11 +208,9 @@ hipError_t launch_transfer_xy(const double *in, double *out, int i0, int i1, int
                               const int32_t *const taps[3], const double *const w[3], const int32_t *const cnt[3],
                               hipStream_t s, int add = 0) {
   const int nb = ((o0 + OX - 1) / OX) * ((o1 + OY - 1) / OY);
-  // planes per block (prefetch pipeline depth); GLS_XFER_ZB overrides (A/B of blocks in flight)
-  static const int zb_env = std::getenv("GLS_XFER_ZB") ? std::atoi(std::getenv("GLS_XFER_ZB")) : 0;
-  // default 2 planes (4x the blocks in flight of the former 8: 93.4-93.6 vs 93.8-94.1 ms per Newton step
+  // planes per block (prefetch pipeline depth): 2 planes (4x the blocks in flight of the former 8: 93.4-93.6 vs 93.8-94.1 ms per Newton step
   // at configs[2], profiles/r04_ab_transfer_planes.txt)
-  const int zb = zb_env > 0 ? zb_env : (nz >= 16 ? 2 : 1);
+  const int zb = nz >= 16 ? 2 : 1;
   hipLaunchKernelGGL((k_transfer_xy<OX, OY, IXM, IYM>), dim3(nb, (nz + zb - 1) / zb), dim3(256), 0, s, in, out, i0, i1,
                      o0, o1, nz, zb, taps[0], w[0], cnt[0], taps[1], w[1], cnt[1], add);
   return hipGetLastError();

@@ -2177,8 +2177,118 @@ int gls_umesh_coarsen_to(const gls_umesh *g, int level, gls_umesh **out) {
 // SolutionTransfer interpolates (gls_fe_space_transfer). Rows of fine hanging DoFs are empty; columns are
 // coarse masters. inject[j] = the fine DoF at coarse DoF j's node (descending the hierarchy to the fine
 // cell holding it). off == NULL: nnz only.
+// p-level pair (same active cells, the coarse space of lower degree, e.g. Q2-Q1 -> Q1-Q1 on the base mesh of a
+// hierarchy): fine DoF i = the coarse degree's interpolant at the fine node's reference position in the same cell
+// (FE_Q's embedding of the lower degree), hanging coarse nodes replaced by their lines; inject[j] = the fine DoF at
+// coarse DoF j's node (the fine degree a multiple of the coarse one).
+static int p_level_transfer(const gls_fe_space *fi, const gls_fe_space *co, int64_t *nnz, int64_t *off, int32_t *col,
+                            double *w, int64_t *inject) {
+  const int dim = fi->dim;
+  const int64_t nvf = fi->n_vnodes, nvc = co->n_vnodes;
+  const bool fsep = fi->kp != fi->k, csep = co->kp != co->k;
+  std::vector<int64_t> inj((size_t)(dim * nvc + co->n_pnodes), -1);
+  std::vector<int32_t> cols;
+  std::vector<double> ws;
+  std::vector<int64_t> roff{0};
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool vel = pass == 0;
+    const int kf = vel ? fi->k : fi->kp, kc = vel ? co->k : co->kp;
+    if (kf % kc) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: degree %d is not a multiple of %d", kf, kc);
+    const int kf1 = kf + 1, kc1 = kc + 1;
+    const int nnf_c = dim == 2 ? kf1 * kf1 : kf1 * kf1 * kf1, nnc_c = dim == 2 ? kc1 * kc1 : kc1 * kc1 * kc1;
+    // node arrays of the field: separate pressure nodes when the space has them, else the velocity nodes
+    const int32_t *fcn = (vel || !fsep) ? fi->cell_vnodes : fi->cell_pnodes;
+    const int32_t *ccn = (vel || !csep) ? co->cell_vnodes : co->cell_pnodes;
+    const int fstride = (vel || !fsep) ? (dim == 2 ? (fi->k + 1) * (fi->k + 1) : (fi->k + 1) * (fi->k + 1) * (fi->k + 1)) : nnf_c;
+    const int cstride = (vel || !csep) ? (dim == 2 ? (co->k + 1) * (co->k + 1) : (co->k + 1) * (co->k + 1) * (co->k + 1)) : nnc_c;
+    const int64_t nnf = vel ? nvf : (fsep ? fi->n_pnodes : nvf);
+    const int64_t nh_c = vel ? co->n_vhang : co->n_phang, nh_f = vel ? fi->n_vhang : fi->n_phang;
+    const int64_t *hc_node = vel ? co->vhang_node : co->phang_node, *hc_off = vel ? co->vhang_off : co->phang_off;
+    const int64_t *hc_mas = vel ? co->vhang_master : co->phang_master;
+    const double *hc_w = vel ? co->vhang_w : co->phang_w;
+    const int64_t *hf_node = vel ? fi->vhang_node : fi->phang_node;
+    std::unordered_map<int64_t, int64_t> cline;
+    for (int64_t i = 0; i < nh_c; ++i) cline[hc_node[i]] = i;
+    std::vector<char> fh((size_t)nnf, 0), seen((size_t)nnf, 0);
+    for (int64_t i = 0; i < nh_f; ++i) fh[(size_t)hf_node[i]] = 1;
+    std::vector<std::vector<std::pair<int32_t, double>>> rows((size_t)nnf);
+    // the fine field's local nodes: the degree-kf lattice of a node array with degree (vel || !fsep ? k : kp)
+    const int kfa = (vel || !fsep) ? fi->k : fi->kp, kca = (vel || !csep) ? co->k : co->kp;
+    if (kfa != kf || kca != kc) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: equal-order pressure degree");
+    for (int64_t f = 0; f < fi->n_cells; ++f) {
+      for (int a = 0; a < nnf_c; ++a) {
+        const int64_t node = fcn[f * fstride + a];
+        if (seen[(size_t)node] || fh[(size_t)node]) continue;
+        seen[(size_t)node] = 1;
+        const int ia[3] = {a % kf1, (a / kf1) % kf1, dim == 3 ? a / (kf1 * kf1) : 0};
+        auto &acc = rows[(size_t)node];
+        for (int b = 0; b < nnc_c; ++b) {
+          const int ib[3] = {b % kc1, (b / kc1) % kc1, dim == 3 ? b / (kc1 * kc1) : 0};
+          double wb = 1.0;
+          for (int d = 0; d < dim; ++d) wb *= lag1(kc, ib[d], (double)ia[d] / kf);
+          if (std::fabs(wb) < 1e-14) continue;
+          const int64_t cn = ccn[f * cstride + b];
+          auto it = cline.find(cn);
+          if (it == cline.end()) acc.push_back({(int32_t)cn, wb});
+          else
+            for (int64_t q = hc_off[it->second]; q < hc_off[it->second + 1]; ++q) acc.push_back({(int32_t)hc_mas[q], wb * hc_w[q]});
+        }
+        std::sort(acc.begin(), acc.end(), [](const std::pair<int32_t, double> &x, const std::pair<int32_t, double> &y) {
+          return x.first < y.first;
+        });
+        size_t m = 0;
+        for (size_t i = 0; i < acc.size(); ++i) {
+          if (m > 0 && acc[m - 1].first == acc[i].first) acc[m - 1].second += acc[i].second;
+          else acc[m++] = acc[i];
+        }
+        acc.resize(m);
+      }
+      for (int b = 0; b < nnc_c; ++b) {  // injection: coarse node b sits on fine local node (kf / kc) * ib
+        const int ib[3] = {b % kc1, (b / kc1) % kc1, dim == 3 ? b / (kc1 * kc1) : 0};
+        int la = 0, st = 1;
+        for (int d = 0; d < dim; ++d) {
+          la += ib[d] * (kf / kc) * st;
+          st *= kf1;
+        }
+        const int64_t cnode = ccn[f * cstride + b], fnode = fcn[f * fstride + la];
+        if (vel)
+          for (int e = 0; e < dim; ++e) inj[(size_t)(cnode * dim + e)] = fnode * dim + e;
+        else
+          inj[(size_t)(dim * nvc + cnode)] = dim * nvf + fnode;
+      }
+    }
+    for (int64_t v = 0; v < nnf; ++v) {
+      const int nrow = vel ? dim : 1;
+      for (int c = 0; c < nrow; ++c) {
+        for (auto &e : rows[(size_t)v]) {
+          cols.push_back(vel ? (int32_t)(e.first * dim + c) : (int32_t)(dim * nvc + e.first));
+          ws.push_back(e.second);
+        }
+        roff.push_back((int64_t)cols.size());
+      }
+    }
+  }
+  *nnz = (int64_t)cols.size();
+  if (off) {
+    if (!col || !w) return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: col / w missing");
+    std::memcpy(off, roff.data(), sizeof(int64_t) * roff.size());
+    std::memcpy(col, cols.data(), sizeof(int32_t) * cols.size());
+    std::memcpy(w, ws.data(), sizeof(double) * ws.size());
+  }
+  if (inject) std::memcpy(inject, inj.data(), sizeof(int64_t) * inj.size());
+  return GLS_OK;
+}
+
 int gls_fe_space_mg_transfer(const gls_fe_space *fi, const gls_fe_space *co, int64_t *nnz, int64_t *off, int32_t *col,
                              double *w, int64_t *inject) {
+  if (fi && co && nnz && fi->dim == co->dim && fi->impl_ && co->impl_ && (fi->k != co->k || fi->kp != co->kp)) {
+    const FESpaceImpl &N = *static_cast<const FESpaceImpl *>(fi->impl_);
+    const FESpaceImpl &O = *static_cast<const FESpaceImpl *>(co->impl_);
+    if (fi->n_cells != co->n_cells || N.hid != O.hid || co->k > fi->k || co->kp > fi->kp)
+      return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: a p-level pair needs the same cells and a "
+                                          "coarse space of lower degree");
+    return p_level_transfer(fi, co, nnz, off, col, w, inject);
+  }
   if (!fi || !co || !nnz || fi->dim != co->dim || fi->k != co->k || fi->kp != co->kp || !fi->impl_ || !co->impl_)
     return gls_io_set_error(GLS_EINVAL, "gls_fe_space_mg_transfer: spaces of different dimension / degree");
   const FESpaceImpl &N = *static_cast<const FESpaceImpl *>(fi->impl_);

@@ -166,8 +166,8 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot(double *__restrict__ w
 }
 
 // 16-byte variants of the Gram-Schmidt passes (one row pair per thread and trip, double2 loads / stores,
-// non-temporal basis loads; single-rank vectors: all rows owned). Default; GLS_VEC16=0 keeps the 8-byte
-// kernels. Orthogonalisation 11.9 -> 11.0 ms per Newton step at configs[2] (4.9 -> 5.3 TB/s,
+// non-temporal basis loads; single-rank vectors: all rows owned), used when the rows are 16-byte aligned
+// (else the 8-byte kernels). Orthogonalisation 11.9 -> 11.0 ms per Newton step at configs[2] (4.9 -> 5.3 TB/s,
 // profiles/r05_ab_vec16.txt)
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 // k_multiaxpy with 16-byte loads / stores (two rows per lane); ZERO: w starts at 0 and is not read
@@ -288,8 +288,7 @@ __global__ void __launch_bounds__(kBlock) k_multiaxpy_dot16(double *__restrict__
   }
 }
 bool vec16(const double *A, int64_t lda, const double *w, int64_t n, int64_t n1, int64_t n2) {
-  static const bool on = !(std::getenv("GLS_VEC16") && std::atoi(std::getenv("GLS_VEC16")) == 0);
-  return on && n2 == 0 && n1 == n && (lda % 2) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)w % 16) == 0;
+  return n2 == 0 && n1 == n && (lda % 2) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)w % 16) == 0;
 }
 
 // constraint lines: x[dof[i]] = sum_{j in [off[i], off[i+1])} w[j] * src[master[j]]
@@ -499,9 +498,9 @@ hipError_t vec_multiaxpy(double *w, const double *A, int64_t lda, int nk, const 
                          hipStream_t s, bool zero_init) {
   const int nb = grid_for(n);
   const bool v16 = vec16(A, lda, w, n, n, 0);
-  if (zero_init && !v16) {
+  if (zero_init && (!v16 || nk <= 0)) {  // nk == 0: w = 0 on both paths (no chunk launch would write it)
     const hipError_t e = vec_fill(w, n, 0.0, s);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || nk <= 0) return e;
   }
   for (int k0 = 0; k0 < nk; k0 += kDotChunk) {
     const int m = nk - k0 < kDotChunk ? nk - k0 : kDotChunk;

@@ -203,6 +203,12 @@ def rccl_comm(rank, world, group=None):
     return _RCCL[key]
 
 
+def drop_rccl():
+    """Forget the cached in-library communicators without calling into them (a pre-flight that failed on some
+    rank may have left one mid-collective; the fallback transport does not use it)."""
+    _RCCL.clear()
+
+
 def rccl_info(comm):
     """(rank, size) of an in-library RCCL communicator as RCCL itself reports them."""
     L = _bind(load())
@@ -406,8 +412,8 @@ def _dof_key(g, dim, nv):
 def local_part(space, rank, world, lines=None, dirichlet=None, vnode_mask=None, force_q=None):
     """What a p::d triangulation hands rank `rank` of the forest `space` (the partitioner's hand-off; the rank
     itself never sees the global arrays): its owned cells (the equal-count range of the space-filling cell
-    order) plus the ghost layer (every cell sharing a node with an owned cell or linked to one through a hanging
-    line), with owners, node keys (= global node ids), the lines on those cells in DoF keys, and the per-cell /
+    order) plus the ghost layer (every cell touching a node of an owned cell, a master node of a hanging line on
+    one, or the DoF node of a line one of whose masters it touches -- gls_dpart_create's contract), with owners, node keys (= global node ids), the lines on those cells in DoF keys, and the per-cell /
     per-node data the rank's context needs (cell_support and force_q of the owned cells, vnode_mask and Dirichlet
     rows on the provided nodes). Feeds dpartition / DistributedGeneralProblem(part=...)."""
     dim, k, kp = int(space["dim"]), int(space["k"]), int(space["kp"])

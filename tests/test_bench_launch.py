@@ -69,3 +69,49 @@ def test_world_size_must_match_gpus(world, gpus):
     assert out.returncode == 1, out.stderr
     assert "WORLD_SIZE=%s but --gpus %d" % (world, gpus) in out.stderr
     assert out.stdout.strip() == ""
+
+
+def _agree_worker(rank, world, port, failed, late, stuck, q):
+    import datetime
+
+    import torch.distributed as dist
+
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=5))
+    if stuck[rank]:  # never reaches the agreement (a rank left inside a data-path collective)
+        import time
+        time.sleep(12)
+        q.put((rank, "stuck"))
+        return
+    q.put((rank, bench.preflight_agreement(dist, ctl, world, failed[rank], late[rank])))
+
+
+@pytest.mark.parametrize("failed,late,stuck,want", [
+    ((False, False), (False, False), (False, False), {0: "ok", 1: "ok"}),
+    ((False, True), (False, False), (False, False), {0: "fallback", 1: "fallback"}),  # before the first collective
+    ((True, True), (True, True), (False, False), {0: "fallback", 1: "fallback"}),     # every rank failed: none stuck
+    ((False, True), (False, True), (False, False), {0: "abort", 1: "abort"}),         # rank 1 only, after it
+    ((False, True), (False, True), (True, False), {1: "abort"}),                      # rank 0 never arrives
+])
+def test_preflight_agreement_over_the_control_group(failed, late, stuck, want):
+    """the native transport falls back to torch.distributed only when no rank can be inside one of
+    its collectives; the ranks agree over a gloo group with a timeout, so a rank whose peer is stuck aborts
+    instead of hanging (gloo, world size 2, CPU)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_agree_worker, args=(r, 2, port, failed, late, stuck, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=90) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    for r, v in want.items():
+        assert got[r] == v, got

@@ -306,26 +306,3 @@ def test_fused_residual_linearization_diagonal(monkeypatch, n, scheme, srf):
             assert np.array_equal(a, b), (env, name, relerr(a, b))
     orc = Oracle(p)
     assert relerr(sep[0], orc.residual(u, u1, u2, u3)) < TOL
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("n,scheme,srf", [(2, "bdf2", False), (4, "bdf2", False), (6, "bdf1", False),
-                                          (4, "steady", True)])
-def test_packed_fp32_smoother_jv(monkeypatch, n, scheme, srf):
-    """The FP32 smoother J.v in packed FP32 (gls_pencil_pair_kernel: two cells per lane as float2, v_pk_*
-    instructions; opt-in with GLS_PENCIL_PAIR=1, measured slower) agrees with the scalar FP32 pencil kernel
-    (the default) to FP32 rounding and with the oracle's FP64 J.v to TOL_F32; n = 2, 4 leave the last brick
-    triple short, case 4 runs the SRF instantiation."""
-    p = _morton_problem(n, 2, scheme, 0.01, srf=srf)
-    u, u1, u2, u3, v = _states(p)
-    ctx = context_for(p)
-    V = cuda(v)
-    ctx.set_state(cuda(u), cuda(u1), cuda(u2), cuda(u3))
-    monkeypatch.setenv("GLS_PENCIL_PAIR", "1")
-    pair = ctx.jacobian_apply_f32(V).cpu().numpy()
-    monkeypatch.delenv("GLS_PENCIL_PAIR")
-    scalar = ctx.jacobian_apply_f32(V).cpu().numpy()
-    ref = Oracle(p).jacobian_apply(u, v, u1, u2, u3)
-    print("packed vs scalar FP32 %.2e, packed vs oracle %.2e" % (relerr(pair, scalar), relerr(pair, ref)))
-    assert relerr(pair, scalar) < 2e-6
-    assert relerr(pair, ref) < TOL_F32

@@ -71,3 +71,55 @@ def test_umesh_mg_transfer(name, dim, spec, flat, k, kp):
             return np.concatenate([vel, lin(sp["pnode_x"], a[dim])])
         uf, uc = field(sf), field(sc)
         assert np.abs((P @ uc)[rows] - uf[rows]).max() < 1e-10 * max(1.0, np.abs(uf).max())
+
+
+@pytest.mark.parametrize("name,dim,spec,flat", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("kf,kpf", [(2, 1), (2, 2)])
+def test_p_level_transfer(name, dim, spec, flat, kf, kpf):
+    """The p-level pair of gls_fe_space_mg_transfer (same cells, Qkf-Qkpf -> Q1-Q1, the coarse space below a
+    hierarchy's base mesh): a partition of unity on every fine master row, empty fine hanging rows, the
+    injection a right inverse of P (P maps each coarse nodal vector onto fine nodes that reproduce it at the
+    coarse nodes), the exact Q2 interpolant of a Q1 field: the values at the vertices and the averages at the
+    midpoints of every cell's reference lattice, on adapted meshes with hanging nodes in both spaces."""
+    m = adapted(name, dim, spec, kf)
+    hf = m.fe_space_handle(kf, kpf, qmapping_all=True)
+    hc = m.fe_space_handle(1, 1, qmapping_all=True)
+    sf, sc = hf.data, hc.data
+    off, col, w, inj = hf.mg_transfer_from(hc)
+    nf = dim * sf["n_vnodes"] + sf["n_pnodes"]
+    nc = dim * sc["n_vnodes"] + sc["n_pnodes"]
+    P = sps.csr_matrix((w, col, off), shape=(nf, nc))
+    hf_d, hc_d = hanging_dofs(sf), hanging_dofs(sc)
+    rows = np.diff(off)
+    for i in range(nf):
+        if i in hf_d:
+            assert rows[i] == 0
+        else:
+            assert abs(P[i].sum() - 1.0) < 1e-12, i
+    assert not set(col.tolist()) & hc_d
+    assert (inj >= 0).all()
+    rng = np.random.default_rng(SEED)
+    xc = rng.uniform(-1, 1, nc)
+    for nd, ln in sc["vhang"].items():  # a conforming coarse field
+        for c in range(dim):
+            xc[nd * dim + c] = sum(wt * xc[mm * dim + c] for mm, wt in ln)
+    for nd, ln in sc["phang"].items():
+        xc[dim * sc["n_vnodes"] + nd] = sum(wt * xc[dim * sc["n_vnodes"] + mm] for mm, wt in ln)
+    xf = P @ xc
+    free = np.array([j for j in range(nc) if j not in hc_d])
+    assert np.abs(xf[inj[free]] - xc[free]).max() < 1e-12
+    # cell by cell: the fine lattice values are the Q1 interpolant of the cell's vertex values
+    kf1 = kf + 1
+    cvf = np.asarray(sf["cell_vnodes"]).reshape(sf["n_cells"], -1)
+    cvc = np.asarray(sc["cell_vnodes"]).reshape(sc["n_cells"], -1)
+    fh = {nd for nd in sf["vhang"]}
+    for cell in range(0, sf["n_cells"], max(1, sf["n_cells"] // 25)):
+        for a in range(cvf.shape[1]):
+            if cvf[cell, a] in fh:
+                continue
+            ia = [(a // kf1 ** d) % kf1 for d in range(dim)]
+            want = 0.0
+            for b in range(2 ** dim):
+                wb = np.prod([(ia[d] / kf) if (b >> d) & 1 else 1 - ia[d] / kf for d in range(dim)])
+                want += wb * xc[cvc[cell, b] * dim]
+            assert abs(xf[cvf[cell, a] * dim] - want) < 1e-12

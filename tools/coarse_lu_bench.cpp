@@ -1,5 +1,6 @@
 // Times the dense coarsest-level factorization options for an n x n FP64 matrix (n = 2916 is the
-// Q2-Q2 4^3 coarsest MG level): rocSOLVER getrf / getrf_npvt / getri / getrs and a plain dgemm.
+// Q2-Q2 4^3 coarsest MG level; n = 25000 the Q1-Q1 p-level of configs[4]'s base mesh): rocSOLVER getrf /
+// getrf_npvt / getri / getrs and a plain dgemm, then getrf / getrs in FP32.
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -48,6 +49,21 @@ int main(int argc, char **argv) {
     std::printf("n=%d getrf %.2f ms getri %.2f ms getrf_npvt %.2f ms getrs(1 rhs) %.3f ms dgemm %.3f ms (%.1f TF) dgemv %.3f ms\n",
                 n, ms(t0, t1), ms(t1, t2), ms(t3, t4), ms(t5, t6), ms(t6, t7), 2.0 * n * n * (double)n / ms(t6, t7) / 1e9,
                 ms(t7, t8));
+  }
+  std::vector<float> Af(A.begin(), A.end());
+  float *fA, *fB;
+  CK(hipMalloc(&fA, sizeof(float) * n * n));
+  CK(hipMalloc(&fB, sizeof(float) * n));
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(fA, Af.data(), sizeof(float) * n * n, hipMemcpyHostToDevice));
+    CK(hipMemcpy(fB, Af.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+    auto t0 = now();
+    CK(rocsolver_sgetrf(h, n, n, fA, n, ipiv, info));
+    auto t1 = now();
+    CK(rocsolver_sgetrs(h, rocblas_operation_none, n, 1, fA, n, ipiv, fB, n));
+    auto t2 = now();
+    std::printf("n=%d sgetrf %.2f ms (%.1f TF) sgetrs(1 rhs) %.3f ms\n", n, ms(t0, t1),
+                2.0 / 3.0 * n * (double)n * n / ms(t0, t1) / 1e9, ms(t1, t2));
   }
   return 0;
 }
