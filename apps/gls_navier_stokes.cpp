@@ -1580,17 +1580,19 @@ struct Solver {
   }
   // the app's Mesh of an FE space of the triangulation (cells, nodes, MappingQ support points, hanging
   // lines, the slip boundaries' averaged node normals)
-  Mesh mesh_of_space(const gls_fe_space &F) {
+  Mesh mesh_of_space(const gls_fe_space &F, int k = -1, int kp = -1) {  // k, kp: the space's degrees (P's default)
+    k = k < 0 ? P.k : k;
+    kp = kp < 0 ? P.kp : kp;
     Mesh r;
     r.dim = P.dim;
-    r.k = P.k;
-    r.kp = P.kp;
+    r.k = k;
+    r.kp = kp;
     r.general = true;
     r.nc = F.n_cells;
     r.nv = F.n_vnodes;
     r.np = F.n_pnodes;
-    const int nvl = P.dim == 3 ? (P.k + 1) * (P.k + 1) * (P.k + 1) : (P.k + 1) * (P.k + 1);
-    const int npl = P.dim == 3 ? (P.kp + 1) * (P.kp + 1) * (P.kp + 1) : (P.kp + 1) * (P.kp + 1);
+    const int nvl = P.dim == 3 ? (k + 1) * (k + 1) * (k + 1) : (k + 1) * (k + 1);
+    const int npl = P.dim == 3 ? (kp + 1) * (kp + 1) * (kp + 1) : (kp + 1) * (kp + 1);
     r.cv.assign(F.cell_vnodes, F.cell_vnodes + r.nc * nvl);
     r.cp.assign(F.cell_pnodes, F.cell_pnodes + r.nc * npl);
     r.vx.assign(F.vnode_x, F.vnode_x + r.nv * P.dim);
@@ -1635,11 +1637,18 @@ struct Solver {
   // the triangulation coarsened one level at a time (gls_umesh_coarsen_to) down to the coarse mesh, each
   // with its FE space, MappingQ geometry, Dirichlet / slip constraints and hanging lines; transfers =
   // FE_Q's embedding (gls_fe_space_mg_transfer); FP64 damped-Jacobi V(2,2) at 0.6, exact LU on the
-  // coarsest level when it is small enough (<= 8192 DoFs), else 30 Jacobi sweeps there.
+  // coarsest level when it is small enough (<= 8192 DoFs), else 30 Jacobi sweeps there. Q2-Q1 / Q2-Q2: below the
+  // base mesh a p-level -- Q1-Q1 on the base mesh's cells (gls_fe_space_mg_transfer's p-level pair), factored by
+  // the dense LU (<= kPLevelDirectMax DoFs) -- whenever the base level is too large for the LU itself; this is also
+  // the whole hierarchy of an unrefined mesh (the reference's setup_AMG, gls_navier_stokes.cc:1180-1240: an
+  // algebraic multilevel preconditioner there, a geometric / polynomial one here, announced on stderr).
+  static constexpr int64_t kPLevelDirectMax = 40000;
+  bool plevel_used = false;
   void attach_umesh_mg() {
     int L = 0;
     for (int64_t c = 0; c < space->n_cells; ++c) L = std::max(L, (int)space->cell_level[c]);
-    if (L < 1) return;
+    plevel_used = false;
+    if (L < 1 && P.k < 2) return;
     std::vector<gls_ctx *> lv{ctx};
     std::vector<gls_fe_space *> spaces;
     std::vector<const gls_fe_space *> sp{space};
@@ -1664,6 +1673,32 @@ struct Solver {
       if (!ld.empty()) ck(gls_set_hanging(g, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging (multigrid level)");
       n_coarse = r.n_dofs();
     }
+    if (P.k >= 2 && (L < 1 || n_coarse > 8192)) {  // the Q1-Q1 p-level on the base mesh
+      gls_umesh *uc = nullptr;
+      ck(gls_umesh_coarsen_to(um, 0, &uc), "gls_umesh_coarsen_to");
+      gls_fe_space *s_ = nullptr;
+      const int rc = gls_umesh_fe_space(uc, 1, 1, P.qmapping_all ? 1 : 0, 0, nullptr, &s_);
+      gls_umesh_destroy(uc);
+      ck(rc, "gls_umesh_fe_space (p-level)");
+      const Mesh r = mesh_of_space(*s_, 1, 1);
+      if (r.n_dofs() <= kPLevelDirectMax) {
+        spaces.push_back(s_);
+        sp.push_back(s_);
+        const Constraints cc = make_constraints(P, r, time);
+        std::vector<int64_t> ld, lo, lm;
+        std::vector<double> lw;
+        constraint_lines(r, cc, ld, lo, lm, lw);
+        gls_ctx *g = make_context(r, cc);
+        mg_levels.push_back(g);
+        lv.push_back(g);
+        if (!ld.empty()) ck(gls_set_hanging(g, (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), lw.data()), "gls_set_hanging (p-level)");
+        n_coarse = r.n_dofs();
+        plevel_used = true;
+      } else {
+        gls_fe_space_destroy(s_);
+      }
+    }
+    if (lv.size() < 2) return;
     const size_t np = lv.size() - 1;
     std::vector<std::vector<int64_t>> off(np), inj(np);
     std::vector<std::vector<int32_t>> col(np);
@@ -1699,7 +1734,7 @@ struct Solver {
     mp.pre_smooth = mp.smoother ? 1 : 2;
     mp.post_smooth = mp.smoother ? 1 : 2;
     mp.omega = 0.6;
-    mp.coarse_direct = n_coarse <= 8192 ? 1 : -1;
+    mp.coarse_direct = n_coarse <= (plevel_used ? kPLevelDirectMax : 8192) ? 1 : -1;
     if (world == 1) {
       ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");
       return;
@@ -2032,9 +2067,10 @@ struct Solver {
     const char *krylov = P.lin_method == 1 ? "BiCGStab" : "GMRES";
     char prec[256];
     if (!mg_levels.empty() && (rmesh || space))
-      std::snprintf(prec, sizeof prec, "geometric multigrid %s on the %s refinement hierarchy (%zu levels)",
+      std::snprintf(prec, sizeof prec, "geometric multigrid %s on the %s refinement hierarchy (%zu levels%s)",
                     P.k != P.kp ? "V(1,1)-cycle with ILU(0) smoothing" : "V(2,2)-cycle with damped-Jacobi smoothing",
-                    rmesh ? "forest's" : "triangulation's", mg_levels.size() + 1);
+                    rmesh ? "forest's" : "triangulation's", mg_levels.size() + 1,
+                    plevel_used ? ", the last a Q1-Q1 p-level on the base mesh, dense LU" : "");
     else if (!mg_levels.empty())
       std::snprintf(prec, sizeof prec, "geometric multigrid V(1,1)-cycle on the nested hyper_cubes");
     else if (use_ilu && P.lin_method == 2)

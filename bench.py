@@ -357,17 +357,23 @@ def bench_cylinder3d(args):
     qall = tc  # configs[3]: MappingQ2 on every cell
     levels, sw = None, 0
     if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh
-        if refine < 1 and not args.cyl_plevel:
+        if refine < 1 and not (args.cyl_plevel or args.cyl_hp):
             sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 or the p-level (a level below the fine mesh)")
         m = mesh(refine)
         base = m.coarsen_to(0)
-        handles = [m.fe_space_handle(2, 1, qmapping_all=qall)] + [
-            m.coarsen_to(refine - l).fe_space_handle(2, 1, qmapping_all=qall) for l in range(1, refine)] + (
-            [base.fe_space_handle(2, 1, qmapping_all=qall)] if refine >= 1 else [])
-        kps = [(2, 1)] * len(handles)
-        if args.cyl_plevel:  # p-level below the base mesh: Q1-Q1 on the same cells, solved exactly
-            handles.append(base.fe_space_handle(1, 1, qmapping_all=qall))
-            kps.append((1, 1))
+        if args.cyl_hp:  # p first: Q2-Q1 fine -> Q1-Q1 on the same mesh -> the Q1-Q1 refinement hierarchy
+            handles = [m.fe_space_handle(2, 1, qmapping_all=qall), m.fe_space_handle(1, 1, qmapping_all=qall)] + [
+                m.coarsen_to(refine - l).fe_space_handle(1, 1, qmapping_all=qall) for l in range(1, refine)] + (
+                [base.fe_space_handle(1, 1, qmapping_all=qall)] if refine >= 1 else [])
+            kps = [(2, 1)] + [(1, 1)] * (len(handles) - 1)
+        else:
+            handles = [m.fe_space_handle(2, 1, qmapping_all=qall)] + [
+                m.coarsen_to(refine - l).fe_space_handle(2, 1, qmapping_all=qall) for l in range(1, refine)] + (
+                [base.fe_space_handle(2, 1, qmapping_all=qall)] if refine >= 1 else [])
+            kps = [(2, 1)] * len(handles)
+            if args.cyl_plevel:  # p-level below the base mesh: Q1-Q1 on the same cells, solved exactly
+                handles.append(base.fe_space_handle(1, 1, qmapping_all=qall))
+                kps.append((1, 1))
         xfer = [handles[l].mg_transfer_from(handles[l + 1]) for l in range(len(handles) - 1)]
         levels = [(taylorcouette3d_context(h.data, k=k_, kp=kp_) if tc else cylinder3d_context(k=k_, kp=kp_, space=h.data))
                   for h, (k_, kp_) in zip(handles, kps)]
@@ -377,7 +383,7 @@ def bench_cylinder3d(args):
         sw = 1 if args.cyl_smoother == "ilu" else 2
         nco = levels[-1][0].n_dofs
         ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
-                                       coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=0.6,
+                                       coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=args.mg_omega_cyl,
                                        coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother)
     else:
         ctx, sp, x = make(mesh(refine).fe_space(2, 1, qmapping_all=qall))
@@ -432,13 +438,15 @@ def bench_cylinder3d(args):
                                "(unadapted%s), Q2-Q1 MappingQ2, nu 0.005, BDF2 dt 0.05" % (
                                    ", %d global refinements (flat)" % args.cyl_refine if args.cyl_refine else "")),
                    "n_dofs": N, "n_cells": nc,
-                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the refinement hierarchy (%d levels, %s smoothing, "
+                   "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the %s (%d levels, %s smoothing, "
                                      "%s on the base mesh), rel 1e-4" % (
-                                         args.restart, sw, sw, len(levels),
+                                         args.restart, sw, sw,
+                                         "h-p hierarchy (Q2-Q1 fine, Q1-Q1 on the fine mesh and its refinement "
+                                         "hierarchy)" if args.cyl_hp else "refinement hierarchy", len(levels),
                                          {"ilu": "multicolor ILU(0)", "jacobi": "damped-Jacobi",
                                           "ilu-coarse": "damped-Jacobi on the finest, multicolor ILU(0) below"}[
                                              args.cyl_smoother],
-                                         ("exact LU of the Q1-Q1 p-level" if args.cyl_plevel else "exact LU")
+                                         ("exact LU of the Q1-Q1 level" if args.cyl_plevel or args.cyl_hp else "exact LU")
                                          if levels[-1][0].n_dofs <= args.direct_max else "%d sweeps" % args.mg_coarse_sweeps_cyl))
                    if levels else "GMRES(%d)+ILU(%d) %s, rel 1e-4" % (
                        args.restart, args.ilu_fill, "multicolor" if args.ilu_fill == 0 else "Cuthill-McKee")},
@@ -705,6 +713,10 @@ def main():
     ap.add_argument("--cyl-plevel", type=int, default=1,
                     help="cylinder3d / taylorcouette3d --cyl-precond hmg: 1 = a Q1-Q1 p-level below the base mesh "
                          "(gls_fe_space_mg_transfer's p-level pair), solved by the dense LU")
+    ap.add_argument("--cyl-hp", type=int, default=0,
+                    help="--cyl-precond hmg: 1 = p first (Q2-Q1 fine -> Q1-Q1 on the fine mesh -> the Q1-Q1 refinement "
+                         "hierarchy, exact LU at the bottom)")
+    ap.add_argument("--mg-omega-cyl", type=float, default=0.6, help="hmg: damped-Jacobi weight")
     ap.add_argument("--direct-max", type=int, default=40000,
                     help="hmg: the coarsest level is factored (dense LU) up to this many DoFs, else smoothed")
     ap.add_argument("--rel", type=float, default=1e-4)

@@ -241,7 +241,8 @@ int gls_mg_attach(gls_ctx *ctx, const gls_mg_params *prm);
  * level-(l+1) state takes (hanging values are then distributed from their lines). Restriction = P^T;
  * the V-cycle zeroes constrained rows (Dirichlet and hanging) after each transfer. Smoothing: damped
  * Jacobi with each level's own operator (per-cell kernels on hanging levels, FP64). One GPU. Host arrays
- * (copied). */
+ * (copied). The levels may differ in element degree (h-p hierarchies: a Q2-Q1 level above Q1-Q1 ones, the
+ * p-level pairs of gls_fe_space_mg_transfer), not in dimension. */
 int gls_mg_attach_transfers(gls_ctx *ctx, const gls_mg_params *prm, const int64_t *const *p_off,
                             const int32_t *const *p_col, const double *const *p_w, const int64_t *const *inject);
 /* The refinement-hierarchy V-cycle ACROSS RANKS on general meshes (the reference's AMG is global,
@@ -715,7 +716,10 @@ int gls_umesh_set_periodic(gls_umesh *mesh, int n_periodic, const int32_t *perio
  * node's reference position, whatever the mapping; fine hanging rows empty, coarse masters as columns --
  * and inject (n_dofs(coarse)): the fine DoF at each coarse DoF's node. off == NULL: nnz only. Feed both to
  * gls_mg_attach_transfers (the reference preconditions these meshes with ILU / ML-AMG,
- * gls_navier_stokes.cc:1161-1240). */
+ * gls_navier_stokes.cc:1161-1240). A P-LEVEL PAIR -- the same active cells (two spaces of one triangulation, or
+ * of copies with the same hierarchy), the coarse space of lower degree (Q2-Q1 -> Q1-Q1) -- gives the coarse
+ * degree's interpolant at the fine nodes (FE_Q's embedding of the lower degree) and the injection at the
+ * shared nodes (the fine degree a multiple of the coarse one); other degree mismatches are GLS_EINVAL. */
 int gls_umesh_coarsen_to(const gls_umesh *mesh, int level, gls_umesh **out);
 int gls_fe_space_mg_transfer(const gls_fe_space *fine, const gls_fe_space *coarse, int64_t *nnz, int64_t *off,
                              int32_t *col, double *w, int64_t *inject);

@@ -505,6 +505,12 @@ struct gls_ctx {
     // the first pressure DoF pinned (enclosed-flow gauge); falls back to the one-workgroup
     // Gauss-Jordan (mg_dense_invert) for small levels or when the LU reports a zero pivot
     bool lu = false;
+    // large coarsest levels (kDirectSmall < n <= kDirectMax, e.g. a Q1-Q1 p-level of a 4.7 k-cell base mesh):
+    // the pinned FP64 matrix rounded to FP32, pivoted sgetrf + sgetri, applied by sgemv (a preconditioner's
+    // coarse solve: FP32 rounding of A^-1 is far below the V-cycle's own error; half the bytes and the FP32
+    // matrix-core rate for the O(n^3) setup)
+    bool lu32 = false;
+    DevBuf<float> probe32, b32, x32;
     int64_t npvt_ipiv_n = -1;  // ipiv holds the identity permutation of this size (unpivoted LU)
     struct Blas {  // owning rocBLAS handle (movable, destroyed with the MG state)
       rocblas_handle h = nullptr;
@@ -2220,6 +2226,7 @@ int gls_set_hanging(gls_ctx *c, int64_t n, const int64_t *dofs, const int64_t *o
 // --------------------------------------------------------------------------------------------
 namespace {
 enum { MB_U = 0, MB_U1, MB_U2, MB_U3, MB_B, MB_X, MB_Y, MB_BOX, MB_N };
+constexpr int64_t kDirectSmall = 8192, kDirectMax = 40000;  // coarsest-level dense LU: FP64 / FP32 ranges
 double *mgbuf(gls_ctx *c, int l, int which) { return c->mg.bufs[(size_t)l * MB_N + which]->p; }
 int64_t mg_nbox(const gls_ctx *c, int l) {
   const auto &d = c->mg.dims[(size_t)l];
@@ -2417,6 +2424,35 @@ int mg_prepare(gls_ctx *c) {
     }
     const auto t1 = tick();
     mg.lu = false;
+    mg.lu32 = false;
+    if (n > kDirectSmall) {  // FP32 pivoted LU + explicit inverse of the pinned matrix
+      const int64_t pin = (int64_t)g->dim * g->n_vnodes;  // the first pressure DoF
+      if (pin >= n) return set_err(GLS_EINVAL, "mg: coarsest level without pressure DoFs");
+      HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
+      HIP_TRY(gls::vec_to_f32(mg.probe.p, mg.probe32.p, n * n, c->stream));
+      int inf = -1;
+      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+          rocsolver_sgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+              rocblas_status_success)
+        return set_err(GLS_EHIP, "rocsolver_sgetrf failed");
+      HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      const auto t2 = tick();
+      if (inf == 0) {
+        if (rocsolver_sgetri(mg.blas, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+            rocblas_status_success)
+          return set_err(GLS_EHIP, "rocsolver_sgetri failed");
+        HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+      }
+      if (verbose)
+        std::printf("mg: coarse FP32 LU n=%lld info=%d: levels+probe %.2f ms, sgetrf %.2f ms, sgetri done at %.2f ms\n",
+                    (long long)n, inf, ms(t0, t1), ms(t1, t2), ms(t0, tick()));
+      if (inf != 0) return set_err(GLS_EINVAL, "coarse FP32 LU: zero pivot %d", inf);
+      mg.lu32 = mg.direct_ok = true;
+      mg.dirty = false;
+      return GLS_OK;
+    }
     // gj | lu | lu_npvt. Default: LU without pivoting (rocSOLVER's pivoted panel factorization is ~1 ms of
     // a Newton step at n = 500, profiles/r04_ab_env_switches.txt) with a pivoted retry when a pivot vanishes
     const char *cs = std::getenv("GLS_MG_COARSE_SOLVER");
@@ -2754,6 +2790,17 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
     return GLS_OK;
   }
   if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
+    if (mg.lu32) {  // x = A^-1 b in FP32, the pinned pressure DoF's correction zero
+      const float one = 1.0f, zero = 0.0f;
+      HIP_TRY(gls::vec_to_f32(b, mg.b32.p, n, c->stream));
+      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+          rocblas_sgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe32.p,
+                        (rocblas_int)n, mg.b32.p, 1, &zero, mg.x32.p, 1) != rocblas_status_success)
+        return set_err(GLS_EHIP, "rocblas_sgemv failed");
+      HIP_TRY(gls::vec_from_f32(mg.x32.p, x, n, c->stream));
+      HIP_TRY(hipMemsetAsync(x + (int64_t)g->dim * g->n_vnodes, 0, sizeof(double), c->stream));
+      return GLS_OK;
+    }
     if (mg.lu) {
       const double one = 1.0, zero = 0.0;
       if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
@@ -3312,14 +3359,20 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
       mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
-  // direct coarsest solve: single GPU, small coarsest level (probing costs n J.v launches per state)
+  // direct coarsest solve: single GPU, coarsest level up to kDirectMax DoFs (FP64 LU up to kDirectSmall, FP32 above)
   {
     const int64_t nco = mg.lev.back()->n_dofs;
     const int want = p->coarse_direct;
-    if (want > 0 && (mg.boxed || nco > 8192)) return set_err(GLS_EINVAL, "mg: direct coarse solve needs one GPU, <= 8192 DoFs");
+    if (want > 0 && (mg.boxed || nco > kDirectMax))
+      return set_err(GLS_EINVAL, "mg: direct coarse solve needs one GPU, <= %lld DoFs", (long long)kDirectMax);
     mg.direct = want > 0 || (want == 0 && !mg.boxed && nco <= 2048);
     if (mg.direct) {
       GLS_TRY(mg.probe.alloc((size_t)(nco * nco)));
+      if (nco > kDirectSmall) {
+        GLS_TRY(mg.probe32.alloc((size_t)(nco * nco)));
+        GLS_TRY(mg.b32.alloc((size_t)nco));
+        GLS_TRY(mg.x32.alloc((size_t)nco));
+      }
       if (std::getenv("GLS_MG_COARSE_SOLVER")) GLS_TRY(mg.aug.alloc((size_t)(2 * nco * nco)));  // gj experiments
       GLS_TRY(mg.ipiv.alloc((size_t)nco));
       GLS_TRY(mg.info.alloc(1));
@@ -3433,8 +3486,10 @@ int gls_mg_attach_transfers(gls_ctx *c, const gls_mg_params *p, const int64_t *c
   mg.csr = true;
   for (int l = 0; l < p->n_levels; ++l) {
     gls_ctx *g = p->levels[l];
-    if (!g || g->dim != c->dim || g->k != c->k || g->kp != c->kp || g->dist.on)
-      return set_err(GLS_EINVAL, "mg level %d: dimension / order differs from level 0, or distributed", l);
+    // the levels may differ in degree (h-p hierarchies: the CSR transfers carry the p-level pairs of
+    // gls_fe_space_mg_transfer), not in dimension
+    if (!g || g->dim != c->dim || g->dist.on)
+      return set_err(GLS_EINVAL, "mg level %d: dimension differs from level 0, or distributed", l);
     mg.lev.push_back(g);
     mg.dims.push_back({0, 0, 0});
   }

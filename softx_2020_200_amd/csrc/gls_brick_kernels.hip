@@ -1083,6 +1083,17 @@ hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+__global__ void k_from_f32(const float *__restrict__ a, double *__restrict__ b, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) b[i] = (double)a[i];
+}
+hipError_t vec_from_f32(const float *a, double *b, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1 << 16);
+  hipLaunchKernelGGL(k_from_f32, dim3((unsigned)blocks), dim3(256), 0, s, a, b, n);
+  return hipGetLastError();
+}
+
 int brick_boundary_nodes(int k) { return k == 1 ? BrickCfg<1>::NBND : (k == 2 ? BrickCfg<2>::NBND : 0); }
 
 // y[node] (4 fields) = sum of the bricks' partial sums over the node's slab slots (fixed order:

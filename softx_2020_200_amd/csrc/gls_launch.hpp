@@ -21,6 +21,7 @@ size_t brick_qdata_size(int k, int n_cells);  // doubles of MODE_LIN storage
 // J.v in FP32 arithmetic from P.qdf (FP32 linearization); v, y FP64 (multigrid smoother operator)
 hipError_t launch_brick_jv_f32(int k, const OpParams &P, const Tables1D &T, hipStream_t s);
 hipError_t vec_to_f32(const double *a, float *b, int64_t n, hipStream_t s);
+hipError_t vec_from_f32(const float *a, double *b, int64_t n, hipStream_t s);
 // Q2 brick J.v in the pencil dataflow (gls_brick_pencil.hip; FP64 from P.qd or FP32 from P.qdf), same
 // contract as the lane-per-point MODE_JVQ launch with a slab; hipErrorNotSupported when not applicable
 // (probing, colored launches, no slab). GLS_PENCIL=0 disables it.

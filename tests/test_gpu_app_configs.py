@@ -157,8 +157,10 @@ def check_configs3_pipeline(out, dumps, tol):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("np_ranks", [1, 2])
-def test_configs4_cylinder3d_re200_bdf2_kelly_pipeline(tmp_path, np_ranks):
+@pytest.mark.parametrize("np_ranks,precond", [(1, None), (2, None), (1, "hmg")])
+def test_configs4_cylinder3d_re200_bdf2_kelly_pipeline(tmp_path, np_ranks, precond):
+    """precond hmg: the hierarchy multigrid with the Q1-Q1 p-level on the base mesh (dense LU) below it -- on the
+    first (unadapted) mesh the whole hierarchy is that p-level pair"""
     from oracle.oracle import Oracle, kelly_from_face_pieces
     from softx_2020_200_amd.native import UMesh
     prm = open(os.path.join(CASES, "cylinder3d_q2q1_re200_kelly.prm")).read()
@@ -168,8 +170,12 @@ def test_configs4_cylinder3d_re200_bdf2_kelly_pipeline(tmp_path, np_ranks):
     prm = setprm(prm, "tolerance", "%g" % tol)
     prm = setprm(prm, "relative residual", "1e-10")
     prm = setprm(prm, "minimum residual", "1e-13")
-    out, dumps = run_app(tmp_path, prm, [os.path.join(MESHES, "cylinder3d_1layer.msh")], extra=("--np", str(np_ranks)))
+    out, dumps = run_app(tmp_path, prm, [os.path.join(MESHES, "cylinder3d_1layer.msh")],
+                         extra=("--np", str(np_ranks)) + (("--precond", precond) if precond else ()))
     assert len(dumps) == 3, out
+    if precond == "hmg":
+        err = (tmp_path / "stderr.txt").read_text()
+        assert "Q1-Q1 p-level on the base mesh, dense LU" in err, err[-1500:]
     assert "Running on %d MPI rank(s)" % np_ranks in out
     nu = 0.005
     m = UMesh(3, gmsh=os.path.join(MESHES, "cylinder3d_1layer.msh"))

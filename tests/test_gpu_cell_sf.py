@@ -1,6 +1,6 @@
 """The sum-factorized per-cell J.v (softx_2020_200_amd/csrc/gls_cell_sf.hip: 3D Q2-Q1 and Q2-Q2 cells, the
 default for every per-cell J.v from the linearization cache) against the dense per-cell kernel (GLS_CELL_SF=0,
-read per launch) and the oracle's assembled, constraint-eliminated operator (gls_navier_stokes.cc:548-622):
+read per launch), the MFMA variant of the dense contractions (GLS_CELL_SF=2, v_mfma_f64_16x16x4f64) and the oracle's assembled, constraint-eliminated operator (gls_navier_stokes.cc:548-622):
 MappingQ2 curved cells (cylinder shell, cylinder, unstructured gmsh), adapted meshes with hanging lines,
 axis-aligned boxes on the per-cell path, transient and steady schemes, SRF. FP64 throughout: 1e-12 against
 the oracle, 1e-13 between the two kernels (same per-point arithmetic, different summation order)."""
@@ -39,11 +39,13 @@ def _check(monkeypatch, p, ctx, seed=20200200):
     assert np.array_equal(ctx.jacobian_apply(V).cpu().numpy(), sf)  # fixed-order sums: bitwise repeatable
     monkeypatch.setenv("GLS_CELL_SF", "0")
     dense = ctx.jacobian_apply(V).cpu().numpy()
+    monkeypatch.setenv("GLS_CELL_SF", "2")  # the MFMA contractions (A/B variant)
+    mfma = ctx.jacobian_apply(V).cpu().numpy()
     monkeypatch.delenv("GLS_CELL_SF")
     ref = Oracle(p).jacobian_apply(u, v, u1, u2)
-    e_d, e_o = relerr(sf, dense), relerr(sf, ref)
-    print("sum-factorized J.v vs dense %.2e, vs oracle %.2e" % (e_d, e_o))
-    assert e_d < 1e-13 and e_o < 1e-12, (e_d, e_o)
+    e_d, e_o, e_m = relerr(sf, dense), relerr(sf, ref), relerr(mfma, ref)
+    print("sum-factorized J.v vs dense %.2e, vs oracle %.2e; MFMA J.v vs oracle %.2e" % (e_d, e_o, e_m))
+    assert e_d < 1e-13 and e_o < 1e-12 and e_m < 1e-12, (e_d, e_o, e_m)
 
 
 MAPPED = [("cshell", 1, "bdf2", False), ("cshell", 2, "steady", True), ("cylinder", 1, "bdf1", True),
