@@ -391,21 +391,24 @@ struct gls_ctx {
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
     std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
-    DevBuf<int32_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc ints)
+    DevBuf<int64_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc int64)
     DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
     DevBuf<uint16_t> mc_map;   // per (row, pivot, upper entry of the pivot row): position in the row
     std::vector<int32_t> mc_cg;          // per color: first node group (host, n_colors + 1)
-    DevBuf<int32_t> mc_grow, mc_lsp, mc_usp;  // node group -> first row; per row: L / U split entries
-    DevBuf<int32_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
+    DevBuf<int32_t> mc_grow;             // node group -> first row
+    DevBuf<int64_t> mc_lsp, mc_usp;      // per row: L / U split entries
+    DevBuf<int64_t> ghost_diag;          // across ranks: diagonal entries of the ghost (identity) rows
     // across ranks, complete owned rows: the neighbours' cell contributions to the owned x owned block
     // arrive per probe round through the export exchange (n_rounds = the largest probe count of any
     // rank); round p adds send_buf slots into CSR entries ru[rr[p] .. rr[p+1]) in a fixed order
     bool complete = false;
     int n_rounds = 0;
     std::vector<int64_t> rr;
-    DevBuf<int32_t> ru, ruoff, rslot;
+    DevBuf<int64_t> ru;
+    DevBuf<int32_t> ruoff, rslot;
     std::vector<int64_t> pdoff, peoff;   // per probe: offsets into pdofs and (pent, prow)
-    DevBuf<int32_t> pdofs, pent, prow;   // probe unit DoFs; CSR entries filled by the probe and their rows
+    DevBuf<int32_t> pdofs, prow;         // probe unit DoFs; the rows of the CSR entries filled by the probe
+    DevBuf<int64_t> pent;                // those entries (positions: 64-bit, the fine levels pass 2^31 entries)
     DevBuf<int32_t> pdpid, pepid;        // probe of each unit DoF / each extracted entry (batched probing)
     DevBuf<double> bV, bC, bY;           // batched probing: probe vectors, C V (hanging lines), results [batch][n_dofs]
     // batched probing's activity: which (probe, cell batch) pairs have a nonzero C e_p on their cells depends on
@@ -416,7 +419,10 @@ struct gls_ctx {
     std::vector<int64_t> woff;
     int wB = 0;
     int64_t wnblk = 0;
-    DevBuf<int32_t> rowp, col, didx;     // CSR pattern (Cuthill-McKee order), diagonal entry per row
+    // CSR pattern (Cuthill-McKee or multicolor order), diagonal entry per row: 64-bit positions (a 13 M-DoF Q2-Q1
+    // level has ~2.9e9 entries); rowp32: the 32-bit row pointers rocSPARSE takes, when the pattern fits them
+    DevBuf<int64_t> rowp, didx;
+    DevBuf<int32_t> col, rowp32;
     DevBuf<int32_t> perm;                // DoF -> its row in the factored (renumbered) matrix
     DevBuf<double> val, vbuf, ybuf, tbuf;
     DevBuf<char> work;
@@ -2979,7 +2985,7 @@ static int ilu_probe_batched(gls_ctx *c) {
     const int64_t e0 = I.peoff[(size_t)p0], e1 = I.peoff[(size_t)(p0 + nb)];
     HIP_TRY(gls::probe_extract_batched(I.val.p, I.pent.p + e0, I.prow.p + e0, I.pepid.p + e0, p0, e1 - e0, I.bY.p, n, s));
   }
-  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
+  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed64(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
   if (record) {
     GLS_TRY(I.wlist.upload(hlist.data(), hlist.size()));
     I.woff.swap(hoff);
@@ -3019,10 +3025,10 @@ static int ilu_probe(gls_ctx *c) {  // I.val <- the operator's CSR values (gls_j
     else if (D.n_recv) HIP_TRY(gls::vec_fill(D.recv_buf, D.n_recv, 0.0, s));
     if (D.xchg(D.user, 1) != 0) return set_err(GLS_ECOMM, "ILU probe exchange failed");
     const int64_t a = I.rr[(size_t)p], b = I.rr[(size_t)p + 1];
-    if (b > a) HIP_TRY(gls::vec_add_dofs_ordered(I.val.p, I.ru.p + a, I.ruoff.p + a, I.rslot.p, b - a, D.send_buf, s));
+    if (b > a) HIP_TRY(gls::vec_add_pos_ordered(I.val.p, I.ru.p + a, I.ruoff.p + a, I.rslot.p, b - a, D.send_buf, s));
   }
   c->probe_local = false;
-  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
+  if (I.ghost_diag.n) HIP_TRY(gls::vec_set_const_indexed64(I.val.p, I.ghost_diag.p, (int64_t)I.ghost_diag.n, 1.0, s));
   return GLS_OK;
 }
 static int apply_ilu(gls_ctx *c, const double *v, double *z);
@@ -3047,7 +3053,7 @@ static int ensure_ilu(gls_ctx *c) {
                                I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, I.mc_moff.p,
                                I.mc_map.n ? I.mc_map.p : nullptr, s));
   else
-    RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
+    RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
   I.valid = true;
   if (verbose) {
     const auto t2 = now();
@@ -3075,9 +3081,9 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
-  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dL, I.val.p, I.rowp.p, I.col.p, I.info,
+  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dL, I.val.p, I.rowp32.p, I.col.p, I.info,
                                 I.vbuf.p, I.tbuf.p, rocsparse_solve_policy_auto, I.work.p));
-  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
+  RS_TRY(rocsparse_dcsrsv_solve(I.h, rocsparse_operation_none, m, nnz, &one, I.dU, I.val.p, I.rowp32.p, I.col.p, I.info,
                                 I.tbuf.p, I.vbuf.p, rocsparse_solve_policy_auto, I.work.p));
   HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
   return GLS_OK;
@@ -4581,9 +4587,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       std::sort(buf.begin(), buf.end());
       acol.insert(acol.end(), buf.begin(), buf.end());
       aoff[(size_t)i + 1] = (int64_t)acol.size();
-      if (aoff[(size_t)i + 1] >= INT32_MAX)  // the factored CSR is 32-bit (rocSPARSE / the multicolor kernels)
-        return set_err(GLS_EINVAL, "gls_ilu_attach: the matrix has more than %d entries (32-bit CSR): use the "
-                                   "multigrid (or damped-Jacobi smoothing on this level)", INT32_MAX);
     }
   }
   // node graph of that pattern (x ~ y when a row of x holds a DoF of y) for the distance-2 coloring
@@ -4964,7 +4967,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     olddof[(size_t)r] = (int32_t)order[(size_t)r];
   }
   // the system matrix's pattern in the new numbering, then its ILU(fill) pattern
-  std::vector<int32_t> arow((size_t)n + 1, 0), acl;
+  std::vector<int64_t> arow((size_t)n + 1, 0);
+  std::vector<int32_t> acl;
   std::vector<char> aclown;  // entry probed on this rank (pent / prow); else filled by the neighbours only
   acl.reserve(acol.size());
   {
@@ -4979,18 +4983,19 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
         acl.push_back(e.first);
         aclown.push_back(e.second);
       }
-      arow[(size_t)r + 1] = (int32_t)acl.size();
+      arow[(size_t)r + 1] = (int64_t)acl.size();
     }
   }
-  std::vector<int32_t> rowp, col;
-  if (gls::iluk_pattern(n, arow.data(), acl.data(), fill, rowp, col) != GLS_OK)
+  std::vector<int64_t> rowp;
+  std::vector<int32_t> col;
+  if (gls::iluk_pattern<int64_t>(n, arow.data(), acl.data(), fill, rowp, col) != GLS_OK)
     return set_err(GLS_EINVAL, "gls_ilu_attach: ILU(%d) pattern", fill);
-  std::vector<int32_t> didx((size_t)n, -1);
+  std::vector<int64_t> didx((size_t)n, -1);
   for (int64_t r = 0; r < n; ++r) {
     const auto b = col.begin() + rowp[(size_t)r], e = col.begin() + rowp[(size_t)r + 1];
     const auto it = std::lower_bound(b, e, (int32_t)r);
     if (it == e || *it != r) return set_err(GLS_EINVAL, "gls_ilu_attach: row %lld has no diagonal", (long long)r);
-    didx[(size_t)r] = (int32_t)(it - col.begin());
+    didx[(size_t)r] = (int64_t)(it - col.begin());
   }
   // multicolor solves: node groups (consecutive rows of one node), per color their range, per row
   // the split of its entries into other colors / own node; valid while no entry couples two nodes of
@@ -5000,7 +5005,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int64_t> mc_moff_h;  // position map offsets (empty: no map)
   if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
     const int ncl = I.n_order_colors;
-    std::vector<int32_t> cstart((size_t)ncl + 2, (int32_t)n), grow, cg((size_t)ncl + 1, 0), lsp((size_t)n), usp((size_t)n);
+    std::vector<int32_t> cstart((size_t)ncl + 2, (int32_t)n), grow, cg((size_t)ncl + 1, 0);
+    std::vector<int64_t> lsp((size_t)n), usp((size_t)n);
     for (int64_t r = n - 1; r >= 0; --r) cstart[(size_t)dcolor[(size_t)olddof[(size_t)r]]] = (int32_t)r;
     for (int c = ncl - 1; c >= 0; --c) cstart[(size_t)c] = std::min(cstart[(size_t)c], cstart[(size_t)c + 1]);
     bool ok = true;
@@ -5009,7 +5015,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       if (r == 0 || x != dnode_[(size_t)olddof[(size_t)r - 1]]) grow.push_back((int32_t)r);
       if (r + 1 - grow.back() > gls::kMaxGroupRows) ok = false;
       const int cr = dcolor[(size_t)olddof[(size_t)r]];
-      int32_t e = rowp[(size_t)r];
+      int64_t e = rowp[(size_t)r];
       while (e < rowp[(size_t)r + 1] && col[(size_t)e] < cstart[(size_t)cr]) ++e;
       lsp[(size_t)r] = e;
       while (e < rowp[(size_t)r + 1] && col[(size_t)e] < cstart[(size_t)cr + 1]) {
@@ -5029,15 +5035,15 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       GLS_TRY(I.mc_usp.upload(usp.data(), usp.size()));
       {
         const size_t ng = grow.size() - 1;
-        std::vector<int32_t> desc(ng * gls::kGroupDesc, 0);
+        std::vector<int64_t> desc(ng * gls::kGroupDesc, 0);
         for (size_t g = 0; g < ng; ++g) {
-          int32_t *d = &desc[g * gls::kGroupDesc];
+          int64_t *d = &desc[g * gls::kGroupDesc];
           const int32_t r0 = grow[g], nr = grow[g + 1] - r0;
           d[0] = r0;
           d[1] = nr;
           d[2] = rowp[(size_t)r0];
           d[3] = rowp[(size_t)(r0 + nr)];
-          for (int t = 1; t < 4; ++t) d[3 + t] = t < nr ? rowp[(size_t)(r0 + t)] : INT32_MAX;
+          for (int t = 1; t < 4; ++t) d[3 + t] = t < nr ? rowp[(size_t)(r0 + t)] : INT64_MAX;
           for (int t = 0; t < nr; ++t) {
             d[8 + t] = lsp[(size_t)(r0 + t)];
             d[12 + t] = usp[(size_t)(r0 + t)];
@@ -5049,14 +5055,14 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       }
       I.mc_cg = cg;
       I.mc_solve = true;
-      int32_t maxrow = 0;
+      int64_t maxrow = 0;
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
       I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
       if (I.mc_factor) {  // the position map (uint16 per entry), when it fits a quarter of free memory
         mc_moff_h.assign((size_t)n + 1, 0);
         for (int64_t r = 0; r < n; ++r) {
           int64_t m = 0;
-          for (int32_t e = rowp[(size_t)r]; e < lsp[(size_t)r]; ++e) {
+          for (int64_t e = rowp[(size_t)r]; e < lsp[(size_t)r]; ++e) {
             const int32_t k = col[(size_t)e];
             m += (rowp[(size_t)k + 1] - didx[(size_t)k] - 1 + 3) & ~3;  // segments padded to quads
           }
@@ -5101,21 +5107,22 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   std::vector<int64_t> pdoff((size_t)nprobe + 1, 0), peoff((size_t)nprobe + 1, 0);
   for (int64_t d = 0; d < n; ++d) ++pdoff[(size_t)probe_of(d) + 1];
   for (int64_t r = 0; r < n; ++r)
-    for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t)
+    for (int64_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t)
       if (aclown[(size_t)t]) ++peoff[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]]) + 1];
   for (int p = 0; p < nprobe; ++p) {
     pdoff[(size_t)p + 1] += pdoff[(size_t)p];
     peoff[(size_t)p + 1] += peoff[(size_t)p];
   }
-  std::vector<int32_t> pdofs((size_t)pdoff[(size_t)nprobe]), pent((size_t)peoff[(size_t)nprobe]), prow(pent.size());
+  std::vector<int32_t> pdofs((size_t)pdoff[(size_t)nprobe]), prow((size_t)peoff[(size_t)nprobe]);
+  std::vector<int64_t> pent(prow.size());
   {
     std::vector<int64_t> f1(pdoff.begin(), pdoff.end() - 1), f2(peoff.begin(), peoff.end() - 1);
     // (complete rows: the unconstrained ghost DoFs are probed too)
     for (int64_t d = 0; d < n; ++d)
       pdofs[(size_t)f1[(size_t)probe_of(d)]++] = ghost(d) && !(cmpl && !fcons[(size_t)d]) ? -1 : (int32_t)d;
     for (int64_t r = 0; r < n; ++r) {
-      int32_t pos = rowp[(size_t)r];
-      for (int32_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) {
+      int64_t pos = rowp[(size_t)r];
+      for (int64_t t = arow[(size_t)r]; t < arow[(size_t)r + 1]; ++t) {
         while (col[(size_t)pos] < acl[(size_t)t]) ++pos;  // both rows sorted; A's pattern is a subset
         if (!aclown[(size_t)t]) continue;
         const int64_t k = f2[(size_t)probe_of(olddof[(size_t)acl[(size_t)t]])]++;
@@ -5147,7 +5154,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     }
     pdofs.swap(pd2);
     pdoff.swap(pdoff2);
-    std::vector<int32_t> gd;
+    std::vector<int64_t> gd;
     for (int64_t r = 0; r < n; ++r)
       if (ghost(olddof[(size_t)r])) gd.push_back(didx[(size_t)r]);
     GLS_TRY(I.ghost_diag.upload(gd.data(), gd.size()));
@@ -5168,12 +5175,13 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
     std::stable_sort(key.begin(), key.end(), [](const std::pair<int64_t, int64_t> &a, const std::pair<int64_t, int64_t> &b) {
       return a.first < b.first;
     });
-    std::vector<int32_t> ru, ruoff{0}, rslot;
+    std::vector<int64_t> ru;
+    std::vector<int32_t> ruoff{0}, rslot;
     std::vector<int64_t> rr((size_t)std::max(n_rounds, 0) + 1, 0);
     for (size_t t = 0; t < key.size(); ++t) {
       if (t == 0 || key[t].first != key[t - 1].first) {
         if (t) ruoff.push_back((int32_t)rslot.size());
-        ru.push_back((int32_t)(key[t].first % nnz));
+        ru.push_back(key[t].first % nnz);
         ++rr[(size_t)(key[t].first / nnz) + 1];
       }
       rslot.push_back(remote[(size_t)key[t].second].slot);
@@ -5216,6 +5224,20 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   I.n_blocks = nblk;
   I.athresh = athresh;
   I.rthresh = rthresh;
+  if (I.nnz >= INT32_MAX) {  // past 2^31 entries: the multicolor kernels only (rocSPARSE takes 32-bit CSR)
+    if (!I.mc_factor || !I.mc_solve)
+      return set_err(GLS_EINVAL, "gls_ilu_attach: %lld entries (> 2^31): the multicolor order with fill 0 is needed",
+                     (long long)I.nnz);
+    I.boost_tol = athresh > 0 ? athresh : 1e-300;  // as below, read by the multicolor factorization
+    I.boost_val = athresh > 0 ? athresh : 1e-12;
+    I.valid = false;
+    I.on = true;
+    return GLS_OK;
+  }
+  {
+    std::vector<int32_t> rp32(rowp.begin(), rowp.end());
+    GLS_TRY(I.rowp32.upload(rp32.data(), rp32.size()));
+  }
   RS_TRY(rocsparse_create_handle(&I.h));
   RS_TRY(rocsparse_set_stream(I.h, c->stream));
   RS_TRY(rocsparse_create_mat_descr(&I.dA));
@@ -5228,15 +5250,15 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   RS_TRY(rocsparse_create_mat_info(&I.info));
   const rocsparse_int m = (rocsparse_int)n, nnz = (rocsparse_int)I.nnz;
   size_t b0 = 0, b1 = 0, b2 = 0;
-  RS_TRY(rocsparse_dcsrilu0_buffer_size(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, &b0));
-  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp.p, I.col.p, I.info, &b1));
-  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp.p, I.col.p, I.info, &b2));
+  RS_TRY(rocsparse_dcsrilu0_buffer_size(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, &b0));
+  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp32.p, I.col.p, I.info, &b1));
+  RS_TRY(rocsparse_dcsrsv_buffer_size(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp32.p, I.col.p, I.info, &b2));
   GLS_TRY(I.work.alloc(std::max(std::max(b0, b1), std::max(b2, (size_t)16))));
-  RS_TRY(rocsparse_dcsrilu0_analysis(I.h, m, nnz, I.dA, I.val.p, I.rowp.p, I.col.p, I.info, rocsparse_analysis_policy_reuse,
+  RS_TRY(rocsparse_dcsrilu0_analysis(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, rocsparse_analysis_policy_reuse,
                                      rocsparse_solve_policy_auto, I.work.p));
-  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp.p, I.col.p, I.info,
+  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dL, I.val.p, I.rowp32.p, I.col.p, I.info,
                                    rocsparse_analysis_policy_reuse, rocsparse_solve_policy_auto, I.work.p));
-  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp.p, I.col.p, I.info,
+  RS_TRY(rocsparse_dcsrsv_analysis(I.h, rocsparse_operation_none, m, nnz, I.dU, I.val.p, I.rowp32.p, I.col.p, I.info,
                                    rocsparse_analysis_policy_reuse, rocsparse_solve_policy_auto, I.work.p));
   // pivots that end below athresh in magnitude are boosted to athresh (enclosed-flow pressure mode)
   // (rocsparse stores the two pointers and reads them at every csrilu0: they must outlive this call;
@@ -5277,9 +5299,11 @@ extern "C" int gls_ilu_matrix(gls_ctx *c, int32_t *rowp, int32_t *col, double *v
   HIP_TRY(hipStreamSynchronize(c->stream));
   // renumbered CSR on the device; returned in the context's DoF numbering
   const int64_t n = c->n_dofs;
-  std::vector<int32_t> rp((size_t)n + 1), cl((size_t)I.nnz), pm((size_t)n);
+  if (I.nnz >= INT32_MAX) return set_err(GLS_EINVAL, "gls_ilu_matrix: %lld entries do not fit its 32-bit CSR", (long long)I.nnz);
+  std::vector<int64_t> rp((size_t)n + 1);
+  std::vector<int32_t> cl((size_t)I.nnz), pm((size_t)n);
   std::vector<double> vl((size_t)I.nnz);
-  HIP_TRY(hipMemcpy(rp.data(), I.rowp.p, sizeof(int32_t) * rp.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(rp.data(), I.rowp.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(cl.data(), I.col.p, sizeof(int32_t) * cl.size(), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(vl.data(), I.val.p, sizeof(double) * vl.size(), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(pm.data(), I.perm.p, sizeof(int32_t) * pm.size(), hipMemcpyDeviceToHost));
@@ -5287,7 +5311,7 @@ extern "C" int gls_ilu_matrix(gls_ctx *c, int32_t *rowp, int32_t *col, double *v
   for (int64_t i = 0; i < n; ++i) old[(size_t)pm[(size_t)i]] = (int32_t)i;
   std::vector<std::vector<std::pair<int32_t, double>>> rows((size_t)n);
   for (int64_t r = 0; r < n; ++r)
-    for (int32_t e = rp[(size_t)r]; e < rp[(size_t)r + 1]; ++e) rows[(size_t)old[(size_t)r]].push_back({old[(size_t)cl[(size_t)e]], vl[(size_t)e]});
+    for (int64_t e = rp[(size_t)r]; e < rp[(size_t)r + 1]; ++e) rows[(size_t)old[(size_t)r]].push_back({old[(size_t)cl[(size_t)e]], vl[(size_t)e]});
   int64_t k = 0;
   if (rowp) rowp[0] = 0;
   for (int64_t i = 0; i < n; ++i) {
@@ -5313,7 +5337,12 @@ extern "C" int gls_ilu_factors(gls_ctx *c, int32_t *perm, int32_t *rowp, int32_t
   GLS_TRY(ensure_ilu(c));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (perm) HIP_TRY(hipMemcpy(perm, I.perm.p, sizeof(int32_t) * (size_t)c->n_dofs, hipMemcpyDeviceToHost));
-  if (rowp) HIP_TRY(hipMemcpy(rowp, I.rowp.p, sizeof(int32_t) * (size_t)(c->n_dofs + 1), hipMemcpyDeviceToHost));
+  if (I.nnz >= INT32_MAX) return set_err(GLS_EINVAL, "gls_ilu_factors: %lld entries do not fit its 32-bit CSR", (long long)I.nnz);
+  if (rowp) {
+    std::vector<int64_t> rp((size_t)c->n_dofs + 1);
+    HIP_TRY(hipMemcpy(rp.data(), I.rowp.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < rp.size(); ++i) rowp[i] = (int32_t)rp[i];
+  }
   if (col) HIP_TRY(hipMemcpy(col, I.col.p, sizeof(int32_t) * (size_t)I.nnz, hipMemcpyDeviceToHost));
   if (val) HIP_TRY(hipMemcpy(val, I.val.p, sizeof(double) * (size_t)I.nnz, hipMemcpyDeviceToHost));
   return GLS_OK;

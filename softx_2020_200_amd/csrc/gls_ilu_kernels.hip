@@ -40,11 +40,11 @@ __device__ __forceinline__ double pick4(const double *a, int j) {
 // upper: x_i = (y_i - sum_{j > i} U_ij x_j) / U_ii; entries [sp_i, rowp_{i+1}) lie in later colors,
 //        (didx_i, sp_i) in the row's own node (sp = usp).
 // In both, the gathered vector is the output (x / y of the other colors, already final).
-// Each node group's row extents come from one 96-byte descriptor (kGroupDesc ints, built at attach:
+// Each node group's row extents come from one 192-byte descriptor (kGroupDesc int64, built at attach:
 // r0, nr, entry range, row boundaries, lsp, usp, didx, row ends), so the first dependent load round
 // of a launch is the descriptor itself rather than grow -> rowp / lsp / usp / didx.
 template <int WPG, bool LOWER>
-__global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdesc, int g0, int g1,
+__global__ void __launch_bounds__(256) k_mc_tri(const int64_t *__restrict__ gdesc, int g0, int g1,
                                                 const int32_t *__restrict__ col, const double *__restrict__ val,
                                                 const double *__restrict__ rhs, double *__restrict__ out) {
   constexpr int GPB = 4 / WPG;  // node groups per 256-thread block
@@ -53,20 +53,19 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdes
   const int g = g0 + (int)blockIdx.x * GPB + gl;
   const bool live = g < g1;
   __shared__ double red[4][kMaxGroupRows];
-  int32_t dsc[kGroupDesc];
+  int64_t dsc[kGroupDesc];
   {
-    const int4 *d4 = reinterpret_cast<const int4 *>(gdesc + (int64_t)(live ? g : g0) * kGroupDesc);
+    typedef long long ll2 __attribute__((ext_vector_type(2)));
+    const ll2 *d2 = reinterpret_cast<const ll2 *>(gdesc + (int64_t)(live ? g : g0) * kGroupDesc);
 #pragma unroll
-    for (int k = 0; k < kGroupDesc / 4; ++k) {
-      const int4 q = d4[k];
-      dsc[4 * k] = q.x;
-      dsc[4 * k + 1] = q.y;
-      dsc[4 * k + 2] = q.z;
-      dsc[4 * k + 3] = q.w;
+    for (int k = 0; k < kGroupDesc / 2; ++k) {
+      const ll2 q = d2[k];
+      dsc[2 * k] = q.x;
+      dsc[2 * k + 1] = q.y;
     }
   }
-  const int r0 = dsc[0], nr = live ? dsc[1] : 0;
-  int32_t bnd[kMaxGroupRows], lo[kMaxGroupRows], hi[kMaxGroupRows], dix[kMaxGroupRows];
+  const int r0 = (int)dsc[0], nr = live ? (int)dsc[1] : 0;
+  int64_t bnd[kMaxGroupRows], lo[kMaxGroupRows], hi[kMaxGroupRows], dix[kMaxGroupRows];
 #pragma unroll
   for (int t = 0; t < kMaxGroupRows; ++t) {
     const bool in = t < nr;
@@ -84,8 +83,8 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdes
     for (int t = 0; t < kMaxGroupRows; ++t) {
       const int i = r0 + t;
       const bool in = t < nr;
-      const int d = in ? dix[t] : 0;
-      const int ob = !in ? 0 : LOWER ? dsc[8 + t] : d + 1, oe = !in ? 0 : LOWER ? d : dsc[12 + t];
+      const int64_t d = in ? dix[t] : 0;
+      const int64_t ob = !in ? 0 : LOWER ? dsc[8 + t] : d + 1, oe = !in ? 0 : LOWER ? d : dsc[12 + t];
       rb[t] = in ? rhs[i] : 0.0;
       if (!LOWER) dg[t] = in ? val[d] : 1.0;
 #pragma unroll
@@ -99,7 +98,8 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdes
   // other-color gather-dot over the rows' segments [lo_t, hi_t) concatenated (virtual index v:
   // row t = number of segment prefix sums <= v), so no lane walks entries of the other triangle
   double acc[kMaxGroupRows] = {0.0, 0.0, 0.0, 0.0};
-  const int P1 = hi[0] - lo[0], P2 = P1 + hi[1] - lo[1], P3 = P2 + hi[2] - lo[2], tot = P3 + hi[3] - lo[3];
+  const int P1 = (int)(hi[0] - lo[0]), P2 = P1 + (int)(hi[1] - lo[1]), P3 = P2 + (int)(hi[2] - lo[2]),
+            tot = P3 + (int)(hi[3] - lo[3]);
   for (int v0 = tig; v0 < tot; v0 += 64 * WPG * kGatherUnroll) {
     int c[kGatherUnroll], tt[kGatherUnroll];
     double v[kGatherUnroll], xv[kGatherUnroll];
@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) k_mc_tri(const int32_t *__restrict__ gdes
     for (int u = 0; u < kGatherUnroll; ++u) {
       const int vi = v0 + 64 * WPG * u;
       const int t = (vi >= P1) + (vi >= P2) + (vi >= P3);
-      const int e = vi + (t == 0 ? lo[0] : t == 1 ? lo[1] - P1 : t == 2 ? lo[2] - P2 : lo[3] - P3);
+      const int64_t e = vi + (t == 0 ? lo[0] : t == 1 ? lo[1] - P1 : t == 2 ? lo[2] - P2 : lo[3] - P3);
       const bool ok = vi < tot;
       tt[u] = ok ? t : -1;
       c[u] = ok ? col[e] : 0;
@@ -190,22 +190,25 @@ __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_
 constexpr uint16_t kMapMiss = 0xffff;
 template <bool MAP, int NS>
 __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *__restrict__ grow, int g0, int g1,
-                                                                const int32_t *__restrict__ rowp,
+                                                                const int64_t *__restrict__ rowp,
                                                                 const int32_t *__restrict__ col, double *__restrict__ val,
-                                                                const int32_t *__restrict__ lsp,
-                                                                const int32_t *__restrict__ didx, double boost_tol,
+                                                                const int64_t *__restrict__ lsp,
+                                                                const int64_t *__restrict__ didx, double boost_tol,
                                                                 double boost_val, const int64_t *__restrict__ moff,
                                                                 const uint16_t *__restrict__ map) {
   __shared__ int32_t sc[kMaxGroupRows][kIluMaxRow + 1];
   __shared__ double sv[kMaxGroupRows][kIluMaxRow + 1];  // + a dummy slot for the MAP step's idle lanes
-  __shared__ int32_t sdk[kMaxGroupRows][kIluMaxRow], se1[kMaxGroupRows][kIluMaxRow];  // pivot-row extents
+  // pivot-row extents: the diagonal's position and the upper part's length
+  __shared__ int64_t sdk[kMaxGroupRows][kIluMaxRow];
+  __shared__ int32_t sul[kMaxGroupRows][kIluMaxRow];
   __shared__ int32_t smo[MAP ? kMaxGroupRows : 1][MAP ? kIluMaxRow : 1];  // per pivot: map offset in the row
   const int g = g0 + (int)blockIdx.x;
   if (g >= g1) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r0 = grow[g], nr = grow[g + 1] - r0;
   const int i = r0 + w;
-  const int rp = w < nr ? rowp[i] : 0, len = w < nr ? rowp[i + 1] - rp : 0;
+  const int64_t rp = w < nr ? rowp[i] : 0;
+  const int len = w < nr ? (int)(rowp[i + 1] - rp) : 0;
   for (int e = lane; e < len; e += 64) {
     sc[w][e] = col[rp + e];
     sv[w][e] = val[rp + e];
@@ -223,17 +226,18 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
   // updates. (An LDS hash of the row's columns measured slower, 47 vs 23 ms: most lookups miss.)
   if (w < nr) {
     constexpr int PF = kIluPrefetch;  // upper entries per lane held in registers (64 * PF per pivot row)
-    const int nl = lsp[i] - rp;
+    const int nl = (int)(lsp[i] - rp);
     int mrun = 0;  // MAP: running offset of the pivot's map segment in the row's
     for (int p0 = 0; p0 < nl; p0 += 64) {
       const int p = p0 + lane;
       int m = 0;
       if (p < nl) {
         const int k = sc[w][p];
-        const int dk = didx[k], e1 = rowp[k + 1];
+        const int64_t dk = didx[k];
+        const int ul = (int)(rowp[k + 1] - dk - 1);
         sdk[w][p] = dk;
-        se1[w][p] = e1;
-        m = MAP ? (e1 - dk - 1 + 3) & ~3 : e1 - dk - 1;  // MAP segments are padded to quads
+        sul[w][p] = ul;
+        m = MAP ? (ul + 3) & ~3 : ul;  // MAP segments are padded to quads
       }
       if (MAP) {  // exclusive prefix sum of the upper-entry counts over the wave
         int x = m;
@@ -251,7 +255,8 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     const int64_t mbase = MAP ? moff[i] : 0;
     struct Stage {
       double piv, v[PF];
-      int c[PF], dk, e1, mo;  // c: the upper entries' columns
+      int64_t dk, e1;
+      int c[PF], mo;  // c: the upper entries' columns
       uint64_t mq;            // MAP: the row positions of the lane's quad, 4 x 16 bit (unpacked only
                               // when used: touching a register still in flight waits for its load)
     } S[NS];
@@ -260,7 +265,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     auto issue = [&](int p, Stage &st) {
       const bool in = p < nl;
       st.dk = in ? sdk[w][p] : rp;
-      st.e1 = in ? se1[w][p] : rp;
+      st.e1 = in ? st.dk + 1 + sul[w][p] : rp;
       st.piv = val[st.dk];
       if (MAP) {  // lane l: the quad of upper entries 4l .. 4l+3 (one 8-byte map load, one address
                   // for the values; past the row's end they are masked in the step, and the value
@@ -275,8 +280,8 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
       }
 #pragma unroll
       for (int t = 0; t < PF; ++t) {
-        const int e = st.dk + 1 + lane + 64 * t;
-        const int ec = e < st.e1 ? e : st.dk;
+        const int64_t e = st.dk + 1 + lane + 64 * t;
+        const int64_t ec = e < st.e1 ? e : st.dk;
         // raw; validity (e < e1) is applied where the stage is used, so no instruction touches these
         // registers before the stage's step
         st.c[t] = col[ec];
@@ -286,7 +291,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     auto step = [&](int p, const Stage &st) {
       const double lik = sv[w][p] / st.piv;
       if (MAP) {  // branchless: all four reads, then all four writes (idle lanes on the dummy slot)
-        const int m = st.e1 - st.dk - 1;
+        const int m = (int)(st.e1 - st.dk - 1);
         int qa[PF];
         double r[PF];
 #pragma unroll
@@ -328,7 +333,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
           }
         }
       }
-      for (int e = st.dk + 1 + lane + 64 * PF; e < st.e1; e += 64) {  // longer pivot rows: the rest directly
+      for (int64_t e = st.dk + 1 + lane + 64 * PF; e < st.e1; e += 64) {  // longer pivot rows: the rest directly
         const int q = lds_find(sc[w], p + 1, len, col[e]);
         if (q >= 0) sv[w][q] -= lik * val[e];
       }
@@ -354,10 +359,10 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
   // phase 2: the own-node pivots (entries [lsp_i, didx_i): rows r0 .. i-1 of this group), row by row
   for (int t = 0; t < nr; ++t) {
     if (w == t) {
-      const int pd = didx[i] - rp;
-      for (int p = lsp[i] - rp; p < pd; ++p) {
+      const int pd = (int)(didx[i] - rp);
+      for (int p = (int)(lsp[i] - rp); p < pd; ++p) {
         const int tk = sc[w][p] - r0;  // own-node row, final (phase 2 of row tk done, pivot boosted)
-        const int lk = rowp[r0 + tk + 1] - rowp[r0 + tk], dpk = didx[r0 + tk] - rowp[r0 + tk];
+        const int lk = (int)(rowp[r0 + tk + 1] - rowp[r0 + tk]), dpk = (int)(didx[r0 + tk] - rowp[r0 + tk]);
         const double lik = sv[w][p] / sv[tk][dpk];
         for (int e = dpk + 1 + lane; e < lk; e += 64) {
           const int q = lds_find(sc[w], p + 1, len, sc[tk][e]);
@@ -377,15 +382,16 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
 // the MAP positions: one wavefront per row, its columns staged in LDS; for every pivot k_p (entries
 // [rowp_i, lsp_i)) and every upper entry of row k_p, the position of that column in row i (> p) or
 // kMapMiss. Segments follow the pivots in order from moff[i].
-__global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int32_t *__restrict__ rowp,
-                                                     const int32_t *__restrict__ col, const int32_t *__restrict__ lsp,
-                                                     const int32_t *__restrict__ didx,
+__global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int64_t *__restrict__ rowp,
+                                                     const int32_t *__restrict__ col, const int64_t *__restrict__ lsp,
+                                                     const int64_t *__restrict__ didx,
                                                      const int64_t *__restrict__ moff, uint16_t *__restrict__ map) {
   __shared__ int32_t sc[4][kIluMaxRow + 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 4 + w;
   if (i >= n) return;
-  const int rp = rowp[i], len = rowp[i + 1] - rp, nl = lsp[i] - rp;
+  const int64_t rp = rowp[i];
+  const int len = (int)(rowp[i + 1] - rp), nl = (int)(lsp[i] - rp);
   for (int e = lane; e < len; e += 64) sc[w][e] = col[rp + e];
   if (lane == 0) sc[w][len] = 0x7fffffff;
   __builtin_amdgcn_wave_barrier();
@@ -393,7 +399,8 @@ __global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int32_t *_
   int64_t o = moff[i];
   for (int p = 0; p < nl; ++p) {
     const int k = sc[w][p];
-    const int dk = didx[k], m = rowp[k + 1] - dk - 1, mp = (m + 3) & ~3;  // segments padded to quads
+    const int64_t dk = didx[k];
+    const int m = (int)(rowp[k + 1] - dk - 1), mp = (m + 3) & ~3;  // segments padded to quads
     for (int e = lane; e < mp; e += 64) {
       const int q = e < m ? lds_find(sc[w], p + 1, len, col[dk + 1 + e]) : -1;
       map[o + e] = q >= 0 ? (uint16_t)q : kMapMiss;
@@ -403,15 +410,15 @@ __global__ void __launch_bounds__(256) k_mc_ilu0_map(int64_t n, const int32_t *_
 }
 }  // namespace
 
-hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col, const int32_t *lsp,
-                             const int32_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s) {
+hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col, const int64_t *lsp,
+                             const int64_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_mc_ilu0_map, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, n, rowp, col, lsp, didx, moff, map);
   return hipGetLastError();
 }
 
-hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
-                         const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
+hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
+                         const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
                          double boost_val, const int64_t *moff, const uint16_t *map, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
@@ -427,7 +434,7 @@ hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n
   return hipGetLastError();
 }
 
-hipError_t ilu_mc_solve(const int32_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
                         const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
                         const uint8_t *waves_upper, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {

@@ -100,18 +100,18 @@ hipError_t vec_gather_scale_set(double *y, const double *d, const double *v, con
 // assembled-ILU helpers: x[idx] = a; val[ent] = y[row] (probe extraction; add: val[ent] += y[row]);
 // a_ii <- r a_ii + sign(a_ii) t
 hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s);
-hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
+hipError_t csr_probe_extract(double *val, const int64_t *ent, const int32_t *row, int64_t m, const double *y,
                              hipStream_t s, bool add = false);
 // dense column-major A (n x n, A[j * n + i] = A_ij, DoF numbering) from the ILU's probed CSR (rows / columns
 // in its renumbered order, perm: DoF -> row); inv (n ints, scratch) receives row -> DoF. A is not zeroed here
-hipError_t csr_to_dense(double *A, const int32_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
+hipError_t csr_to_dense(double *A, const int64_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
                         const int32_t *inv, int64_t n, hipStream_t s);
 hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_t n, int dir, hipStream_t s);
 // batched probing of the per-cell operator (nb probe vectors at stride bs / ys, element vectors at evs;
 // pid[e] = probe of entry e, p0 = the batch's first probe)
 hipError_t probe_set_batched(double *V, int64_t n, const int32_t *dofs, const int32_t *pid, int p0, int64_t m,
                              hipStream_t s);
-hipError_t probe_extract_batched(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+hipError_t probe_extract_batched(double *val, const int64_t *ent, const int32_t *row, const int32_t *pid, int p0,
                                  int64_t m, const double *Y, int64_t n, hipStream_t s);
 hipError_t vec_csr_gather_set_b(double *x, const int64_t *dof, const int64_t *off, const int64_t *master,
                                 const double *w, int64_t n, int nb, int64_t bs, hipStream_t s);
@@ -127,16 +127,16 @@ hipError_t gather_element_vectors_b(double *y, const double *ev, const int64_t *
 constexpr int kMaxGroupRows = 4;
 // multicolor ILU numeric factorization in place (same structures; rows of <= kIluMaxRow entries)
 constexpr int kIluMaxRow = 640;
-hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int32_t *rowp,
-                         const int32_t *col, double *val, const int32_t *lsp, const int32_t *didx, double boost_tol,
+hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
+                         const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
                          double boost_val, const int64_t *moff, const uint16_t *map, hipStream_t s);
 // the factorization's row-position map (map == nullptr in ilu_mc_factor: column searches instead)
-hipError_t ilu_mc_factor_map(int64_t n, const int32_t *rowp, const int32_t *col, const int32_t *lsp,
-                             const int32_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s);
-// per node group: r0, nr, rowp[r0], rowp[r0 + nr], rowp[r0 + 1..3] (INT32_MAX past nr), 0, lsp[4], usp[4],
-// didx[4], rowp[r0 + 1..4] (the solves' group descriptor)
+hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col, const int64_t *lsp,
+                             const int64_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s);
+// per node group (int64): r0, nr, rowp[r0], rowp[r0 + nr], rowp[r0 + 1..3] (INT64_MAX past nr), 0, lsp[4],
+// usp[4], didx[4], rowp[r0 + 1..4] (the solves' group descriptor)
 constexpr int kGroupDesc = 24;
-hipError_t ilu_mc_solve(const int32_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
                         const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
                         const uint8_t *waves_upper, hipStream_t s);
 hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
@@ -145,7 +145,11 @@ hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off,
                                 const double *buf, hipStream_t s);
 hipError_t vec_add_nodes_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,
                                  int64_t voff, const double *buf, hipStream_t s);  // 4 values per node slot
-hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh, hipStream_t s);
+hipError_t csr_diag_perturb(double *val, const int64_t *didx, int64_t n, double athresh, double rthresh, hipStream_t s);
+hipError_t vec_set_const_indexed64(double *x, const int64_t *idx, int64_t m, double a, hipStream_t s);
+// x[u[i]] += sum of buf[slot[j]] over j in [off[i], off[i+1]) in order (u: 64-bit positions, the ILU's remote entries)
+hipError_t vec_add_pos_ordered(double *x, const int64_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                               const double *buf, hipStream_t s);
 hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, int64_t m, hipStream_t s);  // y[idx]=vals (vals null -> 0)
 int multidot_work_size();
 

@@ -22,12 +22,29 @@
 
 namespace gls {
 
-int iluk_pattern(int64_t n, const int32_t *rowp, const int32_t *col, int fill, std::vector<int32_t> &orow,
+template <typename RP>
+int iluk_pattern(int64_t n, const RP *rowp, const int32_t *col, int fill, std::vector<RP> &orow,
                  std::vector<int32_t> &ocol, std::vector<int32_t> *olev) {
   if (n < 0 || fill < 0 || !rowp || (n > 0 && !col)) return GLS_EINVAL;
   orow.assign((size_t)n + 1, 0);
   ocol.clear();
   if (olev) olev->clear();
+  if (fill == 0) {  // ILU(0): the graph itself (rows sorted, the diagonal added); no U lists kept
+    ocol.reserve((size_t)rowp[n] + (size_t)n);
+    std::vector<int32_t> row;
+    for (int64_t i = 0; i < n; ++i) {
+      row.assign(col + rowp[i], col + rowp[i + 1]);
+      row.push_back((int32_t)i);
+      std::sort(row.begin(), row.end());
+      row.erase(std::unique(row.begin(), row.end()), row.end());
+      if (row.front() < 0 || row.back() >= n) return GLS_EINVAL;
+      ocol.insert(ocol.end(), row.begin(), row.end());
+      if (olev) olev->insert(olev->end(), row.size(), 0);
+      if (sizeof(RP) < 8 && ocol.size() > (size_t)INT32_MAX) return GLS_ENOMEM;
+      orow[(size_t)i + 1] = (RP)ocol.size();
+    }
+    return GLS_OK;
+  }
   // U part (col > row) of every finished row with its levels: (ucol, ulev)[uoff[k] .. uoff[k+1])
   std::vector<int64_t> uoff((size_t)n + 1, 0);
   std::vector<int32_t> ucol, ulev;
@@ -78,12 +95,16 @@ int iluk_pattern(int64_t n, const int32_t *rowp, const int32_t *col, int fill, s
         ulev.push_back(lev[(size_t)c]);
       }
     }
-    if (ocol.size() > (size_t)INT32_MAX) return GLS_ENOMEM;
-    orow[(size_t)i + 1] = (int32_t)ocol.size();
+    if (sizeof(RP) < 8 && ocol.size() > (size_t)INT32_MAX) return GLS_ENOMEM;
+    orow[(size_t)i + 1] = (RP)ocol.size();
     uoff[(size_t)i + 1] = (int64_t)ucol.size();
   }
   return GLS_OK;
 }
+template int iluk_pattern<int32_t>(int64_t, const int32_t *, const int32_t *, int, std::vector<int32_t> &,
+                                   std::vector<int32_t> &, std::vector<int32_t> *);
+template int iluk_pattern<int64_t>(int64_t, const int64_t *, const int32_t *, int, std::vector<int64_t> &,
+                                   std::vector<int32_t> &, std::vector<int32_t> *);
 
 void cuthill_mckee_nodes(int64_t nnodes, const std::vector<int64_t> &adj_off, const std::vector<int64_t> &adj,
                          const std::vector<int64_t> &dof_off, const std::vector<int64_t> &dofs,

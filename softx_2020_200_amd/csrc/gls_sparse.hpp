@@ -6,7 +6,9 @@
 namespace gls {
 // Ifpack ILU(k) level-of-fill pattern of the CSR graph (rowp, col) of an n x n matrix; the diagonal is
 // always included. Output rows sorted; olev (optional) holds each entry's level.
-int iluk_pattern(int64_t n, const int32_t *rowp, const int32_t *col, int fill, std::vector<int32_t> &orow,
+// RP: the row-pointer / entry-position type (int32_t, or int64_t for matrices past 2^31 entries).
+template <typename RP>
+int iluk_pattern(int64_t n, const RP *rowp, const int32_t *col, int fill, std::vector<RP> &orow,
                  std::vector<int32_t> &ocol, std::vector<int32_t> *olev = nullptr);
 // deal.II Cuthill-McKee on a node graph (adj: a node's row nodes, itself included) whose nodes own
 // the consecutive DoFs dofs[dof_off[x] .. dof_off[x+1]); order[new index] = DoF

@@ -735,9 +735,19 @@ hipError_t vec_set_indexed(double *y, const int64_t *idx, const double *vals, in
 // ---- assembled-ILU preconditioner helpers (gls_api.cpp ilu_*): probe vectors and value extraction
 namespace gls {
 namespace {
-__global__ void k_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a) {
+template <typename I>
+__global__ void k_set_const_indexed(double *x, const I *idx, int64_t m, double a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < m) x[idx[i]] = a;
+}
+// the ILU's remote entries (64-bit positions): x[u[i]] += buf[slot[j]], j in [off[i], off[i+1]) in order
+__global__ void k_add_pos_ordered(double *__restrict__ x, const int64_t *__restrict__ u, const int32_t *__restrict__ off,
+                                  const int32_t *__restrict__ slot, int64_t n, const double *__restrict__ buf) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    double s = x[u[i]];
+    for (int j = off[i]; j < off[i + 1]; ++j) s += buf[slot[j]];
+    x[u[i]] = s;
+  }
 }
 // batched probes p0 .. : V[(pid[e] - p0) * n + dofs[e]] = 1 (V zeroed) and the extraction
 // val[ent[e]] = Y[(pid[e] - p0) * n + row[e]]
@@ -745,19 +755,19 @@ __global__ void k_probe_set_b(double *V, int64_t n, const int32_t *dofs, const i
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < m) V[(int64_t)(pid[e] - p0) * n + dofs[e]] = 1.0;
 }
-__global__ void k_probe_extract_b(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+__global__ void k_probe_extract_b(double *val, const int64_t *ent, const int32_t *row, const int32_t *pid, int p0,
                                   int64_t m, const double *Y, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e < m) val[ent[e]] = Y[(int64_t)(pid[e] - p0) * n + row[e]];
 }
 // CSR values of the entries whose column belongs to one probe: val[ent[i]] = y[row[i]]
-__global__ void k_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
+__global__ void k_probe_extract(double *val, const int64_t *ent, const int32_t *row, int64_t m, const double *y,
                                 int add) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < m) val[ent[i]] = add ? val[ent[i]] + y[row[i]] : y[row[i]];
 }
 // Ifpack-style diagonal perturbation before the factorisation: a_ii <- rthresh a_ii + sign(a_ii) athresh
-__global__ void k_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh) {
+__global__ void k_diag_perturb(double *val, const int64_t *didx, int64_t n, double athresh, double rthresh) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double a = val[didx[i]];
@@ -766,12 +776,12 @@ __global__ void k_diag_perturb(double *val, const int32_t *didx, int64_t n, doub
 // out[idx[i]] = in[i] (scatter, dir 0) or out[i] = in[idx[i]] (gather, dir 1)
 // dense column-major A (A[j * n + i] = A_ij in DoF numbering) from a CSR in a renumbered order (perm: DoF -> CSR
 // row, inv: CSR row -> DoF); positions outside the pattern are left as they are (the caller zeroes A)
-__global__ void k_csr_to_dense(double *__restrict__ A, const int32_t *__restrict__ rowp, const int32_t *__restrict__ col,
+__global__ void k_csr_to_dense(double *__restrict__ A, const int64_t *__restrict__ rowp, const int32_t *__restrict__ col,
                                const double *__restrict__ val, const int32_t *__restrict__ perm,
                                const int32_t *__restrict__ inv, int64_t n) {
   for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < n; d += (int64_t)gridDim.x * blockDim.x) {
     const int r = perm[d];
-    for (int e = rowp[r]; e < rowp[r + 1]; ++e) A[(int64_t)inv[col[e]] * n + d] = val[e];
+    for (int64_t e = rowp[r]; e < rowp[r + 1]; ++e) A[(int64_t)inv[col[e]] * n + d] = val[e];
   }
 }
 __global__ void k_invert_perm(int32_t *__restrict__ inv, const int32_t *__restrict__ perm, int64_t n) {
@@ -785,7 +795,7 @@ __global__ void k_permute(double *out, const double *in, const int32_t *idx, int
   else out[i] = in[idx[i]];
 }
 }  // namespace
-hipError_t csr_to_dense(double *A, const int32_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
+hipError_t csr_to_dense(double *A, const int64_t *rowp, const int32_t *col, const double *val, const int32_t *perm,
                         const int32_t *inv, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_invert_perm, dim3(grid_for(n)), dim3(kBlock), 0, s, const_cast<int32_t *>(inv), perm, n);
   hipLaunchKernelGGL(k_csr_to_dense, dim3(grid_for(n)), dim3(kBlock), 0, s, A, rowp, col, val, perm, inv, n);
@@ -798,7 +808,18 @@ hipError_t vec_permute(double *out, const double *in, const int32_t *idx, int64_
 }
 hipError_t vec_set_const_indexed(double *x, const int32_t *idx, int64_t m, double a, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_set_const_indexed, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, x, idx, m, a);
+  hipLaunchKernelGGL(k_set_const_indexed<int32_t>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, x, idx, m, a);
+  return hipGetLastError();
+}
+hipError_t vec_set_const_indexed64(double *x, const int64_t *idx, int64_t m, double a, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_const_indexed<int64_t>, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, x, idx, m, a);
+  return hipGetLastError();
+}
+hipError_t vec_add_pos_ordered(double *x, const int64_t *u, const int32_t *off, const int32_t *slot, int64_t n,
+                               const double *buf, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_add_pos_ordered, dim3(grid_for(n)), dim3(kBlock), 0, s, x, u, off, slot, n, buf);
   return hipGetLastError();
 }
 hipError_t probe_set_batched(double *V, int64_t n, const int32_t *dofs, const int32_t *pid, int p0, int64_t m,
@@ -807,7 +828,7 @@ hipError_t probe_set_batched(double *V, int64_t n, const int32_t *dofs, const in
   hipLaunchKernelGGL(k_probe_set_b, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, V, n, dofs, pid, p0, m);
   return hipGetLastError();
 }
-hipError_t probe_extract_batched(double *val, const int32_t *ent, const int32_t *row, const int32_t *pid, int p0,
+hipError_t probe_extract_batched(double *val, const int64_t *ent, const int32_t *row, const int32_t *pid, int p0,
                                  int64_t m, const double *Y, int64_t n, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_probe_extract_b, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, pid, p0, m, Y, n);
@@ -840,14 +861,14 @@ hipError_t gather_element_vectors_b(double *y, const double *ev, const int64_t *
                      pslot, np, dim, ys, evs, act, el, cb, nblk);
   return hipGetLastError();
 }
-hipError_t csr_probe_extract(double *val, const int32_t *ent, const int32_t *row, int64_t m, const double *y,
+hipError_t csr_probe_extract(double *val, const int64_t *ent, const int32_t *row, int64_t m, const double *y,
                              hipStream_t s, bool add) {
   if (m <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_probe_extract, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, val, ent, row, m, y,
                      add ? 1 : 0);
   return hipGetLastError();
 }
-hipError_t csr_diag_perturb(double *val, const int32_t *didx, int64_t n, double athresh, double rthresh,
+hipError_t csr_diag_perturb(double *val, const int64_t *didx, int64_t n, double athresh, double rthresh,
                             hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_diag_perturb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, val, didx, n, athresh, rthresh);

@@ -50,6 +50,24 @@ int main(int argc, char **argv) {
                 n, ms(t0, t1), ms(t1, t2), ms(t3, t4), ms(t5, t6), ms(t6, t7), 2.0 * n * n * (double)n / ms(t6, t7) / 1e9,
                 ms(t7, t8));
   }
+  // the unpivoted factor applied by two rocBLAS triangular solves (1 RHS), and the triangular inverses
+  for (int rep = 0; rep < 2; ++rep) {
+    CK(hipMemcpy(dA, A.data(), sizeof(double) * n * n, hipMemcpyHostToDevice));
+    CK(rocsolver_dgetrf_npvt(h, n, n, dA, n, info));
+    CK(hipMemcpy(dB, A.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    auto t0 = now();
+    CK(rocblas_dtrsv(h, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_unit, n, dA, n, dB, 1));
+    CK(rocblas_dtrsv(h, rocblas_fill_upper, rocblas_operation_none, rocblas_diagonal_non_unit, n, dA, n, dB, 1));
+    auto t1 = now();
+    CK(hipMemcpy(dC, dA, sizeof(double) * n * n, hipMemcpyDeviceToDevice));
+    auto t2 = now();
+    CK(rocsolver_dtrtri(h, rocblas_fill_upper, rocblas_diagonal_non_unit, n, dC, n, info));
+    auto t3 = now();
+    CK(rocsolver_dtrtri(h, rocblas_fill_lower, rocblas_diagonal_unit, n, dC, n, info));
+    auto t4 = now();
+    std::printf("n=%d dtrsv L+U (1 rhs) %.3f ms, dtrtri upper %.2f ms, dtrtri lower %.2f ms\n", n, ms(t0, t1), ms(t2, t3),
+                ms(t3, t4));
+  }
   std::vector<float> Af(A.begin(), A.end());
   float *fA, *fB;
   CK(hipMalloc(&fA, sizeof(float) * n * n));
@@ -62,8 +80,15 @@ int main(int argc, char **argv) {
     auto t1 = now();
     CK(rocsolver_sgetrs(h, rocblas_operation_none, n, 1, fA, n, ipiv, fB, n));
     auto t2 = now();
-    std::printf("n=%d sgetrf %.2f ms (%.1f TF) sgetrs(1 rhs) %.3f ms\n", n, ms(t0, t1),
-                2.0 / 3.0 * n * (double)n * n / ms(t0, t1) / 1e9, ms(t1, t2));
+    CK(hipMemcpy(fA, Af.data(), sizeof(float) * n * n, hipMemcpyHostToDevice));
+    auto t3 = now();
+    CK(rocsolver_sgetrf_npvt(h, n, n, fA, n, info));
+    auto t4 = now();
+    CK(rocblas_strsv(h, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_unit, n, fA, n, fB, 1));
+    CK(rocblas_strsv(h, rocblas_fill_upper, rocblas_operation_none, rocblas_diagonal_non_unit, n, fA, n, fB, 1));
+    auto t5 = now();
+    std::printf("n=%d sgetrf %.2f ms (%.1f TF) sgetrs(1 rhs) %.3f ms sgetrf_npvt %.2f ms strsv L+U %.3f ms\n", n,
+                ms(t0, t1), 2.0 / 3.0 * n * (double)n * n / ms(t0, t1) / 1e9, ms(t1, t2), ms(t3, t4), ms(t4, t5));
   }
   return 0;
 }
