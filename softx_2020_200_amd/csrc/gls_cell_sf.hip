@@ -177,7 +177,12 @@ __global__ void __launch_bounds__(64) k_cell_sf_jv(const OpParams P, const Table
   }
   const int n_run = P.cell_list ? P.cell_list_n : P.n_cells;
   const int nblk = (n_run + kSfCells - 1) / kSfCells;
-  const int blk = xcd_swizzle((int)blockIdx.x, nblk);  // XCD-aware: neighbouring cells share an L2
+  // batched ILU probing from the recorded work list: block = one (probe vector, 2-cell batch) pair known active
+  const bool listed = P.work != nullptr;
+  const int wb = xcd_swizzle((int)blockIdx.x, listed ? P.n_work : nblk);  // XCD-aware: neighbouring cells share an L2
+  const int blk = listed ? P.work[2 * wb + 1] : wb;
+  const double *Pv = listed ? P.v + (int64_t)P.work[2 * wb] * P.bv_stride : P.v;
+  double *Pev = listed ? P.ev + (int64_t)P.work[2 * wb] * P.bev_stride : P.ev;
   const int cl = lane / 27, id = lane % 27;
   const int crun = blk * kSfCells + cl;
   const bool act = cl < kSfCells && crun < n_run;
@@ -192,12 +197,12 @@ __global__ void __launch_bounds__(64) k_cell_sf_jv(const OpParams P, const Table
   if (act) {
     const int node = P.cell_vnodes[cell * NV + id];
     const unsigned m = P.vmask ? P.vmask[node] : 0u;
-    const double *pv = P.v + (int64_t)node * 3;
+    const double *pv = Pv + (int64_t)node * 3;
 #pragma unroll
     for (int c = 0; c < 3; ++c) V3[c][id] = ((m >> c) & 1u) ? 0.0 : pv[c];
     if (id < NP) {
       const int pn = P.cell_pnodes ? P.cell_pnodes[cell * NP + id] : node;
-      V3[3][id] = P.v[voff + pn];
+      V3[3][id] = Pv[voff + pn];
     }
   }
   wave_sync();
@@ -390,7 +395,7 @@ __global__ void __launch_bounds__(64) k_cell_sf_jv(const OpParams P, const Table
       const double *Y = R2 + 2 * f * 27 + b;
       out[f] = v0 * Y[0] + v1 * Y[1] + v2 * Y[2] + d0 * Y[27] + d1 * Y[28] + d2 * Y[29];
     }
-    double *e = P.ev + cell * (NV * 3 + NP);
+    double *e = Pev + cell * (NV * 3 + NP);
 #pragma unroll
     for (int c = 0; c < 3; ++c) e[id * 3 + c] = out[c];
     if constexpr (PSF) e[NV * 3 + id] = out[3];
@@ -578,9 +583,22 @@ bool cell_sf_enabled() { return cell_sf_mode() != 0; }
 // launch is not the sum-factorized kernel's (2D, other degrees, probing batches, no cache, atomics)
 hipError_t launch_cell_sf_jv(int dim, int k, int kp, int nq1d, const OpParams &P, const Tables1D &T, hipStream_t s) {
   if (!cell_sf_enabled() || dim != 3 || k != 2 || nq1d != 3 || (kp != 1 && kp != 2)) return hipErrorNotSupported;
-  if (!P.cq || P.cq_mode != 2 || P.bv_stride || P.work || !P.ev || P.oseen) return hipErrorNotSupported;
+  if (!P.cq || P.cq_mode != 2 || (P.bv_stride && !P.work) || !P.ev || P.oseen) return hipErrorNotSupported;
+  if (P.work && P.cell_list) return hipErrorNotSupported;  // probes run over all cells
   const int n_run = P.cell_list ? P.cell_list_n : P.n_cells;
-  if (n_run <= 0) return hipSuccess;
+  if (n_run <= 0 || (P.work && P.n_work <= 0)) return hipSuccess;
+  if (P.work) {  // listed (probe vector, 2-cell batch) blocks: the dense probe kernel's batches of 64 / 27 = 2 cells
+    static_assert(kSfCells == 2, "work-list batches are the 64-thread dense kernel's 2-cell batches");
+    if (cell_sf_mode() == 2) return hipErrorNotSupported;
+    if (kp == 1) {
+      if (P.gq) hipLaunchKernelGGL((k_cell_sf_jv<1, true>), dim3((unsigned)P.n_work), dim3(64), 0, s, P, T);
+      else hipLaunchKernelGGL((k_cell_sf_jv<1, false>), dim3((unsigned)P.n_work), dim3(64), 0, s, P, T);
+    } else {
+      if (P.gq) hipLaunchKernelGGL((k_cell_sf_jv<2, true>), dim3((unsigned)P.n_work), dim3(64), 0, s, P, T);
+      else hipLaunchKernelGGL((k_cell_sf_jv<2, false>), dim3((unsigned)P.n_work), dim3(64), 0, s, P, T);
+    }
+    return hipGetLastError();
+  }
   if (cell_sf_mode() == 2) {
     const unsigned mb = (unsigned)((n_run + kMfCells - 1) / kMfCells);
     if (kp == 1) {

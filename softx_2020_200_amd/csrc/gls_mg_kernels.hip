@@ -501,6 +501,75 @@ hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, 
   return hipGetLastError();
 }
 
+// ---- dense LU solves of the coarsest level (FP32 factor of rocSOLVER getrf_npvt: column-major, lda = n, unit
+// lower L below the diagonal, U on and above it); x overwritten. Block-column steps of kLuB rows: step k has the
+// block k solution final; its workgroup 0 applies that block's column to the rows of the next block and solves the
+// next diagonal block in LDS (one column at a time), the other workgroups apply it to the rows beyond. 2 n / kLuB
+// launches per solve against rocBLAS trsv's 62 ms at n = 25000 (profiles/r06_lu25k.txt).
+constexpr int kLuB = 128;
+namespace {
+template <bool LOWER>
+__device__ __forceinline__ void lu_diag_solve(const float *__restrict__ A, int64_t n, int r0, int nr, float v,
+                                              float *__restrict__ x, float *xb) {
+  const int t = threadIdx.x;
+  if (LOWER) {  // unit diagonal
+    for (int c = 0; c < nr; ++c) {
+      if (t == c) xb[c] = v;
+      __syncthreads();
+      if (t > c && t < nr) v -= A[(r0 + t) + (int64_t)(r0 + c) * n] * xb[c];
+    }
+  } else {
+    for (int c = nr - 1; c >= 0; --c) {
+      if (t == c) xb[c] = v / A[(r0 + c) + (int64_t)(r0 + c) * n];
+      __syncthreads();
+      if (t < c) v -= A[(r0 + t) + (int64_t)(r0 + c) * n] * xb[c];
+    }
+  }
+  __syncthreads();
+  if (t < nr) x[r0 + t] = xb[t];
+}
+// k < 0: the first diagonal block alone (block 0 forward, the last block backward)
+template <bool LOWER>
+__global__ void __launch_bounds__(kLuB) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k) {
+  __shared__ float xk[kLuB], xb[kLuB];
+  const int t = threadIdx.x, nb = (n + kLuB - 1) / kLuB;
+  if (k < 0) {
+    const int kb = LOWER ? 0 : nb - 1, r0 = kb * kLuB, nr = min(kLuB, n - r0);
+    lu_diag_solve<LOWER>(A, n, r0, nr, t < nr ? x[r0 + t] : 0.f, x, xb);
+    return;
+  }
+  const int j0 = k * kLuB, nj = min(kLuB, n - j0);
+  if (t < nj) xk[t] = x[j0 + t];
+  __syncthreads();
+  auto update = [&](int i) {
+    float s = x[i];
+    for (int j = 0; j < nj; ++j) s -= A[i + (int64_t)(j0 + j) * n] * xk[j];
+    return s;
+  };
+  const int kn = LOWER ? k + 1 : k - 1;  // the next diagonal block
+  if (blockIdx.x == 0) {
+    const int r0 = kn * kLuB, nr = min(kLuB, n - r0);
+    lu_diag_solve<LOWER>(A, n, r0, nr, t < nr ? update(r0 + t) : 0.f, x, xb);
+    return;
+  }
+  // rows beyond the next block: after it (forward) or before it (backward)
+  const int i = LOWER ? (k + 2) * kLuB + ((int)blockIdx.x - 1) * kLuB + t : ((int)blockIdx.x - 1) * kLuB + t;
+  if (LOWER ? i < n : i < kn * kLuB) x[i] = update(i);
+}
+}  // namespace
+hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int nb = (n + kLuB - 1) / kLuB;
+  hipLaunchKernelGGL(k_lu_step<true>, dim3(1), dim3(kLuB), 0, s, LU, n, x, -1);
+  for (int k = 0; k + 1 < nb; ++k) {
+    const int rest = n - (k + 2) * kLuB;
+    hipLaunchKernelGGL(k_lu_step<true>, dim3(1 + (rest > 0 ? (rest + kLuB - 1) / kLuB : 0)), dim3(kLuB), 0, s, LU, n, x, k);
+  }
+  hipLaunchKernelGGL(k_lu_step<false>, dim3(1), dim3(kLuB), 0, s, LU, n, x, -1);
+  for (int k = nb - 1; k >= 1; --k) hipLaunchKernelGGL(k_lu_step<false>, dim3(1 + (k - 1)), dim3(kLuB), 0, s, LU, n, x, k);
+  return hipGetLastError();
+}
+
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s) {
   hipLaunchKernelGGL(k_jacobi_update, dim3(grid_for(n)), dim3(256), 0, s, x, b, y, d, omega, n, zero_start);
