@@ -40,6 +40,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+
+
+def cell_jv_kernel_name(kp):
+    """the per-cell J.v kernel a 3D Q2 cell runs (gls_cell_sf.hip: GLS_CELL_SF, read per launch, 1 by default)"""
+    mode = os.environ.get("GLS_CELL_SF", "1")
+    return {"0": "gls_cell_kernel<3,2,%d,3,MODE_JV,GEN> (dense per-cell)" % kp,
+            "2": "k_cell_mfma_jv<%d,GEN> (MFMA per-cell)" % kp}.get(mode, "k_cell_sf_jv<%d,GEN> (sum-factorized per-cell)" % kp)
 PMC_TRAFFIC_FILE = "r04_pmc_traffic_pencil_128.txt"  # tools/pmc_traffic.sh summary of the pencil J.v (fallback)
 LDS_MODEL_FILE = "r05_lds_model.json"                # tools/lds_model.py (static model, source-hash tagged)
 FP64_PEAK_TFS = 78.6        # MI355X FP64 (vector = matrix) spec; measured 61-64 TF (profiles/r01_microbench_fp64.txt)
@@ -384,7 +391,9 @@ def bench_cylinder3d(args):
         nco = levels[-1][0].n_dofs
         ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
                                        coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=args.mg_omega_cyl,
-                                       coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother)
+                                       coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother,
+                                       # the ILU smoothers' solves read FP32 copies of their FP64 factors
+                                       mixed_precision=int(args.mg_precision == "f32" and args.cyl_smoother == "ilu"))
     else:
         ctx, sp, x = make(mesh(refine).fe_space(2, 1, qmapping_all=qall))
         ctx.set_time(scheme, ts)
@@ -453,7 +462,7 @@ def bench_cylinder3d(args):
         "setup_s": t_setup,
         "mdof_per_s": N * its_per_s / 1e6,
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
-        "roofline": {"bound": "hbm", "kernel": "gls_cell_kernel<3,2,1,3,MODE_JV,GEN>", "achieved": B / (ms * 1e-3) / 1e9,
+        "roofline": {"bound": "hbm", "kernel": cell_jv_kernel_name(1), "achieved": B / (ms * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": B, "launch_ms": ms},
     }
@@ -537,7 +546,7 @@ def bench_octree(args):
         "linear_iterations_per_step": float(np.mean([s_["linear_iterations"] for s_ in stats])),
         "forest_bricks": ctx.forest_bricks(),
         "roofline": {"bound": "hbm", "kernel": "gls_pencil_kernel<double,MODE_JVQ> (sibling-group bricks) + "
-                                               "gls_cell_kernel<3,2,2,3,MODE_JV> (other leaves) + k_gather_ev",
+                                               "%s (other leaves) + k_gather_ev" % cell_jv_kernel_name(2),
                      "achieved": B / (ms * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": B, "launch_ms": ms},
@@ -1042,6 +1051,7 @@ def main():
                                         "slab_sum": sl_ms / (1e3 * elapsed_instr)}},
         "roofline": {"bound": "hbm", "kernel": ("gls_pencil_kernel<double,MODE_JVQ> + slab sum" if pencil_jv else
                                                 "gls_brick_kernel<%d,MODE_JVQ> + k_slab_sum" % args.k) if ctx.uses_brick_kernels
+                     else cell_jv_kernel_name(args.kp) if args.k == 2
                      else "gls_cell_kernel<3,%d,%d,%d,MODE_JV>" % (args.k, args.kp, args.k + 1), "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "algorithmic_bytes_per_launch": B_jv, "launch_ms": op_ms,

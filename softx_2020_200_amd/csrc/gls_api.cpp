@@ -390,6 +390,11 @@ struct gls_ctx {
     // color-by-color solves of gls_ilu_kernels.hip replace rocSPARSE csrsv
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
+    bool mc_compact = false;  // ... by the compact-LDS kernel (rows <= kIluCompactRow)
+    // a multigrid smoother's ILU with gls_mg_params.mixed_precision: the color solves read an FP32 copy of the
+    // factors (factored in FP64; 12 -> 8 bytes per entry of the solves' stream)
+    bool solve32 = false;
+    DevBuf<float> val32;
     std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
     DevBuf<int64_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc int64)
     DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
@@ -544,6 +549,45 @@ struct gls_ctx {
     DevBuf<double> probe_bak;  // the probed coarse matrix kept for the pivoted retry of an unpivoted LU
     DevBuf<double> chk;        // coarse_inverse_check's y = A^-1 e and z = A y
     DevBuf<int> status;
+    // the FP32 unpivoted factorization and its check run on a stream of their own, overlapping the finer levels'
+    // ILU setup and first smoothing on the context stream; the first coarse solve waits for them
+    // (coarse_lu32_finish). Declared after the buffers it uses, so it is destroyed (synchronized) first.
+    struct Side {
+      hipStream_t s = nullptr;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      Side() = default;
+      Side(const Side &) = delete;
+      Side &operator=(const Side &) = delete;
+      Side(Side &&o) noexcept : s(o.s), e0(o.e0), e1(o.e1) { o.s = nullptr, o.e0 = o.e1 = nullptr; }
+      Side &operator=(Side &&o) noexcept {
+        if (this != &o) {
+          reset();
+          s = o.s, e0 = o.e0, e1 = o.e1;
+          o.s = nullptr, o.e0 = o.e1 = nullptr;
+        }
+        return *this;
+      }
+      hipError_t ensure() {
+        if (s) return hipSuccess;
+        hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&e0, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+        return e;
+      }
+      void reset() {
+        if (s) {
+          (void)hipStreamSynchronize(s);
+          (void)hipStreamDestroy(s);
+        }
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        s = nullptr, e0 = e1 = nullptr;
+      }
+      ~Side() { reset(); }
+    } side;
+    bool lu_pending = false;  // side-stream factorization in flight, not yet checked
+    int64_t lu_n = 0, lu_pin = 0;
+    DevBuf<double> lu_rel;  // |A x - 1| of the check (device pointer mode)
     // coarsest-level Jacobi sweeps (single rank, fused brick path) replayed as one HIP graph: the
     // ~2×csweeps tiny launches per V-cycle are captured once per state (mg_prepare) and launched
     // as a single graph by every V-cycle of that Newton step
@@ -2332,9 +2376,85 @@ int mg_probe_setup(gls_ctx *c, gls_ctx *g) {
   return GLS_OK;
 }
 
+// the large coarsest level's FP32 factorization (kDirectSmall < n): rocSOLVER sgetrf_npvt of the pinned matrix (138 ms
+// at n = 25000 against sgetrf's 410 + sgetri's ~800) and its check |A x - 1| / |1| on the side stream, ordered after
+// the context stream's probing / rounding; nothing here waits on the host
+int coarse_lu32_start(gls_ctx *c, int64_t n, int64_t pin) {
+  auto &mg = c->mg;
+  HIP_TRY(mg.side.ensure());
+  hipStream_t s = mg.side.s;
+  if (mg.chk32.n != (size_t)(2 * n)) GLS_TRY(mg.chk32.alloc((size_t)(2 * n)));
+  if (mg.lu_rel.n != 1) GLS_TRY(mg.lu_rel.alloc(1));
+  HIP_TRY(hipEventRecord(mg.side.e0, c->stream));
+  HIP_TRY(hipStreamWaitEvent(s, mg.side.e0, 0));
+  const double one = 1.0, mone = -1.0;
+  const bool ok =
+      rocblas_set_stream(mg.blas, s) == rocblas_status_success &&
+      rocsolver_sgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.info.p) ==
+          rocblas_status_success &&
+      gls::vec_fill(mg.chk32.p, n, 1.0, s) == hipSuccess && gls::mg_zero_row(mg.chk32.p, 1, pin, s) == hipSuccess &&
+      gls::vec_to_f32(mg.chk32.p, mg.x32.p, n, s) == hipSuccess &&
+      gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, s) == hipSuccess &&
+      gls::vec_from_f32(mg.x32.p, mg.chk32.p + n, n, s) == hipSuccess &&
+      rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe.p, (rocblas_int)n,
+                    mg.chk32.p + n, 1, &mone, mg.chk32.p, 1) == rocblas_status_success &&
+      rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_device) == rocblas_status_success &&
+      rocblas_dnrm2(mg.blas, (rocblas_int)n, mg.chk32.p, 1, mg.lu_rel.p) == rocblas_status_success;
+  (void)rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
+  (void)rocblas_set_stream(mg.blas, c->stream);
+  if (!ok) return set_err(GLS_EHIP, "coarse FP32 LU (side stream) failed to launch");
+  HIP_TRY(hipEventRecord(mg.side.e1, s));
+  mg.lu_pending = true;
+  mg.lu_n = n;
+  mg.lu_pin = pin;
+  return GLS_OK;
+}
+// before the first coarse solve of the state: the side stream's factorization checked; a factorization that pivot growth
+// broke (O(1) or non-finite residual) is replaced by the pivoted sgetrf + sgetri inverse on the context stream. A
+// coarse-grid correction accurate to 1 % is exact enough for the V-cycle.
+int coarse_lu32_finish(gls_ctx *c) {
+  auto &mg = c->mg;
+  if (!mg.lu_pending) return GLS_OK;
+  mg.lu_pending = false;
+  const int64_t n = mg.lu_n;
+  int inf = -1;
+  double rn = INFINITY;
+  HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, mg.side.s));
+  HIP_TRY(hipMemcpyAsync(&rn, mg.lu_rel.p, sizeof(double), hipMemcpyDeviceToHost, mg.side.s));
+  HIP_TRY(hipStreamSynchronize(mg.side.s));
+  const double rel = inf == 0 ? rn / std::sqrt((double)n) : INFINITY;
+  const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
+  if (verbose)
+    std::printf("mg: coarse FP32 unpivoted LU n=%lld info=%d, check |A x - 1| / |1| = %.2e\n", (long long)n, inf, rel);
+  if (inf == 0 && rel < 1e-2) return GLS_OK;
+  mg.lu32_npvt = false;
+  HIP_TRY(gls::vec_to_f32(mg.probe.p, mg.probe32.p, n * n, c->stream));  // the pinned matrix again
+  if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+      rocsolver_sgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+          rocblas_status_success)
+    return set_err(GLS_EHIP, "rocsolver_sgetrf failed");
+  HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (inf == 0) {
+    if (rocsolver_sgetri(mg.blas, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
+        rocblas_status_success)
+      return set_err(GLS_EHIP, "rocsolver_sgetri failed");
+    HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  if (verbose) std::printf("mg: coarse FP32 pivoted LU + inverse n=%lld info=%d\n", (long long)n, inf);
+  if (inf != 0) {
+    mg.direct_ok = mg.lu32 = false;
+    mg.dirty = true;
+    return set_err(GLS_EINVAL, "coarse FP32 LU: zero pivot %d", inf);
+  }
+  return GLS_OK;
+}
+
 int mg_prepare(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.dirty) return GLS_OK;
+  GLS_TRY(coarse_lu32_finish(c));  // (its buffers are re-probed below)
   const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
   auto tick = [&]() {  // host wall time of the preparation phases (verbose only: synchronizes)
     if (verbose) (void)hipStreamSynchronize(c->stream);
@@ -2438,63 +2558,10 @@ int mg_prepare(gls_ctx *c) {
       if (pin >= n) return set_err(GLS_EINVAL, "mg: coarsest level without pressure DoFs");
       HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
       HIP_TRY(gls::vec_to_f32(mg.probe.p, mg.probe32.p, n * n, c->stream));
-      int inf = -1;
-      mg.lu32_npvt = false;
-      {  // rocSOLVER sgetrf_npvt (138 ms at n = 25000 against sgetrf's 410 + sgetri's ~800), checked on A x = 1
-        if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-            rocsolver_sgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.info.p) !=
-                rocblas_status_success)
-          return set_err(GLS_EHIP, "rocsolver_sgetrf_npvt failed");
-        HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        double rel = INFINITY;
-        if (inf == 0) {
-          if (mg.chk32.n != (size_t)(2 * n)) GLS_TRY(mg.chk32.alloc((size_t)(2 * n)));
-          HIP_TRY(gls::vec_fill(mg.chk32.p, n, 1.0, c->stream));
-          HIP_TRY(gls::mg_zero_row(mg.chk32.p, 1, pin, c->stream));  // (the pinned row: x = 0 there)
-          HIP_TRY(gls::vec_to_f32(mg.chk32.p, mg.x32.p, n, c->stream));
-          HIP_TRY(gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, c->stream));
-          HIP_TRY(gls::vec_from_f32(mg.x32.p, mg.chk32.p + n, n, c->stream));
-          const double one = 1.0, mone = -1.0;
-          double rn = 0.0, bn = 0.0;
-          if (rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe.p,
-                            (rocblas_int)n, mg.chk32.p + n, 1, &mone, mg.chk32.p, 1) != rocblas_status_success ||
-              rocblas_dnrm2(mg.blas, (rocblas_int)n, mg.chk32.p, 1, &rn) != rocblas_status_success)
-            return set_err(GLS_EHIP, "coarse LU check failed");
-          bn = std::sqrt((double)n);
-          rel = rn / bn;
-        }
-        if (verbose)
-          std::printf("mg: coarse FP32 unpivoted LU n=%lld info=%d, check |A x - 1| / |1| = %.2e, at %.2f ms\n", (long long)n,
-                      inf, rel, ms(t0, tick()));
-        // (a coarse-grid correction accurate to 1 % is exact enough for the V-cycle; a factorization that pivot growth
-        // broke gives O(1) or non-finite residuals and takes the pivoted route)
-        if (inf == 0 && rel < 1e-2) {
-          mg.lu32 = mg.lu32_npvt = mg.direct_ok = true;
-          mg.dirty = false;
-          return GLS_OK;
-        }
-        HIP_TRY(gls::vec_to_f32(mg.probe.p, mg.probe32.p, n * n, c->stream));  // the pivoted route below
-      }
-      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-          rocsolver_sgetrf(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
-              rocblas_status_success)
-        return set_err(GLS_EHIP, "rocsolver_sgetrf failed");
-      HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      const auto t2 = tick();
-      if (inf == 0) {
-        if (rocsolver_sgetri(mg.blas, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.ipiv.p, mg.info.p) !=
-            rocblas_status_success)
-          return set_err(GLS_EHIP, "rocsolver_sgetri failed");
-        HIP_TRY(hipMemcpyAsync(&inf, mg.info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-      }
-      if (verbose)
-        std::printf("mg: coarse FP32 LU n=%lld info=%d: levels+probe %.2f ms, sgetrf %.2f ms, sgetri done at %.2f ms\n",
-                    (long long)n, inf, ms(t0, t1), ms(t1, t2), ms(t0, tick()));
-      if (inf != 0) return set_err(GLS_EINVAL, "coarse FP32 LU: zero pivot %d", inf);
-      mg.lu32 = mg.direct_ok = true;
+      GLS_TRY(coarse_lu32_start(c, n, pin));
+      if (verbose) std::printf("mg: coarse FP32 unpivoted LU n=%lld queued on the side stream at %.2f ms\n", (long long)n,
+                               ms(t0, tick()));
+      mg.lu32 = mg.lu32_npvt = mg.direct_ok = true;
       mg.dirty = false;
       return GLS_OK;
     }
@@ -2834,6 +2901,7 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
     HIP_TRY(gls::vec_pack_dofs(mg.rep_x.p, mg.rep_map.p, n, x, c->stream));
     return GLS_OK;
   }
+  if (l == L - 1 && mg.direct_ok) GLS_TRY(coarse_lu32_finish(c));
   if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
     if (mg.lu32 && mg.lu32_npvt) {  // x = U^-1 L^-1 b in FP32, the pinned pressure DoF's correction zero
       HIP_TRY(gls::vec_to_f32(b, mg.x32.p, n, c->stream));
@@ -3097,9 +3165,13 @@ static int ensure_ilu(gls_ctx *c) {
   if (I.mc_factor)
     HIP_TRY(gls::ilu_mc_factor(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
                                I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, I.mc_moff.p,
-                               I.mc_map.n ? I.mc_map.p : nullptr, s));
+                               I.mc_map.n ? I.mc_map.p : nullptr, I.mc_compact, s));
   else
     RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
+  if (I.solve32 && I.mc_solve) {  // the smoother's FP32 copy of the factors (one pass per factorization)
+    if (I.val32.n != (size_t)I.nnz + 256) GLS_TRY(I.val32.alloc((size_t)I.nnz + 256));
+    HIP_TRY(gls::vec_to_f32(I.val.p, I.val32.p, I.nnz, s));
+  }
   I.valid = true;
   if (verbose) {
     const auto t2 = now();
@@ -3122,8 +3194,9 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   // z = P^T U^-1 L^-1 P v (P: the Cuthill-McKee renumbering the factors live in)
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
   if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
-    HIP_TRY(gls::ilu_mc_solve(I.mc_desc.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.col.p, I.val.p, I.vbuf.p,
-                              I.tbuf.p, I.vbuf.p, I.mc_wl.data(), I.mc_wu.data(), c->stream));
+    HIP_TRY(gls::ilu_mc_solve(I.mc_desc.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.col.p, I.val.p,
+                              I.solve32 ? I.val32.p : nullptr, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_wl.data(),
+                              I.mc_wu.data(), c->stream));
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
@@ -3409,6 +3482,7 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       // 1.72 -> 0.08 s (profiles/r05_app_configs3_hmg_ilu_order.txt)
       GLS_TRY(gls_ilu_set_options(g, GLS_ILU_ORDER_MULTICOLOR, 0));
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
+      g->ilu.solve32 = p->mixed_precision != 0;
       mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
   // direct coarsest solve: single GPU, coarsest level up to kDirectMax DoFs (FP64 LU up to kDirectSmall, FP32 above)
@@ -3744,6 +3818,7 @@ int gls_mg_detach(gls_ctx *c) {
   // the ILU(0) smoothers the attach put on the levels (level 0 is this context) go with the multigrid, so
   // the preconditioner falls back to Jacobi (gls_native.h) and not to a leftover smoother ILU
   for (auto *g : c->mg.ilu_levels) GLS_TRY(gls_ilu_detach(g));
+  c->mg.side.reset();  // (a coarse factorization in flight reads the buffers the assignment frees)
   c->mg = gls_ctx::MG();
   return GLS_OK;
 }
@@ -5048,6 +5123,9 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   // one color (fill 0; fill-in can create such entries: then rocSPARSE csrsv solves)
   I.mc_solve = false;
   I.mc_factor = false;
+  I.mc_compact = false;
+  I.solve32 = false;
+  I.val32.release();
   std::vector<int64_t> mc_moff_h;  // position map offsets (empty: no map)
   if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
     const int ncl = I.n_order_colors;
@@ -5104,6 +5182,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       int64_t maxrow = 0;
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
       I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
+      I.mc_compact = maxrow <= gls::kIluCompactRow && rowp.back() < (int64_t(1) << 36);
       if (I.mc_factor) {  // the position map (uint16 per entry), when it fits a quarter of free memory
         mc_moff_h.assign((size_t)n + 1, 0);
         for (int64_t r = 0; r < n; ++r) {
@@ -5270,7 +5349,10 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   I.n_blocks = nblk;
   I.athresh = athresh;
   I.rthresh = rthresh;
-  if (I.nnz >= INT32_MAX) {  // past 2^31 entries: the multicolor kernels only (rocSPARSE takes 32-bit CSR)
+  // the multicolor kernels factor and solve: no rocSPARSE state (its csrilu0 / csrsv analyses were a setup cost of
+  // ~0.9 s at 1.7 M DoFs, a radix sort each, for solves that never ran); past 2^31 entries they are the only route
+  // (rocSPARSE takes 32-bit CSR)
+  if (I.nnz >= INT32_MAX || (I.mc_factor && I.mc_solve)) {
     if (!I.mc_factor || !I.mc_solve)
       return set_err(GLS_EINVAL, "gls_ilu_attach: %lld entries (> 2^31): the multicolor order with fill 0 is needed",
                      (long long)I.nnz);

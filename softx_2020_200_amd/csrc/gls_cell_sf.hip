@@ -154,7 +154,7 @@ __device__ __forceinline__ void jv_point(const OpParams &P, int64_t cell, int q,
 
 template <int KP, bool GEN>
 __global__ void __launch_bounds__(64) k_cell_sf_jv(const OpParams P, const Tables1D T) {
-  constexpr int NV = 27, NQ = 27, NP = (KP + 1) * (KP + 1) * (KP + 1), NCQ = 16;
+  constexpr int NV = 27, NQ = 27, NP = (KP + 1) * (KP + 1) * (KP + 1);
   constexpr bool PSF = KP == 2;  // pressure through the sweeps too
   __shared__ double sV[3][3], sD[3][3], sS[3][3], sW[3];  // [q][node] Q2 tables, Gauss weights
   __shared__ double sVp[3][KP + 1], sDp[3][KP + 1];

@@ -43,9 +43,11 @@ __device__ __forceinline__ double pick4(const double *a, int j) {
 // Each node group's row extents come from one 192-byte descriptor (kGroupDesc int64, built at attach:
 // r0, nr, entry range, row boundaries, lsp, usp, didx, row ends), so the first dependent load round
 // of a launch is the descriptor itself rather than grow -> rowp / lsp / usp / didx.
-template <int WPG, bool LOWER>
+// T: the factors' storage (double, or the FP32 copy a multigrid smoother reads: gls_mg_params.mixed_precision);
+// the sums are FP64 either way.
+template <int WPG, bool LOWER, typename T>
 __global__ void __launch_bounds__(256) k_mc_tri(const int64_t *__restrict__ gdesc, int g0, int g1,
-                                                const int32_t *__restrict__ col, const double *__restrict__ val,
+                                                const int32_t *__restrict__ col, const T *__restrict__ val,
                                                 const double *__restrict__ rhs, double *__restrict__ out) {
   constexpr int GPB = 4 / WPG;  // node groups per 256-thread block
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
@@ -187,8 +189,14 @@ __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_
 // factorization streams them with the upper values instead of searching: the step's LDS chain
 // shrinks to sv[p] / U_kk and one read-modify-write per lane. Same updates in the same order, so the
 // factors are bitwise those of the searching kernel.
+//
+// R: the LDS capacity of a row (entries; its pivots too). Every workgroup holds its group's rows and
+// pivot extents in LDS: 28 bytes per entry at R = kIluMaxRow (72 KB, two workgroups per CU). The
+// compact instantiation (R = kIluCompactRow, rows of Q2-Q1 3D cells: <= 402 entries) packs each pivot's
+// diagonal position (36 bits), upper length (10) and map offset (18) into one word: 20 bytes per entry,
+// 36 KB, four workgroups per CU -- twice the waves to hide the step's LDS / division latency chain
 constexpr uint16_t kMapMiss = 0xffff;
-template <bool MAP, int NS>
+template <bool MAP, int NS, int R>
 __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *__restrict__ grow, int g0, int g1,
                                                                 const int64_t *__restrict__ rowp,
                                                                 const int32_t *__restrict__ col, double *__restrict__ val,
@@ -196,12 +204,13 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
                                                                 const int64_t *__restrict__ didx, double boost_tol,
                                                                 double boost_val, const int64_t *__restrict__ moff,
                                                                 const uint16_t *__restrict__ map) {
-  __shared__ int32_t sc[kMaxGroupRows][kIluMaxRow + 1];
-  __shared__ double sv[kMaxGroupRows][kIluMaxRow + 1];  // + a dummy slot for the MAP step's idle lanes
-  // pivot-row extents: the diagonal's position and the upper part's length
-  __shared__ int64_t sdk[kMaxGroupRows][kIluMaxRow];
-  __shared__ int32_t sul[kMaxGroupRows][kIluMaxRow];
-  __shared__ int32_t smo[MAP ? kMaxGroupRows : 1][MAP ? kIluMaxRow : 1];  // per pivot: map offset in the row
+  constexpr bool PACK = R <= kIluCompactRow;
+  __shared__ int32_t sc[kMaxGroupRows][R + 1];
+  __shared__ double sv[kMaxGroupRows][R + 1];  // + a dummy slot for the MAP step's idle lanes
+  // pivot-row extents: the diagonal's position and the upper part's length (PACK: with the map offset in one word)
+  __shared__ int64_t sdk[kMaxGroupRows][R];
+  __shared__ int32_t sul[PACK ? 1 : kMaxGroupRows][PACK ? 1 : R];
+  __shared__ int32_t smo[MAP && !PACK ? kMaxGroupRows : 1][MAP && !PACK ? R : 1];  // per pivot: map offset in the row
   const int g = g0 + (int)blockIdx.x;
   if (g >= g1) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -230,15 +239,15 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     int mrun = 0;  // MAP: running offset of the pivot's map segment in the row's
     for (int p0 = 0; p0 < nl; p0 += 64) {
       const int p = p0 + lane;
-      int m = 0;
+      int m = 0, ul = 0;
+      int64_t dk = 0;
       if (p < nl) {
         const int k = sc[w][p];
-        const int64_t dk = didx[k];
-        const int ul = (int)(rowp[k + 1] - dk - 1);
-        sdk[w][p] = dk;
-        sul[w][p] = ul;
+        dk = didx[k];
+        ul = (int)(rowp[k + 1] - dk - 1);
         m = MAP ? (ul + 3) & ~3 : ul;  // MAP segments are padded to quads
       }
+      int mo = 0;
       if (MAP) {  // exclusive prefix sum of the upper-entry counts over the wave
         int x = m;
 #pragma unroll
@@ -246,8 +255,17 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
           const int y = __shfl_up(x, o, 64);
           if (lane >= o) x += y;
         }
-        if (p < nl) smo[w][p] = mrun + x - m;
+        mo = mrun + x - m;
         mrun += __shfl(x, 63, 64);
+      }
+      if (p < nl) {
+        if (PACK) {
+          sdk[w][p] = dk | ((int64_t)ul << 36) | ((int64_t)mo << 46);
+        } else {
+          sdk[w][p] = dk;
+          sul[w][p] = ul;
+          if (MAP) smo[w][p] = mo;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -264,13 +282,14 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     // waitcnt pass sees straight-line code and waits for exactly the stage in use, not vmcnt(0)
     auto issue = [&](int p, Stage &st) {
       const bool in = p < nl;
-      st.dk = in ? sdk[w][p] : rp;
-      st.e1 = in ? st.dk + 1 + sul[w][p] : rp;
+      const int64_t pk = in ? sdk[w][p] : 0;
+      st.dk = in ? (PACK ? pk & ((int64_t(1) << 36) - 1) : pk) : rp;
+      st.e1 = in ? st.dk + 1 + (PACK ? (int)((pk >> 36) & 1023) : sul[w][p]) : rp;
       st.piv = val[st.dk];
       if (MAP) {  // lane l: the quad of upper entries 4l .. 4l+3 (one 8-byte map load, one address
                   // for the values; past the row's end they are masked in the step, and the value
                   // array is padded for the last rows)
-        st.mo = in ? smo[w][p] : 0;
+        st.mo = in ? (PACK ? (int)((uint64_t)pk >> 46) : smo[w][p]) : 0;
         const bool ok = 4 * lane < st.e1 - st.dk - 1;
         st.mq = reinterpret_cast<const uint64_t *>(map + mbase + st.mo)[ok ? lane : 0];
         const double *vp = val + st.dk + 1 + 4 * lane;
@@ -297,7 +316,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
 #pragma unroll
         for (int t = 0; t < PF; ++t) {
           const int q = (int)((st.mq >> (16 * t)) & 0xffffu);
-          qa[t] = 4 * lane + t < m && q != kMapMiss ? q : kIluMaxRow;
+          qa[t] = 4 * lane + t < m && q != kMapMiss ? q : R;
         }
 #pragma unroll
         for (int t = 0; t < PF; ++t) r[t] = sv[w][qa[t]];
@@ -419,42 +438,53 @@ hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col,
 
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
                          const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
-                         double boost_val, const int64_t *moff, const uint16_t *map, hipStream_t s) {
+                         double boost_val, const int64_t *moff, const uint16_t *map, bool compact, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     const dim3 gr((unsigned)(g1 - g0)), bl(64 * kMaxGroupRows);
-    if (map)
-      hipLaunchKernelGGL((k_mc_ilu0<true, 3>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
-                         boost_val, moff, map);
-    else
-      hipLaunchKernelGGL((k_mc_ilu0<false, 3>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol,
-                         boost_val, moff, map);
+#define GLS_MC_ILU0(MAP, R)                                                                                 \
+  hipLaunchKernelGGL((k_mc_ilu0<MAP, 3, R>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol, \
+                     boost_val, moff, map)
+    if (map && compact) GLS_MC_ILU0(true, kIluCompactRow);
+    else if (map) GLS_MC_ILU0(true, kIluMaxRow);
+    else if (compact) GLS_MC_ILU0(false, kIluCompactRow);
+    else GLS_MC_ILU0(false, kIluMaxRow);
+#undef GLS_MC_ILU0
   }
   return hipGetLastError();
 }
 
-hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
-                        const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
-                        const uint8_t *waves_upper, hipStream_t s) {
+namespace {
+template <typename T>
+void mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col, const T *val,
+              const double *b, double *y, double *x, const uint8_t *waves_lower, const uint8_t *waves_upper,
+              hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_lower[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, true>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, b, y);
+      hipLaunchKernelGGL((k_mc_tri<4, true, T>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, b, y);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, true>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
-                         val, b, y);
+      hipLaunchKernelGGL((k_mc_tri<1, true, T>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1,
+                         col, val, b, y);
   }
   for (int c = n_colors - 1; c >= 0; --c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_upper[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, false>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, y, x);
+      hipLaunchKernelGGL((k_mc_tri<4, false, T>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, y, x);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, false>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
-                         val, y, x);
+      hipLaunchKernelGGL((k_mc_tri<1, false, T>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1,
+                         col, val, y, x);
   }
+}
+}  // namespace
+hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+                        const double *val, const float *val32, const double *b, double *y, double *x,
+                        const uint8_t *waves_lower, const uint8_t *waves_upper, hipStream_t s) {
+  if (val32) mc_solve(gdesc, color_groups, n_colors, col, val32, b, y, x, waves_lower, waves_upper, s);
+  else mc_solve(gdesc, color_groups, n_colors, col, val, b, y, x, waves_lower, waves_upper, s);
   return hipGetLastError();
 }
 

@@ -508,53 +508,89 @@ hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, 
 // launches per solve against rocBLAS trsv's 62 ms at n = 25000 (profiles/r06_lu25k.txt).
 constexpr int kLuB = 128;
 namespace {
-template <bool LOWER>
-__device__ __forceinline__ void lu_diag_solve(const float *__restrict__ A, int64_t n, int r0, int nr, float v,
-                                              float *__restrict__ x, float *xb) {
-  const int t = threadIdx.x;
-  if (LOWER) {  // unit diagonal
-    for (int c = 0; c < nr; ++c) {
-      if (t == c) xb[c] = v;
-      __syncthreads();
-      if (t > c && t < nr) v -= A[(r0 + t) + (int64_t)(r0 + c) * n] * xb[c];
-    }
-  } else {
-    for (int c = nr - 1; c >= 0; --c) {
-      if (t == c) xb[c] = v / A[(r0 + c) + (int64_t)(r0 + c) * n];
-      __syncthreads();
-      if (t < c) v -= A[(r0 + t) + (int64_t)(r0 + c) * n] * xb[c];
-    }
-  }
-  __syncthreads();
-  if (t < nr) x[r0 + t] = xb[t];
-}
-// k < 0: the first diagonal block alone (block 0 forward, the last block backward)
+// Step k (k < 0: the first diagonal block alone, block 0 forward / the last block backward): workgroup 0
+// applies block column k to the next diagonal block's rows and stages that diagonal block in LDS, the others
+// apply block column k to the rows beyond. Every global load of a launch is issued in rounds of 32 per operand
+// with no dependence between them (clamped addresses, select afterwards): the first versions walked 128
+// dependent rounds of 8-16 loads and spent 34-113 us per launch on memory latency (profiles/r06_lu_solve_ab.txt).
+// The diagonal block is then solved by its two wavefronts in turn, one column at a time with the column's value
+// broadcast from its lane by v_readlane (no workgroup barrier in the sequential part; one hands the first half
+// to the second).
 template <bool LOWER>
 __global__ void __launch_bounds__(kLuB) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k) {
-  __shared__ float xk[kLuB], xb[kLuB];
-  const int t = threadIdx.x, nb = (n + kLuB - 1) / kLuB;
-  if (k < 0) {
-    const int kb = LOWER ? 0 : nb - 1, r0 = kb * kLuB, nr = min(kLuB, n - r0);
-    lu_diag_solve<LOWER>(A, n, r0, nr, t < nr ? x[r0 + t] : 0.f, x, xb);
+  __shared__ float xk[kLuB], xb[kLuB], rd[kLuB];
+  __shared__ float D[kLuB][kLuB + 1];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, nb = (n + kLuB - 1) / kLuB;
+  const bool first = k < 0, diag = blockIdx.x == 0;
+  const int j0 = first ? 0 : k * kLuB, nj = first ? 1 : min(kLuB, n - j0);
+  const int kn = first ? (LOWER ? 0 : nb - 1) : (LOWER ? k + 1 : k - 1);  // the diagonal block solved here
+  const int r0 = kn * kLuB, nr = min(kLuB, n - r0);
+  const int i = diag ? r0 + t
+                     : LOWER ? (k + 2) * kLuB + ((int)blockIdx.x - 1) * kLuB + t : ((int)blockIdx.x - 1) * kLuB + t;
+  const bool live = diag ? t < nr : LOWER ? i < n : i < kn * kLuB;
+  const int ic = min(i, n - 1), tc = min(t, nr - 1);
+  if (!first) {
+    xk[t] = t < nj ? x[j0 + t] : 0.f;
+    __syncthreads();
+  }
+  float v = x[ic];
+  // (rounds of 32 loads per operand: 64 in one round measured slower, 9.3 against 8.2 ms per solve at n = 25000)
+  for (int c0 = 0; c0 < kLuB; c0 += 32) {
+    float a[32], d[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      if (!first) a[u] = A[ic + (int64_t)(j0 + min(c0 + u, nj - 1)) * n];
+      if (diag) d[u] = A[(r0 + tc) + (int64_t)(r0 + min(c0 + u, nr - 1)) * n];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int c = c0 + u;
+      if (!first) v -= a[u] * xk[c];  // (xk = 0 past the block's end)
+      if (diag) D[t][c] = t < nr && c < nr ? d[u] : (t == c ? 1.f : 0.f);  // outside the block: identity
+    }
+  }
+  if (!diag) {
+    if (live) x[i] = v;
     return;
   }
-  const int j0 = k * kLuB, nj = min(kLuB, n - j0);
-  if (t < nj) xk[t] = x[j0 + t];
   __syncthreads();
-  auto update = [&](int i) {
-    float s = x[i];
-    for (int j = 0; j < nj; ++j) s -= A[i + (int64_t)(j0 + j) * n] * xk[j];
-    return s;
-  };
-  const int kn = LOWER ? k + 1 : k - 1;  // the next diagonal block
-  if (blockIdx.x == 0) {
-    const int r0 = kn * kLuB, nr = min(kLuB, n - r0);
-    lu_diag_solve<LOWER>(A, n, r0, nr, t < nr ? update(r0 + t) : 0.f, x, xb);
-    return;
+  if (!LOWER) {  // (read back by the writing wavefront only)
+    rd[t] = 1.f / D[t][t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
-  // rows beyond the next block: after it (forward) or before it (backward)
-  const int i = LOWER ? (k + 2) * kLuB + ((int)blockIdx.x - 1) * kLuB + t : ((int)blockIdx.x - 1) * kLuB + t;
-  if (LOWER ? i < n : i < kn * kLuB) x[i] = update(i);
+  auto bcast = [](float q, int c) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q), c)); };
+  auto tri = [&](int cb) {  // the wavefront's own 64 x 64 triangle
+    if (LOWER) {
+#pragma unroll
+      for (int c = 0; c < 64; ++c) {
+        const float xc = bcast(v, c), dv = D[t][cb + c];
+        v = __builtin_fmaf(lane > c ? -dv : 0.f, xc, v);
+      }
+    } else {
+      float xs = 0.f;
+#pragma unroll
+      for (int c = 63; c >= 0; --c) {
+        const float xc = bcast(v, c) * rd[cb + c], dv = D[t][cb + c];
+        xs = lane == c ? xc : xs;
+        v = __builtin_fmaf(lane < c ? -dv : 0.f, xc, v);
+      }
+      v = xs;
+    }
+  };
+  const int wf = LOWER ? 0 : 1;  // the wavefront solved first
+  if (w == wf) {
+    tri(64 * wf);
+    xb[t] = v;
+  }
+  __syncthreads();
+  if (w != wf) {
+    const int cb = 64 * wf;
+#pragma unroll 16
+    for (int c = 0; c < 64; ++c) v -= D[t][cb + c] * xb[cb + c];
+    tri(64 * w);
+  }
+  if (live) x[i] = v;
 }
 }  // namespace
 hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s) {
