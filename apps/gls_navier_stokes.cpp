@@ -1734,7 +1734,6 @@ struct Solver {
     mp.pre_smooth = mp.smoother ? 1 : 2;
     mp.post_smooth = mp.smoother ? 1 : 2;
     mp.omega = 0.6;
-    mp.mixed_precision = mp.smoother;  // the ILU smoothers' solves read FP32 copies of their FP64 factors
     mp.coarse_direct = n_coarse <= (plevel_used ? kPLevelDirectMax : 8192) ? 1 : -1;
     if (world == 1) {
       ck(gls_mg_attach_transfers(ctx, &mp, po.data(), pc.data(), pw.data(), pi.data()), "gls_mg_attach_transfers");

@@ -391,9 +391,7 @@ def bench_cylinder3d(args):
         nco = levels[-1][0].n_dofs
         ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
                                        coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=args.mg_omega_cyl,
-                                       coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother,
-                                       # the ILU smoothers' solves read FP32 copies of their FP64 factors
-                                       mixed_precision=int(args.mg_precision == "f32" and args.cyl_smoother == "ilu"))
+                                       coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother)
     else:
         ctx, sp, x = make(mesh(refine).fe_space(2, 1, qmapping_all=qall))
         ctx.set_time(scheme, ts)

@@ -215,9 +215,9 @@ typedef struct {
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
                                                  arithmetic from an FP32 copy of the linearization
                                                  (brick path; vectors, transfers and the outer GMRES
-                                                 operator stay FP64); the ILU(0) smoothers' triangular
-                                                 solves read an FP32 copy of their FP64 factors (FP64
-                                                 sums). 0: all FP64 */
+                                                 operator stay FP64). 0: all FP64 (an FP32 copy of the
+                                                 ILU smoothers' factors measured slower:
+                                                 profiles/r06_ab_ilu_fp32_factors.txt) */
   const int *level_sweeps;                    /* optional (NULL: uniform): 2*n_levels ints, the
                                                  pre / post sweep counts of each level (the entries of
                                                  the coarsest level are ignored) */

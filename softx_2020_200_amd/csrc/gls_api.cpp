@@ -391,10 +391,6 @@ struct gls_ctx {
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
     bool mc_compact = false;  // ... by the compact-LDS kernel (rows <= kIluCompactRow)
-    // a multigrid smoother's ILU with gls_mg_params.mixed_precision: the color solves read an FP32 copy of the
-    // factors (factored in FP64; 12 -> 8 bytes per entry of the solves' stream)
-    bool solve32 = false;
-    DevBuf<float> val32;
     std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
     DevBuf<int64_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc int64)
     DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
@@ -3168,10 +3164,6 @@ static int ensure_ilu(gls_ctx *c) {
                                I.mc_map.n ? I.mc_map.p : nullptr, I.mc_compact, s));
   else
     RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
-  if (I.solve32 && I.mc_solve) {  // the smoother's FP32 copy of the factors (one pass per factorization)
-    if (I.val32.n != (size_t)I.nnz + 256) GLS_TRY(I.val32.alloc((size_t)I.nnz + 256));
-    HIP_TRY(gls::vec_to_f32(I.val.p, I.val32.p, I.nnz, s));
-  }
   I.valid = true;
   if (verbose) {
     const auto t2 = now();
@@ -3194,9 +3186,8 @@ static int apply_ilu(gls_ctx *c, const double *v, double *z) {
   // z = P^T U^-1 L^-1 P v (P: the Cuthill-McKee renumbering the factors live in)
   HIP_TRY(gls::vec_permute(I.vbuf.p, v, I.perm.p, c->n_dofs, 0, c->stream));
   if (I.mc_solve) {  // multicolor order: color-by-color solves (gls_ilu_kernels.hip)
-    HIP_TRY(gls::ilu_mc_solve(I.mc_desc.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.col.p, I.val.p,
-                              I.solve32 ? I.val32.p : nullptr, I.vbuf.p, I.tbuf.p, I.vbuf.p, I.mc_wl.data(),
-                              I.mc_wu.data(), c->stream));
+    HIP_TRY(gls::ilu_mc_solve(I.mc_desc.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.col.p, I.val.p, I.vbuf.p,
+                              I.tbuf.p, I.vbuf.p, I.mc_wl.data(), I.mc_wu.data(), c->stream));
     HIP_TRY(gls::vec_permute(z, I.vbuf.p, I.perm.p, c->n_dofs, 1, c->stream));
     return GLS_OK;
   }
@@ -3482,7 +3473,6 @@ static int mg_attach_common(gls_ctx *c, const gls_mg_params *p) {
       // 1.72 -> 0.08 s (profiles/r05_app_configs3_hmg_ilu_order.txt)
       GLS_TRY(gls_ilu_set_options(g, GLS_ILU_ORDER_MULTICOLOR, 0));
       GLS_TRY(gls_ilu_attach(g, 0, 1e-12, 1.0));
-      g->ilu.solve32 = p->mixed_precision != 0;
       mg.ilu_levels.push_back(g);  // detached again by gls_mg_detach
     }
   // direct coarsest solve: single GPU, coarsest level up to kDirectMax DoFs (FP64 LU up to kDirectSmall, FP32 above)
@@ -5124,8 +5114,6 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
   I.mc_solve = false;
   I.mc_factor = false;
   I.mc_compact = false;
-  I.solve32 = false;
-  I.val32.release();
   std::vector<int64_t> mc_moff_h;  // position map offsets (empty: no map)
   if (I.ordering == GLS_ILU_ORDER_MULTICOLOR) {
     const int ncl = I.n_order_colors;

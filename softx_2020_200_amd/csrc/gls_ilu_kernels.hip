@@ -43,11 +43,9 @@ __device__ __forceinline__ double pick4(const double *a, int j) {
 // Each node group's row extents come from one 192-byte descriptor (kGroupDesc int64, built at attach:
 // r0, nr, entry range, row boundaries, lsp, usp, didx, row ends), so the first dependent load round
 // of a launch is the descriptor itself rather than grow -> rowp / lsp / usp / didx.
-// T: the factors' storage (double, or the FP32 copy a multigrid smoother reads: gls_mg_params.mixed_precision);
-// the sums are FP64 either way.
-template <int WPG, bool LOWER, typename T>
+template <int WPG, bool LOWER>
 __global__ void __launch_bounds__(256) k_mc_tri(const int64_t *__restrict__ gdesc, int g0, int g1,
-                                                const int32_t *__restrict__ col, const T *__restrict__ val,
+                                                const int32_t *__restrict__ col, const double *__restrict__ val,
                                                 const double *__restrict__ rhs, double *__restrict__ out) {
   constexpr int GPB = 4 / WPG;  // node groups per 256-thread block
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
@@ -455,36 +453,27 @@ hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n
   return hipGetLastError();
 }
 
-namespace {
-template <typename T>
-void mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col, const T *val,
-              const double *b, double *y, double *x, const uint8_t *waves_lower, const uint8_t *waves_upper,
-              hipStream_t s) {
+hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
+                        const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
+                        const uint8_t *waves_upper, hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_lower[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, true, T>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, b, y);
+      hipLaunchKernelGGL((k_mc_tri<4, true>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, b, y);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, true, T>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1,
-                         col, val, b, y);
+      hipLaunchKernelGGL((k_mc_tri<1, true>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
+                         val, b, y);
   }
   for (int c = n_colors - 1; c >= 0; --c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     if (waves_upper[c] >= 4)
-      hipLaunchKernelGGL((k_mc_tri<4, false, T>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, y, x);
+      hipLaunchKernelGGL((k_mc_tri<4, false>), dim3((unsigned)(g1 - g0)), dim3(256), 0, s, gdesc, g0, g1, col, val, y, x);
     else
-      hipLaunchKernelGGL((k_mc_tri<1, false, T>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1,
-                         col, val, y, x);
+      hipLaunchKernelGGL((k_mc_tri<1, false>), dim3((unsigned)((g1 - g0 + 3) / 4)), dim3(256), 0, s, gdesc, g0, g1, col,
+                         val, y, x);
   }
-}
-}  // namespace
-hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
-                        const double *val, const float *val32, const double *b, double *y, double *x,
-                        const uint8_t *waves_lower, const uint8_t *waves_upper, hipStream_t s) {
-  if (val32) mc_solve(gdesc, color_groups, n_colors, col, val32, b, y, x, waves_lower, waves_upper, s);
-  else mc_solve(gdesc, color_groups, n_colors, col, val, b, y, x, waves_lower, waves_upper, s);
   return hipGetLastError();
 }
 

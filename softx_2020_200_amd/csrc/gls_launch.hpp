@@ -139,10 +139,9 @@ hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col,
 // per node group (int64): r0, nr, rowp[r0], rowp[r0 + nr], rowp[r0 + 1..3] (INT64_MAX past nr), 0, lsp[4],
 // usp[4], didx[4], rowp[r0 + 1..4] (the solves' group descriptor)
 constexpr int kGroupDesc = 24;
-// (val32 != nullptr: the factors' FP32 copy is read instead of val)
 hipError_t ilu_mc_solve(const int64_t *gdesc, const int32_t *color_groups, int n_colors, const int32_t *col,
-                        const double *val, const float *val32, const double *b, double *y, double *x,
-                        const uint8_t *waves_lower, const uint8_t *waves_upper, hipStream_t s);
+                        const double *val, const double *b, double *y, double *x, const uint8_t *waves_lower,
+                        const uint8_t *waves_upper, hipStream_t s);
 hipError_t vec_pack_dofs(const double *x, const int32_t *dofs, int64_t m, double *buf, hipStream_t s);
 hipError_t vec_unpack_dofs(double *x, const int32_t *dofs, int64_t m, const double *buf, hipStream_t s);
 hipError_t vec_add_dofs_ordered(double *x, const int32_t *u, const int32_t *off, const int32_t *slot, int64_t n,

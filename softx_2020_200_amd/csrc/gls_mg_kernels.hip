@@ -508,53 +508,84 @@ hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, 
 // launches per solve against rocBLAS trsv's 62 ms at n = 25000 (profiles/r06_lu25k.txt).
 constexpr int kLuB = 128;
 namespace {
-// Step k (k < 0: the first diagonal block alone, block 0 forward / the last block backward): workgroup 0
-// applies block column k to the next diagonal block's rows and stages that diagonal block in LDS, the others
-// apply block column k to the rows beyond. Every global load of a launch is issued in rounds of 32 per operand
-// with no dependence between them (clamped addresses, select afterwards): the first versions walked 128
-// dependent rounds of 8-16 loads and spent 34-113 us per launch on memory latency (profiles/r06_lu_solve_ab.txt).
-// The diagonal block is then solved by its two wavefronts in turn, one column at a time with the column's value
-// broadcast from its lane by v_readlane (no workgroup barrier in the sequential part; one hands the first half
-// to the second).
-template <bool LOWER>
-__global__ void __launch_bounds__(kLuB) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k) {
-  __shared__ float xk[kLuB], xb[kLuB], rd[kLuB];
-  __shared__ float D[kLuB][kLuB + 1];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, nb = (n + kLuB - 1) / kLuB;
+// Step k (k < 0: the first diagonal block alone, block 0 forward / the last block backward): workgroup 0 applies
+// block column k to the next diagonal block's rows and solves that diagonal block, the others apply block column k
+// to the rows beyond. A launch is bound by memory latency, so every global load of it is issued in ONE round before
+// anything waits: the right-hand side, block k's solution, and the two 128 x 128 blocks workgroup 0 reads (its rows
+// of block column k, the diagonal block), 16-byte loads along the columns, 16 + 16 per thread of 256, staged in LDS.
+// (Rounds of dependent loads cost ~2 us each: 128 rounds of one load per thread, 72 / 113 us per forward / backward
+// launch; rounds of 32, 21 us; profiles/r06_lu_solve_ab.txt.) The diagonal block is then solved by two wavefronts
+// in turn, one column at a time with the column's value broadcast from its lane by v_readlane (no workgroup
+// barrier in the sequential part; one hands the first half to the second).
+constexpr int kLuT = 256;
+template <bool LOWER, bool VEC>
+__global__ void __launch_bounds__(kLuT) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k) {
+  __shared__ float xk[kLuB], xb[kLuB], rd[kLuB], part[2][kLuB];
+  __shared__ float D[kLuB][kLuB + 1], C[kLuB][kLuB + 1];
+  const int t = threadIdx.x, nb = (n + kLuB - 1) / kLuB;
   const bool first = k < 0, diag = blockIdx.x == 0;
   const int j0 = first ? 0 : k * kLuB, nj = first ? 1 : min(kLuB, n - j0);
   const int kn = first ? (LOWER ? 0 : nb - 1) : (LOWER ? k + 1 : k - 1);  // the diagonal block solved here
   const int r0 = kn * kLuB, nr = min(kLuB, n - r0);
-  const int i = diag ? r0 + t
-                     : LOWER ? (k + 2) * kLuB + ((int)blockIdx.x - 1) * kLuB + t : ((int)blockIdx.x - 1) * kLuB + t;
-  const bool live = diag ? t < nr : LOWER ? i < n : i < kn * kLuB;
-  const int ic = min(i, n - 1), tc = min(t, nr - 1);
+  const int rb = diag ? r0 : LOWER ? (k + 1 + (int)blockIdx.x) * kLuB : ((int)blockIdx.x - 1) * kLuB;  // row block
+  const int row = t & (kLuB - 1), half = t >> 7;
+  const int i = rb + row;
+  const bool live = half == 0 && (diag ? row < nr : LOWER ? i < n : i < kn * kLuB);
+  // the round of loads
+  const float xi = x[min(i, n - 1)];
+  const float xkt = first ? 0.f : x[j0 + min(row, nj - 1)];
+  const int r4 = t & 31, cq = t >> 5;  // this thread's 4-row slot and column (of 8) in each 16-byte load round
+  auto ld = [&](int rbase, int cb, int ncol, int q) {
+    const int r = rbase + 4 * r4;
+    const int64_t c = (int64_t)(cb + min(q * 8 + cq, ncol - 1)) * n;
+    if (VEC && r + 3 < n) return *reinterpret_cast<const float4 *>(A + r + c);
+    return make_float4(A[min(r, n - 1) + c], A[min(r + 1, n - 1) + c], A[min(r + 2, n - 1) + c], A[min(r + 3, n - 1) + c]);
+  };
+  float4 qc[16], qd[16];
   if (!first) {
-    xk[t] = t < nj ? x[j0 + t] : 0.f;
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) qc[q] = ld(rb, j0, nj, q);
   }
-  float v = x[ic];
-  // (rounds of 32 loads per operand: 64 in one round measured slower, 9.3 against 8.2 ms per solve at n = 25000)
-  for (int c0 = 0; c0 < kLuB; c0 += 32) {
-    float a[32], d[32];
+  if (diag) {
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (!first) a[u] = A[ic + (int64_t)(j0 + min(c0 + u, nj - 1)) * n];
-      if (diag) d[u] = A[(r0 + tc) + (int64_t)(r0 + min(c0 + u, nr - 1)) * n];
-    }
+    for (int q = 0; q < 16; ++q) qd[q] = ld(r0, r0, nr, q);
+  }
+  if (half == 0) xk[row] = row < nj ? xkt : 0.f;
+  if (!first) {
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int c = c0 + u;
-      if (!first) v -= a[u] * xk[c];  // (xk = 0 past the block's end)
-      if (diag) D[t][c] = t < nr && c < nr ? d[u] : (t == c ? 1.f : 0.f);  // outside the block: identity
+    for (int q = 0; q < 16; ++q) {
+      const int c = q * 8 + cq;
+      C[4 * r4][c] = qc[q].x, C[4 * r4 + 1][c] = qc[q].y, C[4 * r4 + 2][c] = qc[q].z, C[4 * r4 + 3][c] = qc[q].w;
     }
+  }
+  if (diag) {  // outside the block: identity
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = q * 8 + cq;
+      const float e[4] = {qd[q].x, qd[q].y, qd[q].z, qd[q].w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr = 4 * r4 + u;
+        D[rr][c] = rr < nr && c < nr ? e[u] : (rr == c ? 1.f : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+  float v = xi;
+  if (!first) {  // the block column's product, two threads per row (halves of the columns)
+    float sacc = 0.f;
+#pragma unroll 16
+    for (int c = 0; c < 64; ++c) sacc += C[row][64 * half + c] * xk[64 * half + c];  // (xk = 0 past the block)
+    part[half][row] = sacc;
+    __syncthreads();
+    v = xi - part[0][row] - part[1][row];
   }
   if (!diag) {
     if (live) x[i] = v;
     return;
   }
-  __syncthreads();
-  if (!LOWER) {  // (read back by the writing wavefront only)
+  const int lane = t & 63, w = t >> 6;
+  if (!LOWER && half == 0) {  // (read back by the writing wavefront only)
     rd[t] = 1.f / D[t][t];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -584,7 +615,7 @@ __global__ void __launch_bounds__(kLuB) k_lu_step(const float *__restrict__ A, i
     xb[t] = v;
   }
   __syncthreads();
-  if (w != wf) {
+  if (w == 1 - wf) {
     const int cb = 64 * wf;
 #pragma unroll 16
     for (int c = 0; c < 64; ++c) v -= D[t][cb + c] * xb[cb + c];
@@ -592,17 +623,24 @@ __global__ void __launch_bounds__(kLuB) k_lu_step(const float *__restrict__ A, i
   }
   if (live) x[i] = v;
 }
+template <bool VEC>
+void lu_solve(const float *LU, int n, float *x, hipStream_t s) {
+  const int nb = (n + kLuB - 1) / kLuB;
+  hipLaunchKernelGGL((k_lu_step<true, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1);
+  for (int k = 0; k + 1 < nb; ++k) {
+    const int rest = n - (k + 2) * kLuB;
+    hipLaunchKernelGGL((k_lu_step<true, VEC>), dim3(1 + (rest > 0 ? (rest + kLuB - 1) / kLuB : 0)), dim3(kLuT), 0, s, LU,
+                       n, x, k);
+  }
+  hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1);
+  for (int k = nb - 1; k >= 1; --k)
+    hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1 + (k - 1)), dim3(kLuT), 0, s, LU, n, x, k);
+}
 }  // namespace
 hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const int nb = (n + kLuB - 1) / kLuB;
-  hipLaunchKernelGGL(k_lu_step<true>, dim3(1), dim3(kLuB), 0, s, LU, n, x, -1);
-  for (int k = 0; k + 1 < nb; ++k) {
-    const int rest = n - (k + 2) * kLuB;
-    hipLaunchKernelGGL(k_lu_step<true>, dim3(1 + (rest > 0 ? (rest + kLuB - 1) / kLuB : 0)), dim3(kLuB), 0, s, LU, n, x, k);
-  }
-  hipLaunchKernelGGL(k_lu_step<false>, dim3(1), dim3(kLuB), 0, s, LU, n, x, -1);
-  for (int k = nb - 1; k >= 1; --k) hipLaunchKernelGGL(k_lu_step<false>, dim3(1 + (k - 1)), dim3(kLuB), 0, s, LU, n, x, k);
+  if (n % 4 == 0 && reinterpret_cast<uintptr_t>(LU) % 16 == 0) lu_solve<true>(LU, n, x, s);
+  else lu_solve<false>(LU, n, x, s);
   return hipGetLastError();
 }
 

@@ -769,8 +769,7 @@ class GLSContext:
         """The V-cycle on a general hierarchy (gls_mg_attach_transfers): levels [self] + coarse_levels
         (hanging lines set on each), transfers[l] = (off, col, w, inject) from level l+1 to level l
         (octree_mg_transfer). Smoothing: damped Jacobi, or smoother="ilu" (ILU(0) per level); mixed_precision=1:
-        the levels' forest bricks apply the pencil J.v in FP32 (the other cells stay FP64) and the ILU smoothers'
-        color solves read FP32 copies of their FP64 factors."""
+        the levels' forest bricks apply the pencil J.v in FP32 (the other cells stay FP64)."""
         levels = [self] + list(coarse_levels)
         if len(transfers) != len(levels) - 1:
             raise GLSError("attach_multigrid_transfers: one transfer per level pair")

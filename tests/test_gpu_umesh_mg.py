@@ -30,7 +30,7 @@ def mapped_level(sp, nu):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,dim,spec,flat", [c for c in CASES if c[0] in ("shell", "cylshell", "rect3d")],
                          ids=["shell", "rect3d", "cylshell"])
-@pytest.mark.parametrize("k,kp,smoother", [(1, 1, "jacobi"), (2, 2, "jacobi"), (2, 1, "ilu"), (2, 1, "ilu-f32")])
+@pytest.mark.parametrize("k,kp,smoother", [(1, 1, "jacobi"), (2, 2, "jacobi"), (2, 1, "ilu")])
 def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k, kp, smoother):
     m = make_mesh(dim, spec)
     m.refine_global(1)
@@ -53,10 +53,8 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k, kp, smoother):
         ctxs = [context_for(q) for q in (probs if mg else probs[:1])]
         if mg:
             sw = 2 if smoother == "jacobi" else 1
-            # ilu-f32: the ILU smoothers' color solves read FP32 copies of their factors (mixed_precision)
             ctxs[0].attach_multigrid_transfers(ctxs[1:], xfer, pre_smooth=sw, post_smooth=sw, omega=0.6, coarse_direct=1,
-                                               smoother=smoother.replace("-f32", ""),
-                                               mixed_precision=int(smoother.endswith("-f32")))
+                                               smoother=smoother)
         U, U1 = cuda(u), cuda(np.zeros(p.n_dofs))
         ctxs[0].apply_dirichlet(U)
         ctxs[0].set_state(U, U1)
