@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 #include <set>
+#include <thread>
 
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -548,20 +549,30 @@ struct gls_ctx {
     // the FP32 unpivoted factorization and its check run on a stream of their own, overlapping the finer levels'
     // ILU setup and first smoothing on the context stream; the first coarse solve waits for them
     // (coarse_lu32_finish). Declared after the buffers it uses, so it is destroyed (synchronized) first.
+    // rocSOLVER's getrf returns to the host only when the factorization is done (82-89 ms of host time at
+    // n = 25000, box r06v), so the calls are made from a worker thread: the host thread queues the finer levels'
+    // setup meanwhile
     struct Side {
       hipStream_t s = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
+      std::thread worker;
+      int rc = 0;  // the worker's result: 0, or the failing call's number
       Side() = default;
       Side(const Side &) = delete;
       Side &operator=(const Side &) = delete;
-      Side(Side &&o) noexcept : s(o.s), e0(o.e0), e1(o.e1) { o.s = nullptr, o.e0 = o.e1 = nullptr; }
+      Side(Side &&o) noexcept : s(o.s), e0(o.e0), e1(o.e1), worker(std::move(o.worker)), rc(o.rc) {
+        o.s = nullptr, o.e0 = o.e1 = nullptr;
+      }
       Side &operator=(Side &&o) noexcept {
         if (this != &o) {
           reset();
-          s = o.s, e0 = o.e0, e1 = o.e1;
+          s = o.s, e0 = o.e0, e1 = o.e1, worker = std::move(o.worker), rc = o.rc;
           o.s = nullptr, o.e0 = o.e1 = nullptr;
         }
         return *this;
+      }
+      void join() {
+        if (worker.joinable()) worker.join();
       }
       hipError_t ensure() {
         if (s) return hipSuccess;
@@ -571,6 +582,7 @@ struct gls_ctx {
         return e;
       }
       void reset() {
+        join();
         if (s) {
           (void)hipStreamSynchronize(s);
           (void)hipStreamDestroy(s);
@@ -2383,23 +2395,37 @@ int coarse_lu32_start(gls_ctx *c, int64_t n, int64_t pin) {
   if (mg.lu_rel.n != 1) GLS_TRY(mg.lu_rel.alloc(1));
   HIP_TRY(hipEventRecord(mg.side.e0, c->stream));
   HIP_TRY(hipStreamWaitEvent(s, mg.side.e0, 0));
-  const double one = 1.0, mone = -1.0;
-  const bool ok =
-      rocblas_set_stream(mg.blas, s) == rocblas_status_success &&
-      rocsolver_sgetrf_npvt(mg.blas, (rocblas_int)n, (rocblas_int)n, mg.probe32.p, (rocblas_int)n, mg.info.p) ==
-          rocblas_status_success &&
-      gls::vec_fill(mg.chk32.p, n, 1.0, s) == hipSuccess && gls::mg_zero_row(mg.chk32.p, 1, pin, s) == hipSuccess &&
-      gls::vec_to_f32(mg.chk32.p, mg.x32.p, n, s) == hipSuccess &&
-      gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, s) == hipSuccess &&
-      gls::vec_from_f32(mg.x32.p, mg.chk32.p + n, n, s) == hipSuccess &&
-      rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe.p, (rocblas_int)n,
-                    mg.chk32.p + n, 1, &mone, mg.chk32.p, 1) == rocblas_status_success &&
-      rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_device) == rocblas_status_success &&
-      rocblas_dnrm2(mg.blas, (rocblas_int)n, mg.chk32.p, 1, mg.lu_rel.p) == rocblas_status_success;
-  (void)rocblas_set_pointer_mode(mg.blas, rocblas_pointer_mode_host);
-  (void)rocblas_set_stream(mg.blas, c->stream);
-  if (!ok) return set_err(GLS_EHIP, "coarse FP32 LU (side stream) failed to launch");
-  HIP_TRY(hipEventRecord(mg.side.e1, s));
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  mg.side.join();
+  mg.side.rc = 0;
+  auto *m = &mg;
+  const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
+  mg.side.worker = std::thread([m, s, n, pin, dev, verbose]() {
+    const double one = 1.0, mone = -1.0;
+    int &rc = m->side.rc;
+    const auto h0 = std::chrono::steady_clock::now();
+    if (hipSetDevice(dev) != hipSuccess) rc = 1;
+    else if (rocblas_set_stream(m->blas, s) != rocblas_status_success) rc = 2;
+    else if (rocsolver_sgetrf_npvt(m->blas, (rocblas_int)n, (rocblas_int)n, m->probe32.p, (rocblas_int)n, m->info.p) !=
+             rocblas_status_success)
+      rc = 3;
+    if (verbose)
+      std::printf("mg: sgetrf_npvt returned to its worker thread after %.2f ms\n",
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
+    if (!rc &&
+        !(gls::vec_fill(m->chk32.p, n, 1.0, s) == hipSuccess && gls::mg_zero_row(m->chk32.p, 1, pin, s) == hipSuccess &&
+          gls::vec_to_f32(m->chk32.p, m->x32.p, n, s) == hipSuccess &&
+          gls::dense_lu_solve_f32(m->probe32.p, (int)n, m->x32.p, s) == hipSuccess &&
+          gls::vec_from_f32(m->x32.p, m->chk32.p + n, n, s) == hipSuccess &&
+          rocblas_dgemv(m->blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, m->probe.p,
+                        (rocblas_int)n, m->chk32.p + n, 1, &mone, m->chk32.p, 1) == rocblas_status_success &&
+          rocblas_set_pointer_mode(m->blas, rocblas_pointer_mode_device) == rocblas_status_success &&
+          rocblas_dnrm2(m->blas, (rocblas_int)n, m->chk32.p, 1, m->lu_rel.p) == rocblas_status_success))
+      rc = 4;
+    (void)rocblas_set_pointer_mode(m->blas, rocblas_pointer_mode_host);
+    if (!rc && hipEventRecord(m->side.e1, s) != hipSuccess) rc = 5;
+  });
   mg.lu_pending = true;
   mg.lu_n = n;
   mg.lu_pin = pin;
@@ -2412,6 +2438,13 @@ int coarse_lu32_finish(gls_ctx *c) {
   auto &mg = c->mg;
   if (!mg.lu_pending) return GLS_OK;
   mg.lu_pending = false;
+  mg.side.join();
+  (void)rocblas_set_stream(mg.blas, c->stream);
+  if (mg.side.rc) {
+    mg.direct_ok = mg.lu32 = false;
+    mg.dirty = true;
+    return set_err(GLS_EHIP, "coarse FP32 LU on the side stream failed (step %d)", mg.side.rc);
+  }
   const int64_t n = mg.lu_n;
   int inf = -1;
   double rn = INFINITY;
@@ -5169,8 +5202,8 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       I.mc_solve = true;
       int64_t maxrow = 0;
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
-      I.mc_factor = maxrow <= gls::kIluMaxRow && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
-      I.mc_compact = maxrow <= gls::kIluCompactRow && rowp.back() < (int64_t(1) << 36);
+      I.mc_factor = maxrow <= gls::kIluMaxRow && rowp.back() < (int64_t(1) << 35) && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
+      I.mc_compact = maxrow <= gls::kIluCompactRow;
       if (I.mc_factor) {  // the position map (uint16 per entry), when it fits a quarter of free memory
         mc_moff_h.assign((size_t)n + 1, 0);
         for (int64_t r = 0; r < n; ++r) {

@@ -189,10 +189,10 @@ __device__ __forceinline__ int lds_find(const int32_t *c, int lo, int hi, int32_
 // factors are bitwise those of the searching kernel.
 //
 // R: the LDS capacity of a row (entries; its pivots too). Every workgroup holds its group's rows and
-// pivot extents in LDS: 28 bytes per entry at R = kIluMaxRow (72 KB, two workgroups per CU). The
-// compact instantiation (R = kIluCompactRow, rows of Q2-Q1 3D cells: <= 402 entries) packs each pivot's
-// diagonal position (36 bits), upper length (10) and map offset (18) into one word: 20 bytes per entry,
-// 36 KB, four workgroups per CU -- twice the waves to hide the step's LDS / division latency chain
+// pivot extents in LDS, each pivot's diagonal position (35 bits), upper length (10) and map offset (19) packed
+// into one word: 20 bytes per entry, 51 KB at R = kIluMaxRow (three workgroups per CU; unpacked, 72 KB and
+// two), 36 KB at R = kIluCompactRow (rows of Q2-Q1 3D cells of valence <= 8: <= 402 entries; four per CU)
+// -- waves to hide the step's LDS / division latency chain
 constexpr uint16_t kMapMiss = 0xffff;
 template <bool MAP, int NS, int R>
 __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *__restrict__ grow, int g0, int g1,
@@ -202,13 +202,11 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
                                                                 const int64_t *__restrict__ didx, double boost_tol,
                                                                 double boost_val, const int64_t *__restrict__ moff,
                                                                 const uint16_t *__restrict__ map) {
-  constexpr bool PACK = R <= kIluCompactRow;
+  static_assert(R < 1024 && R * R < (1 << 19), "packed pivot extents");
   __shared__ int32_t sc[kMaxGroupRows][R + 1];
   __shared__ double sv[kMaxGroupRows][R + 1];  // + a dummy slot for the MAP step's idle lanes
-  // pivot-row extents: the diagonal's position and the upper part's length (PACK: with the map offset in one word)
-  __shared__ int64_t sdk[kMaxGroupRows][R];
-  __shared__ int32_t sul[PACK ? 1 : kMaxGroupRows][PACK ? 1 : R];
-  __shared__ int32_t smo[MAP && !PACK ? kMaxGroupRows : 1][MAP && !PACK ? R : 1];  // per pivot: map offset in the row
+  // pivot-row extents: the diagonal's position, the upper part's length and the map offset in the row, one word
+  __shared__ uint64_t sdk[kMaxGroupRows][R];
   const int g = g0 + (int)blockIdx.x;
   if (g >= g1) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -256,15 +254,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
         mo = mrun + x - m;
         mrun += __shfl(x, 63, 64);
       }
-      if (p < nl) {
-        if (PACK) {
-          sdk[w][p] = dk | ((int64_t)ul << 36) | ((int64_t)mo << 46);
-        } else {
-          sdk[w][p] = dk;
-          sul[w][p] = ul;
-          if (MAP) smo[w][p] = mo;
-        }
-      }
+      if (p < nl) sdk[w][p] = (uint64_t)dk | ((uint64_t)ul << 35) | ((uint64_t)mo << 45);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -280,14 +270,14 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     // waitcnt pass sees straight-line code and waits for exactly the stage in use, not vmcnt(0)
     auto issue = [&](int p, Stage &st) {
       const bool in = p < nl;
-      const int64_t pk = in ? sdk[w][p] : 0;
-      st.dk = in ? (PACK ? pk & ((int64_t(1) << 36) - 1) : pk) : rp;
-      st.e1 = in ? st.dk + 1 + (PACK ? (int)((pk >> 36) & 1023) : sul[w][p]) : rp;
+      const uint64_t pk = in ? sdk[w][p] : 0;
+      st.dk = in ? (int64_t)(pk & ((uint64_t(1) << 35) - 1)) : rp;
+      st.e1 = in ? st.dk + 1 + (int)((pk >> 35) & 1023) : rp;
       st.piv = val[st.dk];
       if (MAP) {  // lane l: the quad of upper entries 4l .. 4l+3 (one 8-byte map load, one address
                   // for the values; past the row's end they are masked in the step, and the value
                   // array is padded for the last rows)
-        st.mo = in ? (PACK ? (int)((uint64_t)pk >> 46) : smo[w][p]) : 0;
+        st.mo = in ? (int)(pk >> 45) : 0;
         const bool ok = 4 * lane < st.e1 - st.dk - 1;
         st.mq = reinterpret_cast<const uint64_t *>(map + mbase + st.mo)[ok ? lane : 0];
         const double *vp = val + st.dk + 1 + 4 * lane;

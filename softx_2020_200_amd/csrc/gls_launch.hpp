@@ -127,8 +127,8 @@ hipError_t gather_element_vectors_b(double *y, const double *ev, const int64_t *
 constexpr int kMaxGroupRows = 4;
 // multicolor ILU numeric factorization in place (same structures; rows of <= kIluMaxRow entries)
 constexpr int kIluMaxRow = 640;
-// the compact factorization (twice the workgroups per CU): rows of <= kIluCompactRow entries (Q2-Q1 3D: <= 402), fewer
-// than 2^36 entries in all
+// the compact factorization (four workgroups per CU instead of three): rows of <= kIluCompactRow entries (Q2-Q1 3D
+// cells of vertex valence <= 8: <= 402). Either needs fewer than 2^35 entries in all.
 constexpr int kIluCompactRow = 448;
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
                          const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
