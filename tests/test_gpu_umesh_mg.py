@@ -70,3 +70,42 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k, kp, smoother):
     print("umesh GMG %s Q%dQ%d %s: %d levels %s DoFs, GMRES its %d (Jacobi %d)" % (name, k, kp, smoother, len(probs),
                                                                            [q.n_dofs for q in probs], its_mg, its_j))
     assert its_mg * 2 < its_j, (its_mg, its_j)
+
+
+@pytest.mark.gpu
+def test_large_coarsest_level_fp32_lu(monkeypatch, capfd):
+    """a coarsest level above 8192 DoFs (the Q2-Q1 cylinder shell at refinement 2, 30816 DoFs, under its
+    refinement-3 level): the FP32 unpivoted LU factored by the worker thread on the side stream, its check
+    |A x - 1| / |1| < 1e-2 taken (no pivoted fallback), and the V-cycle-preconditioned GMRES converging"""
+    from softx_2020_200_amd.native import UMesh
+    m = UMesh(3, "cylinder_shell", "1 : 0.25 : 1 : 8 : 2")
+    m.refine_global(3)
+    hf = m.fe_space_handle(2, 1, qmapping_all=True)
+    hc = m.coarsen_to(2).fe_space_handle(2, 1, qmapping_all=True)
+    probs = [mapped_level(h.data, 1.0) for h in (hf, hc)]
+    assert 8192 < probs[1].n_dofs <= 40000, probs[1].n_dofs
+    p = probs[0]
+    Xv = hf.data["vnode_x"]
+    u = np.concatenate([np.stack([-Xv[:, 1], Xv[:, 0], 0.3 * np.sin(3 * Xv[:, 2])], 1).reshape(-1),
+                        np.cos(hf.data["pnode_x"][:, 0])])
+    p.apply_nonzero_constraints(u)
+    ctxs = [context_for(q) for q in probs]
+    monkeypatch.setenv("GLS_MG_VERBOSE", "1")
+    ctxs[0].attach_multigrid_transfers(ctxs[1:], [hf.mg_transfer_from(hc)], pre_smooth=1, post_smooth=1, omega=0.6,
+                                       coarse_direct=1, smoother="ilu")
+    U = cuda(u)
+    ctxs[0].apply_dirichlet(U)
+    ctxs[0].set_state(U, cuda(np.zeros(p.n_dofs)))
+    rhs = ctxs[0].residual()
+    x, its, res, ok = ctxs[0].solve_linear(rhs, ctxs[0].zeros(), max_iterations=200, restart=50,
+                                           relative_residual=1e-8, minimum_residual=1e-300, true_residual=True)
+    monkeypatch.delenv("GLS_MG_VERBOSE")
+    import ctypes
+    ctypes.CDLL(None).fflush(None)  # the library's printf lines (stdout is a pipe under pytest: block-buffered)
+    log = capfd.readouterr().out
+    checks = [float(l.rsplit("=", 1)[1]) for l in log.splitlines() if "unpivoted LU" in l and "check" in l]
+    print("large coarsest level: %d DoFs, GMRES its %d, LU checks %s" % (probs[1].n_dofs, its, checks))
+    assert ok and res <= 1e-8 * float(rhs.norm()) * 1.01, (its, res)
+    assert checks and max(checks) < 1e-2, log[-2000:]
+    assert "pivoted LU + inverse" not in log, log[-2000:]
+    assert its <= 40, its
