@@ -1245,14 +1245,77 @@ struct Solver {
     const bool sep = mm.kp != mm.k;
     const int dim = mm.dim, nvc = dim == 3 ? (mm.k + 1) * (mm.k + 1) * (mm.k + 1) : (mm.k + 1) * (mm.k + 1);
     const int npc = dim == 3 ? (mm.kp + 1) * (mm.kp + 1) * (mm.kp + 1) : (mm.kp + 1) * (mm.kp + 1);
+    // what a p::d triangulation hands this rank (dist.py local_part, the gls_dpart_create contract): its owned
+    // cells (the equal-count range of the cell order) plus the ghost layer -- every cell touching a node of an
+    // owned cell, a master of a line on one, or the DoF node of a line one of whose masters it touches -- with
+    // owners, node keys (= the global node ids) and those cells' lines in DoF keys; the partition is built
+    // from that part alone (gls_dpart_create), not from the global arrays
+    const int64_t cb = mm.nc * rank / world, ce = mm.nc * (rank + 1) / world, NVD0 = (int64_t)dim * mm.nv;
+    const int64_t nun = mm.nv + (sep ? mm.np : 0);
+    auto unode = [&](int64_t g) { return g < NVD0 ? g / dim : (sep ? mm.nv : 0) + g - NVD0; };  // DoF -> node
+    auto dkey = [&](int64_t g) {  // DoF -> DoF key (node key * (dim + 1) + component, dim for pressure)
+      return g < NVD0 ? (g / dim) * (dim + 1) + g % dim : (g - NVD0) * (dim + 1) + dim;
+    };
+    auto cell_touch = [&](int64_t c, const std::vector<uint8_t> &S) {
+      for (int a = 0; a < nvc; ++a)
+        if (S[(size_t)mm.cv[(size_t)(c * nvc + a)]]) return true;
+      if (sep)
+        for (int a = 0; a < npc; ++a)
+          if (S[(size_t)(mm.nv + mm.cp[(size_t)(c * npc + a)])]) return true;
+      return false;
+    };
+    std::vector<uint8_t> S((size_t)nun, 0);
+    for (int64_t c = cb; c < ce; ++c) {
+      for (int a = 0; a < nvc; ++a) S[(size_t)mm.cv[(size_t)(c * nvc + a)]] = 1;
+      if (sep)
+        for (int a = 0; a < npc; ++a) S[(size_t)(mm.nv + mm.cp[(size_t)(c * npc + a)])] = 1;
+    }
+    {
+      std::vector<uint8_t> add(S);
+      for (size_t i = 0; i < ld.size(); ++i)
+        for (int64_t j = lo[i]; j < lo[i + 1]; ++j) {
+          const int64_t dn = unode(ld[i]), mn = unode(lm[(size_t)j]);
+          if (S[(size_t)dn]) add[(size_t)mn] = 1;  // masters of the lines on the owned cells' nodes
+          if (S[(size_t)mn]) add[(size_t)dn] = 1;  // DoF nodes of the lines whose master an owned cell touches
+        }
+      S.swap(add);
+    }
+    std::vector<int32_t> powner;
+    std::vector<int64_t> pvk, ppk;
+    std::vector<uint8_t> pnode((size_t)nun, 0);
+    for (int64_t c = 0; c < mm.nc; ++c) {
+      if (!cell_touch(c, S)) continue;
+      int r = (int)std::min<int64_t>(world - 1, c * world / std::max<int64_t>(mm.nc, 1));
+      while (r > 0 && c < mm.nc * r / world) --r;
+      while (r < world - 1 && c >= mm.nc * (r + 1) / world) ++r;
+      powner.push_back(r);
+      for (int a = 0; a < nvc; ++a) {
+        pvk.push_back(mm.cv[(size_t)(c * nvc + a)]);
+        pnode[(size_t)mm.cv[(size_t)(c * nvc + a)]] = 1;
+      }
+      if (sep)
+        for (int a = 0; a < npc; ++a) {
+          ppk.push_back(mm.cp[(size_t)(c * npc + a)]);
+          pnode[(size_t)(mm.nv + mm.cp[(size_t)(c * npc + a)])] = 1;
+        }
+    }
+    std::vector<int64_t> lkd, lko{0}, lkm;  // the part's lines (DoF node on a provided cell), in DoF keys
+    for (size_t i = 0; i < ld.size(); ++i) {
+      if (!pnode[(size_t)unode(ld[i])]) continue;
+      lkd.push_back(dkey(ld[i]));
+      for (int64_t j = lo[i]; j < lo[i + 1]; ++j) lkm.push_back(dkey(lm[(size_t)j]));
+      lko.push_back((int64_t)lkm.size());
+    }
     gls_gpart *gp = nullptr;
-    ck(gls_gpart_create(dim, mm.k, mm.kp, mm.nc, mm.cv.data(), sep ? mm.cp.data() : nullptr, mm.nv, mm.np,
-                        (int64_t)ld.size(), ld.data(), lo.data(), lm.data(), rank, world, &gp),
-       "gls_gpart_create");
-    int64_t cb, ce, nvl, npl, nov, nop, ns, nr;
+    ck(gls_dpart_create(dim, mm.k, mm.kp, (int64_t)powner.size(), powner.data(), pvk.data(), sep ? ppk.data() : nullptr,
+                        (int64_t)lkd.size(), lkd.data(), lko.data(), lkm.data(), rank, world, &gp),
+       "gls_dpart_create");
+    int64_t cb_l, ce_l, nvl, npl, nov, nop, ns, nr;
     int nn;
-    ck(gls_gpart_sizes(gp, &cb, &ce, &nvl, &npl, &nov, &nop, &nn, &ns, &nr), "gls_gpart_sizes");
-    const int64_t ncl = ce - cb;
+    ck(gls_gpart_sizes(gp, &cb_l, &ce_l, &nvl, &npl, &nov, &nop, &nn, &ns, &nr), "gls_gpart_sizes");
+    const int64_t ncl = ce_l - cb_l;
+    if (ncl != ce - cb) die("--np: the local part's owned cells (%lld) differ from the rank's range (%lld)", (long long)ncl,
+                            (long long)(ce - cb));
     std::vector<int32_t> lcv((size_t)(ncl * nvc)), lcp(sep ? (size_t)(ncl * npc) : 0), sd((size_t)ns), rd((size_t)nr);
     std::vector<int64_t> vl2g((size_t)nvl), pl2g((size_t)npl), soff((size_t)nn + 1, 0), roff((size_t)nn + 1, 0);
     std::vector<int> nbrs((size_t)nn);
