@@ -392,6 +392,7 @@ struct gls_ctx {
     bool mc_solve = false;
     bool mc_factor = false;  // multicolor order: color-by-color numeric factorization (no rocSPARSE csrilu0)
     bool mc_compact = false;  // ... by the compact-LDS kernel (rows <= kIluCompactRow)
+    DevBuf<double> rdiag;     // ... its 1 / U_ii per row
     std::vector<uint8_t> mc_wl, mc_wu;  // per color: wavefronts per node group in the lower / upper solve
     DevBuf<int64_t> mc_desc;   // per node group: the solves' descriptor (gls::kGroupDesc int64)
     DevBuf<int64_t> mc_moff;   // factorization position map: per row, its first entry
@@ -3194,7 +3195,7 @@ static int ensure_ilu(gls_ctx *c) {
   if (I.mc_factor)
     HIP_TRY(gls::ilu_mc_factor(I.mc_grow.p, I.mc_cg.data(), (int)I.mc_cg.size() - 1, I.rowp.p, I.col.p, I.val.p,
                                I.mc_lsp.p, I.didx.p, I.boost_tol, I.boost_val, I.mc_moff.p,
-                               I.mc_map.n ? I.mc_map.p : nullptr, I.mc_compact, s));
+                               I.mc_map.n ? I.mc_map.p : nullptr, I.mc_compact, I.rdiag.p, s));
   else
     RS_TRY(rocsparse_dcsrilu0(I.h, m, nnz, I.dA, I.val.p, I.rowp32.p, I.col.p, I.info, rocsparse_solve_policy_auto, I.work.p));
   I.valid = true;
@@ -5204,6 +5205,7 @@ extern "C" int gls_ilu_attach(gls_ctx *c, int fill, double athresh, double rthre
       for (int64_t r = 0; r < n; ++r) maxrow = std::max(maxrow, rowp[(size_t)r + 1] - rowp[(size_t)r]);
       I.mc_factor = maxrow <= gls::kIluMaxRow && rowp.back() < (int64_t(1) << 35) && !std::getenv("GLS_ILU_ROCSPARSE_FACTOR");
       I.mc_compact = maxrow <= gls::kIluCompactRow;
+      if (I.mc_factor) GLS_TRY(I.rdiag.alloc((size_t)n));
       if (I.mc_factor) {  // the position map (uint16 per entry), when it fits a quarter of free memory
         mc_moff_h.assign((size_t)n + 1, 0);
         for (int64_t r = 0; r < n; ++r) {

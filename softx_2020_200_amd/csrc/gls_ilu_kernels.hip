@@ -201,7 +201,8 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
                                                                 const int64_t *__restrict__ lsp,
                                                                 const int64_t *__restrict__ didx, double boost_tol,
                                                                 double boost_val, const int64_t *__restrict__ moff,
-                                                                const uint16_t *__restrict__ map) {
+                                                                const uint16_t *__restrict__ map,
+                                                                double *__restrict__ rdiag) {
   static_assert(R < 1024 && R * R < (1 << 19), "packed pivot extents");
   __shared__ int32_t sc[kMaxGroupRows][R + 1];
   __shared__ double sv[kMaxGroupRows][R + 1];  // + a dummy slot for the MAP step's idle lanes
@@ -260,7 +261,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const int64_t mbase = MAP ? moff[i] : 0;
     struct Stage {
-      double piv, v[PF];
+      double rpiv, v[PF];  // rpiv: 1 / U_kk of the pivot row (rdiag, written with the row)
       int64_t dk, e1;
       int c[PF], mo;  // c: the upper entries' columns
       uint64_t mq;            // MAP: the row positions of the lane's quad, 4 x 16 bit (unpacked only
@@ -273,7 +274,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
       const uint64_t pk = in ? sdk[w][p] : 0;
       st.dk = in ? (int64_t)(pk & ((uint64_t(1) << 35) - 1)) : rp;
       st.e1 = in ? st.dk + 1 + (int)((pk >> 35) & 1023) : rp;
-      st.piv = val[st.dk];
+      st.rpiv = rdiag[in ? sc[w][p] : 0];
       if (MAP) {  // lane l: the quad of upper entries 4l .. 4l+3 (one 8-byte map load, one address
                   // for the values; past the row's end they are masked in the step, and the value
                   // array is padded for the last rows)
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
       }
     };
     auto step = [&](int p, const Stage &st) {
-      const double lik = sv[w][p] / st.piv;
+      const double lik = sv[w][p] * st.rpiv;  // (a division here sat on the step's dependency chain)
       if (MAP) {  // branchless: all four reads, then all four writes (idle lanes on the dummy slot)
         const int m = (int)(st.e1 - st.dk - 1);
         int qa[PF];
@@ -380,6 +381,7 @@ __global__ void __launch_bounds__(64 * kMaxGroupRows) k_mc_ilu0(const int32_t *_
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       }
       if (lane == 0 && fabs(sv[w][pd]) <= boost_tol) sv[w][pd] = boost_val;
+      if (lane == 0) rdiag[i] = 1.0 / sv[w][pd];
     }
     __syncthreads();
   }
@@ -426,14 +428,15 @@ hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col,
 
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
                          const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
-                         double boost_val, const int64_t *moff, const uint16_t *map, bool compact, hipStream_t s) {
+                         double boost_val, const int64_t *moff, const uint16_t *map, bool compact, double *rdiag,
+                         hipStream_t s) {
   for (int c = 0; c < n_colors; ++c) {
     const int g0 = color_groups[c], g1 = color_groups[c + 1];
     if (g1 <= g0) continue;
     const dim3 gr((unsigned)(g1 - g0)), bl(64 * kMaxGroupRows);
 #define GLS_MC_ILU0(MAP, R)                                                                                 \
   hipLaunchKernelGGL((k_mc_ilu0<MAP, 3, R>), gr, bl, 0, s, grow, g0, g1, rowp, col, val, lsp, didx, boost_tol, \
-                     boost_val, moff, map)
+                     boost_val, moff, map, rdiag)
     if (map && compact) GLS_MC_ILU0(true, kIluCompactRow);
     else if (map) GLS_MC_ILU0(true, kIluMaxRow);
     else if (compact) GLS_MC_ILU0(false, kIluCompactRow);

@@ -132,7 +132,8 @@ constexpr int kIluMaxRow = 640;
 constexpr int kIluCompactRow = 448;
 hipError_t ilu_mc_factor(const int32_t *grow, const int32_t *color_groups, int n_colors, const int64_t *rowp,
                          const int32_t *col, double *val, const int64_t *lsp, const int64_t *didx, double boost_tol,
-                         double boost_val, const int64_t *moff, const uint16_t *map, bool compact, hipStream_t s);
+                         double boost_val, const int64_t *moff, const uint16_t *map, bool compact, double *rdiag,
+                         hipStream_t s);  // rdiag (n): 1 / U_ii, written row by row (read for the later colors' pivots)
 // the factorization's row-position map (map == nullptr in ilu_mc_factor: column searches instead)
 hipError_t ilu_mc_factor_map(int64_t n, const int64_t *rowp, const int32_t *col, const int64_t *lsp,
                              const int64_t *didx, const int64_t *moff, uint16_t *map, hipStream_t s);
