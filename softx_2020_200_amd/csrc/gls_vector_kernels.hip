@@ -399,12 +399,18 @@ __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ e
   if (act) act += (int64_t)blockIdx.y * nblk;  // batched probing: cell batches the kernel skipped hold 0
   auto live = [&](int64_t slot) { return !act || act[slot / el / cb]; };
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  constexpr int kIn = 8;  // incidences gathered at once (all slots, then all values: one dependent round each)
-  if (i < nv && !act && voff[i + 1] - voff[i] <= kIn) {
+  constexpr int kIn = 8;  // incidences gathered at once (all slots, then all activity flags, then all values: one
+                          // dependent round each; the batched probes walked them one by one, 160 us per launch at
+                          // 1.72 M DoFs)
+  if (i < nv && voff[i + 1] - voff[i] <= kIn) {
     const int64_t j0 = voff[i], nj = voff[i + 1] - j0;
     int64_t sl[kIn];
 #pragma unroll
     for (int t = 0; t < kIn; ++t) sl[t] = t < nj ? vslot[j0 + t] : -1;
+    if (act) {
+#pragma unroll
+      for (int t = 0; t < kIn; ++t) sl[t] = sl[t] >= 0 && live(sl[t]) ? sl[t] : -1;
+    }
     double e[kIn][3];
 #pragma unroll
     for (int t = 0; t < kIn; ++t)
@@ -412,8 +418,8 @@ __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ e
       for (int c = 0; c < 3; ++c) e[t][c] = (sl[t] >= 0 && c < dim) ? ev[sl[t] + c] : 0.;
     double acc[3] = {0., 0., 0.};
 #pragma unroll
-    for (int t = 0; t < kIn; ++t)  // ascending slot order, as the general loop below
-      if (t < nj)
+    for (int t = 0; t < kIn; ++t)  // ascending slot order, as the general loop below (skipped slots add nothing)
+      if (sl[t] >= 0)
 #pragma unroll
         for (int c = 0; c < 3; ++c) acc[c] += e[t][c];
     for (int c = 0; c < dim; ++c) y[i * dim + c] = acc[c];
@@ -425,6 +431,23 @@ __global__ void k_gather_ev(double *__restrict__ y, const double *__restrict__ e
       for (int c = 0; c < dim; ++c) acc[c] += e[c];
     }
     for (int c = 0; c < dim; ++c) y[i * dim + c] = acc[c];
+  } else if (i < nv + np && poff[i - nv + 1] - poff[i - nv] <= kIn) {
+    const int64_t q = i - nv, j0 = poff[q], nj = poff[q + 1] - j0;
+    int64_t sl[kIn];
+#pragma unroll
+    for (int t = 0; t < kIn; ++t) sl[t] = t < nj ? pslot[j0 + t] : -1;
+    if (act) {
+#pragma unroll
+      for (int t = 0; t < kIn; ++t) sl[t] = sl[t] >= 0 && live(sl[t]) ? sl[t] : -1;
+    }
+    double e[kIn];
+#pragma unroll
+    for (int t = 0; t < kIn; ++t) e[t] = sl[t] >= 0 ? ev[sl[t]] : 0.;
+    double acc = 0.;
+#pragma unroll
+    for (int t = 0; t < kIn; ++t)
+      if (sl[t] >= 0) acc += e[t];
+    y[dim * nv + q] = acc;
   } else if (i < nv + np) {
     const int64_t q = i - nv;
     double acc = 0.;
