@@ -3850,7 +3850,8 @@ int gls_mg_detach(gls_ctx *c) {
 // --------------------------------------------------------------------------------------------
 // GMRES(m), right preconditioned (Jacobi, the V-cycle or the assembled ILU). Orthogonalisation:
 // Gram-corrected classical Gram–Schmidt (one projection pass per iteration, see the loop) or, with
-// GLS_GMRES_CGS2=1, classical Gram–Schmidt with one DGKS re-orthogonalisation pass; fused multi-dot /
+// gls_linear_params.orthogonalization = GLS_ORTHO_CGS2, classical Gram–Schmidt with one DGKS re-orthogonalisation
+// pass; fused multi-dot /
 // multi-axpy kernels (one pass over the Krylov basis per Gram–Schmidt sweep). Stopping test on the unpreconditioned residual
 // ||b - A x|| <= max(rel*||b||, abs) (deal.II SolverControl / AztecOO AZ_noscaled).
 // --------------------------------------------------------------------------------------------
