@@ -204,14 +204,21 @@ typedef struct {
   double omega;                               /* damped-Jacobi weight of the smoother, 0 -> 0.6 */
   double coarse_omega;                        /* weight of the coarsest-level sweeps, 0 -> omega */
   int coarse_direct;                          /* coarsest level: 0 auto (exact solve when on one GPU
-                                                 with <= 2048 DoFs), 1 exact solve (<= 8192 DoFs), -1
-                                                 Jacobi sweeps. The exact solve probes the coarsest
-                                                 Jacobian and inverts it by rocSOLVER LU with the
-                                                 first pressure DoF pinned (the enclosed-flow gauge):
-                                                 unpivoted by default, the inverse checked by
-                                                 max|A (A^-1 e) - e| and finiteness; a zero pivot or a
-                                                 failed check refactors with partial pivoting
-                                                 (GLS_MG_COARSE_SOLVER=lu: always pivoted) */
+                                                 with <= 2048 DoFs), 1 direct solve (<= 40000 DoFs;
+                                                 a gls_mg_attach_replica level <= 8192),
+                                                 -1 Jacobi sweeps. The direct solve probes the coarsest
+                                                 Jacobian and factors it by rocSOLVER LU with the
+                                                 first pressure DoF pinned (the enclosed-flow gauge).
+                                                 Up to 8192 DoFs FP64: unpivoted by default, the
+                                                 inverse checked by max|A (A^-1 e) - e| and finiteness;
+                                                 a zero pivot or a failed check refactors with partial
+                                                 pivoting (GLS_MG_COARSE_SOLVER=lu: always pivoted).
+                                                 Above: FP32 unpivoted (sgetrf_npvt by a library worker
+                                                 thread on a side stream, overlapping the finer levels'
+                                                 setup), applied by blocked triangular solves; checked
+                                                 by |A x - 1| / |1|: < 1e-3 as it is, < 0.5 with one
+                                                 refinement step against the FP64 matrix, else pivoted
+                                                 FP32 LU + explicit inverse */
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32
                                                  arithmetic from an FP32 copy of the linearization
                                                  (brick path; vectors, transfers and the outer GMRES
