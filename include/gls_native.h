@@ -216,7 +216,7 @@ typedef struct {
                                                  Above: FP32 unpivoted (sgetrf_npvt by a library worker
                                                  thread on a side stream, overlapping the finer levels'
                                                  setup), applied by blocked triangular solves; checked
-                                                 by |A x - 1| / |1|: < 1e-3 as it is, < 0.5 with one
+                                                 by |A x - 1| / |1|: < 1e-2 as it is, < 0.5 with one
                                                  refinement step against the FP64 matrix, else pivoted
                                                  FP32 LU + explicit inverse */
   int mixed_precision;                        /* 1: the V-cycle's smoothing / residual J.v run in FP32

@@ -521,6 +521,13 @@ struct gls_ctx {
     bool lu32 = false;
     bool lu32_npvt = false;  // the FP32 factor is unpivoted (applied by dense_lu_solve_f32), else an explicit inverse
     bool lu32_refine = false;  // ... applied with one step of iterative refinement against the FP64 matrix
+    // banded coarse matrix: the probed CSR's Cuthill-McKee order kept (the dense array holds A in that order), its
+    // lower / upper bandwidths; the factorization works by column blocks as wide as the band (no fill outside it
+    // without pivoting) and the solves skip the blocks outside it. configs[4]'s 25 k-DoF Q1-Q1 p-level: ~1.9 k
+    bool lu_cm = false;
+    int64_t lu_bl = -1, lu_bu = -1, lu_pin_cm = -1;
+    DevBuf<int32_t> lu_ident;  // identity permutation (csr_to_dense in the CSR's own order)
+    DevBuf<double> lu_tmp;     // the coarse right-hand side / correction in that order
     DevBuf<float> probe32, b32, x32;
     DevBuf<double> chk32;    // the FP32 factor's check: A x - b for b = 1 (FP64)
     int64_t npvt_ipiv_n = -1;  // ipiv holds the identity permutation of this size (unpivoted LU)
@@ -2403,22 +2410,45 @@ int coarse_lu32_start(gls_ctx *c, int64_t n, int64_t pin) {
   mg.side.rc = 0;
   auto *m = &mg;
   const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
-  mg.side.worker = std::thread([m, s, n, pin, dev, verbose]() {
+  const int64_t bl = mg.lu_cm ? mg.lu_bl : -1, bu = mg.lu_cm ? mg.lu_bu : -1;
+  mg.side.worker = std::thread([m, s, n, pin, dev, verbose, bl, bu]() {
     const double one = 1.0, mone = -1.0;
     int &rc = m->side.rc;
     const auto h0 = std::chrono::steady_clock::now();
+    // banded: right-looking by column blocks as wide as the band (rocSOLVER's calls return only when done, so few
+    // wide blocks: 256-wide ones took 98 calls and longer than the dense factorization, profiles/
+    // r06_ab_banded_coarse_lu.txt): the block's panel down to the lower band, its rows of U to the upper band, the
+    // trailing band update; without pivoting nothing outside the band fills
+    const int64_t nb = bl < 0 ? n : std::max<int64_t>(512, ((std::max(bl, bu) + 255) / 256) * 256);
     if (hipSetDevice(dev) != hipSuccess) rc = 1;
     else if (rocblas_set_stream(m->blas, s) != rocblas_status_success) rc = 2;
-    else if (rocsolver_sgetrf_npvt(m->blas, (rocblas_int)n, (rocblas_int)n, m->probe32.p, (rocblas_int)n, m->info.p) !=
-             rocblas_status_success)
-      rc = 3;
+    const float fone = 1.0f, fmone = -1.0f;
+    float *A = m->probe32.p;
+    for (int64_t k0 = 0; k0 < n && !rc; k0 += nb) {
+      const int64_t kb = std::min(nb, n - k0), mr = bl < 0 ? n - k0 : std::min(n - k0, kb + bl);
+      const int64_t nc = bl < 0 ? 0 : std::min(n - k0 - kb, bu);
+      float *A11 = A + k0 + k0 * n, *A12 = A + k0 + (k0 + kb) * n;
+      if (rocsolver_sgetrf_npvt(m->blas, (rocblas_int)mr, (rocblas_int)kb, A11, (rocblas_int)n, m->info.p) !=
+          rocblas_status_success)
+        rc = 3;
+      else if (nc > 0 &&
+               rocblas_strsm(m->blas, rocblas_side_left, rocblas_fill_lower, rocblas_operation_none, rocblas_diagonal_unit,
+                             (rocblas_int)kb, (rocblas_int)nc, &fone, A11, (rocblas_int)n, A12, (rocblas_int)n) !=
+                   rocblas_status_success)
+        rc = 3;
+      else if (nc > 0 && mr > kb &&
+               rocblas_sgemm(m->blas, rocblas_operation_none, rocblas_operation_none, (rocblas_int)(mr - kb),
+                             (rocblas_int)nc, (rocblas_int)kb, &fmone, A11 + kb, (rocblas_int)n, A12, (rocblas_int)n,
+                             &fone, A12 + kb, (rocblas_int)n) != rocblas_status_success)
+        rc = 3;
+    }
     if (verbose)
-      std::printf("mg: sgetrf_npvt returned to its worker thread after %.2f ms\n",
+      std::printf("mg: the %s FP32 LU returned to its worker thread after %.2f ms\n", bl < 0 ? "dense" : "banded",
                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count());
     if (!rc &&
         !(gls::vec_fill(m->chk32.p, n, 1.0, s) == hipSuccess && gls::mg_zero_row(m->chk32.p, 1, pin, s) == hipSuccess &&
           gls::vec_to_f32(m->chk32.p, m->x32.p, n, s) == hipSuccess &&
-          gls::dense_lu_solve_f32(m->probe32.p, (int)n, m->x32.p, s) == hipSuccess &&
+          gls::dense_lu_solve_f32(m->probe32.p, (int)n, m->x32.p, s, (int)bl, (int)bu) == hipSuccess &&
           gls::vec_from_f32(m->x32.p, m->chk32.p + n, n, s) == hipSuccess &&
           rocblas_dgemv(m->blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, m->probe.p,
                         (rocblas_int)n, m->chk32.p + n, 1, &mone, m->chk32.p, 1) == rocblas_status_success &&
@@ -2455,10 +2485,10 @@ int coarse_lu32_finish(gls_ctx *c) {
   HIP_TRY(hipStreamSynchronize(mg.side.s));
   const double rel = inf == 0 ? rn / std::sqrt((double)n) : INFINITY;
   const bool verbose = std::getenv("GLS_MG_VERBOSE") != nullptr;
-  // (below 1e-3 the correction is used as it is; up to 0.5 with one refinement step x += LU^-1 (b - A x) against the
+  // (below 1e-2 the correction is used as it is; up to 0.5 with one refinement step x += LU^-1 (b - A x) against the
   // FP64 matrix (an extra solve and one FP64 matrix pass per coarse solve: residual error ~ rel^2); beyond, or a
   // broken factorization, the pivoted route)
-  mg.lu32_refine = inf == 0 && rel >= 1e-3 && rel < 0.5;
+  mg.lu32_refine = inf == 0 && rel >= 1e-2 && rel < 0.5;
   if (verbose)
     std::printf("mg: coarse FP32 unpivoted LU n=%lld info=%d, check |A x - 1| / |1| = %.2e%s\n", (long long)n, inf, rel,
                 mg.lu32_refine ? ", applied with one refinement step" : "");
@@ -2578,7 +2608,33 @@ int mg_prepare(gls_ctx *c) {
       GLS_TRY(ilu_probe(g));
       HIP_TRY(hipMemsetAsync(mg.probe.p, 0, sizeof(double) * (size_t)(n * n), c->stream));
       const auto &I = g->ilu;
-      HIP_TRY(gls::csr_to_dense(mg.probe.p, I.rowp.p, I.col.p, I.val.p, I.perm.p, mg.pinv.p, n, c->stream));
+      mg.lu_cm = n > kDirectSmall;
+      if (mg.lu_cm) {  // FP32 range: keep the CSR's Cuthill-McKee order (banded), bandwidths from its pattern once
+        if (mg.lu_bl < 0) {
+          std::vector<int64_t> rp((size_t)n + 1);
+          std::vector<int32_t> cl((size_t)I.nnz), pm((size_t)n), id((size_t)n);
+          HIP_TRY(hipMemcpy(rp.data(), I.rowp.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(cl.data(), I.col.p, sizeof(int32_t) * cl.size(), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(pm.data(), I.perm.p, sizeof(int32_t) * pm.size(), hipMemcpyDeviceToHost));
+          int64_t bl = 0, bu = 0;
+          for (int64_t r = 0; r < n; ++r)
+            for (int64_t e = rp[(size_t)r]; e < rp[(size_t)r + 1]; ++e) {
+              bl = std::max<int64_t>(bl, r - cl[(size_t)e]);
+              bu = std::max<int64_t>(bu, cl[(size_t)e] - r);
+            }
+          for (int64_t i = 0; i < n; ++i) id[(size_t)i] = (int32_t)i;
+          GLS_TRY(mg.lu_ident.upload(id.data(), id.size()));
+          GLS_TRY(mg.lu_tmp.alloc((size_t)n));
+          mg.lu_bl = bl;
+          mg.lu_bu = bu;
+          mg.lu_pin_cm = pm[(size_t)((int64_t)g->dim * g->n_vnodes)];  // the first pressure DoF's row
+          if (verbose) std::printf("mg: coarse matrix n=%lld in Cuthill-McKee order: bandwidths %lld / %lld\n", (long long)n,
+                                   (long long)bl, (long long)bu);
+        }
+        HIP_TRY(gls::csr_to_dense(mg.probe.p, I.rowp.p, I.col.p, I.val.p, mg.lu_ident.p, mg.pinv.p, n, c->stream));
+      } else {
+        HIP_TRY(gls::csr_to_dense(mg.probe.p, I.rowp.p, I.col.p, I.val.p, I.perm.p, mg.pinv.p, n, c->stream));
+      }
     } else {
       HIP_TRY(gls::vec_fill(mg.unit.p, n, 0.0, c->stream));
       for (int64_t j = 0; j < n; ++j) {
@@ -2590,8 +2646,10 @@ int mg_prepare(gls_ctx *c) {
     mg.lu = false;
     mg.lu32 = false;
     if (n > kDirectSmall) {  // FP32 LU of the pinned matrix: unpivoted (checked), else pivoted + explicit inverse
-      const int64_t pin = (int64_t)g->dim * g->n_vnodes;  // the first pressure DoF
-      if (pin >= n) return set_err(GLS_EINVAL, "mg: coarsest level without pressure DoFs");
+      const int64_t pin0 = (int64_t)g->dim * g->n_vnodes;  // the first pressure DoF
+      if (pin0 >= n) return set_err(GLS_EINVAL, "mg: coarsest level without pressure DoFs");
+      if (!(mg.probe_ilu == g && g->ilu.on)) mg.lu_cm = false;
+      const int64_t pin = mg.lu_cm ? mg.lu_pin_cm : pin0;  // (its row in the matrix's order)
       HIP_TRY(gls::mg_pin_dof(mg.probe.p, n, pin, c->stream));
       HIP_TRY(gls::vec_to_f32(mg.probe.p, mg.probe32.p, n * n, c->stream));
       GLS_TRY(coarse_lu32_start(c, n, pin));
@@ -2939,35 +2997,44 @@ int mg_vcycle(gls_ctx *c, int l, const double *b, double *x) {
   }
   if (l == L - 1 && mg.direct_ok) GLS_TRY(coarse_lu32_finish(c));
   if (l == L - 1 && mg.direct_ok) {  // exact coarsest-level solve
-    if (mg.lu32 && mg.lu32_npvt) {  // x = U^-1 L^-1 b in FP32, the pinned pressure DoF's correction zero
-      HIP_TRY(gls::vec_to_f32(b, mg.x32.p, n, c->stream));
-      HIP_TRY(gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, c->stream));
-      HIP_TRY(gls::vec_from_f32(mg.x32.p, x, n, c->stream));
-      if (mg.lu32_refine) {  // r = b - A x (the pinned FP64 matrix), x += LU^-1 r
-        const double one = 1.0, mone = -1.0;
-        double *r = mg.chk32.p, *dx = mg.chk32.p + n;
-        HIP_TRY(gls::vec_copy(r, b, n, c->stream));
-        if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-            rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &mone, mg.probe.p,
-                          (rocblas_int)n, x, 1, &one, r, 1) != rocblas_status_success)
-          return set_err(GLS_EHIP, "rocblas_dgemv failed");
-        HIP_TRY(gls::vec_to_f32(r, mg.x32.p, n, c->stream));
-        HIP_TRY(gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, c->stream));
-        HIP_TRY(gls::vec_from_f32(mg.x32.p, dx, n, c->stream));
-        HIP_TRY(gls::vec_axpy(x, 1.0, dx, n, c->stream));
+    if (mg.lu32) {  // the FP32 factor / inverse, in the matrix's order (banded: the CSR's Cuthill-McKee order)
+      const double *bb = b;
+      double *xx = x;
+      if (mg.lu_cm) {
+        HIP_TRY(gls::vec_permute(mg.lu_tmp.p, b, g->ilu.perm.p, n, 0, c->stream));
+        bb = xx = mg.lu_tmp.p;
       }
-      HIP_TRY(hipMemsetAsync(x + (int64_t)g->dim * g->n_vnodes, 0, sizeof(double), c->stream));
-      return GLS_OK;
-    }
-    if (mg.lu32) {  // x = A^-1 b in FP32, the pinned pressure DoF's correction zero
-      const float one = 1.0f, zero = 0.0f;
-      HIP_TRY(gls::vec_to_f32(b, mg.b32.p, n, c->stream));
-      if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
-          rocblas_sgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe32.p,
-                        (rocblas_int)n, mg.b32.p, 1, &zero, mg.x32.p, 1) != rocblas_status_success)
-        return set_err(GLS_EHIP, "rocblas_sgemv failed");
-      HIP_TRY(gls::vec_from_f32(mg.x32.p, x, n, c->stream));
-      HIP_TRY(hipMemsetAsync(x + (int64_t)g->dim * g->n_vnodes, 0, sizeof(double), c->stream));
+      if (mg.lu32_npvt) {  // x = U^-1 L^-1 b
+        const int bl = mg.lu_cm ? (int)mg.lu_bl : -1, bu = mg.lu_cm ? (int)mg.lu_bu : -1;
+        HIP_TRY(gls::vec_to_f32(bb, mg.x32.p, n, c->stream));
+        HIP_TRY(gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, c->stream, bl, bu));
+        if (mg.lu32_refine) {  // r = b - A x (the pinned FP64 matrix), x += LU^-1 r
+          const double one = 1.0, mone = -1.0;
+          double *r = mg.chk32.p, *x0 = mg.chk32.p + n;
+          HIP_TRY(gls::vec_from_f32(mg.x32.p, x0, n, c->stream));
+          HIP_TRY(gls::vec_copy(r, bb, n, c->stream));
+          if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+              rocblas_dgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &mone, mg.probe.p,
+                            (rocblas_int)n, x0, 1, &one, r, 1) != rocblas_status_success)
+            return set_err(GLS_EHIP, "rocblas_dgemv failed");
+          HIP_TRY(gls::vec_to_f32(r, mg.x32.p, n, c->stream));
+          HIP_TRY(gls::dense_lu_solve_f32(mg.probe32.p, (int)n, mg.x32.p, c->stream, bl, bu));
+          HIP_TRY(gls::vec_from_f32(mg.x32.p, xx, n, c->stream));
+          HIP_TRY(gls::vec_axpy(xx, 1.0, x0, n, c->stream));
+        } else {
+          HIP_TRY(gls::vec_from_f32(mg.x32.p, xx, n, c->stream));
+        }
+      } else {  // x = A^-1 b
+        const float one = 1.0f, zero = 0.0f;
+        HIP_TRY(gls::vec_to_f32(bb, mg.b32.p, n, c->stream));
+        if (rocblas_set_stream(mg.blas, c->stream) != rocblas_status_success ||
+            rocblas_sgemv(mg.blas, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n, &one, mg.probe32.p,
+                          (rocblas_int)n, mg.b32.p, 1, &zero, mg.x32.p, 1) != rocblas_status_success)
+          return set_err(GLS_EHIP, "rocblas_sgemv failed");
+        HIP_TRY(gls::vec_from_f32(mg.x32.p, xx, n, c->stream));
+      }
+      if (mg.lu_cm) HIP_TRY(gls::vec_permute(x, mg.lu_tmp.p, g->ilu.perm.p, n, 1, c->stream));
+      HIP_TRY(hipMemsetAsync(x + (int64_t)g->dim * g->n_vnodes, 0, sizeof(double), c->stream));  // pinned: no correction
       return GLS_OK;
     }
     if (mg.lu) {

@@ -211,7 +211,7 @@ hipError_t mg_dense_apply(const double *aug, int n, const double *b, double *x, 
 hipError_t mg_pin_dof(double *A, int64_t n, int64_t pin, hipStream_t s);
 hipError_t mg_zero_row(double *A, int64_t n, int64_t row, hipStream_t s);
 // x <- (LU)^-1 x for a dense FP32 LU factor without pivoting (column-major, lda = n; gls_mg_kernels.hip)
-hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s);
+hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s, int bl = -1, int bu = -1);  // bl / bu: bandwidths (-1 dense)
 hipError_t mg_jacobi_update(double *x, const double *b, const double *y, const double *d, double omega, int64_t n,
                             int zero_start, hipStream_t s);
 

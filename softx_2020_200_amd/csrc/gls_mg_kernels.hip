@@ -519,7 +519,8 @@ namespace {
 // barrier in the sequential part; one hands the first half to the second).
 constexpr int kLuT = 256;
 template <bool LOWER, bool VEC>
-__global__ void __launch_bounds__(kLuT) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k) {
+__global__ void __launch_bounds__(kLuT) k_lu_step(const float *__restrict__ A, int n, float *__restrict__ x, int k,
+                                                  int rlo) {  // rlo: backward, the first row block the others update
   __shared__ float xk[kLuB], xb[kLuB], rd[kLuB], part[2][kLuB];
   __shared__ float D[kLuB][kLuB + 1], C[kLuB][kLuB + 1];
   const int t = threadIdx.x, nb = (n + kLuB - 1) / kLuB;
@@ -527,7 +528,7 @@ __global__ void __launch_bounds__(kLuT) k_lu_step(const float *__restrict__ A, i
   const int j0 = first ? 0 : k * kLuB, nj = first ? 1 : min(kLuB, n - j0);
   const int kn = first ? (LOWER ? 0 : nb - 1) : (LOWER ? k + 1 : k - 1);  // the diagonal block solved here
   const int r0 = kn * kLuB, nr = min(kLuB, n - r0);
-  const int rb = diag ? r0 : LOWER ? (k + 1 + (int)blockIdx.x) * kLuB : ((int)blockIdx.x - 1) * kLuB;  // row block
+  const int rb = diag ? r0 : LOWER ? (k + 1 + (int)blockIdx.x) * kLuB : (rlo + (int)blockIdx.x - 1) * kLuB;  // row block
   const int row = t & (kLuB - 1), half = t >> 7;
   const int i = rb + row;
   const bool live = half == 0 && (diag ? row < nr : LOWER ? i < n : i < kn * kLuB);
@@ -623,24 +624,29 @@ __global__ void __launch_bounds__(kLuT) k_lu_step(const float *__restrict__ A, i
   }
   if (live) x[i] = v;
 }
+// bl / bu >= 0: lower / upper bandwidths -- a step updates only the row blocks its block column reaches
 template <bool VEC>
-void lu_solve(const float *LU, int n, float *x, hipStream_t s) {
+void lu_solve(const float *LU, int n, float *x, hipStream_t s, int bl, int bu) {
   const int nb = (n + kLuB - 1) / kLuB;
-  hipLaunchKernelGGL((k_lu_step<true, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1);
+  hipLaunchKernelGGL((k_lu_step<true, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1, 0);
   for (int k = 0; k + 1 < nb; ++k) {
-    const int rest = n - (k + 2) * kLuB;
+    const int end = bl < 0 ? n : std::min(n, (k + 1) * kLuB + bl);  // rows below reached by block column k
+    const int rest = end - (k + 2) * kLuB;
     hipLaunchKernelGGL((k_lu_step<true, VEC>), dim3(1 + (rest > 0 ? (rest + kLuB - 1) / kLuB : 0)), dim3(kLuT), 0, s, LU,
-                       n, x, k);
+                       n, x, k, 0);
   }
-  hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1);
-  for (int k = nb - 1; k >= 1; --k)
-    hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1 + (k - 1)), dim3(kLuT), 0, s, LU, n, x, k);
+  hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1), dim3(kLuT), 0, s, LU, n, x, -1, 0);
+  for (int k = nb - 1; k >= 1; --k) {
+    const int rlo = bu < 0 ? 0 : std::max(0, k * kLuB - bu) / kLuB;  // rows above reached by block column k
+    const int nblk = std::max(0, (k - 1) - rlo);
+    hipLaunchKernelGGL((k_lu_step<false, VEC>), dim3(1 + nblk), dim3(kLuT), 0, s, LU, n, x, k, rlo);
+  }
 }
 }  // namespace
-hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s) {
+hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s, int bl, int bu) {
   if (n <= 0) return hipSuccess;
-  if (n % 4 == 0 && reinterpret_cast<uintptr_t>(LU) % 16 == 0) lu_solve<true>(LU, n, x, s);
-  else lu_solve<false>(LU, n, x, s);
+  if (n % 4 == 0 && reinterpret_cast<uintptr_t>(LU) % 16 == 0) lu_solve<true>(LU, n, x, s, bl, bu);
+  else lu_solve<false>(LU, n, x, s, bl, bu);
   return hipGetLastError();
 }
 

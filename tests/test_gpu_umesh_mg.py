@@ -76,8 +76,8 @@ def test_umesh_multigrid_linear_solve(name, dim, spec, flat, k, kp, smoother):
 def test_large_coarsest_level_fp32_lu(monkeypatch, capfd):
     """a coarsest level above 8192 DoFs (the Q2-Q1 cylinder shell at refinement 2, 30816 DoFs, under its
     refinement-3 level): the FP32 unpivoted LU factored by the worker thread on the side stream, its check
-    |A x - 1| / |1| taken (here ~9e-3: applied with one refinement step, no pivoted fallback), and the
-    V-cycle-preconditioned GMRES converging"""
+    |A x - 1| / |1| taken (no pivoted fallback; the matrix kept banded in the probe CSR's Cuthill-McKee order), and
+    the V-cycle-preconditioned GMRES converging"""
     from softx_2020_200_amd.native import UMesh
     m = UMesh(3, "cylinder_shell", "1 : 0.25 : 1 : 8 : 2")
     m.refine_global(3)
@@ -110,8 +110,8 @@ def test_large_coarsest_level_fp32_lu(monkeypatch, capfd):
     refined = ["refinement step" in l for l in lines]
     print("large coarsest level: %d DoFs, GMRES its %d, LU checks %s, refined %s" % (probs[1].n_dofs, its, checks, refined))
     assert ok and res <= 1e-8 * float(rhs.norm()) * 1.01, (its, res)
-    # the check decides: below 1e-3 as it is, up to 0.5 with one refinement step (this level: ~9e-3), else pivoted
+    # the check decides: below 1e-2 as it is, up to 0.5 with one refinement step, else pivoted
     assert checks and max(checks) < 0.5, log[-2000:]
-    assert all(r == (c >= 1e-3) for r, c in zip(refined, checks)), lines
+    assert all(r == (c >= 1e-2) for r, c in zip(refined, checks)), lines
     assert "pivoted LU + inverse" not in log, log[-2000:]
     assert its <= 40, its
