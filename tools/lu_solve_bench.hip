@@ -13,7 +13,7 @@
 #include <vector>
 
 namespace gls {
-hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s);
+hipError_t dense_lu_solve_f32(const float *LU, int n, float *x, hipStream_t s, int bl, int bu);
 }
 
 #define CK(x)                                                                        \
@@ -118,7 +118,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(dA, h.data(), sizeof(float) * (size_t)n * n, hipMemcpyHostToDevice));
     for (int variant = 0; variant < 2; ++variant) {
       auto run = [&]() {
-        if (variant == 0) CK(gls::dense_lu_solve_f32(dA, n, dx, s));
+        if (variant == 0) CK(gls::dense_lu_solve_f32(dA, n, dx, s, -1, -1));
         else solve_barrier(dA, n, dx, s);
       };
       CK(hipMemcpy(dx, b.data(), sizeof(float) * n, hipMemcpyHostToDevice));
