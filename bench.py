@@ -362,7 +362,7 @@ def bench_cylinder3d(args):
     mesh = (lambda r: taylorcouette3d_mesh(r)) if tc else (lambda r: cylinder3d_mesh(r))
     make = (lambda sp_: taylorcouette3d_context(sp_)) if tc else (lambda sp_: cylinder3d_context(space=sp_))
     qall = tc  # configs[3]: MappingQ2 on every cell
-    levels, sw = None, 0
+    levels, sw, pre, post = None, 0, 0, 0
     if args.cyl_precond == "hmg":  # the refinement hierarchy of the globally refined mesh
         if refine < 1 and not (args.cyl_plevel or args.cyl_hp):
             sys.exit("bench.py: --cyl-precond hmg needs --cyl-refine >= 1 or the p-level (a level below the fine mesh)")
@@ -388,8 +388,12 @@ def bench_cylinder3d(args):
         for c_, _, _ in levels:
             c_.set_time(scheme, ts)
         sw = 1 if args.cyl_smoother == "ilu" else 2
+        # configs[3] (steady, nu 1): post-smoothing only, V(0,1), 7 GMRES its in 160 ms against V(1,1)'s 5 in 176;
+        # configs[4]: V(1,1) (V(0,1) 184 ms, V(2,1) 175; profiles/r06_hmg_sweeps.txt)
+        pre, post = args.cyl_sweeps if args.cyl_sweeps else ((0, 1) if tc and args.cyl_smoother == "ilu" else (sw, sw))
         nco = levels[-1][0].n_dofs
-        ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=sw, post_smooth=sw,
+        ctx.attach_multigrid_transfers([c_ for c_, _, _ in levels[1:]], xfer, pre_smooth=pre if pre > 0 else -1,
+                                       post_smooth=post,
                                        coarse_sweeps=args.mg_coarse_sweeps_cyl, omega=args.mg_omega_cyl,
                                        coarse_direct=1 if nco <= args.direct_max else -1, smoother=args.cyl_smoother)
     else:
@@ -447,7 +451,7 @@ def bench_cylinder3d(args):
                    "n_dofs": N, "n_cells": nc,
                    "linear_solver": ("GMRES(%d)+GMG V(%d,%d) on the %s (%d levels, %s smoothing, "
                                      "%s on the base mesh), rel 1e-4" % (
-                                         args.restart, sw, sw,
+                                         args.restart, pre, post,
                                          "h-p hierarchy (Q2-Q1 fine, Q1-Q1 on the fine mesh and its refinement "
                                          "hierarchy)" if args.cyl_hp else "refinement hierarchy", len(levels),
                                          {"ilu": "multicolor ILU(0)", "jacobi": "damped-Jacobi",
@@ -720,6 +724,9 @@ def main():
     ap.add_argument("--cyl-plevel", type=int, default=1,
                     help="cylinder3d / taylorcouette3d --cyl-precond hmg: 1 = a Q1-Q1 p-level below the base mesh "
                          "(gls_fe_space_mg_transfer's p-level pair), solved by the dense LU")
+    ap.add_argument("--cyl-sweeps", type=int, nargs=2, default=None, metavar=("PRE", "POST"),
+                    help="--cyl-precond hmg: pre / post smoothing sweeps per level (default: ILU 0 1 on taylorcouette3d, "
+                         "1 1 on cylinder3d; Jacobi 2 2)")
     ap.add_argument("--cyl-hp", type=int, default=0,
                     help="--cyl-precond hmg: 1 = p first (Q2-Q1 fine -> Q1-Q1 on the fine mesh -> the Q1-Q1 refinement "
                          "hierarchy, exact LU at the bottom)")
